@@ -1,0 +1,169 @@
+/*
+ * kair_hip.h — C ABI of libkair_hip.so, the MI355X (gfx950) kernels behind the KAIR hot path.
+ *
+ * The reference (Owen1B/KAIR) has NO native code on this path: models/network_{swinir,dncnn,
+ * rrdb,rrdbnet,usrnet}.py run on ATen (cuDNN / cuBLAS in the reference).  These entry points
+ * replace the ATen calls that those files make; each declaration names the reference site.
+ *
+ * Conventions:
+ *   - plain device pointers + sizes, caller (PyTorch caching allocator) owns every buffer,
+ *     including outputs and workspaces; no allocation, no host sync, no global mutable state;
+ *   - every call takes the hipStream_t to launch on (passed as void* to keep this header
+ *     HIP-free) and is graph-capturable;
+ *   - return 0 on success or a negative KAIR_ERR_* code; kair_last_error() returns a
+ *     thread-local message for the last failure.
+ *
+ * Activation layouts: NHWC token matrices with the channel dimension padded
+ * to a multiple of 32 (e.g. SwinIR C=180 -> 192), head-padded q/k/v (head_dim 30 -> 32),
+ * fp32 residual stream, bf16 (or fp32 in parity mode) GEMM operands, fp32 accumulation.
+ */
+#ifndef KAIR_HIP_H
+#define KAIR_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KAIR_OK 0
+#define KAIR_ERR_ARG (-1)
+#define KAIR_ERR_HIP (-2)
+
+typedef enum { KAIR_F32 = 0, KAIR_BF16 = 1 } kair_dtype;
+
+/* How a GEMM operand element (row m, column k) is addressed. */
+typedef enum {
+  KAIR_LD_ROWS = 0,    /* ptr[rowmap(m) * ld + k]                                           */
+  KAIR_LD_IM2COL3 = 1, /* 3x3/pad1/stride1 patch of an NHWC image [B, im_H, im_W, im_C]:
+                          k = tap * im_C + c                                                 */
+  KAIR_LD_QKVBLK = 2   /* head-blocked q/k/v: [part][window][head][tok][hdp], k = part*nh*hdp
+                          + head*hdp + d                                                    */
+} kair_load_mode;
+
+typedef struct {
+  const void* ptr;
+  int dtype;           /* kair_dtype                                                         */
+  int mode;            /* kair_load_mode                                                     */
+  long ld;             /* ROWS: row stride in elements                                       */
+  int win_H, win_W, win_ws, win_shift; /* ROWS: Swin window->token row map (ws==0: identity)  */
+  int im_H, im_W, im_C, im_flip;       /* IM2COL3 (im_flip: tap (dy,dx) -> (-dy,-dx), dgrad)  */
+  int qkv_nh, qkv_hdp, qkv_tok;        /* QKVBLK                                              */
+  const float* rowscale; int rows_per_scale; /* optional per-sample scale (DropPath)          */
+  int ones_col;        /* >=0: this column reads as 1.0 (fused bias gradient), else -1       */
+} kair_operand;
+
+typedef enum {
+  KAIR_OUT_ROWS = 0,      /* out[rowmap(m) * ldo + n]                                         */
+  KAIR_OUT_QKVBLK = 1,    /* head-blocked q/k/v layout (as KAIR_LD_QKVBLK)                    */
+  KAIR_OUT_PSHUF = 2,     /* PixelShuffle(r): m=(b,y,x) of [ps_H,ps_W], n=c*r*r+i*r+j
+                             -> out NHWC [b, y*r+i, x*r+j, c] with channel stride ldo          */
+  KAIR_OUT_PUNSHUF = 3,   /* inverse: m = pixel of the [ps_H*r, ps_W*r] image, n = c
+                             -> out[(b,y,x) of ps_H x ps_W][c*r*r+i*r+j], stride ldo          */
+  KAIR_OUT_NCHW = 4       /* image out[b][n][y][x] (n < img_C) of [img_H, img_W],
+                             value = v / img_range + img_mean[n]                              */
+} kair_out_mode;
+
+typedef enum { KAIR_ACT_NONE = 0, KAIR_ACT_GELU = 1, KAIR_ACT_LEAKY = 2, KAIR_ACT_RELU = 3 } kair_act;
+
+typedef struct {
+  void* out; int out_dtype; int out_mode; long ldo;
+  int win_H, win_W, win_ws, win_shift;  /* row map for KAIR_OUT_ROWS / residual / gate         */
+  const float* bias;                    /* [N] or NULL                                        */
+  int act; float slope;                 /* kair_act; slope for LEAKY                          */
+  void* out_pre; int pre_dtype; long ldp; /* optional: pre-activation copy (same row map)     */
+  const float* resid; long ldr;          /* optional: out = resid + rowscale * value (fp32)    */
+  const float* rowscale; int rows_per_scale;
+  const void* gate; int gate_dtype; long ldg; int gate_kind; /* value *= act'(gate):
+                                           1 gelu'(gate)  2 leaky'(sign of gate)  3 relu'     */
+  int ps_r, ps_H, ps_W;                 /* pixel (un)shuffle geometry                         */
+  int qkv_nh, qkv_hdp, qkv_tok;         /* KAIR_OUT_QKVBLK                                    */
+  const float* img_mean; float img_range; int img_C, img_H, img_W; /* KAIR_OUT_NCHW          */
+} kair_epilogue;
+
+/* C[m,n] = sum_k A[m,k] * B[n,k]  (+ epilogue).  compute: KAIR_BF16 -> v_mfma_f32_16x16x32_bf16,
+ * KAIR_F32 -> v_mfma_f32_16x16x4_f32 (exact fp32).  K must be a multiple of 8.
+ * Replaces: nn.Linear (network_swinir.py:19-20,105,107 forward/dgrad), nn.Conv2d 3x3
+ * (network_swinir.py:465,669,729,742,745,584; network_dncnn.py:62-66; network_rrdbnet.py:82-90)
+ * forward and input-gradient. */
+int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const kair_epilogue* E,
+                 long M, int N, int K, int compute, void* stream);
+
+/* Weight gradient: partial[s][n][k] = sum_{m in split s} A[m,n] * B[m,k]; then
+ * kair_wgrad_finalize sums the splits.  ws needs splits*N*K floats (kair_wgrad_splits()).
+ * Replaces the weight-gradient half of the same nn.Linear / nn.Conv2d backward. */
+int kair_wgrad_splits(long M, int N, int K);
+int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float* ws, int splits,
+                 long M, int N, int K, int compute, void* stream);
+
+/* Weight layout maps between reference (fp32 master, torch layout) and packed (padded) forms. */
+typedef struct {
+  int kind;          /* 0 linear [N][K]; 1 conv3x3 [Co][Ci][3][3] -> [Cop][9*Cip];
+                        2 conv3x3 dgrad form -> [Cip][9*Cop] (flipped taps, swapped channels);
+                        3 linear transposed -> [Kp][Np]                                      */
+  int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
+  int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
+  int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp                   */
+} kair_wmap;
+
+/* dst (packed, dtype) <- src (reference fp32).  Pad entries written as 0. */
+int kair_pack_weight(const float* src, void* dst, int dst_dtype, const kair_wmap* map, void* stream);
+/* grad_ref (fp32 reference layout) = sum_s partial[s] (packed layout [Np][Kp]);
+ * bias_grad (if non-NULL) = column ones_col of the sum.  accumulate: += instead of =. */
+int kair_wgrad_finalize(const float* partial, int splits, const kair_wmap* map, float* grad_ref,
+                        float* bias_grad, int ones_col, int accumulate, void* stream);
+/* bias_grad[n_ref] (+)= sum_m G[m][n]  for an operand G of width Np (conv biases without a pad
+ * column).  ws: 1024 * N floats. */
+int kair_colsum(const kair_operand* G, long M, int Np, const kair_wmap* map, float* bias_grad,
+                float* ws, int accumulate, void* stream);
+
+/* LayerNorm over the last dim (nn.LayerNorm eps 1e-5; network_swinir.py:199,205,520,725).
+ * x fp32 [M, ldx] token order -> y (dtype) at rows rowmap^-1 (window order when win_ws > 0),
+ * y pad columns [C, ldy) written 0.  mean/rstd fp32 [M] indexed by token row. */
+int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype, long ldy, const float* gamma,
+                       const float* beta, float* mean, float* rstd, long M, int C, float eps,
+                       int win_H, int win_W, int win_ws, int win_shift, void* stream);
+/* dx_acc[t] (+)= LN-backward(dy) for token rows t; dgamma/dbeta (+)= column sums.
+ * dy (dtype) is addressed like y in the forward.  ws: 2 * 1024 * C floats. */
+int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int dy_dtype, long ldy,
+                       const float* gamma, const float* mean, const float* rstd, float* dx_acc,
+                       long ld_dx, int dx_accumulate, float* dgamma, float* dbeta, int dparam_accumulate,
+                       float* ws, long M, int C, int win_H, int win_W, int win_ws, int win_shift,
+                       void* stream);
+
+/* Fused Swin window attention (network_swinir.py:114-145) for ws=8 (64 tokens), head_dim <= 32:
+ *   O = softmax(q*scale @ k^T + table[relidx] + shift_mask) @ v   per (window, head).
+ * qkv: head-blocked [3][nWin][nh][64][32] (dtype); table: fp32 [(2ws-1)^2][nh] (reference
+ * layout); O written to rows [nWin*64, ldo] window order, head h at columns h*32..h*32+31;
+ * lse fp32 [nWin][nh][64] (for backward).  Region mask is computed analytically for a
+ * shift>0 block on an H x W token grid (calculate_mask, network_swinir.py:216-237). */
+int kair_window_attn_fwd(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
+                         long nWin, int nh, int hd, float scale, int H, int W, int shift, void* stream);
+/* Backward: dO rows [nWin*64, lddo] (dtype, same layout as O); writes dqkv head-blocked (dtype);
+ * dtable (+)= bias-table gradient (ws: nh*64*64*partials floats, kair_window_attn_bwd_ws()). */
+long kair_window_attn_bwd_ws(long nWin, int nh);
+int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
+                         const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
+                         float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
+                         void* stream);
+
+/* Elementwise / small kernels ------------------------------------------------------------- */
+/* NCHW fp32 image -> NHWC (dtype) with channel stride ldc, x' = (x - mean[c]) * img_range
+ * (network_swinir.py:809-810); mean may be NULL.  Pad channels written 0. */
+int kair_image_to_nhwc(const float* img, void* out, int dtype, int ldc, const float* mean, float img_range,
+                       int B, int C, int H, int W, void* stream);
+/* L1 loss (nn.L1Loss, mean): loss_out[0] = weight*mean|E-H|; grad dE = weight*sign(E-H)/numel written
+ * NHWC (dtype, channel stride ldc) for the last conv's dgrad.  ws: 1024 floats. */
+int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, float weight,
+                 int B, int C, int Hh, int Ww, float* ws, void* stream);
+/* Fused Adam (torch.optim.Adam maths, model_plain.py:210-222,302) + EMA (model_base.py:247-252)
+ * over flat fp32 buffers.  step_lr[0] = lr, step_lr[1] = t (incremented in-kernel by a
+ * single thread after use is NOT done: caller passes t). ema may be NULL. */
+int kair_adam_ema(float* p, const float* g, float* m, float* v, float* ema, long n, const float* lr_t,
+                  float beta1, float beta2, float eps, float weight_decay, float ema_decay, void* stream);
+
+const char* kair_last_error(void);
+int kair_device_arch(char* buf, int len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,278 @@
+"""ctypes binding of libkair_hip.so (include/kair_hip.h).
+
+This is the ONLY way the product reaches its kernels.  There is no CPU or PyTorch fallback: if the
+library is missing or a call fails, a RuntimeError is raised (tests/test_boundary.py checks both).
+Tensors are passed as raw device pointers; the current torch stream is passed explicitly.
+"""
+import ctypes
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libkair_hip.so")
+
+F32, BF16 = 0, 1
+LD_ROWS, LD_IM2COL3, LD_QKVBLK = 0, 1, 2
+OUT_ROWS, OUT_QKVBLK, OUT_PSHUF, OUT_PUNSHUF, OUT_NCHW = 0, 1, 2, 3, 4
+ACT_NONE, ACT_GELU, ACT_LEAKY, ACT_RELU = 0, 1, 2, 3
+
+c_long, c_int, c_float, c_vp = ctypes.c_long, ctypes.c_int, ctypes.c_float, ctypes.c_void_p
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [("ptr", c_vp), ("dtype", c_int), ("mode", c_int), ("ld", c_long),
+                ("win_H", c_int), ("win_W", c_int), ("win_ws", c_int), ("win_shift", c_int),
+                ("im_H", c_int), ("im_W", c_int), ("im_C", c_int), ("im_flip", c_int),
+                ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
+                ("rowscale", c_vp), ("rows_per_scale", c_int), ("ones_col", c_int)]
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [("out", c_vp), ("out_dtype", c_int), ("out_mode", c_int), ("ldo", c_long),
+                ("win_H", c_int), ("win_W", c_int), ("win_ws", c_int), ("win_shift", c_int),
+                ("bias", c_vp), ("act", c_int), ("slope", c_float),
+                ("out_pre", c_vp), ("pre_dtype", c_int), ("ldp", c_long),
+                ("resid", c_vp), ("ldr", c_long),
+                ("rowscale", c_vp), ("rows_per_scale", c_int),
+                ("gate", c_vp), ("gate_dtype", c_int), ("ldg", c_long), ("gate_kind", c_int),
+                ("ps_r", c_int), ("ps_H", c_int), ("ps_W", c_int),
+                ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
+                ("img_mean", c_vp), ("img_range", c_float), ("img_C", c_int), ("img_H", c_int), ("img_W", c_int)]
+
+
+class WMap(ctypes.Structure):
+    _fields_ = [("kind", c_int), ("N", c_int), ("K", c_int), ("nG", c_int), ("nGr", c_int), ("nGp", c_int),
+                ("kG", c_int), ("kGr", c_int), ("kGp", c_int)]
+
+
+_SIGS = {
+    "kair_gemm_nt": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), ctypes.POINTER(Epilogue), c_long, c_int, c_int,
+                     c_int, c_vp],
+    "kair_wgrad_splits": [c_long, c_int, c_int],
+    "kair_gemm_tn": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), c_vp, c_int, c_long, c_int, c_int, c_int, c_vp],
+    "kair_pack_weight": [c_vp, c_vp, c_int, ctypes.POINTER(WMap), c_vp],
+    "kair_wgrad_finalize": [c_vp, c_int, ctypes.POINTER(WMap), c_vp, c_vp, c_int, c_int, c_vp],
+    "kair_colsum": [ctypes.POINTER(Operand), c_long, c_int, ctypes.POINTER(WMap), c_vp, c_vp, c_int, c_vp],
+    "kair_layernorm_fwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_float, c_int,
+                           c_int, c_int, c_int, c_vp],
+    "kair_layernorm_bwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_vp, c_vp, c_int,
+                           c_vp, c_long, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "kair_window_attn_fwd": [c_vp, c_int, c_vp, c_vp, c_long, c_vp, c_long, c_int, c_int, c_float, c_int, c_int, c_int,
+                             c_vp],
+    "kair_window_attn_bwd_ws": [c_long, c_int],
+    "kair_window_attn_bwd": [c_vp, c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_int,
+                             c_int, c_float, c_int, c_int, c_int, c_vp],
+    "kair_image_to_nhwc": [c_vp, c_vp, c_int, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
+    "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "kair_adam_ema": [c_vp, c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp],
+    "kair_last_error": [],
+    "kair_device_arch": [ctypes.c_char_p, c_int],
+}
+_RESTYPE = {"kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long}
+
+_lib = None
+
+
+def lib():
+    """Load libkair_hip.so once.  Raises RuntimeError (never falls back) when it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"kair_amd: HIP kernel library not built ({LIB_PATH}); run `python -m kair_amd.build`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPE.get(name, c_int)
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().kair_last_error().decode(errors="replace")
+        raise RuntimeError(f"kair_hip {what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def require_device(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("kair_amd runs on the HIP device only (got a CPU tensor); there is no CPU fallback")
+
+
+# ------------------------------------------------------------------------------------------
+# descriptor builders
+# ------------------------------------------------------------------------------------------
+def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1):
+    """Row-major operand; win = (H, W, ws, shift) applies the Swin window->token row map."""
+    o = Operand()
+    o._keep = (t, rowscale)  # keep the tensors alive until the launch has been issued
+    o.ptr = ptr(t)
+    o.dtype = dtype_code(t)
+    o.mode = LD_ROWS
+    o.ld = ld if ld is not None else t.shape[-1]
+    if win:
+        o.win_H, o.win_W, o.win_ws, o.win_shift = win
+    o.rowscale = ptr(rowscale)
+    o.rows_per_scale = rows_per_scale
+    o.ones_col = ones_col
+    return o
+
+
+def im2col(t, H, W, C, flip=False, ones_col=-1):
+    o = Operand()
+    o._keep = t
+    o.ptr = ptr(t)
+    o.dtype = dtype_code(t)
+    o.mode = LD_IM2COL3
+    o.im_H, o.im_W, o.im_C, o.im_flip = H, W, C, int(flip)
+    o.ones_col = ones_col
+    o.rows_per_scale = 1
+    return o
+
+
+def qkvblk(t, nh, hdp=32, tok=64, rowscale=None, rows_per_scale=1):
+    o = Operand()
+    o._keep = (t, rowscale)
+    o.ptr = ptr(t)
+    o.dtype = dtype_code(t)
+    o.mode = LD_QKVBLK
+    o.qkv_nh, o.qkv_hdp, o.qkv_tok = nh, hdp, tok
+    o.rowscale = ptr(rowscale)
+    o.rows_per_scale = rows_per_scale
+    o.ones_col = -1
+    return o
+
+
+def epilogue(out, mode=OUT_ROWS, ldo=None, win=None, bias=None, act=ACT_NONE, slope=0.0, pre=None, ldp=None,
+             resid=None, ldr=None, rowscale=None, rows_per_scale=1, gate=None, ldg=None, gate_kind=0,
+             ps=None, qkv=None, img=None):
+    e = Epilogue()
+    e._keep = (out, bias, pre, resid, rowscale, gate, img)
+    e.out = ptr(out)
+    e.out_dtype = dtype_code(out)
+    e.out_mode = mode
+    e.ldo = ldo if ldo is not None else out.shape[-1]
+    if win:
+        e.win_H, e.win_W, e.win_ws, e.win_shift = win
+    e.bias = ptr(bias)
+    e.act, e.slope = act, slope
+    if pre is not None:
+        e.out_pre, e.pre_dtype, e.ldp = ptr(pre), dtype_code(pre), (ldp if ldp is not None else pre.shape[-1])
+    if resid is not None:
+        e.resid, e.ldr = ptr(resid), (ldr if ldr is not None else resid.shape[-1])
+    e.rowscale, e.rows_per_scale = ptr(rowscale), rows_per_scale
+    if gate is not None:
+        e.gate, e.gate_dtype, e.ldg, e.gate_kind = ptr(gate), dtype_code(gate), (ldg if ldg is not None else gate.shape[-1]), gate_kind
+    if ps:
+        e.ps_r, e.ps_H, e.ps_W = ps
+    if qkv:
+        e.qkv_nh, e.qkv_hdp, e.qkv_tok = qkv
+    if img:
+        mean, rng, C, H, W = img
+        e.img_mean, e.img_range, e.img_C, e.img_H, e.img_W = ptr(mean), rng, C, H, W
+    return e
+
+
+def wmap(kind, N, K, n_groups=(1, None, None), k_groups=(1, None, None)):
+    """n_groups = (G, real, padded) for the out dim; k_groups likewise for the in dim."""
+    m = WMap()
+    m.kind, m.N, m.K = kind, N, K
+    nG, nr, npd = n_groups
+    kG, kr, kpd = k_groups
+    m.nG, m.nGr, m.nGp = nG, nr or N // nG, npd or nr or N // nG
+    m.kG, m.kGr, m.kGp = kG, kr or (K // kG if K else 1), kpd or kr or (K // kG if K else 1)
+    return m
+
+
+# ------------------------------------------------------------------------------------------
+# thin call wrappers (raise on error)
+# ------------------------------------------------------------------------------------------
+def gemm_nt(A, B, E, M, N, K, compute):
+    check(lib().kair_gemm_nt(ctypes.byref(A), ctypes.byref(B), ctypes.byref(E), M, N, K, compute, stream_ptr()), "gemm_nt")
+
+
+def wgrad_splits(M, N, K):
+    return lib().kair_wgrad_splits(M, N, K)
+
+
+def gemm_tn(A, B, ws, splits, M, N, K, compute):
+    check(lib().kair_gemm_tn(ctypes.byref(A), ctypes.byref(B), ptr(ws), splits, M, N, K, compute, stream_ptr()), "gemm_tn")
+
+
+def pack_weight(src, dst, m):
+    check(lib().kair_pack_weight(ptr(src), ptr(dst), dtype_code(dst), ctypes.byref(m), stream_ptr()), "pack_weight")
+
+
+def wgrad_finalize(partial, splits, m, grad, bias_grad=None, ones_col=-1, accumulate=False):
+    check(lib().kair_wgrad_finalize(ptr(partial), splits, ctypes.byref(m), ptr(grad), ptr(bias_grad), ones_col,
+                                    int(accumulate), stream_ptr()), "wgrad_finalize")
+
+
+def colsum(G, M, Np, m, bias_grad, ws, accumulate=False):
+    check(lib().kair_colsum(ctypes.byref(G), M, Np, ctypes.byref(m), ptr(bias_grad), ptr(ws), int(accumulate),
+                            stream_ptr()), "colsum")
+
+
+def layernorm_fwd(x, ldx, y, ldy, gamma, beta, mean, rstd, M, C, eps=1e-5, win=(0, 0, 0, 0)):
+    check(lib().kair_layernorm_fwd(ptr(x), ldx, ptr(y), dtype_code(y), ldy, ptr(gamma), ptr(beta), ptr(mean), ptr(rstd),
+                                   M, C, eps, *win, stream_ptr()), "layernorm_fwd")
+
+
+def layernorm_bwd(x, ldx, dy, ldy, gamma, mean, rstd, dx, ld_dx, dx_acc, dgamma, dbeta, dparam_acc, ws, M, C,
+                  win=(0, 0, 0, 0)):
+    check(lib().kair_layernorm_bwd(ptr(x), ldx, ptr(dy), dtype_code(dy), ldy, ptr(gamma), ptr(mean), ptr(rstd), ptr(dx),
+                                   ld_dx, int(dx_acc), ptr(dgamma), ptr(dbeta), int(dparam_acc), ptr(ws), M, C, *win,
+                                   stream_ptr()), "layernorm_bwd")
+
+
+def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift):
+    check(lib().kair_window_attn_fwd(ptr(qkv), dtype_code(qkv), ptr(table), ptr(O), ldo, ptr(lse), nWin, nh, hd, scale,
+                                     H, W, shift, stream_ptr()), "window_attn_fwd")
+
+
+def window_attn_bwd_ws(nWin, nh):
+    return lib().kair_window_attn_bwd_ws(nWin, nh)
+
+
+def window_attn_bwd(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc, ws, nWin, nh, hd, scale, H, W, shift):
+    check(lib().kair_window_attn_bwd(ptr(qkv), ptr(O), ldo, ptr(dO), lddo, dtype_code(qkv), ptr(table), ptr(lse),
+                                     ptr(dqkv), ptr(dtable), int(dtable_acc), ptr(ws), nWin, nh, hd, scale, H, W, shift,
+                                     stream_ptr()), "window_attn_bwd")
+
+
+def image_to_nhwc(img, out, ldc, mean, img_range, B, C, H, W):
+    check(lib().kair_image_to_nhwc(ptr(img), ptr(out), dtype_code(out), ldc, ptr(mean), img_range, B, C, H, W,
+                                   stream_ptr()), "image_to_nhwc")
+
+
+def l1_loss(E, H, loss_out, dE, ldc, weight, B, C, Hh, Ww, ws):
+    check(lib().kair_l1_loss(ptr(E), ptr(H), ptr(loss_out), ptr(dE), dtype_code(dE), ldc, weight, B, C, Hh, Ww, ptr(ws),
+                             stream_ptr()), "l1_loss")
+
+
+def adam_ema(p, g, m, v, ema, n, lr_t, beta1, beta2, eps, wd, decay):
+    check(lib().kair_adam_ema(ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), n, ptr(lr_t), beta1, beta2, eps, wd, decay,
+                              stream_ptr()), "adam_ema")

@@ -1,0 +1,78 @@
+// Shared device helpers for the KAIR MI355X (gfx950 / CDNA4) kernels.
+// Wave64 everywhere; bf16 storage is the compiler's __bf16 (RNE conversions via v_cvt_pk_bf16_f32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kair_hip.h"
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) short short4v;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+#define KAIR_DEV __device__ __forceinline__
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+// ---------------------------------------------------------------------------------------------
+// error plumbing for the C-ABI: every entry point returns 0 or a negative code and leaves a
+// thread-local message behind (kair_last_error()).
+// ---------------------------------------------------------------------------------------------
+int kair_set_error(int code, const char* fmt, ...);
+
+#define KAIR_CHECK_ARG(cond, ...)                                                  \
+  do {                                                                             \
+    if (!(cond)) return kair_set_error(KAIR_ERR_ARG, __VA_ARGS__);                 \
+  } while (0)
+
+#define KAIR_CHECK_LAUNCH()                                                        \
+  do {                                                                             \
+    hipError_t e__ = hipGetLastError();                                            \
+    if (e__ != hipSuccess)                                                         \
+      return kair_set_error(KAIR_ERR_HIP, "%s: %s", __func__, hipGetErrorString(e__)); \
+  } while (0)
+
+template <typename T> KAIR_DEV float to_f(T v) { return (float)v; }
+template <typename T> KAIR_DEV T from_f(float v) { return (T)v; }
+
+KAIR_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+KAIR_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+KAIR_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+KAIR_DEV float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// Swin window <-> token row map (network_swinir.py:33-62 + torch.roll at :250/:270):
+// GEMM row m enumerates tokens window-major (b, wy, wx, r, c); the token it reads / writes lives at
+// ((wy*ws + r + shift) % H, (wx*ws + c + shift) % W) of image b.
+struct WinMap {
+  int H, W, ws, shift;  // ws == 0 => identity map
+};
+KAIR_DEV long win_to_token(long m, const WinMap& w) {
+  if (w.ws == 0) return m;
+  const int ws2 = w.ws * w.ws;
+  const int nWw = w.W / w.ws, nW = (w.H / w.ws) * nWw;
+  const long win = m / ws2;
+  const int t = (int)(m - win * ws2);
+  const long b = win / nW;
+  const int wi = (int)(win - b * nW);
+  const int wy = wi / nWw, wx = wi - wy * nWw;
+  int y = wy * w.ws + t / w.ws + w.shift;
+  int x = wx * w.ws + t % w.ws + w.shift;
+  if (y >= w.H) y -= w.H;
+  if (x >= w.W) x -= w.W;
+  return (b * w.H + y) * (long)w.W + x;
+}

@@ -1,0 +1,274 @@
+// Memory-bound helpers around the KAIR training step on gfx950: weight packing into the padded
+// MFMA layouts, deterministic weight-gradient finalisation, image <-> token layout, the L1 loss
+// (nn.L1Loss mean, model_plain.py:183-188) and the fused Adam + EMA update (torch.optim.Adam maths,
+// model_plain.py:210-222/302; ModelBase.update_E model_base.py:247-252).
+#include "common.h"
+
+namespace {
+
+// padded index -> reference index along one grouped dim (-1 for pad)
+KAIR_DEV int unpad(int ip, int G, int Gr, int Gp) {
+  const int g = ip / Gp, i = ip - g * Gp;
+  return (g < G && i < Gr) ? g * Gr + i : -1;
+}
+
+__global__ void pack_kernel(const float* __restrict__ src, void* __restrict__ dst, int dt, kair_wmap mp, long total) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int Np = mp.nG * mp.nGp, Kp = mp.kG * mp.kGp;
+  float v = 0.f;
+  if (mp.kind == 0 || mp.kind == 3) {  // linear [Np][Kp] (or transposed [Kp][Np])
+    int np, kp;
+    if (mp.kind == 0) { np = (int)(t / Kp); kp = (int)(t - (long)np * Kp); }
+    else { kp = (int)(t / Np); np = (int)(t - (long)kp * Np); }
+    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
+  } else if (mp.kind == 1) {  // conv [Cop][9*Cip], k = tap*Cip + ci
+    const int np = (int)(t / (9 * Kp));
+    const int kk = (int)(t - (long)np * 9 * Kp);
+    const int tap = kk / Kp, cip = kk - tap * Kp;
+    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
+  } else if (mp.kind == 2) {  // conv dgrad form [Cip][9*Cop], k = tap*Cop + co (loader negates taps)
+    const int cip = (int)(t / (9 * Np));
+    const int kk = (int)(t - (long)cip * 9 * Np);
+    const int tap = kk / Np, cop = kk - tap * Np;
+    const int n = unpad(cop, mp.nG, mp.nGr, mp.nGp), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
+  } else {  // bias vector
+    const int n = unpad((int)t, mp.nG, mp.nGr, mp.nGp);
+    if (n >= 0) v = src[n];
+  }
+  if (dt == KAIR_BF16) ((bf16*)dst)[t] = (bf16)v;
+  else ((float*)dst)[t] = v;
+}
+
+// one thread per reference weight element (+ bias elements): sum of the split partials
+__global__ void wgrad_finalize_kernel(const float* __restrict__ part, int splits, kair_wmap mp, float* grad,
+                                      float* bias_grad, int ones_col, int acc, long nw, long Kt, long plane) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long nb = bias_grad ? mp.N : 0;
+  if (t >= nw + nb) return;
+  long off;
+  if (t < nw) {
+    if (mp.kind == 0) {
+      const int n = (int)(t / mp.K), k = (int)(t - (long)n * mp.K);
+      const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr, kp = (k / mp.kGr) * mp.kGp + k % mp.kGr;
+      off = (long)np * Kt + kp;
+    } else {  // conv: grad[co][ci][tap]
+      const int co = (int)(t / ((long)mp.K * 9));
+      const int rem = (int)(t - (long)co * mp.K * 9);
+      const int ci = rem / 9, tap = rem - (rem / 9) * 9;
+      const int np = (co / mp.nGr) * mp.nGp + co % mp.nGr;
+      const int cip = (ci / mp.kGr) * mp.kGp + ci % mp.kGr;
+      const int Cip = mp.kG * mp.kGp;
+      off = (long)np * Kt + (long)tap * Cip + cip;
+    }
+  } else {
+    const int n = (int)(t - nw);
+    const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr;
+    off = (long)np * Kt + ones_col;
+  }
+  float s = 0.f;
+  for (int i = 0; i < splits; ++i) s += part[(long)i * plane + off];
+  float* o = t < nw ? grad + t : bias_grad + (t - nw);
+  *o = acc ? *o + s : s;
+}
+
+template <typename T>
+__global__ void colsum_partial(const T* __restrict__ g, long ld, long M, int Np, float* __restrict__ ws, long rows_per) {
+  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  if (c >= Np) return;
+  const long r0 = (long)blockIdx.x * rows_per;
+  long r1 = r0 + rows_per;
+  if (r1 > M) r1 = M;
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) s += (float)g[r * ld + c];
+  ws[(long)blockIdx.x * Np + c] = s;
+}
+
+__global__ void colsum_final(const float* __restrict__ ws, int nb, int Np, kair_wmap mp, float* out, int acc) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= mp.N) return;
+  const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += ws[(long)b * Np + np];
+  out[n] = acc ? out[n] + s : s;
+}
+
+template <typename T>
+__global__ void image_to_nhwc_kernel(const float* __restrict__ img, T* __restrict__ out, int ldc,
+                                     const float* __restrict__ mean, float range, int C, long HW, long total) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const long pix = t / ldc;
+  const int c = (int)(t - pix * ldc);
+  float v = 0.f;
+  if (c < C) {
+    const long b = pix / HW, p = pix - b * HW;
+    v = (img[(b * C + c) * HW + p] - (mean ? mean[c] : 0.f)) * range;
+  }
+  out[t] = (T)v;
+}
+
+template <typename T>
+__global__ void l1_kernel(const float* __restrict__ E, const float* __restrict__ H, T* __restrict__ dE, int ldc, float gscale,
+                          int C, long HW, long npix, float* __restrict__ ws) {
+  __shared__ float red[256];
+  float s = 0.f;
+  const long total = npix * ldc;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long pix = t / ldc;
+    const int c = (int)(t - pix * ldc);
+    float g = 0.f;
+    if (c < C) {
+      const long b = pix / HW, p = pix - b * HW;
+      const long i = (b * C + c) * HW + p;
+      const float d = E[i] - H[i];
+      s += fabsf(d);
+      g = d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f);
+    }
+    dE[t] = (T)g;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ws[blockIdx.x] = red[0];
+}
+
+__global__ void l1_final(const float* __restrict__ ws, int nb, float scale, float* out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) s += ws[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0] * scale;
+}
+
+// lr_t[0] = step_size = lr / (1 - b1^t),  lr_t[1] = sqrt(1 - b2^t)
+__global__ void adam_ema_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                float* __restrict__ v, float* __restrict__ ema, long n, const float* __restrict__ lr_t,
+                                float b1, float b2, float eps, float wd, float decay) {
+  const float step = lr_t[0], bc2s = lr_t[1];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    float pi = p[i];
+    if (wd != 0.f) gi = gi + wd * pi;
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);  // lerp_(g, 1-b1)
+    float vi = v[i] * b2;
+    vi = vi + (1.f - b2) * (gi * gi);   // mul_(b2).addcmul_(g, g, 1-b2)
+    const float denom = sqrtf(vi) / bc2s + eps;
+    pi = pi + (-step) * (mi / denom);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    if (ema) ema[i] = ema[i] * decay + (1.f - decay) * pi;
+  }
+}
+
+inline unsigned nblk(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+extern "C" int kair_pack_weight(const float* src, void* dst, int dst_dtype, const kair_wmap* map, void* stream) {
+  KAIR_CHECK_ARG(src && dst && map, "pack_weight: null pointer");
+  const kair_wmap& mp = *map;
+  KAIR_CHECK_ARG(mp.nG > 0 && mp.nGr > 0 && mp.nGp >= mp.nGr && mp.nG * mp.nGr == mp.N, "pack_weight: bad N map");
+  KAIR_CHECK_ARG(mp.kind == 4 || (mp.kG > 0 && mp.kGr > 0 && mp.kGp >= mp.kGr && mp.kG * mp.kGr == mp.K),
+                 "pack_weight: bad K map");
+  const long Np = (long)mp.nG * mp.nGp, Kp = (long)mp.kG * mp.kGp;
+  long total;
+  if (mp.kind == 0 || mp.kind == 3) total = Np * Kp;
+  else if (mp.kind == 1 || mp.kind == 2) total = Np * 9 * Kp;
+  else if (mp.kind == 4) total = Np;
+  else return kair_set_error(KAIR_ERR_ARG, "pack_weight: bad kind %d", mp.kind);
+  hipLaunchKernelGGL(pack_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, src, dst, dst_dtype, mp, total);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_wgrad_finalize(const float* partial, int splits, const kair_wmap* map, float* grad_ref,
+                                   float* bias_grad, int ones_col, int accumulate, void* stream) {
+  KAIR_CHECK_ARG(partial && map && grad_ref && splits > 0, "wgrad_finalize: null pointer");
+  const kair_wmap& mp = *map;
+  KAIR_CHECK_ARG(mp.kind == 0 || mp.kind == 1, "wgrad_finalize: kind must be 0 (linear) or 1 (conv)");
+  KAIR_CHECK_ARG(!bias_grad || ones_col >= 0, "wgrad_finalize: bias needs ones_col");
+  const long Np = (long)mp.nG * mp.nGp;
+  const long Kt = mp.kind == 0 ? (long)mp.kG * mp.kGp : 9L * mp.kG * mp.kGp;
+  const long nw = (long)mp.N * mp.K * (mp.kind == 1 ? 9 : 1);
+  const long tot = nw + (bias_grad ? mp.N : 0);
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(nblk(tot, 256)), dim3(256), 0, (hipStream_t)stream, partial, splits, mp,
+                     grad_ref, bias_grad, ones_col, accumulate, nw, Kt, Np * Kt);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_colsum(const kair_operand* G, long M, int Np, const kair_wmap* map, float* bias_grad, float* ws,
+                           int accumulate, void* stream) {
+  KAIR_CHECK_ARG(G && G->ptr && map && bias_grad && ws, "colsum: null pointer");
+  KAIR_CHECK_ARG(G->mode == KAIR_LD_ROWS && G->win_ws == 0, "colsum: plain row operands only");
+  const int nb = 1024;
+  const long rows_per = (M + nb - 1) / nb;
+  dim3 grid(nb, (Np + 255) / 256);
+  hipStream_t s = (hipStream_t)stream;
+  if (G->dtype == KAIR_BF16)
+    hipLaunchKernelGGL(colsum_partial<bf16>, grid, dim3(256), 0, s, (const bf16*)G->ptr, G->ld, M, Np, ws, rows_per);
+  else
+    hipLaunchKernelGGL(colsum_partial<float>, grid, dim3(256), 0, s, (const float*)G->ptr, G->ld, M, Np, ws, rows_per);
+  KAIR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_final, dim3(nblk(map->N, 256)), dim3(256), 0, s, ws, nb, Np, *map, bias_grad, accumulate);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_image_to_nhwc(const float* img, void* out, int dtype, int ldc, const float* mean, float img_range,
+                                  int B, int C, int H, int W, void* stream) {
+  KAIR_CHECK_ARG(img && out && ldc >= C, "image_to_nhwc: bad args");
+  const long total = (long)B * H * W * ldc;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == KAIR_BF16)
+    hipLaunchKernelGGL(image_to_nhwc_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, s, img, (bf16*)out, ldc, mean,
+                       img_range, C, (long)H * W, total);
+  else
+    hipLaunchKernelGGL(image_to_nhwc_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, img, (float*)out, ldc, mean,
+                       img_range, C, (long)H * W, total);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, float weight,
+                            int B, int C, int Hh, int Ww, float* ws, void* stream) {
+  KAIR_CHECK_ARG(E && H && loss_out && dE && ws && ldc >= C, "l1_loss: bad args");
+  const long npix = (long)B * Hh * Ww;
+  const double numel = (double)npix * C;
+  const int nb = 1024;
+  hipStream_t s = (hipStream_t)stream;
+  const float gs = (float)(weight / numel);
+  if (dtype == KAIR_BF16)
+    hipLaunchKernelGGL(l1_kernel<bf16>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, ldc, gs, C, (long)Hh * Ww, npix, ws);
+  else
+    hipLaunchKernelGGL(l1_kernel<float>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, ldc, gs, C, (long)Hh * Ww, npix, ws);
+  KAIR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_adam_ema(float* p, const float* g, float* m, float* v, float* ema, long n, const float* lr_t,
+                             float beta1, float beta2, float eps, float weight_decay, float ema_decay, void* stream) {
+  KAIR_CHECK_ARG(p && g && m && v && lr_t && n > 0, "adam_ema: bad args");
+  long nb = (n + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(adam_ema_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n, lr_t,
+                     beta1, beta2, eps, weight_decay, ema_decay);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,524 @@
+// Fused Swin window attention for gfx950 (network_swinir.py:114-145, WindowAttention.forward):
+//   S = (q*scale) k^T + table[relative_position_index] (+ shifted-window region mask, -100)
+//   P = softmax(S) ; O = P v          per (window, head), window 8x8 = 64 tokens, head_dim <= 32
+// and its backward (dq, dk, dv, d table), flash-style: P is recomputed from q, k and the saved
+// row log-sum-exp, nothing of size 64x64 per (window, head) touches HBM.
+//
+// One wave64 owns one (window, head) tile at a time; q/k/v (4 KB each in bf16) are staged
+// global -> LDS with 16-byte coalesced loads.  bf16 mode uses v_mfma_f32_32x32x16_bf16, the
+// accumulator of the first product feeds the second directly as an MFMA operand (k order permuted
+// in-register, the other operand fetched with ds_read_b64_tr_b16 in the matching order).  fp32
+// (parity) mode uses v_mfma_f32_32x32x2_f32 with the same dataflow.  The relative position bias
+// and the shift mask are computed from indices (no 64x64 tables are read).
+#include "common.h"
+
+namespace {
+
+constexpr int WS = 8, TOK = 64, HDP = 32;
+template <bool BF> constexpr int NWAVES = BF ? 4 : 2;  // fp32 tiles need twice the LDS
+
+template <bool BF> struct AT {
+  using T = typename std::conditional<BF, bf16, float>::type;
+  static constexpr int LD = BF ? 40 : 33;  // LDS row stride (elements) of a [64][32] tile
+};
+
+// Each wave works only on its own LDS slice, so a wave-local fence replaces __syncthreads (waves of
+// a block may run different trip counts).  LDS operations of one wave complete in issue order.
+KAIR_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+KAIR_DEV int relidx(int q, int k) { return ((q >> 3) - (k >> 3) + WS - 1) * (2 * WS - 1) + ((q & 7) - (k & 7) + WS - 1); }
+
+KAIR_DEV int region(int coord, int n, int shift) { return coord < n - WS ? 0 : (coord < n - shift ? 1 : 2); }
+
+// region id of token t of window `wi` (index within the image) on the shifted H x W grid
+KAIR_DEV int token_region(int wi, int t, int H, int W, int shift) {
+  const int nWw = W / WS;
+  const int wy = wi / nWw, wx = wi - wy * nWw;
+  return region(wy * WS + (t >> 3), H, shift) * 3 + region(wx * WS + (t & 7), W, shift);
+}
+
+// stage a [64][32] tile (element type T in global, contiguous rows of `ld` elements starting at
+// column c0) into LDS with row stride LD
+template <bool BF>
+KAIR_DEV void stage_tile(typename AT<BF>::T* lds, const typename AT<BF>::T* g, long ld, int lane) {
+  using T = typename AT<BF>::T;
+  constexpr int LD = AT<BF>::LD;
+  constexpr int EPC = 16 / sizeof(T);              // elements per 16-byte chunk
+  constexpr int CPR = HDP / EPC;                   // chunks per row
+#pragma unroll
+  for (int i = 0; i < TOK * CPR / 64; ++i) {
+    const int c = lane + 64 * i;
+    const int row = c / CPR, col = (c % CPR) * EPC;
+    if constexpr (BF) {
+      *(bf16x8*)(lds + row * LD + col) = *(const bf16x8*)(g + row * ld + col);
+    } else {
+      const float4 v = *(const float4*)(g + row * ld + col);
+      float* d = (float*)lds + row * LD + col;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+  }
+}
+
+typedef short __attribute__((ext_vector_type(8))) short8v;
+
+KAIR_DEV bf16x8 tr_read8(const bf16* p0, const bf16* p1) {
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)p0);
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)p1);
+  const short8v s = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, s);
+}
+
+// B fragment (32x32x16) of a row-major [64][32] LDS tile X, contraction over X's rows in the
+// PERMUTED order produced by using a 32x32 accumulator as the other operand:
+// element j of lane half h <-> row base + 16*s + 8*(j>>2) + 4*h + (j&3), column = lane&31.
+KAIR_DEV bf16x8 frag_rows_perm(const bf16* X, int base, int s, int lane) {
+  constexpr int LD = AT<true>::LD;
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int h = G >> 1, c0 = (G & 1) * 16;
+  const bf16* a = X + (base + 16 * s + 4 * h + q) * LD + c0 + 4 * p;
+  return tr_read8(a, a + 8 * LD);
+}
+// same, natural order: element j of lane half h <-> row base + 16*s + 8*h + j
+KAIR_DEV bf16x8 frag_rows_nat(const bf16* X, int base, int s, int lane) {
+  constexpr int LD = AT<true>::LD;
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int h = G >> 1, c0 = (G & 1) * 16;
+  const bf16* a = X + (base + 16 * s + 8 * h + q) * LD + c0 + 4 * p;
+  return tr_read8(a, a + 4 * LD);
+}
+// A/B fragment from a row-major tile where the lane's row is `row` and the 8 contiguous
+// contraction elements start at column 16*s + 8*(lane>>5)
+KAIR_DEV bf16x8 frag_cols(const bf16* X, int ld, int row, int s, int lane) {
+  return *(const bf16x8*)(X + row * ld + 16 * s + 8 * (lane >> 5));
+}
+
+KAIR_DEV bf16x8 pack8(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
+  return r;
+}
+
+// accumulator row (within a 32x32 tile) held by register r of lane half h
+KAIR_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <bool BF>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const typename AT<BF>::T* __restrict__ qkv,
+                                                       const float* __restrict__ table, typename AT<BF>::T* __restrict__ O,
+                                                       long ldo, float* __restrict__ lse, long nWin, int nh, float scale,
+                                                       int H, int W, int shift) {
+  using T = typename AT<BF>::T;
+  constexpr int LD = AT<BF>::LD;
+  constexpr int WAVES = NWAVES<BF>;
+  __shared__ __attribute__((aligned(16))) T sQ[WAVES][TOK * LD];
+  __shared__ __attribute__((aligned(16))) T sK[WAVES][TOK * LD];
+  __shared__ __attribute__((aligned(16))) T sV[WAVES][TOK * LD];
+  __shared__ float sTab[WAVES][232];
+  __shared__ int sReg[WAVES][TOK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long task = (long)blockIdx.x * WAVES + w;
+  if (task >= nWin * nh) return;
+  const long win = task / nh;
+  const int h = (int)(task - win * nh);
+  const long M = nWin * TOK;
+  const long blk = (win * nh + h) * TOK * HDP;
+  const long part = M * nh * HDP;
+  T* q = sQ[w]; T* k = sK[w]; T* v = sV[w];
+  stage_tile<BF>(q, qkv + blk, HDP, lane);
+  stage_tile<BF>(k, qkv + part + blk, HDP, lane);
+  stage_tile<BF>(v, qkv + 2 * part + blk, HDP, lane);
+  for (int i = lane; i < (2 * WS - 1) * (2 * WS - 1); i += 64) sTab[w][i] = table[i * nh + h];
+  const int nW = (H / WS) * (W / WS);
+  const int wi = (int)(win % nW);
+  sReg[w][lane] = shift > 0 ? token_region(wi, lane, H, W, shift) : 0;
+  wave_sync();
+
+  // S^T = K Q^T : tiles [kt][qt], lane column = query, registers = keys
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int l31 = lane & 31, hh = lane >> 5;
+  if constexpr (BF) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 fk[2], fq[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        fk[t] = frag_cols(k, LD, t * 32 + l31, s, lane);
+        fq[t] = frag_cols(q, LD, t * 32 + l31, s, lane);
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+          acc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk[kt], fq[qt], acc[kt][qt], 0, 0, 0);
+    }
+  } else {
+#pragma unroll 4
+    for (int s = 0; s < HDP / 2; ++s) {
+      float fk[2], fq[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        fk[t] = k[(t * 32 + l31) * LD + 2 * s + hh];
+        fq[t] = q[(t * 32 + l31) * LD + 2 * s + hh];
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+          acc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(fk[kt], fq[qt], acc[kt][qt], 0, 0, 0);
+    }
+  }
+  // scores: scale, bias, mask ; softmax over keys (registers + lane^32)
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = qt * 32 + l31;
+    const int rq = sReg[w][qi];
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ki = kt * 32 + acc_row(r, hh);
+        float sc = acc[kt][qt][r] * scale + sTab[w][relidx(qi, ki)];
+        if (shift > 0 && sReg[w][ki] != rq) sc += -100.f;
+        acc[kt][qt][r] = sc;
+        mx = fmaxf(mx, sc);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __expf(acc[kt][qt][r] - mx);
+        acc[kt][qt][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[kt][qt][r] *= inv;
+    if (hh == 0) lse[task * TOK + qi] = mx + __logf(sum);
+  }
+  // O = P V : out tile [qt] rows = query, columns = d (lane)
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    f32x16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    if constexpr (BF) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pack8(acc[kt][qt], s), frag_rows_perm(v, kt * 32, s, lane), o, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          o = __builtin_amdgcn_mfma_f32_32x32x2f32(acc[kt][qt][s], v[(kt * 32 + acc_row(s, hh)) * LD + l31], o, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = qt * 32 + acc_row(r, hh);
+      O[(win * TOK + qi) * ldo + h * HDP + l31] = (T)o[r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward: one wave per (head, group of windows); dS summed over the group in registers for the
+// relative-position-bias gradient
+// ------------------------------------------------------------------------------------------
+template <bool BF>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(const typename AT<BF>::T* __restrict__ qkv,
+                                                       const typename AT<BF>::T* __restrict__ O, long ldo,
+                                                       const typename AT<BF>::T* __restrict__ dO, long lddo,
+                                                       const float* __restrict__ table, const float* __restrict__ lse,
+                                                       typename AT<BF>::T* __restrict__ dqkv, float* __restrict__ dB_part,
+                                                       long nWin, int nh, int wpg, float scale, int H, int W, int shift) {
+  using T = typename AT<BF>::T;
+  constexpr int LD = AT<BF>::LD;
+  constexpr int WAVES = NWAVES<BF>;
+  constexpr int LDS_ = 72;  // dS tile row stride (bf16: 144 B; fp32 reads use 65)
+  __shared__ __attribute__((aligned(16))) T sQ[WAVES][TOK * LD];
+  __shared__ __attribute__((aligned(16))) T sK[WAVES][TOK * LD];
+  __shared__ __attribute__((aligned(16))) T sV[WAVES][TOK * LD];
+  __shared__ __attribute__((aligned(16))) T sdO[WAVES][TOK * LD];
+  __shared__ __attribute__((aligned(16))) T sdS[WAVES][TOK * (BF ? LDS_ : 65)];
+  __shared__ float sTab[WAVES][232];
+  __shared__ float sRow[WAVES][2][TOK];  // lse, delta
+  __shared__ int sReg[WAVES][TOK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long gtask = (long)blockIdx.x * WAVES + w;
+  const long ngroups = (nWin + wpg - 1) / wpg;
+  if (gtask >= ngroups * nh) return;
+  const int h = (int)(gtask % nh);
+  const long grp = gtask / nh;
+  const long M = nWin * TOK;
+  const long part = M * nh * HDP;
+  const int l31 = lane & 31, hh = lane >> 5;
+  T* q = sQ[w]; T* k = sK[w]; T* v = sV[w]; T* go = sdO[w]; T* ds = sdS[w];
+  for (int i = lane; i < (2 * WS - 1) * (2 * WS - 1); i += 64) sTab[w][i] = table[i * nh + h];
+  const int nW = (H / WS) * (W / WS);
+
+  // dS accumulator for the bias gradient: S-layout tiles [qt][kt], lane = key, regs = query
+  f32x16 dB[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dB[a][b][r] = 0.f;
+
+  const long w0 = grp * wpg;
+  long w1 = w0 + wpg;
+  if (w1 > nWin) w1 = nWin;
+  for (long win = w0; win < w1; ++win) {
+    const long blk = (win * nh + h) * TOK * HDP;
+    wave_sync();
+    stage_tile<BF>(q, qkv + blk, HDP, lane);
+    stage_tile<BF>(k, qkv + part + blk, HDP, lane);
+    stage_tile<BF>(v, qkv + 2 * part + blk, HDP, lane);
+    stage_tile<BF>(go, dO + win * TOK * lddo + h * HDP, lddo, lane);
+    {
+      // delta[q] = sum_d dO[q][d] * O[q][d]  (lane = query)
+      const T* orow = O + (win * TOK + lane) * ldo + h * HDP;
+      const T* grow = dO + (win * TOK + lane) * lddo + h * HDP;
+      float d = 0.f;
+#pragma unroll
+      for (int c = 0; c < HDP; ++c) d += (float)orow[c] * (float)grow[c];
+      sRow[w][1][lane] = d;
+      sRow[w][0][lane] = lse[((long)win * nh + h) * TOK + lane];
+      sReg[w][lane] = shift > 0 ? token_region((int)(win % nW), lane, H, W, shift) : 0;
+    }
+    wave_sync();
+
+    // S = Q K^T and dP = dO V^T : tiles [qt][kt], lane = key, regs = query
+    f32x16 S[2][2], dP[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { S[a][b][r] = 0.f; dP[a][b][r] = 0.f; }
+    if constexpr (BF) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 fq[2], fk[2], fg[2], fv[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          fq[t] = frag_cols(q, LD, t * 32 + l31, s, lane);
+          fk[t] = frag_cols(k, LD, t * 32 + l31, s, lane);
+          fg[t] = frag_cols(go, LD, t * 32 + l31, s, lane);
+          fv[t] = frag_cols(v, LD, t * 32 + l31, s, lane);
+        }
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            S[qt][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fq[qt], fk[kt], S[qt][kt], 0, 0, 0);
+            dP[qt][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fg[qt], fv[kt], dP[qt][kt], 0, 0, 0);
+          }
+      }
+    } else {
+#pragma unroll 4
+      for (int s = 0; s < HDP / 2; ++s) {
+        float fq[2], fk[2], fg[2], fv[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          fq[t] = q[(t * 32 + l31) * LD + 2 * s + hh];
+          fk[t] = k[(t * 32 + l31) * LD + 2 * s + hh];
+          fg[t] = go[(t * 32 + l31) * LD + 2 * s + hh];
+          fv[t] = v[(t * 32 + l31) * LD + 2 * s + hh];
+        }
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            S[qt][kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(fq[qt], fk[kt], S[qt][kt], 0, 0, 0);
+            dP[qt][kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(fg[qt], fv[kt], dP[qt][kt], 0, 0, 0);
+          }
+      }
+    }
+    // P = exp(S*scale + bias + mask - lse) ; dS = P (dP - delta)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int ki = kt * 32 + l31;
+      const int rk = sReg[w][ki];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = qt * 32 + acc_row(r, hh);
+          float sc = S[qt][kt][r] * scale + sTab[w][relidx(qi, ki)];
+          if (shift > 0 && sReg[w][qi] != rk) sc += -100.f;
+          const float p = __expf(sc - sRow[w][0][qi]);
+          S[qt][kt][r] = p;
+          const float d = p * (dP[qt][kt][r] - sRow[w][1][qi]);
+          dP[qt][kt][r] = d;
+          dB[qt][kt][r] += d;
+        }
+    }
+    // dV = P^T dO and dK = scale * dS^T Q : tiles [kt], rows = key, lane = d
+    T* dq_out = dqkv + blk;
+    T* dk_out = dqkv + part + blk;
+    T* dv_out = dqkv + 2 * part + blk;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      f32x16 av, ak;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { av[r] = 0.f; ak[r] = 0.f; }
+      if constexpr (BF) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            av = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pack8(S[qt][kt], s), frag_rows_perm(go, qt * 32, s, lane), av, 0, 0, 0);
+            ak = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pack8(dP[qt][kt], s), frag_rows_perm(q, qt * 32, s, lane), ak, 0, 0, 0);
+          }
+      } else {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            const int qr = (qt * 32 + acc_row(s, hh)) * LD + l31;
+            av = __builtin_amdgcn_mfma_f32_32x32x2f32(S[qt][kt][s], go[qr], av, 0, 0, 0);
+            ak = __builtin_amdgcn_mfma_f32_32x32x2f32(dP[qt][kt][s], q[qr], ak, 0, 0, 0);
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ki = kt * 32 + acc_row(r, hh);
+        dv_out[ki * HDP + l31] = (T)av[r];
+        dk_out[ki * HDP + l31] = (T)(ak[r] * scale);
+      }
+    }
+    // dQ = scale * dS K : dS through LDS ([q][key] row-major)
+    constexpr int LDD = BF ? LDS_ : 65;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ds[(qt * 32 + acc_row(r, hh)) * LDD + kt * 32 + l31] = (T)dP[qt][kt][r];
+    wave_sync();
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 aq;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) aq[r] = 0.f;
+      if constexpr (BF) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          aq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_cols(ds, LDD, qt * 32 + l31, s, lane),
+                                                      frag_rows_nat(k, 0, s, lane), aq, 0, 0, 0);
+      } else {
+#pragma unroll 8
+        for (int s = 0; s < 32; ++s)
+          aq = __builtin_amdgcn_mfma_f32_32x32x2f32(ds[(qt * 32 + l31) * LDD + 2 * s + hh], k[(2 * s + hh) * LD + l31], aq,
+                                                   0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq_out[(qt * 32 + acc_row(r, hh)) * HDP + l31] = (T)(aq[r] * scale);
+    }
+  }
+  // partial bias gradient of this (group, head): [q][key]
+  float* out = dB_part + (grp * nh + h) * TOK * TOK;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[(qt * 32 + acc_row(r, hh)) * TOK + kt * 32 + l31] = dB[qt][kt][r];
+}
+
+// dtable[idx][h] (+)= sum_groups sum_{(q,k): relidx(q,k)=idx} dB_part[g][h][q][k]
+__global__ void attn_dtable_kernel(const float* __restrict__ dB_part, long ngroups, int nh, float* dtable, int acc) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nidx = (2 * WS - 1) * (2 * WS - 1);
+  if (t >= nidx * nh) return;
+  const int idx = t / nh, h = t - (t / nh) * nh;
+  const int dy = idx / (2 * WS - 1) - (WS - 1), dx = idx % (2 * WS - 1) - (WS - 1);
+  float s = 0.f;
+  for (long g = 0; g < ngroups; ++g) {
+    const float* p = dB_part + (g * nh + h) * TOK * TOK;
+    for (int qy = 0; qy < WS; ++qy) {
+      const int ky = qy - dy;
+      if (ky < 0 || ky >= WS) continue;
+      for (int qx = 0; qx < WS; ++qx) {
+        const int kx = qx - dx;
+        if (kx < 0 || kx >= WS) continue;
+        s += p[(qy * WS + qx) * TOK + ky * WS + kx];
+      }
+    }
+  }
+  dtable[idx * nh + h] = acc ? dtable[idx * nh + h] + s : s;
+}
+
+constexpr int WPG = 4;  // windows per backward wave
+
+}  // namespace
+
+extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
+                                    long nWin, int nh, int hd, float scale, int H, int W, int shift, void* stream) {
+  KAIR_CHECK_ARG(qkv && table && O && lse, "window_attn_fwd: null pointer");
+  KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_fwd: head_dim %d must be <= 32", hd);
+  KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)),
+                 "window_attn_fwd: grid %dx%d / shift %d", H, W, shift);
+  KAIR_CHECK_ARG(ldo >= nh * HDP && ldo % 8 == 0, "window_attn_fwd: ldo");
+  const long tasks = nWin * nh;
+  const int nw = dtype == KAIR_BF16 ? NWAVES<true> : NWAVES<false>;
+  const long nb = (tasks + nw - 1) / nw;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == KAIR_BF16)
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
+                       lse, nWin, nh, scale, H, W, shift);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, table, (float*)O,
+                       ldo, lse, nWin, nh, scale, H, W, shift);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) { return ((nWin + WPG - 1) / WPG) * nh * TOK * TOK; }
+
+extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
+                                    const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
+                                    float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
+                                    void* stream) {
+  KAIR_CHECK_ARG(qkv && O && dO && table && lse && dqkv && dtable && ws, "window_attn_bwd: null pointer");
+  KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_bwd: head_dim");
+  KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)), "window_attn_bwd: geometry");
+  KAIR_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0, "window_attn_bwd: strides");
+  const long ngroups = (nWin + WPG - 1) / WPG;
+  const int nw = dtype == KAIR_BF16 ? NWAVES<true> : NWAVES<false>;
+  const long nb = (ngroups * nh + nw - 1) / nw;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == KAIR_BF16)
+    hipLaunchKernelGGL(attn_bwd_kernel<true>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
+                       (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, WPG, scale, H, W, shift);
+  else
+    hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
+                       ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, WPG, scale, H, W, shift);
+  KAIR_CHECK_LAUNCH();
+  const int nt = (2 * WS - 1) * (2 * WS - 1) * nh;
+  hipLaunchKernelGGL(attn_dtable_kernel, dim3((nt + 127) / 128), dim3(128), 0, s, ws, ngroups, nh, dtable,
+                     dtable_accumulate);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}

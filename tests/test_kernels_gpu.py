@@ -1,0 +1,303 @@
+"""Per-kernel parity on the MI355X: every libkair_hip entry point against a plain fp32 PyTorch
+reference of the same op (CPU, float64 where cheap).  fp32 compute mode must match to ~1e-5
+relative (exact fp32 MFMA); bf16 mode to bf16 rounding (~1e-2 relative)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from kair_amd import _hip as H  # noqa: E402
+from oracle.swinir import relative_position_index, shift_region_mask  # noqa: E402
+
+dev = torch.device("cuda")
+TOL = {H.F32: (2e-5, 2e-5), H.BF16: (2e-2, 2e-2)}
+DT = {H.F32: torch.float32, H.BF16: torch.bfloat16}
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def win_perm(B, Hh, Ww, ws, shift):
+    """row m (window order) -> token index, as the kernels' WinMap does"""
+    idx = torch.arange(B * Hh * Ww).view(B, Hh, Ww)
+    idx = torch.roll(idx, (-shift, -shift), (1, 2))
+    return idx.view(B, Hh // ws, ws, Ww // ws, ws).permute(0, 1, 3, 2, 4).reshape(-1)
+
+
+@pytest.mark.parametrize("compute", [H.F32, H.BF16])
+@pytest.mark.parametrize("M,N,K", [(1000, 576, 192), (4096, 180, 192), (333, 16, 72), (2048, 64, 1728)])
+def test_gemm_nt_rows(compute, M, N, K):
+    g = torch.Generator().manual_seed(M + N)
+    a = torch.randn(M, K, generator=g)
+    b = torch.randn(N, K, generator=g) * 0.1
+    bias = torch.randn(N, generator=g)
+    ref = a.double() @ b.double().T + bias.double()
+    A = a.to(dev, DT[compute])
+    Bw = b.to(dev, DT[compute])
+    out = torch.empty(M, N, device=dev)
+    H.gemm_nt(H.rows(A), H.rows(Bw), H.epilogue(out, bias=bias.to(dev)), M, N, K, compute)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < TOL[compute][0]
+
+
+@pytest.mark.parametrize("compute", [H.F32, H.BF16])
+def test_gemm_window_map_gelu_resid(compute):
+    B, Hh, Ww, ws, shift, C, N = 2, 16, 24, 8, 4, 64, 96
+    M = B * Hh * Ww
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(M, C, generator=g)
+    w = torch.randn(N, C, generator=g) * 0.1
+    res = torch.randn(M, N, generator=g)
+    perm = win_perm(B, Hh, Ww, ws, shift)
+    win = (Hh, Ww, ws, shift)
+    # A gathered through the window map, output scattered back to token rows, + residual
+    out = torch.empty(M, N, device=dev)
+    pre = torch.empty(M, N, device=dev)
+    H.gemm_nt(H.rows(x.to(dev, DT[compute]), win=win), H.rows(w.to(dev, DT[compute])),
+              H.epilogue(out, win=win, act=H.ACT_GELU, pre=pre, resid=res.to(dev)), M, N, C, compute)
+    torch.cuda.synchronize()
+    y_win = x[perm] @ w.T                      # rows in window order
+    ref = torch.empty(M, N)
+    ref[perm] = torch.nn.functional.gelu(y_win)
+    ref += res
+    pref = torch.empty(M, N)
+    pref[perm] = y_win
+    assert rel_err(out, ref) < TOL[compute][0]
+    assert rel_err(pre, pref) < TOL[compute][0]
+
+
+@pytest.mark.parametrize("compute", [H.F32, H.BF16])
+@pytest.mark.parametrize("flip", [False, True])
+def test_conv3x3_implicit_gemm(compute, flip):
+    B, Hh, Ww, Cin, Cout = 2, 12, 20, 24, 40
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, Cin, Hh, Ww, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1
+    if flip:  # dgrad: conv of dy with the transposed kernel == conv_transpose
+        ref = torch.nn.functional.conv_transpose2d(x, w.transpose(0, 1).contiguous(), padding=1)  # Cin->Cout flipped
+        wk = w.transpose(0, 1).contiguous()  # [Cin_as_out? ] build packed [Cout][9*Cin] for transpose conv
+        # conv_transpose2d(x, W') with W' [Cin, Cout, 3, 3] == sum_tap x[p - off] W'[ci, co, tap]
+        packed = wk.permute(1, 2, 3, 0).reshape(Cout, 9 * Cin)  # [co][tap*Cin + ci] = W'[ci][co][tap]
+    else:
+        ref = torch.nn.functional.conv2d(x, w, padding=1)
+        packed = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)  # [co][tap*Cin + ci]
+    xin = x.permute(0, 2, 3, 1).contiguous().view(B * Hh * Ww, Cin)
+    out = torch.empty(B * Hh * Ww, Cout, device=dev)
+    H.gemm_nt(H.im2col(xin.to(dev, DT[compute]), Hh, Ww, Cin, flip=flip), H.rows(packed.to(dev, DT[compute])),
+              H.epilogue(out), B * Hh * Ww, Cout, 9 * Cin, compute)
+    torch.cuda.synchronize()
+    got = out.cpu().view(B, Hh, Ww, Cout).permute(0, 3, 1, 2)
+    assert rel_err(got, ref) < TOL[compute][0]
+
+
+@pytest.mark.parametrize("compute", [H.F32, H.BF16])
+def test_conv_pixelshuffle_and_nchw(compute):
+    B, Hh, Ww, Cin, r = 2, 8, 8, 16, 2
+    Cout = 8 * r * r
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(B, Cin, Hh, Ww, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1
+    bias = torch.randn(Cout, generator=g)
+    ref = torch.nn.functional.pixel_shuffle(torch.nn.functional.conv2d(x, w, bias, padding=1), r)
+    xin = x.permute(0, 2, 3, 1).contiguous().view(-1, Cin).to(dev, DT[compute])
+    packed = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin).to(dev, DT[compute])
+    out = torch.empty(B * Hh * r * Ww * r, 8, device=dev)
+    H.gemm_nt(H.im2col(xin, Hh, Ww, Cin), H.rows(packed),
+              H.epilogue(out, mode=H.OUT_PSHUF, bias=bias.to(dev), ps=(r, Hh, Ww)), B * Hh * Ww, Cout, 9 * Cin, compute)
+    torch.cuda.synchronize()
+    assert rel_err(out.cpu().view(B, Hh * r, Ww * r, 8).permute(0, 3, 1, 2), ref) < TOL[compute][0]
+    # NCHW image epilogue with mean/range
+    mean = torch.tensor([0.1, 0.2, 0.3])
+    w3 = torch.randn(3, Cin, 3, 3, generator=g) * 0.1
+    img = torch.empty(B, 3, Hh, Ww, device=dev)
+    p3 = torch.zeros(16, 9 * Cin)
+    p3[:3] = w3.permute(0, 2, 3, 1).reshape(3, 9 * Cin)
+    H.gemm_nt(H.im2col(xin, Hh, Ww, Cin), H.rows(p3.to(dev, DT[compute])),
+              H.epilogue(img, mode=H.OUT_NCHW, ldo=0, img=(mean.to(dev), 1.0, 3, Hh, Ww)), B * Hh * Ww, 16, 9 * Cin,
+              compute)
+    torch.cuda.synchronize()
+    ref3 = torch.nn.functional.conv2d(x, w3, padding=1) + mean.view(1, 3, 1, 1)
+    assert rel_err(img, ref3) < TOL[compute][0]
+
+
+@pytest.mark.parametrize("compute", [H.F32, H.BF16])
+@pytest.mark.parametrize("M,N,K", [(5000, 576, 192), (4096, 64, 64), (777, 192, 384)])
+def test_gemm_tn_wgrad(compute, M, N, K):
+    g = torch.Generator().manual_seed(11)
+    dy = torch.randn(M, N, generator=g)
+    x = torch.randn(M, K, generator=g)
+    ones = K - 3
+    xr = x.clone()
+    xr[:, ones] = 1.0
+    ref = dy.double().T @ xr.double()
+    S = H.wgrad_splits(M, N, K)
+    ws = torch.empty(S, N, K, device=dev)
+    H.gemm_tn(H.rows(dy.to(dev, DT[compute])), H.rows(x.to(dev, DT[compute]), ones_col=ones), ws, S, M, N, K, compute)
+    torch.cuda.synchronize()
+    got = ws.sum(0).cpu()
+    assert rel_err(got, ref) < TOL[compute][0]
+    # finalize into reference layout [N][K-?] with bias from the ones column
+    m = H.wmap(0, N, ones, (1, N, N), (1, ones, K))
+    grad = torch.empty(N, ones, device=dev)
+    bg = torch.empty(N, device=dev)
+    H.wgrad_finalize(ws, S, m, grad, bg, ones)
+    torch.cuda.synchronize()
+    assert rel_err(grad, ref[:, :ones]) < TOL[compute][0]
+    assert rel_err(bg, dy.double().sum(0)) < TOL[compute][0]
+
+
+@pytest.mark.parametrize("compute", [H.F32, H.BF16])
+def test_conv_wgrad_im2col(compute):
+    B, Hh, Ww, Cin, Cout = 2, 10, 12, 16, 24
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(B, Cin, Hh, Ww, generator=g, requires_grad=True)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, requires_grad=True)
+    y = torch.nn.functional.conv2d(x, w, padding=1)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    M = B * Hh * Ww
+    dy = gy.permute(0, 2, 3, 1).reshape(M, Cout)
+    xin = x.detach().permute(0, 2, 3, 1).reshape(M, Cin)
+    K = 9 * Cin
+    S = H.wgrad_splits(M, Cout, K)
+    ws = torch.empty(S, Cout, K, device=dev)
+    H.gemm_tn(H.rows(dy.to(dev, DT[compute])), H.im2col(xin.contiguous().to(dev, DT[compute]), Hh, Ww, Cin), ws, S, M, Cout,
+              K, compute)
+    grad = torch.empty(Cout, Cin, 3, 3, device=dev)
+    H.wgrad_finalize(ws, S, H.wmap(1, Cout, Cin), grad)
+    torch.cuda.synchronize()
+    assert rel_err(grad, w.grad) < TOL[compute][0]
+
+
+@pytest.mark.parametrize("dtype", [H.F32, H.BF16])
+@pytest.mark.parametrize("win", [(0, 0, 0, 0), (16, 16, 8, 4)])
+def test_layernorm(dtype, win):
+    M, C, ld = 2 * 256, 180, 192
+    g = torch.Generator().manual_seed(17)
+    x = torch.zeros(M, ld)
+    x[:, :C] = torch.randn(M, C, generator=g) * 2 + 0.5
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.1
+    xr = x[:, :C].clone().requires_grad_(True)
+    gm, bt = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    y = torch.nn.functional.layer_norm(xr, (C,), gm, bt, 1e-5)
+    gy = torch.randn(M, C, generator=g)
+    y.backward(gy)
+    perm = win_perm(2, 16, 16, 8, 4) if win[2] else torch.arange(M)
+    xd = x.to(dev)
+    yo = torch.empty(M, ld, device=dev, dtype=DT[dtype])
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    H.layernorm_fwd(xd, ld, yo, ld, gamma.to(dev), beta.to(dev), mean, rstd, M, C, 1e-5, win)
+    torch.cuda.synchronize()
+    assert rel_err(yo[:, :C].float(), y.detach()[perm]) < TOL[dtype][0]
+    assert yo[:, C:].abs().max().item() == 0
+    dy = torch.zeros(M, ld)
+    dy[:, :C] = gy[perm]
+    dx = torch.ones(M, ld, device=dev)  # accumulate onto ones
+    dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    ws = torch.empty(2 * 1024 * C, device=dev)
+    H.layernorm_bwd(xd, ld, dy.to(dev, DT[dtype]), ld, gamma.to(dev), mean, rstd, dx, ld, True, dg, db, False, ws, M, C, win)
+    torch.cuda.synchronize()
+    assert rel_err(dx[:, :C] - 1, xr.grad) < TOL[dtype][0]
+    assert rel_err(dg, gm.grad) < TOL[dtype][0]
+    assert rel_err(db, bt.grad) < TOL[dtype][0]
+
+
+def _attn_ref(q, k, v, table, nh, shift, Hh, Ww, scale):
+    """q,k,v [nWin, nh, 64, hd] fp32 -> O [nWin, 64, nh, hd] and grads helper"""
+    idx = relative_position_index(8)
+    bias = table[idx.view(-1)].view(64, 64, nh).permute(2, 0, 1)
+    s = (q * scale) @ k.transpose(-2, -1) + bias
+    if shift:
+        mask = shift_region_mask(Hh, Ww, 8, shift)
+        nW = mask.shape[0]
+        s = (s.view(-1, nW, nh, 64, 64) + mask[None, :, None]).view(-1, nh, 64, 64)
+    return torch.softmax(s, -1) @ v
+
+
+@pytest.mark.parametrize("dtype", [H.F32, H.BF16])
+@pytest.mark.parametrize("shift", [0, 4])
+def test_window_attention_fwd_bwd(dtype, shift):
+    B, Hh, Ww, nh, hd = 2, 16, 24, 6, 30
+    nWin = B * (Hh // 8) * (Ww // 8)
+    scale = hd ** -0.5
+    g = torch.Generator().manual_seed(19)
+    q = torch.randn(nWin, nh, 64, hd, generator=g)
+    k = torch.randn(nWin, nh, 64, hd, generator=g)
+    v = torch.randn(nWin, nh, 64, hd, generator=g)
+    table = torch.randn(225, nh, generator=g) * 0.5
+    if dtype == H.BF16:  # compare on the bf16-rounded inputs
+        q, k, v = (t.bfloat16().float() for t in (q, k, v))
+    qr, kr, vr, tr = (t.clone().requires_grad_(True) for t in (q, k, v, table))
+    o = _attn_ref(qr, kr, vr, tr, nh, shift, Hh, Ww, scale)
+    go = torch.randn(o.shape, generator=g)
+    if dtype == H.BF16:
+        go = go.bfloat16().float()
+    o.backward(go)
+    # pack into the head-blocked padded layout [3][nWin][nh][64][32]
+    qkv = torch.zeros(3, nWin, nh, 64, 32)
+    qkv[0, ..., :hd], qkv[1, ..., :hd], qkv[2, ..., :hd] = q, k, v
+    qkv_d = qkv.to(dev, DT[dtype]).contiguous()
+    O = torch.empty(nWin * 64, nh * 32, device=dev, dtype=DT[dtype])
+    lse = torch.empty(nWin, nh, 64, device=dev)
+    H.window_attn_fwd(qkv_d, table.to(dev), O, nh * 32, lse, nWin, nh, hd, scale, Hh, Ww, shift)
+    torch.cuda.synchronize()
+    got = O.float().cpu().view(nWin, 64, nh, 32)[..., :hd].permute(0, 2, 1, 3)
+    tol = 2e-5 if dtype == H.F32 else 1.5e-2
+    assert rel_err(got, o.detach()) < tol
+    assert O.float().cpu().view(nWin, 64, nh, 32)[..., hd:].abs().max() == 0
+    dO = torch.zeros(nWin, 64, nh, 32)
+    dO[..., :hd] = go.permute(0, 2, 1, 3)
+    dqkv = torch.empty_like(qkv_d)
+    dtab = torch.empty(225, nh, device=dev)
+    ws = torch.empty(H.window_attn_bwd_ws(nWin, nh), device=dev)
+    H.window_attn_bwd(qkv_d, O, nh * 32, dO.view(nWin * 64, nh * 32).to(dev, DT[dtype]), nh * 32, table.to(dev), lse,
+                      dqkv, dtab, False, ws, nWin, nh, hd, scale, Hh, Ww, shift)
+    torch.cuda.synchronize()
+    d = dqkv.float().cpu()
+    tolb = 5e-5 if dtype == H.F32 else 3e-2
+    assert rel_err(d[0, ..., :hd], qr.grad) < tolb
+    assert rel_err(d[1, ..., :hd], kr.grad) < tolb
+    assert rel_err(d[2, ..., :hd], vr.grad) < tolb
+    assert rel_err(dtab, tr.grad) < tolb
+
+
+def test_l1_and_adam():
+    g = torch.Generator().manual_seed(23)
+    E = torch.rand(2, 3, 8, 8, generator=g)
+    Hh = torch.rand(2, 3, 8, 8, generator=g)
+    Er = E.clone().requires_grad_(True)
+    loss = torch.nn.functional.l1_loss(Er, Hh)
+    loss.backward()
+    out = torch.empty(1, device=dev)
+    dE = torch.empty(2 * 64, 16, device=dev)
+    ws = torch.empty(1024, device=dev)
+    H.l1_loss(E.to(dev), Hh.to(dev), out, dE, 16, 1.0, 2, 3, 8, 8, ws)
+    torch.cuda.synchronize()
+    assert abs(out.item() - loss.item()) < 1e-6
+    assert rel_err(dE.cpu().view(2, 8, 8, 16)[..., :3].permute(0, 3, 1, 2), Er.grad) < 1e-6
+    # Adam + EMA against torch.optim.Adam (single tensor) for 3 steps
+    p = torch.randn(1000, generator=g)
+    pt = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=2e-4, betas=(0.9, 0.999), foreach=False)
+    ema_ref = p.clone()
+    pd, md, vd = p.to(dev), torch.zeros(1000, device=dev), torch.zeros(1000, device=dev)
+    ed = p.to(dev)
+    for t in range(1, 4):
+        grad = torch.randn(1000, generator=g)
+        pt.grad = grad.clone()
+        opt.step()
+        with torch.no_grad():
+            ema_ref.mul_(0.999).add_(pt, alpha=0.001)
+        lr_t = torch.tensor([2e-4 / (1 - 0.9 ** t), math.sqrt(1 - 0.999 ** t)], device=dev)
+        H.adam_ema(pd, grad.to(dev), md, vd, ed, 1000, lr_t, 0.9, 0.999, 1e-8, 0.0, 0.999)
+    torch.cuda.synchronize()
+    assert rel_err(pd, pt.detach()) < 1e-6
+    assert rel_err(ed, ema_ref) < 1e-6
