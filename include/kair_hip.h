@@ -58,8 +58,10 @@ typedef enum {
                              -> out NHWC [b, y*r+i, x*r+j, c] with channel stride ldo          */
   KAIR_OUT_PUNSHUF = 3,   /* inverse: m = pixel of the [ps_H*r, ps_W*r] image, n = c
                              -> out[(b,y,x) of ps_H x ps_W][c*r*r+i*r+j], stride ldo          */
-  KAIR_OUT_NCHW = 4       /* image out[b][n][y][x] (n < img_C) of [img_H, img_W],
+  KAIR_OUT_NCHW = 4,      /* image out[b][n][y][x] (n < img_C) of [img_H, img_W],
                              value = v / img_range + img_mean[n]                              */
+  KAIR_OUT_PSHUF_NCHW = 5 /* PixelShuffle(r) straight into an NCHW image [b][c][y*r+i][x*r+j]
+                             (c < img_C), value = v / img_range + img_mean[c]  (UpsampleOneStep) */
 } kair_out_mode;
 
 typedef enum { KAIR_ACT_NONE = 0, KAIR_ACT_GELU = 1, KAIR_ACT_LEAKY = 2, KAIR_ACT_RELU = 3 } kair_act;
@@ -111,7 +113,7 @@ int kair_pack_weight(const float* src, void* dst, int dst_dtype, const kair_wmap
 int kair_wgrad_finalize(const float* partial, int splits, const kair_wmap* map, float* grad_ref,
                         float* bias_grad, int ones_col, int accumulate, void* stream);
 /* bias_grad[n_ref] (+)= sum_m G[m][n]  for an operand G of width Np (conv biases without a pad
- * column).  ws: 1024 * N floats. */
+ * column).  ws: 1024 * Np floats. */
 int kair_colsum(const kair_operand* G, long M, int Np, const kair_wmap* map, float* bias_grad,
                 float* ws, int accumulate, void* stream);
 
@@ -151,12 +153,15 @@ int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* d
 int kair_image_to_nhwc(const float* img, void* out, int dtype, int ldc, const float* mean, float img_range,
                        int B, int C, int H, int W, void* stream);
 /* L1 loss (nn.L1Loss, mean): loss_out[0] = weight*mean|E-H|; grad dE = weight*sign(E-H)/numel written
- * NHWC (dtype, channel stride ldc) for the last conv's dgrad.  ws: 1024 floats. */
-int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, float weight,
+ * for the last conv's dgrad: NHWC (dtype, channel stride ldc) when ps_r == 1, or in the
+ * pre-PixelShuffle(ps_r) layout [b][y/r][x/r][c*r*r + (y%r)*r + x%r] otherwise.  ws: 1024 floats. */
+int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, int ps_r, float weight,
                  int B, int C, int Hh, int Ww, float* ws, void* stream);
+/* y[i] += a * x[i] over n fp32 elements (residual-gradient merges). */
+int kair_axpy(float* y, const float* x, float a, long n, void* stream);
 /* Fused Adam (torch.optim.Adam maths, model_plain.py:210-222,302) + EMA (model_base.py:247-252)
- * over flat fp32 buffers.  step_lr[0] = lr, step_lr[1] = t (incremented in-kernel by a
- * single thread after use is NOT done: caller passes t). ema may be NULL. */
+ * over flat fp32 buffers.  lr_t is a DEVICE array {lr / (1 - beta1^t), sqrt(1 - beta2^t)} written by
+ * the host before each (graph-replayed) step; ema may be NULL (E_decay = 0). */
 int kair_adam_ema(float* p, const float* g, float* m, float* v, float* ema, long n, const float* lr_t,
                   float beta1, float beta2, float eps, float weight_decay, float ema_decay, void* stream);
 

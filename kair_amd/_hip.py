@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libk
 
 F32, BF16 = 0, 1
 LD_ROWS, LD_IM2COL3, LD_QKVBLK = 0, 1, 2
-OUT_ROWS, OUT_QKVBLK, OUT_PSHUF, OUT_PUNSHUF, OUT_NCHW = 0, 1, 2, 3, 4
+OUT_ROWS, OUT_QKVBLK, OUT_PSHUF, OUT_PUNSHUF, OUT_NCHW, OUT_PSHUF_NCHW = 0, 1, 2, 3, 4, 5
 ACT_NONE, ACT_GELU, ACT_LEAKY, ACT_RELU = 0, 1, 2, 3
 
 c_long, c_int, c_float, c_vp = ctypes.c_long, ctypes.c_int, ctypes.c_float, ctypes.c_void_p
@@ -63,7 +63,8 @@ _SIGS = {
     "kair_window_attn_bwd": [c_vp, c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_int,
                              c_int, c_float, c_int, c_int, c_int, c_vp],
     "kair_image_to_nhwc": [c_vp, c_vp, c_int, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
-    "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "kair_axpy": [c_vp, c_vp, c_float, c_long, c_vp],
     "kair_adam_ema": [c_vp, c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
@@ -268,9 +269,13 @@ def image_to_nhwc(img, out, ldc, mean, img_range, B, C, H, W):
                                    stream_ptr()), "image_to_nhwc")
 
 
-def l1_loss(E, H, loss_out, dE, ldc, weight, B, C, Hh, Ww, ws):
-    check(lib().kair_l1_loss(ptr(E), ptr(H), ptr(loss_out), ptr(dE), dtype_code(dE), ldc, weight, B, C, Hh, Ww, ptr(ws),
-                             stream_ptr()), "l1_loss")
+def l1_loss(E, H, loss_out, dE, ldc, weight, B, C, Hh, Ww, ws, ps_r=1):
+    check(lib().kair_l1_loss(ptr(E), ptr(H), ptr(loss_out), ptr(dE), dtype_code(dE), ldc, ps_r, weight, B, C, Hh, Ww,
+                             ptr(ws), stream_ptr()), "l1_loss")
+
+
+def axpy(y, x, a, n=None):
+    check(lib().kair_axpy(ptr(y), ptr(x), a, n if n is not None else y.numel(), stream_ptr()), "axpy")
 
 
 def adam_ema(p, g, m, v, ema, n, lr_t, beta1, beta2, eps, wd, decay):

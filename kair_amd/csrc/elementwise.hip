@@ -112,18 +112,24 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ img, T* __restric
 }
 
 template <typename T>
-__global__ void l1_kernel(const float* __restrict__ E, const float* __restrict__ H, T* __restrict__ dE, int ldc, float gscale,
-                          int C, long HW, long npix, float* __restrict__ ws) {
+__global__ void l1_kernel(const float* __restrict__ E, const float* __restrict__ H, T* __restrict__ dE, int ldc, int r,
+                          float gscale, int C, int Hh, int Ww, long npix, float* __restrict__ ws) {
+  // dE element t = (pixel of the [Hh/r, Ww/r] grid, channel slot); slot -> (c, i, j) when r > 1
   __shared__ float red[256];
   float s = 0.f;
   const long total = npix * ldc;
+  const int hs = Hh / r, wsm = Ww / r, r2 = r * r;
+  const long HW = (long)Hh * Ww;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
     const long pix = t / ldc;
-    const int c = (int)(t - pix * ldc);
+    const int slot = (int)(t - pix * ldc);
+    const int c = slot / r2, ij = slot - c * r2;
     float g = 0.f;
     if (c < C) {
-      const long b = pix / HW, p = pix - b * HW;
-      const long i = (b * C + c) * HW + p;
+      const long b = pix / ((long)hs * wsm);
+      const int pp = (int)(pix - b * hs * wsm);
+      const int y = (pp / wsm) * r + ij / r, x = (pp % wsm) * r + ij % r;
+      const long i = (b * C + c) * HW + (long)y * Ww + x;
       const float d = E[i] - H[i];
       s += fabsf(d);
       g = d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f);
@@ -172,6 +178,18 @@ __global__ void adam_ema_kernel(float* __restrict__ p, const float* __restrict__
     p[i] = pi;
     if (ema) ema[i] = ema[i] * decay + (1.f - decay) * pi;
   }
+}
+
+__global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, float a, long n) {
+  const long n4 = n / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 yv = ((float4*)y)[i];
+    const float4 xv = ((const float4*)x)[i];
+    yv.x += a * xv.x; yv.y += a * xv.y; yv.z += a * xv.z; yv.w += a * xv.w;
+    ((float4*)y)[i] = yv;
+  }
+  for (long i = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] += a * x[i];
 }
 
 inline unsigned nblk(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -244,18 +262,19 @@ extern "C" int kair_image_to_nhwc(const float* img, void* out, int dtype, int ld
   return 0;
 }
 
-extern "C" int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, float weight,
-                            int B, int C, int Hh, int Ww, float* ws, void* stream) {
-  KAIR_CHECK_ARG(E && H && loss_out && dE && ws && ldc >= C, "l1_loss: bad args");
-  const long npix = (long)B * Hh * Ww;
-  const double numel = (double)npix * C;
+extern "C" int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, int ps_r,
+                            float weight, int B, int C, int Hh, int Ww, float* ws, void* stream) {
+  KAIR_CHECK_ARG(E && H && loss_out && dE && ws && ps_r >= 1 && ldc >= C * ps_r * ps_r, "l1_loss: bad args");
+  KAIR_CHECK_ARG(Hh % ps_r == 0 && Ww % ps_r == 0, "l1_loss: image not divisible by r");
+  const long npix = (long)B * (Hh / ps_r) * (Ww / ps_r);
+  const double numel = (double)B * Hh * Ww * C;
   const int nb = 1024;
   hipStream_t s = (hipStream_t)stream;
   const float gs = (float)(weight / numel);
   if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(l1_kernel<bf16>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, ldc, gs, C, (long)Hh * Ww, npix, ws);
+    hipLaunchKernelGGL(l1_kernel<bf16>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
   else
-    hipLaunchKernelGGL(l1_kernel<float>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, ldc, gs, C, (long)Hh * Ww, npix, ws);
+    hipLaunchKernelGGL(l1_kernel<float>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
   KAIR_CHECK_LAUNCH();
   hipLaunchKernelGGL(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);
   KAIR_CHECK_LAUNCH();
@@ -269,6 +288,16 @@ extern "C" int kair_adam_ema(float* p, const float* g, float* m, float* v, float
   if (nb > 8192) nb = 8192;
   hipLaunchKernelGGL(adam_ema_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n, lr_t,
                      beta1, beta2, eps, weight_decay, ema_decay);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_axpy(float* y, const float* x, float a, long n, void* stream) {
+  KAIR_CHECK_ARG(y && x && n >= 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)x % 16) == 0, "axpy: bad args");
+  long nb = (n / 4 + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(axpy_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, y, x, a, n);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

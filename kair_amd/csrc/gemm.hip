@@ -179,6 +179,15 @@ KAIR_DEV void epi_store(const Epi& e, long m, int n, float v) {
       v *= (e.gkind == 2) ? (g > 0.f ? 1.f : e.slope) : (g > 0.f ? 1.f : 0.f);
     }
     st(e.out, e.odt, orow * e.ldo + oc, v);
+  } else if (e.omode == KAIR_OUT_PSHUF_NCHW) {
+    const int r = e.r, r2 = r * r;
+    const int c = n / r2, ij = n - c * r2, i = ij / r, j = ij - i * r;
+    if (c >= e.imgC) return;
+    const long hw = (long)e.psH * e.psW;
+    const long b = m / hw;
+    const int p = (int)(m - b * hw), y = p / e.psW, x = p - (p / e.psW) * e.psW;
+    v = v / e.range + (e.mean ? e.mean[c] : 0.f);
+    ((float*)e.out)[((b * e.imgC + c) * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + j] = v;
   } else {  // NCHW image
     if (n >= e.imgC) return;
     const long hw = (long)e.imgH * e.imgW;

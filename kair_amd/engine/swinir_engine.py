@@ -1,0 +1,569 @@
+"""SwinIR step program for MI355X: the whole forward and backward of network_swinir.py as an
+explicit sequence of libkair_hip launches over preallocated HBM buffers.
+
+Reference call stack replaced: SwinIR.forward network_swinir.py:805-839 ->
+forward_features :790-803 -> RSTB.forward :481-482 -> SwinTransformerBlock.forward :239-279 ->
+WindowAttention.forward :114-145 / Mlp.forward :24-30.
+
+Layout: tokens are rows of NHWC matrices; channels padded C -> Cp (a multiple of
+32 with at least one spare column that serves as the fused bias-gradient "ones" column); heads
+padded hd -> 32; MLP hidden Hd -> Hdp.  The residual stream and every tensor a LayerNorm reads
+are fp32; GEMM operands are bf16 (or fp32 in parity mode); accumulation is fp32.  Window
+partition + cyclic shift never materialise: LayerNorm-1 writes window-ordered rows, the proj
+epilogue scatters back to token order.  PixelShuffle is a store remap of the upsampling conv.
+
+The program is launch-only (no host syncs, no allocation after planning), so a whole training
+step can be captured in a HIP graph (kair_amd/engine/trainer.py).
+"""
+import math
+import weakref
+
+import torch
+
+from .. import _hip as H
+
+WS_TOK = 64
+
+
+def _rup(x, m):
+    return (x + m - 1) // m * m
+
+
+def swinir_flops(net, Hh, Ww):
+    """Dense-contraction FLOPs per patch (GEMM + conv, 2 per MAC), the quantity FlopCounterMode
+    reports (60.25 G fwd / 180.73 G train for classical x4 @48)."""
+    C = net.embed_dim
+    HW = Hh * Ww
+    f = 2 * HW * 9 * net.conv_first.in_channels * C                       # conv_first
+    for layer in net.layers:
+        for blk in layer.residual_group.blocks:
+            Hd = blk.mlp.fc1.out_features
+            f += 2 * HW * C * 3 * C + 2 * HW * C * C                      # qkv, proj
+            f += 2 * 2 * HW * (blk.window_size ** 2) * C                 # q k^T, p v
+            f += 2 * 2 * HW * C * Hd                                     # fc1, fc2
+        f += 2 * HW * 9 * C * C                                           # RSTB conv
+    f += 2 * HW * 9 * C * C                                               # conv_after_body
+    first_dgrad = 2 * HW * 9 * net.conv_first.in_channels * C
+    if net.upsampler == "pixelshuffle":
+        nf = 64
+        f += 2 * HW * 9 * C * nf
+        hw = HW
+        for m in net.upsample:
+            if isinstance(m, torch.nn.Conv2d):
+                f += 2 * hw * 9 * nf * m.out_channels
+                hw *= m.out_channels // nf
+        f += 2 * hw * 9 * nf * net.conv_last.out_channels
+    else:
+        conv = net.upsample[0]
+        f += 2 * HW * 9 * C * conv.out_channels
+    return {"fwd": f, "train": 3 * f - first_dgrad}
+
+
+class _Lin:
+    """A linear layer's packed forms.  n/k groupings map reference rows/cols to padded ones."""
+
+    def __init__(self, eng, mod, n_grp, k_grp):
+        self.w, self.b = mod.weight, mod.bias
+        N, K = self.w.shape
+        self.N, self.K = N, K
+        self.map = H.wmap(0, N, K, n_grp, k_grp)
+        self.mapT = H.wmap(3, N, K, n_grp, k_grp)
+        self.mapb = H.wmap(4, N, 0, n_grp, (1, 1, 1))
+        self.Np = n_grp[0] * n_grp[2]
+        self.Kp = k_grp[0] * k_grp[2]
+        dev = self.w.device
+        self.Wp = torch.empty(self.Np, self.Kp, device=dev, dtype=eng.tdt)
+        self.Wt = torch.empty(self.Kp, self.Np, device=dev, dtype=eng.tdt)
+        self.bp = torch.empty(self.Np, device=dev)
+
+    def pack(self):
+        H.pack_weight(self.w.detach(), self.Wp, self.map)
+        H.pack_weight(self.w.detach(), self.Wt, self.mapT)
+        H.pack_weight(self.b.detach(), self.bp, self.mapb)
+
+
+class _Conv:
+    """A 3x3 conv's packed forms: forward [Cop][9*Cip] and input-gradient [Cip][9*Cop]."""
+
+    def __init__(self, eng, mod, Cop, Cip, need_dgrad=True):
+        self.w, self.b = mod.weight, mod.bias
+        Co, Ci = self.w.shape[:2]
+        self.Co, self.Ci, self.Cop, self.Cip = Co, Ci, Cop, Cip
+        self.map = H.wmap(1, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
+        self.mapd = H.wmap(2, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
+        self.mapb = H.wmap(4, Co, 0, (1, Co, Cop), (1, 1, 1))
+        dev = self.w.device
+        self.Wf = torch.empty(Cop, 9 * Cip, device=dev, dtype=eng.tdt)
+        self.Wd = torch.empty(Cip, 9 * Cop, device=dev, dtype=eng.tdt) if need_dgrad else None
+        self.bp = torch.empty(Cop, device=dev)
+
+    def pack(self):
+        H.pack_weight(self.w.detach(), self.Wf, self.map)
+        if self.Wd is not None:
+            H.pack_weight(self.w.detach(), self.Wd, self.mapd)
+        H.pack_weight(self.b.detach(), self.bp, self.mapb)
+
+
+class _Blk:
+    def __init__(self, eng, blk):
+        C, Cp, nh = eng.C, eng.Cp, eng.nh
+        hd = C // nh
+        self.mod = blk
+        self.shift = blk.shift_size
+        self.dp = blk.drop_path_rate
+        self.n1, self.n2 = blk.norm1, blk.norm2
+        self.table = blk.attn.relative_position_bias_table
+        self.scale = blk.attn.scale
+        Hd = blk.mlp.fc1.out_features
+        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp))
+        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32))
+        self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp))
+        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp))
+
+    def linears(self):
+        return (self.qkv, self.proj, self.fc1, self.fc2)
+
+
+class SwinIREngine:
+    def __init__(self, net, compute_dtype="bf16"):
+        self.net_ref = weakref.ref(net)
+        if compute_dtype not in ("bf16", "fp32"):
+            raise ValueError(compute_dtype)
+        self.cd = H.BF16 if compute_dtype == "bf16" else H.F32
+        self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
+        self.C = net.embed_dim
+        heads = {l.residual_group.blocks[0].num_heads for l in net.layers}
+        if len(heads) != 1:
+            raise NotImplementedError("kair_amd SwinIR: per-stage head counts must match")
+        self.nh = heads.pop()
+        hd = self.C // self.nh
+        if hd >= 32 or self.C % self.nh:
+            raise NotImplementedError("kair_amd SwinIR: head_dim must be < 32")
+        self.ws = net.window_size
+        if self.ws != 8:
+            raise NotImplementedError("kair_amd SwinIR: window_size 8 only (fused attention tile)")
+        self.Cp = _rup(self.C + 1, 32)
+        Hd = net.layers[0].residual_group.blocks[0].mlp.fc1.out_features
+        self.Hdp = _rup(Hd + 1, 32)
+        self.upsampler, self.scale = net.upsampler, net.upscale
+        self.in_ch = net.conv_first.in_channels
+        self.img_range = float(net.img_range)
+        self.Cin_p = 8
+        self.device = net.conv_first.weight.device
+        dev = self.device
+        self.mean = net.mean.view(-1).to(dev, torch.float32).contiguous()
+        # layer objects
+        self.conv_first = _Conv(self, net.conv_first, self.Cp, self.Cin_p, need_dgrad=False)
+        self.pe_norm = net.patch_embed.norm
+        self.rstb = []
+        for layer in net.layers:
+            blks = [_Blk(self, b) for b in layer.residual_group.blocks]
+            self.rstb.append((blks, _Conv(self, layer.conv, self.Cp, self.Cp)))
+        self.norm = net.norm
+        self.cab = _Conv(self, net.conv_after_body, self.Cp, self.Cp)
+        nf = 64
+        if self.upsampler == "pixelshuffle":
+            self.cbu = _Conv(self, net.conv_before_upsample[0], nf, self.Cp)
+            self.ups = []
+            for m in net.upsample:
+                if isinstance(m, torch.nn.Conv2d):
+                    self.ups.append(_Conv(self, m, m.out_channels, nf))
+            self.ups_r = [int(math.isqrt(c.Co // nf)) for c in self.ups]
+            self.last = _Conv(self, net.conv_last, 16, nf)
+        elif self.upsampler == "pixelshuffledirect":
+            conv = net.upsample[0]
+            self.ups_r = [self.scale]
+            self.up1 = _Conv(self, conv, _rup(conv.out_channels, 16), self.Cp)
+        else:
+            raise NotImplementedError(self.upsampler)
+        self.blocks = [b for blks, _ in self.rstb for b in blks]
+        self.plans = {}
+        self._packed_version = None
+
+    # ------------------------------------------------------------------------------------
+    def convs(self):
+        cs = [self.conv_first] + [c for _, c in self.rstb] + [self.cab]
+        if self.upsampler == "pixelshuffle":
+            cs += [self.cbu] + self.ups + [self.last]
+        else:
+            cs += [self.up1]
+        return cs
+
+    def pack(self, force=False):
+        net = self.net_ref()
+        ver = None if force else tuple(p._version for p in net.parameters())
+        if ver is not None and ver == self._packed_version:
+            return
+        for c in self.convs():
+            c.pack()
+        for b in self.blocks:
+            for l in b.linears():
+                l.pack()
+        self._packed_version = ver
+
+    def plan(self, B, Hh, Ww):
+        key = (B, Hh, Ww)
+        if key in self.plans:
+            return self.plans[key]
+        dev, T, f32 = self.device, self.tdt, torch.float32
+        M = B * Hh * Ww
+        Cp, Hdp, nh = self.Cp, self.Hdp, self.nh
+        nWin = M // WS_TOK
+        e = lambda *s, dt=f32: torch.empty(*s, device=dev, dtype=dt)
+        P = {"B": B, "H": Hh, "W": Ww, "M": M, "nWin": nWin}
+        P["xin"] = e(M, self.Cin_p, dt=T)
+        P["f0"] = e(M, Cp)
+        P["pe_mean"], P["pe_rstd"] = e(M), e(M)
+        P["s0"] = e(M, Cp)
+        blocks = []
+        for _ in self.blocks:
+            blocks.append({
+                "mid": e(M, Cp), "out": e(M, Cp), "ln1": e(M, Cp, dt=T), "m1": e(M), "r1": e(M),
+                "qkv": e(3 * M * nh * 32, dt=T), "O": e(M, nh * 32, dt=T), "lse": e(nWin * nh * WS_TOK),
+                "ln2": e(M, Cp, dt=T), "m2": e(M), "r2": e(M), "u": e(M, Hdp, dt=T), "h": e(M, Hdp, dt=T)})
+        P["blocks"] = blocks
+        P["rstb_out"] = [e(M, Cp) for _ in self.rstb]
+        P["nf"], P["n_mean"], P["n_rstd"] = e(M, Cp), e(M), e(M)
+        P["fb"] = e(M, Cp)
+        if self.upsampler == "pixelshuffle":
+            nf = 64
+            P["a0"] = e(M, nf, dt=T)
+            acts, hw = [], M
+            for r in self.ups_r:
+                hw *= r * r
+                acts.append(e(hw, nf, dt=T))
+            P["ups_act"] = acts
+            P["M_hr"] = hw
+        P["E"] = e(B, self.in_ch, Hh * self.scale, Ww * self.scale)
+        # backward scratch
+        P["D"], P["G"] = e(M, Cp), e(M, Cp)
+        P["dU"], P["dxn"] = e(M, Hdp, dt=T), e(M, Cp, dt=T)
+        P["dO"], P["dqkv"] = e(M, nh * 32, dt=T), e(3 * M * nh * 32, dt=T)
+        P["ln_ws"] = e(2 * 1024 * Cp)
+        P["attn_ws"] = e(H.window_attn_bwd_ws(nWin, nh))
+        P["loss"] = e(1)
+        P["loss_ws"] = e(1024)
+        P["colsum_ws"] = e(1024 * 256)
+        if self.upsampler == "pixelshuffle":
+            P["dE"] = e(P["M_hr"], 16, dt=T)
+            dpre, hw = [], M
+            for c in self.ups:
+                dpre.append(e(hw, c.Co, dt=T))
+                hw *= c.Co // 64
+            P["dpre"] = dpre
+            P["da0"] = e(M, 64, dt=T)
+        else:
+            P["dE"] = e(M, self.up1.Cop, dt=T)
+        P["dfb"] = e(M, Cp)
+        # one shared wgrad workspace sized for the largest (splits * N * K)
+        P["wg_ws"] = e(self._max_wgrad_ws(M, P))
+        self.plans[key] = P
+        return P
+
+    def _wgrad_shapes(self, M, P):
+        """(M_rows, N, K) of every weight-gradient GEMM in the step."""
+        Cp, Hdp, nh = self.Cp, self.Hdp, self.nh
+        out = [(M, Cp, 9 * self.Cin_p)]
+        for blks, conv in self.rstb:
+            for _ in blks:
+                out += [(M, Cp, Hdp), (M, Hdp, Cp), (M, Cp, nh * 32), (M, 3 * nh * 32, Cp)]
+            out.append((M, Cp, 9 * Cp))
+        out.append((M, Cp, 9 * Cp))
+        if self.upsampler == "pixelshuffle":
+            out.append((M, 64, 9 * Cp))
+            hw = M
+            for c in self.ups:
+                out.append((hw, c.Co, 9 * 64))
+                hw *= c.Co // 64
+            out.append((hw, 16, 9 * 64))
+        else:
+            out.append((M, self.up1.Cop, 9 * Cp))
+        return out
+
+    def _max_wgrad_ws(self, M, P):
+        return max(H.wgrad_splits(m, n, k) * n * k for m, n, k in self._wgrad_shapes(M, P))
+
+    # ------------------------------------------------------------------------------------
+    # forward
+    # ------------------------------------------------------------------------------------
+    def forward(self, x, drop_scales=None):
+        """x: [B, in_ch, H, W] fp32 on the device (H, W multiples of 8).  Returns P['E'] (NCHW fp32).
+        drop_scales: optional [nblocks, 2, B] fp32 DropPath scales (0 or 1/keep)."""
+        B, _, Hh, Ww = x.shape
+        P = self.plan(B, Hh, Ww)
+        self.pack()
+        cd, T = self.cd, self.tdt
+        M, Cp, nh = P["M"], self.Cp, self.nh
+        HW = Hh * Ww
+        x = x.contiguous()
+        self.cur = P
+        P["x"] = x
+        P["drop"] = drop_scales
+        H.image_to_nhwc(x, P["xin"], self.Cin_p, self.mean, self.img_range, B, self.in_ch, Hh, Ww)
+        c = self.conv_first
+        H.gemm_nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), H.rows(c.Wf), H.epilogue(P["f0"], bias=c.bp), M, Cp,
+                  9 * self.Cin_p, cd)
+        n = self.pe_norm
+        H.layernorm_fwd(P["f0"], Cp, P["s0"], Cp, n.weight, n.bias, P["pe_mean"], P["pe_rstd"], M, self.C, n.eps)
+        cur = P["s0"]
+        bi = 0
+        for gi, (blks, conv) in enumerate(self.rstb):
+            g_in = cur
+            for blk in blks:
+                cur = self._block_fwd(blk, P, P["blocks"][bi], cur, bi)
+                bi += 1
+            out = P["rstb_out"][gi]
+            H.gemm_nt(H.im2col(cur, Hh, Ww, Cp), H.rows(conv.Wf), H.epilogue(out, bias=conv.bp, resid=g_in), M, Cp,
+                      9 * Cp, cd)
+            cur = out
+        n = self.norm
+        H.layernorm_fwd(cur, Cp, P["nf"], Cp, n.weight, n.bias, P["n_mean"], P["n_rstd"], M, self.C, n.eps)
+        H.gemm_nt(H.im2col(P["nf"], Hh, Ww, Cp), H.rows(self.cab.Wf), H.epilogue(P["fb"], bias=self.cab.bp, resid=P["f0"]),
+                  M, Cp, 9 * Cp, cd)
+        img = (self.mean, self.img_range, self.in_ch, Hh * self.scale, Ww * self.scale)
+        if self.upsampler == "pixelshuffle":
+            c = self.cbu
+            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), H.rows(c.Wf),
+                      H.epilogue(P["a0"], bias=c.bp, act=H.ACT_LEAKY, slope=0.01), M, 64, 9 * Cp, cd)
+            src, h, w = P["a0"], Hh, Ww
+            for c, r, dst in zip(self.ups, self.ups_r, P["ups_act"]):
+                H.gemm_nt(H.im2col(src, h, w, 64), H.rows(c.Wf), H.epilogue(dst, mode=H.OUT_PSHUF, ldo=64, bias=c.bp,
+                                                                            ps=(r, h, w)), B * h * w, c.Co, 9 * 64, cd)
+                src, h, w = dst, h * r, w * r
+            c = self.last
+            H.gemm_nt(H.im2col(src, h, w, 64), H.rows(c.Wf),
+                      H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(self.mean, self.img_range, self.in_ch, h, w)),
+                      B * h * w, c.Cop, 9 * 64, cd)
+        else:
+            c = self.up1
+            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), H.rows(c.Wf),
+                      H.epilogue(P["E"], mode=H.OUT_PSHUF_NCHW, ldo=0, bias=c.bp, ps=(self.scale, Hh, Ww),
+                                 img=(self.mean, self.img_range, self.in_ch, Hh, Ww)), M, c.Cop, 9 * Cp, cd)
+        return P["E"]
+
+    def _block_fwd(self, blk, P, S, x, bi):
+        cd = self.cd
+        M, Cp, nh, Hh, Ww = P["M"], self.Cp, self.nh, P["H"], P["W"]
+        HW = Hh * Ww
+        win = (Hh, Ww, 8, blk.shift)
+        drop = P["drop"]
+        s_attn = drop[bi, 0] if drop is not None else None
+        s_mlp = drop[bi, 1] if drop is not None else None
+        H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps, win)
+        l = blk.qkv
+        H.gemm_nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
+                                                               qkv=(nh, 32, WS_TOK)), M, l.Np, Cp, cd)
+        H.window_attn_fwd(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale, Hh, Ww,
+                          blk.shift)
+        l = blk.proj
+        H.gemm_nt(H.rows(S["O"]), H.rows(l.Wp), H.epilogue(S["mid"], win=win, bias=l.bp, resid=x, rowscale=s_attn,
+                                                            rows_per_scale=HW), M, Cp, nh * 32, cd)
+        H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps)
+        l = blk.fc1
+        H.gemm_nt(H.rows(S["ln2"]), H.rows(l.Wp), H.epilogue(S["h"], bias=l.bp, act=H.ACT_GELU, pre=S["u"]), M, l.Np, Cp, cd)
+        l = blk.fc2
+        H.gemm_nt(H.rows(S["h"]), H.rows(l.Wp), H.epilogue(S["out"], bias=l.bp, resid=S["mid"], rowscale=s_mlp,
+                                                            rows_per_scale=HW), M, Cp, self.Hdp, cd)
+        return S["out"]
+
+    # ------------------------------------------------------------------------------------
+    # backward
+    # ------------------------------------------------------------------------------------
+    def _wgrad(self, P, A, Bop, M, N, K, layer_map, wgrad, bgrad=None, ones_col=-1):
+        S = H.wgrad_splits(M, N, K)
+        ws = P["wg_ws"]
+        H.gemm_tn(A, Bop, ws, S, M, N, K, self.cd)
+        H.wgrad_finalize(ws, S, layer_map, wgrad, bgrad, ones_col)
+
+    def _bias_colsum(self, P, G, M, Np, layer_map, bgrad):
+        H.colsum(G, M, Np, layer_map, bgrad, P["colsum_ws"])
+
+    def backward_from_loss(self, H_img, grads, loss_weight=1.0):
+        """L1 loss (mean) against H_img, then the full backward.  grads: {param: fp32 tensor to write}.
+        Returns the device loss tensor [1]."""
+        P = self.cur
+        B, Hh, Ww = P["B"], P["H"], P["W"]
+        if self.upsampler == "pixelshuffle":
+            H.l1_loss(P["E"], H_img, P["loss"], P["dE"], 16, loss_weight, B, self.in_ch, Hh * self.scale, Ww * self.scale,
+                      P["loss_ws"])
+        else:
+            H.l1_loss(P["E"], H_img, P["loss"], P["dE"], self.up1.Cop, loss_weight, B, self.in_ch, Hh * self.scale,
+                      Ww * self.scale, P["loss_ws"], ps_r=self.scale)
+        self.backward(grads, P)
+        return P["loss"]
+
+    def backward_from_grad(self, gE, grads):
+        """Backward given dL/dE (NCHW fp32), for the generic autograd path."""
+        P = self.cur
+        B, Hh, Ww = P["B"], P["H"], P["W"]
+        # dE = gE through the same layout the loss kernel writes: reuse l1 machinery is not possible,
+        # so scatter with the image->nhwc kernel (channel stride / pre-shuffle layout).
+        if self.upsampler == "pixelshuffle":
+            H.image_to_nhwc(gE.contiguous(), P["dE"], 16, None, 1.0, B, self.in_ch, Hh * self.scale, Ww * self.scale)
+        else:
+            tmp = torch.nn.functional.pixel_unshuffle(gE.contiguous(), self.scale)   # [B, C*r*r, H, W]
+            H.image_to_nhwc(tmp.contiguous(), P["dE"], self.up1.Cop, None, 1.0, B, tmp.shape[1], Hh, Ww)
+        self.backward(grads, P)
+
+    def backward(self, grads, P):
+        cd = self.cd
+        B, Hh, Ww, M = P["B"], P["H"], P["W"], P["M"]
+        Cp = self.Cp
+        g = lambda p: grads[p]
+        # ---- reconstruction tail -------------------------------------------------------
+        if self.upsampler == "pixelshuffle":
+            h, w = Hh, Ww
+            for r in self.ups_r:
+                h, w = h * r, w * r
+            c = self.last
+            src = P["ups_act"][-1]
+            # conv_last: dgrad into the pre-shuffle layout of the last upsampling conv
+            r_last = self.ups_r[-1]
+            H.gemm_nt(H.im2col(P["dE"], h, w, 16, flip=True), H.rows(c.Wd),
+                      H.epilogue(P["dpre"][-1], mode=H.OUT_PUNSHUF, ldo=self.ups[-1].Co, ps=(r_last, h // r_last, w // r_last)),
+                      B * h * w, 64, 9 * 16, cd)
+            self._wgrad(P, H.rows(P["dE"]), H.im2col(src, h, w, 64), B * h * w, 16, 9 * 64, c.map, g(c.w))
+            self._bias_colsum(P, H.rows(P["dE"]), B * h * w, 16, c.mapb, g(c.b))
+            # upsampling convs, last to first
+            for i in range(len(self.ups) - 1, -1, -1):
+                c, r = self.ups[i], self.ups_r[i]
+                h, w = h // r, w // r
+                dpre = P["dpre"][i]
+                src = P["ups_act"][i - 1] if i > 0 else P["a0"]
+                if i > 0:
+                    rp = self.ups_r[i - 1]
+                    H.gemm_nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),
+                              H.epilogue(P["dpre"][i - 1], mode=H.OUT_PUNSHUF, ldo=self.ups[i - 1].Co, ps=(rp, h // rp, w // rp)),
+                              B * h * w, 64, 9 * c.Co, cd)
+                else:
+                    H.gemm_nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),
+                              H.epilogue(P["da0"], gate=P["a0"], gate_kind=2, slope=0.01), M, 64, 9 * c.Co, cd)
+                self._wgrad(P, H.rows(dpre), H.im2col(src, h, w, 64), B * h * w, c.Co, 9 * 64, c.map, g(c.w))
+                self._bias_colsum(P, H.rows(dpre), B * h * w, c.Co, c.mapb, g(c.b))
+            c = self.cbu
+            H.gemm_nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)
+            self._wgrad(P, H.rows(P["da0"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, 64, 9 * Cp, c.map,
+                        g(c.w), g(c.b), self.C)
+        else:
+            c = self.up1
+            H.gemm_nt(H.im2col(P["dE"], Hh, Ww, c.Cop, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * c.Cop, cd)
+            self._wgrad(P, H.rows(P["dE"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, c.Cop, 9 * Cp, c.map,
+                        g(c.w), g(c.b), self.C)
+        # ---- conv_after_body (fb = cab(nf) + f0) ------------------------------------------
+        c = self.cab
+        G, D = P["G"], P["D"]
+        H.gemm_nt(H.im2col(P["dfb"], Hh, Ww, Cp, flip=True), H.rows(c.Wd), H.epilogue(D), M, Cp, 9 * Cp, cd)
+        self._wgrad(P, H.rows(P["dfb"]), H.im2col(P["nf"], Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, c.map, g(c.w),
+                    g(c.b), self.C)
+        # ---- final norm: nf = LN(u_G) -----------------------------------------------------
+        n = self.norm
+        last_in = P["rstb_out"][-1]
+        H.layernorm_bwd(last_in, Cp, D, Cp, n.weight, P["n_mean"], P["n_rstd"], G, Cp, False, g(n.weight), g(n.bias), False,
+                        P["ln_ws"], M, self.C)
+        # G = dL/d u_G
+        bi = len(self.blocks)
+        for gi in range(len(self.rstb) - 1, -1, -1):
+            blks, conv = self.rstb[gi]
+            t_d = P["blocks"][bi - 1]["out"]
+            # u_{g+1} = conv(t_d) + u_g : conv dgrad -> D = dL/dt_d
+            H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(conv.Wd), H.epilogue(D), M, Cp, 9 * Cp, cd)
+            self._wgrad(P, H.rows(G), H.im2col(t_d, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, conv.map, g(conv.w),
+                        g(conv.b), self.C)
+            for j in range(len(blks) - 1, -1, -1):
+                bi -= 1
+                x_in = P["blocks"][bi - 1]["out"] if j > 0 else (P["rstb_out"][gi - 1] if gi > 0 else P["s0"])
+                self._block_bwd(blks[j], P, P["blocks"][bi], x_in, D, bi, grads)
+            H.axpy(G, D, 1.0)   # dL/du_g = skip + blocks path
+        # ---- patch_embed norm: s0 = LN(f0); f0 also feeds fb (long skip) --------------------
+        n = self.pe_norm
+        H.layernorm_bwd(P["f0"], Cp, G, Cp, n.weight, P["pe_mean"], P["pe_rstd"], P["dfb"], Cp, True, g(n.weight),
+                        g(n.bias), False, P["ln_ws"], M, self.C)
+        c = self.conv_first
+        self._wgrad(P, H.rows(P["dfb"]), H.im2col(P["xin"], Hh, Ww, self.Cin_p, ones_col=self.in_ch), M, Cp,
+                    9 * self.Cin_p, c.map, g(c.w), g(c.b), self.in_ch)
+
+    def _block_bwd(self, blk, P, S, x_in, D, bi, grads):
+        """D: dL/d out (fp32, token rows) -> updated in place to dL/d x_in."""
+        cd, g = self.cd, (lambda p: grads[p])
+        M, Cp, nh, Hh, Ww = P["M"], self.Cp, self.nh, P["H"], P["W"]
+        HW = Hh * Ww
+        win = (Hh, Ww, 8, blk.shift)
+        drop = P["drop"]
+        s_attn = drop[bi, 0] if drop is not None else None
+        s_mlp = drop[bi, 1] if drop is not None else None
+        hd = self.C // nh
+        # MLP: out = mid + s_mlp * fc2(gelu(fc1(LN2(mid))))
+        l = blk.fc2
+        H.gemm_nt(H.rows(D, rowscale=s_mlp, rows_per_scale=HW), H.rows(l.Wt),
+                  H.epilogue(P["dU"], gate=S["u"], gate_kind=1), M, self.Hdp, Cp, cd)
+        self._wgrad(P, H.rows(D, rowscale=s_mlp, rows_per_scale=HW), H.rows(S["h"], ones_col=l.K), M, Cp, self.Hdp, l.map,
+                    g(l.w), g(l.b), l.K)
+        l = blk.fc1
+        H.gemm_nt(H.rows(P["dU"]), H.rows(l.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
+        self._wgrad(P, H.rows(P["dU"]), H.rows(S["ln2"], ones_col=self.C), M, self.Hdp, Cp, l.map, g(l.w), g(l.b), self.C)
+        n = blk.n2
+        H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, g(n.weight), g(n.bias), False,
+                        P["ln_ws"], M, self.C)
+        # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
+        l = blk.proj
+        H.gemm_nt(H.rows(D, win=win, rowscale=s_attn, rows_per_scale=HW), H.rows(l.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp,
+                  cd)
+        self._wgrad(P, H.rows(D, win=win, rowscale=s_attn, rows_per_scale=HW), H.rows(S["O"], ones_col=hd), M, Cp,
+                    nh * 32, l.map, g(l.w), g(l.b), hd)
+        H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], P["dqkv"], g(blk.table), False,
+                          P["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
+        l = blk.qkv
+        H.gemm_nt(H.qkvblk(P["dqkv"], nh), H.rows(l.Wt), H.epilogue(P["dxn"]), M, Cp, l.Np, cd)
+        self._wgrad(P, H.qkvblk(P["dqkv"], nh), H.rows(S["ln1"], ones_col=self.C), M, l.Np, Cp, l.map, g(l.w), g(l.b),
+                    self.C)
+        n = blk.n1
+        H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, g(n.weight), g(n.bias), False,
+                        P["ln_ws"], M, self.C, win)
+
+
+class SwinIRFunction(torch.autograd.Function):
+    """The whole SwinIR forward/backward as one autograd node (params are inputs so that any
+    optimizer / DDP reducer sees ordinary .grad tensors)."""
+
+    @staticmethod
+    def forward(ctx, engine, x, *params):
+        net = engine.net_ref()
+        B, C, H0, W0 = x.shape
+        ws = engine.ws
+        ph, pw = (ws - H0 % ws) % ws, (ws - W0 % ws) % ws
+        if ph or pw:   # check_image_size (network_swinir.py:783-788)
+            x = torch.nn.functional.pad(x, (0, pw, 0, ph), "reflect")
+        drop = None
+        if net.training and torch.is_grad_enabled() and any(b.dp > 0 for b in engine.blocks):
+            drop = drop_path_scales(engine, x.shape[0], x.device)
+        E = engine.forward(x.float(), drop)
+        ctx.engine = engine
+        ctx.params = params
+        ctx.plan = engine.cur
+        out = E[:, :, :H0 * engine.scale, :W0 * engine.scale]
+        return out.clone() if (ph or pw) else E.clone()
+
+    @staticmethod
+    def backward(ctx, gE):
+        eng = ctx.engine
+        flat = torch.empty(sum(p.numel() for p in ctx.params), device=gE.device)
+        grads, off = {}, 0
+        for p in ctx.params:
+            grads[p] = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        P = ctx.plan
+        eng.cur = P
+        full = gE
+        if gE.shape[-2:] != P["E"].shape[-2:]:
+            full = torch.zeros_like(P["E"])
+            full[:, :, :gE.shape[2], :gE.shape[3]] = gE
+        eng.backward_from_grad(full.float(), grads)
+        return (None, None) + tuple(grads[p] for p in ctx.params)
+
+
+def drop_path_scales(engine, B, device, generator=None):
+    """Per-block, per-branch stochastic-depth scales (timm DropPath semantics: keep-mask / keep)."""
+    rates = torch.tensor([b.dp for b in engine.blocks], device=device)
+    keep = (1.0 - rates).view(-1, 1, 1)
+    u = torch.rand(len(engine.blocks), 2, B, device=device, generator=generator)
+    return (u < keep).float() / keep

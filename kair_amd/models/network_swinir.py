@@ -1,0 +1,246 @@
+"""SwinIR on MI355X — drop-in for /root/reference/models/network_swinir.py.
+
+The module tree, parameter names/shapes, buffers (relative_position_index int64, attn_mask on
+shifted blocks) and initialisation follow the reference (network_swinir.py:65-773), so reference
+checkpoints load strictly and define_G() callers see the same object.  The compute does NOT go
+through these submodules: SwinIR.forward hands the whole network to the HIP step program in
+kair_amd/engine/swinir_engine.py (fused window attention, implicit-GEMM convs, fused epilogues),
+exposed to autograd as one node.  There is no CPU path; a CPU input raises.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from ..engine.swinir_engine import SwinIREngine, SwinIRFunction
+
+
+def _pair(x):
+    return tuple(x) if isinstance(x, (tuple, list)) else (x, x)
+
+
+def _trunc_normal(t, std=0.02):
+    return nn.init.trunc_normal_(t, std=std, a=-2.0, b=2.0)
+
+
+def _relative_position_index(ws):
+    """network_swinir.py:92-102."""
+    ys, xs = torch.meshgrid(torch.arange(ws), torch.arange(ws), indexing="ij")
+    ys, xs = ys.flatten(), xs.flatten()
+    return (ys[:, None] - ys[None, :] + ws - 1) * (2 * ws - 1) + (xs[:, None] - xs[None, :] + ws - 1)
+
+
+def _shift_mask(H, W, ws, shift):
+    """network_swinir.py:216-237 (calculate_mask), kept only as the state_dict buffer."""
+    def region(n):
+        r = torch.zeros(n, dtype=torch.long)
+        r[n - ws:n - shift] = 1
+        r[n - shift:] = 2
+        return r
+    rid = region(H)[:, None] * 3 + region(W)[None, :]
+    win = rid.view(H // ws, ws, W // ws, ws).permute(0, 2, 1, 3).reshape(-1, ws * ws)
+    d = win[:, None, :] - win[:, :, None]
+    return torch.zeros(d.shape).masked_fill(d != 0, -100.0)
+
+
+class Mlp(nn.Module):
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.0):
+        super().__init__()
+        self.fc1 = nn.Linear(in_features, hidden_features or in_features)
+        self.act = act_layer()
+        self.fc2 = nn.Linear(hidden_features or in_features, out_features or in_features)
+        self.drop = nn.Dropout(drop)
+
+
+class WindowAttention(nn.Module):
+    def __init__(self, dim, window_size, num_heads, qkv_bias=True, qk_scale=None, attn_drop=0.0, proj_drop=0.0):
+        super().__init__()
+        self.dim, self.window_size, self.num_heads = dim, _pair(window_size), num_heads
+        self.scale = qk_scale or (dim // num_heads) ** -0.5
+        ws = self.window_size[0]
+        self.relative_position_bias_table = nn.Parameter(torch.zeros((2 * ws - 1) * (2 * ws - 1), num_heads))
+        self.register_buffer("relative_position_index", _relative_position_index(ws))
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+        _trunc_normal(self.relative_position_bias_table)
+        self.softmax = nn.Softmax(dim=-1)
+
+
+class SwinTransformerBlock(nn.Module):
+    def __init__(self, dim, input_resolution, num_heads, window_size=7, shift_size=0, mlp_ratio=4.0, qkv_bias=True,
+                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, act_layer=nn.GELU, norm_layer=nn.LayerNorm):
+        super().__init__()
+        self.dim, self.input_resolution, self.num_heads = dim, tuple(input_resolution), num_heads
+        self.window_size, self.shift_size, self.mlp_ratio = window_size, shift_size, mlp_ratio
+        if min(self.input_resolution) <= self.window_size:
+            self.shift_size, self.window_size = 0, min(self.input_resolution)
+        self.norm1 = norm_layer(dim)
+        self.attn = WindowAttention(dim, self.window_size, num_heads, qkv_bias, qk_scale, attn_drop, drop)
+        self.drop_path_rate = float(drop_path)
+        self.drop_path = nn.Identity()
+        self.norm2 = norm_layer(dim)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
+        mask = _shift_mask(*self.input_resolution, self.window_size, self.shift_size) if self.shift_size > 0 else None
+        self.register_buffer("attn_mask", mask)
+
+
+class BasicLayer(nn.Module):
+    def __init__(self, dim, input_resolution, depth, num_heads, window_size, mlp_ratio=4.0, qkv_bias=True,
+                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=nn.LayerNorm, downsample=None,
+                 use_checkpoint=False):
+        super().__init__()
+        self.dim, self.input_resolution, self.depth = dim, input_resolution, depth
+        self.blocks = nn.ModuleList([
+            SwinTransformerBlock(dim, input_resolution, num_heads, window_size, 0 if i % 2 == 0 else window_size // 2,
+                                 mlp_ratio, qkv_bias, qk_scale, drop, attn_drop,
+                                 drop_path[i] if isinstance(drop_path, list) else drop_path, norm_layer=norm_layer)
+            for i in range(depth)])
+        self.downsample = None
+
+
+class PatchEmbed(nn.Module):
+    def __init__(self, img_size=224, patch_size=4, in_chans=3, embed_dim=96, norm_layer=None):
+        super().__init__()
+        img_size, patch_size = _pair(img_size), _pair(patch_size)
+        self.img_size, self.patch_size = img_size, patch_size
+        self.patches_resolution = [img_size[0] // patch_size[0], img_size[1] // patch_size[1]]
+        self.num_patches = self.patches_resolution[0] * self.patches_resolution[1]
+        self.in_chans, self.embed_dim = in_chans, embed_dim
+        self.norm = norm_layer(embed_dim) if norm_layer is not None else None
+
+
+class PatchUnEmbed(PatchEmbed):
+    def __init__(self, img_size=224, patch_size=4, in_chans=3, embed_dim=96, norm_layer=None):
+        super().__init__(img_size, patch_size, in_chans, embed_dim, None)
+
+
+class RSTB(nn.Module):
+    def __init__(self, dim, input_resolution, depth, num_heads, window_size, mlp_ratio=4.0, qkv_bias=True,
+                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=nn.LayerNorm, downsample=None,
+                 use_checkpoint=False, img_size=224, patch_size=4, resi_connection="1conv"):
+        super().__init__()
+        if resi_connection != "1conv":
+            raise NotImplementedError("kair_amd SwinIR: resi_connection '3conv' is not on the MI355X path yet")
+        self.dim, self.input_resolution = dim, input_resolution
+        self.residual_group = BasicLayer(dim, input_resolution, depth, num_heads, window_size, mlp_ratio, qkv_bias,
+                                         qk_scale, drop, attn_drop, drop_path, norm_layer)
+        self.conv = nn.Conv2d(dim, dim, 3, 1, 1)
+        self.patch_embed = PatchEmbed(img_size, patch_size, 0, dim, None)
+        self.patch_unembed = PatchUnEmbed(img_size, patch_size, 0, dim, None)
+
+
+class Upsample(nn.Sequential):
+    def __init__(self, scale, num_feat):
+        m = []
+        if scale & (scale - 1) == 0:
+            for _ in range(int(math.log2(scale))):
+                m += [nn.Conv2d(num_feat, 4 * num_feat, 3, 1, 1), nn.PixelShuffle(2)]
+        elif scale == 3:
+            m += [nn.Conv2d(num_feat, 9 * num_feat, 3, 1, 1), nn.PixelShuffle(3)]
+        else:
+            raise ValueError(f"scale {scale} is not supported. Supported scales: 2^n and 3.")
+        super().__init__(*m)
+
+
+class UpsampleOneStep(nn.Sequential):
+    def __init__(self, scale, num_feat, num_out_ch, input_resolution=None):
+        self.num_feat, self.input_resolution = num_feat, input_resolution
+        super().__init__(nn.Conv2d(num_feat, scale ** 2 * num_out_ch, 3, 1, 1), nn.PixelShuffle(scale))
+
+
+class SwinIR(nn.Module):
+    """Same constructor signature as the reference SwinIR (network_swinir.py:646-652).
+
+    Extra (engine) options, all keyword-only and absent from the reference:
+      compute_dtype  'bf16' (default, MFMA bf16 with fp32 accumulation/master weights) or 'fp32'
+                     (exact fp32 MFMA; the parity mode)
+    """
+
+    def __init__(self, img_size=64, patch_size=1, in_chans=3, embed_dim=96, depths=(6, 6, 6, 6),
+                 num_heads=(6, 6, 6, 6), window_size=7, mlp_ratio=4.0, qkv_bias=True, qk_scale=None, drop_rate=0.0,
+                 attn_drop_rate=0.0, drop_path_rate=0.1, norm_layer=nn.LayerNorm, ape=False, patch_norm=True,
+                 use_checkpoint=False, upscale=2, img_range=1.0, upsampler="", resi_connection="1conv",
+                 compute_dtype="bf16", **kwargs):
+        super().__init__()
+        if ape or not patch_norm or patch_size != 1 or not qkv_bias or qk_scale is not None:
+            raise NotImplementedError("kair_amd SwinIR: ape / patch_norm=False / patch_size!=1 / custom qk are off-path")
+        num_in_ch = num_out_ch = in_chans
+        num_feat = 64
+        self.img_range = img_range
+        self.mean = torch.Tensor((0.4488, 0.4371, 0.4040)).view(1, 3, 1, 1) if in_chans == 3 else torch.zeros(1, 1, 1, 1)
+        self.upscale, self.upsampler, self.window_size = upscale, upsampler, window_size
+        self.conv_first = nn.Conv2d(num_in_ch, embed_dim, 3, 1, 1)
+        self.num_layers, self.embed_dim, self.ape, self.patch_norm = len(depths), embed_dim, ape, patch_norm
+        self.num_features, self.mlp_ratio = embed_dim, mlp_ratio
+        self.patch_embed = PatchEmbed(img_size, patch_size, embed_dim, embed_dim, norm_layer if patch_norm else None)
+        self.patches_resolution = self.patch_embed.patches_resolution
+        self.patch_unembed = PatchUnEmbed(img_size, patch_size, embed_dim, embed_dim, None)
+        self.pos_drop = nn.Dropout(p=drop_rate)
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, sum(depths))]   # network_swinir.py:701
+        self.layers = nn.ModuleList()
+        for i in range(self.num_layers):
+            self.layers.append(RSTB(embed_dim, tuple(self.patches_resolution), depths[i], num_heads[i], window_size,
+                                    mlp_ratio, qkv_bias, qk_scale, drop_rate, attn_drop_rate,
+                                    dpr[sum(depths[:i]):sum(depths[:i + 1])], norm_layer, None, use_checkpoint,
+                                    img_size, patch_size, resi_connection))
+        self.norm = norm_layer(self.num_features)
+        self.conv_after_body = nn.Conv2d(embed_dim, embed_dim, 3, 1, 1)
+        if upsampler == "pixelshuffle":
+            self.conv_before_upsample = nn.Sequential(nn.Conv2d(embed_dim, num_feat, 3, 1, 1), nn.LeakyReLU(inplace=True))
+            self.upsample = Upsample(upscale, num_feat)
+            self.conv_last = nn.Conv2d(num_feat, num_out_ch, 3, 1, 1)
+        elif upsampler == "pixelshuffledirect":
+            self.upsample = UpsampleOneStep(upscale, embed_dim, num_out_ch, tuple(self.patches_resolution))
+        else:
+            raise NotImplementedError(f"kair_amd SwinIR: upsampler '{upsampler}' is not on the MI355X path yet")
+        self.apply(self._init_weights)
+        self.compute_dtype = compute_dtype
+        self._engine = None
+
+    @staticmethod
+    def _init_weights(m):
+        """network_swinir.py:766-773."""
+        if isinstance(m, nn.Linear):
+            _trunc_normal(m.weight)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+
+    @torch.jit.ignore
+    def no_weight_decay(self):
+        return {"absolute_pos_embed"}
+
+    @torch.jit.ignore
+    def no_weight_decay_keywords(self):
+        return {"relative_position_bias_table"}
+
+    # ------------------------------------------------------------------------------------
+    def engine(self):
+        if self._engine is None or self._engine.net_ref() is not self:
+            self._engine = SwinIREngine(self, self.compute_dtype)
+        return self._engine
+
+    def _apply(self, fn, *args, **kwargs):
+        self._engine = None     # packed buffers live on the old device / dtype
+        return super()._apply(fn, *args, **kwargs)
+
+    def set_compute_dtype(self, dtype):
+        self.compute_dtype = dtype
+        self._engine = None
+        return self
+
+    def forward(self, x):
+        if not x.is_cuda:
+            raise RuntimeError("kair_amd SwinIR runs on the MI355X (HIP) only; got a CPU tensor (no CPU fallback)")
+        params = [p for p in self.parameters()]
+        return SwinIRFunction.apply(self.engine(), x, *params)
+
+    def flops(self):
+        """Training FLOPs are tracked by kair_amd.engine.swinir_engine.swinir_flops()."""
+        from ..engine.swinir_engine import swinir_flops
+        H, W = self.patches_resolution
+        return swinir_flops(self, H, W)["fwd"]

@@ -1,0 +1,135 @@
+"""SwinIR on the MI355X vs the reference (golden vectors) and vs the CPU oracle at full size.
+
+Tolerances (stated per north_star): fp32 compute mode — tensors within 1e-4 relative (L2), PSNR
+within 1e-3 dB (float and uint8/border forms); bf16 compute mode — tensors within 2e-2 relative,
+PSNR delta reported and bounded by 2e-2 dB."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from conftest import load_golden, sub_grads, sub_state  # noqa: E402
+from kair_amd.engine.trainer import FusedTrainer  # noqa: E402
+from kair_amd.models.network_swinir import SwinIR  # noqa: E402
+from oracle import image as oimg  # noqa: E402
+from oracle import swinir as osw  # noqa: E402
+from oracle.train import OracleTrainer  # noqa: E402
+
+dev = torch.device("cuda")
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def small(ups, sc, dt):
+    return SwinIR(upscale=sc, in_chans=3, img_size=16, window_size=8, img_range=1.0, depths=[2, 2], embed_dim=60,
+                  num_heads=[6, 6], mlp_ratio=2, upsampler=ups, resi_connection="1conv", drop_path_rate=0.0,
+                  compute_dtype=dt)
+
+
+@pytest.mark.parametrize("dt,tol", [("fp32", 1e-4), ("bf16", 2e-2)])
+@pytest.mark.parametrize("tag,ups,sc", [("classical", "pixelshuffle", 4), ("light", "pixelshuffledirect", 2)])
+def test_swinir_small_vs_golden(dt, tol, tag, ups, sc):
+    z = load_golden("swinir_small")
+    pre = tag + "."
+    net = small(ups, sc, dt)
+    net.load_state_dict(sub_state(z, pre), strict=True)
+    net = net.to(dev).train()
+    L = torch.from_numpy(z[pre + "L"]).to(dev)
+    Hh = torch.from_numpy(z[pre + "H"]).to(dev)
+    E = net(L)
+    assert rel(E, torch.from_numpy(z[pre + "E"])) < tol
+    loss = torch.nn.functional.l1_loss(E, Hh)
+    assert abs(loss.item() - float(z[pre + "loss"])) < 10 * tol * float(z[pre + "loss"])
+    loss.backward()
+    g = sub_grads(z, pre)
+    worst = max(rel(p.grad, g[k]) for k, p in net.named_parameters())
+    assert worst < (2e-3 if dt == "fp32" else 8e-2), worst
+
+
+def classical_x4(dt, seed=0):
+    torch.manual_seed(seed)
+    return SwinIR(upscale=4, in_chans=3, img_size=48, window_size=8, img_range=1.0, depths=[6] * 6, embed_dim=180,
+                  num_heads=[6] * 6, mlp_ratio=2, upsampler="pixelshuffle", resi_connection="1conv", drop_path_rate=0.0,
+                  compute_dtype=dt)
+
+
+def synth_batch(B, lq=48, sc=4, seed=0):
+    """HR = clamp(bicubic-up(U[0,1) at H/8) + 0.02 N, 0, 1); LQ = MATLAB bicubic x1/sc."""
+    g = torch.Generator().manual_seed(seed)
+    hr_s = lq * sc
+    base = torch.rand(B, 3, hr_s // 8, hr_s // 8, generator=g)
+    Hh = torch.nn.functional.interpolate(base, size=(hr_s, hr_s), mode="bicubic", align_corners=False)
+    Hh = (Hh + 0.02 * torch.randn(Hh.shape, generator=g)).clamp(0, 1)
+    L = torch.stack([oimg.imresize_matlab(h, 1 / sc) for h in Hh])
+    return L, Hh
+
+
+def test_swinir_classical_full_fp32_vs_oracle():
+    net = classical_x4("fp32")
+    ref = osw.SwinIR(4, 3, 48, 8, 1.0, [6] * 6, 180, [6] * 6, 2, "pixelshuffle")
+    ref.load_state_dict(net.state_dict(), strict=True)
+    L, Hh = synth_batch(2)
+    Er = ref(L)
+    lr_ = torch.nn.functional.l1_loss(Er, Hh)
+    lr_.backward()
+    net = net.to(dev).train()
+    E = net(L.to(dev))
+    assert rel(E, Er) < 1e-4
+    # PSNR parity, both forms
+    for i in range(2):
+        pf_gpu, pf_cpu = oimg.psnr_float(E[i].cpu(), Hh[i]), oimg.psnr_float(Er[i].detach(), Hh[i])
+        assert abs(pf_gpu - pf_cpu) < 1e-3
+        pu_gpu = oimg.calculate_psnr(oimg.tensor2uint(E[i].cpu()), oimg.tensor2uint(Hh[i]), border=4)
+        pu_cpu = oimg.calculate_psnr(oimg.tensor2uint(Er[i].detach()), oimg.tensor2uint(Hh[i]), border=4)
+        assert abs(pu_gpu - pu_cpu) < 1e-3
+    loss = torch.nn.functional.l1_loss(E, Hh.to(dev))
+    loss.backward()
+    gref = dict(ref.named_parameters())
+    worst = max((rel(p.grad, gref[k].grad), k) for k, p in net.named_parameters())
+    assert worst[0] < 1e-3, worst
+
+
+def test_swinir_classical_full_bf16_psnr_delta():
+    net = classical_x4("bf16", seed=1)
+    ref = osw.SwinIR(4, 3, 48, 8, 1.0, [6] * 6, 180, [6] * 6, 2, "pixelshuffle")
+    ref.load_state_dict(net.state_dict(), strict=True)
+    L, Hh = synth_batch(2, seed=1)
+    with torch.no_grad():
+        Er = ref(L)
+        E = net.to(dev).eval()(L.to(dev)).cpu()
+    assert rel(E, Er) < 2e-2
+    d = abs(oimg.psnr_float(E, Hh) - oimg.psnr_float(Er, Hh))
+    print("bf16 float-PSNR delta (dB):", d)
+    assert d < 2e-2
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_trainer_matches_reference_trajectory(use_graph):
+    """3 steps of the fused trainer (fp32 mode) against the reference ModelPlain trajectory."""
+    z = load_golden("train_trajectory")
+    mk = lambda: SwinIR(upscale=4, in_chans=3, img_size=16, window_size=8, img_range=1.0, depths=[2, 2], embed_dim=60,
+                        num_heads=[6, 6], mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.0,
+                        compute_dtype="fp32")
+    net, ema = mk(), mk()
+    net.load_state_dict(sub_state(z, "init."), strict=True)
+    ema.load_state_dict(sub_state(z, "init."), strict=True)
+    net, ema = net.to(dev).train(), ema.to(dev).eval()
+    tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999, use_graph=use_graph)
+    milestones, lr0 = [2, 100], 2e-4
+    losses = []
+    for s in range(1, 4):
+        tr.lr = lr0 * 0.5 ** sum(1 for m in milestones if m <= s)   # MultiStepLR stepped before the step
+        loss = tr.step(torch.from_numpy(z[f"step{s}.L"]).to(dev), torch.from_numpy(z[f"step{s}.H"]).to(dev))
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, z["losses"], rtol=1e-4)
+    fg, fe = sub_state(z, "final.G."), sub_state(z, "final.E.")
+    for k, v in net.state_dict().items():
+        assert rel(v.float(), fg[k].float()) < 1e-4, k
+    for k, v in ema.state_dict().items():
+        assert rel(v.float(), fe[k].float()) < 1e-4, k
