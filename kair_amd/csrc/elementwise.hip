@@ -87,13 +87,21 @@ __global__ void colsum_partial(const T* __restrict__ g, long ld, long M, int Np,
   ws[(long)blockIdx.x * Np + c] = s;
 }
 
-__global__ void colsum_final(const float* __restrict__ ws, int nb, int Np, kair_wmap mp, float* out, int acc) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= mp.N) return;
-  const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr;
+__global__ __launch_bounds__(256) void colsum_final(const float* __restrict__ ws, int nb, int Np, kair_wmap mp, float* out,
+                                                    int acc) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + tx;
+  const int np = n < mp.N ? (n / mp.nGr) * mp.nGp + n % mp.nGr : 0;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += ws[(long)b * Np + np];
-  out[n] = acc ? out[n] + s : s;
+  if (n < mp.N)
+    for (int b = ty; b < nb; b += 4) s += ws[(long)b * Np + np];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && n < mp.N) {
+    s = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+    out[n] = acc ? out[n] + s : s;
+  }
 }
 
 template <typename T>
@@ -233,7 +241,7 @@ extern "C" int kair_colsum(const kair_operand* G, long M, int Np, const kair_wma
                            int accumulate, void* stream) {
   KAIR_CHECK_ARG(G && G->ptr && map && bias_grad && ws, "colsum: null pointer");
   KAIR_CHECK_ARG(G->mode == KAIR_LD_ROWS && G->win_ws == 0, "colsum: plain row operands only");
-  const int nb = 1024;
+  const int nb = 512;
   const long rows_per = (M + nb - 1) / nb;
   dim3 grid(nb, (Np + 255) / 256);
   hipStream_t s = (hipStream_t)stream;
@@ -242,7 +250,7 @@ extern "C" int kair_colsum(const kair_operand* G, long M, int Np, const kair_wma
   else
     hipLaunchKernelGGL(colsum_partial<float>, grid, dim3(256), 0, s, (const float*)G->ptr, G->ld, M, Np, ws, rows_per);
   KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_final, dim3(nblk(map->N, 256)), dim3(256), 0, s, ws, nb, Np, *map, bias_grad, accumulate);
+  hipLaunchKernelGGL(colsum_final, dim3(nblk(map->N, 64)), dim3(256), 0, s, ws, nb, Np, *map, bias_grad, accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

@@ -1,15 +1,20 @@
 // Implicit-GEMM kernels for gfx950 (CDNA4): the contractions of nn.Linear and 3x3 nn.Conv2d on the
 // KAIR hot path (forward, input gradient and weight gradient), with fused prologue address maps
 // (Swin window partition + cyclic shift, im2col, head-blocked q/k/v) and fused epilogues
-// (bias, GELU / LeakyReLU, residual add, PixelShuffle store, NCHW image store, act' gating).
+// (bias, GELU / LeakyReLU, residual add, DropPath scale, PixelShuffle store, NCHW image store,
+// act' gating).
 //
-//   kair_gemm_nt : C[m,n] = sum_k A[m,k] B[n,k]          (forward, dgrad)
-//   kair_gemm_tn : P[s][n,k] = sum_{m in s} A[m,n] B[m,k]  (wgrad, split over m, deterministic)
+//   kair_gemm_nt : C[m,n] = sum_k A[m,k] B[n,k]            (forward, input gradient)
+//   kair_gemm_tn : P[s][n,k] = sum_{m in s} A[m,n] B[m,k]   (weight gradient, split over m)
 //
-// Tiles: 256 threads = 4 waves, BK = 32.  bf16 compute uses v_mfma_f32_16x16x32_bf16 (8 bf16 of K
-// per lane, one ds_read_b128 per fragment); f32 compute uses v_mfma_f32_16x16x4_f32 (exact fp32,
-// parity mode).  Operands are staged global -> registers -> LDS with the next K-tile's global
-// loads issued before the current tile's MFMAs (register double buffering).
+// Structure (both): 256 threads = 4 waves (2x2), 128x128 (or smaller) output tile, K-step 64
+// (bf16) / 32 (fp32), double-buffered LDS filled by register staging: the next K-step's global
+// loads are issued before the current step's MFMAs and written to the other LDS buffer after them,
+// one barrier per K-step.  Operand modes are template parameters and every per-row address is
+// computed once before the K loop.  bf16 compute uses v_mfma_f32_16x16x32_bf16 fed by
+// ds_read_b128 (NT) or ds_read_b64_tr_b16 (TN, m-major tiles); fp32 (parity) compute uses the exact
+// v_mfma_f32_16x16x4_f32.  The NT epilogue stages the accumulator tile through LDS so every thread
+// finishes 8 consecutive columns of one row with 16-byte loads/stores.
 #include <stdarg.h>
 #include <stdio.h>
 
@@ -17,15 +22,16 @@
 
 namespace {
 
-constexpr int BK = 32;
 constexpr int NT = 256;
+enum { AM_ROWS = 0, AM_IM2COL = 1, AM_QKV = 2 };
+
+template <typename CT> struct KStep { static constexpr int BK = sizeof(CT) == 2 ? 64 : 32; };
 
 // ------------------------------------------------------------------------------------------
-// operand chunk loader: 8 consecutive columns [k, k+8) of row m, returned as fp32
+// operand description (trimmed copy of kair_operand, passed by value)
 // ------------------------------------------------------------------------------------------
 struct Op {
   const void* ptr;
-  int dtype, mode;
   long ld;
   WinMap win;
   int imH, imW, imC, flip;
@@ -33,62 +39,12 @@ struct Op {
   const float* rowscale;
   int rps;
   int ones_col;
-  long M;  // total rows (QKVBLK part stride)
+  long M;  // rows of this operand
 };
-
-KAIR_DEV void load8(const Op& op, long m, int k, int K, float (&v)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = 0.f;
-  if (m >= op.M || k >= K) return;
-  long off;
-  long srow = m;
-  if (op.mode == KAIR_LD_ROWS) {
-    srow = win_to_token(m, op.win);
-    off = srow * op.ld + k;
-  } else if (op.mode == KAIR_LD_IM2COL3) {
-    const int tap = k / op.imC;
-    const int c = k - tap * op.imC;
-    int dy = tap / 3 - 1, dx = tap % 3 - 1;
-    if (op.flip) { dy = -dy; dx = -dx; }
-    const long hw = (long)op.imH * op.imW;
-    const long b = m / hw;
-    const int p = (int)(m - b * hw);
-    const int y = p / op.imW + dy, x = p % op.imW + dx;
-    if (y < 0 || y >= op.imH || x < 0 || x >= op.imW) {
-      if (op.ones_col >= k && op.ones_col < k + 8) v[op.ones_col - k] = 1.f;
-      return;
-    }
-    off = ((b * op.imH + y) * op.imW + x) * op.imC + c;
-  } else {  // QKVBLK
-    const int pw = op.nh * op.hdp;
-    const int part = k / pw;
-    const int r = k - part * pw;
-    const int h = r / op.hdp, d = r - h * op.hdp;
-    const long win = m / op.tok;
-    const int t = (int)(m - win * op.tok);
-    off = (long)part * op.M * pw + ((win * op.nh + h) * op.tok + t) * op.hdp + d;
-  }
-  if (op.dtype == KAIR_BF16) {
-    const bf16x8 q = *(const bf16x8*)((const bf16*)op.ptr + off);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
-  } else {
-    const float4 a = *(const float4*)((const float*)op.ptr + off);
-    const float4 b = *(const float4*)((const float*)op.ptr + off + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  }
-  if (op.rowscale) {
-    const float s = op.rowscale[srow / op.rps];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] *= s;
-  }
-  if (op.ones_col >= k && op.ones_col < k + 8) v[op.ones_col - k] = 1.f;
-}
 
 Op make_op(const kair_operand& o, long M) {
   Op op;
-  op.ptr = o.ptr; op.dtype = o.dtype; op.mode = o.mode; op.ld = o.ld;
+  op.ptr = o.ptr; op.ld = o.ld;
   op.win = WinMap{o.win_H, o.win_W, o.win_ws, o.win_shift};
   op.imH = o.im_H; op.imW = o.im_W; op.imC = o.im_C; op.flip = o.im_flip;
   op.nh = o.qkv_nh; op.hdp = o.qkv_hdp; op.tok = o.qkv_tok;
@@ -96,6 +52,105 @@ Op make_op(const kair_operand& o, long M) {
   op.ones_col = o.ones_col;
   op.M = M;
   return op;
+}
+
+KAIR_DEV void zero8(float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.f;
+}
+
+template <typename T>
+KAIR_DEV void gload8(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 q = *(const bf16x8*)p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
+  } else {
+    const float4 a = *(const float4*)p;
+    const float4 b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+
+// Per-chunk row state: resolved once before the K loop.
+struct RowState {
+  long base;   // element offset of the row start (ROWS) / pixel index (IM2COL) / token offset (QKV)
+  int y, x;    // IM2COL pixel coordinates
+  float scale;
+  bool valid;
+};
+
+template <int AM, typename T>
+KAIR_DEV RowState row_state(const Op& op, long m) {
+  RowState r;
+  r.valid = m < op.M;
+  r.scale = 1.f;
+  r.y = r.x = 0;
+  r.base = 0;
+  if (!r.valid) return r;
+  if constexpr (AM == AM_ROWS) {
+    const long t = win_to_token(m, op.win);
+    r.base = t * op.ld;
+    if (op.rowscale) r.scale = op.rowscale[t / op.rps];
+  } else if constexpr (AM == AM_IM2COL) {
+    const int hw = op.imH * op.imW;
+    const int b = (int)(m / hw);
+    const int p = (int)(m - (long)b * hw);
+    r.y = p / op.imW;
+    r.x = p - r.y * op.imW;
+    r.base = (long)p + (long)b * hw;
+  } else {
+    const long win = m / op.tok;
+    const int t = (int)(m - win * op.tok);
+    r.base = (win * op.nh * op.tok + t) * op.hdp;
+    if (op.rowscale) r.scale = op.rowscale[m / op.rps];
+  }
+  return r;
+}
+
+// load 8 consecutive columns [k, k+8) of a resolved row
+template <int AM, typename T>
+KAIR_DEV void load_chunk(const Op& op, const RowState& r, int k, int K, float (&v)[8]) {
+  zero8(v);
+  if (r.valid && k < K) {
+    const T* P = (const T*)op.ptr;
+    if constexpr (AM == AM_ROWS) {
+      gload8<T>(P + r.base + k, v);
+    } else if constexpr (AM == AM_IM2COL) {
+      const int tap = k / op.imC;
+      const int c = k - tap * op.imC;
+      int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+      if (op.flip) { dy = -dy; dx = -dx; }
+      const int y = r.y + dy, x = r.x + dx;
+      if (y >= 0 && y < op.imH && x >= 0 && x < op.imW)
+        gload8<T>(P + (r.base + (long)dy * op.imW + dx) * op.imC + c, v);
+    } else {
+      const int pw = op.nh * op.hdp;
+      const int part = k / pw;
+      const int rr = k - part * pw;
+      const int h = rr / op.hdp, d = rr - h * op.hdp;
+      gload8<T>(P + (long)part * op.M * pw + r.base + (long)h * op.tok * op.hdp + d, v);
+    }
+    if (r.scale != 1.f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= r.scale;
+    }
+  }
+  if (op.ones_col >= k && op.ones_col < k + 8) v[op.ones_col - k] = 1.f;
+}
+
+template <typename CT>
+KAIR_DEV void lds_store8(CT* base, const float (&v)[8]) {
+  if constexpr (sizeof(CT) == 2) {
+    bf16x8 q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = (bf16)v[j];
+    *(bf16x8*)base = q;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) *(float2*)(base + j) = make_float2(v[j], v[j + 1]);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -116,88 +171,6 @@ struct Epi {
   long M; int N;
 };
 
-KAIR_DEV void st(void* p, int dt, long off, float v) {
-  if (dt == KAIR_BF16) ((bf16*)p)[off] = (bf16)v;
-  else ((float*)p)[off] = v;
-}
-KAIR_DEV float ld1(const void* p, int dt, long off) {
-  return dt == KAIR_BF16 ? (float)((const bf16*)p)[off] : ((const float*)p)[off];
-}
-
-KAIR_DEV void epi_store(const Epi& e, long m, int n, float v) {
-  if (m >= e.M || n >= e.N) return;
-  if (e.bias) v += e.bias[n];
-  const float pre = v;
-  if (e.act == KAIR_ACT_GELU) v = gelu_erf(v);
-  else if (e.act == KAIR_ACT_LEAKY) v = v > 0.f ? v : v * e.slope;
-  else if (e.act == KAIR_ACT_RELU) v = fmaxf(v, 0.f);
-  if (e.omode == KAIR_OUT_ROWS) {
-    const long row = win_to_token(m, e.win);
-    if (e.gate) {
-      const float g = ld1(e.gate, e.gdt, row * e.ldg + n);
-      if (e.gkind == 1) v *= gelu_erf_grad(g);
-      else if (e.gkind == 2) v *= (g > 0.f ? 1.f : e.slope);
-      else v *= (g > 0.f ? 1.f : 0.f);
-    }
-    if (e.resid) {
-      const float s = e.rowscale ? e.rowscale[row / e.rps] : 1.f;
-      v = e.resid[row * e.ldr + n] + s * v;
-    }
-    st(e.out, e.odt, row * e.ldo + n, v);
-    if (e.pre) st(e.pre, e.pdt, row * e.ldp + n, pre);
-  } else if (e.omode == KAIR_OUT_QKVBLK) {
-    const int pw = e.nh * e.hdp;
-    const int part = n / pw, rr = n - part * pw;
-    const int h = rr / e.hdp, d = rr - h * e.hdp;
-    const long win = m / e.tok;
-    const int t = (int)(m - win * e.tok);
-    st(e.out, e.odt, (long)part * e.M * pw + ((win * e.nh + h) * e.tok + t) * e.hdp + d, v);
-  } else if (e.omode == KAIR_OUT_PSHUF) {
-    const int r = e.r, r2 = r * r;
-    const int c = n / r2, ij = n - c * r2, i = ij / r, j = ij - i * r;
-    const long hw = (long)e.psH * e.psW;
-    const long b = m / hw;
-    const int p = (int)(m - b * hw), y = p / e.psW, x = p - (p / e.psW) * e.psW;
-    const long orow = (b * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + j;
-    if (e.gate) {
-      const float g = ld1(e.gate, e.gdt, orow * e.ldg + c);
-      v *= (e.gkind == 2) ? (g > 0.f ? 1.f : e.slope) : (g > 0.f ? 1.f : 0.f);
-    }
-    st(e.out, e.odt, orow * e.ldo + c, v);
-    if (e.pre) st(e.pre, e.pdt, orow * e.ldp + c, pre);
-  } else if (e.omode == KAIR_OUT_PUNSHUF) {
-    const int r = e.r;
-    const long HW = (long)e.psH * r * e.psW * r;
-    const long b = m / HW;
-    const long p = m - b * HW;
-    const int Y = (int)(p / (e.psW * r)), X = (int)(p - (long)Y * e.psW * r);
-    const int y = Y / r, i = Y - y * r, x = X / r, j = X - x * r;
-    const long orow = (b * e.psH + y) * e.psW + x;
-    const int oc = n * r * r + i * r + j;
-    if (e.gate) {
-      const float g = ld1(e.gate, e.gdt, orow * e.ldg + oc);
-      v *= (e.gkind == 2) ? (g > 0.f ? 1.f : e.slope) : (g > 0.f ? 1.f : 0.f);
-    }
-    st(e.out, e.odt, orow * e.ldo + oc, v);
-  } else if (e.omode == KAIR_OUT_PSHUF_NCHW) {
-    const int r = e.r, r2 = r * r;
-    const int c = n / r2, ij = n - c * r2, i = ij / r, j = ij - i * r;
-    if (c >= e.imgC) return;
-    const long hw = (long)e.psH * e.psW;
-    const long b = m / hw;
-    const int p = (int)(m - b * hw), y = p / e.psW, x = p - (p / e.psW) * e.psW;
-    v = v / e.range + (e.mean ? e.mean[c] : 0.f);
-    ((float*)e.out)[((b * e.imgC + c) * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + j] = v;
-  } else {  // NCHW image
-    if (n >= e.imgC) return;
-    const long hw = (long)e.imgH * e.imgW;
-    const long b = m / hw;
-    const long p = m - b * hw;
-    v = v / e.range + (e.mean ? e.mean[n] : 0.f);
-    ((float*)e.out)[(b * e.imgC + n) * hw + p] = v;
-  }
-}
-
 Epi make_epi(const kair_epilogue& o, long M, int N) {
   Epi e;
   e.out = o.out; e.odt = o.out_dtype; e.omode = o.out_mode; e.ldo = o.ldo;
@@ -214,7 +187,125 @@ Epi make_epi(const kair_epilogue& o, long M, int N) {
   return e;
 }
 
-// bijective XCD-aware remap: logical tiles [x*q + min(x,r) ...] live on the same XCD group
+KAIR_DEV void load8_any(const void* p, int dt, long off, float (&v)[8]) {
+  if (dt == KAIR_BF16) gload8<bf16>((const bf16*)p + off, v);
+  else gload8<float>((const float*)p + off, v);
+}
+KAIR_DEV void store8_any(void* p, int dt, long off, const float (&v)[8]) {
+  if (dt == KAIR_BF16) {
+    bf16x8 q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = (bf16)v[j];
+    *(bf16x8*)((bf16*)p + off) = q;
+  } else {
+    float* d = (float*)p + off;
+    *(float4*)d = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+KAIR_DEV void st1(void* p, int dt, long off, float v) {
+  if (dt == KAIR_BF16) ((bf16*)p)[off] = (bf16)v;
+  else ((float*)p)[off] = v;
+}
+
+// finish 8 consecutive columns [n, n+8) of GEMM row m (n % 8 == 0)
+KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
+  if (m >= e.M || n >= e.N) return;
+  const bool full = n + 8 <= e.N;
+  if (e.bias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += (n + j < e.N) ? e.bias[n + j] : 0.f;
+  }
+  float pre[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    pre[j] = v[j];
+    if (e.act == KAIR_ACT_GELU) v[j] = gelu_erf(v[j]);
+    else if (e.act == KAIR_ACT_LEAKY) v[j] = v[j] > 0.f ? v[j] : v[j] * e.slope;
+    else if (e.act == KAIR_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
+  }
+  if (e.omode == KAIR_OUT_ROWS) {
+    const long row = win_to_token(m, e.win);
+    if (e.gate) {
+      float g[8];
+      if (full) load8_any(e.gate, e.gdt, row * e.ldg + n, g);
+      else
+        for (int j = 0; j < 8; ++j)
+          g[j] = n + j < e.N ? (e.gdt == KAIR_BF16 ? (float)((const bf16*)e.gate)[row * e.ldg + n + j]
+                                                    : ((const float*)e.gate)[row * e.ldg + n + j]) : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (e.gkind == 1) v[j] *= gelu_erf_grad(g[j]);
+        else if (e.gkind == 2) v[j] *= (g[j] > 0.f ? 1.f : e.slope);
+        else v[j] *= (g[j] > 0.f ? 1.f : 0.f);
+      }
+    }
+    if (e.resid) {
+      const float s = e.rowscale ? e.rowscale[row / e.rps] : 1.f;
+      for (int j = 0; j < 8; ++j)
+        if (n + j < e.N) v[j] = e.resid[row * e.ldr + n + j] + s * v[j];
+    }
+    if (full && (e.ldo % 8) == 0) {
+      store8_any(e.out, e.odt, row * e.ldo + n, v);
+      if (e.pre) store8_any(e.pre, e.pdt, row * e.ldp + n, pre);
+    } else {
+      for (int j = 0; j < 8 && n + j < e.N; ++j) {
+        st1(e.out, e.odt, row * e.ldo + n + j, v[j]);
+        if (e.pre) st1(e.pre, e.pdt, row * e.ldp + n + j, pre[j]);
+      }
+    }
+  } else if (e.omode == KAIR_OUT_QKVBLK) {
+    const int pw = e.nh * e.hdp;
+    const int part = n / pw, rr = n - part * pw;
+    const int h = rr / e.hdp, d = rr - h * e.hdp;
+    const long win = m / e.tok;
+    const int t = (int)(m - win * e.tok);
+    store8_any(e.out, e.odt, (long)part * e.M * pw + ((win * e.nh + h) * e.tok + t) * e.hdp + d, v);
+  } else if (e.omode == KAIR_OUT_PSHUF || e.omode == KAIR_OUT_PSHUF_NCHW) {
+    const int r = e.r, r2 = r * r;
+    const long hw = (long)e.psH * e.psW;
+    const long b = m / hw;
+    const int p = (int)(m - b * hw), y = p / e.psW, x = p - (p / e.psW) * e.psW;
+    for (int j = 0; j < 8 && n + j < e.N; ++j) {
+      const int nn = n + j;
+      const int c = nn / r2, ij = nn - c * r2, i = ij / r, jj = ij - i * r;
+      if (e.omode == KAIR_OUT_PSHUF) {
+        const long orow = (b * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + jj;
+        st1(e.out, e.odt, orow * e.ldo + c, v[j]);
+        if (e.pre) st1(e.pre, e.pdt, orow * e.ldp + c, pre[j]);
+      } else if (c < e.imgC) {
+        const float o = v[j] / e.range + (e.mean ? e.mean[c] : 0.f);
+        ((float*)e.out)[((b * e.imgC + c) * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + jj] = o;
+      }
+    }
+  } else if (e.omode == KAIR_OUT_PUNSHUF) {
+    const int r = e.r;
+    const long HW = (long)e.psH * r * e.psW * r;
+    const long b = m / HW;
+    const long p = m - b * HW;
+    const int Y = (int)(p / (e.psW * r)), X = (int)(p - (long)Y * e.psW * r);
+    const int y = Y / r, i = Y - y * r, x = X / r, jj = X - x * r;
+    const long orow = (b * e.psH + y) * e.psW + x;
+    for (int j = 0; j < 8 && n + j < e.N; ++j) {
+      const int oc = (n + j) * r * r + i * r + jj;
+      float val = v[j];
+      if (e.gate) {
+        const float g = e.gdt == KAIR_BF16 ? (float)((const bf16*)e.gate)[orow * e.ldg + oc]
+                                            : ((const float*)e.gate)[orow * e.ldg + oc];
+        val *= (e.gkind == 2) ? (g > 0.f ? 1.f : e.slope) : (g > 0.f ? 1.f : 0.f);
+      }
+      st1(e.out, e.odt, orow * e.ldo + oc, val);
+    }
+  } else {  // NCHW image
+    const long hw = (long)e.imgH * e.imgW;
+    const long b = m / hw;
+    const long p = m - b * hw;
+    for (int j = 0; j < 8 && n + j < e.imgC && n + j < e.N; ++j)
+      ((float*)e.out)[(b * e.imgC + n + j) * hw + p] = v[j] / e.range + (e.mean ? e.mean[n + j] : 0.f);
+  }
+}
+
+// bijective XCD-aware remap: consecutive logical tiles share an XCD (L2)
 KAIR_DEV int xcd_remap(int hw, int nwg) {
   const int q = nwg / 8, r = nwg % 8;
   const int x = hw % 8, pos = hw / 8;
@@ -222,41 +313,24 @@ KAIR_DEV int xcd_remap(int hw, int nwg) {
 }
 
 // ------------------------------------------------------------------------------------------
-// LDS tile helpers
-// ------------------------------------------------------------------------------------------
-template <typename CT> struct Lds;
-template <> struct Lds<bf16> {
-  static constexpr int LD = BK + 8;  // 80-byte rows: ds_read_b128 fragment reads conflict-free
-};
-template <> struct Lds<float> {
-  static constexpr int LD = BK + 2;  // 136-byte rows
-};
-
-template <typename CT>
-KAIR_DEV void lds_store8(CT* base, const float (&v)[8]) {
-  if constexpr (sizeof(CT) == 2) {
-    bf16x8 q;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) q[j] = (bf16)v[j];
-    *(bf16x8*)base = q;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) *(float2*)(base + j) = make_float2(v[j], v[j + 1]);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // NT kernel
 // ------------------------------------------------------------------------------------------
-template <typename CT, int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(NT) void gemm_nt_kernel(Op A, Op B, Epi E, int K, int tilesN, int nwg) {
-  constexpr int LD = Lds<CT>::LD;
-  constexpr int TM = BM / WM, TN = BN / WN;  // per-wave tile
+template <typename CT, typename TA, int AM, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(NT, 2) void gemm_nt_kernel(Op A, Op B, Epi E, int K, int tilesN, int nwg) {
+  constexpr int BK = KStep<CT>::BK;
+  constexpr int LD = BK + (sizeof(CT) == 2 ? 8 : 2);
+  constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int RM = TM / 16, RN = TN / 16;
-  constexpr int CA = BM * BK / 8, CB = BN * BK / 8;  // 8-element chunks per tile
+  constexpr int CPR = BK / 8;                      // chunks per tile row
+  constexpr int CA = BM * CPR, CB = BN * CPR;
   constexpr int PA = (CA + NT - 1) / NT, PB = (CB + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) CT sA[BM * LD];
-  __shared__ __attribute__((aligned(16))) CT sB[BN * LD];
+  constexpr int STAGE = (BM + BN) * LD;            // elements per LDS stage
+  constexpr int EPI_LD = BN + 4;                   // fp32 epilogue tile row stride
+  constexpr int LDS_BYTES_MAIN = 2 * STAGE * (int)sizeof(CT);
+  constexpr int LDS_BYTES_EPI = BM * EPI_LD * 4;
+  constexpr int LDS_BYTES = LDS_BYTES_MAIN > LDS_BYTES_EPI ? LDS_BYTES_MAIN : LDS_BYTES_EPI;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  CT* lds = (CT*)smem;
 
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int tm = tile / tilesN, tn = tile - tm * tilesN;
@@ -265,29 +339,36 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(Op A, Op B, Epi E, int K, i
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
 
-  float ra[PA][8], rb[PB][8];
+  RowState ra[PA], rb[PB];
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    const int c = tid + p * NT;
+    ra[p] = row_state<AM, TA>(A, c < CA ? m0 + c / CPR : A.M);
+  }
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    const int c = tid + p * NT;
+    rb[p] = row_state<AM_ROWS, CT>(B, c < CB ? (long)(n0 + c / CPR) : B.M);
+  }
+  float va[PA][8], vb[PB][8];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int p = 0; p < PA; ++p) {
-      const int c = tid + p * NT;
-      if (c < CA) load8(A, m0 + c / 4, k0 + (c & 3) * 8, K, ra[p]);
-    }
+    for (int p = 0; p < PA; ++p) load_chunk<AM, TA>(A, ra[p], k0 + ((tid + p * NT) % CPR) * 8, K, va[p]);
 #pragma unroll
-    for (int p = 0; p < PB; ++p) {
-      const int c = tid + p * NT;
-      if (c < CB) load8(B, n0 + c / 4, k0 + (c & 3) * 8, K, rb[p]);
-    }
+    for (int p = 0; p < PB; ++p) load_chunk<AM_ROWS, CT>(B, rb[p], k0 + ((tid + p * NT) % CPR) * 8, K, vb[p]);
   };
-  auto sstore = [&]() {
+  auto sstore = [&](int st) {
+    CT* sA = lds + st * STAGE;
+    CT* sB = sA + BM * LD;
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
       const int c = tid + p * NT;
-      if (c < CA) lds_store8<CT>(sA + (c / 4) * LD + (c & 3) * 8, ra[p]);
+      if (c < CA) lds_store8<CT>(sA + (c / CPR) * LD + (c % CPR) * 8, va[p]);
     }
 #pragma unroll
     for (int p = 0; p < PB; ++p) {
       const int c = tid + p * NT;
-      if (c < CB) lds_store8<CT>(sB + (c / 4) * LD + (c & 3) * 8, rb[p]);
+      if (c < CB) lds_store8<CT>(sB + (c / CPR) * LD + (c % CPR) * 8, vb[p]);
     }
   };
 
@@ -298,24 +379,29 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(Op A, Op B, Epi E, int K, i
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (K + BK - 1) / BK;
+  const int fr = lane & 15, fq = lane >> 4;
   gload(0);
+  sstore(0);
+  __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    __syncthreads();
-    sstore();
-    __syncthreads();
+    const int st = kt & 1;
     if (kt + 1 < nk) gload((kt + 1) * BK);
-    const int fr = lane & 15, fq = lane >> 4;
+    const CT* sA = lds + st * STAGE;
+    const CT* sB = sA + BM * LD;
     if constexpr (sizeof(CT) == 2) {
-      bf16x8 af[RM], bfr[RN];
 #pragma unroll
-      for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sA + (wm * TM + i * 16 + fr) * LD + fq * 8);
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 af[RM], bfr[RN];
 #pragma unroll
-      for (int j = 0; j < RN; ++j) bfr[j] = *(const bf16x8*)(sB + (wn * TN + j * 16 + fr) * LD + fq * 8);
+        for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sA + (wm * TM + i * 16 + fr) * LD + ks * 32 + fq * 8);
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+        for (int j = 0; j < RN; ++j) bfr[j] = *(const bf16x8*)(sB + (wn * TN + j * 16 + fr) * LD + ks * 32 + fq * 8);
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int s = 0; s < BK / 4; ++s) {
@@ -331,37 +417,47 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(Op A, Op B, Epi E, int K, i
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (kt + 1 < nk) sstore(st ^ 1);
+    __syncthreads();
   }
-  // epilogue: 16x16 C/D map  col = lane&15, row = (lane>>4)*4 + r
+  // epilogue: accumulator tile -> LDS (fp32) -> 8-column row chunks
+  float* et = (float*)smem;
 #pragma unroll
   for (int i = 0; i < RM; ++i)
 #pragma unroll
     for (int j = 0; j < RN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long m = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
-        const int n = n0 + wn * TN + j * 16 + (lane & 15);
-        epi_store(E, m, n, acc[i][j][r]);
-      }
+      for (int r = 0; r < 4; ++r) et[(wm * TM + i * 16 + fq * 4 + r) * EPI_LD + wn * TN + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  constexpr int CH = BM * BN / 8;
+  for (int c = tid; c < CH; c += NT) {
+    const int row = c / (BN / 8), col = (c % (BN / 8)) * 8;
+    float v[8];
+    const float4 a = *(const float4*)(et + row * EPI_LD + col);
+    const float4 b = *(const float4*)(et + row * EPI_LD + col + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    epi_chunk(E, m0 + row, n0 + col, v);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
 // TN kernel (weight gradient): P[s][n][k] = sum_{m in split s} A[m][n] * B[m][k]
-// LDS holds both operands m-major ([32 m][BN], [32 m][BK]) exactly as loaded; bf16 fragments
-// (8 consecutive m for one n) come from two ds_read_b64_tr_b16 transposed reads.
+// LDS holds both operands m-major ([BMr m][BN], [BMr m][BKo]) as loaded; bf16 fragments (8
+// consecutive m of one column) come from two ds_read_b64_tr_b16 transposed reads.
 // ------------------------------------------------------------------------------------------
-template <typename CT, int BN, int BKo>
-__global__ __launch_bounds__(NT) void gemm_tn_kernel(Op A, Op B, float* ws, long M, int N, int K, long rows_per_split,
-                                                     int tilesK) {
-  constexpr int LDA = BN + 8, LDB = BKo + 8;  // m-major rows, padded
+template <typename CT, typename TA, typename TB, int AMA, int AMB, int BN, int BKo>
+__global__ __launch_bounds__(NT, 2) void gemm_tn_kernel(Op A, Op B, float* ws, long M, int N, int K, long rows_per_split,
+                                                        int tilesK) {
+  constexpr int BMr = sizeof(CT) == 2 ? 64 : 32;   // reduction rows per step
+  constexpr int LDA = BN + 8, LDB = BKo + 8;
   constexpr int WN = 2, WK = 2;
   constexpr int TN_ = BN / WN, TK_ = BKo / WK;
   constexpr int RN = TN_ / 16, RK = TK_ / 16;
-  constexpr int CA = BK * BN / 8, CB = BK * BKo / 8;
+  constexpr int CPA = BN / 8, CPB = BKo / 8;
+  constexpr int CA = BMr * CPA, CB = BMr * CPB;
   constexpr int PA = (CA + NT - 1) / NT, PB = (CB + NT - 1) / NT;
-  constexpr int CPA = BN / 8, CPB = BKo / 8;  // chunks per m-row
-  __shared__ __attribute__((aligned(16))) CT sA[BK * LDA];
-  __shared__ __attribute__((aligned(16))) CT sB[BK * LDB];
+  constexpr int STAGE = BMr * (LDA + LDB);
+  __shared__ __attribute__((aligned(16))) CT lds[2 * STAGE];
 
   const int tn = blockIdx.x / tilesK, tk = blockIdx.x - (blockIdx.x / tilesK) * tilesK;
   const int n0 = tn * BN, k0 = tk * BKo;
@@ -371,17 +467,16 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(Op A, Op B, float* ws, long
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WK, wk = wave % WK;
 
-  float ra[PA][8], rb[PB][8];
+  float va[PA][8], vb[PB][8];
   auto gload = [&](long mb) {
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
       const int c = tid + p * NT;
       if (c < CA) {
         const long m = mb + c / CPA;
-        if (m < mend) load8(A, m, n0 + (c % CPA) * 8, N, ra[p]);
-        else
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ra[p][j] = 0.f;
+        const RowState r = row_state<AMA, TA>(A, m < mend ? m : A.M);
+        load_chunk<AMA, TA>(A, r, n0 + (c % CPA) * 8, N, va[p]);
+        if (m >= mend) zero8(va[p]);
       }
     }
 #pragma unroll
@@ -389,23 +484,24 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(Op A, Op B, float* ws, long
       const int c = tid + p * NT;
       if (c < CB) {
         const long m = mb + c / CPB;
-        if (m < mend) load8(B, m, k0 + (c % CPB) * 8, K, rb[p]);
-        else
-#pragma unroll
-          for (int j = 0; j < 8; ++j) rb[p][j] = 0.f;
+        const RowState r = row_state<AMB, TB>(B, m < mend ? m : B.M);
+        load_chunk<AMB, TB>(B, r, k0 + (c % CPB) * 8, K, vb[p]);
+        if (m >= mend) zero8(vb[p]);
       }
     }
   };
-  auto sstore = [&]() {
+  auto sstore = [&](int st) {
+    CT* sA = lds + st * STAGE;
+    CT* sB = sA + BMr * LDA;
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
       const int c = tid + p * NT;
-      if (c < CA) lds_store8<CT>(sA + (c / CPA) * LDA + (c % CPA) * 8, ra[p]);
+      if (c < CA) lds_store8<CT>(sA + (c / CPA) * LDA + (c % CPA) * 8, va[p]);
     }
 #pragma unroll
     for (int p = 0; p < PB; ++p) {
       const int c = tid + p * NT;
-      if (c < CB) lds_store8<CT>(sB + (c / CPB) * LDB + (c % CPB) * 8, rb[p]);
+      if (c < CB) lds_store8<CT>(sB + (c / CPB) * LDB + (c % CPB) * 8, vb[p]);
     }
   };
 
@@ -416,33 +512,37 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(Op A, Op B, float* ws, long
     for (int j = 0; j < RK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  if (mbeg < mend) {
+  const int nsteps = mbeg < mend ? (int)((mend - mbeg + BMr - 1) / BMr) : 0;
+  if (nsteps > 0) {
     gload(mbeg);
-    for (long mb = mbeg; mb < mend; mb += BK) {
-      __syncthreads();
-      sstore();
-      __syncthreads();
-      if (mb + BK < mend) gload(mb + BK);
-      if constexpr (sizeof(CT) == 2) {
-        // lane 4q+p of 16-lane group g supplies row (8g + q [+4]) and columns c0 + 4p;
-        // it receives column c0 + (lane&15) at rows 8g + 0..3 [4..7].
-        const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, g8 = (lane >> 4) * 8;
+    sstore(0);
+    __syncthreads();
+  }
+  for (int it = 0; it < nsteps; ++it) {
+    const int st = it & 1;
+    if (it + 1 < nsteps) gload(mbeg + (long)(it + 1) * BMr);
+    const CT* sA = lds + st * STAGE;
+    const CT* sB = sA + BMr * LDA;
+    if constexpr (sizeof(CT) == 2) {
+      const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, g8 = (lane >> 4) * 8;
+#pragma unroll
+      for (int ks = 0; ks < BMr / 32; ++ks) {
         bf16x8 af[RN], bfr[RK];
 #pragma unroll
         for (int i = 0; i < RN; ++i) {
-          const CT* base = sA + (g8 + q) * LDA + wn * TN_ + i * 16 + p4;
-          const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base));
-          const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) short4v*)(base + 4 * LDA));
+          const CT* base = sA + (ks * 32 + g8 + q) * LDA + wn * TN_ + i * 16 + p4;
+          const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base);
+          const short4v hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base + 4 * LDA));
           short __attribute__((ext_vector_type(8))) s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           af[i] = __builtin_bit_cast(bf16x8, s8);
         }
 #pragma unroll
         for (int j = 0; j < RK; ++j) {
-          const CT* base = sB + (g8 + q) * LDB + wk * TK_ + j * 16 + p4;
-          const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base));
-          const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) short4v*)(base + 4 * LDB));
+          const CT* base = sB + (ks * 32 + g8 + q) * LDB + wk * TK_ + j * 16 + p4;
+          const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base);
+          const short4v hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base + 4 * LDB));
           short __attribute__((ext_vector_type(8))) s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           bfr[j] = __builtin_bit_cast(bf16x8, s8);
         }
@@ -451,22 +551,24 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(Op A, Op B, float* ws, long
 #pragma unroll
           for (int j = 0; j < RK; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      } else {
+      }
+    } else {
 #pragma unroll
-        for (int s = 0; s < BK / 4; ++s) {
-          float af[RN], bfr[RK];
+      for (int s = 0; s < BMr / 4; ++s) {
+        float af[RN], bfr[RK];
 #pragma unroll
-          for (int i = 0; i < RN; ++i) af[i] = sA[(s * 4 + fq) * LDA + wn * TN_ + i * 16 + fr];
+        for (int i = 0; i < RN; ++i) af[i] = sA[(s * 4 + fq) * LDA + wn * TN_ + i * 16 + fr];
 #pragma unroll
-          for (int j = 0; j < RK; ++j) bfr[j] = sB[(s * 4 + fq) * LDB + wk * TK_ + j * 16 + fr];
+        for (int j = 0; j < RK; ++j) bfr[j] = sB[(s * 4 + fq) * LDB + wk * TK_ + j * 16 + fr];
 #pragma unroll
-          for (int i = 0; i < RN; ++i)
+        for (int i = 0; i < RN; ++i)
 #pragma unroll
-            for (int j = 0; j < RK; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
+          for (int j = 0; j < RK; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (it + 1 < nsteps) sstore(st ^ 1);
+    __syncthreads();
   }
   float* P = ws + (long)blockIdx.y * N * K;
 #pragma unroll
@@ -481,24 +583,58 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(Op A, Op B, float* ws, long
       }
 }
 
-template <typename CT, int BM, int BN, int WM, int WN>
+// ------------------------------------------------------------------------------------------
+// dispatch
+// ------------------------------------------------------------------------------------------
+template <typename CT, typename TA, int AM, int BM, int BN, int WM, int WN>
 int launch_nt(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
   const long tilesM = (M + BM - 1) / BM;
   const int tilesN = (N + BN - 1) / BN;
   const long nwg = tilesM * tilesN;
   if (nwg > 0x7fffffff) return kair_set_error(KAIR_ERR_ARG, "gemm_nt: grid too large");
-  hipLaunchKernelGGL((gemm_nt_kernel<CT, BM, BN, WM, WN>), dim3((unsigned)nwg), dim3(NT), 0, s, A, B, E, K, tilesN,
+  hipLaunchKernelGGL((gemm_nt_kernel<CT, TA, AM, BM, BN, WM, WN>), dim3((unsigned)nwg), dim3(NT), 0, s, A, B, E, K, tilesN,
                      (int)nwg);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
 
-template <typename CT>
-int dispatch_nt(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
-  if (N <= 16) return launch_nt<CT, 256, 16, 4, 1>(A, B, E, M, N, K, s);
-  if (N <= 32) return launch_nt<CT, 256, 32, 4, 1>(A, B, E, M, N, K, s);
-  if (N <= 64) return launch_nt<CT, 128, 64, 2, 2>(A, B, E, M, N, K, s);
-  return launch_nt<CT, 128, 128, 2, 2>(A, B, E, M, N, K, s);
+template <typename CT, typename TA, int AM>
+int nt_tiles(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
+  if (N <= 16) return launch_nt<CT, TA, AM, 256, 16, 4, 1>(A, B, E, M, N, K, s);
+  if (N <= 64) return launch_nt<CT, TA, AM, 128, 64, 2, 2>(A, B, E, M, N, K, s);
+  return launch_nt<CT, TA, AM, 128, 128, 2, 2>(A, B, E, M, N, K, s);
+}
+
+template <typename CT, typename TA>
+int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
+  if (mode == KAIR_LD_ROWS) return nt_tiles<CT, TA, AM_ROWS>(A, B, E, M, N, K, s);
+  if (mode == KAIR_LD_IM2COL3) return nt_tiles<CT, TA, AM_IM2COL>(A, B, E, M, N, K, s);
+  if constexpr (sizeof(TA) == sizeof(CT)) return nt_tiles<CT, TA, AM_QKV>(A, B, E, M, N, K, s);
+  return kair_set_error(KAIR_ERR_ARG, "gemm_nt: q/k/v operand must have the compute dtype");
+}
+
+template <typename CT, typename TA, typename TB, int AMA, int AMB>
+int launch_tn(const Op& a, const Op& b, float* ws, int splits, long M, int N, int K, long rps, hipStream_t s) {
+  if (N <= 64 && K <= 64) {
+    const int tilesN = (N + 63) / 64, tilesK = (K + 63) / 64;
+    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 64, 64>), dim3(tilesN * tilesK, splits), dim3(NT), 0, s, a, b,
+                       ws, M, N, K, rps, tilesK);
+  } else {
+    const int tilesN = (N + 127) / 128, tilesK = (K + 127) / 128;
+    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 128, 128>), dim3(tilesN * tilesK, splits), dim3(NT), 0, s, a,
+                       b, ws, M, N, K, rps, tilesK);
+  }
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename CT, typename TA, int AMA>
+int tn_b(int bmode, int bdt, const Op& a, const Op& b, float* ws, int splits, long M, int N, int K, long rps, hipStream_t s) {
+  if (bmode == KAIR_LD_ROWS)
+    return bdt == KAIR_BF16 ? launch_tn<CT, TA, bf16, AMA, AM_ROWS>(a, b, ws, splits, M, N, K, rps, s)
+                            : launch_tn<CT, TA, float, AMA, AM_ROWS>(a, b, ws, splits, M, N, K, rps, s);
+  return bdt == KAIR_BF16 ? launch_tn<CT, TA, bf16, AMA, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, s)
+                          : launch_tn<CT, TA, float, AMA, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, s);
 }
 
 }  // namespace
@@ -548,19 +684,27 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
   if ((rc = check_operand(B, "gemm_nt B"))) return rc;
   KAIR_CHECK_ARG(E && E->out, "gemm_nt: null epilogue/out");
   KAIR_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 8 == 0, "gemm_nt: bad M/N/K (%ld,%d,%d), K%%8 must be 0", M, N, K);
-  KAIR_CHECK_ARG(E->out_mode != KAIR_OUT_PSHUF || E->ps_r > 0, "gemm_nt: pixel shuffle r");
+  KAIR_CHECK_ARG(B->mode == KAIR_LD_ROWS && B->dtype == compute && B->win_ws == 0,
+                 "gemm_nt: B must be packed rows of the compute dtype");
+  KAIR_CHECK_ARG(compute == KAIR_BF16 || A->dtype == KAIR_F32, "gemm_nt: fp32 compute needs fp32 A");
+  KAIR_CHECK_ARG((E->out_mode != KAIR_OUT_PSHUF && E->out_mode != KAIR_OUT_PUNSHUF && E->out_mode != KAIR_OUT_PSHUF_NCHW) ||
+                     E->ps_r > 0, "gemm_nt: pixel shuffle r");
+  KAIR_CHECK_ARG(E->out_mode != KAIR_OUT_QKVBLK || (E->qkv_hdp % 8 == 0 && E->qkv_tok > 0), "gemm_nt: qkv epilogue");
   const Op a = make_op(*A, M), b = make_op(*B, N);
   const Epi e = make_epi(*E, M, N);
   hipStream_t s = (hipStream_t)stream;
-  if (compute == KAIR_BF16) return dispatch_nt<bf16>(a, b, e, M, N, K, s);
-  if (compute == KAIR_F32) return dispatch_nt<float>(a, b, e, M, N, K, s);
+  if (compute == KAIR_BF16) {
+    if (A->dtype == KAIR_BF16) return nt_modes<bf16, bf16>(A->mode, a, b, e, M, N, K, s);
+    return nt_modes<bf16, float>(A->mode, a, b, e, M, N, K, s);
+  }
+  if (compute == KAIR_F32) return nt_modes<float, float>(A->mode, a, b, e, M, N, K, s);
   return kair_set_error(KAIR_ERR_ARG, "gemm_nt: bad compute type");
 }
 
 extern "C" int kair_wgrad_splits(long M, int N, int K) {
-  const long tiles = (long)((N + 127) / 128) * ((K + 127) / 128);
-  long s = 512 / (tiles > 0 ? tiles : 1);
-  const long maxs = (M + 255) / 256;
+  const long tiles = (N <= 64 && K <= 64) ? 1 : (long)((N + 127) / 128) * ((K + 127) / 128);
+  long s = 640 / (tiles > 0 ? tiles : 1);
+  const long maxs = (M + 511) / 512;
   if (s > maxs) s = maxs;
   if (s < 1) s = 1;
   return (int)s;
@@ -573,26 +717,25 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
   if ((rc = check_operand(B, "gemm_tn B"))) return rc;
   KAIR_CHECK_ARG(ws, "gemm_tn: null workspace");
   KAIR_CHECK_ARG(M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % 8 == 0 && splits > 0, "gemm_tn: bad sizes");
-  Op a = make_op(*A, M), b = make_op(*B, M);
+  KAIR_CHECK_ARG(A->mode != KAIR_LD_IM2COL3, "gemm_tn: A cannot be im2col");
+  KAIR_CHECK_ARG(B->mode != KAIR_LD_QKVBLK, "gemm_tn: B cannot be q/k/v blocked");
+  KAIR_CHECK_ARG(compute == KAIR_BF16 || (A->dtype == KAIR_F32 && B->dtype == KAIR_F32),
+                 "gemm_tn: fp32 compute needs fp32 operands");
+  KAIR_CHECK_ARG(A->mode != KAIR_LD_QKVBLK || A->dtype == compute, "gemm_tn: q/k/v operand dtype");
+  const Op a = make_op(*A, M), b = make_op(*B, M);
+  const int BMr = compute == KAIR_BF16 ? 64 : 32;
   long rps = (M + splits - 1) / splits;
-  rps = (rps + BK - 1) / BK * BK;
+  rps = (rps + BMr - 1) / BMr * BMr;
   hipStream_t s = (hipStream_t)stream;
-  const bool small = (N <= 64 && K <= 64);
-  if (small) {
-    const int tilesN = (N + 63) / 64, tilesK = (K + 63) / 64;
-    dim3 grid(tilesN * tilesK, splits);
-    if (compute == KAIR_BF16)
-      hipLaunchKernelGGL((gemm_tn_kernel<bf16, 64, 64>), grid, dim3(NT), 0, s, a, b, ws, M, N, K, rps, tilesK);
-    else
-      hipLaunchKernelGGL((gemm_tn_kernel<float, 64, 64>), grid, dim3(NT), 0, s, a, b, ws, M, N, K, rps, tilesK);
-  } else {
-    const int tilesN = (N + 127) / 128, tilesK = (K + 127) / 128;
-    dim3 grid(tilesN * tilesK, splits);
-    if (compute == KAIR_BF16)
-      hipLaunchKernelGGL((gemm_tn_kernel<bf16, 128, 128>), grid, dim3(NT), 0, s, a, b, ws, M, N, K, rps, tilesK);
-    else
-      hipLaunchKernelGGL((gemm_tn_kernel<float, 128, 128>), grid, dim3(NT), 0, s, a, b, ws, M, N, K, rps, tilesK);
+  if (compute == KAIR_BF16) {
+    if (A->mode == KAIR_LD_QKVBLK) return tn_b<bf16, bf16, AM_QKV>(B->mode, B->dtype, a, b, ws, splits, M, N, K, rps, s);
+    if (A->dtype == KAIR_BF16) return tn_b<bf16, bf16, AM_ROWS>(B->mode, B->dtype, a, b, ws, splits, M, N, K, rps, s);
+    return tn_b<bf16, float, AM_ROWS>(B->mode, B->dtype, a, b, ws, splits, M, N, K, rps, s);
   }
-  KAIR_CHECK_LAUNCH();
-  return 0;
+  if (A->mode == KAIR_LD_QKVBLK) {
+    if (B->mode == KAIR_LD_ROWS) return launch_tn<float, float, float, AM_QKV, AM_ROWS>(a, b, ws, splits, M, N, K, rps, s);
+    return launch_tn<float, float, float, AM_QKV, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, s);
+  }
+  if (B->mode == KAIR_LD_ROWS) return launch_tn<float, float, float, AM_ROWS, AM_ROWS>(a, b, ws, splits, M, N, K, rps, s);
+  return launch_tn<float, float, float, AM_ROWS, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, s);
 }

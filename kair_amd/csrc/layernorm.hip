@@ -114,18 +114,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   }
 }
 
-__global__ void ln_param_reduce(const float* __restrict__ part, int nb, int C, float* dgamma, float* dbeta, int acc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * C) return;
+// 64 columns per block, 4 row-phases per column, fixed summation order (deterministic)
+__global__ __launch_bounds__(256) void ln_param_reduce(const float* __restrict__ part, int nb, int C, float* dgamma,
+                                                       float* dbeta, int acc) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(long)b * 2 * C + c];
-  float* o = c < C ? dgamma + c : dbeta + (c - C);
-  *o = acc ? *o + s : s;
+  if (c < 2 * C)
+    for (int b = ty; b < nb; b += 4) s += part[(long)b * 2 * C + c];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < 2 * C) {
+    s = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+    float* o = c < C ? dgamma + c : dbeta + (c - C);
+    *o = acc ? *o + s : s;
+  }
 }
 
 }  // namespace
 
-constexpr int LN_BLOCKS = 1024;
+constexpr int LN_BLOCKS = 512;
 
 extern "C" int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype, long ldy, const float* gamma,
                                   const float* beta, float* mean, float* rstd, long M, int C, float eps, int win_H,
@@ -164,7 +173,7 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
     hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const float*)dy, ldy, gamma,
                        mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm);
   KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 255) / 256), dim3(256), 0, s, ws, (int)nb, C, dgamma, dbeta,
+  hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 63) / 64), dim3(256), 0, s, ws, (int)nb, C, dgamma, dbeta,
                      dparam_accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;

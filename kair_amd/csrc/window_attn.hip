@@ -447,24 +447,32 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const typename AT<BF>::T*
       for (int r = 0; r < 16; ++r) out[(qt * 32 + acc_row(r, hh)) * TOK + kt * 32 + l31] = dB[qt][kt][r];
 }
 
-// dtable[idx][h] (+)= sum_groups sum_{(q,k): relidx(q,k)=idx} dB_part[g][h][q][k]
-__global__ void attn_dtable_kernel(const float* __restrict__ dB_part, long ngroups, int nh, float* dtable, int acc) {
+// stage 1: dB[h][q][k] = sum over groups of the per-group partials (coalesced, one thread per entry)
+__global__ void attn_dbias_sum_kernel(const float* __restrict__ dB_part, long ngroups, int nh, float* __restrict__ dB) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = nh * TOK * TOK;
+  if (t >= n) return;
+  float s = 0.f;
+  for (long g = 0; g < ngroups; ++g) s += dB_part[g * n + t];
+  dB[t] = s;
+}
+
+// stage 2: dtable[idx][h] (+)= sum_{(q,k): relidx(q,k)=idx} dB[h][q][k]
+__global__ void attn_dtable_kernel(const float* __restrict__ dB, int nh, float* dtable, int acc) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int nidx = (2 * WS - 1) * (2 * WS - 1);
   if (t >= nidx * nh) return;
   const int idx = t / nh, h = t - (t / nh) * nh;
   const int dy = idx / (2 * WS - 1) - (WS - 1), dx = idx % (2 * WS - 1) - (WS - 1);
+  const float* p = dB + (long)h * TOK * TOK;
   float s = 0.f;
-  for (long g = 0; g < ngroups; ++g) {
-    const float* p = dB_part + (g * nh + h) * TOK * TOK;
-    for (int qy = 0; qy < WS; ++qy) {
-      const int ky = qy - dy;
-      if (ky < 0 || ky >= WS) continue;
-      for (int qx = 0; qx < WS; ++qx) {
-        const int kx = qx - dx;
-        if (kx < 0 || kx >= WS) continue;
-        s += p[(qy * WS + qx) * TOK + ky * WS + kx];
-      }
+  for (int qy = 0; qy < WS; ++qy) {
+    const int ky = qy - dy;
+    if (ky < 0 || ky >= WS) continue;
+    for (int qx = 0; qx < WS; ++qx) {
+      const int kx = qx - dx;
+      if (kx < 0 || kx >= WS) continue;
+      s += p[(qy * WS + qx) * TOK + ky * WS + kx];
     }
   }
   dtable[idx * nh + h] = acc ? dtable[idx * nh + h] + s : s;
@@ -495,7 +503,7 @@ extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* tab
   return 0;
 }
 
-extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) { return ((nWin + WPG - 1) / WPG) * nh * TOK * TOK; }
+extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) { return ((nWin + WPG - 1) / WPG + 1) * nh * TOK * TOK; }
 
 extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
                                     const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
@@ -516,9 +524,11 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
     hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
                        ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, WPG, scale, H, W, shift);
   KAIR_CHECK_LAUNCH();
+  float* dB = ws + ngroups * nh * TOK * TOK;
+  hipLaunchKernelGGL(attn_dbias_sum_kernel, dim3((nh * TOK * TOK + 255) / 256), dim3(256), 0, s, ws, ngroups, nh, dB);
+  KAIR_CHECK_LAUNCH();
   const int nt = (2 * WS - 1) * (2 * WS - 1) * nh;
-  hipLaunchKernelGGL(attn_dtable_kernel, dim3((nt + 127) / 128), dim3(128), 0, s, ws, ngroups, nh, dtable,
-                     dtable_accumulate);
+  hipLaunchKernelGGL(attn_dtable_kernel, dim3((nt + 127) / 128), dim3(128), 0, s, dB, nh, dtable, dtable_accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

@@ -563,7 +563,9 @@ class SwinIRFunction(torch.autograd.Function):
 
 def drop_path_scales(engine, B, device, generator=None):
     """Per-block, per-branch stochastic-depth scales (timm DropPath semantics: keep-mask / keep)."""
-    rates = torch.tensor([b.dp for b in engine.blocks], device=device)
-    keep = (1.0 - rates).view(-1, 1, 1)
+    keep = getattr(engine, "_keep", None)
+    if keep is None or keep.device != torch.device(device):   # built once, outside any graph capture
+        rates = torch.tensor([b.dp for b in engine.blocks], dtype=torch.float32)
+        keep = engine._keep = (1.0 - rates).view(-1, 1, 1).to(device)
     u = torch.rand(len(engine.blocks), 2, B, device=device, generator=generator)
     return (u < keep).float() / keep

@@ -65,6 +65,9 @@ class FusedTrainer:
         self.static = None
         self.warm = 0
         self.engine._packed_version = None
+        if any(b.dp > 0 for b in self.engine.blocks):
+            from .swinir_engine import drop_path_scales
+            drop_path_scales(self.engine, 1, self.device)   # materialise the keep-prob table eagerly
 
     # ------------------------------------------------------------------------------------
     def _allreduce(self):
@@ -100,7 +103,9 @@ class FusedTrainer:
         """One training step on the batch (L, Hh) (device tensors).  Returns the device loss [1]."""
         self._set_scalars()
         if not self.use_graph:
-            return self._body(L, Hh)
+            out = self._body(L, Hh)
+            self.engine._packed_version = None
+            return out
         if self.static is None or self.static[0].shape != L.shape or self.static[1].shape != Hh.shape:
             self.static = (torch.empty_like(L), torch.empty_like(Hh))
             self.graph = None
@@ -116,6 +121,9 @@ class FusedTrainer:
             self.graph = g
         if self.graph is not None:
             self.graph.replay()
-            return self.loss_out
-        self.warm += 1
-        return self._body(*self.static)
+            out = self.loss_out
+        else:
+            self.warm += 1
+            out = self._body(*self.static)
+        self.engine._packed_version = None   # params were updated in place by the Adam kernel
+        return out
