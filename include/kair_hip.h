@@ -108,6 +108,21 @@ typedef struct {
 
 /* dst (packed, dtype) <- src (reference fp32).  Pad entries written as 0. */
 int kair_pack_weight(const float* src, void* dst, int dst_dtype, const kair_wmap* map, void* stream);
+/* Batched packing: every weight re-pack of a step in one launch (one job per kair_pack_weight call). */
+typedef struct kair_pack_job {
+  const float* src;
+  void* dst;
+  int dst_dtype;
+  int reserved;
+  kair_wmap map;
+  long total; /* filled by kair_pack_table_build */
+} kair_pack_job;
+/* bytes of device memory the job table needs */
+long kair_pack_table_bytes(int njobs);
+/* validate jobs, copy the table to device memory (synchronous); returns the launch's block count
+ * (> 0) or a negative error code.  Call outside stream capture. */
+long kair_pack_table_build(kair_pack_job* jobs, int njobs, void* table_dev);
+int kair_pack_weights(const void* table_dev, int njobs, long nblocks, void* stream);
 /* grad_ref (fp32 reference layout) = sum_s partial[s] (packed layout [Np][Kp]);
  * bias_grad (if non-NULL) = column ones_col of the sum.  accumulate: += instead of =. */
 int kair_wgrad_finalize(const float* partial, int splits, const kair_wmap* map, float* grad_ref,

@@ -45,12 +45,20 @@ class WMap(ctypes.Structure):
                 ("kG", c_int), ("kGr", c_int), ("kGp", c_int)]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [("src", c_vp), ("dst", c_vp), ("dst_dtype", c_int), ("reserved", c_int), ("map", WMap),
+                ("total", c_long)]
+
+
 _SIGS = {
     "kair_gemm_nt": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), ctypes.POINTER(Epilogue), c_long, c_int, c_int,
                      c_int, c_vp],
     "kair_wgrad_splits": [c_long, c_int, c_int],
     "kair_gemm_tn": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), c_vp, c_int, c_long, c_int, c_int, c_int, c_vp],
     "kair_pack_weight": [c_vp, c_vp, c_int, ctypes.POINTER(WMap), c_vp],
+    "kair_pack_table_bytes": [c_int],
+    "kair_pack_table_build": [ctypes.POINTER(PackJob), c_int, c_vp],
+    "kair_pack_weights": [c_vp, c_int, c_long, c_vp],
     "kair_wgrad_finalize": [c_vp, c_int, ctypes.POINTER(WMap), c_vp, c_vp, c_int, c_int, c_vp],
     "kair_colsum": [ctypes.POINTER(Operand), c_long, c_int, ctypes.POINTER(WMap), c_vp, c_vp, c_int, c_vp],
     "kair_layernorm_fwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_float, c_int,
@@ -69,7 +77,8 @@ _SIGS = {
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
-_RESTYPE = {"kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long}
+_RESTYPE = {"kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
+            "kair_pack_table_build": c_long}
 
 _lib = None
 
@@ -225,6 +234,26 @@ def gemm_tn(A, B, ws, splits, M, N, K, compute):
 
 def pack_weight(src, dst, m):
     check(lib().kair_pack_weight(ptr(src), ptr(dst), dtype_code(dst), ctypes.byref(m), stream_ptr()), "pack_weight")
+
+
+class PackTable:
+    """Every (src, dst, map) re-pack of a network, launched as ONE kernel (kair_pack_weights)."""
+
+    def __init__(self, jobs):
+        n = len(jobs)
+        arr = (PackJob * n)()
+        for i, (src, dst, m) in enumerate(jobs):
+            arr[i].src, arr[i].dst, arr[i].dst_dtype, arr[i].map = ptr(src), ptr(dst), dtype_code(dst), m
+        self._keep = [(s, d) for s, d, _ in jobs]
+        self.n = n
+        self.table = torch.empty(lib().kair_pack_table_bytes(n), dtype=torch.uint8, device=jobs[0][1].device)
+        nb = lib().kair_pack_table_build(arr, n, ptr(self.table))
+        if nb <= 0:
+            check(int(nb) or -1, "pack_table_build")
+        self.nblocks = nb
+
+    def run(self):
+        check(lib().kair_pack_weights(ptr(self.table), self.n, self.nblocks, stream_ptr()), "pack_weights")
 
 
 def wgrad_finalize(partial, splits, m, grad, bias_grad=None, ones_col=-1, accumulate=False):

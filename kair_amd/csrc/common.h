@@ -76,3 +76,28 @@ KAIR_DEV long win_to_token(long m, const WinMap& w) {
   if (x >= w.W) x -= w.W;
   return (b * w.H + y) * (long)w.W + x;
 }
+
+// Deterministic sum over `nparts` partial planes for 64 consecutive outputs per 1024-thread block:
+// thread (tx, ty) sums planes ty, ty+16, ... at plane offset `off`, then the 16 phases are added in
+// fixed order.  Returns the total in threads with ty == 0 (others get 0).
+KAIR_DEV float split_sum16(const float* __restrict__ part, long nparts, long plane, long off, bool valid) {
+  __shared__ float red[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  float s0 = 0.f, s1 = 0.f;
+  if (valid) {
+    long i = ty;
+    for (; i + 16 < nparts; i += 32) {
+      s0 += part[i * plane + off];
+      s1 += part[(i + 16) * plane + off];
+    }
+    if (i < nparts) s0 += part[i * plane + off];
+  }
+  red[ty][tx] = s0 + s1;
+  __syncthreads();
+  float s = 0.f;
+  if (ty == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][tx];
+  }
+  return s;
+}

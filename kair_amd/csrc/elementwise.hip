@@ -2,6 +2,9 @@
 // MFMA layouts, deterministic weight-gradient finalisation, image <-> token layout, the L1 loss
 // (nn.L1Loss mean, model_plain.py:183-188) and the fused Adam + EMA update (torch.optim.Adam maths,
 // model_plain.py:210-222/302; ModelBase.update_E model_base.py:247-252).
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.h"
 
 namespace {
@@ -12,9 +15,7 @@ KAIR_DEV int unpad(int ip, int G, int Gr, int Gp) {
   return (g < G && i < Gr) ? g * Gr + i : -1;
 }
 
-__global__ void pack_kernel(const float* __restrict__ src, void* __restrict__ dst, int dt, kair_wmap mp, long total) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= total) return;
+KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst, int dt, const kair_wmap& mp, long t) {
   const int Np = mp.nG * mp.nGp, Kp = mp.kG * mp.kGp;
   float v = 0.f;
   if (mp.kind == 0 || mp.kind == 3) {  // linear [Np][Kp] (or transposed [Kp][Np])
@@ -43,36 +44,62 @@ __global__ void pack_kernel(const float* __restrict__ src, void* __restrict__ ds
   else ((float*)dst)[t] = v;
 }
 
-// one thread per reference weight element (+ bias elements): sum of the split partials
-__global__ void wgrad_finalize_kernel(const float* __restrict__ part, int splits, kair_wmap mp, float* grad,
-                                      float* bias_grad, int ones_col, int acc, long nw, long Kt, long plane) {
+__global__ void pack_kernel(const float* __restrict__ src, void* __restrict__ dst, int dt, kair_wmap mp, long total) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long nb = bias_grad ? mp.N : 0;
-  if (t >= nw + nb) return;
-  long off;
-  if (t < nw) {
-    if (mp.kind == 0) {
-      const int n = (int)(t / mp.K), k = (int)(t - (long)n * mp.K);
-      const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr, kp = (k / mp.kGr) * mp.kGp + k % mp.kGr;
-      off = (long)np * Kt + kp;
-    } else {  // conv: grad[co][ci][tap]
-      const int co = (int)(t / ((long)mp.K * 9));
-      const int rem = (int)(t - (long)co * mp.K * 9);
-      const int ci = rem / 9, tap = rem - (rem / 9) * 9;
-      const int np = (co / mp.nGr) * mp.nGp + co % mp.nGr;
-      const int cip = (ci / mp.kGr) * mp.kGp + ci % mp.kGr;
-      const int Cip = mp.kG * mp.kGp;
-      off = (long)np * Kt + (long)tap * Cip + cip;
-    }
-  } else {
-    const int n = (int)(t - nw);
-    const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr;
-    off = (long)np * Kt + ones_col;
+  if (t < total) pack_element(src, dst, dt, mp, t);
+}
+
+// All packs of a network in one launch: table = kair_pack_job[njobs] followed by the first block
+// of every job (long[njobs + 1]); each block finds its job by binary search (uniform, scalar loads).
+__global__ __launch_bounds__(256) void pack_batched_kernel(const kair_pack_job* __restrict__ jobs, int njobs,
+                                                           const long* __restrict__ first) {
+  const long bid = blockIdx.x;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (first[mid] <= bid) lo = mid;
+    else hi = mid - 1;
   }
-  float s = 0.f;
-  for (int i = 0; i < splits; ++i) s += part[(long)i * plane + off];
-  float* o = t < nw ? grad + t : bias_grad + (t - nw);
-  *o = acc ? *o + s : s;
+  const kair_pack_job& j = jobs[lo];
+  const long t = (bid - first[lo]) * 256 + threadIdx.x;
+  if (t < j.total) pack_element(j.src, j.dst, j.dst_dtype, j.map, t);
+}
+
+// 64 reference weight elements (+ bias elements) per 1024-thread block; 16 split phases per
+// element, fixed summation order (deterministic).
+__global__ __launch_bounds__(1024) void wgrad_finalize_kernel(const float* __restrict__ part, int splits, kair_wmap mp,
+                                                              float* grad, float* bias_grad, int ones_col, int acc,
+                                                              long nw, long Kt, long plane) {
+  const long t = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const long nb = bias_grad ? mp.N : 0;
+  const bool valid = t < nw + nb;
+  long off = 0;
+  if (valid) {
+    if (t < nw) {
+      if (mp.kind == 0) {
+        const int n = (int)(t / mp.K), k = (int)(t - (long)n * mp.K);
+        const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr, kp = (k / mp.kGr) * mp.kGp + k % mp.kGr;
+        off = (long)np * Kt + kp;
+      } else {  // conv: grad[co][ci][tap]
+        const int co = (int)(t / ((long)mp.K * 9));
+        const int rem = (int)(t - (long)co * mp.K * 9);
+        const int ci = rem / 9, tap = rem - (rem / 9) * 9;
+        const int np = (co / mp.nGr) * mp.nGp + co % mp.nGr;
+        const int cip = (ci / mp.kGr) * mp.kGp + ci % mp.kGr;
+        const int Cip = mp.kG * mp.kGp;
+        off = (long)np * Kt + (long)tap * Cip + cip;
+      }
+    } else {
+      const int n = (int)(t - nw);
+      const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr;
+      off = (long)np * Kt + ones_col;
+    }
+  }
+  const float s = split_sum16(part, splits, plane, off, valid);
+  if (valid && threadIdx.x < 64) {
+    float* o = t < nw ? grad + t : bias_grad + (t - nw);
+    *o = acc ? *o + s : s;
+  }
 }
 
 template <typename T>
@@ -204,19 +231,61 @@ inline unsigned nblk(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
 
-extern "C" int kair_pack_weight(const float* src, void* dst, int dst_dtype, const kair_wmap* map, void* stream) {
-  KAIR_CHECK_ARG(src && dst && map, "pack_weight: null pointer");
-  const kair_wmap& mp = *map;
+static int pack_total(const kair_wmap& mp, long* total) {
   KAIR_CHECK_ARG(mp.nG > 0 && mp.nGr > 0 && mp.nGp >= mp.nGr && mp.nG * mp.nGr == mp.N, "pack_weight: bad N map");
   KAIR_CHECK_ARG(mp.kind == 4 || (mp.kG > 0 && mp.kGr > 0 && mp.kGp >= mp.kGr && mp.kG * mp.kGr == mp.K),
                  "pack_weight: bad K map");
   const long Np = (long)mp.nG * mp.nGp, Kp = (long)mp.kG * mp.kGp;
-  long total;
-  if (mp.kind == 0 || mp.kind == 3) total = Np * Kp;
-  else if (mp.kind == 1 || mp.kind == 2) total = Np * 9 * Kp;
-  else if (mp.kind == 4) total = Np;
+  if (mp.kind == 0 || mp.kind == 3) *total = Np * Kp;
+  else if (mp.kind == 1 || mp.kind == 2) *total = Np * 9 * Kp;
+  else if (mp.kind == 4) *total = Np;
   else return kair_set_error(KAIR_ERR_ARG, "pack_weight: bad kind %d", mp.kind);
-  hipLaunchKernelGGL(pack_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, src, dst, dst_dtype, mp, total);
+  return 0;
+}
+
+extern "C" int kair_pack_weight(const float* src, void* dst, int dst_dtype, const kair_wmap* map, void* stream) {
+  KAIR_CHECK_ARG(src && dst && map, "pack_weight: null pointer");
+  long total;
+  if (int rc = pack_total(*map, &total)) return rc;
+  hipLaunchKernelGGL(pack_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, src, dst, dst_dtype, *map,
+                     total);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" long kair_pack_table_bytes(int njobs) {
+  return (long)njobs * (long)sizeof(kair_pack_job) + (long)(njobs + 1) * (long)sizeof(long);
+}
+
+extern "C" long kair_pack_table_build(kair_pack_job* jobs, int njobs, void* table_dev) {
+  KAIR_CHECK_ARG(jobs && table_dev && njobs > 0, "pack_table_build: bad args");
+  const size_t jb = (size_t)njobs * sizeof(kair_pack_job);
+  char* host = (char*)malloc(jb + (size_t)(njobs + 1) * sizeof(long));
+  if (!host) return kair_set_error(KAIR_ERR_ARG, "pack_table_build: out of host memory");
+  long* first = (long*)(host + jb);
+  long nb = 0;
+  for (int i = 0; i < njobs; ++i) {
+    long total;
+    int rc = jobs[i].src && jobs[i].dst ? pack_total(jobs[i].map, &total)
+                                        : kair_set_error(KAIR_ERR_ARG, "pack_table_build: job %d null pointer", i);
+    if (rc) { free(host); return rc; }
+    jobs[i].total = total;
+    first[i] = nb;
+    nb += (total + 255) / 256;
+  }
+  first[njobs] = nb;
+  memcpy(host, jobs, jb);
+  const hipError_t e = hipMemcpy(table_dev, host, jb + (size_t)(njobs + 1) * sizeof(long), hipMemcpyHostToDevice);
+  free(host);
+  if (e != hipSuccess) return kair_set_error(KAIR_ERR_HIP, "pack_table_build: %s", hipGetErrorString(e));
+  return nb;
+}
+
+extern "C" int kair_pack_weights(const void* table_dev, int njobs, long nblocks, void* stream) {
+  KAIR_CHECK_ARG(table_dev && njobs > 0 && nblocks > 0, "pack_weights: bad args");
+  const kair_pack_job* jobs = (const kair_pack_job*)table_dev;
+  const long* first = (const long*)((const char*)table_dev + (size_t)njobs * sizeof(kair_pack_job));
+  hipLaunchKernelGGL(pack_batched_kernel, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs, first);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -231,7 +300,7 @@ extern "C" int kair_wgrad_finalize(const float* partial, int splits, const kair_
   const long Kt = mp.kind == 0 ? (long)mp.kG * mp.kGp : 9L * mp.kG * mp.kGp;
   const long nw = (long)mp.N * mp.K * (mp.kind == 1 ? 9 : 1);
   const long tot = nw + (bias_grad ? mp.N : 0);
-  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(nblk(tot, 256)), dim3(256), 0, (hipStream_t)stream, partial, splits, mp,
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(nblk(tot, 64)), dim3(1024), 0, (hipStream_t)stream, partial, splits, mp,
                      grad_ref, bias_grad, ones_col, accumulate, nw, Kt, Np * Kt);
   KAIR_CHECK_LAUNCH();
   return 0;

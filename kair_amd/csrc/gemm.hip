@@ -109,47 +109,92 @@ KAIR_DEV RowState row_state(const Op& op, long m) {
   return r;
 }
 
-// load 8 consecutive columns [k, k+8) of a resolved row
-template <int AM, typename T>
-KAIR_DEV void load_chunk(const Op& op, const RowState& r, int k, int K, float (&v)[8]) {
-  zero8(v);
-  if (r.valid && k < K) {
-    const T* P = (const T*)op.ptr;
-    if constexpr (AM == AM_ROWS) {
-      gload8<T>(P + r.base + k, v);
-    } else if constexpr (AM == AM_IM2COL) {
-      const int tap = k / op.imC;
-      const int c = k - tap * op.imC;
-      int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-      if (op.flip) { dy = -dy; dx = -dx; }
-      const int y = r.y + dy, x = r.x + dx;
-      if (y >= 0 && y < op.imH && x >= 0 && x < op.imW)
-        gload8<T>(P + (r.base + (long)dy * op.imW + dx) * op.imC + c, v);
-    } else {
-      const int pw = op.nh * op.hdp;
-      const int part = k / pw;
-      const int rr = k - part * pw;
-      const int h = rr / op.hdp, d = rr - h * op.hdp;
-      gload8<T>(P + (long)part * op.M * pw + r.base + (long)h * op.tok * op.hdp + d, v);
-    }
-    if (r.scale != 1.f) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= r.scale;
-    }
+// Two-phase chunk loads: issue() computes the address of 8 consecutive columns [k, k+8) of a
+// resolved row and starts the global load into raw registers WITHOUT consuming it (invalid chunks
+// load from the buffer start and are masked later); commit() converts / masks / scales and writes
+// LDS after the MFMAs of the current step, so the load latency overlaps them.
+template <typename T> struct Raw;
+template <> struct Raw<bf16> { uint4 a; };
+template <> struct Raw<float> { uint4 a, b; };
+
+struct Pend {
+  float scale;   // 0 => masked chunk
+  int ones;      // index in [0, 8) of the fused ones column, else -1
+};
+
+template <typename T>
+KAIR_DEV void raw_load(const T* p, Raw<T>& r) {
+  if constexpr (sizeof(T) == 2) {
+    r.a = *(const uint4*)p;
+  } else {
+    r.a = *(const uint4*)p;
+    r.b = *(const uint4*)(p + 4);
   }
-  if (op.ones_col >= k && op.ones_col < k + 8) v[op.ones_col - k] = 1.f;
 }
 
-template <typename CT>
-KAIR_DEV void lds_store8(CT* base, const float (&v)[8]) {
+template <int AM, typename T>
+KAIR_DEV void issue_chunk(const Op& op, const RowState& r, int k, int K, Raw<T>& raw, Pend& pd) {
+  bool ok = r.valid && k < K;
+  long off = 0;
+  if constexpr (AM == AM_ROWS) {
+    off = r.base + k;
+  } else if constexpr (AM == AM_IM2COL) {
+    const int tap = k / op.imC;
+    const int c = k - tap * op.imC;
+    int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    if (op.flip) { dy = -dy; dx = -dx; }
+    const int y = r.y + dy, x = r.x + dx;
+    ok = ok && y >= 0 && y < op.imH && x >= 0 && x < op.imW;
+    off = (r.base + (long)dy * op.imW + dx) * op.imC + c;
+  } else {
+    const int pw = op.nh * op.hdp;
+    const int part = k / pw;
+    const int rr = k - part * pw;
+    const int h = rr / op.hdp, d = rr - h * op.hdp;
+    off = (long)part * op.M * pw + r.base + (long)h * op.tok * op.hdp + d;
+  }
+  raw_load<T>((const T*)op.ptr + (ok ? off : 0), raw);
+  pd.scale = ok ? r.scale : 0.f;
+  pd.ones = (r.valid && op.ones_col >= k && op.ones_col < k + 8) ? op.ones_col - k : -1;
+}
+
+template <typename T>
+KAIR_DEV void raw_to_f32(const Raw<T>& r, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 q = __builtin_bit_cast(bf16x8, r.a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
+  } else {
+    const float4 a = __builtin_bit_cast(float4, r.a), b = __builtin_bit_cast(float4, r.b);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+
+template <typename CT, typename T>
+KAIR_DEV void commit_chunk(CT* dst, const Raw<T>& raw, const Pend& pd) {
+  if constexpr (sizeof(CT) == 2 && sizeof(T) == 2) {
+    if (pd.scale == 1.f && pd.ones < 0) {          // common case: raw bf16 straight to LDS
+      *(uint4*)dst = raw.a;
+      return;
+    }
+    if (pd.scale == 0.f && pd.ones < 0) {
+      *(uint4*)dst = make_uint4(0, 0, 0, 0);
+      return;
+    }
+  }
+  float v[8];
+  raw_to_f32<T>(raw, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (j == pd.ones) ? 1.f : (pd.scale == 0.f ? 0.f : v[j] * pd.scale);
   if constexpr (sizeof(CT) == 2) {
     bf16x8 q;
 #pragma unroll
     for (int j = 0; j < 8; ++j) q[j] = (bf16)v[j];
-    *(bf16x8*)base = q;
+    *(bf16x8*)dst = q;
   } else {
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) *(float2*)(base + j) = make_float2(v[j], v[j + 1]);
+    for (int j = 0; j < 8; j += 2) *(float2*)(dst + j) = make_float2(v[j], v[j + 1]);
   }
 }
 
@@ -350,12 +395,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_kernel(Op A, Op B, Epi E, int K
     const int c = tid + p * NT;
     rb[p] = row_state<AM_ROWS, CT>(B, c < CB ? (long)(n0 + c / CPR) : B.M);
   }
-  float va[PA][8], vb[PB][8];
+  Raw<TA> va[PA];
+  Raw<CT> vb[PB];
+  Pend pa[PA], pb[PB];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int p = 0; p < PA; ++p) load_chunk<AM, TA>(A, ra[p], k0 + ((tid + p * NT) % CPR) * 8, K, va[p]);
+    for (int p = 0; p < PA; ++p) issue_chunk<AM, TA>(A, ra[p], k0 + ((tid + p * NT) % CPR) * 8, K, va[p], pa[p]);
 #pragma unroll
-    for (int p = 0; p < PB; ++p) load_chunk<AM_ROWS, CT>(B, rb[p], k0 + ((tid + p * NT) % CPR) * 8, K, vb[p]);
+    for (int p = 0; p < PB; ++p) issue_chunk<AM_ROWS, CT>(B, rb[p], k0 + ((tid + p * NT) % CPR) * 8, K, vb[p], pb[p]);
   };
   auto sstore = [&](int st) {
     CT* sA = lds + st * STAGE;
@@ -363,12 +410,12 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_kernel(Op A, Op B, Epi E, int K
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
       const int c = tid + p * NT;
-      if (c < CA) lds_store8<CT>(sA + (c / CPR) * LD + (c % CPR) * 8, va[p]);
+      if (c < CA) commit_chunk<CT, TA>(sA + (c / CPR) * LD + (c % CPR) * 8, va[p], pa[p]);
     }
 #pragma unroll
     for (int p = 0; p < PB; ++p) {
       const int c = tid + p * NT;
-      if (c < CB) lds_store8<CT>(sB + (c / CPR) * LD + (c % CPR) * 8, vb[p]);
+      if (c < CB) commit_chunk<CT, CT>(sB + (c / CPR) * LD + (c % CPR) * 8, vb[p], pb[p]);
     }
   };
 
@@ -467,7 +514,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_tn_kernel(Op A, Op B, float* ws, l
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WK, wk = wave % WK;
 
-  float va[PA][8], vb[PB][8];
+  Raw<TA> va[PA];
+  Raw<TB> vb[PB];
+  Pend pa[PA], pb[PB];
   auto gload = [&](long mb) {
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
@@ -475,8 +524,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_tn_kernel(Op A, Op B, float* ws, l
       if (c < CA) {
         const long m = mb + c / CPA;
         const RowState r = row_state<AMA, TA>(A, m < mend ? m : A.M);
-        load_chunk<AMA, TA>(A, r, n0 + (c % CPA) * 8, N, va[p]);
-        if (m >= mend) zero8(va[p]);
+        issue_chunk<AMA, TA>(A, r, n0 + (c % CPA) * 8, N, va[p], pa[p]);
       }
     }
 #pragma unroll
@@ -485,8 +533,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_tn_kernel(Op A, Op B, float* ws, l
       if (c < CB) {
         const long m = mb + c / CPB;
         const RowState r = row_state<AMB, TB>(B, m < mend ? m : B.M);
-        load_chunk<AMB, TB>(B, r, k0 + (c % CPB) * 8, K, vb[p]);
-        if (m >= mend) zero8(vb[p]);
+        issue_chunk<AMB, TB>(B, r, k0 + (c % CPB) * 8, K, vb[p], pb[p]);
       }
     }
   };
@@ -496,12 +543,12 @@ __global__ __launch_bounds__(NT, 2) void gemm_tn_kernel(Op A, Op B, float* ws, l
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
       const int c = tid + p * NT;
-      if (c < CA) lds_store8<CT>(sA + (c / CPA) * LDA + (c % CPA) * 8, va[p]);
+      if (c < CA) commit_chunk<CT, TA>(sA + (c / CPA) * LDA + (c % CPA) * 8, va[p], pa[p]);
     }
 #pragma unroll
     for (int p = 0; p < PB; ++p) {
       const int c = tid + p * NT;
-      if (c < CB) lds_store8<CT>(sB + (c / CPB) * LDB + (c % CPB) * 8, vb[p]);
+      if (c < CB) commit_chunk<CT, TB>(sB + (c / CPB) * LDB + (c % CPB) * 8, vb[p], pb[p]);
     }
   };
 
@@ -703,8 +750,10 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
 
 extern "C" int kair_wgrad_splits(long M, int N, int K) {
   const long tiles = (N <= 64 && K <= 64) ? 1 : (long)((N + 127) / 128) * ((K + 127) / 128);
-  long s = 640 / (tiles > 0 ? tiles : 1);
-  const long maxs = (M + 511) / 512;
+  // enough (tile, split) CTAs for ~2 per CU, but >= 1024 rows per split so the fp32 partial
+  // planes stay small next to the operand traffic (wgrad_finalize reads them all back)
+  long s = 512 / (tiles > 0 ? tiles : 1);
+  const long maxs = (M + 1023) / 1024;
   if (s > maxs) s = maxs;
   if (s < 1) s = 1;
   return (int)s;

@@ -1,49 +1,87 @@
 // LayerNorm over the channel dim of token matrices (nn.LayerNorm(C), eps 1e-5:
-// network_swinir.py:199,205,520,725).  One wave per token row; C <= 256 fits 4 values per lane.
-// The forward can write its output straight into Swin window order (the gather that
-// torch.roll + window_partition perform in network_swinir.py:250-256), so the QKV GEMM reads a
-// plain row-major operand.  Backward accumulates into the fp32 residual-stream gradient and
-// produces deterministic per-block partial sums for dgamma / dbeta.
+// network_swinir.py:199,205,520,725).  16 lanes own one token row (4 rows per wave64), each lane
+// holding float4 column groups, so a wave keeps four independent rows in flight and the row
+// reductions are 4 shuffle steps.  The forward can write its output straight into Swin window
+// order (the gather that torch.roll + window_partition perform in network_swinir.py:250-256), so the
+// QKV GEMM reads a plain row-major operand.  Backward accumulates into the fp32 residual-stream
+// gradient and produces deterministic per-block partial sums for dgamma / dbeta.
 #include "common.h"
 
 namespace {
 
-constexpr int MAXV = 4;  // C <= 256
+constexpr int LPR = 16;              // lanes per row
+constexpr int NV = 4;                // float4 groups per lane: C <= 16 * 4 * 4 = 256
+constexpr int ROWS_PER_BLOCK_ITER = 16;  // 4 waves x 4 rows
+
+KAIR_DEV float group_sum16(float v) {
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T> KAIR_DEV void store4(T* p, float a, float b, float c, float d);
+template <> KAIR_DEV void store4<float>(float* p, float a, float b, float c, float d) {
+  *(float4*)p = make_float4(a, b, c, d);
+}
+template <> KAIR_DEV void store4<bf16>(bf16* p, float a, float b, float c, float d) {
+  bf16x4 q = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+  *(bf16x4*)p = q;
+}
+template <typename T> KAIR_DEV float4 load4(const T* p);
+template <> KAIR_DEV float4 load4<float>(const float* p) { return *(const float4*)p; }
+template <> KAIR_DEV float4 load4<bf16>(const bf16* p) {
+  const bf16x4 q = *(const bf16x4*)p;
+  return make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, long ldx, T* __restrict__ y, long ldy,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
                                                       int C, float eps, WinMap wm) {
-  const int lane = threadIdx.x & 63;
-  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const long nw = (long)gridDim.x * 4;
-  for (long r = wave; r < M; r += nw) {       // r = output row (window order if wm.ws > 0)
-    const long t = win_to_token(r, wm);         // token row
-    float v[MAXV];
+  const int sub = threadIdx.x & (LPR - 1);
+  const long grp = (long)blockIdx.x * ROWS_PER_BLOCK_ITER + (threadIdx.x >> 4);
+  const long ng = (long)gridDim.x * ROWS_PER_BLOCK_ITER;
+  for (long r = grp; r < M; r += ng) {        // r = output row (window order if wm.ws > 0)
+    const long t = win_to_token(r, wm);
+    float4 v[NV];
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const int c = lane + 64 * i;
-      v[i] = c < C ? x[t * ldx + c] : 0.f;
-      s += v[i];
+    for (int i = 0; i < NV; ++i) {
+      const int c = (sub + LPR * i) * 4;
+      v[i] = c < C ? *(const float4*)(x + t * ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c + 4 > C) {  // column group straddling C: pad lanes do not count
+        if (c + 1 >= C) v[i].y = 0.f;
+        if (c + 2 >= C) v[i].z = 0.f;
+        if (c + 3 >= C) v[i].w = 0.f;
+      }
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
     }
-    const float mu = wave_sum(s) / C;
+    const float mu = group_sum16(s) / C;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const int c = lane + 64 * i;
-      const float d = c < C ? v[i] - mu : 0.f;
-      q += d * d;
+    for (int i = 0; i < NV; ++i) {
+      const int c = (sub + LPR * i) * 4;
+      if (c < C) {
+        const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
+        // the column group straddling C (C % 4 != 0) must not count pad lanes
+        q += a * a + (c + 1 < C ? b * b : 0.f) + (c + 2 < C ? cc * cc : 0.f) + (c + 3 < C ? d * d : 0.f);
+      }
     }
-    const float rs = rsqrtf(wave_sum(q) / C + eps);
+    const float rs = rsqrtf(group_sum16(q) / C + eps);
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const int c = lane + 64 * i;
-      if (c < C) y[r * ldy + c] = (T)((v[i] - mu) * rs * gamma[c] + beta[c]);
-      else if (c < ldy) y[r * ldy + c] = (T)0.f;
+    for (int i = 0; i < NV; ++i) {
+      const int c = (sub + LPR * i) * 4;
+      if (c < ldy) {
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+        const float xv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (c + j < C) o[j] = (xv[j] - mu) * rs * gamma[c + j] + beta[c + j];
+        store4<T>(y + r * ldy + c, o[0], o[1], o[2], o[3]);
+      }
     }
-    if (lane == 0) {
+    if (sub == 0) {
       mean_out[t] = mu;
       rstd_out[t] = rs;
     }
@@ -56,77 +94,96 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
                                                       float* dx, long ld_dx, int dx_acc, float* __restrict__ part,
                                                       long M, int C, WinMap wm) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long wave = (long)blockIdx.x * 4 + w;
-  const long nw = (long)gridDim.x * 4;
-  float dg[MAXV] = {0.f, 0.f, 0.f, 0.f}, db[MAXV] = {0.f, 0.f, 0.f, 0.f};
-  float g[MAXV];
+  const int sub = threadIdx.x & (LPR - 1);
+  const long grp = (long)blockIdx.x * ROWS_PER_BLOCK_ITER + (threadIdx.x >> 4);
+  const long ng = (long)gridDim.x * ROWS_PER_BLOCK_ITER;
+  float dg[NV][4], db[NV][4], g[NV][4];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int c = lane + 64 * i;
-    g[i] = c < C ? gamma[c] : 0.f;
-  }
-  for (long r = wave; r < M; r += nw) {
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = (sub + LPR * i) * 4 + j;
+      dg[i][j] = db[i][j] = 0.f;
+      g[i][j] = c < C ? gamma[c] : 0.f;
+    }
+  for (long r = grp; r < M; r += ng) {
     const long t = win_to_token(r, wm);
     const float mu = mean[t], rs = rstd[t];
-    float xh[MAXV], gy[MAXV];
+    float xh[NV][4], gy[NV][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const int c = lane + 64 * i;
+    for (int i = 0; i < NV; ++i) {
+      const int c = (sub + LPR * i) * 4;
+      float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), dv = xv;
       if (c < C) {
-        const float d = (float)dy[r * ldy + c];
-        xh[i] = (x[t * ldx + c] - mu) * rs;
-        gy[i] = d * g[i];
-        dg[i] += d * xh[i];
-        db[i] += d;
-      } else {
-        xh[i] = 0.f;
-        gy[i] = 0.f;
+        xv = *(const float4*)(x + t * ldx + c);
+        dv = load4<T>(dy + r * ldy + c);
       }
-      s1 += gy[i];
-      s2 += gy[i] * xh[i];
-    }
-    s1 = wave_sum(s1) / C;
-    s2 = wave_sum(s2) / C;
+      const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, da[4] = {dv.x, dv.y, dv.z, dv.w};
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const int c = lane + 64 * i;
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = c + j < C;
+        xh[i][j] = ok ? (xa[j] - mu) * rs : 0.f;
+        const float d = ok ? da[j] : 0.f;
+        gy[i][j] = d * g[i][j];
+        dg[i][j] += d * xh[i][j];
+        db[i][j] += d;
+        s1 += gy[i][j];
+        s2 += gy[i][j] * xh[i][j];
+      }
+    }
+    s1 = group_sum16(s1) / C;
+    s2 = group_sum16(s2) / C;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (sub + LPR * i) * 4;
       if (c < C) {
-        const float d = rs * (gy[i] - s1 - xh[i] * s2);
         float* o = dx + t * ld_dx + c;
-        *o = dx_acc ? *o + d : d;
+        float4 cur = dx_acc ? *(const float4*)o : make_float4(0.f, 0.f, 0.f, 0.f);
+        float d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = (c + j < C) ? rs * (gy[i][j] - s1 - xh[i][j] * s2) : 0.f;
+        cur.x += d[0]; cur.y += d[1]; cur.z += d[2]; cur.w += d[3];
+        *(float4*)o = cur;
       }
     }
   }
-  // block-level reduction of dgamma/dbeta partials (deterministic order)
-  __shared__ float red[2][4][256];
+  // block reduction of dgamma/dbeta partials: 16 row-groups share each column (fixed order)
+  __shared__ float red[2][16][260];
+  const int rg = threadIdx.x >> 4;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int c = lane + 64 * i;
-    red[0][w][c] = dg[i];
-    red[1][w][c] = db[i];
-  }
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = (sub + LPR * i) * 4 + j;
+      red[0][rg][c] = dg[i][j];
+      red[1][rg][c] = db[i][j];
+    }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    part[(long)blockIdx.x * 2 * C + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    part[(long)blockIdx.x * 2 * C + C + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  for (int c = threadIdx.x; c < 2 * C; c += 256) {
+    const int w = c < C ? 0 : 1, cc = c < C ? c : c - C;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[w][k][cc];
+    part[(long)blockIdx.x * 2 * C + c] = s;
   }
 }
 
-// 64 columns per block, 4 row-phases per column, fixed summation order (deterministic)
-__global__ __launch_bounds__(256) void ln_param_reduce(const float* __restrict__ part, int nb, int C, float* dgamma,
-                                                       float* dbeta, int acc) {
-  __shared__ float red[4][64];
+// 64 columns per block, 16 row-phases per column, fixed summation order (deterministic)
+__global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict__ part, int nb, int C, float* dgamma,
+                                                        float* dbeta, int acc) {
+  __shared__ float red[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   float s = 0.f;
   if (c < 2 * C)
-    for (int b = ty; b < nb; b += 4) s += part[(long)b * 2 * C + c];
+    for (int b = ty; b < nb; b += 16) s += part[(long)b * 2 * C + c];
   red[ty][tx] = s;
   __syncthreads();
   if (ty == 0 && c < 2 * C) {
-    s = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+    s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][tx];
     float* o = c < C ? dgamma + c : dbeta + (c - C);
     *o = acc ? *o + s : s;
   }
@@ -134,16 +191,17 @@ __global__ __launch_bounds__(256) void ln_param_reduce(const float* __restrict__
 
 }  // namespace
 
-constexpr int LN_BLOCKS = 512;
+constexpr int LN_BLOCKS = 1024;  // ws holds LN_BLOCKS * 2 * C floats (kair_hip.h)
 
 extern "C" int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype, long ldy, const float* gamma,
                                   const float* beta, float* mean, float* rstd, long M, int C, float eps, int win_H,
                                   int win_W, int win_ws, int win_shift, void* stream) {
   KAIR_CHECK_ARG(x && y && gamma && beta && mean && rstd, "layernorm_fwd: null pointer");
-  KAIR_CHECK_ARG(C > 0 && C <= 256 && ldx >= C && ldy >= C && M > 0, "layernorm_fwd: bad sizes");
+  KAIR_CHECK_ARG(C > 0 && C <= 256 && ldx >= C && ldy >= C && ldy <= 256 && M > 0, "layernorm_fwd: bad sizes");
+  KAIR_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)x % 16) == 0, "layernorm_fwd: strides must be multiples of 4");
   KAIR_CHECK_ARG(win_ws == 0 || (win_H % win_ws == 0 && win_W % win_ws == 0), "layernorm_fwd: window geometry");
   const WinMap wm{win_H, win_W, win_ws, win_shift};
-  long nb = (M + 3) / 4;
+  long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;
   if (nb > 8192) nb = 8192;
   hipStream_t s = (hipStream_t)stream;
   if (y_dtype == KAIR_BF16)
@@ -162,9 +220,10 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
                                   int win_H, int win_W, int win_ws, int win_shift, void* stream) {
   KAIR_CHECK_ARG(x && dy && gamma && mean && rstd && dx_acc && dgamma && dbeta && ws, "layernorm_bwd: null pointer");
   KAIR_CHECK_ARG(C > 0 && C <= 256 && M > 0, "layernorm_bwd: bad sizes");
+  KAIR_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && ld_dx % 4 == 0, "layernorm_bwd: strides must be multiples of 4");
   const WinMap wm{win_H, win_W, win_ws, win_shift};
   hipStream_t s = (hipStream_t)stream;
-  long nb = (M + 3) / 4;
+  long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;
   if (nb > LN_BLOCKS) nb = LN_BLOCKS;
   if (dy_dtype == KAIR_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const bf16*)dy, ldy, gamma,
@@ -173,7 +232,7 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
     hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const float*)dy, ldy, gamma,
                        mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm);
   KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 63) / 64), dim3(256), 0, s, ws, (int)nb, C, dgamma, dbeta,
+  hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, dgamma, dbeta,
                      dparam_accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;

@@ -448,13 +448,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const typename AT<BF>::T*
 }
 
 // stage 1: dB[h][q][k] = sum over groups of the per-group partials (coalesced, one thread per entry)
-__global__ void attn_dbias_sum_kernel(const float* __restrict__ dB_part, long ngroups, int nh, float* __restrict__ dB) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = nh * TOK * TOK;
-  if (t >= n) return;
-  float s = 0.f;
-  for (long g = 0; g < ngroups; ++g) s += dB_part[g * n + t];
-  dB[t] = s;
+__global__ __launch_bounds__(1024) void attn_dbias_sum_kernel(const float* __restrict__ dB_part, long ngroups, int nh,
+                                                              float* __restrict__ dB) {
+  const long n = (long)nh * TOK * TOK;
+  const long t = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s = split_sum16(dB_part, ngroups, n, t, t < n);
+  if (t < n && threadIdx.x < 64) dB[t] = s;
 }
 
 // stage 2: dtable[idx][h] (+)= sum_{(q,k): relidx(q,k)=idx} dB[h][q][k]
@@ -525,7 +524,7 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
                        ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, WPG, scale, H, W, shift);
   KAIR_CHECK_LAUNCH();
   float* dB = ws + ngroups * nh * TOK * TOK;
-  hipLaunchKernelGGL(attn_dbias_sum_kernel, dim3((nh * TOK * TOK + 255) / 256), dim3(256), 0, s, ws, ngroups, nh, dB);
+  hipLaunchKernelGGL(attn_dbias_sum_kernel, dim3((nh * TOK * TOK + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dB);
   KAIR_CHECK_LAUNCH();
   const int nt = (2 * WS - 1) * (2 * WS - 1) * nh;
   hipLaunchKernelGGL(attn_dtable_kernel, dim3((nt + 127) / 128), dim3(128), 0, s, dB, nh, dtable, dtable_accumulate);

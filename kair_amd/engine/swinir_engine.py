@@ -76,10 +76,9 @@ class _Lin:
         self.Wt = torch.empty(self.Kp, self.Np, device=dev, dtype=eng.tdt)
         self.bp = torch.empty(self.Np, device=dev)
 
-    def pack(self):
-        H.pack_weight(self.w.detach(), self.Wp, self.map)
-        H.pack_weight(self.w.detach(), self.Wt, self.mapT)
-        H.pack_weight(self.b.detach(), self.bp, self.mapb)
+    def pack_jobs(self):
+        w, b = self.w.detach(), self.b.detach()
+        return [(w, self.Wp, self.map), (w, self.Wt, self.mapT), (b, self.bp, self.mapb)]
 
 
 class _Conv:
@@ -97,11 +96,12 @@ class _Conv:
         self.Wd = torch.empty(Cip, 9 * Cop, device=dev, dtype=eng.tdt) if need_dgrad else None
         self.bp = torch.empty(Cop, device=dev)
 
-    def pack(self):
-        H.pack_weight(self.w.detach(), self.Wf, self.map)
+    def pack_jobs(self):
+        w, b = self.w.detach(), self.b.detach()
+        jobs = [(w, self.Wf, self.map), (b, self.bp, self.mapb)]
         if self.Wd is not None:
-            H.pack_weight(self.w.detach(), self.Wd, self.mapd)
-        H.pack_weight(self.b.detach(), self.bp, self.mapb)
+            jobs.append((w, self.Wd, self.mapd))
+        return jobs
 
 
 class _Blk:
@@ -179,6 +179,7 @@ class SwinIREngine:
         self.blocks = [b for blks, _ in self.rstb for b in blks]
         self.plans = {}
         self._packed_version = None
+        self._pack_table = None
 
     # ------------------------------------------------------------------------------------
     def convs(self):
@@ -194,11 +195,12 @@ class SwinIREngine:
         ver = None if force else tuple(p._version for p in net.parameters())
         if ver is not None and ver == self._packed_version:
             return
-        for c in self.convs():
-            c.pack()
-        for b in self.blocks:
-            for l in b.linears():
-                l.pack()
+        ptrs = tuple(p.data_ptr() for p in net.parameters())
+        if self._pack_table is None or self._pack_table[0] != ptrs:   # params re-homed (e.g. flattened)
+            jobs = [j for c in self.convs() for j in c.pack_jobs()]
+            jobs += [j for b in self.blocks for l in b.linears() for j in l.pack_jobs()]
+            self._pack_table = (ptrs, H.PackTable(jobs))
+        self._pack_table[1].run()
         self._packed_version = ver
 
     def plan(self, B, Hh, Ww):

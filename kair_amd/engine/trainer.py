@@ -18,6 +18,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _hip as H
+from .comm import allreduce_mean_, broadcast_params_
 
 
 def flatten_params(module, device):
@@ -41,6 +42,7 @@ class FusedTrainer:
         self.device = next(netG.parameters()).device
         self.engine = netG.engine()
         self.flat_p, self.params = flatten_params(netG, self.device)
+        broadcast_params_(self.flat_p, 0, process_group)   # identical start on every rank (DDP init)
         self.flat_g = torch.zeros_like(self.flat_p)
         self.m = torch.zeros_like(self.flat_p)
         self.v = torch.zeros_like(self.flat_p)
@@ -71,15 +73,10 @@ class FusedTrainer:
 
     # ------------------------------------------------------------------------------------
     def _allreduce(self):
-        if self.world == 1:
-            return
-        n = self.flat_g.numel()
-        for off in range(0, n, self.bucket):   # reverse-layer order is what the reducer uses;
-            seg = self.flat_g[off:off + self.bucket]   # here all grads are ready at once
-            dist.all_reduce(seg, group=self.pg)
-        self.flat_g.mul_(1.0 / self.world)
+        if self.world > 1:
+            allreduce_mean_(self.flat_g, self.bucket, self.pg, self.world)
 
-    def _body(self, L, Hh):
+    def _fwd_bwd(self, L, Hh):
         eng = self.engine
         drop = None
         if any(b.dp > 0 for b in eng.blocks) and self.net.training:
@@ -87,10 +84,16 @@ class FusedTrainer:
             drop = drop_path_scales(eng, L.shape[0], L.device)
         eng._packed_version = None           # weights change every step: always repack
         eng.forward(L, drop)
-        loss = eng.backward_from_loss(Hh, self.grads, self.loss_weight)
-        self._allreduce()
+        return eng.backward_from_loss(Hh, self.grads, self.loss_weight)
+
+    def _update(self):
         H.adam_ema(self.flat_p, self.flat_g, self.m, self.v, self.flat_e, self.flat_p.numel(), self.scal,
                    self.betas[0], self.betas[1], self.eps, self.wd, self.E_decay if self.flat_e is not None else 0.0)
+
+    def _body(self, L, Hh):
+        loss = self._fwd_bwd(L, Hh)
+        self._allreduce()
+        self._update()
         return loss
 
     def _set_scalars(self):
@@ -113,14 +116,27 @@ class FusedTrainer:
         self.static[0].copy_(L)
         self.static[1].copy_(Hh)
         if self.graph is None and self.warm >= 2:
+            # world > 1: the RCCL all-reduce stays outside the captured graphs (fwd+bwd graph,
+            # eager bucketed all-reduce, update graph); single GPU: one graph for the whole step
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):        # records only; the replay below executes this step
-                self.loss_out = self._body(*self.static)
+                if self.world > 1:
+                    self.loss_out = self._fwd_bwd(*self.static)
+                else:
+                    self.loss_out = self._body(*self.static)
+            g2 = None
+            if self.world > 1:
+                g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g2):
+                    self._update()
             torch.cuda.synchronize()
-            self.graph = g
+            self.graph = (g, g2)
         if self.graph is not None:
-            self.graph.replay()
+            self.graph[0].replay()
+            if self.graph[1] is not None:
+                self._allreduce()
+                self.graph[1].replay()
             out = self.loss_out
         else:
             self.warm += 1

@@ -1,0 +1,100 @@
+"""define_G — the drop-in boundary (mirror of /root/reference/models/select_network.py:16-274).
+
+`opt['netG']['net_type']` selects the network; constructor kwargs are taken from opt['netG'] under
+the reference's key names, and init_weights() runs when opt['is_train'] (select_network.py:268-272).
+Networks on the MI355X path: swinir, dncnn, fdncnn, rrdb, rrdbnet, usrnet.  Everything else the
+reference's define_G knows (ffdnet, srmd, dpsr, msrresnet*, imdn, drunet, vrt, rvrt, ...) is out of
+scope for this build and raises NotImplementedError naming the type.
+"""
+import functools
+
+from torch.nn import init
+
+_ON_PATH = ("swinir", "dncnn", "fdncnn", "rrdb", "rrdbnet", "usrnet")
+
+
+def define_G(opt):
+    o = opt["netG"]
+    t = o["net_type"]
+    if t == "swinir":
+        from .network_swinir import SwinIR
+        net = SwinIR(upscale=o["upscale"], in_chans=o["in_chans"], img_size=o["img_size"], window_size=o["window_size"],
+                     img_range=o["img_range"], depths=o["depths"], embed_dim=o["embed_dim"], num_heads=o["num_heads"],
+                     mlp_ratio=o["mlp_ratio"], upsampler=o["upsampler"], resi_connection=o["resi_connection"],
+                     **_engine_kwargs(o))
+    elif t in ("dncnn", "fdncnn"):
+        from .network_dncnn import DnCNN, FDnCNN
+        cls = DnCNN if t == "dncnn" else FDnCNN
+        net = cls(in_nc=o["in_nc"], out_nc=o["out_nc"], nc=o["nc"], nb=o["nb"], act_mode=o["act_mode"],
+                  **_engine_kwargs(o))
+    elif t == "rrdb":
+        from .network_rrdb import RRDB
+        net = RRDB(in_nc=o["in_nc"], out_nc=o["out_nc"], nc=o["nc"], nb=o["nb"], gc=o["gc"], upscale=o["scale"],
+                   act_mode=o["act_mode"], upsample_mode=o["upsample_mode"], **_engine_kwargs(o))
+    elif t == "rrdbnet":
+        from .network_rrdbnet import RRDBNet
+        net = RRDBNet(in_nc=o["in_nc"], out_nc=o["out_nc"], nf=o["nf"], nb=o["nb"], gc=o["gc"], sf=o["scale"],
+                      **_engine_kwargs(o))
+    elif t == "usrnet":
+        from .network_usrnet import USRNet
+        net = USRNet(n_iter=o["n_iter"], h_nc=o["h_nc"], in_nc=o["in_nc"], out_nc=o["out_nc"], nc=o["nc"], nb=o["nb"],
+                     act_mode=o["act_mode"], downsample_mode=o["downsample_mode"], upsample_mode=o["upsample_mode"],
+                     **_engine_kwargs(o))
+    else:
+        raise NotImplementedError("netG [{:s}] is not on the kair_amd MI355X path (supported: {})".format(
+            t, ", ".join(_ON_PATH)))
+    if opt.get("is_train"):
+        init_weights(net, init_type=o.get("init_type", "default") or "default",
+                     init_bn_type=o.get("init_bn_type", "uniform") or "uniform", gain=o.get("init_gain", 1) or 1)
+    return net
+
+
+def _engine_kwargs(o):
+    """Build-only option: netG.compute_dtype ('bf16' default, 'fp32' parity mode)."""
+    return {"compute_dtype": o["compute_dtype"]} if o.get("compute_dtype") else {}
+
+
+def init_weights(net, init_type="xavier_uniform", init_bn_type="uniform", gain=1):
+    """select_network.py:370-440 (same initialisers, same Conv/Linear/BatchNorm2d matching by class name)."""
+
+    def init_fn(m, init_type, init_bn_type, gain):
+        name = m.__class__.__name__
+        if name.find("Conv") != -1 or name.find("Linear") != -1:
+            w = m.weight.data
+            if init_type == "normal":
+                init.normal_(w, 0, 0.1)
+                w.clamp_(-1, 1).mul_(gain)
+            elif init_type == "uniform":
+                init.uniform_(w, -0.2, 0.2)
+                w.mul_(gain)
+            elif init_type == "xavier_normal":
+                init.xavier_normal_(w, gain=gain)
+                w.clamp_(-1, 1)
+            elif init_type == "xavier_uniform":
+                init.xavier_uniform_(w, gain=gain)
+            elif init_type == "kaiming_normal":
+                init.kaiming_normal_(w, a=0, mode="fan_in", nonlinearity="relu")
+                w.clamp_(-1, 1).mul_(gain)
+            elif init_type == "kaiming_uniform":
+                init.kaiming_uniform_(w, a=0, mode="fan_in", nonlinearity="relu")
+                w.mul_(gain)
+            elif init_type == "orthogonal":
+                init.orthogonal_(w, gain=gain)
+            else:
+                raise NotImplementedError("Initialization method [{:s}] is not implemented".format(init_type))
+            if getattr(m, "bias", None) is not None:
+                m.bias.data.zero_()
+        elif name.find("BatchNorm2d") != -1:
+            if init_bn_type == "uniform":
+                if m.affine:
+                    init.uniform_(m.weight.data, 0.1, 1.0)
+                    init.constant_(m.bias.data, 0.0)
+            elif init_bn_type == "constant":
+                if m.affine:
+                    init.constant_(m.weight.data, 1.0)
+                    init.constant_(m.bias.data, 0.0)
+            else:
+                raise NotImplementedError("Initialization method [{:s}] is not implemented".format(init_bn_type))
+
+    if init_type not in ("default", "none"):
+        net.apply(functools.partial(init_fn, init_type=init_type, init_bn_type=init_bn_type, gain=gain))

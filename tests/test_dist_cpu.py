@@ -1,0 +1,94 @@
+"""Data-parallel exchange on CPU (gloo, world_size 2): the same code the trainer runs over RCCL.
+
+* bucket_bounds tiles the flat buffer exactly, last layers first;
+* allreduce_mean_ of the flat gradient buffer == the mean over ranks for any bucket size;
+* SURVEY §8e equivalence: two ranks with 2-patch shards, grads flattened + all-reduced through the
+  trainer's exchange == the 4-patch single-process gradient (oracle network, L1 mean).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from kair_amd.engine.comm import allreduce_mean_, bucket_bounds, broadcast_params_
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bucket_bounds_tile_reverse():
+    for n, b in [(10, 3), (9, 3), (1, 5), (1000, 1000), (1001, 1000)]:
+        bb = bucket_bounds(n, b)
+        assert bb[0][1] == n and bb[-1][0] == 0
+        assert all(hi - lo <= b for lo, hi in bb)
+        assert all(bb[i][0] == bb[i + 1][1] for i in range(len(bb) - 1))
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = {}
+        # (1) plain mean for several bucket sizes
+        for b in (1, 7, 64, 10 ** 6):
+            g = torch.arange(100, dtype=torch.float32) * (rank + 1)
+            allreduce_mean_(g, b)
+            res[f"mean{b}"] = g.clone()
+        # (2) broadcast makes rank 1 start from rank 0's params
+        p = torch.full((5,), float(rank + 3))
+        broadcast_params_(p)
+        res["bcast"] = p.clone()
+        # (3) DP equivalence on the oracle SwinIR
+        from oracle import swinir as osw
+        torch.manual_seed(0)
+        net = osw.SwinIR(2, 3, 16, 8, 1.0, [2], 60, [6], 2, "pixelshuffledirect")
+        g = torch.Generator().manual_seed(5)
+        L = torch.rand(4, 3, 16, 16, generator=g)
+        Hh = torch.rand(4, 3, 32, 32, generator=g)
+        sl = slice(2 * rank, 2 * rank + 2)
+        loss = torch.nn.functional.l1_loss(net(L[sl]), Hh[sl])
+        loss.backward()
+        flat = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
+        allreduce_mean_(flat, 4096)
+        res["dp_grad"] = flat
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_allreduce_and_dp_equivalence():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    want = torch.arange(100, dtype=torch.float32) * 1.5
+    for r in range(world):
+        for b in (1, 7, 64, 10 ** 6):
+            torch.testing.assert_close(out[r][f"mean{b}"], want)
+        torch.testing.assert_close(out[r]["bcast"], torch.full((5,), 3.0))
+    torch.testing.assert_close(out[0]["dp_grad"], out[1]["dp_grad"])
+    # single-process full-batch reference
+    from oracle import swinir as osw
+    torch.manual_seed(0)
+    net = osw.SwinIR(2, 3, 16, 8, 1.0, [2], 60, [6], 2, "pixelshuffledirect")
+    g = torch.Generator().manual_seed(5)
+    L = torch.rand(4, 3, 16, 16, generator=g)
+    Hh = torch.rand(4, 3, 32, 32, generator=g)
+    torch.nn.functional.l1_loss(net(L), Hh).backward()
+    full = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
+    torch.testing.assert_close(out[0]["dp_grad"], full, rtol=1e-4, atol=1e-6)
