@@ -61,6 +61,23 @@ KAIR_DEV float gelu_erf_grad(float x) {
 struct WinMap {
   int H, W, ws, shift;  // ws == 0 => identity map
 };
+// 32-bit form (row counts < 2^31) for per-tile address setup in the GEMM mainloops
+KAIR_DEV int win_to_token32(int m, const WinMap& w) {
+  if (w.ws == 0) return m;
+  const int ws2 = w.ws * w.ws;
+  const int nWw = w.W / w.ws, nW = (w.H / w.ws) * nWw;
+  const int win = m / ws2;
+  const int t = m - win * ws2;
+  const int b = win / nW;
+  const int wi = win - b * nW;
+  const int wy = wi / nWw, wx = wi - wy * nWw;
+  const int ty = t / w.ws;
+  int y = wy * w.ws + ty + w.shift;
+  int x = wx * w.ws + (t - ty * w.ws) + w.shift;
+  if (y >= w.H) y -= w.H;
+  if (x >= w.W) x -= w.W;
+  return (b * w.H + y) * w.W + x;
+}
 KAIR_DEV long win_to_token(long m, const WinMap& w) {
   if (w.ws == 0) return m;
   const int ws2 = w.ws * w.ws;

@@ -17,6 +17,7 @@
 // finishes 8 consecutive columns of one row with 16-byte loads/stores.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -488,6 +489,236 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_kernel(Op A, Op B, Epi E, int K
 }
 
 // ------------------------------------------------------------------------------------------
+// 4-column register epilogue (ring kernel): lane holds columns [n, n+4) of one output row.
+// ------------------------------------------------------------------------------------------
+enum { EM_ROWS = 0, EM_QKV = 1 };
+
+KAIR_DEV void ld4_any(const void* p, int dt, long off, float (&g)[4]) {
+  if (dt == KAIR_BF16) {
+    const bf16x4 q = *(const bf16x4*)((const bf16*)p + off);
+    g[0] = (float)q[0]; g[1] = (float)q[1]; g[2] = (float)q[2]; g[3] = (float)q[3];
+  } else {
+    const float4 a = *(const float4*)((const float*)p + off);
+    g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w;
+  }
+}
+KAIR_DEV void st4_any(void* p, int dt, long off, const float (&v)[4]) {
+  if (dt == KAIR_BF16) {
+    bf16x4 q = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    *(bf16x4*)((bf16*)p + off) = q;
+  } else {
+    *(float4*)((float*)p + off) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+template <int EM>
+KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4]) {
+  if (e.bias) {
+    const float4 b = *(const float4*)(e.bias + n);
+    v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+  }
+  if constexpr (EM == EM_QKV) {
+    const int pw = e.nh * e.hdp;
+    const int part = n / pw, rr = n - part * pw;
+    const int h = rr / e.hdp, d = rr - h * e.hdp;
+    const long win = m / e.tok;
+    const int t = (int)(m - win * e.tok);
+    st4_any(e.out, e.odt, (long)part * e.M * pw + ((win * e.nh + h) * e.tok + t) * e.hdp + d, v);
+  } else {
+    float pre[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pre[j] = v[j];
+      if (e.act == KAIR_ACT_GELU) v[j] = gelu_erf(v[j]);
+      else if (e.act == KAIR_ACT_LEAKY) v[j] = v[j] > 0.f ? v[j] : v[j] * e.slope;
+      else if (e.act == KAIR_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
+    }
+    if (e.gate) {
+      float g[4];
+      ld4_any(e.gate, e.gdt, row * e.ldg + n, g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (e.gkind == 1) v[j] *= gelu_erf_grad(g[j]);
+        else if (e.gkind == 2) v[j] *= (g[j] > 0.f ? 1.f : e.slope);
+        else v[j] *= (g[j] > 0.f ? 1.f : 0.f);
+      }
+    }
+    if (e.resid) {
+      const float4 r = *(const float4*)(e.resid + row * e.ldr + n);
+      v[0] = r.x + rs * v[0]; v[1] = r.y + rs * v[1]; v[2] = r.z + rs * v[2]; v[3] = r.w + rs * v[3];
+    }
+    st4_any(e.out, e.odt, row * e.ldo + n, v);
+    if (e.pre) st4_any(e.pre, e.pdt, row * e.ldp + n, pre);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// NT ring kernel (bf16 A rows / head-blocked q,k,v; K % 64 == 0, K <= 576): one 512-thread CTA
+// per CU, persistent over the M-tiles of ONE N-tile.
+//  * the CTA's BN x K slice of the packed weights is loaded into LDS once and stays resident;
+//  * A streams through an NS-deep ring of 128x64 bf16 chunks filled by LDS-DMA
+//    (global_load_lds_dwordx4, 2 wave-instructions per wave per chunk, source-address XOR swizzle
+//    so the lane-linear image reads conflict-light), waited with a counted vmcnt and a raw
+//    s_barrier, so NS-2 chunks stay in flight across barriers and across tile boundaries;
+//  * MFMA operands are swapped (D = B . A^T) so each lane owns 4 consecutive output columns of one
+//    row: the fused epilogue runs from the accumulators with 8/16-byte vector accesses.
+// ------------------------------------------------------------------------------------------
+constexpr int RING_BM = 128, RING_BK = 64;
+constexpr int RING_B_ELEMS = 38400;   // max BN * (K + 8) over the (BN, K) pairs dispatched below
+
+KAIR_DEV void ring_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BN, int NS, int AM, int EM>
+__global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
+  constexpr int BM = RING_BM, BK = RING_BK;
+  constexpr int TN = BN / 2, RM = 2, RN = TN / 16;
+  constexpr int STAGE_BYTES = BM * BK * 2;   // 16 KiB
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE_BYTES + RING_B_ELEMS * 2];
+  bf16* sB = (bf16*)(smem + NS * STAGE_BYTES);
+  const int LDB = K + 8;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;   // 4 (M) x 2 (N) waves
+  const int fr = lane & 15, fq = lane >> 4;
+  const int cta = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = cta % tilesN;
+  const int mstride = gridDim.x / tilesN;
+  const int mt0 = cta / tilesN;
+  if (mt0 >= tilesM) return;
+  const int ntile_m = (tilesM - mt0 + mstride - 1) / mstride;
+  const int nk = K / BK;
+  const int total = ntile_m * nk;
+  const int n0 = nt * BN;
+
+  // resident B slice [BN][K] (rows >= N are zero)
+  {
+    const bf16* bp = (const bf16*)B.ptr;
+    const int cpr = K / 8;
+    for (int c = tid; c < BN * cpr; c += 512) {
+      const int r = c / cpr, k8 = (c - r * cpr) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n0 + r < B.M) v = *(const uint4*)(bp + (long)(n0 + r) * B.ld + k8);
+      *(uint4*)(sB + r * LDB + k8) = v;
+    }
+  }
+
+  // loader state: this lane's two rows of the chunk being LOADED
+  const int q = lane & 7;
+  int ld_tile = -1;
+  long rbase[2];
+  int rsw[2];   // row & 7 (swizzle key)
+  auto load_rows = [&](int i) {
+    const int mt = mt0 + i * mstride;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int r = (wave * 2 + ii) * 8 + (lane >> 3);
+      int m = mt * BM + r;
+      if (m >= (int)A.M) m = 0;   // rows past M load row 0; the epilogue skips them
+      rsw[ii] = r & 7;
+      if constexpr (AM == AM_ROWS) {
+        rbase[ii] = (long)win_to_token32(m, A.win) * A.ld;
+      } else {
+        const int win = m / A.tok, t = m - win * A.tok;
+        rbase[ii] = ((long)win * A.nh * A.tok + t) * A.hdp;
+      }
+    }
+  };
+  auto issue = [&](int j) {
+    const int i = j / nk, kc = j - (j / nk) * nk;
+    if (i != ld_tile) { load_rows(i); ld_tile = i; }
+    char* st = smem + (j % NS) * STAGE_BYTES;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int k = kc * BK + ((q ^ rsw[ii]) << 3);
+      long off;
+      if constexpr (AM == AM_ROWS) {
+        off = rbase[ii] + k;
+      } else {
+        const int pw = A.nh * A.hdp;
+        const int part = k / pw, rr = k - part * pw;
+        const int h = rr / A.hdp, d = rr - h * A.hdp;
+        off = (long)part * A.M * pw + rbase[ii] + (long)h * A.tok * A.hdp + d;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)((const bf16*)A.ptr + off),
+                                       (__attribute__((address_space(3))) void*)(st + (wave * 2 + ii) * 1024), 16, 0, 0);
+    }
+  };
+
+  // prologue: B slice visible to every wave, then NS-1 chunks in flight
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < total) issue(j);
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int j = 0; j < total; ++j) {
+    // chunk j landed for this wave; at most min(NS-2, total-1-j) younger chunks may remain in flight
+    const int ahead = (total - 1 - j) < (NS - 2) ? (total - 1 - j) : (NS - 2);
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ring_barrier();   // every wave's part of chunk j is in LDS; stage (j-1)%NS is free
+    const int kc = j % nk;
+    const bool tile_end = kc == nk - 1;
+    if (!tile_end && j + NS - 1 < total) issue(j + NS - 1);
+    const char* st = smem + (j % NS) * STAGE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int r = wm * 32 + i * 16 + fr;
+        af[i] = *(const bf16x8*)(st + r * 128 + (((ks * 4 + fq) ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn)
+        bfr[jn] = *(const bf16x8*)(sB + (wn * TN + jn * 16 + fr) * LDB + kc * BK + ks * 32 + fq * 8);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn)
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
+    }
+    if (tile_end) {
+      const int mt = mt0 + (j / nk) * mstride;
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int m = mt * BM + wm * 32 + i * 16 + fr;
+        if (m < (int)E.M) {
+          long row = m;
+          float rs = 1.f;
+          if constexpr (EM == EM_ROWS) {
+            row = win_to_token32(m, E.win);
+            if (E.rowscale) rs = E.rowscale[(int)row / E.rps];
+          }
+#pragma unroll
+          for (int jn = 0; jn < RN; ++jn) {
+            const int n = n0 + wn * TN + jn * 16 + fq * 4;
+            if (n < E.N) {
+              float v[4] = {acc[i][jn][0], acc[i][jn][1], acc[i][jn][2], acc[i][jn][3]};
+              epi4<EM>(E, m, row, rs, n, v);
+            }
+          }
+        }
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (j + NS - 1 < total) issue(j + NS - 1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // TN kernel (weight gradient): P[s][n][k] = sum_{m in split s} A[m][n] * B[m][k]
 // LDS holds both operands m-major ([BMr m][BN], [BMr m][BKo]) as loaded; bf16 fragments (8
 // consecutive m of one column) come from two ds_read_b64_tr_b16 transposed reads.
@@ -652,8 +883,71 @@ int nt_tiles(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipSt
   return launch_nt<CT, TA, AM, 128, 128, 2, 2>(A, B, E, M, N, K, s);
 }
 
+static int g_num_cus = 0;
+static int g_ring_mode = -1;
+
+static void init_num_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    n = 256;
+  g_num_cus = n > 0 ? n : 256;
+}
+
+// 4-column register epilogue: ROWS / QKV outputs whose vectors are 4-aligned
+static bool epi4_ok(const Epi& e, int N) {
+  if (N % 4 != 0 || N <= 64) return false;
+  if (e.omode == KAIR_OUT_QKVBLK) return e.hdp % 4 == 0;
+  if (e.omode != KAIR_OUT_ROWS) return false;
+  return e.ldo % 4 == 0 && (!e.pre || e.ldp % 4 == 0) && (!e.resid || e.ldr % 4 == 0) && (!e.gate || e.ldg % 4 == 0);
+}
+
+template <int BN, int NS, int AM>
+int launch_ring(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
+  const int tilesN = (N + BN - 1) / BN;
+  const int tilesM = (int)((M + RING_BM - 1) / RING_BM);
+  int grid = (g_num_cus / tilesN) * tilesN;
+  if (grid < tilesN) grid = tilesN;
+  const int need = tilesM * tilesN;
+  if (grid > need) grid = need;
+  if (E.omode == KAIR_OUT_QKVBLK)
+    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_QKV>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesN, tilesM);
+  else
+    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesN, tilesM);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+// ring kernel: bf16 A (rows, optionally window-mapped, or head-blocked q/k/v) with no row scale
+static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, int N, int K) {
+  if (K % RING_BK != 0 || K > 576 || M >= (1L << 30)) return false;
+  if (amode != KAIR_LD_ROWS && amode != KAIR_LD_QKVBLK) return false;
+  if (A.rowscale || A.ones_col >= 0) return false;
+  if (amode == KAIR_LD_ROWS && A.ld % 8 != 0) return false;
+  if (amode == KAIR_LD_QKVBLK && (A.hdp % 8 != 0)) return false;
+  if (B.ld % 8 != 0 || B.ones_col >= 0) return false;
+  return epi4_ok(e, N);
+}
+
+template <int AM>
+int ring_bn(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
+  if (K <= 192) return launch_ring<192, 5, AM>(A, B, E, M, N, K, s);
+  if (K <= 384) return launch_ring<96, 5, AM>(A, B, E, M, N, K, s);
+  return launch_ring<64, 5, AM>(A, B, E, M, N, K, s);
+}
+
 template <typename CT, typename TA>
 int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
+  if constexpr (sizeof(CT) == 2 && sizeof(TA) == 2) {
+    if (g_ring_mode < 0) {   // KAIR_GEMM_RING=0 disables the LDS-DMA ring kernel (A/B timing only)
+      const char* v = getenv("KAIR_GEMM_RING");
+      g_ring_mode = (v && v[0] == '0') ? 0 : 1;
+    }
+    if (g_ring_mode && ring_ok(mode, A, B, E, M, N, K)) {
+      if (g_num_cus == 0) init_num_cus();
+      if (mode == KAIR_LD_ROWS) return ring_bn<AM_ROWS>(A, B, E, M, N, K, s);
+      return ring_bn<AM_QKV>(A, B, E, M, N, K, s);
+    }
+  }
   if (mode == KAIR_LD_ROWS) return nt_tiles<CT, TA, AM_ROWS>(A, B, E, M, N, K, s);
   if (mode == KAIR_LD_IM2COL3) return nt_tiles<CT, TA, AM_IM2COL>(A, B, E, M, N, K, s);
   if constexpr (sizeof(TA) == sizeof(CT)) return nt_tiles<CT, TA, AM_QKV>(A, B, E, M, N, K, s);

@@ -301,3 +301,59 @@ def test_l1_and_adam():
     torch.cuda.synchronize()
     assert rel_err(pd, pt.detach()) < 1e-6
     assert rel_err(ed, ema_ref) < 1e-6
+
+
+@pytest.mark.parametrize("a_dtype", [H.F32, H.BF16])
+def test_gemm_stream_epilogues(a_dtype):
+    """bf16 compute, N > 64: the streaming kernel — fp32/bf16 A, gelu' gate, DropPath rowscale +
+    residual (rows_per_scale), and the head-blocked q/k/v output layout."""
+    B, Hh, Ww, nh = 2, 16, 16, 6
+    M, C, Np = B * Hh * Ww, 192, 576
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(M, C, generator=g)
+    w = torch.randn(384, C, generator=g) * 0.1
+    gate = torch.randn(M, 384, generator=g)
+    res = torch.randn(M, 384, generator=g)
+    scale = torch.tensor([0.5, 2.0])
+    out = torch.empty(M, 384, device=dev)
+    A = x.to(dev, DT[a_dtype])
+    H.gemm_nt(H.rows(A), H.rows(w.to(dev, torch.bfloat16)),
+              H.epilogue(out, resid=res.to(dev), rowscale=scale.to(dev), rows_per_scale=Hh * Ww,
+                         gate=gate.to(dev, torch.bfloat16), gate_kind=1), M, 384, C, H.BF16)
+    xa = A.float().cpu().double()
+    y = xa @ w.to(torch.bfloat16).double().T
+    gb = gate.to(torch.bfloat16).double()
+    cdf = 0.5 * (1 + torch.erf(gb / 2 ** 0.5))
+    y = y * (cdf + gb * torch.exp(-0.5 * gb * gb) / (2 * torch.pi) ** 0.5)
+    s = scale.double().repeat_interleave(Hh * Ww)[:, None]
+    ref = res.double() + s * y
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-2
+    # q/k/v head-blocked output [3][M/64][nh][64][32] from a window-mapped A
+    wq = torch.randn(Np, C, generator=g) * 0.1
+    bq = torch.randn(Np, generator=g)
+    qkv = torch.empty(3 * M * nh * 32, device=dev, dtype=torch.bfloat16)
+    win = (Hh, Ww, 8, 4)
+    H.gemm_nt(H.rows(A, win=win), H.rows(wq.to(dev, torch.bfloat16)),
+              H.epilogue(qkv, mode=H.OUT_QKVBLK, ldo=0, bias=bq.to(dev), qkv=(nh, 32, 64)), M, Np, C, H.BF16)
+    perm = win_perm(B, Hh, Ww, 8, 4)
+    yq = xa[perm] @ wq.to(torch.bfloat16).double().T + bq.double()      # [M(window order), 576]
+    refq = yq.view(M // 64, 64, 3, nh, 32).permute(2, 0, 3, 1, 4).reshape(-1)
+    torch.cuda.synchronize()
+    assert rel_err(qkv.float(), refq) < 1e-2
+
+
+def test_gemm_qkvblk_A_operand():
+    """A read from the head-blocked q/k/v layout (the q/k/v input-gradient GEMM), K = 576."""
+    nWin, nh, tok, hdp = 12, 6, 64, 32
+    M, N, K = nWin * tok, 192, 3 * nh * hdp
+    g = torch.Generator().manual_seed(13)
+    blk = torch.randn(3, nWin, nh, tok, hdp, generator=g)
+    w = torch.randn(N, K, generator=g) * 0.05
+    out = torch.empty(M, N, device=dev)
+    H.gemm_nt(H.qkvblk(blk.to(dev, torch.bfloat16).reshape(-1), nh), H.rows(w.to(dev, torch.bfloat16)), H.epilogue(out),
+              M, N, K, H.BF16)
+    a = blk.to(torch.bfloat16).double().permute(1, 3, 0, 2, 4).reshape(M, K)   # row m=(win,t), col=(part,h,d)
+    ref = a @ w.to(torch.bfloat16).double().T
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-2
