@@ -57,7 +57,7 @@ def time_dominant_kernel(engine, reps=30):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     flops = 2.0 * M * l.N * l.K
-    return {"kernel": "gemm_nt_kernel<bf16,128,128,2,2> (block QKV projection, network_swinir.py:121)",
+    return {"kernel": "gemm_nt_ring<192,5,0,1> (block QKV projection, network_swinir.py:121; rocprof name _ZN..gemm_nt_ringILi192ELi5ELi0ELi1E..)",
             "ms": ms, "flops": flops, "M": M, "N": l.N, "K": l.K}
 
 

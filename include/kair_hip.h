@@ -138,13 +138,26 @@ int kair_colsum(const kair_operand* G, long M, int Np, const kair_wmap* map, flo
 int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype, long ldy, const float* gamma,
                        const float* beta, float* mean, float* rstd, long M, int C, float eps,
                        int win_H, int win_W, int win_ws, int win_shift, void* stream);
+/* A row-scaled, cast copy of an fp32 token-row matrix (the next GEMM's A operand):
+ * out[token_to_win(t)][c] = rowscale[t / rows_per_scale] * src[t][c]  (window order when win_ws > 0). */
+typedef struct {
+  void* out;
+  int dtype;
+  long ld;
+  const float* rowscale; /* NULL => 1 */
+  int rows_per_scale;
+  int win_H, win_W, win_ws, win_shift;
+} kair_copy_desc;
+int kair_row_copy(const float* src, long ld_src, long M, int C, const kair_copy_desc* copy, void* stream);
+
 /* dx_acc[t] (+)= LN-backward(dy) for token rows t; dgamma/dbeta (+)= column sums.
- * dy (dtype) is addressed like y in the forward.  ws: 2 * 1024 * C floats. */
+ * dy (dtype) is addressed like y in the forward.  ws: 2 * 1024 * C floats.
+ * copy (optional): also write the finished dx rows as a kair_copy_desc. */
 int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int dy_dtype, long ldy,
                        const float* gamma, const float* mean, const float* rstd, float* dx_acc,
                        long ld_dx, int dx_accumulate, float* dgamma, float* dbeta, int dparam_accumulate,
                        float* ws, long M, int C, int win_H, int win_W, int win_ws, int win_shift,
-                       void* stream);
+                       const kair_copy_desc* copy, void* stream);
 
 /* Fused Swin window attention (network_swinir.py:114-145) for ws=8 (64 tokens), head_dim <= 32:
  *   O = softmax(q*scale @ k^T + table[relidx] + shift_mask) @ v   per (window, head).

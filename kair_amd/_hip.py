@@ -27,6 +27,23 @@ class Operand(ctypes.Structure):
                 ("rowscale", c_vp), ("rows_per_scale", c_int), ("ones_col", c_int)]
 
 
+class CopyDesc(ctypes.Structure):
+    _fields_ = [("out", c_vp), ("dtype", c_int), ("ld", c_long), ("rowscale", c_vp), ("rows_per_scale", c_int),
+                ("win_H", c_int), ("win_W", c_int), ("win_ws", c_int), ("win_shift", c_int)]
+
+
+def copy_desc(out, ld=None, rowscale=None, rows_per_scale=1, win=None):
+    """Row-scaled cast copy target (GEMM A operand); win puts the rows in Swin window order."""
+    d = CopyDesc()
+    d._keep = (out, rowscale)
+    d.out, d.dtype = ptr(out), dtype_code(out)
+    d.ld = ld if ld is not None else out.shape[-1]
+    d.rowscale, d.rows_per_scale = ptr(rowscale), rows_per_scale
+    if win:
+        d.win_H, d.win_W, d.win_ws, d.win_shift = win
+    return d
+
+
 class Epilogue(ctypes.Structure):
     _fields_ = [("out", c_vp), ("out_dtype", c_int), ("out_mode", c_int), ("ldo", c_long),
                 ("win_H", c_int), ("win_W", c_int), ("win_ws", c_int), ("win_shift", c_int),
@@ -64,7 +81,8 @@ _SIGS = {
     "kair_layernorm_fwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_float, c_int,
                            c_int, c_int, c_int, c_vp],
     "kair_layernorm_bwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_vp, c_vp, c_int,
-                           c_vp, c_long, c_int, c_int, c_int, c_int, c_int, c_vp],
+                           c_vp, c_long, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(CopyDesc), c_vp],
+    "kair_row_copy": [c_vp, c_long, c_long, c_int, ctypes.POINTER(CopyDesc), c_vp],
     "kair_window_attn_fwd": [c_vp, c_int, c_vp, c_vp, c_long, c_vp, c_long, c_int, c_int, c_float, c_int, c_int, c_int,
                              c_vp],
     "kair_window_attn_bwd_ws": [c_long, c_int],
@@ -272,10 +290,14 @@ def layernorm_fwd(x, ldx, y, ldy, gamma, beta, mean, rstd, M, C, eps=1e-5, win=(
 
 
 def layernorm_bwd(x, ldx, dy, ldy, gamma, mean, rstd, dx, ld_dx, dx_acc, dgamma, dbeta, dparam_acc, ws, M, C,
-                  win=(0, 0, 0, 0)):
+                  win=(0, 0, 0, 0), copy=None):
     check(lib().kair_layernorm_bwd(ptr(x), ldx, ptr(dy), dtype_code(dy), ldy, ptr(gamma), ptr(mean), ptr(rstd), ptr(dx),
                                    ld_dx, int(dx_acc), ptr(dgamma), ptr(dbeta), int(dparam_acc), ptr(ws), M, C, *win,
-                                   stream_ptr()), "layernorm_bwd")
+                                   ctypes.byref(copy) if copy is not None else None, stream_ptr()), "layernorm_bwd")
+
+
+def row_copy(src, ld_src, M, C, copy):
+    check(lib().kair_row_copy(ptr(src), ld_src, M, C, ctypes.byref(copy), stream_ptr()), "row_copy")
 
 
 def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift):

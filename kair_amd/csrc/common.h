@@ -78,6 +78,19 @@ KAIR_DEV int win_to_token32(int m, const WinMap& w) {
   if (x >= w.W) x -= w.W;
   return (b * w.H + y) * w.W + x;
 }
+// inverse of win_to_token: window-order row of token t
+KAIR_DEV long token_to_win(long t, const WinMap& w) {
+  if (w.ws == 0) return t;
+  const long hw = (long)w.H * w.W;
+  const long b = t / hw;
+  const int p = (int)(t - b * hw);
+  int y = p / w.W, x = p - (p / w.W) * w.W;
+  y -= w.shift; if (y < 0) y += w.H;
+  x -= w.shift; if (x < 0) x += w.W;
+  const int nWw = w.W / w.ws, nW = (w.H / w.ws) * nWw;
+  const int wy = y / w.ws, wx = x / w.ws;
+  return ((b * nW + wy * nWw + wx) * w.ws + (y - wy * w.ws)) * w.ws + (x - wx * w.ws);
+}
 KAIR_DEV long win_to_token(long m, const WinMap& w) {
   if (w.ws == 0) return m;
   const int ws2 = w.ws * w.ws;

@@ -102,6 +102,25 @@ __global__ __launch_bounds__(1024) void wgrad_finalize_kernel(const float* __res
   }
 }
 
+// dst[token_to_win(t)] = scale(t) * src[t] (cast), 4 columns per thread
+template <typename T>
+__global__ void row_copy_kernel(const float* __restrict__ src, long lds, T* __restrict__ dst, long ldd,
+                                const float* __restrict__ scale, int rps, WinMap wm, long M, int C4) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C4) return;
+  const long t = i / C4;
+  const int c = (int)(i - t * C4) * 4;
+  const float4 v = *(const float4*)(src + t * lds + c);
+  const float sc = scale ? scale[t / rps] : 1.f;
+  T* o = dst + token_to_win(t, wm) * ldd + c;
+  if constexpr (sizeof(T) == 2) {
+    bf16x4 q = {(bf16)(sc * v.x), (bf16)(sc * v.y), (bf16)(sc * v.z), (bf16)(sc * v.w)};
+    *(bf16x4*)o = q;
+  } else {
+    *(float4*)o = make_float4(sc * v.x, sc * v.y, sc * v.z, sc * v.w);
+  }
+}
+
 template <typename T>
 __global__ void colsum_partial(const T* __restrict__ g, long ld, long M, int Np, float* __restrict__ ws, long rows_per) {
   const int c = blockIdx.y * blockDim.x + threadIdx.x;
@@ -302,6 +321,25 @@ extern "C" int kair_wgrad_finalize(const float* partial, int splits, const kair_
   const long tot = nw + (bias_grad ? mp.N : 0);
   hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(nblk(tot, 64)), dim3(1024), 0, (hipStream_t)stream, partial, splits, mp,
                      grad_ref, bias_grad, ones_col, accumulate, nw, Kt, Np * Kt);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_row_copy(const float* src, long lds, long M, int C, const kair_copy_desc* copy, void* stream) {
+  KAIR_CHECK_ARG(src && copy && copy->out && M > 0 && C > 0, "row_copy: bad args");
+  KAIR_CHECK_ARG(C % 4 == 0 && lds % 4 == 0 && copy->ld % 4 == 0, "row_copy: widths must be multiples of 4");
+  KAIR_CHECK_ARG(copy->win_ws == 0 || (copy->win_H % copy->win_ws == 0 && copy->win_W % copy->win_ws == 0),
+                 "row_copy: window geometry");
+  const WinMap wm{copy->win_H, copy->win_W, copy->win_ws, copy->win_shift};
+  const int rps = copy->rows_per_scale > 0 ? copy->rows_per_scale : 1;
+  const long n = M * (C / 4);
+  hipStream_t s = (hipStream_t)stream;
+  if (copy->dtype == KAIR_BF16)
+    hipLaunchKernelGGL(row_copy_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (bf16*)copy->out, copy->ld,
+                       copy->rowscale, rps, wm, M, C / 4);
+  else
+    hipLaunchKernelGGL(row_copy_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (float*)copy->out, copy->ld,
+                       copy->rowscale, rps, wm, M, C / 4);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

@@ -93,7 +93,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
                                                       long ldy, const float* __restrict__ gamma,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
                                                       float* dx, long ld_dx, int dx_acc, float* __restrict__ part,
-                                                      long M, int C, WinMap wm) {
+                                                      long M, int C, WinMap wm, void* cp, int cp_dt, long ldc,
+                                                      const float* __restrict__ cp_scale, int cp_rps, WinMap cwm) {
   const int sub = threadIdx.x & (LPR - 1);
   const long grp = (long)blockIdx.x * ROWS_PER_BLOCK_ITER + (threadIdx.x >> 4);
   const long ng = (long)gridDim.x * ROWS_PER_BLOCK_ITER;
@@ -145,6 +146,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
         for (int j = 0; j < 4; ++j) d[j] = (c + j < C) ? rs * (gy[i][j] - s1 - xh[i][j] * s2) : 0.f;
         cur.x += d[0]; cur.y += d[1]; cur.z += d[2]; cur.w += d[3];
         *(float4*)o = cur;
+        if (cp) {   // GEMM-operand copy of the finished gradient row: scaled, cast, optionally window-ordered
+          const float sc = cp_scale ? cp_scale[t / cp_rps] : 1.f;
+          const long cr = token_to_win(t, cwm);
+          if (cp_dt == KAIR_BF16) store4<bf16>((bf16*)cp + cr * ldc + c, sc * cur.x, sc * cur.y, sc * cur.z, sc * cur.w);
+          else store4<float>((float*)cp + cr * ldc + c, sc * cur.x, sc * cur.y, sc * cur.z, sc * cur.w);
+        }
       }
     }
   }
@@ -217,20 +224,34 @@ extern "C" int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype
 extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int dy_dtype, long ldy, const float* gamma,
                                   const float* mean, const float* rstd, float* dx_acc, long ld_dx, int dx_accumulate,
                                   float* dgamma, float* dbeta, int dparam_accumulate, float* ws, long M, int C,
-                                  int win_H, int win_W, int win_ws, int win_shift, void* stream) {
+                                  int win_H, int win_W, int win_ws, int win_shift, const kair_copy_desc* copy,
+                                  void* stream) {
   KAIR_CHECK_ARG(x && dy && gamma && mean && rstd && dx_acc && dgamma && dbeta && ws, "layernorm_bwd: null pointer");
   KAIR_CHECK_ARG(C > 0 && C <= 256 && M > 0, "layernorm_bwd: bad sizes");
   KAIR_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && ld_dx % 4 == 0, "layernorm_bwd: strides must be multiples of 4");
   const WinMap wm{win_H, win_W, win_ws, win_shift};
+  void* cp = nullptr;
+  int cp_dt = KAIR_F32, cp_rps = 1;
+  long ldc = 0;
+  const float* cp_scale = nullptr;
+  WinMap cwm{0, 0, 0, 0};
+  if (copy && copy->out) {
+    KAIR_CHECK_ARG(copy->ld % 4 == 0 && copy->ld >= C, "layernorm_bwd: copy stride");
+    KAIR_CHECK_ARG(copy->win_ws == 0 || (copy->win_H % copy->win_ws == 0 && copy->win_W % copy->win_ws == 0),
+                   "layernorm_bwd: copy window geometry");
+    cp = copy->out; cp_dt = copy->dtype; ldc = copy->ld; cp_scale = copy->rowscale;
+    cp_rps = copy->rows_per_scale > 0 ? copy->rows_per_scale : 1;
+    cwm = WinMap{copy->win_H, copy->win_W, copy->win_ws, copy->win_shift};
+  }
   hipStream_t s = (hipStream_t)stream;
   long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;
   if (nb > LN_BLOCKS) nb = LN_BLOCKS;
   if (dy_dtype == KAIR_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const bf16*)dy, ldy, gamma,
-                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm);
+                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm);
   else
     hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const float*)dy, ldy, gamma,
-                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm);
+                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm);
   KAIR_CHECK_LAUNCH();
   hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, dgamma, dbeta,
                      dparam_accumulate);

@@ -240,6 +240,7 @@ class SwinIREngine:
         # backward scratch
         P["D"], P["G"] = e(M, Cp), e(M, Cp)
         P["dU"], P["dxn"] = e(M, Hdp, dt=T), e(M, Cp, dt=T)
+        P["Dc"] = e(M, Cp, dt=T)   # compute-dtype GEMM operand copy of the residual-stream gradient
         P["dO"], P["dqkv"] = e(M, nh * 32, dt=T), e(3 * M * nh * 32, dt=T)
         P["ln_ws"] = e(2 * 1024 * Cp)
         P["attn_ws"] = e(H.window_attn_bwd_ws(nWin, nh))
@@ -471,10 +472,14 @@ class SwinIREngine:
             H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(conv.Wd), H.epilogue(D), M, Cp, 9 * Cp, cd)
             self._wgrad(P, H.rows(G), H.im2col(t_d, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, conv.map, g(conv.w),
                         g(conv.b), self.C)
+            # GEMM-operand copy of D for the last block's MLP branch: s_mlp * D in compute dtype
+            drop = P["drop"]
+            H.row_copy(D, Cp, M, Cp, H.copy_desc(P["Dc"], rowscale=drop[bi - 1, 1] if drop is not None else None,
+                                                 rows_per_scale=Hh * Ww))
             for j in range(len(blks) - 1, -1, -1):
                 bi -= 1
                 x_in = P["blocks"][bi - 1]["out"] if j > 0 else (P["rstb_out"][gi - 1] if gi > 0 else P["s0"])
-                self._block_bwd(blks[j], P, P["blocks"][bi], x_in, D, bi, grads)
+                self._block_bwd(blks[j], P, P["blocks"][bi], x_in, D, bi, grads, copy_prev=j > 0)
             H.axpy(G, D, 1.0)   # dL/du_g = skip + blocks path
         # ---- patch_embed norm: s0 = LN(f0); f0 also feeds fb (long skip) --------------------
         n = self.pe_norm
@@ -484,8 +489,12 @@ class SwinIREngine:
         self._wgrad(P, H.rows(P["dfb"]), H.im2col(P["xin"], Hh, Ww, self.Cin_p, ones_col=self.in_ch), M, Cp,
                     9 * self.Cin_p, c.map, g(c.w), g(c.b), self.in_ch)
 
-    def _block_bwd(self, blk, P, S, x_in, D, bi, grads):
-        """D: dL/d out (fp32, token rows) -> updated in place to dL/d x_in."""
+    def _block_bwd(self, blk, P, S, x_in, D, bi, grads, copy_prev=False):
+        """D: dL/d out (fp32, token rows) -> updated in place to dL/d x_in.
+
+        P["Dc"] holds the compute-dtype GEMM operand copy of D: on entry s_mlp * D (token order);
+        LN2-backward rewrites it as s_attn * D_mid in window order (proj); LN1-backward, when the
+        previous block is in the same RSTB, as that block's s_mlp * D_in (token order)."""
         cd, g = self.cd, (lambda p: grads[p])
         M, Cp, nh, Hh, Ww = P["M"], self.Cp, self.nh, P["H"], P["W"]
         HW = Hh * Ww
@@ -495,23 +504,20 @@ class SwinIREngine:
         s_mlp = drop[bi, 1] if drop is not None else None
         hd = self.C // nh
         # MLP: out = mid + s_mlp * fc2(gelu(fc1(LN2(mid))))
+        Dc = P["Dc"]
         l = blk.fc2
-        H.gemm_nt(H.rows(D, rowscale=s_mlp, rows_per_scale=HW), H.rows(l.Wt),
-                  H.epilogue(P["dU"], gate=S["u"], gate_kind=1), M, self.Hdp, Cp, cd)
-        self._wgrad(P, H.rows(D, rowscale=s_mlp, rows_per_scale=HW), H.rows(S["h"], ones_col=l.K), M, Cp, self.Hdp, l.map,
-                    g(l.w), g(l.b), l.K)
+        H.gemm_nt(H.rows(Dc), H.rows(l.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=1), M, self.Hdp, Cp, cd)
+        self._wgrad(P, H.rows(Dc), H.rows(S["h"], ones_col=l.K), M, Cp, self.Hdp, l.map, g(l.w), g(l.b), l.K)
         l = blk.fc1
         H.gemm_nt(H.rows(P["dU"]), H.rows(l.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
         self._wgrad(P, H.rows(P["dU"]), H.rows(S["ln2"], ones_col=self.C), M, self.Hdp, Cp, l.map, g(l.w), g(l.b), self.C)
         n = blk.n2
         H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, g(n.weight), g(n.bias), False,
-                        P["ln_ws"], M, self.C)
+                        P["ln_ws"], M, self.C, copy=H.copy_desc(Dc, rowscale=s_attn, rows_per_scale=HW, win=win))
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         l = blk.proj
-        H.gemm_nt(H.rows(D, win=win, rowscale=s_attn, rows_per_scale=HW), H.rows(l.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp,
-                  cd)
-        self._wgrad(P, H.rows(D, win=win, rowscale=s_attn, rows_per_scale=HW), H.rows(S["O"], ones_col=hd), M, Cp,
-                    nh * 32, l.map, g(l.w), g(l.b), hd)
+        H.gemm_nt(H.rows(Dc), H.rows(l.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
+        self._wgrad(P, H.rows(Dc), H.rows(S["O"], ones_col=hd), M, Cp, nh * 32, l.map, g(l.w), g(l.b), hd)
         H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], P["dqkv"], g(blk.table), False,
                           P["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
         l = blk.qkv
@@ -519,8 +525,11 @@ class SwinIREngine:
         self._wgrad(P, H.qkvblk(P["dqkv"], nh), H.rows(S["ln1"], ones_col=self.C), M, l.Np, Cp, l.map, g(l.w), g(l.b),
                     self.C)
         n = blk.n1
+        cp = None
+        if copy_prev:
+            cp = H.copy_desc(Dc, rowscale=drop[bi - 1, 1] if drop is not None else None, rows_per_scale=HW)
         H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, g(n.weight), g(n.bias), False,
-                        P["ln_ws"], M, self.C, win)
+                        P["ln_ws"], M, self.C, win, copy=cp)
 
 
 class SwinIRFunction(torch.autograd.Function):

@@ -203,9 +203,18 @@ def test_layernorm(dtype, win):
     dx = torch.ones(M, ld, device=dev)  # accumulate onto ones
     dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
     ws = torch.empty(2 * 1024 * C, device=dev)
-    H.layernorm_bwd(xd, ld, dy.to(dev, DT[dtype]), ld, gamma.to(dev), mean, rstd, dx, ld, True, dg, db, False, ws, M, C, win)
+    # GEMM-operand copy of the finished dx: per-sample scale, Swin window order (the other map)
+    cwin = (16, 16, 8, 4) if not win[2] else None
+    sc = torch.tensor([0.5, 2.0], device=dev)
+    cp = torch.zeros(M, ld, device=dev, dtype=DT[dtype])
+    H.layernorm_bwd(xd, ld, dy.to(dev, DT[dtype]), ld, gamma.to(dev), mean, rstd, dx, ld, True, dg, db, False, ws, M, C, win,
+                    copy=H.copy_desc(cp, rowscale=sc, rows_per_scale=256, win=cwin))
     torch.cuda.synchronize()
     assert rel_err(dx[:, :C] - 1, xr.grad) < TOL[dtype][0]
+    want = dx.cpu() * sc.cpu().repeat_interleave(256)[:, None]
+    if cwin:
+        want = want[win_perm(2, 16, 16, 8, 4)]
+    assert rel_err(cp[:, :C].float(), want[:, :C]) < TOL[dtype][0] / 4
     assert rel_err(dg, gm.grad) < TOL[dtype][0]
     assert rel_err(db, bt.grad) < TOL[dtype][0]
 
@@ -357,3 +366,16 @@ def test_gemm_qkvblk_A_operand():
     ref = a @ w.to(torch.bfloat16).double().T
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [H.F32, H.BF16])
+def test_row_copy(dtype):
+    M, C, ld = 512, 192, 200
+    g = torch.Generator().manual_seed(19)
+    src = torch.randn(M, ld, generator=g)
+    sc = torch.tensor([3.0, -1.0])
+    out = torch.empty(M, C, device=dev, dtype=DT[dtype])
+    H.row_copy(src.to(dev), ld, M, C, H.copy_desc(out, rowscale=sc.to(dev), rows_per_scale=256, win=(16, 16, 8, 4)))
+    want = (src[:, :C] * sc.repeat_interleave(256)[:, None])[win_perm(2, 16, 16, 8, 4)]
+    torch.cuda.synchronize()
+    assert rel_err(out.float(), want) < TOL[dtype][0] / 4
