@@ -49,6 +49,8 @@ typedef struct {
   int qkv_nh, qkv_hdp, qkv_tok;        /* QKVBLK                                              */
   const float* rowscale; int rows_per_scale; /* optional per-sample scale (DropPath)          */
   int ones_col;        /* >=0: this column reads as 1.0 (fused bias gradient), else -1       */
+  int ones_in_data;    /* 1: the producer already stored 1.0 in column ones_col of every row
+                          (lets DMA loaders skip the injection); 0: loaders inject it         */
 } kair_operand;
 
 typedef enum {
@@ -79,6 +81,8 @@ typedef struct {
   int ps_r, ps_H, ps_W;                 /* pixel (un)shuffle geometry                         */
   int qkv_nh, qkv_hdp, qkv_tok;         /* KAIR_OUT_QKVBLK                                    */
   const float* img_mean; float img_range; int img_C, img_H, img_W; /* KAIR_OUT_NCHW          */
+  int out_ones_col_p1;                  /* ROWS: 1 + column whose `out` value is forced to 1.0
+                                           (the next weight-gradient GEMM's ones column); 0 none */
 } kair_epilogue;
 
 /* C[m,n] = sum_k A[m,k] * B[n,k]  (+ epilogue).  compute: KAIR_BF16 -> v_mfma_f32_16x16x32_bf16,
@@ -137,7 +141,7 @@ int kair_colsum(const kair_operand* G, long M, int Np, const kair_wmap* map, flo
  * y pad columns [C, ldy) written 0.  mean/rstd fp32 [M] indexed by token row. */
 int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype, long ldy, const float* gamma,
                        const float* beta, float* mean, float* rstd, long M, int C, float eps,
-                       int win_H, int win_W, int win_ws, int win_shift, void* stream);
+                       int win_H, int win_W, int win_ws, int win_shift, int one_col, void* stream);
 /* A row-scaled, cast copy of an fp32 token-row matrix (the next GEMM's A operand):
  * out[token_to_win(t)][c] = rowscale[t / rows_per_scale] * src[t][c]  (window order when win_ws > 0). */
 typedef struct {
@@ -166,7 +170,8 @@ int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int dy_dtype, l
  * lse fp32 [nWin][nh][64] (for backward).  Region mask is computed analytically for a
  * shift>0 block on an H x W token grid (calculate_mask, network_swinir.py:216-237). */
 int kair_window_attn_fwd(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
-                         long nWin, int nh, int hd, float scale, int H, int W, int shift, void* stream);
+                         long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
+                         void* stream);
 /* Backward: dO rows [nWin*64, lddo] (dtype, same layout as O); writes dqkv head-blocked (dtype);
  * dtable (+)= bias-table gradient (ws: nh*64*64*partials floats, kair_window_attn_bwd_ws()). */
 long kair_window_attn_bwd_ws(long nWin, int nh);

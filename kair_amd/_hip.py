@@ -24,7 +24,7 @@ class Operand(ctypes.Structure):
                 ("win_H", c_int), ("win_W", c_int), ("win_ws", c_int), ("win_shift", c_int),
                 ("im_H", c_int), ("im_W", c_int), ("im_C", c_int), ("im_flip", c_int),
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
-                ("rowscale", c_vp), ("rows_per_scale", c_int), ("ones_col", c_int)]
+                ("rowscale", c_vp), ("rows_per_scale", c_int), ("ones_col", c_int), ("ones_in_data", c_int)]
 
 
 class CopyDesc(ctypes.Structure):
@@ -54,7 +54,8 @@ class Epilogue(ctypes.Structure):
                 ("gate", c_vp), ("gate_dtype", c_int), ("ldg", c_long), ("gate_kind", c_int),
                 ("ps_r", c_int), ("ps_H", c_int), ("ps_W", c_int),
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
-                ("img_mean", c_vp), ("img_range", c_float), ("img_C", c_int), ("img_H", c_int), ("img_W", c_int)]
+                ("img_mean", c_vp), ("img_range", c_float), ("img_C", c_int), ("img_H", c_int), ("img_W", c_int),
+                ("out_ones_col_p1", c_int)]
 
 
 class WMap(ctypes.Structure):
@@ -79,12 +80,12 @@ _SIGS = {
     "kair_wgrad_finalize": [c_vp, c_int, ctypes.POINTER(WMap), c_vp, c_vp, c_int, c_int, c_vp],
     "kair_colsum": [ctypes.POINTER(Operand), c_long, c_int, ctypes.POINTER(WMap), c_vp, c_vp, c_int, c_vp],
     "kair_layernorm_fwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_float, c_int,
-                           c_int, c_int, c_int, c_vp],
+                           c_int, c_int, c_int, c_int, c_vp],
     "kair_layernorm_bwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_vp, c_vp, c_int,
                            c_vp, c_long, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(CopyDesc), c_vp],
     "kair_row_copy": [c_vp, c_long, c_long, c_int, ctypes.POINTER(CopyDesc), c_vp],
     "kair_window_attn_fwd": [c_vp, c_int, c_vp, c_vp, c_long, c_vp, c_long, c_int, c_int, c_float, c_int, c_int, c_int,
-                             c_vp],
+                             c_int, c_vp],
     "kair_window_attn_bwd_ws": [c_long, c_int],
     "kair_window_attn_bwd": [c_vp, c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_int,
                              c_int, c_float, c_int, c_int, c_int, c_vp],
@@ -153,7 +154,7 @@ def require_device(*ts):
 # ------------------------------------------------------------------------------------------
 # descriptor builders
 # ------------------------------------------------------------------------------------------
-def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1):
+def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1, ones_in_data=False):
     """Row-major operand; win = (H, W, ws, shift) applies the Swin window->token row map."""
     o = Operand()
     o._keep = (t, rowscale)  # keep the tensors alive until the launch has been issued
@@ -166,6 +167,7 @@ def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1):
     o.rowscale = ptr(rowscale)
     o.rows_per_scale = rows_per_scale
     o.ones_col = ones_col
+    o.ones_in_data = int(ones_in_data)
     return o
 
 
@@ -196,12 +198,13 @@ def qkvblk(t, nh, hdp=32, tok=64, rowscale=None, rows_per_scale=1):
 
 def epilogue(out, mode=OUT_ROWS, ldo=None, win=None, bias=None, act=ACT_NONE, slope=0.0, pre=None, ldp=None,
              resid=None, ldr=None, rowscale=None, rows_per_scale=1, gate=None, ldg=None, gate_kind=0,
-             ps=None, qkv=None, img=None):
+             ps=None, qkv=None, img=None, ones_col=-1):
     e = Epilogue()
     e._keep = (out, bias, pre, resid, rowscale, gate, img)
     e.out = ptr(out)
     e.out_dtype = dtype_code(out)
     e.out_mode = mode
+    e.out_ones_col_p1 = ones_col + 1
     e.ldo = ldo if ldo is not None else out.shape[-1]
     if win:
         e.win_H, e.win_W, e.win_ws, e.win_shift = win
@@ -284,9 +287,9 @@ def colsum(G, M, Np, m, bias_grad, ws, accumulate=False):
                             stream_ptr()), "colsum")
 
 
-def layernorm_fwd(x, ldx, y, ldy, gamma, beta, mean, rstd, M, C, eps=1e-5, win=(0, 0, 0, 0)):
+def layernorm_fwd(x, ldx, y, ldy, gamma, beta, mean, rstd, M, C, eps=1e-5, win=(0, 0, 0, 0), one_col=-1):
     check(lib().kair_layernorm_fwd(ptr(x), ldx, ptr(y), dtype_code(y), ldy, ptr(gamma), ptr(beta), ptr(mean), ptr(rstd),
-                                   M, C, eps, *win, stream_ptr()), "layernorm_fwd")
+                                   M, C, eps, *win, one_col, stream_ptr()), "layernorm_fwd")
 
 
 def layernorm_bwd(x, ldx, dy, ldy, gamma, mean, rstd, dx, ld_dx, dx_acc, dgamma, dbeta, dparam_acc, ws, M, C,
@@ -300,9 +303,9 @@ def row_copy(src, ld_src, M, C, copy):
     check(lib().kair_row_copy(ptr(src), ld_src, M, C, ctypes.byref(copy), stream_ptr()), "row_copy")
 
 
-def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift):
+def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, ones_col=-1):
     check(lib().kair_window_attn_fwd(ptr(qkv), dtype_code(qkv), ptr(table), ptr(O), ldo, ptr(lse), nWin, nh, hd, scale,
-                                     H, W, shift, stream_ptr()), "window_attn_fwd")
+                                     H, W, shift, ones_col, stream_ptr()), "window_attn_fwd")
 
 
 def window_attn_bwd_ws(nWin, nh):

@@ -55,56 +55,92 @@ KAIR_DEV float gelu_erf_grad(float x) {
   return cdf + x * pdf;
 }
 
+// Fast integer division for 0 <= n < 2^24 (row / column indices): float reciprocal + one
+// correction step (exact there).  Runtime-divisor integer division costs ~30-40 VALU on CDNA;
+// this is ~6.
+struct FDiv {
+  int d;
+  float r;
+};
+inline FDiv make_fdiv(int d) { return FDiv{d, d > 0 ? 1.0f / (float)d : 0.f}; }
+KAIR_DEV int fdiv(int n, const FDiv& f) {
+  int q = (int)((float)n * f.r);
+  const int rem = n - q * f.d;
+  if (rem < 0) --q;
+  else if (rem >= f.d) ++q;
+  return q;
+}
+
+// Fast erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 absolute): ~12 VALU with one rcp and
+// one exp, against ~30 for erff.  Used only on bf16-compute epilogues, where the output rounding
+// (2^-9 relative) dominates; the fp32 parity path keeps erff.
+KAIR_DEV float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __frcp_rn(1.0f + 0.3275911f * ax);
+  float y = 1.061405429f;
+  y = fmaf(y, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  y = 1.0f - y * t * __expf(-ax * ax);
+  return copysignf(y, x);
+}
+KAIR_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+KAIR_DEV float gelu_grad_fast(float x) {
+  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
+  return cdf + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
 // Swin window <-> token row map (network_swinir.py:33-62 + torch.roll at :250/:270):
 // GEMM row m enumerates tokens window-major (b, wy, wx, r, c); the token it reads / writes lives at
-// ((wy*ws + r + shift) % H, (wx*ws + c + shift) % W) of image b.
+// ((wy*ws + r + shift) % H, (wx*ws + c + shift) % W) of image b.  Indices < 2^24 (checked at the
+// C-ABI entry points that take a window map).
 struct WinMap {
   int H, W, ws, shift;  // ws == 0 => identity map
+  FDiv dws2, dnW, dnWw, dws, dW, dHW;
 };
-// 32-bit form (row counts < 2^31) for per-tile address setup in the GEMM mainloops
+inline WinMap make_winmap(int H, int W, int ws, int shift) {
+  WinMap w{H, W, ws, shift, {}, {}, {}, {}, {}, {}};
+  if (ws > 0) {
+    const int nWw = W / ws, nW = (H / ws) * nWw;
+    w.dws2 = make_fdiv(ws * ws);
+    w.dnW = make_fdiv(nW);
+    w.dnWw = make_fdiv(nWw);
+    w.dws = make_fdiv(ws);
+    w.dW = make_fdiv(W);
+    w.dHW = make_fdiv(H * W);
+  }
+  return w;
+}
+constexpr long KAIR_MAX_MAPPED_ROWS = 1L << 24;
+
 KAIR_DEV int win_to_token32(int m, const WinMap& w) {
   if (w.ws == 0) return m;
-  const int ws2 = w.ws * w.ws;
-  const int nWw = w.W / w.ws, nW = (w.H / w.ws) * nWw;
-  const int win = m / ws2;
-  const int t = m - win * ws2;
-  const int b = win / nW;
-  const int wi = win - b * nW;
-  const int wy = wi / nWw, wx = wi - wy * nWw;
-  const int ty = t / w.ws;
+  const int win = fdiv(m, w.dws2);
+  const int t = m - win * w.dws2.d;
+  const int b = fdiv(win, w.dnW);
+  const int wi = win - b * w.dnW.d;
+  const int wy = fdiv(wi, w.dnWw), wx = wi - wy * w.dnWw.d;
+  const int ty = fdiv(t, w.dws);
   int y = wy * w.ws + ty + w.shift;
   int x = wx * w.ws + (t - ty * w.ws) + w.shift;
   if (y >= w.H) y -= w.H;
   if (x >= w.W) x -= w.W;
   return (b * w.H + y) * w.W + x;
 }
+KAIR_DEV long win_to_token(long m, const WinMap& w) { return w.ws == 0 ? m : (long)win_to_token32((int)m, w); }
+
 // inverse of win_to_token: window-order row of token t
-KAIR_DEV long token_to_win(long t, const WinMap& w) {
-  if (w.ws == 0) return t;
-  const long hw = (long)w.H * w.W;
-  const long b = t / hw;
-  const int p = (int)(t - b * hw);
-  int y = p / w.W, x = p - (p / w.W) * w.W;
+KAIR_DEV long token_to_win(long tl, const WinMap& w) {
+  if (w.ws == 0) return tl;
+  const int t = (int)tl;
+  const int b = fdiv(t, w.dHW);
+  const int p = t - b * w.dHW.d;
+  int y = fdiv(p, w.dW), x = p - y * w.W;
   y -= w.shift; if (y < 0) y += w.H;
   x -= w.shift; if (x < 0) x += w.W;
-  const int nWw = w.W / w.ws, nW = (w.H / w.ws) * nWw;
-  const int wy = y / w.ws, wx = x / w.ws;
-  return ((b * nW + wy * nWw + wx) * w.ws + (y - wy * w.ws)) * w.ws + (x - wx * w.ws);
-}
-KAIR_DEV long win_to_token(long m, const WinMap& w) {
-  if (w.ws == 0) return m;
-  const int ws2 = w.ws * w.ws;
-  const int nWw = w.W / w.ws, nW = (w.H / w.ws) * nWw;
-  const long win = m / ws2;
-  const int t = (int)(m - win * ws2);
-  const long b = win / nW;
-  const int wi = (int)(win - b * nW);
-  const int wy = wi / nWw, wx = wi - wy * nWw;
-  int y = wy * w.ws + t / w.ws + w.shift;
-  int x = wx * w.ws + t % w.ws + w.shift;
-  if (y >= w.H) y -= w.H;
-  if (x >= w.W) x -= w.W;
-  return (b * w.H + y) * (long)w.W + x;
+  const int wy = fdiv(y, w.dws), wx = fdiv(x, w.dws);
+  return (((long)b * w.dnW.d + wy * w.dnWw.d + wx) * w.ws + (y - wy * w.ws)) * w.ws + (x - wx * w.ws);
 }
 
 // Deterministic sum over `nparts` partial planes for 64 consecutive outputs per 1024-thread block:

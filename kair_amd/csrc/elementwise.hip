@@ -328,9 +328,10 @@ extern "C" int kair_wgrad_finalize(const float* partial, int splits, const kair_
 extern "C" int kair_row_copy(const float* src, long lds, long M, int C, const kair_copy_desc* copy, void* stream) {
   KAIR_CHECK_ARG(src && copy && copy->out && M > 0 && C > 0, "row_copy: bad args");
   KAIR_CHECK_ARG(C % 4 == 0 && lds % 4 == 0 && copy->ld % 4 == 0, "row_copy: widths must be multiples of 4");
+  KAIR_CHECK_ARG(M < KAIR_MAX_MAPPED_ROWS, "row_copy: M must be < 2^24");
   KAIR_CHECK_ARG(copy->win_ws == 0 || (copy->win_H % copy->win_ws == 0 && copy->win_W % copy->win_ws == 0),
                  "row_copy: window geometry");
-  const WinMap wm{copy->win_H, copy->win_W, copy->win_ws, copy->win_shift};
+  const WinMap wm = make_winmap(copy->win_H, copy->win_W, copy->win_ws, copy->win_shift);
   const int rps = copy->rows_per_scale > 0 ? copy->rows_per_scale : 1;
   const long n = M * (C / 4);
   hipStream_t s = (hipStream_t)stream;

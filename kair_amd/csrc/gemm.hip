@@ -40,18 +40,24 @@ struct Op {
   const float* rowscale;
   int rps;
   int ones_col;
+  int ones_in_data;
   long M;  // rows of this operand
+  FDiv d_rps, d_imC, d_imW, d_hw, d_tok, d_hdp, d_pw;
 };
 
 Op make_op(const kair_operand& o, long M) {
   Op op;
   op.ptr = o.ptr; op.ld = o.ld;
-  op.win = WinMap{o.win_H, o.win_W, o.win_ws, o.win_shift};
+  op.win = make_winmap(o.win_H, o.win_W, o.win_ws, o.win_shift);
   op.imH = o.im_H; op.imW = o.im_W; op.imC = o.im_C; op.flip = o.im_flip;
   op.nh = o.qkv_nh; op.hdp = o.qkv_hdp; op.tok = o.qkv_tok;
   op.rowscale = o.rowscale; op.rps = o.rows_per_scale > 0 ? o.rows_per_scale : 1;
   op.ones_col = o.ones_col;
+  op.ones_in_data = o.ones_in_data;
   op.M = M;
+  op.d_rps = make_fdiv(op.rps);
+  op.d_imC = make_fdiv(op.imC); op.d_imW = make_fdiv(op.imW); op.d_hw = make_fdiv(op.imH * op.imW);
+  op.d_tok = make_fdiv(op.tok); op.d_hdp = make_fdiv(op.hdp); op.d_pw = make_fdiv(op.nh * op.hdp);
   return op;
 }
 
@@ -93,19 +99,19 @@ KAIR_DEV RowState row_state(const Op& op, long m) {
   if constexpr (AM == AM_ROWS) {
     const long t = win_to_token(m, op.win);
     r.base = t * op.ld;
-    if (op.rowscale) r.scale = op.rowscale[t / op.rps];
+    if (op.rowscale) r.scale = op.rowscale[fdiv((int)t, op.d_rps)];
   } else if constexpr (AM == AM_IM2COL) {
-    const int hw = op.imH * op.imW;
-    const int b = (int)(m / hw);
-    const int p = (int)(m - (long)b * hw);
-    r.y = p / op.imW;
+    const int hw = op.d_hw.d;
+    const int b = fdiv((int)m, op.d_hw);
+    const int p = (int)m - b * hw;
+    r.y = fdiv(p, op.d_imW);
     r.x = p - r.y * op.imW;
     r.base = (long)p + (long)b * hw;
   } else {
-    const long win = m / op.tok;
-    const int t = (int)(m - win * op.tok);
-    r.base = (win * op.nh * op.tok + t) * op.hdp;
-    if (op.rowscale) r.scale = op.rowscale[m / op.rps];
+    const int win = fdiv((int)m, op.d_tok);
+    const int t = (int)m - win * op.tok;
+    r.base = ((long)win * op.nh * op.tok + t) * op.hdp;
+    if (op.rowscale) r.scale = op.rowscale[fdiv((int)m, op.d_rps)];
   }
   return r;
 }
@@ -140,7 +146,7 @@ KAIR_DEV void issue_chunk(const Op& op, const RowState& r, int k, int K, Raw<T>&
   if constexpr (AM == AM_ROWS) {
     off = r.base + k;
   } else if constexpr (AM == AM_IM2COL) {
-    const int tap = k / op.imC;
+    const int tap = fdiv(k, op.d_imC);
     const int c = k - tap * op.imC;
     int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
     if (op.flip) { dy = -dy; dx = -dx; }
@@ -148,10 +154,10 @@ KAIR_DEV void issue_chunk(const Op& op, const RowState& r, int k, int K, Raw<T>&
     ok = ok && y >= 0 && y < op.imH && x >= 0 && x < op.imW;
     off = (r.base + (long)dy * op.imW + dx) * op.imC + c;
   } else {
-    const int pw = op.nh * op.hdp;
-    const int part = k / pw;
+    const int pw = op.d_pw.d;
+    const int part = fdiv(k, op.d_pw);
     const int rr = k - part * pw;
-    const int h = rr / op.hdp, d = rr - h * op.hdp;
+    const int h = fdiv(rr, op.d_hdp), d = rr - h * op.hdp;
     off = (long)part * op.M * pw + r.base + (long)h * op.tok * op.hdp + d;
   }
   raw_load<T>((const T*)op.ptr + (ok ? off : 0), raw);
@@ -214,13 +220,15 @@ struct Epi {
   int r, psH, psW;
   int nh, hdp, tok;
   const float* mean; float range; int imgC, imgH, imgW;
+  int ones_col;   // -1 none
   long M; int N;
+  FDiv d_rps, d_tok, d_hdp, d_pw;
 };
 
 Epi make_epi(const kair_epilogue& o, long M, int N) {
   Epi e;
   e.out = o.out; e.odt = o.out_dtype; e.omode = o.out_mode; e.ldo = o.ldo;
-  e.win = WinMap{o.win_H, o.win_W, o.win_ws, o.win_shift};
+  e.win = make_winmap(o.win_H, o.win_W, o.win_ws, o.win_shift);
   e.bias = o.bias; e.act = o.act; e.slope = o.slope;
   e.pre = o.out_pre; e.pdt = o.pre_dtype; e.ldp = o.ldp;
   e.resid = o.resid; e.ldr = o.ldr;
@@ -229,7 +237,9 @@ Epi make_epi(const kair_epilogue& o, long M, int N) {
   e.r = o.ps_r; e.psH = o.ps_H; e.psW = o.ps_W;
   e.nh = o.qkv_nh; e.hdp = o.qkv_hdp; e.tok = o.qkv_tok;
   e.mean = o.img_mean; e.range = o.img_range; e.imgC = o.img_C; e.imgH = o.img_H; e.imgW = o.img_W;
+  e.ones_col = o.out_ones_col_p1 - 1;
   e.M = M; e.N = N;
+  e.d_rps = make_fdiv(e.rps); e.d_tok = make_fdiv(e.tok); e.d_hdp = make_fdiv(e.hdp); e.d_pw = make_fdiv(e.nh * e.hdp);
   return e;
 }
 
@@ -287,9 +297,14 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
       }
     }
     if (e.resid) {
-      const float s = e.rowscale ? e.rowscale[row / e.rps] : 1.f;
+      const float s = e.rowscale ? e.rowscale[fdiv((int)row, e.d_rps)] : 1.f;
       for (int j = 0; j < 8; ++j)
         if (n + j < e.N) v[j] = e.resid[row * e.ldr + n + j] + s * v[j];
+    }
+    if (e.ones_col >= n && e.ones_col < n + 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (n + j == e.ones_col) v[j] = 1.f;
     }
     if (full && (e.ldo % 8) == 0) {
       store8_any(e.out, e.odt, row * e.ldo + n, v);
@@ -302,9 +317,9 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
     }
   } else if (e.omode == KAIR_OUT_QKVBLK) {
     const int pw = e.nh * e.hdp;
-    const int part = n / pw, rr = n - part * pw;
-    const int h = rr / e.hdp, d = rr - h * e.hdp;
-    const long win = m / e.tok;
+    const int part = fdiv(n, e.d_pw), rr = n - part * pw;
+    const int h = fdiv(rr, e.d_hdp), d = rr - h * e.hdp;
+    const long win = fdiv((int)m, e.d_tok);
     const int t = (int)(m - win * e.tok);
     store8_any(e.out, e.odt, (long)part * e.M * pw + ((win * e.nh + h) * e.tok + t) * e.hdp + d, v);
   } else if (e.omode == KAIR_OUT_PSHUF || e.omode == KAIR_OUT_PSHUF_NCHW) {
@@ -519,9 +534,9 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
   }
   if constexpr (EM == EM_QKV) {
     const int pw = e.nh * e.hdp;
-    const int part = n / pw, rr = n - part * pw;
-    const int h = rr / e.hdp, d = rr - h * e.hdp;
-    const long win = m / e.tok;
+    const int part = fdiv(n, e.d_pw), rr = n - part * pw;
+    const int h = fdiv(rr, e.d_hdp), d = rr - h * e.hdp;
+    const long win = fdiv((int)m, e.d_tok);
     const int t = (int)(m - win * e.tok);
     st4_any(e.out, e.odt, (long)part * e.M * pw + ((win * e.nh + h) * e.tok + t) * e.hdp + d, v);
   } else {
@@ -529,7 +544,7 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       pre[j] = v[j];
-      if (e.act == KAIR_ACT_GELU) v[j] = gelu_erf(v[j]);
+      if (e.act == KAIR_ACT_GELU) v[j] = gelu_fast(v[j]);
       else if (e.act == KAIR_ACT_LEAKY) v[j] = v[j] > 0.f ? v[j] : v[j] * e.slope;
       else if (e.act == KAIR_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
     }
@@ -538,7 +553,7 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
       ld4_any(e.gate, e.gdt, row * e.ldg + n, g);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (e.gkind == 1) v[j] *= gelu_erf_grad(g[j]);
+        if (e.gkind == 1) v[j] *= gelu_grad_fast(g[j]);
         else if (e.gkind == 2) v[j] *= (g[j] > 0.f ? 1.f : e.slope);
         else v[j] *= (g[j] > 0.f ? 1.f : 0.f);
       }
@@ -546,6 +561,11 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
     if (e.resid) {
       const float4 r = *(const float4*)(e.resid + row * e.ldr + n);
       v[0] = r.x + rs * v[0]; v[1] = r.y + rs * v[1]; v[2] = r.z + rs * v[2]; v[3] = r.w + rs * v[3];
+    }
+    if (e.ones_col >= n && e.ones_col < n + 4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j == e.ones_col) v[j] = 1.f;
     }
     st4_any(e.out, e.odt, row * e.ldo + n, v);
     if (e.pre) st4_any(e.pre, e.pdt, row * e.ldp + n, pre);
@@ -622,7 +642,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
       if constexpr (AM == AM_ROWS) {
         rbase[ii] = (long)win_to_token32(m, A.win) * A.ld;
       } else {
-        const int win = m / A.tok, t = m - win * A.tok;
+        const int win = fdiv(m, A.d_tok), t = m - win * A.tok;
         rbase[ii] = ((long)win * A.nh * A.tok + t) * A.hdp;
       }
     }
@@ -638,9 +658,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
       if constexpr (AM == AM_ROWS) {
         off = rbase[ii] + k;
       } else {
-        const int pw = A.nh * A.hdp;
-        const int part = k / pw, rr = k - part * pw;
-        const int h = rr / A.hdp, d = rr - h * A.hdp;
+        const int pw = A.d_pw.d;
+        const int part = fdiv(k, A.d_pw), rr = k - part * pw;
+        const int h = fdiv(rr, A.d_hdp), d = rr - h * A.hdp;
         off = (long)part * A.M * pw + rbase[ii] + (long)h * A.tok * A.hdp + d;
       }
       __builtin_amdgcn_global_load_lds((const void*)((const bf16*)A.ptr + off),
@@ -699,7 +719,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
           float rs = 1.f;
           if constexpr (EM == EM_ROWS) {
             row = win_to_token32(m, E.win);
-            if (E.rowscale) rs = E.rowscale[(int)row / E.rps];
+            if (E.rowscale) rs = E.rowscale[fdiv((int)row, E.d_rps)];
           }
 #pragma unroll
           for (int jn = 0; jn < RN; ++jn) {
@@ -716,6 +736,128 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
       if (j + NS - 1 < total) issue(j + NS - 1);
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// TN ring kernel (weight gradients of the Swin block projections, bf16):
+//   P[s][n][k] = sum_{m in split s} A[m][n] * B[m][k],   one 192x192 (n,k) tile per CTA.
+// 512 threads, one CTA per CU; A and B row chunks (32 rows) stream through a 6-deep LDS ring by
+// LDS-DMA (3 wave-instructions per wave per chunk), counted vmcnt + raw barrier; fragments are
+// ds_read_b64_tr_b16 transposed reads; D = B^T.A so each lane stores 4 consecutive k (16 B).
+// Rows past the split (and columns past N / K) read a zero line.  The bias-gradient "ones" column
+// must already be in B (kair_operand.ones_in_data).
+// ------------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(64))) unsigned char g_kair_zero_line[64];
+
+constexpr int TNR_BN = 192, TNR_BK = 192, TNR_RB = 32, TNR_NS = 6;
+
+template <int AMA>
+__global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
+                                                       int rows_per_split) {
+  constexpr int BNt = TNR_BN, BKt = TNR_BK, RB = TNR_RB, NS = TNR_NS;
+  constexpr int PART = RB * BNt * 2;            // 12 KiB (A part; B part the same since BKt == BNt)
+  constexpr int STAGE = 2 * PART;
+  constexpr int ROWB = BNt * 2;                  // 384 B per LDS row
+  constexpr int RN = 6, RK = 3;                  // wave tile 96 (n) x 48 (k)
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+
+  const int cta = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = cta % ntiles, split = cta / ntiles;
+  const int tn = tile / tilesK, tk = tile - (tile / tilesK) * tilesK;
+  const int n0 = tn * BNt, k0 = tk * BKt;
+  const int mbeg = split * rows_per_split;
+  int mend = mbeg + rows_per_split;
+  if (mend > M) mend = M;
+  const int nchunks = mbeg < mend ? (mend - mbeg + RB - 1) / RB : 0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 2, wk = wave & 3;
+
+  auto issue = [&](int j) {
+    const int m0 = mbeg + j * RB;
+    char* st = smem + (j % NS) * STAGE;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int g = wave * 3 + i;                // 0..23: 12 KiB of A then 12 KiB of B
+      const bool isB = g >= 12;
+      const int off = (isB ? g - 12 : g) * 1024 + lane * 16;
+      const int r = off / ROWB, c = (off - (off / ROWB) * ROWB) >> 1;
+      const int m = m0 + r;
+      const void* src = g_kair_zero_line;
+      if (m < mend) {
+        if (isB) {
+          if (k0 + c < K) src = (const bf16*)B.ptr + (long)m * B.ld + k0 + c;
+        } else if (n0 + c < N) {
+          if constexpr (AMA == AM_ROWS) {
+            src = (const bf16*)A.ptr + (long)m * A.ld + n0 + c;
+          } else {
+            const int n = n0 + c, pw = A.d_pw.d;
+            const int part = fdiv(n, A.d_pw), rr = n - part * pw;
+            const int h = fdiv(rr, A.d_hdp), d = rr - h * A.hdp;
+            const int win = fdiv(m, A.d_tok), t = m - win * A.tok;
+            src = (const bf16*)A.ptr + (long)part * M * pw + (((long)win * A.nh + h) * A.tok + t) * A.hdp + d;
+          }
+        }
+      }
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + (isB ? PART : 0) + (g % 12) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < nchunks) issue(j);
+
+  f32x4 acc[RK][RN];
+#pragma unroll
+  for (int j = 0; j < RK; ++j)
+#pragma unroll
+    for (int i = 0; i < RN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, g8 = (lane >> 4) * 8;
+  for (int j = 0; j < nchunks; ++j) {
+    const int ahead = (nchunks - 1 - j) < (NS - 2) ? (nchunks - 1 - j) : (NS - 2);
+    if (ahead >= 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (ahead == 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ring_barrier();
+    if (j + NS - 1 < nchunks) issue(j + NS - 1);
+    const bf16* sA = (const bf16*)(smem + (j % NS) * STAGE);
+    const bf16* sB = sA + RB * BNt;
+    bf16x8 af[RN], bfr[RK];
+#pragma unroll
+    for (int i = 0; i < RN; ++i) {
+      const bf16* base = sA + (g8 + q) * BNt + wn * 96 + i * 16 + p4;
+      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base);
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base + 4 * BNt));
+      short __attribute__((ext_vector_type(8))) s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[i] = __builtin_bit_cast(bf16x8, s8);
+    }
+#pragma unroll
+    for (int jk = 0; jk < RK; ++jk) {
+      const bf16* base = sB + (g8 + q) * BKt + wk * 48 + jk * 16 + p4;
+      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base);
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base + 4 * BKt));
+      short __attribute__((ext_vector_type(8))) s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bfr[jk] = __builtin_bit_cast(bf16x8, s8);
+    }
+#pragma unroll
+    for (int jk = 0; jk < RK; ++jk)
+#pragma unroll
+      for (int i = 0; i < RN; ++i)
+        acc[jk][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jk], af[i], acc[jk][i], 0, 0, 0);
+  }
+  // lane holds k = kb + 4*(lane>>4) + r (r < 4) of column n = nb + (lane & 15)
+  float* P = ws + (long)split * N * K;
+#pragma unroll
+  for (int jk = 0; jk < RK; ++jk)
+#pragma unroll
+    for (int i = 0; i < RN; ++i) {
+      const int n = n0 + wn * 96 + i * 16 + (lane & 15);
+      const int k = k0 + wk * 48 + jk * 16 + 4 * (lane >> 4);
+      if (n < N && k < K) *(float4*)(P + (long)n * K + k) = make_float4(acc[jk][i][0], acc[jk][i][1], acc[jk][i][2], acc[jk][i][3]);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1031,6 +1173,8 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
   KAIR_CHECK_ARG((E->out_mode != KAIR_OUT_PSHUF && E->out_mode != KAIR_OUT_PUNSHUF && E->out_mode != KAIR_OUT_PSHUF_NCHW) ||
                      E->ps_r > 0, "gemm_nt: pixel shuffle r");
   KAIR_CHECK_ARG(E->out_mode != KAIR_OUT_QKVBLK || (E->qkv_hdp % 8 == 0 && E->qkv_tok > 0), "gemm_nt: qkv epilogue");
+  KAIR_CHECK_ARG(M < KAIR_MAX_MAPPED_ROWS && N < KAIR_MAX_MAPPED_ROWS && K < KAIR_MAX_MAPPED_ROWS,
+                 "gemm_nt: dimensions must be < 2^24");
   const Op a = make_op(*A, M), b = make_op(*B, N);
   const Epi e = make_epi(*E, M, N);
   hipStream_t s = (hipStream_t)stream;
@@ -1042,7 +1186,19 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
   return kair_set_error(KAIR_ERR_ARG, "gemm_nt: bad compute type");
 }
 
+static bool tn_ring_shape(long M, int N, int K) {
+  return N <= 576 && K <= 576 && N % 8 == 0 && K % 8 == 0 && N > 64 && K > 64 && M < (1L << 30);
+}
+
 extern "C" int kair_wgrad_splits(long M, int N, int K) {
+  if (tn_ring_shape(M, N, K)) {   // ring kernel: one 192x192 tile per CTA, one CTA per CU
+    if (g_num_cus == 0) init_num_cus();
+    const int tiles = ((N + TNR_BN - 1) / TNR_BN) * ((K + TNR_BK - 1) / TNR_BK);
+    long s = g_num_cus / tiles;
+    const long maxs = (M + 255) / 256;
+    if (s > maxs) s = maxs;
+    return (int)(s < 1 ? 1 : s);
+  }
   const long tiles = (N <= 64 && K <= 64) ? 1 : (long)((N + 127) / 128) * ((K + 127) / 128);
   // enough (tile, split) CTAs for ~2 per CU, but >= 1024 rows per split so the fp32 partial
   // planes stay small next to the operand traffic (wgrad_finalize reads them all back)
@@ -1065,7 +1221,32 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
   KAIR_CHECK_ARG(compute == KAIR_BF16 || (A->dtype == KAIR_F32 && B->dtype == KAIR_F32),
                  "gemm_tn: fp32 compute needs fp32 operands");
   KAIR_CHECK_ARG(A->mode != KAIR_LD_QKVBLK || A->dtype == compute, "gemm_tn: q/k/v operand dtype");
+  KAIR_CHECK_ARG(M < KAIR_MAX_MAPPED_ROWS && N < KAIR_MAX_MAPPED_ROWS && K < KAIR_MAX_MAPPED_ROWS,
+                 "gemm_tn: dimensions must be < 2^24");
   const Op a = make_op(*A, M), b = make_op(*B, M);
+  hipStream_t s0 = (hipStream_t)stream;
+  if (g_ring_mode < 0) {
+    const char* v = getenv("KAIR_GEMM_RING");
+    g_ring_mode = (v && v[0] == '0') ? 0 : 1;
+  }
+  if (g_ring_mode && compute == KAIR_BF16 && tn_ring_shape(M, N, K) && A->dtype == KAIR_BF16 && B->dtype == KAIR_BF16 &&
+      (A->mode == KAIR_LD_ROWS || A->mode == KAIR_LD_QKVBLK) && B->mode == KAIR_LD_ROWS && !A->rowscale && !B->rowscale &&
+      A->win_ws == 0 && B->win_ws == 0 && A->ones_col < 0 && (B->ones_col < 0 || B->ones_in_data) &&
+      (A->mode != KAIR_LD_ROWS || A->ld % 8 == 0) && B->ld % 8 == 0 && (A->mode != KAIR_LD_QKVBLK || A->qkv_hdp % 8 == 0)) {
+    const int tilesN = (N + TNR_BN - 1) / TNR_BN, tilesK = (K + TNR_BK - 1) / TNR_BK;
+    const int ntiles = tilesN * tilesK;
+    long rps = (M + splits - 1) / splits;
+    rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
+    const long grid = (long)ntiles * splits;
+    if (A->mode == KAIR_LD_ROWS)
+      hipLaunchKernelGGL(gemm_tn_ring<AM_ROWS>, dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK, ntiles,
+                         (int)rps);
+    else
+      hipLaunchKernelGGL(gemm_tn_ring<AM_QKV>, dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK, ntiles,
+                         (int)rps);
+    KAIR_CHECK_LAUNCH();
+    return 0;
+  }
   const int BMr = compute == KAIR_BF16 ? 64 : 32;
   long rps = (M + splits - 1) / splits;
   rps = (rps + BMr - 1) / BMr * BMr;

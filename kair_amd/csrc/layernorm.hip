@@ -38,7 +38,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, long ldx, T* __restrict__ y, long ldy,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
-                                                      int C, float eps, WinMap wm) {
+                                                      int C, float eps, WinMap wm, int one_col) {
   const int sub = threadIdx.x & (LPR - 1);
   const long grp = (long)blockIdx.x * ROWS_PER_BLOCK_ITER + (threadIdx.x >> 4);
   const long ng = (long)gridDim.x * ROWS_PER_BLOCK_ITER;
@@ -76,8 +76,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
         float o[4] = {0.f, 0.f, 0.f, 0.f};
         const float xv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
           if (c + j < C) o[j] = (xv[j] - mu) * rs * gamma[c + j] + beta[c + j];
+          else if (c + j == one_col) o[j] = 1.f;   // ones column for the weight-gradient GEMM
+        }
         store4<T>(y + r * ldy + c, o[0], o[1], o[2], o[3]);
       }
     }
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
         cur.x += d[0]; cur.y += d[1]; cur.z += d[2]; cur.w += d[3];
         *(float4*)o = cur;
         if (cp) {   // GEMM-operand copy of the finished gradient row: scaled, cast, optionally window-ordered
-          const float sc = cp_scale ? cp_scale[t / cp_rps] : 1.f;
+          const float sc = cp_scale ? cp_scale[(int)t / cp_rps] : 1.f;
           const long cr = token_to_win(t, cwm);
           if (cp_dt == KAIR_BF16) store4<bf16>((bf16*)cp + cr * ldc + c, sc * cur.x, sc * cur.y, sc * cur.z, sc * cur.w);
           else store4<float>((float*)cp + cr * ldc + c, sc * cur.x, sc * cur.y, sc * cur.z, sc * cur.w);
@@ -202,21 +204,23 @@ constexpr int LN_BLOCKS = 1024;  // ws holds LN_BLOCKS * 2 * C floats (kair_hip.
 
 extern "C" int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype, long ldy, const float* gamma,
                                   const float* beta, float* mean, float* rstd, long M, int C, float eps, int win_H,
-                                  int win_W, int win_ws, int win_shift, void* stream) {
+                                  int win_W, int win_ws, int win_shift, int one_col, void* stream) {
   KAIR_CHECK_ARG(x && y && gamma && beta && mean && rstd, "layernorm_fwd: null pointer");
-  KAIR_CHECK_ARG(C > 0 && C <= 256 && ldx >= C && ldy >= C && ldy <= 256 && M > 0, "layernorm_fwd: bad sizes");
+  KAIR_CHECK_ARG(C > 0 && C <= 256 && ldx >= C && ldy >= C && ldy <= 256 && M > 0 && M < KAIR_MAX_MAPPED_ROWS,
+                 "layernorm_fwd: bad sizes");
   KAIR_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)x % 16) == 0, "layernorm_fwd: strides must be multiples of 4");
   KAIR_CHECK_ARG(win_ws == 0 || (win_H % win_ws == 0 && win_W % win_ws == 0), "layernorm_fwd: window geometry");
-  const WinMap wm{win_H, win_W, win_ws, win_shift};
+  KAIR_CHECK_ARG(one_col < 0 || (one_col >= C && one_col < ldy), "layernorm_fwd: ones column must be a pad column");
+  const WinMap wm = make_winmap(win_H, win_W, win_ws, win_shift);
   long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;
   if (nb > 8192) nb = 8192;
   hipStream_t s = (hipStream_t)stream;
   if (y_dtype == KAIR_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (bf16*)y, ldy, gamma, beta,
-                       mean, rstd, M, C, eps, wm);
+                       mean, rstd, M, C, eps, wm, one_col);
   else
     hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (float*)y, ldy, gamma, beta,
-                       mean, rstd, M, C, eps, wm);
+                       mean, rstd, M, C, eps, wm, one_col);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -227,21 +231,21 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
                                   int win_H, int win_W, int win_ws, int win_shift, const kair_copy_desc* copy,
                                   void* stream) {
   KAIR_CHECK_ARG(x && dy && gamma && mean && rstd && dx_acc && dgamma && dbeta && ws, "layernorm_bwd: null pointer");
-  KAIR_CHECK_ARG(C > 0 && C <= 256 && M > 0, "layernorm_bwd: bad sizes");
+  KAIR_CHECK_ARG(C > 0 && C <= 256 && M > 0 && M < KAIR_MAX_MAPPED_ROWS, "layernorm_bwd: bad sizes");
   KAIR_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && ld_dx % 4 == 0, "layernorm_bwd: strides must be multiples of 4");
-  const WinMap wm{win_H, win_W, win_ws, win_shift};
+  const WinMap wm = make_winmap(win_H, win_W, win_ws, win_shift);
   void* cp = nullptr;
   int cp_dt = KAIR_F32, cp_rps = 1;
   long ldc = 0;
   const float* cp_scale = nullptr;
-  WinMap cwm{0, 0, 0, 0};
+  WinMap cwm = make_winmap(0, 0, 0, 0);
   if (copy && copy->out) {
     KAIR_CHECK_ARG(copy->ld % 4 == 0 && copy->ld >= C, "layernorm_bwd: copy stride");
     KAIR_CHECK_ARG(copy->win_ws == 0 || (copy->win_H % copy->win_ws == 0 && copy->win_W % copy->win_ws == 0),
                    "layernorm_bwd: copy window geometry");
     cp = copy->out; cp_dt = copy->dtype; ldc = copy->ld; cp_scale = copy->rowscale;
     cp_rps = copy->rows_per_scale > 0 ? copy->rows_per_scale : 1;
-    cwm = WinMap{copy->win_H, copy->win_W, copy->win_ws, copy->win_shift};
+    cwm = make_winmap(copy->win_H, copy->win_W, copy->win_ws, copy->win_shift);
   }
   hipStream_t s = (hipStream_t)stream;
   long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;

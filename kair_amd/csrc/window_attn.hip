@@ -112,7 +112,7 @@ template <bool BF>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename AT<BF>::T* __restrict__ qkv,
                                                        const float* __restrict__ table, typename AT<BF>::T* __restrict__ O,
                                                        long ldo, float* __restrict__ lse, long nWin, int nh, float scale,
-                                                       int H, int W, int shift) {
+                                                       int H, int W, int shift, int ones_col) {
   using T = typename AT<BF>::T;
   constexpr int LD = AT<BF>::LD;
   constexpr int WAVES = NWAVES<BF>;
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename AT<BF>::T*
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qi = qt * 32 + acc_row(r, hh);
-      O[(win * TOK + qi) * ldo + h * HDP + l31] = (T)o[r];
+      O[(win * TOK + qi) * ldo + h * HDP + l31] = (T)(h * HDP + l31 == ones_col ? 1.f : o[r]);
     }
   }
 }
@@ -482,22 +482,24 @@ constexpr int WPG = 4;  // windows per backward wave
 }  // namespace
 
 extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
-                                    long nWin, int nh, int hd, float scale, int H, int W, int shift, void* stream) {
+                                    long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
+                                    void* stream) {
   KAIR_CHECK_ARG(qkv && table && O && lse, "window_attn_fwd: null pointer");
   KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_fwd: head_dim %d must be <= 32", hd);
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)),
                  "window_attn_fwd: grid %dx%d / shift %d", H, W, shift);
   KAIR_CHECK_ARG(ldo >= nh * HDP && ldo % 8 == 0, "window_attn_fwd: ldo");
+  KAIR_CHECK_ARG(ones_col < 0 || (ones_col < nh * HDP && ones_col % HDP >= hd), "window_attn_fwd: ones column must be a pad column");
   const long tasks = nWin * nh;
   const int nw = dtype == KAIR_BF16 ? NWAVES<true> : NWAVES<false>;
   const long nb = (tasks + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
     hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
-                       lse, nWin, nh, scale, H, W, shift);
+                       lse, nWin, nh, scale, H, W, shift, ones_col);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, table, (float*)O,
-                       ldo, lse, nWin, nh, scale, H, W, shift);
+                       ldo, lse, nWin, nh, scale, H, W, shift, ones_col);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

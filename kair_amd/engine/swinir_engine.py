@@ -352,18 +352,23 @@ class SwinIREngine:
         drop = P["drop"]
         s_attn = drop[bi, 0] if drop is not None else None
         s_mlp = drop[bi, 1] if drop is not None else None
-        H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps, win)
+        # LN1 / LN2 / fc1 / attention write 1.0 into their first pad column: the ones column the
+        # weight-gradient GEMMs use for the bias gradient (the packed weights are 0 there)
+        H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps, win,
+                        one_col=self.C)
         l = blk.qkv
         H.gemm_nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
                                                                qkv=(nh, 32, WS_TOK)), M, l.Np, Cp, cd)
         H.window_attn_fwd(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale, Hh, Ww,
-                          blk.shift)
+                          blk.shift, ones_col=self.C // nh)
         l = blk.proj
         H.gemm_nt(H.rows(S["O"]), H.rows(l.Wp), H.epilogue(S["mid"], win=win, bias=l.bp, resid=x, rowscale=s_attn,
                                                             rows_per_scale=HW), M, Cp, nh * 32, cd)
-        H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps)
+        H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps,
+                        one_col=self.C)
         l = blk.fc1
-        H.gemm_nt(H.rows(S["ln2"]), H.rows(l.Wp), H.epilogue(S["h"], bias=l.bp, act=H.ACT_GELU, pre=S["u"]), M, l.Np, Cp, cd)
+        H.gemm_nt(H.rows(S["ln2"]), H.rows(l.Wp), H.epilogue(S["h"], bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N),
+                  M, l.Np, Cp, cd)
         l = blk.fc2
         H.gemm_nt(H.rows(S["h"]), H.rows(l.Wp), H.epilogue(S["out"], bias=l.bp, resid=S["mid"], rowscale=s_mlp,
                                                             rows_per_scale=HW), M, Cp, self.Hdp, cd)
@@ -507,23 +512,26 @@ class SwinIREngine:
         Dc = P["Dc"]
         l = blk.fc2
         H.gemm_nt(H.rows(Dc), H.rows(l.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=1), M, self.Hdp, Cp, cd)
-        self._wgrad(P, H.rows(Dc), H.rows(S["h"], ones_col=l.K), M, Cp, self.Hdp, l.map, g(l.w), g(l.b), l.K)
+        self._wgrad(P, H.rows(Dc), H.rows(S["h"], ones_col=l.K, ones_in_data=True), M, Cp, self.Hdp, l.map, g(l.w),
+                    g(l.b), l.K)
         l = blk.fc1
         H.gemm_nt(H.rows(P["dU"]), H.rows(l.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
-        self._wgrad(P, H.rows(P["dU"]), H.rows(S["ln2"], ones_col=self.C), M, self.Hdp, Cp, l.map, g(l.w), g(l.b), self.C)
+        self._wgrad(P, H.rows(P["dU"]), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), M, self.Hdp, Cp, l.map,
+                    g(l.w), g(l.b), self.C)
         n = blk.n2
         H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, g(n.weight), g(n.bias), False,
                         P["ln_ws"], M, self.C, copy=H.copy_desc(Dc, rowscale=s_attn, rows_per_scale=HW, win=win))
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         l = blk.proj
         H.gemm_nt(H.rows(Dc), H.rows(l.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
-        self._wgrad(P, H.rows(Dc), H.rows(S["O"], ones_col=hd), M, Cp, nh * 32, l.map, g(l.w), g(l.b), hd)
+        self._wgrad(P, H.rows(Dc), H.rows(S["O"], ones_col=hd, ones_in_data=True), M, Cp, nh * 32, l.map, g(l.w),
+                    g(l.b), hd)
         H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], P["dqkv"], g(blk.table), False,
                           P["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
         l = blk.qkv
         H.gemm_nt(H.qkvblk(P["dqkv"], nh), H.rows(l.Wt), H.epilogue(P["dxn"]), M, Cp, l.Np, cd)
-        self._wgrad(P, H.qkvblk(P["dqkv"], nh), H.rows(S["ln1"], ones_col=self.C), M, l.Np, Cp, l.map, g(l.w), g(l.b),
-                    self.C)
+        self._wgrad(P, H.qkvblk(P["dqkv"], nh), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), M, l.Np, Cp, l.map,
+                    g(l.w), g(l.b), self.C)
         n = blk.n1
         cp = None
         if copy_prev:

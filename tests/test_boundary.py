@@ -51,7 +51,7 @@ def test_error_channel_without_gpu():
     """Argument validation runs on the host: a bad call returns an error code + message, no launch."""
     from kair_amd import _hip
     L = _hip.lib()
-    rc = L.kair_layernorm_fwd(None, 0, None, 0, 0, None, None, None, None, 0, 0, 1e-5, 0, 0, 0, 0, None)
+    rc = L.kair_layernorm_fwd(None, 0, None, 0, 0, None, None, None, None, 0, 0, 1e-5, 0, 0, 0, 0, -1, None)
     assert rc != 0
     assert b"layernorm_fwd" in L.kair_last_error()
 

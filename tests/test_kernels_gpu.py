@@ -127,9 +127,11 @@ def test_conv_pixelshuffle_and_nchw(compute):
     assert rel_err(img, ref3) < TOL[compute][0]
 
 
+@pytest.mark.parametrize("in_data", [False, True])
 @pytest.mark.parametrize("compute", [H.F32, H.BF16])
-@pytest.mark.parametrize("M,N,K", [(5000, 576, 192), (4096, 64, 64), (777, 192, 384)])
-def test_gemm_tn_wgrad(compute, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(5000, 576, 192), (4096, 64, 64), (777, 192, 384), (2000, 384, 200)])
+def test_gemm_tn_wgrad(compute, M, N, K, in_data):
+    """in_data=True: the ones column is stored by the producer (bf16: the LDS-DMA ring kernel)."""
     g = torch.Generator().manual_seed(11)
     dy = torch.randn(M, N, generator=g)
     x = torch.randn(M, K, generator=g)
@@ -139,7 +141,9 @@ def test_gemm_tn_wgrad(compute, M, N, K):
     ref = dy.double().T @ xr.double()
     S = H.wgrad_splits(M, N, K)
     ws = torch.empty(S, N, K, device=dev)
-    H.gemm_tn(H.rows(dy.to(dev, DT[compute])), H.rows(x.to(dev, DT[compute]), ones_col=ones), ws, S, M, N, K, compute)
+    xin = xr if in_data else x
+    H.gemm_tn(H.rows(dy.to(dev, DT[compute])), H.rows(xin.to(dev, DT[compute]), ones_col=ones, ones_in_data=in_data), ws,
+              S, M, N, K, compute)
     torch.cuda.synchronize()
     got = ws.sum(0).cpu()
     assert rel_err(got, ref) < TOL[compute][0]
@@ -194,9 +198,11 @@ def test_layernorm(dtype, win):
     xd = x.to(dev)
     yo = torch.empty(M, ld, device=dev, dtype=DT[dtype])
     mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
-    H.layernorm_fwd(xd, ld, yo, ld, gamma.to(dev), beta.to(dev), mean, rstd, M, C, 1e-5, win)
+    H.layernorm_fwd(xd, ld, yo, ld, gamma.to(dev), beta.to(dev), mean, rstd, M, C, 1e-5, win, one_col=C + 1)
     torch.cuda.synchronize()
     assert rel_err(yo[:, :C].float(), y.detach()[perm]) < TOL[dtype][0]
+    assert (yo[:, C + 1] == 1).all().item()
+    yo[:, C + 1] = 0
     assert yo[:, C:].abs().max().item() == 0
     dy = torch.zeros(M, ld)
     dy[:, :C] = gy[perm]
@@ -379,3 +385,21 @@ def test_row_copy(dtype):
     want = (src[:, :C] * sc.repeat_interleave(256)[:, None])[win_perm(2, 16, 16, 8, 4)]
     torch.cuda.synchronize()
     assert rel_err(out.float(), want) < TOL[dtype][0] / 4
+
+
+def test_gemm_tn_ring_qkvblk_A():
+    """Weight gradient of the q/k/v projection: A read from the head-blocked layout (ring kernel)."""
+    nWin, nh, tok, hdp = 40, 6, 64, 32
+    M, N, K = nWin * tok, 3 * nh * hdp, 192
+    g = torch.Generator().manual_seed(23)
+    blk = torch.randn(3, nWin, nh, tok, hdp, generator=g).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    x[:, 180] = 1.0
+    S = H.wgrad_splits(M, N, K)
+    ws = torch.empty(S, N, K, device=dev)
+    H.gemm_tn(H.qkvblk(blk.to(dev).reshape(-1), nh), H.rows(x.to(dev), ones_col=180, ones_in_data=True), ws, S, M, N, K,
+              H.BF16)
+    a = blk.double().permute(1, 3, 0, 2, 4).reshape(M, N)
+    ref = a.T @ x.double()
+    torch.cuda.synchronize()
+    assert rel_err(ws.sum(0).cpu(), ref) < 1e-2

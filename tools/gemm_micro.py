@@ -67,6 +67,15 @@ def cases():
     o3 = torch.empty(M, 192, device=dev)
     out["f32A_resid_192"] = (lambda: H.gemm_nt(H.rows(D), H.rows(W3), H.epilogue(o3, resid=R), M, 192, 192, H.BF16),
                              None, 2.0 * M * 192 * 192, nbytes(D, W3, R, o3))
+    Db = torch.randn(M, 192, device=dev).to(bf)
+    o4 = torch.empty(M, 384, device=dev, dtype=bf)
+    out["fc2_dgrad_gate"] = (lambda: H.gemm_nt(H.rows(Db), H.rows(W), H.epilogue(o4, gate=gate, gate_kind=1),
+                                               M, 384, 192, H.BF16), None, 2.0 * M * 384 * 192, nbytes(Db, W, gate, o4))
+    sc = torch.rand(B_, device=dev) + 0.5
+    o5 = torch.empty(M, 192, device=dev)
+    out["proj_fwd_full"] = (lambda: H.gemm_nt(H.rows(Db), H.rows(W3), H.epilogue(o5, win=(HH, WW, 8, 4), resid=R, rowscale=sc,
+                                                                                rows_per_scale=HH * WW), M, 192, 192, H.BF16),
+                            None, 2.0 * M * 192 * 192, nbytes(Db, W3, R, o5))
     x = torch.randn(M, CP, device=dev)
     Wc = torch.randn(CP, 9 * CP, device=dev).to(bf) * 0.02
     oc = torch.empty(M, CP, device=dev)
@@ -75,13 +84,14 @@ def cases():
     out["conv3x3_fwd"] = (lambda: H.gemm_nt(H.im2col(x, HH, WW, CP), H.rows(Wc), H.epilogue(oc), M, CP, 9 * CP, H.BF16),
                           lambda: torch.nn.functional.conv2d(xb, wb, padding=1), 2.0 * M * CP * 9 * CP,
                           nbytes(x, Wc, oc))
-    for name, N, K in [("fc1_wgrad", 384, 192), ("qkv_wgrad", 576, 192)]:
+    for name, N, K in [("fc1_wgrad", 384, 192), ("qkv_wgrad", 576, 192), ("proj_wgrad", 192, 192), ("fc2_wgrad", 192, 384)]:
         G = torch.randn(M, N, device=dev).to(bf)
         X = torch.randn(M, K, device=dev).to(bf)
+        X[:, K - 1] = 1.0
         S = H.wgrad_splits(M, N, K)
         ws = torch.empty(S, N, K, device=dev)
         out[name + f"(S={S})"] = (lambda G=G, X=X, ws=ws, S=S, N=N, K=K:
-                                  H.gemm_tn(H.rows(G), H.rows(X, ones_col=K - 1), ws, S, M, N, K, H.BF16),
+                                  H.gemm_tn(H.rows(G), H.rows(X, ones_col=K - 1, ones_in_data=True), ws, S, M, N, K, H.BF16),
                                   lambda G=G, X=X: torch.matmul(G.T, X), 2.0 * M * N * K, nbytes(G, X, ws))
     return out
 

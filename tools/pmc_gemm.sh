@@ -1,10 +1,12 @@
+#!/bin/bash
+# PMC counters for one gemm_micro case (run via gpurun from the repo root): tools/pmc_gemm.sh <case> [outdir]
 set -e
+C=${1:-qkv_fwd}; O=${2:-gpurun_out/pmc}
+R=$(pwd); mkdir -p $R/$O
 cd /tmp && export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-C=proj_fwd
-for S in 0 1; do
-  KAIR_GEMM_STREAM=$S timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $R/gpurun_out/pmc$S -o a -- python3 $R/tools/gemm_micro.py $C --no-torch --reps 5 > $R/gpurun_out/pmc${S}a.log 2>&1
-  KAIR_GEMM_STREAM=$S timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d $R/gpurun_out/pmc$S -o b -- python3 $R/tools/gemm_micro.py $C --no-torch --reps 5 > $R/gpurun_out/pmc${S}b.log 2>&1
-  KAIR_GEMM_STREAM=$S timeout -k 10 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc$S -o c -- python3 $R/tools/gemm_micro.py $C --no-torch --reps 5 > $R/gpurun_out/pmc${S}c.log 2>&1
-  KAIR_GEMM_STREAM=$S timeout -k 10 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --output-format csv -d $R/gpurun_out/pmc$S -o d -- python3 $R/tools/gemm_micro.py $C --no-torch --reps 5 > $R/gpurun_out/pmc${S}d.log 2>&1
-done
+run() { timeout -k 10 120 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $R/$O -o p$N -- python3 $R/tools/gemm_micro.py $C --no-torch --reps 5 > $R/$O/log$N.txt 2>&1; N=$((N+1)); }
+N=0
+run SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU
+run SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE
+run FETCH_SIZE
+run WRITE_SIZE TCC_HIT_sum TCC_MISS_sum
