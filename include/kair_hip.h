@@ -45,12 +45,15 @@ typedef struct {
   int mode;            /* kair_load_mode                                                     */
   long ld;             /* ROWS: row stride in elements                                       */
   int win_H, win_W, win_ws, win_shift; /* ROWS: Swin window->token row map (ws==0: identity)  */
-  int im_H, im_W, im_C, im_flip;       /* IM2COL3 (im_flip: tap (dy,dx) -> (-dy,-dx), dgrad)  */
+  int im_H, im_W, im_C, im_flip;       /* IM2COL3 (im_flip: tap (dy,dx) -> (-dy,-dx), dgrad)
+                                          im_H x im_W is the CONV grid; ld = pixel stride (0: im_C) */
   int qkv_nh, qkv_hdp, qkv_tok;        /* QKVBLK                                              */
   const float* rowscale; int rows_per_scale; /* optional per-sample scale (DropPath)          */
   int ones_col;        /* >=0: this column reads as 1.0 (fused bias gradient), else -1       */
   int ones_in_data;    /* 1: the producer already stored 1.0 in column ones_col of every row
                           (lets DMA loaders skip the injection); 0: loaders inject it         */
+  int im_up;           /* IM2COL3: 2 = the source image is im_H/2 x im_W/2 and is read through a
+                          nearest x2 upsample (F.interpolate(scale 2, 'nearest')); 0/1 = none  */
 } kair_operand;
 
 typedef enum {
@@ -192,6 +195,31 @@ int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int 
                  int B, int C, int Hh, int Ww, float* ws, void* stream);
 /* y[i] += a * x[i] over n fp32 elements (residual-gradient merges). */
 int kair_axpy(float* y, const float* x, float a, long n, void* stream);
+/* BatchNorm2d over NHWC rows z [M, C] fp32 (basicblock.py:69: momentum 0.9, eps 1e-4), fused act
+ * (0 none, 1 ReLU, 2 LeakyReLU(slope)).  training: batch statistics (two-pass, deterministic) ->
+ * mean/rstd [C] and the running-stat update (unbiased running_var); else running statistics.
+ * ws: kair_bn_ws(C) floats.  (network_dncnn.py:40-71 BN layers) */
+long kair_bn_ws(int C);
+int kair_bn_fwd(const float* z, long ldz, void* out, int out_dtype, long ldo, long M, int C, const float* gamma,
+                const float* beta, float* running_mean, float* running_var, float momentum, float eps, int training,
+                float* mean, float* rstd, int act, float slope, float* ws, void* stream);
+/* dz = BN'(act'(a) * da) with the saved mean/rstd; dgamma/dbeta (+)= column sums. */
+int kair_bn_bwd(const float* z, long ldz, const void* a, int a_dtype, long lda, const float* da, long ldda, void* dz,
+                int dz_dtype, long lddz, long M, int C, const float* gamma, const float* mean, const float* rstd,
+                int act, float slope, float* dgamma, float* dbeta, int accumulate, float* ws, void* stream);
+
+/* y = a * x + b * y (fp32, n elements) */
+int kair_axpby(float* y, const float* x, float a, float b, long n, void* stream);
+/* y[m][c] = a * x[m][c] + b * y[m][c] for c < C over strided fp32 rows */
+int kair_axpby_rows(float* y, long ldy, const float* x, long ldx, long M, int C, float a, float b, void* stream);
+/* out[m][c] (dtype) = G[m][c] * act'(X[m][c]) for c < C  (act' from the POST-activation value X:
+ * kind 1 ReLU, 2 LeakyReLU(slope); 0 identity), optionally * scale.  Row strides ldg / ldx / ldo. */
+int kair_act_grad_cast(const float* G, long ldg, const void* X, int x_dtype, long ldx, void* out, int out_dtype,
+                       long ldo, long M, int C, int kind, float slope, float scale, void* stream);
+/* 2x2 sum-pool (adjoint of nearest x2 upsample): dst[b][y][x][c] (+)= sum_{i,j<2} src[b][2y+i][2x+j][c].
+ * src fp32 [B, 2H, 2W] rows of stride lds; dst fp32 [B, H, W] rows of stride ldd. */
+int kair_sumpool2x(const float* src, long lds, float* dst, long ldd, int B, int H, int W, int C, int accumulate,
+                   void* stream);
 /* Fused Adam (torch.optim.Adam maths, model_plain.py:210-222,302) + EMA (model_base.py:247-252)
  * over flat fp32 buffers.  lr_t is a DEVICE array {lr / (1 - beta1^t), sqrt(1 - beta2^t)} written by
  * the host before each (graph-replayed) step; ema may be NULL (E_decay = 0). */

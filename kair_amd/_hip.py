@@ -24,7 +24,8 @@ class Operand(ctypes.Structure):
                 ("win_H", c_int), ("win_W", c_int), ("win_ws", c_int), ("win_shift", c_int),
                 ("im_H", c_int), ("im_W", c_int), ("im_C", c_int), ("im_flip", c_int),
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
-                ("rowscale", c_vp), ("rows_per_scale", c_int), ("ones_col", c_int), ("ones_in_data", c_int)]
+                ("rowscale", c_vp), ("rows_per_scale", c_int), ("ones_col", c_int), ("ones_in_data", c_int),
+                ("im_up", c_int)]
 
 
 class CopyDesc(ctypes.Structure):
@@ -92,11 +93,21 @@ _SIGS = {
     "kair_image_to_nhwc": [c_vp, c_vp, c_int, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
     "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "kair_axpy": [c_vp, c_vp, c_float, c_long, c_vp],
+    "kair_axpby": [c_vp, c_vp, c_float, c_float, c_long, c_vp],
+    "kair_bn_ws": [c_int],
+    "kair_bn_fwd": [c_vp, c_long, c_vp, c_int, c_long, c_long, c_int, c_vp, c_vp, c_vp, c_vp, c_float, c_float, c_int,
+                    c_vp, c_vp, c_int, c_float, c_vp, c_vp],
+    "kair_bn_bwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_long, c_vp, c_int, c_long, c_long, c_int, c_vp, c_vp, c_vp,
+                    c_int, c_float, c_vp, c_vp, c_int, c_vp, c_vp],
+    "kair_axpby_rows": [c_vp, c_long, c_vp, c_long, c_long, c_int, c_float, c_float, c_vp],
+    "kair_act_grad_cast": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_int, c_long, c_long, c_int, c_int, c_float, c_float,
+                           c_vp],
+    "kair_sumpool2x": [c_vp, c_long, c_vp, c_long, c_int, c_int, c_int, c_int, c_int, c_vp],
     "kair_adam_ema": [c_vp, c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
-_RESTYPE = {"kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
+_RESTYPE = {"kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
             "kair_pack_table_build": c_long}
 
 _lib = None
@@ -171,13 +182,17 @@ def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1, one
     return o
 
 
-def im2col(t, H, W, C, flip=False, ones_col=-1):
+def im2col(t, H, W, C, flip=False, ones_col=-1, ld=None, up=1):
+    """3x3 / pad 1 im2col view of an NHWC map: H x W is the CONV grid, ld the pixel stride
+    (default C), up=2 reads the source (H/2 x W/2) through a nearest x2 upsample."""
     o = Operand()
     o._keep = t
     o.ptr = ptr(t)
     o.dtype = dtype_code(t)
     o.mode = LD_IM2COL3
+    o.ld = ld if ld is not None else C
     o.im_H, o.im_W, o.im_C, o.im_flip = H, W, C, int(flip)
+    o.im_up = up
     o.ones_col = ones_col
     o.rows_per_scale = 1
     return o
@@ -335,3 +350,41 @@ def axpy(y, x, a, n=None):
 def adam_ema(p, g, m, v, ema, n, lr_t, beta1, beta2, eps, wd, decay):
     check(lib().kair_adam_ema(ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), n, ptr(lr_t), beta1, beta2, eps, wd, decay,
                               stream_ptr()), "adam_ema")
+
+
+def axpby(y, x, a, b, n=None):
+    """y = a * x + b * y (fp32)."""
+    check(lib().kair_axpby(ptr(y), ptr(x), a, b, n if n is not None else y.numel(), stream_ptr()), "axpby")
+
+
+def act_grad_cast(G, ldg, X, ldx, out, ldo, M, C, kind, slope=0.0, scale=1.0):
+    """out = scale * G * act'(X) (act' read from the post-activation X; kind 0 none, 1 relu, 2 leaky)."""
+    check(lib().kair_act_grad_cast(ptr(G), ldg, ptr(X), dtype_code(X) if X is not None else F32, ldx, ptr(out),
+                                   dtype_code(out), ldo, M, C, kind, slope, scale, stream_ptr()), "act_grad_cast")
+
+
+def sumpool2x(src, lds, dst, ldd, B, H, W, C, accumulate=False):
+    """dst (+)= 2x2 sum-pool of src (the adjoint of nearest x2 upsampling)."""
+    check(lib().kair_sumpool2x(ptr(src), lds, ptr(dst), ldd, B, H, W, C, int(accumulate), stream_ptr()), "sumpool2x")
+
+
+def axpby_rows(y, ldy, x, ldx, M, C, a, b):
+    """y[:, :C] = a * x[:, :C] + b * y[:, :C] over strided fp32 rows."""
+    check(lib().kair_axpby_rows(ptr(y), ldy, ptr(x), ldx, M, C, a, b, stream_ptr()), "axpby_rows")
+
+
+def bn_ws(C):
+    return lib().kair_bn_ws(C)
+
+
+def bn_fwd(z, ldz, out, ldo, M, C, gamma, beta, running_mean, running_var, momentum, eps, training, mean, rstd, act,
+           slope, ws):
+    check(lib().kair_bn_fwd(ptr(z), ldz, ptr(out), dtype_code(out), ldo, M, C, ptr(gamma), ptr(beta), ptr(running_mean),
+                            ptr(running_var), momentum, eps, int(training), ptr(mean), ptr(rstd), act, slope, ptr(ws),
+                            stream_ptr()), "bn_fwd")
+
+
+def bn_bwd(z, ldz, a, lda, da, ldda, dz, lddz, M, C, gamma, mean, rstd, act, slope, dgamma, dbeta, accumulate, ws):
+    check(lib().kair_bn_bwd(ptr(z), ldz, ptr(a), dtype_code(a) if a is not None else F32, lda, ptr(da), ldda, ptr(dz),
+                            dtype_code(dz), lddz, M, C, ptr(gamma), ptr(mean), ptr(rstd), act, slope, ptr(dgamma), ptr(dbeta),
+                            int(accumulate), ptr(ws), stream_ptr()), "bn_bwd")

@@ -246,6 +246,54 @@ __global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, 
     y[i] += a * x[i];
 }
 
+__global__ void axpby_kernel(float* __restrict__ y, const float* __restrict__ x, float a, float b, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = a * x[i] + b * y[i];
+}
+
+__global__ void axpby_rows_kernel(float* __restrict__ y, long ldy, const float* __restrict__ x, long ldx, long M, int C,
+                                  float a, float b) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const long m = i / C;
+  const int c = (int)(i - m * C);
+  float* o = y + m * ldy + c;
+  *o = a * x[m * ldx + c] + b * *o;
+}
+
+template <typename TX, typename TO>
+__global__ void act_grad_cast_kernel(const float* __restrict__ G, long ldg, const TX* __restrict__ X, long ldx,
+                                     TO* __restrict__ out, long ldo, long M, int C, int kind, float slope, float scale) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const long m = i / C;
+  const int c = (int)(i - m * C);
+  float g = G[m * ldg + c] * scale;
+  if (kind) {
+    const float xv = (float)X[m * ldx + c];
+    g = xv > 0.f ? g : (kind == 2 ? g * slope : 0.f);
+  }
+  out[m * ldo + c] = (TO)g;
+}
+
+__global__ void sumpool2x_kernel(const float* __restrict__ src, long lds, float* __restrict__ dst, long ldd, int B, int H,
+                                 int W, int C, int acc) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * H * W * C;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  const long pix = i / C;
+  const int x = (int)(pix % W);
+  const long by = pix / W;
+  const int y = (int)(by % H);
+  const long b = by / H;
+  const long r0 = (b * 2 * H + 2 * y) * (2L * W) + 2 * x;
+  const float s = src[r0 * lds + c] + src[(r0 + 1) * lds + c] + src[(r0 + 2L * W) * lds + c] +
+                  src[(r0 + 2L * W + 1) * lds + c];
+  float* o = dst + pix * ldd + c;
+  *o = acc ? *o + s : s;
+}
+
 inline unsigned nblk(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
@@ -404,6 +452,59 @@ extern "C" int kair_adam_ema(float* p, const float* g, float* m, float* v, float
   if (nb > 8192) nb = 8192;
   hipLaunchKernelGGL(adam_ema_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n, lr_t,
                      beta1, beta2, eps, weight_decay, ema_decay);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_axpby(float* y, const float* x, float a, float b, long n, void* stream) {
+  KAIR_CHECK_ARG(y && x && n >= 0, "axpby: bad args");
+  long nb = (n + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(axpby_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, y, x, a, b, n);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_axpby_rows(float* y, long ldy, const float* x, long ldx, long M, int C, float a, float b,
+                                void* stream) {
+  KAIR_CHECK_ARG(y && x && M > 0 && C > 0 && ldy >= C && ldx >= C, "axpby_rows: bad args");
+  hipLaunchKernelGGL(axpby_rows_kernel, dim3(nblk(M * C, 256)), dim3(256), 0, (hipStream_t)stream, y, ldy, x, ldx, M, C, a, b);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_act_grad_cast(const float* G, long ldg, const void* X, int x_dtype, long ldx, void* out, int out_dtype,
+                                  long ldo, long M, int C, int kind, float slope, float scale, void* stream) {
+  KAIR_CHECK_ARG(G && out && M > 0 && C > 0 && (kind == 0 || X), "act_grad_cast: bad args");
+  const long n = M * C;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(nblk(n, 256)), b(256);
+  if (x_dtype == KAIR_BF16) {
+    if (out_dtype == KAIR_BF16)
+      hipLaunchKernelGGL((act_grad_cast_kernel<bf16, bf16>), g, b, 0, s, G, ldg, (const bf16*)X, ldx, (bf16*)out, ldo, M, C,
+                         kind, slope, scale);
+    else
+      hipLaunchKernelGGL((act_grad_cast_kernel<bf16, float>), g, b, 0, s, G, ldg, (const bf16*)X, ldx, (float*)out, ldo, M,
+                         C, kind, slope, scale);
+  } else {
+    if (out_dtype == KAIR_BF16)
+      hipLaunchKernelGGL((act_grad_cast_kernel<float, bf16>), g, b, 0, s, G, ldg, (const float*)X, ldx, (bf16*)out, ldo, M,
+                         C, kind, slope, scale);
+    else
+      hipLaunchKernelGGL((act_grad_cast_kernel<float, float>), g, b, 0, s, G, ldg, (const float*)X, ldx, (float*)out, ldo,
+                         M, C, kind, slope, scale);
+  }
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_sumpool2x(const float* src, long lds, float* dst, long ldd, int B, int H, int W, int C, int accumulate,
+                              void* stream) {
+  KAIR_CHECK_ARG(src && dst && B > 0 && H > 0 && W > 0 && C > 0 && lds >= C && ldd >= C, "sumpool2x: bad args");
+  const long n = (long)B * H * W * C;
+  hipLaunchKernelGGL(sumpool2x_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, src, lds, dst, ldd, B, H, W,
+                     C, accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

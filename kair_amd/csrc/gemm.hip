@@ -36,6 +36,7 @@ struct Op {
   long ld;
   WinMap win;
   int imH, imW, imC, flip;
+  int up_sh;   // IM2COL: log2 of the nearest-upsample factor (source image imH>>up_sh x imW>>up_sh)
   int nh, hdp, tok;
   const float* rowscale;
   int rps;
@@ -50,6 +51,8 @@ Op make_op(const kair_operand& o, long M) {
   op.ptr = o.ptr; op.ld = o.ld;
   op.win = make_winmap(o.win_H, o.win_W, o.win_ws, o.win_shift);
   op.imH = o.im_H; op.imW = o.im_W; op.imC = o.im_C; op.flip = o.im_flip;
+  op.up_sh = o.im_up == 2 ? 1 : 0;
+  if (o.mode == KAIR_LD_IM2COL3 && op.ld == 0) op.ld = o.im_C;
   op.nh = o.qkv_nh; op.hdp = o.qkv_hdp; op.tok = o.qkv_tok;
   op.rowscale = o.rowscale; op.rps = o.rows_per_scale > 0 ? o.rows_per_scale : 1;
   op.ones_col = o.ones_col;
@@ -106,7 +109,7 @@ KAIR_DEV RowState row_state(const Op& op, long m) {
     const int p = (int)m - b * hw;
     r.y = fdiv(p, op.d_imW);
     r.x = p - r.y * op.imW;
-    r.base = (long)p + (long)b * hw;
+    r.base = (long)b * (hw >> (2 * op.up_sh));   // first pixel of image b in the SOURCE image
   } else {
     const int win = fdiv((int)m, op.d_tok);
     const int t = (int)m - win * op.tok;
@@ -152,7 +155,7 @@ KAIR_DEV void issue_chunk(const Op& op, const RowState& r, int k, int K, Raw<T>&
     if (op.flip) { dy = -dy; dx = -dx; }
     const int y = r.y + dy, x = r.x + dx;
     ok = ok && y >= 0 && y < op.imH && x >= 0 && x < op.imW;
-    off = (r.base + (long)dy * op.imW + dx) * op.imC + c;
+    off = (r.base + (long)(y >> op.up_sh) * (op.imW >> op.up_sh) + (x >> op.up_sh)) * op.ld + c;
   } else {
     const int pw = op.d_pw.d;
     const int part = fdiv(k, op.d_pw);
@@ -1153,7 +1156,12 @@ static int check_operand(const kair_operand* o, const char* what) {
   const int esz = o->dtype == KAIR_BF16 ? 2 : 4;
   KAIR_CHECK_ARG(((uintptr_t)o->ptr % 16) == 0, "%s: pointer not 16-byte aligned", what);
   if (o->mode == KAIR_LD_ROWS) KAIR_CHECK_ARG((o->ld * esz) % 16 == 0, "%s: row stride not 16-byte aligned", what);
-  if (o->mode == KAIR_LD_IM2COL3) KAIR_CHECK_ARG(o->im_C % 8 == 0 && o->im_H > 0 && o->im_W > 0, "%s: im2col geometry", what);
+  if (o->mode == KAIR_LD_IM2COL3) {
+    KAIR_CHECK_ARG(o->im_C % 8 == 0 && o->im_H > 0 && o->im_W > 0, "%s: im2col geometry", what);
+    KAIR_CHECK_ARG(o->ld == 0 || (o->ld >= o->im_C && (o->ld * esz) % 16 == 0), "%s: im2col pixel stride", what);
+    KAIR_CHECK_ARG(o->im_up == 0 || o->im_up == 1 || (o->im_up == 2 && o->im_H % 2 == 0 && o->im_W % 2 == 0),
+                   "%s: im2col upsample factor", what);
+  }
   if (o->mode == KAIR_LD_QKVBLK) KAIR_CHECK_ARG(o->qkv_hdp % 8 == 0 && o->qkv_tok > 0 && o->qkv_nh > 0, "%s: qkv geometry", what);
   if (o->win_ws > 0)
     KAIR_CHECK_ARG(o->win_H % o->win_ws == 0 && o->win_W % o->win_ws == 0, "%s: window map geometry", what);

@@ -1,0 +1,289 @@
+"""RRDBNet (ESRGAN generator) step program for MI355X.
+
+Reference: /root/reference/models/network_rrdbnet.py:35-119 (ResidualDenseBlock_5C, RRDB,
+RRDBNet.forward).  SURVEY §8 row a15.
+
+Layout: NHWC feature rows.  Each residual dense block owns ONE compute-dtype
+buffer [M, nf + 4 gc] = [x | x1 | x2 | x3 | x4]: every conv reads a prefix of it through the
+im2col address map (pixel stride nf + 4 gc) and its epilogue (bias + LeakyReLU 0.2) writes its
+gc output channels straight into the next slice, so torch.cat never materialises.  conv5's
+epilogue applies the 0.2-scaled residual in fp32.  The nearest x2 upsamples of the tail are an
+im2col address mode (`im_up`); their adjoint is a 2x2 sum-pool.  Backward accumulates the input
+gradients of the five convs into one fp32 buffer of the same width (dgrad epilogues add in place),
+gates them with LeakyReLU' read from the saved post-activation slices, and reduces weight / bias
+gradients with the split-M TN GEMM + deterministic finalize / column sums.
+"""
+import weakref
+
+import torch
+
+from .. import _hip as H
+from .swinir_engine import _Conv
+
+
+class ConvEngineBase:
+    """Shared plumbing of the conv-net step programs: packed weights (one batched launch), plan
+    cache, conv forward / weight-gradient helpers."""
+
+    def __init__(self, net, compute_dtype):
+        self.net_ref = weakref.ref(net)
+        if compute_dtype not in ("bf16", "fp32"):
+            raise ValueError(compute_dtype)
+        self.cd = H.BF16 if compute_dtype == "bf16" else H.F32
+        self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
+        self.plans = {}
+        self._packed_version = None
+        self._pack_table = None
+        self.blocks = []          # no stochastic depth in the conv nets (FusedTrainer checks this)
+
+    def convs(self):
+        raise NotImplementedError
+
+    def pack(self, force=False):
+        net = self.net_ref()
+        ver = None if force else tuple(p._version for p in net.parameters())
+        if ver is not None and ver == self._packed_version:
+            return
+        ptrs = tuple(p.data_ptr() for p in net.parameters())
+        if self._pack_table is None or self._pack_table[0] != ptrs:
+            jobs = [j for c in self.convs() for j in c.pack_jobs()]
+            self._pack_table = (ptrs, H.PackTable(jobs))
+        self._pack_table[1].run()
+        self._packed_version = ver
+
+    def _e(self, *shape, dt=torch.float32):
+        return torch.empty(*shape, device=self.device, dtype=dt)
+
+    def conv_wgrad(self, P, c, dz, ld_dz, src_op, M, grads):
+        """weight + bias gradient of conv c: dz [M, Cop] rows (compute dtype), src_op its im2col input."""
+        K = 9 * c.Cip
+        S = H.wgrad_splits(M, c.Cop, K)
+        H.gemm_tn(H.rows(dz, ld=ld_dz), src_op, P["wg_ws"], S, M, c.Cop, K, self.cd)
+        H.wgrad_finalize(P["wg_ws"], S, c.map, grads[c.w])
+        H.colsum(H.rows(dz, ld=ld_dz), M, c.Cop, c.mapb, grads[c.b], P["colsum_ws"])
+
+    def wgrad_ws_size(self, shapes):
+        return max(H.wgrad_splits(m, n, k) * n * k for m, n, k in shapes)
+
+
+class RRDBNetEngine(ConvEngineBase):
+    def __init__(self, net, compute_dtype="bf16"):
+        super().__init__(net, compute_dtype)
+        self.device = net.conv_first.weight.device
+        self.sf = net.sf
+        if self.sf not in (2, 4):
+            raise NotImplementedError("kair_amd RRDBNet: sf 2 or 4")
+        self.nf = net.conv_first.out_channels
+        self.gc = net.RRDB_trunk[0].RDB1.conv1.out_channels
+        if self.nf % 8 or self.gc % 8:
+            raise NotImplementedError("kair_amd RRDBNet: nf, gc must be multiples of 8")
+        self.in_ch, self.out_ch = net.conv_first.in_channels, net.conv_last.out_channels
+        self.Cin_p = 8
+        self.CD = self.nf + 4 * self.gc
+        nf, gc = self.nf, self.gc
+        self.conv_first = _Conv(self, net.conv_first, nf, self.Cin_p, need_dgrad=False)
+        self.rdbs = []
+        for rr in net.RRDB_trunk:
+            for rdb in (rr.RDB1, rr.RDB2, rr.RDB3):
+                cs = [rdb.conv1, rdb.conv2, rdb.conv3, rdb.conv4, rdb.conv5]
+                self.rdbs.append([_Conv(self, m, m.out_channels, m.in_channels) for m in cs])
+        self.nrr = len(net.RRDB_trunk)
+        self.trunk = _Conv(self, net.trunk_conv, nf, nf)
+        self.up = [_Conv(self, net.upconv1, nf, nf)] + ([_Conv(self, net.upconv2, nf, nf)] if self.sf == 4 else [])
+        self.hr = _Conv(self, net.HRconv, nf, nf)
+        self.last = _Conv(self, net.conv_last, 16, nf)
+
+    def convs(self):
+        return [self.conv_first] + [c for r in self.rdbs for c in r] + [self.trunk] + self.up + [self.hr, self.last]
+
+    # ------------------------------------------------------------------------------------
+    def plan(self, B, Hh, Ww):
+        key = (B, Hh, Ww)
+        if key in self.plans:
+            return self.plans[key]
+        T, e = self.tdt, self._e
+        nf, gc, CD = self.nf, self.gc, self.CD
+        M = B * Hh * Ww
+        nr = len(self.rdbs)
+        P = {"B": B, "H": Hh, "W": Ww, "M": M}
+        P["xin"] = e(M, self.Cin_p, dt=T)
+        P["fea"] = e(M, nf)
+        P["dense"] = [e(M, CD, dt=T) for _ in range(nr + 1)]    # +1: slice 0 = trunk_conv input
+        P["y"] = [e(M, nf) for _ in range(nr)]
+        P["fea2"], P["fea2b"] = e(M, nf), e(M, nf, dt=T)
+        levels, h, w = [], Hh, Ww
+        for _ in self.up:
+            h, w = 2 * h, 2 * w
+            levels.append((h, w))
+        P["levels"] = levels
+        P["upa"] = [e(B * hh * ww, nf, dt=T) for hh, ww in levels]
+        HL, WL = levels[-1]
+        ML = B * HL * WL
+        P["ML"] = ML
+        P["hr"] = e(ML, nf, dt=T)
+        P["E"] = e(B, self.out_ch, HL, WL)
+        P["alpha"] = torch.full((1,), 0.2, device=self.device)
+        # backward
+        P["dE"] = e(ML, 16, dt=T)
+        P["G_hr"], P["dz_hr"], P["G_hi"] = e(ML, nf), e(ML, nf, dt=T), e(ML, nf)
+        P["G_lv"] = [e(B * hh * ww, nf) for hh, ww in levels]
+        P["Gt"], P["dzt"], P["G_R"] = e(M, nf), e(M, nf, dt=T), e(M, nf)
+        P["Gd"], P["dz5"], P["dzg"], P["gy"] = e(M, CD), e(M, nf, dt=T), e(M, gc, dt=T), e(M, nf)
+        P["loss"], P["loss_ws"] = e(1), e(1024)
+        P["colsum_ws"] = e(1024 * 256)
+        shapes = [(M, nf, 9 * self.Cin_p), (M, nf, 9 * nf), (ML, 16, 9 * nf), (ML, nf, 9 * nf)]
+        shapes += [(B * hh * ww, nf, 9 * nf) for hh, ww in levels]
+        shapes += [(M, c.Cop, 9 * c.Cip) for c in self.rdbs[0]]
+        P["wg_ws"] = e(self.wgrad_ws_size(shapes))
+        self.plans[key] = P
+        return P
+
+    # ------------------------------------------------------------------------------------
+    def forward(self, x, drop_scales=None):
+        B, _, Hh, Ww = x.shape
+        P = self.plan(B, Hh, Ww)
+        self.pack()
+        cd, nf, gc, CD = self.cd, self.nf, self.gc, self.CD
+        M = P["M"]
+        x = x.contiguous()
+        self.cur = P
+        H.image_to_nhwc(x, P["xin"], self.Cin_p, None, 1.0, B, self.in_ch, Hh, Ww)
+        c = self.conv_first
+        H.gemm_nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), H.rows(c.Wf), H.epilogue(P["fea"], bias=c.bp), M, nf,
+                  9 * self.Cin_p, cd)
+        dense = P["dense"]
+        H.row_copy(P["fea"], nf, M, nf, H.copy_desc(dense[0], ld=CD))
+        rr_in = P["fea"]
+        for r, cs in enumerate(self.rdbs):
+            x_in = rr_in if r % 3 == 0 else P["y"][r - 1]
+            D = dense[r]
+            for j in range(4):          # x_{j+1} = lrelu(conv_{j+1}(cat(x, x1..x_j)))
+                c, cin = cs[j], nf + j * gc
+                H.gemm_nt(H.im2col(D, Hh, Ww, cin, ld=CD), H.rows(c.Wf),
+                          H.epilogue(D[:, cin:cin + gc], ldo=CD, bias=c.bp, act=H.ACT_LEAKY, slope=0.2), M, gc, 9 * cin, cd)
+            c = cs[4]                    # y = x + 0.2 * conv5(cat(x, x1..x4))
+            y = P["y"][r]
+            H.gemm_nt(H.im2col(D, Hh, Ww, CD, ld=CD), H.rows(c.Wf),
+                      H.epilogue(y, bias=c.bp, resid=x_in, rowscale=P["alpha"], rows_per_scale=M), M, nf, 9 * CD, cd)
+            if r % 3 == 2:               # RRDB: out = 0.2 * RDB3 + x   (in place over y)
+                H.axpby(y, rr_in, 1.0, 0.2)
+                rr_in = y
+            H.row_copy(y, nf, M, nf, H.copy_desc(dense[r + 1], ld=CD))
+        c = self.trunk                   # fea = fea + trunk_conv(trunk)
+        H.gemm_nt(H.im2col(dense[-1], Hh, Ww, nf, ld=CD), H.rows(c.Wf), H.epilogue(P["fea2"], bias=c.bp, resid=P["fea"]),
+                  M, nf, 9 * nf, cd)
+        H.row_copy(P["fea2"], nf, M, nf, H.copy_desc(P["fea2b"]))
+        src = P["fea2b"]
+        for c, (hh, ww), dst in zip(self.up, P["levels"], P["upa"]):   # lrelu(upconv(nearest x2))
+            H.gemm_nt(H.im2col(src, hh, ww, nf, up=2), H.rows(c.Wf), H.epilogue(dst, bias=c.bp, act=H.ACT_LEAKY, slope=0.2),
+                      B * hh * ww, nf, 9 * nf, cd)
+            src = dst
+        HL, WL = P["levels"][-1]
+        ML = P["ML"]
+        c = self.hr
+        H.gemm_nt(H.im2col(src, HL, WL, nf), H.rows(c.Wf), H.epilogue(P["hr"], bias=c.bp, act=H.ACT_LEAKY, slope=0.2), ML,
+                  nf, 9 * nf, cd)
+        c = self.last
+        H.gemm_nt(H.im2col(P["hr"], HL, WL, nf), H.rows(c.Wf),
+                  H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(None, 1.0, self.out_ch, HL, WL)), ML, c.Cop,
+                  9 * nf, cd)
+        return P["E"]
+
+    # ------------------------------------------------------------------------------------
+    def backward_from_loss(self, H_img, grads, loss_weight=1.0):
+        P = self.cur
+        HL, WL = P["levels"][-1]
+        H.l1_loss(P["E"], H_img, P["loss"], P["dE"], 16, loss_weight, P["B"], self.out_ch, HL, WL, P["loss_ws"])
+        self.backward(grads, P)
+        return P["loss"]
+
+    def backward_from_grad(self, gE, grads):
+        P = self.cur
+        HL, WL = P["levels"][-1]
+        H.image_to_nhwc(gE.contiguous(), P["dE"], 16, None, 1.0, P["B"], self.out_ch, HL, WL)
+        self.backward(grads, P)
+
+    def backward(self, grads, P):
+        cd, nf, gc, CD = self.cd, self.nf, self.gc, self.CD
+        B, Hh, Ww, M, ML = P["B"], P["H"], P["W"], P["M"], P["ML"]
+        HL, WL = P["levels"][-1]
+        # conv_last
+        c = self.last
+        H.gemm_nt(H.im2col(P["dE"], HL, WL, 16, flip=True), H.rows(c.Wd), H.epilogue(P["G_hr"]), ML, nf, 9 * 16, cd)
+        self.conv_wgrad(P, c, P["dE"], 16, H.im2col(P["hr"], HL, WL, nf), ML, grads)
+        # HRconv (lrelu)
+        c = self.hr
+        H.act_grad_cast(P["G_hr"], nf, P["hr"], nf, P["dz_hr"], nf, ML, nf, 2, 0.2)
+        G = P["G_lv"][-1]
+        H.gemm_nt(H.im2col(P["dz_hr"], HL, WL, nf, flip=True), H.rows(c.Wd), H.epilogue(G), ML, nf, 9 * nf, cd)
+        self.conv_wgrad(P, c, P["dz_hr"], nf, H.im2col(P["upa"][-1], HL, WL, nf), ML, grads)
+        # upsampling convs, last to first: G = dL/d(post-lrelu output of up[i])
+        for i in range(len(self.up) - 1, -1, -1):
+            c, (hh, ww), a = self.up[i], P["levels"][i], P["upa"][i]
+            Mi = B * hh * ww
+            dz = P["dz_hr"][:Mi]
+            H.act_grad_cast(G, nf, a, nf, dz, nf, Mi, nf, 2, 0.2)
+            Ghi = P["G_hi"][:Mi]
+            H.gemm_nt(H.im2col(dz, hh, ww, nf, flip=True), H.rows(c.Wd), H.epilogue(Ghi), Mi, nf, 9 * nf, cd)
+            src = P["upa"][i - 1] if i > 0 else P["fea2b"]
+            self.conv_wgrad(P, c, dz, nf, H.im2col(src, hh, ww, nf, up=2), Mi, grads)
+            Gn = P["G_lv"][i - 1] if i > 0 else P["Gt"]
+            H.sumpool2x(Ghi, nf, Gn, nf, B, hh // 2, ww // 2, nf)
+            G = Gn
+        # fea2 = fea + trunk_conv(R):  Gt = dL/d fea2
+        c = self.trunk
+        H.act_grad_cast(P["Gt"], nf, None, 0, P["dzt"], nf, M, nf, 0)
+        H.gemm_nt(H.im2col(P["dzt"], Hh, Ww, nf, flip=True), H.rows(c.Wd), H.epilogue(P["G_R"]), M, nf, 9 * nf, cd)
+        self.conv_wgrad(P, c, P["dzt"], nf, H.im2col(P["dense"][-1], Hh, Ww, nf, ld=CD), M, grads)
+        # RRDB trunk, last to first.  G_R = dL/d(RRDB output)
+        gy = P["gy"]
+        for i in range(self.nrr - 1, -1, -1):
+            H.act_grad_cast(P["G_R"], nf, None, 0, gy, nf, M, nf, 0, 0.0, 0.2)     # dL/d RDB3 output
+            for r in (3 * i + 2, 3 * i + 1, 3 * i):
+                self._rdb_bwd(P, r, grads)                                          # gy -> dL/d RDB input
+            H.axpby(P["G_R"], gy, 1.0, 1.0)                                          # + skip
+        # conv_first: dL/d fea = Gt (long skip) + G_R (trunk)
+        H.axpby(P["G_R"], P["Gt"], 1.0, 1.0)
+        H.act_grad_cast(P["G_R"], nf, None, 0, P["dzt"], nf, M, nf, 0)
+        c = self.conv_first
+        self.conv_wgrad(P, c, P["dzt"], nf, H.im2col(P["xin"], Hh, Ww, self.Cin_p), M, grads)
+
+    def _rdb_bwd(self, P, r, grads):
+        """gy = dL/dy (y = x + 0.2 conv5(...)) -> replaced by dL/dx."""
+        cd, nf, gc, CD = self.cd, self.nf, self.gc, self.CD
+        Hh, Ww, M = P["H"], P["W"], P["M"]
+        cs, D, Gd, gy = self.rdbs[r], P["dense"][r], P["Gd"], P["gy"]
+        c = cs[4]
+        H.act_grad_cast(gy, nf, None, 0, P["dz5"], nf, M, nf, 0, 0.0, 0.2)
+        H.gemm_nt(H.im2col(P["dz5"], Hh, Ww, nf, flip=True), H.rows(c.Wd), H.epilogue(Gd), M, CD, 9 * nf, cd)
+        self.conv_wgrad(P, c, P["dz5"], nf, H.im2col(D, Hh, Ww, CD, ld=CD), M, grads)
+        for j in range(3, -1, -1):
+            c, cin = cs[j], nf + j * gc
+            dz = P["dzg"]
+            H.act_grad_cast(Gd[:, cin:], CD, D[:, cin:], CD, dz, gc, M, gc, 2, 0.2)
+            H.gemm_nt(H.im2col(dz, Hh, Ww, gc, flip=True), H.rows(c.Wd), H.epilogue(Gd, ldo=CD, resid=Gd, ldr=CD), M, cin,
+                      9 * gc, cd)
+            self.conv_wgrad(P, c, dz, gc, H.im2col(D, Hh, Ww, cin, ld=CD), M, grads)
+        H.axpby_rows(gy, nf, Gd, CD, M, nf, 1.0, 1.0)
+
+
+class ConvNetFunction(torch.autograd.Function):
+    """A whole conv network (RRDBNet / DnCNN / ...) as one autograd node on its step program."""
+
+    @staticmethod
+    def forward(ctx, engine, x, *params):
+        E = engine.forward(x.float().contiguous())
+        ctx.engine, ctx.params, ctx.plan = engine, params, engine.cur
+        return E.clone()
+
+    @staticmethod
+    def backward(ctx, gE):
+        eng = ctx.engine
+        flat = torch.empty(sum(p.numel() for p in ctx.params), device=gE.device)
+        grads, off = {}, 0
+        for p in ctx.params:
+            grads[p] = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        eng.cur = ctx.plan
+        eng.backward_from_grad(gE.float(), grads)
+        return (None, None) + tuple(grads[p] for p in ctx.params)

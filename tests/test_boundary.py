@@ -85,6 +85,10 @@ NETG_CFGS = {
     "swinir_light_x2": {"net_type": "swinir", "upscale": 2, "in_chans": 3, "img_size": 64, "window_size": 8,
                         "img_range": 1.0, "depths": [6] * 4, "embed_dim": 60, "num_heads": [6] * 4, "mlp_ratio": 2,
                         "upsampler": "pixelshuffledirect", "resi_connection": "1conv", "init_type": "default"},
+    "dncnn": {"net_type": "dncnn", "in_nc": 1, "out_nc": 1, "nc": 64, "nb": 17, "act_mode": "BR",
+              "init_type": "orthogonal", "init_bn_type": "uniform", "init_gain": 0.2},
+    "rrdbnet": {"net_type": "rrdbnet", "in_nc": 3, "out_nc": 3, "nf": 64, "nb": 23, "gc": 32, "scale": 4,
+                "init_type": "default"},
 }
 
 
