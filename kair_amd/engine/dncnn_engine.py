@@ -75,6 +75,7 @@ class DnCNNEngine(ConvEngineBase):
         P["dEf"] = torch.zeros(M, 16, device=self.device)
         P["dn"] = e(M, 16, dt=T)
         P["G"], P["dz"] = e(M, nc), e(M, nc, dt=T)
+        P["dzf"] = e(M, nc)   # fp32 gradient rows before the compute-dtype cast (bias gradients)
         P["bn_ws"] = e(H.bn_ws(nc))
         P["loss"], P["loss_ws"] = e(1), e(1024)
         P["colsum_ws"] = e(1024 * 256)
@@ -141,12 +142,16 @@ class DnCNNEngine(ConvEngineBase):
             c, bn, act, slope = self.layers[li]
             a, dz = P["a"][li], P["dz"]
             if bn is not None:
-                H.bn_bwd(P["z"][li], nc, a, nc, G, nc, dz, nc, M, nc, bn.weight, P["mean"][li], P["rstd"][li], act, slope,
+                dzf = dz if cd == H.F32 else P["dzf"]
+                H.bn_bwd(P["z"][li], nc, a, nc, G, nc, dzf, nc, M, nc, bn.weight, P["mean"][li], P["rstd"][li], act, slope,
                          grads[bn.weight], grads[bn.bias], False, P["bn_ws"])
+                if cd != H.F32:
+                    H.row_copy(dzf, nc, M, nc, H.copy_desc(dz))
+                bs = (dzf, nc)
             else:
-                H.act_grad_cast(G, nc, a, nc, dz, nc, M, nc, act, slope)
+                bs = self.gate_cast(P, G, nc, a, nc, dz, nc, M, nc, act, slope)
             if li > 0:
                 H.gemm_nt(H.im2col(dz, Hh, Ww, nc, flip=True), H.rows(c.Wd), H.epilogue(G), M, nc, 9 * nc, cd)
-                self.conv_wgrad(P, c, dz, nc, H.im2col(P["a"][li - 1], Hh, Ww, nc), M, grads)
+                self.conv_wgrad(P, c, dz, nc, H.im2col(P["a"][li - 1], Hh, Ww, nc), M, grads, *bs)
             else:
-                self.conv_wgrad(P, c, dz, nc, H.im2col(P["xin"], Hh, Ww, self.Cin_p), M, grads)
+                self.conv_wgrad(P, c, dz, nc, H.im2col(P["xin"], Hh, Ww, self.Cin_p), M, grads, *bs)

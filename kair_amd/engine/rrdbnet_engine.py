@@ -54,13 +54,27 @@ class ConvEngineBase:
     def _e(self, *shape, dt=torch.float32):
         return torch.empty(*shape, device=self.device, dtype=dt)
 
-    def conv_wgrad(self, P, c, dz, ld_dz, src_op, M, grads):
-        """weight + bias gradient of conv c: dz [M, Cop] rows (compute dtype), src_op its im2col input."""
+    def conv_wgrad(self, P, c, dz, ld_dz, src_op, M, grads, bias_src=None, ld_bias=None):
+        """weight + bias gradient of conv c: dz [M, Cop] rows (compute dtype), src_op its im2col input;
+        bias_src: the fp32 rows dz was cast from (bias gradient summed before rounding)."""
         K = 9 * c.Cip
         S = H.wgrad_splits(M, c.Cop, K)
         H.gemm_tn(H.rows(dz, ld=ld_dz), src_op, P["wg_ws"], S, M, c.Cop, K, self.cd)
         H.wgrad_finalize(P["wg_ws"], S, c.map, grads[c.w])
-        H.colsum(H.rows(dz, ld=ld_dz), M, c.Cop, c.mapb, grads[c.b], P["colsum_ws"])
+        if bias_src is None:
+            bias_src, ld_bias = dz, ld_dz
+        H.colsum(H.rows(bias_src, ld=ld_bias), M, c.Cop, c.mapb, grads[c.b], P["colsum_ws"])
+
+    def gate_cast(self, P, G, ldg, X, ldx, out, ldo, M, C, kind, slope=0.0, scale=1.0):
+        """out (compute dtype) = scale * G * act'(X).  Returns the fp32 rows to take the bias gradient
+        from: `out` itself in fp32 mode, else an fp32 scratch holding the values before rounding."""
+        if self.cd == H.F32:
+            H.act_grad_cast(G, ldg, X, ldx, out, ldo, M, C, kind, slope, scale)
+            return out, ldo
+        f = P["dzf"].view(-1)[:M * C].view(M, C)
+        H.act_grad_cast(G, ldg, X, ldx, f, C, M, C, kind, slope, scale)
+        H.row_copy(f, C, M, C, H.copy_desc(out, ld=ldo))
+        return f, C
 
     def wgrad_ws_size(self, shapes):
         return max(H.wgrad_splits(m, n, k) * n * k for m, n, k in shapes)
@@ -129,6 +143,7 @@ class RRDBNetEngine(ConvEngineBase):
         P["G_lv"] = [e(B * hh * ww, nf) for hh, ww in levels]
         P["Gt"], P["dzt"], P["G_R"] = e(M, nf), e(M, nf, dt=T), e(M, nf)
         P["Gd"], P["dz5"], P["dzg"], P["gy"] = e(M, CD), e(M, nf, dt=T), e(M, gc, dt=T), e(M, nf)
+        P["dzf"] = e(ML, nf)   # fp32 gradient rows before the compute-dtype cast (bias gradients)
         P["loss"], P["loss_ws"] = e(1), e(1024)
         P["colsum_ws"] = e(1024 * 256)
         shapes = [(M, nf, 9 * self.Cin_p), (M, nf, 9 * nf), (ML, 16, 9 * nf), (ML, nf, 9 * nf)]
@@ -213,20 +228,20 @@ class RRDBNetEngine(ConvEngineBase):
         self.conv_wgrad(P, c, P["dE"], 16, H.im2col(P["hr"], HL, WL, nf), ML, grads)
         # HRconv (lrelu)
         c = self.hr
-        H.act_grad_cast(P["G_hr"], nf, P["hr"], nf, P["dz_hr"], nf, ML, nf, 2, 0.2)
+        bs = self.gate_cast(P, P["G_hr"], nf, P["hr"], nf, P["dz_hr"], nf, ML, nf, 2, 0.2)
         G = P["G_lv"][-1]
         H.gemm_nt(H.im2col(P["dz_hr"], HL, WL, nf, flip=True), H.rows(c.Wd), H.epilogue(G), ML, nf, 9 * nf, cd)
-        self.conv_wgrad(P, c, P["dz_hr"], nf, H.im2col(P["upa"][-1], HL, WL, nf), ML, grads)
+        self.conv_wgrad(P, c, P["dz_hr"], nf, H.im2col(P["upa"][-1], HL, WL, nf), ML, grads, *bs)
         # upsampling convs, last to first: G = dL/d(post-lrelu output of up[i])
         for i in range(len(self.up) - 1, -1, -1):
             c, (hh, ww), a = self.up[i], P["levels"][i], P["upa"][i]
             Mi = B * hh * ww
             dz = P["dz_hr"][:Mi]
-            H.act_grad_cast(G, nf, a, nf, dz, nf, Mi, nf, 2, 0.2)
+            bs = self.gate_cast(P, G, nf, a, nf, dz, nf, Mi, nf, 2, 0.2)
             Ghi = P["G_hi"][:Mi]
             H.gemm_nt(H.im2col(dz, hh, ww, nf, flip=True), H.rows(c.Wd), H.epilogue(Ghi), Mi, nf, 9 * nf, cd)
             src = P["upa"][i - 1] if i > 0 else P["fea2b"]
-            self.conv_wgrad(P, c, dz, nf, H.im2col(src, hh, ww, nf, up=2), Mi, grads)
+            self.conv_wgrad(P, c, dz, nf, H.im2col(src, hh, ww, nf, up=2), Mi, grads, *bs)
             Gn = P["G_lv"][i - 1] if i > 0 else P["Gt"]
             H.sumpool2x(Ghi, nf, Gn, nf, B, hh // 2, ww // 2, nf)
             G = Gn
@@ -234,7 +249,7 @@ class RRDBNetEngine(ConvEngineBase):
         c = self.trunk
         H.act_grad_cast(P["Gt"], nf, None, 0, P["dzt"], nf, M, nf, 0)
         H.gemm_nt(H.im2col(P["dzt"], Hh, Ww, nf, flip=True), H.rows(c.Wd), H.epilogue(P["G_R"]), M, nf, 9 * nf, cd)
-        self.conv_wgrad(P, c, P["dzt"], nf, H.im2col(P["dense"][-1], Hh, Ww, nf, ld=CD), M, grads)
+        self.conv_wgrad(P, c, P["dzt"], nf, H.im2col(P["dense"][-1], Hh, Ww, nf, ld=CD), M, grads, P["Gt"], nf)
         # RRDB trunk, last to first.  G_R = dL/d(RRDB output)
         gy = P["gy"]
         for i in range(self.nrr - 1, -1, -1):
@@ -246,7 +261,7 @@ class RRDBNetEngine(ConvEngineBase):
         H.axpby(P["G_R"], P["Gt"], 1.0, 1.0)
         H.act_grad_cast(P["G_R"], nf, None, 0, P["dzt"], nf, M, nf, 0)
         c = self.conv_first
-        self.conv_wgrad(P, c, P["dzt"], nf, H.im2col(P["xin"], Hh, Ww, self.Cin_p), M, grads)
+        self.conv_wgrad(P, c, P["dzt"], nf, H.im2col(P["xin"], Hh, Ww, self.Cin_p), M, grads, P["G_R"], nf)
 
     def _rdb_bwd(self, P, r, grads):
         """gy = dL/dy (y = x + 0.2 conv5(...)) -> replaced by dL/dx."""
@@ -254,16 +269,16 @@ class RRDBNetEngine(ConvEngineBase):
         Hh, Ww, M = P["H"], P["W"], P["M"]
         cs, D, Gd, gy = self.rdbs[r], P["dense"][r], P["Gd"], P["gy"]
         c = cs[4]
-        H.act_grad_cast(gy, nf, None, 0, P["dz5"], nf, M, nf, 0, 0.0, 0.2)
+        bs = self.gate_cast(P, gy, nf, None, 0, P["dz5"], nf, M, nf, 0, 0.0, 0.2)
         H.gemm_nt(H.im2col(P["dz5"], Hh, Ww, nf, flip=True), H.rows(c.Wd), H.epilogue(Gd), M, CD, 9 * nf, cd)
-        self.conv_wgrad(P, c, P["dz5"], nf, H.im2col(D, Hh, Ww, CD, ld=CD), M, grads)
+        self.conv_wgrad(P, c, P["dz5"], nf, H.im2col(D, Hh, Ww, CD, ld=CD), M, grads, *bs)
         for j in range(3, -1, -1):
             c, cin = cs[j], nf + j * gc
             dz = P["dzg"]
-            H.act_grad_cast(Gd[:, cin:], CD, D[:, cin:], CD, dz, gc, M, gc, 2, 0.2)
+            bs = self.gate_cast(P, Gd[:, cin:], CD, D[:, cin:], CD, dz, gc, M, gc, 2, 0.2)
             H.gemm_nt(H.im2col(dz, Hh, Ww, gc, flip=True), H.rows(c.Wd), H.epilogue(Gd, ldo=CD, resid=Gd, ldr=CD), M, cin,
                       9 * gc, cd)
-            self.conv_wgrad(P, c, dz, gc, H.im2col(D, Hh, Ww, cin, ld=CD), M, grads)
+            self.conv_wgrad(P, c, dz, gc, H.im2col(D, Hh, Ww, cin, ld=CD), M, grads, *bs)
         H.axpby_rows(gy, nf, Gd, CD, M, nf, 1.0, 1.0)
 
 
