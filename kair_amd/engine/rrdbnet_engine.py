@@ -81,31 +81,41 @@ class ConvEngineBase:
 
 
 class RRDBNetEngine(ConvEngineBase):
-    def __init__(self, net, compute_dtype="bf16"):
+    """Also runs network_rrdb.RRDB (option net_type 'rrdb', basicblock.py:393-428 + upsample_upconv
+    455-465): same topology with a configurable activation; see spec_from_rrdb()."""
+
+    def __init__(self, net, compute_dtype="bf16", spec=None):
         super().__init__(net, compute_dtype)
-        self.device = net.conv_first.weight.device
-        self.sf = net.sf
-        if self.sf not in (2, 4):
-            raise NotImplementedError("kair_amd RRDBNet: sf 2 or 4")
-        self.nf = net.conv_first.out_channels
-        self.gc = net.RRDB_trunk[0].RDB1.conv1.out_channels
+        if spec is None:
+            spec = {"first": net.conv_first, "rrdbs": [(r.RDB1, r.RDB2, r.RDB3) for r in net.RRDB_trunk],
+                    "rdb_convs": lambda d: [d.conv1, d.conv2, d.conv3, d.conv4, d.conv5], "trunk": net.trunk_conv,
+                    "up": [net.upconv1] + ([net.upconv2] if net.sf == 4 else []), "hr": net.HRconv,
+                    "last": net.conv_last, "act": 2, "slope": 0.2}
+        self.act, self.slope = spec["act"], spec["slope"]
+        self.act_epi = H.ACT_LEAKY if self.act == 2 else H.ACT_RELU
+        first = spec["first"]
+        self.device = first.weight.device
+        self.nf = first.out_channels
+        rdb_convs = spec["rdb_convs"]
+        self.gc = rdb_convs(spec["rrdbs"][0][0])[0].out_channels
         if self.nf % 8 or self.gc % 8:
-            raise NotImplementedError("kair_amd RRDBNet: nf, gc must be multiples of 8")
-        self.in_ch, self.out_ch = net.conv_first.in_channels, net.conv_last.out_channels
+            raise NotImplementedError("kair_amd RRDB: nf, gc must be multiples of 8")
+        self.in_ch, self.out_ch = first.in_channels, spec["last"].out_channels
         self.Cin_p = 8
         self.CD = self.nf + 4 * self.gc
-        nf, gc = self.nf, self.gc
-        self.conv_first = _Conv(self, net.conv_first, nf, self.Cin_p, need_dgrad=False)
+        nf = self.nf
+        self.conv_first = _Conv(self, first, nf, self.Cin_p, need_dgrad=False)
         self.rdbs = []
-        for rr in net.RRDB_trunk:
-            for rdb in (rr.RDB1, rr.RDB2, rr.RDB3):
-                cs = [rdb.conv1, rdb.conv2, rdb.conv3, rdb.conv4, rdb.conv5]
-                self.rdbs.append([_Conv(self, m, m.out_channels, m.in_channels) for m in cs])
-        self.nrr = len(net.RRDB_trunk)
-        self.trunk = _Conv(self, net.trunk_conv, nf, nf)
-        self.up = [_Conv(self, net.upconv1, nf, nf)] + ([_Conv(self, net.upconv2, nf, nf)] if self.sf == 4 else [])
-        self.hr = _Conv(self, net.HRconv, nf, nf)
-        self.last = _Conv(self, net.conv_last, 16, nf)
+        for rr in spec["rrdbs"]:
+            for rdb in rr:
+                self.rdbs.append([_Conv(self, m, m.out_channels, m.in_channels) for m in rdb_convs(rdb)])
+        self.nrr = len(spec["rrdbs"])
+        self.trunk = _Conv(self, spec["trunk"], nf, nf)
+        self.up = [_Conv(self, m, nf, nf) for m in spec["up"]]
+        if not self.up:
+            raise NotImplementedError("kair_amd RRDB: x2 / x4 upscaling only")
+        self.hr = _Conv(self, spec["hr"], nf, nf)
+        self.last = _Conv(self, spec["last"], 16, nf)
 
     def convs(self):
         return [self.conv_first] + [c for r in self.rdbs for c in r] + [self.trunk] + self.up + [self.hr, self.last]
@@ -175,7 +185,7 @@ class RRDBNetEngine(ConvEngineBase):
             for j in range(4):          # x_{j+1} = lrelu(conv_{j+1}(cat(x, x1..x_j)))
                 c, cin = cs[j], nf + j * gc
                 H.gemm_nt(H.im2col(D, Hh, Ww, cin, ld=CD), H.rows(c.Wf),
-                          H.epilogue(D[:, cin:cin + gc], ldo=CD, bias=c.bp, act=H.ACT_LEAKY, slope=0.2), M, gc, 9 * cin, cd)
+                          H.epilogue(D[:, cin:cin + gc], ldo=CD, bias=c.bp, act=self.act_epi, slope=self.slope), M, gc, 9 * cin, cd)
             c = cs[4]                    # y = x + 0.2 * conv5(cat(x, x1..x4))
             y = P["y"][r]
             H.gemm_nt(H.im2col(D, Hh, Ww, CD, ld=CD), H.rows(c.Wf),
@@ -190,13 +200,13 @@ class RRDBNetEngine(ConvEngineBase):
         H.row_copy(P["fea2"], nf, M, nf, H.copy_desc(P["fea2b"]))
         src = P["fea2b"]
         for c, (hh, ww), dst in zip(self.up, P["levels"], P["upa"]):   # lrelu(upconv(nearest x2))
-            H.gemm_nt(H.im2col(src, hh, ww, nf, up=2), H.rows(c.Wf), H.epilogue(dst, bias=c.bp, act=H.ACT_LEAKY, slope=0.2),
+            H.gemm_nt(H.im2col(src, hh, ww, nf, up=2), H.rows(c.Wf), H.epilogue(dst, bias=c.bp, act=self.act_epi, slope=self.slope),
                       B * hh * ww, nf, 9 * nf, cd)
             src = dst
         HL, WL = P["levels"][-1]
         ML = P["ML"]
         c = self.hr
-        H.gemm_nt(H.im2col(src, HL, WL, nf), H.rows(c.Wf), H.epilogue(P["hr"], bias=c.bp, act=H.ACT_LEAKY, slope=0.2), ML,
+        H.gemm_nt(H.im2col(src, HL, WL, nf), H.rows(c.Wf), H.epilogue(P["hr"], bias=c.bp, act=self.act_epi, slope=self.slope), ML,
                   nf, 9 * nf, cd)
         c = self.last
         H.gemm_nt(H.im2col(P["hr"], HL, WL, nf), H.rows(c.Wf),
@@ -228,7 +238,7 @@ class RRDBNetEngine(ConvEngineBase):
         self.conv_wgrad(P, c, P["dE"], 16, H.im2col(P["hr"], HL, WL, nf), ML, grads)
         # HRconv (lrelu)
         c = self.hr
-        bs = self.gate_cast(P, P["G_hr"], nf, P["hr"], nf, P["dz_hr"], nf, ML, nf, 2, 0.2)
+        bs = self.gate_cast(P, P["G_hr"], nf, P["hr"], nf, P["dz_hr"], nf, ML, nf, self.act, self.slope)
         G = P["G_lv"][-1]
         H.gemm_nt(H.im2col(P["dz_hr"], HL, WL, nf, flip=True), H.rows(c.Wd), H.epilogue(G), ML, nf, 9 * nf, cd)
         self.conv_wgrad(P, c, P["dz_hr"], nf, H.im2col(P["upa"][-1], HL, WL, nf), ML, grads, *bs)
@@ -237,7 +247,7 @@ class RRDBNetEngine(ConvEngineBase):
             c, (hh, ww), a = self.up[i], P["levels"][i], P["upa"][i]
             Mi = B * hh * ww
             dz = P["dz_hr"][:Mi]
-            bs = self.gate_cast(P, G, nf, a, nf, dz, nf, Mi, nf, 2, 0.2)
+            bs = self.gate_cast(P, G, nf, a, nf, dz, nf, Mi, nf, self.act, self.slope)
             Ghi = P["G_hi"][:Mi]
             H.gemm_nt(H.im2col(dz, hh, ww, nf, flip=True), H.rows(c.Wd), H.epilogue(Ghi), Mi, nf, 9 * nf, cd)
             src = P["upa"][i - 1] if i > 0 else P["fea2b"]
@@ -275,7 +285,7 @@ class RRDBNetEngine(ConvEngineBase):
         for j in range(3, -1, -1):
             c, cin = cs[j], nf + j * gc
             dz = P["dzg"]
-            bs = self.gate_cast(P, Gd[:, cin:], CD, D[:, cin:], CD, dz, gc, M, gc, 2, 0.2)
+            bs = self.gate_cast(P, Gd[:, cin:], CD, D[:, cin:], CD, dz, gc, M, gc, self.act, self.slope)
             H.gemm_nt(H.im2col(dz, Hh, Ww, gc, flip=True), H.rows(c.Wd), H.epilogue(Gd, ldo=CD, resid=Gd, ldr=CD), M, cin,
                       9 * gc, cd)
             self.conv_wgrad(P, c, dz, gc, H.im2col(D, Hh, Ww, cin, ld=CD), M, grads, *bs)

@@ -87,6 +87,8 @@ NETG_CFGS = {
                         "upsampler": "pixelshuffledirect", "resi_connection": "1conv", "init_type": "default"},
     "dncnn": {"net_type": "dncnn", "in_nc": 1, "out_nc": 1, "nc": 64, "nb": 17, "act_mode": "BR",
               "init_type": "orthogonal", "init_bn_type": "uniform", "init_gain": 0.2},
+    "rrdb": {"net_type": "rrdb", "in_nc": 3, "out_nc": 3, "nc": 64, "nb": 23, "gc": 32, "scale": 4, "act_mode": "R",
+             "upsample_mode": "upconv", "init_type": "orthogonal", "init_bn_type": "uniform", "init_gain": 0.2},
     "rrdbnet": {"net_type": "rrdbnet", "in_nc": 3, "out_nc": 3, "nf": 64, "nb": 23, "gc": 32, "scale": 4,
                 "init_type": "default"},
 }
