@@ -35,8 +35,12 @@ typedef enum {
   KAIR_LD_ROWS = 0,    /* ptr[rowmap(m) * ld + k]                                           */
   KAIR_LD_IM2COL3 = 1, /* 3x3/pad1/stride1 patch of an NHWC image [B, im_H, im_W, im_C]:
                           k = tap * im_C + c                                                 */
-  KAIR_LD_QKVBLK = 2   /* head-blocked q/k/v: [part][window][head][tok][hdp], k = part*nh*hdp
+  KAIR_LD_QKVBLK = 2,  /* head-blocked q/k/v: [part][window][head][tok][hdp], k = part*nh*hdp
                           + head*hdp + d                                                    */
+  KAIR_LD_S2D = 3      /* 2x2 / stride-2 patch (space-to-depth) of an NHWC image
+                          [B, 2*im_H, 2*im_W, im_C]: row m = (b, y, x) of the im_H x im_W OUTPUT grid,
+                          k = (i*2 + j) * im_C + c -> pixel (2y+i, 2x+j); ld = pixel stride (0: im_C).
+                          basicblock.downsample_strideconv forward / upsample_convtranspose dgrad */
 } kair_load_mode;
 
 typedef struct {
@@ -86,6 +90,8 @@ typedef struct {
   const float* img_mean; float img_range; int img_C, img_H, img_W; /* KAIR_OUT_NCHW          */
   int out_ones_col_p1;                  /* ROWS: 1 + column whose `out` value is forced to 1.0
                                            (the next weight-gradient GEMM's ones column); 0 none */
+  const float* resid2; long ldr2;        /* optional second fp32 residual (ROWS): out += resid2
+                                           (U-Net skip additions, network_usrnet_v1.py:159-162)  */
 } kair_epilogue;
 
 /* C[m,n] = sum_k A[m,k] * B[n,k]  (+ epilogue).  compute: KAIR_BF16 -> v_mfma_f32_16x16x32_bf16,
@@ -107,7 +113,11 @@ int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float* ws, int sp
 typedef struct {
   int kind;          /* 0 linear [N][K]; 1 conv3x3 [Co][Ci][3][3] -> [Cop][9*Cip];
                         2 conv3x3 dgrad form -> [Cip][9*Cop] (flipped taps, swapped channels);
-                        3 linear transposed -> [Kp][Np]                                      */
+                        3 linear transposed -> [Kp][Np]; 4 bias vector;
+                        7 conv2x2 [N][K][2][2] -> [Np][4*Kp], k = tap*Kp + kp (stride-2 conv
+                          forward / transposed-conv dgrad over (N, K) = (Ci, Co));
+                        8 conv2x2 -> [4*Kp][Np], row = kp*4 + tap (pixel-shuffle forms: stride-2
+                          conv dgrad, transposed-conv forward over (N, K) = (Ci, Co))           */
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
   int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp                   */
@@ -225,6 +235,50 @@ int kair_sumpool2x(const float* src, long lds, float* dst, long ldd, int B, int 
  * the host before each (graph-replayed) step; ema may be NULL (E_decay = 0). */
 int kair_adam_ema(float* p, const float* g, float* m, float* v, float* ema, long n, const float* lr_t,
                   float beta1, float beta2, float eps, float weight_decay, float ema_decay, void* stream);
+
+/* USRNet (network_usrnet_v1.py) -------------------------------------------------------------
+ * Complex plane sets are float2 [planes][W][H] (TRANSPOSED: column-major per plane).            */
+#define KAIR_USR_SRC_NCHW 0  /* fp32 NCHW planes [planes][H][W]                                    */
+#define KAIR_USR_SRC_PSF 1   /* p2o of a PSF [B][1][kh][kw]: zero-pad + circular shift (v1:48-69)  */
+#define KAIR_USR_SRC_ZUP 2   /* s-fold zero-upsample of LQ planes [planes][H/sf][W/sf] (v1:72-82)   */
+#define KAIR_USR_SRC_NHWC 3  /* channel plane%C of fp32 NHWC rows [B][H][W][ld]                     */
+#define KAIR_USR_COL_FB 0        /* T <- FB (in place), invW[b][g][u'] = alias-mean |FB|^2           */
+#define KAIR_USR_COL_FBFY 1      /* T <- conj(FB) * F(T)                                             */
+#define KAIR_USR_COL_DATA_FWD 2  /* DataNet.forward (v1:183-194); FR saved when non-null            */
+#define KAIR_USR_COL_DATA_BWD 3  /* DataNet backward: T <- dL/dx spectrum, part <- partial dL/dalpha */
+#define KAIR_USR_CHAN_CHUNKS 64
+/* forward DFT along W of every row, written transposed (replaces torch.fft.fftn's first axis,
+ * v1:66/185/251 and the p2o / upsample inputs) */
+int kair_usr_fft_rows(const float* src, int src_mode, int C, long ld, int kh, int kw, int sf, void* T,
+                      int planes, int H, int W, void* stream);
+/* DFT along H of sf alias column lines per CTA + the closed form of `mode`, then (data modes) the
+ * inverse DFT along H.  alpha[b * alpha_stride]; part: [planes][W/sf] (bwd). */
+int kair_usr_fft_cols(int mode, const void* T, void* T_out, const void* FB, const void* FBFy, void* FR,
+                      float* invW, const float* alpha, int alpha_stride, float* part, int planes, int C,
+                      int H, int W, int sf, void* stream);
+/* inverse DFT along W, real part * scale: NCHW fp32 planes (nhwc 0) or channel plane%C of NHWC
+ * rows [B][H][W][ld] of dst_dtype (nhwc 1)  (torch.real(torch.fft.ifftn(..)), v1:192) */
+int kair_usr_ifft_rows(const void* T, void* dst, int nhwc, int dst_dtype, int C, long ld, float scale,
+                       int planes, int H, int W, void* stream);
+/* out[s*ostride] (+)= scale * sum_j ws[s*seglen + j]  (fixed order) */
+int kair_usr_seg_sum(const float* ws, int seglen, int nseg, float scale, float* out, int ostride,
+                     int accumulate, void* stream);
+/* out[b*ostride] (+)= sum_p x[(b*HW + p)*ld + c]  (ws: B * KAIR_USR_CHAN_CHUNKS floats) */
+int kair_usr_chan_sum(const float* x, long ld, int c, long HW, int B, float* ws, float* out, int ostride,
+                      int accumulate, void* stream);
+/* F.interpolate(x, scale_factor=sf, mode='nearest') of fp32 NCHW planes (v1:252) */
+int kair_usr_upsample_nearest(const float* L, float* out, int planes, int h, int w, int sf, void* stream);
+/* ResUNet input torch.cat((x, beta), 1) (v1:261) as NHWC rows of width ld: x channels, beta[b*bstride], 0 */
+int kair_usr_pack_input(const float* x, const float* beta, int beta_stride, void* out, int dtype, int ld,
+                        int B, int C, long HW, void* stream);
+/* HyPaNet (v1:204-216) on [sigma, sf]: ab [B][no] = softplus(MLP) + 1e-6; one block (B*(4hc+2no)*4 <= 64 KiB) */
+int kair_hypanet_fwd(const float* sigma, float sf, const float* W1, const float* b1, const float* W2,
+                     const float* b2, const float* W3, const float* b3, int hc, int no, int B, float* ab,
+                     void* stream);
+int kair_hypanet_bwd(const float* sigma, float sf, const float* W1, const float* b1, const float* W2,
+                     const float* b2, const float* W3, const float* b3, int hc, int no, int B, const float* gab,
+                     float* gW1, float* gb1, float* gW2, float* gb2, float* gW3, float* gb3, int accumulate,
+                     void* stream);
 
 const char* kair_last_error(void);
 int kair_device_arch(char* buf, int len);

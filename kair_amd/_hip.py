@@ -12,7 +12,10 @@ import torch
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libkair_hip.so")
 
 F32, BF16 = 0, 1
-LD_ROWS, LD_IM2COL3, LD_QKVBLK = 0, 1, 2
+LD_ROWS, LD_IM2COL3, LD_QKVBLK, LD_S2D = 0, 1, 2, 3
+USR_SRC_NCHW, USR_SRC_PSF, USR_SRC_ZUP, USR_SRC_NHWC = 0, 1, 2, 3
+USR_COL_FB, USR_COL_FBFY, USR_COL_DATA_FWD, USR_COL_DATA_BWD = 0, 1, 2, 3
+USR_CHAN_CHUNKS = 64
 OUT_ROWS, OUT_QKVBLK, OUT_PSHUF, OUT_PUNSHUF, OUT_NCHW, OUT_PSHUF_NCHW = 0, 1, 2, 3, 4, 5
 ACT_NONE, ACT_GELU, ACT_LEAKY, ACT_RELU = 0, 1, 2, 3
 
@@ -56,7 +59,7 @@ class Epilogue(ctypes.Structure):
                 ("ps_r", c_int), ("ps_H", c_int), ("ps_W", c_int),
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
                 ("img_mean", c_vp), ("img_range", c_float), ("img_C", c_int), ("img_H", c_int), ("img_W", c_int),
-                ("out_ones_col_p1", c_int)]
+                ("out_ones_col_p1", c_int), ("resid2", c_vp), ("ldr2", c_long)]
 
 
 class WMap(ctypes.Structure):
@@ -104,6 +107,16 @@ _SIGS = {
                            c_vp],
     "kair_sumpool2x": [c_vp, c_long, c_vp, c_long, c_int, c_int, c_int, c_int, c_int, c_vp],
     "kair_adam_ema": [c_vp, c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp],
+    "kair_usr_fft_rows": [c_vp, c_int, c_int, c_long, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],
+    "kair_usr_fft_cols": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
+                          c_vp],
+    "kair_usr_ifft_rows": [c_vp, c_vp, c_int, c_int, c_int, c_long, c_float, c_int, c_int, c_int, c_vp],
+    "kair_usr_seg_sum": [c_vp, c_int, c_int, c_float, c_vp, c_int, c_int, c_vp],
+    "kair_usr_chan_sum": [c_vp, c_long, c_int, c_long, c_int, c_vp, c_vp, c_int, c_int, c_vp],
+    "kair_usr_upsample_nearest": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "kair_usr_pack_input": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_long, c_vp],
+    "kair_hypanet_fwd": [c_vp, c_float] + [c_vp] * 6 + [c_int, c_int, c_int, c_vp, c_vp],
+    "kair_hypanet_bwd": [c_vp, c_float] + [c_vp] * 6 + [c_int, c_int, c_int, c_vp] + [c_vp] * 6 + [c_int, c_vp],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
@@ -198,6 +211,21 @@ def im2col(t, H, W, C, flip=False, ones_col=-1, ld=None, up=1):
     return o
 
 
+def s2d(t, H, W, C, ld=None):
+    """2x2 / stride-2 space-to-depth view of an NHWC map: H x W is the OUTPUT grid (the source is
+    2H x 2W), column k = (i*2 + j) * C + c reads pixel (2y+i, 2x+j), channel c."""
+    o = Operand()
+    o._keep = t
+    o.ptr = ptr(t)
+    o.dtype = dtype_code(t)
+    o.mode = LD_S2D
+    o.ld = ld if ld is not None else C
+    o.im_H, o.im_W, o.im_C = H, W, C
+    o.ones_col = -1
+    o.rows_per_scale = 1
+    return o
+
+
 def qkvblk(t, nh, hdp=32, tok=64, rowscale=None, rows_per_scale=1):
     o = Operand()
     o._keep = (t, rowscale)
@@ -213,9 +241,11 @@ def qkvblk(t, nh, hdp=32, tok=64, rowscale=None, rows_per_scale=1):
 
 def epilogue(out, mode=OUT_ROWS, ldo=None, win=None, bias=None, act=ACT_NONE, slope=0.0, pre=None, ldp=None,
              resid=None, ldr=None, rowscale=None, rows_per_scale=1, gate=None, ldg=None, gate_kind=0,
-             ps=None, qkv=None, img=None, ones_col=-1):
+             ps=None, qkv=None, img=None, ones_col=-1, resid2=None, ldr2=None):
     e = Epilogue()
-    e._keep = (out, bias, pre, resid, rowscale, gate, img)
+    e._keep = (out, bias, pre, resid, rowscale, gate, img, resid2)
+    if resid2 is not None:
+        e.resid2, e.ldr2 = ptr(resid2), (ldr2 if ldr2 is not None else resid2.shape[-1])
     e.out = ptr(out)
     e.out_dtype = dtype_code(out)
     e.out_mode = mode
@@ -371,6 +401,53 @@ def sumpool2x(src, lds, dst, ldd, B, H, W, C, accumulate=False):
 def axpby_rows(y, ldy, x, ldx, M, C, a, b):
     """y[:, :C] = a * x[:, :C] + b * y[:, :C] over strided fp32 rows."""
     check(lib().kair_axpby_rows(ptr(y), ldy, ptr(x), ldx, M, C, a, b, stream_ptr()), "axpby_rows")
+
+
+# ------------------------------------------------------------------------------------------
+# USRNet (network_usrnet_v1.py): complex planes are fp32 tensors holding float2 [planes][W][H]
+# ------------------------------------------------------------------------------------------
+def usr_fft_rows(src, mode, C, ld, kh, kw, sf, T, planes, Hh, Ww):
+    check(lib().kair_usr_fft_rows(ptr(src), mode, C, ld, kh, kw, sf, ptr(T), planes, Hh, Ww, stream_ptr()), "usr_fft_rows")
+
+
+def usr_fft_cols(mode, T, Tout, FB, FBFy, FR, invW, alpha, alpha_stride, part, planes, C, Hh, Ww, sf):
+    check(lib().kair_usr_fft_cols(mode, ptr(T), ptr(Tout), ptr(FB), ptr(FBFy), ptr(FR), ptr(invW), ptr(alpha),
+                                  alpha_stride, ptr(part), planes, C, Hh, Ww, sf, stream_ptr()), "usr_fft_cols")
+
+
+def usr_ifft_rows(T, dst, nhwc, C, ld, scale, planes, Hh, Ww):
+    check(lib().kair_usr_ifft_rows(ptr(T), ptr(dst), int(nhwc), dtype_code(dst), C, ld, scale, planes, Hh, Ww,
+                                   stream_ptr()), "usr_ifft_rows")
+
+
+def usr_seg_sum(ws, seglen, nseg, scale, out, ostride, accumulate=False):
+    check(lib().kair_usr_seg_sum(ptr(ws), seglen, nseg, scale, ptr(out), ostride, int(accumulate), stream_ptr()),
+          "usr_seg_sum")
+
+
+def usr_chan_sum(x, ld, c, HW, B, ws, out, ostride, accumulate=False):
+    check(lib().kair_usr_chan_sum(ptr(x), ld, c, HW, B, ptr(ws), ptr(out), ostride, int(accumulate), stream_ptr()),
+          "usr_chan_sum")
+
+
+def usr_upsample_nearest(L, out, planes, h, w, sf):
+    check(lib().kair_usr_upsample_nearest(ptr(L), ptr(out), planes, h, w, sf, stream_ptr()), "usr_upsample_nearest")
+
+
+def usr_pack_input(x, beta, beta_stride, out, ld, B, C, HW):
+    check(lib().kair_usr_pack_input(ptr(x), ptr(beta), beta_stride, ptr(out), dtype_code(out), ld, B, C, HW,
+                                    stream_ptr()), "usr_pack_input")
+
+
+def hypanet_fwd(sigma, sf, W1, b1, W2, b2, W3, b3, hc, no, B, ab):
+    check(lib().kair_hypanet_fwd(ptr(sigma), sf, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(W3), ptr(b3), hc, no, B, ptr(ab),
+                                 stream_ptr()), "hypanet_fwd")
+
+
+def hypanet_bwd(sigma, sf, W1, b1, W2, b2, W3, b3, hc, no, B, gab, gW1, gb1, gW2, gb2, gW3, gb3, accumulate=False):
+    check(lib().kair_hypanet_bwd(ptr(sigma), sf, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(W3), ptr(b3), hc, no, B, ptr(gab),
+                                 ptr(gW1), ptr(gb1), ptr(gW2), ptr(gb2), ptr(gW3), ptr(gb3), int(accumulate),
+                                 stream_ptr()), "hypanet_bwd")
 
 
 def bn_ws(C):

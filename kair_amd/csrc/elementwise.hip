@@ -36,6 +36,17 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const int tap = kk / Np, cop = kk - tap * Np;
     const int n = unpad(cop, mp.nG, mp.nGr, mp.nGp), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
+  } else if (mp.kind == 7) {  // conv2x2 [Np][4*Kp], k = tap*Kp + kp (stride-2 conv fwd / transposed-conv dgrad)
+    const int np = (int)(t / (4 * Kp));
+    const int kk = (int)(t - (long)np * 4 * Kp);
+    const int tap = kk / Kp, kp = kk - tap * Kp;
+    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && k >= 0) v = src[((long)n * mp.K + k) * 4 + tap];
+  } else if (mp.kind == 8) {  // conv2x2 [4*Kp][Np], row = kp*4 + tap (pixel-shuffle forms)
+    const int row = (int)(t / Np), np = (int)(t - (long)row * Np);
+    const int kp = row >> 2, tap = row & 3;
+    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && k >= 0) v = src[((long)n * mp.K + k) * 4 + tap];
   } else {  // bias vector
     const int n = unpad((int)t, mp.nG, mp.nGr, mp.nGp);
     if (n >= 0) v = src[n];
@@ -69,7 +80,7 @@ __global__ __launch_bounds__(256) void pack_batched_kernel(const kair_pack_job* 
 // element, fixed summation order (deterministic).
 __global__ __launch_bounds__(1024) void wgrad_finalize_kernel(const float* __restrict__ part, int splits, kair_wmap mp,
                                                               float* grad, float* bias_grad, int ones_col, int acc,
-                                                              long nw, long Kt, long plane) {
+                                                              long nw, long Kt, long plane, int taps) {
   const long t = (long)blockIdx.x * 64 + (threadIdx.x & 63);
   const long nb = bias_grad ? mp.N : 0;
   const bool valid = t < nw + nb;
@@ -80,10 +91,10 @@ __global__ __launch_bounds__(1024) void wgrad_finalize_kernel(const float* __res
         const int n = (int)(t / mp.K), k = (int)(t - (long)n * mp.K);
         const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr, kp = (k / mp.kGr) * mp.kGp + k % mp.kGr;
         off = (long)np * Kt + kp;
-      } else {  // conv: grad[co][ci][tap]
-        const int co = (int)(t / ((long)mp.K * 9));
-        const int rem = (int)(t - (long)co * mp.K * 9);
-        const int ci = rem / 9, tap = rem - (rem / 9) * 9;
+      } else {  // conv: grad[co][ci][tap] (3x3: 9 taps; 2x2: 4 taps)
+        const int co = (int)(t / ((long)mp.K * taps));
+        const int rem = (int)(t - (long)co * mp.K * taps);
+        const int ci = rem / taps, tap = rem - (rem / taps) * taps;
         const int np = (co / mp.nGr) * mp.nGp + co % mp.nGr;
         const int cip = (ci / mp.kGr) * mp.kGp + ci % mp.kGr;
         const int Cip = mp.kG * mp.kGp;
@@ -305,6 +316,7 @@ static int pack_total(const kair_wmap& mp, long* total) {
   const long Np = (long)mp.nG * mp.nGp, Kp = (long)mp.kG * mp.kGp;
   if (mp.kind == 0 || mp.kind == 3) *total = Np * Kp;
   else if (mp.kind == 1 || mp.kind == 2) *total = Np * 9 * Kp;
+  else if (mp.kind == 7 || mp.kind == 8) *total = Np * 4 * Kp;
   else if (mp.kind == 4) *total = Np;
   else return kair_set_error(KAIR_ERR_ARG, "pack_weight: bad kind %d", mp.kind);
   return 0;
@@ -361,14 +373,16 @@ extern "C" int kair_wgrad_finalize(const float* partial, int splits, const kair_
                                    float* bias_grad, int ones_col, int accumulate, void* stream) {
   KAIR_CHECK_ARG(partial && map && grad_ref && splits > 0, "wgrad_finalize: null pointer");
   const kair_wmap& mp = *map;
-  KAIR_CHECK_ARG(mp.kind == 0 || mp.kind == 1, "wgrad_finalize: kind must be 0 (linear) or 1 (conv)");
+  KAIR_CHECK_ARG(mp.kind == 0 || mp.kind == 1 || mp.kind == 7,
+                 "wgrad_finalize: kind must be 0 (linear), 1 (conv3x3) or 7 (conv2x2)");
   KAIR_CHECK_ARG(!bias_grad || ones_col >= 0, "wgrad_finalize: bias needs ones_col");
+  const int taps = mp.kind == 0 ? 1 : (mp.kind == 1 ? 9 : 4);
   const long Np = (long)mp.nG * mp.nGp;
-  const long Kt = mp.kind == 0 ? (long)mp.kG * mp.kGp : 9L * mp.kG * mp.kGp;
-  const long nw = (long)mp.N * mp.K * (mp.kind == 1 ? 9 : 1);
+  const long Kt = (long)taps * mp.kG * mp.kGp;
+  const long nw = (long)mp.N * mp.K * taps;
   const long tot = nw + (bias_grad ? mp.N : 0);
   hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(nblk(tot, 64)), dim3(1024), 0, (hipStream_t)stream, partial, splits, mp,
-                     grad_ref, bias_grad, ones_col, accumulate, nw, Kt, Np * Kt);
+                     grad_ref, bias_grad, ones_col, accumulate, nw, Kt, Np * Kt, taps);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

@@ -24,7 +24,7 @@
 namespace {
 
 constexpr int NT = 256;
-enum { AM_ROWS = 0, AM_IM2COL = 1, AM_QKV = 2 };
+enum { AM_ROWS = 0, AM_IM2COL = 1, AM_QKV = 2, AM_S2D = 3 };
 
 template <typename CT> struct KStep { static constexpr int BK = sizeof(CT) == 2 ? 64 : 32; };
 
@@ -52,7 +52,7 @@ Op make_op(const kair_operand& o, long M) {
   op.win = make_winmap(o.win_H, o.win_W, o.win_ws, o.win_shift);
   op.imH = o.im_H; op.imW = o.im_W; op.imC = o.im_C; op.flip = o.im_flip;
   op.up_sh = o.im_up == 2 ? 1 : 0;
-  if (o.mode == KAIR_LD_IM2COL3 && op.ld == 0) op.ld = o.im_C;
+  if ((o.mode == KAIR_LD_IM2COL3 || o.mode == KAIR_LD_S2D) && op.ld == 0) op.ld = o.im_C;
   op.nh = o.qkv_nh; op.hdp = o.qkv_hdp; op.tok = o.qkv_tok;
   op.rowscale = o.rowscale; op.rps = o.rows_per_scale > 0 ? o.rows_per_scale : 1;
   op.ones_col = o.ones_col;
@@ -110,6 +110,13 @@ KAIR_DEV RowState row_state(const Op& op, long m) {
     r.y = fdiv(p, op.d_imW);
     r.x = p - r.y * op.imW;
     r.base = (long)b * (hw >> (2 * op.up_sh));   // first pixel of image b in the SOURCE image
+  } else if constexpr (AM == AM_S2D) {
+    const int hw = op.d_hw.d;
+    const int b = fdiv((int)m, op.d_hw);
+    const int p = (int)m - b * hw;
+    r.y = fdiv(p, op.d_imW);
+    r.x = p - r.y * op.imW;
+    r.base = (long)b * (4L * hw);                // the source image is 2H x 2W
   } else {
     const int win = fdiv((int)m, op.d_tok);
     const int t = (int)m - win * op.tok;
@@ -156,6 +163,11 @@ KAIR_DEV void issue_chunk(const Op& op, const RowState& r, int k, int K, Raw<T>&
     const int y = r.y + dy, x = r.x + dx;
     ok = ok && y >= 0 && y < op.imH && x >= 0 && x < op.imW;
     off = (r.base + (long)(y >> op.up_sh) * (op.imW >> op.up_sh) + (x >> op.up_sh)) * op.ld + c;
+  } else if constexpr (AM == AM_S2D) {
+    const int tap = fdiv(k, op.d_imC);
+    const int c = k - tap * op.imC;
+    const int y = 2 * r.y + (tap >> 1), x = 2 * r.x + (tap & 1);
+    off = (r.base + (long)y * (2 * op.imW) + x) * op.ld + c;
   } else {
     const int pw = op.d_pw.d;
     const int part = fdiv(k, op.d_pw);
@@ -224,6 +236,7 @@ struct Epi {
   int nh, hdp, tok;
   const float* mean; float range; int imgC, imgH, imgW;
   int ones_col;   // -1 none
+  const float* resid2; long ldr2;
   long M; int N;
   FDiv d_rps, d_tok, d_hdp, d_pw;
 };
@@ -241,6 +254,7 @@ Epi make_epi(const kair_epilogue& o, long M, int N) {
   e.nh = o.qkv_nh; e.hdp = o.qkv_hdp; e.tok = o.qkv_tok;
   e.mean = o.img_mean; e.range = o.img_range; e.imgC = o.img_C; e.imgH = o.img_H; e.imgW = o.img_W;
   e.ones_col = o.out_ones_col_p1 - 1;
+  e.resid2 = o.resid2; e.ldr2 = o.ldr2;
   e.M = M; e.N = N;
   e.d_rps = make_fdiv(e.rps); e.d_tok = make_fdiv(e.tok); e.d_hdp = make_fdiv(e.hdp); e.d_pw = make_fdiv(e.nh * e.hdp);
   return e;
@@ -303,6 +317,10 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
       const float s = e.rowscale ? e.rowscale[fdiv((int)row, e.d_rps)] : 1.f;
       for (int j = 0; j < 8; ++j)
         if (n + j < e.N) v[j] = e.resid[row * e.ldr + n + j] + s * v[j];
+    }
+    if (e.resid2) {
+      for (int j = 0; j < 8; ++j)
+        if (n + j < e.N) v[j] += e.resid2[row * e.ldr2 + n + j];
     }
     if (e.ones_col >= n && e.ones_col < n + 8) {
 #pragma unroll
@@ -1040,7 +1058,7 @@ static void init_num_cus() {
 
 // 4-column register epilogue: ROWS / QKV outputs whose vectors are 4-aligned
 static bool epi4_ok(const Epi& e, int N) {
-  if (N % 4 != 0 || N <= 64) return false;
+  if (N % 4 != 0 || N <= 64 || e.resid2) return false;
   if (e.omode == KAIR_OUT_QKVBLK) return e.hdp % 4 == 0;
   if (e.omode != KAIR_OUT_ROWS) return false;
   return e.ldo % 4 == 0 && (!e.pre || e.ldp % 4 == 0) && (!e.resid || e.ldr % 4 == 0) && (!e.gate || e.ldg % 4 == 0);
@@ -1095,6 +1113,7 @@ int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, in
   }
   if (mode == KAIR_LD_ROWS) return nt_tiles<CT, TA, AM_ROWS>(A, B, E, M, N, K, s);
   if (mode == KAIR_LD_IM2COL3) return nt_tiles<CT, TA, AM_IM2COL>(A, B, E, M, N, K, s);
+  if (mode == KAIR_LD_S2D) return nt_tiles<CT, TA, AM_S2D>(A, B, E, M, N, K, s);
   if constexpr (sizeof(TA) == sizeof(CT)) return nt_tiles<CT, TA, AM_QKV>(A, B, E, M, N, K, s);
   return kair_set_error(KAIR_ERR_ARG, "gemm_nt: q/k/v operand must have the compute dtype");
 }
@@ -1119,6 +1138,9 @@ int tn_b(int bmode, int bdt, const Op& a, const Op& b, float* ws, int splits, lo
   if (bmode == KAIR_LD_ROWS)
     return bdt == KAIR_BF16 ? launch_tn<CT, TA, bf16, AMA, AM_ROWS>(a, b, ws, splits, M, N, K, rps, s)
                             : launch_tn<CT, TA, float, AMA, AM_ROWS>(a, b, ws, splits, M, N, K, rps, s);
+  if (bmode == KAIR_LD_S2D)
+    return bdt == KAIR_BF16 ? launch_tn<CT, TA, bf16, AMA, AM_S2D>(a, b, ws, splits, M, N, K, rps, s)
+                            : launch_tn<CT, TA, float, AMA, AM_S2D>(a, b, ws, splits, M, N, K, rps, s);
   return bdt == KAIR_BF16 ? launch_tn<CT, TA, bf16, AMA, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, s)
                           : launch_tn<CT, TA, float, AMA, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, s);
 }
@@ -1152,7 +1174,7 @@ extern "C" int kair_device_arch(char* buf, int len) {
 static int check_operand(const kair_operand* o, const char* what) {
   KAIR_CHECK_ARG(o && o->ptr, "%s: null operand", what);
   KAIR_CHECK_ARG(o->dtype == KAIR_F32 || o->dtype == KAIR_BF16, "%s: bad dtype", what);
-  KAIR_CHECK_ARG(o->mode >= 0 && o->mode <= 2, "%s: bad mode", what);
+  KAIR_CHECK_ARG(o->mode >= 0 && o->mode <= 3, "%s: bad mode", what);
   const int esz = o->dtype == KAIR_BF16 ? 2 : 4;
   KAIR_CHECK_ARG(((uintptr_t)o->ptr % 16) == 0, "%s: pointer not 16-byte aligned", what);
   if (o->mode == KAIR_LD_ROWS) KAIR_CHECK_ARG((o->ld * esz) % 16 == 0, "%s: row stride not 16-byte aligned", what);
@@ -1161,6 +1183,10 @@ static int check_operand(const kair_operand* o, const char* what) {
     KAIR_CHECK_ARG(o->ld == 0 || (o->ld >= o->im_C && (o->ld * esz) % 16 == 0), "%s: im2col pixel stride", what);
     KAIR_CHECK_ARG(o->im_up == 0 || o->im_up == 1 || (o->im_up == 2 && o->im_H % 2 == 0 && o->im_W % 2 == 0),
                    "%s: im2col upsample factor", what);
+  }
+  if (o->mode == KAIR_LD_S2D) {
+    KAIR_CHECK_ARG(o->im_C % 8 == 0 && o->im_H > 0 && o->im_W > 0, "%s: space-to-depth geometry", what);
+    KAIR_CHECK_ARG(o->ld == 0 || (o->ld >= o->im_C && (o->ld * esz) % 16 == 0), "%s: space-to-depth pixel stride", what);
   }
   if (o->mode == KAIR_LD_QKVBLK) KAIR_CHECK_ARG(o->qkv_hdp % 8 == 0 && o->qkv_tok > 0 && o->qkv_nh > 0, "%s: qkv geometry", what);
   if (o->win_ws > 0)
@@ -1224,7 +1250,7 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
   if ((rc = check_operand(B, "gemm_tn B"))) return rc;
   KAIR_CHECK_ARG(ws, "gemm_tn: null workspace");
   KAIR_CHECK_ARG(M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % 8 == 0 && splits > 0, "gemm_tn: bad sizes");
-  KAIR_CHECK_ARG(A->mode != KAIR_LD_IM2COL3, "gemm_tn: A cannot be im2col");
+  KAIR_CHECK_ARG(A->mode != KAIR_LD_IM2COL3 && A->mode != KAIR_LD_S2D, "gemm_tn: A cannot be im2col / space-to-depth");
   KAIR_CHECK_ARG(B->mode != KAIR_LD_QKVBLK, "gemm_tn: B cannot be q/k/v blocked");
   KAIR_CHECK_ARG(compute == KAIR_BF16 || (A->dtype == KAIR_F32 && B->dtype == KAIR_F32),
                  "gemm_tn: fp32 compute needs fp32 operands");
@@ -1269,5 +1295,6 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
     return launch_tn<float, float, float, AM_QKV, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, s);
   }
   if (B->mode == KAIR_LD_ROWS) return launch_tn<float, float, float, AM_ROWS, AM_ROWS>(a, b, ws, splits, M, N, K, rps, s);
+  if (B->mode == KAIR_LD_S2D) return launch_tn<float, float, float, AM_ROWS, AM_S2D>(a, b, ws, splits, M, N, K, rps, s);
   return launch_tn<float, float, float, AM_ROWS, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, s);
 }

@@ -75,7 +75,7 @@ class ModelBase:
 
     def model_to_device(self, network):
         network = network.to(self.device)
-        if hasattr(network, "engine"):
+        if hasattr(network, "engine") and getattr(network, "fused_trainable", True):
             return network           # fused engine: FusedTrainer owns the gradient all-reduce
         if self.opt.get("dist"):
             return DistributedDataParallel(network, device_ids=[torch.cuda.current_device()],

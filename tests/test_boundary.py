@@ -91,6 +91,9 @@ NETG_CFGS = {
              "upsample_mode": "upconv", "init_type": "orthogonal", "init_bn_type": "uniform", "init_gain": 0.2},
     "rrdbnet": {"net_type": "rrdbnet", "in_nc": 3, "out_nc": 3, "nf": 64, "nb": 23, "gc": 32, "scale": 4,
                 "init_type": "default"},
+    "usrnet": {"net_type": "usrnet", "n_iter": 6, "h_nc": 32, "in_nc": 4, "out_nc": 3, "nc": [16, 32, 64, 64], "nb": 2,
+               "act_mode": "R", "downsample_mode": "strideconv", "upsample_mode": "convtranspose",
+               "init_type": "orthogonal", "init_bn_type": "uniform", "init_gain": 0.2},
 }
 
 

@@ -59,7 +59,7 @@ def _worker(rank, world, port, q):
         flat = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
         allreduce_mean_(flat, 4096)
         res["dp_grad"] = flat
-        q.put((rank, res))
+        q.put((rank, {k: v.numpy() for k, v in res.items()}))   # by value (no shared-memory fds)
     finally:
         dist.destroy_process_group()
 
@@ -72,7 +72,7 @@ def test_gloo_world2_allreduce_and_dp_equivalence():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=240) for _ in range(world))
+    out = {r: {k: torch.from_numpy(v) for k, v in d.items()} for r, d in (q.get(timeout=240) for _ in range(world))}
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
