@@ -34,6 +34,13 @@ def allreduce_mean_(flat, bucket_elems, group=None, world=None):
     return flat
 
 
+def allreduce_sum_(flat, bucket_elems, group=None):
+    """In-place sum over ranks, bucketed from the end (the mean scale is applied by the caller)."""
+    for lo, hi in bucket_bounds(flat.numel(), bucket_elems):
+        dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=group)
+    return flat
+
+
 def broadcast_params_(flat, src=0, group=None):
     """Make every rank start from rank `src`'s parameters (DDP's construction-time broadcast)."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:

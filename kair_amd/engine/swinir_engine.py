@@ -180,6 +180,29 @@ class SwinIREngine:
         self.plans = {}
         self._packed_version = None
         self._pack_table = None
+        self.seg_hook = None   # called between the gradient segments of backward() (grad_segments())
+
+    def grad_segments(self):
+        """Parameter groups in the order backward() completes their gradients; seg_hook() fires
+        between consecutive groups.  Each group is contiguous in registration order, so the data-
+        parallel trainer can all-reduce it as one bucket while the rest of backward runs."""
+        net = self.net_ref()
+        tail = list(net.norm.parameters()) + list(net.conv_after_body.parameters())
+        if self.upsampler == "pixelshuffle":
+            tail += (list(net.conv_before_upsample.parameters()) + list(net.upsample.parameters()) +
+                     list(net.conv_last.parameters()))
+        else:
+            tail += list(net.upsample.parameters())
+        segs = [tail]
+        for gi in range(len(net.layers) - 1, 0, -1):
+            segs.append(list(net.layers[gi].parameters()))
+        segs.append(list(net.conv_first.parameters()) + list(net.patch_embed.parameters()) +
+                    list(net.layers[0].parameters()))
+        return segs
+
+    def _segment_done(self):
+        if self.seg_hook is not None:
+            self.seg_hook()
 
     # ------------------------------------------------------------------------------------
     def convs(self):
@@ -468,6 +491,7 @@ class SwinIREngine:
         last_in = P["rstb_out"][-1]
         H.layernorm_bwd(last_in, Cp, D, Cp, n.weight, P["n_mean"], P["n_rstd"], G, Cp, False, g(n.weight), g(n.bias), False,
                         P["ln_ws"], M, self.C)
+        self._segment_done()   # reconstruction tail + conv_after_body + norm gradients are final
         # G = dL/d u_G
         bi = len(self.blocks)
         for gi in range(len(self.rstb) - 1, -1, -1):
@@ -486,6 +510,8 @@ class SwinIREngine:
                 x_in = P["blocks"][bi - 1]["out"] if j > 0 else (P["rstb_out"][gi - 1] if gi > 0 else P["s0"])
                 self._block_bwd(blks[j], P, P["blocks"][bi], x_in, D, bi, grads, copy_prev=j > 0)
             H.axpy(G, D, 1.0)   # dL/du_g = skip + blocks path
+            if gi > 0:
+                self._segment_done()   # RSTB gi's gradients are final (RSTB 0 joins the head segment)
         # ---- patch_embed norm: s0 = LN(f0); f0 also feeds fb (long skip) --------------------
         n = self.pe_norm
         H.layernorm_bwd(P["f0"], Cp, G, Cp, n.weight, P["pe_mean"], P["pe_rstd"], P["dfb"], Cp, True, g(n.weight),

@@ -8,9 +8,16 @@ ModelBase.update_E (model_base.py:247-252) + the DDP reducer (model_base.py:113-
   -> fused Adam + EMA over the flat parameter / state buffers (one kernel)
 
 Parameters of netG (and netE) become views into flat fp32 buffers, so state_dict()/load_state_dict
-and checkpoints are unchanged.  The step is launch-only and is captured into a HIP graph after a
+and checkpoints are unchanged.  The step is launch-only and is captured into HIP graphs after a
 warm-up (torch.cuda.CUDAGraph drives HIP graphs on ROCm); replays only refresh the input batch
 and the two Adam scalars.
+
+Data parallel (world > 1): the fwd+bwd capture is cut into one graph per gradient segment of the
+engine (engine.grad_segments(): for SwinIR the reconstruction tail, then each RSTB, last to first).
+After replaying segment k the host issues the RCCL all-reduce of bucket k (async, on RCCL's own
+stream, ordered after the replay by an event) and goes on replaying segment k+1, so every bucket
+but the last overlaps the remaining backward.  The update graph (mean scale + Adam + EMA) waits
+for all buckets.  RCCL is never captured inside a graph.
 """
 import math
 
@@ -18,7 +25,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _hip as H
-from .comm import allreduce_mean_, broadcast_params_
+from .comm import allreduce_mean_, allreduce_sum_, broadcast_params_
 
 
 def flatten_params(module, device):
@@ -35,9 +42,31 @@ def flatten_params(module, device):
     return flat, params
 
 
+def segment_buckets(params, segs):
+    """Flat-buffer ranges [(lo, hi)] (params laid out in `params` order) of the gradient segments
+    `segs` (parameter lists in backward order), or None when a segment is not contiguous or the
+    segments do not tile the buffer."""
+    pos, off = {}, 0
+    for p in params:
+        pos[p] = (off, off + p.numel())
+        off += p.numel()
+    out = []
+    for plist in segs:
+        if not plist:
+            return None
+        lo, hi = min(pos[p][0] for p in plist), max(pos[p][1] for p in plist)
+        if hi - lo != sum(p.numel() for p in plist):
+            return None
+        out.append((lo, hi))
+    cover = sorted(out)
+    if cover[0][0] != 0 or cover[-1][1] != off or any(a[1] != b[0] for a, b in zip(cover, cover[1:])):
+        return None
+    return out
+
+
 class FusedTrainer:
     def __init__(self, netG, netE=None, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, E_decay=0.999,
-                 loss_weight=1.0, use_graph=True, process_group=None, bucket_mb=25):
+                 loss_weight=1.0, use_graph=True, process_group=None, bucket_mb=25, segment_graphs=None):
         self.net, self.ema_net = netG, netE
         self.device = next(netG.parameters()).device
         self.engine = netG.engine()
@@ -63,6 +92,8 @@ class FusedTrainer:
                                                             (dist.is_available() and dist.is_initialized())) else 1
         self.bucket = max(1, int(bucket_mb * 2 ** 20 // 4))
         self.use_graph = use_graph
+        # one graph per gradient segment: on for world > 1 (overlapped all-reduce); forcible on one GPU
+        self.segment_graphs = (self.world > 1) if segment_graphs is None else bool(segment_graphs)
         self.graph = None
         self.static = None
         self.warm = 0
@@ -102,6 +133,73 @@ class FusedTrainer:
         host = torch.tensor([self.lr / (1 - b1 ** self.t), math.sqrt(1 - b2 ** self.t)], dtype=torch.float32)
         self.scal.copy_(host)   # pageable source: the host buffer is consumed before copy_ returns
 
+    def segment_buckets(self):
+        segs = getattr(self.engine, "grad_segments", None)
+        return segment_buckets(self.params, segs()) if segs is not None else None
+
+    def _capture(self):
+        """Record the step: [fwd+bwd] (+ [update] when world > 1 or segmented), or one graph per
+        gradient segment when segment_graphs is on."""
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        buckets = self.segment_buckets() if self.segment_graphs else None
+        graphs, gu = [], None
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            if self.world == 1 and not buckets:
+                g = torch.cuda.CUDAGraph()
+                g.capture_begin(pool=pool)
+                self.loss_out = self._body(*self.static)
+                g.capture_end()
+                graphs.append(g)
+            else:
+                cur = {"g": torch.cuda.CUDAGraph()}
+                cur["g"].capture_begin(pool=pool)
+
+                def cut():
+                    cur["g"].capture_end()
+                    graphs.append(cur["g"])
+                    cur["g"] = torch.cuda.CUDAGraph()
+                    cur["g"].capture_begin(pool=pool)
+
+                self.engine.seg_hook = cut if buckets else None
+                try:
+                    self.loss_out = self._fwd_bwd(*self.static)
+                finally:
+                    self.engine.seg_hook = None
+                cur["g"].capture_end()
+                graphs.append(cur["g"])
+                gu = torch.cuda.CUDAGraph()
+                gu.capture_begin(pool=pool)
+                if self.world > 1:
+                    self.flat_g.mul_(1.0 / self.world)
+                self._update()
+                gu.capture_end()
+        torch.cuda.current_stream().wait_stream(cs)
+        torch.cuda.synchronize()
+        if buckets is not None and len(buckets) != len(graphs):
+            raise RuntimeError(f"segmented capture: {len(graphs)} graphs for {len(buckets)} gradient buckets")
+        self.buckets = buckets
+        self.graph = (graphs, gu)
+
+    def _replay(self):
+        graphs, gu = self.graph
+        if gu is None:
+            graphs[0].replay()
+            return
+        works = []
+        for k, g in enumerate(graphs):
+            g.replay()
+            if self.world > 1 and self.buckets:
+                lo, hi = self.buckets[k]
+                works.append(dist.all_reduce(self.flat_g[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        if self.world > 1 and not self.buckets:
+            allreduce_sum_(self.flat_g, self.bucket, self.pg)
+        for w in works:
+            w.wait()   # the current stream waits for RCCL's stream (no host block)
+        gu.replay()
+
     def step(self, L, Hh):
         """One training step on the batch (L, Hh) (device tensors).  Returns the device loss [1]."""
         self._set_scalars()
@@ -116,27 +214,9 @@ class FusedTrainer:
         self.static[0].copy_(L)
         self.static[1].copy_(Hh)
         if self.graph is None and self.warm >= 2:
-            # world > 1: the RCCL all-reduce stays outside the captured graphs (fwd+bwd graph,
-            # eager bucketed all-reduce, update graph); single GPU: one graph for the whole step
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):        # records only; the replay below executes this step
-                if self.world > 1:
-                    self.loss_out = self._fwd_bwd(*self.static)
-                else:
-                    self.loss_out = self._body(*self.static)
-            g2 = None
-            if self.world > 1:
-                g2 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g2):
-                    self._update()
-            torch.cuda.synchronize()
-            self.graph = (g, g2)
+            self._capture()                  # records only; the replay below executes this step
         if self.graph is not None:
-            self.graph[0].replay()
-            if self.graph[1] is not None:
-                self._allreduce()
-                self.graph[1].replay()
+            self._replay()
             out = self.loss_out
         else:
             self.warm += 1

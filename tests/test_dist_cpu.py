@@ -92,3 +92,21 @@ def test_gloo_world2_allreduce_and_dp_equivalence():
     torch.nn.functional.l1_loss(net(L), Hh).backward()
     full = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
     torch.testing.assert_close(out[0]["dp_grad"], full, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("ups", ["pixelshuffle", "pixelshuffledirect"])
+def test_swinir_gradient_segments_tile_the_flat_buffer(ups):
+    """The all-reduce buckets the trainer overlaps with backward: the engine's gradient segments are
+    contiguous in parameter order, tile the flat buffer and come last layer first."""
+    from kair_amd.engine.swinir_engine import SwinIREngine
+    from kair_amd.engine.trainer import segment_buckets
+    from kair_amd.models.network_swinir import SwinIR
+    net = SwinIR(upscale=4 if ups == "pixelshuffle" else 2, in_chans=3, img_size=48, window_size=8, img_range=1.0,
+                 depths=[6] * 6, embed_dim=180, num_heads=[6] * 6, mlp_ratio=2, upsampler=ups, resi_connection="1conv")
+    eng = SwinIREngine(net, "bf16")
+    params = list(net.parameters())
+    b = segment_buckets(params, eng.grad_segments())
+    assert b is not None and len(b) == 7
+    assert b[0][1] == sum(p.numel() for p in params)      # the tail bucket ends the buffer
+    assert [lo for lo, _ in b] == sorted([lo for lo, _ in b], reverse=True)
+    assert b[-1][0] == 0
