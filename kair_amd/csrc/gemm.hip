@@ -646,6 +646,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
       *(uint4*)(sB + r * LDB + k8) = v;
     }
   }
+  // bias of this CTA's columns (fixed N tile): loaded once, landed by the barrier below
+  float4 bias4[RN];
+#pragma unroll
+  for (int jn = 0; jn < RN; ++jn) {
+    const int n = n0 + wn * TN + jn * 16 + fq * 4;
+    bias4[jn] = (E.bias && n < E.N) ? *(const float4*)(E.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 
   // loader state: this lane's two rows of the chunk being LOADED
   const int q = lane & 7;
@@ -731,29 +738,112 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
           acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
     }
     if (tile_end) {
+      // Epilogue: every global load (row scales, residual / gate operands) is issued before the
+      // first store, so a tile costs one load round trip instead of a load->use->store chain per
+      // fragment (each use would also wait on the stores issued before it).
       const int mt = mt0 + (j / nk) * mstride;
+      int mv[RM];
+      long rowv[RM];
+      float rsv[RM];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int m = mt * BM + wm * 32 + i * 16 + fr;
-        if (m < (int)E.M) {
-          long row = m;
-          float rs = 1.f;
-          if constexpr (EM == EM_ROWS) {
-            row = win_to_token32(m, E.win);
-            if (E.rowscale) rs = E.rowscale[fdiv((int)row, E.d_rps)];
-          }
+        mv[i] = m;
+        const int mm = m < (int)E.M ? m : 0;
+        rowv[i] = mm;
+        rsv[i] = 1.f;
+        if constexpr (EM == EM_ROWS) {
+          rowv[i] = win_to_token32(mm, E.win);
+          if (E.rowscale) rsv[i] = E.rowscale[fdiv((int)rowv[i], E.d_rps)];
+        }
+      }
+      if constexpr (EM == EM_QKV) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
 #pragma unroll
           for (int jn = 0; jn < RN; ++jn) {
             const int n = n0 + wn * TN + jn * 16 + fq * 4;
-            if (n < E.N) {
-              float v[4] = {acc[i][jn][0], acc[i][jn][1], acc[i][jn][2], acc[i][jn][3]};
-              epi4<EM>(E, m, row, rs, n, v);
+            if (mv[i] < (int)E.M && n < E.N) {
+              const float4 b = bias4[jn];
+              float v[4] = {acc[i][jn][0] + b.x, acc[i][jn][1] + b.y, acc[i][jn][2] + b.z, acc[i][jn][3] + b.w};
+              const int pw = E.nh * E.hdp;
+              const int part = fdiv(n, E.d_pw), rr = n - part * pw;
+              const int h = fdiv(rr, E.d_hdp), d = rr - h * E.hdp;
+              const long win = fdiv(mv[i], E.d_tok);
+              const int t = (int)(mv[i] - win * E.tok);
+              st4_any(E.out, E.odt, (long)part * E.M * pw + ((win * E.nh + h) * E.tok + t) * E.hdp + d, v);
             }
           }
+      } else {
+        float4 ex[RM][RN];   // the residual (fp32) or the gate operand of each fragment
+        const bool has_ex = E.resid || E.gate;
+        if (has_ex) {
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int jn = 0; jn < RN; ++jn) {
+              const int n = n0 + wn * TN + jn * 16 + fq * 4;
+              const int nn = n < E.N ? n : 0;
+              if (E.resid) {
+                ex[i][jn] = *(const float4*)(E.resid + rowv[i] * E.ldr + nn);
+              } else {
+                float g[4];
+                ld4_any(E.gate, E.gdt, rowv[i] * E.ldg + nn, g);
+                ex[i][jn] = make_float4(g[0], g[1], g[2], g[3]);
+              }
+            }
         }
 #pragma unroll
-        for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int jn = 0; jn < RN; ++jn) {
+            const int n = n0 + wn * TN + jn * 16 + fq * 4;
+            if (mv[i] >= (int)E.M || n >= E.N) continue;
+            const float4 b = bias4[jn];
+            float v[4] = {acc[i][jn][0] + b.x, acc[i][jn][1] + b.y, acc[i][jn][2] + b.z, acc[i][jn][3] + b.w};
+            float pre[4] = {v[0], v[1], v[2], v[3]};
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              if (E.act == KAIR_ACT_GELU) v[q4] = gelu_fast(v[q4]);
+              else if (E.act == KAIR_ACT_LEAKY) v[q4] = v[q4] > 0.f ? v[q4] : v[q4] * E.slope;
+              else if (E.act == KAIR_ACT_RELU) v[q4] = fmaxf(v[q4], 0.f);
+            }
+            const float x4[4] = {ex[i][jn].x, ex[i][jn].y, ex[i][jn].z, ex[i][jn].w};
+            if (E.gate && !E.resid) {
+#pragma unroll
+              for (int q4 = 0; q4 < 4; ++q4) {
+                if (E.gkind == 1) v[q4] *= gelu_grad_fast(x4[q4]);
+                else if (E.gkind == 2) v[q4] *= (x4[q4] > 0.f ? 1.f : E.slope);
+                else v[q4] *= (x4[q4] > 0.f ? 1.f : 0.f);
+              }
+            }
+            if (E.resid) {
+              if (E.gate) {   // both operands (no caller uses it): gate read here, after the batch
+                float g[4];
+                ld4_any(E.gate, E.gdt, rowv[i] * E.ldg + n, g);
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                  if (E.gkind == 1) v[q4] *= gelu_grad_fast(g[q4]);
+                  else if (E.gkind == 2) v[q4] *= (g[q4] > 0.f ? 1.f : E.slope);
+                  else v[q4] *= (g[q4] > 0.f ? 1.f : 0.f);
+                }
+              }
+#pragma unroll
+              for (int q4 = 0; q4 < 4; ++q4) v[q4] = x4[q4] + rsv[i] * v[q4];
+            }
+            if (E.ones_col >= n && E.ones_col < n + 4) {
+#pragma unroll
+              for (int q4 = 0; q4 < 4; ++q4)
+                if (n + q4 == E.ones_col) v[q4] = 1.f;
+            }
+            st4_any(E.out, E.odt, rowv[i] * E.ldo + n, v);
+            if (E.pre) st4_any(E.pre, E.pdt, rowv[i] * E.ldp + n, pre);
+          }
       }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (j + NS - 1 < total) issue(j + NS - 1);
     }
   }
@@ -1039,21 +1129,29 @@ int launch_nt(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipS
   return 0;
 }
 
-template <typename CT, typename TA, int AM>
-int nt_tiles(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
-  if (N <= 16) return launch_nt<CT, TA, AM, 256, 16, 4, 1>(A, B, E, M, N, K, s);
-  if (N <= 64) return launch_nt<CT, TA, AM, 128, 64, 2, 2>(A, B, E, M, N, K, s);
-  return launch_nt<CT, TA, AM, 128, 128, 2, 2>(A, B, E, M, N, K, s);
-}
-
 static int g_num_cus = 0;
 static int g_ring_mode = -1;
+static long g_ring_min_tiles = -1;
 
 static void init_num_cus() {
   int dev = 0, n = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     n = 256;
   g_num_cus = n > 0 ? n : 256;
+  const char* v = getenv("KAIR_RING_MIN_TILES");   // A/B knob: ring kernel only with >= this many tiles
+  g_ring_min_tiles = v ? atol(v) : g_num_cus;
+}
+
+// Tile choice of the register-staged kernel: the largest tile that still gives >= 2 CTAs per CU
+// (small per-GPU batches, e.g. 4 patches/GPU at 8 GPUs, would otherwise leave most CUs idle).
+template <typename CT, typename TA, int AM>
+int nt_tiles(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
+  if (N <= 16) return launch_nt<CT, TA, AM, 256, 16, 4, 1>(A, B, E, M, N, K, s);
+  if (g_num_cus == 0) init_num_cus();
+  const long tm = (M + 127) / 128;
+  if (N > 64 && tm * ((N + 127) / 128) >= 2L * g_num_cus) return launch_nt<CT, TA, AM, 128, 128, 2, 2>(A, B, E, M, N, K, s);
+  if (tm * ((N + 63) / 64) >= 2L * g_num_cus || M <= 64) return launch_nt<CT, TA, AM, 128, 64, 2, 2>(A, B, E, M, N, K, s);
+  return launch_nt<CT, TA, AM, 64, 64, 2, 2>(A, B, E, M, N, K, s);
 }
 
 // 4-column register epilogue: ROWS / QKV outputs whose vectors are 4-aligned
@@ -1107,8 +1205,12 @@ int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, in
     }
     if (g_ring_mode && ring_ok(mode, A, B, E, M, N, K)) {
       if (g_num_cus == 0) init_num_cus();
-      if (mode == KAIR_LD_ROWS) return ring_bn<AM_ROWS>(A, B, E, M, N, K, s);
-      return ring_bn<AM_QKV>(A, B, E, M, N, K, s);
+      const int bn = K <= 192 ? 192 : (K <= 384 ? 96 : 64);   // ring_bn's choice
+      const long tiles = ((M + RING_BM - 1) / RING_BM) * ((N + bn - 1) / bn);
+      if (tiles >= g_ring_min_tiles) {
+        if (mode == KAIR_LD_ROWS) return ring_bn<AM_ROWS>(A, B, E, M, N, K, s);
+        return ring_bn<AM_QKV>(A, B, E, M, N, K, s);
+      }
     }
   }
   if (mode == KAIR_LD_ROWS) return nt_tiles<CT, TA, AM_ROWS>(A, B, E, M, N, K, s);
