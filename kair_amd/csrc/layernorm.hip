@@ -178,21 +178,29 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   }
 }
 
-// 64 columns per block, 16 row-phases per column, fixed summation order (deterministic)
-__global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict__ part, int nb, int C, float* dgamma,
-                                                        float* dbeta, int acc) {
-  __shared__ float red[16][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
-  float s = 0.f;
-  if (c < 2 * C)
-    for (int b = ty; b < nb; b += 16) s += part[(long)b * 2 * C + c];
-  red[ty][tx] = s;
+// 8 columns per 256-thread block, 32 row-phases per column, fixed summation order (deterministic).
+// Many small blocks: the reduction reads an L2-resident [nb][2C] partial array and is latency-bound,
+// so it wants every CU issuing loads rather than a handful of wide blocks.
+__global__ __launch_bounds__(256) void ln_param_reduce(const float* __restrict__ part, int nb, int C, float* dgamma,
+                                                       float* dbeta, int acc) {
+  __shared__ float red[32][8];
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + tx;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < 2 * C) {
+    int b = ty;
+    for (; b + 32 < nb; b += 64) {
+      s0 += part[(long)b * 2 * C + c];
+      s1 += part[(long)(b + 32) * 2 * C + c];
+    }
+    if (b < nb) s0 += part[(long)b * 2 * C + c];
+  }
+  red[ty][tx] = s0 + s1;
   __syncthreads();
   if (ty == 0 && c < 2 * C) {
-    s = 0.f;
+    float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) s += red[k][tx];
+    for (int k = 0; k < 32; ++k) s += red[k][tx];
     float* o = c < C ? dgamma + c : dbeta + (c - C);
     *o = acc ? *o + s : s;
   }
@@ -257,7 +265,7 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
     hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const float*)dy, ldy, gamma,
                        mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm);
   KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, dgamma, dbeta,
+  hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 7) / 8), dim3(256), 0, s, ws, (int)nb, C, dgamma, dbeta,
                      dparam_accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;

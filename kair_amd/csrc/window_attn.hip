@@ -456,25 +456,20 @@ __global__ __launch_bounds__(1024) void attn_dbias_sum_kernel(const float* __res
   if (t < n && threadIdx.x < 64) dB[t] = s;
 }
 
-// stage 2: dtable[idx][h] (+)= sum_{(q,k): relidx(q,k)=idx} dB[h][q][k]
-__global__ void attn_dtable_kernel(const float* __restrict__ dB, int nh, float* dtable, int acc) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+// stage 2: dtable[idx][h] (+)= sum_{(q,k): relidx(q,k)=idx} dB[h][q][k] — one wave per (idx, h):
+// lane = query token q, its key k = q - (dy, dx) when inside the window; wave sum in fixed order.
+__global__ __launch_bounds__(256) void attn_dtable_kernel(const float* __restrict__ dB, int nh, float* dtable, int acc) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int nidx = (2 * WS - 1) * (2 * WS - 1);
   if (t >= nidx * nh) return;
   const int idx = t / nh, h = t - (t / nh) * nh;
   const int dy = idx / (2 * WS - 1) - (WS - 1), dx = idx % (2 * WS - 1) - (WS - 1);
-  const float* p = dB + (long)h * TOK * TOK;
-  float s = 0.f;
-  for (int qy = 0; qy < WS; ++qy) {
-    const int ky = qy - dy;
-    if (ky < 0 || ky >= WS) continue;
-    for (int qx = 0; qx < WS; ++qx) {
-      const int kx = qx - dx;
-      if (kx < 0 || kx >= WS) continue;
-      s += p[(qy * WS + qx) * TOK + ky * WS + kx];
-    }
-  }
-  dtable[idx * nh + h] = acc ? dtable[idx * nh + h] + s : s;
+  const int qy = lane >> 3, qx = lane & 7, ky = qy - dy, kx = qx - dx;
+  float v = 0.f;
+  if (ky >= 0 && ky < WS && kx >= 0 && kx < WS) v = dB[(long)h * TOK * TOK + lane * TOK + ky * WS + kx];
+  v = wave_sum(v);
+  if (lane == 0) dtable[idx * nh + h] = acc ? dtable[idx * nh + h] + v : v;
 }
 
 constexpr int WPG = 4;  // windows per backward wave
@@ -529,7 +524,7 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
   hipLaunchKernelGGL(attn_dbias_sum_kernel, dim3((nh * TOK * TOK + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dB);
   KAIR_CHECK_LAUNCH();
   const int nt = (2 * WS - 1) * (2 * WS - 1) * nh;
-  hipLaunchKernelGGL(attn_dtable_kernel, dim3((nt + 127) / 128), dim3(128), 0, s, dB, nh, dtable, dtable_accumulate);
+  hipLaunchKernelGGL(attn_dtable_kernel, dim3((nt + 3) / 4), dim3(256), 0, s, dB, nh, dtable, dtable_accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
