@@ -113,6 +113,50 @@ __global__ __launch_bounds__(1024) void wgrad_finalize_kernel(const float* __res
   }
 }
 
+// Vectorised form: each block sums 64 float4 of the PACKED partial planes with 4 split-phases
+// (fixed order, deterministic), then scatters the 4 sums to the reference layout — pad entries are
+// dropped, the fused ones column goes to the bias gradient.  Needs N*K rows of whole float4s.
+__global__ __launch_bounds__(256) void wgrad_finalize4_kernel(const float* __restrict__ part, int splits, kair_wmap mp,
+                                                              float* grad, float* bias_grad, int ones_col, int acc,
+                                                              long Kt, long plane, int taps) {
+  __shared__ float4 red[4][64];
+  const int q = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const long e4 = (long)blockIdx.x * 64 + q;
+  const bool valid = e4 * 4 < plane;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+    for (int sp = ph; sp < splits; sp += 4) {
+      const float4 v = ((const float4*)(part + (long)sp * plane))[e4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[ph][q] = s;
+  __syncthreads();
+  if (ph != 0 || !valid) return;
+  const float4 a = red[0][q], b = red[1][q], c = red[2][q], d = red[3][q];
+  const float t4[4] = {((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y, ((a.z + b.z) + c.z) + d.z,
+                       ((a.w + b.w) + c.w) + d.w};
+  const int Cip = mp.kG * mp.kGp;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long pe = e4 * 4 + j;
+    const int np = (int)(pe / Kt);
+    const int kk = (int)(pe - (long)np * Kt);
+    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp);
+    if (n < 0) continue;
+    float* o = nullptr;
+    if (bias_grad && kk == ones_col) {
+      o = bias_grad + n;
+    } else {
+      const int tap = taps == 1 ? 0 : kk / Cip;
+      const int k = unpad(taps == 1 ? kk : kk - tap * Cip, mp.kG, mp.kGr, mp.kGp);
+      if (k < 0) continue;
+      o = grad + ((long)n * mp.K + k) * taps + tap;
+    }
+    *o = acc ? *o + t4[j] : t4[j];
+  }
+}
+
 // dst[token_to_win(t)] = scale(t) * src[t] (cast), 4 columns per thread
 template <typename T>
 __global__ void row_copy_kernel(const float* __restrict__ src, long lds, T* __restrict__ dst, long ldd,
@@ -381,8 +425,13 @@ extern "C" int kair_wgrad_finalize(const float* partial, int splits, const kair_
   const long Kt = (long)taps * mp.kG * mp.kGp;
   const long nw = (long)mp.N * mp.K * taps;
   const long tot = nw + (bias_grad ? mp.N : 0);
-  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(nblk(tot, 64)), dim3(1024), 0, (hipStream_t)stream, partial, splits, mp,
-                     grad_ref, bias_grad, ones_col, accumulate, nw, Kt, Np * Kt, taps);
+  if ((Np * Kt) % 4 == 0 && ((uintptr_t)partial % 16) == 0) {
+    hipLaunchKernelGGL(wgrad_finalize4_kernel, dim3(nblk(Np * Kt / 4, 64)), dim3(256), 0, (hipStream_t)stream, partial,
+                       splits, mp, grad_ref, bias_grad, ones_col, accumulate, Kt, Np * Kt, taps);
+  } else {
+    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(nblk(tot, 64)), dim3(1024), 0, (hipStream_t)stream, partial, splits, mp,
+                       grad_ref, bias_grad, ones_col, accumulate, nw, Kt, Np * Kt, taps);
+  }
   KAIR_CHECK_LAUNCH();
   return 0;
 }

@@ -593,74 +593,6 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
   }
 }
 
-// ring-kernel epilogue helpers -----------------------------------------------------------------
-KAIR_DEV void lds_wave_sync() {   // this wave's LDS writes visible to its own lanes
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-template <int EM>
-KAIR_DEV void ring_rowinfo(const Epi& E, int m, long& row, float& rs) {
-  const int mm = m < (int)E.M ? m : 0;
-  row = mm;
-  rs = 1.f;
-  if constexpr (EM == EM_ROWS) {
-    row = win_to_token32(mm, E.win);
-    if (E.rowscale) rs = E.rowscale[fdiv((int)row, E.d_rps)];
-  }
-}
-
-// the residual (fp32) or, without one, the gate operand of 4 consecutive columns of a row
-KAIR_DEV float4 ring_operand(const Epi& E, long row, int n) {
-  const int nn = n < E.N ? n : 0;
-  if (E.resid) return *(const float4*)(E.resid + row * E.ldr + nn);
-  float g[4];
-  ld4_any(E.gate, E.gdt, row * E.ldg + nn, g);
-  return make_float4(g[0], g[1], g[2], g[3]);
-}
-
-template <int EM>
-KAIR_DEV void ring_finish(const Epi& E, int m, long row, float rs, int n, float4 a, float4 b, float4 x) {
-  if (m >= (int)E.M || n >= E.N) return;
-  float v[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
-  if constexpr (EM == EM_QKV) {
-    const int pw = E.nh * E.hdp;
-    const int part = fdiv(n, E.d_pw), rr = n - part * pw;
-    const int h = fdiv(rr, E.d_hdp), d = rr - h * E.hdp;
-    const long win = fdiv(m, E.d_tok);
-    const int t = (int)(m - win * E.tok);
-    st4_any(E.out, E.odt, (long)part * E.M * pw + ((win * E.nh + h) * E.tok + t) * E.hdp + d, v);
-  } else {
-    const float pre[4] = {v[0], v[1], v[2], v[3]};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (E.act == KAIR_ACT_GELU) v[q] = gelu_fast(v[q]);
-      else if (E.act == KAIR_ACT_LEAKY) v[q] = v[q] > 0.f ? v[q] : v[q] * E.slope;
-      else if (E.act == KAIR_ACT_RELU) v[q] = fmaxf(v[q], 0.f);
-    }
-    if (E.gate) {
-      float g[4] = {x.x, x.y, x.z, x.w};
-      if (E.resid) ld4_any(E.gate, E.gdt, row * E.ldg + n, g);   // both operands: no caller does this
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (E.gkind == 1) v[q] *= gelu_grad_fast(g[q]);
-        else if (E.gkind == 2) v[q] *= (g[q] > 0.f ? 1.f : E.slope);
-        else v[q] *= (g[q] > 0.f ? 1.f : 0.f);
-      }
-    }
-    if (E.resid) {
-      v[0] = x.x + rs * v[0]; v[1] = x.y + rs * v[1]; v[2] = x.z + rs * v[2]; v[3] = x.w + rs * v[3];
-    }
-    if (E.ones_col >= n && E.ones_col < n + 4) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (n + q == E.ones_col) v[q] = 1.f;
-    }
-    st4_any(E.out, E.odt, row * E.ldo + n, v);
-    if (E.pre) st4_any(E.pre, E.pdt, row * E.ldp + n, pre);
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // NT ring kernel (bf16 A rows / head-blocked q,k,v; K % 64 == 0, K <= 576): one 512-thread CTA
 // per CU, persistent over the M-tiles of ONE N-tile.
@@ -706,29 +638,31 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
   // resident B slice [BN][K] (rows >= N are zero)
   {
     const bf16* bp = (const bf16*)B.ptr;
+    // all loads first (<= 9 16-byte pieces per thread: BN * K <= RING_B_ELEMS), then the LDS
+    // stores, so the slice costs one L2 round trip rather than one per piece
+    constexpr int PER = (RING_B_ELEMS / 8 + 511) / 512;
     const int cpr = K / 8;
-    for (int c = tid; c < BN * cpr; c += 512) {
+    uint4 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 512;
       const int r = c / cpr, k8 = (c - r * cpr) * 8;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (n0 + r < B.M) v = *(const uint4*)(bp + (long)(n0 + r) * B.ld + k8);
-      *(uint4*)(sB + r * LDB + k8) = v;
+      v[i] = make_uint4(0, 0, 0, 0);
+      if (c < BN * cpr && n0 + r < B.M) v[i] = *(const uint4*)(bp + (long)(n0 + r) * B.ld + k8);
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 512;
+      const int r = c / cpr, k8 = (c - r * cpr) * 8;
+      if (c < BN * cpr) *(uint4*)(sB + r * LDB + k8) = v[i];
     }
   }
-  // bias of this CTA's columns in the epilogue's read-back layout (fixed N tile): loaded once,
-  // landed by the barrier below.  Rounds: NP pairs of 16-column fragments (32 columns, 8 lanes per
-  // row) and, when RN is odd, one single fragment (16 columns, 4 lanes per row).
-  constexpr int NP = RN / 2;
-  constexpr bool ODD = (RN & 1) != 0;
-  const int nb = n0 + wn * TN;
-  float4 biasP[NP > 0 ? NP : 1], biasS = make_float4(0.f, 0.f, 0.f, 0.f);
+  // bias of this CTA's columns (fixed N tile): loaded once, landed by the barrier below
+  float4 bias4[RN];
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int n = nb + 32 * p + (lane & 7) * 4;
-    biasP[p] = (E.bias && n < E.N) ? *(const float4*)(E.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  if constexpr (ODD) {
-    const int n = nb + 16 * (RN - 1) + (lane & 3) * 4;
-    biasS = (E.bias && n < E.N) ? *(const float4*)(E.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int jn = 0; jn < RN; ++jn) {
+    const int n = n0 + wn * TN + jn * 16 + fq * 4;
+    bias4[jn] = (E.bias && n < E.N) ? *(const float4*)(E.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
   // loader state: this lane's two rows of the chunk being LOADED
@@ -815,63 +749,107 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
           acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
     }
     if (tile_end) {
-      // Epilogue through LDS: each wave stages its accumulators, one 16-row x 32-column piece at a
-      // time, in the ring stage every wave has just consumed, and reads them back row-contiguous, so
-      // stores and residual / gate loads move 64-128 B row segments instead of 16-32 B pieces.  All
-      // global loads of the tile are issued before its first store.
-      ring_barrier();                                    // stage j % NS is free in every wave
-      float* stg = (float*)(smem + (j % NS) * STAGE_BYTES) + wave * 512;   // 2 KiB per wave
+      // Epilogue: every global load (row scales, residual / gate operands) is issued before the
+      // first store, so a tile costs one load round trip instead of a load->use->store chain per
+      // fragment (each use would also wait on the stores issued before it).
       const int mt = mt0 + (j / nk) * mstride;
-      const int mb = mt * BM + wm * 32;
-      int mP[RM][2], mS[RM];
-      long rP[RM][2], rS[RM];
-      float sP[RM][2], sS[RM];
+      int mv[RM];
+      long rowv[RM];
+      float rsv[RM];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          mP[i][h] = mb + i * 16 + (lane >> 3) + 8 * h;
-          ring_rowinfo<EM>(E, mP[i][h], rP[i][h], sP[i][h]);
-        }
-        mS[i] = mb + i * 16 + (lane >> 2);
-        if constexpr (ODD) ring_rowinfo<EM>(E, mS[i], rS[i], sS[i]);
-      }
-      float4 exP[RM][NP > 0 ? NP : 1][2], exS[RM];
-      if constexpr (EM == EM_ROWS) {
-        if (E.resid || E.gate) {
-#pragma unroll
-          for (int i = 0; i < RM; ++i) {
-#pragma unroll
-            for (int p = 0; p < NP; ++p)
-#pragma unroll
-              for (int h = 0; h < 2; ++h) exP[i][p][h] = ring_operand(E, rP[i][h], nb + 32 * p + (lane & 7) * 4);
-            if constexpr (ODD) exS[i] = ring_operand(E, rS[i], nb + 16 * (RN - 1) + (lane & 3) * 4);
-          }
+        const int m = mt * BM + wm * 32 + i * 16 + fr;
+        mv[i] = m;
+        const int mm = m < (int)E.M ? m : 0;
+        rowv[i] = mm;
+        rsv[i] = 1.f;
+        if constexpr (EM == EM_ROWS) {
+          rowv[i] = win_to_token32(mm, E.win);
+          if (E.rowscale) rsv[i] = E.rowscale[fdiv((int)rowv[i], E.d_rps)];
         }
       }
+      if constexpr (EM == EM_QKV) {
 #pragma unroll
-      for (int i = 0; i < RM; ++i) {
+        for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int p = 0; p < NP; ++p) {
-          *(f32x4*)(stg + fr * 32 + (((2 * 0 + 0) * 4 + fq) ^ (fr & 7)) * 4) = acc[i][2 * p];
-          *(f32x4*)(stg + fr * 32 + ((4 + fq) ^ (fr & 7)) * 4) = acc[i][2 * p + 1];
-          lds_wave_sync();
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int r = (lane >> 3) + 8 * h;
-            const float4 v = *(const float4*)(stg + r * 32 + (((lane & 7) ^ (r & 7)) * 4));
-            ring_finish<EM>(E, mP[i][h], rP[i][h], sP[i][h], nb + 32 * p + (lane & 7) * 4, v, biasP[p], exP[i][p][h]);
+          for (int jn = 0; jn < RN; ++jn) {
+            const int n = n0 + wn * TN + jn * 16 + fq * 4;
+            if (mv[i] < (int)E.M && n < E.N) {
+              const float4 b = bias4[jn];
+              float v[4] = {acc[i][jn][0] + b.x, acc[i][jn][1] + b.y, acc[i][jn][2] + b.z, acc[i][jn][3] + b.w};
+              const int pw = E.nh * E.hdp;
+              const int part = fdiv(n, E.d_pw), rr = n - part * pw;
+              const int h = fdiv(rr, E.d_hdp), d = rr - h * E.hdp;
+              const long win = fdiv(mv[i], E.d_tok);
+              const int t = (int)(mv[i] - win * E.tok);
+              st4_any(E.out, E.odt, (long)part * E.M * pw + ((win * E.nh + h) * E.tok + t) * E.hdp + d, v);
+            }
           }
-          lds_wave_sync();
+      } else {
+        float4 ex[RM][RN];   // the residual (fp32) or the gate operand of each fragment
+        const bool has_ex = E.resid || E.gate;
+        if (has_ex) {
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int jn = 0; jn < RN; ++jn) {
+              const int n = n0 + wn * TN + jn * 16 + fq * 4;
+              const int nn = n < E.N ? n : 0;
+              if (E.resid) {
+                ex[i][jn] = *(const float4*)(E.resid + rowv[i] * E.ldr + nn);
+              } else {
+                float g[4];
+                ld4_any(E.gate, E.gdt, rowv[i] * E.ldg + nn, g);
+                ex[i][jn] = make_float4(g[0], g[1], g[2], g[3]);
+              }
+            }
         }
-        if constexpr (ODD) {
-          *(f32x4*)(stg + fr * 16 + ((fq ^ (fr & 3)) * 4)) = acc[i][RN - 1];
-          lds_wave_sync();
-          const int r = lane >> 2;
-          const float4 v = *(const float4*)(stg + r * 16 + (((lane & 3) ^ (r & 3)) * 4));
-          ring_finish<EM>(E, mS[i], rS[i], sS[i], nb + 16 * (RN - 1) + (lane & 3) * 4, v, biasS, exS[i]);
-          lds_wave_sync();
-        }
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int jn = 0; jn < RN; ++jn) {
+            const int n = n0 + wn * TN + jn * 16 + fq * 4;
+            if (mv[i] >= (int)E.M || n >= E.N) continue;
+            const float4 b = bias4[jn];
+            float v[4] = {acc[i][jn][0] + b.x, acc[i][jn][1] + b.y, acc[i][jn][2] + b.z, acc[i][jn][3] + b.w};
+            float pre[4] = {v[0], v[1], v[2], v[3]};
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              if (E.act == KAIR_ACT_GELU) v[q4] = gelu_fast(v[q4]);
+              else if (E.act == KAIR_ACT_LEAKY) v[q4] = v[q4] > 0.f ? v[q4] : v[q4] * E.slope;
+              else if (E.act == KAIR_ACT_RELU) v[q4] = fmaxf(v[q4], 0.f);
+            }
+            const float x4[4] = {ex[i][jn].x, ex[i][jn].y, ex[i][jn].z, ex[i][jn].w};
+            if (E.gate && !E.resid) {
+#pragma unroll
+              for (int q4 = 0; q4 < 4; ++q4) {
+                if (E.gkind == 1) v[q4] *= gelu_grad_fast(x4[q4]);
+                else if (E.gkind == 2) v[q4] *= (x4[q4] > 0.f ? 1.f : E.slope);
+                else v[q4] *= (x4[q4] > 0.f ? 1.f : 0.f);
+              }
+            }
+            if (E.resid) {
+              if (E.gate) {   // both operands (no caller uses it): gate read here, after the batch
+                float g[4];
+                ld4_any(E.gate, E.gdt, rowv[i] * E.ldg + n, g);
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                  if (E.gkind == 1) v[q4] *= gelu_grad_fast(g[q4]);
+                  else if (E.gkind == 2) v[q4] *= (g[q4] > 0.f ? 1.f : E.slope);
+                  else v[q4] *= (g[q4] > 0.f ? 1.f : 0.f);
+                }
+              }
+#pragma unroll
+              for (int q4 = 0; q4 < 4; ++q4) v[q4] = x4[q4] + rsv[i] * v[q4];
+            }
+            if (E.ones_col >= n && E.ones_col < n + 4) {
+#pragma unroll
+              for (int q4 = 0; q4 < 4; ++q4)
+                if (n + q4 == E.ones_col) v[q4] = 1.f;
+            }
+            st4_any(E.out, E.odt, rowv[i] * E.ldo + n, v);
+            if (E.pre) st4_any(E.pre, E.pdt, rowv[i] * E.ldp + n, pre);
+          }
       }
 #pragma unroll
       for (int i = 0; i < RM; ++i)
