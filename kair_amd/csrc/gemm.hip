@@ -239,6 +239,7 @@ struct Epi {
   const float* resid2; long ldr2;
   long M; int N;
   FDiv d_rps, d_tok, d_hdp, d_pw;
+  int dbg;   // ring-kernel ablation bits (KAIR_RING_DBG, perf investigation only): 1 no stores, 2 no MFMA, 4 no A loads
 };
 
 Epi make_epi(const kair_epilogue& o, long M, int N) {
@@ -257,6 +258,8 @@ Epi make_epi(const kair_epilogue& o, long M, int N) {
   e.resid2 = o.resid2; e.ldr2 = o.ldr2;
   e.M = M; e.N = N;
   e.d_rps = make_fdiv(e.rps); e.d_tok = make_fdiv(e.tok); e.d_hdp = make_fdiv(e.hdp); e.d_pw = make_fdiv(e.nh * e.hdp);
+  static const int dbg = getenv("KAIR_RING_DBG") ? atoi(getenv("KAIR_RING_DBG")) : 0;
+  e.dbg = dbg;
   return e;
 }
 
@@ -602,7 +605,12 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
 //    so the lane-linear image reads conflict-light), waited with a counted vmcnt and a raw
 //    s_barrier, so NS-2 chunks stay in flight across barriers and across tile boundaries;
 //  * MFMA operands are swapped (D = B . A^T) so each lane owns 4 consecutive output columns of one
-//    row: the fused epilogue runs from the accumulators with 8/16-byte vector accesses.
+//    row: the fused epilogue runs from the accumulators with 8/16-byte vector accesses;
+//  * vmcnt counts the epilogue's stores too (in issue order with the LDS-DMA loads), so the chunk
+//    wait adds the stores this wave issued after the awaited chunk: a tile's stores drain under the
+//    next tile's MFMAs instead of being waited for at its first chunk.  The count used is the number
+//    of store instructions that MUST have issued (fragments with at least one valid lane); a
+//    compiler that also issues fully masked ones only makes the wait stricter.
 // ------------------------------------------------------------------------------------------
 constexpr int RING_BM = 128, RING_BK = 64;
 constexpr int RING_B_ELEMS = 38400;   // max BN * (K + 8) over the (BN, K) pairs dispatched below
@@ -613,7 +621,43 @@ KAIR_DEV void ring_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BN, int NS, int AM, int EM>
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4 into lds_base + 16 * lane) issued from
+// inline asm.  hipcc treats the builtin form as a pending LDS write and emits s_waitcnt vmcnt(0)
+// before the next ds_read of the shared array -- every chunk of a ring would drain all the DMA (and
+// stores) in flight.  Hidden in asm, the DMA is waited for only by the ring's own counted vmcnt.
+KAIR_DEV void glds16(const void* src, const char* lds_base) {
+  const unsigned la = __builtin_amdgcn_readfirstlane(
+      (unsigned)(unsigned long)(__attribute__((address_space(3))) const char*)lds_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(la) : "memory", "m0");
+}
+
+// Wait for an ordinary (compiler-visible) load's result HERE, on every path: a load still pending
+// at a loop back-edge on any path makes hipcc wait vmcnt(0) at the next write of its register.
+KAIR_DEV void land(float& v) { asm volatile("" : "+v"(v)); }
+KAIR_DEV void land(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
+// ring epilogue operand kinds (compile-time, so the plain kernels carry no epilogue loads at all)
+enum { EX_NONE = 0, EX_RESID = 1, EX_GATE_BF16 = 2, EX_GATE_F32 = 3 };
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit field: waiting for more
+// than asked is always safe)
+#define KAIR_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+KAIR_DEV void vm_wait(int n) {
+  switch (n < 63 ? n : 63) {
+    KAIR_VMW(0) KAIR_VMW(1) KAIR_VMW(2) KAIR_VMW(3) KAIR_VMW(4) KAIR_VMW(5) KAIR_VMW(6) KAIR_VMW(7)
+    KAIR_VMW(8) KAIR_VMW(9) KAIR_VMW(10) KAIR_VMW(11) KAIR_VMW(12) KAIR_VMW(13) KAIR_VMW(14) KAIR_VMW(15)
+    KAIR_VMW(16) KAIR_VMW(17) KAIR_VMW(18) KAIR_VMW(19) KAIR_VMW(20) KAIR_VMW(21) KAIR_VMW(22) KAIR_VMW(23)
+    KAIR_VMW(24) KAIR_VMW(25) KAIR_VMW(26) KAIR_VMW(27) KAIR_VMW(28) KAIR_VMW(29) KAIR_VMW(30) KAIR_VMW(31)
+    KAIR_VMW(32) KAIR_VMW(33) KAIR_VMW(34) KAIR_VMW(35) KAIR_VMW(36) KAIR_VMW(37) KAIR_VMW(38) KAIR_VMW(39)
+    KAIR_VMW(40) KAIR_VMW(41) KAIR_VMW(42) KAIR_VMW(43) KAIR_VMW(44) KAIR_VMW(45) KAIR_VMW(46) KAIR_VMW(47)
+    KAIR_VMW(48) KAIR_VMW(49) KAIR_VMW(50) KAIR_VMW(51) KAIR_VMW(52) KAIR_VMW(53) KAIR_VMW(54) KAIR_VMW(55)
+    KAIR_VMW(56) KAIR_VMW(57) KAIR_VMW(58) KAIR_VMW(59) KAIR_VMW(60) KAIR_VMW(61) KAIR_VMW(62)
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+  }
+}
+#undef KAIR_VMW
+
+template <int BN, int NS, int AM, int EM, int EX>
 __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
   constexpr int BM = RING_BM, BK = RING_BK;
   constexpr int TN = BN / 2, RM = 2, RN = TN / 16;
@@ -663,6 +707,25 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
   for (int jn = 0; jn < RN; ++jn) {
     const int n = n0 + wn * TN + jn * 16 + fq * 4;
     bias4[jn] = (E.bias && n < E.N) ? *(const float4*)(E.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    land(bias4[jn]);
+  }
+  // fragments of this wave's columns that hold a valid lane (its lane fq = 0 column is < N)
+  int ncv = 0;
+#pragma unroll
+  for (int jn = 0; jn < RN; ++jn) ncv += (n0 + wn * TN + jn * 16 < E.N) ? 1 : 0;
+  const int st_per_frag = (EM == EM_ROWS && E.pre) ? 2 : 1;
+  // QKV store: column part of the head-blocked offset, fixed per CTA
+  long colq[EM == EM_QKV ? RN : 1];
+  if constexpr (EM == EM_QKV) {
+    const int pw = E.nh * E.hdp;
+#pragma unroll
+    for (int jn = 0; jn < RN; ++jn) {
+      int n = n0 + wn * TN + jn * 16 + fq * 4;
+      n = n < E.N ? n : 0;
+      const int part = fdiv(n, E.d_pw), rr = n - part * pw;
+      const int h = fdiv(rr, E.d_hdp), d = rr - h * E.hdp;
+      colq[jn] = (long)part * E.M * pw + (long)h * E.tok * E.hdp + d;
+    }
   }
 
   // loader state: this lane's two rows of the chunk being LOADED
@@ -687,6 +750,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
     }
   };
   auto issue = [&](int j) {
+    if (E.dbg & 4) return;
     const int i = j / nk, kc = j - (j / nk) * nk;
     if (i != ld_tile) { load_rows(i); ld_tile = i; }
     char* st = smem + (j % NS) * STAGE_BYTES;
@@ -702,8 +766,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
         const int h = fdiv(rr, A.d_hdp), d = rr - h * A.hdp;
         off = (long)part * A.M * pw + rbase[ii] + (long)h * A.tok * A.hdp + d;
       }
-      __builtin_amdgcn_global_load_lds((const void*)((const bf16*)A.ptr + off),
-                                       (__attribute__((address_space(3))) void*)(st + (wave * 2 + ii) * 1024), 16, 0, 0);
+      glds16((const bf16*)A.ptr + off, st + (wave * 2 + ii) * 1024);
     }
   };
 
@@ -719,20 +782,20 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
 #pragma unroll
     for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  static_assert(NS == 5, "the store bookkeeping below assumes chunk j is issued at iteration j-4");
+  int sq1 = 0, sq2 = 0, sq3 = 0;   // store instructions this wave issued at iterations j-1, j-2, j-3
   for (int j = 0; j < total; ++j) {
-    // chunk j landed for this wave; at most min(NS-2, total-1-j) younger chunks may remain in flight
+    // chunk j landed for this wave: younger than it are min(NS-2, total-1-j) chunks (2 DMA
+    // instructions each) and the stores of the epilogues run at iterations j-3 .. j-1
     const int ahead = (total - 1 - j) < (NS - 2) ? (total - 1 - j) : (NS - 2);
-    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait(2 * ahead + sq1 + sq2 + sq3);
     ring_barrier();   // every wave's part of chunk j is in LDS; stage (j-1)%NS is free
     const int kc = j % nk;
     const bool tile_end = kc == nk - 1;
     if (!tile_end && j + NS - 1 < total) issue(j + NS - 1);
     const char* st = smem + (j % NS) * STAGE_BYTES;
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
+    for (int ks = 0; ks < ((E.dbg & 2) ? 0 : BK / 32); ++ks) {
       bf16x8 af[RM], bfr[RN];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
@@ -748,6 +811,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
         for (int jn = 0; jn < RN; ++jn)
           acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
     }
+    int sj = 0;
     if (tile_end) {
       // Epilogue: every global load (row scales, residual / gate operands) is issued before the
       // first store, so a tile costs one load round trip instead of a load->use->store chain per
@@ -759,57 +823,66 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int m = mt * BM + wm * 32 + i * 16 + fr;
+        sj += (mt * BM + wm * 32 + i * 16 < (int)E.M && !(E.dbg & 1)) ? ncv * st_per_frag : 0;
         mv[i] = m;
         const int mm = m < (int)E.M ? m : 0;
         rowv[i] = mm;
         rsv[i] = 1.f;
         if constexpr (EM == EM_ROWS) {
           rowv[i] = win_to_token32(mm, E.win);
-          if (E.rowscale) rsv[i] = E.rowscale[fdiv((int)rowv[i], E.d_rps)];
+          if constexpr (EX == EX_RESID) {
+            rsv[i] = E.rowscale ? E.rowscale[fdiv((int)rowv[i], E.d_rps)] : 1.f;
+            land(rsv[i]);
+          }
         }
       }
       if constexpr (EM == EM_QKV) {
 #pragma unroll
-        for (int i = 0; i < RM; ++i)
+        for (int i = 0; i < RM; ++i) {
+          const int win = fdiv(mv[i], E.d_tok), t = mv[i] - win * E.tok;
+          const long rowq = ((long)win * E.nh * E.tok + t) * E.hdp;
 #pragma unroll
           for (int jn = 0; jn < RN; ++jn) {
             const int n = n0 + wn * TN + jn * 16 + fq * 4;
-            if (mv[i] < (int)E.M && n < E.N) {
+            if (mv[i] < (int)E.M && n < E.N && !(E.dbg & 1)) {
               const float4 b = bias4[jn];
               float v[4] = {acc[i][jn][0] + b.x, acc[i][jn][1] + b.y, acc[i][jn][2] + b.z, acc[i][jn][3] + b.w};
-              const int pw = E.nh * E.hdp;
-              const int part = fdiv(n, E.d_pw), rr = n - part * pw;
-              const int h = fdiv(rr, E.d_hdp), d = rr - h * E.hdp;
-              const long win = fdiv(mv[i], E.d_tok);
-              const int t = (int)(mv[i] - win * E.tok);
-              st4_any(E.out, E.odt, (long)part * E.M * pw + ((win * E.nh + h) * E.tok + t) * E.hdp + d, v);
+              st4_any(E.out, E.odt, colq[jn] + rowq, v);
             }
           }
+        }
       } else {
-        float4 ex[RM][RN];   // the residual (fp32) or the gate operand of each fragment
-        const bool has_ex = E.resid || E.gate;
-        if (has_ex) {
+        // the residual (EX 1, fp32) or the gate operand (EX 2 bf16, EX 3 fp32) of each fragment:
+        // loaded unconditionally (clamped rows / columns) and landed at once, so no path leaves a
+        // load pending into the next chunk (hipcc would drain the ring with vmcnt(0) for it)
+        float4 ex[RM][RN];
+        if constexpr (EX != EX_NONE) {
 #pragma unroll
           for (int i = 0; i < RM; ++i)
 #pragma unroll
             for (int jn = 0; jn < RN; ++jn) {
               const int n = n0 + wn * TN + jn * 16 + fq * 4;
               const int nn = n < E.N ? n : 0;
-              if (E.resid) {
+              if constexpr (EX == EX_RESID) {
                 ex[i][jn] = *(const float4*)(E.resid + rowv[i] * E.ldr + nn);
+              } else if constexpr (EX == EX_GATE_BF16) {
+                const bf16x4 g = *(const bf16x4*)((const bf16*)E.gate + rowv[i] * E.ldg + nn);
+                ex[i][jn] = make_float4((float)g[0], (float)g[1], (float)g[2], (float)g[3]);
               } else {
-                float g[4];
-                ld4_any(E.gate, E.gdt, rowv[i] * E.ldg + nn, g);
-                ex[i][jn] = make_float4(g[0], g[1], g[2], g[3]);
+                ex[i][jn] = *(const float4*)((const float*)E.gate + rowv[i] * E.ldg + nn);
               }
             }
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int jn = 0; jn < RN; ++jn) land(ex[i][jn]);
         }
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
           for (int jn = 0; jn < RN; ++jn) {
             const int n = n0 + wn * TN + jn * 16 + fq * 4;
-            if (mv[i] >= (int)E.M || n >= E.N) continue;
+            if (mv[i] >= (int)E.M || n >= E.N || (E.dbg & 1)) continue;
             const float4 b = bias4[jn];
             float v[4] = {acc[i][jn][0] + b.x, acc[i][jn][1] + b.y, acc[i][jn][2] + b.z, acc[i][jn][3] + b.w};
             float pre[4] = {v[0], v[1], v[2], v[3]};
@@ -820,7 +893,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
               else if (E.act == KAIR_ACT_RELU) v[q4] = fmaxf(v[q4], 0.f);
             }
             const float x4[4] = {ex[i][jn].x, ex[i][jn].y, ex[i][jn].z, ex[i][jn].w};
-            if (E.gate && !E.resid) {
+            if constexpr (EX == EX_GATE_BF16 || EX == EX_GATE_F32) {
 #pragma unroll
               for (int q4 = 0; q4 < 4; ++q4) {
                 if (E.gkind == 1) v[q4] *= gelu_grad_fast(x4[q4]);
@@ -828,17 +901,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
                 else v[q4] *= (x4[q4] > 0.f ? 1.f : 0.f);
               }
             }
-            if (E.resid) {
-              if (E.gate) {   // both operands (no caller uses it): gate read here, after the batch
-                float g[4];
-                ld4_any(E.gate, E.gdt, rowv[i] * E.ldg + n, g);
-#pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4) {
-                  if (E.gkind == 1) v[q4] *= gelu_grad_fast(g[q4]);
-                  else if (E.gkind == 2) v[q4] *= (g[q4] > 0.f ? 1.f : E.slope);
-                  else v[q4] *= (g[q4] > 0.f ? 1.f : 0.f);
-                }
-              }
+            if constexpr (EX == EX_RESID) {
 #pragma unroll
               for (int q4 = 0; q4 < 4; ++q4) v[q4] = x4[q4] + rsv[i] * v[q4];
             }
@@ -857,6 +920,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
         for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (j + NS - 1 < total) issue(j + NS - 1);
     }
+    sq3 = sq2; sq2 = sq1; sq1 = sj;
   }
 }
 
@@ -894,6 +958,11 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 2, wk = wave & 3;
 
+  // operand bases as scalars: selecting A or B fields per lane below would otherwise read the
+  // kernel-argument struct through a VGPR pointer (a global load + vmcnt(0) before every DMA)
+  const bf16* const Ap = (const bf16*)A.ptr;
+  const bf16* const Bp = (const bf16*)B.ptr;
+  const long Ald = A.ld, Bld = B.ld;
   auto issue = [&](int j) {
     const int m0 = mbeg + j * RB;
     char* st = smem + (j % NS) * STAGE;
@@ -907,21 +976,20 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, in
       const void* src = g_kair_zero_line;
       if (m < mend) {
         if (isB) {
-          if (k0 + c < K) src = (const bf16*)B.ptr + (long)m * B.ld + k0 + c;
+          if (k0 + c < K) src = Bp + (long)m * Bld + k0 + c;
         } else if (n0 + c < N) {
           if constexpr (AMA == AM_ROWS) {
-            src = (const bf16*)A.ptr + (long)m * A.ld + n0 + c;
+            src = Ap + (long)m * Ald + n0 + c;
           } else {
             const int n = n0 + c, pw = A.d_pw.d;
             const int part = fdiv(n, A.d_pw), rr = n - part * pw;
             const int h = fdiv(rr, A.d_hdp), d = rr - h * A.hdp;
             const int win = fdiv(m, A.d_tok), t = m - win * A.tok;
-            src = (const bf16*)A.ptr + (long)part * M * pw + (((long)win * A.nh + h) * A.tok + t) * A.hdp + d;
+            src = Ap + (long)part * M * pw + (((long)win * A.nh + h) * A.tok + t) * A.hdp + d;
           }
         }
       }
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + (isB ? PART : 0) + (g % 12) * 1024),
-                                       16, 0, 0);
+      glds16(src, st + (isB ? PART : 0) + (g % 12) * 1024);
     }
   };
 
@@ -1181,10 +1249,17 @@ int launch_ring(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hi
   if (grid < tilesN) grid = tilesN;
   const int need = tilesM * tilesN;
   if (grid > need) grid = need;
+  const dim3 g(grid), b(512);
   if (E.omode == KAIR_OUT_QKVBLK)
-    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_QKV>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesN, tilesM);
+    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_QKV, EX_NONE>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
+  else if (E.resid)
+    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_RESID>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
+  else if (E.gate && E.gdt == KAIR_BF16)
+    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_GATE_BF16>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
+  else if (E.gate)
+    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_GATE_F32>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
   else
-    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesN, tilesM);
+    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_NONE>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1197,6 +1272,8 @@ static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, i
   if (amode == KAIR_LD_ROWS && A.ld % 8 != 0) return false;
   if (amode == KAIR_LD_QKVBLK && (A.hdp % 8 != 0)) return false;
   if (B.ld % 8 != 0 || B.ones_col >= 0) return false;
+  if (e.resid && e.gate) return false;   // one epilogue operand per ring kernel
+  if (e.rowscale && !e.resid) return false;
   return epi4_ok(e, N);
 }
 

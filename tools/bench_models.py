@@ -1,0 +1,111 @@
+"""Training throughput of the other BASELINE.json configs on one MI355X (the headline SwinIR
+classical x4 line is bench.py's).  One JSON line per config:
+
+    python tools/bench_models.py [dncnn|swinir_light|rrdbnet|usrnet ...] [--steps K] [--warmup W]
+
+C1 DnCNN sigma 25, 40x40, batch 64 (BN, fused trainer)        network_dncnn.py, options/train_dncnn.json
+C2 SwinIR-lightweight x2, 64-px LQ, batch 64 (fused trainer)   options/swinir/train_swinir_sr_lightweight.json
+C5 RRDBNet x4, 32-px LQ, batch 16 (fused trainer)              options/train_rrdb_psnr.json
+C3 USRNet x4, 128-px LQ (512^2 HR), batch 48, n_iter 6         options/train_usrnet.json (ModelPlain4 step:
+                                                                autograd node + torch Adam, no EMA)
+Synthetic seeded inputs resident in HBM; bf16 MFMA operands, fp32 accumulation.
+FLOP/patch from BASELINE.md (FlopCounterMode, GEMM + conv only; USRNet FFTs not counted).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PEAK_BF16_TFLOPS = 2500.0
+TRAIN_GFLOP = {"dncnn": 5.32, "swinir_light": 25.68, "rrdbnet": 110.14, "usrnet": 577.25}
+
+
+def timed(step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps, out
+
+
+def run(name, steps, warmup, dev):
+    from kair_amd.engine.trainer import FusedTrainer
+    torch.manual_seed(0)
+    g = torch.Generator().manual_seed(1)
+    if name == "dncnn":
+        from kair_amd.models.network_dncnn import DnCNN
+        mk = lambda: DnCNN(1, 1, 64, 17, "BR")   # noqa: E731
+        B, shp, sc = 64, (1, 40, 40), 1
+    elif name == "swinir_light":
+        from kair_amd.models.network_swinir import SwinIR
+        mk = lambda: SwinIR(upscale=2, in_chans=3, img_size=64, window_size=8, img_range=1.0, depths=[6] * 4,   # noqa: E731
+                            embed_dim=60, num_heads=[6] * 4, mlp_ratio=2, upsampler="pixelshuffledirect",
+                            resi_connection="1conv")
+        B, shp, sc = 64, (3, 64, 64), 2
+    elif name == "rrdbnet":
+        from kair_amd.models.network_rrdbnet import RRDBNet
+        mk = lambda: RRDBNet(3, 3, 64, 23, 32, 4)   # noqa: E731
+        B, shp, sc = 16, (3, 32, 32), 4
+    elif name == "usrnet":
+        return run_usrnet(steps, warmup, dev)
+    else:
+        raise SystemExit(f"unknown config {name}")
+    net, ema = mk().to(dev).train(), mk().to(dev).eval()
+    ema.load_state_dict(net.state_dict())
+    tr = FusedTrainer(net, ema, lr=1e-4, E_decay=0.999, use_graph=True)
+    L = torch.rand(B, *shp, generator=g).to(dev)
+    Hh = torch.rand(B, shp[0], shp[1] * sc, shp[2] * sc, generator=g).to(dev)
+    dt, loss = timed(lambda: tr.step(L, Hh), steps, warmup)
+    return B, dt, float(loss.item())
+
+
+def run_usrnet(steps, warmup, dev):
+    from kair_amd.models.network_usrnet import USRNet
+    net = USRNet(n_iter=6, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2).to(dev).train()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    g = torch.Generator().manual_seed(2)
+    B, lq, sf = 48, 128, 4
+    L = torch.rand(B, 3, lq, lq, generator=g).to(dev)
+    Hh = torch.rand(B, 3, lq * sf, lq * sf, generator=g).to(dev)
+    k = torch.rand(B, 1, 25, 25, generator=g)
+    k = (k / k.sum((-2, -1), keepdim=True)).to(dev)
+    sigma = (torch.rand(B, 1, 1, 1, generator=g) * 25 / 255).to(dev)
+
+    def step():   # ModelPlain.optimize_parameters (model_plain.py:270-318) with ModelPlain4's forward
+        opt.zero_grad(set_to_none=True)
+        loss = torch.nn.functional.l1_loss(net(L, k, sf, sigma), Hh)
+        loss.backward()
+        opt.step()
+        return loss
+    dt, loss = timed(step, steps, warmup)
+    return B, dt, float(loss.item())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["dncnn", "swinir_light", "rrdbnet", "usrnet"])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=4)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    for name in a.configs:
+        B, dt, loss = run(name, a.steps, a.warmup, dev)
+        pps = B / dt
+        tf = pps * TRAIN_GFLOP[name] / 1e3
+        print(json.dumps({"config": name, "patches_per_s": round(pps, 2), "ms_per_step": round(dt * 1e3, 3), "batch": B,
+                          "train_gflop_per_patch": TRAIN_GFLOP[name], "achieved_tflops": round(tf, 2),
+                          "frac_of_bf16_peak": round(tf / PEAK_BF16_TFLOPS, 4), "loss": round(loss, 6),
+                          "dtype": "bf16", "n_gpus": 1}), flush=True)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -22,13 +22,25 @@ M = B_ * HH * WW
 
 
 def timeit(fn, reps):
+    """Average us per launch of `reps` launches captured in one HIP graph (host launch cost of the
+    Python wrappers excluded, as in the graph-replayed training step)."""
     for _ in range(3):
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g.capture_begin()
+        for _ in range(reps):
+            fn()
+        g.capture_end()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
     e0.record()
-    for _ in range(reps):
-        fn()
+    g.replay()
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps * 1e3  # us
