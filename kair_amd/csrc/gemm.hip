@@ -550,6 +550,17 @@ KAIR_DEV void st4_any(void* p, int dt, long off, const float (&v)[4]) {
   }
 }
 
+// 8 consecutive columns: one 16-byte store for bf16, two for fp32
+KAIR_DEV void st8_any(void* p, int dt, long off, const float (&v)[8]) {
+  if (dt == KAIR_BF16) {
+    const bf16x8 q = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+    *(bf16x8*)((bf16*)p + off) = q;
+  } else {
+    *(float4*)((float*)p + off) = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)((float*)p + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
 template <int EM>
 KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4]) {
   if (e.bias) {
@@ -614,6 +625,7 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
 // ------------------------------------------------------------------------------------------
 constexpr int RING_BM = 128, RING_BK = 64;
 constexpr int RING_B_ELEMS = 38400;   // max BN * (K + 8) over the (BN, K) pairs dispatched below
+constexpr int RING_RS_MAX = 1024;     // per-sample residual scales kept in LDS by the ring kernel
 
 KAIR_DEV void ring_barrier() {
   asm volatile("" ::: "memory");
@@ -639,10 +651,14 @@ KAIR_DEV void land(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z
 // ring epilogue operand kinds (compile-time, so the plain kernels carry no epilogue loads at all)
 enum { EX_NONE = 0, EX_RESID = 1, EX_GATE_BF16 = 2, EX_GATE_F32 = 3 };
 
+// a zero line for masked loads (read-only; zero-initialised device memory)
+__device__ __attribute__((aligned(64))) unsigned char g_kair_zero_line[64];
+
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit field: waiting for more
 // than asked is always safe)
 #define KAIR_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
 KAIR_DEV void vm_wait(int n) {
+  n = __builtin_amdgcn_readfirstlane(n);   // scalar branch tree, not exec-masked
   switch (n < 63 ? n : 63) {
     KAIR_VMW(0) KAIR_VMW(1) KAIR_VMW(2) KAIR_VMW(3) KAIR_VMW(4) KAIR_VMW(5) KAIR_VMW(6) KAIR_VMW(7)
     KAIR_VMW(8) KAIR_VMW(9) KAIR_VMW(10) KAIR_VMW(11) KAIR_VMW(12) KAIR_VMW(13) KAIR_VMW(14) KAIR_VMW(15)
@@ -660,14 +676,19 @@ KAIR_DEV void vm_wait(int n) {
 template <int BN, int NS, int AM, int EM, int EX>
 __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
   constexpr int BM = RING_BM, BK = RING_BK;
-  constexpr int TN = BN / 2, RM = 2, RN = TN / 16;
+  // 8 waves as WM (rows) x WN (columns); each wave's columns split into 16-wide fragment pairs
+  constexpr int WN = BN == 96 ? 1 : 2, WM = 8 / WN, WROWS = BM / WM;
+  constexpr int TN = BN / WN, RM = WROWS / 16, RN = TN / 16;
   constexpr int STAGE_BYTES = BM * BK * 2;   // 16 KiB
-  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE_BYTES + RING_B_ELEMS * 2];
+  constexpr int NP = RN / 2;                  // fragment pairs per wave row (8-column epilogue groups)
+  static_assert(RN % 2 == 0, "fragment pairs");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE_BYTES + RING_B_ELEMS * 2 + RING_RS_MAX * 4];
   bf16* sB = (bf16*)(smem + NS * STAGE_BYTES);
+  float* sRS = (float*)(smem + NS * STAGE_BYTES + RING_B_ELEMS * 2);
   const int LDB = K + 8;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;   // 4 (M) x 2 (N) waves
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fq = lane >> 4;
   const int cta = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = cta % tilesN;
@@ -682,7 +703,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
   // resident B slice [BN][K] (rows >= N are zero)
   {
     const bf16* bp = (const bf16*)B.ptr;
-    // all loads first (<= 9 16-byte pieces per thread: BN * K <= RING_B_ELEMS), then the LDS
+    // all loads first (<= 10 16-byte pieces per thread: BN * K <= RING_B_ELEMS), then the LDS
     // stores, so the slice costs one L2 round trip rather than one per piece
     constexpr int PER = (RING_B_ELEMS / 8 + 511) / 512;
     const int cpr = K / 8;
@@ -691,8 +712,17 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * 512;
       const int r = c / cpr, k8 = (c - r * cpr) * 8;
-      v[i] = make_uint4(0, 0, 0, 0);
-      if (c < BN * cpr && n0 + r < B.M) v[i] = *(const uint4*)(bp + (long)(n0 + r) * B.ld + k8);
+      // unconditional (clamped) loads, zeroed after: a conditional load becomes a branch with its
+      // own wait, i.e. one L2 round trip per piece
+      const bool ok = c < BN * cpr && n0 + r < B.M;
+      const long row = ok ? n0 + r : 0;
+      v[i] = *(const uint4*)(bp + row * B.ld + (ok ? k8 : 0));
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 512;
+      const int r = c / cpr;
+      if (!(c < BN * cpr && n0 + r < B.M)) v[i] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -701,36 +731,43 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
       if (c < BN * cpr) *(uint4*)(sB + r * LDB + k8) = v[i];
     }
   }
-  // bias of this CTA's columns (fixed N tile): loaded once, landed by the barrier below
-  float4 bias4[RN];
-#pragma unroll
-  for (int jn = 0; jn < RN; ++jn) {
-    const int n = n0 + wn * TN + jn * 16 + fq * 4;
-    bias4[jn] = (E.bias && n < E.N) ? *(const float4*)(E.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    land(bias4[jn]);
-  }
-  // fragments of this wave's columns that hold a valid lane (its lane fq = 0 column is < N)
-  int ncv = 0;
-#pragma unroll
-  for (int jn = 0; jn < RN; ++jn) ncv += (n0 + wn * TN + jn * 16 < E.N) ? 1 : 0;
-  const int st_per_frag = (EM == EM_ROWS && E.pre) ? 2 : 1;
-  // QKV store: column part of the head-blocked offset, fixed per CTA
-  long colq[EM == EM_QKV ? RN : 1];
-  if constexpr (EM == EM_QKV) {
-    const int pw = E.nh * E.hdp;
-#pragma unroll
-    for (int jn = 0; jn < RN; ++jn) {
-      int n = n0 + wn * TN + jn * 16 + fq * 4;
-      n = n < E.N ? n : 0;
-      const int part = fdiv(n, E.d_pw), rr = n - part * pw;
-      const int h = fdiv(rr, E.d_hdp), d = rr - h * E.hdp;
-      colq[jn] = (long)part * E.M * pw + (long)h * E.tok * E.hdp + d;
+  // per-sample residual scales (DropPath) in LDS: the epilogue reads them without a global load
+  if constexpr (EX == EX_RESID) {
+    if (E.rowscale) {
+      const int nrs = (int)((E.M + E.rps - 1) / E.rps);
+      for (int i = tid; i < nrs; i += 512) sRS[i] = E.rowscale[i];
     }
   }
 
+  // Epilogue columns (fixed per CTA).  After a v_permlane16_swap of fragment pair (2p, 2p+1) a
+  // lane owns 8 consecutive columns of fragment 2p + (fq & 1): c8 = that fragment's base +
+  // (fq >> 1) * 8, so bf16 outputs leave as one 16-byte store per lane instead of two 8-byte ones.
+  int c8v[NP];
+  long colo[NP];   // ROWS: output column; QKV: column part of the head-blocked offset
+  float4 bias8[NP][2];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int n = n0 + wn * TN + (2 * p + (fq & 1)) * 16 + (fq >> 1) * 8;
+    c8v[p] = n;
+    const int nn = n < E.N ? n : 0;
+    if constexpr (EM == EM_QKV) {
+      const int pw = E.nh * E.hdp;
+      const int part = fdiv(nn, E.d_pw), rr = nn - part * pw;
+      const int h = fdiv(rr, E.d_hdp), d = rr - h * E.hdp;
+      colo[p] = (long)part * E.M * pw + (long)h * E.tok * E.hdp + d;
+    } else {
+      colo[p] = nn;
+    }
+    // unconditional loads (a zero line stands in for a missing bias / column)
+    bias8[p][0] = *(const float4*)(E.bias && n < E.N ? E.bias + n : (const float*)g_kair_zero_line);
+    bias8[p][1] = *(const float4*)(E.bias && n + 4 < E.N ? E.bias + n + 4 : (const float*)g_kair_zero_line);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) { land(bias8[p][0]); land(bias8[p][1]); }
+  const int st_per_frag = (EM == EM_ROWS && E.pre) ? 2 : 1;
+
   // loader state: this lane's two rows of the chunk being LOADED
-  const int q = lane & 7;
-  int ld_tile = -1;
+  const int q8 = lane & 7;
   long rbase[2];
   int rsw[2];   // row & 7 (swizzle key)
   auto load_rows = [&](int i) {
@@ -749,32 +786,38 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
       }
     }
   };
-  auto issue = [&](int j) {
-    if (E.dbg & 4) return;
-    const int i = j / nk, kc = j - (j / nk) * nk;
-    if (i != ld_tile) { load_rows(i); ld_tile = i; }
-    char* st = smem + (j % NS) * STAGE_BYTES;
+  // loader cursor: the next chunk to issue is lj = lt * nk + lkc, into stage ls (all wave-uniform
+  // counters advanced incrementally -- no per-chunk divisions)
+  int lj = 0, lt = 0, lkc = 0, ls = 0;
+  auto issue_next = [&]() {
+    if (lkc == 0) load_rows(lt);
+    if (!(E.dbg & 4)) {
+      char* st = smem + ls * STAGE_BYTES;
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii) {
-      const int k = kc * BK + ((q ^ rsw[ii]) << 3);
-      long off;
-      if constexpr (AM == AM_ROWS) {
-        off = rbase[ii] + k;
-      } else {
-        const int pw = A.d_pw.d;
-        const int part = fdiv(k, A.d_pw), rr = k - part * pw;
-        const int h = fdiv(rr, A.d_hdp), d = rr - h * A.hdp;
-        off = (long)part * A.M * pw + rbase[ii] + (long)h * A.tok * A.hdp + d;
+      for (int ii = 0; ii < 2; ++ii) {
+        const int k = lkc * BK + ((q8 ^ rsw[ii]) << 3);
+        long off;
+        if constexpr (AM == AM_ROWS) {
+          off = rbase[ii] + k;
+        } else {
+          const int pw = A.d_pw.d;
+          const int part = fdiv(k, A.d_pw), rr = k - part * pw;
+          const int h = fdiv(rr, A.d_hdp), d = rr - h * A.hdp;
+          off = (long)part * A.M * pw + rbase[ii] + (long)h * A.tok * A.hdp + d;
+        }
+        glds16((const bf16*)A.ptr + off, st + (wave * 2 + ii) * 1024);
       }
-      glds16((const bf16*)A.ptr + off, st + (wave * 2 + ii) * 1024);
     }
+    ++lj;
+    if (++lkc == nk) { lkc = 0; ++lt; }
+    if (++ls == NS) ls = 0;
   };
 
   // prologue: B slice visible to every wave, then NS-1 chunks in flight
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j)
-    if (j < total) issue(j);
+    if (lj < total) issue_next();
 
   f32x4 acc[RM][RN];
 #pragma unroll
@@ -784,22 +827,22 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
 
   static_assert(NS == 5, "the store bookkeeping below assumes chunk j is issued at iteration j-4");
   int sq1 = 0, sq2 = 0, sq3 = 0;   // store instructions this wave issued at iterations j-1, j-2, j-3
+  int kc = 0, cs = 0, ct = 0;      // consumer cursor: chunk j = ct * nk + kc, in stage cs
   for (int j = 0; j < total; ++j) {
     // chunk j landed for this wave: younger than it are min(NS-2, total-1-j) chunks (2 DMA
     // instructions each) and the stores of the epilogues run at iterations j-3 .. j-1
     const int ahead = (total - 1 - j) < (NS - 2) ? (total - 1 - j) : (NS - 2);
     vm_wait(2 * ahead + sq1 + sq2 + sq3);
     ring_barrier();   // every wave's part of chunk j is in LDS; stage (j-1)%NS is free
-    const int kc = j % nk;
     const bool tile_end = kc == nk - 1;
-    if (!tile_end && j + NS - 1 < total) issue(j + NS - 1);
-    const char* st = smem + (j % NS) * STAGE_BYTES;
+    if (!tile_end && lj < total) issue_next();   // lj == j + NS - 1
+    const char* st = smem + cs * STAGE_BYTES;
 #pragma unroll
     for (int ks = 0; ks < ((E.dbg & 2) ? 0 : BK / 32); ++ks) {
       bf16x8 af[RM], bfr[RN];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
-        const int r = wm * 32 + i * 16 + fr;
+        const int r = wm * WROWS + i * 16 + fr;
         af[i] = *(const bf16x8*)(st + r * 128 + (((ks * 4 + fq) ^ (r & 7)) << 4));
       }
 #pragma unroll
@@ -813,114 +856,118 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
     }
     int sj = 0;
     if (tile_end) {
-      // Epilogue: every global load (row scales, residual / gate operands) is issued before the
-      // first store, so a tile costs one load round trip instead of a load->use->store chain per
-      // fragment (each use would also wait on the stores issued before it).
-      const int mt = mt0 + (j / nk) * mstride;
-      int mv[RM];
-      long rowv[RM];
-      float rsv[RM];
+      // Epilogue from registers: fragment pairs are re-laid by v_permlane16_swap so each lane
+      // holds 8 consecutive columns of one row; every epilogue load is issued before the first
+      // store and landed at once (no path leaves a load pending into the next chunk, where hipcc
+      // would drain the ring for it).
+      const int mt = mt0 + ct * mstride;
+      int mv[RM], rowv[RM];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
-        const int m = mt * BM + wm * 32 + i * 16 + fr;
-        sj += (mt * BM + wm * 32 + i * 16 < (int)E.M && !(E.dbg & 1)) ? ncv * st_per_frag : 0;
+        const int m = mt * BM + wm * WROWS + i * 16 + fr;
         mv[i] = m;
         const int mm = m < (int)E.M ? m : 0;
-        rowv[i] = mm;
-        rsv[i] = 1.f;
         if constexpr (EM == EM_ROWS) {
           rowv[i] = win_to_token32(mm, E.win);
-          if constexpr (EX == EX_RESID) {
-            rsv[i] = E.rowscale ? E.rowscale[fdiv((int)rowv[i], E.d_rps)] : 1.f;
-            land(rsv[i]);
-          }
+        } else {
+          const int win = fdiv(mm, E.d_tok);
+          rowv[i] = win * E.nh * E.tok + (mm - win * E.tok);
         }
       }
-      if constexpr (EM == EM_QKV) {
-#pragma unroll
-        for (int i = 0; i < RM; ++i) {
-          const int win = fdiv(mv[i], E.d_tok), t = mv[i] - win * E.tok;
-          const long rowq = ((long)win * E.nh * E.tok + t) * E.hdp;
-#pragma unroll
-          for (int jn = 0; jn < RN; ++jn) {
-            const int n = n0 + wn * TN + jn * 16 + fq * 4;
-            if (mv[i] < (int)E.M && n < E.N && !(E.dbg & 1)) {
-              const float4 b = bias4[jn];
-              float v[4] = {acc[i][jn][0] + b.x, acc[i][jn][1] + b.y, acc[i][jn][2] + b.z, acc[i][jn][3] + b.w};
-              st4_any(E.out, E.odt, colq[jn] + rowq, v);
-            }
-          }
-        }
-      } else {
-        // the residual (EX 1, fp32) or the gate operand (EX 2 bf16, EX 3 fp32) of each fragment:
-        // loaded unconditionally (clamped rows / columns) and landed at once, so no path leaves a
-        // load pending into the next chunk (hipcc would drain the ring with vmcnt(0) for it)
-        float4 ex[RM][RN];
-        if constexpr (EX != EX_NONE) {
-#pragma unroll
-          for (int i = 0; i < RM; ++i)
-#pragma unroll
-            for (int jn = 0; jn < RN; ++jn) {
-              const int n = n0 + wn * TN + jn * 16 + fq * 4;
-              const int nn = n < E.N ? n : 0;
-              if constexpr (EX == EX_RESID) {
-                ex[i][jn] = *(const float4*)(E.resid + rowv[i] * E.ldr + nn);
-              } else if constexpr (EX == EX_GATE_BF16) {
-                const bf16x4 g = *(const bf16x4*)((const bf16*)E.gate + rowv[i] * E.ldg + nn);
-                ex[i][jn] = make_float4((float)g[0], (float)g[1], (float)g[2], (float)g[3]);
-              } else {
-                ex[i][jn] = *(const float4*)((const float*)E.gate + rowv[i] * E.ldg + nn);
-              }
-            }
-#pragma unroll
-          for (int i = 0; i < RM; ++i)
-#pragma unroll
-            for (int jn = 0; jn < RN; ++jn) land(ex[i][jn]);
-        }
+      float4 ex[RM][NP][2];
+      if constexpr (EX != EX_NONE) {
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
-          for (int jn = 0; jn < RN; ++jn) {
-            const int n = n0 + wn * TN + jn * 16 + fq * 4;
-            if (mv[i] >= (int)E.M || n >= E.N || (E.dbg & 1)) continue;
-            const float4 b = bias4[jn];
-            float v[4] = {acc[i][jn][0] + b.x, acc[i][jn][1] + b.y, acc[i][jn][2] + b.z, acc[i][jn][3] + b.w};
-            float pre[4] = {v[0], v[1], v[2], v[3]};
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-              if (E.act == KAIR_ACT_GELU) v[q4] = gelu_fast(v[q4]);
-              else if (E.act == KAIR_ACT_LEAKY) v[q4] = v[q4] > 0.f ? v[q4] : v[q4] * E.slope;
-              else if (E.act == KAIR_ACT_RELU) v[q4] = fmaxf(v[q4], 0.f);
-            }
-            const float x4[4] = {ex[i][jn].x, ex[i][jn].y, ex[i][jn].z, ex[i][jn].w};
-            if constexpr (EX == EX_GATE_BF16 || EX == EX_GATE_F32) {
-#pragma unroll
-              for (int q4 = 0; q4 < 4; ++q4) {
-                if (E.gkind == 1) v[q4] *= gelu_grad_fast(x4[q4]);
-                else if (E.gkind == 2) v[q4] *= (x4[q4] > 0.f ? 1.f : E.slope);
-                else v[q4] *= (x4[q4] > 0.f ? 1.f : 0.f);
-              }
-            }
+          for (int p = 0; p < NP; ++p) {
+            const long rr = rowv[i];
+            const long c = colo[p];   // clamped rows / columns read valid memory
             if constexpr (EX == EX_RESID) {
-#pragma unroll
-              for (int q4 = 0; q4 < 4; ++q4) v[q4] = x4[q4] + rsv[i] * v[q4];
+              ex[i][p][0] = *(const float4*)(E.resid + rr * E.ldr + c);
+              ex[i][p][1] = *(const float4*)(E.resid + rr * E.ldr + c + 4);
+            } else if constexpr (EX == EX_GATE_BF16) {
+              const bf16x8 g = *(const bf16x8*)((const bf16*)E.gate + rr * E.ldg + c);
+              ex[i][p][0] = make_float4((float)g[0], (float)g[1], (float)g[2], (float)g[3]);
+              ex[i][p][1] = make_float4((float)g[4], (float)g[5], (float)g[6], (float)g[7]);
+            } else {
+              ex[i][p][0] = *(const float4*)((const float*)E.gate + rr * E.ldg + c);
+              ex[i][p][1] = *(const float4*)((const float*)E.gate + rr * E.ldg + c + 4);
             }
-            if (E.ones_col >= n && E.ones_col < n + 4) {
-#pragma unroll
-              for (int q4 = 0; q4 < 4; ++q4)
-                if (n + q4 == E.ones_col) v[q4] = 1.f;
-            }
-            st4_any(E.out, E.odt, rowv[i] * E.ldo + n, v);
-            if (E.pre) st4_any(E.pre, E.pdt, rowv[i] * E.ldp + n, pre);
           }
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int p = 0; p < NP; ++p) { land(ex[i][p][0]); land(ex[i][p][1]); }
       }
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          float v[8];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][c]),
+                                                            __float_as_uint(acc[i][2 * p + 1][c]), false, false);
+            v[c] = __uint_as_float(r[0]);
+            v[4 + c] = __uint_as_float(r[1]);
+          }
+          const int n = c8v[p];
+          const bool ok = mv[i] < (int)E.M && n < E.N && !(E.dbg & 1);   // N % 8 == 0: whole groups
+          const float b8[8] = {bias8[p][0].x, bias8[p][0].y, bias8[p][0].z, bias8[p][0].w,
+                               bias8[p][1].x, bias8[p][1].y, bias8[p][1].z, bias8[p][1].w};
+#pragma unroll
+          for (int c = 0; c < 8; ++c) v[c] += b8[c];
+          if constexpr (EM == EM_QKV) {
+            const long off = colo[p] + (long)rowv[i] * E.hdp;
+            if (ok) st8_any(E.out, E.odt, off, v);
+            sj += __ballot(ok) != 0 ? 1 : 0;
+          } else {
+            float pre[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+              pre[c] = v[c];
+              if (E.act == KAIR_ACT_GELU) v[c] = gelu_fast(v[c]);
+              else if (E.act == KAIR_ACT_LEAKY) v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
+              else if (E.act == KAIR_ACT_RELU) v[c] = fmaxf(v[c], 0.f);
+            }
+            if constexpr (EX != EX_NONE) {
+              const float x8[8] = {ex[i][p][0].x, ex[i][p][0].y, ex[i][p][0].z, ex[i][p][0].w,
+                                   ex[i][p][1].x, ex[i][p][1].y, ex[i][p][1].z, ex[i][p][1].w};
+              if constexpr (EX == EX_RESID) {
+                const float rs = E.rowscale ? sRS[fdiv(rowv[i], E.d_rps)] : 1.f;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) v[c] = x8[c] + rs * v[c];
+              } else {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                  if (E.gkind == 1) v[c] *= gelu_grad_fast(x8[c]);
+                  else if (E.gkind == 2) v[c] *= (x8[c] > 0.f ? 1.f : E.slope);
+                  else v[c] *= (x8[c] > 0.f ? 1.f : 0.f);
+                }
+              }
+            }
+            if (E.ones_col >= n && E.ones_col < n + 8) {
+#pragma unroll
+              for (int c = 0; c < 8; ++c)
+                if (n + c == E.ones_col) v[c] = 1.f;
+            }
+            const long rr = rowv[i];
+            if (ok) {
+              st8_any(E.out, E.odt, rr * E.ldo + n, v);
+              if (E.pre) st8_any(E.pre, E.pdt, rr * E.ldp + n, pre);
+            }
+            sj += __ballot(ok) != 0 ? st_per_frag : 0;
+          }
+        }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
         for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (j + NS - 1 < total) issue(j + NS - 1);
+      if (lj < total) issue_next();
     }
     sq3 = sq2; sq2 = sq1; sq1 = sj;
+    if (++kc == nk) { kc = 0; ++ct; }
+    if (++cs == NS) cs = 0;
   }
 }
 
@@ -933,7 +980,6 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
 // Rows past the split (and columns past N / K) read a zero line.  The bias-gradient "ones" column
 // must already be in B (kair_operand.ones_in_data).
 // ------------------------------------------------------------------------------------------
-__device__ __attribute__((aligned(64))) unsigned char g_kair_zero_line[64];
 
 constexpr int TNR_BN = 192, TNR_BK = 192, TNR_RB = 32, TNR_NS = 6;
 
@@ -955,7 +1001,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, in
   int mend = mbeg + rows_per_split;
   if (mend > M) mend = M;
   const int nchunks = mbeg < mend ? (mend - mbeg + RB - 1) / RB : 0;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wk = wave & 3;
 
   // operand bases as scalars: selecting A or B fields per lane below would otherwise read the
@@ -1273,7 +1319,20 @@ static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, i
   if (amode == KAIR_LD_QKVBLK && (A.hdp % 8 != 0)) return false;
   if (B.ld % 8 != 0 || B.ones_col >= 0) return false;
   if (e.resid && e.gate) return false;   // one epilogue operand per ring kernel
-  if (e.rowscale && !e.resid) return false;
+  // 8-column epilogue groups: whole groups, 16-byte aligned rows / pointers
+  if (N % 8 != 0) return false;
+  auto al16 = [](const void* q) { return ((unsigned long)q & 15) == 0; };
+  if (!al16(e.out) || (e.pre && !al16(e.pre)) || (e.gate && !al16(e.gate)) || (e.resid && !al16(e.resid)))
+    return false;
+  if ((e.odt == KAIR_BF16 && e.ldo % 8) || (e.pre && e.pdt == KAIR_BF16 && e.ldp % 8) ||
+      (e.gate && e.gdt == KAIR_BF16 && e.ldg % 8))
+    return false;
+  if (e.omode == KAIR_OUT_QKVBLK && e.hdp % 8) return false;
+  if (e.rowscale && (!e.resid || (M + e.rps - 1) / e.rps > RING_RS_MAX)) return false;
+  if (e.omode == KAIR_OUT_QKVBLK) {         // the staged store groups whole heads per wave
+    const int TN = (K <= 192 ? 192 : K <= 384 ? 96 : 64) / 2;
+    if (e.hdp <= 0 || TN % e.hdp != 0) return false;
+  }
   return epi4_ok(e, N);
 }
 
