@@ -42,6 +42,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   const int sub = threadIdx.x & (LPR - 1);
   const long grp = (long)blockIdx.x * ROWS_PER_BLOCK_ITER + (threadIdx.x >> 4);
   const long ng = (long)gridDim.x * ROWS_PER_BLOCK_ITER;
+  // this lane's affine parameters, loaded once (not per row and element)
+  float ga[NV][4], be[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = (sub + LPR * i) * 4 + j;
+      ga[i][j] = c < C ? gamma[c] : 0.f;
+      be[i][j] = c < C ? beta[c] : (c == one_col ? 1.f : 0.f);   // ones column for the weight-gradient GEMM
+    }
   for (long r = grp; r < M; r += ng) {        // r = output row (window order if wm.ws > 0)
     const long t = win_to_token(r, wm);
     float4 v[NV];
@@ -73,13 +83,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
     for (int i = 0; i < NV; ++i) {
       const int c = (sub + LPR * i) * 4;
       if (c < ldy) {
-        float o[4] = {0.f, 0.f, 0.f, 0.f};
+        float o[4];
         const float xv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (c + j < C) o[j] = (xv[j] - mu) * rs * gamma[c + j] + beta[c + j];
-          else if (c + j == one_col) o[j] = 1.f;   // ones column for the weight-gradient GEMM
-        }
+        for (int j = 0; j < 4; ++j) o[j] = (xv[j] - mu) * rs * ga[i][j] + be[i][j];   // pad columns: 0 (or the ones column)
         store4<T>(y + r * ldy + c, o[0], o[1], o[2], o[3]);
       }
     }
@@ -113,14 +120,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
     const long t = win_to_token(r, wm);
     const float mu = mean[t], rs = rstd[t];
     float xh[NV][4], gy[NV][4];
+    float4 cur[NV];   // the accumulated gradient row, loaded together with x and dy (one round trip)
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (sub + LPR * i) * 4;
       float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), dv = xv;
+      cur[i] = xv;
       if (c < C) {
         xv = *(const float4*)(x + t * ldx + c);
         dv = load4<T>(dy + r * ldy + c);
+        if (dx_acc) cur[i] = *(const float4*)(dx + t * ld_dx + c);
       }
       const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, da[4] = {dv.x, dv.y, dv.z, dv.w};
 #pragma unroll
@@ -137,22 +147,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
     }
     s1 = group_sum16(s1) / C;
     s2 = group_sum16(s2) / C;
+    // GEMM-operand copy row and scale: once per row
+    const float sc = cp && cp_scale ? cp_scale[(int)t / cp_rps] : 1.f;
+    const long cr = cp ? token_to_win(t, cwm) : 0;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (sub + LPR * i) * 4;
       if (c < C) {
         float* o = dx + t * ld_dx + c;
-        float4 cur = dx_acc ? *(const float4*)o : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 cu = cur[i];
         float d[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) d[j] = (c + j < C) ? rs * (gy[i][j] - s1 - xh[i][j] * s2) : 0.f;
-        cur.x += d[0]; cur.y += d[1]; cur.z += d[2]; cur.w += d[3];
-        *(float4*)o = cur;
+        cu.x += d[0]; cu.y += d[1]; cu.z += d[2]; cu.w += d[3];
+        *(float4*)o = cu;
         if (cp) {   // GEMM-operand copy of the finished gradient row: scaled, cast, optionally window-ordered
-          const float sc = cp_scale ? cp_scale[(int)t / cp_rps] : 1.f;
-          const long cr = token_to_win(t, cwm);
-          if (cp_dt == KAIR_BF16) store4<bf16>((bf16*)cp + cr * ldc + c, sc * cur.x, sc * cur.y, sc * cur.z, sc * cur.w);
-          else store4<float>((float*)cp + cr * ldc + c, sc * cur.x, sc * cur.y, sc * cur.z, sc * cur.w);
+          if (cp_dt == KAIR_BF16) store4<bf16>((bf16*)cp + cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w);
+          else store4<float>((float*)cp + cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w);
         }
       }
     }
