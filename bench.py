@@ -36,7 +36,12 @@ def build_net(dtype, drop_path=0.1, seed=0):
 
 def time_dominant_kernel(engine, reps=30):
     """HIP-event timing (torch's current stream = the stream the kernels launch on) of the QKV
-    projection GEMM of block 0 at the step's exact arguments.  Algorithmic FLOPs = 2*M*540*180."""
+    projection GEMM of block 0 at the step's exact arguments.
+
+    The projection is HBM-bound at these shapes (2*K*N/(K+N) = 135 FLOP/B against the MI355X ridge
+    of 2500 TFLOP/s / 8 TB/s = 312 FLOP/B), so its roofline is bytes: algorithmic bytes = the bf16
+    operand M x K, the bf16 weight N x K and the bf16 q/k/v output M x N, each moved once
+    (K = 180, N = 540: the unpadded layer)."""
     from kair_amd import _hip as H
     P = engine.cur
     blk, S = engine.blocks[0], P["blocks"][0]
@@ -57,8 +62,27 @@ def time_dominant_kernel(engine, reps=30):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     flops = 2.0 * M * l.N * l.K
-    return {"kernel": "gemm_nt_ring<192,5,0,1> (block QKV projection, network_swinir.py:121; rocprof name _ZN..gemm_nt_ringILi192ELi5ELi0ELi1E..)",
-            "ms": ms, "flops": flops, "M": M, "N": l.N, "K": l.K}
+    nbytes = 2.0 * (M * l.K + l.N * l.K + M * l.N)
+    return {"kernel": "gemm_nt_ring<192,5,0,1,0> (block QKV projection, network_swinir.py:121; rocprof name "
+                      "_ZN..gemm_nt_ringILi192ELi5ELi0ELi1ELi0E..)",
+            "rocprof_key": "gemm_nt_ring<192, 5, 0, 1, 0>",
+            "ms": ms, "flops": flops, "bytes": nbytes, "M": M, "N": l.N, "K": l.K}
+
+
+def pmc_traffic(key):
+    """HBM bytes per launch of kernel `key` from the committed rocprofv3 PMC summary
+    (profiles/r01_pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950
+    correction + WRITE_SIZE, KiB -> bytes), or None when absent."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+        for name, v in rec["kernels"].items():
+            if key in name:
+                return v["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        pass
+    return None
 
 
 def cpu_baseline(batch=2, steps=2):
@@ -199,7 +223,8 @@ def main():
     step_tflops = fl["train"] * gbatch / (wall / args.steps) / 1e12 / world   # per GPU
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     k = time_dominant_kernel(tr.engine)
-    ach = k["flops"] / (k["ms"] * 1e-3) / 1e12
+    ach_gbs = k["bytes"] / (k["ms"] * 1e-3) / 1e9
+    ach_tf = k["flops"] / (k["ms"] * 1e-3) / 1e12
     out = {
         "metric": "train patches/sec + PSNR, SwinIR x4 48-px LQ, at 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -209,10 +234,11 @@ def main():
                    "global_batch": gbatch, "per_gpu_batch": bpg, "lq": 48, "hr": 192, "embed_dim": 180,
                    "depths": [6] * 6, "heads": 6, "window": 8, "drop_path_rate": args.drop_path,
                    "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
-        "roofline": {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(ach / peak, 4), "traffic": None, "kernel": k["kernel"],
-                     "kernel_ms": round(k["ms"], 5), "flops_per_launch": k["flops"],
-                     "shape_MNK": [k["M"], k["N"], k["K"]]},
+        "roofline": {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(ach_gbs / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(k["rocprof_key"]),
+                     "kernel": k["kernel"], "kernel_ms": round(k["ms"], 5), "bytes_per_launch": k["bytes"],
+                     "flops_per_launch": k["flops"], "achieved_tflops": round(ach_tf, 2),
+                     "mfma_frac": round(ach_tf / peak, 4), "shape_MNK": [k["M"], k["N"], k["K"]]},
         "step_roofline": {"train_flop_per_patch": fl["train"], "achieved_tflops_per_gpu": round(step_tflops, 2),
                           "frac_of_bf16_peak": round(step_tflops / peak, 4)},
         "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
