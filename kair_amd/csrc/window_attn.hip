@@ -447,6 +447,203 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const typename AT<BF>::T*
       for (int r = 0; r < 16; ++r) out[(qt * 32 + acc_row(r, hh)) * TOK + kt * 32 + l31] = dB[qt][kt][r];
 }
 
+// ------------------------------------------------------------------------------------------
+// bf16 backward, software-pipelined.  Per wave: one head, a group of windows.  The q/k/v/dO/O
+// fragments of the NEXT window are loaded into registers (16-byte loads, the frag_cols layout the
+// S / dP products consume directly) while the current window is computed; q, k and dO are also
+// written to LDS for the transposed fragment reads of dV, dK and dQ.  delta = rowsum(dO o O)
+// comes from the register fragments (lane half + partner lane).  dV, dK and dQ are produced
+// transposed (D[d][token]: lane = token, 4 consecutive d per register group), so each lane
+// stores 8 bytes at a time instead of 2.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ O,
+                                                            long ldo, const bf16* __restrict__ dO, long lddo,
+                                                            const float* __restrict__ table, const float* __restrict__ lse,
+                                                            bf16* __restrict__ dqkv, float* __restrict__ dB_part,
+                                                            long nWin, int nh, int wpg, float scale, int H, int W,
+                                                            int shift) {
+  constexpr int LD = AT<true>::LD, LDD = 72, NW = 4;
+  __shared__ __attribute__((aligned(16))) bf16 sQ[NW][TOK * LD];
+  __shared__ __attribute__((aligned(16))) bf16 sK[NW][TOK * LD];
+  __shared__ __attribute__((aligned(16))) bf16 sG[NW][TOK * LD];
+  __shared__ __attribute__((aligned(16))) bf16 sdS[NW][TOK * LDD];
+  __shared__ float sTab[NW][232];
+  __shared__ float sRow[NW][2][TOK];  // lse, delta
+  __shared__ int sReg[NW][TOK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long gtask = (long)blockIdx.x * NW + w;
+  const long ngroups = (nWin + wpg - 1) / wpg;
+  if (gtask >= ngroups * nh) return;
+  const int h = (int)(gtask % nh);
+  const long grp = gtask / nh;
+  const long M = nWin * TOK;
+  const long part = M * nh * HDP;
+  const int l31 = lane & 31, hh = lane >> 5;
+  bf16* q = sQ[w]; bf16* k = sK[w]; bf16* go = sG[w]; bf16* ds = sdS[w];
+  for (int i = lane; i < (2 * WS - 1) * (2 * WS - 1); i += 64) sTab[w][i] = table[i * nh + h];
+  const int nW = (H / WS) * (W / WS);
+
+  f32x16 dB[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dB[a][b][r] = 0.f;
+
+  // register fragments of one window: rows t*32 + l31, columns 16 s + 8 hh
+  bf16x8 Fq[2][2], Fk[2][2], Fv[2][2], Fg[2][2], Fo[2][2];
+  float Fl[2];
+  auto ldfrag = [&](const bf16* g, long ld, bf16x8 (&f)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) f[t][s] = *(const bf16x8*)(g + (long)(t * 32 + l31) * ld + 16 * s + 8 * hh);
+  };
+  auto load_win = [&](long win) {
+    const long blk = (win * nh + h) * TOK * HDP;
+    ldfrag(qkv + blk, HDP, Fq);
+    ldfrag(qkv + part + blk, HDP, Fk);
+    ldfrag(qkv + 2 * part + blk, HDP, Fv);
+    ldfrag(dO + win * TOK * lddo + h * HDP, lddo, Fg);
+    ldfrag(O + win * TOK * ldo + h * HDP, ldo, Fo);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) Fl[t] = lse[(win * nh + h) * TOK + t * 32 + l31];
+  };
+
+  const long w0 = grp * wpg;
+  long w1 = w0 + wpg;
+  if (w1 > nWin) w1 = nWin;
+  load_win(w0);
+  for (long win = w0; win < w1; ++win) {
+    const long blk = (win * nh + h) * TOK * HDP;
+    wave_sync();   // the previous window's LDS tiles are no longer read
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int o = (t * 32 + l31) * LD + 16 * s + 8 * hh;
+        *(bf16x8*)(q + o) = Fq[t][s];
+        *(bf16x8*)(k + o) = Fk[t][s];
+        *(bf16x8*)(go + o) = Fg[t][s];
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float d = 0.f;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += (float)Fg[t][s][j] * (float)Fo[t][s][j];
+      d += __shfl_xor(d, 32, 64);
+      if (hh == 0) {
+        sRow[w][0][t * 32 + l31] = Fl[t];
+        sRow[w][1][t * 32 + l31] = d;
+      }
+    }
+    sReg[w][lane] = shift > 0 ? token_region((int)(win % nW), lane, H, W, shift) : 0;
+
+    // S = Q K^T and dP = dO V^T : tiles [qt][kt], lane = key, regs = query
+    f32x16 S[2][2], dP[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { S[a][b][r] = 0.f; dP[a][b][r] = 0.f; }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          S[qt][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fq[qt][s], Fk[kt][s], S[qt][kt], 0, 0, 0);
+          dP[qt][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fg[qt][s], Fv[kt][s], dP[qt][kt], 0, 0, 0);
+        }
+    // the next window's fragments load under the rest of this window's work
+    if (win + 1 < w1) load_win(win + 1);
+    wave_sync();
+
+    // P = exp(S*scale + bias + mask - lse) ; dS = P (dP - delta)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int ki = kt * 32 + l31;
+      const int rk = sReg[w][ki];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = qt * 32 + acc_row(r, hh);
+          float sc = S[qt][kt][r] * scale + sTab[w][relidx(qi, ki)];
+          if (shift > 0 && sReg[w][qi] != rk) sc += -100.f;
+          const float p = __expf(sc - sRow[w][0][qi]);
+          S[qt][kt][r] = p;
+          const float d = p * (dP[qt][kt][r] - sRow[w][1][qi]);
+          dP[qt][kt][r] = d;
+          dB[qt][kt][r] += d;
+        }
+    }
+    // dV^T = dO^T P and dK^T = scale * Q^T dS : tiles [kt], rows = d, lane = key
+    bf16* dq_out = dqkv + blk;
+    bf16* dk_out = dqkv + part + blk;
+    bf16* dv_out = dqkv + 2 * part + blk;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      f32x16 av, ak;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { av[r] = 0.f; ak[r] = 0.f; }
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          av = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_rows_perm(go, qt * 32, s, lane), pack8(S[qt][kt], s), av, 0, 0, 0);
+          ak = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_rows_perm(q, qt * 32, s, lane), pack8(dP[qt][kt], s), ak, 0, 0, 0);
+        }
+      const int key = kt * 32 + l31;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const bf16x4 vv = {(bf16)av[4 * g], (bf16)av[4 * g + 1], (bf16)av[4 * g + 2], (bf16)av[4 * g + 3]};
+        const bf16x4 kk = {(bf16)(ak[4 * g] * scale), (bf16)(ak[4 * g + 1] * scale), (bf16)(ak[4 * g + 2] * scale),
+                           (bf16)(ak[4 * g + 3] * scale)};
+        *(bf16x4*)(dv_out + key * HDP + 8 * g + 4 * hh) = vv;
+        *(bf16x4*)(dk_out + key * HDP + 8 * g + 4 * hh) = kk;
+      }
+    }
+    // dQ^T = scale * K^T dS^T : dS through LDS ([q][key] row-major)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ds[(qt * 32 + acc_row(r, hh)) * LDD + kt * 32 + l31] = (bf16)dP[qt][kt][r];
+    wave_sync();
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 aq;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) aq[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        aq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_rows_nat(k, 0, s, lane), frag_cols(ds, LDD, qt * 32 + l31, s, lane),
+                                                    aq, 0, 0, 0);
+      const int qi = qt * 32 + l31;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const bf16x4 vq = {(bf16)(aq[4 * g] * scale), (bf16)(aq[4 * g + 1] * scale), (bf16)(aq[4 * g + 2] * scale),
+                           (bf16)(aq[4 * g + 3] * scale)};
+        *(bf16x4*)(dq_out + qi * HDP + 8 * g + 4 * hh) = vq;
+      }
+    }
+  }
+  // partial bias gradient of this (group, head): [q][key]
+  float* out = dB_part + (grp * nh + h) * TOK * TOK;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[(qt * 32 + acc_row(r, hh)) * TOK + kt * 32 + l31] = dB[qt][kt][r];
+}
+
 // stage 1: dB[h][q][k] = sum over groups of the per-group partials (coalesced, one thread per entry)
 __global__ __launch_bounds__(1024) void attn_dbias_sum_kernel(const float* __restrict__ dB_part, long ngroups, int nh,
                                                               float* __restrict__ dB) {
@@ -510,11 +707,11 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)), "window_attn_bwd: geometry");
   KAIR_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0, "window_attn_bwd: strides");
   const long ngroups = (nWin + WPG - 1) / WPG;
-  const int nw = dtype == KAIR_BF16 ? NWAVES<true> : NWAVES<false>;
+  const int nw = dtype == KAIR_BF16 ? 4 : NWAVES<false>;
   const long nb = (ngroups * nh + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(attn_bwd_kernel<true>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
+    hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
                        (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, WPG, scale, H, W, shift);
   else
     hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
