@@ -669,7 +669,24 @@ __global__ __launch_bounds__(256) void attn_dtable_kernel(const float* __restric
   if (lane == 0) dtable[idx * nh + h] = acc ? dtable[idx * nh + h] + v : v;
 }
 
-constexpr int WPG = 4;  // windows per backward wave
+constexpr int WPG = 4;  // windows per backward wave (fp32 parity path)
+
+// bf16 backward: windows per wave so that the (group, head) waves fill every CU's 4 wave slots in
+// one round (1 wave per SIMD: the kernel holds ~500 VGPRs) -- e.g. 1152 windows x 6 heads on 256
+// CUs -> 7 windows per wave, 990 waves
+static int bwd_wpg_bf16(long nWin, int nh) {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      ncu = n;
+    if (ncu <= 0) ncu = 256;
+  }
+  const long slots = 4L * ncu;
+  const long w = (nWin * nh + slots - 1) / slots;
+  return (int)(w < 1 ? 1 : w);
+}
+static long bwd_groups(long nWin, int wpg) { return (nWin + wpg - 1) / wpg; }
 
 }  // namespace
 
@@ -696,7 +713,10 @@ extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* tab
   return 0;
 }
 
-extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) { return ((nWin + WPG - 1) / WPG + 1) * nh * TOK * TOK; }
+extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) {
+  const long g32 = bwd_groups(nWin, WPG), g16 = bwd_groups(nWin, bwd_wpg_bf16(nWin, nh));
+  return ((g32 > g16 ? g32 : g16) + 1) * nh * TOK * TOK;
+}
 
 extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
                                     const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
@@ -706,16 +726,17 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
   KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_bwd: head_dim");
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)), "window_attn_bwd: geometry");
   KAIR_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0, "window_attn_bwd: strides");
-  const long ngroups = (nWin + WPG - 1) / WPG;
+  const int wpg = dtype == KAIR_BF16 ? bwd_wpg_bf16(nWin, nh) : WPG;
+  const long ngroups = bwd_groups(nWin, wpg);
   const int nw = dtype == KAIR_BF16 ? 4 : NWAVES<false>;
   const long nb = (ngroups * nh + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
     hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
-                       (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, WPG, scale, H, W, shift);
+                       (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift);
   else
     hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
-                       ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, WPG, scale, H, W, shift);
+                       ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift);
   KAIR_CHECK_LAUNCH();
   float* dB = ws + ngroups * nh * TOK * TOK;
   hipLaunchKernelGGL(attn_dbias_sum_kernel, dim3((nh * TOK * TOK + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dB);
