@@ -550,14 +550,24 @@ KAIR_DEV void st4_any(void* p, int dt, long off, const float (&v)[4]) {
   }
 }
 
+// 16-byte store with a cache policy: 0 plain, 1 nt, 2 sc1 (write-through)
+typedef unsigned __attribute__((ext_vector_type(4))) u32x4;
+KAIR_DEV void st16_pol(void* p, u32x4 v, int pol) {
+  if (pol == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+  else if (pol == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else *(u32x4*)p = v;
+}
+
 // 8 consecutive columns: one 16-byte store for bf16, two for fp32
-KAIR_DEV void st8_any(void* p, int dt, long off, const float (&v)[8]) {
+KAIR_DEV void st8_any(void* p, int dt, long off, const float (&v)[8], int pol = 0) {
   if (dt == KAIR_BF16) {
     const bf16x8 q = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
-    *(bf16x8*)((bf16*)p + off) = q;
+    st16_pol((bf16*)p + off, __builtin_bit_cast(u32x4, q), pol);
   } else {
-    *(float4*)((float*)p + off) = make_float4(v[0], v[1], v[2], v[3]);
-    *(float4*)((float*)p + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    const u32x4 a = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+    const u32x4 b = {__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
+    st16_pol((float*)p + off, a, pol);
+    st16_pol((float*)p + off + 4, b, pol);
   }
 }
 
@@ -826,13 +836,14 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
     for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   static_assert(NS == 5, "the store bookkeeping below assumes chunk j is issued at iteration j-4");
-  int sq1 = 0, sq2 = 0, sq3 = 0;   // store instructions this wave issued at iterations j-1, j-2, j-3
+  int sq1 = 0, sq2 = 0, sq3 = 0, sq4 = 0;   // store instructions this wave issued at iterations j-1 .. j-4
+  const bool early = (E.dbg & 32) != 0;     // tile end: issue the deferred chunk before the stores
   int kc = 0, cs = 0, ct = 0;      // consumer cursor: chunk j = ct * nk + kc, in stage cs
   for (int j = 0; j < total; ++j) {
     // chunk j landed for this wave: younger than it are min(NS-2, total-1-j) chunks (2 DMA
     // instructions each) and the stores of the epilogues run at iterations j-3 .. j-1
     const int ahead = (total - 1 - j) < (NS - 2) ? (total - 1 - j) : (NS - 2);
-    vm_wait(2 * ahead + sq1 + sq2 + sq3);
+    vm_wait(2 * ahead + sq1 + sq2 + sq3 + (early ? sq4 : 0));
     ring_barrier();   // every wave's part of chunk j is in LDS; stage (j-1)%NS is free
     const bool tile_end = kc == nk - 1;
     if (!tile_end && lj < total) issue_next();   // lj == j + NS - 1
@@ -855,6 +866,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
           acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
     }
     int sj = 0;
+    const int pol = (E.dbg >> 3) & 3;
+    if (tile_end && early && lj < total) issue_next();
     if (tile_end) {
       // Epilogue from registers: fragment pairs are re-laid by v_permlane16_swap so each lane
       // holds 8 consecutive columns of one row; every epilogue load is issued before the first
@@ -919,7 +932,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
           for (int c = 0; c < 8; ++c) v[c] += b8[c];
           if constexpr (EM == EM_QKV) {
             const long off = colo[p] + (long)rowv[i] * E.hdp;
-            if (ok) st8_any(E.out, E.odt, off, v);
+            if (ok) st8_any(E.out, E.odt, off, v, pol);
             sj += __ballot(ok) != 0 ? 1 : 0;
           } else {
             float pre[8];
@@ -953,8 +966,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
             }
             const long rr = rowv[i];
             if (ok) {
-              st8_any(E.out, E.odt, rr * E.ldo + n, v);
-              if (E.pre) st8_any(E.pre, E.pdt, rr * E.ldp + n, pre);
+              st8_any(E.out, E.odt, rr * E.ldo + n, v, pol);
+              if (E.pre) st8_any(E.pre, E.pdt, rr * E.ldp + n, pre, pol);
             }
             sj += __ballot(ok) != 0 ? st_per_frag : 0;
           }
@@ -963,9 +976,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (lj < total) issue_next();
+      if (!early && lj < total) issue_next();
     }
-    sq3 = sq2; sq2 = sq1; sq1 = sj;
+    sq4 = sq3; sq3 = sq2; sq2 = sq1; sq1 = sj;
     if (++kc == nk) { kc = 0; ++ct; }
     if (++cs == NS) cs = 0;
   }
@@ -1256,6 +1269,8 @@ int launch_nt(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipS
 
 static int g_num_cus = 0;
 static int g_ring_mode = -1;
+// KAIR_CONV_HALO=0 disables the halo 3x3 conv kernel (A/B timing only)
+static const int g_halo_mode = getenv("KAIR_CONV_HALO") && getenv("KAIR_CONV_HALO")[0] == '0' ? 0 : 1;
 static long g_ring_min_tiles = -1;
 
 static void init_num_cus() {
@@ -1343,8 +1358,236 @@ int ring_bn(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStr
   return launch_ring<64, 5, AM>(A, B, E, M, N, K, s);
 }
 
+// ------------------------------------------------------------------------------------------
+// 3x3 conv (stride 1, pad 1; forward, or input gradient with flipped taps) as implicit GEMM with
+// the input tile's halo resident in LDS.  Tile = 96 output pixels (96/W whole image rows of width
+// W <= 96, or 96 pixels of a wider row) x all N <= 192 output channels; one 512-thread CTA per CU,
+// persistent over tiles.  Each input pixel is fetched once per tile instead of once per tap (the
+// register-staged im2col GEMM re-reads it 9 times and is L2-bandwidth bound); the weights
+// [N][9 Cin] stream through a double-buffered LDS stage, two k-steps ahead in registers.
+// MFMA operands swapped (D = W . X^T) so each lane finishes 4 consecutive channels of a pixel.
+// ------------------------------------------------------------------------------------------
+constexpr int HC_BM = 96, HC_BN = 192, HC_BK = 64;
+constexpr int HC_HALO_ELEMS = 40960;   // bf16 elements: (RPT + 2) x (XW + 2) x (Cin + 8)
+constexpr int HC_PER = HC_HALO_ELEMS / 8 / 512;
+
+template <typename TA, int EX>
+__global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E, int K, int tilesM) {
+  constexpr int WM = 2, WN = 4, TM = HC_BM / WM, TN = HC_BN / WN, RM = TM / 16, RN = TN / 16;
+  __shared__ __attribute__((aligned(16))) bf16 sHalo[HC_HALO_ELEMS];
+  __shared__ __attribute__((aligned(16))) bf16 sBw[2][HC_BN * HC_BK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int H = A.imH, W = A.imW, C = A.imC;
+  const int XW = W < HC_BM ? W : HC_BM, RPT = HC_BM / XW, HWD = XW + 2, HR = RPT + 2, PS = C + 8;
+  const int cpt = C / HC_BK, nks = 9 * cpt, c8n = C / 8;
+  const int halo_pieces = HR * HWD * c8n;
+  const bf16* Bp = (const bf16*)B.ptr;
+  const TA* Ap = (const TA*)A.ptr;
+  const int N = E.N;
+
+  // per-lane constants: halo element offset of each fragment row's centre pixel, weight rows
+  int hb[RM];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int row = wm * TM + i * 16 + fr;
+    const int ry = row / XW, rx = row - (row / XW) * XW;
+    hb[i] = ((ry + 1) * HWD + rx + 1) * PS;
+  }
+  int nrow[RN];
+#pragma unroll
+  for (int jn = 0; jn < RN; ++jn) nrow[jn] = wn * TN + jn * 16 + fr;
+  float4 bias4[RN];
+#pragma unroll
+  for (int jn = 0; jn < RN; ++jn) {
+    const int n = wn * TN + jn * 16 + fq * 4;
+    bias4[jn] = *(const float4*)(E.bias && n < N ? E.bias + n : (const float*)g_kair_zero_line);
+  }
+#pragma unroll
+  for (int jn = 0; jn < RN; ++jn) land(bias4[jn]);
+
+  // weight chunk j (192 rows x 64 k): 1536 16-byte pieces, 3 per thread; rows >= N read as zero
+  auto bload = [&](int j, uint4 (&r)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int idx = tid + 512 * p, row = idx >> 3, q = idx & 7;
+      const bool ok = row < N;
+      const uint4 v = *(const uint4*)(Bp + (long)(ok ? row : 0) * B.ld + j * HC_BK + q * 8);
+      r[p] = ok ? v : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto bstore = [&](int buf, const uint4 (&r)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int idx = tid + 512 * p, row = idx >> 3, q = idx & 7;
+      *(uint4*)(&sBw[buf][row * HC_BK + ((q ^ (row & 7)) << 3)]) = r[p];
+    }
+  };
+  f32x4 acc[RM][RN];
+  auto compute = [&](int buf, int j) {
+    const int tap = j / cpt, cc = j - tap * cpt;
+    int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    if (A.flip) { dy = -dy; dx = -dx; }
+    const int hoff = (dy * HWD + dx) * PS + cc * HC_BK;
+#pragma unroll
+    for (int ks = 0; ks < HC_BK / 32; ++ks) {
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sHalo + hb[i] + hoff + ks * 32 + fq * 8);
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn)
+        bfr[jn] = *(const bf16x8*)(&sBw[buf][nrow[jn] * HC_BK + (((ks * 4 + fq) ^ (nrow[jn] & 7)) << 3)]);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn)
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
+    }
+  };
+
+  uint4 RA[3], RB[3];
+  for (int t = blockIdx.x; t < tilesM; t += gridDim.x) {
+    const long p0 = (long)t * HC_BM;
+    const int b = (int)(p0 / ((long)H * W));
+    const int rem = (int)(p0 - (long)b * H * W);
+    const int y0 = rem / W, x0 = rem - (rem / W) * W;
+    // halo of this tile (every wave finished the previous tile's reads before its last barrier):
+    // all loads first, then the converts and LDS writes
+    {
+      uint4 hv[HC_PER];
+#pragma unroll
+      for (int i = 0; i < HC_PER; ++i) {
+        const int idx = tid + 512 * i;
+        const int pix = idx / c8n, c8 = idx - (idx / c8n) * c8n;
+        const int hr = pix / HWD, hc = pix - (pix / HWD) * HWD;
+        const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+        const bool ok = idx < halo_pieces && y >= 0 && y < H && x >= 0 && x < W;
+        const long src = ok ? ((long)(b * H + y) * W + x) * A.ld + c8 * 8 : 0;
+        if constexpr (sizeof(TA) == 4) {
+          float4 u = *(const float4*)(Ap + src), v = *(const float4*)(Ap + src + 4);
+          if (!ok) u = v = make_float4(0.f, 0.f, 0.f, 0.f);
+          const bf16x8 q = {(bf16)u.x, (bf16)u.y, (bf16)u.z, (bf16)u.w, (bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+          hv[i] = __builtin_bit_cast(uint4, q);
+        } else {
+          const uint4 v = *(const uint4*)(Ap + src);
+          hv[i] = ok ? v : make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < HC_PER; ++i) {
+        const int idx = tid + 512 * i;
+        if (idx < halo_pieces) {
+          const int pix = idx / c8n, c8 = idx - (idx / c8n) * c8n;
+          *(uint4*)(sHalo + pix * PS + c8 * 8) = hv[i];
+        }
+      }
+    }
+    bload(0, RA);
+    if (1 < nks) bload(1, RB);
+    bstore(0, RA);
+    if (2 < nks) bload(2, RA);
+    __syncthreads();   // halo + weight chunk 0 visible
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < nks; j += 2) {
+      // even step: sBw[0] = W(j); RB = W(j+1), RA = W(j+2) in flight
+      if (j + 1 < nks) bstore(1, RB);
+      compute(0, j);
+      __syncthreads();
+      if (j + 3 < nks) bload(j + 3, RB);
+      if (j + 1 >= nks) break;
+      // odd step: sBw[1] = W(j+1); RA = W(j+2), RB = W(j+3) in flight
+      if (j + 2 < nks) bstore(0, RA);
+      compute(1, j + 1);
+      __syncthreads();
+      if (j + 4 < nks) bload(j + 4, RA);
+    }
+    // epilogue: bias (+ act) (+ fp32 residual), 4 consecutive channels per lane
+    float4 ex[RM][RN];
+    if constexpr (EX == EX_RESID) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) {
+          const long m = p0 + wm * TM + i * 16 + fr;
+          const int n = wn * TN + jn * 16 + fq * 4;
+          ex[i][jn] = *(const float4*)(E.resid + m * E.ldr + (n < N ? n : 0));
+        }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) land(ex[i][jn]);
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn) {
+        const long m = p0 + wm * TM + i * 16 + fr;
+        const int n = wn * TN + jn * 16 + fq * 4;
+        const float4 bb = bias4[jn];
+        float v[4] = {acc[i][jn][0] + bb.x, acc[i][jn][1] + bb.y, acc[i][jn][2] + bb.z, acc[i][jn][3] + bb.w};
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          if (E.act == KAIR_ACT_GELU) v[q4] = gelu_fast(v[q4]);
+          else if (E.act == KAIR_ACT_LEAKY) v[q4] = v[q4] > 0.f ? v[q4] : v[q4] * E.slope;
+          else if (E.act == KAIR_ACT_RELU) v[q4] = fmaxf(v[q4], 0.f);
+        }
+        if constexpr (EX == EX_RESID) {
+          v[0] += ex[i][jn].x; v[1] += ex[i][jn].y; v[2] += ex[i][jn].z; v[3] += ex[i][jn].w;
+        }
+        if (E.ones_col >= n && E.ones_col < n + 4) {
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4)
+            if (n + q4 == E.ones_col) v[q4] = 1.f;
+        }
+        if (n < N) st4_any(E.out, E.odt, m * E.ldo + n, v);
+      }
+  }
+}
+
+// halo conv applicability (host): geometry, epilogue features and alignment the kernel assumes
+template <typename TA>
+static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, int K) {
+  const int H = A.imH, W = A.imW, C = A.imC;
+  if (A.up_sh != 0 || C % HC_BK != 0 || C > 192 || K != 9 * C || N > HC_BN || N % 4 != 0) return false;
+  if (W <= 0 || H <= 0) return false;
+  if (W <= HC_BM) {
+    if (HC_BM % W != 0 || H % (HC_BM / W) != 0) return false;
+  } else if (W % HC_BM != 0) {
+    return false;
+  }
+  const int XW = W < HC_BM ? W : HC_BM, RPT = HC_BM / XW;
+  if ((long)(RPT + 2) * (XW + 2) * (C + 8) > HC_HALO_ELEMS) return false;
+  if (M % HC_BM != 0 || M % ((long)H * W) != 0) return false;
+  if (A.ld % 8 != 0 || ((unsigned long)A.ptr & 15) || B.ld % 8 != 0 || ((unsigned long)B.ptr & 15)) return false;
+  if (e.omode != KAIR_OUT_ROWS || e.win.ws != 0 || e.gate || e.pre || e.resid2 || e.rowscale) return false;
+  if (e.ldo % 4 != 0 || ((unsigned long)e.out & 15) || (e.resid && (e.ldr % 4 != 0 || ((unsigned long)e.resid & 15))))
+    return false;
+  return true;
+}
+
+template <typename TA>
+static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int K, hipStream_t s) {
+  if (g_num_cus == 0) init_num_cus();
+  const int tilesM = (int)(M / HC_BM);
+  const int grid = tilesM < g_num_cus ? tilesM : g_num_cus;
+  if (E.resid)
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_RESID>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
+  else
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
 template <typename CT, typename TA>
 int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
+  if constexpr (sizeof(CT) == 2) {
+    if (mode == KAIR_LD_IM2COL3 && g_halo_mode != 0 && conv_halo_ok<TA>(A, B, E, M, N, K))
+      return launch_conv_halo<TA>(A, B, E, M, K, s);
+  }
   if constexpr (sizeof(CT) == 2 && sizeof(TA) == 2) {
     if (g_ring_mode < 0) {   // KAIR_GEMM_RING=0 disables the LDS-DMA ring kernel (A/B timing only)
       const char* v = getenv("KAIR_GEMM_RING");
@@ -1478,7 +1721,8 @@ extern "C" int kair_wgrad_splits(long M, int N, int K) {
     if (g_num_cus == 0) init_num_cus();
     const int tiles = ((N + TNR_BN - 1) / TNR_BN) * ((K + TNR_BK - 1) / TNR_BK);
     long s = g_num_cus / tiles;
-    const long maxs = (M + 255) / 256;
+    static const long min_rows = getenv("KAIR_TN_ROWS") ? atol(getenv("KAIR_TN_ROWS")) : 256;   // A/B knob
+    const long maxs = (M + min_rows - 1) / min_rows;
     if (s > maxs) s = maxs;
     return (int)(s < 1 ? 1 : s);
   }

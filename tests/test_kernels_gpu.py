@@ -97,6 +97,40 @@ def test_conv3x3_implicit_gemm(compute, flip):
     assert rel_err(got, ref) < TOL[compute][0]
 
 
+@pytest.mark.parametrize("shape", [(2, 48, 48, 192, 192), (1, 12, 96, 64, 64), (1, 6, 192, 64, 180), (3, 24, 32, 128, 96)])
+@pytest.mark.parametrize("flip", [False, True])
+@pytest.mark.parametrize("a_f32", [False, True])
+@pytest.mark.parametrize("resid", [False, True])
+def test_conv3x3_halo_path(shape, flip, a_f32, resid):
+    """bf16 3x3 convs whose geometry selects the LDS-halo kernel (W | 96 or 96 | W, Cin % 64 == 0,
+    N <= 192): fp32 or bf16 input rows, forward or flipped taps, bias + optional fp32 residual."""
+    B, Hh, Ww, Cin, Cout = shape
+    g = torch.Generator().manual_seed(Hh * Ww + Cin)
+    x = torch.randn(B, Cin, Hh, Ww, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.05).bfloat16().float()
+    bias = torch.randn(Cout, generator=g)
+    r = torch.randn(B * Hh * Ww, Cout, generator=g)
+    if flip:
+        ref = torch.nn.functional.conv_transpose2d(x, w.transpose(0, 1).contiguous(), padding=1)
+        packed = w.transpose(0, 1).contiguous().permute(1, 2, 3, 0).reshape(Cout, 9 * Cin)
+    else:
+        ref = torch.nn.functional.conv2d(x, w, padding=1)
+        packed = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
+    ref = ref + bias.view(1, -1, 1, 1)
+    xin = x.permute(0, 2, 3, 1).contiguous().view(B * Hh * Ww, Cin)
+    M = B * Hh * Ww
+    out = torch.empty(M, Cout, device=dev)
+    A = xin.to(dev, torch.float32 if a_f32 else torch.bfloat16)
+    H.gemm_nt(H.im2col(A, Hh, Ww, Cin, flip=flip), H.rows(packed.to(dev, torch.bfloat16)),
+              H.epilogue(out, bias=bias.to(dev), resid=r.to(dev) if resid else None), M, Cout, 9 * Cin, H.BF16)
+    torch.cuda.synchronize()
+    got = out.cpu()
+    if resid:
+        got = got - r
+    got = got.view(B, Hh, Ww, Cout).permute(0, 3, 1, 2)
+    assert rel_err(got, ref) < 1e-2
+
+
 @pytest.mark.parametrize("compute", [H.F32, H.BF16])
 def test_conv_pixelshuffle_and_nchw(compute):
     B, Hh, Ww, Cin, r = 2, 8, 8, 16, 2
