@@ -1375,7 +1375,7 @@ template <typename TA, int EX>
 __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E, int K, int tilesM) {
   constexpr int WM = 2, WN = 4, TM = HC_BM / WM, TN = HC_BN / WN, RM = TM / 16, RN = TN / 16;
   __shared__ __attribute__((aligned(16))) bf16 sHalo[HC_HALO_ELEMS];
-  __shared__ __attribute__((aligned(16))) bf16 sBw[2][HC_BN * HC_BK];
+  __shared__ __attribute__((aligned(16))) bf16 sBw[3][HC_BN * HC_BK];   // LDS-DMA ring of weight chunks
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fq = lane >> 4;
@@ -1407,21 +1407,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
 #pragma unroll
   for (int jn = 0; jn < RN; ++jn) land(bias4[jn]);
 
-  // weight chunk j (192 rows x 64 k): 1536 16-byte pieces, 3 per thread; rows >= N read as zero
-  auto bload = [&](int j, uint4 (&r)[3]) {
+  // weight chunk j (192 rows x 64 k = 24 KiB) -> ring stage j % 3 by LDS-DMA: 3 wave-instructions
+  // per wave, each 8 rows x 128 B; source pieces XOR-swizzled by row so the fragment reads are
+  // conflict-light.  Rows >= N re-read row N-1: they only feed output columns >= N, never stored.
+  auto bissue = [&](int j) {
+    char* st = (char*)sBw[j % 3];
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      const int idx = tid + 512 * p, row = idx >> 3, q = idx & 7;
-      const bool ok = row < N;
-      const uint4 v = *(const uint4*)(Bp + (long)(ok ? row : 0) * B.ld + j * HC_BK + q * 8);
-      r[p] = ok ? v : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto bstore = [&](int buf, const uint4 (&r)[3]) {
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      const int idx = tid + 512 * p, row = idx >> 3, q = idx & 7;
-      *(uint4*)(&sBw[buf][row * HC_BK + ((q ^ (row & 7)) << 3)]) = r[p];
+    for (int ii = 0; ii < 3; ++ii) {
+      const int r = (wave * 3 + ii) * 8 + (lane >> 3), q = lane & 7;
+      const int rr = r < N ? r : N - 1;
+      glds16(Bp + (long)rr * B.ld + j * HC_BK + ((q ^ (r & 7)) << 3), st + (wave * 3 + ii) * 1024);
     }
   };
   f32x4 acc[RM][RN];
@@ -1446,64 +1441,71 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
     }
   };
 
-  uint4 RA[3], RB[3];
   for (int t = blockIdx.x; t < tilesM; t += gridDim.x) {
     const long p0 = (long)t * HC_BM;
     const int b = (int)(p0 / ((long)H * W));
     const int rem = (int)(p0 - (long)b * H * W);
     const int y0 = rem / W, x0 = rem - (rem / W) * W;
-    // halo of this tile (every wave finished the previous tile's reads before its last barrier):
+    __syncthreads();   // every wave is done reading the previous tile's halo and ring
+    // halo of this tile:
     // all loads first, then the converts and LDS writes
     {
-      uint4 hv[HC_PER];
+      // (1) every load issued unconditionally (clamped address), (2) landed in order, (3) masked,
+      // converted and written: a load whose value a path ignores becomes a branch + wait each
+      constexpr int HP = 5;   // pieces per batch (register budget for fp32 pieces)
 #pragma unroll
-      for (int i = 0; i < HC_PER; ++i) {
-        const int idx = tid + 512 * i;
-        const int pix = idx / c8n, c8 = idx - (idx / c8n) * c8n;
-        const int hr = pix / HWD, hc = pix - (pix / HWD) * HWD;
-        const int y = y0 - 1 + hr, x = x0 - 1 + hc;
-        const bool ok = idx < halo_pieces && y >= 0 && y < H && x >= 0 && x < W;
-        const long src = ok ? ((long)(b * H + y) * W + x) * A.ld + c8 * 8 : 0;
-        if constexpr (sizeof(TA) == 4) {
-          float4 u = *(const float4*)(Ap + src), v = *(const float4*)(Ap + src + 4);
-          if (!ok) u = v = make_float4(0.f, 0.f, 0.f, 0.f);
-          const bf16x8 q = {(bf16)u.x, (bf16)u.y, (bf16)u.z, (bf16)u.w, (bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
-          hv[i] = __builtin_bit_cast(uint4, q);
-        } else {
-          const uint4 v = *(const uint4*)(Ap + src);
-          hv[i] = ok ? v : make_uint4(0, 0, 0, 0);
-        }
-      }
+      for (int h0 = 0; h0 < HC_PER; h0 += HP) {
+        uint4 lo[HP], hi[HP];
+        bool okv[HP];
 #pragma unroll
-      for (int i = 0; i < HC_PER; ++i) {
-        const int idx = tid + 512 * i;
-        if (idx < halo_pieces) {
+        for (int i = 0; i < HP; ++i) {
+          const int idx = tid + 512 * (h0 + i);
           const int pix = idx / c8n, c8 = idx - (idx / c8n) * c8n;
-          *(uint4*)(sHalo + pix * PS + c8 * 8) = hv[i];
+          const int hr = pix / HWD, hc = pix - (pix / HWD) * HWD;
+          const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+          okv[i] = idx < halo_pieces && y >= 0 && y < H && x >= 0 && x < W;
+          const long src = okv[i] ? ((long)(b * H + y) * W + x) * A.ld + c8 * 8 : 0;
+          lo[i] = *(const uint4*)(Ap + src);
+          if constexpr (sizeof(TA) == 4) hi[i] = *(const uint4*)(Ap + src + 4);
+        }
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+          asm volatile("" : "+v"(lo[i].x), "+v"(lo[i].y), "+v"(lo[i].z), "+v"(lo[i].w));
+          if constexpr (sizeof(TA) == 4) asm volatile("" : "+v"(hi[i].x), "+v"(hi[i].y), "+v"(hi[i].z), "+v"(hi[i].w));
+        }
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+          const int idx = tid + 512 * (h0 + i);
+          uint4 q;
+          if constexpr (sizeof(TA) == 4) {
+            const float4 u = __builtin_bit_cast(float4, lo[i]), v = __builtin_bit_cast(float4, hi[i]);
+            const bf16x8 qq = {(bf16)u.x, (bf16)u.y, (bf16)u.z, (bf16)u.w, (bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+            q = __builtin_bit_cast(uint4, qq);
+          } else {
+            q = lo[i];
+          }
+          if (!okv[i]) q = make_uint4(0, 0, 0, 0);
+          if (idx < halo_pieces) {
+            const int pix = idx / c8n, c8 = idx - (idx / c8n) * c8n;
+            *(uint4*)(sHalo + pix * PS + c8 * 8) = q;
+          }
         }
       }
     }
-    bload(0, RA);
-    if (1 < nks) bload(1, RB);
-    bstore(0, RA);
-    if (2 < nks) bload(2, RA);
-    __syncthreads();   // halo + weight chunk 0 visible
+    __syncthreads();   // halo visible
+    bissue(0);
+    if (1 < nks) bissue(1);
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
       for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < nks; j += 2) {
-      // even step: sBw[0] = W(j); RB = W(j+1), RA = W(j+2) in flight
-      if (j + 1 < nks) bstore(1, RB);
-      compute(0, j);
-      __syncthreads();
-      if (j + 3 < nks) bload(j + 3, RB);
-      if (j + 1 >= nks) break;
-      // odd step: sBw[1] = W(j+1); RA = W(j+2), RB = W(j+3) in flight
-      if (j + 2 < nks) bstore(0, RA);
-      compute(1, j + 1);
-      __syncthreads();
-      if (j + 4 < nks) bload(j + 4, RA);
+    for (int j = 0; j < nks; ++j) {
+      // chunk j landed for this wave (younger: chunk j+1's 3 DMA instructions), then all waves
+      if (j + 1 < nks) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ring_barrier();   // chunk j visible; stage (j+2) % 3 = (j-1) % 3 is free
+      if (j + 2 < nks) bissue(j + 2);
+      compute(j % 3, j);
     }
     // epilogue: bias (+ act) (+ fp32 residual), 4 consecutive channels per lane
     float4 ex[RM][RN];
