@@ -241,6 +241,123 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename AT<BF>::T*
 }
 
 // ------------------------------------------------------------------------------------------
+// bf16 forward: q / k fragments straight from global into registers (the frag_cols layout the
+// S^T = K Q^T product consumes), only v staged in LDS (for the transposed P.V fragments), so a
+// wave needs 6 KiB of LDS and 8 waves fit a CU; O is produced transposed (O^T = V^T P^T: lane =
+// query, 4 consecutive d per register group) and stored 8 bytes at a time.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(const bf16* __restrict__ qkv, const float* __restrict__ table,
+                                                            bf16* __restrict__ O, long ldo, float* __restrict__ lse,
+                                                            long nWin, int nh, float scale, int H, int W, int shift,
+                                                            int ones_col) {
+  constexpr int LD = AT<true>::LD, NW = 4;
+  __shared__ __attribute__((aligned(16))) bf16 sV[NW][TOK * LD];
+  __shared__ float sTab[NW][232];
+  __shared__ int sReg[NW][TOK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long task = (long)blockIdx.x * NW + w;
+  if (task >= nWin * nh) return;
+  const long win = task / nh;
+  const int h = (int)(task - win * nh);
+  const long M = nWin * TOK;
+  const long blk = (win * nh + h) * TOK * HDP;
+  const long part = M * nh * HDP;
+  const int l31 = lane & 31, hh = lane >> 5;
+  bf16x8 Fq[2][2], Fk[2][2], Fv[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const long o = (long)(t * 32 + l31) * HDP + 16 * s + 8 * hh;
+      Fq[t][s] = *(const bf16x8*)(qkv + blk + o);
+      Fk[t][s] = *(const bf16x8*)(qkv + part + blk + o);
+      Fv[t][s] = *(const bf16x8*)(qkv + 2 * part + blk + o);
+    }
+  bf16* v = sV[w];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) *(bf16x8*)(v + (t * 32 + l31) * LD + 16 * s + 8 * hh) = Fv[t][s];
+  for (int i = lane; i < (2 * WS - 1) * (2 * WS - 1); i += 64) sTab[w][i] = table[i * nh + h];
+  const int nW = (H / WS) * (W / WS);
+  sReg[w][lane] = shift > 0 ? token_region((int)(win % nW), lane, H, W, shift) : 0;
+
+  // S^T = K Q^T : tiles [kt][qt], lane column = query, registers = keys
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+        acc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fk[kt][s], Fq[qt][s], acc[kt][qt], 0, 0, 0);
+  wave_sync();
+  // scores: scale, bias, mask ; softmax over keys (registers + lane^32)
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = qt * 32 + l31;
+    const int rq = sReg[w][qi];
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ki = kt * 32 + acc_row(r, hh);
+        float sc = acc[kt][qt][r] * scale + sTab[w][relidx(qi, ki)];
+        if (shift > 0 && sReg[w][ki] != rq) sc += -100.f;
+        acc[kt][qt][r] = sc;
+        mx = fmaxf(mx, sc);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __expf(acc[kt][qt][r] - mx);
+        acc[kt][qt][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[kt][qt][r] *= inv;
+    if (hh == 0) lse[task * TOK + qi] = mx + __logf(sum);
+  }
+  // O^T = V^T P^T : tile [qt] rows = d, lane = query
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    f32x16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_rows_perm(v, kt * 32, s, lane), pack8(acc[kt][qt], s), o, 0, 0, 0);
+    const int qi = qt * 32 + l31;
+    bf16* orow = O + (win * TOK + qi) * ldo + h * HDP;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = 8 * g + 4 * hh;
+      float r4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r4[j] = (h * HDP + d0 + j == ones_col) ? 1.f : o[4 * g + j];
+      const bf16x4 q4 = {(bf16)r4[0], (bf16)r4[1], (bf16)r4[2], (bf16)r4[3]};
+      *(bf16x4*)(orow + d0) = q4;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // backward: one wave per (head, group of windows); dS summed over the group in registers for the
 // relative-position-bias gradient
 // ------------------------------------------------------------------------------------------
@@ -704,7 +821,7 @@ extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* tab
   const long nb = (tasks + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
+    hipLaunchKernelGGL(attn_fwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
                        lse, nWin, nh, scale, H, W, shift, ones_col);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, table, (float*)O,
