@@ -188,6 +188,47 @@ __global__ void colsum_partial(const T* __restrict__ g, long ld, long M, int Np,
   ws[(long)blockIdx.x * Np + c] = s;
 }
 
+// Vectorised partial column sums (Np % 8 == 0, Np <= 256, 16-byte aligned rows): Np/8 lanes cover
+// a row with 16-byte loads, 256/(Np/8) row phases run in parallel (4 rows in flight per thread),
+// then the phases are added in fixed order through LDS (deterministic).
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_v(const T* __restrict__ g, long ld, long M, int Np,
+                                                        float* __restrict__ ws, long rows_per) {
+  __shared__ float red[256 * 8];
+  const int cpr = Np >> 3, rp = 256 / cpr;
+  const int cg = threadIdx.x % cpr, ph = threadIdx.x / cpr;
+  const long r0 = (long)blockIdx.x * rows_per;
+  long r1 = r0 + rows_per;
+  if (r1 > M) r1 = M;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto add = [&](long r) {
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 q = *(const bf16x8*)(g + r * ld + cg * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += (float)q[j];
+    } else {
+      const float4 a = *(const float4*)(g + r * ld + cg * 8), b = *(const float4*)(g + r * ld + cg * 8 + 4);
+      s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w; s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
+    }
+  };
+  if (ph < rp) {
+    long r = r0 + ph;
+    for (; r + 3 * rp < r1; r += 4 * rp) {   // four independent rows in flight, summed in row order
+      add(r); add(r + rp); add(r + 2 * rp); add(r + 3 * rp);
+    }
+    for (; r < r1; r += rp) add(r);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = s[j];
+  __syncthreads();
+  if (threadIdx.x < Np) {
+    const int c = threadIdx.x, cgc = c >> 3, j = c & 7;
+    float t = 0.f;
+    for (int p = 0; p < rp; ++p) t += red[(p * cpr + cgc) * 8 + j];
+    ws[(long)blockIdx.x * Np + c] = t;
+  }
+}
+
 __global__ __launch_bounds__(256) void colsum_final(const float* __restrict__ ws, int nb, int Np, kair_wmap mp, float* out,
                                                     int acc) {
   __shared__ float red[4][64];
@@ -464,7 +505,12 @@ extern "C" int kair_colsum(const kair_operand* G, long M, int Np, const kair_wma
   const long rows_per = (M + nb - 1) / nb;
   dim3 grid(nb, (Np + 255) / 256);
   hipStream_t s = (hipStream_t)stream;
-  if (G->dtype == KAIR_BF16)
+  const bool vec = Np % 8 == 0 && Np <= 256 && G->ld % 8 == 0 && ((uintptr_t)G->ptr & 15) == 0;
+  if (vec && G->dtype == KAIR_BF16)
+    hipLaunchKernelGGL(colsum_partial_v<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)G->ptr, G->ld, M, Np, ws, rows_per);
+  else if (vec)
+    hipLaunchKernelGGL(colsum_partial_v<float>, dim3(nb), dim3(256), 0, s, (const float*)G->ptr, G->ld, M, Np, ws, rows_per);
+  else if (G->dtype == KAIR_BF16)
     hipLaunchKernelGGL(colsum_partial<bf16>, grid, dim3(256), 0, s, (const bf16*)G->ptr, G->ld, M, Np, ws, rows_per);
   else
     hipLaunchKernelGGL(colsum_partial<float>, grid, dim3(256), 0, s, (const float*)G->ptr, G->ld, M, Np, ws, rows_per);

@@ -131,6 +131,26 @@ def test_conv3x3_halo_path(shape, flip, a_f32, resid):
     assert rel_err(got, ref) < 1e-2
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,Np,ld", [(100003, 16, 16), (70000, 256, 256), (4097, 64, 72), (5000, 20, 20)])
+def test_colsum_bias_gradient(dt, M, Np, ld):
+    """Bias gradient = column sums of the output-gradient rows (vectorised and scalar paths),
+    deterministic (two launches agree bit for bit)."""
+    g = torch.Generator().manual_seed(M)
+    x = torch.randn(M, ld, generator=g).to(dt)
+    ref = x[:, :Np].double().sum(0)
+    m = H.wmap(0, Np, 0)
+    out = torch.empty(Np, device=dev)
+    out2 = torch.empty(Np, device=dev)
+    ws = torch.empty(512 * max(Np, 256), device=dev)
+    G = H.rows(x.to(dev))
+    H.colsum(G, M, Np, m, out, ws)
+    H.colsum(G, M, Np, m, out2, ws)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    assert (out.double().cpu() - ref).abs().max().item() < 1e-3 * (1 + ref.abs().max().item())
+
+
 @pytest.mark.parametrize("compute", [H.F32, H.BF16])
 def test_conv_pixelshuffle_and_nchw(compute):
     B, Hh, Ww, Cin, r = 2, 8, 8, 16, 2
