@@ -125,8 +125,20 @@ __global__ __launch_bounds__(256) void wgrad_finalize4_kernel(const float* __res
   const bool valid = e4 * 4 < plane;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (valid) {
-    for (int sp = ph; sp < splits; sp += 4) {
-      const float4 v = ((const float4*)(part + (long)sp * plane))[e4];
+    // the ring TN kernel leaves up to 256 split planes: issue 8 plane loads per phase before adding
+    // (a load-add chain waits out one memory latency per split); the sum order is unchanged
+    const float4* p = (const float4*)part + e4;
+    const long st = plane / 4;
+    int sp = ph;
+    for (; sp + 28 < splits; sp += 32) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(long)(sp + 4 * u) * st];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+    for (; sp < splits; sp += 4) {
+      const float4 v = p[(long)sp * st];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
   }

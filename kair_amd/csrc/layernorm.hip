@@ -200,6 +200,17 @@ __global__ __launch_bounds__(256) void ln_param_reduce(const float* __restrict__
   float s0 = 0.f, s1 = 0.f;
   if (c < 2 * C) {
     int b = ty;
+    // 8 loads in flight per thread, then the same alternating s0/s1 order as the pair loop below
+    for (; b + 224 < nb; b += 256) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)(b + 32 * u) * 2 * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        s0 += v[u];
+        s1 += v[u + 1];
+      }
+    }
     for (; b + 32 < nb; b += 64) {
       s0 += part[(long)b * 2 * C + c];
       s1 += part[(long)(b + 32) * 2 * C + c];

@@ -181,6 +181,13 @@ class SwinIREngine:
         self._packed_version = None
         self._pack_table = None
         self.seg_hook = None   # called between the gradient segments of backward() (grad_segments())
+        # KAIR_WGRAD_OVERLAP=1: Swin-block weight gradients on a side stream beside the data-gradient
+        # chain.  Off by default: measured 798 -> 737 patches/s at B=32 and 312 -> 305 at B=4 (the
+        # ring kernels hold one LDS-full CTA per CU, so the two streams cannot co-reside)
+        import os
+        self.wgrad_overlap = os.environ.get("KAIR_WGRAD_OVERLAP", "0") == "1"
+        self._side = None
+        self._ev_qkv = None
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -203,6 +210,40 @@ class SwinIREngine:
     def _segment_done(self):
         if self.seg_hook is not None:
             self.seg_hook()
+
+    # side stream for the block weight gradients --------------------------------------------
+    def _side_stream(self):
+        if not self.wgrad_overlap or not torch.cuda.is_available():
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+        return self._side
+
+    def _on_side(self, fn):
+        """Run fn (weight-gradient launches) on the side stream once everything issued so far on the
+        current stream is done; returns the event marking fn's completion (None: ran inline)."""
+        side = self._side_stream()
+        if side is None:
+            fn()
+            return None
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            fn()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        return ev
+
+    @staticmethod
+    def _after(ev):
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+
+    def _join_side(self):
+        """The current stream waits for every side-stream launch (before the shared weight-gradient
+        workspace is used on the main stream, a gradient segment ends, or backward returns)."""
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
+        self._ev_qkv = None
 
     # ------------------------------------------------------------------------------------
     def convs(self):
@@ -509,6 +550,7 @@ class SwinIREngine:
                 bi -= 1
                 x_in = P["blocks"][bi - 1]["out"] if j > 0 else (P["rstb_out"][gi - 1] if gi > 0 else P["s0"])
                 self._block_bwd(blks[j], P, P["blocks"][bi], x_in, D, bi, grads, copy_prev=j > 0)
+            self._join_side()   # the RSTB conv's weight gradient below shares the workspace
             H.axpy(G, D, 1.0)   # dL/du_g = skip + blocks path
             if gi > 0:
                 self._segment_done()   # RSTB gi's gradients are final (RSTB 0 joins the head segment)
@@ -535,33 +577,39 @@ class SwinIREngine:
         s_mlp = drop[bi, 1] if drop is not None else None
         hd = self.C // nh
         # MLP: out = mid + s_mlp * fc2(gelu(fc1(LN2(mid))))
+        # Weight gradients go to the side stream (_on_side) as soon as their operands exist; the main
+        # stream waits for one only before it overwrites an operand that gradient still reads:
+        # Dc (LN2 / LN1 backward rewrite it), dU (the next block's fc2 dgrad), dqkv (the next
+        # block's attention backward).  Every kernel's arithmetic is unchanged (bit-identical).
         Dc = P["Dc"]
-        l = blk.fc2
-        H.gemm_nt(H.rows(Dc), H.rows(l.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=1), M, self.Hdp, Cp, cd)
-        self._wgrad(P, H.rows(Dc), H.rows(S["h"], ones_col=l.K, ones_in_data=True), M, Cp, self.Hdp, l.map, g(l.w),
-                    g(l.b), l.K)
-        l = blk.fc1
-        H.gemm_nt(H.rows(P["dU"]), H.rows(l.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
-        self._wgrad(P, H.rows(P["dU"]), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), M, self.Hdp, Cp, l.map,
-                    g(l.w), g(l.b), self.C)
+        fc2, fc1 = blk.fc2, blk.fc1
+        ev_fc2 = self._on_side(lambda: self._wgrad(P, H.rows(Dc), H.rows(S["h"], ones_col=fc2.K, ones_in_data=True), M,
+                                                   Cp, self.Hdp, fc2.map, g(fc2.w), g(fc2.b), fc2.K))
+        H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=1), M, self.Hdp, Cp, cd)
+        self._on_side(lambda: self._wgrad(P, H.rows(P["dU"]), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), M,
+                                          self.Hdp, Cp, fc1.map, g(fc1.w), g(fc1.b), self.C))
+        H.gemm_nt(H.rows(P["dU"]), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
         n = blk.n2
+        self._after(ev_fc2)                  # LN2 backward rewrites Dc
         H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, g(n.weight), g(n.bias), False,
                         P["ln_ws"], M, self.C, copy=H.copy_desc(Dc, rowscale=s_attn, rows_per_scale=HW, win=win))
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
-        l = blk.proj
-        H.gemm_nt(H.rows(Dc), H.rows(l.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
-        self._wgrad(P, H.rows(Dc), H.rows(S["O"], ones_col=hd, ones_in_data=True), M, Cp, nh * 32, l.map, g(l.w),
-                    g(l.b), hd)
+        proj, qkv = blk.proj, blk.qkv
+        ev_proj = self._on_side(lambda: self._wgrad(P, H.rows(Dc), H.rows(S["O"], ones_col=hd, ones_in_data=True), M,
+                                                    Cp, nh * 32, proj.map, g(proj.w), g(proj.b), hd))
+        H.gemm_nt(H.rows(Dc), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
+        self._after(self._ev_qkv)            # the previous block's qkv weight gradient still reads dqkv
         H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], P["dqkv"], g(blk.table), False,
                           P["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
-        l = blk.qkv
-        H.gemm_nt(H.qkvblk(P["dqkv"], nh), H.rows(l.Wt), H.epilogue(P["dxn"]), M, Cp, l.Np, cd)
-        self._wgrad(P, H.qkvblk(P["dqkv"], nh), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), M, l.Np, Cp, l.map,
-                    g(l.w), g(l.b), self.C)
+        self._ev_qkv = self._on_side(lambda: self._wgrad(P, H.qkvblk(P["dqkv"], nh),
+                                                         H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), M, qkv.Np,
+                                                         Cp, qkv.map, g(qkv.w), g(qkv.b), self.C))
+        H.gemm_nt(H.qkvblk(P["dqkv"], nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
         n = blk.n1
         cp = None
         if copy_prev:
             cp = H.copy_desc(Dc, rowscale=drop[bi - 1, 1] if drop is not None else None, rows_per_scale=HW)
+        self._after(ev_proj)                 # LN1 backward rewrites Dc (and the fc1 one is done: dU is free)
         H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, g(n.weight), g(n.bias), False,
                         P["ln_ws"], M, self.C, win, copy=cp)
 
