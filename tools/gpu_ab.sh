@@ -8,8 +8,10 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 for v in ${AB_VARIANTS:-base}; do
   envs=""; [ "$v" != base ] && envs="$v"
-  env $envs timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/b32_$v.log 2>&1 || { echo "b32 $v failed"; exit 1; }
-  if [ -n "$AB_B4" ]; then
+  if [ -z "$AB_ONLY_B4" ]; then
+    env $envs timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/b32_$v.log 2>&1 || { echo "b32 $v failed"; exit 1; }
+  fi
+  if [ -n "$AB_B4$AB_ONLY_B4" ]; then
     env $envs timeout -k 10 300 python bench.py --global-batch 4 --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/b4_$v.log 2>&1 || { echo "b4 $v failed"; exit 1; }
   fi
 done
