@@ -1353,7 +1353,11 @@ static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, i
 
 template <int AM>
 int ring_bn(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
-  if (K <= 192) return launch_ring<192, 5, AM>(A, B, E, M, N, K, s);
+  // one 192-wide N tile leaves the persistent CTAs unevenly loaded (B = 32: 576 M-tiles on 256 CUs
+  // -> 3 vs 2.25 on average); two 96-wide tiles balance better (measured 815 -> 823 patches/s;
+  // A/B knob KAIR_RING_SPLIT_N=0)
+  static const int split_n = getenv("KAIR_RING_SPLIT_N") ? atoi(getenv("KAIR_RING_SPLIT_N")) : 1;
+  if (K <= 192 && !(split_n && N <= 192 && E.omode != KAIR_OUT_QKVBLK)) return launch_ring<192, 5, AM>(A, B, E, M, N, K, s);
   if (K <= 384) return launch_ring<96, 5, AM>(A, B, E, M, N, K, s);
   return launch_ring<64, 5, AM>(A, B, E, M, N, K, s);
 }

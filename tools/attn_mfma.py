@@ -6,8 +6,12 @@ backward) from a rocprofv3 kernel trace of `bench.py` (classical x4, B = 32 per 
 Each training step is the stretch between two adam_ema launches; inside it the L1-loss kernel
 splits forward from backward.  Roles are told apart by kernel instance and, where one instance
 serves two roles, by position:
-  forward   gemm_nt_ring<192,5,0,1,0> = QKV, attn_fwd = q.k^T + p.v, gemm_nt_ring<192,5,0,0,1> = proj
-  backward  gemm_nt_ring<192,5,0,0,0> = proj dgrad, gemm_tn_ring<0> #3 of each block = proj wgrad,
+  forward   gemm_nt_ring<192,5,0,1,0> = QKV, attn_fwd = q.k^T + p.v, the first residual ring GEMM
+            after it = proj (fc2 is the second)
+  backward  after each fc2 dgrad (gemm_nt_ring<192,5,0,0,2>) the second gemm_nt_ring<96,5,0,0,0> is
+            proj dgrad (the first is fc1 dgrad; with KAIR_RING_SPLIT_N=0 proj dgrad is
+            gemm_nt_ring<192,5,0,0,0>),
+            gemm_tn_ring<0> #3 of each block = proj wgrad,
             attn_bwd = the five attention products, gemm_nt_ring<64,5,2,0,0> = QKV dgrad,
             gemm_tn_ring<2> = QKV wgrad (+ the wgrad_finalize that follows each wgrad)
 FLOPs and bytes are algorithmic at the reference dims (C = 180, 6 heads x 30, 64-token windows):
@@ -34,24 +38,49 @@ ROLES = {   # role: (flops per launch, algorithmic HBM bytes per launch)
 }
 
 
-def classify(name, in_bwd, tn0_idx):
-    if "gemm_nt_ring<192, 5, 0, 1, 0>" in name or "gemm_nt_ringILi192ELi5ELi0ELi1ELi0E" in name:
-        return "qkv_fwd" if not in_bwd else None
-    if "attn_fwd_bf16_kernel" in name:
-        return "attn_fwd" if not in_bwd else None
-    if "gemm_nt_ring<192, 5, 0, 0, 1>" in name:
-        return "proj_fwd" if not in_bwd else None
-    if "gemm_nt_ring<192, 5, 0, 0, 0>" in name:
-        return "proj_dgrad" if in_bwd else None
-    if "gemm_tn_ring<0>" in name and in_bwd:
-        return "proj_wgrad" if tn0_idx % 3 == 2 else None
-    if "attn_bwd_bf16_kernel" in name:
-        return "attn_bwd"
-    if "gemm_nt_ring<64, 5, 2, 0, 0>" in name:
-        return "qkv_dgrad"
-    if "gemm_tn_ring<2>" in name:
-        return "qkv_wgrad"
-    return None
+def _ring(name, em, ex):
+    """gemm_nt_ring<BN, 5, 0, em, ex> with BN 96 or 192 (K <= 192 GEMMs split N into two 96-wide
+    tiles unless KAIR_RING_SPLIT_N=0)."""
+    return any(f"gemm_nt_ring<{bn}, 5, 0, {em}, {ex}>" in name for bn in (96, 192))
+
+
+class Classifier:
+    """Per-step state: proj fwd is the first residual ring GEMM after each attn_fwd (fc2 fwd is the
+    second); see the module docstring for the backward."""
+
+    def __init__(self):
+        self.in_bwd, self.tn0, self.after_attn, self.plain_bwd = False, 0, False, 0
+
+    def __call__(self, name):
+        if "l1_kernel" in name:
+            self.in_bwd = True
+            return None
+        if "gemm_nt_ring<192, 5, 0, 1, 0>" in name:
+            return "qkv_fwd" if not self.in_bwd else None
+        if "attn_fwd_bf16_kernel" in name:
+            self.after_attn = True
+            return "attn_fwd" if not self.in_bwd else None
+        if _ring(name, 0, 1) and not self.in_bwd:
+            first, self.after_attn = self.after_attn, False
+            return "proj_fwd" if first else None
+        if self.in_bwd and "gemm_nt_ring<192, 5, 0, 0, 2>" in name:   # fc2 dgrad opens a block backward
+            self.plain_bwd = 0
+            return None
+        if self.in_bwd and "gemm_nt_ring<96, 5, 0, 0, 0>" in name:     # fc1 dgrad, then (split-N) proj dgrad
+            self.plain_bwd += 1
+            return "proj_dgrad" if self.plain_bwd == 2 else None
+        if self.in_bwd and "gemm_nt_ring<192, 5, 0, 0, 0>" in name:    # proj dgrad (KAIR_RING_SPLIT_N=0)
+            return "proj_dgrad"
+        if "gemm_tn_ring<0>" in name and self.in_bwd:
+            self.tn0 += 1
+            return "proj_wgrad" if self.tn0 % 3 == 0 else None
+        if "attn_bwd_bf16_kernel" in name:
+            return "attn_bwd"
+        if "gemm_nt_ring<64, 5, 2, 0, 0>" in name:
+            return "qkv_dgrad"
+        if "gemm_tn_ring<2>" in name:
+            return "qkv_wgrad"
+        return None
 
 
 def main(path, out=None):
@@ -61,20 +90,15 @@ def main(path, out=None):
     dur = {k: [] for k in ROLES}
     fin = {"proj_wgrad": [], "qkv_wgrad": []}
     for a, b in zip(steps[:-1], steps[1:]):
-        in_bwd, tn0, pending = False, 0, None
+        cls, pending = Classifier(), None
         for r in rows[a + 1:b]:
             n = r["Kernel_Name"]
             d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-            if "l1_kernel" in n:
-                in_bwd = True
-                continue
             if pending and "wgrad_finalize" in n:
                 fin[pending].append(d)
                 pending = None
                 continue
-            role = classify(n, in_bwd, tn0)
-            if "gemm_tn_ring<0>" in n and in_bwd:
-                tn0 += 1
+            role = cls(n)
             if role:
                 dur[role].append(d)
                 pending = role if role in fin else None
