@@ -152,6 +152,16 @@ KAIR_DEV float split_sum16(const float* __restrict__ part, long nparts, long pla
   float s0 = 0.f, s1 = 0.f;
   if (valid) {
     long i = ty;
+    for (; i + 112 < nparts; i += 128) {   // 8 loads in flight, then the pair loop's s0/s1 order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(i + 16 * u) * plane + off];
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        s0 += v[u];
+        s1 += v[u + 1];
+      }
+    }
     for (; i + 16 < nparts; i += 32) {
       s0 += part[i * plane + off];
       s1 += part[(i + 16) * plane + off];
