@@ -1288,6 +1288,12 @@ template <typename CT, typename TA, int AM>
 int nt_tiles(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
   if (N <= 16) return launch_nt<CT, TA, AM, 256, 16, 4, 1>(A, B, E, M, N, K, s);
   if (g_num_cus == 0) init_num_cus();
+  // 32x32 tiles for N <= 32 (RRDB dense-block convs, growth 32; ResUNet level-2 convs): no half-empty
+  // 64-wide N tile, twice the CTAs on these small-M, long-K convs (RRDBNet B=16: 421 -> 436
+  // patches/s; 64x32 tiles 429).  A/B knob KAIR_NT_N32 = 0 / 1 (64x32) / 2 (32x32)
+  static const int n32 = getenv("KAIR_NT_N32") ? atoi(getenv("KAIR_NT_N32")) : 2;
+  if (N <= 32 && n32 == 1) return launch_nt<CT, TA, AM, 64, 32, 2, 2>(A, B, E, M, N, K, s);
+  if (N <= 32 && n32 == 2) return launch_nt<CT, TA, AM, 32, 32, 2, 2>(A, B, E, M, N, K, s);
   const long tm = (M + 127) / 128;
   if (N > 64 && tm * ((N + 127) / 128) >= 2L * g_num_cus) return launch_nt<CT, TA, AM, 128, 128, 2, 2>(A, B, E, M, N, K, s);
   if (tm * ((N + 63) / 64) >= 2L * g_num_cus || M <= 64) return launch_nt<CT, TA, AM, 128, 64, 2, 2>(A, B, E, M, N, K, s);
