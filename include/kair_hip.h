@@ -168,7 +168,7 @@ typedef struct {
 int kair_row_copy(const float* src, long ld_src, long M, int C, const kair_copy_desc* copy, void* stream);
 
 /* dx_acc[t] (+)= LN-backward(dy) for token rows t; dgamma/dbeta (+)= column sums.
- * dy (dtype) is addressed like y in the forward.  ws: 2 * 1024 * C floats.
+ * dy (dtype) is addressed like y in the forward.  ws: 2 * 2048 * C floats.
  * copy (optional): also write the finished dx rows as a kair_copy_desc. */
 int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int dy_dtype, long ldy,
                        const float* gamma, const float* mean, const float* rstd, float* dx_acc,

@@ -170,24 +170,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
       }
     }
   }
-  // block reduction of dgamma/dbeta partials: 16 row-groups share each column (fixed order)
-  __shared__ float red[2][16][260];
+  // block reduction of dgamma/dbeta partials: 16 row-groups share each column (fixed order); one
+  // 16.6 KB buffer used twice (dgamma, then dbeta) so LDS admits more resident blocks per CU
+  __shared__ float red[16][260];
   const int rg = threadIdx.x >> 4;
+  for (int w = 0; w < 2; ++w) {
 #pragma unroll
-  for (int i = 0; i < NV; ++i)
+    for (int i = 0; i < NV; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = (sub + LPR * i) * 4 + j;
-      red[0][rg][c] = dg[i][j];
-      red[1][rg][c] = db[i][j];
+      for (int j = 0; j < 4; ++j) red[rg][(sub + LPR * i) * 4 + j] = w == 0 ? dg[i][j] : db[i][j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += red[k][c];
+      part[(long)blockIdx.x * 2 * C + w * C + c] = s;
     }
-  __syncthreads();
-  for (int c = threadIdx.x; c < 2 * C; c += 256) {
-    const int w = c < C ? 0 : 1, cc = c < C ? c : c - C;
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) s += red[w][k][cc];
-    part[(long)blockIdx.x * 2 * C + c] = s;
+    __syncthreads();
   }
 }
 
@@ -232,7 +231,7 @@ __global__ __launch_bounds__(256) void ln_param_reduce(const float* __restrict__
 
 }  // namespace
 
-constexpr int LN_BLOCKS = 1024;  // ws holds LN_BLOCKS * 2 * C floats (kair_hip.h)
+constexpr int LN_BLOCKS = 2048;  // ws holds LN_BLOCKS * 2 * C floats (kair_hip.h)
 
 extern "C" int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype, long ldy, const float* gamma,
                                   const float* beta, float* mean, float* rstd, long M, int C, float eps, int win_H,

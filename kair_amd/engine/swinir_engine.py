@@ -306,7 +306,7 @@ class SwinIREngine:
         P["dU"], P["dxn"] = e(M, Hdp, dt=T), e(M, Cp, dt=T)
         P["Dc"] = e(M, Cp, dt=T)   # compute-dtype GEMM operand copy of the residual-stream gradient
         P["dO"], P["dqkv"] = e(M, nh * 32, dt=T), e(3 * M * nh * 32, dt=T)
-        P["ln_ws"] = e(2 * 1024 * Cp)
+        P["ln_ws"] = e(2 * 2048 * Cp)   # kair_layernorm_bwd: 2 * 2048 * C floats
         P["attn_ws"] = e(H.window_attn_bwd_ws(nWin, nh))
         P["loss"] = e(1)
         P["loss_ws"] = e(1024)

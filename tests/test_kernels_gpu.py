@@ -262,7 +262,7 @@ def test_layernorm(dtype, win):
     dy[:, :C] = gy[perm]
     dx = torch.ones(M, ld, device=dev)  # accumulate onto ones
     dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
-    ws = torch.empty(2 * 1024 * C, device=dev)
+    ws = torch.empty(2 * 2048 * C, device=dev)
     # GEMM-operand copy of the finished dx: per-sample scale, Swin window order (the other map)
     cwin = (16, 16, 8, 4) if not win[2] else None
     sc = torch.tensor([0.5, 2.0], device=dev)
