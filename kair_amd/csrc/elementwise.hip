@@ -288,25 +288,26 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ img, T* __restric
   out[t] = (T)v;
 }
 
-template <typename T>
+// I: index type (int when every index fits: 32-bit divisions are a fraction of the 64-bit ones)
+template <typename T, typename I>
 __global__ void l1_kernel(const float* __restrict__ E, const float* __restrict__ H, T* __restrict__ dE, int ldc, int r,
                           float gscale, int C, int Hh, int Ww, long npix, float* __restrict__ ws) {
   // dE element t = (pixel of the [Hh/r, Ww/r] grid, channel slot); slot -> (c, i, j) when r > 1
   __shared__ float red[256];
   float s = 0.f;
-  const long total = npix * ldc;
+  const I total = (I)(npix * ldc);
   const int hs = Hh / r, wsm = Ww / r, r2 = r * r;
-  const long HW = (long)Hh * Ww;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const long pix = t / ldc;
+  const I HW = (I)Hh * Ww;
+  for (I t = (I)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
+    const I pix = t / ldc;
     const int slot = (int)(t - pix * ldc);
     const int c = slot / r2, ij = slot - c * r2;
     float g = 0.f;
     if (c < C) {
-      const long b = pix / ((long)hs * wsm);
+      const I b = pix / ((I)hs * wsm);
       const int pp = (int)(pix - b * hs * wsm);
       const int y = (pp / wsm) * r + ij / r, x = (pp % wsm) * r + ij % r;
-      const long i = (b * C + c) * HW + (long)y * Ww + x;
+      const I i = (b * C + c) * HW + (I)y * Ww + x;
       const float d = E[i] - H[i];
       s += fabsf(d);
       g = d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f);
@@ -571,10 +572,16 @@ extern "C" int kair_l1_loss(const float* E, const float* H, float* loss_out, voi
   const int nb = 1024;
   hipStream_t s = (hipStream_t)stream;
   const float gs = (float)(weight / numel);
-  if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(l1_kernel<bf16>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
+  // int indices when the largest index (dE element or image element) and the grid stride fit
+  const bool i32 = (double)npix * ldc < 2.0e9 && numel < 2.0e9;
+  if (dtype == KAIR_BF16 && i32)
+    hipLaunchKernelGGL((l1_kernel<bf16, int>), dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
+  else if (dtype == KAIR_BF16)
+    hipLaunchKernelGGL((l1_kernel<bf16, long>), dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
+  else if (i32)
+    hipLaunchKernelGGL((l1_kernel<float, int>), dim3(nb), dim3(256), 0, s, E, H, (float*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
   else
-    hipLaunchKernelGGL(l1_kernel<float>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
+    hipLaunchKernelGGL((l1_kernel<float, long>), dim3(nb), dim3(256), 0, s, E, H, (float*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
   KAIR_CHECK_LAUNCH();
   hipLaunchKernelGGL(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);
   KAIR_CHECK_LAUNCH();
