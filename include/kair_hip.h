@@ -58,6 +58,12 @@ typedef struct {
                           (lets DMA loaders skip the injection); 0: loaders inject it         */
   int im_up;           /* IM2COL3: 2 = the source image is im_H/2 x im_W/2 and is read through a
                           nearest x2 upsample (F.interpolate(scale 2, 'nearest')); 0/1 = none  */
+  int w_split;         /* kair_gemm_nt B only (bf16 compute): 1 = the packed weight rows hold a
+                          hi/lo bf16 pair per value (w = hi + lo, pack kind 9), interleaved per 64
+                          columns [hi k0..k0+63 | lo k0..k0+63 | hi k0+64.. ...]; row length
+                          2*ceil(K/64)*64.  The A operand is read once per pair, so the product
+                          carries ~16 mantissa bits of the fp32 master weights (bf16 weight
+                          rounding biases the output, see DESIGN.md "parity at bf16")        */
 } kair_operand;
 
 typedef enum {
@@ -117,7 +123,9 @@ typedef struct {
                         7 conv2x2 [N][K][2][2] -> [Np][4*Kp], k = tap*Kp + kp (stride-2 conv
                           forward / transposed-conv dgrad over (N, K) = (Ci, Co));
                         8 conv2x2 -> [4*Kp][Np], row = kp*4 + tap (pixel-shuffle forms: stride-2
-                          conv dgrad, transposed-conv forward over (N, K) = (Ci, Co))           */
+                          conv dgrad, transposed-conv forward over (N, K) = (Ci, Co));
+                        9 conv3x3 forward, hi/lo split (bf16 only): [Cop][2*ceil(9*Cip/64)*64],
+                          64-column chunks alternate hi = bf16(w), lo = bf16(w - hi)             */
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
   int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp                   */

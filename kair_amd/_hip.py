@@ -28,7 +28,7 @@ class Operand(ctypes.Structure):
                 ("im_H", c_int), ("im_W", c_int), ("im_C", c_int), ("im_flip", c_int),
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
                 ("rowscale", c_vp), ("rows_per_scale", c_int), ("ones_col", c_int), ("ones_in_data", c_int),
-                ("im_up", c_int)]
+                ("im_up", c_int), ("w_split", c_int)]
 
 
 class CopyDesc(ctypes.Structure):
@@ -178,8 +178,9 @@ def require_device(*ts):
 # ------------------------------------------------------------------------------------------
 # descriptor builders
 # ------------------------------------------------------------------------------------------
-def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1, ones_in_data=False):
-    """Row-major operand; win = (H, W, ws, shift) applies the Swin window->token row map."""
+def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1, ones_in_data=False, w_split=False):
+    """Row-major operand; win = (H, W, ws, shift) applies the Swin window->token row map.
+    w_split: packed hi/lo bf16 weight rows (pack kind 9; gemm_nt B operand only)."""
     o = Operand()
     o._keep = (t, rowscale)  # keep the tensors alive until the launch has been issued
     o.ptr = ptr(t)
@@ -192,6 +193,7 @@ def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1, one
     o.rows_per_scale = rows_per_scale
     o.ones_col = ones_col
     o.ones_in_data = int(ones_in_data)
+    o.w_split = int(w_split)
     return o
 
 

@@ -42,6 +42,19 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const int tap = kk / Kp, kp = kk - tap * Kp;
     const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && k >= 0) v = src[((long)n * mp.K + k) * 4 + tap];
+  } else if (mp.kind == 9) {  // conv3x3 forward, hi/lo split: [Cop][KS], 64-col chunks alternate hi / lo
+    const int Kc = 9 * Kp, KS = 2 * ((Kc + 63) / 64) * 64;
+    const int np = (int)(t / KS);
+    const int kk = (int)(t - (long)np * KS);
+    const int half = (kk >> 6) & 1, k = ((kk >> 7) << 6) + (kk & 63);
+    if (k < Kc) {
+      const int tap = k / Kp, cip = k - tap * Kp;
+      const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
+      if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
+    }
+    const bf16 hi = (bf16)v;
+    ((bf16*)dst)[t] = half ? (bf16)(v - (float)hi) : hi;
+    return;
   } else if (mp.kind == 8) {  // conv2x2 [4*Kp][Np], row = kp*4 + tap (pixel-shuffle forms)
     const int row = (int)(t / Np), np = (int)(t - (long)row * Np);
     const int kp = row >> 2, tap = row & 3;
@@ -422,7 +435,8 @@ inline unsigned nblk(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
 
-static int pack_total(const kair_wmap& mp, long* total) {
+static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
+  KAIR_CHECK_ARG(mp.kind != 9 || dst_dtype == KAIR_BF16, "pack_weight: the hi/lo split form (kind 9) is bf16 only");
   KAIR_CHECK_ARG(mp.nG > 0 && mp.nGr > 0 && mp.nGp >= mp.nGr && mp.nG * mp.nGr == mp.N, "pack_weight: bad N map");
   KAIR_CHECK_ARG(mp.kind == 4 || (mp.kG > 0 && mp.kGr > 0 && mp.kGp >= mp.kGr && mp.kG * mp.kGr == mp.K),
                  "pack_weight: bad K map");
@@ -430,6 +444,7 @@ static int pack_total(const kair_wmap& mp, long* total) {
   if (mp.kind == 0 || mp.kind == 3) *total = Np * Kp;
   else if (mp.kind == 1 || mp.kind == 2) *total = Np * 9 * Kp;
   else if (mp.kind == 7 || mp.kind == 8) *total = Np * 4 * Kp;
+  else if (mp.kind == 9) *total = Np * 2 * ((9L * Kp + 63) / 64) * 64;
   else if (mp.kind == 4) *total = Np;
   else return kair_set_error(KAIR_ERR_ARG, "pack_weight: bad kind %d", mp.kind);
   return 0;
@@ -438,7 +453,7 @@ static int pack_total(const kair_wmap& mp, long* total) {
 extern "C" int kair_pack_weight(const float* src, void* dst, int dst_dtype, const kair_wmap* map, void* stream) {
   KAIR_CHECK_ARG(src && dst && map, "pack_weight: null pointer");
   long total;
-  if (int rc = pack_total(*map, &total)) return rc;
+  if (int rc = pack_total(*map, dst_dtype, &total)) return rc;
   hipLaunchKernelGGL(pack_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, src, dst, dst_dtype, *map,
                      total);
   KAIR_CHECK_LAUNCH();
@@ -458,7 +473,7 @@ extern "C" long kair_pack_table_build(kair_pack_job* jobs, int njobs, void* tabl
   long nb = 0;
   for (int i = 0; i < njobs; ++i) {
     long total;
-    int rc = jobs[i].src && jobs[i].dst ? pack_total(jobs[i].map, &total)
+    int rc = jobs[i].src && jobs[i].dst ? pack_total(jobs[i].map, jobs[i].dst_dtype, &total)
                                         : kair_set_error(KAIR_ERR_ARG, "pack_table_build: job %d null pointer", i);
     if (rc) { free(host); return rc; }
     jobs[i].total = total;

@@ -43,6 +43,7 @@ struct Op {
   int ones_col;
   int ones_in_data;
   long M;  // rows of this operand
+  int wsplit;  // B only: hi/lo bf16 weight pairs interleaved per 64 columns (kair_operand.w_split)
   FDiv d_rps, d_imC, d_imW, d_hw, d_tok, d_hdp, d_pw;
 };
 
@@ -58,6 +59,7 @@ Op make_op(const kair_operand& o, long M) {
   op.ones_col = o.ones_col;
   op.ones_in_data = o.ones_in_data;
   op.M = M;
+  op.wsplit = o.w_split ? 1 : 0;
   op.d_rps = make_fdiv(op.rps);
   op.d_imC = make_fdiv(op.imC); op.d_imW = make_fdiv(op.imW); op.d_hw = make_fdiv(op.imH * op.imW);
   op.d_tok = make_fdiv(op.tok); op.d_hdp = make_fdiv(op.hdp); op.d_pw = make_fdiv(op.nh * op.hdp);
@@ -438,11 +440,17 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_kernel(Op A, Op B, Epi E, int K
   Raw<TA> va[PA];
   Raw<CT> vb[PB];
   Pend pa[PA], pb[PB];
-  auto gload = [&](int k0) {
+  // hi/lo split weights (bf16): K-step kt reads A columns of step kt >> 1 and B columns kt * BK of
+  // the interleaved [hi | lo] rows, so the A chunk is fetched twice from L1/L2 but once from HBM
+  const int sh = (sizeof(CT) == 2 && B.wsplit) ? 1 : 0;
+  const int nk = ((K + BK - 1) / BK) << sh;
+  const int KB = sh ? nk * BK : K;
+  auto gload = [&](int kt) {
+    const int ka = (kt >> sh) * BK, kb = kt * BK;
 #pragma unroll
-    for (int p = 0; p < PA; ++p) issue_chunk<AM, TA>(A, ra[p], k0 + ((tid + p * NT) % CPR) * 8, K, va[p], pa[p]);
+    for (int p = 0; p < PA; ++p) issue_chunk<AM, TA>(A, ra[p], ka + ((tid + p * NT) % CPR) * 8, K, va[p], pa[p]);
 #pragma unroll
-    for (int p = 0; p < PB; ++p) issue_chunk<AM_ROWS, CT>(B, rb[p], k0 + ((tid + p * NT) % CPR) * 8, K, vb[p], pb[p]);
+    for (int p = 0; p < PB; ++p) issue_chunk<AM_ROWS, CT>(B, rb[p], kb + ((tid + p * NT) % CPR) * 8, KB, vb[p], pb[p]);
   };
   auto sstore = [&](int st) {
     CT* sA = lds + st * STAGE;
@@ -465,14 +473,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_kernel(Op A, Op B, Epi E, int K
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + BK - 1) / BK;
   const int fr = lane & 15, fq = lane >> 4;
   gload(0);
   sstore(0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int st = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+    if (kt + 1 < nk) gload(kt + 1);
     const CT* sA = lds + st * STAGE;
     const CT* sB = sA + BM * LD;
     if constexpr (sizeof(CT) == 2) {
@@ -1338,7 +1345,7 @@ static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, i
   if (A.rowscale || A.ones_col >= 0) return false;
   if (amode == KAIR_LD_ROWS && A.ld % 8 != 0) return false;
   if (amode == KAIR_LD_QKVBLK && (A.hdp % 8 != 0)) return false;
-  if (B.ld % 8 != 0 || B.ones_col >= 0) return false;
+  if (B.ld % 8 != 0 || B.ones_col >= 0 || B.wsplit) return false;
   if (e.resid && e.gate) return false;   // one epilogue operand per ring kernel
   // 8-column epilogue groups: whole groups, 16-byte aligned rows / pointers
   if (N % 8 != 0) return false;
@@ -1391,7 +1398,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
   const int fr = lane & 15, fq = lane >> 4;
   const int H = A.imH, W = A.imW, C = A.imC;
   const int XW = W < HC_BM ? W : HC_BM, RPT = HC_BM / XW, HWD = XW + 2, HR = RPT + 2, PS = C + 8;
-  const int cpt = C / HC_BK, nks = 9 * cpt, c8n = C / 8;
+  const int sh = B.wsplit;   // hi/lo split weights: weight chunk j pairs with halo chunk j >> 1
+  const int cpt = C / HC_BK, nks = (9 * cpt) << sh, c8n = C / 8;
   const int halo_pieces = HR * HWD * c8n;
   const bf16* Bp = (const bf16*)B.ptr;
   const TA* Ap = (const TA*)A.ptr;
@@ -1430,7 +1438,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
     }
   };
   f32x4 acc[RM][RN];
-  auto compute = [&](int buf, int j) {
+  auto compute = [&](int buf, int jw) {
+    const int j = jw >> sh;
     const int tap = j / cpt, cc = j - tap * cpt;
     int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
     if (A.flip) { dy = -dy; dx = -dx; }
@@ -1708,6 +1717,9 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
   KAIR_CHECK_ARG(B->mode == KAIR_LD_ROWS && B->dtype == compute && B->win_ws == 0,
                  "gemm_nt: B must be packed rows of the compute dtype");
   KAIR_CHECK_ARG(compute == KAIR_BF16 || A->dtype == KAIR_F32, "gemm_nt: fp32 compute needs fp32 A");
+  KAIR_CHECK_ARG(!B->w_split || (compute == KAIR_BF16 && B->ld >= 2L * ((K + 63) / 64) * 64),
+                 "gemm_nt: hi/lo split weights need bf16 compute and rows of 2*ceil(K/64)*64 columns");
+  KAIR_CHECK_ARG(!A->w_split, "gemm_nt: w_split is a B-operand flag");
   KAIR_CHECK_ARG((E->out_mode != KAIR_OUT_PSHUF && E->out_mode != KAIR_OUT_PUNSHUF && E->out_mode != KAIR_OUT_PSHUF_NCHW) ||
                      E->ps_r > 0, "gemm_nt: pixel shuffle r");
   KAIR_CHECK_ARG(E->out_mode != KAIR_OUT_QKVBLK || (E->qkv_hdp % 8 == 0 && E->qkv_tok > 0), "gemm_nt: qkv epilogue");

@@ -58,10 +58,8 @@ class DnCNNEngine(ConvEngineBase):
     def convs(self):
         return [c for c, _, _, _ in self.layers]
 
-    def plan(self, B, Hh, Ww):
-        key = (B, Hh, Ww)
-        if key in self.plans:
-            return self.plans[key]
+    def _build_plan(self, key, infer):
+        B, Hh, Ww = key
         T, e, nc = self.tdt, self._e, self.nc
         M = B * Hh * Ww
         P = {"B": B, "H": Hh, "W": Ww, "M": M}
@@ -81,7 +79,6 @@ class DnCNNEngine(ConvEngineBase):
         P["colsum_ws"] = e(1024 * 256)
         shapes = [(M, c.Cop, 9 * c.Cip) for c, _, _, _ in self.layers]
         P["wg_ws"] = e(self.wgrad_ws_size(shapes))
-        self.plans[key] = P
         return P
 
     def forward(self, x, drop_scales=None):
@@ -99,19 +96,19 @@ class DnCNNEngine(ConvEngineBase):
         for li, (c, bn, act, slope) in enumerate(self.layers[:-1]):
             a = P["a"][li]
             if bn is None:
-                H.gemm_nt(H.im2col(src, Hh, Ww, Cs, ld=ldsrc), H.rows(c.Wf),
+                H.gemm_nt(H.im2col(src, Hh, Ww, Cs, ld=ldsrc), c.fwd(),
                           H.epilogue(a, bias=c.bp, act=(H.ACT_RELU if act == 1 else H.ACT_LEAKY) if act else H.ACT_NONE,
                                      slope=slope), M, nc, 9 * c.Cip, cd)
             else:
                 z = P["z"][li]
-                H.gemm_nt(H.im2col(src, Hh, Ww, Cs, ld=ldsrc), H.rows(c.Wf), H.epilogue(z, bias=c.bp), M, nc, 9 * c.Cip, cd)
+                H.gemm_nt(H.im2col(src, Hh, Ww, Cs, ld=ldsrc), c.fwd(), H.epilogue(z, bias=c.bp), M, nc, 9 * c.Cip, cd)
                 H.bn_fwd(z, nc, a, nc, M, nc, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
                          training, P["mean"][li], P["rstd"][li], act, slope, P["bn_ws"])
                 if training:
                     bn.num_batches_tracked.add_(1)
             src, ldsrc, Cs = a, nc, nc
         c = self.layers[-1][0]
-        H.gemm_nt(H.im2col(src, Hh, Ww, nc), H.rows(c.Wf),
+        H.gemm_nt(H.im2col(src, Hh, Ww, nc), c.fwd(),
                   H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(None, 1.0, self.out_ch, Hh, Ww)), M, c.Cop,
                   9 * nc, cd)
         if self.residual:

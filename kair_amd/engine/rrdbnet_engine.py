@@ -18,6 +18,7 @@ import weakref
 import torch
 
 from .. import _hip as H
+from .plans import Lease, PlanPool, autograd_mode, plan_mode
 from .swinir_engine import _Conv
 
 
@@ -31,12 +32,19 @@ class ConvEngineBase:
             raise ValueError(compute_dtype)
         self.cd = H.BF16 if compute_dtype == "bf16" else H.F32
         self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
-        self.plans = {}
+        self.plans = PlanPool(self._build_plan)
+        self.plan_mode = "primary"
         self._packed_version = None
         self._pack_table = None
         self.blocks = []          # no stochastic depth in the conv nets (FusedTrainer checks this)
 
     def convs(self):
+        raise NotImplementedError
+
+    def plan(self, B, Hh, Ww):
+        return self.plans.get((B, Hh, Ww), self.plan_mode)
+
+    def _build_plan(self, key, infer):
         raise NotImplementedError
 
     def pack(self, force=False):
@@ -121,10 +129,8 @@ class RRDBNetEngine(ConvEngineBase):
         return [self.conv_first] + [c for r in self.rdbs for c in r] + [self.trunk] + self.up + [self.hr, self.last]
 
     # ------------------------------------------------------------------------------------
-    def plan(self, B, Hh, Ww):
-        key = (B, Hh, Ww)
-        if key in self.plans:
-            return self.plans[key]
+    def _build_plan(self, key, infer):
+        B, Hh, Ww = key
         T, e = self.tdt, self._e
         nf, gc, CD = self.nf, self.gc, self.CD
         M = B * Hh * Ww
@@ -160,7 +166,6 @@ class RRDBNetEngine(ConvEngineBase):
         shapes += [(B * hh * ww, nf, 9 * nf) for hh, ww in levels]
         shapes += [(M, c.Cop, 9 * c.Cip) for c in self.rdbs[0]]
         P["wg_ws"] = e(self.wgrad_ws_size(shapes))
-        self.plans[key] = P
         return P
 
     # ------------------------------------------------------------------------------------
@@ -174,7 +179,7 @@ class RRDBNetEngine(ConvEngineBase):
         self.cur = P
         H.image_to_nhwc(x, P["xin"], self.Cin_p, None, 1.0, B, self.in_ch, Hh, Ww)
         c = self.conv_first
-        H.gemm_nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), H.rows(c.Wf), H.epilogue(P["fea"], bias=c.bp), M, nf,
+        H.gemm_nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), c.fwd(), H.epilogue(P["fea"], bias=c.bp), M, nf,
                   9 * self.Cin_p, cd)
         dense = P["dense"]
         H.row_copy(P["fea"], nf, M, nf, H.copy_desc(dense[0], ld=CD))
@@ -184,32 +189,32 @@ class RRDBNetEngine(ConvEngineBase):
             D = dense[r]
             for j in range(4):          # x_{j+1} = lrelu(conv_{j+1}(cat(x, x1..x_j)))
                 c, cin = cs[j], nf + j * gc
-                H.gemm_nt(H.im2col(D, Hh, Ww, cin, ld=CD), H.rows(c.Wf),
+                H.gemm_nt(H.im2col(D, Hh, Ww, cin, ld=CD), c.fwd(),
                           H.epilogue(D[:, cin:cin + gc], ldo=CD, bias=c.bp, act=self.act_epi, slope=self.slope), M, gc, 9 * cin, cd)
             c = cs[4]                    # y = x + 0.2 * conv5(cat(x, x1..x4))
             y = P["y"][r]
-            H.gemm_nt(H.im2col(D, Hh, Ww, CD, ld=CD), H.rows(c.Wf),
+            H.gemm_nt(H.im2col(D, Hh, Ww, CD, ld=CD), c.fwd(),
                       H.epilogue(y, bias=c.bp, resid=x_in, rowscale=P["alpha"], rows_per_scale=M), M, nf, 9 * CD, cd)
             if r % 3 == 2:               # RRDB: out = 0.2 * RDB3 + x   (in place over y)
                 H.axpby(y, rr_in, 1.0, 0.2)
                 rr_in = y
             H.row_copy(y, nf, M, nf, H.copy_desc(dense[r + 1], ld=CD))
         c = self.trunk                   # fea = fea + trunk_conv(trunk)
-        H.gemm_nt(H.im2col(dense[-1], Hh, Ww, nf, ld=CD), H.rows(c.Wf), H.epilogue(P["fea2"], bias=c.bp, resid=P["fea"]),
+        H.gemm_nt(H.im2col(dense[-1], Hh, Ww, nf, ld=CD), c.fwd(), H.epilogue(P["fea2"], bias=c.bp, resid=P["fea"]),
                   M, nf, 9 * nf, cd)
         H.row_copy(P["fea2"], nf, M, nf, H.copy_desc(P["fea2b"]))
         src = P["fea2b"]
         for c, (hh, ww), dst in zip(self.up, P["levels"], P["upa"]):   # lrelu(upconv(nearest x2))
-            H.gemm_nt(H.im2col(src, hh, ww, nf, up=2), H.rows(c.Wf), H.epilogue(dst, bias=c.bp, act=self.act_epi, slope=self.slope),
+            H.gemm_nt(H.im2col(src, hh, ww, nf, up=2), c.fwd(), H.epilogue(dst, bias=c.bp, act=self.act_epi, slope=self.slope),
                       B * hh * ww, nf, 9 * nf, cd)
             src = dst
         HL, WL = P["levels"][-1]
         ML = P["ML"]
         c = self.hr
-        H.gemm_nt(H.im2col(src, HL, WL, nf), H.rows(c.Wf), H.epilogue(P["hr"], bias=c.bp, act=self.act_epi, slope=self.slope), ML,
+        H.gemm_nt(H.im2col(src, HL, WL, nf), c.fwd(), H.epilogue(P["hr"], bias=c.bp, act=self.act_epi, slope=self.slope), ML,
                   nf, 9 * nf, cd)
         c = self.last
-        H.gemm_nt(H.im2col(P["hr"], HL, WL, nf), H.rows(c.Wf),
+        H.gemm_nt(H.im2col(P["hr"], HL, WL, nf), c.fwd(),
                   H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(None, 1.0, self.out_ch, HL, WL)), ML, c.Cop,
                   9 * nf, cd)
         return P["E"]
@@ -293,22 +298,32 @@ class RRDBNetEngine(ConvEngineBase):
 
 
 class ConvNetFunction(torch.autograd.Function):
-    """A whole conv network (RRDBNet / DnCNN / ...) as one autograd node on its step program."""
+    """A whole conv network (RRDBNet / DnCNN / ...) as one autograd node on its step program; the
+    node leases its plan from forward to backward (kair_amd/engine/plans.py)."""
+
+    @classmethod
+    def run(cls, engine, x, params):
+        return cls.apply(engine, autograd_mode(params), x, *params)
 
     @staticmethod
-    def forward(ctx, engine, x, *params):
-        E = engine.forward(x.float().contiguous())
-        ctx.engine, ctx.params, ctx.plan = engine, params, engine.cur
+    def forward(ctx, engine, mode, x, *params):
+        with plan_mode(engine, mode):
+            E = engine.forward(x.float().contiguous())
+        ctx.engine, ctx.params = engine, params
+        ctx.lease = Lease(engine.cur) if mode == "lease" else None
         return E.clone()
 
     @staticmethod
     def backward(ctx, gE):
         eng = ctx.engine
+        if ctx.lease is None or ctx.lease.plan is None:
+            raise RuntimeError("kair_amd: backward through a forward whose activations were released")
         flat = torch.empty(sum(p.numel() for p in ctx.params), device=gE.device)
         grads, off = {}, 0
         for p in ctx.params:
             grads[p] = flat[off:off + p.numel()].view_as(p)
             off += p.numel()
-        eng.cur = ctx.plan
+        eng.cur = ctx.lease.plan
         eng.backward_from_grad(gE.float(), grads)
-        return (None, None) + tuple(grads[p] for p in ctx.params)
+        ctx.lease.release()
+        return (None, None, None) + tuple(grads[p] for p in ctx.params)

@@ -21,6 +21,7 @@ import weakref
 import torch
 
 from .. import _hip as H
+from .plans import Lease, PlanPool, autograd_mode, plan_mode
 
 WS_TOK = 64
 
@@ -82,23 +83,37 @@ class _Lin:
 
 
 class _Conv:
-    """A 3x3 conv's packed forms: forward [Cop][9*Cip] and input-gradient [Cip][9*Cop]."""
+    """A 3x3 conv's packed forms: forward [Cop][9*Cip] and input-gradient [Cip][9*Cop].
 
-    def __init__(self, eng, mod, Cop, Cip, need_dgrad=True):
+    split (bf16 engines): the forward form holds a hi/lo bf16 pair per weight (pack kind 9,
+    kair_operand.w_split), so the forward product sees the fp32 master weight to ~16 bits.  Plain
+    bf16 weight rounding shifts every output pixel by the same sum(dW * a) and biases PSNR
+    (DESIGN.md "parity at bf16"); activation rounding is unbiased and averages out."""
+
+    def __init__(self, eng, mod, Cop, Cip, need_dgrad=True, split=None):
         self.w, self.b = mod.weight, mod.bias
         Co, Ci = self.w.shape[:2]
         self.Co, self.Ci, self.Cop, self.Cip = Co, Ci, Cop, Cip
+        if split is None:
+            split = getattr(eng, "split_conv", False)
+        self.split = bool(split) and eng.tdt == torch.bfloat16
         self.map = H.wmap(1, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
+        self.mapf = H.wmap(9, Co, Ci, (1, Co, Cop), (1, Ci, Cip)) if self.split else self.map
         self.mapd = H.wmap(2, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
         self.mapb = H.wmap(4, Co, 0, (1, Co, Cop), (1, 1, 1))
         dev = self.w.device
-        self.Wf = torch.empty(Cop, 9 * Cip, device=dev, dtype=eng.tdt)
+        kf = 2 * _rup(9 * Cip, 64) if self.split else 9 * Cip
+        self.Wf = torch.empty(Cop, kf, device=dev, dtype=eng.tdt)
         self.Wd = torch.empty(Cip, 9 * Cop, device=dev, dtype=eng.tdt) if need_dgrad else None
         self.bp = torch.empty(Cop, device=dev)
 
+    def fwd(self):
+        """The forward GEMM's B operand."""
+        return H.rows(self.Wf, w_split=self.split)
+
     def pack_jobs(self):
         w, b = self.w.detach(), self.b.detach()
-        jobs = [(w, self.Wf, self.map), (b, self.bp, self.mapb)]
+        jobs = [(w, self.Wf, self.mapf), (b, self.bp, self.mapb)]
         if self.Wd is not None:
             jobs.append((w, self.Wd, self.mapd))
         return jobs
@@ -125,12 +140,14 @@ class _Blk:
 
 
 class SwinIREngine:
-    def __init__(self, net, compute_dtype="bf16"):
+    def __init__(self, net, compute_dtype="bf16", split_conv=True):
+        """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv)."""
         self.net_ref = weakref.ref(net)
         if compute_dtype not in ("bf16", "fp32"):
             raise ValueError(compute_dtype)
         self.cd = H.BF16 if compute_dtype == "bf16" else H.F32
         self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
+        self.split_conv = bool(split_conv) and compute_dtype == "bf16"
         self.C = net.embed_dim
         heads = {l.residual_group.blocks[0].num_heads for l in net.layers}
         if len(heads) != 1:
@@ -177,7 +194,8 @@ class SwinIREngine:
         else:
             raise NotImplementedError(self.upsampler)
         self.blocks = [b for blks, _ in self.rstb for b in blks]
-        self.plans = {}
+        self.plans = PlanPool(self._build_plan)
+        self.plan_mode = "primary"
         self._packed_version = None
         self._pack_table = None
         self.seg_hook = None   # called between the gradient segments of backward() (grad_segments())
@@ -268,9 +286,12 @@ class SwinIREngine:
         self._packed_version = ver
 
     def plan(self, B, Hh, Ww):
-        key = (B, Hh, Ww)
-        if key in self.plans:
-            return self.plans[key]
+        return self.plans.get((B, Hh, Ww), self.plan_mode)
+
+    def _build_plan(self, key, infer):
+        """Buffers of one input shape.  infer=True: forward only -- the Swin blocks ping-pong between
+        two buffer sets (nothing is kept for a backward) and no backward scratch is allocated."""
+        B, Hh, Ww = key
         dev, T, f32 = self.device, self.tdt, torch.float32
         M = B * Hh * Ww
         Cp, Hdp, nh = self.Cp, self.Hdp, self.nh
@@ -282,13 +303,18 @@ class SwinIREngine:
         P["pe_mean"], P["pe_rstd"] = e(M), e(M)
         P["s0"] = e(M, Cp)
         blocks = []
-        for _ in self.blocks:
+        for bi in range(len(self.blocks)):
+            if infer and bi >= 2:
+                blocks.append(blocks[bi % 2])
+                continue
             blocks.append({
                 "mid": e(M, Cp), "out": e(M, Cp), "ln1": e(M, Cp, dt=T), "m1": e(M), "r1": e(M),
                 "qkv": e(3 * M * nh * 32, dt=T), "O": e(M, nh * 32, dt=T), "lse": e(nWin * nh * WS_TOK),
                 "ln2": e(M, Cp, dt=T), "m2": e(M), "r2": e(M), "u": e(M, Hdp, dt=T), "h": e(M, Hdp, dt=T)})
         P["blocks"] = blocks
-        P["rstb_out"] = [e(M, Cp) for _ in self.rstb]
+        P["rstb_out"] = [e(M, Cp) for _ in range(min(2, len(self.rstb)) if infer else len(self.rstb))]
+        if infer:
+            P["rstb_out"] = [P["rstb_out"][i % len(P["rstb_out"])] for i in range(len(self.rstb))]
         P["nf"], P["n_mean"], P["n_rstd"] = e(M, Cp), e(M), e(M)
         P["fb"] = e(M, Cp)
         if self.upsampler == "pixelshuffle":
@@ -301,6 +327,9 @@ class SwinIREngine:
             P["ups_act"] = acts
             P["M_hr"] = hw
         P["E"] = e(B, self.in_ch, Hh * self.scale, Ww * self.scale)
+        P["infer"] = infer
+        if infer:
+            return P
         # backward scratch
         P["D"], P["G"] = e(M, Cp), e(M, Cp)
         P["dU"], P["dxn"] = e(M, Hdp, dt=T), e(M, Cp, dt=T)
@@ -324,7 +353,6 @@ class SwinIREngine:
         P["dfb"] = e(M, Cp)
         # one shared wgrad workspace sized for the largest (splits * N * K)
         P["wg_ws"] = e(self._max_wgrad_ws(M, P))
-        self.plans[key] = P
         return P
 
     def _wgrad_shapes(self, M, P):
@@ -368,7 +396,7 @@ class SwinIREngine:
         P["drop"] = drop_scales
         H.image_to_nhwc(x, P["xin"], self.Cin_p, self.mean, self.img_range, B, self.in_ch, Hh, Ww)
         c = self.conv_first
-        H.gemm_nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), H.rows(c.Wf), H.epilogue(P["f0"], bias=c.bp), M, Cp,
+        H.gemm_nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), c.fwd(), H.epilogue(P["f0"], bias=c.bp), M, Cp,
                   9 * self.Cin_p, cd)
         n = self.pe_norm
         H.layernorm_fwd(P["f0"], Cp, P["s0"], Cp, n.weight, n.bias, P["pe_mean"], P["pe_rstd"], M, self.C, n.eps)
@@ -380,30 +408,30 @@ class SwinIREngine:
                 cur = self._block_fwd(blk, P, P["blocks"][bi], cur, bi)
                 bi += 1
             out = P["rstb_out"][gi]
-            H.gemm_nt(H.im2col(cur, Hh, Ww, Cp), H.rows(conv.Wf), H.epilogue(out, bias=conv.bp, resid=g_in), M, Cp,
+            H.gemm_nt(H.im2col(cur, Hh, Ww, Cp), conv.fwd(), H.epilogue(out, bias=conv.bp, resid=g_in), M, Cp,
                       9 * Cp, cd)
             cur = out
         n = self.norm
         H.layernorm_fwd(cur, Cp, P["nf"], Cp, n.weight, n.bias, P["n_mean"], P["n_rstd"], M, self.C, n.eps)
-        H.gemm_nt(H.im2col(P["nf"], Hh, Ww, Cp), H.rows(self.cab.Wf), H.epilogue(P["fb"], bias=self.cab.bp, resid=P["f0"]),
+        H.gemm_nt(H.im2col(P["nf"], Hh, Ww, Cp), self.cab.fwd(), H.epilogue(P["fb"], bias=self.cab.bp, resid=P["f0"]),
                   M, Cp, 9 * Cp, cd)
         img = (self.mean, self.img_range, self.in_ch, Hh * self.scale, Ww * self.scale)
         if self.upsampler == "pixelshuffle":
             c = self.cbu
-            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), H.rows(c.Wf),
+            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
                       H.epilogue(P["a0"], bias=c.bp, act=H.ACT_LEAKY, slope=0.01), M, 64, 9 * Cp, cd)
             src, h, w = P["a0"], Hh, Ww
             for c, r, dst in zip(self.ups, self.ups_r, P["ups_act"]):
-                H.gemm_nt(H.im2col(src, h, w, 64), H.rows(c.Wf), H.epilogue(dst, mode=H.OUT_PSHUF, ldo=64, bias=c.bp,
+                H.gemm_nt(H.im2col(src, h, w, 64), c.fwd(), H.epilogue(dst, mode=H.OUT_PSHUF, ldo=64, bias=c.bp,
                                                                             ps=(r, h, w)), B * h * w, c.Co, 9 * 64, cd)
                 src, h, w = dst, h * r, w * r
             c = self.last
-            H.gemm_nt(H.im2col(src, h, w, 64), H.rows(c.Wf),
+            H.gemm_nt(H.im2col(src, h, w, 64), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(self.mean, self.img_range, self.in_ch, h, w)),
                       B * h * w, c.Cop, 9 * 64, cd)
         else:
             c = self.up1
-            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), H.rows(c.Wf),
+            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_PSHUF_NCHW, ldo=0, bias=c.bp, ps=(self.scale, Hh, Ww),
                                  img=(self.mean, self.img_range, self.in_ch, Hh, Ww)), M, c.Cop, 9 * Cp, cd)
         return P["E"]
@@ -616,10 +644,20 @@ class SwinIREngine:
 
 class SwinIRFunction(torch.autograd.Function):
     """The whole SwinIR forward/backward as one autograd node (params are inputs so that any
-    optimizer / DDP reducer sees ordinary .grad tensors)."""
+    optimizer / DDP reducer sees ordinary .grad tensors).
+
+    The node leases its plan (kair_amd/engine/plans.py) from forward to backward, so two forwards
+    before one backward each keep their own saved activations; no-grad forwards use a small
+    inference plan."""
+
+    @classmethod
+    def run(cls, engine, x, params):
+        """Entry point: the plan mode is decided here, where the caller's grad mode is visible
+        (inside Function.forward autograd has switched it off)."""
+        return cls.apply(engine, autograd_mode(params), x, *params)
 
     @staticmethod
-    def forward(ctx, engine, x, *params):
+    def forward(ctx, engine, mode, x, *params):
         net = engine.net_ref()
         B, C, H0, W0 = x.shape
         ws = engine.ws
@@ -627,31 +665,36 @@ class SwinIRFunction(torch.autograd.Function):
         if ph or pw:   # check_image_size (network_swinir.py:783-788)
             x = torch.nn.functional.pad(x, (0, pw, 0, ph), "reflect")
         drop = None
-        if net.training and torch.is_grad_enabled() and any(b.dp > 0 for b in engine.blocks):
+        if mode == "lease" and net.training and any(b.dp > 0 for b in engine.blocks):
             drop = drop_path_scales(engine, x.shape[0], x.device)
-        E = engine.forward(x.float(), drop)
+        with plan_mode(engine, mode):
+            E = engine.forward(x.float(), drop)
         ctx.engine = engine
         ctx.params = params
-        ctx.plan = engine.cur
+        ctx.lease = Lease(engine.cur) if mode == "lease" else None
         out = E[:, :, :H0 * engine.scale, :W0 * engine.scale]
         return out.clone() if (ph or pw) else E.clone()
 
     @staticmethod
     def backward(ctx, gE):
         eng = ctx.engine
+        if ctx.lease is None or ctx.lease.plan is None:
+            raise RuntimeError("kair_amd SwinIR: backward through a forward whose activations were released "
+                               "(a second backward needs retain_graph-style reuse, which is not supported)")
         flat = torch.empty(sum(p.numel() for p in ctx.params), device=gE.device)
         grads, off = {}, 0
         for p in ctx.params:
             grads[p] = flat[off:off + p.numel()].view_as(p)
             off += p.numel()
-        P = ctx.plan
+        P = ctx.lease.plan
         eng.cur = P
         full = gE
         if gE.shape[-2:] != P["E"].shape[-2:]:
             full = torch.zeros_like(P["E"])
             full[:, :, :gE.shape[2], :gE.shape[3]] = gE
         eng.backward_from_grad(full.float(), grads)
-        return (None, None) + tuple(grads[p] for p in ctx.params)
+        ctx.lease.release()
+        return (None, None, None) + tuple(grads[p] for p in ctx.params)
 
 
 def drop_path_scales(engine, B, device, generator=None):

@@ -30,6 +30,7 @@ import torch
 import torch.nn as nn
 
 from .. import _hip as H
+from .plans import Lease, PlanPool, autograd_mode, plan_mode
 
 C8 = 8   # channel stride of the ResUNet input (x, beta) and of the tail-output gradient rows
 
@@ -132,7 +133,8 @@ class USRNetEngine:
         self.nc = [self.head.Co] + [d.Co for d in self.downs]
         if any(c % 8 for c in self.nc):
             raise NotImplementedError("kair_amd USRNet: ResUNet channel counts must be multiples of 8")
-        self.plans = {}
+        self.plans = PlanPool(self._build_plan)
+        self.plan_mode = "primary"
         self._packed_version = None
         self._pack_table = None
         self.blocks = []
@@ -167,9 +169,10 @@ class USRNetEngine:
         return [{"h": self._e(M, c, dt=self.tdt), "out": self._e(M, c)} for _ in range(n)]
 
     def plan(self, B, h, w, sf, kh, kw):
-        key = (B, h, w, sf, kh, kw)
-        if key in self.plans:
-            return self.plans[key]
+        return self.plans.get((B, h, w, sf, kh, kw), self.plan_mode)
+
+    def _build_plan(self, key, infer):
+        B, h, w, sf, kh, kw = key
         Hh, Ww = h * sf, w * sf
         if Hh % 8 or Ww % 8:
             raise NotImplementedError("kair_amd USRNet: the HR size must be a multiple of 8 (the ResUNet's "
@@ -206,7 +209,6 @@ class USRNetEngine:
         shapes += [(M[l], nc[l], 9 * nc[l]) for l in range(4)]
         shapes += [(M[l + 1], nc[l + 1], 4 * nc[l]) for l in range(3)]
         P["wg_ws"] = e(max(H.wgrad_splits(m, n, k) * n * k for m, n, k in shapes))
-        self.plans[key] = P
         return P
 
     # ------------------------------------------------------------------------------------
@@ -389,22 +391,32 @@ class USRNetEngine:
 
 
 class USRNetFunction(torch.autograd.Function):
-    """The whole unfolded USRNet forward/backward as one autograd node (params are inputs)."""
+    """The whole unfolded USRNet forward/backward as one autograd node (params are inputs); the
+    node leases its plan from forward to backward (kair_amd/engine/plans.py)."""
+
+    @classmethod
+    def run(cls, engine, x, k, sf, sigma, params):
+        return cls.apply(engine, autograd_mode(params), x, k, sf, sigma, *params)
 
     @staticmethod
-    def forward(ctx, engine, x, k, sf, sigma, *params):
-        E = engine.forward(x, k, sf, sigma)
-        ctx.engine, ctx.params, ctx.plan = engine, params, engine.cur
+    def forward(ctx, engine, mode, x, k, sf, sigma, *params):
+        with plan_mode(engine, mode):
+            E = engine.forward(x, k, sf, sigma)
+        ctx.engine, ctx.params = engine, params
+        ctx.lease = Lease(engine.cur) if mode == "lease" else None
         return E.clone()
 
     @staticmethod
     def backward(ctx, gE):
         eng = ctx.engine
+        if ctx.lease is None or ctx.lease.plan is None:
+            raise RuntimeError("kair_amd USRNet: backward through a forward whose activations were released")
         flat = torch.empty(sum(p.numel() for p in ctx.params), device=gE.device)
         grads, off = {}, 0
         for p in ctx.params:
             grads[p] = flat[off:off + p.numel()].view_as(p)
             off += p.numel()
-        eng.cur = ctx.plan
+        eng.cur = ctx.lease.plan
         eng.backward_from_grad(gE.float(), grads)
-        return (None,) * 5 + tuple(grads[p] for p in ctx.params)
+        ctx.lease.release()
+        return (None,) * 6 + tuple(grads[p] for p in ctx.params)

@@ -3,10 +3,14 @@
 Kept: network save/load (strict, or non-strict copy-by-position; 'params' key unwrap,
 model_base.py:158-216), optimizer / scheduler save & load in torch's own state_dict formats
 (221-245), update_E EMA over parameters only (247-252), get_bare_model.
-Changed for MI355X: model_to_device does not wrap the fused-engine networks in DDP — their
-gradient all-reduce is done by kair_amd.engine.trainer.FusedTrainer on the flat gradient buffer
-(RCCL); other modules keep DistributedDataParallel.  The SPECT evaluation helpers
-(model_base.py:280-569) are out of scope.
+Changed for MI355X: a network with a HIP step program (`engine`) is not wrapped in DDP here.
+When ModelPlain then uses the fused trainer, kair_amd.engine.trainer.FusedTrainer owns the
+gradient all-reduce (RCCL, flat buffer); when it falls back to the autograd + torch.optim path
+(l2 loss, grad clipping, regularizers, ...) ModelPlain.define_optimizer wraps the network in
+DistributedDataParallel then (wrap_ddp), so ranks never train divergent replicas.  With dist on,
+rank 0's parameters and buffers are broadcast at construction (the reference's DDP construction
+does this, model_base.py:116) before netE is seeded from netG.
+The SPECT evaluation helpers (model_base.py:280-569) are out of scope.
 """
 import os
 
@@ -19,9 +23,14 @@ class ModelBase:
     def __init__(self, opt):
         self.opt = opt
         self.save_dir = opt["path"]["models"]
-        if not torch.cuda.is_available():
-            raise RuntimeError("kair_amd trains on the MI355X (HIP device) only; no CPU fallback")
-        self.device = torch.device("cuda", torch.cuda.current_device())
+        # model_base.py:18 -- 'cuda' when gpu_ids is set, else the host.  Only DnCNN (BASELINE
+        # config 1) has a host path; the other networks raise on CPU tensors.
+        if opt.get("gpu_ids") is not None:
+            if not torch.cuda.is_available():
+                raise RuntimeError("kair_amd: gpu_ids is set but no HIP device is visible")
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        else:
+            self.device = torch.device("cpu")
         self.is_train = opt["is_train"]
         self.schedulers = []
 
@@ -75,12 +84,32 @@ class ModelBase:
 
     def model_to_device(self, network):
         network = network.to(self.device)
-        if hasattr(network, "engine") and getattr(network, "fused_trainable", True):
-            return network           # fused engine: FusedTrainer owns the gradient all-reduce
         if self.opt.get("dist"):
-            return DistributedDataParallel(network, device_ids=[torch.cuda.current_device()],
-                                           find_unused_parameters=self.opt.get("find_unused_parameters", False))
+            self.broadcast_from_rank0(network)
+        if hasattr(network, "engine") and self.device.type == "cuda":
+            return network           # DDP decided in define_optimizer (fused trainer or wrap_ddp)
+        if self.opt.get("dist"):
+            return self.wrap_ddp(network)
         return network
+
+    def wrap_ddp(self, network):
+        """DistributedDataParallel as in model_base.py:113-119 (no-op when already wrapped)."""
+        if isinstance(network, (DataParallel, DistributedDataParallel)):
+            return network
+        ids = [torch.cuda.current_device()] if self.device.type == "cuda" else None
+        net = DistributedDataParallel(network, device_ids=ids,
+                                      find_unused_parameters=self.opt.get("find_unused_parameters", False))
+        if self.opt.get("use_static_graph"):
+            net._set_static_graph()
+        return net
+
+    @staticmethod
+    @torch.no_grad()
+    def broadcast_from_rank0(network):
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            for t in network.state_dict().values():
+                dist.broadcast(t, 0)
 
     # -------------------------------------------------------------- info
     def describe_network(self, network):

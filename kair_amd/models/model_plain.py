@@ -48,16 +48,38 @@ class FusedAdam(torch.optim.Optimizer):
         return {"state": st, "param_groups": groups}
 
     def load_state_dict(self, sd):
+        """torch.optim.Adam state_dict format; validated like torch (group sizes, per-parameter
+        shapes, one shared step count) before anything is copied."""
         t = self.trainer
+        groups = sd.get("param_groups", [])
+        if len(groups) != len(self.param_groups) or sum(len(g["params"]) for g in groups) != len(t.params):
+            raise ValueError("loaded state dict contains a parameter group that doesn't match the size of "
+                             "optimizer's group")
+        ids = [i for g in groups for i in g["params"]]
+        state = sd.get("state", {})
+        steps = set()
+        for i, p in zip(ids, t.params):
+            s = state.get(i, state.get(str(i)))
+            if s is None:
+                continue
+            if tuple(s["exp_avg"].shape) != tuple(p.shape) or tuple(s["exp_avg_sq"].shape) != tuple(p.shape):
+                raise ValueError(f"optimizer state for parameter {i}: shape {tuple(s['exp_avg'].shape)} != {tuple(p.shape)}")
+            steps.add(int(float(s["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"optimizer state has per-parameter step counts {sorted(steps)}; the fused Adam keeps one")
         off = 0
-        for i, p in enumerate(t.params):
+        for i, p in zip(ids, t.params):
             n = p.numel()
-            s = sd["state"].get(i) or sd["state"].get(str(i))
+            s = state.get(i, state.get(str(i)))
             if s is not None:
                 t.m[off:off + n].copy_(s["exp_avg"].reshape(-1))
                 t.v[off:off + n].copy_(s["exp_avg_sq"].reshape(-1))
-                t.t = int(float(s["step"]))
+            else:
+                t.m[off:off + n].zero_()
+                t.v[off:off + n].zero_()
             off += n
+        if steps:
+            t.t = steps.pop()
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             for k in ("lr", "betas", "eps", "weight_decay", "initial_lr"):
                 if k in sg:
@@ -157,7 +179,8 @@ class ModelPlain(ModelBase):
 
     def _fused_ok(self):
         net = self.get_bare_model(self.netG)
-        return (hasattr(net, "engine") and self.G_lossfn_type == "l1" and not self.opt_train.get("G_optimizer_clipgrad")
+        return (hasattr(net, "engine") and self.device.type == "cuda" and all(p.requires_grad for p in net.parameters())
+                and self.G_lossfn_type == "l1" and not self.opt_train.get("G_optimizer_clipgrad")
                 and self.opt_train["G_optimizer_type"] == "adam" and not self.amp_enabled
                 and not self.opt_train.get("G_regularizer_orthstep") and not self.opt_train.get("G_regularizer_clipstep"))
 
@@ -176,6 +199,9 @@ class ModelPlain(ModelBase):
         else:
             if tr["G_optimizer_type"] != "adam":
                 raise NotImplementedError
+            self.trainer = None
+            if self.opt.get("dist"):   # autograd path: DDP owns the all-reduce (model_base.py:113-119)
+                self.netG = self.wrap_ddp(self.netG)
             self.G_optimizer = Adam(params, lr=tr["G_optimizer_lr"], betas=tr["G_optimizer_betas"],
                                     weight_decay=tr["G_optimizer_wd"])
 

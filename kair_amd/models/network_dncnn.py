@@ -2,8 +2,13 @@
 
 `model` is the flattened Sequential basicblock.sequential builds (basicblock.py:61-98): conv,
 act, [conv, BatchNorm2d(momentum 0.9, eps 1e-4), act] x (nb-2), conv — so state_dict keys
-(model.0.weight, model.3.running_mean, ...) match the reference.  `forward` runs the whole
-network as one autograd node on the HIP step program (kair_amd/engine/dncnn_engine.py).
+(model.0.weight, model.3.running_mean, ...) match the reference.
+
+`forward` on a HIP tensor runs the whole network as one autograd node on the HIP step program
+(kair_amd/engine/dncnn_engine.py); it raises if libkair_hip.so is missing.  On a CPU tensor it
+runs the module list itself: that is BASELINE config 1 ("DnCNN sigma=25, main_train_dncnn.py on
+CPU, plumbing, no GPU"), the one configuration the reference specifies for the host -- never a
+substitute for a device call.
 """
 import torch
 import torch.nn as nn
@@ -50,6 +55,10 @@ class _Base(nn.Module):
             self._engine = DnCNNEngine(self, self.compute_dtype, residual=self.residual)
         return self._engine
 
+    def invalidate_engine(self):
+        """The module list changed (utils_bnorm.merge_bn / tidy_sequential): rebuild on next use."""
+        self._engine = None
+
     def _apply(self, fn, *args, **kwargs):
         self._engine = None
         return super()._apply(fn, *args, **kwargs)
@@ -60,9 +69,12 @@ class _Base(nn.Module):
         return self
 
     def forward(self, x):
-        if not x.is_cuda:
-            raise RuntimeError("kair_amd DnCNN runs on the MI355X (HIP) only; got a CPU tensor (no CPU fallback)")
-        return ConvNetFunction.apply(self.engine(), x, *list(self.parameters()))
+        if x.is_cuda:
+            return ConvNetFunction.run(self.engine(), x, list(self.parameters()))
+        if next(self.parameters()).is_cuda:
+            raise RuntimeError("kair_amd DnCNN: CPU input for a network on the HIP device")
+        n = self.model(x)                                   # config 1: host execution (network_dncnn.py:69-71)
+        return x - n if self.residual else n
 
 
 class DnCNN(_Base):

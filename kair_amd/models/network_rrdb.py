@@ -97,4 +97,4 @@ class RRDB(nn.Module):
     def forward(self, x):
         if not x.is_cuda:
             raise RuntimeError("kair_amd RRDB runs on the MI355X (HIP) only; got a CPU tensor (no CPU fallback)")
-        return ConvNetFunction.apply(self.engine(), x, *list(self.parameters()))
+        return ConvNetFunction.run(self.engine(), x, list(self.parameters()))

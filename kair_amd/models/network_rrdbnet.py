@@ -95,4 +95,4 @@ class RRDBNet(nn.Module):
     def forward(self, x):
         if not x.is_cuda:
             raise RuntimeError("kair_amd RRDBNet runs on the MI355X (HIP) only; got a CPU tensor (no CPU fallback)")
-        return ConvNetFunction.apply(self.engine(), x, *list(self.parameters()))
+        return ConvNetFunction.run(self.engine(), x, list(self.parameters()))

@@ -156,13 +156,15 @@ class SwinIR(nn.Module):
     Extra (engine) options, all keyword-only and absent from the reference:
       compute_dtype  'bf16' (default, MFMA bf16 with fp32 accumulation/master weights) or 'fp32'
                      (exact fp32 MFMA; the parity mode)
+      split_conv     bf16 only (default True): forward 3x3 convs use hi/lo bf16 weight pairs, which
+                     removes the output bias of bf16 weight rounding (DESIGN.md "parity at bf16")
     """
 
     def __init__(self, img_size=64, patch_size=1, in_chans=3, embed_dim=96, depths=(6, 6, 6, 6),
                  num_heads=(6, 6, 6, 6), window_size=7, mlp_ratio=4.0, qkv_bias=True, qk_scale=None, drop_rate=0.0,
                  attn_drop_rate=0.0, drop_path_rate=0.1, norm_layer=nn.LayerNorm, ape=False, patch_norm=True,
                  use_checkpoint=False, upscale=2, img_range=1.0, upsampler="", resi_connection="1conv",
-                 compute_dtype="bf16", **kwargs):
+                 compute_dtype="bf16", split_conv=True, **kwargs):
         super().__init__()
         if ape or not patch_norm or patch_size != 1 or not qkv_bias or qk_scale is not None:
             raise NotImplementedError("kair_amd SwinIR: ape / patch_norm=False / patch_size!=1 / custom qk are off-path")
@@ -197,6 +199,7 @@ class SwinIR(nn.Module):
             raise NotImplementedError(f"kair_amd SwinIR: upsampler '{upsampler}' is not on the MI355X path yet")
         self.apply(self._init_weights)
         self.compute_dtype = compute_dtype
+        self.split_conv = split_conv
         self._engine = None
 
     @staticmethod
@@ -221,7 +224,7 @@ class SwinIR(nn.Module):
     # ------------------------------------------------------------------------------------
     def engine(self):
         if self._engine is None or self._engine.net_ref() is not self:
-            self._engine = SwinIREngine(self, self.compute_dtype)
+            self._engine = SwinIREngine(self, self.compute_dtype, self.split_conv)
         return self._engine
 
     def _apply(self, fn, *args, **kwargs):
@@ -237,7 +240,7 @@ class SwinIR(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("kair_amd SwinIR runs on the MI355X (HIP) only; got a CPU tensor (no CPU fallback)")
         params = [p for p in self.parameters()]
-        return SwinIRFunction.apply(self.engine(), x, *params)
+        return SwinIRFunction.run(self.engine(), x, params)
 
     def flops(self):
         """Training FLOPs are tracked by kair_amd.engine.swinir_engine.swinir_flops()."""

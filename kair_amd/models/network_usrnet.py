@@ -100,4 +100,4 @@ class USRNet(nn.Module):
     def forward(self, x, k, sf, sigma):
         if not x.is_cuda:
             raise RuntimeError("kair_amd USRNet runs on the MI355X (HIP) only; got a CPU tensor (no CPU fallback)")
-        return USRNetFunction.apply(self.engine(), x, k, int(sf), sigma, *list(self.parameters()))
+        return USRNetFunction.run(self.engine(), x, k, int(sf), sigma, list(self.parameters()))

@@ -117,8 +117,11 @@ class SwinTransformerBlock(nn.Module):
             a = torch.roll(a, (self.shift, self.shift), (1, 2))
         a = a.reshape(B, L, C)
         if keep is not None:                                              # DropPath (train only)
-            x = x + a * keep
-            return x + self.mlp(self.norm2(x)) * keep
+            # timm DropPath draws the two branches' masks independently (:268, :275): keep may be
+            # one per-sample scale for both branches or an (attn, mlp) pair
+            ka, km = keep if isinstance(keep, (tuple, list)) else (keep, keep)
+            x = x + a * ka
+            return x + self.mlp(self.norm2(x)) * km
         x = x + a
         return x + self.mlp(self.norm2(x))
 

@@ -131,6 +131,35 @@ def test_conv3x3_halo_path(shape, flip, a_f32, resid):
     assert rel_err(got, ref) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 48, 48, 192, 180), (2, 12, 20, 64, 256), (1, 16, 16, 8, 180), (2, 24, 24, 64, 16)])
+def test_conv3x3_split_weights(shape):
+    """hi/lo split bf16 weights (pack kind 9, kair_operand.w_split) through the halo kernel (first
+    shape) and the register-staged kernel (others, incl. K = 72 with a partial last chunk): with
+    bf16-exact activations the product must carry the fp32 weights to ~2^-16, against ~2^-9 for
+    plain bf16 weights."""
+    B, Hh, Ww, Cin, Cout = shape
+    g = torch.Generator().manual_seed(Hh + Cin + Cout)
+    x = torch.randn(B, Cin, Hh, Ww, generator=g).bfloat16().float()
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) * 0.05
+    bias = torch.randn(Cout, generator=g)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), padding=1) + bias.double().view(1, -1, 1, 1)
+    M = B * Hh * Ww
+    xin = x.permute(0, 2, 3, 1).contiguous().view(M, Cin).to(dev, torch.bfloat16)
+    kf = 2 * ((9 * Cin + 63) // 64) * 64
+    Wsplit = torch.empty(Cout, kf, device=dev, dtype=torch.bfloat16)
+    H.pack_weight(w.to(dev), Wsplit, H.wmap(9, Cout, Cin, (1, Cout, Cout), (1, Cin, Cin)))
+    Wplain = torch.empty(Cout, 9 * Cin, device=dev, dtype=torch.bfloat16)
+    H.pack_weight(w.to(dev), Wplain, H.wmap(1, Cout, Cin, (1, Cout, Cout), (1, Cin, Cin)))
+    errs = []
+    for Wb, split in ((Wsplit, True), (Wplain, False)):
+        out = torch.empty(M, Cout, device=dev)
+        H.gemm_nt(H.im2col(xin, Hh, Ww, Cin), H.rows(Wb, w_split=split), H.epilogue(out, bias=bias.to(dev)), M, Cout,
+                  9 * Cin, H.BF16)
+        torch.cuda.synchronize()
+        errs.append(rel_err(out.cpu().view(B, Hh, Ww, Cout).permute(0, 3, 1, 2), ref))
+    assert errs[0] < 3e-5 and errs[1] > 8 * errs[0], errs
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,Np,ld", [(100003, 16, 16), (70000, 256, 256), (4097, 64, 72), (5000, 20, 20)])
 def test_colsum_bias_gradient(dt, M, Np, ld):
