@@ -288,6 +288,22 @@ int kair_hypanet_bwd(const float* sigma, float sf, const float* W1, const float*
                      float* gW1, float* gb1, float* gW2, float* gb2, float* gW3, float* gb3, int accumulate,
                      void* stream);
 
+/* ---- training-patch synthesis ------------------------------------------
+ * pool: fp32 NCHW image pool [N][C][Hs][Ws] in [0, 1] (HBM-resident); params: int4 per sample
+ * {image, rnd_h, rnd_w, mode} (rnd_* in L coordinates for SR, H coordinates for denoising; mode the
+ * utils_image.augment_img mode 0..7).  Outputs fp32 NCHW [B][C][PS][PS] (H) and L.
+ * kair_synth_sr replaces DatasetSR.__getitem__ (data/dataset_sr.py:35-92): L = MATLAB bicubic x1/sf
+ * of the whole image (utils_image.imresize, utils_image.py:938-1005; separable taps wh/ih [Hs/sf][P],
+ * ww/iw [Ws/sf][P] from calculate_weights_indices :880-932, source indices already reflected),
+ * cropped at (rnd_h, rnd_w) and augmented; H the aligned sf x larger crop.
+ * kair_synth_dn replaces DatasetDnCNN.__getitem__ train branch (data/dataset_dncnn.py:50-75):
+ * L = H + sigma * N(0,1) (sigma = sigma_255 / 255), Philox-4x32-10 normals keyed by (seed, step). */
+int kair_synth_sr(const float* pool, int C, int Hs, int Ws, const int* params, int B, int PS, int sf,
+                  const float* wh, const int* ih, const float* ww, const int* iw, int P, float* outH,
+                  float* outL, void* stream);
+int kair_synth_dn(const float* pool, int C, int Hs, int Ws, const int* params, int B, int PS, float sigma,
+                  unsigned long long seed, unsigned long long step, float* outH, float* outL, void* stream);
+
 const char* kair_last_error(void);
 int kair_device_arch(char* buf, int len);
 

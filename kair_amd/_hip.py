@@ -117,6 +117,10 @@ _SIGS = {
     "kair_usr_pack_input": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_long, c_vp],
     "kair_hypanet_fwd": [c_vp, c_float] + [c_vp] * 6 + [c_int, c_int, c_int, c_vp, c_vp],
     "kair_hypanet_bwd": [c_vp, c_float] + [c_vp] * 6 + [c_int, c_int, c_int, c_vp] + [c_vp] * 6 + [c_int, c_vp],
+    "kair_synth_sr": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp,
+                      c_vp],
+    "kair_synth_dn": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_float, ctypes.c_ulonglong, ctypes.c_ulonglong,
+                      c_vp, c_vp, c_vp],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
@@ -467,3 +471,21 @@ def bn_bwd(z, ldz, a, lda, da, ldda, dz, lddz, M, C, gamma, mean, rstd, act, slo
     check(lib().kair_bn_bwd(ptr(z), ldz, ptr(a), dtype_code(a) if a is not None else F32, lda, ptr(da), ldda, ptr(dz),
                             dtype_code(dz), lddz, M, C, ptr(gamma), ptr(mean), ptr(rstd), act, slope, ptr(dgamma), ptr(dbeta),
                             int(accumulate), ptr(ws), stream_ptr()), "bn_bwd")
+
+
+# ------------------------------------------------------------------------------------------
+# training-patch synthesis (kair_amd/data/gpu_synth.py)
+# ------------------------------------------------------------------------------------------
+def synth_sr(pool, params, B, PS, sf, taps_h, taps_w, outH, outL):
+    require_device(pool, params, outH, outL)
+    N, C, Hs, Ws = pool.shape
+    (ih, wh), (iw, ww) = taps_h, taps_w
+    check(lib().kair_synth_sr(ptr(pool), C, Hs, Ws, ptr(params), B, PS, sf, ptr(wh), ptr(ih), ptr(ww), ptr(iw),
+                              wh.shape[1], ptr(outH), ptr(outL), stream_ptr()), "synth_sr")
+
+
+def synth_dn(pool, params, B, PS, sigma, seed, step, outH, outL):
+    require_device(pool, params, outH, outL)
+    N, C, Hs, Ws = pool.shape
+    check(lib().kair_synth_dn(ptr(pool), C, Hs, Ws, ptr(params), B, PS, sigma, seed, step, ptr(outH), ptr(outL),
+                              stream_ptr()), "synth_dn")

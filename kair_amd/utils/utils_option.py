@@ -97,8 +97,10 @@ def parse(opt_path, is_train=True):
 def find_last_checkpoint(save_dir, net_type="G", pretrained_path=None):
     """utils_option.py:213-235: newest '{iter}_{net_type}.pth' in save_dir, else the pretrained path."""
     files = glob.glob(os.path.join(save_dir, "*_{}.pth".format(net_type)))
-    if files:
-        iters = [int(re.findall(r"(\d+)_{}.pth".format(net_type), f)[0]) for f in files]
+    # numbered files only: the reference indexes re.findall(...)[0] and raises on 'latest_G.pth'
+    iters = [int(m.group(1)) for m in (re.fullmatch(r"(\d+)_{}\.pth".format(re.escape(net_type)), os.path.basename(f))
+                                        for f in files) if m]
+    if iters:
         it = max(iters)
         return it, os.path.join(save_dir, "{}_{}.pth".format(it, net_type))
     return 0, pretrained_path
