@@ -189,17 +189,19 @@ int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int dy_dtype, l
  * qkv: head-blocked [3][nWin][nh][64][32] (dtype); table: fp32 [(2ws-1)^2][nh] (reference
  * layout); O written to rows [nWin*64, ldo] window order, head h at columns h*32..h*32+31;
  * lse fp32 [nWin][nh][64] (for backward).  Region mask is computed analytically for a
- * shift>0 block on an H x W token grid (calculate_mask, network_swinir.py:216-237). */
+ * shift>0 block on an H x W token grid (calculate_mask, network_swinir.py:216-237).
+ * mask (optional, shift must be 0): an explicit additive fp32 mask [mask_nw][64][64] indexed by
+ * window % mask_nw -- WindowAttention.forward(x, mask) with a caller-built mask (:132-136). */
 int kair_window_attn_fwd(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
                          long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
-                         void* stream);
+                         const float* mask, int mask_nw, void* stream);
 /* Backward: dO rows [nWin*64, lddo] (dtype, same layout as O); writes dqkv head-blocked (dtype);
  * dtable (+)= bias-table gradient (ws: nh*64*64*partials floats, kair_window_attn_bwd_ws()). */
 long kair_window_attn_bwd_ws(long nWin, int nh);
 int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
                          const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
                          float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
-                         void* stream);
+                         const float* mask, int mask_nw, void* stream);
 
 /* Elementwise / small kernels ------------------------------------------------------------- */
 /* NCHW fp32 image -> NHWC (dtype) with channel stride ldc, x' = (x - mean[c]) * img_range
@@ -231,7 +233,8 @@ int kair_axpby(float* y, const float* x, float a, float b, long n, void* stream)
 /* y[m][c] = a * x[m][c] + b * y[m][c] for c < C over strided fp32 rows */
 int kair_axpby_rows(float* y, long ldy, const float* x, long ldx, long M, int C, float a, float b, void* stream);
 /* out[m][c] (dtype) = G[m][c] * act'(X[m][c]) for c < C  (act' from the POST-activation value X:
- * kind 1 ReLU, 2 LeakyReLU(slope); 0 identity), optionally * scale.  Row strides ldg / ldx / ldo. */
+ * kind 1 ReLU, 2 LeakyReLU(slope); 0 identity; kind 3: exact-erf GELU' of the PRE-activation X),
+ * optionally * scale.  Row strides ldg / ldx / ldo. */
 int kair_act_grad_cast(const float* G, long ldg, const void* X, int x_dtype, long ldx, void* out, int out_dtype,
                        long ldo, long M, int C, int kind, float slope, float scale, void* stream);
 /* 2x2 sum-pool (adjoint of nearest x2 upsample): dst[b][y][x][c] (+)= sum_{i,j<2} src[b][2y+i][2x+j][c].

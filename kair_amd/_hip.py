@@ -89,10 +89,10 @@ _SIGS = {
                            c_vp, c_long, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(CopyDesc), c_vp],
     "kair_row_copy": [c_vp, c_long, c_long, c_int, ctypes.POINTER(CopyDesc), c_vp],
     "kair_window_attn_fwd": [c_vp, c_int, c_vp, c_vp, c_long, c_vp, c_long, c_int, c_int, c_float, c_int, c_int, c_int,
-                             c_int, c_vp],
+                             c_int, c_vp, c_int, c_vp],
     "kair_window_attn_bwd_ws": [c_long, c_int],
     "kair_window_attn_bwd": [c_vp, c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_int,
-                             c_int, c_float, c_int, c_int, c_int, c_vp],
+                             c_int, c_float, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "kair_image_to_nhwc": [c_vp, c_vp, c_int, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
     "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "kair_axpy": [c_vp, c_vp, c_float, c_long, c_vp],
@@ -354,19 +354,22 @@ def row_copy(src, ld_src, M, C, copy):
     check(lib().kair_row_copy(ptr(src), ld_src, M, C, ctypes.byref(copy), stream_ptr()), "row_copy")
 
 
-def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, ones_col=-1):
+def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, ones_col=-1, mask=None):
+    mnw = mask.shape[0] if mask is not None else 0
     check(lib().kair_window_attn_fwd(ptr(qkv), dtype_code(qkv), ptr(table), ptr(O), ldo, ptr(lse), nWin, nh, hd, scale,
-                                     H, W, shift, ones_col, stream_ptr()), "window_attn_fwd")
+                                     H, W, shift, ones_col, ptr(mask), mnw, stream_ptr()), "window_attn_fwd")
 
 
 def window_attn_bwd_ws(nWin, nh):
     return lib().kair_window_attn_bwd_ws(nWin, nh)
 
 
-def window_attn_bwd(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc, ws, nWin, nh, hd, scale, H, W, shift):
+def window_attn_bwd(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc, ws, nWin, nh, hd, scale, H, W, shift,
+                    mask=None):
+    mnw = mask.shape[0] if mask is not None else 0
     check(lib().kair_window_attn_bwd(ptr(qkv), ptr(O), ldo, ptr(dO), lddo, dtype_code(qkv), ptr(table), ptr(lse),
                                      ptr(dqkv), ptr(dtable), int(dtable_acc), ptr(ws), nWin, nh, hd, scale, H, W, shift,
-                                     stream_ptr()), "window_attn_bwd")
+                                     ptr(mask), mnw, stream_ptr()), "window_attn_bwd")
 
 
 def image_to_nhwc(img, out, ldc, mean, img_range, B, C, H, W):

@@ -406,7 +406,9 @@ __global__ void act_grad_cast_kernel(const float* __restrict__ G, long ldg, cons
   const long m = i / C;
   const int c = (int)(i - m * C);
   float g = G[m * ldg + c] * scale;
-  if (kind) {
+  if (kind == 3) {
+    g *= gelu_erf_grad((float)X[m * ldx + c]);   // X = pre-activation (nn.GELU backward)
+  } else if (kind) {
     const float xv = (float)X[m * ldx + c];
     g = xv > 0.f ? g : (kind == 2 ? g * slope : 0.f);
   }

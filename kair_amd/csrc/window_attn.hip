@@ -112,7 +112,8 @@ template <bool BF>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename AT<BF>::T* __restrict__ qkv,
                                                        const float* __restrict__ table, typename AT<BF>::T* __restrict__ O,
                                                        long ldo, float* __restrict__ lse, long nWin, int nh, float scale,
-                                                       int H, int W, int shift, int ones_col) {
+                                                       int H, int W, int shift, int ones_col,
+                                                       const float* __restrict__ amask, int mask_nw) {
   using T = typename AT<BF>::T;
   constexpr int LD = AT<BF>::LD;
   constexpr int WAVES = NWAVES<BF>;
@@ -192,6 +193,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename AT<BF>::T*
         const int ki = kt * 32 + acc_row(r, hh);
         float sc = acc[kt][qt][r] * scale + sTab[w][relidx(qi, ki)];
         if (shift > 0 && sReg[w][ki] != rq) sc += -100.f;
+        if (amask) sc += amask[((win % mask_nw) * TOK + qi) * TOK + ki];
         acc[kt][qt][r] = sc;
         mx = fmaxf(mx, sc);
       }
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename AT<BF>::T*
 __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(const bf16* __restrict__ qkv, const float* __restrict__ table,
                                                             bf16* __restrict__ O, long ldo, float* __restrict__ lse,
                                                             long nWin, int nh, float scale, int H, int W, int shift,
-                                                            int ones_col) {
+                                                            int ones_col, const float* __restrict__ amask, int mask_nw) {
   constexpr int LD = AT<true>::LD, NW = 4;
   __shared__ __attribute__((aligned(16))) bf16 sV[NW][TOK * LD];
   __shared__ float sTab[NW][232];
@@ -311,6 +313,7 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(const bf16* __restri
         const int ki = kt * 32 + acc_row(r, hh);
         float sc = acc[kt][qt][r] * scale + sTab[w][relidx(qi, ki)];
         if (shift > 0 && sReg[w][ki] != rq) sc += -100.f;
+        if (amask) sc += amask[((win % mask_nw) * TOK + qi) * TOK + ki];
         acc[kt][qt][r] = sc;
         mx = fmaxf(mx, sc);
       }
@@ -367,7 +370,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const typename AT<BF>::T*
                                                        const typename AT<BF>::T* __restrict__ dO, long lddo,
                                                        const float* __restrict__ table, const float* __restrict__ lse,
                                                        typename AT<BF>::T* __restrict__ dqkv, float* __restrict__ dB_part,
-                                                       long nWin, int nh, int wpg, float scale, int H, int W, int shift) {
+                                                       long nWin, int nh, int wpg, float scale, int H, int W, int shift,
+                                                       const float* __restrict__ amask, int mask_nw) {
   using T = typename AT<BF>::T;
   constexpr int LD = AT<BF>::LD;
   constexpr int WAVES = NWAVES<BF>;
@@ -484,6 +488,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const typename AT<BF>::T*
           const int qi = qt * 32 + acc_row(r, hh);
           float sc = S[qt][kt][r] * scale + sTab[w][relidx(qi, ki)];
           if (shift > 0 && sReg[w][qi] != rk) sc += -100.f;
+          if (amask) sc += amask[((win % mask_nw) * TOK + qi) * TOK + ki];
           const float p = __expf(sc - sRow[w][0][qi]);
           S[qt][kt][r] = p;
           const float d = p * (dP[qt][kt][r] - sRow[w][1][qi]);
@@ -578,7 +583,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
                                                             const float* __restrict__ table, const float* __restrict__ lse,
                                                             bf16* __restrict__ dqkv, float* __restrict__ dB_part,
                                                             long nWin, int nh, int wpg, float scale, int H, int W,
-                                                            int shift) {
+                                                            int shift, const float* __restrict__ amask, int mask_nw) {
   constexpr int LD = AT<true>::LD, LDD = 72, NW = 4;
   __shared__ __attribute__((aligned(16))) bf16 sQ[NW][TOK * LD];
   __shared__ __attribute__((aligned(16))) bf16 sK[NW][TOK * LD];
@@ -692,6 +697,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
           const int qi = qt * 32 + acc_row(r, hh);
           float sc = S[qt][kt][r] * scale + sTab[w][relidx(qi, ki)];
           if (shift > 0 && sReg[w][qi] != rk) sc += -100.f;
+          if (amask) sc += amask[((win % mask_nw) * TOK + qi) * TOK + ki];
           const float p = __expf(sc - sRow[w][0][qi]);
           S[qt][kt][r] = p;
           const float d = p * (dP[qt][kt][r] - sRow[w][1][qi]);
@@ -809,7 +815,8 @@ static long bwd_groups(long nWin, int wpg) { return (nWin + wpg - 1) / wpg; }
 
 extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
                                     long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
-                                    void* stream) {
+                                    const float* mask, int mask_nw, void* stream) {
+  KAIR_CHECK_ARG(!mask || (mask_nw > 0 && shift == 0), "window_attn_fwd: an explicit mask needs mask_nw > 0 and shift 0");
   KAIR_CHECK_ARG(qkv && table && O && lse, "window_attn_fwd: null pointer");
   KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_fwd: head_dim %d must be <= 32", hd);
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)),
@@ -822,10 +829,10 @@ extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* tab
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
     hipLaunchKernelGGL(attn_fwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
-                       lse, nWin, nh, scale, H, W, shift, ones_col);
+                       lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, table, (float*)O,
-                       ldo, lse, nWin, nh, scale, H, W, shift, ones_col);
+                       ldo, lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -838,7 +845,8 @@ extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) {
 extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
                                     const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
                                     float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
-                                    void* stream) {
+                                    const float* mask, int mask_nw, void* stream) {
+  KAIR_CHECK_ARG(!mask || (mask_nw > 0 && shift == 0), "window_attn_bwd: an explicit mask needs mask_nw > 0 and shift 0");
   KAIR_CHECK_ARG(qkv && O && dO && table && lse && dqkv && dtable && ws, "window_attn_bwd: null pointer");
   KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_bwd: head_dim");
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)), "window_attn_bwd: geometry");
@@ -850,10 +858,10 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
     hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
-                       (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift);
+                       (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw);
   else
     hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
-                       ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift);
+                       ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw);
   KAIR_CHECK_LAUNCH();
   float* dB = ws + ngroups * nh * TOK * TOK;
   hipLaunchKernelGGL(attn_dbias_sum_kernel, dim3((nh * TOK * TOK + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dB);

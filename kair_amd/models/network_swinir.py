@@ -2,17 +2,71 @@
 
 The module tree, parameter names/shapes, buffers (relative_position_index int64, attn_mask on
 shifted blocks) and initialisation follow the reference (network_swinir.py:65-773), so reference
-checkpoints load strictly and define_G() callers see the same object.  The compute does NOT go
-through these submodules: SwinIR.forward hands the whole network to the HIP step program in
-kair_amd/engine/swinir_engine.py (fused window attention, implicit-GEMM convs, fused epilogues),
-exposed to autograd as one node.  There is no CPU path; a CPU input raises.
+checkpoints load strictly and define_G() callers see the same object.
+
+Two ways in:
+  * SwinIR.forward hands the whole network to the HIP step program in
+    kair_amd/engine/swinir_engine.py (fused window attention, implicit-GEMM convs, fused
+    epilogues, one autograd node) -- the training / inference hot path;
+  * every submodule is also callable on its own, as in the reference -- Mlp.forward,
+    WindowAttention.forward(x, mask), SwinTransformerBlock.forward(x, x_size),
+    BasicLayer/RSTB.forward(x, x_size), PatchEmbed/PatchUnEmbed, SwinIR.forward_features /
+    check_image_size -- dispatching to the torch.ops.kair.* custom ops (kair_amd/ops.py) with
+    autograd per op.
+There is no CPU path; a CPU input raises.  Module-level ops compute in exact fp32 unless the
+owning SwinIR was built with compute_dtype 'bf16' (attribute `compute` on each op module).
 """
 import math
 
 import torch
 import torch.nn as nn
 
+from .. import ops as kops  # noqa: F401  (registers torch.ops.kair.*)
 from ..engine.swinir_engine import SwinIREngine, SwinIRFunction
+
+
+def _need_device(x):
+    if not x.is_cuda:
+        raise RuntimeError("kair_amd SwinIR modules run on the MI355X (HIP) only; got a CPU tensor (no CPU fallback)")
+
+
+class Linear(nn.Linear):
+    """nn.Linear whose forward is torch.ops.kair.linear (same parameters / state_dict)."""
+    compute = 0
+
+    def forward(self, x):
+        _need_device(x)
+        shp = x.shape
+        y, _ = torch.ops.kair.linear(x.reshape(-1, shp[-1]), self.weight, self.bias, 0, self.compute)
+        return y.view(*shp[:-1], self.out_features)
+
+
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm whose forward is torch.ops.kair.layernorm."""
+
+    def forward(self, x):
+        _need_device(x)
+        shp = x.shape
+        y, _, _ = torch.ops.kair.layernorm(x.reshape(-1, shp[-1]), self.weight, self.bias, self.eps)
+        return y.view(shp)
+
+
+class Conv3x3(nn.Conv2d):
+    """nn.Conv2d(C, C, 3, 1, 1) whose forward is torch.ops.kair.conv3x3."""
+    compute = 0
+
+    def forward(self, x):
+        _need_device(x)
+        return torch.ops.kair.conv3x3(x, self.weight, self.bias, self.compute)
+
+
+def _drop_path(x, rate, training):
+    """timm DropPath (network_swinir.py:204): per-sample keep mask / keep."""
+    if rate == 0.0 or not training:
+        return x
+    keep = 1.0 - rate
+    m = (torch.rand((x.shape[0],) + (1,) * (x.dim() - 1), device=x.device) < keep).to(x.dtype)
+    return x * m / keep
 
 
 def _pair(x):
@@ -46,10 +100,17 @@ def _shift_mask(H, W, ws, shift):
 class Mlp(nn.Module):
     def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.0):
         super().__init__()
-        self.fc1 = nn.Linear(in_features, hidden_features or in_features)
+        self.fc1 = Linear(in_features, hidden_features or in_features)
         self.act = act_layer()
-        self.fc2 = nn.Linear(hidden_features or in_features, out_features or in_features)
+        self.fc2 = Linear(hidden_features or in_features, out_features or in_features)
         self.drop = nn.Dropout(drop)
+
+    def forward(self, x):
+        """network_swinir.py:24-30: fc1 -> GELU (fused in the fc1 epilogue) -> fc2 (dropout p=0)."""
+        _need_device(x)
+        shp = x.shape
+        h, _ = torch.ops.kair.linear(x.reshape(-1, shp[-1]), self.fc1.weight, self.fc1.bias, 1, self.fc1.compute)
+        return self.drop(self.fc2(self.drop(h))).view(*shp[:-1], self.fc2.out_features)
 
 
 class WindowAttention(nn.Module):
@@ -60,17 +121,29 @@ class WindowAttention(nn.Module):
         ws = self.window_size[0]
         self.relative_position_bias_table = nn.Parameter(torch.zeros((2 * ws - 1) * (2 * ws - 1), num_heads))
         self.register_buffer("relative_position_index", _relative_position_index(ws))
-        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.qkv = Linear(dim, dim * 3, bias=qkv_bias)
         self.attn_drop = nn.Dropout(attn_drop)
-        self.proj = nn.Linear(dim, dim)
+        self.proj = Linear(dim, dim)
         self.proj_drop = nn.Dropout(proj_drop)
         _trunc_normal(self.relative_position_bias_table)
         self.softmax = nn.Softmax(dim=-1)
 
+    def forward(self, x, mask=None):
+        """network_swinir.py:114-145.  x [num_windows*B, 64, C]; mask (0/-100) [num_windows, 64, 64] or
+        None.  q*scale @ k^T + rel-pos bias (+ mask), softmax, @ v in one HIP kernel per (window, head);
+        the relative-position gather is computed from indices (relative_position_index is the buffer
+        of :92-103, kept for checkpoints)."""
+        _need_device(x)
+        B_, N, C = x.shape
+        qkv = self.qkv(x)
+        o, _, _ = torch.ops.kair.window_attn(qkv, self.relative_position_bias_table, mask, self.num_heads,
+                                             float(self.scale), self.qkv.compute)
+        return self.proj_drop(self.proj(o))
+
 
 class SwinTransformerBlock(nn.Module):
     def __init__(self, dim, input_resolution, num_heads, window_size=7, shift_size=0, mlp_ratio=4.0, qkv_bias=True,
-                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, act_layer=nn.GELU, norm_layer=nn.LayerNorm):
+                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, act_layer=nn.GELU, norm_layer=LayerNorm):
         super().__init__()
         self.dim, self.input_resolution, self.num_heads = dim, tuple(input_resolution), num_heads
         self.window_size, self.shift_size, self.mlp_ratio = window_size, shift_size, mlp_ratio
@@ -85,10 +158,37 @@ class SwinTransformerBlock(nn.Module):
         mask = _shift_mask(*self.input_resolution, self.window_size, self.shift_size) if self.shift_size > 0 else None
         self.register_buffer("attn_mask", mask)
 
+    def calculate_mask(self, x_size):
+        """network_swinir.py:216-237."""
+        return _shift_mask(x_size[0], x_size[1], self.window_size, self.shift_size)
+
+    def forward(self, x, x_size):
+        """network_swinir.py:239-279: LN1, cyclic shift, window partition, W-MSA, reverse, residual +
+        DropPath, LN2, MLP, residual + DropPath (roll / partition are device tensor views here; the
+        engine folds them into address maps)."""
+        _need_device(x)
+        Hh, Ww = x_size
+        B, L, C = x.shape
+        ws, sh = self.window_size, self.shift_size
+        h = self.norm1(x).view(B, Hh, Ww, C)
+        if sh > 0:
+            h = torch.roll(h, shifts=(-sh, -sh), dims=(1, 2))
+        win = h.view(B, Hh // ws, ws, Ww // ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(-1, ws * ws, C)
+        if sh > 0:
+            mask = self.attn_mask if tuple(x_size) == tuple(self.input_resolution) else self.calculate_mask(x_size).to(x.device)
+        else:
+            mask = None
+        a = self.attn(win, mask=mask)
+        a = a.view(B, Hh // ws, Ww // ws, ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B, Hh, Ww, C)
+        if sh > 0:
+            a = torch.roll(a, shifts=(sh, sh), dims=(1, 2))
+        x = x + _drop_path(a.reshape(B, Hh * Ww, C), self.drop_path_rate, self.training)
+        return x + _drop_path(self.mlp(self.norm2(x)), self.drop_path_rate, self.training)
+
 
 class BasicLayer(nn.Module):
     def __init__(self, dim, input_resolution, depth, num_heads, window_size, mlp_ratio=4.0, qkv_bias=True,
-                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=nn.LayerNorm, downsample=None,
+                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=LayerNorm, downsample=None,
                  use_checkpoint=False):
         super().__init__()
         self.dim, self.input_resolution, self.depth = dim, input_resolution, depth
@@ -98,6 +198,11 @@ class BasicLayer(nn.Module):
                                  drop_path[i] if isinstance(drop_path, list) else drop_path, norm_layer=norm_layer)
             for i in range(depth)])
         self.downsample = None
+
+    def forward(self, x, x_size):
+        for blk in self.blocks:
+            x = blk(x, x_size)
+        return x
 
 
 class PatchEmbed(nn.Module):
@@ -110,15 +215,25 @@ class PatchEmbed(nn.Module):
         self.in_chans, self.embed_dim = in_chans, embed_dim
         self.norm = norm_layer(embed_dim) if norm_layer is not None else None
 
+    def forward(self, x):
+        """network_swinir.py:524-528: [B, C, H, W] -> [B, HW, C] (+ LayerNorm)."""
+        x = x.flatten(2).transpose(1, 2)
+        return self.norm(x) if self.norm is not None else x
+
 
 class PatchUnEmbed(PatchEmbed):
     def __init__(self, img_size=224, patch_size=4, in_chans=3, embed_dim=96, norm_layer=None):
         super().__init__(img_size, patch_size, in_chans, embed_dim, None)
 
+    def forward(self, x, x_size):
+        """network_swinir.py:562-565: [B, HW, C] -> [B, C, H, W]."""
+        B, HW, C = x.shape
+        return x.transpose(1, 2).reshape(B, self.embed_dim, x_size[0], x_size[1])
+
 
 class RSTB(nn.Module):
     def __init__(self, dim, input_resolution, depth, num_heads, window_size, mlp_ratio=4.0, qkv_bias=True,
-                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=nn.LayerNorm, downsample=None,
+                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=LayerNorm, downsample=None,
                  use_checkpoint=False, img_size=224, patch_size=4, resi_connection="1conv"):
         super().__init__()
         if resi_connection != "1conv":
@@ -126,9 +241,13 @@ class RSTB(nn.Module):
         self.dim, self.input_resolution = dim, input_resolution
         self.residual_group = BasicLayer(dim, input_resolution, depth, num_heads, window_size, mlp_ratio, qkv_bias,
                                          qk_scale, drop, attn_drop, drop_path, norm_layer)
-        self.conv = nn.Conv2d(dim, dim, 3, 1, 1)
+        self.conv = Conv3x3(dim, dim, 3, 1, 1)
         self.patch_embed = PatchEmbed(img_size, patch_size, 0, dim, None)
         self.patch_unembed = PatchUnEmbed(img_size, patch_size, 0, dim, None)
+
+    def forward(self, x, x_size):
+        """network_swinir.py:481-482."""
+        return self.patch_embed(self.conv(self.patch_unembed(self.residual_group(x, x_size), x_size))) + x
 
 
 class Upsample(nn.Sequential):
@@ -162,7 +281,7 @@ class SwinIR(nn.Module):
 
     def __init__(self, img_size=64, patch_size=1, in_chans=3, embed_dim=96, depths=(6, 6, 6, 6),
                  num_heads=(6, 6, 6, 6), window_size=7, mlp_ratio=4.0, qkv_bias=True, qk_scale=None, drop_rate=0.0,
-                 attn_drop_rate=0.0, drop_path_rate=0.1, norm_layer=nn.LayerNorm, ape=False, patch_norm=True,
+                 attn_drop_rate=0.0, drop_path_rate=0.1, norm_layer=LayerNorm, ape=False, patch_norm=True,
                  use_checkpoint=False, upscale=2, img_range=1.0, upsampler="", resi_connection="1conv",
                  compute_dtype="bf16", split_conv=True, **kwargs):
         super().__init__()
@@ -199,6 +318,7 @@ class SwinIR(nn.Module):
             raise NotImplementedError(f"kair_amd SwinIR: upsampler '{upsampler}' is not on the MI355X path yet")
         self.apply(self._init_weights)
         self.compute_dtype = compute_dtype
+        self._set_op_compute()
         self.split_conv = split_conv
         self._engine = None
 
@@ -234,7 +354,30 @@ class SwinIR(nn.Module):
     def set_compute_dtype(self, dtype):
         self.compute_dtype = dtype
         self._engine = None
+        self._set_op_compute()
         return self
+
+    def _set_op_compute(self):
+        for m in self.modules():
+            if isinstance(m, (Linear, Conv3x3)):
+                m.compute = 1 if self.compute_dtype == "bf16" else 0
+
+    def check_image_size(self, x):
+        """network_swinir.py:783-788: reflect-pad H, W up to multiples of window_size."""
+        _, _, h, w = x.size()
+        ph = (self.window_size - h % self.window_size) % self.window_size
+        pw = (self.window_size - w % self.window_size) % self.window_size
+        return torch.nn.functional.pad(x, (0, pw, 0, ph), "reflect") if (ph or pw) else x
+
+    def forward_features(self, x):
+        """network_swinir.py:790-803 on the torch.ops.kair.* module path: x [B, C, H, W] (after
+        conv_first) -> normalised deep features [B, C, H, W]."""
+        _need_device(x)
+        x_size = (x.shape[2], x.shape[3])
+        x = self.pos_drop(self.patch_embed(x))
+        for layer in self.layers:
+            x = layer(x, x_size)
+        return self.patch_unembed(self.norm(x), x_size)
 
     def forward(self, x):
         if not x.is_cuda:

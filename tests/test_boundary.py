@@ -107,3 +107,15 @@ def test_define_G_state_dict_matches_reference(name):
     sd = net.state_dict()
     assert [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()] == ref["keys"]
     assert sum(p.numel() for p in net.parameters()) == ref["n_params"]
+
+
+def test_custom_ops_registered_and_refuse_cpu():
+    """torch.ops.kair.* exist (schema per op) and have no CPU kernel: a host tensor raises."""
+    from kair_amd import ops
+    for name in ops.registered_ops():
+        assert hasattr(torch.ops.kair, name), name
+    with pytest.raises(NotImplementedError):
+        torch.ops.kair.linear(torch.zeros(4, 8), torch.zeros(4, 8), None, 0, 0)
+    from kair_amd.models.network_swinir import WindowAttention
+    with pytest.raises(RuntimeError):
+        WindowAttention(60, (8, 8), 6)(torch.zeros(1, 64, 60))
