@@ -125,7 +125,10 @@ typedef struct {
                         8 conv2x2 -> [4*Kp][Np], row = kp*4 + tap (pixel-shuffle forms: stride-2
                           conv dgrad, transposed-conv forward over (N, K) = (Ci, Co));
                         9 conv3x3 forward, hi/lo split (bf16 only): [Cop][2*ceil(9*Cip/64)*64],
-                          64-column chunks alternate hi = bf16(w), lo = bf16(w - hi)             */
+                          64-column chunks alternate hi = bf16(w), lo = bf16(w - hi);
+                        10 linear in MFMA-fragment order [Np/32][Kp/16][64][8]: the
+                          v_mfma_f32_32x32x16 operand of rows 32nb.. and k-step kb is one
+                          contiguous 1 KiB block (lane l: row 32nb + l%32, k 16kb + 8(l/32) + j) */
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
   int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp                   */
@@ -202,6 +205,21 @@ int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* d
                          const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
                          float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
                          const float* mask, int mask_nw, void* stream);
+
+/* Fused attention half of a Swin block (bf16; nh = 6 heads, C < 32*nh, window 8):
+ *   out = x + rowscale * proj(W-MSA(LN1(x)))        network_swinir.py:239-272 + 114-145
+ * in one launch (one workgroup per window, one wave per head).  x / out fp32 token rows; the LN1
+ * output (window order, 1.0 at column C), mean / rstd, the head-blocked q/k/v, O (1.0 at
+ * o_ones_col) and lse are stored exactly as kair_layernorm_fwd / kair_gemm_nt / kair_window_attn_fwd
+ * would, for the unchanged backward.  wqkv: [3*nh*32][32*nh] (head-padded rows), wproj:
+ * [32*nh][nh*32], both in MFMA-fragment order (pack kind 10); rowscale per sample
+ * (rows_per_scale = H*W) or NULL. */
+int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, const float* beta, float eps, int C,
+                       void* ln, long ldln, float* mean, float* rstd, const void* wqkv, const float* bqkv,
+                       void* qkv, const float* table, float scale, void* O, long ldo, int o_ones_col,
+                       float* lse, const void* wproj, const float* bproj, const float* rowscale,
+                       int rows_per_scale, float* out, long ldout, long nWin, int nh, int H, int W, int shift,
+                       void* stream);
 
 /* Elementwise / small kernels ------------------------------------------------------------- */
 /* NCHW fp32 image -> NHWC (dtype) with channel stride ldc, x' = (x - mean[c]) * img_range

@@ -121,6 +121,9 @@ _SIGS = {
                       c_vp],
     "kair_synth_dn": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_float, ctypes.c_ulonglong, ctypes.c_ulonglong,
                       c_vp, c_vp, c_vp],
+    "kair_swin_attn_fwd": [c_vp, c_long, c_vp, c_vp, c_float, c_int, c_vp, c_long, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                           c_float, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_long, c_int,
+                           c_int, c_int, c_int, c_vp],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
@@ -492,3 +495,12 @@ def synth_dn(pool, params, B, PS, sigma, seed, step, outH, outL):
     N, C, Hs, Ws = pool.shape
     check(lib().kair_synth_dn(ptr(pool), C, Hs, Ws, ptr(params), B, PS, sigma, seed, step, ptr(outH), ptr(outL),
                               stream_ptr()), "synth_dn")
+
+
+def swin_attn_fwd(x, ldx, gamma, beta, eps, C, ln, ldln, mean, rstd, wqkv, bqkv, qkv, table, scale, O, ldo, o_ones_col,
+                  lse, wproj, bproj, rowscale, rows_per_scale, out, ldout, nWin, nh, H, W, shift):
+    """Fused LN1 -> qkv -> window attention -> proj + residual (kair_swin_attn_fwd)."""
+    check(lib().kair_swin_attn_fwd(ptr(x), ldx, ptr(gamma), ptr(beta), eps, C, ptr(ln), ldln, ptr(mean), ptr(rstd),
+                                   ptr(wqkv), ptr(bqkv), ptr(qkv), ptr(table), scale, ptr(O), ldo, o_ones_col, ptr(lse),
+                                   ptr(wproj), ptr(bproj), ptr(rowscale), rows_per_scale, ptr(out), ldout, nWin, nh, H, W,
+                                   shift, stream_ptr()), "swin_attn_fwd")

@@ -48,6 +48,20 @@ KAIR_DEV float wave_max(float v) {
   return v;
 }
 
+// Sum over each aligned group of 16 lanes with DPP lane moves only (no LDS permute): quad
+// butterflies (quad_perm [1,0,3,2], [2,3,0,1]) then row_half_mirror and row_mirror, which pair
+// the quads and then the half-rows of a 16-lane DPP row.  Every lane of the group gets the sum.
+template <int CTRL> KAIR_DEV float dpp_movc(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+KAIR_DEV float dpp_sum16(float v) {
+  v += dpp_movc<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_movc<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_movc<0x141>(v);   // row_half_mirror
+  v += dpp_movc<0x140>(v);   // row_mirror
+  return v;
+}
+
 KAIR_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 KAIR_DEV float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));

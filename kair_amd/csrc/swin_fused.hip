@@ -1,0 +1,456 @@
+// Fused Swin Transformer block halves for gfx950 (bf16 MFMA, fp32 accumulation): the attention half
+//
+//   mid = x + s * proj( W-MSA( LN1(x) ) )          network_swinir.py:239-272 (SwinTransformerBlock
+//                                                   .forward up to the first residual) with
+//                                                   WindowAttention.forward :114-145
+//
+// as ONE launch: one workgroup per 8x8 window, one wave per head (nh = 6, Cp = 32 * nh = 192).
+//   A  LN1 of the window's 64 token rows (read through the cyclic-shift + window-partition row map)
+//      into an LDS tile (bf16), also stored for backward (window order, ones column at C) with the
+//      per-token mean / rstd;
+//   B  per head: Q^T = Wq_h . LN^T, K^T = Wk_h . LN^T, V = LN . Wv_h^T with v_mfma_f32_32x32x16_bf16;
+//      the accumulators ARE the attention operands -- register r of lane half hh holds d =
+//      acc_row(r, hh), so packing registers 8s..8s+7 gives an MFMA fragment whose contraction
+//      index runs over a permutation of d that is the same for q and k (and of the keys for P and
+//      v): q, k, v never pass through LDS.  Stored head-blocked for backward;
+//   C  S^T = K Q^T * scale + rel-pos bias (+ shift-region mask), wave64 softmax, O^T = V^T P^T;
+//      O stored for backward (ones column) and into the LDS tile (LN no longer needed);
+//   D  proj: wave w makes output channels [32w, 32w+32) of the 64 rows, + bias, * DropPath scale,
+//      + the fp32 residual x, scattered back to token order (window_reverse + reverse roll).
+// The saved tensors are exactly those of the unfused path (ln1, m1, r1, qkv, O, lse), so the
+// backward program is unchanged.  Per window the kernel moves x (49 KB fp32) in and mid (49 KB)
+// + ln1 / O (2 x 24.6 KB) + q/k/v (73.7 KB) out: 221 KB, against ~4x that across the separate
+// LayerNorm / QKV / attention / proj kernels it replaces.
+#include "common.h"
+
+namespace {
+
+constexpr int TOK = 64, WSZ = 8;
+
+KAIR_DEV int acc_row32(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+KAIR_DEV int shift_region(int coord, int n, int shift) { return coord < n - WSZ ? 0 : (coord < n - shift ? 1 : 2); }
+
+struct AttnFwdArgs {
+  const float* x; long ldx;                  // residual stream fp32 [M][ldx], token order
+  const float* gamma; const float* beta;     // LN1
+  float eps; int C;
+  bf16* ln; long ldln;                       // saved LN1 output, window order, ones column at C
+  float* mean; float* rstd;                  // [M], token order
+  const bf16* wqkv; const float* bqkv;       // fragment order (pack kind 10) of [3*nh*32][Cp], bias
+  bf16* qkv;                                 // head-blocked [3][nWin][nh][64][32]
+  const float* table; float scale;           // [225][nh]
+  bf16* O; long ldo; int o_ones_col;         // [M][ldo], window order
+  float* lse;                                // [nWin][nh][64]
+  const bf16* wproj; const float* bproj;     // fragment order (pack kind 10) of [Cp][nh*32], bias
+  const float* rowscale; int win_per_scale;  // DropPath per-sample scale (NULL = 1)
+  float* out; long ldout;                    // mid fp32 [M][ldout], token order
+  long nWin; int H, W, shift;
+  WinMap wm;
+};
+
+KAIR_DEV bf16x8 pack8r(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
+  return r;
+}
+
+// Persistent: one workgroup per CU loops over windows.  Memory-operation order: vmcnt counts
+// loads AND stores in issue order, so a wait for a load issued after a store also waits for that
+// store.  Within an iteration the global loads (the NEXT window's x rows, the weight fragments)
+// are issued ahead of the iteration's stores; the x rows of window i+1 are in flight during
+// window i's proj GEMM and stores (the kernel is otherwise latency-bound: one window is ~50 k
+// cycles of dependent phases on 6 waves).  The fp32 x rows also stay in LDS for the residual,
+// so nothing is re-read.
+
+template <int NH>
+__global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArgs a) {
+  constexpr int CP = 32 * NH, LDT = CP + 8, LDX = CP + 4, KB = CP / 16;
+  constexpr int RPW = (TOK + NH - 1) / NH, PF = 3;
+  static_assert(KB % PF == 0, "k-steps must be a multiple of the prefetch depth");
+  __shared__ __attribute__((aligned(16))) bf16 sT[TOK * LDT];   // LN1 tile
+  __shared__ __attribute__((aligned(16))) bf16 sO[TOK * LDT];   // O tile
+  __shared__ __attribute__((aligned(16))) float sX[TOK * LDX];  // x rows (fp32) for the residual
+  __shared__ float sTabR[NH][232];          // relative-position bias, REVERSED: sTabR[h][224 - idx]
+  __shared__ float sBias[3 * NH * 32];       // qkv bias (packed, head-padded)
+  __shared__ float sGB[2][CP];               // LN1 gamma, beta (0 past C)
+  __shared__ int sReg[TOK];
+  __shared__ int sRow[TOK];
+  __shared__ float sMean[TOK], sRstd[TOK];
+  constexpr int LDV = 40;                    // v transpose scratch row stride (80 B, 16 B aligned)
+  __shared__ __attribute__((aligned(16))) bf16 sV[NH][TOK * LDV];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l31 = lane & 31, hh = lane >> 5;
+  const long M = a.nWin * TOK;
+  bf16* sVw = sV[w];
+  const int h = w;
+  const int c = 32 * w + l31;   // phase D output channel of this lane
+  long win = blockIdx.x;
+
+  // ---- prologue: first window's x rows, first q/k/v weight fragments, per-head tables ------------
+  // x rows: 16 lanes per row (lane group g, lane jl in it), channels 4 jl + 64 k (k < 3: 768 B
+  // of a row per 16 lanes, coalesced); pass p covers row index i = 4 p + g of the wave's rows
+  // w + NH i.
+  static_assert(CP == 192, "the fused attention kernel is laid out for Cp = 192");
+  constexpr int NPASS = (RPW + 3) / 4;
+  const int g = lane >> 4, jl = lane & 15;
+  float4 xv[NPASS][3];
+  auto load_x = [&](long wn) {
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int i = 4 * p + g, r = w + NH * i;
+      const bool ok = wn < a.nWin && i < RPW && r < TOK;
+      const long base = ok ? win_to_token(wn * TOK + r, a.wm) * a.ldx : 0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        xv[p][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) xv[p][k] = *(const float4*)(a.x + base + 4 * jl + 64 * k);
+      }
+    }
+  };
+  load_x(win);
+  const bf16* wq = a.wqkv + ((long)((0 * NH + h) * KB) * 64 + lane) * 8;
+  const bf16* wk = a.wqkv + ((long)((1 * NH + h) * KB) * 64 + lane) * 8;
+  const bf16* wv = a.wqkv + ((long)((2 * NH + h) * KB) * 64 + lane) * 8;
+  const bf16* wp = a.wproj + ((long)(w * KB) * 64 + lane) * 8;
+  bf16x8 pq[PF], pk[PF], pv[PF];
+  auto load_w = [&]() {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      pq[i] = *(const bf16x8*)(wq + i * 512);
+      pk[i] = *(const bf16x8*)(wk + i * 512);
+      pv[i] = *(const bf16x8*)(wv + i * 512);
+    }
+  };
+  load_w();
+  for (int i = lane; i < (2 * WSZ - 1) * (2 * WSZ - 1); i += 64) sTabR[w][224 - i] = a.table[i * NH + w];
+  for (int i = tid; i < 3 * NH * 32; i += 64 * NH) sBias[i] = a.bqkv[i];
+  for (int i = tid; i < CP; i += 64 * NH) {
+    sGB[0][i] = i < a.C ? a.gamma[i] : 0.f;
+    sGB[1][i] = i < a.C ? a.beta[i] : 0.f;
+  }
+  const float bvl = a.bqkv[(2 * NH + h) * 32 + l31];
+  const float bc = a.bproj[c];
+  __syncthreads();   // sTabR, sBias, sGB visible
+  const float inv_c = 1.0f / (float)a.C;
+  const int nWw = a.W / WSZ, nW = (a.H / WSZ) * nWw;
+
+  for (; win < a.nWin; win += gridDim.x) {
+    // row map and shift regions of this window (readers are behind the LN barrier; the previous
+    // iteration's last readers are behind its closing barrier)
+    const int wi = (int)(win % nW), wy = wi / nWw, wx = wi - wy * nWw;
+    if (tid < TOK) {
+      sRow[tid] = (int)win_to_token(win * TOK + tid, a.wm);
+      sReg[tid] = a.shift > 0 ? shift_region(wy * WSZ + (tid >> 3), a.H, a.shift) * 3 +
+                                    shift_region(wx * WSZ + (tid & 7), a.W, a.shift)
+                              : 0;
+    }
+    const bool mixed = a.shift > 0 && (wy == a.H / WSZ - 1 || wx == nWw - 1);
+
+    // ---- A: LayerNorm, 16 lanes per row (DPP sums, no LDS permutes); x rows -> sX (fp32), LN rows
+    // -> sT (bf16, 1.0 in column C)
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int i = 4 * p + g, r = w + NH * i;
+      const bool ok = i < RPW && r < TOK;
+      float sm = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * jl + 64 * k;
+        sm += (cb + 0 < a.C ? xv[p][k].x : 0.f) + (cb + 1 < a.C ? xv[p][k].y : 0.f) +
+              (cb + 2 < a.C ? xv[p][k].z : 0.f) + (cb + 3 < a.C ? xv[p][k].w : 0.f);
+      }
+      const float mu = dpp_sum16(sm) * inv_c;
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * jl + 64 * k;
+        const float vv[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = cb + j < a.C ? vv[j] - mu : 0.f;
+          q += d * d;
+        }
+      }
+      const float rs = rsqrtf(dpp_sum16(q) * inv_c + a.eps);
+      if (ok) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int cb = 4 * jl + 64 * k;
+          const float vv[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cc = cb + j;
+            o[j] = (bf16)(cc < a.C ? (vv[j] - mu) * rs * sGB[0][cc] + sGB[1][cc] : (cc == a.C ? 1.f : 0.f));
+          }
+          *(bf16x4*)(sT + r * LDT + cb) = o;
+          *(float4*)(sX + r * LDX + cb) = xv[p][k];
+        }
+        if (jl == 0) {
+          sMean[r] = mu;
+          sRstd[r] = rs;
+        }
+      }
+    }
+    __syncthreads();           // LN tile, sX, sRow, sReg visible
+
+    // ---- B: q^T, k^T, v of head h = w (weight fragments PF k-steps ahead) -----------------------
+    f32x16 QT[2], KT[2], V[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) QT[t][r] = KT[t][r] = V[t][r] = 0.f;
+#pragma unroll 1
+    for (int kb0 = 0; kb0 < KB; kb0 += PF) {
+#pragma unroll
+      for (int sl = 0; sl < PF; ++sl) {
+        const int kb = kb0 + sl;
+        const bf16x8 fq = pq[sl], fk = pk[sl], fv = pv[sl];
+        if (kb + PF < KB) {
+          pq[sl] = *(const bf16x8*)(wq + (kb + PF) * 512);
+          pk[sl] = *(const bf16x8*)(wk + (kb + PF) * 512);
+          pv[sl] = *(const bf16x8*)(wv + (kb + PF) * 512);
+        }
+        bf16x8 fl[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) fl[t] = *(const bf16x8*)(sT + (t * 32 + l31) * LDT + kb * 16 + 8 * hh);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          QT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fq, fl[t], QT[t], 0, 0, 0);
+          KT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk, fl[t], KT[t], 0, 0, 0);
+          V[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl[t], fv, V[t], 0, 0, 0);
+        }
+      }
+    }
+    // proj weight fragments for the first PF k-steps of phase D, in flight during the attention
+    bf16x8 pw[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) pw[i] = *(const bf16x8*)(wp + i * 512);
+    // + bias, round to bf16 (the values attention and the saved q/k/v both use)
+    const float* bq = sBias + (0 * NH + h) * 32;
+    const float* bk = sBias + (1 * NH + h) * 32;
+    bf16x8 Fq[2][2], Fk[2][2], Fv[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int d = acc_row32(8 * s + j, hh);
+          Fq[t][s][j] = (bf16)(QT[t][8 * s + j] + bq[d]);
+          Fk[t][s][j] = (bf16)(KT[t][8 * s + j] + bk[d]);
+          Fv[t][s][j] = (bf16)(V[t][8 * s + j] + bvl);
+        }
+
+    // the saved q / k / v go out now (their registers are needed until the attention's last MFMA
+    // anyway); the loads after them (proj weights) were issued before
+    {   // q / k / v, head-blocked [part][win][h][tok][32]
+      const long part = M * NH * 32;
+      bf16* qb = a.qkv + (win * NH + h) * TOK * 32;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int tok = t * 32 + l31;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d0 = 8 * g + 4 * hh, s = g >> 1, j0 = 4 * (g & 1);
+          const bf16x4 q4 = {Fq[t][s][j0], Fq[t][s][j0 + 1], Fq[t][s][j0 + 2], Fq[t][s][j0 + 3]};
+          const bf16x4 k4 = {Fk[t][s][j0], Fk[t][s][j0 + 1], Fk[t][s][j0 + 2], Fk[t][s][j0 + 3]};
+          *(bf16x4*)(qb + tok * 32 + d0) = q4;
+          *(bf16x4*)(qb + part + tok * 32 + d0) = k4;
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sVw[(t * 32 + acc_row32(8 * s + j, hh)) * LDV + l31] = Fv[t][s][j];
+      }
+      // v: lane = d in registers -> token rows through the wave's LDS scratch, 16-byte stores
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int id = lane + 64 * i, tok = id >> 2, q8 = (id & 3) * 8;
+        *(uint4*)(qb + 2 * part + tok * 32 + q8) = *(const uint4*)(sVw + tok * LDV + q8);
+      }
+    }
+
+    // ---- C: attention of head h ------------------------------------------------------------------
+    f32x16 S[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) S[kt][qt][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+          S[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fk[kt][s], Fq[qt][s], S[kt][qt], 0, 0, 0);
+    float lse_v[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qi = qt * 32 + l31;
+      // rel index = (qy - ky + 7) * 15 + (qx - kx + 7); in the reversed table the key part is a
+      // compile-time offset per register: 15 ky + kx = 15 (4 kt + r / 4) + r % 4 + 4 hh
+      const float* tb = &sTabR[h][112 - 15 * (qi >> 3) - (qi & 7) + 4 * hh];
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float sc = fmaf(S[kt][qt][r], a.scale, tb[15 * (4 * kt + (r >> 2)) + (r & 3)]);
+          S[kt][qt][r] = sc;
+          mx = fmaxf(mx, sc);
+        }
+      if (mixed) {   // shifted block, window on the image's last window row / column: region mask
+        const int rq = sReg[qi];
+        mx = -3.0e38f;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if (sReg[kt * 32 + acc_row32(r, hh)] != rq) S[kt][qt][r] += -100.f;
+            mx = fmaxf(mx, S[kt][qt][r]);
+          }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __expf(S[kt][qt][r] - mx);
+          S[kt][qt][r] = e;
+          sum += e;
+        }
+      sum += __shfl_xor(sum, 32, 64);
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) S[kt][qt][r] *= inv;
+      lse_v[qt] = mx + __logf(sum);
+    }
+    // O^T = V^T P^T: lane = query, registers = d -> the O tile (LDS)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 o;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fv[kt][s], pack8r(S[kt][qt], s), o, 0, 0, 0);
+      const int qi = qt * 32 + l31;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = 8 * g + 4 * hh;
+        float r4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r4[j] = (h * 32 + d0 + j == a.o_ones_col) ? 1.f : o[4 * g + j];
+        *(bf16x4*)(sO + qi * LDT + h * 32 + d0) = bf16x4{(bf16)r4[0], (bf16)r4[1], (bf16)r4[2], (bf16)r4[3]};
+      }
+    }
+    load_x(win + gridDim.x);   // the next window's rows, in flight through phase D and the stores
+    __syncthreads();           // the O tile is complete
+
+    // ---- D: proj + bias, DropPath scale, fp32 residual from sX ------------------------------------
+    f32x16 P[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) P[t][r] = 0.f;
+#pragma unroll 1
+    for (int kb0 = 0; kb0 < KB; kb0 += PF) {
+#pragma unroll
+      for (int sl = 0; sl < PF; ++sl) {
+        const int kb = kb0 + sl;
+        const bf16x8 fw = pw[sl];
+        if (kb + PF < KB) pw[sl] = *(const bf16x8*)(wp + (kb + PF) * 512);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 fo = *(const bf16x8*)(sO + (t * 32 + l31) * LDT + kb * 16 + 8 * hh);
+          P[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fo, fw, P[t], 0, 0, 0);
+        }
+      }
+    }
+    load_w();   // the next window's first q/k/v weight fragments, still ahead of this window's stores
+    const float rs = a.rowscale ? a.rowscale[win / a.win_per_scale] : 1.f;
+
+    // ---- stores: mid (token order), then everything saved for backward ---------------------------
+    // mid = x + s * (proj + bias), formed in place in sX, then stored row-contiguous
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float* px = sX + (t * 32 + acc_row32(r, hh)) * LDX + c;
+        *px = *px + rs * (P[t][r] + bc);
+      }
+    __syncthreads();
+    constexpr int C4 = CP / 4;
+    for (int i = tid; i < TOK * C4; i += 64 * NH) {
+      const int r = i / C4, q = (i - (i / C4) * C4) * 4;
+      *(float4*)(a.out + (long)sRow[r] * a.ldout + q) = *(const float4*)(sX + r * LDX + q);
+    }
+    if (hh == 0) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) a.lse[(win * NH + h) * TOK + qt * 32 + l31] = lse_v[qt];
+    }
+    // LN1 rows and O rows from LDS, 16 bytes per lane (window order)
+    constexpr int CH = CP / 8;   // 16-byte chunks per row
+    for (int i = tid; i < TOK * CH; i += 64 * NH) {
+      const int r = i / CH, q = (i - (i / CH) * CH) * 8;
+      *(uint4*)(a.ln + (win * TOK + r) * a.ldln + q) = *(const uint4*)(sT + r * LDT + q);
+      *(uint4*)(a.O + (win * TOK + r) * a.ldo + q) = *(const uint4*)(sO + r * LDT + q);
+    }
+    if (tid < TOK) {
+      const long t = sRow[tid];
+      a.mean[t] = sMean[tid];
+      a.rstd[t] = sRstd[tid];
+    }
+    __syncthreads();   // every LDS tile / row map of this window consumed
+  }
+}
+
+}  // namespace
+
+extern "C" int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, const float* beta, float eps, int C,
+                                  void* ln, long ldln, float* mean, float* rstd, const void* wqkv, const float* bqkv,
+                                  void* qkv, const float* table, float scale, void* O, long ldo, int o_ones_col,
+                                  float* lse, const void* wproj, const float* bproj, const float* rowscale,
+                                  int rows_per_scale, float* out, long ldout, long nWin, int nh, int H, int W, int shift,
+                                  void* stream) {
+  KAIR_CHECK_ARG(x && gamma && beta && ln && mean && rstd && wqkv && bqkv && qkv && table && O && lse && wproj && bproj && out,
+                 "swin_attn_fwd: null pointer");
+  KAIR_CHECK_ARG(nh == 6 && C > 0 && C < 32 * nh && C % nh == 0 && C / nh <= 32,
+                 "swin_attn_fwd: nh must be 6 with C < 32*nh (C %d, nh %d)", C, nh);
+  KAIR_CHECK_ARG(H % WSZ == 0 && W % WSZ == 0 && (shift == 0 || (shift > 0 && shift < WSZ)), "swin_attn_fwd: geometry");
+  KAIR_CHECK_ARG(nWin > 0 && nWin * TOK < KAIR_MAX_MAPPED_ROWS && (nWin * TOK) % ((long)H * W) == 0,
+                 "swin_attn_fwd: nWin * 64 must be a whole number of H x W images, < 2^24");
+  KAIR_CHECK_ARG(ldx >= 32 * nh && ldx % 4 == 0 && ldout >= 32 * nh && ldln >= 32 * nh && ldln % 4 == 0 && ldo >= 32 * nh &&
+                     ldo % 4 == 0 && ((uintptr_t)x & 15) == 0,
+                 "swin_attn_fwd: strides");
+  KAIR_CHECK_ARG(!rowscale || (rows_per_scale > 0 && rows_per_scale % TOK == 0), "swin_attn_fwd: rows_per_scale");
+  AttnFwdArgs a;
+  a.x = x; a.ldx = ldx; a.gamma = gamma; a.beta = beta; a.eps = eps; a.C = C;
+  a.ln = (bf16*)ln; a.ldln = ldln; a.mean = mean; a.rstd = rstd;
+  a.wqkv = (const bf16*)wqkv; a.bqkv = bqkv; a.qkv = (bf16*)qkv;
+  a.table = table; a.scale = scale;
+  a.O = (bf16*)O; a.ldo = ldo; a.o_ones_col = o_ones_col; a.lse = lse;
+  a.wproj = (const bf16*)wproj; a.bproj = bproj;
+  a.rowscale = rowscale; a.win_per_scale = rowscale ? rows_per_scale / TOK : 1;
+  a.out = out; a.ldout = ldout;
+  a.nWin = nWin; a.H = H; a.W = W; a.shift = shift;
+  a.wm = make_winmap(H, W, WSZ, shift);
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  const long grid = nWin < ncu ? nWin : ncu;   // persistent: one workgroup per CU
+  hipLaunchKernelGGL(swin_attn_fwd_kernel<6>, dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}

@@ -63,7 +63,7 @@ def swinir_flops(net, Hh, Ww):
 class _Lin:
     """A linear layer's packed forms.  n/k groupings map reference rows/cols to padded ones."""
 
-    def __init__(self, eng, mod, n_grp, k_grp):
+    def __init__(self, eng, mod, n_grp, k_grp, frag=False):
         self.w, self.b = mod.weight, mod.bias
         N, K = self.w.shape
         self.N, self.K = N, K
@@ -76,10 +76,16 @@ class _Lin:
         self.Wp = torch.empty(self.Np, self.Kp, device=dev, dtype=eng.tdt)
         self.Wt = torch.empty(self.Kp, self.Np, device=dev, dtype=eng.tdt)
         self.bp = torch.empty(self.Np, device=dev)
+        # MFMA-fragment order of Wp (pack kind 10) for the fused block kernels
+        self.mapg = H.wmap(10, N, K, n_grp, k_grp) if frag else None
+        self.Wg = torch.empty(self.Np, self.Kp, device=dev, dtype=eng.tdt) if frag else None
 
     def pack_jobs(self):
         w, b = self.w.detach(), self.b.detach()
-        return [(w, self.Wp, self.map), (w, self.Wt, self.mapT), (b, self.bp, self.mapb)]
+        jobs = [(w, self.Wp, self.map), (w, self.Wt, self.mapT), (b, self.bp, self.mapb)]
+        if self.Wg is not None:
+            jobs.append((w, self.Wg, self.mapg))
+        return jobs
 
 
 class _Conv:
@@ -130,8 +136,8 @@ class _Blk:
         self.table = blk.attn.relative_position_bias_table
         self.scale = blk.attn.scale
         Hd = blk.mlp.fc1.out_features
-        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp))
-        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32))
+        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=eng.fused_attn)
+        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=eng.fused_attn)
         self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp))
         self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp))
 
@@ -140,8 +146,10 @@ class _Blk:
 
 
 class SwinIREngine:
-    def __init__(self, net, compute_dtype="bf16", split_conv=True):
-        """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv)."""
+    def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True):
+        """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv).
+        fused_blocks (bf16 only): each Swin block's attention half runs as one kernel
+        (kair_swin_attn_fwd) where the geometry allows it (6 heads, Cp = 192)."""
         self.net_ref = weakref.ref(net)
         if compute_dtype not in ("bf16", "fp32"):
             raise ValueError(compute_dtype)
@@ -160,6 +168,7 @@ class SwinIREngine:
         if self.ws != 8:
             raise NotImplementedError("kair_amd SwinIR: window_size 8 only (fused attention tile)")
         self.Cp = _rup(self.C + 1, 32)
+        self.fused_attn = bool(fused_blocks) and compute_dtype == "bf16" and self.nh == 6 and self.Cp == 32 * self.nh
         Hd = net.layers[0].residual_group.blocks[0].mlp.fc1.out_features
         self.Hdp = _rup(Hd + 1, 32)
         self.upsampler, self.scale = net.upsampler, net.upscale
@@ -446,16 +455,22 @@ class SwinIREngine:
         s_mlp = drop[bi, 1] if drop is not None else None
         # LN1 / LN2 / fc1 / attention write 1.0 into their first pad column: the ones column the
         # weight-gradient GEMMs use for the bias gradient (the packed weights are 0 there)
-        H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps, win,
-                        one_col=self.C)
-        l = blk.qkv
-        H.gemm_nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
-                                                               qkv=(nh, 32, WS_TOK)), M, l.Np, Cp, cd)
-        H.window_attn_fwd(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale, Hh, Ww,
-                          blk.shift, ones_col=self.C // nh)
-        l = blk.proj
-        H.gemm_nt(H.rows(S["O"]), H.rows(l.Wp), H.epilogue(S["mid"], win=win, bias=l.bp, resid=x, rowscale=s_attn,
-                                                            rows_per_scale=HW), M, Cp, nh * 32, cd)
+        if self.fused_attn:   # LN1 -> qkv -> window attention -> proj + residual in one launch
+            H.swin_attn_fwd(x, Cp, blk.n1.weight, blk.n1.bias, blk.n1.eps, self.C, S["ln1"], Cp, S["m1"], S["r1"],
+                            blk.qkv.Wg, blk.qkv.bp, S["qkv"], blk.table, blk.scale, S["O"], nh * 32, self.C // nh,
+                            S["lse"], blk.proj.Wg, blk.proj.bp, s_attn, HW, S["mid"], Cp, P["nWin"], nh, Hh, Ww,
+                            blk.shift)
+        else:
+            H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps, win,
+                            one_col=self.C)
+            l = blk.qkv
+            H.gemm_nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
+                                                                   qkv=(nh, 32, WS_TOK)), M, l.Np, Cp, cd)
+            H.window_attn_fwd(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale, Hh,
+                              Ww, blk.shift, ones_col=self.C // nh)
+            l = blk.proj
+            H.gemm_nt(H.rows(S["O"]), H.rows(l.Wp), H.epilogue(S["mid"], win=win, bias=l.bp, resid=x, rowscale=s_attn,
+                                                                rows_per_scale=HW), M, Cp, nh * 32, cd)
         H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps,
                         one_col=self.C)
         l = blk.fc1

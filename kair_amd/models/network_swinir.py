@@ -277,13 +277,14 @@ class SwinIR(nn.Module):
                      (exact fp32 MFMA; the parity mode)
       split_conv     bf16 only (default True): forward 3x3 convs use hi/lo bf16 weight pairs, which
                      removes the output bias of bf16 weight rounding (DESIGN.md "parity at bf16")
+      fused_blocks   bf16 only (default True): fused Swin-block kernels where the geometry allows
     """
 
     def __init__(self, img_size=64, patch_size=1, in_chans=3, embed_dim=96, depths=(6, 6, 6, 6),
                  num_heads=(6, 6, 6, 6), window_size=7, mlp_ratio=4.0, qkv_bias=True, qk_scale=None, drop_rate=0.0,
                  attn_drop_rate=0.0, drop_path_rate=0.1, norm_layer=LayerNorm, ape=False, patch_norm=True,
                  use_checkpoint=False, upscale=2, img_range=1.0, upsampler="", resi_connection="1conv",
-                 compute_dtype="bf16", split_conv=True, **kwargs):
+                 compute_dtype="bf16", split_conv=True, fused_blocks=True, **kwargs):
         super().__init__()
         if ape or not patch_norm or patch_size != 1 or not qkv_bias or qk_scale is not None:
             raise NotImplementedError("kair_amd SwinIR: ape / patch_norm=False / patch_size!=1 / custom qk are off-path")
@@ -320,6 +321,7 @@ class SwinIR(nn.Module):
         self.compute_dtype = compute_dtype
         self._set_op_compute()
         self.split_conv = split_conv
+        self.fused_blocks = fused_blocks
         self._engine = None
 
     @staticmethod
@@ -344,7 +346,7 @@ class SwinIR(nn.Module):
     # ------------------------------------------------------------------------------------
     def engine(self):
         if self._engine is None or self._engine.net_ref() is not self:
-            self._engine = SwinIREngine(self, self.compute_dtype, self.split_conv)
+            self._engine = SwinIREngine(self, self.compute_dtype, self.split_conv, self.fused_blocks)
         return self._engine
 
     def _apply(self, fn, *args, **kwargs):

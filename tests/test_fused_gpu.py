@@ -1,0 +1,87 @@
+"""Fused Swin-block kernels (csrc/swin_fused.hip) against the unfused launch sequence they replace,
+on the same weights and the same DropPath scales: the saved tensors the backward reads (ln1, mean,
+rstd, q/k/v, O, lse), the block outputs, the network output and every gradient.  Both paths run
+bf16 MFMA with fp32 accumulation, so they agree to bf16 rounding (a few ulp of the stored bf16
+values), not bitwise; each path is separately pinned to the CPU oracle in test_swinir_gpu.py."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from kair_amd.models.network_swinir import SwinIR  # noqa: E402
+
+dev = torch.device("cuda")
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _pair(fused_first=True, depths=(2, 2), img=24):
+    torch.manual_seed(11)
+    nets = []
+    for fused in (True, False):
+        n = SwinIR(upscale=2, in_chans=3, img_size=img, window_size=8, img_range=1.0, depths=list(depths), embed_dim=180,
+                   num_heads=[6] * len(depths), mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.2,
+                   compute_dtype="bf16", fused_blocks=fused)
+        nets.append(n)
+    nets[1].load_state_dict(nets[0].state_dict())
+    for n in nets:
+        with torch.no_grad():
+            for b in (blk for l in n.layers for blk in l.residual_group.blocks):
+                b.attn.relative_position_bias_table.normal_(0, 0.5)
+    nets[1].load_state_dict(nets[0].state_dict())
+    return [n.to(dev).train() for n in nets]
+
+
+@pytest.mark.parametrize("shape", [(2, 24, 24), (1, 16, 40)])
+def test_fused_attention_half_matches_unfused(shape):
+    B, Hh, Ww = shape
+    fz, un = _pair()
+    ef, eu = fz.engine(), un.engine()
+    assert ef.fused_attn and not eu.fused_attn
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(B, 3, Hh, Ww, generator=g).to(dev)
+    nb = len(ef.blocks)
+    D = ((torch.rand(nb, 2, B, generator=g) < 0.7).float() / 0.7).to(dev)
+    Ef = ef.forward(x, D).clone()
+    Eu = eu.forward(x, D).clone()
+    Pf, Pu = ef.cur, eu.cur
+    # block 0 sees identical inputs in both paths: tight; later blocks inherit bf16-level input drift
+    for bi in range(nb):
+        Sf, Su = Pf["blocks"][bi], Pu["blocks"][bi]
+        tb, tf = (5e-3, 2e-3) if bi == 0 else (2e-2, 1e-2)
+        for k in ("ln1", "qkv", "O"):
+            assert rel(Sf[k].float(), Su[k].float()) < tb, (bi, k)
+        assert (Sf["m1"] - Su["m1"]).abs().max().item() < (1e-6 if bi == 0 else 1e-3), bi
+        for k in ("r1", "lse", "mid", "out"):
+            assert rel(Sf[k], Su[k]) < tf, (bi, k)
+    assert rel(Ef, Eu) < 5e-3
+    # gradients: both bf16 paths against the exact-fp32 engine on the same weights / scales; the
+    # fused path must be as close to it as the unfused one (bf16 noise on small sums such as the
+    # LayerNorm bias gradients is of the same order in both)
+    ref = SwinIR(upscale=2, in_chans=3, img_size=24, window_size=8, img_range=1.0, depths=[2, 2], embed_dim=180,
+                 num_heads=[6, 6], mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.2, compute_dtype="fp32")
+    ref.load_state_dict(fz.state_dict())
+    ref = ref.to(dev).train()
+    er = ref.engine()
+    Er = er.forward(x, D).clone()
+    assert rel(Ef, Er) < 2e-2
+    gE = torch.randn(Ef.shape, generator=g).to(dev)
+    grads = []
+    for eng, net in ((ef, fz), (eu, un), (er, ref)):
+        params = list(net.parameters())
+        flat = torch.zeros(sum(p.numel() for p in params), device=dev)
+        gd, off = {}, 0
+        for p in params:
+            gd[p] = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        eng.backward_from_grad(gE, gd)
+        grads.append([gd[p] for p in params])
+    names = [k for k, _ in fz.named_parameters()]
+    for a, b, r, n in zip(grads[0], grads[1], grads[2], names):
+        ef_, eu_ = rel(a, r), rel(b, r)
+        assert ef_ <= 1.5 * eu_ + 1e-2, (n, ef_, eu_)
