@@ -128,7 +128,9 @@ typedef struct {
                           64-column chunks alternate hi = bf16(w), lo = bf16(w - hi);
                         10 linear in MFMA-fragment order [Np/32][Kp/16][64][8]: the
                           v_mfma_f32_32x32x16 operand of rows 32nb.. and k-step kb is one
-                          contiguous 1 KiB block (lane l: row 32nb + l%32, k 16kb + 8(l/32) + j) */
+                          contiguous 1 KiB block (lane l: row 32nb + l%32, k 16kb + 8(l/32) + j);
+                        12 kind 10 with hi/lo halves (bf16 only): [Np/32][Kp/16][2][64][8], the hi
+                          block of (nb, kb) followed by its lo block */
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
   int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp                   */
@@ -212,14 +214,25 @@ int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* d
  * output (window order, 1.0 at column C), mean / rstd, the head-blocked q/k/v, O (1.0 at
  * o_ones_col) and lse are stored exactly as kair_layernorm_fwd / kair_gemm_nt / kair_window_attn_fwd
  * would, for the unchanged backward.  wqkv: [3*nh*32][32*nh] (head-padded rows), wproj:
- * [32*nh][nh*32], both in MFMA-fragment order (pack kind 10); rowscale per sample
- * (rows_per_scale = H*W) or NULL. */
+ * [32*nh][nh*32], both in MFMA-fragment order (pack kind 10, or kind 12 hi/lo pairs when
+ * w_split); rowscale per sample (rows_per_scale = H*W) or NULL. */
 int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, const float* beta, float eps, int C,
                        void* ln, long ldln, float* mean, float* rstd, const void* wqkv, const float* bqkv,
                        void* qkv, const float* table, float scale, void* O, long ldo, int o_ones_col,
                        float* lse, const void* wproj, const float* bproj, const float* rowscale,
                        int rows_per_scale, float* out, long ldout, long nWin, int nh, int H, int W, int shift,
-                       void* stream);
+                       int w_split, void* stream);
+/* Fused MLP half of a Swin block (bf16; Cp = 192, hidden padded to Hp = 384):
+ *   out = x + rowscale * fc2(GELU(fc1(LN2(x))))     network_swinir.py:274-276, Mlp.forward :24-30
+ * in one launch over 64-row tiles of token rows.  Saved for the unchanged backward as
+ * kair_layernorm_fwd / kair_gemm_nt store them: ln (1.0 at column C), mean / rstd, u = the fc1
+ * pre-activation and h = GELU(u) (1.0 at column hd), both [M][ldh].  w1 [Hp][Cp] and w2 [Cp][Hp]
+ * in MFMA-fragment order (kind 10, or kind 12 when w_split); b1 [Hp], b2 [Cp] padded. */
+int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, const float* beta, float eps, int C,
+                      void* ln, long ldln, float* mean, float* rstd, const void* w1, const float* b1, void* u,
+                      void* h, long ldh, int hd, const void* w2, const float* b2, const float* rowscale,
+                      int rows_per_scale, float* out, long ldout, long M, int Cp, int Hp, int w_split,
+                      void* stream);
 
 /* Elementwise / small kernels ------------------------------------------------------------- */
 /* NCHW fp32 image -> NHWC (dtype) with channel stride ldc, x' = (x - mean[c]) * img_range

@@ -123,7 +123,9 @@ _SIGS = {
                       c_vp, c_vp, c_vp],
     "kair_swin_attn_fwd": [c_vp, c_long, c_vp, c_vp, c_float, c_int, c_vp, c_long, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                            c_float, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_long, c_int,
-                           c_int, c_int, c_int, c_vp],
+                           c_int, c_int, c_int, c_int, c_vp],
+    "kair_swin_mlp_fwd": [c_vp, c_long, c_vp, c_vp, c_float, c_int, c_vp, c_long, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                          c_long, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_long, c_int, c_int, c_int, c_vp],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
@@ -498,9 +500,17 @@ def synth_dn(pool, params, B, PS, sigma, seed, step, outH, outL):
 
 
 def swin_attn_fwd(x, ldx, gamma, beta, eps, C, ln, ldln, mean, rstd, wqkv, bqkv, qkv, table, scale, O, ldo, o_ones_col,
-                  lse, wproj, bproj, rowscale, rows_per_scale, out, ldout, nWin, nh, H, W, shift):
+                  lse, wproj, bproj, rowscale, rows_per_scale, out, ldout, nWin, nh, H, W, shift, w_split=False):
     """Fused LN1 -> qkv -> window attention -> proj + residual (kair_swin_attn_fwd)."""
     check(lib().kair_swin_attn_fwd(ptr(x), ldx, ptr(gamma), ptr(beta), eps, C, ptr(ln), ldln, ptr(mean), ptr(rstd),
                                    ptr(wqkv), ptr(bqkv), ptr(qkv), ptr(table), scale, ptr(O), ldo, o_ones_col, ptr(lse),
                                    ptr(wproj), ptr(bproj), ptr(rowscale), rows_per_scale, ptr(out), ldout, nWin, nh, H, W,
-                                   shift, stream_ptr()), "swin_attn_fwd")
+                                   shift, int(w_split), stream_ptr()), "swin_attn_fwd")
+
+
+def swin_mlp_fwd(x, ldx, gamma, beta, eps, C, ln, ldln, mean, rstd, w1, b1, u, h, ldh, hd, w2, b2, rowscale,
+                 rows_per_scale, out, ldout, M, Cp, Hp, w_split=False):
+    """Fused LN2 -> fc1 + GELU -> fc2 + residual (kair_swin_mlp_fwd)."""
+    check(lib().kair_swin_mlp_fwd(ptr(x), ldx, ptr(gamma), ptr(beta), eps, C, ptr(ln), ldln, ptr(mean), ptr(rstd),
+                                  ptr(w1), ptr(b1), ptr(u), ptr(h), ldh, hd, ptr(w2), ptr(b2), ptr(rowscale),
+                                  rows_per_scale, ptr(out), ldout, M, Cp, Hp, int(w_split), stream_ptr()), "swin_mlp_fwd")

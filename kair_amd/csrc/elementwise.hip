@@ -63,6 +63,17 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const int np = nb * 32 + (ln & 31), kp = kb * 16 + 8 * (ln >> 5) + j;
     const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
+  } else if (mp.kind == 12) {  // linear, fragment order with hi/lo halves: [Np/32][Kp/16][2][64 lanes][8]
+    const int KB = Kp / 16;
+    const int j = (int)(t & 7), ln = (int)((t >> 3) & 63), half = (int)((t >> 9) & 1);
+    const long blk = t >> 10;
+    const int kb = (int)(blk % KB), nb = (int)(blk / KB);
+    const int np = nb * 32 + (ln & 31), kp = kb * 16 + 8 * (ln >> 5) + j;
+    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
+    const bf16 hi = (bf16)v;
+    ((bf16*)dst)[t] = half ? (bf16)(v - (float)hi) : hi;
+    return;
   } else if (mp.kind == 8) {  // conv2x2 [4*Kp][Np], row = kp*4 + tap (pixel-shuffle forms)
     const int row = (int)(t / Np), np = (int)(t - (long)row * Np);
     const int kp = row >> 2, tap = row & 3;
@@ -446,13 +457,16 @@ inline unsigned nblk(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 }  // namespace
 
 static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
-  KAIR_CHECK_ARG(mp.kind != 9 || dst_dtype == KAIR_BF16, "pack_weight: the hi/lo split form (kind 9) is bf16 only");
+  KAIR_CHECK_ARG((mp.kind != 9 && mp.kind != 12) || dst_dtype == KAIR_BF16,
+                 "pack_weight: the hi/lo split forms (kinds 9, 12) are bf16 only");
   KAIR_CHECK_ARG(mp.nG > 0 && mp.nGr > 0 && mp.nGp >= mp.nGr && mp.nG * mp.nGr == mp.N, "pack_weight: bad N map");
   KAIR_CHECK_ARG(mp.kind == 4 || (mp.kG > 0 && mp.kGr > 0 && mp.kGp >= mp.kGr && mp.kG * mp.kGr == mp.K),
                  "pack_weight: bad K map");
   const long Np = (long)mp.nG * mp.nGp, Kp = (long)mp.kG * mp.kGp;
-  KAIR_CHECK_ARG(mp.kind != 10 || (Np % 32 == 0 && Kp % 16 == 0), "pack_weight: fragment order needs Np %% 32 == 0, Kp %% 16 == 0");
+  KAIR_CHECK_ARG((mp.kind != 10 && mp.kind != 12) || (Np % 32 == 0 && Kp % 16 == 0),
+                 "pack_weight: fragment order needs Np %% 32 == 0, Kp %% 16 == 0");
   if (mp.kind == 0 || mp.kind == 3 || mp.kind == 10) *total = Np * Kp;
+  else if (mp.kind == 12) *total = 2 * Np * Kp;
   else if (mp.kind == 1 || mp.kind == 2) *total = Np * 9 * Kp;
   else if (mp.kind == 7 || mp.kind == 8) *total = Np * 4 * Kp;
   else if (mp.kind == 9) *total = Np * 2 * ((9L * Kp + 63) / 64) * 64;

@@ -21,6 +21,8 @@
 // backward program is unchanged.  Per window the kernel moves x (49 KB fp32) in and mid (49 KB)
 // + ln1 / O (2 x 24.6 KB) + q/k/v (73.7 KB) out: 221 KB, against ~4x that across the separate
 // LayerNorm / QKV / attention / proj kernels it replaces.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -63,10 +65,12 @@ KAIR_DEV bf16x8 pack8r(const f32x16& a, int s) {
 // cycles of dependent phases on 6 waves).  The fp32 x rows also stay in LDS for the residual,
 // so nothing is re-read.
 
-template <int NH>
+// NS = 2: hi/lo split weights (pack kind 12), each k-step multiplies the same LN / O fragment by
+// the hi and the lo half, so the products see the fp32 master weights to ~16 mantissa bits.
+template <int NH, int NS>
 __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArgs a) {
   constexpr int CP = 32 * NH, LDT = CP + 8, LDX = CP + 4, KB = CP / 16;
-  constexpr int RPW = (TOK + NH - 1) / NH, PF = 3;
+  constexpr int RPW = (TOK + NH - 1) / NH, PF = NS == 1 ? 3 : 2, WS = 512 * NS;   // WS: k-step stride
   static_assert(KB % PF == 0, "k-steps must be a multiple of the prefetch depth");
   __shared__ __attribute__((aligned(16))) bf16 sT[TOK * LDT];   // LN1 tile
   __shared__ __attribute__((aligned(16))) bf16 sO[TOK * LDT];   // O tile
@@ -109,18 +113,20 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
     }
   };
   load_x(win);
-  const bf16* wq = a.wqkv + ((long)((0 * NH + h) * KB) * 64 + lane) * 8;
-  const bf16* wk = a.wqkv + ((long)((1 * NH + h) * KB) * 64 + lane) * 8;
-  const bf16* wv = a.wqkv + ((long)((2 * NH + h) * KB) * 64 + lane) * 8;
-  const bf16* wp = a.wproj + ((long)(w * KB) * 64 + lane) * 8;
-  bf16x8 pq[PF], pk[PF], pv[PF];
+  const bf16* wq = a.wqkv + (long)((0 * NH + h) * KB) * WS + lane * 8;
+  const bf16* wk = a.wqkv + (long)((1 * NH + h) * KB) * WS + lane * 8;
+  const bf16* wv = a.wqkv + (long)((2 * NH + h) * KB) * WS + lane * 8;
+  const bf16* wp = a.wproj + (long)(w * KB) * WS + lane * 8;
+  bf16x8 pq[PF][NS], pk[PF][NS], pv[PF][NS];
   auto load_w = [&]() {
 #pragma unroll
-    for (int i = 0; i < PF; ++i) {
-      pq[i] = *(const bf16x8*)(wq + i * 512);
-      pk[i] = *(const bf16x8*)(wk + i * 512);
-      pv[i] = *(const bf16x8*)(wv + i * 512);
-    }
+    for (int i = 0; i < PF; ++i)
+#pragma unroll
+      for (int e = 0; e < NS; ++e) {
+        pq[i][e] = *(const bf16x8*)(wq + i * WS + e * 512);
+        pk[i][e] = *(const bf16x8*)(wk + i * WS + e * 512);
+        pv[i][e] = *(const bf16x8*)(wv + i * WS + e * 512);
+      }
   };
   load_w();
   for (int i = lane; i < (2 * WSZ - 1) * (2 * WSZ - 1); i += 64) sTabR[w][224 - i] = a.table[i * NH + w];
@@ -206,27 +212,37 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
 #pragma unroll
       for (int sl = 0; sl < PF; ++sl) {
         const int kb = kb0 + sl;
-        const bf16x8 fq = pq[sl], fk = pk[sl], fv = pv[sl];
-        if (kb + PF < KB) {
-          pq[sl] = *(const bf16x8*)(wq + (kb + PF) * 512);
-          pk[sl] = *(const bf16x8*)(wk + (kb + PF) * 512);
-          pv[sl] = *(const bf16x8*)(wv + (kb + PF) * 512);
+        bf16x8 fq[NS], fk[NS], fv[NS];
+#pragma unroll
+        for (int e = 0; e < NS; ++e) {
+          fq[e] = pq[sl][e];
+          fk[e] = pk[sl][e];
+          fv[e] = pv[sl][e];
+          if (kb + PF < KB) {
+            pq[sl][e] = *(const bf16x8*)(wq + (kb + PF) * WS + e * 512);
+            pk[sl][e] = *(const bf16x8*)(wk + (kb + PF) * WS + e * 512);
+            pv[sl][e] = *(const bf16x8*)(wv + (kb + PF) * WS + e * 512);
+          }
         }
         bf16x8 fl[2];
 #pragma unroll
         for (int t = 0; t < 2; ++t) fl[t] = *(const bf16x8*)(sT + (t * 32 + l31) * LDT + kb * 16 + 8 * hh);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          QT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fq, fl[t], QT[t], 0, 0, 0);
-          KT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk, fl[t], KT[t], 0, 0, 0);
-          V[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl[t], fv, V[t], 0, 0, 0);
-        }
+        for (int e = 0; e < NS; ++e)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            QT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fq[e], fl[t], QT[t], 0, 0, 0);
+            KT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk[e], fl[t], KT[t], 0, 0, 0);
+            V[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl[t], fv[e], V[t], 0, 0, 0);
+          }
       }
     }
     // proj weight fragments for the first PF k-steps of phase D, in flight during the attention
-    bf16x8 pw[PF];
+    bf16x8 pw[PF][NS];
 #pragma unroll
-    for (int i = 0; i < PF; ++i) pw[i] = *(const bf16x8*)(wp + i * 512);
+    for (int i = 0; i < PF; ++i)
+#pragma unroll
+      for (int e = 0; e < NS; ++e) pw[i][e] = *(const bf16x8*)(wp + i * WS + e * 512);
     // + bias, round to bf16 (the values attention and the saved q/k/v both use)
     const float* bq = sBias + (0 * NH + h) * 32;
     const float* bk = sBias + (1 * NH + h) * 32;
@@ -368,12 +384,17 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
 #pragma unroll
       for (int sl = 0; sl < PF; ++sl) {
         const int kb = kb0 + sl;
-        const bf16x8 fw = pw[sl];
-        if (kb + PF < KB) pw[sl] = *(const bf16x8*)(wp + (kb + PF) * 512);
+        bf16x8 fw[NS];
+#pragma unroll
+        for (int e = 0; e < NS; ++e) {
+          fw[e] = pw[sl][e];
+          if (kb + PF < KB) pw[sl][e] = *(const bf16x8*)(wp + (kb + PF) * WS + e * 512);
+        }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const bf16x8 fo = *(const bf16x8*)(sO + (t * 32 + l31) * LDT + kb * 16 + 8 * hh);
-          P[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fo, fw, P[t], 0, 0, 0);
+#pragma unroll
+          for (int e = 0; e < NS; ++e) P[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fo, fw[e], P[t], 0, 0, 0);
         }
       }
     }
@@ -415,6 +436,288 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
   }
 }
 
+
+// ---- MLP half ------------------------------------------------------------------------------------
+//   out = mid + s * fc2( GELU( fc1( LN2(mid) ) ) )      network_swinir.py:274-276 + Mlp.forward :24-30
+// one workgroup per 64 token rows (persistent, two per CU), 6 waves.  Rows are token order (no window
+// map).  Saved for backward exactly as the unfused path stores them: LN2 output (1.0 at column C),
+// mean / rstd, u = fc1 pre-activation, h = GELU(u) (1.0 at column hd).  The u / h tile and then the
+// fp32 output tile are staged in one LDS buffer, so every global store is a 16-byte row-contiguous
+// access; the residual is re-read from L2 at the end instead of being held in LDS (the LDS budget
+// stays under half a CU: two workgroups per CU overlap one's LayerNorm / stores with the other's
+// MFMAs).  Per 64 rows it moves mid in (49 KB fp32, read twice, the second from L2) and ln2 (24.6
+// KB) + u + h (2 x 49 KB) + out (49 KB) out, against the ~1.6x that the LN2 / fc1 / fc2 kernels move.
+struct MlpFwdArgs {
+  const float* x; long ldx;                  // mid fp32 [M][ldx]
+  const float* gamma; const float* beta;     // LN2
+  float eps; int C;
+  bf16* ln; long ldln;                       // saved LN2 output, 1.0 at column C
+  float* mean; float* rstd;                  // [M]
+  const bf16* w1; const float* b1;           // fragment order [HP/32][CP/16][S][64][8], bias [HP]
+  bf16* u; bf16* hact; long ldh; int hd;     // pre-activation / GELU output [M][ldh], 1.0 at h column hd
+  const bf16* w2; const float* b2;           // fragment order [CP/32][HP/16][S][64][8], bias [CP]
+  const float* rowscale; int tiles_per_scale;
+  float* out; long ldout;
+  long nTiles;
+  int dbg;   // ablation bits (KAIR_MLP_DBG, perf investigation only): 1 no fc1 MFMA, 2 no fc2 MFMA, 4 no u/h pass
+};
+
+template <int S>
+__global__ __launch_bounds__(384, 3) void swin_mlp_fwd_kernel(const MlpFwdArgs a) {
+  constexpr int NW = 6, CP = 192, HP = 384, LDT = CP + 8, LDH = HP + 8, LDO = CP + 4;
+  constexpr int KB1 = CP / 16, KB2 = HP / 16, WS = 512 * S;
+  constexpr int PF1 = 2, PF2 = 2;   // weight prefetch depths (k-steps)
+  constexpr int RPW = (TOK + NW - 1) / NW, NPASS = (RPW + 3) / 4;
+  static_assert(KB1 % PF1 == 0 && KB2 % PF2 == 0, "k-steps must be a multiple of the prefetch depth");
+  static_assert(TOK * LDH * 2 == TOK * LDO * 4, "the fp32 output tile reuses the u / h tile");
+  __shared__ __attribute__((aligned(16))) bf16 sT[TOK * LDT];   // LN2 tile
+  __shared__ __attribute__((aligned(16))) bf16 sH[TOK * LDH];   // u, then h; then the fp32 output tile
+  __shared__ __attribute__((aligned(16))) float sB1[HP];
+  __shared__ __attribute__((aligned(16))) float sB2[CP];
+  __shared__ float sGB[2][CP];
+  __shared__ float sMean[TOK], sRstd[TOK];
+  float* sOut = (float*)sH;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l31 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, jl = lane & 15;
+  long tile = blockIdx.x;
+
+  for (int i = tid; i < HP; i += 64 * NW) sB1[i] = a.b1[i];
+  for (int i = tid; i < CP; i += 64 * NW) sB2[i] = a.b2[i];
+  for (int i = tid; i < CP; i += 64 * NW) {
+    sGB[0][i] = i < a.C ? a.gamma[i] : 0.f;
+    sGB[1][i] = i < a.C ? a.beta[i] : 0.f;
+  }
+  // fc1: wave w makes hidden columns [64w, 64w + 64) (two 32-column tiles); fc2: output columns
+  // [32w, 32w + 32).  MFMA D = W . X^T: lane = token row, registers = 4-column groups.
+  const bf16* w1p = a.w1 + (long)(2 * w) * KB1 * WS + lane * 8;
+  const bf16* w2p = a.w2 + (long)w * KB2 * WS + lane * 8;
+  bf16x8 p1[PF1][2][S], p2[PF2][S];
+  auto load_w1 = [&]() {
+#pragma unroll
+    for (int i = 0; i < PF1; ++i)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int e = 0; e < S; ++e) p1[i][ct][e] = *(const bf16x8*)(w1p + (long)ct * KB1 * WS + i * WS + e * 512);
+  };
+  float4 xv[NPASS][3];
+  auto load_x = [&](long tl) {
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int i = 4 * p + g, r = w + NW * i;
+      const bool ok = tl < a.nTiles && i < RPW && r < TOK;
+      const long base = ok ? (tl * TOK + r) * a.ldx : 0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        xv[p][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) xv[p][k] = *(const float4*)(a.x + base + 4 * jl + 64 * k);
+      }
+    }
+  };
+  __syncthreads();   // sB1, sB2, sGB visible
+  const float inv_c = 1.0f / (float)a.C;
+
+  for (; tile < a.nTiles; tile += gridDim.x) {
+    const long row0 = tile * TOK;
+    load_x(tile);   // no cross-tile prefetch: the second workgroup on the CU hides this latency
+    load_w1();
+    // ---- LayerNorm 2: 16 lanes per row, DPP sums -> sT (bf16, 1.0 in column C)
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int i = 4 * p + g, r = w + NW * i;
+      const bool ok = i < RPW && r < TOK;
+      float sm = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * jl + 64 * k;
+        sm += (cb + 0 < a.C ? xv[p][k].x : 0.f) + (cb + 1 < a.C ? xv[p][k].y : 0.f) +
+              (cb + 2 < a.C ? xv[p][k].z : 0.f) + (cb + 3 < a.C ? xv[p][k].w : 0.f);
+      }
+      const float mu = dpp_sum16(sm) * inv_c;
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * jl + 64 * k;
+        const float vv[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = cb + j < a.C ? vv[j] - mu : 0.f;
+          q += d * d;
+        }
+      }
+      const float rs = rsqrtf(dpp_sum16(q) * inv_c + a.eps);
+      if (ok) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int cb = 4 * jl + 64 * k;
+          const float vv[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cc = cb + j;
+            o[j] = (bf16)(cc < a.C ? (vv[j] - mu) * rs * sGB[0][cc] + sGB[1][cc] : (cc == a.C ? 1.f : 0.f));
+          }
+          *(bf16x4*)(sT + r * LDT + cb) = o;
+        }
+        if (jl == 0) {
+          sMean[r] = mu;
+          sRstd[r] = rs;
+        }
+      }
+    }
+    __syncthreads();   // LN tile visible
+
+    // ---- fc1: U^T tiles (hidden columns x token rows)
+    f32x16 U[2][2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) U[ct][rt][r] = 0.f;
+#pragma unroll 1
+    for (int kb0 = 0; kb0 < ((a.dbg & 1) ? 0 : KB1); kb0 += PF1) {
+#pragma unroll
+      for (int sl = 0; sl < PF1; ++sl) {
+        const int kb = kb0 + sl;
+        bf16x8 fw[2][S];
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int e = 0; e < S; ++e) {
+            fw[ct][e] = p1[sl][ct][e];
+            if (kb + PF1 < KB1) p1[sl][ct][e] = *(const bf16x8*)(w1p + (long)ct * KB1 * WS + (kb + PF1) * WS + e * 512);
+          }
+        bf16x8 fl[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) fl[rt] = *(const bf16x8*)(sT + (rt * 32 + l31) * LDT + kb * 16 + 8 * hh);
+#pragma unroll
+        for (int e = 0; e < S; ++e)
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+              U[ct][rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[ct][e], fl[rt], U[ct][rt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PF2; ++i)
+#pragma unroll
+      for (int e = 0; e < S; ++e) p2[i][e] = *(const bf16x8*)(w2p + i * WS + e * 512);
+    // u = acc + b1 -> sH (bf16): lane row rt*32 + l31, columns 64w + 32ct + 8gg + 4hh + e
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int col = 64 * w + 32 * ct + 8 * gg + 4 * hh;
+        const float4 bb = *(const float4*)(sB1 + col);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const f32x16& acc = U[ct][rt];
+          *(bf16x4*)(sH + (rt * 32 + l31) * LDH + col) =
+              bf16x4{(bf16)(acc[4 * gg] + bb.x), (bf16)(acc[4 * gg + 1] + bb.y), (bf16)(acc[4 * gg + 2] + bb.z),
+                     (bf16)(acc[4 * gg + 3] + bb.w)};
+        }
+      }
+    // LN2 rows and statistics out (sT is read-only from here on)
+    {
+      constexpr int CH = CP / 8;
+      for (int i = tid; i < TOK * CH; i += 64 * NW) {
+        const int r = i / CH, q = (i - (i / CH) * CH) * 8;
+        *(uint4*)(a.ln + (row0 + r) * a.ldln + q) = *(const uint4*)(sT + r * LDT + q);
+      }
+      if (tid < TOK) {
+        a.mean[row0 + tid] = sMean[tid];
+        a.rstd[row0 + tid] = sRstd[tid];
+      }
+    }
+    __syncthreads();   // u tile complete
+    // u out, h = GELU(u) (1.0 at column hd) -> sH and out; 16 bytes per lane
+    {
+      constexpr int CH = HP / 8;
+      for (int i = tid; i < ((a.dbg & 4) ? 0 : TOK * CH); i += 64 * NW) {
+        const int r = i / CH, q = (i - (i / CH) * CH) * 8;
+        bf16* ps = sH + r * LDH + q;
+        const bf16x8 uv = *(const bf16x8*)ps;
+        *(bf16x8*)(a.u + (row0 + r) * a.ldh + q) = uv;
+        bf16x8 hv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int cc = q + j;
+          hv[j] = cc < a.hd ? (bf16)gelu_fast((float)uv[j]) : (bf16)(cc == a.hd ? 1.f : 0.f);
+        }
+        *(bf16x8*)ps = hv;
+        *(bf16x8*)(a.hact + (row0 + r) * a.ldh + q) = hv;
+      }
+    }
+    __syncthreads();   // h tile complete
+
+    // ---- fc2: out^T tile (output columns 32w.. x token rows)
+    f32x16 O2[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) O2[rt][r] = 0.f;
+#pragma unroll 1
+    for (int kb0 = 0; kb0 < ((a.dbg & 2) ? 0 : KB2); kb0 += PF2) {
+#pragma unroll
+      for (int sl = 0; sl < PF2; ++sl) {
+        const int kb = kb0 + sl;
+        bf16x8 fw[S];
+#pragma unroll
+        for (int e = 0; e < S; ++e) {
+          fw[e] = p2[sl][e];
+          if (kb + PF2 < KB2) p2[sl][e] = *(const bf16x8*)(w2p + (kb + PF2) * WS + e * 512);
+        }
+        bf16x8 fh[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) fh[rt] = *(const bf16x8*)(sH + (rt * 32 + l31) * LDH + kb * 16 + 8 * hh);
+#pragma unroll
+        for (int e = 0; e < S; ++e)
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt) O2[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[e], fh[rt], O2[rt], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // every wave is done reading the h tile
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int col = 32 * w + 8 * gg + 4 * hh;
+      const float4 bb = *(const float4*)(sB2 + col);
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const f32x16& acc = O2[rt];
+        *(float4*)(sOut + (rt * 32 + l31) * LDO + col) =
+            make_float4(acc[4 * gg] + bb.x, acc[4 * gg + 1] + bb.y, acc[4 * gg + 2] + bb.z, acc[4 * gg + 3] + bb.w);
+      }
+    }
+    __syncthreads();   // output tile complete
+    {
+      const float rs = a.rowscale ? a.rowscale[tile / a.tiles_per_scale] : 1.f;
+      constexpr int C4 = CP / 4, PER = TOK * C4 / (64 * NW), HALF = PER / 2;
+      static_assert(TOK * C4 % (64 * NW) == 0 && PER % 2 == 0, "output pass");
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        float4 xr[HALF];
+#pragma unroll
+        for (int k = 0; k < HALF; ++k) {
+          const int i = tid + (hf * HALF + k) * 64 * NW, r = i / C4, q = (i - (i / C4) * C4) * 4;
+          xr[k] = *(const float4*)(a.x + (row0 + r) * a.ldx + q);
+        }
+#pragma unroll
+        for (int k = 0; k < HALF; ++k) {
+          const int i = tid + (hf * HALF + k) * 64 * NW, r = i / C4, q = (i - (i / C4) * C4) * 4;
+          const float4 v = *(const float4*)(sOut + r * LDO + q);
+          *(float4*)(a.out + (row0 + r) * a.ldout + q) =
+              make_float4(xr[k].x + rs * v.x, xr[k].y + rs * v.y, xr[k].z + rs * v.z, xr[k].w + rs * v.w);
+        }
+      }
+    }
+    // next iteration: its first LDS writes (sT, sMean) follow reads that precede the barriers above;
+    // its u writes to sH follow its own LN barrier, after every wave has left this output pass
+  }
+}
+
 }  // namespace
 
 extern "C" int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, const float* beta, float eps, int C,
@@ -422,7 +725,7 @@ extern "C" int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, 
                                   void* qkv, const float* table, float scale, void* O, long ldo, int o_ones_col,
                                   float* lse, const void* wproj, const float* bproj, const float* rowscale,
                                   int rows_per_scale, float* out, long ldout, long nWin, int nh, int H, int W, int shift,
-                                  void* stream) {
+                                  int w_split, void* stream) {
   KAIR_CHECK_ARG(x && gamma && beta && ln && mean && rstd && wqkv && bqkv && qkv && table && O && lse && wproj && bproj && out,
                  "swin_attn_fwd: null pointer");
   KAIR_CHECK_ARG(nh == 6 && C > 0 && C < 32 * nh && C % nh == 0 && C / nh <= 32,
@@ -450,7 +753,47 @@ extern "C" int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, 
       ncu <= 0)
     ncu = 256;
   const long grid = nWin < ncu ? nWin : ncu;   // persistent: one workgroup per CU
-  hipLaunchKernelGGL(swin_attn_fwd_kernel<6>, dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
+  if (w_split)
+    hipLaunchKernelGGL((swin_attn_fwd_kernel<6, 2>), dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL((swin_attn_fwd_kernel<6, 1>), dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, const float* beta, float eps, int C,
+                                 void* ln, long ldln, float* mean, float* rstd, const void* w1, const float* b1, void* u,
+                                 void* h, long ldh, int hd, const void* w2, const float* b2, const float* rowscale,
+                                 int rows_per_scale, float* out, long ldout, long M, int Cp, int Hp, int w_split,
+                                 void* stream) {
+  KAIR_CHECK_ARG(x && gamma && beta && ln && mean && rstd && w1 && b1 && u && h && w2 && b2 && out,
+                 "swin_mlp_fwd: null pointer");
+  KAIR_CHECK_ARG(Cp == 192 && Hp == 384 && C > 0 && C < Cp && hd > 0 && hd < Hp,
+                 "swin_mlp_fwd: laid out for Cp 192 / hidden 384 (C %d, Cp %d, hd %d, Hp %d)", C, Cp, hd, Hp);
+  KAIR_CHECK_ARG(M > 0 && M % TOK == 0, "swin_mlp_fwd: M must be a multiple of 64");
+  KAIR_CHECK_ARG(ldx >= Cp && ldx % 4 == 0 && ldout >= Cp && ldout % 4 == 0 && ldln >= Cp && ldln % 8 == 0 && ldh >= Hp &&
+                     ldh % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)b2 & 15) == 0,
+                 "swin_mlp_fwd: strides / alignment");
+  KAIR_CHECK_ARG(!rowscale || (rows_per_scale > 0 && rows_per_scale % TOK == 0), "swin_mlp_fwd: rows_per_scale");
+  MlpFwdArgs a;
+  a.x = x; a.ldx = ldx; a.gamma = gamma; a.beta = beta; a.eps = eps; a.C = C;
+  a.ln = (bf16*)ln; a.ldln = ldln; a.mean = mean; a.rstd = rstd;
+  a.w1 = (const bf16*)w1; a.b1 = b1; a.u = (bf16*)u; a.hact = (bf16*)h; a.ldh = ldh; a.hd = hd;
+  a.w2 = (const bf16*)w2; a.b2 = b2;
+  a.rowscale = rowscale; a.tiles_per_scale = rowscale ? rows_per_scale / TOK : 1;
+  a.out = out; a.ldout = ldout;
+  a.nTiles = M / TOK;
+  static const int dbg = getenv("KAIR_MLP_DBG") ? atoi(getenv("KAIR_MLP_DBG")) : 0;
+  a.dbg = dbg;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  const long grid = a.nTiles < 2L * ncu ? a.nTiles : 2L * ncu;   // persistent: two workgroups per CU
+  if (w_split)
+    hipLaunchKernelGGL(swin_mlp_fwd_kernel<2>, dim3((unsigned)grid), dim3(384), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(swin_mlp_fwd_kernel<1>, dim3((unsigned)grid), dim3(384), 0, (hipStream_t)stream, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

@@ -63,7 +63,7 @@ def swinir_flops(net, Hh, Ww):
 class _Lin:
     """A linear layer's packed forms.  n/k groupings map reference rows/cols to padded ones."""
 
-    def __init__(self, eng, mod, n_grp, k_grp, frag=False):
+    def __init__(self, eng, mod, n_grp, k_grp, frag=False, split=False):
         self.w, self.b = mod.weight, mod.bias
         N, K = self.w.shape
         self.N, self.K = N, K
@@ -76,9 +76,12 @@ class _Lin:
         self.Wp = torch.empty(self.Np, self.Kp, device=dev, dtype=eng.tdt)
         self.Wt = torch.empty(self.Kp, self.Np, device=dev, dtype=eng.tdt)
         self.bp = torch.empty(self.Np, device=dev)
-        # MFMA-fragment order of Wp (pack kind 10) for the fused block kernels
-        self.mapg = H.wmap(10, N, K, n_grp, k_grp) if frag else None
-        self.Wg = torch.empty(self.Np, self.Kp, device=dev, dtype=eng.tdt) if frag else None
+        # MFMA-fragment order of Wp for the fused block kernels: pack kind 10, or kind 12 (hi/lo
+        # bf16 pairs, the same ~16-bit weight precision as the split convs) when split
+        self.split = bool(frag and split)
+        self.mapg = H.wmap(12 if self.split else 10, N, K, n_grp, k_grp) if frag else None
+        self.Wg = (torch.empty((2 if self.split else 1) * self.Np, self.Kp, device=dev, dtype=eng.tdt)
+                   if frag else None)
 
     def pack_jobs(self):
         w, b = self.w.detach(), self.b.detach()
@@ -136,20 +139,26 @@ class _Blk:
         self.table = blk.attn.relative_position_bias_table
         self.scale = blk.attn.scale
         Hd = blk.mlp.fc1.out_features
-        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=eng.fused_attn)
-        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=eng.fused_attn)
-        self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp))
-        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp))
+        sp = eng.split_linear
+        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=eng.fused_attn, split=sp)
+        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=eng.fused_attn, split=sp)
+        self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp), frag=eng.fused_mlp, split=sp)
+        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=eng.fused_mlp, split=sp)
 
     def linears(self):
         return (self.qkv, self.proj, self.fc1, self.fc2)
 
 
 class SwinIREngine:
-    def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True):
-        """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv).
-        fused_blocks (bf16 only): each Swin block's attention half runs as one kernel
-        (kair_swin_attn_fwd) where the geometry allows it (6 heads, Cp = 192)."""
+    def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True, fused_mlp=None,
+                 split_linear=None):
+        """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
+        see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
+        fused block kernels (_Lin, pack kind 12).
+        fused_blocks (bf16 only): each Swin block's attention half and MLP half run as one kernel
+        each (kair_swin_attn_fwd, kair_swin_mlp_fwd) where the geometry allows it (6 heads,
+        Cp = 192, hidden padded to 384); fused_mlp (default: fused_blocks) selects the MLP-half
+        kernel separately."""
         self.net_ref = weakref.ref(net)
         if compute_dtype not in ("bf16", "fp32"):
             raise ValueError(compute_dtype)
@@ -171,6 +180,16 @@ class SwinIREngine:
         self.fused_attn = bool(fused_blocks) and compute_dtype == "bf16" and self.nh == 6 and self.Cp == 32 * self.nh
         Hd = net.layers[0].residual_group.blocks[0].mlp.fc1.out_features
         self.Hdp = _rup(Hd + 1, 32)
+        import os
+        # the fused MLP half is off by default: 146-168 us per block at B=32 against 162 us for the
+        # LN2 / fc1 / fc2 launches; KAIR_FUSED_MLP=1 turns it on (A/B timing)
+        if fused_mlp is None:
+            fused_mlp = fused_blocks and os.environ.get("KAIR_FUSED_MLP", "0") == "1"
+        self.fused_mlp = bool(fused_mlp) and compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384
+        # split linears measured: the PSNR effect of bf16 linear-weight rounding is ~1e-4 dB against
+        # ~5e-4 dB of activation-rounding noise per image (tools/parity_seeds.py, DESIGN.md "parity at
+        # bf16"), at +45 us per block for the attention kernel -- off unless asked for
+        self.split_linear = bool(split_linear) and compute_dtype == "bf16"
         self.upsampler, self.scale = net.upsampler, net.upscale
         self.in_ch = net.conv_first.in_channels
         self.img_range = float(net.img_range)
@@ -424,7 +443,11 @@ class SwinIREngine:
         H.layernorm_fwd(cur, Cp, P["nf"], Cp, n.weight, n.bias, P["n_mean"], P["n_rstd"], M, self.C, n.eps)
         H.gemm_nt(H.im2col(P["nf"], Hh, Ww, Cp), self.cab.fwd(), H.epilogue(P["fb"], bias=self.cab.bp, resid=P["f0"]),
                   M, Cp, 9 * Cp, cd)
-        img = (self.mean, self.img_range, self.in_ch, Hh * self.scale, Ww * self.scale)
+        return self._forward_tail(P)
+
+    def _forward_tail(self, P):
+        """Reconstruction tail: P['fb'] (conv_after_body + residual) -> P['E']."""
+        cd, Cp, M, B, Hh, Ww = self.cd, self.Cp, P["M"], P["B"], P["H"], P["W"]
         if self.upsampler == "pixelshuffle":
             c = self.cbu
             H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
@@ -459,7 +482,7 @@ class SwinIREngine:
             H.swin_attn_fwd(x, Cp, blk.n1.weight, blk.n1.bias, blk.n1.eps, self.C, S["ln1"], Cp, S["m1"], S["r1"],
                             blk.qkv.Wg, blk.qkv.bp, S["qkv"], blk.table, blk.scale, S["O"], nh * 32, self.C // nh,
                             S["lse"], blk.proj.Wg, blk.proj.bp, s_attn, HW, S["mid"], Cp, P["nWin"], nh, Hh, Ww,
-                            blk.shift)
+                            blk.shift, w_split=blk.qkv.split)
         else:
             H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps, win,
                             one_col=self.C)
@@ -471,6 +494,12 @@ class SwinIREngine:
             l = blk.proj
             H.gemm_nt(H.rows(S["O"]), H.rows(l.Wp), H.epilogue(S["mid"], win=win, bias=l.bp, resid=x, rowscale=s_attn,
                                                                 rows_per_scale=HW), M, Cp, nh * 32, cd)
+        if self.fused_mlp:   # LN2 -> fc1 + GELU -> fc2 + residual in one launch
+            f1, f2 = blk.fc1, blk.fc2
+            H.swin_mlp_fwd(S["mid"], Cp, blk.n2.weight, blk.n2.bias, blk.n2.eps, self.C, S["ln2"], Cp, S["m2"], S["r2"],
+                           f1.Wg, f1.bp, S["u"], S["h"], self.Hdp, f1.N, f2.Wg, f2.bp, s_mlp, HW, S["out"], Cp, M, Cp,
+                           self.Hdp, w_split=f1.split)
+            return S["out"]
         H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps,
                         one_col=self.C)
         l = blk.fc1

@@ -10,6 +10,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():
     pytest.skip("needs a HIP device", allow_module_level=True)
 
+from kair_amd.engine.swinir_engine import SwinIREngine  # noqa: E402
 from kair_amd.models.network_swinir import SwinIR  # noqa: E402
 
 dev = torch.device("cuda")
@@ -20,13 +21,17 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def _pair(fused_first=True, depths=(2, 2), img=24):
+def blk_hd(net):
+    return net.layers[0].residual_group.blocks[0].mlp.fc1.out_features
+
+
+def _pair(split=False, depths=(2, 2), img=24):
     torch.manual_seed(11)
     nets = []
     for fused in (True, False):
         n = SwinIR(upscale=2, in_chans=3, img_size=img, window_size=8, img_range=1.0, depths=list(depths), embed_dim=180,
                    num_heads=[6] * len(depths), mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.2,
-                   compute_dtype="bf16", fused_blocks=fused)
+                   compute_dtype="bf16", fused_blocks=fused, split_conv=split)
         nets.append(n)
     nets[1].load_state_dict(nets[0].state_dict())
     for n in nets:
@@ -34,15 +39,24 @@ def _pair(fused_first=True, depths=(2, 2), img=24):
             for b in (blk for l in n.layers for blk in l.residual_group.blocks):
                 b.attn.relative_position_bias_table.normal_(0, 0.5)
     nets[1].load_state_dict(nets[0].state_dict())
-    return [n.to(dev).train() for n in nets]
+    nets = [n.to(dev).train() for n in nets]
+    # the fused net with split linears too when split (pack kind 12 through both fused kernels)
+    nets[0]._engine = SwinIREngine(nets[0], "bf16", split_conv=split, fused_blocks=True, fused_mlp=True,
+                                   split_linear=split)
+    return nets
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("shape", [(2, 24, 24), (1, 16, 40)])
-def test_fused_attention_half_matches_unfused(shape):
+def test_fused_block_halves_match_unfused(shape, split):
+    """split=False: both paths multiply the same bf16 weights.  split=True: the fused kernels use
+    hi/lo weight pairs (pack kind 12) and the unfused GEMMs plain bf16 weights, so the two differ by
+    the bf16 weight rounding (checked looser)."""
     B, Hh, Ww = shape
-    fz, un = _pair()
+    fz, un = _pair(split)
     ef, eu = fz.engine(), un.engine()
-    assert ef.fused_attn and not eu.fused_attn
+    assert ef.fused_attn and ef.fused_mlp and not eu.fused_attn and not eu.fused_mlp
+    assert all(l.split == split for b in ef.blocks for l in b.linears())
     g = torch.Generator().manual_seed(1)
     x = torch.rand(B, 3, Hh, Ww, generator=g).to(dev)
     nb = len(ef.blocks)
@@ -54,12 +68,17 @@ def test_fused_attention_half_matches_unfused(shape):
     for bi in range(nb):
         Sf, Su = Pf["blocks"][bi], Pu["blocks"][bi]
         tb, tf = (5e-3, 2e-3) if bi == 0 else (2e-2, 1e-2)
-        for k in ("ln1", "qkv", "O"):
+        if split:
+            tb, tf = 2 * tb, 2 * tf
+        for k in ("ln1", "qkv", "O", "ln2", "u", "h"):
             assert rel(Sf[k].float(), Su[k].float()) < tb, (bi, k)
         assert (Sf["m1"] - Su["m1"]).abs().max().item() < (1e-6 if bi == 0 else 1e-3), bi
-        for k in ("r1", "lse", "mid", "out"):
-            assert rel(Sf[k], Su[k]) < tf, (bi, k)
-    assert rel(Ef, Eu) < 5e-3
+        for k in ("r1", "lse", "mid", "m2", "r2", "out"):
+            assert rel(Sf[k], Su[k]) < (tf if k != "m2" else 10 * tf), (bi, k)
+        # the ones columns the weight-gradient GEMMs use for bias gradients
+        assert (Sf["ln2"][:, ef.C] == 1).all() and (Sf["h"][:, blk_hd(fz)] == 1).all()
+        assert (Sf["u"][:, blk_hd(fz):] == 0).all() and (Sf["h"][:, blk_hd(fz) + 1:] == 0).all()
+    assert rel(Ef, Eu) < (5e-3 if not split else 1e-2)
     # gradients: both bf16 paths against the exact-fp32 engine on the same weights / scales; the
     # fused path must be as close to it as the unfused one (bf16 noise on small sums such as the
     # LayerNorm bias gradients is of the same order in both)
@@ -70,6 +89,9 @@ def test_fused_attention_half_matches_unfused(shape):
     er = ref.engine()
     Er = er.forward(x, D).clone()
     assert rel(Ef, Er) < 2e-2
+    # activation rounding dominates the rms error in both paths (the weight-rounding part is
+    # systematic but small in norm), so the fused path must simply not be the worse one
+    assert rel(Ef, Er) < 1.1 * rel(Eu, Er), (rel(Ef, Er), rel(Eu, Er))
     gE = torch.randn(Ef.shape, generator=g).to(dev)
     grads = []
     for eng, net in ((ef, fz), (eu, un), (er, ref)):

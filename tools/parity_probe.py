@@ -70,6 +70,31 @@ def main():
                           "mean": [round(float(d[:, c].mean()), 7) for c in range(3)]}), flush=True)
 
     report("bf16_engine(split conv)", run("bf16", sd))
+
+    # body / tail attribution: run both engines, then swap P['fb'] and re-run one tail
+    def engine_of(dtype, fused=True):
+        n = build_net(dtype, 0.0)
+        n.fused_blocks = fused
+        n = n.to(dev).eval()
+        n.load_state_dict(sd, strict=True)
+        return n, n.engine()
+    x = Le.to(dev)
+    with torch.no_grad():
+        n32, e32 = engine_of("fp32")
+        n16, e16 = engine_of("bf16")
+        e32.forward(x)
+        P32 = e32.cur
+        fb32 = P32["fb"].clone()
+        e16.forward(x)
+        P16 = e16.cur
+        fb16 = P16["fb"].clone()
+        P16["fb"].copy_(fb32)
+        report("bf16 tail on fp32 body", e16._forward_tail(P16).float().cpu())
+        P32["fb"].copy_(fb16)
+        report("fp32 tail on bf16 body", e32._forward_tail(P32).float().cpu())
+        print(json.dumps({"fb_rel_rms(bf16 body)": float((fb16 - fb32).pow(2).mean().sqrt() / fb32.pow(2).mean().sqrt())}))
+        nu, eu = engine_of("bf16", fused=False)
+        report("bf16_engine(unfused blocks)", nu(x).float().cpu())
     report("bf16_engine(no split)", run("bf16", sd, split=False))
     for name, sel in groups(net).items():
         st = {k: (v.to(torch.bfloat16).float() if (sel(k) and k.endswith("weight") and v.dim() >= 2) else v)
