@@ -21,7 +21,8 @@ def define_G(opt):
         net = SwinIR(upscale=o["upscale"], in_chans=o["in_chans"], img_size=o["img_size"], window_size=o["window_size"],
                      img_range=o["img_range"], depths=o["depths"], embed_dim=o["embed_dim"], num_heads=o["num_heads"],
                      mlp_ratio=o["mlp_ratio"], upsampler=o["upsampler"], resi_connection=o["resi_connection"],
-                     **_engine_kwargs(o))
+                     **_engine_kwargs(o), **({"drop_path_rate": o["drop_path_rate"]} if o.get("drop_path_rate") is not None
+                                             else {}))
     elif t in ("dncnn", "fdncnn"):
         from .network_dncnn import DnCNN, FDnCNN
         cls = DnCNN if t == "dncnn" else FDnCNN
@@ -50,7 +51,9 @@ def define_G(opt):
 
 
 def _engine_kwargs(o):
-    """Build-only option: netG.compute_dtype ('bf16' default, 'fp32' parity mode)."""
+    """Build-only option: netG.compute_dtype ('bf16' default, 'fp32' parity mode).  (netG.drop_path_rate,
+    SwinIR only, is passed through when present; absent, SwinIR's own default 0.1 applies exactly as
+    the reference's define_G leaves it.)"""
     return {"compute_dtype": o["compute_dtype"]} if o.get("compute_dtype") else {}
 
 

@@ -343,8 +343,11 @@ def gen_dncnn_kat():
     psnr_noisy = util.calculate_psnr(util.single2uint(img_L.squeeze()), img_H)
     psnr_den = util.calculate_psnr(E_u, img_H)
     print("DnCNN KAT noisy %.4f denoised %.4f" % (psnr_noisy, psnr_den))
+    # the pretrained weights themselves (weights-only load above), so the HIP DnCNN can run the KAT
+    # on the GPU box where the reference does not exist: keys "w/<state_dict key>"
+    weights = {"w/" + k: _np(v) for k, v in sd.items()}
     _save("dncnn_kat", img_H=img_H, img_L=img_L.astype(np.float32).squeeze(), E=_np(E).squeeze(),
-          psnr_noisy=np.float64(psnr_noisy), psnr_denoised=np.float64(psnr_den))
+          psnr_noisy=np.float64(psnr_noisy), psnr_denoised=np.float64(psnr_den), **weights)
 
 
 def gen_state_dict_layouts():

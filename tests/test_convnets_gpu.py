@@ -183,3 +183,26 @@ def test_fused_trainer_conv_nets_vs_oracle_trainer(kind):
     for k, v in ema.state_dict().items():
         if "running" not in k and "num_batches" not in k and k not in pre_bn:
             assert rel(v.float(), ref_e.state_dict()[k].float()) < 1e-4, k
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_dncnn_kat_on_hip(dt):
+    """Reference-held known-answer test on the HIP path: model_zoo/dncnn_25.pth (stored weights-only
+    in dncnn_kat.npz by make_golden.py) on utils/test.bmp + sigma-25 noise -> 29.8535 dB
+    (main_test_dncnn.py).  fp32 within 1e-3 dB; bf16 (split conv weights) reported and within 2e-2."""
+    from kair_amd.models.network_dncnn import DnCNN
+    from kair_amd.utils import utils_image as U
+    z = load_golden("dncnn_kat")
+    net = DnCNN(1, 1, 64, 17, "R", compute_dtype=dt)
+    sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w/")}
+    net.load_state_dict(sd, strict=True)
+    net = net.to(dev).eval()
+    L = torch.from_numpy(z["img_L"]).view(1, 1, *z["img_L"].shape).to(dev)
+    with torch.no_grad():
+        E = net(L).float().cpu()
+    psnr = U.calculate_psnr(U.tensor2uint(E), z["img_H"], border=0)
+    print(f"DnCNN KAT {dt}: {psnr:.5f} dB (reference 29.8535)")
+    assert abs(psnr - 29.8535) < (1e-3 if dt == "fp32" else 2e-2), psnr
+    # and the denoised image itself against the reference's recorded output
+    ref = torch.from_numpy(z["E"])
+    assert (E.squeeze() - ref).abs().max().item() < (1e-4 if dt == "fp32" else 2e-2)
