@@ -341,6 +341,11 @@ int kair_synth_dn(const float* pool, int C, int Hs, int Ws, const int* params, i
 const char* kair_last_error(void);
 int kair_device_arch(char* buf, int len);
 
+/* Perf investigation only: per-wave phase stamps of the last bf16 attention backward launched with
+ * KAIR_ATTN_STAMP=1 in the environment (s_memtime cycles, 8 per wave: 7 phase boundaries of the
+ * wave's third window + its window count).  n = number of u64 values to copy. */
+int kair_debug_attn_stamps(unsigned long long* host, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1744,7 +1744,8 @@ extern "C" int kair_wgrad_splits(long M, int N, int K) {
   if (tn_ring_shape(M, N, K)) {   // ring kernel: one 192x192 tile per CTA, one CTA per CU
     if (g_num_cus == 0) init_num_cus();
     const int tiles = ((N + TNR_BN - 1) / TNR_BN) * ((K + TNR_BK - 1) / TNR_BK);
-    long s = g_num_cus / tiles;
+    static const long sdiv = getenv("KAIR_TN_SPLIT_DIV") ? atol(getenv("KAIR_TN_SPLIT_DIV")) : 1;   // A/B knob
+    long s = g_num_cus / tiles / (sdiv > 0 ? sdiv : 1);
     // >= 128 rows per split (A/B knob KAIR_TN_ROWS; binds only at small M: at B = 4, 256 -> 128 rows
     // measured 311 -> 316-320 patches/s, 64 / 32 no better, 512 / 1024 slower)
     static const long min_rows = getenv("KAIR_TN_ROWS") ? atol(getenv("KAIR_TN_ROWS")) : 128;

@@ -10,6 +10,8 @@
 // in-register, the other operand fetched with ds_read_b64_tr_b16 in the matching order).  fp32
 // (parity) mode uses v_mfma_f32_32x32x2_f32 with the same dataflow.  The relative position bias
 // and the shift mask are computed from indices (no 64x64 tables are read).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -476,22 +478,32 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const typename AT<BF>::T*
           }
       }
     }
-    // P = exp(S*scale + bias + mask - lse) ; dS = P (dP - delta)
+    // P = exp(S*scale + bias + mask - lse) ; dS = P (dP - delta).  Lane = key ki, register r of
+    // tile qt = query qi = 32 qt + 8 (r/4) + r%4 + 4 hh, so every per-element LDS operand sits at a
+    // compile-time offset from a per-lane base: relidx(qi, ki) = 15 (4 qt + r/4) + r%4 + [15 (7 - ky)
+    // + 7 - kx + 4 hh]; lse / delta / region of qi at [32 qt + 8 (r/4) + r%4] + 4 hh.  The reads
+    // issue back to back instead of one dependent address computation each.
+    const int wi_img = (int)(win % nW), nWw = W / WS;
+    const bool mixed = shift > 0 && ((wi_img / nWw) == H / WS - 1 || (wi_img % nWw) == nWw - 1);
+    const float* rl = &sRow[w][0][4 * hh];
+    const float* rd = &sRow[w][1][4 * hh];
+    const int* rg = &sReg[w][4 * hh];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       const int ki = kt * 32 + l31;
       const int rk = sReg[w][ki];
+      const float* tb = &sTab[w][15 * (WS - 1 - (ki >> 3)) + (WS - 1 - (ki & 7)) + 4 * hh];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int qi = qt * 32 + acc_row(r, hh);
-          float sc = S[qt][kt][r] * scale + sTab[w][relidx(qi, ki)];
-          if (shift > 0 && sReg[w][qi] != rk) sc += -100.f;
-          if (amask) sc += amask[((win % mask_nw) * TOK + qi) * TOK + ki];
-          const float p = __expf(sc - sRow[w][0][qi]);
+          const int o = 32 * qt + 8 * (r >> 2) + (r & 3);
+          float sc = S[qt][kt][r] * scale + tb[15 * (4 * qt + (r >> 2)) + (r & 3)];
+          if (mixed && rg[o] != rk) sc += -100.f;
+          if (amask) sc += amask[((win % mask_nw) * TOK + qt * 32 + acc_row(r, hh)) * TOK + ki];
+          const float p = __expf(sc - rl[o]);
           S[qt][kt][r] = p;
-          const float d = p * (dP[qt][kt][r] - sRow[w][1][qi]);
+          const float d = p * (dP[qt][kt][r] - rd[o]);
           dP[qt][kt][r] = d;
           dB[qt][kt][r] += d;
         }
@@ -569,6 +581,16 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const typename AT<BF>::T*
       for (int r = 0; r < 16; ++r) out[(qt * 32 + acc_row(r, hh)) * TOK + kt * 32 + l31] = dB[qt][kt][r];
 }
 
+// perf-investigation phase stamps (KAIR_ATTN_STAMP=1, read with kair_debug_attn_stamps): per wave,
+// s_memtime at the phase boundaries of its third window
+constexpr int STAMP_WAVES = 8192, STAMP_N = 8;
+__device__ unsigned long long g_attn_stamps[STAMP_WAVES * STAMP_N];
+KAIR_DEV unsigned long long stamp_now() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
 // ------------------------------------------------------------------------------------------
 // bf16 backward, software-pipelined.  Per wave: one head, a group of windows.  The q/k/v/dO/O
 // fragments of the NEXT window are loaded into registers (16-byte loads, the frag_cols layout the
@@ -583,12 +605,16 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
                                                             const float* __restrict__ table, const float* __restrict__ lse,
                                                             bf16* __restrict__ dqkv, float* __restrict__ dB_part,
                                                             long nWin, int nh, int wpg, float scale, int H, int W,
-                                                            int shift, const float* __restrict__ amask, int mask_nw) {
-  constexpr int LD = AT<true>::LD, LDD = 72, NW = 4;
-  __shared__ __attribute__((aligned(16))) bf16 sQ[NW][TOK * LD];
+                                                            int shift, const float* __restrict__ amask, int mask_nw,
+                                                            int stamp) {
+  constexpr int LD = AT<true>::LD, LDD = 72, NW = 4, LDB = 72;
+  static_assert(TOK * LDD <= 2 * TOK * LD, "the dS tile reuses the q / dO tiles");
+  // per wave: q and dO tiles (after dV / dK they hold the dS tile), k tile, and the running bias
+  // gradient [q][key] in fp32 (row stride 72: the two lane halves' rows 4 apart fall in opposite
+  // bank halves) -- in LDS rather than 64 accumulator registers the kernel does not have
+  __shared__ __attribute__((aligned(16))) bf16 sQG[NW][2 * TOK * LD];
   __shared__ __attribute__((aligned(16))) bf16 sK[NW][TOK * LD];
-  __shared__ __attribute__((aligned(16))) bf16 sG[NW][TOK * LD];
-  __shared__ __attribute__((aligned(16))) bf16 sdS[NW][TOK * LDD];
+  __shared__ __attribute__((aligned(16))) float sDB[NW][TOK * LDB];
   __shared__ float sTab[NW][232];
   __shared__ float sRow[NW][2][TOK];  // lse, delta
   __shared__ int sReg[NW][TOK];
@@ -601,17 +627,11 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
   const long M = nWin * TOK;
   const long part = M * nh * HDP;
   const int l31 = lane & 31, hh = lane >> 5;
-  bf16* q = sQ[w]; bf16* k = sK[w]; bf16* go = sG[w]; bf16* ds = sdS[w];
+  bf16* q = sQG[w]; bf16* go = sQG[w] + TOK * LD; bf16* k = sK[w]; bf16* ds = sQG[w];
+  float* db = sDB[w];
   for (int i = lane; i < (2 * WS - 1) * (2 * WS - 1); i += 64) sTab[w][i] = table[i * nh + h];
+  for (int i = lane; i < TOK * LDB / 4; i += 64) ((float4*)db)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   const int nW = (H / WS) * (W / WS);
-
-  f32x16 dB[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dB[a][b][r] = 0.f;
 
   // register fragments of one window: rows t*32 + l31, columns 16 s + 8 hh
   bf16x8 Fq[2][2], Fk[2][2], Fv[2][2], Fg[2][2], Fo[2][2];
@@ -637,7 +657,11 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
   long w1 = w0 + wpg;
   if (w1 > nWin) w1 = nWin;
   load_win(w0);
+  unsigned long long ts[STAMP_N];
+  const bool stamping = stamp && gtask < STAMP_WAVES;
   for (long win = w0; win < w1; ++win) {
+    const bool st_on = stamping && win == w0 + 2;
+    if (st_on) ts[0] = stamp_now();
     const long blk = (win * nh + h) * TOK * HDP;
     wave_sync();   // the previous window's LDS tiles are no longer read
 #pragma unroll
@@ -663,6 +687,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
       }
     }
     sReg[w][lane] = shift > 0 ? token_region((int)(win % nW), lane, H, W, shift) : 0;
+    if (st_on) ts[1] = stamp_now();
 
     // S = Q K^T and dP = dO V^T : tiles [qt][kt], lane = key, regs = query
     f32x16 S[2][2], dP[2][2];
@@ -681,30 +706,65 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
           S[qt][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fq[qt][s], Fk[kt][s], S[qt][kt], 0, 0, 0);
           dP[qt][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fg[qt][s], Fv[kt][s], dP[qt][kt], 0, 0, 0);
         }
-    // the next window's fragments load under the rest of this window's work
-    if (win + 1 < w1) load_win(win + 1);
+    // the next window's fragments load under the rest of this window's work (unconditionally --
+    // the last window reloads itself -- so every path reaches the loop back-edge with the same
+    // loads pending and hipcc can wait for exactly them instead of draining the window's stores)
+    load_win(win + 1 < w1 ? win + 1 : win);
     wave_sync();
+    if (st_on) ts[2] = stamp_now();
 
-    // P = exp(S*scale + bias + mask - lse) ; dS = P (dP - delta)
+    // P = exp(S*scale + bias + mask - lse) ; dS = P (dP - delta).  Lane = key ki, register r of
+    // tile qt = query qi = 32 qt + 8 (r/4) + r%4 + 4 hh, so every per-element LDS operand sits at a
+    // compile-time offset from a per-lane base: relidx(qi, ki) = 15 (4 qt + r/4) + r%4 + [15 (7 - ky)
+    // + 7 - kx + 4 hh]; lse / delta / region of qi at [32 qt + 8 (r/4) + r%4] + 4 hh.  The reads
+    // issue back to back instead of one dependent address computation each.
+    const int wi_img = (int)(win % nW), nWw = W / WS;
+    const bool mixed = shift > 0 && ((wi_img / nWw) == H / WS - 1 || (wi_img % nWw) == nWw - 1);
+    const float* rl = &sRow[w][0][4 * hh];
+    const float* rd = &sRow[w][1][4 * hh];
+    const int* rg = &sReg[w][4 * hh];
+    float* dbl = db + 4 * hh * LDB + l31;
+    // Per 16-element block: every LDS read first, then the math, then the dB writes -- no branch
+    // and no possibly-aliasing store between the reads, so they issue back to back (one wave per
+    // SIMD: an LDS round trip per element would be the whole cost of this phase).
+    const bool plain = !mixed && !amask;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       const int ki = kt * 32 + l31;
-      const int rk = sReg[w][ki];
+      const float* tb = &sTab[w][15 * (WS - 1 - (ki >> 3)) + (WS - 1 - (ki & 7)) + 4 * hh];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+      for (int qt = 0; qt < 2; ++qt) {
+        float tv[16], lv[16], dv[16], bv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int qi = qt * 32 + acc_row(r, hh);
-          float sc = S[qt][kt][r] * scale + sTab[w][relidx(qi, ki)];
-          if (shift > 0 && sReg[w][qi] != rk) sc += -100.f;
-          if (amask) sc += amask[((win % mask_nw) * TOK + qi) * TOK + ki];
-          const float p = __expf(sc - sRow[w][0][qi]);
-          S[qt][kt][r] = p;
-          const float d = p * (dP[qt][kt][r] - sRow[w][1][qi]);
-          dP[qt][kt][r] = d;
-          dB[qt][kt][r] += d;
+          const int o = 32 * qt + 8 * (r >> 2) + (r & 3);
+          tv[r] = tb[15 * (4 * qt + (r >> 2)) + (r & 3)];
+          lv[r] = rl[o];
+          dv[r] = rd[o];
+          bv[r] = dbl[o * LDB + 32 * kt];   // each (q, key) entry belongs to one lane / register
         }
+        if (!plain) {   // shifted window on the image's last row / column, or an explicit mask
+          const int rk = sReg[w][ki];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int o = 32 * qt + 8 * (r >> 2) + (r & 3);
+            if (mixed && rg[o] != rk) tv[r] += -100.f;
+            if (amask) tv[r] += amask[((win % mask_nw) * TOK + qt * 32 + acc_row(r, hh)) * TOK + ki];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __expf(fmaf(S[qt][kt][r], scale, tv[r]) - lv[r]);
+          S[qt][kt][r] = p;
+          const float d = p * (dP[qt][kt][r] - dv[r]);
+          dP[qt][kt][r] = d;
+          bv[r] += d;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dbl[(32 * qt + 8 * (r >> 2) + (r & 3)) * LDB + 32 * kt] = bv[r];
+      }
     }
+    if (st_on) ts[3] = stamp_now();
     // dV^T = dO^T P and dK^T = scale * Q^T dS : tiles [kt], rows = d, lane = key
     bf16* dq_out = dqkv + blk;
     bf16* dk_out = dqkv + part + blk;
@@ -731,7 +791,9 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
         *(bf16x4*)(dk_out + key * HDP + 8 * g + 4 * hh) = kk;
       }
     }
-    // dQ^T = scale * K^T dS^T : dS through LDS ([q][key] row-major)
+    if (st_on) ts[4] = stamp_now();
+    // dQ^T = scale * K^T dS^T : dS through LDS ([q][key] row-major), written over the q / dO tiles
+    wave_sync();   // the dV / dK fragment reads of q and dO are complete
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
@@ -739,6 +801,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
 #pragma unroll
         for (int r = 0; r < 16; ++r) ds[(qt * 32 + acc_row(r, hh)) * LDD + kt * 32 + l31] = (bf16)dP[qt][kt][r];
     wave_sync();
+    if (st_on) ts[5] = stamp_now();
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       f32x16 aq;
@@ -756,15 +819,26 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
         *(bf16x4*)(dq_out + qi * HDP + 8 * g + 4 * hh) = vq;
       }
     }
+    if (st_on) {
+      ts[6] = stamp_now();
+      ts[7] = (unsigned long long)(w1 - w0);
+      if (lane < STAMP_N) {
+        unsigned long long v = ts[0];
+#pragma unroll
+        for (int i = 1; i < STAMP_N; ++i)
+          if (lane == i) v = ts[i];
+        g_attn_stamps[gtask * STAMP_N + lane] = v;   // vector store, one lane per stamp
+      }
+    }
   }
-  // partial bias gradient of this (group, head): [q][key]
+  // partial bias gradient of this (group, head): [q][key], row-contiguous 16-byte stores
+  wave_sync();
   float* out = dB_part + (grp * nh + h) * TOK * TOK;
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) out[(qt * 32 + acc_row(r, hh)) * TOK + kt * 32 + l31] = dB[qt][kt][r];
+  for (int i = 0; i < TOK * TOK / 4 / 64; ++i) {
+    const int c = lane + 64 * i, row = c >> 4, c4 = (c & 15) * 4;
+    *(float4*)(out + row * TOK + c4) = *(const float4*)(db + row * LDB + c4);
+  }
 }
 
 // stage 1: dB[h][q][k] = sum over groups of the per-group partials (coalesced, one thread per entry)
@@ -837,6 +911,16 @@ extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* tab
   return 0;
 }
 
+static const int g_stamp = getenv("KAIR_ATTN_STAMP") ? atoi(getenv("KAIR_ATTN_STAMP")) : 0;
+
+// copy the attention-backward phase stamps to the host (perf investigation only)
+extern "C" int kair_debug_attn_stamps(unsigned long long* host, int n) {
+  KAIR_CHECK_ARG(host && n > 0 && n <= STAMP_WAVES * STAMP_N, "debug_attn_stamps: bad args");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), sizeof(unsigned long long) * n, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return kair_set_error(KAIR_ERR_HIP, "debug_attn_stamps: copy failed");
+  return 0;
+}
+
 extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) {
   const long g32 = bwd_groups(nWin, WPG), g16 = bwd_groups(nWin, bwd_wpg_bf16(nWin, nh));
   return ((g32 > g16 ? g32 : g16) + 1) * nh * TOK * TOK;
@@ -858,7 +942,8 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
     hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
-                       (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw);
+                       (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw,
+                       g_stamp);
   else
     hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
                        ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw);
