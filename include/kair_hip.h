@@ -90,7 +90,8 @@ typedef struct {
   const float* resid; long ldr;          /* optional: out = resid + rowscale * value (fp32)    */
   const float* rowscale; int rows_per_scale;
   const void* gate; int gate_dtype; long ldg; int gate_kind; /* value *= act'(gate):
-                                           1 gelu'(gate)  2 leaky'(sign of gate)  3 relu'     */
+                                           1 gelu'(gate)  2 leaky'(sign of gate)  3 relu'
+                                           4 gate itself (a stored activation derivative)     */
   int ps_r, ps_H, ps_W;                 /* pixel (un)shuffle geometry                         */
   int qkv_nh, qkv_hdp, qkv_tok;         /* KAIR_OUT_QKVBLK                                    */
   const float* img_mean; float img_range; int img_C, img_H, img_W; /* KAIR_OUT_NCHW          */
@@ -98,6 +99,9 @@ typedef struct {
                                            (the next weight-gradient GEMM's ones column); 0 none */
   const float* resid2; long ldr2;        /* optional second fp32 residual (ROWS): out += resid2
                                            (U-Net skip additions, network_usrnet_v1.py:159-162)  */
+  int pre_kind;                         /* out_pre holds: 0 the pre-activation x; 1 act'(x) (GELU
+                                           only: the backward gate, gate_kind 4, with no erf
+                                           left in the backward epilogue)                        */
 } kair_epilogue;
 
 /* C[m,n] = sum_k A[m,k] * B[n,k]  (+ epilogue).  compute: KAIR_BF16 -> v_mfma_f32_16x16x32_bf16,
@@ -225,8 +229,8 @@ int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, const float
 /* Fused MLP half of a Swin block (bf16; Cp = 192, hidden padded to Hp = 384):
  *   out = x + rowscale * fc2(GELU(fc1(LN2(x))))     network_swinir.py:274-276, Mlp.forward :24-30
  * in one launch over 64-row tiles of token rows.  Saved for the unchanged backward as
- * kair_layernorm_fwd / kair_gemm_nt store them: ln (1.0 at column C), mean / rstd, u = the fc1
- * pre-activation and h = GELU(u) (1.0 at column hd), both [M][ldh].  w1 [Hp][Cp] and w2 [Cp][Hp]
+ * kair_layernorm_fwd / kair_gemm_nt (pre_kind 1) store them: ln (1.0 at column C), mean / rstd,
+ * u = GELU'(x) of the fc1 pre-activation x and h = GELU(x) (1.0 at column hd), both [M][ldh].  w1 [Hp][Cp] and w2 [Cp][Hp]
  * in MFMA-fragment order (kind 10, or kind 12 when w_split); b1 [Hp], b2 [Cp] padded. */
 int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, const float* beta, float eps, int C,
                       void* ln, long ldln, float* mean, float* rstd, const void* w1, const float* b1, void* u,

@@ -59,7 +59,7 @@ class Epilogue(ctypes.Structure):
                 ("ps_r", c_int), ("ps_H", c_int), ("ps_W", c_int),
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
                 ("img_mean", c_vp), ("img_range", c_float), ("img_C", c_int), ("img_H", c_int), ("img_W", c_int),
-                ("out_ones_col_p1", c_int), ("resid2", c_vp), ("ldr2", c_long)]
+                ("out_ones_col_p1", c_int), ("resid2", c_vp), ("ldr2", c_long), ("pre_kind", c_int)]
 
 
 class WMap(ctypes.Structure):
@@ -252,8 +252,10 @@ def qkvblk(t, nh, hdp=32, tok=64, rowscale=None, rows_per_scale=1):
 
 def epilogue(out, mode=OUT_ROWS, ldo=None, win=None, bias=None, act=ACT_NONE, slope=0.0, pre=None, ldp=None,
              resid=None, ldr=None, rowscale=None, rows_per_scale=1, gate=None, ldg=None, gate_kind=0,
-             ps=None, qkv=None, img=None, ones_col=-1, resid2=None, ldr2=None):
+             ps=None, qkv=None, img=None, ones_col=-1, resid2=None, ldr2=None, pre_grad=False):
+    """pre_grad: `pre` receives act'(x) instead of x (GELU; read back with gate_kind=4)."""
     e = Epilogue()
+    e.pre_kind = int(bool(pre_grad))
     e._keep = (out, bias, pre, resid, rowscale, gate, img, resid2)
     if resid2 is not None:
         e.resid2, e.ldr2 = ptr(resid2), (ldr2 if ldr2 is not None else resid2.shape[-1])

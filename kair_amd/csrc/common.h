@@ -99,6 +99,20 @@ KAIR_DEV float erf_fast(float x) {
   y = 1.0f - y * t * __expf(-ax * ax);
   return copysignf(y, x);
 }
+// GELU and GELU' of the same x sharing one rcp and one exp (gelu_fast / gelu_grad_fast maths)
+KAIR_DEV void gelu_pair_fast(float x, float& y, float& dy) {
+  const float z = x * 0.70710678118654752f, az = fabsf(z);
+  const float t = __frcp_rn(1.0f + 0.3275911f * az);
+  float p = 1.061405429f;
+  p = fmaf(p, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __expf(-az * az);   // = exp(-x^2 / 2)
+  const float cdf = 0.5f * (1.0f + copysignf(1.0f - p * t * e, z));
+  y = x * cdf;
+  dy = cdf + x * 0.39894228040143268f * e;
+}
 KAIR_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 KAIR_DEV float gelu_grad_fast(float x) {
   const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));

@@ -234,6 +234,7 @@ struct Epi {
   const float* resid; long ldr;
   const float* rowscale; int rps;
   const void* gate; int gdt; long ldg; int gkind;
+  int prek;   // 1: pre receives act'(x) (GELU)
   int r, psH, psW;
   int nh, hdp, tok;
   const float* mean; float range; int imgC, imgH, imgW;
@@ -253,6 +254,7 @@ Epi make_epi(const kair_epilogue& o, long M, int N) {
   e.resid = o.resid; e.ldr = o.ldr;
   e.rowscale = o.rowscale; e.rps = o.rows_per_scale > 0 ? o.rows_per_scale : 1;
   e.gate = o.gate; e.gdt = o.gate_dtype; e.ldg = o.ldg; e.gkind = o.gate_kind;
+  e.prek = o.pre_kind;
   e.r = o.ps_r; e.psH = o.ps_H; e.psW = o.ps_W;
   e.nh = o.qkv_nh; e.hdp = o.qkv_hdp; e.tok = o.qkv_tok;
   e.mean = o.img_mean; e.range = o.img_range; e.imgC = o.img_C; e.imgH = o.img_H; e.imgW = o.img_W;
@@ -297,7 +299,7 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
   float pre[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    pre[j] = v[j];
+    pre[j] = (e.prek && e.act == KAIR_ACT_GELU) ? gelu_erf_grad(v[j]) : v[j];
     if (e.act == KAIR_ACT_GELU) v[j] = gelu_erf(v[j]);
     else if (e.act == KAIR_ACT_LEAKY) v[j] = v[j] > 0.f ? v[j] : v[j] * e.slope;
     else if (e.act == KAIR_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
@@ -315,6 +317,7 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
       for (int j = 0; j < 8; ++j) {
         if (e.gkind == 1) v[j] *= gelu_erf_grad(g[j]);
         else if (e.gkind == 2) v[j] *= (g[j] > 0.f ? 1.f : e.slope);
+        else if (e.gkind == 4) v[j] *= g[j];
         else v[j] *= (g[j] > 0.f ? 1.f : 0.f);
       }
     }
@@ -379,7 +382,7 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
       if (e.gate) {
         const float g = e.gdt == KAIR_BF16 ? (float)((const bf16*)e.gate)[orow * e.ldg + oc]
                                             : ((const float*)e.gate)[orow * e.ldg + oc];
-        val *= (e.gkind == 2) ? (g > 0.f ? 1.f : e.slope) : (g > 0.f ? 1.f : 0.f);
+        val *= (e.gkind == 2) ? (g > 0.f ? 1.f : e.slope) : (e.gkind == 4 ? g : (g > 0.f ? 1.f : 0.f));
       }
       st1(e.out, e.odt, orow * e.ldo + oc, val);
     }
@@ -596,8 +599,12 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       pre[j] = v[j];
-      if (e.act == KAIR_ACT_GELU) v[j] = gelu_fast(v[j]);
-      else if (e.act == KAIR_ACT_LEAKY) v[j] = v[j] > 0.f ? v[j] : v[j] * e.slope;
+      if (e.act == KAIR_ACT_GELU) {
+        float y, dy;
+        gelu_pair_fast(v[j], y, dy);
+        v[j] = y;
+        if (e.prek) pre[j] = dy;
+      } else if (e.act == KAIR_ACT_LEAKY) v[j] = v[j] > 0.f ? v[j] : v[j] * e.slope;
       else if (e.act == KAIR_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
     }
     if (e.gate) {
@@ -607,6 +614,7 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
       for (int j = 0; j < 4; ++j) {
         if (e.gkind == 1) v[j] *= gelu_grad_fast(g[j]);
         else if (e.gkind == 2) v[j] *= (g[j] > 0.f ? 1.f : e.slope);
+        else if (e.gkind == 4) v[j] *= g[j];
         else v[j] *= (g[j] > 0.f ? 1.f : 0.f);
       }
     }
@@ -946,8 +954,12 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
               pre[c] = v[c];
-              if (E.act == KAIR_ACT_GELU) v[c] = gelu_fast(v[c]);
-              else if (E.act == KAIR_ACT_LEAKY) v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
+              if (E.act == KAIR_ACT_GELU) {
+                float y, dy;
+                gelu_pair_fast(v[c], y, dy);
+                v[c] = y;
+                if (E.prek) pre[c] = dy;
+              } else if (E.act == KAIR_ACT_LEAKY) v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
               else if (E.act == KAIR_ACT_RELU) v[c] = fmaxf(v[c], 0.f);
             }
             if constexpr (EX != EX_NONE) {
@@ -962,6 +974,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
                 for (int c = 0; c < 8; ++c) {
                   if (E.gkind == 1) v[c] *= gelu_grad_fast(x8[c]);
                   else if (E.gkind == 2) v[c] *= (x8[c] > 0.f ? 1.f : E.slope);
+                  else if (E.gkind == 4) v[c] *= x8[c];
                   else v[c] *= (x8[c] > 0.f ? 1.f : 0.f);
                 }
               }

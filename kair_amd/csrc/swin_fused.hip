@@ -441,7 +441,8 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
 //   out = mid + s * fc2( GELU( fc1( LN2(mid) ) ) )      network_swinir.py:274-276 + Mlp.forward :24-30
 // one workgroup per 64 token rows (persistent, two per CU), 6 waves.  Rows are token order (no window
 // map).  Saved for backward exactly as the unfused path stores them: LN2 output (1.0 at column C),
-// mean / rstd, u = fc1 pre-activation, h = GELU(u) (1.0 at column hd).  The u / h tile and then the
+// mean / rstd, g = GELU'(u) of the fc1 pre-activation u (the fc2-dgrad gate), h = GELU(u) (1.0 at
+// column hd).  The u / h tile and then the
 // fp32 output tile are staged in one LDS buffer, so every global store is a 16-byte row-contiguous
 // access; the residual is re-read from L2 at the end instead of being held in LDS (the LDS budget
 // stays under half a CU: two workgroups per CU overlap one's LayerNorm / stores with the other's
@@ -454,7 +455,7 @@ struct MlpFwdArgs {
   bf16* ln; long ldln;                       // saved LN2 output, 1.0 at column C
   float* mean; float* rstd;                  // [M]
   const bf16* w1; const float* b1;           // fragment order [HP/32][CP/16][S][64][8], bias [HP]
-  bf16* u; bf16* hact; long ldh; int hd;     // pre-activation / GELU output [M][ldh], 1.0 at h column hd
+  bf16* u; bf16* hact; long ldh; int hd;     // GELU'(pre-activation) / GELU output [M][ldh], 1.0 at h column hd
   const bf16* w2; const float* b2;           // fragment order [CP/32][HP/16][S][64][8], bias [CP]
   const float* rowscale; int tiles_per_scale;
   float* out; long ldout;
@@ -640,14 +641,17 @@ __global__ __launch_bounds__(384, 3) void swin_mlp_fwd_kernel(const MlpFwdArgs a
         const int r = i / CH, q = (i - (i / CH) * CH) * 8;
         bf16* ps = sH + r * LDH + q;
         const bf16x8 uv = *(const bf16x8*)ps;
-        *(bf16x8*)(a.u + (row0 + r) * a.ldh + q) = uv;
-        bf16x8 hv;
+        bf16x8 hv, gv;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int cc = q + j;
-          hv[j] = cc < a.hd ? (bf16)gelu_fast((float)uv[j]) : (bf16)(cc == a.hd ? 1.f : 0.f);
+          float y, dy;
+          gelu_pair_fast((float)uv[j], y, dy);
+          hv[j] = cc < a.hd ? (bf16)y : (bf16)(cc == a.hd ? 1.f : 0.f);
+          gv[j] = (bf16)dy;
         }
         *(bf16x8*)ps = hv;
+        *(bf16x8*)(a.u + (row0 + r) * a.ldh + q) = gv;
         *(bf16x8*)(a.hact + (row0 + r) * a.ldh + q) = hv;
       }
     }

@@ -503,8 +503,8 @@ class SwinIREngine:
         H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps,
                         one_col=self.C)
         l = blk.fc1
-        H.gemm_nt(H.rows(S["ln2"]), H.rows(l.Wp), H.epilogue(S["h"], bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N),
-                  M, l.Np, Cp, cd)
+        H.gemm_nt(H.rows(S["ln2"]), H.rows(l.Wp), H.epilogue(S["h"], bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N,
+                                                               pre_grad=True), M, l.Np, Cp, cd)
         l = blk.fc2
         H.gemm_nt(H.rows(S["h"]), H.rows(l.Wp), H.epilogue(S["out"], bias=l.bp, resid=S["mid"], rowscale=s_mlp,
                                                             rows_per_scale=HW), M, Cp, self.Hdp, cd)
@@ -657,7 +657,8 @@ class SwinIREngine:
         fc2, fc1 = blk.fc2, blk.fc1
         ev_fc2 = self._on_side(lambda: self._wgrad(P, H.rows(Dc), H.rows(S["h"], ones_col=fc2.K, ones_in_data=True), M,
                                                    Cp, self.Hdp, fc2.map, g(fc2.w), g(fc2.b), fc2.K))
-        H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=1), M, self.Hdp, Cp, cd)
+        # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
+        H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
         self._on_side(lambda: self._wgrad(P, H.rows(P["dU"]), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), M,
                                           self.Hdp, Cp, fc1.map, g(fc1.w), g(fc1.b), self.C))
         H.gemm_nt(H.rows(P["dU"]), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)

@@ -77,7 +77,8 @@ def test_fused_block_halves_match_unfused(shape, split):
             assert rel(Sf[k], Su[k]) < (tf if k != "m2" else 10 * tf), (bi, k)
         # the ones columns the weight-gradient GEMMs use for bias gradients
         assert (Sf["ln2"][:, ef.C] == 1).all() and (Sf["h"][:, blk_hd(fz)] == 1).all()
-        assert (Sf["u"][:, blk_hd(fz):] == 0).all() and (Sf["h"][:, blk_hd(fz) + 1:] == 0).all()
+        # u holds GELU'(pre-activation): 0.5 on the zero pre-activation of the pad columns
+        assert (Sf["u"][:, blk_hd(fz):] == 0.5).all() and (Sf["h"][:, blk_hd(fz) + 1:] == 0).all()
     assert rel(Ef, Eu) < (5e-3 if not split else 1e-2)
     # gradients: both bf16 paths against the exact-fp32 engine on the same weights / scales; the
     # fused path must be as close to it as the unfused one (bf16 noise on small sums such as the

@@ -50,6 +50,8 @@ def main():
     fc2, fc1, proj, qkv = blk.fc2, blk.fc1, blk.proj, blk.qkv
     out["fc2_dgrad_gelu_gate"] = timeit(lambda: H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=1),
                                                           M, Hdp, Cp, cd), reps)
+    out["fc2_dgrad_mul_gate"] = timeit(lambda: H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=4),
+                                                         M, Hdp, Cp, cd), reps)
     out["fc2_dgrad_relu_gate"] = timeit(lambda: H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=0),
                                                           M, Hdp, Cp, cd), reps)
     out["fc2_dgrad_no_gate"] = timeit(lambda: H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"]), M, Hdp, Cp, cd), reps)
