@@ -48,6 +48,7 @@ struct AttnFwdArgs {
   float* out; long ldout;                    // mid fp32 [M][ldout], token order
   long nWin; int H, W, shift;
   WinMap wm;
+  int dbg;   // ablation bits (KAIR_ATTN_DBG, perf investigation only): 1 no q/k/v stores, 2 no end-of-window stores
 };
 
 KAIR_DEV bf16x8 pack8r(const f32x16& a, int s) {
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
 
     // the saved q / k / v go out now (their registers are needed until the attention's last MFMA
     // anyway); the loads after them (proj weights) were issued before
-    {   // q / k / v, head-blocked [part][win][h][tok][32]
+    if (!(a.dbg & 1)) {   // q / k / v, head-blocked [part][win][h][tok][32]
       const long part = M * NH * 32;
       bf16* qb = a.qkv + (win * NH + h) * TOK * 32;
 #pragma unroll
@@ -412,22 +413,22 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
       }
     __syncthreads();
     constexpr int C4 = CP / 4;
-    for (int i = tid; i < TOK * C4; i += 64 * NH) {
+    for (int i = tid; i < ((a.dbg & 2) ? 0 : TOK * C4); i += 64 * NH) {
       const int r = i / C4, q = (i - (i / C4) * C4) * 4;
       *(float4*)(a.out + (long)sRow[r] * a.ldout + q) = *(const float4*)(sX + r * LDX + q);
     }
-    if (hh == 0) {
+    if (hh == 0 && !(a.dbg & 2)) {
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) a.lse[(win * NH + h) * TOK + qt * 32 + l31] = lse_v[qt];
     }
     // LN1 rows and O rows from LDS, 16 bytes per lane (window order)
     constexpr int CH = CP / 8;   // 16-byte chunks per row
-    for (int i = tid; i < TOK * CH; i += 64 * NH) {
+    for (int i = tid; i < ((a.dbg & 2) ? 0 : TOK * CH); i += 64 * NH) {
       const int r = i / CH, q = (i - (i / CH) * CH) * 8;
       *(uint4*)(a.ln + (win * TOK + r) * a.ldln + q) = *(const uint4*)(sT + r * LDT + q);
       *(uint4*)(a.O + (win * TOK + r) * a.ldo + q) = *(const uint4*)(sO + r * LDT + q);
     }
-    if (tid < TOK) {
+    if (tid < TOK && !(a.dbg & 2)) {
       const long t = sRow[tid];
       a.mean[t] = sMean[tid];
       a.rstd[t] = sRstd[tid];
@@ -439,15 +440,21 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
 
 // ---- MLP half ------------------------------------------------------------------------------------
 //   out = mid + s * fc2( GELU( fc1( LN2(mid) ) ) )      network_swinir.py:274-276 + Mlp.forward :24-30
-// one workgroup per 64 token rows (persistent, two per CU), 6 waves.  Rows are token order (no window
-// map).  Saved for backward exactly as the unfused path stores them: LN2 output (1.0 at column C),
-// mean / rstd, g = GELU'(u) of the fc1 pre-activation u (the fc2-dgrad gate), h = GELU(u) (1.0 at
-// column hd).  The u / h tile and then the
-// fp32 output tile are staged in one LDS buffer, so every global store is a 16-byte row-contiguous
-// access; the residual is re-read from L2 at the end instead of being held in LDS (the LDS budget
-// stays under half a CU: two workgroups per CU overlap one's LayerNorm / stores with the other's
-// MFMAs).  Per 64 rows it moves mid in (49 KB fp32, read twice, the second from L2) and ln2 (24.6
-// KB) + u + h (2 x 49 KB) + out (49 KB) out, against the ~1.6x that the LN2 / fc1 / fc2 kernels move.
+// Persistent, one 1024-thread workgroup per CU looping over 64-row tiles of token rows, WARP-
+// SPECIALISED: 12 compute waves never issue a global store, 4 store waves never issue a load.
+// On gfx950 vmcnt counts loads and stores in issue order, so in a wave that stores a tile's outputs
+// every later load (the streamed weight fragments of the next k-steps, the next tile's rows) waits
+// for those stores to drain; here the compute waves' loads wait only for loads, and the store
+// waves drain the outputs from LDS while the compute waves run the next phase.
+// The hidden layer runs in two 192-column halves so the whole working set fits one CU's LDS:
+//   compute: LN2 (x rows prefetched a tile ahead in registers) -> sT, x -> sX (fp32)
+//            per half: fc1 (one 32x32 tile per wave) -> u -> sU | GELU pair: h -> sU, g -> sG |
+//            fc2 partial (one 32x32 output tile per wave, accumulated over both halves)
+//            out = x + s * (fc2 + b2) in place in sX
+//   store:   ln2 / mean / rstd from sT | per half g, h from sG, sU | out rows from sX
+// Saved for backward as the unfused path stores them (pre_kind 1): LN2 output (1.0 at column C),
+// mean / rstd, g = GELU'(u) of the fc1 pre-activation, h = GELU(u) (1.0 at column hd).  Per 64
+// rows it moves mid in (49 KB fp32, once) and ln2 (24.6 KB) + g + h (2 x 49 KB) + out (49 KB) out.
 struct MlpFwdArgs {
   const float* x; long ldx;                  // mid fp32 [M][ldx]
   const float* gamma; const float* beta;     // LN2
@@ -460,53 +467,45 @@ struct MlpFwdArgs {
   const float* rowscale; int tiles_per_scale;
   float* out; long ldout;
   long nTiles;
-  int dbg;   // ablation bits (KAIR_MLP_DBG, perf investigation only): 1 no fc1 MFMA, 2 no fc2 MFMA, 4 no u/h pass
+  int dbg;   // ablation bits (KAIR_MLP_DBG, perf investigation only): 1 no fc1 MFMA, 2 no fc2 MFMA, 4 no store-wave stores
 };
 
 template <int S>
-__global__ __launch_bounds__(384, 3) void swin_mlp_fwd_kernel(const MlpFwdArgs a) {
-  constexpr int NW = 6, CP = 192, HP = 384, LDT = CP + 8, LDH = HP + 8, LDO = CP + 4;
-  constexpr int KB1 = CP / 16, KB2 = HP / 16, WS = 512 * S;
-  constexpr int PF1 = 2, PF2 = 2;   // weight prefetch depths (k-steps)
-  constexpr int RPW = (TOK + NW - 1) / NW, NPASS = (RPW + 3) / 4;
-  static_assert(KB1 % PF1 == 0 && KB2 % PF2 == 0, "k-steps must be a multiple of the prefetch depth");
-  static_assert(TOK * LDH * 2 == TOK * LDO * 4, "the fp32 output tile reuses the u / h tile");
-  __shared__ __attribute__((aligned(16))) bf16 sT[TOK * LDT];   // LN2 tile
-  __shared__ __attribute__((aligned(16))) bf16 sH[TOK * LDH];   // u, then h; then the fp32 output tile
+__global__ __launch_bounds__(1024) void swin_mlp_fwd_kernel(const MlpFwdArgs a) {
+  constexpr int NC = 12, NST = 256, CP = 192, HP = 384, HH = HP / 2;
+  constexpr int LDT = CP + 8, LDU = HH + 8, LDX = CP + 4;
+  constexpr int KB1 = CP / 16, KB2 = HP / 16, KBH = HH / 16, WS = 512 * S, PF = S == 1 ? 4 : 3;
+  constexpr int RPW = (TOK + NC - 1) / NC, NPASS = (RPW + 3) / 4;   // LN rows per compute wave
+  static_assert(KB1 % PF == 0 && KBH % PF == 0, "k-steps must be a multiple of the prefetch depth");
+  __shared__ __attribute__((aligned(16))) bf16 sT[TOK * LDT];    // LN2 tile
+  __shared__ __attribute__((aligned(16))) bf16 sU[TOK * LDU];    // h of one hidden half
+  __shared__ __attribute__((aligned(16))) bf16 sG[TOK * LDU];    // GELU'(u) of one hidden half
+  __shared__ __attribute__((aligned(16))) float sX[TOK * LDX];   // x rows (fp32), then the output rows
   __shared__ __attribute__((aligned(16))) float sB1[HP];
   __shared__ __attribute__((aligned(16))) float sB2[CP];
   __shared__ float sGB[2][CP];
   __shared__ float sMean[TOK], sRstd[TOK];
-  float* sOut = (float*)sH;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bool compute = w < NC;
+  const int sid = tid - 64 * NC;   // store-wave thread index (0..255)
   const int l31 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, jl = lane & 15;
-  long tile = blockIdx.x;
 
-  for (int i = tid; i < HP; i += 64 * NW) sB1[i] = a.b1[i];
-  for (int i = tid; i < CP; i += 64 * NW) sB2[i] = a.b2[i];
-  for (int i = tid; i < CP; i += 64 * NW) {
+  for (int i = tid; i < HP; i += 1024) sB1[i] = a.b1[i];
+  for (int i = tid; i < CP; i += 1024) {
+    sB2[i] = a.b2[i];
     sGB[0][i] = i < a.C ? a.gamma[i] : 0.f;
     sGB[1][i] = i < a.C ? a.beta[i] : 0.f;
   }
-  // fc1: wave w makes hidden columns [64w, 64w + 64) (two 32-column tiles); fc2: output columns
-  // [32w, 32w + 32).  MFMA D = W . X^T: lane = token row, registers = 4-column groups.
-  const bf16* w1p = a.w1 + (long)(2 * w) * KB1 * WS + lane * 8;
-  const bf16* w2p = a.w2 + (long)w * KB2 * WS + lane * 8;
-  bf16x8 p1[PF1][2][S], p2[PF2][S];
-  auto load_w1 = [&]() {
-#pragma unroll
-    for (int i = 0; i < PF1; ++i)
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int e = 0; e < S; ++e) p1[i][ct][e] = *(const bf16x8*)(w1p + (long)ct * KB1 * WS + i * WS + e * 512);
-  };
+  // compute wave w owns one 32x32 tile of each GEMM: columns 32 (w % 6) (of the hidden half for
+  // fc1, of the output for fc2), token rows 32 (w / 6).  MFMA D = W . X^T: lane = token row,
+  // registers = columns.
+  const int ct = w % 6, rt = w / 6;
   float4 xv[NPASS][3];
   auto load_x = [&](long tl) {
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
-      const int i = 4 * p + g, r = w + NW * i;
+      const int i = 4 * p + g, r = w + NC * i;
       const bool ok = tl < a.nTiles && i < RPW && r < TOK;
       const long base = ok ? (tl * TOK + r) * a.ldx : 0;
 #pragma unroll
@@ -516,209 +515,183 @@ __global__ __launch_bounds__(384, 3) void swin_mlp_fwd_kernel(const MlpFwdArgs a
       }
     }
   };
+  long tile = blockIdx.x;
+  if (compute) load_x(tile);
   __syncthreads();   // sB1, sB2, sGB visible
   const float inv_c = 1.0f / (float)a.C;
 
   for (; tile < a.nTiles; tile += gridDim.x) {
     const long row0 = tile * TOK;
-    load_x(tile);   // no cross-tile prefetch: the second workgroup on the CU hides this latency
-    load_w1();
-    // ---- LayerNorm 2: 16 lanes per row, DPP sums -> sT (bf16, 1.0 in column C)
+    // ---- [compute] LayerNorm 2 (16 lanes per row, DPP sums) -> sT (bf16, 1.0 in column C); x -> sX
+    if (compute) {
 #pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const int i = 4 * p + g, r = w + NW * i;
-      const bool ok = i < RPW && r < TOK;
-      float sm = 0.f;
+      for (int p = 0; p < NPASS; ++p) {
+        const int i = 4 * p + g, r = w + NC * i;
+        const bool ok = i < RPW && r < TOK;
+        float sm = 0.f;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int cb = 4 * jl + 64 * k;
-        sm += (cb + 0 < a.C ? xv[p][k].x : 0.f) + (cb + 1 < a.C ? xv[p][k].y : 0.f) +
-              (cb + 2 < a.C ? xv[p][k].z : 0.f) + (cb + 3 < a.C ? xv[p][k].w : 0.f);
-      }
-      const float mu = dpp_sum16(sm) * inv_c;
-      float q = 0.f;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int cb = 4 * jl + 64 * k;
-        const float vv[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float d = cb + j < a.C ? vv[j] - mu : 0.f;
-          q += d * d;
+        for (int k = 0; k < 3; ++k) {
+          const int cb = 4 * jl + 64 * k;
+          sm += (cb + 0 < a.C ? xv[p][k].x : 0.f) + (cb + 1 < a.C ? xv[p][k].y : 0.f) +
+                (cb + 2 < a.C ? xv[p][k].z : 0.f) + (cb + 3 < a.C ? xv[p][k].w : 0.f);
         }
-      }
-      const float rs = rsqrtf(dpp_sum16(q) * inv_c + a.eps);
-      if (ok) {
+        const float mu = dpp_sum16(sm) * inv_c;
+        float q = 0.f;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           const int cb = 4 * jl + 64 * k;
           const float vv[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
-          bf16x4 o;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int cc = cb + j;
-            o[j] = (bf16)(cc < a.C ? (vv[j] - mu) * rs * sGB[0][cc] + sGB[1][cc] : (cc == a.C ? 1.f : 0.f));
+            const float d = cb + j < a.C ? vv[j] - mu : 0.f;
+            q += d * d;
           }
-          *(bf16x4*)(sT + r * LDT + cb) = o;
         }
-        if (jl == 0) {
-          sMean[r] = mu;
-          sRstd[r] = rs;
+        const float rs = rsqrtf(dpp_sum16(q) * inv_c + a.eps);
+        if (ok) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const int cb = 4 * jl + 64 * k;
+            const float vv[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
+            bf16x4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int cc = cb + j;
+              o[j] = (bf16)(cc < a.C ? (vv[j] - mu) * rs * sGB[0][cc] + sGB[1][cc] : (cc == a.C ? 1.f : 0.f));
+            }
+            *(bf16x4*)(sT + r * LDT + cb) = o;
+            *(float4*)(sX + r * LDX + cb) = xv[p][k];
+          }
+          if (jl == 0) {
+            sMean[r] = mu;
+            sRstd[r] = rs;
+          }
         }
       }
     }
-    __syncthreads();   // LN tile visible
-
-    // ---- fc1: U^T tiles (hidden columns x token rows)
-    f32x16 U[2][2];
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) U[ct][rt][r] = 0.f;
-#pragma unroll 1
-    for (int kb0 = 0; kb0 < ((a.dbg & 1) ? 0 : KB1); kb0 += PF1) {
-#pragma unroll
-      for (int sl = 0; sl < PF1; ++sl) {
-        const int kb = kb0 + sl;
-        bf16x8 fw[2][S];
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int e = 0; e < S; ++e) {
-            fw[ct][e] = p1[sl][ct][e];
-            if (kb + PF1 < KB1) p1[sl][ct][e] = *(const bf16x8*)(w1p + (long)ct * KB1 * WS + (kb + PF1) * WS + e * 512);
-          }
-        bf16x8 fl[2];
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) fl[rt] = *(const bf16x8*)(sT + (rt * 32 + l31) * LDT + kb * 16 + 8 * hh);
-#pragma unroll
-        for (int e = 0; e < S; ++e)
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-              U[ct][rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[ct][e], fl[rt], U[ct][rt], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < PF2; ++i)
-#pragma unroll
-      for (int e = 0; e < S; ++e) p2[i][e] = *(const bf16x8*)(w2p + i * WS + e * 512);
-    // u = acc + b1 -> sH (bf16): lane row rt*32 + l31, columns 64w + 32ct + 8gg + 4hh + e
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        const int col = 64 * w + 32 * ct + 8 * gg + 4 * hh;
-        const float4 bb = *(const float4*)(sB1 + col);
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          const f32x16& acc = U[ct][rt];
-          *(bf16x4*)(sH + (rt * 32 + l31) * LDH + col) =
-              bf16x4{(bf16)(acc[4 * gg] + bb.x), (bf16)(acc[4 * gg + 1] + bb.y), (bf16)(acc[4 * gg + 2] + bb.z),
-                     (bf16)(acc[4 * gg + 3] + bb.w)};
-        }
-      }
-    // LN2 rows and statistics out (sT is read-only from here on)
-    {
+    __syncthreads();   // (1) LN tile and x rows visible; the previous tile's output rows are stored
+    if (!compute && !(a.dbg & 4)) {   // ---- [store] LN2 rows and statistics
       constexpr int CH = CP / 8;
-      for (int i = tid; i < TOK * CH; i += 64 * NW) {
+      for (int i = sid; i < TOK * CH; i += NST) {
         const int r = i / CH, q = (i - (i / CH) * CH) * 8;
         *(uint4*)(a.ln + (row0 + r) * a.ldln + q) = *(const uint4*)(sT + r * LDT + q);
       }
-      if (tid < TOK) {
-        a.mean[row0 + tid] = sMean[tid];
-        a.rstd[row0 + tid] = sRstd[tid];
+      if (sid < TOK) {
+        a.mean[row0 + sid] = sMean[sid];
+        a.rstd[row0 + sid] = sRstd[sid];
       }
     }
-    __syncthreads();   // u tile complete
-    // u out, h = GELU(u) (1.0 at column hd) -> sH and out; 16 bytes per lane
-    {
-      constexpr int CH = HP / 8;
-      for (int i = tid; i < ((a.dbg & 4) ? 0 : TOK * CH); i += 64 * NW) {
-        const int r = i / CH, q = (i - (i / CH) * CH) * 8;
-        bf16* ps = sH + r * LDH + q;
-        const bf16x8 uv = *(const bf16x8*)ps;
-        bf16x8 hv, gv;
+    f32x16 O2;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int cc = q + j;
-          float y, dy;
-          gelu_pair_fast((float)uv[j], y, dy);
-          hv[j] = cc < a.hd ? (bf16)y : (bf16)(cc == a.hd ? 1.f : 0.f);
-          gv[j] = (bf16)dy;
-        }
-        *(bf16x8*)ps = hv;
-        *(bf16x8*)(a.u + (row0 + r) * a.ldh + q) = gv;
-        *(bf16x8*)(a.hact + (row0 + r) * a.ldh + q) = hv;
-      }
-    }
-    __syncthreads();   // h tile complete
-
-    // ---- fc2: out^T tile (output columns 32w.. x token rows)
-    f32x16 O2[2];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) O2[rt][r] = 0.f;
+    for (int r = 0; r < 16; ++r) O2[r] = 0.f;
 #pragma unroll 1
-    for (int kb0 = 0; kb0 < ((a.dbg & 2) ? 0 : KB2); kb0 += PF2) {
+    for (int half = 0; half < 2; ++half) {
+      if (compute) {
+        // ---- [compute] fc1, hidden columns 192 half + 32 ct.., rows 32 rt..
+        const bf16* w1p = a.w1 + (long)(6 * half + ct) * KB1 * WS + lane * 8;
+        bf16x8 pw[PF][S];
 #pragma unroll
-      for (int sl = 0; sl < PF2; ++sl) {
-        const int kb = kb0 + sl;
-        bf16x8 fw[S];
+        for (int i = 0; i < PF; ++i)
 #pragma unroll
-        for (int e = 0; e < S; ++e) {
-          fw[e] = p2[sl][e];
-          if (kb + PF2 < KB2) p2[sl][e] = *(const bf16x8*)(w2p + (kb + PF2) * WS + e * 512);
+          for (int e = 0; e < S; ++e) pw[i][e] = *(const bf16x8*)(w1p + i * WS + e * 512);
+        f32x16 U;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) U[r] = 0.f;
+#pragma unroll 1
+        for (int kb0 = 0; kb0 < ((a.dbg & 1) ? 0 : KB1); kb0 += PF) {
+#pragma unroll
+          for (int sl = 0; sl < PF; ++sl) {
+            const int kb = kb0 + sl;
+            bf16x8 fw[S];
+#pragma unroll
+            for (int e = 0; e < S; ++e) {
+              fw[e] = pw[sl][e];
+              if (kb + PF < KB1) pw[sl][e] = *(const bf16x8*)(w1p + (kb + PF) * WS + e * 512);
+            }
+            const bf16x8 fl = *(const bf16x8*)(sT + (rt * 32 + l31) * LDT + kb * 16 + 8 * hh);
+#pragma unroll
+            for (int e = 0; e < S; ++e) U = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[e], fl, U, 0, 0, 0);
+          }
         }
-        bf16x8 fh[2];
+        // pre-activation x = acc + b1 (fp32) -> h = GELU(x) -> sU, g = GELU'(x) -> sG (bf16): lane row
+        // 32 rt + l31, half-local columns 32 ct + 8 gg + 4 hh + e; h is 1.0 at column hd, 0 past it
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt) fh[rt] = *(const bf16x8*)(sH + (rt * 32 + l31) * LDH + kb * 16 + 8 * hh);
+        for (int gg = 0; gg < 4; ++gg) {
+          const int col = 32 * ct + 8 * gg + 4 * hh;
+          const float4 bb = *(const float4*)(sB1 + HH * half + col);
+          const float xs[4] = {U[4 * gg] + bb.x, U[4 * gg + 1] + bb.y, U[4 * gg + 2] + bb.z, U[4 * gg + 3] + bb.w};
+          bf16x4 hv, gv;
 #pragma unroll
-        for (int e = 0; e < S; ++e)
-#pragma unroll
-          for (int rt = 0; rt < 2; ++rt) O2[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[e], fh[rt], O2[rt], 0, 0, 0);
+          for (int e = 0; e < 4; ++e) {
+            const int cc = HH * half + col + e;
+            float y, dy;
+            gelu_pair_fast(xs[e], y, dy);
+            hv[e] = cc < a.hd ? (bf16)y : (bf16)(cc == a.hd ? 1.f : 0.f);
+            gv[e] = (bf16)dy;
+          }
+          *(bf16x4*)(sU + (rt * 32 + l31) * LDU + col) = hv;
+          *(bf16x4*)(sG + (rt * 32 + l31) * LDU + col) = gv;
+        }
       }
-    }
-    __syncthreads();   // every wave is done reading the h tile
+      __syncthreads();   // (3) h and g halves complete
+      if (!compute) {
+        if (!(a.dbg & 4)) {   // ---- [store] g and h of this half
+          constexpr int CH = HH / 8;
+          for (int i = sid; i < TOK * CH; i += NST) {
+            const int r = i / CH, q = (i - (i / CH) * CH) * 8;
+            *(uint4*)(a.u + (row0 + r) * a.ldh + HH * half + q) = *(const uint4*)(sG + r * LDU + q);
+            *(uint4*)(a.hact + (row0 + r) * a.ldh + HH * half + q) = *(const uint4*)(sU + r * LDU + q);
+          }
+        }
+      } else {
+        if (half == 1) load_x(tile + gridDim.x);   // the next tile's rows (nothing to wait behind)
+        // ---- [compute] fc2 partial over this half's 192 hidden rows
+        const bf16* w2p = a.w2 + ((long)ct * KB2 + KBH * half) * WS + lane * 8;
+        bf16x8 pw[PF][S];
 #pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      const int col = 32 * w + 8 * gg + 4 * hh;
-      const float4 bb = *(const float4*)(sB2 + col);
+        for (int i = 0; i < PF; ++i)
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const f32x16& acc = O2[rt];
-        *(float4*)(sOut + (rt * 32 + l31) * LDO + col) =
-            make_float4(acc[4 * gg] + bb.x, acc[4 * gg + 1] + bb.y, acc[4 * gg + 2] + bb.z, acc[4 * gg + 3] + bb.w);
+          for (int e = 0; e < S; ++e) pw[i][e] = *(const bf16x8*)(w2p + i * WS + e * 512);
+#pragma unroll 1
+        for (int kb0 = 0; kb0 < ((a.dbg & 2) ? 0 : KBH); kb0 += PF) {
+#pragma unroll
+          for (int sl = 0; sl < PF; ++sl) {
+            const int kb = kb0 + sl;
+            bf16x8 fw[S];
+#pragma unroll
+            for (int e = 0; e < S; ++e) {
+              fw[e] = pw[sl][e];
+              if (kb + PF < KBH) pw[sl][e] = *(const bf16x8*)(w2p + (kb + PF) * WS + e * 512);
+            }
+            const bf16x8 fh = *(const bf16x8*)(sU + (rt * 32 + l31) * LDU + kb * 16 + 8 * hh);
+#pragma unroll
+            for (int e = 0; e < S; ++e) O2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[e], fh, O2, 0, 0, 0);
+          }
+        }
       }
+      __syncthreads();   // (4) the h / g halves are no longer read (fc2, the stores)
     }
-    __syncthreads();   // output tile complete
-    {
+    if (compute) {   // ---- [compute] out = x + s * (fc2 + b2), in place in sX
       const float rs = a.rowscale ? a.rowscale[tile / a.tiles_per_scale] : 1.f;
-      constexpr int C4 = CP / 4, PER = TOK * C4 / (64 * NW), HALF = PER / 2;
-      static_assert(TOK * C4 % (64 * NW) == 0 && PER % 2 == 0, "output pass");
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        float4 xr[HALF];
-#pragma unroll
-        for (int k = 0; k < HALF; ++k) {
-          const int i = tid + (hf * HALF + k) * 64 * NW, r = i / C4, q = (i - (i / C4) * C4) * 4;
-          xr[k] = *(const float4*)(a.x + (row0 + r) * a.ldx + q);
-        }
-#pragma unroll
-        for (int k = 0; k < HALF; ++k) {
-          const int i = tid + (hf * HALF + k) * 64 * NW, r = i / C4, q = (i - (i / C4) * C4) * 4;
-          const float4 v = *(const float4*)(sOut + r * LDO + q);
-          *(float4*)(a.out + (row0 + r) * a.ldout + q) =
-              make_float4(xr[k].x + rs * v.x, xr[k].y + rs * v.y, xr[k].z + rs * v.z, xr[k].w + rs * v.w);
-        }
+      for (int gg = 0; gg < 4; ++gg) {
+        const int col = 32 * ct + 8 * gg + 4 * hh;
+        const float4 bb = *(const float4*)(sB2 + col);
+        float* px = sX + (rt * 32 + l31) * LDX + col;
+        const float4 xr = *(const float4*)px;
+        *(float4*)px = make_float4(xr.x + rs * (O2[4 * gg] + bb.x), xr.y + rs * (O2[4 * gg + 1] + bb.y),
+                                   xr.z + rs * (O2[4 * gg + 2] + bb.z), xr.w + rs * (O2[4 * gg + 3] + bb.w));
       }
     }
-    // next iteration: its first LDS writes (sT, sMean) follow reads that precede the barriers above;
-    // its u writes to sH follow its own LN barrier, after every wave has left this output pass
+    __syncthreads();   // (5) output rows complete
+    if (!compute && !(a.dbg & 4)) {   // ---- [store] output rows (the next LN waits at barrier 1... via (6))
+      constexpr int C4 = CP / 4;
+      for (int i = sid; i < TOK * C4; i += NST) {
+        const int r = i / C4, q = (i - (i / C4) * C4) * 4;
+        *(float4*)(a.out + (row0 + r) * a.ldout + q) = *(const float4*)(sX + r * LDX + q);
+      }
+    }
+    __syncthreads();   // (6) sX / sT free for the next tile
   }
 }
 
@@ -752,6 +725,8 @@ extern "C" int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, 
   a.out = out; a.ldout = ldout;
   a.nWin = nWin; a.H = H; a.W = W; a.shift = shift;
   a.wm = make_winmap(H, W, WSZ, shift);
+  static const int dbg = getenv("KAIR_ATTN_DBG") ? atoi(getenv("KAIR_ATTN_DBG")) : 0;
+  a.dbg = dbg;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       ncu <= 0)
@@ -793,11 +768,11 @@ extern "C" int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, c
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       ncu <= 0)
     ncu = 256;
-  const long grid = a.nTiles < 2L * ncu ? a.nTiles : 2L * ncu;   // persistent: two workgroups per CU
+  const long grid = a.nTiles < ncu ? a.nTiles : ncu;   // persistent: one 16-wave workgroup per CU
   if (w_split)
-    hipLaunchKernelGGL(swin_mlp_fwd_kernel<2>, dim3((unsigned)grid), dim3(384), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(swin_mlp_fwd_kernel<2>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(swin_mlp_fwd_kernel<1>, dim3((unsigned)grid), dim3(384), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(swin_mlp_fwd_kernel<1>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

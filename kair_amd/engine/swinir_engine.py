@@ -181,10 +181,9 @@ class SwinIREngine:
         Hd = net.layers[0].residual_group.blocks[0].mlp.fc1.out_features
         self.Hdp = _rup(Hd + 1, 32)
         import os
-        # the fused MLP half is off by default: 146-168 us per block at B=32 against 162 us for the
-        # LN2 / fc1 / fc2 launches; KAIR_FUSED_MLP=1 turns it on (A/B timing)
+        # KAIR_FUSED_MLP=0: the LN2 / fc1 / fc2 launches instead of the fused MLP half (A/B timing)
         if fused_mlp is None:
-            fused_mlp = fused_blocks and os.environ.get("KAIR_FUSED_MLP", "0") == "1"
+            fused_mlp = fused_blocks and os.environ.get("KAIR_FUSED_MLP", "1") == "1"
         self.fused_mlp = bool(fused_mlp) and compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384
         # split linears measured: the PSNR effect of bf16 linear-weight rounding is ~1e-4 dB against
         # ~5e-4 dB of activation-rounding noise per image (tools/parity_seeds.py, DESIGN.md "parity at
