@@ -34,32 +34,7 @@ def build_net(dtype, drop_path=0.1, seed=0):
                   drop_path_rate=drop_path, compute_dtype=dtype)
 
 
-def time_dominant_kernel(engine, reps=30):
-    """HIP-event timing (torch's current stream = the stream the kernels launch on) of the fused
-    Swin attention-half kernel of block 0 (kair_swin_attn_fwd: LN1 + QKV + window attention + proj +
-    residual, network_swinir.py:239-272 / 114-145) at the step's exact arguments -- with the
-    attention backward, the largest single share of the step (profiles/r02_bench_kernel_stats.csv).
-
-    Algorithmic bytes per 64-token window (unpadded C = 180): x in (fp32) and mid out
-    (fp32) 2 x 46080, the saved LN1 / O (bf16) 2 x 23040, q/k/v (bf16) 69120, lse 1536, mean/rstd
-    512 = 209408 B, plus the two weight matrices once per launch.  Algorithmic FLOPs per window:
-    qkv 12.44 M + q.k^T and p.v 2.95 M + proj 4.15 M = 19.54 MFLOP.  The kernel sits at ~135
-    FLOP/B (ridge 312), so the byte roofline is the binding one."""
-    from kair_amd import _hip as H
-    P = engine.cur
-    blk, S = engine.blocks[0], P["blocks"][0]
-    nh, Cp, C = engine.nh, engine.Cp, engine.C
-    M, Hh, Ww = P["M"], P["H"], P["W"]
-    nWin = P["nWin"]
-    x = P["s0"]
-    if not engine.fused_attn:
-        raise RuntimeError("bench roofline: the fused attention kernel is not in use")
-
-    def launch():
-        H.swin_attn_fwd(x, Cp, blk.n1.weight, blk.n1.bias, blk.n1.eps, C, S["ln1"], Cp, S["m1"], S["r1"],
-                        blk.qkv.Wg, blk.qkv.bp, S["qkv"], blk.table, blk.scale, S["O"], nh * 32, C // nh, S["lse"],
-                        blk.proj.Wg, blk.proj.bp, None, Hh * Ww, S["mid"], Cp, nWin, nh, Hh, Ww, blk.shift,
-                        w_split=blk.qkv.split)
+def _time(launch, reps):
     for _ in range(3):
         launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,15 +44,60 @@ def time_dominant_kernel(engine, reps=30):
         launch()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    return e0.elapsed_time(e1) / reps
+
+
+def time_fused_kernels(engine, reps=30):
+    """HIP-event timing (torch's current stream = the stream the kernels launch on) of the two fused
+    Swin-block kernels of block 0 at the step's exact arguments -- the two largest shares of the step
+    (profiles/r02_step_breakdown_b32.txt):
+
+      mlp:  kair_swin_mlp_fwd  (LN2 + fc1 + GELU + fc2 + residual, network_swinir.py:274-276, 24-30)
+      attn: kair_swin_attn_fwd (LN1 + QKV + window attention + proj + residual, :239-272, 114-145)
+
+    Algorithmic bytes / FLOPs (unpadded C = 180, hidden 360, 64-token units):
+      mlp  per 64 rows: x in + out (fp32) 2 x 46080, ln2 23040, g = GELU'(u) and h (bf16) 2 x 46080,
+           mean/rstd 512 = 207872 B; 2 x 2 x 64 x 180 x 360 = 16.59 MFLOP
+      attn per window: x in + mid out (fp32) 2 x 46080, ln1 / O 2 x 23040, q/k/v 69120, lse 1536,
+           mean/rstd 512 = 209408 B; qkv 12.44 + q.k^T / p.v 2.95 + proj 4.15 = 19.54 MFLOP
+    plus each kernel's weights once per launch.  Both sit near 80-135 FLOP/B, below the 312 FLOP/B
+    ridge, so the byte roofline binds."""
+    from kair_amd import _hip as H
+    P = engine.cur
+    blk, S = engine.blocks[0], P["blocks"][0]
+    nh, Cp, C = engine.nh, engine.Cp, engine.C
+    M, Hh, Ww = P["M"], P["H"], P["W"]
+    nWin = P["nWin"]
+    if not (engine.fused_attn and engine.fused_mlp):
+        raise RuntimeError("bench roofline: the fused block kernels are not in use")
     T = 64
-    per_win = 2 * T * C * 4 + 2 * T * C * 2 + 3 * T * C * 2 + nh * T * 4 + T * 8
-    nbytes = nWin * per_win + 2 * (3 * C * C + C * C)
-    flops = nWin * (2 * T * C * 3 * C + 2 * 2 * T * T * C + 2 * T * C * C)
-    return {"kernel": "swin_attn_fwd_kernel<6,1> (fused LN1+QKV+window attention+proj+residual, "
-                      "network_swinir.py:239-272; rocprof name swin_attn_fwd_kernel<6, 1>)",
-            "rocprof_key": "swin_attn_fwd_kernel<6, 1>",
-            "ms": ms, "flops": flops, "bytes": nbytes, "windows": nWin, "bytes_per_window": per_win}
+    out = {}
+
+    def attn():
+        H.swin_attn_fwd(P["s0"], Cp, blk.n1.weight, blk.n1.bias, blk.n1.eps, C, S["ln1"], Cp, S["m1"], S["r1"],
+                        blk.qkv.Wg, blk.qkv.bp, S["qkv"], blk.table, blk.scale, S["O"], nh * 32, C // nh, S["lse"],
+                        blk.proj.Wg, blk.proj.bp, None, Hh * Ww, S["mid"], Cp, nWin, nh, Hh, Ww, blk.shift,
+                        w_split=blk.qkv.split)
+    per = 2 * T * C * 4 + 2 * T * C * 2 + 3 * T * C * 2 + nh * T * 4 + T * 8
+    out["attn"] = {"kernel": "swin_attn_fwd_kernel<6,1> (fused LN1+QKV+window attention+proj+residual, "
+                             "network_swinir.py:239-272)", "rocprof_key": "swin_attn_fwd_kernel<6, 1>",
+                   "ms": _time(attn, reps), "units": nWin, "bytes_per_unit": per,
+                   "bytes": nWin * per + 2 * (3 * C * C + C * C),
+                   "flops": nWin * (2 * T * C * 3 * C + 2 * 2 * T * T * C + 2 * T * C * C)}
+    f1, f2 = blk.fc1, blk.fc2
+    Hd = f1.N
+
+    def mlp():
+        H.swin_mlp_fwd(S["mid"], Cp, blk.n2.weight, blk.n2.bias, blk.n2.eps, C, S["ln2"], Cp, S["m2"], S["r2"],
+                       f1.Wg, f1.bp, S["u"], S["h"], engine.Hdp, Hd, f2.Wg, f2.bp, None, Hh * Ww, S["out"], Cp, M, Cp,
+                       engine.Hdp, w_split=f1.split)
+    tiles = M // T
+    per = 2 * T * C * 4 + T * C * 2 + 2 * T * Hd * 2 + T * 8
+    out["mlp"] = {"kernel": "swin_mlp_fwd_kernel<1> (fused LN2+fc1+GELU+fc2+residual, network_swinir.py:274-276, "
+                            "24-30)", "rocprof_key": "swin_mlp_fwd_kernel<1>",
+                  "ms": _time(mlp, reps), "units": tiles, "bytes_per_unit": per,
+                  "bytes": tiles * per + 2 * 2 * C * Hd, "flops": tiles * 2 * 2 * T * C * Hd}
+    return out
 
 
 def pmc_traffic(key):
@@ -203,6 +223,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--drop-path", type=float, default=0.1)
     ap.add_argument("--no-fp32-line", action="store_true", help="skip the fp32 parity-config throughput line")
+    ap.add_argument("--data", default="pool", choices=["pool", "static"],
+                    help="pool: every step synthesises a fresh batch on the GPU from an HBM-resident HR pool "
+                         "(kair_synth_sr: crop + 8-way augment + MATLAB bicubic x1/4, DatasetSR semantics) inside "
+                         "the timed loop; static: one staged batch reused")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -234,10 +258,17 @@ def main():
         for t in list(net.state_dict().values()) + list(ema.state_dict().values()):
             dist.broadcast(t, 0)
     tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999, use_graph=not args.no_graph)
-    L, Hh = synth_sr_batch(bpg, 48, 4, seed=1000 + rank, device=device)
+    if args.data == "pool":
+        from kair_amd.data.gpu_synth import PatchSynth, synthetic_pool
+        pool = synthetic_pool(64, 3, 256, 256, seed=99, device=device)
+        synth = PatchSynth(pool, task="sr", scale=4, H_size=192, seed=1000, rank=rank, world=world)
+        batch = lambda: synth.next(bpg)
+    else:
+        L, Hh = synth_sr_batch(bpg, 48, 4, seed=1000 + rank, device=device)
+        batch = lambda: (L, Hh)
 
     for _ in range(args.warmup):
-        loss = tr.step(L, Hh)
+        loss = tr.step(*batch())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -246,7 +277,7 @@ def main():
     t0 = time.perf_counter()
     e0.record()
     for _ in range(args.steps):
-        loss = tr.step(L, Hh)
+        loss = tr.step(*batch())
     e1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -270,24 +301,33 @@ def main():
     ms_step = 1000.0 * wall / args.steps
     step_tflops = fl["train"] * gbatch / (wall / args.steps) / 1e12 / world   # per GPU
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
-    k = time_dominant_kernel(tr.engine)
-    ach_gbs = k["bytes"] / (k["ms"] * 1e-3) / 1e9
-    ach_tf = k["flops"] / (k["ms"] * 1e-3) / 1e12
+    try:
+        ks = time_fused_kernels(tr.engine)
+    except RuntimeError as e:   # fp32 engine: no fused block kernels
+        ks = {"err": repr(e)}
+
+    def roof(k):
+        ach_gbs = k["bytes"] / (k["ms"] * 1e-3) / 1e9
+        ach_tf = k["flops"] / (k["ms"] * 1e-3) / 1e12
+        return {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(ach_gbs / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(k["rocprof_key"]),
+                "kernel": k["kernel"], "kernel_ms": round(k["ms"], 5), "bytes_per_launch": k["bytes"],
+                "units_per_launch": k["units"], "bytes_per_unit": k["bytes_per_unit"],
+                "flops_per_launch": k["flops"], "achieved_tflops": round(ach_tf, 2), "mfma_frac": round(ach_tf / peak, 4)}
     out = {
         "metric": "train patches/sec + PSNR, SwinIR x4 48-px LQ, at 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
-        "dtype": args.dtype, "data": "synthetic (seeded bicubic-LR / HR patches resident in HBM, SURVEY §8d)",
+        "dtype": args.dtype,
+        "data": ("synthetic: per step a fresh batch synthesised on the GPU (crop / augment / MATLAB bicubic) from "
+                 "a 64-image 256x256 HR pool resident in HBM (SURVEY §8d recipe)" if args.data == "pool" else
+                 "synthetic (one seeded bicubic-LR / HR batch resident in HBM, SURVEY §8d)"),
         "config": {"workload": "SwinIR classical x4 SR train step (fwd+L1+bwd+allreduce+Adam+EMA), 48-px LQ",
                    "global_batch": gbatch, "per_gpu_batch": bpg, "lq": 48, "hr": 192, "embed_dim": 180,
                    "depths": [6] * 6, "heads": 6, "window": 8, "drop_path_rate": args.drop_path,
                    "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
-        "roofline": {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(ach_gbs / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(k["rocprof_key"]),
-                     "kernel": k["kernel"], "kernel_ms": round(k["ms"], 5), "bytes_per_launch": k["bytes"],
-                     "flops_per_launch": k["flops"], "achieved_tflops": round(ach_tf, 2),
-                     "mfma_frac": round(ach_tf / peak, 4), "windows": k["windows"],
-                     "bytes_per_window": k["bytes_per_window"]},
+        "roofline": roof(ks["mlp"]) if "mlp" in ks else {"error": ks["err"]},
+        "roofline_attention": roof(ks["attn"]) if "attn" in ks else None,
         "step_roofline": {"train_flop_per_patch": fl["train"], "achieved_tflops_per_gpu": round(step_tflops, 2),
                           "frac_of_bf16_peak": round(step_tflops / peak, 4)},
         "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),

@@ -48,6 +48,7 @@ class PatchSynth:
         elif task != "dn":
             raise ValueError(task)
         self._par_host = None
+        self._par_ev = None
 
     def _next_index(self):
         if self.pos >= len(self.order):
@@ -74,8 +75,20 @@ class PatchSynth:
         return torch.tensor(rows, dtype=torch.int32)
 
     def next(self, B, out=None):
-        par = self.draw(B).to(self.pool.device, non_blocking=False)
+        """The next batch (L, H), produced on the current stream.  The per-sample geometry goes up
+        through a pinned staging buffer with an async copy, so a training loop that calls next()
+        every step never blocks the host on the device."""
         dev = self.pool.device
+        host = self.draw(B)
+        if self._par_host is None or self._par_host.shape[0] < B:
+            self._par_host = torch.empty(B, 4, dtype=torch.int32).pin_memory()
+            self._par_ev = None
+        if self._par_ev is not None:
+            self._par_ev.synchronize()   # the previous batch's copy has read the staging buffer
+        self._par_host[:B].copy_(host)
+        par = self._par_host[:B].to(dev, non_blocking=True)
+        self._par_ev = torch.cuda.Event()
+        self._par_ev.record()
         ls = self.PS // self.sf
         if out is None:
             Hp = torch.empty(B, self.C, self.PS, self.PS, device=dev)

@@ -1,0 +1,9 @@
+#!/bin/bash
+# data tests, bench (GPU-synthesised batches) at B=32 / B=4, then the PMC traffic passes
+set -o pipefail
+R=$(pwd); mkdir -p $R/gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_data_gpu.py -x -q --timeout 240 --timeout-method thread > $R/gpurun_out/t_data.log 2>&1 || { tail -30 $R/gpurun_out/t_data.log; exit 1; }
+tail -1 $R/gpurun_out/t_data.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/gpurun_out/q32.log 2>&1 || { echo "b32 failed"; tail -5 $R/gpurun_out/q32.log; exit 1; }
+timeout -k 10 300 python bench.py --global-batch 4 --steps 30 --warmup 5 --no-cpu-baseline --no-fp32-line > $R/gpurun_out/q4.log 2>&1 || { echo "b4 failed"; exit 1; }
+bash tools/gpu_pmc.sh
