@@ -75,8 +75,12 @@ typedef enum {
                              -> out[(b,y,x) of ps_H x ps_W][c*r*r+i*r+j], stride ldo          */
   KAIR_OUT_NCHW = 4,      /* image out[b][n][y][x] (n < img_C) of [img_H, img_W],
                              value = v / img_range + img_mean[n]                              */
-  KAIR_OUT_PSHUF_NCHW = 5 /* PixelShuffle(r) straight into an NCHW image [b][c][y*r+i][x*r+j]
+  KAIR_OUT_PSHUF_NCHW = 5, /* PixelShuffle(r) straight into an NCHW image [b][c][y*r+i][x*r+j]
                              (c < img_C), value = v / img_range + img_mean[c]  (UpsampleOneStep) */
+  KAIR_OUT_PSHUF_SPM = 6, /* as PSHUF with the GEMM columns sub-pixel-major, n = (i*r+j)*(N/r^2) + c
+                             (weights packed with kair_wmap.n_perm = r^2): 8 consecutive columns
+                             are 8 consecutive channels of one output pixel -> 16-byte stores      */
+  KAIR_OUT_PUNSHUF_SPM = 7 /* inverse of PSHUF_SPM: out[(b,y,x)][(i*r+j)*ldc + c], ldc = ps_C       */
 } kair_out_mode;
 
 typedef enum { KAIR_ACT_NONE = 0, KAIR_ACT_GELU = 1, KAIR_ACT_LEAKY = 2, KAIR_ACT_RELU = 3 } kair_act;
@@ -138,6 +142,9 @@ typedef struct {
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
   int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp                   */
+  int n_perm;        /* > 1: the out dim is stored sub-pixel-major for a PixelShuffle(r), n_perm =
+                        r*r: packed (unpadded) row s*(N/r^2) + c holds reference row c*r^2 + s
+                        (KAIR_OUT_PSHUF_SPM / KAIR_OUT_PUNSHUF_SPM layouts); 0 or 1: identity     */
 } kair_wmap;
 
 /* dst (packed, dtype) <- src (reference fp32).  Pad entries written as 0. */

@@ -17,6 +17,7 @@ USR_SRC_NCHW, USR_SRC_PSF, USR_SRC_ZUP, USR_SRC_NHWC = 0, 1, 2, 3
 USR_COL_FB, USR_COL_FBFY, USR_COL_DATA_FWD, USR_COL_DATA_BWD = 0, 1, 2, 3
 USR_CHAN_CHUNKS = 64
 OUT_ROWS, OUT_QKVBLK, OUT_PSHUF, OUT_PUNSHUF, OUT_NCHW, OUT_PSHUF_NCHW = 0, 1, 2, 3, 4, 5
+OUT_PSHUF_SPM, OUT_PUNSHUF_SPM = 6, 7
 ACT_NONE, ACT_GELU, ACT_LEAKY, ACT_RELU = 0, 1, 2, 3
 
 c_long, c_int, c_float, c_vp = ctypes.c_long, ctypes.c_int, ctypes.c_float, ctypes.c_void_p
@@ -64,7 +65,7 @@ class Epilogue(ctypes.Structure):
 
 class WMap(ctypes.Structure):
     _fields_ = [("kind", c_int), ("N", c_int), ("K", c_int), ("nG", c_int), ("nGr", c_int), ("nGp", c_int),
-                ("kG", c_int), ("kGr", c_int), ("kGp", c_int)]
+                ("kG", c_int), ("kGr", c_int), ("kGp", c_int), ("n_perm", c_int)]
 
 
 class PackJob(ctypes.Structure):
@@ -126,6 +127,7 @@ _SIGS = {
                            c_int, c_int, c_int, c_int, c_vp],
     "kair_swin_mlp_fwd": [c_vp, c_long, c_vp, c_vp, c_float, c_int, c_vp, c_long, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                           c_long, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_long, c_int, c_int, c_int, c_vp],
+    "kair_debug_attn_stamps": [c_vp, c_int],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
@@ -285,10 +287,12 @@ def epilogue(out, mode=OUT_ROWS, ldo=None, win=None, bias=None, act=ACT_NONE, sl
     return e
 
 
-def wmap(kind, N, K, n_groups=(1, None, None), k_groups=(1, None, None)):
-    """n_groups = (G, real, padded) for the out dim; k_groups likewise for the in dim."""
+def wmap(kind, N, K, n_groups=(1, None, None), k_groups=(1, None, None), n_perm=0):
+    """n_groups = (G, real, padded) for the out dim; k_groups likewise for the in dim; n_perm = r*r
+    stores the out dim sub-pixel-major (PixelShuffle SPM layouts)."""
     m = WMap()
     m.kind, m.N, m.K = kind, N, K
+    m.n_perm = n_perm
     nG, nr, npd = n_groups
     kG, kr, kpd = k_groups
     m.nG, m.nGr, m.nGp = nG, nr or N // nG, npd or nr or N // nG
@@ -516,3 +520,10 @@ def swin_mlp_fwd(x, ldx, gamma, beta, eps, C, ln, ldln, mean, rstd, w1, b1, u, h
     check(lib().kair_swin_mlp_fwd(ptr(x), ldx, ptr(gamma), ptr(beta), eps, C, ptr(ln), ldln, ptr(mean), ptr(rstd),
                                   ptr(w1), ptr(b1), ptr(u), ptr(h), ldh, hd, ptr(w2), ptr(b2), ptr(rowscale),
                                   rows_per_scale, ptr(out), ldout, M, Cp, Hp, int(w_split), stream_ptr()), "swin_mlp_fwd")
+
+
+def debug_attn_stamps(n=8192 * 8):
+    """Phase stamps of the last bf16 attention backward run with KAIR_ATTN_STAMP=1 (perf only)."""
+    buf = (ctypes.c_ulonglong * n)()
+    check(lib().kair_debug_attn_stamps(ctypes.cast(buf, c_vp), n), "debug_attn_stamps")
+    return list(buf)

@@ -15,6 +15,18 @@ KAIR_DEV int unpad(int ip, int G, int Gr, int Gp) {
   return (g < G && i < Gr) ? g * Gr + i : -1;
 }
 
+// kair_wmap.n_perm: the out dim stored sub-pixel-major (packed s*nf + c <-> reference c*r2 + s)
+KAIR_DEV int nperm_fwd(const kair_wmap& mp, int n) {   // packed (unpadded) -> reference
+  if (mp.n_perm <= 1 || n < 0) return n;
+  const int nf = mp.N / mp.n_perm;
+  return (n % nf) * mp.n_perm + n / nf;
+}
+KAIR_DEV int nperm_inv(const kair_wmap& mp, int co) {  // reference -> packed (unpadded)
+  if (mp.n_perm <= 1) return co;
+  const int nf = mp.N / mp.n_perm;
+  return (co % mp.n_perm) * nf + co / mp.n_perm;
+}
+
 KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst, int dt, const kair_wmap& mp, long t) {
   const int Np = mp.nG * mp.nGp, Kp = mp.kG * mp.kGp;
   float v = 0.f;
@@ -22,25 +34,25 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     int np, kp;
     if (mp.kind == 0) { np = (int)(t / Kp); kp = (int)(t - (long)np * Kp); }
     else { kp = (int)(t / Np); np = (int)(t - (long)kp * Np); }
-    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
   } else if (mp.kind == 1) {  // conv [Cop][9*Cip], k = tap*Cip + ci
     const int np = (int)(t / (9 * Kp));
     const int kk = (int)(t - (long)np * 9 * Kp);
     const int tap = kk / Kp, cip = kk - tap * Kp;
-    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
   } else if (mp.kind == 2) {  // conv dgrad form [Cip][9*Cop], k = tap*Cop + co (loader negates taps)
     const int cip = (int)(t / (9 * Np));
     const int kk = (int)(t - (long)cip * 9 * Np);
     const int tap = kk / Np, cop = kk - tap * Np;
-    const int n = unpad(cop, mp.nG, mp.nGr, mp.nGp), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
+    const int n = nperm_fwd(mp, unpad(cop, mp.nG, mp.nGr, mp.nGp)), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
   } else if (mp.kind == 7) {  // conv2x2 [Np][4*Kp], k = tap*Kp + kp (stride-2 conv fwd / transposed-conv dgrad)
     const int np = (int)(t / (4 * Kp));
     const int kk = (int)(t - (long)np * 4 * Kp);
     const int tap = kk / Kp, kp = kk - tap * Kp;
-    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && k >= 0) v = src[((long)n * mp.K + k) * 4 + tap];
   } else if (mp.kind == 9) {  // conv3x3 forward, hi/lo split: [Cop][KS], 64-col chunks alternate hi / lo
     const int Kc = 9 * Kp, KS = 2 * ((Kc + 63) / 64) * 64;
@@ -49,7 +61,7 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const int half = (kk >> 6) & 1, k = ((kk >> 7) << 6) + (kk & 63);
     if (k < Kc) {
       const int tap = k / Kp, cip = k - tap * Kp;
-      const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
+      const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
       if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
     }
     const bf16 hi = (bf16)v;
@@ -61,7 +73,7 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const long blk = t >> 9;
     const int kb = (int)(blk % KB), nb = (int)(blk / KB);
     const int np = nb * 32 + (ln & 31), kp = kb * 16 + 8 * (ln >> 5) + j;
-    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
   } else if (mp.kind == 12) {  // linear, fragment order with hi/lo halves: [Np/32][Kp/16][2][64 lanes][8]
     const int KB = Kp / 16;
@@ -69,7 +81,7 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const long blk = t >> 10;
     const int kb = (int)(blk % KB), nb = (int)(blk / KB);
     const int np = nb * 32 + (ln & 31), kp = kb * 16 + 8 * (ln >> 5) + j;
-    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
     const bf16 hi = (bf16)v;
     ((bf16*)dst)[t] = half ? (bf16)(v - (float)hi) : hi;
@@ -77,10 +89,10 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
   } else if (mp.kind == 8) {  // conv2x2 [4*Kp][Np], row = kp*4 + tap (pixel-shuffle forms)
     const int row = (int)(t / Np), np = (int)(t - (long)row * Np);
     const int kp = row >> 2, tap = row & 3;
-    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && k >= 0) v = src[((long)n * mp.K + k) * 4 + tap];
   } else {  // bias vector
-    const int n = unpad((int)t, mp.nG, mp.nGr, mp.nGp);
+    const int n = nperm_fwd(mp, unpad((int)t, mp.nG, mp.nGr, mp.nGp));
     if (n >= 0) v = src[n];
   }
   if (dt == KAIR_BF16) ((bf16*)dst)[t] = (bf16)v;
@@ -127,13 +139,14 @@ __global__ __launch_bounds__(1024) void wgrad_finalize_kernel(const float* __res
         const int co = (int)(t / ((long)mp.K * taps));
         const int rem = (int)(t - (long)co * mp.K * taps);
         const int ci = rem / taps, tap = rem - (rem / taps) * taps;
-        const int np = (co / mp.nGr) * mp.nGp + co % mp.nGr;
+        const int cq = nperm_inv(mp, co);
+        const int np = (cq / mp.nGr) * mp.nGp + cq % mp.nGr;
         const int cip = (ci / mp.kGr) * mp.kGp + ci % mp.kGr;
         const int Cip = mp.kG * mp.kGp;
         off = (long)np * Kt + (long)tap * Cip + cip;
       }
     } else {
-      const int n = (int)(t - nw);
+      const int n = nperm_inv(mp, (int)(t - nw));
       const int np = (n / mp.nGr) * mp.nGp + n % mp.nGr;
       off = (long)np * Kt + ones_col;
     }
@@ -186,7 +199,7 @@ __global__ __launch_bounds__(256) void wgrad_finalize4_kernel(const float* __res
     const long pe = e4 * 4 + j;
     const int np = (int)(pe / Kt);
     const int kk = (int)(pe - (long)np * Kt);
-    const int n = unpad(np, mp.nG, mp.nGr, mp.nGp);
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp));
     if (n < 0) continue;
     float* o = nullptr;
     if (bias_grad && kk == ones_col) {
@@ -282,7 +295,8 @@ __global__ __launch_bounds__(256) void colsum_final(const float* __restrict__ ws
   const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
   const int n = blockIdx.x * 8 + tx;
   const bool ok = n < mp.N;
-  const int np = ok ? (n / mp.nGr) * mp.nGp + n % mp.nGr : 0;
+  const int nq = ok ? nperm_inv(mp, n) : 0;
+  const int np = ok ? (nq / mp.nGr) * mp.nGp + nq % mp.nGr : 0;
   float s = 0.f;
   if (ok) {
     int b = ty;
@@ -462,6 +476,7 @@ static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
   KAIR_CHECK_ARG(mp.nG > 0 && mp.nGr > 0 && mp.nGp >= mp.nGr && mp.nG * mp.nGr == mp.N, "pack_weight: bad N map");
   KAIR_CHECK_ARG(mp.kind == 4 || (mp.kG > 0 && mp.kGr > 0 && mp.kGp >= mp.kGr && mp.kG * mp.kGr == mp.K),
                  "pack_weight: bad K map");
+  KAIR_CHECK_ARG(mp.n_perm <= 1 || (mp.nG == 1 && mp.N % mp.n_perm == 0), "pack_weight: n_perm needs nG == 1, N %% n_perm == 0");
   const long Np = (long)mp.nG * mp.nGp, Kp = (long)mp.kG * mp.kGp;
   KAIR_CHECK_ARG((mp.kind != 10 && mp.kind != 12) || (Np % 32 == 0 && Kp % 16 == 0),
                  "pack_weight: fragment order needs Np %% 32 == 0, Kp %% 16 == 0");
@@ -529,6 +544,7 @@ extern "C" int kair_wgrad_finalize(const float* partial, int splits, const kair_
   KAIR_CHECK_ARG(mp.kind == 0 || mp.kind == 1 || mp.kind == 7,
                  "wgrad_finalize: kind must be 0 (linear), 1 (conv3x3) or 7 (conv2x2)");
   KAIR_CHECK_ARG(!bias_grad || ones_col >= 0, "wgrad_finalize: bias needs ones_col");
+  KAIR_CHECK_ARG(mp.n_perm <= 1 || (mp.nG == 1 && mp.N % mp.n_perm == 0), "wgrad_finalize: n_perm needs nG == 1");
   const int taps = mp.kind == 0 ? 1 : (mp.kind == 1 ? 9 : 4);
   const long Np = (long)mp.nG * mp.nGp;
   const long Kt = (long)taps * mp.kG * mp.kGp;

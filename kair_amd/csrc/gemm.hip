@@ -368,6 +368,52 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
         ((float*)e.out)[((b * e.imgC + c) * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + jj] = o;
       }
     }
+  } else if (e.omode == KAIR_OUT_PSHUF_SPM) {
+    // columns sub-pixel-major: n = (i*r + j)*nf + c, so a chunk of 8 is 8 channels of one pixel
+    const int r = e.r, nf = e.N / (r * r);
+    const long hw = (long)e.psH * e.psW;
+    const long b = m / hw;
+    const int p = (int)(m - b * hw), y = p / e.psW, x = p - (p / e.psW) * e.psW;
+    const int sp = n / nf, c = n - sp * nf, i = sp / r, jj = sp - i * r;
+    const long orow = (b * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + jj;
+    if (full && c + 8 <= nf && (e.ldo % 8) == 0 && (c % 8) == 0) {
+      store8_any(e.out, e.odt, orow * e.ldo + c, v);
+      if (e.pre) store8_any(e.pre, e.pdt, orow * e.ldp + c, pre);
+    } else {
+      for (int j = 0; j < 8 && n + j < e.N; ++j) {
+        const int nn = n + j, s2 = nn / nf, c2 = nn - s2 * nf, i2 = s2 / r, j2 = s2 - i2 * r;
+        const long orow2 = (b * e.psH * r + (long)y * r + i2) * ((long)e.psW * r) + (long)x * r + j2;
+        st1(e.out, e.odt, orow2 * e.ldo + c2, v[j]);
+        if (e.pre) st1(e.pre, e.pdt, orow2 * e.ldp + c2, pre[j]);
+      }
+    }
+  } else if (e.omode == KAIR_OUT_PUNSHUF_SPM) {
+    // pixel (b, Y, X) of the shuffled image, column c -> pre-shuffle row (b, Y/r, X/r), column
+    // (i*r + j)*N + c: a chunk of 8 columns is 8 contiguous pre-shuffle channels
+    const int r = e.r;
+    const long HW = (long)e.psH * r * e.psW * r;
+    const long b = m / HW;
+    const long p = m - b * HW;
+    const int Y = (int)(p / (e.psW * r)), X = (int)(p - (long)Y * e.psW * r);
+    const int y = Y / r, i = Y - y * r, x = X / r, jj = X - x * r;
+    const long orow = (b * e.psH + y) * e.psW + x;
+    const long o0 = orow * e.ldo + (long)(i * r + jj) * e.N + n;
+    if (e.gate) {
+      float g[8];
+      if (full) load8_any(e.gate, e.gdt, orow * e.ldg + (long)(i * r + jj) * e.N + n, g);
+      else
+        for (int j = 0; j < 8; ++j)
+          g[j] = n + j < e.N ? (e.gdt == KAIR_BF16 ? (float)((const bf16*)e.gate)[orow * e.ldg + (long)(i * r + jj) * e.N + n + j]
+                                                    : ((const float*)e.gate)[orow * e.ldg + (long)(i * r + jj) * e.N + n + j]) : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] *= (e.gkind == 2) ? (g[j] > 0.f ? 1.f : e.slope) : (e.gkind == 4 ? g[j] : (g[j] > 0.f ? 1.f : 0.f));
+    }
+    if (full && (e.ldo % 8) == 0 && (e.N % 8) == 0) {
+      store8_any(e.out, e.odt, o0, v);
+    } else {
+      for (int j = 0; j < 8 && n + j < e.N; ++j) st1(e.out, e.odt, o0 + j, v[j]);
+    }
   } else if (e.omode == KAIR_OUT_PUNSHUF) {
     const int r = e.r;
     const long HW = (long)e.psH * r * e.psW * r;
@@ -1733,8 +1779,12 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
   KAIR_CHECK_ARG(!B->w_split || (compute == KAIR_BF16 && B->ld >= 2L * ((K + 63) / 64) * 64),
                  "gemm_nt: hi/lo split weights need bf16 compute and rows of 2*ceil(K/64)*64 columns");
   KAIR_CHECK_ARG(!A->w_split, "gemm_nt: w_split is a B-operand flag");
-  KAIR_CHECK_ARG((E->out_mode != KAIR_OUT_PSHUF && E->out_mode != KAIR_OUT_PUNSHUF && E->out_mode != KAIR_OUT_PSHUF_NCHW) ||
+  KAIR_CHECK_ARG((E->out_mode != KAIR_OUT_PSHUF && E->out_mode != KAIR_OUT_PUNSHUF && E->out_mode != KAIR_OUT_PSHUF_NCHW &&
+                  E->out_mode != KAIR_OUT_PSHUF_SPM && E->out_mode != KAIR_OUT_PUNSHUF_SPM) ||
                      E->ps_r > 0, "gemm_nt: pixel shuffle r");
+  KAIR_CHECK_ARG(E->out_mode != KAIR_OUT_PSHUF_SPM || N % (E->ps_r * E->ps_r) == 0, "gemm_nt: PSHUF_SPM needs N %% r^2 == 0");
+  KAIR_CHECK_ARG(E->out_mode != KAIR_OUT_PUNSHUF_SPM || E->ldo >= (long)N * E->ps_r * E->ps_r,
+                 "gemm_nt: PUNSHUF_SPM needs ldo >= N * r^2");
   KAIR_CHECK_ARG(E->out_mode != KAIR_OUT_QKVBLK || (E->qkv_hdp % 8 == 0 && E->qkv_tok > 0), "gemm_nt: qkv epilogue");
   KAIR_CHECK_ARG(M < KAIR_MAX_MAPPED_ROWS && N < KAIR_MAX_MAPPED_ROWS && K < KAIR_MAX_MAPPED_ROWS,
                  "gemm_nt: dimensions must be < 2^24");

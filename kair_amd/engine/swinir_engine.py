@@ -99,17 +99,20 @@ class _Conv:
     bf16 weight rounding shifts every output pixel by the same sum(dW * a) and biases PSNR
     (DESIGN.md "parity at bf16"); activation rounding is unbiased and averages out."""
 
-    def __init__(self, eng, mod, Cop, Cip, need_dgrad=True, split=None):
+    def __init__(self, eng, mod, Cop, Cip, need_dgrad=True, split=None, n_perm=0):
+        """n_perm = r*r: output channels stored sub-pixel-major for a following PixelShuffle(r)
+        (kair_wmap.n_perm; the KAIR_OUT_PSHUF_SPM / PUNSHUF_SPM epilogues store 16 bytes at a time)."""
         self.w, self.b = mod.weight, mod.bias
         Co, Ci = self.w.shape[:2]
         self.Co, self.Ci, self.Cop, self.Cip = Co, Ci, Cop, Cip
         if split is None:
             split = getattr(eng, "split_conv", False)
         self.split = bool(split) and eng.tdt == torch.bfloat16
-        self.map = H.wmap(1, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
-        self.mapf = H.wmap(9, Co, Ci, (1, Co, Cop), (1, Ci, Cip)) if self.split else self.map
-        self.mapd = H.wmap(2, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
-        self.mapb = H.wmap(4, Co, 0, (1, Co, Cop), (1, 1, 1))
+        self.n_perm = n_perm
+        self.map = H.wmap(1, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
+        self.mapf = H.wmap(9, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm) if self.split else self.map
+        self.mapd = H.wmap(2, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
+        self.mapb = H.wmap(4, Co, 0, (1, Co, Cop), (1, 1, 1), n_perm=n_perm)
         dev = self.w.device
         kf = 2 * _rup(9 * Cip, 64) if self.split else 9 * Cip
         self.Wf = torch.empty(Cop, kf, device=dev, dtype=eng.tdt)
@@ -210,8 +213,8 @@ class SwinIREngine:
             self.cbu = _Conv(self, net.conv_before_upsample[0], nf, self.Cp)
             self.ups = []
             for m in net.upsample:
-                if isinstance(m, torch.nn.Conv2d):
-                    self.ups.append(_Conv(self, m, m.out_channels, nf))
+                if isinstance(m, torch.nn.Conv2d):   # output channels sub-pixel-major (PSHUF_SPM)
+                    self.ups.append(_Conv(self, m, m.out_channels, nf, n_perm=m.out_channels // nf))
             self.ups_r = [int(math.isqrt(c.Co // nf)) for c in self.ups]
             self.last = _Conv(self, net.conv_last, 16, nf)
         elif self.upsampler == "pixelshuffledirect":
@@ -453,7 +456,7 @@ class SwinIREngine:
                       H.epilogue(P["a0"], bias=c.bp, act=H.ACT_LEAKY, slope=0.01), M, 64, 9 * Cp, cd)
             src, h, w = P["a0"], Hh, Ww
             for c, r, dst in zip(self.ups, self.ups_r, P["ups_act"]):
-                H.gemm_nt(H.im2col(src, h, w, 64), c.fwd(), H.epilogue(dst, mode=H.OUT_PSHUF, ldo=64, bias=c.bp,
+                H.gemm_nt(H.im2col(src, h, w, 64), c.fwd(), H.epilogue(dst, mode=H.OUT_PSHUF_SPM, ldo=64, bias=c.bp,
                                                                             ps=(r, h, w)), B * h * w, c.Co, 9 * 64, cd)
                 src, h, w = dst, h * r, w * r
             c = self.last
@@ -563,7 +566,8 @@ class SwinIREngine:
             # conv_last: dgrad into the pre-shuffle layout of the last upsampling conv
             r_last = self.ups_r[-1]
             H.gemm_nt(H.im2col(P["dE"], h, w, 16, flip=True), H.rows(c.Wd),
-                      H.epilogue(P["dpre"][-1], mode=H.OUT_PUNSHUF, ldo=self.ups[-1].Co, ps=(r_last, h // r_last, w // r_last)),
+                      H.epilogue(P["dpre"][-1], mode=H.OUT_PUNSHUF_SPM, ldo=self.ups[-1].Co,
+                                 ps=(r_last, h // r_last, w // r_last)),
                       B * h * w, 64, 9 * 16, cd)
             self._wgrad(P, H.rows(P["dE"]), H.im2col(src, h, w, 64), B * h * w, 16, 9 * 64, c.map, g(c.w))
             self._bias_colsum(P, H.rows(P["dE"]), B * h * w, 16, c.mapb, g(c.b))
@@ -576,7 +580,8 @@ class SwinIREngine:
                 if i > 0:
                     rp = self.ups_r[i - 1]
                     H.gemm_nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),
-                              H.epilogue(P["dpre"][i - 1], mode=H.OUT_PUNSHUF, ldo=self.ups[i - 1].Co, ps=(rp, h // rp, w // rp)),
+                              H.epilogue(P["dpre"][i - 1], mode=H.OUT_PUNSHUF_SPM, ldo=self.ups[i - 1].Co,
+                                         ps=(rp, h // rp, w // rp)),
                               B * h * w, 64, 9 * c.Co, cd)
                 else:
                     H.gemm_nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),

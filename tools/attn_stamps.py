@@ -3,7 +3,6 @@ window per wave, over all waves, at B=32.
 
     python tools/attn_stamps.py [B]
 """
-import ctypes
 import json
 import os
 import sys
@@ -35,10 +34,7 @@ def main():
         H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], P["dqkv"], grads[blk.table],
                           False, P["attn_ws"], P["nWin"], nh, eng.C // nh, blk.scale, 48, 48, blk.shift)
     torch.cuda.synchronize()
-    n = 8192 * 8
-    buf = (ctypes.c_ulonglong * n)()
-    H.check(H.lib().kair_debug_attn_stamps(buf, n), "stamps")
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    a = np.array(H.debug_attn_stamps(), dtype=np.uint64).reshape(-1, 8).astype(np.int64)
     a = a[a[:, 0] > 0]
     d = np.diff(a[:, :7], axis=1)
     names = ["lds_writes+delta", "S,dP mfma+next loads", "P,dS elementwise", "dV,dK mfma+stores", "dS to LDS", "dQ mfma+stores"]
