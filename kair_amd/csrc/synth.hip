@@ -67,6 +67,67 @@ __global__ __launch_bounds__(256) void synth_sr_kernel(const float* __restrict__
   outL[u] = acc;
 }
 
+// Separable form, one workgroup per (sample, channel): the vertical bicubic pass for the patch's
+// LS L-rows over the source-column window the horizontal taps touch is staged in LDS once, then
+// every L pixel is P horizontal taps over it -- LS*W*P + LS*LS*P MACs instead of LS*LS*P*P, with
+// the same summation order as synth_sr_kernel (each vertical sum over a, then over bq), so the
+// output is bitwise the same.  The block also writes the (augmented) H crop.
+__global__ __launch_bounds__(256) void synth_sr_sep_kernel(const float* __restrict__ pool, int C, int Hs, int Ws,
+                                                           const int4* __restrict__ par, int PS, int sf,
+                                                           const float* __restrict__ wh, const int* __restrict__ ih,
+                                                           const float* __restrict__ ww, const int* __restrict__ iw, int P,
+                                                           int Wmax, float* __restrict__ outH, float* __restrict__ outL) {
+  extern __shared__ float sV[];   // [LS][Wmax]
+  __shared__ int sLo, sHi;
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x / C, c = blockIdx.x - (blockIdx.x / C) * C;
+  const int4 pr = par[b];   // x = image, y = rnd_h (LQ rows), z = rnd_w, w = mode
+  const int LS = PS / sf;
+  const float* img = pool + ((long)pr.x * C + c) * Hs * Ws;
+  // H crop
+  float* oH = outH + (long)(b * C + c) * PS * PS;
+  for (int t = tid; t < PS * PS; t += 256) {
+    const int i = t / PS, j = t - (t / PS) * PS;
+    int si, sj;
+    aug_src(pr.w, i, j, PS, si, sj);
+    oH[t] = img[(long)(pr.y * sf + si) * Ws + pr.z * sf + sj];
+  }
+  // source-column window of the horizontal taps of L columns pr.z .. pr.z + LS - 1
+  if (tid == 0) { sLo = Ws; sHi = 0; }
+  __syncthreads();
+  int lo = Ws, hi = 0;
+  for (int t = tid; t < LS * P; t += 256) {
+    const int x = iw[(pr.z + t / P) * P + t - (t / P) * P];
+    lo = min(lo, x);
+    hi = max(hi, x + 1);
+  }
+  atomicMin(&sLo, lo);
+  atomicMax(&sHi, hi);
+  __syncthreads();
+  lo = sLo;
+  // W <= PS + P + 2 sf <= Wmax by the tap geometry (reflected indices fold inward); clamped anyway
+  const int W = min(sHi - lo, Wmax);
+  // vertical pass: V[r][x - lo] = sum_a wh[gy][a] * img[ih[gy][a]][x], gy = pr.y + r
+  for (int t = tid; t < LS * W; t += 256) {
+    const int r = t / W, xo = t - (t / W) * W, gy = pr.y + r;
+    float acc = 0.f;
+    for (int a = 0; a < P; ++a) acc = fmaf(wh[gy * P + a], img[(long)ih[gy * P + a] * Ws + lo + xo], acc);
+    sV[r * Wmax + xo] = acc;
+  }
+  __syncthreads();
+  // horizontal pass with the augment map on the output
+  float* oL = outL + (long)(b * C + c) * LS * LS;
+  for (int t = tid; t < LS * LS; t += 256) {
+    const int i = t / LS, j = t - (t / LS) * LS;
+    int si, sj;
+    aug_src(pr.w, i, j, LS, si, sj);
+    const int gx = pr.z + sj;
+    float acc = 0.f;
+    for (int bq = 0; bq < P; ++bq) acc = fmaf(ww[gx * P + bq], sV[si * Wmax + iw[gx * P + bq] - lo], acc);
+    oL[t] = acc;
+  }
+}
+
 // Philox-4x32-10 (Salmon et al., SC'11)
 KAIR_DEV uint4 philox(uint4 ctr, uint2 key) {
 #pragma unroll
@@ -121,9 +182,19 @@ extern "C" int kair_synth_sr(const float* pool, int C, int Hs, int Ws, const int
   KAIR_CHECK_ARG(C > 0 && Hs > 0 && Ws > 0 && B > 0 && sf > 0 && PS > 0 && PS % sf == 0 && P > 0,
                  "synth_sr: bad sizes (C %d, %dx%d, B %d, PS %d, sf %d, P %d)", C, Hs, Ws, B, PS, sf, P);
   KAIR_CHECK_ARG(PS <= Hs && PS <= Ws, "synth_sr: pool images smaller than the patch");
-  const long total = (long)B * C * PS * PS + (long)B * C * (PS / sf) * (PS / sf);
-  hipLaunchKernelGGL(synth_sr_kernel, dim3((unsigned)nblocks(total)), dim3(256), 0, (hipStream_t)stream, pool, C, Hs, Ws,
-                     (const int4*)params, B, PS, sf, wh, ih, ww, iw, P, outH, outL);
+  // separable kernel when the staged vertical pass fits in LDS: the horizontal taps of LS L columns
+  // span at most PS + 2P source columns (+ 2 sf of rounding slack)
+  const int LS = PS / sf;
+  const int Wmax = (PS + 2 * P + 2 * sf) < Ws ? (PS + 2 * P + 2 * sf) : Ws;
+  const size_t lds = (size_t)LS * Wmax * sizeof(float);
+  if (lds <= 60 * 1024) {
+    hipLaunchKernelGGL(synth_sr_sep_kernel, dim3((unsigned)(B * C)), dim3(256), lds, (hipStream_t)stream, pool, C, Hs, Ws,
+                       (const int4*)params, PS, sf, wh, ih, ww, iw, P, Wmax, outH, outL);
+  } else {
+    const long total = (long)B * C * PS * PS + (long)B * C * LS * LS;
+    hipLaunchKernelGGL(synth_sr_kernel, dim3((unsigned)nblocks(total)), dim3(256), 0, (hipStream_t)stream, pool, C, Hs, Ws,
+                       (const int4*)params, B, PS, sf, wh, ih, ww, iw, P, outH, outL);
+  }
   KAIR_CHECK_LAUNCH();
   return 0;
 }
