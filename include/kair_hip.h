@@ -138,7 +138,9 @@ typedef struct {
                           v_mfma_f32_32x32x16 operand of rows 32nb.. and k-step kb is one
                           contiguous 1 KiB block (lane l: row 32nb + l%32, k 16kb + 8(l/32) + j);
                         12 kind 10 with hi/lo halves (bf16 only): [Np/32][Kp/16][2][64][8], the hi
-                          block of (nb, kb) followed by its lo block */
+                          block of (nb, kb) followed by its lo block;
+                        13 kind 10 of the TRANSPOSED weight: [Kp/32][Np/16][64][8], lane l: W[n][k]
+                          with k = 32kb' + l%32 (output), n = 16kb + 8(l/32) + j (contraction) */
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
   int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp                   */
@@ -244,6 +246,21 @@ int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, const float*
                       void* h, long ldh, int hd, const void* w2, const float* b2, const float* rowscale,
                       int rows_per_scale, float* out, long ldout, long M, int Cp, int Hp, int w_split,
                       void* stream);
+
+/* Fused MLP half backward (bf16; Cp = 192, hidden 384): with D = dL/dout (fp32 token rows) and
+ * dc = rowscale_mlp * D (bf16 token rows),
+ *   du  = (dc . W2) * gd            gd = GELU'(fc1 pre-activation) as the forward stored it
+ *   D  += LN2-backward(du . W1)     (network_swinir.py:274-276 backward)  -> dL/dmid
+ *   dco = rowscale * dL/dmid         bf16, rows in window order (H, W, shift): the proj operand
+ *   dgamma / dbeta (+)= LN2 parameter gradients (dparam_acc)
+ * in one launch + a small reduction.  w2t / w1t: fc2 / fc1 weights in transposed fragment order
+ * (pack kind 13).  dco must not alias dc.  ws: kair_swin_mlp_bwd_ws() floats. */
+long kair_swin_mlp_bwd_ws(void);
+int kair_swin_mlp_bwd(const void* dc, long lddc, const void* gd, long ldg, const void* w2t, const void* w1t,
+                      void* du, long lddu, const float* x, long ldx, const float* gamma, const float* mean,
+                      const float* rstd, int C, float* D, long ldD, void* dco, long lddo, const float* rowscale,
+                      int rows_per_scale, int H, int W, int shift, float* dgamma, float* dbeta, int dparam_acc,
+                      float* ws, long M, int Cp, int Hp, void* stream);
 
 /* Elementwise / small kernels ------------------------------------------------------------- */
 /* NCHW fp32 image -> NHWC (dtype) with channel stride ldc, x' = (x - mean[c]) * img_range

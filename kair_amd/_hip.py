@@ -128,10 +128,14 @@ _SIGS = {
     "kair_swin_mlp_fwd": [c_vp, c_long, c_vp, c_vp, c_float, c_int, c_vp, c_long, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                           c_long, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_long, c_int, c_int, c_int, c_vp],
     "kair_debug_attn_stamps": [c_vp, c_int],
+    "kair_swin_mlp_bwd_ws": [],
+    "kair_swin_mlp_bwd": [c_vp, c_long, c_vp, c_long, c_vp, c_vp, c_vp, c_long, c_vp, c_long, c_vp, c_vp, c_vp, c_int,
+                          c_vp, c_long, c_vp, c_long, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_long,
+                          c_int, c_int, c_vp],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
-_RESTYPE = {"kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
+_RESTYPE = {"kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
             "kair_pack_table_build": c_long}
 
 _lib = None
@@ -527,3 +531,16 @@ def debug_attn_stamps(n=8192 * 8):
     buf = (ctypes.c_ulonglong * n)()
     check(lib().kair_debug_attn_stamps(ctypes.cast(buf, c_vp), n), "debug_attn_stamps")
     return list(buf)
+
+
+def swin_mlp_bwd_ws():
+    return lib().kair_swin_mlp_bwd_ws()
+
+
+def swin_mlp_bwd(dc, gd, w2t, w1t, du, x, gamma, mean, rstd, C, D, dco, rowscale, rows_per_scale, H, W, shift,
+                 dgamma, dbeta, ws, M, Cp, Hp, dparam_acc=False):
+    """Fused MLP-half backward (kair_swin_mlp_bwd)."""
+    check(lib().kair_swin_mlp_bwd(ptr(dc), dc.shape[-1], ptr(gd), gd.shape[-1], ptr(w2t), ptr(w1t), ptr(du), du.shape[-1],
+                                  ptr(x), x.shape[-1], ptr(gamma), ptr(mean), ptr(rstd), C, ptr(D), D.shape[-1], ptr(dco),
+                                  dco.shape[-1], ptr(rowscale), rows_per_scale, H, W, shift, ptr(dgamma), ptr(dbeta),
+                                  int(dparam_acc), ptr(ws), M, Cp, Hp, stream_ptr()), "swin_mlp_bwd")

@@ -75,6 +75,14 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const int np = nb * 32 + (ln & 31), kp = kb * 16 + 8 * (ln >> 5) + j;
     const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
+  } else if (mp.kind == 13) {  // transposed linear in fragment order: [Kp/32][Np/16][64 lanes][8] of W^T
+    const int KB = Np / 16;
+    const int j = (int)(t & 7), ln = (int)((t >> 3) & 63);
+    const long blk = t >> 9;
+    const int kb = (int)(blk % KB), ob = (int)(blk / KB);
+    const int kp = ob * 32 + (ln & 31), np = kb * 16 + 8 * (ln >> 5) + j;
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
   } else if (mp.kind == 12) {  // linear, fragment order with hi/lo halves: [Np/32][Kp/16][2][64 lanes][8]
     const int KB = Kp / 16;
     const int j = (int)(t & 7), ln = (int)((t >> 3) & 63), half = (int)((t >> 9) & 1);
@@ -480,7 +488,8 @@ static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
   const long Np = (long)mp.nG * mp.nGp, Kp = (long)mp.kG * mp.kGp;
   KAIR_CHECK_ARG((mp.kind != 10 && mp.kind != 12) || (Np % 32 == 0 && Kp % 16 == 0),
                  "pack_weight: fragment order needs Np %% 32 == 0, Kp %% 16 == 0");
-  if (mp.kind == 0 || mp.kind == 3 || mp.kind == 10) *total = Np * Kp;
+  KAIR_CHECK_ARG(mp.kind != 13 || (Kp % 32 == 0 && Np % 16 == 0), "pack_weight: transposed fragment order needs Kp %% 32 == 0, Np %% 16 == 0");
+  if (mp.kind == 0 || mp.kind == 3 || mp.kind == 10 || mp.kind == 13) *total = Np * Kp;
   else if (mp.kind == 12) *total = 2 * Np * Kp;
   else if (mp.kind == 1 || mp.kind == 2) *total = Np * 9 * Kp;
   else if (mp.kind == 7 || mp.kind == 8) *total = Np * 4 * Kp;

@@ -695,6 +695,261 @@ __global__ __launch_bounds__(1024) void swin_mlp_fwd_kernel(const MlpFwdArgs a) 
   }
 }
 
+
+// ---- MLP half, backward ---------------------------------------------------------------------------
+// Given D = dL/dout (fp32) and Dc = s_mlp * D (bf16), one persistent warp-specialised launch makes
+//   dU   = (Dc . W2) * GELU'(u)                       (fc2 input gradient through the stored gate)
+//   dxn  = dU . W1                                    (fc1 input gradient)
+//   D   += LN2-backward(dxn)   -> dL/dmid             (network_swinir.py:274-276 backward)
+//   Dco  = s_attn * dL/dmid   (bf16, window order: the proj input-gradient operand)
+//   dgamma / dbeta partials of LN2 per workgroup
+// replacing the fc2 / fc1 input-gradient GEMMs and the LayerNorm backward: dxn never touches HBM,
+// dU is written once (the fc1 weight gradient reads it), D is read and written once.
+// 12 compute waves run only the GEMMs (they issue no global store, so their streamed weight
+// fragments never wait behind one); 4 memory waves store dU and run the LayerNorm backward of the
+// PREVIOUS tile (dxn from LDS, x / D / statistics from HBM, results stored straight from
+// registers) while the compute waves run this tile's first GEMM.  Hidden dimension in two
+// 192-wide halves; weights in transposed fragment order (pack kind 13).
+struct MlpBwdArgs {
+  const bf16* dc; long lddc;                 // s_mlp * dL/dout, token rows
+  const bf16* gd; long ldg;                  // GELU'(fc1 pre-activation), token rows
+  const bf16* w2t; const bf16* w1t;          // kind 13 of fc2 ([HP/32][CP/16]) and fc1 ([CP/32][HP/16])
+  bf16* du; long lddu;                       // out: dL/d(fc1 pre-activation)
+  const float* x; long ldx;                  // LN2 input (mid), token rows
+  const float* gamma; const float* mean; const float* rstd; int C;
+  float* D; long ldD;                        // dL/dout in, dL/dmid out (token rows)
+  bf16* dco; long lddo;                      // out: s_attn * dL/dmid, window-order rows
+  const float* rowscale; int tiles_per_scale;
+  WinMap wm;
+  float* part;                               // [gridDim][2][CP]
+  long nTiles;
+  int dbg;   // ablation bits (KAIR_MLPB_DBG, perf only): 1 no dH GEMM, 2 no dxn GEMM, 4 no memory-wave work
+};
+
+__global__ __launch_bounds__(512) void swin_mlp_bwd_kernel(const MlpBwdArgs a) {
+  constexpr int NC = 6, NT = 512, NST = NT - 64 * NC, NG = NST / 16, CP = 192, HH = 192, LDA = CP + 8, LDY = CP + 4;
+  constexpr int KBC = CP / 16, KBH = HH / 16, PF = 4;
+  static_assert(KBC % PF == 0 && KBH % PF == 0, "k-steps must be a multiple of the prefetch depth");
+  __shared__ __attribute__((aligned(16))) bf16 sA[TOK * LDA];    // Dc tile
+  __shared__ __attribute__((aligned(16))) bf16 sU[TOK * LDA];    // dU half
+  __shared__ __attribute__((aligned(16))) bf16 sG[TOK * LDA];    // GELU' half
+  __shared__ __attribute__((aligned(16))) float sY[TOK * LDY];   // dxn (fp32) of the last tile
+  __shared__ float sGam[CP];
+  __shared__ float sPart[NG][2][CP];   // LN2 parameter-gradient partials, one row per memory-wave row group
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bool compute = w < NC;
+  const int sid = tid - 64 * NC;
+  const int l31 = lane & 31, hh = lane >> 5;
+  const int ct = w;   // compute wave w: hidden / output column tile w, both 32-row tiles
+  // memory waves: 16 lanes per LN row, NG rows per pass (row group sg = sid / 16, lane sj)
+  const int sg = sid >> 4, sj = sid & 15;
+  for (int i = tid; i < CP; i += NT) sGam[i] = i < a.C ? a.gamma[i] : 0.f;
+  for (int i = tid; i < NG * 2 * CP; i += NT) (&sPart[0][0][0])[i] = 0.f;
+  __syncthreads();
+  const float inv_c = 1.0f / (float)a.C;
+
+  // LayerNorm-2 backward of tile tl (dxn in sY) by the memory waves: D += rstd (g dy - mean(g dy) -
+  // xh mean(g dy xh)); the finished rows also as s_attn * row (bf16, window order)
+  auto ln_bwd = [&](long tl) {
+    const long row0 = tl * TOK;
+    const float sc = a.rowscale ? a.rowscale[tl / a.tiles_per_scale] : 1.f;
+#pragma unroll 1
+    for (int p = 0; p < TOK / NG; ++p) {
+      const int r = NG * p + sg;
+      const long t = row0 + r;
+      const float mu = a.mean[t], rs = a.rstd[t];
+      float4 xq[3], dcur[3], dv[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        dcur[k] = *(const float4*)(a.D + t * a.ldD + 4 * sj + 64 * k);
+        xq[k] = *(const float4*)(a.x + t * a.ldx + 4 * sj + 64 * k);
+        dv[k] = *(const float4*)(sY + r * LDY + 4 * sj + 64 * k);
+      }
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * sj + 64 * k;
+        const float xa[4] = {xq[k].x, xq[k].y, xq[k].z, xq[k].w};
+        const float da[4] = {dv[k].x, dv[k].y, dv[k].z, dv[k].w};
+        float4 pgv = *(const float4*)&sPart[sg][0][cb], pbv = *(const float4*)&sPart[sg][1][cb];
+        float pgs[4] = {pgv.x, pgv.y, pgv.z, pgv.w}, pbs[4] = {pbv.x, pbv.y, pbv.z, pbv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool in = cb + e < a.C;
+          const float xh = in ? (xa[e] - mu) * rs : 0.f;
+          const float d = in ? da[e] : 0.f;
+          const float gy = d * sGam[cb + e];
+          pgs[e] += d * xh;
+          pbs[e] += d;
+          s1 += gy;
+          s2 += gy * xh;
+        }
+        *(float4*)&sPart[sg][0][cb] = make_float4(pgs[0], pgs[1], pgs[2], pgs[3]);
+        *(float4*)&sPart[sg][1][cb] = make_float4(pbs[0], pbs[1], pbs[2], pbs[3]);
+      }
+      s1 = dpp_sum16(s1) * inv_c;
+      s2 = dpp_sum16(s2) * inv_c;
+      const long wr = token_to_win(t, a.wm);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {   // second pass: x-hat and gamma * dy recomputed, not kept live
+        const int cb = 4 * sj + 64 * k;
+        const float xa[4] = {xq[k].x, xq[k].y, xq[k].z, xq[k].w};
+        const float da[4] = {dv[k].x, dv[k].y, dv[k].z, dv[k].w};
+        const float cu[4] = {dcur[k].x, dcur[k].y, dcur[k].z, dcur[k].w};
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool in = cb + e < a.C;
+          const float xh = (xa[e] - mu) * rs, gy = da[e] * sGam[cb + e];
+          o[e] = cu[e] + (in ? rs * (gy - s1 - xh * s2) : 0.f);
+        }
+        *(float4*)(a.D + t * a.ldD + cb) = make_float4(o[0], o[1], o[2], o[3]);
+        *(bf16x4*)(a.dco + wr * a.lddo + cb) = bf16x4{(bf16)(sc * o[0]), (bf16)(sc * o[1]), (bf16)(sc * o[2]), (bf16)(sc * o[3])};
+      }
+    }
+  };
+
+  long prev = -1;
+  for (long tile = blockIdx.x; tile < a.nTiles; tile += gridDim.x) {
+    const long row0 = tile * TOK;
+    if (compute) {
+      // Dc tile and the first GELU' half into LDS
+      constexpr int CH = CP / 8;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = tid + 64 * NC * k, r = i / CH, q = (i - (i / CH) * CH) * 8;
+        *(uint4*)(sA + r * LDA + q) = *(const uint4*)(a.dc + (row0 + r) * a.lddc + q);
+        *(uint4*)(sG + r * LDA + q) = *(const uint4*)(a.gd + (row0 + r) * a.ldg + q);
+      }
+    }
+    __syncthreads();   // (1) Dc tile and GELU' half 0 visible
+    // the previous tile's LayerNorm backward (memory waves), under this tile's first GEMM
+    if (!compute && prev >= 0 && !(a.dbg & 4)) ln_bwd(prev);
+    uint4 g1[4];
+    if (compute) {   // the second GELU' half, into registers until half 0 has consumed the first
+      constexpr int CH = CP / 8;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = tid + 64 * NC * k, r = i / CH, q = (i - (i / CH) * CH) * 8;
+        g1[k] = *(const uint4*)(a.gd + (row0 + r) * a.ldg + HH + q);
+      }
+    }
+    f32x16 DX[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) DX[rt][r] = 0.f;
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      if (compute) {
+        // dH tile (hidden columns 192 half + 32 ct.., rows 32 rt..) = W2^T . Dc^T, times GELU'
+        const bf16* wp = a.w2t + ((long)(6 * half + ct) * KBC * 64 + lane) * 8;
+        bf16x8 pw[PF];
+#pragma unroll
+        for (int i = 0; i < PF; ++i) pw[i] = *(const bf16x8*)(wp + i * 512);
+        f32x16 U[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) U[rt][r] = 0.f;
+#pragma unroll 1
+        for (int kb0 = 0; kb0 < ((a.dbg & 1) ? 0 : KBC); kb0 += PF) {
+#pragma unroll
+          for (int sl = 0; sl < PF; ++sl) {
+            const int kb = kb0 + sl;
+            const bf16x8 fw = pw[sl];
+            if (kb + PF < KBC) pw[sl] = *(const bf16x8*)(wp + (kb + PF) * 512);
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+              const bf16x8 fa = *(const bf16x8*)(sA + (rt * 32 + l31) * LDA + kb * 16 + 8 * hh);
+              U[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw, fa, U[rt], 0, 0, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+          for (int gg = 0; gg < 4; ++gg) {
+            const int col = 32 * ct + 8 * gg + 4 * hh;
+            const bf16x4 gv = *(const bf16x4*)(sG + (rt * 32 + l31) * LDA + col);
+            *(bf16x4*)(sU + (rt * 32 + l31) * LDA + col) =
+                bf16x4{(bf16)(U[rt][4 * gg] * (float)gv[0]), (bf16)(U[rt][4 * gg + 1] * (float)gv[1]),
+                       (bf16)(U[rt][4 * gg + 2] * (float)gv[2]), (bf16)(U[rt][4 * gg + 3] * (float)gv[3])};
+          }
+      }
+      __syncthreads();   // (2) dU half complete; GELU' half and the previous dxn no longer read
+      if (!compute) {   // ---- [memory] dU half
+        constexpr int CH = HH / 8;
+        for (int i = sid; i < ((a.dbg & 4) ? 0 : TOK * CH); i += NST) {
+          const int r = i / CH, q = (i - (i / CH) * CH) * 8;
+          *(uint4*)(a.du + (row0 + r) * a.lddu + HH * half + q) = *(const uint4*)(sU + r * LDA + q);
+        }
+      } else {
+        if (half == 0) {   // the second GELU' half into LDS
+          constexpr int CH = HH / 8;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int i = tid + 64 * NC * k, r = i / CH, q = (i - (i / CH) * CH) * 8;
+            *(uint4*)(sG + r * LDA + q) = g1[k];
+          }
+        }
+        // dxn tile (columns 32 ct.., rows 32 rt..) += W1^T(half) . dU_half^T
+        const bf16* wp = a.w1t + ((long)ct * (2 * KBH) + KBH * half) * 512 + lane * 8;
+        bf16x8 pw[PF];
+#pragma unroll
+        for (int i = 0; i < PF; ++i) pw[i] = *(const bf16x8*)(wp + i * 512);
+#pragma unroll 1
+        for (int kb0 = 0; kb0 < ((a.dbg & 2) ? 0 : KBH); kb0 += PF) {
+#pragma unroll
+          for (int sl = 0; sl < PF; ++sl) {
+            const int kb = kb0 + sl;
+            const bf16x8 fw = pw[sl];
+            if (kb + PF < KBH) pw[sl] = *(const bf16x8*)(wp + (kb + PF) * 512);
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+              const bf16x8 fu = *(const bf16x8*)(sU + (rt * 32 + l31) * LDA + kb * 16 + 8 * hh);
+              DX[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw, fu, DX[rt], 0, 0, 0);
+            }
+          }
+        }
+      }
+      __syncthreads();   // (3) dU half consumed (fc1 input gradient, stores); GELU' half 1 visible
+    }
+    if (compute) {
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+          *(float4*)(sY + (rt * 32 + l31) * LDY + 32 * ct + 8 * gg + 4 * hh) =
+              make_float4(DX[rt][4 * gg], DX[rt][4 * gg + 1], DX[rt][4 * gg + 2], DX[rt][4 * gg + 3]);
+    }
+    __syncthreads();   // (4) dxn tile complete
+    prev = tile;
+  }
+  if (!compute && prev >= 0 && !(a.dbg & 4)) ln_bwd(prev);
+  // LN2 parameter-gradient partials: the 16 memory-wave row groups, summed in a fixed order
+  __syncthreads();
+  for (int i = tid; i < 2 * CP; i += NT) {
+    const int which = i / CP, c = i - which * CP;
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) sum += sPart[q][which][c];
+    a.part[(long)blockIdx.x * 2 * CP + i] = sum;
+  }
+}
+
+// dgamma / dbeta (+)= sum over workgroups of the partials, fixed order
+__global__ __launch_bounds__(256) void mlp_bwd_param_reduce(const float* __restrict__ part, int nb, int C, int CPd,
+                                                            float* dgamma, float* dbeta, int acc) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * C) return;
+  const int which = i / C, c = i - which * C;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(long)b * 2 * CPd + which * CPd + c];
+  float* o = which == 0 ? dgamma + c : dbeta + c;
+  *o = acc ? *o + s : s;
+}
+
 }  // namespace
 
 extern "C" int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, const float* beta, float eps, int C,
@@ -773,6 +1028,53 @@ extern "C" int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, c
     hipLaunchKernelGGL(swin_mlp_fwd_kernel<2>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(swin_mlp_fwd_kernel<1>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" long kair_swin_mlp_bwd_ws(void) {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  return (long)ncu * 2 * 192;
+}
+
+extern "C" int kair_swin_mlp_bwd(const void* dc, long lddc, const void* gd, long ldg, const void* w2t, const void* w1t,
+                                 void* du, long lddu, const float* x, long ldx, const float* gamma, const float* mean,
+                                 const float* rstd, int C, float* D, long ldD, void* dco, long lddo, const float* rowscale,
+                                 int rows_per_scale, int H, int W, int shift, float* dgamma, float* dbeta, int dparam_acc,
+                                 float* ws, long M, int Cp, int Hp, void* stream) {
+  KAIR_CHECK_ARG(dc && gd && w2t && w1t && du && x && gamma && mean && rstd && D && dco && dgamma && dbeta && ws,
+                 "swin_mlp_bwd: null pointer");
+  KAIR_CHECK_ARG(Cp == 192 && Hp == 384 && C > 0 && C < Cp, "swin_mlp_bwd: laid out for Cp 192 / hidden 384");
+  KAIR_CHECK_ARG(M > 0 && M % TOK == 0 && M < KAIR_MAX_MAPPED_ROWS, "swin_mlp_bwd: M must be a multiple of 64");
+  KAIR_CHECK_ARG(H % WSZ == 0 && W % WSZ == 0 && shift >= 0 && shift < WSZ && M % ((long)H * W) == 0, "swin_mlp_bwd: geometry");
+  KAIR_CHECK_ARG(lddc >= Cp && lddc % 8 == 0 && ldg >= Hp && ldg % 8 == 0 && lddu >= Hp && lddu % 8 == 0 && ldx >= Cp &&
+                     ldx % 4 == 0 && ldD >= Cp && ldD % 4 == 0 && lddo >= Cp && lddo % 8 == 0,
+                 "swin_mlp_bwd: strides");
+  KAIR_CHECK_ARG(dco != dc, "swin_mlp_bwd: dco must not alias dc (rows are read and written by different tiles)");
+  KAIR_CHECK_ARG(!rowscale || (rows_per_scale > 0 && rows_per_scale % TOK == 0), "swin_mlp_bwd: rows_per_scale");
+  MlpBwdArgs a;
+  a.dc = (const bf16*)dc; a.lddc = lddc; a.gd = (const bf16*)gd; a.ldg = ldg;
+  a.w2t = (const bf16*)w2t; a.w1t = (const bf16*)w1t; a.du = (bf16*)du; a.lddu = lddu;
+  a.x = x; a.ldx = ldx; a.gamma = gamma; a.mean = mean; a.rstd = rstd; a.C = C;
+  a.D = D; a.ldD = ldD; a.dco = (bf16*)dco; a.lddo = lddo;
+  a.rowscale = rowscale; a.tiles_per_scale = rowscale ? rows_per_scale / TOK : 1;
+  a.wm = make_winmap(H, W, WSZ, shift);
+  a.part = ws;
+  a.nTiles = M / TOK;
+  static const int dbg = getenv("KAIR_MLPB_DBG") ? atoi(getenv("KAIR_MLPB_DBG")) : 0;
+  a.dbg = dbg;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  const long grid = a.nTiles < ncu ? a.nTiles : ncu;
+  hipLaunchKernelGGL(swin_mlp_bwd_kernel, dim3((unsigned)grid), dim3(512), 0, (hipStream_t)stream, a);
+  KAIR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(mlp_bwd_param_reduce, dim3((unsigned)((2 * C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws,
+                     (int)grid, C, 192, dgamma, dbeta, dparam_acc);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

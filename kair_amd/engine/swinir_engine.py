@@ -63,7 +63,7 @@ def swinir_flops(net, Hh, Ww):
 class _Lin:
     """A linear layer's packed forms.  n/k groupings map reference rows/cols to padded ones."""
 
-    def __init__(self, eng, mod, n_grp, k_grp, frag=False, split=False):
+    def __init__(self, eng, mod, n_grp, k_grp, frag=False, split=False, frag_t=False):
         self.w, self.b = mod.weight, mod.bias
         N, K = self.w.shape
         self.N, self.K = N, K
@@ -82,12 +82,17 @@ class _Lin:
         self.mapg = H.wmap(12 if self.split else 10, N, K, n_grp, k_grp) if frag else None
         self.Wg = (torch.empty((2 if self.split else 1) * self.Np, self.Kp, device=dev, dtype=eng.tdt)
                    if frag else None)
+        # transposed fragment order (pack kind 13) for the fused MLP backward
+        self.mapgt = H.wmap(13, N, K, n_grp, k_grp) if frag_t else None
+        self.Wgt = torch.empty(self.Kp, self.Np, device=dev, dtype=eng.tdt) if frag_t else None
 
     def pack_jobs(self):
         w, b = self.w.detach(), self.b.detach()
         jobs = [(w, self.Wp, self.map), (w, self.Wt, self.mapT), (b, self.bp, self.mapb)]
         if self.Wg is not None:
             jobs.append((w, self.Wg, self.mapg))
+        if self.Wgt is not None:
+            jobs.append((w, self.Wgt, self.mapgt))
         return jobs
 
 
@@ -145,8 +150,9 @@ class _Blk:
         sp = eng.split_linear
         self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=eng.fused_attn, split=sp)
         self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=eng.fused_attn, split=sp)
-        self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp), frag=eng.fused_mlp, split=sp)
-        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=eng.fused_mlp, split=sp)
+        fb = eng.fused_mlp_bwd
+        self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp), frag=eng.fused_mlp, split=sp, frag_t=fb)
+        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=eng.fused_mlp, split=sp, frag_t=fb)
 
     def linears(self):
         return (self.qkv, self.proj, self.fc1, self.fc2)
@@ -188,6 +194,11 @@ class SwinIREngine:
         if fused_mlp is None:
             fused_mlp = fused_blocks and os.environ.get("KAIR_FUSED_MLP", "1") == "1"
         self.fused_mlp = bool(fused_mlp) and compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384
+        # the MLP-half backward kernel: off by default -- 205 us per block at B = 32 against 172-186 us
+        # for the fc2 / fc1 input-gradient GEMMs + LN2 backward it replaces (its memory
+        # waves' LayerNorm rows and the tile loads run latency-exposed); KAIR_FUSED_MLP_BWD=1 enables it
+        self.fused_mlp_bwd = (bool(fused_blocks) and compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384
+                              and os.environ.get("KAIR_FUSED_MLP_BWD", "0") == "1")
         # split linears measured: the PSNR effect of bf16 linear-weight rounding is ~1e-4 dB against
         # ~5e-4 dB of activation-rounding noise per image (tools/parity_seeds.py, DESIGN.md "parity at
         # bf16"), at +45 us per block for the attention kernel -- off unless asked for
@@ -364,6 +375,9 @@ class SwinIREngine:
         P["D"], P["G"] = e(M, Cp), e(M, Cp)
         P["dU"], P["dxn"] = e(M, Hdp, dt=T), e(M, Cp, dt=T)
         P["Dc"] = e(M, Cp, dt=T)   # compute-dtype GEMM operand copy of the residual-stream gradient
+        if self.fused_mlp_bwd:     # the attention branch's operand, written by the fused MLP backward
+            P["Dc2"] = e(M, Cp, dt=T)
+            P["mlp_ws"] = e(H.swin_mlp_bwd_ws())
         P["dO"], P["dqkv"] = e(M, nh * 32, dt=T), e(3 * M * nh * 32, dt=T)
         P["ln_ws"] = e(2 * 2048 * Cp)   # kair_layernorm_bwd: 2 * 2048 * C floats
         P["attn_ws"] = e(H.window_attn_bwd_ws(nWin, nh))
@@ -659,22 +673,31 @@ class SwinIREngine:
         # block's attention backward).  Every kernel's arithmetic is unchanged (bit-identical).
         Dc = P["Dc"]
         fc2, fc1 = blk.fc2, blk.fc1
+        n = blk.n2
         ev_fc2 = self._on_side(lambda: self._wgrad(P, H.rows(Dc), H.rows(S["h"], ones_col=fc2.K, ones_in_data=True), M,
                                                    Cp, self.Hdp, fc2.map, g(fc2.w), g(fc2.b), fc2.K))
-        # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
-        H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
+        if self.fused_mlp_bwd:
+            # fc2 / fc1 input gradients + LN2 backward in one launch; the attention branch's operand goes
+            # to Dc2 (Dc is read by other tiles of the same launch)
+            H.swin_mlp_bwd(Dc, S["u"], fc2.Wgt, fc1.Wgt, P["dU"], S["mid"], n.weight, S["m2"], S["r2"], self.C, D, P["Dc2"],
+                           s_attn, HW, Hh, Ww, blk.shift, g(n.weight), g(n.bias), P["mlp_ws"], M, Cp, self.Hdp)
+            Da = P["Dc2"]
+        else:
+            # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
+            H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
         self._on_side(lambda: self._wgrad(P, H.rows(P["dU"]), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), M,
                                           self.Hdp, Cp, fc1.map, g(fc1.w), g(fc1.b), self.C))
-        H.gemm_nt(H.rows(P["dU"]), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
-        n = blk.n2
-        self._after(ev_fc2)                  # LN2 backward rewrites Dc
-        H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, g(n.weight), g(n.bias), False,
-                        P["ln_ws"], M, self.C, copy=H.copy_desc(Dc, rowscale=s_attn, rows_per_scale=HW, win=win))
+        if not self.fused_mlp_bwd:
+            H.gemm_nt(H.rows(P["dU"]), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
+            self._after(ev_fc2)                  # LN2 backward rewrites Dc
+            H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, g(n.weight), g(n.bias),
+                            False, P["ln_ws"], M, self.C, copy=H.copy_desc(Dc, rowscale=s_attn, rows_per_scale=HW, win=win))
+            Da = Dc
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         proj, qkv = blk.proj, blk.qkv
-        ev_proj = self._on_side(lambda: self._wgrad(P, H.rows(Dc), H.rows(S["O"], ones_col=hd, ones_in_data=True), M,
+        ev_proj = self._on_side(lambda: self._wgrad(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), M,
                                                     Cp, nh * 32, proj.map, g(proj.w), g(proj.b), hd))
-        H.gemm_nt(H.rows(Dc), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
+        H.gemm_nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
         self._after(self._ev_qkv)            # the previous block's qkv weight gradient still reads dqkv
         H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], P["dqkv"], g(blk.table), False,
                           P["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
@@ -687,6 +710,7 @@ class SwinIREngine:
         if copy_prev:
             cp = H.copy_desc(Dc, rowscale=drop[bi - 1, 1] if drop is not None else None, rows_per_scale=HW)
         self._after(ev_proj)                 # LN1 backward rewrites Dc (and the fc1 one is done: dU is free)
+        self._after(ev_fc2)
         H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, g(n.weight), g(n.bias), False,
                         P["ln_ws"], M, self.C, win, copy=cp)
 

@@ -3,6 +3,8 @@ on the same weights and the same DropPath scales: the saved tensors the backward
 rstd, q/k/v, O, lse), the block outputs, the network output and every gradient.  Both paths run
 bf16 MFMA with fp32 accumulation, so they agree to bf16 rounding (a few ulp of the stored bf16
 values), not bitwise; each path is separately pinned to the CPU oracle in test_swinir_gpu.py."""
+import os
+
 import pytest
 import torch
 
@@ -41,8 +43,13 @@ def _pair(split=False, depths=(2, 2), img=24):
     nets[1].load_state_dict(nets[0].state_dict())
     nets = [n.to(dev).train() for n in nets]
     # the fused net with split linears too when split (pack kind 12 through both fused kernels)
-    nets[0]._engine = SwinIREngine(nets[0], "bf16", split_conv=split, fused_blocks=True, fused_mlp=True,
-                                   split_linear=split)
+    os.environ["KAIR_FUSED_MLP_BWD"] = "1"   # the fused MLP backward too (off by default, still tested)
+    try:
+        nets[0]._engine = SwinIREngine(nets[0], "bf16", split_conv=split, fused_blocks=True, fused_mlp=True,
+                                       split_linear=split)
+    finally:
+        del os.environ["KAIR_FUSED_MLP_BWD"]
+    assert nets[0]._engine.fused_mlp_bwd
     return nets
 
 
