@@ -116,7 +116,7 @@ def pmc_traffic(key):
     return None
 
 
-def cpu_baseline(batch=2, steps=2):
+def cpu_baseline(batch=4, steps=4):
     """The CPU oracle (fp32 restatement of ModelPlain.optimize_parameters) on the host cores."""
     from oracle import swinir as osw
     from oracle.train import OracleTrainer
@@ -211,11 +211,39 @@ def psnr_parity(net_gpu, device, n_eval=8):
             "max_abs_bf16_vs_oracle": float((E - Er).abs().max())}
 
 
+def other_configs(device):
+    """The other BASELINE.json configs, one short fused-trainer (USRNet: autograd + torch Adam) run each
+    on this GPU (tools/bench_models.py; synthetic seeded inputs resident in HBM): patches/s and the
+    fraction of the dense bf16 MFMA peak their training FLOPs reach.  C1 (DnCNN) is a CPU config in
+    the reference; its network's GPU step is reported for completeness."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    import bench_models as bm
+    labels = {"swinir_light": "C2 SwinIR-lightweight x2, 64-px LQ, batch 64",
+              "usrnet": "C3 USRNet x4, 128-px LQ (512^2 HR), batch 48, n_iter 6",
+              "rrdbnet": "C5 RRDBNet x4, 32-px LQ, batch 16 (the N=1 shape of global batch 16)",
+              "dncnn": "C1 DnCNN sigma 25, 40x40, batch 64 (GPU step of the CPU config's network)"}
+    res = {}
+    for name, label in labels.items():
+        try:
+            B, dt, loss = bm.run(name, 5, 3, device)
+            pps = B / dt
+            tf = pps * bm.TRAIN_GFLOP[name] / 1e3
+            res[name] = {"config": label, "value": round(pps, 2), "unit": "patches/s", "ms_per_step": round(dt * 1e3, 3),
+                         "steps": 5, "warmup": 3, "train_gflop_per_patch": bm.TRAIN_GFLOP[name],
+                         "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
+                                      "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4)},
+                         "final_loss": round(loss, 6)}
+        except Exception as e:  # noqa: BLE001
+            res[name] = {"config": label, "error": repr(e)}
+        torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)   # SURVEY §8d: >= 100 timed steps after >= 20 warm-up
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--global-batch", type=int, default=32)
     ap.add_argument("--per-gpu-batch", type=int, default=None, help="weak scaling: fixed batch per GPU")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -223,6 +251,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--drop-path", type=float, default=0.1)
     ap.add_argument("--no-fp32-line", action="store_true", help="skip the fp32 parity-config throughput line")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the short single-GPU throughput lines of BASELINE.json configs C2 / C3 / C5 (and the "
+                         "C1 network on the GPU)")
     ap.add_argument("--data", default="pool", choices=["pool", "static"],
                     help="pool: every step synthesises a fresh batch on the GPU from an HBM-resident HR pool "
                          "(kair_synth_sr: crop + 8-way augment + MATLAB bicubic x1/4, DatasetSR semantics) inside "
@@ -342,6 +373,8 @@ def main():
         out["psnr"] = psnr_parity(net, device)
     except Exception as e:  # noqa: BLE001
         out["psnr"] = {"error": repr(e)}
+    if world == 1 and args.dtype == "bf16" and not args.no_other_configs:
+        out["other_configs"] = other_configs(device)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     print(json.dumps(out), flush=True)

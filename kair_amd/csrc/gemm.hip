@@ -1577,17 +1577,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
     for (int i = 0; i < RM; ++i)
 #pragma unroll
       for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < nks; ++j) {
-      // chunk j landed for this wave (younger: chunk j+1's 3 DMA instructions), then all waves
-      if (j + 1 < nks) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      ring_barrier();   // chunk j visible; stage (j+2) % 3 = (j-1) % 3 is free
-      if (j + 2 < nks) bissue(j + 2);
-      compute(j % 3, j);
-    }
-    // epilogue: bias (+ act) (+ fp32 residual), 4 consecutive channels per lane
+    // epilogue operand (fp32 residual): loaded two k-chunks before the end, after that chunk's
+    // ring wait, so its latency hides under the last chunks' MFMAs instead of following them
+    // (the younger DMA count is then 0: no chunk is issued after chunk nks-1)
     float4 ex[RM][RN];
-    if constexpr (EX == EX_RESID) {
+    auto load_resid = [&]() {
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -1596,6 +1590,21 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
           const int n = wn * TN + jn * 16 + fq * 4;
           ex[i][jn] = *(const float4*)(E.resid + m * E.ldr + (n < N ? n : 0));
         }
+    };
+    for (int j = 0; j < nks; ++j) {
+      // chunk j landed for this wave (younger: chunk j+1's 3 DMA instructions), then all waves
+      if (j + 1 < nks) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ring_barrier();   // chunk j visible; stage (j+2) % 3 = (j-1) % 3 is free
+      if (j + 2 < nks) bissue(j + 2);
+      if constexpr (EX == EX_RESID) {
+        if (j == nks - 2) load_resid();
+      }
+      compute(j % 3, j);
+    }
+    // epilogue: bias (+ act) (+ fp32 residual), 4 consecutive channels per lane
+    if constexpr (EX == EX_RESID) {
+      if (nks < 2) load_resid();
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
