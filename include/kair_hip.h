@@ -170,6 +170,23 @@ int kair_pack_weights(const void* table_dev, int njobs, long nblocks, void* stre
  * bias_grad (if non-NULL) = column ones_col of the sum.  accumulate: += instead of =. */
 int kair_wgrad_finalize(const float* partial, int splits, const kair_wmap* map, float* grad_ref,
                         float* bias_grad, int ones_col, int accumulate, void* stream);
+/* Grouped weight gradients (bf16): the linear layers of a group of Swin blocks in ONE TN launch +
+ * ONE finalize launch.  Job i: grad_i (reference layout [N_ref][K_ref], via map_i, kind 0) =
+ * sum_m A_i[m][n] * B_i[m][k] over n < N_i, k < K_i (the packed dims), bias_grad_i = column
+ * ones_col_i of that sum (B_i holds 1.0 there: ones_in_data).  A: ROWS or QKVBLK (one q/k/v
+ * geometry per group); B: ROWS.  Up to 24 jobs sharing M rows; ws: kair_wgrad_grouped_ws() floats.
+ * Replaces the weight-gradient half of nn.Linear backward (network_swinir.py:19-20, 105, 107) for
+ * every block of an RSTB at once; the sums are in fixed order (deterministic). */
+typedef struct {
+  kair_operand A, B;
+  int N, K;
+  kair_wmap map;
+  float* grad;
+  float* bias_grad;
+  int ones_col;
+} kair_wgrad_job;
+long kair_wgrad_grouped_ws(const kair_wgrad_job* jobs, int njobs, long M);
+int kair_wgrad_grouped(const kair_wgrad_job* jobs, int njobs, long M, float* ws, void* stream);
 /* bias_grad[n_ref] (+)= sum_m G[m][n]  for an operand G of width Np (conv biases without a pad
  * column).  ws: 1024 * Np floats. */
 int kair_colsum(const kair_operand* G, long M, int Np, const kair_wmap* map, float* bias_grad,

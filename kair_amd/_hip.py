@@ -68,6 +68,11 @@ class WMap(ctypes.Structure):
                 ("kG", c_int), ("kGr", c_int), ("kGp", c_int), ("n_perm", c_int)]
 
 
+class WgradJob(ctypes.Structure):
+    _fields_ = [("A", Operand), ("B", Operand), ("N", c_int), ("K", c_int), ("map", WMap), ("grad", c_vp),
+                ("bias_grad", c_vp), ("ones_col", c_int)]
+
+
 class PackJob(ctypes.Structure):
     _fields_ = [("src", c_vp), ("dst", c_vp), ("dst_dtype", c_int), ("reserved", c_int), ("map", WMap),
                 ("total", c_long)]
@@ -78,6 +83,8 @@ _SIGS = {
                      c_int, c_vp],
     "kair_wgrad_splits": [c_long, c_int, c_int],
     "kair_gemm_tn": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), c_vp, c_int, c_long, c_int, c_int, c_int, c_vp],
+    "kair_wgrad_grouped_ws": [ctypes.POINTER(WgradJob), c_int, c_long],
+    "kair_wgrad_grouped": [ctypes.POINTER(WgradJob), c_int, c_long, c_vp, c_vp],
     "kair_pack_weight": [c_vp, c_vp, c_int, ctypes.POINTER(WMap), c_vp],
     "kair_pack_table_bytes": [c_int],
     "kair_pack_table_build": [ctypes.POINTER(PackJob), c_int, c_vp],
@@ -135,7 +142,7 @@ _SIGS = {
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
-_RESTYPE = {"kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
+_RESTYPE = {"kair_wgrad_grouped_ws": c_long, "kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
             "kair_pack_table_build": c_long}
 
 _lib = None
@@ -317,6 +324,37 @@ def wgrad_splits(M, N, K):
 
 def gemm_tn(A, B, ws, splits, M, N, K, compute):
     check(lib().kair_gemm_tn(ctypes.byref(A), ctypes.byref(B), ptr(ws), splits, M, N, K, compute, stream_ptr()), "gemm_tn")
+
+
+def wgrad_grouped_ws(shapes, M):
+    """Workspace floats of a kair_wgrad_grouped launch over linears of packed (N, K) shapes."""
+    arr = (WgradJob * len(shapes))()
+    for i, (N, K) in enumerate(shapes):
+        arr[i].N, arr[i].K = N, K
+    return lib().kair_wgrad_grouped_ws(arr, len(shapes), M)
+
+
+class WgradGroup:
+    """The weight gradients of several linear layers (kair_wgrad_grouped): one TN launch + one
+    finalize launch.  jobs: (A operand, B operand, N, K, wmap, grad, bias_grad or None, ones_col)."""
+
+    WG_MAX = 24
+
+    def __init__(self, jobs, M):
+        if not 0 < len(jobs) <= self.WG_MAX:
+            raise ValueError(f"kair_wgrad_grouped: 1..{self.WG_MAX} jobs (got {len(jobs)})")
+        arr = (WgradJob * len(jobs))()
+        for i, (A, B, N, K, m, grad, bias, oc) in enumerate(jobs):
+            arr[i].A, arr[i].B, arr[i].N, arr[i].K, arr[i].map = A, B, N, K, m
+            arr[i].grad, arr[i].bias_grad, arr[i].ones_col = ptr(grad), ptr(bias), oc
+        self._keep = jobs
+        self.arr, self.n, self.M = arr, len(jobs), M
+        self.ws_floats = lib().kair_wgrad_grouped_ws(arr, self.n, M)
+
+    def run(self, ws):
+        if ws.numel() < self.ws_floats:
+            raise ValueError("kair_wgrad_grouped: workspace too small")
+        check(lib().kair_wgrad_grouped(self.arr, self.n, self.M, ptr(ws), stream_ptr()), "wgrad_grouped")
 
 
 def pack_weight(src, dst, m):

@@ -205,3 +205,19 @@ KAIR_DEV float split_sum16(const float* __restrict__ part, long nparts, long pla
   }
   return s;
 }
+
+// grouped weight-gradient finalize (kair_wgrad_grouped): one job per linear layer, partial planes
+// [splits][Np][Kt] summed in fixed order and scattered to the reference layout (elementwise.hip)
+constexpr int KAIR_WG_MAX = 24;
+struct FinJob {
+  const float* part; float* grad; float* bias;
+  kair_wmap mp;
+  int ones_col, Kt;
+  long plane, blk0;                            // plane = Np * Kt; blk0 = first block of this job
+};
+struct FinGroup {
+  FinJob j[KAIR_WG_MAX];
+  int njobs, splits;
+  long nblocks;
+};
+int kair_launch_finalize_grouped(const FinGroup& g, hipStream_t s);

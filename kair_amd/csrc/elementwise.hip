@@ -169,12 +169,11 @@ __global__ __launch_bounds__(1024) void wgrad_finalize_kernel(const float* __res
 // Vectorised form: each block sums 64 float4 of the PACKED partial planes with 4 split-phases
 // (fixed order, deterministic), then scatters the 4 sums to the reference layout — pad entries are
 // dropped, the fused ones column goes to the bias gradient.  Needs N*K rows of whole float4s.
-__global__ __launch_bounds__(256) void wgrad_finalize4_kernel(const float* __restrict__ part, int splits, kair_wmap mp,
-                                                              float* grad, float* bias_grad, int ones_col, int acc,
-                                                              long Kt, long plane, int taps) {
+KAIR_DEV void finalize4_body(const float* __restrict__ part, int splits, const kair_wmap& mp, float* grad,
+                             float* bias_grad, int ones_col, int acc, long Kt, long plane, int taps, long blk) {
   __shared__ float4 red[4][64];
   const int q = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const long e4 = (long)blockIdx.x * 64 + q;
+  const long e4 = blk * 64 + q;
   const bool valid = e4 * 4 < plane;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (valid) {
@@ -220,6 +219,23 @@ __global__ __launch_bounds__(256) void wgrad_finalize4_kernel(const float* __res
     }
     *o = acc ? *o + t4[j] : t4[j];
   }
+}
+
+__global__ __launch_bounds__(256) void wgrad_finalize4_kernel(const float* __restrict__ part, int splits, kair_wmap mp,
+                                                              float* grad, float* bias_grad, int ones_col, int acc,
+                                                              long Kt, long plane, int taps) {
+  finalize4_body(part, splits, mp, grad, bias_grad, ones_col, acc, Kt, plane, taps, blockIdx.x);
+}
+
+// every job of a kair_wgrad_grouped launch: block -> job by a scalar scan of the first blocks
+__global__ __launch_bounds__(256) void wgrad_finalize_grouped_kernel(const FinGroup g) {
+  const long b = blockIdx.x;
+  int ji = 0;
+  for (int i = 1; i < g.njobs; ++i)
+    if (g.j[i].blk0 <= b) ji = i;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  const FinJob& jb = g.j[ji];
+  finalize4_body(jb.part, g.splits, jb.mp, jb.grad, jb.bias, jb.ones_col, 0, jb.Kt, jb.plane, 1, b - jb.blk0);
 }
 
 // dst[token_to_win(t)] = scale(t) * src[t] (cast), 4 columns per thread
@@ -542,6 +558,12 @@ extern "C" int kair_pack_weights(const void* table_dev, int njobs, long nblocks,
   const kair_pack_job* jobs = (const kair_pack_job*)table_dev;
   const long* first = (const long*)((const char*)table_dev + (size_t)njobs * sizeof(kair_pack_job));
   hipLaunchKernelGGL(pack_batched_kernel, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs, first);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+int kair_launch_finalize_grouped(const FinGroup& g, hipStream_t s) {
+  hipLaunchKernelGGL(wgrad_finalize_grouped_kernel, dim3((unsigned)g.nblocks), dim3(256), 0, s, g);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

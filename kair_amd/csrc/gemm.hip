@@ -18,6 +18,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 
@@ -1062,32 +1063,32 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
 
 constexpr int TNR_BN = 192, TNR_BK = 192, TNR_RB = 32, TNR_NS = 6;
 
+// One CTA's share of a TN ring product: rows [mbeg, mend) of the (n0, k0) 192x192 tile -> plane P.
+struct TnRingTile {
+  const bf16* Ap; const bf16* Bp;
+  long Ald, Bld;
+  int N, K, M;                                  // M: operand rows (q/k/v part stride)
+  int n0, k0, mbeg, mend;
+  float* P;                                     // this split's fp32 [N][K] plane
+};
+
 template <int AMA>
-__global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
-                                                       int rows_per_split) {
+KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, char* smem) {
   constexpr int BNt = TNR_BN, BKt = TNR_BK, RB = TNR_RB, NS = TNR_NS;
   constexpr int PART = RB * BNt * 2;            // 12 KiB (A part; B part the same since BKt == BNt)
   constexpr int STAGE = 2 * PART;
   constexpr int ROWB = BNt * 2;                  // 384 B per LDS row
   constexpr int RN = 6, RK = 3;                  // wave tile 96 (n) x 48 (k)
-  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
-
-  const int cta = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = cta % ntiles, split = cta / ntiles;
-  const int tn = tile / tilesK, tk = tile - (tile / tilesK) * tilesK;
-  const int n0 = tn * BNt, k0 = tk * BKt;
-  const int mbeg = split * rows_per_split;
-  int mend = mbeg + rows_per_split;
-  if (mend > M) mend = M;
+  const int n0 = t.n0, k0 = t.k0, mbeg = t.mbeg, mend = t.mend, N = t.N, K = t.K, M = t.M;
   const int nchunks = mbeg < mend ? (mend - mbeg + RB - 1) / RB : 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wk = wave & 3;
 
   // operand bases as scalars: selecting A or B fields per lane below would otherwise read the
   // kernel-argument struct through a VGPR pointer (a global load + vmcnt(0) before every DMA)
-  const bf16* const Ap = (const bf16*)A.ptr;
-  const bf16* const Bp = (const bf16*)B.ptr;
-  const long Ald = A.ld, Bld = B.ld;
+  const bf16* const Ap = t.Ap;
+  const bf16* const Bp = t.Bp;
+  const long Ald = t.Ald, Bld = t.Bld;
   auto issue = [&](int j) {
     const int m0 = mbeg + j * RB;
     char* st = smem + (j % NS) * STAGE;
@@ -1109,8 +1110,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, in
             const int n = n0 + c, pw = A.d_pw.d;
             const int part = fdiv(n, A.d_pw), rr = n - part * pw;
             const int h = fdiv(rr, A.d_hdp), d = rr - h * A.hdp;
-            const int win = fdiv(m, A.d_tok), t = m - win * A.tok;
-            src = Ap + (long)part * M * pw + (((long)win * A.nh + h) * A.tok + t) * A.hdp + d;
+            const int win = fdiv(m, A.d_tok), tk = m - win * A.tok;
+            src = Ap + (long)part * M * pw + (((long)win * A.nh + h) * A.tok + tk) * A.hdp + d;
           }
         }
       }
@@ -1164,7 +1165,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, in
         acc[jk][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jk], af[i], acc[jk][i], 0, 0, 0);
   }
   // lane holds k = kb + 4*(lane>>4) + r (r < 4) of column n = nb + (lane & 15)
-  float* P = ws + (long)split * N * K;
+  float* P = t.P;
 #pragma unroll
   for (int jk = 0; jk < RK; ++jk)
 #pragma unroll
@@ -1173,6 +1174,64 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, in
       const int k = k0 + wk * 48 + jk * 16 + 4 * (lane >> 4);
       if (n < N && k < K) *(float4*)(P + (long)n * K + k) = make_float4(acc[jk][i][0], acc[jk][i][1], acc[jk][i][2], acc[jk][i][3]);
     }
+}
+
+template <int AMA>
+__global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
+                                                       int rows_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[TNR_NS * 2 * TNR_RB * TNR_BN * 2];
+  const int cta = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = cta % ntiles, split = cta / ntiles;
+  const int tn = tile / tilesK, tk = tile - (tile / tilesK) * tilesK;
+  TnRingTile t;
+  t.Ap = (const bf16*)A.ptr; t.Bp = (const bf16*)B.ptr;
+  t.Ald = A.ld; t.Bld = B.ld;
+  t.N = N; t.K = K; t.M = M;
+  t.n0 = tn * TNR_BN; t.k0 = tk * TNR_BK;
+  t.mbeg = split * rows_per_split;
+  t.mend = t.mbeg + rows_per_split < M ? t.mbeg + rows_per_split : M;
+  t.P = ws + (long)split * N * K;
+  tn_ring_body<AMA>(t, A, smem);
+}
+
+// ------------------------------------------------------------------------------------------
+// Grouped TN ring (kair_wgrad_grouped): the weight gradients of several layers in ONE launch.
+// Every job is a bf16 [M][N]^T x [M][K] product split into `splits` row ranges; CTA ->
+// (split, global tile) with the job found by a scalar scan of the tile offsets.  The job table is
+// the kernel argument (no device table: graph capture keeps the pointers by value).
+// ------------------------------------------------------------------------------------------
+constexpr int WG_MAX = 24;
+struct TnJob {
+  const bf16* a; const bf16* b; float* ws;      // ws: this job's [splits][N][K] planes
+  int lda, ldb, N, K, tilesK, tile0, qkv, pad;
+};
+struct TnGroup {
+  TnJob j[WG_MAX];
+  int njobs, ntiles, M, rps;
+  Op qa;                                        // q/k/v geometry shared by the QKVBLK jobs
+};
+
+__global__ __launch_bounds__(512, 1) void gemm_tn_ring_grouped(const TnGroup g) {
+  __shared__ __attribute__((aligned(16))) char smem[TNR_NS * 2 * TNR_RB * TNR_BN * 2];
+  const int cta = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = cta % g.ntiles, split = cta / g.ntiles;
+  int ji = 0;
+  for (int i = 1; i < g.njobs; ++i)
+    if (g.j[i].tile0 <= tile) ji = i;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  const TnJob& jb = g.j[ji];
+  const int lt = tile - jb.tile0;
+  const int tn = lt / jb.tilesK, tk = lt - (lt / jb.tilesK) * jb.tilesK;
+  TnRingTile t;
+  t.Ap = jb.a; t.Bp = jb.b;
+  t.Ald = jb.lda; t.Bld = jb.ldb;
+  t.N = jb.N; t.K = jb.K; t.M = g.M;
+  t.n0 = tn * TNR_BN; t.k0 = tk * TNR_BK;
+  t.mbeg = split * g.rps;
+  t.mend = t.mbeg + g.rps < g.M ? t.mbeg + g.rps : g.M;
+  t.P = jb.ws + (long)split * jb.N * jb.K;
+  if (jb.qkv) tn_ring_body<AM_QKV>(t, g.qa, smem);
+  else tn_ring_body<AM_ROWS>(t, g.qa, smem);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1889,4 +1948,82 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
   if (B->mode == KAIR_LD_ROWS) return launch_tn<float, float, float, AM_ROWS, AM_ROWS>(a, b, ws, splits, M, N, K, rps, s);
   if (B->mode == KAIR_LD_S2D) return launch_tn<float, float, float, AM_ROWS, AM_S2D>(a, b, ws, splits, M, N, K, rps, s);
   return launch_tn<float, float, float, AM_ROWS, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, s);
+}
+
+static int grouped_splits(long M, long tiles) {
+  if (g_num_cus == 0) init_num_cus();
+  long s = g_num_cus / (tiles > 0 ? tiles : 1);
+  const long maxs = (M + 255) / 256;   // >= 256 rows per split
+  if (s > maxs) s = maxs;
+  return (int)(s < 1 ? 1 : s);
+}
+
+static long grouped_tiles(const kair_wgrad_job* jobs, int njobs) {
+  long t = 0;
+  for (int i = 0; i < njobs; ++i) t += (long)((jobs[i].N + TNR_BN - 1) / TNR_BN) * ((jobs[i].K + TNR_BK - 1) / TNR_BK);
+  return t;
+}
+
+extern "C" long kair_wgrad_grouped_ws(const kair_wgrad_job* jobs, int njobs, long M) {
+  if (!jobs || njobs <= 0 || M <= 0) return 0;
+  const int splits = grouped_splits(M, grouped_tiles(jobs, njobs));
+  long nk = 0;
+  for (int i = 0; i < njobs; ++i) nk += (long)jobs[i].N * jobs[i].K;
+  return (long)splits * nk;
+}
+
+extern "C" int kair_wgrad_grouped(const kair_wgrad_job* jobs, int njobs, long M, float* ws, void* stream) {
+  KAIR_CHECK_ARG(jobs && ws && njobs > 0 && njobs <= KAIR_WG_MAX && M > 0 && M < (1L << 30),
+                 "wgrad_grouped: 1..%d jobs, M > 0 and a workspace", KAIR_WG_MAX);
+  KAIR_CHECK_ARG(((uintptr_t)ws % 16) == 0, "wgrad_grouped: workspace not 16-byte aligned");
+  int rc;
+  TnGroup g;
+  FinGroup f;
+  memset(&g, 0, sizeof(g));
+  memset(&f, 0, sizeof(f));
+  const long ntiles = grouped_tiles(jobs, njobs);
+  const int splits = grouped_splits(M, ntiles);
+  long rps = (M + splits - 1) / splits;
+  rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
+  int qkv_seen = 0;
+  long tile0 = 0, off = 0, blk0 = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const kair_wgrad_job& J = jobs[i];
+    if ((rc = check_operand(&J.A, "wgrad_grouped A"))) return rc;
+    if ((rc = check_operand(&J.B, "wgrad_grouped B"))) return rc;
+    KAIR_CHECK_ARG(J.A.dtype == KAIR_BF16 && J.B.dtype == KAIR_BF16, "wgrad_grouped: job %d operands must be bf16", i);
+    KAIR_CHECK_ARG((J.A.mode == KAIR_LD_ROWS || J.A.mode == KAIR_LD_QKVBLK) && J.B.mode == KAIR_LD_ROWS,
+                   "wgrad_grouped: job %d: A rows or q/k/v blocked, B rows", i);
+    KAIR_CHECK_ARG(!J.A.rowscale && !J.B.rowscale && J.A.win_ws == 0 && J.B.win_ws == 0 && J.A.ones_col < 0 &&
+                       (J.B.ones_col < 0 || J.B.ones_in_data),
+                   "wgrad_grouped: job %d: no row scale / window map / injected ones column", i);
+    KAIR_CHECK_ARG(tn_ring_shape(M, J.N, J.K) && (J.A.mode != KAIR_LD_ROWS || J.A.ld % 8 == 0) && J.B.ld % 8 == 0,
+                   "wgrad_grouped: job %d shape (N %d, K %d) / strides", i, J.N, J.K);
+    KAIR_CHECK_ARG(J.grad && J.map.kind == 0 && (long)J.map.nG * J.map.nGp == J.N && (long)J.map.kG * J.map.kGp == J.K,
+                   "wgrad_grouped: job %d needs a linear map whose packed dims are (N, K)", i);
+    KAIR_CHECK_ARG(!J.bias_grad || (J.ones_col >= 0 && J.ones_col < J.K), "wgrad_grouped: job %d bias needs ones_col", i);
+    if (J.A.mode == KAIR_LD_QKVBLK) {
+      if (!qkv_seen) g.qa = make_op(J.A, M);
+      KAIR_CHECK_ARG(!qkv_seen || (J.A.qkv_nh == g.qa.nh && J.A.qkv_hdp == g.qa.hdp && J.A.qkv_tok == g.qa.tok),
+                     "wgrad_grouped: q/k/v jobs must share one geometry");
+      qkv_seen = 1;
+    }
+    const int tilesK = (J.K + TNR_BK - 1) / TNR_BK;
+    TnJob& t = g.j[i];
+    t.a = (const bf16*)J.A.ptr; t.b = (const bf16*)J.B.ptr; t.ws = ws + off;
+    t.lda = (int)J.A.ld; t.ldb = (int)J.B.ld; t.N = J.N; t.K = J.K; t.tilesK = tilesK; t.tile0 = (int)tile0;
+    t.qkv = J.A.mode == KAIR_LD_QKVBLK;
+    tile0 += (long)((J.N + TNR_BN - 1) / TNR_BN) * tilesK;
+    FinJob& q = f.j[i];
+    q.part = ws + off; q.grad = J.grad; q.bias = J.bias_grad; q.mp = J.map; q.ones_col = J.bias_grad ? J.ones_col : -1;
+    q.Kt = J.K; q.plane = (long)J.N * J.K; q.blk0 = blk0;
+    blk0 += ((long)J.N * J.K / 4 + 63) / 64;
+    off += (long)splits * J.N * J.K;
+  }
+  g.njobs = njobs; g.ntiles = (int)ntiles; g.M = (int)M; g.rps = (int)rps;
+  f.njobs = njobs; f.splits = splits; f.nblocks = blk0;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gemm_tn_ring_grouped, dim3((unsigned)(ntiles * splits)), dim3(512), 0, s, g);
+  KAIR_CHECK_LAUNCH();
+  return kair_launch_finalize_grouped(f, s);
 }

@@ -63,7 +63,10 @@ def swinir_flops(net, Hh, Ww):
 class _Lin:
     """A linear layer's packed forms.  n/k groupings map reference rows/cols to padded ones."""
 
-    def __init__(self, eng, mod, n_grp, k_grp, frag=False, split=False, frag_t=False):
+    def __init__(self, eng, mod, n_grp, k_grp, frag=False, split=False, frag_t=False, rows=True):
+        """rows: pack the plain [Np][Kp] form (the unfused forward GEMM's operand); frag / frag_t: the
+        fragment-order forms of the fused forward / MLP-backward kernels, which replace [Np][Kp] /
+        [Kp][Np].  Forms no kernel of the engine reads are not packed (kair_pack_weights per step)."""
         self.w, self.b = mod.weight, mod.bias
         N, K = self.w.shape
         self.N, self.K = N, K
@@ -73,8 +76,8 @@ class _Lin:
         self.Np = n_grp[0] * n_grp[2]
         self.Kp = k_grp[0] * k_grp[2]
         dev = self.w.device
-        self.Wp = torch.empty(self.Np, self.Kp, device=dev, dtype=eng.tdt)
-        self.Wt = torch.empty(self.Kp, self.Np, device=dev, dtype=eng.tdt)
+        self.Wp = torch.empty(self.Np, self.Kp, device=dev, dtype=eng.tdt) if rows else None
+        self.Wt = torch.empty(self.Kp, self.Np, device=dev, dtype=eng.tdt) if not frag_t else None
         self.bp = torch.empty(self.Np, device=dev)
         # MFMA-fragment order of Wp for the fused block kernels: pack kind 10, or kind 12 (hi/lo
         # bf16 pairs, the same ~16-bit weight precision as the split convs) when split
@@ -88,7 +91,11 @@ class _Lin:
 
     def pack_jobs(self):
         w, b = self.w.detach(), self.b.detach()
-        jobs = [(w, self.Wp, self.map), (w, self.Wt, self.mapT), (b, self.bp, self.mapb)]
+        jobs = [(b, self.bp, self.mapb)]
+        if self.Wp is not None:
+            jobs.append((w, self.Wp, self.map))
+        if self.Wt is not None:
+            jobs.append((w, self.Wt, self.mapT))
         if self.Wg is not None:
             jobs.append((w, self.Wg, self.mapg))
         if self.Wgt is not None:
@@ -148,11 +155,11 @@ class _Blk:
         self.scale = blk.attn.scale
         Hd = blk.mlp.fc1.out_features
         sp = eng.split_linear
-        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=eng.fused_attn, split=sp)
-        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=eng.fused_attn, split=sp)
-        fb = eng.fused_mlp_bwd
-        self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp), frag=eng.fused_mlp, split=sp, frag_t=fb)
-        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=eng.fused_mlp, split=sp, frag_t=fb)
+        fa, fm, fb = eng.fused_attn, eng.fused_mlp, eng.fused_mlp_bwd
+        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=fa, split=sp, rows=not fa)
+        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=fa, split=sp, rows=not fa)
+        self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp), frag=fm, split=sp, frag_t=fb, rows=not fm)
+        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=fm, split=sp, frag_t=fb, rows=not fm)
 
     def linears(self):
         return (self.qkv, self.proj, self.fc1, self.fc2)
@@ -240,13 +247,13 @@ class SwinIREngine:
         self._packed_version = None
         self._pack_table = None
         self.seg_hook = None   # called between the gradient segments of backward() (grad_segments())
-        # KAIR_WGRAD_OVERLAP=1: Swin-block weight gradients on a side stream beside the data-gradient
-        # chain.  Off by default: measured 798 -> 737 patches/s at B=32 and 312 -> 305 at B=4 (the
-        # ring kernels hold one LDS-full CTA per CU, so the two streams cannot co-reside)
-        import os
-        self.wgrad_overlap = os.environ.get("KAIR_WGRAD_OVERLAP", "0") == "1"
-        self._side = None
-        self._ev_qkv = None
+        # Swin-block weight gradients: deferred to the end of each RSTB and issued as ONE grouped
+        # launch (kair_wgrad_grouped: 4 linears x depth blocks) where the bf16 TN ring takes the shapes;
+        # otherwise one gemm_tn + finalize per linear, issued in place
+        self.grouped_wgrad = (self.tdt == torch.bfloat16 and self.Cp > 64 and self.Hdp <= 576 and
+                              3 * self.nh * 32 <= 576 and
+                              max(len(l.residual_group.blocks) for l in net.layers) <= H.WgradGroup.WG_MAX // 4)
+        self._wg_pending = []
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -269,40 +276,6 @@ class SwinIREngine:
     def _segment_done(self):
         if self.seg_hook is not None:
             self.seg_hook()
-
-    # side stream for the block weight gradients --------------------------------------------
-    def _side_stream(self):
-        if not self.wgrad_overlap or not torch.cuda.is_available():
-            return None
-        if self._side is None:
-            self._side = torch.cuda.Stream()
-        return self._side
-
-    def _on_side(self, fn):
-        """Run fn (weight-gradient launches) on the side stream once everything issued so far on the
-        current stream is done; returns the event marking fn's completion (None: ran inline)."""
-        side = self._side_stream()
-        if side is None:
-            fn()
-            return None
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            fn()
-            ev = torch.cuda.Event()
-            ev.record(side)
-        return ev
-
-    @staticmethod
-    def _after(ev):
-        if ev is not None:
-            torch.cuda.current_stream().wait_event(ev)
-
-    def _join_side(self):
-        """The current stream waits for every side-stream launch (before the shared weight-gradient
-        workspace is used on the main stream, a gradient segment ends, or backward returns)."""
-        if self._side is not None:
-            torch.cuda.current_stream().wait_stream(self._side)
-        self._ev_qkv = None
 
     # ------------------------------------------------------------------------------------
     def convs(self):
@@ -373,12 +346,19 @@ class SwinIREngine:
             return P
         # backward scratch
         P["D"], P["G"] = e(M, Cp), e(M, Cp)
-        P["dU"], P["dxn"] = e(M, Hdp, dt=T), e(M, Cp, dt=T)
-        P["Dc"] = e(M, Cp, dt=T)   # compute-dtype GEMM operand copy of the residual-stream gradient
-        if self.fused_mlp_bwd:     # the attention branch's operand, written by the fused MLP backward
-            P["Dc2"] = e(M, Cp, dt=T)
+        P["dxn"] = e(M, Cp, dt=T)
+        if self.fused_mlp_bwd:
             P["mlp_ws"] = e(H.swin_mlp_bwd_ws())
-        P["dO"], P["dqkv"] = e(M, nh * 32, dt=T), e(3 * M * nh * 32, dt=T)
+        # per block position in an RSTB: the weight-gradient operands of that block, kept until the
+        # RSTB's grouped weight-gradient launch (Dm: s_mlp * dL/dout, token order; Da: s_attn * dL/dmid,
+        # window order -- the compute-dtype copies LayerNorm backward writes; dU: fc1 pre-activation
+        # gradient; dqkv: head-blocked q/k/v gradient)
+        # (zero-filled: the LayerNorm-backward copies write the C real columns only, the GEMMs read Cp)
+        depth = max(len(blks) for blks, _ in self.rstb)
+        z = lambda *s: torch.zeros(*s, device=dev, dtype=T)
+        P["gw"] = [{"Dm": z(M, Cp), "Da": z(M, Cp), "dU": e(M, Hdp, dt=T), "dqkv": e(3 * M * nh * 32, dt=T)}
+                   for _ in range(depth)]
+        P["dO"] = e(M, nh * 32, dt=T)
         P["ln_ws"] = e(2 * 2048 * Cp)   # kair_layernorm_bwd: 2 * 2048 * C floats
         P["attn_ws"] = e(H.window_attn_bwd_ws(nWin, nh))
         P["loss"] = e(1)
@@ -420,7 +400,13 @@ class SwinIREngine:
         return out
 
     def _max_wgrad_ws(self, M, P):
-        return max(H.wgrad_splits(m, n, k) * n * k for m, n, k in self._wgrad_shapes(M, P))
+        ws = max(H.wgrad_splits(m, n, k) * n * k for m, n, k in self._wgrad_shapes(M, P))
+        if self.grouped_wgrad:
+            Cp, Hdp, nh = self.Cp, self.Hdp, self.nh
+            depth = max(len(blks) for blks, _ in self.rstb)
+            shapes = [(Cp, Hdp), (Hdp, Cp), (Cp, nh * 32), (3 * nh * 32, Cp)] * depth
+            ws = max(ws, H.wgrad_grouped_ws(shapes, M))
+        return ws
 
     # ------------------------------------------------------------------------------------
     # forward
@@ -634,13 +620,14 @@ class SwinIREngine:
                         g(conv.b), self.C)
             # GEMM-operand copy of D for the last block's MLP branch: s_mlp * D in compute dtype
             drop = P["drop"]
-            H.row_copy(D, Cp, M, Cp, H.copy_desc(P["Dc"], rowscale=drop[bi - 1, 1] if drop is not None else None,
+            H.row_copy(D, Cp, M, Cp, H.copy_desc(P["gw"][len(blks) - 1]["Dm"],
+                                                 rowscale=drop[bi - 1, 1] if drop is not None else None,
                                                  rows_per_scale=Hh * Ww))
             for j in range(len(blks) - 1, -1, -1):
                 bi -= 1
                 x_in = P["blocks"][bi - 1]["out"] if j > 0 else (P["rstb_out"][gi - 1] if gi > 0 else P["s0"])
-                self._block_bwd(blks[j], P, P["blocks"][bi], x_in, D, bi, grads, copy_prev=j > 0)
-            self._join_side()   # the RSTB conv's weight gradient below shares the workspace
+                self._block_bwd(blks[j], P, P["blocks"][bi], x_in, D, bi, grads, j)
+            self._flush_wgrad(P)   # the RSTB's block weight gradients, before the conv's (shared workspace)
             H.axpy(G, D, 1.0)   # dL/du_g = skip + blocks path
             if gi > 0:
                 self._segment_done()   # RSTB gi's gradients are final (RSTB 0 joins the head segment)
@@ -652,65 +639,64 @@ class SwinIREngine:
         self._wgrad(P, H.rows(P["dfb"]), H.im2col(P["xin"], Hh, Ww, self.Cin_p, ones_col=self.in_ch), M, Cp,
                     9 * self.Cin_p, c.map, g(c.w), g(c.b), self.in_ch)
 
-    def _block_bwd(self, blk, P, S, x_in, D, bi, grads, copy_prev=False):
-        """D: dL/d out (fp32, token rows) -> updated in place to dL/d x_in.
+    def _wg(self, P, A, Bop, N, K, lin, grads, ones_col):
+        """One block linear's weight gradient: queued for the RSTB's grouped launch, or issued now."""
+        g_w, g_b = grads[lin.w], grads[lin.b]
+        if self.grouped_wgrad:
+            self._wg_pending.append((A, Bop, N, K, lin.map, g_w, g_b, ones_col))
+        else:
+            self._wgrad(P, A, Bop, P["M"], N, K, lin.map, g_w, g_b, ones_col)
 
-        P["Dc"] holds the compute-dtype GEMM operand copy of D: on entry s_mlp * D (token order);
-        LN2-backward rewrites it as s_attn * D_mid in window order (proj); LN1-backward, when the
-        previous block is in the same RSTB, as that block's s_mlp * D_in (token order)."""
+    def _flush_wgrad(self, P):
+        if self._wg_pending:
+            jobs, self._wg_pending = self._wg_pending, []
+            for i in range(0, len(jobs), H.WgradGroup.WG_MAX):
+                H.WgradGroup(jobs[i:i + H.WgradGroup.WG_MAX], P["M"]).run(P["wg_ws"])
+
+    def _block_bwd(self, blk, P, S, x_in, D, bi, grads, j):
+        """D: dL/d out (fp32, token rows) -> updated in place to dL/d x_in.  j: the block's position in
+        its RSTB; P["gw"][j] holds this block's weight-gradient operands until the RSTB's grouped
+        launch.  On entry gw[j]["Dm"] = s_mlp * D (compute dtype, token order); LN2 backward writes
+        gw[j]["Da"] = s_attn * D_mid (window order, proj operand); LN1 backward, when the previous block
+        is in the same RSTB, writes that block's gw[j - 1]["Dm"]."""
         cd, g = self.cd, (lambda p: grads[p])
         M, Cp, nh, Hh, Ww = P["M"], self.Cp, self.nh, P["H"], P["W"]
         HW = Hh * Ww
         win = (Hh, Ww, 8, blk.shift)
         drop = P["drop"]
         s_attn = drop[bi, 0] if drop is not None else None
-        s_mlp = drop[bi, 1] if drop is not None else None
         hd = self.C // nh
+        W = P["gw"][j]
+        Dm, Da, dU, dqkv = W["Dm"], W["Da"], W["dU"], W["dqkv"]
         # MLP: out = mid + s_mlp * fc2(gelu(fc1(LN2(mid))))
-        # Weight gradients go to the side stream (_on_side) as soon as their operands exist; the main
-        # stream waits for one only before it overwrites an operand that gradient still reads:
-        # Dc (LN2 / LN1 backward rewrite it), dU (the next block's fc2 dgrad), dqkv (the next
-        # block's attention backward).  Every kernel's arithmetic is unchanged (bit-identical).
-        Dc = P["Dc"]
         fc2, fc1 = blk.fc2, blk.fc1
         n = blk.n2
-        ev_fc2 = self._on_side(lambda: self._wgrad(P, H.rows(Dc), H.rows(S["h"], ones_col=fc2.K, ones_in_data=True), M,
-                                                   Cp, self.Hdp, fc2.map, g(fc2.w), g(fc2.b), fc2.K))
+        self._wg(P, H.rows(Dm), H.rows(S["h"], ones_col=fc2.K, ones_in_data=True), Cp, self.Hdp, fc2, grads, fc2.K)
         if self.fused_mlp_bwd:
-            # fc2 / fc1 input gradients + LN2 backward in one launch; the attention branch's operand goes
-            # to Dc2 (Dc is read by other tiles of the same launch)
-            H.swin_mlp_bwd(Dc, S["u"], fc2.Wgt, fc1.Wgt, P["dU"], S["mid"], n.weight, S["m2"], S["r2"], self.C, D, P["Dc2"],
+            # fc2 / fc1 input gradients + LN2 backward in one launch
+            H.swin_mlp_bwd(Dm, S["u"], fc2.Wgt, fc1.Wgt, dU, S["mid"], n.weight, S["m2"], S["r2"], self.C, D, Da,
                            s_attn, HW, Hh, Ww, blk.shift, g(n.weight), g(n.bias), P["mlp_ws"], M, Cp, self.Hdp)
-            Da = P["Dc2"]
         else:
             # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
-            H.gemm_nt(H.rows(Dc), H.rows(fc2.Wt), H.epilogue(P["dU"], gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
-        self._on_side(lambda: self._wgrad(P, H.rows(P["dU"]), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), M,
-                                          self.Hdp, Cp, fc1.map, g(fc1.w), g(fc1.b), self.C))
-        if not self.fused_mlp_bwd:
-            H.gemm_nt(H.rows(P["dU"]), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
-            self._after(ev_fc2)                  # LN2 backward rewrites Dc
+            H.gemm_nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
+            H.gemm_nt(H.rows(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
             H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, g(n.weight), g(n.bias),
-                            False, P["ln_ws"], M, self.C, copy=H.copy_desc(Dc, rowscale=s_attn, rows_per_scale=HW, win=win))
-            Da = Dc
+                            False, P["ln_ws"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win))
+        self._wg(P, H.rows(dU), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), self.Hdp, Cp, fc1, grads, self.C)
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         proj, qkv = blk.proj, blk.qkv
-        ev_proj = self._on_side(lambda: self._wgrad(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), M,
-                                                    Cp, nh * 32, proj.map, g(proj.w), g(proj.b), hd))
+        self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
         H.gemm_nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
-        self._after(self._ev_qkv)            # the previous block's qkv weight gradient still reads dqkv
-        H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], P["dqkv"], g(blk.table), False,
+        H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, g(blk.table), False,
                           P["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
-        self._ev_qkv = self._on_side(lambda: self._wgrad(P, H.qkvblk(P["dqkv"], nh),
-                                                         H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), M, qkv.Np,
-                                                         Cp, qkv.map, g(qkv.w), g(qkv.b), self.C))
-        H.gemm_nt(H.qkvblk(P["dqkv"], nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
+        self._wg(P, H.qkvblk(dqkv, nh), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads,
+                 self.C)
+        H.gemm_nt(H.qkvblk(dqkv, nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
         n = blk.n1
         cp = None
-        if copy_prev:
-            cp = H.copy_desc(Dc, rowscale=drop[bi - 1, 1] if drop is not None else None, rows_per_scale=HW)
-        self._after(ev_proj)                 # LN1 backward rewrites Dc (and the fc1 one is done: dU is free)
-        self._after(ev_fc2)
+        if j > 0:   # the previous block's MLP operand: s_mlp(prev) * dL/d x_in
+            cp = H.copy_desc(P["gw"][j - 1]["Dm"], rowscale=drop[bi - 1, 1] if drop is not None else None,
+                             rows_per_scale=HW)
         H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, g(n.weight), g(n.bias), False,
                         P["ln_ws"], M, self.C, win, copy=cp)
 
