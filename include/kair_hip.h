@@ -219,6 +219,16 @@ int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int dy_dtype, l
                        float* ws, long M, int C, int win_H, int win_W, int win_ws, int win_shift,
                        const kair_copy_desc* copy, void* stream);
 
+/* Deferred LayerNorm parameter gradients: kair_layernorm_bwd with dgamma = dbeta = NULL leaves its
+ * [kair_layernorm_bwd_blocks(M)][2C] partial sums in ws; one grouped launch then reduces several
+ * LayerNorms' partials (fixed order, the same sums as the immediate form): up to 32 jobs. */
+long kair_layernorm_bwd_blocks(long M);
+typedef struct {
+  const float* part; long nb; int C;
+  float* dgamma; float* dbeta; int accumulate;
+} kair_ln_param_job;
+int kair_ln_param_reduce_grouped(const kair_ln_param_job* jobs, int njobs, void* stream);
+
 /* Fused Swin window attention (network_swinir.py:114-145) for ws=8 (64 tokens), head_dim <= 32:
  *   O = softmax(q*scale @ k^T + table[relidx] + shift_mask) @ v   per (window, head).
  * qkv: head-blocked [3][nWin][nh][64][32] (dtype); table: fp32 [(2ws-1)^2][nh] (reference
@@ -237,6 +247,17 @@ int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* d
                          const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
                          float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
                          const float* mask, int mask_nw, void* stream);
+
+/* Deferred bias-table gradient: kair_window_attn_bwd with dtable = NULL leaves its per-group
+ * partials (kair_window_attn_bwd_groups() planes of [nh][64][64]) in ws; one grouped launch then
+ * reduces several blocks' partials into their dtable (+)= (network_swinir.py:94-98 gather, backward):
+ * up to 32 jobs, deterministic. */
+long kair_window_attn_bwd_groups(long nWin, int nh, int dtype);
+typedef struct {
+  const float* ws; long nWin; int nh; int dtype;
+  float* dtable; int accumulate;
+} kair_attn_dtable_job;
+int kair_attn_dtable_grouped(const kair_attn_dtable_job* jobs, int njobs, void* stream);
 
 /* Fused attention half of a Swin block (bf16; nh = 6 heads, C < 32*nh, window 8):
  *   out = x + rowscale * proj(W-MSA(LN1(x)))        network_swinir.py:239-272 + 114-145

@@ -73,6 +73,14 @@ class WgradJob(ctypes.Structure):
                 ("bias_grad", c_vp), ("ones_col", c_int)]
 
 
+class LnParamJob(ctypes.Structure):
+    _fields_ = [("part", c_vp), ("nb", c_long), ("C", c_int), ("dgamma", c_vp), ("dbeta", c_vp), ("accumulate", c_int)]
+
+
+class DtabJob(ctypes.Structure):
+    _fields_ = [("ws", c_vp), ("nWin", c_long), ("nh", c_int), ("dtype", c_int), ("dtable", c_vp), ("accumulate", c_int)]
+
+
 class PackJob(ctypes.Structure):
     _fields_ = [("src", c_vp), ("dst", c_vp), ("dst_dtype", c_int), ("reserved", c_int), ("map", WMap),
                 ("total", c_long)]
@@ -85,6 +93,10 @@ _SIGS = {
     "kair_gemm_tn": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), c_vp, c_int, c_long, c_int, c_int, c_int, c_vp],
     "kair_wgrad_grouped_ws": [ctypes.POINTER(WgradJob), c_int, c_long],
     "kair_wgrad_grouped": [ctypes.POINTER(WgradJob), c_int, c_long, c_vp, c_vp],
+    "kair_layernorm_bwd_blocks": [c_long],
+    "kair_ln_param_reduce_grouped": [ctypes.POINTER(LnParamJob), c_int, c_vp],
+    "kair_window_attn_bwd_groups": [c_long, c_int, c_int],
+    "kair_attn_dtable_grouped": [ctypes.POINTER(DtabJob), c_int, c_vp],
     "kair_pack_weight": [c_vp, c_vp, c_int, ctypes.POINTER(WMap), c_vp],
     "kair_pack_table_bytes": [c_int],
     "kair_pack_table_build": [ctypes.POINTER(PackJob), c_int, c_vp],
@@ -142,7 +154,7 @@ _SIGS = {
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
-_RESTYPE = {"kair_wgrad_grouped_ws": c_long, "kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
+_RESTYPE = {"kair_layernorm_bwd_blocks": c_long, "kair_window_attn_bwd_groups": c_long, "kair_wgrad_grouped_ws": c_long, "kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
             "kair_pack_table_build": c_long}
 
 _lib = None
@@ -411,6 +423,28 @@ def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, o
     mnw = mask.shape[0] if mask is not None else 0
     check(lib().kair_window_attn_fwd(ptr(qkv), dtype_code(qkv), ptr(table), ptr(O), ldo, ptr(lse), nWin, nh, hd, scale,
                                      H, W, shift, ones_col, ptr(mask), mnw, stream_ptr()), "window_attn_fwd")
+
+
+def layernorm_bwd_blocks(M):
+    return lib().kair_layernorm_bwd_blocks(M)
+
+
+def ln_param_reduce_grouped(jobs):
+    """jobs: (partials left by layernorm_bwd(dgamma=None, dbeta=None), M, C, dgamma, dbeta, accumulate)."""
+    arr = (LnParamJob * len(jobs))()
+    for i, (part, M, C, dg, db, acc) in enumerate(jobs):
+        arr[i].part, arr[i].nb, arr[i].C = ptr(part), layernorm_bwd_blocks(M), C
+        arr[i].dgamma, arr[i].dbeta, arr[i].accumulate = ptr(dg), ptr(db), int(acc)
+    check(lib().kair_ln_param_reduce_grouped(arr, len(jobs), stream_ptr()), "ln_param_reduce_grouped")
+
+
+def attn_dtable_grouped(jobs):
+    """jobs: (ws left by window_attn_bwd(dtable=None), nWin, nh, dtype code, dtable, accumulate)."""
+    arr = (DtabJob * len(jobs))()
+    for i, (ws, nWin, nh, dt, dtable, acc) in enumerate(jobs):
+        arr[i].ws, arr[i].nWin, arr[i].nh, arr[i].dtype = ptr(ws), nWin, nh, dt
+        arr[i].dtable, arr[i].accumulate = ptr(dtable), int(acc)
+    check(lib().kair_attn_dtable_grouped(arr, len(jobs), stream_ptr()), "attn_dtable_grouped")
 
 
 def window_attn_bwd_ws(nWin, nh):

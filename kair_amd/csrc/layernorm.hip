@@ -7,6 +7,8 @@
 // gradient and produces deterministic per-block partial sums for dgamma / dbeta.
 #include <stdlib.h>
 
+#include <string.h>
+
 #include "common.h"
 
 namespace {
@@ -229,9 +231,81 @@ __global__ __launch_bounds__(256) void ln_param_reduce(const float* __restrict__
   }
 }
 
+// every deferred LayerNorm parameter reduction of a group (kair_ln_param_reduce_grouped): block ->
+// job by a scalar scan; the same fixed-order sums as ln_param_reduce
+struct LnParamJob { const float* part; float* dgamma; float* dbeta; int nb, C, acc, blk0; };
+constexpr int LNP_MAX = 32;
+struct LnParamGroup { LnParamJob j[LNP_MAX]; int njobs; };
+
+__global__ __launch_bounds__(256) void ln_param_reduce_grouped(const LnParamGroup g) {
+  int ji = 0;
+  for (int i = 1; i < g.njobs; ++i)
+    if (g.j[i].blk0 <= (int)blockIdx.x) ji = i;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  const LnParamJob& jb = g.j[ji];
+  const int C = jb.C, nb = jb.nb;
+  const float* part = jb.part;
+  __shared__ float red[32][8];
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int c = ((int)blockIdx.x - jb.blk0) * 8 + tx;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < 2 * C) {
+    int b = ty;
+    for (; b + 224 < nb; b += 256) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)(b + 32 * u) * 2 * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        s0 += v[u];
+        s1 += v[u + 1];
+      }
+    }
+    for (; b + 32 < nb; b += 64) {
+      s0 += part[(long)b * 2 * C + c];
+      s1 += part[(long)(b + 32) * 2 * C + c];
+    }
+    if (b < nb) s0 += part[(long)b * 2 * C + c];
+  }
+  red[ty][tx] = s0 + s1;
+  __syncthreads();
+  if (ty == 0 && c < 2 * C) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) s += red[k][tx];
+    float* o = c < C ? jb.dgamma + c : jb.dbeta + (c - C);
+    *o = jb.acc ? *o + s : s;
+  }
+}
+
 }  // namespace
 
-constexpr int LN_BLOCKS = 2048;  // ws holds LN_BLOCKS * 2 * C floats (kair_hip.h)
+constexpr int LN_BLOCKS = 2048;
+
+static long ln_bwd_blocks(long M) {
+  long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;
+  return nb > LN_BLOCKS ? LN_BLOCKS : nb;
+}
+
+extern "C" long kair_layernorm_bwd_blocks(long M) { return M > 0 ? ln_bwd_blocks(M) : 0; }
+
+extern "C" int kair_ln_param_reduce_grouped(const kair_ln_param_job* jobs, int njobs, void* stream) {
+  KAIR_CHECK_ARG(jobs && njobs > 0 && njobs <= LNP_MAX, "ln_param_reduce_grouped: 1..%d jobs", LNP_MAX);
+  LnParamGroup g;
+  memset(&g, 0, sizeof(g));
+  int blk = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const kair_ln_param_job& J = jobs[i];
+    KAIR_CHECK_ARG(J.part && J.dgamma && J.dbeta && J.C > 0 && J.C <= 256 && J.nb > 0,
+                   "ln_param_reduce_grouped: job %d", i);
+    g.j[i] = LnParamJob{J.part, J.dgamma, J.dbeta, (int)J.nb, J.C, J.accumulate ? 1 : 0, blk};
+    blk += (2 * J.C + 7) / 8;
+  }
+  g.njobs = njobs;
+  hipLaunchKernelGGL(ln_param_reduce_grouped, dim3(blk), dim3(256), 0, (hipStream_t)stream, g);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}  // ws holds LN_BLOCKS * 2 * C floats (kair_hip.h)
 
 extern "C" int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype, long ldy, const float* gamma,
                                   const float* beta, float* mean, float* rstd, long M, int C, float eps, int win_H,
@@ -264,7 +338,8 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
                                   float* dgamma, float* dbeta, int dparam_accumulate, float* ws, long M, int C,
                                   int win_H, int win_W, int win_ws, int win_shift, const kair_copy_desc* copy,
                                   void* stream) {
-  KAIR_CHECK_ARG(x && dy && gamma && mean && rstd && dx_acc && dgamma && dbeta && ws, "layernorm_bwd: null pointer");
+  KAIR_CHECK_ARG(x && dy && gamma && mean && rstd && dx_acc && ws && (dgamma != nullptr) == (dbeta != nullptr),
+                 "layernorm_bwd: null pointer");
   KAIR_CHECK_ARG(C > 0 && C <= 256 && M > 0 && M < KAIR_MAX_MAPPED_ROWS, "layernorm_bwd: bad sizes");
   KAIR_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && ld_dx % 4 == 0, "layernorm_bwd: strides must be multiples of 4");
   const WinMap wm = make_winmap(win_H, win_W, win_ws, win_shift);
@@ -282,8 +357,7 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
     cwm = make_winmap(copy->win_H, copy->win_W, copy->win_ws, copy->win_shift);
   }
   hipStream_t s = (hipStream_t)stream;
-  long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;
-  if (nb > LN_BLOCKS) nb = LN_BLOCKS;
+  const long nb = ln_bwd_blocks(M);
   if (dy_dtype == KAIR_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const bf16*)dy, ldy, gamma,
                        mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm);
@@ -291,6 +365,7 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
     hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const float*)dy, ldy, gamma,
                        mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm);
   KAIR_CHECK_LAUNCH();
+  if (!dgamma) return 0;   // deferred: the [nb][2C] partials stay in ws for kair_ln_param_reduce_grouped
   hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 7) / 8), dim3(256), 0, s, ws, (int)nb, C, dgamma, dbeta,
                      dparam_accumulate);
   KAIR_CHECK_LAUNCH();

@@ -67,31 +67,39 @@ __global__ __launch_bounds__(256) void synth_sr_kernel(const float* __restrict__
   outL[u] = acc;
 }
 
-// Separable form, one workgroup per (sample, channel): the vertical bicubic pass for the patch's
-// LS L-rows over the source-column window the horizontal taps touch is staged in LDS once, then
-// every L pixel is P horizontal taps over it -- LS*W*P + LS*LS*P MACs instead of LS*LS*P*P, with
-// the same summation order as synth_sr_kernel (each vertical sum over a, then over bq), so the
-// output is bitwise the same.  The block also writes the (augmented) H crop.
+// Separable form, one workgroup per (sample, channel, band of L source rows): the vertical bicubic
+// pass for the band's L-rows over the source-column window the horizontal taps touch is staged in
+// LDS once, then every L pixel of the band is P horizontal taps over it -- LS*W*P + LS*LS*P MACs
+// instead of LS*LS*P*P, with the same summation order as synth_sr_kernel (each vertical sum over a,
+// then over bq), so the output is bitwise the same.  Bands split each sample's work over several
+// workgroups (a 4-patch batch would otherwise run on 12 CUs); each also writes its share of the
+// (augmented) H crop.  Outputs are addressed through the inverse augment map (dihedral: an
+// involution up to the transpose), so a band writes exactly the L pixels whose source row it holds.
 __global__ __launch_bounds__(256) void synth_sr_sep_kernel(const float* __restrict__ pool, int C, int Hs, int Ws,
                                                            const int4* __restrict__ par, int PS, int sf,
                                                            const float* __restrict__ wh, const int* __restrict__ ih,
                                                            const float* __restrict__ ww, const int* __restrict__ iw, int P,
-                                                           int Wmax, float* __restrict__ outH, float* __restrict__ outL) {
-  extern __shared__ float sV[];   // [LS][Wmax]
+                                                           int Wmax, int nband, float* __restrict__ outH,
+                                                           float* __restrict__ outL) {
+  extern __shared__ float sV[];   // [rows of the band][Wmax]
   __shared__ int sLo, sHi;
   const int tid = threadIdx.x;
-  const int b = blockIdx.x / C, c = blockIdx.x - (blockIdx.x / C) * C;
+  const int sc = blockIdx.x / nband, band = blockIdx.x - sc * nband;
+  const int b = sc / C, c = sc - (sc / C) * C;
   const int4 pr = par[b];   // x = image, y = rnd_h (LQ rows), z = rnd_w, w = mode
   const int LS = PS / sf;
+  const int rpb = (LS + nband - 1) / nband, r0 = band * rpb, r1 = min(LS, r0 + rpb), nr = r1 - r0;
   const float* img = pool + ((long)pr.x * C + c) * Hs * Ws;
-  // H crop
+  // this band's share of the H crop
   float* oH = outH + (long)(b * C + c) * PS * PS;
-  for (int t = tid; t < PS * PS; t += 256) {
+  const int hpb = (PS * PS + nband - 1) / nband, h0 = band * hpb, h1 = min(PS * PS, h0 + hpb);
+  for (int t = h0 + tid; t < h1; t += 256) {
     const int i = t / PS, j = t - (t / PS) * PS;
     int si, sj;
     aug_src(pr.w, i, j, PS, si, sj);
     oH[t] = img[(long)(pr.y * sf + si) * Ws + pr.z * sf + sj];
   }
+  if (nr <= 0) return;
   // source-column window of the horizontal taps of L columns pr.z .. pr.z + LS - 1
   if (tid == 0) { sLo = Ws; sHi = 0; }
   __syncthreads();
@@ -107,24 +115,24 @@ __global__ __launch_bounds__(256) void synth_sr_sep_kernel(const float* __restri
   lo = sLo;
   // W <= PS + P + 2 sf <= Wmax by the tap geometry (reflected indices fold inward); clamped anyway
   const int W = min(sHi - lo, Wmax);
-  // vertical pass: V[r][x - lo] = sum_a wh[gy][a] * img[ih[gy][a]][x], gy = pr.y + r
-  for (int t = tid; t < LS * W; t += 256) {
-    const int r = t / W, xo = t - (t / W) * W, gy = pr.y + r;
+  // vertical pass: V[r - r0][x - lo] = sum_a wh[gy][a] * img[ih[gy][a]][x], gy = pr.y + r
+  for (int t = tid; t < nr * W; t += 256) {
+    const int r = t / W, xo = t - (t / W) * W, gy = pr.y + r0 + r;
     float acc = 0.f;
     for (int a = 0; a < P; ++a) acc = fmaf(wh[gy * P + a], img[(long)ih[gy * P + a] * Ws + lo + xo], acc);
     sV[r * Wmax + xo] = acc;
   }
   __syncthreads();
-  // horizontal pass with the augment map on the output
+  // horizontal pass for source rows si in [r0, r1); output pixel through the inverse augment map
   float* oL = outL + (long)(b * C + c) * LS * LS;
-  for (int t = tid; t < LS * LS; t += 256) {
-    const int i = t / LS, j = t - (t / LS) * LS;
-    int si, sj;
-    aug_src(pr.w, i, j, LS, si, sj);
+  for (int t = tid; t < nr * LS; t += 256) {
+    const int si = r0 + t / LS, sj = t - (t / LS) * LS;
+    const int p = (pr.w & 2) ? LS - 1 - si : si, q = (pr.w & 4) ? LS - 1 - sj : sj;
+    const int i = (pr.w & 1) ? q : p, j = (pr.w & 1) ? p : q;
     const int gx = pr.z + sj;
     float acc = 0.f;
-    for (int bq = 0; bq < P; ++bq) acc = fmaf(ww[gx * P + bq], sV[si * Wmax + iw[gx * P + bq] - lo], acc);
-    oL[t] = acc;
+    for (int bq = 0; bq < P; ++bq) acc = fmaf(ww[gx * P + bq], sV[(si - r0) * Wmax + iw[gx * P + bq] - lo], acc);
+    oL[i * LS + j] = acc;
   }
 }
 
@@ -186,10 +194,14 @@ extern "C" int kair_synth_sr(const float* pool, int C, int Hs, int Ws, const int
   // span at most PS + 2P source columns (+ 2 sf of rounding slack)
   const int LS = PS / sf;
   const int Wmax = (PS + 2 * P + 2 * sf) < Ws ? (PS + 2 * P + 2 * sf) : Ws;
-  const size_t lds = (size_t)LS * Wmax * sizeof(float);
+  // bands of L rows: ~2048 workgroups over the batch (B = 4: one L row per band)
+  int nband = 2048 / (B * C);
+  nband = nband < 1 ? 1 : (nband > LS ? LS : nband);
+  const int rpb = (LS + nband - 1) / nband;
+  const size_t lds = (size_t)rpb * Wmax * sizeof(float);
   if (lds <= 60 * 1024) {
-    hipLaunchKernelGGL(synth_sr_sep_kernel, dim3((unsigned)(B * C)), dim3(256), lds, (hipStream_t)stream, pool, C, Hs, Ws,
-                       (const int4*)params, PS, sf, wh, ih, ww, iw, P, Wmax, outH, outL);
+    hipLaunchKernelGGL(synth_sr_sep_kernel, dim3((unsigned)(B * C * nband)), dim3(256), lds, (hipStream_t)stream, pool, C,
+                       Hs, Ws, (const int4*)params, PS, sf, wh, ih, ww, iw, P, Wmax, nband, outH, outL);
   } else {
     const long total = (long)B * C * PS * PS + (long)B * C * LS * LS;
     hipLaunchKernelGGL(synth_sr_kernel, dim3((unsigned)nblocks(total)), dim3(256), 0, (hipStream_t)stream, pool, C, Hs, Ws,

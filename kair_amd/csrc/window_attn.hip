@@ -12,6 +12,8 @@
 // and the shift mask are computed from indices (no 64x64 tables are read).
 #include <stdlib.h>
 
+#include <string.h>
+
 #include "common.h"
 
 namespace {
@@ -866,6 +868,44 @@ __global__ __launch_bounds__(256) void attn_dtable_kernel(const float* __restric
   if (lane == 0) dtable[idx * nh + h] = acc ? dtable[idx * nh + h] + v : v;
 }
 
+// Grouped bias-table gradient (kair_attn_dtable_grouped): the two stages above for every block of a
+// group, one launch per stage; a block finds its job by a scalar scan of the first-block offsets.
+struct DtabJob { const float* part; float* dtable; long ngroups; int nh, acc, blk0, blk1; };
+constexpr int DTAB_MAX = 32;
+struct DtabGroup { DtabJob j[DTAB_MAX]; int njobs; };
+
+KAIR_DEV int dtab_job(const DtabGroup& g, int b, bool second) {
+  int ji = 0;
+  for (int i = 1; i < g.njobs; ++i)
+    if ((second ? g.j[i].blk1 : g.j[i].blk0) <= b) ji = i;
+  return __builtin_amdgcn_readfirstlane(ji);
+}
+
+__global__ __launch_bounds__(1024) void attn_dbias_sum_grouped(const DtabGroup g) {
+  const DtabJob& jb = g.j[dtab_job(g, blockIdx.x, false)];
+  const long n = (long)jb.nh * TOK * TOK;
+  const long t = (long)(blockIdx.x - jb.blk0) * 64 + (threadIdx.x & 63);
+  const float s = split_sum16(jb.part, jb.ngroups, n, t, t < n);
+  if (t < n && threadIdx.x < 64) (const_cast<float*>(jb.part) + jb.ngroups * n)[t] = s;
+}
+
+__global__ __launch_bounds__(256) void attn_dtable_grouped(const DtabGroup g) {
+  const DtabJob& jb = g.j[dtab_job(g, blockIdx.x, true)];
+  const int nh = jb.nh;
+  const float* dB = jb.part + jb.ngroups * nh * TOK * TOK;
+  const int t = (blockIdx.x - jb.blk1) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nidx = (2 * WS - 1) * (2 * WS - 1);
+  if (t >= nidx * nh) return;
+  const int idx = t / nh, h = t - (t / nh) * nh;
+  const int dy = idx / (2 * WS - 1) - (WS - 1), dx = idx % (2 * WS - 1) - (WS - 1);
+  const int qy = lane >> 3, qx = lane & 7, ky = qy - dy, kx = qx - dx;
+  float v = 0.f;
+  if (ky >= 0 && ky < WS && kx >= 0 && kx < WS) v = dB[(long)h * TOK * TOK + lane * TOK + ky * WS + kx];
+  v = wave_sum(v);
+  if (lane == 0) jb.dtable[idx * nh + h] = jb.acc ? jb.dtable[idx * nh + h] + v : v;
+}
+
 constexpr int WPG = 4;  // windows per backward wave (fp32 parity path)
 
 // bf16 backward: windows per wave so that the (group, head) waves fill every CU's 4 wave slots in
@@ -931,7 +971,7 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
                                     float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
                                     const float* mask, int mask_nw, void* stream) {
   KAIR_CHECK_ARG(!mask || (mask_nw > 0 && shift == 0), "window_attn_bwd: an explicit mask needs mask_nw > 0 and shift 0");
-  KAIR_CHECK_ARG(qkv && O && dO && table && lse && dqkv && dtable && ws, "window_attn_bwd: null pointer");
+  KAIR_CHECK_ARG(qkv && O && dO && table && lse && dqkv && ws, "window_attn_bwd: null pointer");
   KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_bwd: head_dim");
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)), "window_attn_bwd: geometry");
   KAIR_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0, "window_attn_bwd: strides");
@@ -948,11 +988,39 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
     hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
                        ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw);
   KAIR_CHECK_LAUNCH();
+  if (!dtable) return 0;   // deferred: the per-group partials stay in ws for kair_attn_dtable_grouped
   float* dB = ws + ngroups * nh * TOK * TOK;
   hipLaunchKernelGGL(attn_dbias_sum_kernel, dim3((nh * TOK * TOK + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dB);
   KAIR_CHECK_LAUNCH();
   const int nt = (2 * WS - 1) * (2 * WS - 1) * nh;
   hipLaunchKernelGGL(attn_dtable_kernel, dim3((nt + 3) / 4), dim3(256), 0, s, dB, nh, dtable, dtable_accumulate);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" long kair_window_attn_bwd_groups(long nWin, int nh, int dtype) {
+  if (nWin <= 0 || nh <= 0) return 0;
+  return bwd_groups(nWin, dtype == KAIR_BF16 ? bwd_wpg_bf16(nWin, nh) : WPG);
+}
+
+extern "C" int kair_attn_dtable_grouped(const kair_attn_dtable_job* jobs, int njobs, void* stream) {
+  KAIR_CHECK_ARG(jobs && njobs > 0 && njobs <= DTAB_MAX, "attn_dtable_grouped: 1..%d jobs", DTAB_MAX);
+  DtabGroup g;
+  memset(&g, 0, sizeof(g));
+  int b0 = 0, b1 = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const kair_attn_dtable_job& J = jobs[i];
+    KAIR_CHECK_ARG(J.ws && J.dtable && J.nh > 0 && J.nWin > 0, "attn_dtable_grouped: job %d", i);
+    g.j[i] = DtabJob{J.ws, J.dtable, kair_window_attn_bwd_groups(J.nWin, J.nh, J.dtype), J.nh, J.accumulate ? 1 : 0,
+                     b0, b1};
+    b0 += (J.nh * TOK * TOK + 63) / 64;
+    b1 += ((2 * WS - 1) * (2 * WS - 1) * J.nh + 3) / 4;
+  }
+  g.njobs = njobs;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(attn_dbias_sum_grouped, dim3(b0), dim3(1024), 0, s, g);
+  KAIR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(attn_dtable_grouped, dim3(b1), dim3(256), 0, s, g);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

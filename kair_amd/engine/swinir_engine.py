@@ -254,6 +254,8 @@ class SwinIREngine:
                               3 * self.nh * 32 <= 576 and
                               max(len(l.residual_group.blocks) for l in net.layers) <= H.WgradGroup.WG_MAX // 4)
         self._wg_pending = []
+        self._lnp_pending = []    # (partials, M, C, dgamma, dbeta, accumulate) of the RSTB's LayerNorms
+        self._dtab_pending = []   # (partials, nWin, nh, dtype, dtable, accumulate) of its attention blocks
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -356,7 +358,10 @@ class SwinIREngine:
         # (zero-filled: the LayerNorm-backward copies write the C real columns only, the GEMMs read Cp)
         depth = max(len(blks) for blks, _ in self.rstb)
         z = lambda *s: torch.zeros(*s, device=dev, dtype=T)
-        P["gw"] = [{"Dm": z(M, Cp), "Da": z(M, Cp), "dU": e(M, Hdp, dt=T), "dqkv": e(3 * M * nh * 32, dt=T)}
+        P["gw"] = [{"Dm": z(M, Cp), "Da": z(M, Cp), "dU": e(M, Hdp, dt=T), "dqkv": e(3 * M * nh * 32, dt=T),
+                    # LN1 / LN2 parameter partials and the attention bias-table partials of the block, reduced
+                    # by one grouped launch each at the end of the RSTB
+                    "ln1p": e(2 * 2048 * Cp), "ln2p": e(2 * 2048 * Cp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
                    for _ in range(depth)]
         P["dO"] = e(M, nh * 32, dt=T)
         P["ln_ws"] = e(2 * 2048 * Cp)   # kair_layernorm_bwd: 2 * 2048 * C floats
@@ -652,6 +657,12 @@ class SwinIREngine:
             jobs, self._wg_pending = self._wg_pending, []
             for i in range(0, len(jobs), H.WgradGroup.WG_MAX):
                 H.WgradGroup(jobs[i:i + H.WgradGroup.WG_MAX], P["M"]).run(P["wg_ws"])
+        if self._lnp_pending:
+            jobs, self._lnp_pending = self._lnp_pending, []
+            H.ln_param_reduce_grouped(jobs)
+        if self._dtab_pending:
+            jobs, self._dtab_pending = self._dtab_pending, []
+            H.attn_dtable_grouped(jobs)
 
     def _block_bwd(self, blk, P, S, x_in, D, bi, grads, j):
         """D: dL/d out (fp32, token rows) -> updated in place to dL/d x_in.  j: the block's position in
@@ -680,15 +691,17 @@ class SwinIREngine:
             # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
             H.gemm_nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
             H.gemm_nt(H.rows(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
-            H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, g(n.weight), g(n.bias),
-                            False, P["ln_ws"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win))
+            H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, None, None, False,
+                            W["ln2p"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win))
+            self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False))
         self._wg(P, H.rows(dU), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), self.Hdp, Cp, fc1, grads, self.C)
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         proj, qkv = blk.proj, blk.qkv
         self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
         H.gemm_nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
-        H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, g(blk.table), False,
-                          P["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
+        H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
+                          W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
+        self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, self.cd, g(blk.table), False))
         self._wg(P, H.qkvblk(dqkv, nh), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads,
                  self.C)
         H.gemm_nt(H.qkvblk(dqkv, nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
@@ -697,8 +710,9 @@ class SwinIREngine:
         if j > 0:   # the previous block's MLP operand: s_mlp(prev) * dL/d x_in
             cp = H.copy_desc(P["gw"][j - 1]["Dm"], rowscale=drop[bi - 1, 1] if drop is not None else None,
                              rows_per_scale=HW)
-        H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, g(n.weight), g(n.bias), False,
-                        P["ln_ws"], M, self.C, win, copy=cp)
+        H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
+                        W["ln1p"], M, self.C, win, copy=cp)
+        self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False))
 
 
 class SwinIRFunction(torch.autograd.Function):
