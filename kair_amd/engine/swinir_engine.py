@@ -15,6 +15,7 @@ epilogue scatters back to token order.  PixelShuffle is a store remap of the ups
 The program is launch-only (no host syncs, no allocation after planning), so a whole training
 step can be captured in a HIP graph (kair_amd/engine/trainer.py).
 """
+import contextlib
 import math
 import weakref
 
@@ -256,6 +257,8 @@ class SwinIREngine:
         self._wg_pending = []
         self._lnp_pending = []    # (partials, M, C, dgamma, dbeta, accumulate) of the RSTB's LayerNorms
         self._dtab_pending = []   # (partials, nWin, nh, dtype, dtable, accumulate) of its attention blocks
+        self._conv_pending = []   # the RSTB conv's weight gradient (_wgrad arguments)
+        self._side = None         # side stream of the deferred per-RSTB gradient work
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -358,11 +361,13 @@ class SwinIREngine:
         # (zero-filled: the LayerNorm-backward copies write the C real columns only, the GEMMs read Cp)
         depth = max(len(blks) for blks, _ in self.rstb)
         z = lambda *s: torch.zeros(*s, device=dev, dtype=T)
-        P["gw"] = [{"Dm": z(M, Cp), "Da": z(M, Cp), "dU": e(M, Hdp, dt=T), "dqkv": e(3 * M * nh * 32, dt=T),
-                    # LN1 / LN2 parameter partials and the attention bias-table partials of the block, reduced
-                    # by one grouped launch each at the end of the RSTB
-                    "ln1p": e(2 * 2048 * Cp), "ln2p": e(2 * 2048 * Cp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
-                   for _ in range(depth)]
+        # Two sets (RSTB parity): the side stream still reads one RSTB's while the next RSTB writes the other.
+        P["gw"] = [[{"Dm": z(M, Cp), "Da": z(M, Cp), "dU": e(M, Hdp, dt=T), "dqkv": e(3 * M * nh * 32, dt=T),
+                     # LN1 / LN2 parameter partials and the attention bias-table partials of the block, reduced
+                     # by one grouped launch each at the end of the RSTB
+                     "ln1p": e(2 * 2048 * Cp), "ln2p": e(2 * 2048 * Cp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
+                    for _ in range(depth)] for _ in range(2)]
+        P["G3"] = e(M, Cp)   # third residual-gradient buffer (rotation, see backward())
         P["dO"] = e(M, nh * 32, dt=T)
         P["ln_ws"] = e(2 * 2048 * Cp)   # kair_layernorm_bwd: 2 * 2048 * C floats
         P["attn_ws"] = e(H.window_attn_bwd_ws(nWin, nh))
@@ -382,6 +387,7 @@ class SwinIREngine:
         P["dfb"] = e(M, Cp)
         # one shared wgrad workspace sized for the largest (splits * N * K)
         P["wg_ws"] = e(self._max_wgrad_ws(M, P))
+        P["wg_ws2"] = e(P["wg_ws"].numel()) if self.grouped_wgrad else None   # the side stream's
         return P
 
     def _wgrad_shapes(self, M, P):
@@ -520,9 +526,9 @@ class SwinIREngine:
     # ------------------------------------------------------------------------------------
     # backward
     # ------------------------------------------------------------------------------------
-    def _wgrad(self, P, A, Bop, M, N, K, layer_map, wgrad, bgrad=None, ones_col=-1):
+    def _wgrad(self, P, A, Bop, M, N, K, layer_map, wgrad, bgrad=None, ones_col=-1, ws=None):
         S = H.wgrad_splits(M, N, K)
-        ws = P["wg_ws"]
+        ws = P["wg_ws"] if ws is None else ws
         H.gemm_tn(A, Bop, ws, S, M, N, K, self.cd)
         H.wgrad_finalize(ws, S, layer_map, wgrad, bgrad, ones_col)
 
@@ -616,26 +622,44 @@ class SwinIREngine:
         self._segment_done()   # reconstruction tail + conv_after_body + norm gradients are final
         # G = dL/d u_G
         bi = len(self.blocks)
+        # Each RSTB's deferred gradient work (the grouped block weight gradients, LayerNorm-parameter and
+        # bias-table reductions, the RSTB conv's weight gradient) runs on a side stream beside the NEXT
+        # RSTB's data-gradient chain, and is joined at the end of that chain, where RSTB gi's gradient
+        # segment is reported (seg_hook: DDP bucket).  So that the chain never overwrites what the
+        # side stream still reads: the per-block operand sets alternate by RSTB parity (gw[gi % 2]) and
+        # the residual-stream gradient rotates through three buffers (the conv weight gradient reads the
+        # G that entered the RSTB; the chain two RSTBs later is the first to write that buffer again).
+        bufs = [G, D, P["G3"]]
+        side_open = False
         for gi in range(len(self.rstb) - 1, -1, -1):
             blks, conv = self.rstb[gi]
+            G, D, par = bufs[0], bufs[1], gi % 2
             t_d = P["blocks"][bi - 1]["out"]
             # u_{g+1} = conv(t_d) + u_g : conv dgrad -> D = dL/dt_d
             H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(conv.Wd), H.epilogue(D), M, Cp, 9 * Cp, cd)
-            self._wgrad(P, H.rows(G), H.im2col(t_d, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, conv.map, g(conv.w),
-                        g(conv.b), self.C)
+            self._conv_pending.append((H.rows(G), H.im2col(t_d, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, conv.map,
+                                       g(conv.w), g(conv.b), self.C))
             # GEMM-operand copy of D for the last block's MLP branch: s_mlp * D in compute dtype
             drop = P["drop"]
-            H.row_copy(D, Cp, M, Cp, H.copy_desc(P["gw"][len(blks) - 1]["Dm"],
+            H.row_copy(D, Cp, M, Cp, H.copy_desc(P["gw"][par][len(blks) - 1]["Dm"],
                                                  rowscale=drop[bi - 1, 1] if drop is not None else None,
                                                  rows_per_scale=Hh * Ww))
             for j in range(len(blks) - 1, -1, -1):
                 bi -= 1
                 x_in = P["blocks"][bi - 1]["out"] if j > 0 else (P["rstb_out"][gi - 1] if gi > 0 else P["s0"])
-                self._block_bwd(blks[j], P, P["blocks"][bi], x_in, D, bi, grads, j)
-            self._flush_wgrad(P)   # the RSTB's block weight gradients, before the conv's (shared workspace)
-            H.axpy(G, D, 1.0)   # dL/du_g = skip + blocks path
-            if gi > 0:
+                self._block_bwd(blks[j], P, P["blocks"][bi], x_in, D, bi, grads, j, par)
+            H.axpy(D, G, 1.0)   # dL/du_g = skip + blocks path (into D: G stays intact for the conv's wgrad)
+            bufs = [D, bufs[2], G]
+            if side_open:   # RSTB gi + 1's deferred work ran beside this chain: join, report its segment
+                torch.cuda.current_stream().wait_stream(self._side)
+                self._segment_done()
+                side_open = False
+            side_open = self._flush_deferred(P)
+            if not side_open and gi > 0:
                 self._segment_done()   # RSTB gi's gradients are final (RSTB 0 joins the head segment)
+        if side_open:
+            torch.cuda.current_stream().wait_stream(self._side)
+        G = bufs[0]
         # ---- patch_embed norm: s0 = LN(f0); f0 also feeds fb (long skip) --------------------
         n = self.pe_norm
         H.layernorm_bwd(P["f0"], Cp, G, Cp, n.weight, P["pe_mean"], P["pe_rstd"], P["dfb"], Cp, True, g(n.weight),
@@ -652,19 +676,33 @@ class SwinIREngine:
         else:
             self._wgrad(P, A, Bop, P["M"], N, K, lin.map, g_w, g_b, ones_col)
 
-    def _flush_wgrad(self, P):
-        if self._wg_pending:
-            jobs, self._wg_pending = self._wg_pending, []
-            for i in range(0, len(jobs), H.WgradGroup.WG_MAX):
-                H.WgradGroup(jobs[i:i + H.WgradGroup.WG_MAX], P["M"]).run(P["wg_ws"])
-        if self._lnp_pending:
-            jobs, self._lnp_pending = self._lnp_pending, []
-            H.ln_param_reduce_grouped(jobs)
-        if self._dtab_pending:
-            jobs, self._dtab_pending = self._dtab_pending, []
-            H.attn_dtable_grouped(jobs)
+    def _flush_deferred(self, P):
+        """Issue the RSTB's deferred gradient work: on the side stream when the block weight gradients
+        are grouped (returns True: the caller joins it), else in place on the current stream."""
+        side = None
+        if self.grouped_wgrad and torch.cuda.is_available():
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=self.device)
+            side = self._side
+            side.wait_stream(torch.cuda.current_stream())
+        ws = P["wg_ws2"] if side is not None else P["wg_ws"]
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            if self._wg_pending:
+                jobs, self._wg_pending = self._wg_pending, []
+                for i in range(0, len(jobs), H.WgradGroup.WG_MAX):
+                    H.WgradGroup(jobs[i:i + H.WgradGroup.WG_MAX], P["M"]).run(ws)
+            if self._lnp_pending:
+                jobs, self._lnp_pending = self._lnp_pending, []
+                H.ln_param_reduce_grouped(jobs)
+            if self._dtab_pending:
+                jobs, self._dtab_pending = self._dtab_pending, []
+                H.attn_dtable_grouped(jobs)
+            jobs, self._conv_pending = self._conv_pending, []
+            for A, Bop, M, N, K, m, gw, gb, oc in jobs:
+                self._wgrad(P, A, Bop, M, N, K, m, gw, gb, oc, ws=ws)
+        return side is not None
 
-    def _block_bwd(self, blk, P, S, x_in, D, bi, grads, j):
+    def _block_bwd(self, blk, P, S, x_in, D, bi, grads, j, par):
         """D: dL/d out (fp32, token rows) -> updated in place to dL/d x_in.  j: the block's position in
         its RSTB; P["gw"][j] holds this block's weight-gradient operands until the RSTB's grouped
         launch.  On entry gw[j]["Dm"] = s_mlp * D (compute dtype, token order); LN2 backward writes
@@ -677,7 +715,7 @@ class SwinIREngine:
         drop = P["drop"]
         s_attn = drop[bi, 0] if drop is not None else None
         hd = self.C // nh
-        W = P["gw"][j]
+        W = P["gw"][par][j]
         Dm, Da, dU, dqkv = W["Dm"], W["Da"], W["dU"], W["dqkv"]
         # MLP: out = mid + s_mlp * fc2(gelu(fc1(LN2(mid))))
         fc2, fc1 = blk.fc2, blk.fc1
@@ -708,7 +746,7 @@ class SwinIREngine:
         n = blk.n1
         cp = None
         if j > 0:   # the previous block's MLP operand: s_mlp(prev) * dL/d x_in
-            cp = H.copy_desc(P["gw"][j - 1]["Dm"], rowscale=drop[bi - 1, 1] if drop is not None else None,
+            cp = H.copy_desc(P["gw"][par][j - 1]["Dm"], rowscale=drop[bi - 1, 1] if drop is not None else None,
                              rows_per_scale=HW)
         H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
                         W["ln1p"], M, self.C, win, copy=cp)
