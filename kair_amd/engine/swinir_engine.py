@@ -630,13 +630,16 @@ class SwinIREngine:
         # the residual-stream gradient rotates through three buffers (the conv weight gradient reads the
         # G that entered the RSTB; the chain two RSTBs later is the first to write that buffer again).
         bufs = [G, D, P["G3"]]
-        side_open = False
+        side_open = side_pending = False
         for gi in range(len(self.rstb) - 1, -1, -1):
             blks, conv = self.rstb[gi]
             G, D, par = bufs[0], bufs[1], gi % 2
             t_d = P["blocks"][bi - 1]["out"]
             # u_{g+1} = conv(t_d) + u_g : conv dgrad -> D = dL/dt_d
             H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(conv.Wd), H.epilogue(D), M, Cp, 9 * Cp, cd)
+            if side_pending:   # RSTB gi + 1's deferred work, forked behind this conv (which it would starve)
+                side_open = self._flush_deferred(P)
+                side_pending = False
             self._conv_pending.append((H.rows(G), H.im2col(t_d, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, conv.map,
                                        g(conv.w), g(conv.b), self.C))
             # GEMM-operand copy of D for the last block's MLP branch: s_mlp * D in compute dtype
@@ -654,10 +657,15 @@ class SwinIREngine:
                 torch.cuda.current_stream().wait_stream(self._side)
                 self._segment_done()
                 side_open = False
-            side_open = self._flush_deferred(P)
-            if not side_open and gi > 0:
-                self._segment_done()   # RSTB gi's gradients are final (RSTB 0 joins the head segment)
-        if side_open:
+            if self.grouped_wgrad and torch.cuda.is_available():
+                side_pending = True     # forked at the next RSTB (or below, after the last one)
+            else:
+                self._flush_deferred(P)
+                if gi > 0:
+                    self._segment_done()   # RSTB gi's gradients are final (RSTB 0 joins the head segment)
+        if side_pending:
+            self._flush_deferred(P)
+        if side_pending or side_open:
             torch.cuda.current_stream().wait_stream(self._side)
         G = bufs[0]
         # ---- patch_embed norm: s0 = LN(f0); f0 also feeds fb (long skip) --------------------
