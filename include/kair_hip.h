@@ -74,7 +74,8 @@ typedef enum {
   KAIR_OUT_PUNSHUF = 3,   /* inverse: m = pixel of the [ps_H*r, ps_W*r] image, n = c
                              -> out[(b,y,x) of ps_H x ps_W][c*r*r+i*r+j], stride ldo          */
   KAIR_OUT_NCHW = 4,      /* image out[b][n][y][x] (n < img_C) of [img_H, img_W],
-                             value = v / img_range + img_mean[n]                              */
+                             value = v / img_range + img_mean[n] (+ resid[b][n][y][x] when resid
+                             is set: SwinIR's denoising head x + conv_last(res), v:831-835)   */
   KAIR_OUT_PSHUF_NCHW = 5, /* PixelShuffle(r) straight into an NCHW image [b][c][y*r+i][x*r+j]
                              (c < img_C), value = v / img_range + img_mean[c]  (UpsampleOneStep) */
   KAIR_OUT_PSHUF_SPM = 6, /* as PSHUF with the GEMM columns sub-pixel-major, n = (i*r+j)*(N/r^2) + c

@@ -433,12 +433,14 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
       }
       st1(e.out, e.odt, orow * e.ldo + oc, val);
     }
-  } else {  // NCHW image
+  } else {  // NCHW image; resid (optional): an NCHW image of the same shape added after the range
     const long hw = (long)e.imgH * e.imgW;
     const long b = m / hw;
     const long p = m - b * hw;
-    for (int j = 0; j < 8 && n + j < e.imgC && n + j < e.N; ++j)
-      ((float*)e.out)[(b * e.imgC + n + j) * hw + p] = v[j] / e.range + (e.mean ? e.mean[n + j] : 0.f);
+    for (int j = 0; j < 8 && n + j < e.imgC && n + j < e.N; ++j) {
+      const long o = (b * e.imgC + n + j) * hw + p;
+      ((float*)e.out)[o] = v[j] / e.range + (e.mean ? e.mean[n + j] : 0.f) + (e.resid ? e.resid[o] : 0.f);
+    }
   }
 }
 

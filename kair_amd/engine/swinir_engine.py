@@ -37,16 +37,27 @@ def swinir_flops(net, Hh, Ww):
     C = net.embed_dim
     HW = Hh * Ww
     f = 2 * HW * 9 * net.conv_first.in_channels * C                       # conv_first
+    def resi(m):   # '1conv' / '3conv' residual-connection convs
+        if isinstance(m, torch.nn.Sequential):
+            q = m[0].out_channels
+            return 2 * HW * (9 * C * q + q * q + 9 * q * C)
+        return 2 * HW * 9 * C * C
+
     for layer in net.layers:
         for blk in layer.residual_group.blocks:
             Hd = blk.mlp.fc1.out_features
             f += 2 * HW * C * 3 * C + 2 * HW * C * C                      # qkv, proj
             f += 2 * 2 * HW * (blk.window_size ** 2) * C                 # q k^T, p v
             f += 2 * 2 * HW * C * Hd                                     # fc1, fc2
-        f += 2 * HW * 9 * C * C                                           # RSTB conv
-    f += 2 * HW * 9 * C * C                                               # conv_after_body
+        f += resi(layer.conv)                                             # RSTB conv
+    f += resi(net.conv_after_body)                                        # conv_after_body
     first_dgrad = 2 * HW * 9 * net.conv_first.in_channels * C
-    if net.upsampler == "pixelshuffle":
+    if net.upsampler == "nearest+conv":
+        nf = 64
+        f += 2 * HW * 9 * C * nf + 2 * (4 * HW + 16 * HW + 16 * HW) * 9 * nf * nf + 2 * 16 * HW * 9 * nf * net.conv_last.out_channels
+    elif net.upsampler in (None, ""):
+        f += 2 * HW * 9 * C * net.conv_last.out_channels
+    elif net.upsampler == "pixelshuffle":
         nf = 64
         f += 2 * HW * 9 * C * nf
         hw = HW
@@ -69,7 +80,7 @@ class _Lin:
         fragment-order forms of the fused forward / MLP-backward kernels, which replace [Np][Kp] /
         [Kp][Np].  Forms no kernel of the engine reads are not packed (kair_pack_weights per step)."""
         self.w, self.b = mod.weight, mod.bias
-        N, K = self.w.shape
+        N, K = self.w.shape[:2]      # nn.Linear [N, K] or a 1x1 nn.Conv2d [N, K, 1, 1]
         self.N, self.K = N, K
         self.map = H.wmap(0, N, K, n_grp, k_grp)
         self.mapT = H.wmap(3, N, K, n_grp, k_grp)
@@ -142,6 +153,29 @@ class _Conv:
         if self.Wd is not None:
             jobs.append((w, self.Wd, self.mapd))
         return jobs
+
+
+class _Resi3:
+    """resi_connection '3conv' (network_swinir.py:466-471, 730-737): 3x3 C->C/4 + LeakyReLU 0.2 ->
+    1x1 C/4->C/4 + LeakyReLU 0.2 -> 3x3 C/4->C, the bottleneck width padded to Cq (multiple of 8).
+    The LeakyReLU is the producing GEMM's epilogue; backward gates each input gradient in the
+    dgrad epilogue with LeakyReLU' read from the saved post-activation (same sign)."""
+
+    def __init__(self, eng, seq):
+        C = seq[0].in_channels
+        q = seq[0].out_channels
+        self.q, self.Cq = q, _rup(q, 8)
+        self.c1 = _Conv(eng, seq[0], self.Cq, eng.Cp)
+        self.c2 = _Lin(eng, seq[2], (1, q, self.Cq), (1, q, self.Cq))
+        self.c3 = _Conv(eng, seq[4], eng.Cp, self.Cq)
+        assert C == eng.C and seq[4].out_channels == C
+
+    def pack_jobs(self):
+        return self.c1.pack_jobs() + self.c2.pack_jobs() + self.c3.pack_jobs()
+
+
+def _resi(eng, m):
+    return _Resi3(eng, m) if isinstance(m, torch.nn.Sequential) else _Conv(eng, m, eng.Cp, eng.Cp)
 
 
 class _Blk:
@@ -224,9 +258,9 @@ class SwinIREngine:
         self.rstb = []
         for layer in net.layers:
             blks = [_Blk(self, b) for b in layer.residual_group.blocks]
-            self.rstb.append((blks, _Conv(self, layer.conv, self.Cp, self.Cp)))
+            self.rstb.append((blks, _resi(self, layer.conv)))
         self.norm = net.norm
-        self.cab = _Conv(self, net.conv_after_body, self.Cp, self.Cp)
+        self.cab = _resi(self, net.conv_after_body)
         nf = 64
         if self.upsampler == "pixelshuffle":
             self.cbu = _Conv(self, net.conv_before_upsample[0], nf, self.Cp)
@@ -240,6 +274,13 @@ class SwinIREngine:
             conv = net.upsample[0]
             self.ups_r = [self.scale]
             self.up1 = _Conv(self, conv, _rup(conv.out_channels, 16), self.Cp)
+        elif self.upsampler == "nearest+conv":   # x4: two nearest x2 + conv + LeakyReLU 0.2, conv_hr, conv_last
+            self.cbu = _Conv(self, net.conv_before_upsample[0], nf, self.Cp)
+            self.nup = [_Conv(self, net.conv_up1, nf, nf), _Conv(self, net.conv_up2, nf, nf)]
+            self.hrc = _Conv(self, net.conv_hr, nf, nf)
+            self.last = _Conv(self, net.conv_last, 16, nf)
+        elif self.upsampler in (None, ""):        # denoising / JPEG: E = x + conv_last(res)
+            self.last = _Conv(self, net.conv_last, 16, self.Cp)
         else:
             raise NotImplementedError(self.upsampler)
         self.blocks = [b for blks, _ in self.rstb for b in blks]
@@ -269,6 +310,11 @@ class SwinIREngine:
         if self.upsampler == "pixelshuffle":
             tail += (list(net.conv_before_upsample.parameters()) + list(net.upsample.parameters()) +
                      list(net.conv_last.parameters()))
+        elif self.upsampler == "nearest+conv":
+            tail += [p for m in (net.conv_before_upsample, net.conv_up1, net.conv_up2, net.conv_hr, net.conv_last)
+                     for p in m.parameters()]
+        elif self.upsampler in (None, ""):
+            tail += list(net.conv_last.parameters())
         else:
             tail += list(net.upsample.parameters())
         segs = [tail]
@@ -287,6 +333,10 @@ class SwinIREngine:
         cs = [self.conv_first] + [c for _, c in self.rstb] + [self.cab]
         if self.upsampler == "pixelshuffle":
             cs += [self.cbu] + self.ups + [self.last]
+        elif self.upsampler == "nearest+conv":
+            cs += [self.cbu] + self.nup + [self.hrc, self.last]
+        elif self.upsampler in (None, ""):
+            cs += [self.last]
         else:
             cs += [self.up1]
         return cs
@@ -345,6 +395,15 @@ class SwinIREngine:
                 acts.append(e(hw, nf, dt=T))
             P["ups_act"] = acts
             P["M_hr"] = hw
+        elif self.upsampler == "nearest+conv":
+            nf = 64
+            P["a0"] = e(M, nf, dt=T)
+            P["nup_act"] = [e(4 * M, nf, dt=T), e(16 * M, nf, dt=T)]
+            P["nhr"] = e(16 * M, nf, dt=T)
+            P["M_hr"] = 16 * M
+        # '3conv' bottleneck activations (post-LeakyReLU, compute dtype) of every residual connection
+        P["r3"] = {id(r): (e(M, r.Cq, dt=T), e(M, r.Cq, dt=T)) for r in [c for _, c in self.rstb] + [self.cab]
+                   if isinstance(r, _Resi3)}
         P["E"] = e(B, self.in_ch, Hh * self.scale, Ww * self.scale)
         P["infer"] = infer
         if infer:
@@ -382,8 +441,19 @@ class SwinIREngine:
                 hw *= c.Co // 64
             P["dpre"] = dpre
             P["da0"] = e(M, 64, dt=T)
+        elif self.upsampler == "nearest+conv":
+            nf = 64
+            P["dE"] = e(16 * M, 16, dt=T)
+            P["dz_hr"], P["dz_u"] = e(16 * M, nf, dt=T), e(16 * M, nf, dt=T)
+            P["G_hi"], P["G_lo"] = e(16 * M, nf), e(4 * M, nf)
+            P["da0"] = e(M, nf, dt=T)
+        elif self.upsampler in (None, ""):
+            P["dE"] = e(M, 16, dt=T)
         else:
             P["dE"] = e(M, self.up1.Cop, dt=T)
+        if P["r3"]:
+            q = max(r.Cq for r in [c for _, c in self.rstb] + [self.cab] if isinstance(r, _Resi3))
+            P["r3_dz"] = (e(M, q, dt=T), e(M, q, dt=T))
         P["dfb"] = e(M, Cp)
         # one shared wgrad workspace sized for the largest (splits * N * K)
         P["wg_ws"] = e(self._max_wgrad_ws(M, P))
@@ -394,12 +464,23 @@ class SwinIREngine:
         """(M_rows, N, K) of every weight-gradient GEMM in the step."""
         Cp, Hdp, nh = self.Cp, self.Hdp, self.nh
         out = [(M, Cp, 9 * self.Cin_p)]
+
+        def resi(r):
+            if isinstance(r, _Resi3):
+                return [(M, r.Cq, 9 * Cp), (M, r.Cq, r.Cq), (M, Cp, 9 * r.Cq)]
+            return [(M, Cp, 9 * Cp)]
+
         for blks, conv in self.rstb:
             for _ in blks:
                 out += [(M, Cp, Hdp), (M, Hdp, Cp), (M, Cp, nh * 32), (M, 3 * nh * 32, Cp)]
-            out.append((M, Cp, 9 * Cp))
-        out.append((M, Cp, 9 * Cp))
-        if self.upsampler == "pixelshuffle":
+            out += resi(conv)
+        out += resi(self.cab)
+        if self.upsampler == "nearest+conv":
+            out += [(M, 64, 9 * Cp), (4 * M, 64, 9 * 64), (16 * M, 64, 9 * 64), (16 * M, 64, 9 * 64),
+                    (16 * M, 16, 9 * 64)]
+        elif self.upsampler in (None, ""):
+            out.append((M, 16, 9 * Cp))
+        elif self.upsampler == "pixelshuffle":
             out.append((M, 64, 9 * Cp))
             hw = M
             for c in self.ups:
@@ -449,14 +530,52 @@ class SwinIREngine:
                 cur = self._block_fwd(blk, P, P["blocks"][bi], cur, bi)
                 bi += 1
             out = P["rstb_out"][gi]
-            H.gemm_nt(H.im2col(cur, Hh, Ww, Cp), conv.fwd(), H.epilogue(out, bias=conv.bp, resid=g_in), M, Cp,
-                      9 * Cp, cd)
+            self._resi_fwd(conv, P, cur, out, g_in)
             cur = out
         n = self.norm
         H.layernorm_fwd(cur, Cp, P["nf"], Cp, n.weight, n.bias, P["n_mean"], P["n_rstd"], M, self.C, n.eps)
-        H.gemm_nt(H.im2col(P["nf"], Hh, Ww, Cp), self.cab.fwd(), H.epilogue(P["fb"], bias=self.cab.bp, resid=P["f0"]),
-                  M, Cp, 9 * Cp, cd)
+        self._resi_fwd(self.cab, P, P["nf"], P["fb"], P["f0"])
         return self._forward_tail(P)
+
+    def _resi_fwd(self, r, P, src, out, resid):
+        """out = resi_conv(src) + resid (fp32 token rows, Cp columns)."""
+        cd, Cp, M, Hh, Ww = self.cd, self.Cp, P["M"], P["H"], P["W"]
+        if not isinstance(r, _Resi3):
+            H.gemm_nt(H.im2col(src, Hh, Ww, Cp), r.fwd(), H.epilogue(out, bias=r.bp, resid=resid), M, Cp, 9 * Cp, cd)
+            return
+        t1, t2 = P["r3"][id(r)]
+        lk = dict(act=H.ACT_LEAKY, slope=0.2)
+        H.gemm_nt(H.im2col(src, Hh, Ww, Cp), r.c1.fwd(), H.epilogue(t1, bias=r.c1.bp, **lk), M, r.Cq, 9 * Cp, cd)
+        H.gemm_nt(H.rows(t1), H.rows(r.c2.Wp), H.epilogue(t2, bias=r.c2.bp, **lk), M, r.Cq, r.Cq, cd)
+        H.gemm_nt(H.im2col(t2, Hh, Ww, r.Cq), r.c3.fwd(), H.epilogue(out, bias=r.c3.bp, resid=resid), M, Cp, 9 * r.Cq, cd)
+
+    def _resi_bwd(self, r, P, G, src, D, grads):
+        """resi_conv backward for out = resi_conv(src) + resid: G = dL/d out (fp32 rows) -> D = dL/d src
+        (the conv path only; the caller adds the skip).  '1conv' returns its weight-gradient job for
+        the deferred per-RSTB work; '3conv' issues its weight gradients here."""
+        cd, Cp, M, Hh, Ww = self.cd, self.Cp, P["M"], P["H"], P["W"]
+        g = lambda p: grads[p]
+        if not isinstance(r, _Resi3):
+            H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.Wd), H.epilogue(D), M, Cp, 9 * Cp, cd)
+            return (H.rows(G), H.im2col(src, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, r.map, g(r.w), g(r.b), self.C)
+        t1, t2 = P["r3"][id(r)]
+        q = r.Cq
+        lk = dict(gate_kind=2, slope=0.2)
+        # 3x3 Cq -> C: dL/d t2, gated by LeakyReLU'(t2 pre-activation)
+        dz2 = P["r3_dz"][0].view(-1)[:M * q].view(M, q)
+        dz1 = P["r3_dz"][1].view(-1)[:M * q].view(M, q)
+        H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.c3.Wd), H.epilogue(dz2, gate=t2, **lk), M, q, 9 * Cp, cd)
+        self._wgrad(P, H.rows(G), H.im2col(t2, Hh, Ww, q), M, Cp, 9 * q, r.c3.map, g(r.c3.w))
+        self._bias_colsum(P, H.rows(G), M, Cp, r.c3.mapb, g(r.c3.b))
+        # 1x1 Cq -> Cq
+        H.gemm_nt(H.rows(dz2), H.rows(r.c2.Wt), H.epilogue(dz1, gate=t1, **lk), M, q, q, cd)
+        self._wgrad(P, H.rows(dz2), H.rows(t1), M, q, q, r.c2.map, g(r.c2.w))
+        self._bias_colsum(P, H.rows(dz2), M, q, r.c2.mapb, g(r.c2.b))
+        # 3x3 C -> Cq
+        H.gemm_nt(H.im2col(dz1, Hh, Ww, q, flip=True), H.rows(r.c1.Wd), H.epilogue(D), M, Cp, 9 * q, cd)
+        self._wgrad(P, H.rows(dz1), H.im2col(src, Hh, Ww, Cp), M, q, 9 * Cp, r.c1.map, g(r.c1.w))
+        self._bias_colsum(P, H.rows(dz1), M, q, r.c1.mapb, g(r.c1.b))
+        return None
 
     def _forward_tail(self, P):
         """Reconstruction tail: P['fb'] (conv_after_body + residual) -> P['E']."""
@@ -474,6 +593,29 @@ class SwinIREngine:
             H.gemm_nt(H.im2col(src, h, w, 64), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(self.mean, self.img_range, self.in_ch, h, w)),
                       B * h * w, c.Cop, 9 * 64, cd)
+        elif self.upsampler == "nearest+conv":
+            c = self.cbu
+            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
+                      H.epilogue(P["a0"], bias=c.bp, act=H.ACT_LEAKY, slope=0.01), M, 64, 9 * Cp, cd)
+            src, h, w = P["a0"], Hh, Ww
+            for c, dst in zip(self.nup, P["nup_act"]):   # lrelu(conv(nearest x2)): im2col reads through the upsample
+                h, w = 2 * h, 2 * w
+                H.gemm_nt(H.im2col(src, h, w, 64, up=2), c.fwd(), H.epilogue(dst, bias=c.bp, act=H.ACT_LEAKY, slope=0.2),
+                          B * h * w, 64, 9 * 64, cd)
+                src = dst
+            c = self.hrc
+            H.gemm_nt(H.im2col(src, h, w, 64), c.fwd(), H.epilogue(P["nhr"], bias=c.bp, act=H.ACT_LEAKY, slope=0.2),
+                      B * h * w, 64, 9 * 64, cd)
+            c = self.last
+            H.gemm_nt(H.im2col(P["nhr"], h, w, 64), c.fwd(),
+                      H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(self.mean, self.img_range, self.in_ch, h, w)),
+                      B * h * w, c.Cop, 9 * 64, cd)
+        elif self.upsampler in (None, ""):
+            # x/range + mean with x = (x_in - mean) * range + conv_last(res)  ==  x_in + conv_last(res) / range
+            c = self.last
+            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
+                      H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, resid=P["x"],
+                                 img=(None, self.img_range, self.in_ch, Hh, Ww)), M, c.Cop, 9 * Cp, cd)
         else:
             c = self.up1
             H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
@@ -540,12 +682,17 @@ class SwinIREngine:
         Returns the device loss tensor [1]."""
         P = self.cur
         B, Hh, Ww = P["B"], P["H"], P["W"]
-        if self.upsampler == "pixelshuffle":
-            H.l1_loss(P["E"], H_img, P["loss"], P["dE"], 16, loss_weight, B, self.in_ch, Hh * self.scale, Ww * self.scale,
-                      P["loss_ws"])
-        else:
-            H.l1_loss(P["E"], H_img, P["loss"], P["dE"], self.up1.Cop, loss_weight, B, self.in_ch, Hh * self.scale,
+        # E = v / img_range + ...: dL/dv = dL/dE / img_range, folded into the loss kernel's gradient scale
+        # (which also scales the reported loss, undone below)
+        wr = loss_weight / self.img_range
+        if self.upsampler == "pixelshuffledirect":
+            H.l1_loss(P["E"], H_img, P["loss"], P["dE"], self.up1.Cop, wr, B, self.in_ch, Hh * self.scale,
                       Ww * self.scale, P["loss_ws"], ps_r=self.scale)
+        else:
+            H.l1_loss(P["E"], H_img, P["loss"], P["dE"], 16, wr, B, self.in_ch, Hh * self.scale, Ww * self.scale,
+                      P["loss_ws"])
+        if self.img_range != 1.0:
+            P["loss"].mul_(self.img_range)
         self.backward(grads, P)
         return P["loss"]
 
@@ -555,11 +702,12 @@ class SwinIREngine:
         B, Hh, Ww = P["B"], P["H"], P["W"]
         # dE = gE through the same layout the loss kernel writes: reuse l1 machinery is not possible,
         # so scatter with the image->nhwc kernel (channel stride / pre-shuffle layout).
-        if self.upsampler == "pixelshuffle":
-            H.image_to_nhwc(gE.contiguous(), P["dE"], 16, None, 1.0, B, self.in_ch, Hh * self.scale, Ww * self.scale)
+        inv = 1.0 / self.img_range   # E = v / img_range + ...
+        if self.upsampler != "pixelshuffledirect":
+            H.image_to_nhwc(gE.contiguous(), P["dE"], 16, None, inv, B, self.in_ch, Hh * self.scale, Ww * self.scale)
         else:
             tmp = torch.nn.functional.pixel_unshuffle(gE.contiguous(), self.scale)   # [B, C*r*r, H, W]
-            H.image_to_nhwc(tmp.contiguous(), P["dE"], self.up1.Cop, None, 1.0, B, tmp.shape[1], Hh, Ww)
+            H.image_to_nhwc(tmp.contiguous(), P["dE"], self.up1.Cop, None, inv, B, tmp.shape[1], Hh, Ww)
         self.backward(grads, P)
 
     def backward(self, grads, P):
@@ -603,17 +751,18 @@ class SwinIREngine:
             H.gemm_nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)
             self._wgrad(P, H.rows(P["da0"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, 64, 9 * Cp, c.map,
                         g(c.w), g(c.b), self.C)
-        else:
-            c = self.up1
+        elif self.upsampler == "nearest+conv":
+            self._nearest_tail_bwd(P, grads)
+        else:   # pixelshuffledirect (one conv + PixelShuffle) or the denoising conv_last (E = x + conv_last / range)
+            c = self.up1 if self.upsampler == "pixelshuffledirect" else self.last
             H.gemm_nt(H.im2col(P["dE"], Hh, Ww, c.Cop, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * c.Cop, cd)
             self._wgrad(P, H.rows(P["dE"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, c.Cop, 9 * Cp, c.map,
                         g(c.w), g(c.b), self.C)
         # ---- conv_after_body (fb = cab(nf) + f0) ------------------------------------------
-        c = self.cab
         G, D = P["G"], P["D"]
-        H.gemm_nt(H.im2col(P["dfb"], Hh, Ww, Cp, flip=True), H.rows(c.Wd), H.epilogue(D), M, Cp, 9 * Cp, cd)
-        self._wgrad(P, H.rows(P["dfb"]), H.im2col(P["nf"], Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, c.map, g(c.w),
-                    g(c.b), self.C)
+        job = self._resi_bwd(self.cab, P, P["dfb"], P["nf"], D, grads)
+        if job is not None:
+            self._wgrad(P, *job)
         # ---- final norm: nf = LN(u_G) -----------------------------------------------------
         n = self.norm
         last_in = P["rstb_out"][-1]
@@ -636,12 +785,12 @@ class SwinIREngine:
             G, D, par = bufs[0], bufs[1], gi % 2
             t_d = P["blocks"][bi - 1]["out"]
             # u_{g+1} = conv(t_d) + u_g : conv dgrad -> D = dL/dt_d
-            H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(conv.Wd), H.epilogue(D), M, Cp, 9 * Cp, cd)
+            job = self._resi_bwd(conv, P, G, t_d, D, grads)
             if side_pending:   # RSTB gi + 1's deferred work, forked behind this conv (which it would starve)
                 side_open = self._flush_deferred(P)
                 side_pending = False
-            self._conv_pending.append((H.rows(G), H.im2col(t_d, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, conv.map,
-                                       g(conv.w), g(conv.b), self.C))
+            if job is not None:
+                self._conv_pending.append(job)
             # GEMM-operand copy of D for the last block's MLP branch: s_mlp * D in compute dtype
             drop = P["drop"]
             H.row_copy(D, Cp, M, Cp, H.copy_desc(P["gw"][par][len(blks) - 1]["Dm"],
@@ -675,6 +824,46 @@ class SwinIREngine:
         c = self.conv_first
         self._wgrad(P, H.rows(P["dfb"]), H.im2col(P["xin"], Hh, Ww, self.Cin_p, ones_col=self.in_ch), M, Cp,
                     9 * self.Cin_p, c.map, g(c.w), g(c.b), self.in_ch)
+
+    def _nearest_tail_bwd(self, P, grads):
+        """'nearest+conv' reconstruction backward (network_swinir.py:824-830): conv_last, conv_hr and the
+        two conv(nearest x2) stages, each input gradient gated by LeakyReLU' in the dgrad epilogue (conv_hr,
+        conv_up2) or after the 2x2 sum-pool that is nearest x2's adjoint (conv_up2 -> up1 -> cbu);
+        ends with P['dfb'] = dL/d fb."""
+        cd, B, Hh, Ww, M, Cp = self.cd, P["B"], P["H"], P["W"], P["M"], self.Cp
+        g = lambda p: grads[p]
+        h, w = 4 * Hh, 4 * Ww
+        ML = B * h * w
+        c = self.last
+        H.gemm_nt(H.im2col(P["dE"], h, w, 16, flip=True), H.rows(c.Wd),
+                  H.epilogue(P["dz_hr"], gate=P["nhr"], gate_kind=2, slope=0.2), ML, 64, 9 * 16, cd)
+        self._wgrad(P, H.rows(P["dE"]), H.im2col(P["nhr"], h, w, 64), ML, 16, 9 * 64, c.map, g(c.w))
+        self._bias_colsum(P, H.rows(P["dE"]), ML, 16, c.mapb, g(c.b))
+        c = self.hrc
+        H.gemm_nt(H.im2col(P["dz_hr"], h, w, 64, flip=True), H.rows(c.Wd),
+                  H.epilogue(P["dz_u"], gate=P["nup_act"][1], gate_kind=2, slope=0.2), ML, 64, 9 * 64, cd)
+        self._wgrad(P, H.rows(P["dz_hr"]), H.im2col(P["nup_act"][1], h, w, 64), ML, 64, 9 * 64, c.map, g(c.w))
+        self._bias_colsum(P, H.rows(P["dz_hr"]), ML, 64, c.mapb, g(c.b))
+        dz = P["dz_u"]
+        for i in (1, 0):   # conv_up2 then conv_up1: dz = dL/d(pre-activation) on the (h, w) grid
+            c = self.nup[i]
+            Mi = B * h * w
+            src = P["nup_act"][0] if i == 1 else P["a0"]
+            G_hi = P["G_hi"][:Mi]
+            H.gemm_nt(H.im2col(dz, h, w, 64, flip=True), H.rows(c.Wd), H.epilogue(G_hi), Mi, 64, 9 * 64, cd)
+            self._wgrad(P, H.rows(dz), H.im2col(src, h, w, 64, up=2), Mi, 64, 9 * 64, c.map, g(c.w))
+            self._bias_colsum(P, H.rows(dz), Mi, 64, c.mapb, g(c.b))
+            h, w = h // 2, w // 2
+            Mo = B * h * w
+            G_lo = P["G_lo"][:Mo]
+            H.sumpool2x(G_hi, 64, G_lo, 64, B, h, w, 64)
+            nxt = P["dz_hr"][:Mo] if i == 1 else P["da0"]      # dz_hr is free again after conv_hr's wgrad
+            H.act_grad_cast(G_lo, 64, src, 64, nxt, 64, Mo, 64, 2, 0.2 if i == 1 else 0.01)
+            dz = nxt
+        c = self.cbu
+        H.gemm_nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)
+        self._wgrad(P, H.rows(P["da0"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, 64, 9 * Cp, c.map,
+                    g(c.w), g(c.b), self.C)
 
     def _wg(self, P, A, Bop, N, K, lin, grads, ones_col):
         """One block linear's weight gradient: queued for the RSTB's grouped launch, or issued now."""

@@ -231,17 +231,40 @@ class PatchUnEmbed(PatchEmbed):
         return x.transpose(1, 2).reshape(B, self.embed_dim, x_size[0], x_size[1])
 
 
+class Conv1x1(nn.Conv2d):
+    """nn.Conv2d(Ci, Co, 1, 1, 0) whose forward is torch.ops.kair.linear over NHWC pixel rows."""
+    compute = 0
+
+    def forward(self, x):
+        _need_device(x)
+        B, C, Hh, Ww = x.shape
+        rows = x.permute(0, 2, 3, 1).reshape(B * Hh * Ww, C)
+        y, _ = torch.ops.kair.linear(rows, self.weight.view(self.out_channels, C), self.bias, 0, self.compute)
+        return y.view(B, Hh, Ww, -1).permute(0, 3, 1, 2).contiguous()
+
+
+def resi_conv(dim, resi_connection):
+    """The residual-connection conv of RSTB (network_swinir.py:464-471) and conv_after_body (:727-737):
+    '1conv' one 3x3 C->C; '3conv' 3x3 C->C/4, LeakyReLU 0.2, 1x1 C/4->C/4, LeakyReLU 0.2, 3x3 C/4->C
+    (the same Sequential indices as the reference, so the state_dict keys match)."""
+    if resi_connection == "1conv":
+        return Conv3x3(dim, dim, 3, 1, 1)
+    if resi_connection == "3conv":
+        return nn.Sequential(Conv3x3(dim, dim // 4, 3, 1, 1), nn.LeakyReLU(negative_slope=0.2, inplace=True),
+                             Conv1x1(dim // 4, dim // 4, 1, 1, 0), nn.LeakyReLU(negative_slope=0.2, inplace=True),
+                             Conv3x3(dim // 4, dim, 3, 1, 1))
+    raise ValueError(f"resi_connection {resi_connection!r}")
+
+
 class RSTB(nn.Module):
     def __init__(self, dim, input_resolution, depth, num_heads, window_size, mlp_ratio=4.0, qkv_bias=True,
                  qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=LayerNorm, downsample=None,
                  use_checkpoint=False, img_size=224, patch_size=4, resi_connection="1conv"):
         super().__init__()
-        if resi_connection != "1conv":
-            raise NotImplementedError("kair_amd SwinIR: resi_connection '3conv' is not on the MI355X path yet")
         self.dim, self.input_resolution = dim, input_resolution
         self.residual_group = BasicLayer(dim, input_resolution, depth, num_heads, window_size, mlp_ratio, qkv_bias,
                                          qk_scale, drop, attn_drop, drop_path, norm_layer)
-        self.conv = Conv3x3(dim, dim, 3, 1, 1)
+        self.conv = resi_conv(dim, resi_connection)
         self.patch_embed = PatchEmbed(img_size, patch_size, 0, dim, None)
         self.patch_unembed = PatchUnEmbed(img_size, patch_size, 0, dim, None)
 
@@ -308,15 +331,23 @@ class SwinIR(nn.Module):
                                     dpr[sum(depths[:i]):sum(depths[:i + 1])], norm_layer, None, use_checkpoint,
                                     img_size, patch_size, resi_connection))
         self.norm = norm_layer(self.num_features)
-        self.conv_after_body = nn.Conv2d(embed_dim, embed_dim, 3, 1, 1)
+        self.conv_after_body = resi_conv(embed_dim, resi_connection)
         if upsampler == "pixelshuffle":
             self.conv_before_upsample = nn.Sequential(nn.Conv2d(embed_dim, num_feat, 3, 1, 1), nn.LeakyReLU(inplace=True))
             self.upsample = Upsample(upscale, num_feat)
             self.conv_last = nn.Conv2d(num_feat, num_out_ch, 3, 1, 1)
         elif upsampler == "pixelshuffledirect":
             self.upsample = UpsampleOneStep(upscale, embed_dim, num_out_ch, tuple(self.patches_resolution))
-        else:
-            raise NotImplementedError(f"kair_amd SwinIR: upsampler '{upsampler}' is not on the MI355X path yet")
+        elif upsampler == "nearest+conv":   # real-world SR (network_swinir.py:751-760)
+            assert self.upscale == 4, "only support x4 now."
+            self.conv_before_upsample = nn.Sequential(nn.Conv2d(embed_dim, num_feat, 3, 1, 1), nn.LeakyReLU(inplace=True))
+            self.conv_up1 = nn.Conv2d(num_feat, num_feat, 3, 1, 1)
+            self.conv_up2 = nn.Conv2d(num_feat, num_feat, 3, 1, 1)
+            self.conv_hr = nn.Conv2d(num_feat, num_feat, 3, 1, 1)
+            self.conv_last = nn.Conv2d(num_feat, num_out_ch, 3, 1, 1)
+            self.lrelu = nn.LeakyReLU(negative_slope=0.2, inplace=True)
+        else:   # denoising / JPEG artifact reduction, upsampler None or '' (network_swinir.py:761-763)
+            self.conv_last = nn.Conv2d(embed_dim, num_out_ch, 3, 1, 1)
         self.apply(self._init_weights)
         self.compute_dtype = compute_dtype
         self._set_op_compute()
@@ -361,7 +392,7 @@ class SwinIR(nn.Module):
 
     def _set_op_compute(self):
         for m in self.modules():
-            if isinstance(m, (Linear, Conv3x3)):
+            if isinstance(m, (Linear, Conv3x3, Conv1x1)):
                 m.compute = 1 if self.compute_dtype == "bf16" else 0
 
     def check_image_size(self, x):

@@ -132,14 +132,27 @@ class _Group(nn.Module):
         self.blocks = nn.ModuleList(blocks)
 
 
-class RSTB(nn.Module):
-    """network_swinir.py:419-482 (resi_connection='1conv')."""
+def resi_conv(dim, resi_connection):
+    """The residual-connection conv of RSTB (network_swinir.py:464-471) and conv_after_body
+    (:727-737): '1conv' = one 3x3 C->C; '3conv' = 3x3 C->C/4, LeakyReLU 0.2, 1x1 C/4->C/4,
+    LeakyReLU 0.2, 3x3 C/4->C (same Sequential indices, so the state_dict keys match)."""
+    if resi_connection == "1conv":
+        return nn.Conv2d(dim, dim, 3, 1, 1)
+    if resi_connection == "3conv":
+        return nn.Sequential(nn.Conv2d(dim, dim // 4, 3, 1, 1), nn.LeakyReLU(0.2),
+                             nn.Conv2d(dim // 4, dim // 4, 1, 1, 0), nn.LeakyReLU(0.2),
+                             nn.Conv2d(dim // 4, dim, 3, 1, 1))
+    raise ValueError(resi_connection)
 
-    def __init__(self, dim, res, depth, heads, ws, mlp_ratio):
+
+class RSTB(nn.Module):
+    """network_swinir.py:419-482."""
+
+    def __init__(self, dim, res, depth, heads, ws, mlp_ratio, resi_connection="1conv"):
         super().__init__()
         self.residual_group = _Group([SwinTransformerBlock(dim, res, heads, ws, 0 if i % 2 == 0 else ws // 2,
                                                            mlp_ratio) for i in range(depth)])
-        self.conv = nn.Conv2d(dim, dim, 3, 1, 1)
+        self.conv = resi_conv(dim, resi_connection)
 
     def forward(self, x, size, keeps=None):
         h = x
@@ -164,7 +177,6 @@ class SwinIR(nn.Module):
                  depths=(6, 6, 6, 6), embed_dim=96, num_heads=(6, 6, 6, 6), mlp_ratio=4.0,
                  upsampler="", resi_connection="1conv"):
         super().__init__()
-        assert resi_connection == "1conv"
         self.upscale, self.upsampler, self.window_size, self.img_range = upscale, upsampler, window_size, img_range
         self.mean = (torch.tensor([0.4488, 0.4371, 0.4040]) if in_chans == 3 else torch.zeros(1)).view(1, -1, 1, 1)
         img_size = img_size if isinstance(img_size, (tuple, list)) else (img_size, img_size)
@@ -173,10 +185,10 @@ class SwinIR(nn.Module):
         C, nf = embed_dim, 64
         self.conv_first = nn.Conv2d(in_chans, C, 3, 1, 1)
         self.patch_embed = _Norm(C)
-        self.layers = nn.ModuleList([RSTB(C, self.res, d, h, window_size, mlp_ratio)
+        self.layers = nn.ModuleList([RSTB(C, self.res, d, h, window_size, mlp_ratio, resi_connection)
                                      for d, h in zip(depths, num_heads)])
         self.norm = nn.LayerNorm(C)
-        self.conv_after_body = nn.Conv2d(C, C, 3, 1, 1)
+        self.conv_after_body = resi_conv(C, resi_connection)
         if upsampler == "pixelshuffle":
             self.conv_before_upsample = nn.Sequential(nn.Conv2d(C, nf, 3, 1, 1), nn.LeakyReLU(0.01))
             ups = []

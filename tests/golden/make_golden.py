@@ -165,6 +165,36 @@ def gen_swinir_small():
     _save("swinir_small", **res)
 
 
+def gen_swinir_variants():
+    """The reference's other reconstruction heads and residual connection (network_swinir.py:
+    464-471 / 727-737 '3conv', :751-760 / 824-830 'nearest+conv', :761-763 / 831-835 upsampler None:
+    denoising / JPEG, with img_range 255 as in options/swinir/train_swinir_car_jpeg.json)."""
+    from models.network_swinir import SwinIR
+    cfgs = (("realsr3", dict(upscale=4, in_chans=3, img_range=1.0, upsampler="nearest+conv", resi_connection="3conv")),
+            ("dngray", dict(upscale=1, in_chans=1, img_range=1.0, upsampler=None, resi_connection="1conv")),
+            ("car255", dict(upscale=1, in_chans=3, img_range=255.0, upsampler="", resi_connection="3conv")))
+    res = {}
+    for i, (tag, kw) in enumerate(cfgs):
+        torch.manual_seed(40 + i)
+        net = SwinIR(img_size=16, window_size=8, depths=[2], embed_dim=60, num_heads=[6], mlp_ratio=2,
+                     drop_path_rate=0.0, **kw)
+        net.train()
+        torch.manual_seed(50 + i)
+        sc, ci = kw["upscale"], kw["in_chans"]
+        L = torch.rand(2, ci, 16, 16)
+        H = torch.rand(2, ci, 16 * sc, 16 * sc)
+        for p in net.parameters():
+            p.grad = None
+        E = net(L)
+        loss = nn.L1Loss()(E, H)
+        loss.backward()
+        pre = tag + "."
+        res.update({pre + "L": _np(L), pre + "H": _np(H), pre + "E": _np(E), pre + "loss": np.float32(loss.item())})
+        res.update({pre + k: v for k, v in _state(net).items()})
+        res.update({pre + "grad." + k: _np(p.grad) for k, p in net.named_parameters()})
+    _save("swinir_variants", **res)
+
+
 def _opt_dict(netG, train_over=None, E_decay=0.999):
     opt = {
         "model": "plain", "gpu_ids": None, "dist": False, "is_train": True, "scale": netG.get("upscale", 1),
@@ -394,6 +424,6 @@ if __name__ == "__main__":
     _install_stubs()
     torch.set_num_threads(8)
     which = sys.argv[1:] or ["window_attention", "swin_block", "swinir_small", "train_trajectory",
-                             "conv_nets", "usrnet", "image_utils", "dncnn_kat", "state_dict_layouts"]
+                             "conv_nets", "usrnet", "swinir_variants", "image_utils", "dncnn_kat", "state_dict_layouts"]
     for w in which:
         globals()["gen_" + w]()

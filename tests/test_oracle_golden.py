@@ -71,6 +71,31 @@ def test_swinir_small(tag, ups, sc):
         close(p.grad, g[k], rtol=2e-3, atol=2e-5)
 
 
+VARIANTS = {   # tests/golden/make_golden.py gen_swinir_variants
+    "realsr3": dict(upscale=4, in_chans=3, img_range=1.0, upsampler="nearest+conv", resi_connection="3conv"),
+    "dngray": dict(upscale=1, in_chans=1, img_range=1.0, upsampler=None, resi_connection="1conv"),
+    "car255": dict(upscale=1, in_chans=3, img_range=255.0, upsampler="", resi_connection="3conv"),
+}
+
+
+@pytest.mark.parametrize("tag", sorted(VARIANTS))
+def test_swinir_variants(tag):
+    """'nearest+conv' / no-upsampler heads, '3conv' residual connections, img_range 255."""
+    z = load_golden("swinir_variants")
+    pre = tag + "."
+    net = swinir.SwinIR(img_size=16, window_size=8, depths=[2], embed_dim=60, num_heads=[6], mlp_ratio=2,
+                        **VARIANTS[tag])
+    net.load_state_dict(sub_state(z, pre), strict=True)
+    E = net(torch.from_numpy(z[pre + "L"]))
+    close(E, z[pre + "E"])
+    loss = torch.nn.functional.l1_loss(E, torch.from_numpy(z[pre + "H"]))
+    assert abs(loss.item() - float(z[pre + "loss"])) < 1e-6
+    loss.backward()
+    g = sub_grads(z, pre)
+    for k, p in net.named_parameters():
+        close(p.grad, g[k], rtol=2e-3, atol=2e-5)
+
+
 def test_train_trajectory():
     """3 reference ModelPlain steps (MultiStepLR before step, Adam, EMA 0.999)."""
     z = load_golden("train_trajectory")
