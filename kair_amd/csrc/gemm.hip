@@ -1422,8 +1422,10 @@ int nt_tiles(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipSt
   if (N <= 32 && n32 == 1) return launch_nt<CT, TA, AM, 64, 32, 2, 2>(A, B, E, M, N, K, s);
   if (N <= 32 && n32 == 2) return launch_nt<CT, TA, AM, 32, 32, 2, 2>(A, B, E, M, N, K, s);
   const long tm = (M + 127) / 128;
-  if (N > 64 && tm * ((N + 127) / 128) >= 2L * g_num_cus) return launch_nt<CT, TA, AM, 128, 128, 2, 2>(A, B, E, M, N, K, s);
-  if (tm * ((N + 63) / 64) >= 2L * g_num_cus || M <= 64) return launch_nt<CT, TA, AM, 128, 64, 2, 2>(A, B, E, M, N, K, s);
+  // (thresholds at >= 1 or 0.5 CTAs per CU measured slower at B = 4: 476 -> 460 / 390 patches/s)
+  const long min_ctas = 2L * g_num_cus;
+  if (N > 64 && tm * ((N + 127) / 128) >= min_ctas) return launch_nt<CT, TA, AM, 128, 128, 2, 2>(A, B, E, M, N, K, s);
+  if (tm * ((N + 63) / 64) >= min_ctas || M <= 64) return launch_nt<CT, TA, AM, 128, 64, 2, 2>(A, B, E, M, N, K, s);
   return launch_nt<CT, TA, AM, 64, 64, 2, 2>(A, B, E, M, N, K, s);
 }
 
@@ -1760,9 +1762,17 @@ int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, in
   return kair_set_error(KAIR_ERR_ARG, "gemm_nt: q/k/v operand must have the compute dtype");
 }
 
+// Cp = 192 conv weight gradients (N = 192, K = 9 * 192): one 192-wide N tile instead of a full
+// and a half-empty 128-wide one (B = 32: 946 -> 953 patches/s; B = 4 unchanged)
+static bool tn192_shape(int N, int K) { return N > 128 && N <= 192 && K > 128; }
+
 template <typename CT, typename TA, typename TB, int AMA, int AMB>
 int launch_tn(const Op& a, const Op& b, float* ws, int splits, long M, int N, int K, long rps, hipStream_t s) {
-  if (N <= 64 && K <= 64) {
+  if (tn192_shape(N, K)) {   // one 192-wide N tile (Cp = 192 conv weight gradients): no half-empty tile
+    const int tilesK = (K + 127) / 128;
+    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 192, 128>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
+                       ws, M, N, K, rps, tilesK);
+  } else if (N <= 64 && K <= 64) {
     const int tilesN = (N + 63) / 64, tilesK = (K + 63) / 64;
     hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 64, 64>), dim3(tilesN * tilesK, splits), dim3(NT), 0, s, a, b,
                        ws, M, N, K, rps, tilesK);
@@ -1890,6 +1900,10 @@ extern "C" int kair_wgrad_splits(long M, int N, int K) {
   // enough (tile, split) CTAs for ~2 per CU, but >= 1024 rows per split so the fp32 partial
   // planes stay small next to the operand traffic (wgrad_finalize reads them all back)
   long s = 512 / (tiles > 0 ? tiles : 1);
+  if (tn192_shape(N, K)) {   // 192-wide tiles: one CTA per CU (LDS)
+    if (g_num_cus == 0) init_num_cus();
+    s = g_num_cus / ((K + 127) / 128);
+  }
   const long maxs = (M + 1023) / 1024;
   if (s > maxs) s = maxs;
   if (s < 1) s = 1;
