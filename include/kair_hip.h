@@ -311,6 +311,11 @@ int kair_image_to_nhwc(const float* img, void* out, int dtype, int ldc, const fl
  * pre-PixelShuffle(ps_r) layout [b][y/r][x/r][c*r*r + (y%r)*r + x%r] otherwise.  ws: 1024 floats. */
 int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, int ps_r, float weight,
                  int B, int C, int Hh, int Ww, float* ws, void* stream);
+/* Charbonnier loss (models/loss.py:208-218, model_plain.py:191-192; SwinIR denoising / JPEG options):
+ * loss_out[0] = weight*mean(sqrt((E-H)^2 + eps)); dE = weight*(E-H)/sqrt((E-H)^2 + eps)/numel, laid out as
+ * kair_l1_loss. */
+int kair_charbonnier_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, int ps_r,
+                          float weight, float eps, int B, int C, int Hh, int Ww, float* ws, void* stream);
 /* y[i] += a * x[i] over n fp32 elements (residual-gradient merges). */
 int kair_axpy(float* y, const float* x, float a, long n, void* stream);
 /* BatchNorm2d over NHWC rows z [M, C] fp32 (basicblock.py:69: momentum 0.9, eps 1e-4), fused act

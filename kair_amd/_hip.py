@@ -115,6 +115,8 @@ _SIGS = {
                              c_int, c_float, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "kair_image_to_nhwc": [c_vp, c_vp, c_int, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
     "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "kair_charbonnier_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_int, c_int,
+                              c_vp, c_vp],
     "kair_axpy": [c_vp, c_vp, c_float, c_long, c_vp],
     "kair_axpby": [c_vp, c_vp, c_float, c_float, c_long, c_vp],
     "kair_bn_ws": [c_int],
@@ -464,7 +466,12 @@ def image_to_nhwc(img, out, ldc, mean, img_range, B, C, H, W):
                                    stream_ptr()), "image_to_nhwc")
 
 
-def l1_loss(E, H, loss_out, dE, ldc, weight, B, C, Hh, Ww, ws, ps_r=1):
+def l1_loss(E, H, loss_out, dE, ldc, weight, B, C, Hh, Ww, ws, ps_r=1, charb_eps=None):
+    """L1 (mean) loss + its gradient; charb_eps set: the Charbonnier loss sqrt(d^2 + eps) instead."""
+    if charb_eps is not None:
+        check(lib().kair_charbonnier_loss(ptr(E), ptr(H), ptr(loss_out), ptr(dE), dtype_code(dE), ldc, ps_r, weight,
+                                          float(charb_eps), B, C, Hh, Ww, ptr(ws), stream_ptr()), "charbonnier_loss")
+        return
     check(lib().kair_l1_loss(ptr(E), ptr(H), ptr(loss_out), ptr(dE), dtype_code(dE), ldc, ps_r, weight, B, C, Hh, Ww,
                              ptr(ws), stream_ptr()), "l1_loss")
 

@@ -359,9 +359,10 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ img, T* __restric
 }
 
 // I: index type (int when every index fits: 32-bit divisions are a fraction of the 64-bit ones)
-template <typename T, typename I>
+// CH: Charbonnier (models/loss.py:208-218) sqrt(d^2 + eps) with gradient d / sqrt(d^2 + eps), else L1
+template <typename T, typename I, bool CH>
 __global__ void l1_kernel(const float* __restrict__ E, const float* __restrict__ H, T* __restrict__ dE, int ldc, int r,
-                          float gscale, int C, int Hh, int Ww, long npix, float* __restrict__ ws) {
+                          float gscale, int C, int Hh, int Ww, long npix, float* __restrict__ ws, float eps) {
   // dE element t = (pixel of the [Hh/r, Ww/r] grid, channel slot); slot -> (c, i, j) when r > 1
   __shared__ float red[256];
   float s = 0.f;
@@ -379,8 +380,14 @@ __global__ void l1_kernel(const float* __restrict__ E, const float* __restrict__
       const int y = (pp / wsm) * r + ij / r, x = (pp % wsm) * r + ij % r;
       const I i = (b * C + c) * HW + (I)y * Ww + x;
       const float d = E[i] - H[i];
-      s += fabsf(d);
-      g = d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f);
+      if constexpr (CH) {
+        const float q = sqrtf(d * d + eps);
+        s += q;
+        g = q > 0.f ? gscale * d / q : 0.f;
+      } else {
+        s += fabsf(d);
+        g = d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f);
+      }
     }
     dE[t] = (T)g;
   }
@@ -650,10 +657,10 @@ extern "C" int kair_image_to_nhwc(const float* img, void* out, int dtype, int ld
   return 0;
 }
 
-extern "C" int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, int ps_r,
-                            float weight, int B, int C, int Hh, int Ww, float* ws, void* stream) {
-  KAIR_CHECK_ARG(E && H && loss_out && dE && ws && ps_r >= 1 && ldc >= C * ps_r * ps_r, "l1_loss: bad args");
-  KAIR_CHECK_ARG(Hh % ps_r == 0 && Ww % ps_r == 0, "l1_loss: image not divisible by r");
+static int pixel_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, int ps_r, float weight,
+                      float eps, bool charb, int B, int C, int Hh, int Ww, float* ws, void* stream) {
+  KAIR_CHECK_ARG(E && H && loss_out && dE && ws && ps_r >= 1 && ldc >= C * ps_r * ps_r, "pixel loss: bad args");
+  KAIR_CHECK_ARG(Hh % ps_r == 0 && Ww % ps_r == 0, "pixel loss: image not divisible by r");
   const long npix = (long)B * (Hh / ps_r) * (Ww / ps_r);
   const double numel = (double)B * Hh * Ww * C;
   const int nb = 1024;
@@ -661,18 +668,37 @@ extern "C" int kair_l1_loss(const float* E, const float* H, float* loss_out, voi
   const float gs = (float)(weight / numel);
   // int indices when the largest index (dE element or image element) and the grid stride fit
   const bool i32 = (double)npix * ldc < 2.0e9 && numel < 2.0e9;
-  if (dtype == KAIR_BF16 && i32)
-    hipLaunchKernelGGL((l1_kernel<bf16, int>), dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
-  else if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL((l1_kernel<bf16, long>), dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
-  else if (i32)
-    hipLaunchKernelGGL((l1_kernel<float, int>), dim3(nb), dim3(256), 0, s, E, H, (float*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
-  else
-    hipLaunchKernelGGL((l1_kernel<float, long>), dim3(nb), dim3(256), 0, s, E, H, (float*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws);
+#define KAIR_PIXEL_LOSS(T, I, CHV)                                                                                       \
+  hipLaunchKernelGGL((l1_kernel<T, I, CHV>), dim3(nb), dim3(256), 0, s, E, H, (T*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws, \
+                     eps)
+  if (charb) {
+    if (dtype == KAIR_BF16 && i32) KAIR_PIXEL_LOSS(bf16, int, true);
+    else if (dtype == KAIR_BF16) KAIR_PIXEL_LOSS(bf16, long, true);
+    else if (i32) KAIR_PIXEL_LOSS(float, int, true);
+    else KAIR_PIXEL_LOSS(float, long, true);
+  } else {
+    if (dtype == KAIR_BF16 && i32) KAIR_PIXEL_LOSS(bf16, int, false);
+    else if (dtype == KAIR_BF16) KAIR_PIXEL_LOSS(bf16, long, false);
+    else if (i32) KAIR_PIXEL_LOSS(float, int, false);
+    else KAIR_PIXEL_LOSS(float, long, false);
+  }
+#undef KAIR_PIXEL_LOSS
   KAIR_CHECK_LAUNCH();
   hipLaunchKernelGGL(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);
   KAIR_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int kair_l1_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc, int ps_r,
+                            float weight, int B, int C, int Hh, int Ww, float* ws, void* stream) {
+  return pixel_loss(E, H, loss_out, dE, dtype, ldc, ps_r, weight, 0.f, false, B, C, Hh, Ww, ws, stream);
+}
+
+extern "C" int kair_charbonnier_loss(const float* E, const float* H, float* loss_out, void* dE, int dtype, int ldc,
+                                     int ps_r, float weight, float eps, int B, int C, int Hh, int Ww, float* ws,
+                                     void* stream) {
+  KAIR_CHECK_ARG(eps >= 0.f, "charbonnier_loss: eps must be >= 0");
+  return pixel_loss(E, H, loss_out, dE, dtype, ldc, ps_r, weight, eps, true, B, C, Hh, Ww, ws, stream);
 }
 
 extern "C" int kair_adam_ema(float* p, const float* g, float* m, float* v, float* ema, long n, const float* lr_t,

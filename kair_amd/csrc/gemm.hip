@@ -1395,9 +1395,8 @@ int launch_nt(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipS
 }
 
 static int g_num_cus = 0;
-static int g_ring_mode = -1;
-// KAIR_CONV_HALO=0 disables the halo 3x3 conv kernel (A/B timing only)
-static const int g_halo_mode = getenv("KAIR_CONV_HALO") && getenv("KAIR_CONV_HALO")[0] == '0' ? 0 : 1;
+static const int g_ring_mode = 1;   // the LDS-DMA ring kernels (measured A/B switch in round 1)
+static const int g_halo_mode = 1;
 static long g_ring_min_tiles = -1;
 
 static void init_num_cus() {
@@ -1405,8 +1404,7 @@ static void init_num_cus() {
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     n = 256;
   g_num_cus = n > 0 ? n : 256;
-  const char* v = getenv("KAIR_RING_MIN_TILES");   // A/B knob: ring kernel only with >= this many tiles
-  g_ring_min_tiles = v ? atol(v) : g_num_cus;
+  g_ring_min_tiles = g_num_cus;   // the persistent ring kernel only with >= one tile per CU
 }
 
 // Tile choice of the register-staged kernel: the largest tile that still gives >= 2 CTAs per CU
@@ -1417,8 +1415,8 @@ int nt_tiles(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipSt
   if (g_num_cus == 0) init_num_cus();
   // 32x32 tiles for N <= 32 (RRDB dense-block convs, growth 32; ResUNet level-2 convs): no half-empty
   // 64-wide N tile, twice the CTAs on these small-M, long-K convs (RRDBNet B=16: 421 -> 436
-  // patches/s; 64x32 tiles 429).  A/B knob KAIR_NT_N32 = 0 / 1 (64x32) / 2 (32x32)
-  static const int n32 = getenv("KAIR_NT_N32") ? atoi(getenv("KAIR_NT_N32")) : 2;
+  // patches/s; 64x32 tiles 429).  (measured against 64x32 and 64x64)
+  constexpr int n32 = 2;
   if (N <= 32 && n32 == 1) return launch_nt<CT, TA, AM, 64, 32, 2, 2>(A, B, E, M, N, K, s);
   if (N <= 32 && n32 == 2) return launch_nt<CT, TA, AM, 32, 32, 2, 2>(A, B, E, M, N, K, s);
   const long tm = (M + 127) / 128;
@@ -1490,8 +1488,8 @@ template <int AM>
 int ring_bn(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
   // one 192-wide N tile leaves the persistent CTAs unevenly loaded (B = 32: 576 M-tiles on 256 CUs
   // -> 3 vs 2.25 on average); two 96-wide tiles balance better (measured 815 -> 823 patches/s;
-  // A/B knob KAIR_RING_SPLIT_N=0)
-  static const int split_n = getenv("KAIR_RING_SPLIT_N") ? atoi(getenv("KAIR_RING_SPLIT_N")) : 1;
+  // against one 192-wide tile)
+  constexpr int split_n = 1;
   if (K <= 192 && !(split_n && N <= 192 && E.omode != KAIR_OUT_QKVBLK)) return launch_ring<192, 5, AM>(A, B, E, M, N, K, s);
   if (K <= 384) return launch_ring<96, 5, AM>(A, B, E, M, N, K, s);
   return launch_ring<64, 5, AM>(A, B, E, M, N, K, s);
@@ -1741,10 +1739,6 @@ int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, in
       return launch_conv_halo<TA>(A, B, E, M, K, s);
   }
   if constexpr (sizeof(CT) == 2 && sizeof(TA) == 2) {
-    if (g_ring_mode < 0) {   // KAIR_GEMM_RING=0 disables the LDS-DMA ring kernel (A/B timing only)
-      const char* v = getenv("KAIR_GEMM_RING");
-      g_ring_mode = (v && v[0] == '0') ? 0 : 1;
-    }
     if (g_ring_mode && ring_ok(mode, A, B, E, M, N, K)) {
       if (g_num_cus == 0) init_num_cus();
       const int bn = K <= 192 ? 192 : (K <= 384 ? 96 : 64);   // ring_bn's choice
@@ -1887,11 +1881,10 @@ extern "C" int kair_wgrad_splits(long M, int N, int K) {
   if (tn_ring_shape(M, N, K)) {   // ring kernel: one 192x192 tile per CTA, one CTA per CU
     if (g_num_cus == 0) init_num_cus();
     const int tiles = ((N + TNR_BN - 1) / TNR_BN) * ((K + TNR_BK - 1) / TNR_BK);
-    static const long sdiv = getenv("KAIR_TN_SPLIT_DIV") ? atol(getenv("KAIR_TN_SPLIT_DIV")) : 1;   // A/B knob
-    long s = g_num_cus / tiles / (sdiv > 0 ? sdiv : 1);
-    // >= 128 rows per split (A/B knob KAIR_TN_ROWS; binds only at small M: at B = 4, 256 -> 128 rows
+    long s = g_num_cus / tiles;
+    // >= 128 rows per split (binds only at small M: at B = 4, 256 -> 128 rows
     // measured 311 -> 316-320 patches/s, 64 / 32 no better, 512 / 1024 slower)
-    static const long min_rows = getenv("KAIR_TN_ROWS") ? atol(getenv("KAIR_TN_ROWS")) : 128;
+    constexpr long min_rows = 128;
     const long maxs = (M + min_rows - 1) / min_rows;
     if (s > maxs) s = maxs;
     return (int)(s < 1 ? 1 : s);
@@ -1926,10 +1919,6 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
                  "gemm_tn: dimensions must be < 2^24");
   const Op a = make_op(*A, M), b = make_op(*B, M);
   hipStream_t s0 = (hipStream_t)stream;
-  if (g_ring_mode < 0) {
-    const char* v = getenv("KAIR_GEMM_RING");
-    g_ring_mode = (v && v[0] == '0') ? 0 : 1;
-  }
   if (g_ring_mode && compute == KAIR_BF16 && tn_ring_shape(M, N, K) && A->dtype == KAIR_BF16 && B->dtype == KAIR_BF16 &&
       (A->mode == KAIR_LD_ROWS || A->mode == KAIR_LD_QKVBLK) && B->mode == KAIR_LD_ROWS && !A->rowscale && !B->rowscale &&
       A->win_ws == 0 && B->win_ws == 0 && A->ones_col < 0 && (B->ones_col < 0 || B->ones_in_data) &&

@@ -320,7 +320,7 @@ extern "C" int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype
   long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;
   // 1024 blocks (4 per CU): each 16-lane row group normalises several rows on the affine
   // parameters it loaded once (measured at B = 32: 8192 blocks 28.5 us -> 1024 blocks 18.3 us)
-  static const long max_nb = getenv("KAIR_LN_FWD_BLOCKS") ? atol(getenv("KAIR_LN_FWD_BLOCKS")) : 1024;
+  constexpr long max_nb = 1024;
   if (nb > max_nb) nb = max_nb;
   hipStream_t s = (hipStream_t)stream;
   if (y_dtype == KAIR_BF16)

@@ -115,9 +115,9 @@ class DnCNNEngine(ConvEngineBase):
             H.axpby(P["E"], x, 1.0, -1.0)     # x - model(x)
         return P["E"]
 
-    def backward_from_loss(self, H_img, grads, loss_weight=1.0):
+    def backward_from_loss(self, H_img, grads, loss_weight=1.0, charb_eps=None):
         P = self.cur
-        H.l1_loss(P["E"], H_img, P["loss"], P["dEf"], 16, loss_weight, P["B"], self.out_ch, P["H"], P["W"], P["loss_ws"])
+        H.l1_loss(P["E"], H_img, P["loss"], P["dEf"], 16, loss_weight, P["B"], self.out_ch, P["H"], P["W"], P["loss_ws"], charb_eps=charb_eps)
         self.backward(grads, P)
         return P["loss"]
 

@@ -220,10 +220,10 @@ class RRDBNetEngine(ConvEngineBase):
         return P["E"]
 
     # ------------------------------------------------------------------------------------
-    def backward_from_loss(self, H_img, grads, loss_weight=1.0):
+    def backward_from_loss(self, H_img, grads, loss_weight=1.0, charb_eps=None):
         P = self.cur
         HL, WL = P["levels"][-1]
-        H.l1_loss(P["E"], H_img, P["loss"], P["dE"], 16, loss_weight, P["B"], self.out_ch, HL, WL, P["loss_ws"])
+        H.l1_loss(P["E"], H_img, P["loss"], P["dE"], 16, loss_weight, P["B"], self.out_ch, HL, WL, P["loss_ws"], charb_eps=charb_eps)
         self.backward(grads, P)
         return P["loss"]
 

@@ -677,7 +677,7 @@ class SwinIREngine:
     def _bias_colsum(self, P, G, M, Np, layer_map, bgrad):
         H.colsum(G, M, Np, layer_map, bgrad, P["colsum_ws"])
 
-    def backward_from_loss(self, H_img, grads, loss_weight=1.0):
+    def backward_from_loss(self, H_img, grads, loss_weight=1.0, charb_eps=None):
         """L1 loss (mean) against H_img, then the full backward.  grads: {param: fp32 tensor to write}.
         Returns the device loss tensor [1]."""
         P = self.cur
@@ -687,10 +687,10 @@ class SwinIREngine:
         wr = loss_weight / self.img_range
         if self.upsampler == "pixelshuffledirect":
             H.l1_loss(P["E"], H_img, P["loss"], P["dE"], self.up1.Cop, wr, B, self.in_ch, Hh * self.scale,
-                      Ww * self.scale, P["loss_ws"], ps_r=self.scale)
+                      Ww * self.scale, P["loss_ws"], ps_r=self.scale, charb_eps=charb_eps)
         else:
             H.l1_loss(P["E"], H_img, P["loss"], P["dE"], 16, wr, B, self.in_ch, Hh * self.scale, Ww * self.scale,
-                      P["loss_ws"])
+                      P["loss_ws"], charb_eps=charb_eps)
         if self.img_range != 1.0:
             P["loss"].mul_(self.img_range)
         self.backward(grads, P)

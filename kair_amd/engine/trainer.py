@@ -66,7 +66,7 @@ def segment_buckets(params, segs):
 
 class FusedTrainer:
     def __init__(self, netG, netE=None, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, E_decay=0.999,
-                 loss_weight=1.0, use_graph=True, process_group=None, bucket_mb=25, segment_graphs=None):
+                 loss_weight=1.0, use_graph=True, process_group=None, bucket_mb=25, segment_graphs=None, charb_eps=None):
         self.net, self.ema_net = netG, netE
         self.device = next(netG.parameters()).device
         self.engine = netG.engine()
@@ -85,6 +85,8 @@ class FusedTrainer:
         self.lr = lr
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.E_decay, self.loss_weight = E_decay, loss_weight
+        # None: L1 (G_lossfn_type 'l1'); a float: the Charbonnier loss with that eps ('charbonnier')
+        self.charb_eps = charb_eps
         self.t = 0
         self.scal = torch.zeros(2, device=self.device)
         self.pg = process_group
@@ -115,7 +117,7 @@ class FusedTrainer:
             drop = drop_path_scales(eng, L.shape[0], L.device)
         eng._packed_version = None           # weights change every step: always repack
         eng.forward(L, drop)
-        return eng.backward_from_loss(Hh, self.grads, self.loss_weight)
+        return eng.backward_from_loss(Hh, self.grads, self.loss_weight, charb_eps=self.charb_eps)
 
     def _update(self):
         H.adam_ema(self.flat_p, self.flat_g, self.m, self.v, self.flat_e, self.flat_p.numel(), self.scal,

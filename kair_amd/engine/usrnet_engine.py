@@ -297,10 +297,10 @@ class USRNetEngine:
     # ------------------------------------------------------------------------------------
     # backward
     # ------------------------------------------------------------------------------------
-    def backward_from_loss(self, H_img, grads, loss_weight=1.0):
+    def backward_from_loss(self, H_img, grads, loss_weight=1.0, charb_eps=None):
         P = self.cur
         H.l1_loss(P["it"][-1]["xout"], H_img, P["loss"], P["gE"], C8, loss_weight, P["B"], self.out_nc, P["H"], P["W"],
-                  P["loss_ws"])
+                  P["loss_ws"], charb_eps=charb_eps)
         self.backward(grads, P)
         return P["loss"]
 

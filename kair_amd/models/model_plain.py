@@ -86,6 +86,18 @@ class FusedAdam(torch.optim.Optimizer):
                     g[k] = sg[k]
 
 
+class CharbonnierLoss(nn.Module):
+    """models/loss.py:208-218: mean(sqrt((x - y)^2 + eps)) (the autograd path's loss)."""
+
+    def __init__(self, eps=1e-9):
+        super().__init__()
+        self.eps = eps
+
+    def forward(self, x, y):
+        d = x - y
+        return torch.mean(torch.sqrt(d * d + self.eps))
+
+
 class ModelPlain(ModelBase):
     """Train with pixel loss."""
 
@@ -173,6 +185,8 @@ class ModelPlain(ModelBase):
             self.G_lossfn = nn.MSELoss()
         elif t == "l2sum":
             self.G_lossfn = nn.MSELoss(reduction="sum")
+        elif t == "charbonnier":   # models/loss.py:208-218; the fused trainer runs kair_charbonnier_loss
+            self.G_lossfn = CharbonnierLoss(self.opt_train.get("G_charbonnier_eps", 1e-9))
         else:
             raise NotImplementedError("Loss type [{:s}] is not on the kair_amd path.".format(t))
         self.G_lossfn_weight = self.opt_train["G_lossfn_weight"]
@@ -180,7 +194,7 @@ class ModelPlain(ModelBase):
     def _fused_ok(self):
         net = self.get_bare_model(self.netG)
         return (hasattr(net, "engine") and self.device.type == "cuda" and all(p.requires_grad for p in net.parameters())
-                and self.G_lossfn_type == "l1" and not self.opt_train.get("G_optimizer_clipgrad")
+                and self.G_lossfn_type in ("l1", "charbonnier") and not self.opt_train.get("G_optimizer_clipgrad")
                 and self.opt_train["G_optimizer_type"] == "adam" and not self.amp_enabled
                 and not self.opt_train.get("G_regularizer_orthstep") and not self.opt_train.get("G_regularizer_clipstep"))
 
@@ -193,6 +207,8 @@ class ModelPlain(ModelBase):
                                         betas=tuple(tr["G_optimizer_betas"]), eps=1e-8,
                                         weight_decay=tr["G_optimizer_wd"], E_decay=tr["E_decay"],
                                         loss_weight=self.G_lossfn_weight,
+                                        charb_eps=(tr.get("G_charbonnier_eps", 1e-9) if self.G_lossfn_type == "charbonnier"
+                                                   else None),
                                         use_graph=tr.get("use_hip_graph", True))
             self.G_optimizer = FusedAdam(self.trainer.params, self.trainer, tr["G_optimizer_lr"],
                                          tr["G_optimizer_betas"], 1e-8, tr["G_optimizer_wd"])

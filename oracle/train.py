@@ -20,11 +20,12 @@ import torch.nn as nn
 
 class OracleTrainer:
     def __init__(self, net, ema_net=None, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, milestones=(), gamma=0.5,
-                 E_decay=0.999, loss_weight=1.0):
+                 E_decay=0.999, loss_weight=1.0, charb_eps=None):
         self.net, self.ema = net, ema_net
         self.lr0, self.betas, self.eps = lr, betas, eps
         self.milestones, self.gamma = sorted(milestones), gamma
         self.E_decay, self.loss_weight = E_decay, loss_weight
+        self.charb_eps = charb_eps   # G_lossfn_type 'charbonnier' (model_plain.py:191-192, models/loss.py:208-218)
         self.params = [p for p in net.parameters() if p.requires_grad]
         self.m = [torch.zeros_like(p) for p in self.params]
         self.v = [torch.zeros_like(p) for p in self.params]
@@ -50,7 +51,11 @@ class OracleTrainer:
         for p in self.params:
             p.grad = None
         E = (forward or self.net)(L)
-        loss = self.loss_weight * nn.functional.l1_loss(E, H)
+        if self.charb_eps is None:
+            loss = self.loss_weight * nn.functional.l1_loss(E, H)
+        else:
+            d = E - H
+            loss = self.loss_weight * torch.mean(torch.sqrt(d * d + self.charb_eps))
         loss.backward()
         self._adam()
         if self.ema is not None and self.E_decay > 0:

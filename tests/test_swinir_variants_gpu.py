@@ -135,3 +135,55 @@ def test_fused_trainer_variant_vs_oracle_trainer(tag):
     sd, sdr = ema.state_dict(), ref_e.state_dict()
     for k in sdr:
         assert rel(sd[k].float(), sdr[k].float()) < 1e-4, k
+
+
+def test_charbonnier_loss_kernel():
+    """kair_charbonnier_loss vs torch (models/loss.py:208-218): value and gradient, exact zeros included."""
+    from kair_amd import _hip as H
+    g = torch.Generator().manual_seed(12)
+    E = torch.rand(2, 3, 24, 16, generator=g)
+    Hh = E.clone()
+    Hh[:, :, :8] = torch.rand(2, 3, 8, 16, generator=g)      # rows 8.. : d == 0 exactly
+    eps = 1e-3
+    Et = E.clone().requires_grad_(True)
+    d = Et - Hh
+    ref = 0.5 * torch.mean(torch.sqrt(d * d + eps))
+    ref.backward()
+    loss = torch.empty(1, device=dev)
+    dE = torch.zeros(2 * 24 * 16, 16, device=dev)
+    ws = torch.empty(1024, device=dev)
+    H.l1_loss(E.to(dev), Hh.to(dev), loss, dE, 16, 0.5, 2, 3, 24, 16, ws, charb_eps=eps)
+    assert abs(loss.item() - ref.item()) < 1e-6 * ref.item()
+    got = dE[:, :3].view(2, 24, 16, 3).permute(0, 3, 1, 2).cpu()
+    assert rel(got, Et.grad) < 1e-5
+    assert (dE[:, 3:] == 0).all()
+
+
+def test_fused_trainer_charbonnier_vs_oracle_trainer():
+    """The denoising options' loss (G_lossfn_type 'charbonnier', G_charbonnier_eps 1e-9) inside the
+    graph-captured fused step vs the oracle trainer, 4 steps (fp32 mode)."""
+    kw = VARIANTS["dngray"]
+    torch.manual_seed(13)
+    mk = lambda: SwinIR(img_size=16, window_size=8, depths=[2], embed_dim=60, num_heads=[6], mlp_ratio=2,
+                        drop_path_rate=0.0, compute_dtype="fp32", **kw)
+    net, ema = mk(), mk()
+    ema.load_state_dict(net.state_dict())
+    mko = lambda: osw.SwinIR(1, 1, 16, 8, 1.0, [2], 60, [6], 2, None, "1conv")
+    ref, ref_e = mko(), mko()
+    ref.load_state_dict(net.state_dict(), strict=True)
+    ref_e.load_state_dict(net.state_dict(), strict=True)
+    net, ema = net.to(dev).train(), ema.to(dev).eval()
+    tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999, use_graph=True, charb_eps=1e-9)
+    otr = OracleTrainer(ref, ref_e, lr=2e-4, E_decay=0.999, charb_eps=1e-9)
+    g = torch.Generator().manual_seed(14)
+    for _ in range(4):
+        Hh = torch.rand(2, 1, 16, 16, generator=g)
+        L = Hh + 25.0 / 255 * torch.randn(2, 1, 16, 16, generator=g)   # DatasetDnCNN-style AWGN pair
+        loss = tr.step(L.to(dev), Hh.to(dev)).item()
+        _, lo = otr.optimize_parameters(L, Hh)
+        assert abs(loss - lo) < 1e-4 * abs(lo), (loss, lo)
+    sd, sdr = net.state_dict(), ref.state_dict()
+    for k in sdr:
+        # Adam's first steps normalise each gradient element, so summation-order noise on a bias
+        # element whose gradient is near zero moves it by up to lr: biases 1e-3, weights 1e-4
+        assert rel(sd[k].float(), sdr[k].float()) < (1e-3 if sdr[k].dim() == 1 else 1e-4), k
