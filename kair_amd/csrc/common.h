@@ -87,10 +87,11 @@ KAIR_DEV int fdiv(int n, const FDiv& f) {
 
 // Fast erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 absolute): ~12 VALU with one rcp and
 // one exp, against ~30 for erff.  Used only on bf16-compute epilogues, where the output rounding
-// (2^-9 relative) dominates; the fp32 parity path keeps erff.
+// (2^-9 relative) dominates; the fp32 parity path keeps erff.  The reciprocal is the hardware
+// v_rcp_f32 (1 ulp): __frcp_rn compiles to the 8-instruction correctly-rounded division sequence.
 KAIR_DEV float erf_fast(float x) {
   const float ax = fabsf(x);
-  const float t = __frcp_rn(1.0f + 0.3275911f * ax);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * ax);
   float y = 1.061405429f;
   y = fmaf(y, t, -1.453152027f);
   y = fmaf(y, t, 1.421413741f);
@@ -102,7 +103,7 @@ KAIR_DEV float erf_fast(float x) {
 // GELU and GELU' of the same x sharing one rcp and one exp (gelu_fast / gelu_grad_fast maths)
 KAIR_DEV void gelu_pair_fast(float x, float& y, float& dy) {
   const float z = x * 0.70710678118654752f, az = fabsf(z);
-  const float t = __frcp_rn(1.0f + 0.3275911f * az);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * az);
   float p = 1.061405429f;
   p = fmaf(p, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
@@ -110,6 +111,25 @@ KAIR_DEV void gelu_pair_fast(float x, float& y, float& dy) {
   p = fmaf(p, t, 0.254829592f);
   const float e = __expf(-az * az);   // = exp(-x^2 / 2)
   const float cdf = 0.5f * (1.0f + copysignf(1.0f - p * t * e, z));
+  y = x * cdf;
+  dy = cdf + x * 0.39894228040143268f * e;
+}
+// Two elements at once: the polynomial / products as packed fp32 (v_pk_fma_f32 / v_pk_mul_f32,
+// two lanes' worth per instruction); rcp and exp stay per element.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+KAIR_DEV void gelu_pair_fast2(f32x2 x, f32x2& y, f32x2& dy) {
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 az = {fabsf(z.x), fabsf(z.y)};
+  const f32x2 den = az * 0.3275911f + 1.0f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 p = t * 1.061405429f - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const f32x2 sq = -(az * az);
+  const f32x2 e = {__expf(sq.x), __expf(sq.y)};
+  const f32x2 q = 1.0f - p * t * e;
+  const f32x2 cdf = 0.5f * (1.0f + (f32x2){copysignf(q.x, z.x), copysignf(q.y, z.y)});
   y = x * cdf;
   dy = cdf + x * 0.39894228040143268f * e;
 }

@@ -622,12 +622,15 @@ __global__ __launch_bounds__(1024) void swin_mlp_fwd_kernel(const MlpFwdArgs a) 
           const float xs[4] = {U[4 * gg] + bb.x, U[4 * gg + 1] + bb.y, U[4 * gg + 2] + bb.z, U[4 * gg + 3] + bb.w};
           bf16x4 hv, gv;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int cc = HH * half + col + e;
-            float y, dy;
-            gelu_pair_fast(xs[e], y, dy);
-            hv[e] = cc < a.hd ? (bf16)y : (bf16)(cc == a.hd ? 1.f : 0.f);
-            gv[e] = (bf16)dy;
+          for (int e = 0; e < 4; e += 2) {
+            f32x2 y, dy;
+            gelu_pair_fast2((f32x2){xs[e], xs[e + 1]}, y, dy);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int cc = HH * half + col + e + q;
+              hv[e + q] = cc < a.hd ? (bf16)y[q] : (bf16)(cc == a.hd ? 1.f : 0.f);
+              gv[e + q] = (bf16)dy[q];
+            }
           }
           *(bf16x4*)(sU + (rt * 32 + l31) * LDU + col) = hv;
           *(bf16x4*)(sG + (rt * 32 + l31) * LDU + col) = gv;
