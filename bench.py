@@ -247,7 +247,7 @@ def psnr_parity(net_gpu, device, n_eval=8):
 
 
 def other_configs(device):
-    """The other BASELINE.json configs, one short fused-trainer (USRNet: autograd + torch Adam) run each
+    """The other BASELINE.json configs, one short fused-trainer run each (USRNet with (k, sf, sigma) inputs)
     on this GPU (tools/bench_models.py; synthetic seeded inputs resident in HBM): patches/s and the
     fraction of the dense bf16 MFMA peak their training FLOPs reach.  C1 (DnCNN) is a CPU config in
     the reference; its network's GPU step is reported for completeness."""

@@ -109,22 +109,26 @@ class FusedTrainer:
         if self.world > 1:
             allreduce_mean_(self.flat_g, self.bucket, self.pg, self.world)
 
-    def _fwd_bwd(self, L, Hh):
+    def _fwd_bwd(self, L, Hh, *cond):
+        """cond: the network's extra forward inputs (USRNet: k, sf, sigma; model_plain4.py:22-23)."""
         eng = self.engine
         drop = None
         if any(b.dp > 0 for b in eng.blocks) and self.net.training:
             from .swinir_engine import drop_path_scales
             drop = drop_path_scales(eng, L.shape[0], L.device)
         eng._packed_version = None           # weights change every step: always repack
-        eng.forward(L, drop)
+        if cond:
+            eng.forward(L, *cond)
+        else:
+            eng.forward(L, drop)
         return eng.backward_from_loss(Hh, self.grads, self.loss_weight, charb_eps=self.charb_eps)
 
     def _update(self):
         H.adam_ema(self.flat_p, self.flat_g, self.m, self.v, self.flat_e, self.flat_p.numel(), self.scal,
                    self.betas[0], self.betas[1], self.eps, self.wd, self.E_decay if self.flat_e is not None else 0.0)
 
-    def _body(self, L, Hh):
-        loss = self._fwd_bwd(L, Hh)
+    def _body(self, L, Hh, *cond):
+        loss = self._fwd_bwd(L, Hh, *cond)
         self._allreduce()
         self._update()
         return loss
@@ -202,19 +206,25 @@ class FusedTrainer:
             w.wait()   # the current stream waits for RCCL's stream (no host block)
         gu.replay()
 
-    def step(self, L, Hh):
-        """One training step on the batch (L, Hh) (device tensors).  Returns the device loss [1]."""
+    def step(self, L, Hh, *cond):
+        """One training step on the batch (L, Hh) (device tensors); cond: the network's extra forward
+        inputs (USRNet: k [B,1,kh,kw], sf int, sigma [B,1,1,1]).  Returns the device loss [1].
+        The graph is re-recorded when any input's shape or a non-tensor input (sf) changes."""
         self._set_scalars()
         if not self.use_graph:
-            out = self._body(L, Hh)
+            out = self._body(L, Hh, *cond)
             self.engine._packed_version = None
             return out
-        if self.static is None or self.static[0].shape != L.shape or self.static[1].shape != Hh.shape:
-            self.static = (torch.empty_like(L), torch.empty_like(Hh))
+        args = (L, Hh) + tuple(cond)
+        key = tuple(a.shape if torch.is_tensor(a) else ("const", a) for a in args)
+        if self.static is None or self._static_key != key:
+            self.static = tuple(torch.empty_like(a) if torch.is_tensor(a) else a for a in args)
+            self._static_key = key
             self.graph = None
             self.warm = 0
-        self.static[0].copy_(L)
-        self.static[1].copy_(Hh)
+        for dst, src in zip(self.static, args):
+            if torch.is_tensor(src):
+                dst.copy_(src)
         if self.graph is None and self.warm >= 2:
             self._capture()                  # records only; the replay below executes this step
         if self.graph is not None:

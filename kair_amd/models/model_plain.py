@@ -244,7 +244,7 @@ class ModelPlain(ModelBase):
     def optimize_parameters(self, current_step):
         if self.trainer is not None:
             self.trainer.lr = self.G_optimizer.param_groups[0]["lr"]
-            loss = self.trainer.step(self.L, self.H)
+            loss = self.trainer.step(self.L, self.H, *self._step_cond())
             self.E = None  # the fused step keeps E in its plan buffer; test() recomputes
             self.log_dict["G_loss"] = loss.item()
             return
@@ -259,6 +259,10 @@ class ModelPlain(ModelBase):
         self.log_dict["G_loss"] = G_loss.item()
         if self.opt_train["E_decay"] > 0:
             self.update_E(self.opt_train["E_decay"])
+
+    def _step_cond(self):
+        """Extra forward inputs of the fused step (none for the single-input networks)."""
+        return ()
 
     def test(self):
         self.netG.eval()

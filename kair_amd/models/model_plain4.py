@@ -1,7 +1,8 @@
 """ModelPlain4 — four-input trainer for USRNet (mirror of /root/reference/models/model_plain4.py:11-23).
 
 The reference's feed_data uses np.int (removed in numpy 1.24, SURVEY.md §0 gotcha 4); the scale
-factor is read with int() here.
+factor is read with int() here.  optimize_parameters runs the fused trainer (USRNet step program +
+L1 + fused Adam/EMA, one HIP graph per step) with (k, sf, sigma) as the step's extra inputs.
 """
 from .model_plain import ModelPlain
 
@@ -15,8 +16,9 @@ class ModelPlain4(ModelPlain):
         if need_H:
             self.H = data["H"].to(self.device)
 
-    def _fused_ok(self):
-        return False   # USRNet trains through the autograd node (its step is not graph-captured yet)
+    def _step_cond(self):
+        """USRNet's extra forward inputs (model_plain4.py:22-23) for the fused, graph-captured step."""
+        return (self.k, self.sf, self.sigma)
 
     def netG_forward(self):
         self.E = self.netG(self.L, self.k, self.sf, self.sigma)

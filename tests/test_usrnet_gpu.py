@@ -171,7 +171,8 @@ def test_usrnet_option_config_vs_oracle(lq, sf, n_iter):
 
 
 def test_usrnet_modelplain4_step():
-    """define_Model('plain4') drives the USRNet engine through autograd + torch Adam (ModelPlain4)."""
+    """define_Model('plain4') drives the USRNet engine through the fused, graph-captured trainer
+    (ModelPlain4: (k, sf, sigma) are the step's extra inputs)."""
     from kair_amd.models.select_model import define_Model
     from kair_amd.utils.utils_option import dict_to_nonedict
     opt = {"model": "plain4", "is_train": True, "dist": False, "gpu_ids": [0], "scale": 4, "path": {"models": "/tmp/k"},
@@ -195,5 +196,40 @@ def test_usrnet_modelplain4_step():
         model.optimize_parameters(step)
         losses.append(model.log_dict["G_loss"])
     after = model.netG.state_dict()
+    assert model.trainer is not None and model.trainer.graph is not None   # fused path, captured at step 3
     assert all(torch.isfinite(torch.tensor(losses)))
     assert any((after[k] - before[k]).abs().max() > 0 for k in before)
+
+
+def test_usrnet_fused_trainer_vs_oracle_trainer():
+    """4 graph-captured FusedTrainer steps of USRNet (fp32 mode: L1, Adam, EMA) against the oracle
+    trainer on the same (L, k, sf, sigma) batches (model_plain4.py:22-23 / model_plain.py:270-318)."""
+    from kair_amd.engine.trainer import FusedTrainer
+    from oracle.train import OracleTrainer
+    torch.manual_seed(31)
+    mk = lambda: USRNet(n_iter=2, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2, compute_dtype="fp32")
+    net, ema = mk(), mk()
+    ema.load_state_dict(net.state_dict())
+    ref = ocv.USRNet(n_iter=2, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2)
+    ref_e = ocv.USRNet(n_iter=2, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2)
+    ref.load_state_dict(net.state_dict(), strict=True)
+    ref_e.load_state_dict(net.state_dict(), strict=True)
+    net, ema = net.to(dev).train(), ema.to(dev).eval()
+    tr = FusedTrainer(net, ema, lr=1e-4, E_decay=0.999, use_graph=True)
+    otr = OracleTrainer(ref, ref_e, lr=1e-4, E_decay=0.999)
+    g = torch.Generator().manual_seed(32)
+    B, sf = 2, 4
+    for _ in range(4):
+        L = torch.rand(B, 3, 16, 16, generator=g)
+        Hh = torch.rand(B, 3, 64, 64, generator=g)
+        k = rand_kernel(B, 25, g).float()
+        sigma = torch.rand(B, 1, 1, 1, generator=g) * (25.0 / 255)
+        loss = tr.step(L.to(dev), Hh.to(dev), k.to(dev), sf, sigma.to(dev)).item()
+        _, lo = otr.optimize_parameters(L, Hh, forward=lambda x: ref(x, k, sf, sigma))
+        assert abs(loss - lo) < 1e-4 * abs(lo), (loss, lo)
+    assert tr.graph is not None
+    sd, sdr = net.state_dict(), ref.state_dict()
+    for key in sdr:
+        a, b = sd[key].double().cpu(), sdr[key].double()
+        r = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert r < (1e-3 if sdr[key].dim() == 1 else 1e-4), (key, r)

@@ -7,7 +7,7 @@ C1 DnCNN sigma 25, 40x40, batch 64 (BN, fused trainer)        network_dncnn.py, 
 C2 SwinIR-lightweight x2, 64-px LQ, batch 64 (fused trainer)   options/swinir/train_swinir_sr_lightweight.json
 C5 RRDBNet x4, 32-px LQ, batch 16 (fused trainer)              options/train_rrdb_psnr.json
 C3 USRNet x4, 128-px LQ (512^2 HR), batch 48, n_iter 6         options/train_usrnet.json (ModelPlain4 step:
-                                                                autograd node + torch Adam, no EMA)
+                                                                fused trainer with (k, sf, sigma) inputs, no EMA)
 Synthetic seeded inputs resident in HBM; bf16 MFMA operands, fp32 accumulation.
 FLOP/patch from BASELINE.md (FlopCounterMode, GEMM + conv only; USRNet FFTs not counted).
 """
@@ -68,9 +68,10 @@ def run(name, steps, warmup, dev):
 
 
 def run_usrnet(steps, warmup, dev):
+    from kair_amd.engine.trainer import FusedTrainer
     from kair_amd.models.network_usrnet import USRNet
     net = USRNet(n_iter=6, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2).to(dev).train()
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    tr = FusedTrainer(net, None, lr=1e-4, E_decay=0.0, use_graph=True)   # train_usrnet.json: E_decay 0
     g = torch.Generator().manual_seed(2)
     B, lq, sf = 48, 128, 4
     L = torch.rand(B, 3, lq, lq, generator=g).to(dev)
@@ -79,13 +80,8 @@ def run_usrnet(steps, warmup, dev):
     k = (k / k.sum((-2, -1), keepdim=True)).to(dev)
     sigma = (torch.rand(B, 1, 1, 1, generator=g) * 25 / 255).to(dev)
 
-    def step():   # ModelPlain.optimize_parameters (model_plain.py:270-318) with ModelPlain4's forward
-        opt.zero_grad(set_to_none=True)
-        loss = torch.nn.functional.l1_loss(net(L, k, sf, sigma), Hh)
-        loss.backward()
-        opt.step()
-        return loss
-    dt, loss = timed(step, steps, warmup)
+    # ModelPlain.optimize_parameters (model_plain.py:270-318) with ModelPlain4's forward
+    dt, loss = timed(lambda: tr.step(L, Hh, k, sf, sigma), steps, warmup)
     return B, dt, float(loss.item())
 
 
