@@ -245,6 +245,11 @@ class SwinIREngine:
         # ~5e-4 dB of activation-rounding noise per image (tools/parity_seeds.py, DESIGN.md "parity at
         # bf16"), at +45 us per block for the attention kernel -- off unless asked for
         self.split_linear = bool(split_linear) and compute_dtype == "bf16"
+        # the two block GEMMs with no epilogue at all -- the fc1 and proj input gradients, plain bf16
+        # [M, K] x [N, K]^T -- run on the library GEMM (hipBLASLt through torch.matmul): B = 32 956 -> 982,
+        # B = 4 476 -> 480 patches/s (tools/gemm_b4.py: 31 -> 23 / 44 -> 31 us at B = 32 in isolation);
+        # every GEMM with a fused prologue / epilogue stays on the kair kernels.  KAIR_BLAS_DGRAD=0: kair
+        self.blas_dgrad = compute_dtype == "bf16" and os.environ.get("KAIR_BLAS_DGRAD", "1") == "1"
         self.upsampler, self.scale = net.upsampler, net.upscale
         self.in_ch = net.conv_first.in_channels
         self.img_range = float(net.img_range)
@@ -865,6 +870,13 @@ class SwinIREngine:
         self._wgrad(P, H.rows(P["da0"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, 64, 9 * Cp, c.map,
                     g(c.w), g(c.b), self.C)
 
+    def _plain_gemm(self, A, Bw, out, M, N, K):
+        """out[M, N] = A[M, K] . Bw[N, K]^T with no epilogue (the fc1 / proj input gradients)."""
+        if self.blas_dgrad:
+            torch.matmul(A, Bw.t(), out=out)
+        else:
+            H.gemm_nt(H.rows(A), H.rows(Bw), H.epilogue(out), M, N, K, self.cd)
+
     def _wg(self, P, A, Bop, N, K, lin, grads, ones_col):
         """One block linear's weight gradient: queued for the RSTB's grouped launch, or issued now."""
         g_w, g_b = grads[lin.w], grads[lin.b]
@@ -925,7 +937,7 @@ class SwinIREngine:
         else:
             # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
             H.gemm_nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
-            H.gemm_nt(H.rows(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
+            self._plain_gemm(dU, fc1.Wt, P["dxn"], M, Cp, self.Hdp)
             H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, None, None, False,
                             W["ln2p"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win))
             self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False))
@@ -933,7 +945,7 @@ class SwinIREngine:
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         proj, qkv = blk.proj, blk.qkv
         self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
-        H.gemm_nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
+        self._plain_gemm(Da, proj.Wt, P["dO"], M, nh * 32, Cp)
         H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
                           W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
         self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, self.cd, g(blk.table), False))
