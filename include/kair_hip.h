@@ -248,6 +248,13 @@ int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* d
                          const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
                          float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
                          const float* mask, int mask_nw, void* stream);
+/* Same, dqkv_rows != 0 (bf16 only): dqkv written as token rows [nWin*64][3*nh*32] in window order,
+ * column (part*nh + h)*32 + d -- the plain A operand of the q/k/v input-gradient GEMM (hipBLASLt)
+ * and of the q/k/v weight gradient. */
+int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
+                            const float* table, const float* lse, void* dqkv, int dqkv_rows, float* dtable,
+                            int dtable_accumulate, float* ws, long nWin, int nh, int hd, float scale, int H, int W,
+                            int shift, const float* mask, int mask_nw, void* stream);
 
 /* Deferred bias-table gradient: kair_window_attn_bwd with dtable = NULL leaves its per-group
  * partials (kair_window_attn_bwd_groups() planes of [nh][64][64]) in ws; one grouped launch then

@@ -113,6 +113,8 @@ _SIGS = {
     "kair_window_attn_bwd_ws": [c_long, c_int],
     "kair_window_attn_bwd": [c_vp, c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_int,
                              c_int, c_float, c_int, c_int, c_int, c_vp, c_int, c_vp],
+    "kair_window_attn_bwd_ex": [c_vp, c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_long,
+                                c_int, c_int, c_float, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "kair_image_to_nhwc": [c_vp, c_vp, c_int, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
     "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "kair_charbonnier_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_int, c_int,
@@ -454,11 +456,12 @@ def window_attn_bwd_ws(nWin, nh):
 
 
 def window_attn_bwd(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc, ws, nWin, nh, hd, scale, H, W, shift,
-                    mask=None):
+                    mask=None, dqkv_rows=False):
+    """dqkv_rows: dqkv as token rows [nWin*64, 3*nh*32] (bf16) instead of head-blocked."""
     mnw = mask.shape[0] if mask is not None else 0
-    check(lib().kair_window_attn_bwd(ptr(qkv), ptr(O), ldo, ptr(dO), lddo, dtype_code(qkv), ptr(table), ptr(lse),
-                                     ptr(dqkv), ptr(dtable), int(dtable_acc), ptr(ws), nWin, nh, hd, scale, H, W, shift,
-                                     ptr(mask), mnw, stream_ptr()), "window_attn_bwd")
+    check(lib().kair_window_attn_bwd_ex(ptr(qkv), ptr(O), ldo, ptr(dO), lddo, dtype_code(qkv), ptr(table), ptr(lse),
+                                        ptr(dqkv), int(dqkv_rows), ptr(dtable), int(dtable_acc), ptr(ws), nWin, nh, hd,
+                                        scale, H, W, shift, ptr(mask), mnw, stream_ptr()), "window_attn_bwd")
 
 
 def image_to_nhwc(img, out, ldc, mean, img_range, B, C, H, W):

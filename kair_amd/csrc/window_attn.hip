@@ -608,7 +608,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
                                                             bf16* __restrict__ dqkv, float* __restrict__ dB_part,
                                                             long nWin, int nh, int wpg, float scale, int H, int W,
                                                             int shift, const float* __restrict__ amask, int mask_nw,
-                                                            int stamp) {
+                                                            int stamp, int rows) {
   constexpr int LD = AT<true>::LD, LDD = 72, NW = 4, LDB = 72;
   static_assert(TOK * LDD <= 2 * TOK * LD, "the dS tile reuses the q / dO tiles");
   // per wave: q and dO tiles (after dV / dK they hold the dS tile), k tile, and the running bias
@@ -768,9 +768,12 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
     }
     if (st_on) ts[3] = stamp_now();
     // dV^T = dO^T P and dK^T = scale * Q^T dS : tiles [kt], rows = d, lane = key
-    bf16* dq_out = dqkv + blk;
-    bf16* dk_out = dqkv + part + blk;
-    bf16* dv_out = dqkv + 2 * part + blk;
+    // head-blocked [3][nWin][nh][64][32] (token stride 32), or token rows [M][3 nh 32] (rows != 0:
+    // columns (part * nh + h) * 32 + d, the q/k/v input-gradient GEMM's plain A operand)
+    const long tstr = rows ? 3L * nh * HDP : HDP;
+    bf16* dq_out = rows ? dqkv + win * TOK * tstr + h * HDP : dqkv + blk;
+    bf16* dk_out = rows ? dq_out + nh * HDP : dqkv + part + blk;
+    bf16* dv_out = rows ? dq_out + 2 * nh * HDP : dqkv + 2 * part + blk;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       f32x16 av, ak;
@@ -789,8 +792,8 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
         const bf16x4 vv = {(bf16)av[4 * g], (bf16)av[4 * g + 1], (bf16)av[4 * g + 2], (bf16)av[4 * g + 3]};
         const bf16x4 kk = {(bf16)(ak[4 * g] * scale), (bf16)(ak[4 * g + 1] * scale), (bf16)(ak[4 * g + 2] * scale),
                            (bf16)(ak[4 * g + 3] * scale)};
-        *(bf16x4*)(dv_out + key * HDP + 8 * g + 4 * hh) = vv;
-        *(bf16x4*)(dk_out + key * HDP + 8 * g + 4 * hh) = kk;
+        *(bf16x4*)(dv_out + key * tstr + 8 * g + 4 * hh) = vv;
+        *(bf16x4*)(dk_out + key * tstr + 8 * g + 4 * hh) = kk;
       }
     }
     if (st_on) ts[4] = stamp_now();
@@ -818,7 +821,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
       for (int g = 0; g < 4; ++g) {
         const bf16x4 vq = {(bf16)(aq[4 * g] * scale), (bf16)(aq[4 * g + 1] * scale), (bf16)(aq[4 * g + 2] * scale),
                            (bf16)(aq[4 * g + 3] * scale)};
-        *(bf16x4*)(dq_out + qi * HDP + 8 * g + 4 * hh) = vq;
+        *(bf16x4*)(dq_out + qi * tstr + 8 * g + 4 * hh) = vq;
       }
     }
     if (st_on) {
@@ -966,10 +969,11 @@ extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) {
   return ((g32 > g16 ? g32 : g16) + 1) * nh * TOK * TOK;
 }
 
-extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
-                                    const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
-                                    float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
-                                    const float* mask, int mask_nw, void* stream) {
+extern "C" int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
+                                       const float* table, const float* lse, void* dqkv, int dqkv_rows, float* dtable,
+                                       int dtable_accumulate, float* ws, long nWin, int nh, int hd, float scale, int H, int W,
+                                       int shift, const float* mask, int mask_nw, void* stream) {
+  KAIR_CHECK_ARG(!dqkv_rows || dtype == KAIR_BF16, "window_attn_bwd: token-row dqkv is a bf16 layout");
   KAIR_CHECK_ARG(!mask || (mask_nw > 0 && shift == 0), "window_attn_bwd: an explicit mask needs mask_nw > 0 and shift 0");
   KAIR_CHECK_ARG(qkv && O && dO && table && lse && dqkv && ws, "window_attn_bwd: null pointer");
   KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_bwd: head_dim");
@@ -983,7 +987,7 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
   if (dtype == KAIR_BF16)
     hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
                        (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw,
-                       g_stamp);
+                       g_stamp, dqkv_rows);
   else
     hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
                        ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw);
@@ -996,6 +1000,14 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
   hipLaunchKernelGGL(attn_dtable_kernel, dim3((nt + 3) / 4), dim3(256), 0, s, dB, nh, dtable, dtable_accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
+                                    const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
+                                    float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
+                                    const float* mask, int mask_nw, void* stream) {
+  return kair_window_attn_bwd_ex(qkv, O, ldo, dO, lddo, dtype, table, lse, dqkv, 0, dtable, dtable_accumulate, ws, nWin, nh,
+                                 hd, scale, H, W, shift, mask, mask_nw, stream);
 }
 
 extern "C" long kair_window_attn_bwd_groups(long nWin, int nh, int dtype) {

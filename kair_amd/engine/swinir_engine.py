@@ -947,11 +947,15 @@ class SwinIREngine:
         self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
         self._plain_gemm(Da, proj.Wt, P["dO"], M, nh * 32, Cp)
         H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
-                          W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift)
+                          W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, dqkv_rows=self.blas_dgrad)
         self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, self.cd, g(blk.table), False))
-        self._wg(P, H.qkvblk(dqkv, nh), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads,
-                 self.C)
-        H.gemm_nt(H.qkvblk(dqkv, nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
+        # dqkv as token rows (blas_dgrad): a plain A operand for both the weight and the input gradient
+        A_qkv = H.rows(dqkv.view(M, qkv.Np)) if self.blas_dgrad else H.qkvblk(dqkv, nh)
+        self._wg(P, A_qkv, H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads, self.C)
+        if self.blas_dgrad:
+            self._plain_gemm(dqkv.view(M, qkv.Np), qkv.Wt, P["dxn"], M, Cp, qkv.Np)
+        else:
+            H.gemm_nt(H.qkvblk(dqkv, nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
         n = blk.n1
         cp = None
         if j > 0:   # the previous block's MLP operand: s_mlp(prev) * dL/d x_in

@@ -365,6 +365,13 @@ def test_window_attention_fwd_bwd(dtype, shift):
     assert rel_err(d[1, ..., :hd], kr.grad) < tolb
     assert rel_err(d[2, ..., :hd], vr.grad) < tolb
     assert rel_err(dtab, tr.grad) < tolb
+    if dtype == H.BF16:   # token-row dqkv layout [nWin*64][3*nh*32] (kair_window_attn_bwd_ex): the same bits
+        dr = torch.empty(nWin * 64, 3 * nh * 32, device=dev, dtype=torch.bfloat16)
+        H.window_attn_bwd(qkv_d, O, nh * 32, dO.view(nWin * 64, nh * 32).to(dev, DT[dtype]), nh * 32, table.to(dev),
+                          lse, dr, dtab, False, ws, nWin, nh, hd, scale, Hh, Ww, shift, dqkv_rows=True)
+        torch.cuda.synchronize()
+        blocked = dqkv.cpu().permute(1, 3, 0, 2, 4).reshape(nWin * 64, 3 * nh * 32)   # [win][tok][part][h][d]
+        assert torch.equal(dr.cpu(), blocked)
 
 
 def test_l1_and_adam():
