@@ -305,6 +305,9 @@ class SwinIREngine:
         self._dtab_pending = []   # (partials, nWin, nh, dtype, dtable, accumulate) of its attention blocks
         self._conv_pending = []   # the RSTB conv's weight gradient (_wgrad arguments)
         self._side = None         # side stream of the deferred per-RSTB gradient work
+        # KAIR_SIDE_STREAM=0: the deferred per-RSTB work runs in place on the main stream (A/B timing)
+        self.side_stream = (self.grouped_wgrad and torch.cuda.is_available() and
+                            os.environ.get("KAIR_SIDE_STREAM", "1") == "1")
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -811,7 +814,7 @@ class SwinIREngine:
                 torch.cuda.current_stream().wait_stream(self._side)
                 self._segment_done()
                 side_open = False
-            if self.grouped_wgrad and torch.cuda.is_available():
+            if self.side_stream:
                 side_pending = True     # forked at the next RSTB (or below, after the last one)
             else:
                 self._flush_deferred(P)
@@ -889,7 +892,7 @@ class SwinIREngine:
         """Issue the RSTB's deferred gradient work: on the side stream when the block weight gradients
         are grouped (returns True: the caller joins it), else in place on the current stream."""
         side = None
-        if self.grouped_wgrad and torch.cuda.is_available():
+        if self.side_stream:
             if self._side is None:
                 self._side = torch.cuda.Stream(device=self.device)
             side = self._side
