@@ -250,6 +250,10 @@ class SwinIREngine:
         # B = 4 476 -> 480 patches/s (tools/gemm_b4.py: 31 -> 23 / 44 -> 31 us at B = 32 in isolation);
         # every GEMM with a fused prologue / epilogue stays on the kair kernels.  KAIR_BLAS_DGRAD=0: kair
         self.blas_dgrad = compute_dtype == "bf16" and os.environ.get("KAIR_BLAS_DGRAD", "1") == "1"
+        # KAIR_BLAS_FC2=1: the fc2 input gradient on the library GEMM too, its GELU' gate as a separate
+        # multiply (B = 32 1010 -> 1036, B = 4 unchanged) -- off: dU is then rounded to bf16 twice, and the
+        # bench's 8-image uint8 PSNR delta rose 3.6e-4 -> 8.3e-4 dB, too close to the 1e-3 bar
+        self.blas_fc2 = self.blas_dgrad and os.environ.get("KAIR_BLAS_FC2", "0") == "1"
         self.upsampler, self.scale = net.upsampler, net.upscale
         self.in_ch = net.conv_first.in_channels
         self.img_range = float(net.img_range)
@@ -939,7 +943,11 @@ class SwinIREngine:
                            s_attn, HW, Hh, Ww, blk.shift, g(n.weight), g(n.bias), P["mlp_ws"], M, Cp, self.Hdp)
         else:
             # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
-            H.gemm_nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
+            if self.blas_fc2:   # A/B: library GEMM, then the GELU' gate as a separate multiply
+                torch.matmul(Dm, fc2.Wt.t(), out=dU)
+                dU.mul_(S["u"])
+            else:
+                H.gemm_nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
             self._plain_gemm(dU, fc1.Wt, P["dxn"], M, Cp, self.Hdp)
             H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, None, None, False,
                             W["ln2p"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win))
