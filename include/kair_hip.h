@@ -401,6 +401,31 @@ int kair_hypanet_bwd(const float* sigma, float sf, const float* W1, const float*
                      float* gW1, float* gb1, float* gW2, float* gb2, float* gW3, float* gb3, int accumulate,
                      void* stream);
 
+/* ---- Swin-block input gradients as row GEMMs with fused consumers (bf16, rowgemm.hip) --------
+ * Y[m, :] = A[m, :K] . W^T for the input gradient of one block linear (nn.Linear backward,
+ * network_swinir.py:19-20 fc1 / fc2, :105 qkv, :107 proj).  A: bf16 rows [M][lda] (K = 192, 384 or
+ * 576 columns, 16-byte aligned); W: the linear's weight in transposed MFMA-fragment order (pack
+ * kind 13: [N/32][K/16][64][8], the dgrad output dimension N = 192 or 384 first).
+ *   kair_rowgemm_store: out[m][n] = bf16(Y)                       (proj input gradient -> dO)
+ *   kair_rowgemm_gate:  out[m][n] = bf16(Y * gate[m][n])           (fc2 input gradient through the
+ *                                                                   stored GELU'(fc1 pre-activation))
+ *   kair_rowgemm_lnbwd: N = 192; Y = dL/d(LayerNorm output) of rows in the window order `win`
+ *     (nn.LayerNorm backward, network_swinir.py:199 norm1 / :205 norm2): D[t] += LN-backward(Y)
+ *     for token t = win_to_token(m) (x, mean, rstd, D token rows; x and D share the row stride),
+ *     the finished row also written as `copy` (bf16, optional), and the dgamma / dbeta partials
+ *     [kair_rowgemm_ln_blocks(M, K)][2][C] left in `part` for kair_ln_param_reduce_grouped.
+ *   Replaces kair_gemm_nt / hipBLASLt + kair_layernorm_bwd for these products: Y stays fp32 in
+ *   registers (the unfused path rounded it to bf16 and round-tripped it through HBM). */
+int kair_rowgemm_store(const void* A, long lda, long M, int K, const void* W, int N, void* out, long ldo,
+                       void* stream);
+int kair_rowgemm_gate(const void* A, long lda, long M, int K, const void* W, int N, const void* gate, long ldg,
+                      void* out, long ldo, void* stream);
+long kair_rowgemm_ln_blocks(long M, int K);
+int kair_rowgemm_lnbwd(const void* A, long lda, long M, int K, const void* W, const float* x, long ldx,
+                       const float* gamma, const float* mean, const float* rstd, int C, float* D, long ldD,
+                       int win_H, int win_W, int win_ws, int win_shift, const kair_copy_desc* copy, float* part,
+                       void* stream);
+
 /* ---- training-patch synthesis ------------------------------------------
  * pool: fp32 NCHW image pool [N][C][Hs][Ws] in [0, 1] (HBM-resident); params: int4 per sample
  * {image, rnd_h, rnd_w, mode} (rnd_* in L coordinates for SR, H coordinates for denoising; mode the

@@ -155,10 +155,15 @@ _SIGS = {
     "kair_swin_mlp_bwd": [c_vp, c_long, c_vp, c_long, c_vp, c_vp, c_vp, c_long, c_vp, c_long, c_vp, c_vp, c_vp, c_int,
                           c_vp, c_long, c_vp, c_long, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_long,
                           c_int, c_int, c_vp],
+    "kair_rowgemm_store": [c_vp, c_long, c_long, c_int, c_vp, c_int, c_vp, c_long, c_vp],
+    "kair_rowgemm_gate": [c_vp, c_long, c_long, c_int, c_vp, c_int, c_vp, c_long, c_vp, c_long, c_vp],
+    "kair_rowgemm_ln_blocks": [c_long, c_int],
+    "kair_rowgemm_lnbwd": [c_vp, c_long, c_long, c_int, c_vp, c_vp, c_long, c_vp, c_vp, c_vp, c_int, c_vp, c_long,
+                           c_int, c_int, c_int, c_int, ctypes.POINTER(CopyDesc), c_vp, c_vp],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
-_RESTYPE = {"kair_layernorm_bwd_blocks": c_long, "kair_window_attn_bwd_groups": c_long, "kair_wgrad_grouped_ws": c_long, "kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
+_RESTYPE = {"kair_layernorm_bwd_blocks": c_long, "kair_rowgemm_ln_blocks": c_long, "kair_window_attn_bwd_groups": c_long, "kair_wgrad_grouped_ws": c_long, "kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
             "kair_pack_table_build": c_long}
 
 _lib = None
@@ -434,10 +439,13 @@ def layernorm_bwd_blocks(M):
 
 
 def ln_param_reduce_grouped(jobs):
-    """jobs: (partials left by layernorm_bwd(dgamma=None, dbeta=None), M, C, dgamma, dbeta, accumulate)."""
+    """jobs: (partials left by layernorm_bwd(dgamma=None, dbeta=None), M, C, dgamma, dbeta, accumulate[, nb]);
+    nb (the partial-row count) defaults to layernorm_bwd's for M (rowgemm_lnbwd: rowgemm_ln_blocks)."""
     arr = (LnParamJob * len(jobs))()
-    for i, (part, M, C, dg, db, acc) in enumerate(jobs):
-        arr[i].part, arr[i].nb, arr[i].C = ptr(part), layernorm_bwd_blocks(M), C
+    for i, job in enumerate(jobs):
+        part, M, C, dg, db, acc = job[:6]
+        nb = job[6] if len(job) > 6 else layernorm_bwd_blocks(M)
+        arr[i].part, arr[i].nb, arr[i].C = ptr(part), nb, C
         arr[i].dgamma, arr[i].dbeta, arr[i].accumulate = ptr(dg), ptr(db), int(acc)
     check(lib().kair_ln_param_reduce_grouped(arr, len(jobs), stream_ptr()), "ln_param_reduce_grouped")
 
@@ -626,3 +634,44 @@ def swin_mlp_bwd(dc, gd, w2t, w1t, du, x, gamma, mean, rstd, C, D, dco, rowscale
                                   ptr(x), x.shape[-1], ptr(gamma), ptr(mean), ptr(rstd), C, ptr(D), D.shape[-1], ptr(dco),
                                   dco.shape[-1], ptr(rowscale), rows_per_scale, H, W, shift, ptr(dgamma), ptr(dbeta),
                                   int(dparam_acc), ptr(ws), M, Cp, Hp, stream_ptr()), "swin_mlp_bwd")
+
+
+# ------------------------------------------------------------------------------------------
+# Swin-block input gradients as row GEMMs with fused consumers (rowgemm.hip, bf16)
+# ------------------------------------------------------------------------------------------
+def _rg_check(A, W, K):
+    require_device(A, W)
+    if A.dtype != torch.bfloat16 or W.dtype != torch.bfloat16:
+        raise TypeError("kair rowgemm: bf16 operands only")
+    if A.stride(-1) != 1 or A.shape[-1] < K:
+        raise ValueError("kair rowgemm: A must be row-major with at least K columns")
+
+
+def rowgemm_store(A, M, K, W, N, out):
+    """out[m, :N] = bf16(A[m, :K] . W^T), W in pack kind 13 (kair_rowgemm_store)."""
+    _rg_check(A, W, K)
+    check(lib().kair_rowgemm_store(ptr(A), A.stride(0) if A.dim() > 1 else K, M, K, ptr(W), N, ptr(out),
+                                   out.stride(0) if out.dim() > 1 else N, stream_ptr()), "rowgemm_store")
+
+
+def rowgemm_gate(A, M, K, W, N, gate, out):
+    """out[m, :N] = bf16((A[m, :K] . W^T) * gate[m, :N]) (kair_rowgemm_gate)."""
+    _rg_check(A, W, K)
+    check(lib().kair_rowgemm_gate(ptr(A), A.stride(0), M, K, ptr(W), N, ptr(gate), gate.stride(0), ptr(out),
+                                  out.stride(0), stream_ptr()), "rowgemm_gate")
+
+
+def rowgemm_ln_blocks(M, K):
+    n = lib().kair_rowgemm_ln_blocks(M, K)
+    if n < 0:
+        check(-1, "rowgemm_ln_blocks")
+    return n
+
+
+def rowgemm_lnbwd(A, M, K, W, x, gamma, mean, rstd, C, D, part, win=(0, 0, 0, 0), copy=None):
+    """D[t] += LayerNorm-backward(A . W^T) with the copy / dgamma-dbeta partials (kair_rowgemm_lnbwd)."""
+    _rg_check(A, W, K)
+    check(lib().kair_rowgemm_lnbwd(ptr(A), A.stride(0), M, K, ptr(W), ptr(x), x.stride(0), ptr(gamma), ptr(mean),
+                                   ptr(rstd), C, ptr(D), D.stride(0), *win,
+                                   ctypes.byref(copy) if copy is not None else None, ptr(part), stream_ptr()),
+          "rowgemm_lnbwd")

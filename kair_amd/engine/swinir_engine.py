@@ -190,11 +190,12 @@ class _Blk:
         self.scale = blk.attn.scale
         Hd = blk.mlp.fc1.out_features
         sp = eng.split_linear
-        fa, fm, fb = eng.fused_attn, eng.fused_mlp, eng.fused_mlp_bwd
-        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=fa, split=sp, rows=not fa)
-        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=fa, split=sp, rows=not fa)
-        self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp), frag=fm, split=sp, frag_t=fb, rows=not fm)
-        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=fm, split=sp, frag_t=fb, rows=not fm)
+        fa, fm, fb, rg = eng.fused_attn, eng.fused_mlp, eng.fused_mlp_bwd, eng.rowgemm
+        # frag_t (pack kind 13): the input-gradient operand of the row GEMMs / the fused MLP backward
+        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=fa, split=sp, rows=not fa, frag_t=rg)
+        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=fa, split=sp, rows=not fa, frag_t=rg)
+        self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp), frag=fm, split=sp, frag_t=fb or rg, rows=not fm)
+        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=fm, split=sp, frag_t=fb or rg, rows=not fm)
 
     def linears(self):
         return (self.qkv, self.proj, self.fc1, self.fc2)
@@ -245,15 +246,11 @@ class SwinIREngine:
         # ~5e-4 dB of activation-rounding noise per image (tools/parity_seeds.py, DESIGN.md "parity at
         # bf16"), at +45 us per block for the attention kernel -- off unless asked for
         self.split_linear = bool(split_linear) and compute_dtype == "bf16"
-        # the two block GEMMs with no epilogue at all -- the fc1 and proj input gradients, plain bf16
-        # [M, K] x [N, K]^T -- run on the library GEMM (hipBLASLt through torch.matmul): B = 32 956 -> 982,
-        # B = 4 476 -> 480 patches/s (tools/gemm_b4.py: 31 -> 23 / 44 -> 31 us at B = 32 in isolation);
-        # every GEMM with a fused prologue / epilogue stays on the kair kernels.  KAIR_BLAS_DGRAD=0: kair
-        self.blas_dgrad = compute_dtype == "bf16" and os.environ.get("KAIR_BLAS_DGRAD", "1") == "1"
-        # KAIR_BLAS_FC2=1: the fc2 input gradient on the library GEMM too, its GELU' gate as a separate
-        # multiply (B = 32 1010 -> 1036, B = 4 unchanged) -- off: dU is then rounded to bf16 twice, and the
-        # bench's 8-image uint8 PSNR delta rose 3.6e-4 -> 8.3e-4 dB, too close to the 1e-3 bar
-        self.blas_fc2 = self.blas_dgrad and os.environ.get("KAIR_BLAS_FC2", "0") == "1"
+        # Swin-block input gradients on the row GEMMs with fused consumers (kair_rowgemm_*, csrc/rowgemm.hip):
+        # fc2 (GELU' gate), fc1 + LayerNorm-2 backward, proj, q/k/v + LayerNorm-1 backward -- bf16, Cp = 192
+        # geometry (classical / real-world x4); other widths run the same products on kair_gemm_nt +
+        # kair_layernorm_bwd.  No library GEMM is on the training path.
+        self.rowgemm = (compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384 and self.nh * 32 == self.Cp)
         self.upsampler, self.scale = net.upsampler, net.upscale
         self.in_ch = net.conv_first.in_channels
         self.img_range = float(net.img_range)
@@ -439,6 +436,9 @@ class SwinIREngine:
                      "ln1p": e(2 * 2048 * Cp), "ln2p": e(2 * 2048 * Cp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
                     for _ in range(depth)] for _ in range(2)]
         P["G3"] = e(M, Cp)   # third residual-gradient buffer (rotation, see backward())
+        if self.rowgemm:   # LayerNorm-parameter partial rows the fused row GEMMs leave (<= the ln*p buffers' 2048)
+            P["rg_nb"] = {k: H.rowgemm_ln_blocks(M, k) for k in (Hdp, 3 * nh * 32)}
+            assert max(P["rg_nb"].values()) <= 2048, P["rg_nb"]
         P["dO"] = e(M, nh * 32, dt=T)
         P["ln_ws"] = e(2 * 2048 * Cp)   # kair_layernorm_bwd: 2 * 2048 * C floats
         P["attn_ws"] = e(H.window_attn_bwd_ws(nWin, nh))
@@ -877,13 +877,6 @@ class SwinIREngine:
         self._wgrad(P, H.rows(P["da0"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, 64, 9 * Cp, c.map,
                     g(c.w), g(c.b), self.C)
 
-    def _plain_gemm(self, A, Bw, out, M, N, K):
-        """out[M, N] = A[M, K] . Bw[N, K]^T with no epilogue (the fc1 / proj input gradients)."""
-        if self.blas_dgrad:
-            torch.matmul(A, Bw.t(), out=out)
-        else:
-            H.gemm_nt(H.rows(A), H.rows(Bw), H.epilogue(out), M, N, K, self.cd)
-
     def _wg(self, P, A, Bop, N, K, lin, grads, ones_col):
         """One block linear's weight gradient: queued for the RSTB's grouped launch, or issued now."""
         g_w, g_b = grads[lin.w], grads[lin.b]
@@ -941,14 +934,17 @@ class SwinIREngine:
             # fc2 / fc1 input gradients + LN2 backward in one launch
             H.swin_mlp_bwd(Dm, S["u"], fc2.Wgt, fc1.Wgt, dU, S["mid"], n.weight, S["m2"], S["r2"], self.C, D, Da,
                            s_attn, HW, Hh, Ww, blk.shift, g(n.weight), g(n.bias), P["mlp_ws"], M, Cp, self.Hdp)
+        elif self.rowgemm:
+            # S["u"] holds GELU'(fc1 pre-activation), stored by the forward: the fc2 input gradient is gated
+            H.rowgemm_gate(Dm, M, Cp, fc2.Wgt, self.Hdp, S["u"], dU)
+            # fc1 input gradient -> LN2 backward into D, the window-order proj operand Da = s_attn * dL/dmid
+            H.rowgemm_lnbwd(dU, M, self.Hdp, fc1.Wgt, S["mid"], n.weight, S["m2"], S["r2"], self.C, D, W["ln2p"],
+                            copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win))
+            self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False, P["rg_nb"][self.Hdp]))
         else:
             # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
-            if self.blas_fc2:   # A/B: library GEMM, then the GELU' gate as a separate multiply
-                torch.matmul(Dm, fc2.Wt.t(), out=dU)
-                dU.mul_(S["u"])
-            else:
-                H.gemm_nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
-            self._plain_gemm(dU, fc1.Wt, P["dxn"], M, Cp, self.Hdp)
+            H.gemm_nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
+            H.gemm_nt(H.rows(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
             H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, None, None, False,
                             W["ln2p"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win))
             self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False))
@@ -956,25 +952,31 @@ class SwinIREngine:
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         proj, qkv = blk.proj, blk.qkv
         self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
-        self._plain_gemm(Da, proj.Wt, P["dO"], M, nh * 32, Cp)
-        H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
-                          W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, dqkv_rows=self.blas_dgrad)
-        self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, self.cd, g(blk.table), False))
-        # dqkv as token rows (blas_dgrad): a plain A operand for both the weight and the input gradient
-        A_qkv = H.rows(dqkv.view(M, qkv.Np)) if self.blas_dgrad else H.qkvblk(dqkv, nh)
-        self._wg(P, A_qkv, H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads, self.C)
-        if self.blas_dgrad:
-            self._plain_gemm(dqkv.view(M, qkv.Np), qkv.Wt, P["dxn"], M, Cp, qkv.Np)
+        if self.rowgemm:
+            H.rowgemm_store(Da, M, Cp, proj.Wgt, Cp, P["dO"])
         else:
-            H.gemm_nt(H.qkvblk(dqkv, nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
+            H.gemm_nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
+        rows = self.rowgemm   # dq/dk/dv as token rows [M][3 nh 32]: the row GEMM's A operand
+        H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
+                          W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, dqkv_rows=rows)
+        self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, self.cd, g(blk.table), False))
+        A_qkv = H.rows(dqkv.view(M, qkv.Np)) if rows else H.qkvblk(dqkv, nh)
+        self._wg(P, A_qkv, H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads, self.C)
         n = blk.n1
         cp = None
         if j > 0:   # the previous block's MLP operand: s_mlp(prev) * dL/d x_in
             cp = H.copy_desc(P["gw"][par][j - 1]["Dm"], rowscale=drop[bi - 1, 1] if drop is not None else None,
                              rows_per_scale=HW)
-        H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
-                        W["ln1p"], M, self.C, win, copy=cp)
-        self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False))
+        if rows:
+            # q/k/v input gradient (rows in window order) -> LN1 backward into D (+ the previous block's operand)
+            H.rowgemm_lnbwd(dqkv.view(M, qkv.Np), M, qkv.Np, qkv.Wgt, x_in, n.weight, S["m1"], S["r1"], self.C, D,
+                            W["ln1p"], win=win, copy=cp)
+            self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False, P["rg_nb"][qkv.Np]))
+        else:
+            H.gemm_nt(H.qkvblk(dqkv, nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
+            H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
+                            W["ln1p"], M, self.C, win, copy=cp)
+            self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False))
 
 
 class SwinIRFunction(torch.autograd.Function):
