@@ -47,106 +47,137 @@ def _time(launch, reps):
     return e0.elapsed_time(e1) / reps
 
 
-def time_fused_kernels(engine, reps=30):
-    """HIP-event timing (torch's current stream = the stream the kernels launch on) of the two fused
-    Swin-block kernels of block 0 at the step's exact arguments -- the two largest shares of the step
-    (profiles/r02_step_breakdown_b32.txt):
+# ---- in-step kernel timing and algorithmic bytes -------------------------------------------------
+# One eager forward + loss + backward of the timed configuration with a HIP-event pair around every
+# libkair launch, recorded on the stream that launch uses (torch's current stream at the call: the main
+# stream, or the engine's side stream for the deferred weight-gradient work), so concurrency with the
+# side stream is what the graph-replayed step sees.  A launch's role is its call site in the engine.
+_REAL = {576: 540, 384: 360, 192: 180}   # padded operand width -> the reference's width (C 180, 2C, 3C)
 
-      mlp:  kair_swin_mlp_fwd  (LN2 + fc1 + GELU + fc2 + residual, network_swinir.py:274-276, 24-30)
-      attn: kair_swin_attn_fwd (LN1 + QKV + window attention + proj + residual, :239-272, 114-145)
 
-    Algorithmic bytes / FLOPs (unpadded C = 180, hidden 360, 64-token units):
-      mlp  per 64 rows: x in + out (fp32) 2 x 46080, ln2 23040, g = GELU'(u) and h (bf16) 2 x 46080,
-           mean/rstd 512 = 207872 B; 2 x 2 x 64 x 180 x 360 = 16.59 MFLOP
-      attn per window: x in + mid out (fp32) 2 x 46080, ln1 / O 2 x 23040, q/k/v 69120, lse 1536,
-           mean/rstd 512 = 209408 B; qkv 12.44 + q.k^T / p.v 2.95 + proj 4.15 = 19.54 MFLOP
-    plus each kernel's weights once per launch.  Both sit near 80-135 FLOP/B, below the 312 FLOP/B
-    ridge, so the byte roofline binds."""
-    from kair_amd import _hip as H
-    P = engine.cur
-    blk, S = engine.blocks[0], P["blocks"][0]
-    nh, Cp, C = engine.nh, engine.Cp, engine.C
-    M, Hh, Ww = P["M"], P["H"], P["W"]
-    nWin = P["nWin"]
-    if not (engine.fused_attn and engine.fused_mlp):
-        raise RuntimeError("bench roofline: the fused block kernels are not in use")
+def _alg_bytes(fn, a):
+    """Algorithmic bytes of one launch (reference-width operands read / written once, fp32 4 B, bf16 2 B),
+    or None for launch kinds without a formula (never the dominant ones)."""
     T = 64
+    if fn == "swin_mlp_fwd":          # x in + out (fp32), ln2, GELU' and GELU (bf16), mean / rstd; weights once
+        C, hd, M = a[5], a[15], a[22]
+        return (M // T) * (2 * T * C * 4 + T * C * 2 + 2 * T * hd * 2 + T * 8) + 2 * 2 * C * hd
+    if fn == "swin_attn_fwd":         # x in + mid out, ln1 / O, q / k / v, lse, mean / rstd; weights once
+        C, nWin, nh = a[5], a[25], a[26]
+        return nWin * (2 * T * C * 4 + 2 * T * C * 2 + 3 * T * C * 2 + nh * T * 4 + T * 8) + 2 * (3 * C * C + C * C)
+    if fn == "window_attn_bwd":       # q, k, v, O, dO, lse in; dq, dk, dv out
+        nWin, nh, hd = a[11], a[12], a[13]
+        M, Cr = nWin * T, nh * hd
+        return M * (3 * Cr * 2 + 2 * Cr * 2 + nh * 4 + 3 * Cr * 2)
+    if fn == "rowgemm_gate":          # A in, gate in, out
+        M, K, N = a[1], a[2], a[4]
+        return M * (_REAL[K] * 2 + 2 * _REAL[N] * 2)
+    if fn == "rowgemm_store":
+        M, K, N = a[1], a[2], a[4]
+        return M * (_REAL[K] * 2 + _REAL[N] * 2)
+    if fn == "rowgemm_lnbwd":         # A in, x in, D in + out, bf16 copy out, mean / rstd
+        M, K, C = a[1], a[2], a[8]
+        return M * (_REAL[K] * 2 + C * 4 + 2 * C * 4 + C * 2 + 8)
+    return None
+
+
+def _alg_flops(fn, a):
+    T = 64
+    if fn == "swin_attn_fwd":
+        C, nWin = a[5], a[25]
+        return nWin * (2 * T * C * 3 * C + 2 * 2 * T * T * C + 2 * T * C * C)
+    if fn == "swin_mlp_fwd":
+        C, hd, M = a[5], a[15], a[22]
+        return M * 2 * 2 * C * hd
+    if fn == "window_attn_bwd":        # S, dP, dV, dK, dQ: five 64 x 64 x hd products per (window, head)
+        nWin, nh, hd = a[11], a[12], a[13]
+        return nWin * nh * 5 * 2 * T * T * hd
+    if fn in ("rowgemm_gate", "rowgemm_store", "rowgemm_lnbwd"):
+        M, K = a[1], a[2]
+        N = a[4] if fn != "rowgemm_lnbwd" else 192
+        return 2 * M * _REAL[K] * _REAL[N]
+    return None
+
+
+_TIMED = ("gemm_nt", "gemm_tn", "wgrad_finalize", "colsum", "layernorm_fwd", "layernorm_bwd", "row_copy", "window_attn_fwd",
+          "window_attn_bwd", "ln_param_reduce_grouped", "attn_dtable_grouped", "image_to_nhwc", "l1_loss", "axpy",
+          "swin_attn_fwd", "swin_mlp_fwd", "rowgemm_store", "rowgemm_gate", "rowgemm_lnbwd")
+
+
+def time_roles(tr):
+    """{role: {kernel, launches, ms (mean in-step), bytes, flops}} over one eager fwd + loss + bwd."""
+    from kair_amd import _hip as H
+    rec = []
+
+    def wrap(name, f):
+        def g(*a, **k):
+            fr = sys._getframe(1)
+            role = f"{name} @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}"
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            f(*a, **k)
+            e1.record()
+            rec.append((role, name, a, e0, e1))
+        return g
+
+    orig = {n: getattr(H, n) for n in _TIMED}
+    run0 = H.WgradGroup.run
+
+    def wg_run(self, ws):
+        fr = sys._getframe(1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        run0(self, ws)
+        e1.record()
+        rec.append((f"wgrad_grouped @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}", "wgrad_grouped", (), e0, e1))
+    for n in _TIMED:
+        setattr(H, n, wrap(n, orig[n]))
+    H.WgradGroup.run = wg_run
+    try:
+        for _ in range(2):   # the second pass is the one kept (first-touch effects out of the way)
+            rec.clear()
+            tr._fwd_bwd(*tr.static)
+        torch.cuda.synchronize()
+    finally:
+        for n in _TIMED:
+            setattr(H, n, orig[n])
+        H.WgradGroup.run = run0
     out = {}
-
-    def attn():
-        H.swin_attn_fwd(P["s0"], Cp, blk.n1.weight, blk.n1.bias, blk.n1.eps, C, S["ln1"], Cp, S["m1"], S["r1"],
-                        blk.qkv.Wg, blk.qkv.bp, S["qkv"], blk.table, blk.scale, S["O"], nh * 32, C // nh, S["lse"],
-                        blk.proj.Wg, blk.proj.bp, None, Hh * Ww, S["mid"], Cp, nWin, nh, Hh, Ww, blk.shift,
-                        w_split=blk.qkv.split)
-    per = 2 * T * C * 4 + 2 * T * C * 2 + 3 * T * C * 2 + nh * T * 4 + T * 8
-    out["attn"] = {"kernel": "swin_attn_fwd_kernel<6,1> (fused LN1+QKV+window attention+proj+residual, "
-                             "network_swinir.py:239-272)", "rocprof_key": "swin_attn_fwd_kernel<6, 1>",
-                   "ms": _time(attn, reps), "units": nWin, "bytes_per_unit": per,
-                   "bytes": nWin * per + 2 * (3 * C * C + C * C),
-                   "flops": nWin * (2 * T * C * 3 * C + 2 * 2 * T * T * C + 2 * T * C * C)}
-    f1, f2 = blk.fc1, blk.fc2
-    Hd = f1.N
-
-    def mlp():
-        H.swin_mlp_fwd(S["mid"], Cp, blk.n2.weight, blk.n2.bias, blk.n2.eps, C, S["ln2"], Cp, S["m2"], S["r2"],
-                       f1.Wg, f1.bp, S["u"], S["h"], engine.Hdp, Hd, f2.Wg, f2.bp, None, Hh * Ww, S["out"], Cp, M, Cp,
-                       engine.Hdp, w_split=f1.split)
-    tiles = M // T
-    per = 2 * T * C * 4 + T * C * 2 + 2 * T * Hd * 2 + T * 8
-    out["mlp"] = {"kernel": "swin_mlp_fwd_kernel<1> (fused LN2+fc1+GELU+fc2+residual, network_swinir.py:274-276, "
-                            "24-30)", "rocprof_key": "swin_mlp_fwd_kernel<1>",
-                  "ms": _time(mlp, reps), "units": tiles, "bytes_per_unit": per,
-                  "bytes": tiles * per + 2 * 2 * C * Hd, "flops": tiles * 2 * 2 * T * C * Hd}
+    for role, name, a, e0, e1 in rec:
+        d = out.setdefault(role, {"kernel": name, "launches": 0, "ms_total": 0.0, "bytes": _alg_bytes(name, a),
+                                  "flops": _alg_flops(name, a), "rocprof": rocprof_name(name, a)})
+        d["launches"] += 1
+        d["ms_total"] += e0.elapsed_time(e1)
+    for d in out.values():
+        d["ms"] = d["ms_total"] / d["launches"]
     return out
 
 
-def time_in_step(engine, L, drop):
-    """In-step durations of the fused kernels: one eager forward of the step (same batch, DropPath
-    scales, every block's own weights and the caches the preceding kernels leave), a HIP event pair
-    on the launch stream around each kair_swin_attn_fwd / kair_swin_mlp_fwd call.  This is the
-    duration rocprofv3's kernel trace of the graph-replayed step reports (profiles/), unlike the
-    back-to-back timing of one block's launch above, which runs with warm caches."""
-    from kair_amd import _hip as H
-    names = ("swin_attn_fwd", "swin_mlp_fwd")
-    orig = {n: getattr(H, n) for n in names}
-    rec = {n: [] for n in names}
-
-    def wrap(n):
-        def f(*a, **k):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            orig[n](*a, **k)
-            e1.record()
-            rec[n].append((e0, e1))
-        return f
-
-    for n in names:
-        setattr(H, n, wrap(n))
-    try:
-        for _ in range(2):   # the second pass is the one kept
-            for n in names:
-                rec[n].clear()
-            engine.forward(L, drop)
-    finally:
-        for n in names:
-            setattr(H, n, orig[n])
-    torch.cuda.synchronize()
-    return {("attn" if n == "swin_attn_fwd" else "mlp"): sum(a.elapsed_time(b) for a, b in r) / len(r)
-            for n, r in rec.items() if r}
+def rocprof_name(fn, a):
+    """The kernel name rocprofv3 reports for a launch (to match the committed profiles / PMC passes)."""
+    if fn.startswith("rowgemm_"):
+        K, N = a[2], (a[4] if fn != "rowgemm_lnbwd" else 192)
+        kb = K // 16
+        pd = {12: 4, 24: 4, 36: 2}[kb]
+        epi = {"rowgemm_store": 0, "rowgemm_gate": 1, "rowgemm_lnbwd": 2}[fn]
+        return f"rowgemm_kernel<{kb}, {pd}, {N // 96}, {epi}>"
+    return {"swin_mlp_fwd": "swin_mlp_fwd_kernel<1>", "swin_attn_fwd": "swin_attn_fwd_kernel<6, 1>",
+            "window_attn_bwd": "attn_bwd_bf16_kernel"}.get(fn, fn)
 
 
 def pmc_traffic(key):
-    """HBM bytes per launch of kernel `key` from the committed rocprofv3 PMC summary
-    (profiles/r02_pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950
+    """HBM bytes per launch of kernel `key` from the newest committed rocprofv3 PMC summary
+    (profiles/rNN_pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950
     correction + WRITE_SIZE, KiB -> bytes), or None when absent."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")))
     try:
-        with open(path) as f:
+        with open(paths[-1]) as f:
             rec = json.load(f)
         for name, v in rec["kernels"].items():
             if key in name:
                 return v["hbm_bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
+    except (IndexError, OSError, KeyError, ValueError):
         pass
     return None
 
@@ -274,9 +305,62 @@ def other_configs(device):
     return res
 
 
+def launch_plan(gpus, env):
+    """How this invocation runs (reference: one process per GPU, main_train_psnr.py:52-54,122-130 /
+    utils/utils_dist.py:13-28):
+      ("run", W)    already a rank of a W-process launch (torchrun / this script's own spawn): --gpus must
+                    equal W, else SystemExit -- a scaling run must never silently time fewer GPUs;
+      ("spawn", N)  a plain `python bench.py --gpus N` with N > 1: start N rank processes (before any GPU
+                    call in this parent) and wait for them."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {gpus})")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}: launch one process per GPU with matching counts")
+        return ("run", world)
+    return ("spawn", gpus) if gpus > 1 else ("run", 1)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """Run `python bench.py argv` as n ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on
+    127.0.0.1); rank 0's stdout is the JSON line.  Returns the worst exit code."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+def dry_run(world, rank):
+    """--dry-run: the launch path on the CPU (gloo, no GPU call): every rank reports in to rank 0."""
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+        got = [None] * world
+        dist.all_gather_object(got, rank)
+    else:
+        got = [rank]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": got}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); without torchrun the script spawns them")
     ap.add_argument("--steps", type=int, default=100)   # SURVEY §8d: >= 100 timed steps after >= 20 warm-up
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--global-batch", type=int, default=32)
@@ -289,15 +373,22 @@ def main():
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the short single-GPU throughput lines of BASELINE.json configs C2 / C3 / C5 (and the "
                          "C1 network on the GPU)")
+    ap.add_argument("--no-roles", action="store_true", help="skip the in-step per-kernel timing pass")
+    ap.add_argument("--dry-run", action="store_true", help="exercise the rank launch on the CPU (gloo) and exit")
     ap.add_argument("--data", default="pool", choices=["pool", "static"],
                     help="pool: every step synthesises a fresh batch on the GPU from an HBM-resident HR pool "
                          "(kair_synth_sr: crop + 8-way augment + MATLAB bicubic x1/4, DatasetSR semantics) inside "
                          "the timed loop; static: one staged batch reused")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    mode, world = launch_plan(args.gpus, os.environ)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        dry_run(world, rank)
+        return
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -367,29 +458,41 @@ def main():
     ms_step = 1000.0 * wall / args.steps
     step_tflops = fl["train"] * gbatch / (wall / args.steps) / 1e12 / world   # per GPU
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
-    try:
-        ks = time_fused_kernels(tr.engine)
-        from kair_amd.engine.swinir_engine import drop_path_scales
-        Lb = tr.static[0] if tr.static is not None else None
-        if Lb is not None:
-            drop = drop_path_scales(tr.engine, Lb.shape[0], Lb.device) if args.drop_path > 0 else None
-            for k, ms in time_in_step(tr.engine, Lb, drop).items():   # the roofline uses the in-step time
-                ks[k]["ms_isolated"], ks[k]["ms"] = ks[k]["ms"], ms
-    except RuntimeError as e:   # fp32 engine: no fused block kernels
-        ks = {"err": repr(e)}
+    roles = {}
+    if not args.no_roles:
+        try:
+            roles = time_roles(tr)
+        except Exception as e:  # noqa: BLE001
+            roles = {"error": {"kernel": repr(e), "ms_total": 0.0}}
+    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
 
-    def roof(k):
-        ach_gbs = k["bytes"] / (k["ms"] * 1e-3) / 1e9
-        ach_tf = k["flops"] / (k["ms"] * 1e-3) / 1e12
-        return {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(ach_gbs / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(k["rocprof_key"]),
-                "kernel": k["kernel"], "kernel_ms": round(k["ms"], 5),
-                "kernel_ms_timing": "in-step mean over every block of one eager forward (HIP events on the launch stream)"
-                if "ms_isolated" in k else "back-to-back launches of block 0",
-                "kernel_ms_isolated": round(k["ms_isolated"], 5) if "ms_isolated" in k else None,
-                "bytes_per_launch": k["bytes"],
-                "units_per_launch": k["units"], "bytes_per_unit": k["bytes_per_unit"],
-                "flops_per_launch": k["flops"], "achieved_tflops": round(ach_tf, 2), "mfma_frac": round(ach_tf / peak, 4)}
+    def roof(role, d):
+        r = {"bound": "hbm", "kernel": d["rocprof"], "role": role, "launches_per_step": d["launches"],
+             "kernel_ms": round(d["ms"], 5), "step_ms_total": round(d["ms_total"], 4),
+             "kernel_ms_timing": "in-step mean over the step's launches of this role: one eager fwd+loss+bwd, a HIP "
+                                 "event pair on the launch stream around each launch (side-stream concurrency kept)"}
+        if d.get("bytes"):
+            gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+            r.update({"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+                      "bytes_per_launch": d["bytes"], "traffic": pmc_traffic(d["rocprof"])})
+        else:
+            r.update({"achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": None, "traffic": None})
+        if d.get("flops"):
+            tf = d["flops"] / (d["ms"] * 1e-3) / 1e12
+            r.update({"flops_per_launch": d["flops"], "achieved_tflops": round(tf, 2), "mfma_frac": round(tf / peak, 4)})
+        return r
+    ranked = sorted(((k, v) for k, v in roles.items() if k != "error"), key=lambda kv: -kv[1]["ms_total"])
+    # attention GEMMs (QKV / q.k^T / p.v / proj): the fused attention half, the attention backward, the proj and
+    # q/k/v input-gradient row GEMMs -- FLOPs over their in-step time against the dense bf16 MFMA peak
+    att_names = ("swin_attn_fwd_kernel", "attn_bwd_bf16_kernel", "rowgemm_kernel<12, 4, 2, 0>", "rowgemm_kernel<36")
+    att = [v for v in roles.values() if v.get("flops") and v["rocprof"].startswith(att_names)]
+    att_mfma = None
+    if att:
+        fl_att = sum(v["flops"] * v["launches"] for v in att)
+        ms_att = sum(v["ms_total"] for v in att)
+        tf = fl_att / (ms_att * 1e-3) / 1e12
+        att_mfma = {"kernels": sorted({v["rocprof"] for v in att}), "flops_per_step": fl_att, "ms_per_step": round(ms_att, 4),
+                    "achieved_tflops": round(tf, 2), "peak_tflops": peak, "mfma_frac": round(tf / peak, 4)}
     out = {
         "metric": "train patches/sec + PSNR, SwinIR x4 48-px LQ, at 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -402,8 +505,9 @@ def main():
                    "global_batch": gbatch, "per_gpu_batch": bpg, "lq": 48, "hr": 192, "embed_dim": 180,
                    "depths": [6] * 6, "heads": 6, "window": 8, "drop_path_rate": args.drop_path,
                    "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
-        "roofline": roof(ks["mlp"]) if "mlp" in ks else {"error": ks["err"]},
-        "roofline_attention": roof(ks["attn"]) if "attn" in ks else None,
+        "roofline": roof(*ranked[0]) if ranked else {"error": roles.get("error", {}).get("kernel", "roles skipped")},
+        "kernels_in_step": [roof(k, v) for k, v in ranked[:8]],
+        "attention_gemm_mfma": att_mfma,
         "step_roofline": {"train_flop_per_patch": fl["train"], "achieved_tflops_per_gpu": round(step_tflops, 2),
                           "frac_of_bf16_peak": round(step_tflops / peak, 4)},
         "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
