@@ -64,19 +64,64 @@ def run_pair(net, ref, x, sc, tol=1e-4, gtol=2e-3, noise_x=3.0):
     assert not bad, bad
 
 
+class _GateReLU(torch.nn.Module):
+    """ReLU whose gate is given (the engine's forward: a > 0): relu(x) = x * m away from 0, and the backward
+    gates by the same m on both sides of the comparison."""
+
+    def __init__(self, mask):
+        super().__init__()
+        self.mask = mask
+
+    def forward(self, x):
+        return x * self.mask.to(x.dtype)
+
+
 def test_c1_dncnn_full():
+    """DnCNN(1, 1, 64, 17, 'BR'): 15 BatchNorm (batch statistics) + ReLU layers.  Which elements a ReLU
+    passes is a discontinuous function of its input: an element whose pre-activation lies within the
+    forward's rounding of 0 can pass in one fp32 run and not in another, and one such flip moves the
+    gradient of every layer below it by ~1e-3 (tools/dncnn_trace.py: the engine's last-layer dz error
+    4.7e-3 is reproduced exactly by torch's OWN fp32 BatchNorm backward fed the engine's forward z --
+    3 flipped gates of 409,600 against torch fp32's 1).  So the gradients are compared with the ReLU
+    gates fixed to the engine's forward (basicblock.conv 'R', basicblock.py:88-89): float64 and fp32
+    oracle runs through the same gate pattern; the output is compared as computed."""
     from kair_amd.models.network_dncnn import DnCNN
     torch.manual_seed(1)
     net = DnCNN(1, 1, 64, 17, "BR", compute_dtype="fp32")
     ref = ocv.DnCNN(1, 1, 64, 17, "BR").train()
     g = torch.Generator().manual_seed(2)
     x = torch.rand(4, 1, 40, 40, generator=g) + 25.0 / 255 * torch.randn(4, 1, 40, 40, generator=g)
-    # 17 layers of BatchNorm (batch statistics) + ReLU: several weight gradients carry 0.3-0.8 % error
-    # against float64 in the fp32 engine, up to 14x torch fp32's own error on them (0.02-0.12 %), while
-    # the output matches to 1e-6 and the 5-layer golden case to 2e-3 (test_convnets_gpu) -- an open
-    # precision gap of the engine's deep-BN backward, bounded here at 20x the oracle's
-    # fp32 error; the reference-held DnCNN KAT (29.8535 dB) matches to 1e-4 dB
-    run_pair(net, ref, x, 1, noise_x=20.0)
+    ref.load_state_dict(net.state_dict(), strict=True)
+    Hh = torch.rand(x.shape, generator=torch.Generator().manual_seed(7))
+    net = net.to(dev).train()
+    E = net(x.to(dev))
+    torch.nn.functional.l1_loss(E, Hh.to(dev)).backward()
+    eng = net.engine()
+    P = eng.cur
+    B, _, Hs, Ws = x.shape
+    masks = [(a.float().cpu().view(B, Hs, Ws, -1).permute(0, 3, 1, 2) > 0) for a in P["a"]]
+    mods = list(ref.model)
+    relu_idx = [i for i, m in enumerate(mods) if isinstance(m, torch.nn.ReLU)]
+    assert len(relu_idx) == len(masks)
+
+    def gated(model):
+        m = copy.deepcopy(model)
+        for i, mk in zip(relu_idx, masks):
+            m.model[i] = _GateReLU(mk)
+        return m
+    ref32, ref64 = gated(ref), gated(ref).double()
+    Er = ref32(x)
+    torch.nn.functional.l1_loss(Er, Hh).backward()
+    E64 = ref64(x.double())
+    torch.nn.functional.l1_loss(E64, Hh.double()).backward()
+    E_plain = ocv.DnCNN(1, 1, 64, 17, "BR").train().double()
+    E_plain.load_state_dict(ref.state_dict(), strict=True)
+    assert rel(E, E_plain(x.double())) < 1e-4          # the forward, ungated, vs float64
+    g64 = {k: p.grad for k, p in ref64.named_parameters()}
+    ours = grad_errs({k: p.grad for k, p in net.named_parameters()}, g64)
+    oracle32 = grad_errs({k: p.grad for k, p in ref32.named_parameters()}, g64)
+    bad = {k: (ours[k], oracle32[k]) for k in ours if ours[k] > max(2e-3, 3.0 * oracle32[k])}
+    assert not bad, bad
 
 
 def test_c2_swinir_light_full():
