@@ -434,6 +434,9 @@ def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, o
                                      H, W, shift, ones_col, ptr(mask), mnw, stream_ptr()), "window_attn_fwd")
 
 
+GROUP_MAX = 32   # jobs per kair_ln_param_reduce_grouped / kair_attn_dtable_grouped launch (LNP_MAX, DTAB_MAX)
+
+
 def layernorm_bwd_blocks(M):
     return lib().kair_layernorm_bwd_blocks(M)
 

@@ -40,7 +40,12 @@ def _compile(src, force, dep_time):
     return obj, None
 
 
-def build(force=False, jobs=None, verbose=True):
+def build(force=False, jobs=None, verbose=True, debug_ablations=False):
+    """debug_ablations: compile the perf-investigation ablation switches (KAIR_*_DBG environment bits
+    that drop stores / skip GEMMs) into the library -- never for training; the release build has none."""
+    if debug_ablations:
+        FLAGS.append("-DKAIR_DEBUG_ABLATIONS=1")
+        force = True
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
@@ -66,9 +71,10 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--debug-ablations", action="store_true")
     a = ap.parse_args()
     try:
-        build(a.force, a.j)
+        build(a.force, a.j, debug_ablations=a.debug_ablations)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -34,6 +34,17 @@ int kair_set_error(int code, const char* fmt, ...);
       return kair_set_error(KAIR_ERR_HIP, "%s: %s", __func__, hipGetErrorString(e__)); \
   } while (0)
 
+// Perf-investigation ablation bits (store-dropping / compute-skipping switches read from KAIR_*_DBG
+// environment variables) exist only in a library built with -DKAIR_DEBUG_ABLATIONS=1
+// (python -m kair_amd.build --debug-ablations).  The release library reads no environment variable:
+// kair_dbg_env() is 0 and every KAIR_DBG(...) test is a compile-time false, so the kernels carry no
+// ablation code at all.
+#ifndef KAIR_DEBUG_ABLATIONS
+#define KAIR_DEBUG_ABLATIONS 0
+#endif
+#define KAIR_DBG(x) (KAIR_DEBUG_ABLATIONS && (x))
+int kair_dbg_env(const char* name);
+
 template <typename T> KAIR_DEV float to_f(T v) { return (float)v; }
 template <typename T> KAIR_DEV T from_f(float v) { return (T)v; }
 

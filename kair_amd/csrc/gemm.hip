@@ -263,7 +263,7 @@ Epi make_epi(const kair_epilogue& o, long M, int N) {
   e.resid2 = o.resid2; e.ldr2 = o.ldr2;
   e.M = M; e.N = N;
   e.d_rps = make_fdiv(e.rps); e.d_tok = make_fdiv(e.tok); e.d_hdp = make_fdiv(e.hdp); e.d_pw = make_fdiv(e.nh * e.hdp);
-  static const int dbg = getenv("KAIR_RING_DBG") ? atoi(getenv("KAIR_RING_DBG")) : 0;
+  static const int dbg = kair_dbg_env("KAIR_RING_DBG");
   e.dbg = dbg;
   return e;
 }
@@ -865,7 +865,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
   int lj = 0, lt = 0, lkc = 0, ls = 0;
   auto issue_next = [&]() {
     if (lkc == 0) load_rows(lt);
-    if (!(E.dbg & 4)) {
+    if (!KAIR_DBG(E.dbg & 4)) {
       char* st = smem + ls * STAGE_BYTES;
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
@@ -901,7 +901,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
 
   static_assert(NS == 5, "the store bookkeeping below assumes chunk j is issued at iteration j-4");
   int sq1 = 0, sq2 = 0, sq3 = 0, sq4 = 0;   // store instructions this wave issued at iterations j-1 .. j-4
-  const bool early = (E.dbg & 32) != 0;     // tile end: issue the deferred chunk before the stores
+  const bool early = KAIR_DBG(E.dbg & 32);     // tile end: issue the deferred chunk before the stores
   int kc = 0, cs = 0, ct = 0;      // consumer cursor: chunk j = ct * nk + kc, in stage cs
   for (int j = 0; j < total; ++j) {
     // chunk j landed for this wave: younger than it are min(NS-2, total-1-j) chunks (2 DMA
@@ -913,7 +913,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
     if (!tile_end && lj < total) issue_next();   // lj == j + NS - 1
     const char* st = smem + cs * STAGE_BYTES;
 #pragma unroll
-    for (int ks = 0; ks < ((E.dbg & 2) ? 0 : BK / 32); ++ks) {
+    for (int ks = 0; ks < (KAIR_DBG(E.dbg & 2) ? 0 : BK / 32); ++ks) {
       bf16x8 af[RM], bfr[RN];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
@@ -930,7 +930,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
           acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
     }
     int sj = 0;
-    const int pol = (E.dbg >> 3) & 3;
+    const int pol = KAIR_DEBUG_ABLATIONS ? (E.dbg >> 3) & 3 : 0;
     if (tile_end && early && lj < total) issue_next();
     if (tile_end) {
       // Epilogue from registers: fragment pairs are re-laid by v_permlane16_swap so each lane
@@ -989,7 +989,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
             v[4 + c] = __uint_as_float(r[1]);
           }
           const int n = c8v[p];
-          const bool ok = mv[i] < (int)E.M && n < E.N && !(E.dbg & 1);   // N % 8 == 0: whole groups
+          const bool ok = mv[i] < (int)E.M && n < E.N && !KAIR_DBG(E.dbg & 1);   // N % 8 == 0: whole groups
           const float b8[8] = {bias8[p][0].x, bias8[p][0].y, bias8[p][0].z, bias8[p][0].w,
                                bias8[p][1].x, bias8[p][1].y, bias8[p][1].z, bias8[p][1].w};
 #pragma unroll
@@ -1810,6 +1810,16 @@ int kair_set_error(int code, const char* fmt, ...) {
 }
 
 extern "C" const char* kair_last_error(void) { return g_err; }
+
+int kair_dbg_env(const char* name) {
+#if KAIR_DEBUG_ABLATIONS
+  const char* v = getenv(name);
+  return v ? atoi(v) : 0;
+#else
+  (void)name;
+  return 0;
+#endif
+}
 
 extern "C" int kair_device_arch(char* buf, int len) {
   hipDeviceProp_t p;

@@ -262,7 +262,7 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
 
     // the saved q / k / v go out now (their registers are needed until the attention's last MFMA
     // anyway); the loads after them (proj weights) were issued before
-    if (!(a.dbg & 1)) {   // q / k / v, head-blocked [part][win][h][tok][32]
+    if (!KAIR_DBG(a.dbg & 1)) {   // q / k / v, head-blocked [part][win][h][tok][32]
       const long part = M * NH * 32;
       bf16* qb = a.qkv + (win * NH + h) * TOK * 32;
 #pragma unroll
@@ -413,22 +413,22 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
       }
     __syncthreads();
     constexpr int C4 = CP / 4;
-    for (int i = tid; i < ((a.dbg & 2) ? 0 : TOK * C4); i += 64 * NH) {
+    for (int i = tid; i < (KAIR_DBG(a.dbg & 2) ? 0 : TOK * C4); i += 64 * NH) {
       const int r = i / C4, q = (i - (i / C4) * C4) * 4;
       *(float4*)(a.out + (long)sRow[r] * a.ldout + q) = *(const float4*)(sX + r * LDX + q);
     }
-    if (hh == 0 && !(a.dbg & 2)) {
+    if (hh == 0 && !KAIR_DBG(a.dbg & 2)) {
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) a.lse[(win * NH + h) * TOK + qt * 32 + l31] = lse_v[qt];
     }
     // LN1 rows and O rows from LDS, 16 bytes per lane (window order)
     constexpr int CH = CP / 8;   // 16-byte chunks per row
-    for (int i = tid; i < ((a.dbg & 2) ? 0 : TOK * CH); i += 64 * NH) {
+    for (int i = tid; i < (KAIR_DBG(a.dbg & 2) ? 0 : TOK * CH); i += 64 * NH) {
       const int r = i / CH, q = (i - (i / CH) * CH) * 8;
       *(uint4*)(a.ln + (win * TOK + r) * a.ldln + q) = *(const uint4*)(sT + r * LDT + q);
       *(uint4*)(a.O + (win * TOK + r) * a.ldo + q) = *(const uint4*)(sO + r * LDT + q);
     }
-    if (tid < TOK && !(a.dbg & 2)) {
+    if (tid < TOK && !KAIR_DBG(a.dbg & 2)) {
       const long t = sRow[tid];
       a.mean[t] = sMean[tid];
       a.rstd[t] = sRstd[tid];
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(1024) void swin_mlp_fwd_kernel(const MlpFwdArgs a) 
       }
     }
     __syncthreads();   // (1) LN tile and x rows visible; the previous tile's output rows are stored
-    if (!compute && !(a.dbg & 4)) {   // ---- [store] LN2 rows and statistics
+    if (!compute && !KAIR_DBG(a.dbg & 4)) {   // ---- [store] LN2 rows and statistics
       constexpr int CH = CP / 8;
       for (int i = sid; i < TOK * CH; i += NST) {
         const int r = i / CH, q = (i - (i / CH) * CH) * 8;
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(1024) void swin_mlp_fwd_kernel(const MlpFwdArgs a) 
 #pragma unroll
         for (int r = 0; r < 16; ++r) U[r] = 0.f;
 #pragma unroll 1
-        for (int kb0 = 0; kb0 < ((a.dbg & 1) ? 0 : KB1); kb0 += PF) {
+        for (int kb0 = 0; kb0 < (KAIR_DBG(a.dbg & 1) ? 0 : KB1); kb0 += PF) {
 #pragma unroll
           for (int sl = 0; sl < PF; ++sl) {
             const int kb = kb0 + sl;
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(1024) void swin_mlp_fwd_kernel(const MlpFwdArgs a) 
       }
       __syncthreads();   // (3) h and g halves complete
       if (!compute) {
-        if (!(a.dbg & 4)) {   // ---- [store] g and h of this half
+        if (!KAIR_DBG(a.dbg & 4)) {   // ---- [store] g and h of this half
           constexpr int CH = HH / 8;
           for (int i = sid; i < TOK * CH; i += NST) {
             const int r = i / CH, q = (i - (i / CH) * CH) * 8;
@@ -656,7 +656,7 @@ __global__ __launch_bounds__(1024) void swin_mlp_fwd_kernel(const MlpFwdArgs a) 
 #pragma unroll
           for (int e = 0; e < S; ++e) pw[i][e] = *(const bf16x8*)(w2p + i * WS + e * 512);
 #pragma unroll 1
-        for (int kb0 = 0; kb0 < ((a.dbg & 2) ? 0 : KBH); kb0 += PF) {
+        for (int kb0 = 0; kb0 < (KAIR_DBG(a.dbg & 2) ? 0 : KBH); kb0 += PF) {
 #pragma unroll
           for (int sl = 0; sl < PF; ++sl) {
             const int kb = kb0 + sl;
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(1024) void swin_mlp_fwd_kernel(const MlpFwdArgs a) 
       }
     }
     __syncthreads();   // (5) output rows complete
-    if (!compute && !(a.dbg & 4)) {   // ---- [store] output rows (the next LN waits at barrier 1... via (6))
+    if (!compute && !KAIR_DBG(a.dbg & 4)) {   // ---- [store] output rows (the next LN waits at barrier 1... via (6))
       constexpr int C4 = CP / 4;
       for (int i = sid; i < TOK * C4; i += NST) {
         const int r = i / C4, q = (i - (i / C4) * C4) * 4;
@@ -827,7 +827,7 @@ __global__ __launch_bounds__(512) void swin_mlp_bwd_kernel(const MlpBwdArgs a) {
     }
     __syncthreads();   // (1) Dc tile and GELU' half 0 visible
     // the previous tile's LayerNorm backward (memory waves), under this tile's first GEMM
-    if (!compute && prev >= 0 && !(a.dbg & 4)) ln_bwd(prev);
+    if (!compute && prev >= 0 && !KAIR_DBG(a.dbg & 4)) ln_bwd(prev);
     uint4 g1[4];
     if (compute) {   // the second GELU' half, into registers until half 0 has consumed the first
       constexpr int CH = CP / 8;
@@ -856,7 +856,7 @@ __global__ __launch_bounds__(512) void swin_mlp_bwd_kernel(const MlpBwdArgs a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) U[rt][r] = 0.f;
 #pragma unroll 1
-        for (int kb0 = 0; kb0 < ((a.dbg & 1) ? 0 : KBC); kb0 += PF) {
+        for (int kb0 = 0; kb0 < (KAIR_DBG(a.dbg & 1) ? 0 : KBC); kb0 += PF) {
 #pragma unroll
           for (int sl = 0; sl < PF; ++sl) {
             const int kb = kb0 + sl;
@@ -883,7 +883,7 @@ __global__ __launch_bounds__(512) void swin_mlp_bwd_kernel(const MlpBwdArgs a) {
       __syncthreads();   // (2) dU half complete; GELU' half and the previous dxn no longer read
       if (!compute) {   // ---- [memory] dU half
         constexpr int CH = HH / 8;
-        for (int i = sid; i < ((a.dbg & 4) ? 0 : TOK * CH); i += NST) {
+        for (int i = sid; i < (KAIR_DBG(a.dbg & 4) ? 0 : TOK * CH); i += NST) {
           const int r = i / CH, q = (i - (i / CH) * CH) * 8;
           *(uint4*)(a.du + (row0 + r) * a.lddu + HH * half + q) = *(const uint4*)(sU + r * LDA + q);
         }
@@ -902,7 +902,7 @@ __global__ __launch_bounds__(512) void swin_mlp_bwd_kernel(const MlpBwdArgs a) {
 #pragma unroll
         for (int i = 0; i < PF; ++i) pw[i] = *(const bf16x8*)(wp + i * 512);
 #pragma unroll 1
-        for (int kb0 = 0; kb0 < ((a.dbg & 2) ? 0 : KBH); kb0 += PF) {
+        for (int kb0 = 0; kb0 < (KAIR_DBG(a.dbg & 2) ? 0 : KBH); kb0 += PF) {
 #pragma unroll
           for (int sl = 0; sl < PF; ++sl) {
             const int kb = kb0 + sl;
@@ -929,7 +929,7 @@ __global__ __launch_bounds__(512) void swin_mlp_bwd_kernel(const MlpBwdArgs a) {
     __syncthreads();   // (4) dxn tile complete
     prev = tile;
   }
-  if (!compute && prev >= 0 && !(a.dbg & 4)) ln_bwd(prev);
+  if (!compute && prev >= 0 && !KAIR_DBG(a.dbg & 4)) ln_bwd(prev);
   // LN2 parameter-gradient partials: the 16 memory-wave row groups, summed in a fixed order
   __syncthreads();
   for (int i = tid; i < 2 * CP; i += NT) {
@@ -983,7 +983,7 @@ extern "C" int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, 
   a.out = out; a.ldout = ldout;
   a.nWin = nWin; a.H = H; a.W = W; a.shift = shift;
   a.wm = make_winmap(H, W, WSZ, shift);
-  static const int dbg = getenv("KAIR_ATTN_DBG") ? atoi(getenv("KAIR_ATTN_DBG")) : 0;
+  static const int dbg = kair_dbg_env("KAIR_ATTN_DBG");
   a.dbg = dbg;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -1020,7 +1020,7 @@ extern "C" int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, c
   a.rowscale = rowscale; a.tiles_per_scale = rowscale ? rows_per_scale / TOK : 1;
   a.out = out; a.ldout = ldout;
   a.nTiles = M / TOK;
-  static const int dbg = getenv("KAIR_MLP_DBG") ? atoi(getenv("KAIR_MLP_DBG")) : 0;
+  static const int dbg = kair_dbg_env("KAIR_MLP_DBG");
   a.dbg = dbg;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -1067,7 +1067,7 @@ extern "C" int kair_swin_mlp_bwd(const void* dc, long lddc, const void* gd, long
   a.wm = make_winmap(H, W, WSZ, shift);
   a.part = ws;
   a.nTiles = M / TOK;
-  static const int dbg = getenv("KAIR_MLPB_DBG") ? atoi(getenv("KAIR_MLPB_DBG")) : 0;
+  static const int dbg = kair_dbg_env("KAIR_MLPB_DBG");
   a.dbg = dbg;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||

@@ -660,7 +660,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
   if (w1 > nWin) w1 = nWin;
   load_win(w0);
   unsigned long long ts[STAMP_N];
-  const bool stamping = stamp && gtask < STAMP_WAVES;
+  const bool stamping = KAIR_DBG(stamp) && gtask < STAMP_WAVES;
   for (long win = w0; win < w1; ++win) {
     const bool st_on = stamping && win == w0 + 2;
     if (st_on) ts[0] = stamp_now();
@@ -954,7 +954,7 @@ extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* tab
   return 0;
 }
 
-static const int g_stamp = getenv("KAIR_ATTN_STAMP") ? atoi(getenv("KAIR_ATTN_STAMP")) : 0;
+static const int g_stamp = kair_dbg_env("KAIR_ATTN_STAMP");
 
 // copy the attention-backward phase stamps to the host (perf investigation only)
 extern "C" int kair_debug_attn_stamps(unsigned long long* host, int n) {

@@ -4,7 +4,8 @@ A step program (swinir_engine, dncnn/rrdbnet/usrnet engines) runs over prealloca
 the input shape.  Three kinds of users exist:
 
 * the fused trainer (FusedTrainer) runs forward + backward back to back and captures them in a HIP
-  graph: it always gets slot 0 of its shape (``primary``), so the captured pointers stay valid;
+  graph: it always gets the ``primary`` plan of its shape, so the captured pointers stay valid; no
+  lease ever hands that plan out (a graph replay would overwrite a leased node's activations);
 * an autograd node (SwinIRFunction / ConvNetFunction / USRNetFunction) keeps the forward's saved
   activations until its backward: it ``lease``s a training plan, and a second forward of the same
   shape before that backward gets another plan instead of overwriting the first one's activations
@@ -35,7 +36,8 @@ class Lease:
 class PlanPool:
     def __init__(self, build, max_infer=2):
         self.build = build            # build(key, infer: bool) -> plan dict
-        self.train = {}               # key -> [plan, ...]  (slot 0 = primary)
+        self.primary = {}             # key -> the fused trainer's plan (never leased)
+        self.leased = {}              # key -> [plan, ...] for autograd nodes
         self.infer = OrderedDict()    # key -> plan (LRU)
         self.max_infer = max_infer
 
@@ -48,13 +50,13 @@ class PlanPool:
             while len(self.infer) > self.max_infer:
                 self.infer.popitem(last=False)
             return P
-        slots = self.train.setdefault(key, [])
         if mode == "primary":
-            if not slots:
-                slots.append(self.build(key, False))
-            return slots[0]
+            if key not in self.primary:
+                self.primary[key] = self.build(key, False)
+            return self.primary[key]
         if mode != "lease":
             raise ValueError(mode)
+        slots = self.leased.setdefault(key, [])
         for P in slots:
             if P.get("_lease") is None:
                 return P
@@ -63,10 +65,11 @@ class PlanPool:
         return P
 
     def n_train(self, key):
-        return len(self.train.get(key, []))
+        return (key in self.primary) + len(self.leased.get(key, []))
 
     def clear(self):
-        self.train.clear()
+        self.primary.clear()
+        self.leased.clear()
         self.infer.clear()
 
 

@@ -203,7 +203,7 @@ class _Blk:
 
 class SwinIREngine:
     def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True, fused_mlp=None,
-                 split_linear=None):
+                 split_linear=None, fused_mlp_bwd=False, side_stream=True):
         """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
         see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
         fused block kernels (_Lin, pack kind 12).
@@ -232,16 +232,16 @@ class SwinIREngine:
         self.fused_attn = bool(fused_blocks) and compute_dtype == "bf16" and self.nh == 6 and self.Cp == 32 * self.nh
         Hd = net.layers[0].residual_group.blocks[0].mlp.fc1.out_features
         self.Hdp = _rup(Hd + 1, 32)
-        import os
-        # KAIR_FUSED_MLP=0: the LN2 / fc1 / fc2 launches instead of the fused MLP half (A/B timing)
+        # fused_mlp=False: the LN2 / fc1 / fc2 launches instead of the fused MLP half (A/B timing).  Every
+        # engine variant is a constructor argument: no environment variable changes what the engine runs
         if fused_mlp is None:
-            fused_mlp = fused_blocks and os.environ.get("KAIR_FUSED_MLP", "1") == "1"
+            fused_mlp = fused_blocks
         self.fused_mlp = bool(fused_mlp) and compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384
         # the MLP-half backward kernel: off by default -- 205 us per block at B = 32 against 172-186 us
         # for the fc2 / fc1 input-gradient GEMMs + LN2 backward it replaces (its memory
-        # waves' LayerNorm rows and the tile loads run latency-exposed); KAIR_FUSED_MLP_BWD=1 enables it
+        # waves' LayerNorm rows and the tile loads run latency-exposed); fused_mlp_bwd=True enables it
         self.fused_mlp_bwd = (bool(fused_blocks) and compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384
-                              and os.environ.get("KAIR_FUSED_MLP_BWD", "0") == "1")
+                              and bool(fused_mlp_bwd))
         # split linears measured: the PSNR effect of bf16 linear-weight rounding is ~1e-4 dB against
         # ~5e-4 dB of activation-rounding noise per image (tools/parity_seeds.py, DESIGN.md "parity at
         # bf16"), at +45 us per block for the attention kernel -- off unless asked for
@@ -306,9 +306,8 @@ class SwinIREngine:
         self._dtab_pending = []   # (partials, nWin, nh, dtype, dtable, accumulate) of its attention blocks
         self._conv_pending = []   # the RSTB conv's weight gradient (_wgrad arguments)
         self._side = None         # side stream of the deferred per-RSTB gradient work
-        # KAIR_SIDE_STREAM=0: the deferred per-RSTB work runs in place on the main stream (A/B timing)
-        self.side_stream = (self.grouped_wgrad and torch.cuda.is_available() and
-                            os.environ.get("KAIR_SIDE_STREAM", "1") == "1")
+        # side_stream=False: the deferred per-RSTB work runs in place on the main stream (A/B timing)
+        self.side_stream = self.grouped_wgrad and torch.cuda.is_available() and bool(side_stream)
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -900,12 +899,15 @@ class SwinIREngine:
                 jobs, self._wg_pending = self._wg_pending, []
                 for i in range(0, len(jobs), H.WgradGroup.WG_MAX):
                     H.WgradGroup(jobs[i:i + H.WgradGroup.WG_MAX], P["M"]).run(ws)
+            # grouped launches take at most 32 jobs each (LNP_MAX / DTAB_MAX): deep RSTBs run in chunks
             if self._lnp_pending:
                 jobs, self._lnp_pending = self._lnp_pending, []
-                H.ln_param_reduce_grouped(jobs)
+                for i in range(0, len(jobs), H.GROUP_MAX):
+                    H.ln_param_reduce_grouped(jobs[i:i + H.GROUP_MAX])
             if self._dtab_pending:
                 jobs, self._dtab_pending = self._dtab_pending, []
-                H.attn_dtable_grouped(jobs)
+                for i in range(0, len(jobs), H.GROUP_MAX):
+                    H.attn_dtable_grouped(jobs[i:i + H.GROUP_MAX])
             jobs, self._conv_pending = self._conv_pending, []
             for A, Bop, M, N, K, m, gw, gb, oc in jobs:
                 self._wgrad(P, A, Bop, M, N, K, m, gw, gb, oc, ws=ws)

@@ -99,8 +99,6 @@ class _RB:
 
 
 class USRNetEngine:
-    fused_trainable = False
-
     def __init__(self, net, compute_dtype="bf16"):
         self.net_ref = weakref.ref(net)
         if compute_dtype not in ("bf16", "fp32"):

@@ -107,6 +107,8 @@ class ModelPlain(ModelBase):
         self.netG = self.model_to_device(define_G(opt))
         if self.opt_train["E_decay"] > 0:
             self.netE = define_G(opt).to(self.device).eval()
+        # amp_enabled selects the bf16 engine in define_G (select_network.compute_dtype_of); the step itself is
+        # the same fused trainer at either precision
         self.amp_enabled = bool(self.opt_train.get("amp_enabled", False))
         self.trainer = None
         self.log_dict = OrderedDict()
@@ -195,7 +197,7 @@ class ModelPlain(ModelBase):
         net = self.get_bare_model(self.netG)
         return (hasattr(net, "engine") and self.device.type == "cuda" and all(p.requires_grad for p in net.parameters())
                 and self.G_lossfn_type in ("l1", "charbonnier") and not self.opt_train.get("G_optimizer_clipgrad")
-                and self.opt_train["G_optimizer_type"] == "adam" and not self.amp_enabled
+                and self.opt_train["G_optimizer_type"] == "adam"
                 and not self.opt_train.get("G_regularizer_orthstep") and not self.opt_train.get("G_regularizer_clipstep"))
 
     def define_optimizer(self):

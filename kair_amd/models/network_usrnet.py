@@ -70,8 +70,6 @@ class USRNet(nn.Module):
     """network_usrnet_v1.py:228-262 (same constructor signature; compute_dtype is the engine option:
     'bf16' MFMA operands with fp32 accumulation, or 'fp32' exact-MFMA parity mode)."""
 
-    fused_trainable = False   # four-input step: trained through autograd + torch Adam (ModelPlain4)
-
     def __init__(self, n_iter=8, h_nc=64, in_nc=4, out_nc=3, nc=(64, 128, 256, 512), nb=2, act_mode="R",
                  downsample_mode="strideconv", upsample_mode="convtranspose", compute_dtype="bf16"):
         super().__init__()

@@ -16,31 +16,32 @@ _ON_PATH = ("swinir", "dncnn", "fdncnn", "rrdb", "rrdbnet", "usrnet")
 def define_G(opt):
     o = opt["netG"]
     t = o["net_type"]
+    ek = _engine_kwargs(opt)
     if t == "swinir":
         from .network_swinir import SwinIR
         net = SwinIR(upscale=o["upscale"], in_chans=o["in_chans"], img_size=o["img_size"], window_size=o["window_size"],
                      img_range=o["img_range"], depths=o["depths"], embed_dim=o["embed_dim"], num_heads=o["num_heads"],
                      mlp_ratio=o["mlp_ratio"], upsampler=o["upsampler"], resi_connection=o["resi_connection"],
-                     **_engine_kwargs(o), **({"drop_path_rate": o["drop_path_rate"]} if o.get("drop_path_rate") is not None
+                     **ek, **({"drop_path_rate": o["drop_path_rate"]} if o.get("drop_path_rate") is not None
                                              else {}))
     elif t in ("dncnn", "fdncnn"):
         from .network_dncnn import DnCNN, FDnCNN
         cls = DnCNN if t == "dncnn" else FDnCNN
         net = cls(in_nc=o["in_nc"], out_nc=o["out_nc"], nc=o["nc"], nb=o["nb"], act_mode=o["act_mode"],
-                  **_engine_kwargs(o))
+                  **ek)
     elif t == "rrdb":
         from .network_rrdb import RRDB
         net = RRDB(in_nc=o["in_nc"], out_nc=o["out_nc"], nc=o["nc"], nb=o["nb"], gc=o["gc"], upscale=o["scale"],
-                   act_mode=o["act_mode"], upsample_mode=o["upsample_mode"], **_engine_kwargs(o))
+                   act_mode=o["act_mode"], upsample_mode=o["upsample_mode"], **ek)
     elif t == "rrdbnet":
         from .network_rrdbnet import RRDBNet
         net = RRDBNet(in_nc=o["in_nc"], out_nc=o["out_nc"], nf=o["nf"], nb=o["nb"], gc=o["gc"], sf=o["scale"],
-                      **_engine_kwargs(o))
+                      **ek)
     elif t == "usrnet":
         from .network_usrnet import USRNet
         net = USRNet(n_iter=o["n_iter"], h_nc=o["h_nc"], in_nc=o["in_nc"], out_nc=o["out_nc"], nc=o["nc"], nb=o["nb"],
                      act_mode=o["act_mode"], downsample_mode=o["downsample_mode"], upsample_mode=o["upsample_mode"],
-                     **_engine_kwargs(o))
+                     **ek)
     else:
         raise NotImplementedError("netG [{:s}] is not on the kair_amd MI355X path (supported: {})".format(
             t, ", ".join(_ON_PATH)))
@@ -50,11 +51,28 @@ def define_G(opt):
     return net
 
 
-def _engine_kwargs(o):
-    """Build-only option: netG.compute_dtype ('bf16' default, 'fp32' parity mode).  (netG.drop_path_rate,
-    SwinIR only, is passed through when present; absent, SwinIR's own default 0.1 applies exactly as
-    the reference's define_G leaves it.)"""
-    return {"compute_dtype": o["compute_dtype"]} if o.get("compute_dtype") else {}
+def compute_dtype_of(opt):
+    """The engine's arithmetic, decided by the option file as the reference decides it:
+      netG.compute_dtype ('bf16' / 'fp32')  explicit choice (build-side key, absent from reference files);
+      train.amp_enabled: true               the reference's reduced-precision mode (model_plain.py:32-35,
+                                            261-275: fp16 autocast + GradScaler) -> the bf16 MFMA engine
+                                            (fp32 master weights / accumulation; bf16 keeps fp32's exponent
+                                            range, so no loss scaling and no {iter}_scaler.pth);
+      otherwise                             'fp32': the reference's default fp32 arithmetic (exact-fp32 MFMA)."""
+    o = opt["netG"]
+    if o.get("compute_dtype"):
+        if o["compute_dtype"] not in ("bf16", "fp32"):
+            raise ValueError(f"netG.compute_dtype must be 'bf16' or 'fp32' (got {o['compute_dtype']!r})")
+        return o["compute_dtype"]
+    tr = opt.get("train") or {}
+    return "bf16" if tr.get("amp_enabled") else "fp32"
+
+
+def _engine_kwargs(opt):
+    """Constructor kwargs the option file decides beyond the reference's (compute_dtype_of).  (netG.drop_path_rate,
+    SwinIR only, is passed through when present; absent, SwinIR's own default 0.1 applies exactly as the
+    reference's define_G leaves it.)"""
+    return {"compute_dtype": compute_dtype_of(opt)}
 
 
 def init_weights(net, init_type="xavier_uniform", init_bn_type="uniform", gain=1):

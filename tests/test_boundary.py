@@ -119,3 +119,17 @@ def test_custom_ops_registered_and_refuse_cpu():
     from kair_amd.models.network_swinir import WindowAttention
     with pytest.raises(RuntimeError):
         WindowAttention(60, (8, 8), 6)(torch.zeros(1, 64, 60))
+
+
+def test_precision_is_an_option_file_decision():
+    """define_G's arithmetic follows the option file (select_network.compute_dtype_of): the reference's
+    fp32 by default, its amp_enabled reduced-precision mode -> the bf16 engine, netG.compute_dtype explicit."""
+    from kair_amd.models.select_network import compute_dtype_of
+    base = {"netG": {"net_type": "swinir"}}
+    assert compute_dtype_of(base) == "fp32"
+    assert compute_dtype_of({**base, "train": {"amp_enabled": False}}) == "fp32"
+    assert compute_dtype_of({**base, "train": {"amp_enabled": True}}) == "bf16"
+    assert compute_dtype_of({"netG": {"net_type": "swinir", "compute_dtype": "fp32"}, "train": {"amp_enabled": True}}) == "fp32"
+    assert compute_dtype_of({"netG": {"net_type": "swinir", "compute_dtype": "bf16"}}) == "bf16"
+    with pytest.raises(ValueError):
+        compute_dtype_of({"netG": {"net_type": "swinir", "compute_dtype": "fp16"}})

@@ -43,12 +43,9 @@ def _pair(split=False, depths=(2, 2), img=24):
     nets[1].load_state_dict(nets[0].state_dict())
     nets = [n.to(dev).train() for n in nets]
     # the fused net with split linears too when split (pack kind 12 through both fused kernels)
-    os.environ["KAIR_FUSED_MLP_BWD"] = "1"   # the fused MLP backward too (off by default, still tested)
-    try:
-        nets[0]._engine = SwinIREngine(nets[0], "bf16", split_conv=split, fused_blocks=True, fused_mlp=True,
-                                       split_linear=split)
-    finally:
-        del os.environ["KAIR_FUSED_MLP_BWD"]
+    # the fused MLP backward too (off by default, still tested)
+    nets[0]._engine = SwinIREngine(nets[0], "bf16", split_conv=split, fused_blocks=True, fused_mlp=True,
+                                   split_linear=split, fused_mlp_bwd=True)
     assert nets[0]._engine.fused_mlp_bwd
     return nets
 

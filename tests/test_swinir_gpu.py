@@ -200,7 +200,7 @@ def test_eval_plans_bounded():
         for s in (16, 24, 32, 40, 20):
             net(torch.rand(1, 3, s, s, device=dev))
     pool = net.engine().plans
-    assert len(pool.infer) <= 2 and not pool.train
+    assert len(pool.infer) <= 2 and not pool.primary and not pool.leased
 
 
 @pytest.mark.parametrize("use_graph", [False, True])

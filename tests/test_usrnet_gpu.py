@@ -151,15 +151,16 @@ def test_usrnet_vs_golden(dt):
                           sub_grads(z, ""), dt)
 
 
-@pytest.mark.parametrize("lq,sf,n_iter", [(32, 4, 6), (32, 3, 2), (24, 2, 3)])
-def test_usrnet_option_config_vs_oracle(lq, sf, n_iter):
-    """train_usrnet.json widths (h_nc 32, nc 16/32/64/64, nb 2), fp32 parity mode vs the CPU oracle."""
+@pytest.mark.parametrize("lq,sf,n_iter,B", [(32, 4, 6, 2), (32, 3, 2, 2), (24, 2, 3, 2), (128, 4, 6, 1)])
+def test_usrnet_option_config_vs_oracle(lq, sf, n_iter, B):
+    """train_usrnet.json widths (h_nc 32, nc 16/32/64/64, nb 2), fp32 parity mode vs the CPU oracle;
+    (128, 4, 6, 1) is config C3 at its configured size: 128-px LQ, x4, i.e. a 512^2 HR grid through six
+    DataNet + ResUNet stages (network_usrnet_v1.py:237-262), forward and every parameter gradient."""
     torch.manual_seed(21 + sf)
     net = USRNet(n_iter=n_iter, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2, compute_dtype="fp32")
     ref = ocv.USRNet(n_iter=n_iter, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2)
     ref.load_state_dict(net.state_dict(), strict=True)
     g = torch.Generator().manual_seed(22 + sf)
-    B = 2
     x = torch.rand(B, 3, lq, lq, generator=g)
     k = rand_kernel(B, 25, g).float()
     sigma = torch.rand(B, 1, 1, 1, generator=g) * (25.0 / 255)

@@ -51,8 +51,9 @@ def main():
     for w in worst[:12]:
         print("%-60s fused %.4g unfused %.4g" % (w[1], w[2], w[3]))
     for fm in (True, False, True, False):
-        os.environ["KAIR_FUSED_MLP"] = "1" if fm else "0"
+        from kair_amd.engine.swinir_engine import SwinIREngine
         net = build_net("bf16", 0.1).to(dev).train()
+        net._engine = SwinIREngine(net, "bf16", fused_mlp=fm)
         ema = build_net("bf16", 0.1).to(dev).eval()
         ema.load_state_dict(net.state_dict())
         tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999)
