@@ -188,6 +188,11 @@ typedef struct {
 } kair_wgrad_job;
 long kair_wgrad_grouped_ws(const kair_wgrad_job* jobs, int njobs, long M);
 int kair_wgrad_grouped(const kair_wgrad_job* jobs, int njobs, long M, float* ws, void* stream);
+/* As kair_wgrad_grouped with at most max_ctas workgroups (max_ctas <= 0: no cap; fewer row splits,
+ * never fewer tiles): the per-RSTB deferred weight gradients run on a side stream beside the next
+ * RSTB's data-gradient chain, and a launch spread over every CU would hold the chain's kernels off the
+ * chip until it ends.  The workspace of the uncapped form is always large enough. */
+int kair_wgrad_grouped_ex(const kair_wgrad_job* jobs, int njobs, long M, float* ws, int max_ctas, void* stream);
 /* bias_grad[n_ref] (+)= sum_m G[m][n]  for an operand G of width Np (conv biases without a pad
  * column).  ws: 1024 * Np floats. */
 int kair_colsum(const kair_operand* G, long M, int Np, const kair_wmap* map, float* bias_grad,

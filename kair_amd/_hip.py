@@ -93,6 +93,7 @@ _SIGS = {
     "kair_gemm_tn": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), c_vp, c_int, c_long, c_int, c_int, c_int, c_vp],
     "kair_wgrad_grouped_ws": [ctypes.POINTER(WgradJob), c_int, c_long],
     "kair_wgrad_grouped": [ctypes.POINTER(WgradJob), c_int, c_long, c_vp, c_vp],
+    "kair_wgrad_grouped_ex": [ctypes.POINTER(WgradJob), c_int, c_long, c_vp, c_int, c_vp],
     "kair_layernorm_bwd_blocks": [c_long],
     "kair_ln_param_reduce_grouped": [ctypes.POINTER(LnParamJob), c_int, c_vp],
     "kair_window_attn_bwd_groups": [c_long, c_int, c_int],
@@ -343,6 +344,18 @@ def wgrad_splits(M, N, K):
     return lib().kair_wgrad_splits(M, N, K)
 
 
+def wgrad_tiles(N, K):
+    """(N, K) tiles of one kair_gemm_tn split (the launch has tiles x splits workgroups): the 192 x 192
+    ring tile where it applies, a 192-wide N tile for N in (128, 192], else 128 x 128 (gemm.hip)."""
+    if N <= 576 and K <= 576 and N % 8 == 0 and K % 8 == 0 and N > 64 and K > 64:
+        return -(-N // 192) * -(-K // 192)
+    if N <= 64 and K <= 64:
+        return 1
+    if 128 < N <= 192 and K > 128:
+        return -(-K // 128)
+    return -(-N // 128) * -(-K // 128)
+
+
 def gemm_tn(A, B, ws, splits, M, N, K, compute):
     check(lib().kair_gemm_tn(ctypes.byref(A), ctypes.byref(B), ptr(ws), splits, M, N, K, compute, stream_ptr()), "gemm_tn")
 
@@ -372,10 +385,12 @@ class WgradGroup:
         self.arr, self.n, self.M = arr, len(jobs), M
         self.ws_floats = lib().kair_wgrad_grouped_ws(arr, self.n, M)
 
-    def run(self, ws):
+    def run(self, ws, max_ctas=0):
+        """max_ctas > 0: at most that many workgroups (kair_wgrad_grouped_ex: fewer row splits)."""
         if ws.numel() < self.ws_floats:
             raise ValueError("kair_wgrad_grouped: workspace too small")
-        check(lib().kair_wgrad_grouped(self.arr, self.n, self.M, ptr(ws), stream_ptr()), "wgrad_grouped")
+        check(lib().kair_wgrad_grouped_ex(self.arr, self.n, self.M, ptr(ws), int(max_ctas), stream_ptr()),
+              "wgrad_grouped")
 
 
 def pack_weight(src, dst, m):

@@ -1982,6 +1982,17 @@ static long grouped_tiles(const kair_wgrad_job* jobs, int njobs) {
   return t;
 }
 
+// max_ctas > 0: at most that many (tile, split) workgroups -- fewer splits, so the launch holds only part
+// of the chip (the deferred gradient work beside the data-gradient chain, which needs the rest)
+static int grouped_splits_capped(long M, long ntiles, int max_ctas) {
+  int s = grouped_splits(M, ntiles);
+  if (max_ctas > 0) {
+    const long cap = max_ctas / (ntiles > 0 ? ntiles : 1);
+    if (s > cap) s = (int)(cap < 1 ? 1 : cap);
+  }
+  return s;
+}
+
 extern "C" long kair_wgrad_grouped_ws(const kair_wgrad_job* jobs, int njobs, long M) {
   if (!jobs || njobs <= 0 || M <= 0) return 0;
   const int splits = grouped_splits(M, grouped_tiles(jobs, njobs));
@@ -1990,7 +2001,14 @@ extern "C" long kair_wgrad_grouped_ws(const kair_wgrad_job* jobs, int njobs, lon
   return (long)splits * nk;
 }
 
+extern "C" int kair_wgrad_grouped_ex(const kair_wgrad_job* jobs, int njobs, long M, float* ws, int max_ctas,
+                                     void* stream);
 extern "C" int kair_wgrad_grouped(const kair_wgrad_job* jobs, int njobs, long M, float* ws, void* stream) {
+  return kair_wgrad_grouped_ex(jobs, njobs, M, ws, 0, stream);
+}
+
+extern "C" int kair_wgrad_grouped_ex(const kair_wgrad_job* jobs, int njobs, long M, float* ws, int max_ctas,
+                                     void* stream) {
   KAIR_CHECK_ARG(jobs && ws && njobs > 0 && njobs <= KAIR_WG_MAX && M > 0 && M < (1L << 30),
                  "wgrad_grouped: 1..%d jobs, M > 0 and a workspace", KAIR_WG_MAX);
   KAIR_CHECK_ARG(((uintptr_t)ws % 16) == 0, "wgrad_grouped: workspace not 16-byte aligned");
@@ -2000,7 +2018,7 @@ extern "C" int kair_wgrad_grouped(const kair_wgrad_job* jobs, int njobs, long M,
   memset(&g, 0, sizeof(g));
   memset(&f, 0, sizeof(f));
   const long ntiles = grouped_tiles(jobs, njobs);
-  const int splits = grouped_splits(M, ntiles);
+  const int splits = grouped_splits_capped(M, ntiles, max_ctas);
   long rps = (M + splits - 1) / splits;
   rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
   int qkv_seen = 0;

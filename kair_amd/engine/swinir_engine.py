@@ -203,7 +203,7 @@ class _Blk:
 
 class SwinIREngine:
     def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True, fused_mlp=None,
-                 split_linear=None, fused_mlp_bwd=False, side_stream=True):
+                 split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=0):
         """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
         see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
         fused block kernels (_Lin, pack kind 12).
@@ -308,6 +308,13 @@ class SwinIREngine:
         self._side = None         # side stream of the deferred per-RSTB gradient work
         # side_stream=False: the deferred per-RSTB work runs in place on the main stream (A/B timing)
         self.side_stream = self.grouped_wgrad and torch.cuda.is_available() and bool(side_stream)
+        # workgroup budget of the side-stream launches (0: uncapped).  The weight-gradient kernels hold one
+        # 512-thread workgroup per CU; spread over the chip they keep the next RSTB's data-gradient kernels
+        # off it until they end (rocprof: the first fc2 input gradient of every RSTB 43 -> 495 us behind the
+        # grouped launch, the attention backward 80 -> 340 us behind the conv weight gradient).  Measured
+        # (profiles/r03_side_ctas_ab.txt): a cap makes the side work critical at B=32 (48 CTAs: 1080 -> 808
+        # patches/s) and gains ~2% at B=4 (96 CTAs) -- so uncapped by default.
+        self.side_ctas = int(side_ctas)
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -679,8 +686,10 @@ class SwinIREngine:
     # ------------------------------------------------------------------------------------
     # backward
     # ------------------------------------------------------------------------------------
-    def _wgrad(self, P, A, Bop, M, N, K, layer_map, wgrad, bgrad=None, ones_col=-1, ws=None):
+    def _wgrad(self, P, A, Bop, M, N, K, layer_map, wgrad, bgrad=None, ones_col=-1, ws=None, max_ctas=0):
         S = H.wgrad_splits(M, N, K)
+        if max_ctas > 0:   # fewer row splits: at most max_ctas (tile, split) workgroups
+            S = max(1, min(S, max_ctas // H.wgrad_tiles(N, K)))
         ws = P["wg_ws"] if ws is None else ws
         H.gemm_tn(A, Bop, ws, S, M, N, K, self.cd)
         H.wgrad_finalize(ws, S, layer_map, wgrad, bgrad, ones_col)
@@ -894,11 +903,12 @@ class SwinIREngine:
             side = self._side
             side.wait_stream(torch.cuda.current_stream())
         ws = P["wg_ws2"] if side is not None else P["wg_ws"]
+        cap = self.side_ctas if side is not None else 0
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             if self._wg_pending:
                 jobs, self._wg_pending = self._wg_pending, []
                 for i in range(0, len(jobs), H.WgradGroup.WG_MAX):
-                    H.WgradGroup(jobs[i:i + H.WgradGroup.WG_MAX], P["M"]).run(ws)
+                    H.WgradGroup(jobs[i:i + H.WgradGroup.WG_MAX], P["M"]).run(ws, max_ctas=cap)
             # grouped launches take at most 32 jobs each (LNP_MAX / DTAB_MAX): deep RSTBs run in chunks
             if self._lnp_pending:
                 jobs, self._lnp_pending = self._lnp_pending, []
@@ -910,7 +920,7 @@ class SwinIREngine:
                     H.attn_dtable_grouped(jobs[i:i + H.GROUP_MAX])
             jobs, self._conv_pending = self._conv_pending, []
             for A, Bop, M, N, K, m, gw, gb, oc in jobs:
-                self._wgrad(P, A, Bop, M, N, K, m, gw, gb, oc, ws=ws)
+                self._wgrad(P, A, Bop, M, N, K, m, gw, gb, oc, ws=ws, max_ctas=cap)
         return side is not None
 
     def _block_bwd(self, blk, P, S, x_in, D, bi, grads, j, par):
