@@ -374,7 +374,10 @@ def main():
                     help="skip the short single-GPU throughput lines of BASELINE.json configs C2 / C3 / C5 (and the "
                          "C1 network on the GPU)")
     ap.add_argument("--no-roles", action="store_true", help="skip the in-step per-kernel timing pass")
-    ap.add_argument("--side-ctas", type=int, default=None, help="A/B: workgroup budget of the side-stream launches")
+    ap.add_argument("--side-ctas", type=int, default=None,
+                    help="A/B: workgroup budget of the side-stream launches (< 0: that many times more row splits)")
+    ap.add_argument("--side-priority", type=int, default=0, help="A/B: torch priority of the side stream")
+    ap.add_argument("--main-priority", type=int, default=0, help="A/B: torch priority of the step's capture stream")
     ap.add_argument("--no-side-stream", action="store_true",
                     help="A/B: run the deferred per-RSTB gradient work in place on the main stream")
     ap.add_argument("--dry-run", action="store_true", help="exercise the rank launch on the CPU (gloo) and exit")
@@ -417,13 +420,13 @@ def main():
     if world > 1:   # replicas start identical (DDP construction broadcast, model_base.py:116)
         for t in list(net.state_dict().values()) + list(ema.state_dict().values()):
             dist.broadcast(t, 0)
-    if args.no_side_stream or args.side_ctas is not None:
+    if args.no_side_stream or args.side_ctas is not None or args.side_priority:
         from kair_amd.engine.swinir_engine import SwinIREngine
-        kw = {"side_stream": not args.no_side_stream}
+        kw = {"side_stream": not args.no_side_stream, "side_priority": args.side_priority}
         if args.side_ctas is not None:
             kw["side_ctas"] = args.side_ctas
         net._engine = SwinIREngine(net, args.dtype, **kw)
-    tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999, use_graph=not args.no_graph)
+    tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999, use_graph=not args.no_graph, stream_priority=args.main_priority)
     if args.data == "pool":
         from kair_amd.data.gpu_synth import PatchSynth, synthetic_pool
         pool = synthetic_pool(64, 3, 256, 256, seed=99, device=device)

@@ -107,6 +107,12 @@ typedef struct {
   int pre_kind;                         /* out_pre holds: 0 the pre-activation x; 1 act'(x) (GELU
                                            only: the backward gate, gate_kind 4, with no erf
                                            left in the backward epilogue)                        */
+  void* a_copy; long ld_acopy;          /* optional bf16 copy of the A operand's image (IM2COL3 A,
+                                           3x3 halo-conv path only, else KAIR_ERR_ARG): pixel m,
+                                           channels [0, im_C) -> a_copy[m * ld_acopy + c] -- the
+                                           weight gradient's operand, written from the halo the conv
+                                           loads anyway (no extra read of the fp32 image)           */
+  int acopy_ones_col_p1;                /* 1 + channel of a_copy forced to 1.0 (bias gradient); 0 none */
 } kair_epilogue;
 
 /* C[m,n] = sum_k A[m,k] * B[n,k]  (+ epilogue).  compute: KAIR_BF16 -> v_mfma_f32_16x16x32_bf16,
@@ -116,6 +122,11 @@ typedef struct {
  * forward and input-gradient. */
 int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const kair_epilogue* E,
                  long M, int N, int K, int compute, void* stream);
+
+/* 1 if kair_gemm_nt runs a bf16 3x3 conv of this geometry (image H x W x C, M = B*H*W rows, N outputs;
+ * 16-byte aligned rows, pixel stride C, plain ROWS epilogue) on the halo-conv path, the one that can
+ * write kair_epilogue.a_copy; else 0. */
+int kair_conv3x3_halo_geometry(int H, int W, int C, long M, int N);
 
 /* Weight gradient: partial[s][n][k] = sum_{m in split s} A[m,n] * B[m,k]; then
  * kair_wgrad_finalize sums the splits.  ws needs splits*N*K floats (kair_wgrad_splits()).
@@ -188,10 +199,12 @@ typedef struct {
 } kair_wgrad_job;
 long kair_wgrad_grouped_ws(const kair_wgrad_job* jobs, int njobs, long M);
 int kair_wgrad_grouped(const kair_wgrad_job* jobs, int njobs, long M, float* ws, void* stream);
-/* As kair_wgrad_grouped with at most max_ctas workgroups (max_ctas <= 0: no cap; fewer row splits,
+/* As kair_wgrad_grouped with at most max_ctas workgroups (max_ctas == 0: no cap; fewer row splits,
  * never fewer tiles): the per-RSTB deferred weight gradients run on a side stream beside the next
  * RSTB's data-gradient chain, and a launch spread over every CU would hold the chain's kernels off the
- * chip until it ends.  The workspace of the uncapped form is always large enough. */
+ * chip until it ends.  The workspace of the uncapped form is always large enough.  max_ctas < 0:
+ * -max_ctas times the default row splits instead (shorter workgroups; workspace -max_ctas times
+ * kair_wgrad_grouped_ws()). */
 int kair_wgrad_grouped_ex(const kair_wgrad_job* jobs, int njobs, long M, float* ws, int max_ctas, void* stream);
 /* bias_grad[n_ref] (+)= sum_m G[m][n]  for an operand G of width Np (conv biases without a pad
  * column).  ws: 1024 * Np floats. */
@@ -392,6 +405,13 @@ int kair_usr_seg_sum(const float* ws, int seglen, int nseg, float scale, float* 
 /* out[b*ostride] (+)= sum_p x[(b*HW + p)*ld + c]  (ws: B * KAIR_USR_CHAN_CHUNKS floats) */
 int kair_usr_chan_sum(const float* x, long ld, int c, long HW, int B, float* ws, float* out, int ostride,
                       int accumulate, void* stream);
+/* ResUNet's ReplicationPad2d((0, Wp-W, 0, Hp-H)) and crop x[..., :H, :W] (network_usrnet_v1.py:148-151,
+ * 164) with their adjoints.  nb: images (NHWC modes, channel stride ldc) or planes (CROP_NCHW).
+ * REPLICATE / ZERO: H x W -> Hp x Wp (fp32 or bf16); FOLD (replicate adjoint, pad pixels summed onto
+ * the edge they copy): Hp x Wp -> H x W; CROP_NCHW: Hp x Wp planes -> H x W (fp32). */
+enum { KAIR_USR_PAD_REPLICATE = 0, KAIR_USR_PAD_ZERO = 1, KAIR_USR_PAD_FOLD = 2, KAIR_USR_CROP_NCHW = 3 };
+int kair_usr_pad(const void* src, void* dst, int dtype, int mode, int ldc, int nb, int H, int W, int Hp, int Wp,
+                 void* stream);
 /* F.interpolate(x, scale_factor=sf, mode='nearest') of fp32 NCHW planes (v1:252) */
 int kair_usr_upsample_nearest(const float* L, float* out, int planes, int h, int w, int sf, void* stream);
 /* ResUNet input torch.cat((x, beta), 1) (v1:261) as NHWC rows of width ld: x channels, beta[b*bstride], 0 */

@@ -16,6 +16,7 @@ LD_ROWS, LD_IM2COL3, LD_QKVBLK, LD_S2D = 0, 1, 2, 3
 USR_SRC_NCHW, USR_SRC_PSF, USR_SRC_ZUP, USR_SRC_NHWC = 0, 1, 2, 3
 USR_COL_FB, USR_COL_FBFY, USR_COL_DATA_FWD, USR_COL_DATA_BWD = 0, 1, 2, 3
 USR_CHAN_CHUNKS = 64
+USR_PAD_REPLICATE, USR_PAD_ZERO, USR_PAD_FOLD, USR_CROP_NCHW = 0, 1, 2, 3
 OUT_ROWS, OUT_QKVBLK, OUT_PSHUF, OUT_PUNSHUF, OUT_NCHW, OUT_PSHUF_NCHW = 0, 1, 2, 3, 4, 5
 OUT_PSHUF_SPM, OUT_PUNSHUF_SPM = 6, 7
 ACT_NONE, ACT_GELU, ACT_LEAKY, ACT_RELU = 0, 1, 2, 3
@@ -60,7 +61,8 @@ class Epilogue(ctypes.Structure):
                 ("ps_r", c_int), ("ps_H", c_int), ("ps_W", c_int),
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
                 ("img_mean", c_vp), ("img_range", c_float), ("img_C", c_int), ("img_H", c_int), ("img_W", c_int),
-                ("out_ones_col_p1", c_int), ("resid2", c_vp), ("ldr2", c_long), ("pre_kind", c_int)]
+                ("out_ones_col_p1", c_int), ("resid2", c_vp), ("ldr2", c_long), ("pre_kind", c_int),
+                ("a_copy", c_vp), ("ld_acopy", c_long), ("acopy_ones_col_p1", c_int)]
 
 
 class WMap(ctypes.Structure):
@@ -90,6 +92,7 @@ _SIGS = {
     "kair_gemm_nt": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), ctypes.POINTER(Epilogue), c_long, c_int, c_int,
                      c_int, c_vp],
     "kair_wgrad_splits": [c_long, c_int, c_int],
+    "kair_conv3x3_halo_geometry": [c_int, c_int, c_int, c_long, c_int],
     "kair_gemm_tn": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), c_vp, c_int, c_long, c_int, c_int, c_int, c_vp],
     "kair_wgrad_grouped_ws": [ctypes.POINTER(WgradJob), c_int, c_long],
     "kair_wgrad_grouped": [ctypes.POINTER(WgradJob), c_int, c_long, c_vp, c_vp],
@@ -140,6 +143,7 @@ _SIGS = {
     "kair_usr_chan_sum": [c_vp, c_long, c_int, c_long, c_int, c_vp, c_vp, c_int, c_int, c_vp],
     "kair_usr_upsample_nearest": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
     "kair_usr_pack_input": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_long, c_vp],
+    "kair_usr_pad": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "kair_hypanet_fwd": [c_vp, c_float] + [c_vp] * 6 + [c_int, c_int, c_int, c_vp, c_vp],
     "kair_hypanet_bwd": [c_vp, c_float] + [c_vp] * 6 + [c_int, c_int, c_int, c_vp] + [c_vp] * 6 + [c_int, c_vp],
     "kair_synth_sr": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp,
@@ -241,9 +245,11 @@ def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1, one
     return o
 
 
-def im2col(t, H, W, C, flip=False, ones_col=-1, ld=None, up=1):
+def im2col(t, H, W, C, flip=False, ones_col=-1, ld=None, up=1, ones_in_data=False):
     """3x3 / pad 1 im2col view of an NHWC map: H x W is the CONV grid, ld the pixel stride
-    (default C), up=2 reads the source (H/2 x W/2) through a nearest x2 upsample."""
+    (default C), up=2 reads the source (H/2 x W/2) through a nearest x2 upsample.  ones_in_data: the
+    map already holds 1.0 in channel ones_col % C of every pixel (read through the center tap,
+    ones_col = 4 * C + c, by the tap-per-tile weight-gradient ring)."""
     o = Operand()
     o._keep = t
     o.ptr = ptr(t)
@@ -253,6 +259,7 @@ def im2col(t, H, W, C, flip=False, ones_col=-1, ld=None, up=1):
     o.im_H, o.im_W, o.im_C, o.im_flip = H, W, C, int(flip)
     o.im_up = up
     o.ones_col = ones_col
+    o.ones_in_data = int(ones_in_data)
     o.rows_per_scale = 1
     return o
 
@@ -287,11 +294,14 @@ def qkvblk(t, nh, hdp=32, tok=64, rowscale=None, rows_per_scale=1):
 
 def epilogue(out, mode=OUT_ROWS, ldo=None, win=None, bias=None, act=ACT_NONE, slope=0.0, pre=None, ldp=None,
              resid=None, ldr=None, rowscale=None, rows_per_scale=1, gate=None, ldg=None, gate_kind=0,
-             ps=None, qkv=None, img=None, ones_col=-1, resid2=None, ldr2=None, pre_grad=False):
-    """pre_grad: `pre` receives act'(x) instead of x (GELU; read back with gate_kind=4)."""
+             ps=None, qkv=None, img=None, ones_col=-1, resid2=None, ldr2=None, pre_grad=False, acopy=None):
+    """pre_grad: `pre` receives act'(x) instead of x (GELU; read back with gate_kind=4).  acopy = (bf16
+    tensor, ones_col): the 3x3 halo conv also writes its A image there (ones_col >= 0: that channel 1.0)."""
     e = Epilogue()
     e.pre_kind = int(bool(pre_grad))
-    e._keep = (out, bias, pre, resid, rowscale, gate, img, resid2)
+    e._keep = (out, bias, pre, resid, rowscale, gate, img, resid2, acopy)
+    if acopy is not None:
+        e.a_copy, e.ld_acopy, e.acopy_ones_col_p1 = ptr(acopy[0]), acopy[0].shape[-1], acopy[1] + 1
     if resid2 is not None:
         e.resid2, e.ldr2 = ptr(resid2), (ldr2 if ldr2 is not None else resid2.shape[-1])
     e.out = ptr(out)
@@ -340,6 +350,11 @@ def gemm_nt(A, B, E, M, N, K, compute):
     check(lib().kair_gemm_nt(ctypes.byref(A), ctypes.byref(B), ctypes.byref(E), M, N, K, compute, stream_ptr()), "gemm_nt")
 
 
+def conv_halo_geometry(H, W, C, M, N):
+    """True when a bf16 3x3 conv of this geometry runs on the halo path (can write epilogue acopy)."""
+    return bool(lib().kair_conv3x3_halo_geometry(H, W, C, M, N))
+
+
 def wgrad_splits(M, N, K):
     return lib().kair_wgrad_splits(M, N, K)
 
@@ -349,6 +364,8 @@ def wgrad_tiles(N, K):
     ring tile where it applies, a 192-wide N tile for N in (128, 192], else 128 x 128 (gemm.hip)."""
     if N <= 576 and K <= 576 and N % 8 == 0 and K % 8 == 0 and N > 64 and K > 64:
         return -(-N // 192) * -(-K // 192)
+    if N <= 576 and N % 8 == 0 and N > 64 and K == 9 * 192:   # conv weight gradient, one tap per tile
+        return -(-N // 192) * 9
     if N <= 64 and K <= 64:
         return 1
     if 128 < N <= 192 and K > 128:
@@ -386,8 +403,9 @@ class WgradGroup:
         self.ws_floats = lib().kair_wgrad_grouped_ws(arr, self.n, M)
 
     def run(self, ws, max_ctas=0):
-        """max_ctas > 0: at most that many workgroups (kair_wgrad_grouped_ex: fewer row splits)."""
-        if ws.numel() < self.ws_floats:
+        """max_ctas > 0: at most that many workgroups (kair_wgrad_grouped_ex: fewer row splits); < 0:
+        -max_ctas times the default splits (the workspace scales with it)."""
+        if ws.numel() < self.ws_floats * max(1, -max_ctas):
             raise ValueError("kair_wgrad_grouped: workspace too small")
         check(lib().kair_wgrad_grouped_ex(self.arr, self.n, self.M, ptr(ws), int(max_ctas), stream_ptr()),
               "wgrad_grouped")
@@ -564,6 +582,13 @@ def usr_chan_sum(x, ld, c, HW, B, ws, out, ostride, accumulate=False):
 
 def usr_upsample_nearest(L, out, planes, h, w, sf):
     check(lib().kair_usr_upsample_nearest(ptr(L), ptr(out), planes, h, w, sf, stream_ptr()), "usr_upsample_nearest")
+
+
+def usr_pad(src, dst, mode, ldc, nb, H, W, Hp, Wp):
+    """ResUNet replicate pad / crop and adjoints (kair_usr_pad); dst dtype = src dtype."""
+    if src.dtype != dst.dtype:
+        raise ValueError("usr_pad: src and dst dtypes differ")
+    check(lib().kair_usr_pad(ptr(src), ptr(dst), dtype_code(dst), mode, ldc, nb, H, W, Hp, Wp, stream_ptr()), "usr_pad")
 
 
 def usr_pack_input(x, beta, beta_stride, out, ld, B, C, HW):

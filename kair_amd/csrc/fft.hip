@@ -503,6 +503,46 @@ __global__ __launch_bounds__(256) void hypanet_bwd_kernel(const float* __restric
   }
 }
 
+// ResUNet.forward's ReplicationPad2d to a multiple of 8 and crop (network_usrnet_v1.py:148-151, 164)
+// and their adjoints, one element per thread:
+//   REPLICATE  NHWC H x W -> Hp x Wp, edge pixels repeated (the padded U-Net input)
+//   ZERO       NHWC H x W -> Hp x Wp, zeros outside (the crop's adjoint: the output gradient)
+//   FOLD       NHWC Hp x Wp -> H x W, each pad pixel's value added to the edge pixel it copied
+//              (the replicate pad's adjoint: the input gradient), fixed order
+//   CROP_NCHW  planes Hp x Wp -> H x W (the U-Net output)
+template <typename T>
+__global__ __launch_bounds__(256) void usr_pad_kernel(const T* __restrict__ src, T* __restrict__ dst, int mode, int ldc,
+                                                      int H, int W, int Hp, int Wp, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  if (mode == KAIR_USR_CROP_NCHW) {
+    const long pl = i / ((long)H * W);
+    const int r = (int)(i - pl * H * W), y = r / W, x = r - y * W;
+    dst[i] = src[(pl * Hp + y) * Wp + x];
+    return;
+  }
+  const int c = (int)(i % ldc);
+  const long p = i / ldc;
+  if (mode == KAIR_USR_PAD_FOLD) {
+    const int x = (int)(p % W), y = (int)((p / W) % H);
+    const long b = p / ((long)W * H);
+    const int y1 = y == H - 1 ? Hp : y + 1, x1 = x == W - 1 ? Wp : x + 1;
+    float s = 0.f;
+    for (int yy = y; yy < y1; ++yy)
+      for (int xx = x; xx < x1; ++xx) s += (float)src[((b * Hp + yy) * Wp + xx) * ldc + c];
+    dst[i] = (T)s;
+    return;
+  }
+  const int xp = (int)(p % Wp), yp = (int)((p / Wp) % Hp);
+  const long b = p / ((long)Wp * Hp);
+  if (mode == KAIR_USR_PAD_ZERO && (yp >= H || xp >= W)) {
+    dst[i] = (T)0.f;
+    return;
+  }
+  const int y = yp < H ? yp : H - 1, x = xp < W ? xp : W - 1;
+  dst[i] = src[((b * H + y) * W + x) * ldc + c];
+}
+
 int make_plan(int n, FftPlan* p) {
   p->n = n;
   p->nst = 0;
@@ -630,6 +670,25 @@ extern "C" int kair_usr_pack_input(const float* x, const float* beta, int beta_s
   else
     hipLaunchKernelGGL(pack_input_kernel<float>, dim3(nblk(npix, 256)), dim3(256), 0, s, x, beta, beta_stride, (float*)out,
                        ld, C, HW, npix);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_usr_pad(const void* src, void* dst, int dtype, int mode, int ldc, int nb, int H, int W, int Hp, int Wp,
+                            void* stream) {
+  KAIR_CHECK_ARG(src && dst && src != dst && nb > 0 && H > 0 && W > 0 && Hp >= H && Wp >= W, "usr_pad: bad args");
+  KAIR_CHECK_ARG(mode >= KAIR_USR_PAD_REPLICATE && mode <= KAIR_USR_CROP_NCHW, "usr_pad: bad mode");
+  KAIR_CHECK_ARG(mode == KAIR_USR_CROP_NCHW || ldc > 0, "usr_pad: channel stride");
+  KAIR_CHECK_ARG(dtype == KAIR_F32 || (dtype == KAIR_BF16 && mode <= KAIR_USR_PAD_ZERO), "usr_pad: fold / crop are fp32");
+  const long npix = (mode == KAIR_USR_PAD_FOLD || mode == KAIR_USR_CROP_NCHW) ? (long)nb * H * W : (long)nb * Hp * Wp;
+  const long total = mode == KAIR_USR_CROP_NCHW ? npix : npix * ldc;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == KAIR_BF16)
+    hipLaunchKernelGGL(usr_pad_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, s, (const bf16*)src, (bf16*)dst, mode, ldc,
+                       H, W, Hp, Wp, total);
+  else
+    hipLaunchKernelGGL(usr_pad_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, (const float*)src, (float*)dst, mode,
+                       ldc, H, W, Hp, Wp, total);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

@@ -241,6 +241,7 @@ struct Epi {
   const float* mean; float range; int imgC, imgH, imgW;
   int ones_col;   // -1 none
   const float* resid2; long ldr2;
+  bf16* acopy; long ldac; int acones;   // halo conv: bf16 copy of the A image (acones: 1.0 channel, -1 none)
   long M; int N;
   FDiv d_rps, d_tok, d_hdp, d_pw;
   int dbg;   // ring-kernel ablation bits (KAIR_RING_DBG, perf investigation only): 1 no stores, 2 no MFMA, 4 no A loads
@@ -261,6 +262,7 @@ Epi make_epi(const kair_epilogue& o, long M, int N) {
   e.mean = o.img_mean; e.range = o.img_range; e.imgC = o.img_C; e.imgH = o.img_H; e.imgW = o.img_W;
   e.ones_col = o.out_ones_col_p1 - 1;
   e.resid2 = o.resid2; e.ldr2 = o.ldr2;
+  e.acopy = (bf16*)o.a_copy; e.ldac = o.ld_acopy; e.acones = o.acopy_ones_col_p1 - 1;
   e.M = M; e.N = N;
   e.d_rps = make_fdiv(e.rps); e.d_tok = make_fdiv(e.tok); e.d_hdp = make_fdiv(e.hdp); e.d_pw = make_fdiv(e.nh * e.hdp);
   static const int dbg = kair_dbg_env("KAIR_RING_DBG");
@@ -1061,9 +1063,21 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
 // ds_read_b64_tr_b16 transposed reads; D = B^T.A so each lane stores 4 consecutive k (16 B).
 // Rows past the split (and columns past N / K) read a zero line.  The bias-gradient "ones" column
 // must already be in B (kair_operand.ones_in_data).
+// BM_TAP: B is a 3x3 / pad-1 im2col of a bf16 NHWC image with exactly TNR_BK (192) channels, so
+// K-tile tk IS tap tk: row m of the tile reads pixel m + dy*W + dx of the image (a zero line where the
+// tap leaves the image).  The 9 taps of one row split are consecutive CTAs (one XCD: xcd_remap), so
+// the image rows and the A rows come from L2 after the first tap -- the conv weight gradient moves
+// ~1x its operands instead of the 9x re-read of a per-K-tile im2col.
 // ------------------------------------------------------------------------------------------
 
+#ifndef KAIR_TNR_NSG
+#define KAIR_TNR_NSG 6
+#endif
 constexpr int TNR_BN = 192, TNR_BK = 192, TNR_RB = 32, TNR_NS = 6;
+// the grouped launch runs on the side stream beside the data-gradient chain: a shallower ring
+// (TNR_NSG stages, 96 KiB) leaves room on each CU for a chain workgroup of <= 64 KiB LDS
+constexpr int TNR_NSG = KAIR_TNR_NSG;
+constexpr int BM_ROWS = 0, BM_TAP = 1;
 
 // One CTA's share of a TN ring product: rows [mbeg, mend) of the (n0, k0) 192x192 tile -> plane P.
 struct TnRingTile {
@@ -1074,9 +1088,10 @@ struct TnRingTile {
   float* P;                                     // this split's fp32 [N][K] plane
 };
 
-template <int AMA>
-KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, char* smem) {
-  constexpr int BNt = TNR_BN, BKt = TNR_BK, RB = TNR_RB, NS = TNR_NS;
+template <int AMA, int BMB, int NS>
+KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, const Op& Bo, char* smem) {
+  constexpr int BNt = TNR_BN, BKt = TNR_BK, RB = TNR_RB;
+  static_assert(NS >= 3 && NS <= 6, "ring depth: the counted waits below cover 1..4 chunks ahead");
   constexpr int PART = RB * BNt * 2;            // 12 KiB (A part; B part the same since BKt == BNt)
   constexpr int STAGE = 2 * PART;
   constexpr int ROWB = BNt * 2;                  // 384 B per LDS row
@@ -1091,6 +1106,10 @@ KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, char* smem) {
   const bf16* const Ap = t.Ap;
   const bf16* const Bp = t.Bp;
   const long Ald = t.Ald, Bld = t.Bld;
+  // BM_TAP: this tile's tap (dy, dx) and its row offset in the image
+  const int tap = BMB == BM_TAP ? k0 / BKt : 0;
+  const int tdy = tap / 3 - 1, tdx = tap - 3 * (tap / 3) - 1;
+  const int tshift = BMB == BM_TAP ? tdy * Bo.imW + tdx : 0;
   auto issue = [&](int j) {
     const int m0 = mbeg + j * RB;
     char* st = smem + (j % NS) * STAGE;
@@ -1104,7 +1123,14 @@ KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, char* smem) {
       const void* src = g_kair_zero_line;
       if (m < mend) {
         if (isB) {
-          if (k0 + c < K) src = Bp + (long)m * Bld + k0 + c;
+          if constexpr (BMB == BM_TAP) {
+            const int p = m - fdiv(m, Bo.d_hw) * Bo.d_hw.d;   // pixel within the image
+            const int y = fdiv(p, Bo.d_imW), x = p - y * Bo.imW;
+            if ((unsigned)(y + tdy) < (unsigned)Bo.imH && (unsigned)(x + tdx) < (unsigned)Bo.imW)
+              src = Bp + (long)(m + tshift) * Bld + c;
+          } else if (k0 + c < K) {
+            src = Bp + (long)m * Bld + k0 + c;
+          }
         } else if (n0 + c < N) {
           if constexpr (AMA == AM_ROWS) {
             src = Ap + (long)m * Ald + n0 + c;
@@ -1178,10 +1204,12 @@ KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, char* smem) {
     }
 }
 
-template <int AMA>
+// BM_TAP (the conv weight gradients, side stream) runs the grouped launch's shallower ring
+template <int AMA, int BMB>
 __global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
                                                        int rows_per_split) {
-  __shared__ __attribute__((aligned(16))) char smem[TNR_NS * 2 * TNR_RB * TNR_BN * 2];
+  constexpr int NS = BMB == BM_TAP ? TNR_NSG : TNR_NS;
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * TNR_RB * TNR_BN * 2];
   const int cta = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = cta % ntiles, split = cta / ntiles;
   const int tn = tile / tilesK, tk = tile - (tile / tilesK) * tilesK;
@@ -1193,7 +1221,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_ring(Op A, Op B, float* ws, in
   t.mbeg = split * rows_per_split;
   t.mend = t.mbeg + rows_per_split < M ? t.mbeg + rows_per_split : M;
   t.P = ws + (long)split * N * K;
-  tn_ring_body<AMA>(t, A, smem);
+  tn_ring_body<AMA, BMB, NS>(t, A, B, smem);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1214,7 +1242,7 @@ struct TnGroup {
 };
 
 __global__ __launch_bounds__(512, 1) void gemm_tn_ring_grouped(const TnGroup g) {
-  __shared__ __attribute__((aligned(16))) char smem[TNR_NS * 2 * TNR_RB * TNR_BN * 2];
+  __shared__ __attribute__((aligned(16))) char smem[TNR_NSG * 2 * TNR_RB * TNR_BN * 2];
   const int cta = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = cta % g.ntiles, split = cta / g.ntiles;
   int ji = 0;
@@ -1232,8 +1260,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_ring_grouped(const TnGroup g) 
   t.mbeg = split * g.rps;
   t.mend = t.mbeg + g.rps < g.M ? t.mbeg + g.rps : g.M;
   t.P = jb.ws + (long)split * jb.N * jb.K;
-  if (jb.qkv) tn_ring_body<AM_QKV>(t, g.qa, smem);
-  else tn_ring_body<AM_ROWS>(t, g.qa, smem);
+  if (jb.qkv) tn_ring_body<AM_QKV, BM_ROWS, TNR_NSG>(t, g.qa, g.qa, smem);
+  else tn_ring_body<AM_ROWS, BM_ROWS, TNR_NSG>(t, g.qa, g.qa, smem);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1630,6 +1658,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
           if (idx < halo_pieces) {
             const int pix = idx / c8n, c8 = idx - (idx / c8n) * c8n;
             *(uint4*)(sHalo + pix * PS + c8 * 8) = q;
+            if (E.acopy) {   // the tile's own pixels (halo interior): bf16 copy for the weight gradient
+              const int hr = pix / HWD, hc = pix - (pix / HWD) * HWD;
+              if (hr >= 1 && hr <= RPT && hc >= 1 && hc <= XW) {
+                uint4 qc = q;
+                const int oc = E.acones - c8 * 8;
+                if ((unsigned)oc < 8u) {
+                  bf16x8 v8 = __builtin_bit_cast(bf16x8, qc);
+                  v8[oc] = (bf16)1.f;
+                  qc = __builtin_bit_cast(uint4, v8);
+                }
+                const long px = ((long)(b * H + y0 + hr - 1) * W + x0 + hc - 1);
+                *(uint4*)(E.acopy + px * E.ldac + c8 * 8) = qc;
+              }
+            }
           }
         }
       }
@@ -1719,7 +1761,22 @@ static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, 
   if (e.omode != KAIR_OUT_ROWS || e.win.ws != 0 || e.gate || e.pre || e.resid2 || e.rowscale) return false;
   if (e.ldo % 4 != 0 || ((unsigned long)e.out & 15) || (e.resid && (e.ldr % 4 != 0 || ((unsigned long)e.resid & 15))))
     return false;
+  if (e.acopy && (e.ldac % 8 != 0 || ((unsigned long)e.acopy & 15))) return false;
   return true;
+}
+
+// the geometry half of conv_halo_ok, for hosts that pick a_copy (16-byte aligned rows, ld = C, plain
+// ROWS epilogue assumed)
+extern "C" int kair_conv3x3_halo_geometry(int H, int W, int C, long M, int N) {
+  if (C % HC_BK != 0 || C > 192 || N > HC_BN || N % 4 != 0 || W <= 0 || H <= 0 || M <= 0) return 0;
+  if (W <= HC_BM) {
+    if (HC_BM % W != 0 || H % (HC_BM / W) != 0) return 0;
+  } else if (W % HC_BM != 0) {
+    return 0;
+  }
+  const int XW = W < HC_BM ? W : HC_BM, RPT = HC_BM / XW;
+  if ((long)(RPT + 2) * (XW + 2) * (C + 8) > HC_HALO_ELEMS) return 0;
+  return M % HC_BM == 0 && M % ((long)H * W) == 0 && C % 8 == 0;
 }
 
 template <typename TA>
@@ -1740,6 +1797,7 @@ int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, in
   if constexpr (sizeof(CT) == 2) {
     if (mode == KAIR_LD_IM2COL3 && g_halo_mode != 0 && conv_halo_ok<TA>(A, B, E, M, N, K))
       return launch_conv_halo<TA>(A, B, E, M, K, s);
+    if (E.acopy) return kair_set_error(KAIR_ERR_ARG, "gemm_nt: a_copy needs the 3x3 halo-conv path (geometry / epilogue)");
   }
   if constexpr (sizeof(CT) == 2 && sizeof(TA) == 2) {
     if (g_ring_mode && ring_ok(mode, A, B, E, M, N, K)) {
@@ -1866,6 +1924,8 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
   KAIR_CHECK_ARG(!B->w_split || (compute == KAIR_BF16 && B->ld >= 2L * ((K + 63) / 64) * 64),
                  "gemm_nt: hi/lo split weights need bf16 compute and rows of 2*ceil(K/64)*64 columns");
   KAIR_CHECK_ARG(!A->w_split, "gemm_nt: w_split is a B-operand flag");
+  KAIR_CHECK_ARG(!E->a_copy || (compute == KAIR_BF16 && A->mode == KAIR_LD_IM2COL3 && A->im_up <= 1),
+                 "gemm_nt: a_copy is a side output of the bf16 3x3 conv (no upsample)");
   KAIR_CHECK_ARG((E->out_mode != KAIR_OUT_PSHUF && E->out_mode != KAIR_OUT_PUNSHUF && E->out_mode != KAIR_OUT_PSHUF_NCHW &&
                   E->out_mode != KAIR_OUT_PSHUF_SPM && E->out_mode != KAIR_OUT_PUNSHUF_SPM) ||
                      E->ps_r > 0, "gemm_nt: pixel shuffle r");
@@ -1889,9 +1949,13 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
 static bool tn_ring_shape(long M, int N, int K) {
   return N <= 576 && K <= 576 && N % 8 == 0 && K % 8 == 0 && N > 64 && K > 64 && M < (1L << 30);
 }
+// 3x3 conv weight gradient over a 192-channel image: the ring with one tap per K tile (BM_TAP)
+static bool tn_tap_shape(long M, int N, int K) {
+  return N <= 576 && N % 8 == 0 && N > 64 && K == 9 * TNR_BK && M < (1L << 30);
+}
 
 extern "C" int kair_wgrad_splits(long M, int N, int K) {
-  if (tn_ring_shape(M, N, K)) {   // ring kernel: one 192x192 tile per CTA, one CTA per CU
+  if (tn_ring_shape(M, N, K) || tn_tap_shape(M, N, K)) {   // ring kernel: one 192x192 tile per CTA, one CTA per CU
     if (g_num_cus == 0) init_num_cus();
     const int tiles = ((N + TNR_BN - 1) / TNR_BN) * ((K + TNR_BK - 1) / TNR_BK);
     long s = g_num_cus / tiles;
@@ -1942,11 +2006,26 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
     rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
     const long grid = (long)ntiles * splits;
     if (A->mode == KAIR_LD_ROWS)
-      hipLaunchKernelGGL(gemm_tn_ring<AM_ROWS>, dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK, ntiles,
-                         (int)rps);
+      hipLaunchKernelGGL((gemm_tn_ring<AM_ROWS, BM_ROWS>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
+                         ntiles, (int)rps);
     else
-      hipLaunchKernelGGL(gemm_tn_ring<AM_QKV>, dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK, ntiles,
-                         (int)rps);
+      hipLaunchKernelGGL((gemm_tn_ring<AM_QKV, BM_ROWS>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
+                         ntiles, (int)rps);
+    KAIR_CHECK_LAUNCH();
+    return 0;
+  }
+  // conv weight gradient, bf16 rows x bf16 192-channel image (ones column, if any, stored in the data)
+  if (g_ring_mode && compute == KAIR_BF16 && tn_tap_shape(M, N, K) && A->dtype == KAIR_BF16 && B->dtype == KAIR_BF16 &&
+      A->mode == KAIR_LD_ROWS && B->mode == KAIR_LD_IM2COL3 && B->im_C == TNR_BK && !B->im_flip && B->im_up <= 1 &&
+      !A->rowscale && !B->rowscale && A->win_ws == 0 && A->ones_col < 0 && (B->ones_col < 0 || B->ones_in_data) &&
+      A->ld % 8 == 0 && b.ld % 8 == 0 && (long)B->im_H * B->im_W > 0 && M % ((long)B->im_H * B->im_W) == 0) {
+    const int tilesN = (N + TNR_BN - 1) / TNR_BN, tilesK = 9;
+    const int ntiles = tilesN * tilesK;
+    long rps = (M + splits - 1) / splits;
+    rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
+    const long grid = (long)ntiles * splits;
+    hipLaunchKernelGGL((gemm_tn_ring<AM_ROWS, BM_TAP>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
+                       ntiles, (int)rps);
     KAIR_CHECK_LAUNCH();
     return 0;
   }
@@ -1984,11 +2063,17 @@ static long grouped_tiles(const kair_wgrad_job* jobs, int njobs) {
 
 // max_ctas > 0: at most that many (tile, split) workgroups -- fewer splits, so the launch holds only part
 // of the chip (the deferred gradient work beside the data-gradient chain, which needs the rest)
+// max_ctas < 0: -max_ctas times the default splits (shorter workgroups, which hand the CUs back to a
+// concurrent chain sooner; the workspace grows by the same factor), at >= 32 rows per split
 static int grouped_splits_capped(long M, long ntiles, int max_ctas) {
   int s = grouped_splits(M, ntiles);
   if (max_ctas > 0) {
     const long cap = max_ctas / (ntiles > 0 ? ntiles : 1);
     if (s > cap) s = (int)(cap < 1 ? 1 : cap);
+  } else if (max_ctas < 0) {
+    long t = (long)s * -max_ctas;
+    const long maxs = (M + TNR_RB - 1) / TNR_RB;
+    s = (int)(t < maxs ? t : maxs);
   }
   return s;
 }

@@ -203,7 +203,7 @@ class _Blk:
 
 class SwinIREngine:
     def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True, fused_mlp=None,
-                 split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=0):
+                 split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=0, side_priority=0):
         """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
         see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
         fused block kernels (_Lin, pack kind 12).
@@ -308,6 +308,7 @@ class SwinIREngine:
         self._side = None         # side stream of the deferred per-RSTB gradient work
         # side_stream=False: the deferred per-RSTB work runs in place on the main stream (A/B timing)
         self.side_stream = self.grouped_wgrad and torch.cuda.is_available() and bool(side_stream)
+        self.side_priority = side_priority   # torch stream priority of the side stream (0: default)
         # workgroup budget of the side-stream launches (0: uncapped).  The weight-gradient kernels hold one
         # 512-thread workgroup per CU; spread over the chip they keep the next RSTB's data-gradient kernels
         # off it until they end (rocprof: the first fc2 input gradient of every RSTB 43 -> 495 us behind the
@@ -315,6 +316,8 @@ class SwinIREngine:
         # (profiles/r03_side_ctas_ab.txt): a cap makes the side work critical at B=32 (48 CTAs: 1080 -> 808
         # patches/s) and gains ~2% at B=4 (96 CTAs) -- so uncapped by default.
         self.side_ctas = int(side_ctas)
+        # '1conv' weight gradients on the tap-per-tile ring (bf16 copies of G and the conv input)
+        self.conv_tap = self.tdt == torch.bfloat16 and self.Cp == 192 and self.C % 4 == 0
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -473,9 +476,18 @@ class SwinIREngine:
             q = max(r.Cq for r in [c for _, c in self.rstb] + [self.cab] if isinstance(r, _Resi3))
             P["r3_dz"] = (e(M, q, dt=T), e(M, q, dt=T))
         P["dfb"] = e(M, Cp)
+        if self.conv_tap:
+            # bf16 operands of each '1conv' weight gradient: (G, conv input with 1.0 in channel C), written by
+            # the halo convs (forward: input, backward dgrad: G) or, off that path, copied when the job runs
+            P["conv_halo"] = H.conv_halo_geometry(Hh, Ww, Cp, M, Cp)
+            P["conv_bf"] = {}
+            for r in [c for _, c in self.rstb] + [self.cab]:
+                if not isinstance(r, _Resi3):
+                    P["conv_bf"][id(r)] = (torch.zeros(M, Cp, device=dev, dtype=T), torch.zeros(M, Cp, device=dev, dtype=T))
+                    P["conv_bf"][id(r)][1][:, self.C] = 1.0
         # one shared wgrad workspace sized for the largest (splits * N * K)
         P["wg_ws"] = e(self._max_wgrad_ws(M, P))
-        P["wg_ws2"] = e(P["wg_ws"].numel()) if self.grouped_wgrad else None   # the side stream's
+        P["wg_ws2"] = e(P["wg_ws"].numel() * max(1, -self.side_ctas)) if self.grouped_wgrad else None   # the side stream's
         return P
 
     def _wgrad_shapes(self, M, P):
@@ -559,7 +571,10 @@ class SwinIREngine:
         """out = resi_conv(src) + resid (fp32 token rows, Cp columns)."""
         cd, Cp, M, Hh, Ww = self.cd, self.Cp, P["M"], P["H"], P["W"]
         if not isinstance(r, _Resi3):
-            H.gemm_nt(H.im2col(src, Hh, Ww, Cp), r.fwd(), H.epilogue(out, bias=r.bp, resid=resid), M, Cp, 9 * Cp, cd)
+            # training: the halo conv also leaves the bf16 weight-gradient operand (1.0 in channel C)
+            ac = (P["conv_bf"][id(r)][1], self.C) if P.get("conv_halo") else None
+            H.gemm_nt(H.im2col(src, Hh, Ww, Cp), r.fwd(), H.epilogue(out, bias=r.bp, resid=resid, acopy=ac), M, Cp,
+                      9 * Cp, cd)
             return
         t1, t2 = P["r3"][id(r)]
         lk = dict(act=H.ACT_LEAKY, slope=0.2)
@@ -574,7 +589,10 @@ class SwinIREngine:
         cd, Cp, M, Hh, Ww = self.cd, self.Cp, P["M"], P["H"], P["W"]
         g = lambda p: grads[p]
         if not isinstance(r, _Resi3):
-            H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.Wd), H.epilogue(D), M, Cp, 9 * Cp, cd)
+            ac = (P["conv_bf"][id(r)][0], -1) if P.get("conv_halo") else None
+            H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.Wd), H.epilogue(D, acopy=ac), M, Cp, 9 * Cp, cd)
+            if self.conv_tap:   # bf16 operands: the halo convs' copies (else taken when the job runs)
+                return ("tap", G, src, r, g(r.w), g(r.b))
             return (H.rows(G), H.im2col(src, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, r.map, g(r.w), g(r.b), self.C)
         t1, t2 = P["r3"][id(r)]
         q = r.Cq
@@ -690,9 +708,29 @@ class SwinIREngine:
         S = H.wgrad_splits(M, N, K)
         if max_ctas > 0:   # fewer row splits: at most max_ctas (tile, split) workgroups
             S = max(1, min(S, max_ctas // H.wgrad_tiles(N, K)))
+        elif max_ctas < 0:   # more, shorter ones (-max_ctas times the splits, >= 32 rows each)
+            S = min(S * -max_ctas, -(-M // 32))
         ws = P["wg_ws"] if ws is None else ws
         H.gemm_tn(A, Bop, ws, S, M, N, K, self.cd)
         H.wgrad_finalize(ws, S, layer_map, wgrad, bgrad, ones_col)
+
+    def _run_conv_job(self, P, job, ws=None, max_ctas=0):
+        """A '1conv' residual conv's weight gradient (the job _resi_bwd returned).  Tap form: G and the
+        conv input go to bf16 copies (the input with 1.0 in channel C for the bias), then one ring launch
+        with a tap per K tile reads each operand row ~once (gemm.hip BM_TAP) instead of the fp32 im2col
+        kernel's re-read per K tile."""
+        if job[0] != "tap":
+            self._wgrad(P, *job, ws=ws, max_ctas=max_ctas)
+            return
+        _, G, src, r, gw, gb = job
+        Cp, C, M = self.Cp, self.C, P["M"]
+        gbf, xbf = P["conv_bf"][id(r)]
+        if not P["conv_halo"]:
+            H.row_copy(G, Cp, M, C, H.copy_desc(gbf))
+            H.row_copy(src, Cp, M, C, H.copy_desc(xbf))
+        oc = 4 * Cp + C   # the center tap's channel C: 1.0 for every pixel
+        self._wgrad(P, H.rows(gbf), H.im2col(xbf, P["H"], P["W"], Cp, ones_col=oc, ones_in_data=True), M, Cp, 9 * Cp,
+                    r.map, gw, gb, oc, ws=ws, max_ctas=max_ctas)
 
     def _bias_colsum(self, P, G, M, Np, layer_map, bgrad):
         H.colsum(G, M, Np, layer_map, bgrad, P["colsum_ws"])
@@ -782,7 +820,7 @@ class SwinIREngine:
         G, D = P["G"], P["D"]
         job = self._resi_bwd(self.cab, P, P["dfb"], P["nf"], D, grads)
         if job is not None:
-            self._wgrad(P, *job)
+            self._run_conv_job(P, job)
         # ---- final norm: nf = LN(u_G) -----------------------------------------------------
         n = self.norm
         last_in = P["rstb_out"][-1]
@@ -899,7 +937,7 @@ class SwinIREngine:
         side = None
         if self.side_stream:
             if self._side is None:
-                self._side = torch.cuda.Stream(device=self.device)
+                self._side = torch.cuda.Stream(device=self.device, priority=self.side_priority)
             side = self._side
             side.wait_stream(torch.cuda.current_stream())
         ws = P["wg_ws2"] if side is not None else P["wg_ws"]
@@ -919,8 +957,8 @@ class SwinIREngine:
                 for i in range(0, len(jobs), H.GROUP_MAX):
                     H.attn_dtable_grouped(jobs[i:i + H.GROUP_MAX])
             jobs, self._conv_pending = self._conv_pending, []
-            for A, Bop, M, N, K, m, gw, gb, oc in jobs:
-                self._wgrad(P, A, Bop, M, N, K, m, gw, gb, oc, ws=ws, max_ctas=cap)
+            for job in jobs:
+                self._run_conv_job(P, job, ws=ws, max_ctas=cap)
         return side is not None
 
     def _block_bwd(self, blk, P, S, x_in, D, bi, grads, j, par):

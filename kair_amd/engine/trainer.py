@@ -66,8 +66,10 @@ def segment_buckets(params, segs):
 
 class FusedTrainer:
     def __init__(self, netG, netE=None, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, E_decay=0.999,
-                 loss_weight=1.0, use_graph=True, process_group=None, bucket_mb=25, segment_graphs=None, charb_eps=None):
+                 loss_weight=1.0, use_graph=True, process_group=None, bucket_mb=25, segment_graphs=None, charb_eps=None,
+                 stream_priority=0):
         self.net, self.ema_net = netG, netE
+        self.stream_priority = stream_priority   # torch priority of the capture stream (0: default)
         self.device = next(netG.parameters()).device
         self.engine = netG.engine()
         self.flat_p, self.params = flatten_params(netG, self.device)
@@ -150,7 +152,7 @@ class FusedTrainer:
         pool = torch.cuda.graph_pool_handle()
         buckets = self.segment_buckets() if self.segment_graphs else None
         graphs, gu = [], None
-        cs = torch.cuda.Stream()
+        cs = torch.cuda.Stream(priority=self.stream_priority)
         cs.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(cs):
             if self.world == 1 and not buckets:

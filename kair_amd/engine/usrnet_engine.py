@@ -21,8 +21,10 @@ through the pixel-shuffle store, skip gradients added by the first ResBlock of e
 ResUNet weights are shared by the n iterations, so their gradients accumulate.
 
 Maps are NHWC fp32 token rows (ReLU outputs and GEMM-only operands in the compute dtype), complex
-planes float2 [planes][W][H] (kair_hip.h).  The HR size must be a multiple of 8 (the reference's
-ReplicationPad2d to a multiple of 8, v1:150-152, is not implemented) and B*H*W < 2^24.
+planes float2 [planes][W][H] (kair_hip.h).  An HR size that is not a multiple of 8 runs the ResUNet on
+the replicate-padded grid (v1:148-151) and crops its output (v1:164) -- kair_usr_pad, with the zero pad
+(crop adjoint) of the output gradient and the fold (replicate adjoint) of the input gradient in
+backward.  B*Hp*Wp < 2^24.
 """
 import weakref
 
@@ -172,15 +174,15 @@ class USRNetEngine:
     def _build_plan(self, key, infer):
         B, h, w, sf, kh, kw = key
         Hh, Ww = h * sf, w * sf
-        if Hh % 8 or Ww % 8:
-            raise NotImplementedError("kair_amd USRNet: the HR size must be a multiple of 8 (the ResUNet's "
-                                      "ReplicationPad2d, network_usrnet_v1.py:150-152, is not implemented)")
-        M = [B * (Hh >> l) * (Ww >> l) for l in range(4)]
+        Hp, Wp = -(-Hh // 8) * 8, -(-Ww // 8) * 8   # the ResUNet's grid (ReplicationPad2d, v1:148-151)
+        pad = (Hp, Wp) != (Hh, Ww)
+        M = [B * (Hp >> l) * (Wp >> l) for l in range(4)]
         if M[0] >= 1 << 24:
-            raise NotImplementedError("kair_amd USRNet: B*H*W must be < 2^24")
+            raise NotImplementedError("kair_amd USRNet: B*Hp*Wp must be < 2^24")
         T, e, nc, C = self.tdt, self._e, self.nc, self.out_nc
         planes = B * C
-        P = {"B": B, "h": h, "w": w, "sf": sf, "H": Hh, "W": Ww, "M": M}
+        P = {"B": B, "h": h, "w": w, "sf": sf, "H": Hh, "W": Ww, "Hp": Hp, "Wp": Wp, "pad": pad, "M": M}
+        Mu = B * Hh * Ww   # pixels of the HR grid
         cplx = planes * Hh * Ww * 2
         P["T"], P["FBFy"] = e(cplx), e(cplx)
         P["FB"] = e(B * Hh * Ww * 2)
@@ -190,14 +192,17 @@ class USRNetEngine:
         its = []
         for _ in range(self.n):
             its.append({"FR": e(cplx), "xin": e(M[0], C8, dt=T), "xout": e(B, C, Hh, Ww),
+                        "xin_u": e(Mu, C8, dt=T) if pad else None, "xout_p": e(B, C, Hp, Wp) if pad else None,
                         "X": [e(M[l], nc[l]) for l in range(4)],
                         "down": [self._chain(M[l], nc[l], len(self.down_rbs[l])) for l in range(3)],
                         "body": self._chain(M[3], nc[3], len(self.body_rbs)),
                         "t": [e(M[l], nc[l]) for l in range(3)],
                         "up": [self._chain(M[l], nc[l], len(self.up_rbs[2 - l])) for l in range(3)]})
         P["it"] = its
-        P["gE"] = torch.zeros(M[0], C8, device=self.device, dtype=T)
+        P["gE"] = torch.zeros(Mu, C8, device=self.device, dtype=T)
         P["gxin"] = e(M[0], C8)
+        if pad:   # the output gradient on the padded grid (zeros outside), the input gradient folded back
+            P["gE_p"], P["gxin_u"] = e(M[0], C8, dt=T), e(Mu, C8)
         P["G"] = [{"gS": e(M[l], nc[l]), "gc": e(M[l], nc[l]), "ga": e(M[l], nc[l]), "gb": e(M[l], nc[l]),
                    "gz": e(M[l], nc[l], dt=T)} for l in range(4)]
         P["a_ws"] = e(planes * (Ww // sf))
@@ -251,10 +256,15 @@ class USRNetEngine:
         H.usr_fft_cols(H.USR_COL_DATA_FWD, P["T"], P["T"], P["FB"], P["FBFy"], S["FR"], P["invW"], ab[:, i], self.no, None,
                        planes, C, Hh, Ww, sf)
         H.usr_ifft_rows(P["T"], P["z"], False, C, 0, 1.0 / (Hh * Ww), planes, Hh, Ww)
-        H.usr_pack_input(P["z"], ab[:, self.n + i], self.no, S["xin"], C8, B, C, Hh * Ww)
+        if P["pad"]:
+            H.usr_pack_input(P["z"], ab[:, self.n + i], self.no, S["xin_u"], C8, B, C, Hh * Ww)
+            H.usr_pad(S["xin_u"], S["xin"], H.USR_PAD_REPLICATE, C8, B, Hh, Ww, P["Hp"], P["Wp"])
+        else:
+            H.usr_pack_input(P["z"], ab[:, self.n + i], self.no, S["xin"], C8, B, C, Hh * Ww)
 
     def _grid(self, P, l):
-        return P["H"] >> l, P["W"] >> l
+        """The ResUNet's level-l grid (the replicate-padded HR grid at l = 0)."""
+        return P["Hp"] >> l, P["Wp"] >> l
 
     def _chain_fwd(self, rbs, bufs, x, Hl, Wl, M, c, skip=None):
         """ResBlocks x + conv2(relu(conv1(x))); the last adds `skip` (the U-Net skip) too."""
@@ -288,9 +298,12 @@ class USRNetEngine:
                       M[l + 1], 4 * nc[l], nc[l + 1], cd)
             Hl, Wl = self._grid(P, l)
             s = self._chain_fwd(self.up_rbs[u], S["up"][l], S["t"][l], Hl, Wl, M[l], nc[l], skip=S["X"][l])
+        xo = S["xout_p"] if P["pad"] else S["xout"]
         H.gemm_nt(H.im2col(s, H0, W0, nc[0]), H.rows(self.tail.Wf),
-                  H.epilogue(S["xout"], mode=H.OUT_NCHW, ldo=0, img=(None, 1.0, self.out_nc, H0, W0)), M[0], C8,
+                  H.epilogue(xo, mode=H.OUT_NCHW, ldo=0, img=(None, 1.0, self.out_nc, H0, W0)), M[0], C8,
                   9 * nc[0], cd)
+        if P["pad"]:   # x[..., :h, :w] (v1:164)
+            H.usr_pad(xo, S["xout"], H.USR_CROP_NCHW, 0, P["B"] * self.out_nc, P["H"], P["W"], H0, W0)
 
     # ------------------------------------------------------------------------------------
     # backward
@@ -314,10 +327,14 @@ class USRNetEngine:
         for i in range(n - 1, -1, -1):
             S = P["it"][i]
             self._unet_bwd(P, S, grads, acc=i < n - 1)
+            gxin = P["gxin"]
+            if P["pad"]:   # adjoint of the replicate pad: pad pixels' gradients onto the edge they copied
+                gxin = P["gxin_u"]
+                H.usr_pad(P["gxin"], gxin, H.USR_PAD_FOLD, C8, B, Hh, Ww, P["Hp"], P["Wp"])
             # beta_i: channel C of the ResUNet input gradient, summed over pixels
-            H.usr_chan_sum(P["gxin"], C8, C, Hh * Ww, B, P["cs_ws"], gab[:, n + i], self.no)
+            H.usr_chan_sum(gxin, C8, C, Hh * Ww, B, P["cs_ws"], gab[:, n + i], self.no)
             # DataNet_i backward: dL/dx_{i-1} (skipped for i = 0: the upsampled LQ needs none) and dL/dalpha_i
-            H.usr_fft_rows(P["gxin"], H.USR_SRC_NHWC, C, C8, 0, 0, 1, P["T"], planes, Hh, Ww)
+            H.usr_fft_rows(gxin, H.USR_SRC_NHWC, C, C8, 0, 0, 1, P["T"], planes, Hh, Ww)
             H.usr_fft_cols(H.USR_COL_DATA_BWD, P["T"], P["T"] if i > 0 else None, P["FB"], P["FBFy"], S["FR"], P["invW"],
                            ab[:, i], self.no, P["a_ws"], planes, C, Hh, Ww, sf)
             H.usr_seg_sum(P["a_ws"], C * (Ww // sf), B, inv_n, gab[:, i], self.no)
@@ -351,6 +368,9 @@ class USRNetEngine:
         cd, nc, M, Gs = self.cd, self.nc, P["M"], P["G"]
         H0, W0 = self._grid(P, 0)
         gE = P["gE"]
+        if P["pad"]:   # adjoint of the crop: the output gradient on the padded grid, zeros outside
+            H.usr_pad(gE, P["gE_p"], H.USR_PAD_ZERO, C8, P["B"], P["H"], P["W"], H0, W0)
+            gE = P["gE_p"]
         H.gemm_nt(H.im2col(gE, H0, W0, C8, flip=True), H.rows(self.tail.Wd), H.epilogue(Gs[0]["gS"]), M[0], nc[0],
                   9 * C8, cd)
         s1 = S["up"][0][-1]["out"]

@@ -263,6 +263,60 @@ def test_conv_wgrad_im2col(compute):
     assert rel_err(grad, w.grad) < TOL[compute][0]
 
 
+@pytest.mark.parametrize("B,Hh,Ww,Cout", [(2, 16, 16, 180), (3, 10, 12, 96), (1, 64, 64, 180)])
+def test_conv_wgrad_tap_ring(B, Hh, Ww, Cout):
+    """The RSTB conv weight gradient on the tap-per-tile ring (gemm.hip BM_TAP): bf16 G rows x a bf16
+    192-channel image holding 1.0 in channel C (the bias, read through the center tap), against float64
+    conv2d backward on the same bf16 values (network_swinir.py:465 conv 3x3, RSTB.forward :481-482)."""
+    C, Cp = 180, 192
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(B, C, Hh, Ww, generator=g).to(torch.bfloat16).double().requires_grad_(True)
+    w = torch.randn(Cout, C, 3, 3, generator=g, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(Cout, dtype=torch.float64, requires_grad=True)
+    y = torch.nn.functional.conv2d(x, w, b, padding=1)
+    gy = torch.randn(y.shape, generator=g).to(torch.bfloat16).double()
+    y.backward(gy)
+    M, Np = B * Hh * Ww, -(-Cout // 8) * 8
+    dy = torch.zeros(M, Np, dtype=torch.bfloat16)
+    dy[:, :Cout] = gy.permute(0, 2, 3, 1).reshape(M, Cout).to(torch.bfloat16)
+    xin = torch.zeros(M, Cp, dtype=torch.bfloat16)
+    xin[:, :C] = x.detach().permute(0, 2, 3, 1).reshape(M, C).to(torch.bfloat16)
+    xin[:, C] = 1.0
+    K, oc = 9 * Cp, 4 * Cp + C
+    S = H.wgrad_splits(M, Np, K)
+    assert H.wgrad_tiles(Np, K) == -(-Np // 192) * 9
+    ws = torch.full((S, Np, K), float("nan"), device=dev)
+    H.gemm_tn(H.rows(dy.to(dev)), H.im2col(xin.to(dev), Hh, Ww, Cp, ones_col=oc, ones_in_data=True), ws, S, M, Np, K,
+              H.BF16)
+    grad = torch.empty(Cout, C, 3, 3, device=dev)
+    bg = torch.empty(Cout, device=dev)
+    H.wgrad_finalize(ws, S, H.wmap(1, Cout, C, (1, Cout, Np), (1, C, Cp)), grad, bg, oc)
+    torch.cuda.synchronize()
+    assert rel_err(grad, w.grad) < 1e-5
+    assert rel_err(bg, b.grad) < 1e-5
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_conv_halo_acopy(flip):
+    """The halo conv's side output (kair_epilogue.a_copy): the bf16 image of its fp32 A operand, channel
+    ones_col forced to 1.0 -- the tap ring's weight-gradient operand -- next to an unchanged conv."""
+    B, Hh, Ww, C = 2, 48, 48, 192
+    M = B * Hh * Ww
+    assert H.conv_halo_geometry(Hh, Ww, C, M, C) and not H.conv_halo_geometry(16, 16, C, 256, C)
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(M, C, generator=g).to(dev)
+    w = (torch.randn(C, 9 * C, generator=g) * 0.05).to(dev, torch.bfloat16)
+    out0, out1 = torch.empty(M, C, device=dev), torch.empty(M, C, device=dev)
+    cp = torch.full((M, C), float("nan"), device=dev, dtype=torch.bfloat16)
+    H.gemm_nt(H.im2col(x, Hh, Ww, C, flip=flip), H.rows(w), H.epilogue(out0), M, C, 9 * C, H.BF16)
+    H.gemm_nt(H.im2col(x, Hh, Ww, C, flip=flip), H.rows(w), H.epilogue(out1, acopy=(cp, 180)), M, C, 9 * C, H.BF16)
+    torch.cuda.synchronize()
+    ref = x.to(torch.bfloat16)
+    ref[:, 180] = 1.0
+    assert torch.equal(out0, out1)
+    assert torch.equal(cp, ref)
+
+
 @pytest.mark.parametrize("dtype", [H.F32, H.BF16])
 @pytest.mark.parametrize("win", [(0, 0, 0, 0), (16, 16, 8, 4)])
 def test_layernorm(dtype, win):

@@ -151,11 +151,14 @@ def test_usrnet_vs_golden(dt):
                           sub_grads(z, ""), dt)
 
 
-@pytest.mark.parametrize("lq,sf,n_iter,B", [(32, 4, 6, 2), (32, 3, 2, 2), (24, 2, 3, 2), (128, 4, 6, 1)])
+@pytest.mark.parametrize("lq,sf,n_iter,B", [(32, 4, 6, 2), (32, 3, 2, 2), (24, 2, 3, 2), (128, 4, 6, 1), (27, 4, 2, 1),
+                                             (18, 3, 2, 2)])
 def test_usrnet_option_config_vs_oracle(lq, sf, n_iter, B):
     """train_usrnet.json widths (h_nc 32, nc 16/32/64/64, nb 2), fp32 parity mode vs the CPU oracle;
     (128, 4, 6, 1) is config C3 at its configured size: 128-px LQ, x4, i.e. a 512^2 HR grid through six
-    DataNet + ResUNet stages (network_usrnet_v1.py:237-262), forward and every parameter gradient."""
+    DataNet + ResUNet stages (network_usrnet_v1.py:237-262), forward and every parameter gradient.
+    (27, 4) and (18, 3): HR 108^2 / 54^2, not multiples of 8 -- the ResUNet's ReplicationPad2d and crop
+    (v1:148-151, 164) and their adjoints."""
     torch.manual_seed(21 + sf)
     net = USRNet(n_iter=n_iter, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2, compute_dtype="fp32")
     ref = ocv.USRNet(n_iter=n_iter, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2)
