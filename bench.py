@@ -123,11 +123,11 @@ def time_roles(tr):
     orig = {n: getattr(H, n) for n in _TIMED}
     run0 = H.WgradGroup.run
 
-    def wg_run(self, ws):
+    def wg_run(self, ws, **kw):
         fr = sys._getframe(1)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        run0(self, ws)
+        run0(self, ws, **kw)
         e1.record()
         rec.append((f"wgrad_grouped @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}", "wgrad_grouped", (), e0, e1))
     for n in _TIMED:
@@ -158,9 +158,10 @@ def rocprof_name(fn, a):
     if fn.startswith("rowgemm_"):
         K, N = a[2], (a[4] if fn != "rowgemm_lnbwd" else 192)
         kb = K // 16
-        pd = {12: 4, 24: 4, 36: 2}[kb]
         epi = {"rowgemm_store": 0, "rowgemm_gate": 1, "rowgemm_lnbwd": 2}[fn]
-        return f"rowgemm_kernel<{kb}, {pd}, {N // 96}, {epi}>"
+        ks = 2 if N == 384 else 4   # csrc/rowgemm.hip rg_dispatch: <KB, KS, NWC, EPI, HOLD>
+        hold = {12: kb // ks, 24: 5 if epi == 2 else 6, 36: {0: 9, 1: 7, 2: 4}[epi]}[kb]
+        return f"rowgemm_kernel<{kb}, {ks}, {N // 96}, {epi}, {hold}>"
     return {"swin_mlp_fwd": "swin_mlp_fwd_kernel<1>", "swin_attn_fwd": "swin_attn_fwd_kernel<6, 1>",
             "window_attn_bwd": "attn_bwd_bf16_kernel"}.get(fn, fn)
 

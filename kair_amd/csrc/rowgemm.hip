@@ -14,18 +14,17 @@
 //   EPI_GATE  Y * g (g = the stored GELU'(fc1 pre-activation)) -> bf16 rows   (fc2 input gradient);
 //   EPI_STORE Y -> bf16 rows                                                  (proj input gradient).
 //
-// Layout of the work: a workgroup owns one 32-row tile at a time (persistent over tiles), NWC waves
-// each computing 96 output columns of it (3 x v_mfma_f32_32x32x16_bf16 accumulators: lane = column,
-// registers = rows).  One wave per SIMD (the kernel keeps ~350 VGPRs), so every wave streams:
-//   * A fragments straight from HBM into registers, PD k-steps ahead, continuing into the NEXT tile's
-//     first k-steps while this tile finishes (no LDS staging, no barrier in the k-loop);
-//   * W fragments (1 KiB coalesced wave loads, L2-resident) at the SAME distance PD: vmcnt retires
-//     loads in issue order, so a W stream prefetched less deeply than A would make every W wait
-//     also wait for the younger A loads and cut A's latency budget down to W's;
-//   * the epilogue's per-tile operands (x / the gate) at the tile start, landed by the epilogue.
-// The LayerNorm row sums need the whole row: each wave reduces its 96 columns in registers
-// (+ a 32-lane DPP / swizzle reduction) and the NWC waves exchange the per-row partials through
-// LDS (fixed order, deterministic).
+// Layout of the work: a workgroup (one per CU, persistent over 32-row tiles) splits the K = 16 KB
+// contraction over KS groups of NWC waves; wave (group g, column block c) computes 96 output columns
+// (3 x v_mfma_f32_32x32x16_bf16 accumulators: lane = column, registers = rows) over k-steps
+// [g KB/KS, (g+1) KB/KS).  Short per-wave k-loops are what the small per-GPU batch needs (B = 4:
+// 288 tiles for 256 CUs, so a tile's dependent chain IS the kernel time):
+//   * the wave's weight fragments are loaded ONCE and held in registers for every tile (HOLD of its
+//     k-steps; the rest re-read from L2 under the held steps' MFMAs where registers run out);
+//   * the next tile's A rows and epilogue operands are issued right after this tile's MFMAs, so they
+//     land under the partial-sum exchange and the epilogue; no LDS staging, no barrier in the k-loop.
+// The KS partial products meet in LDS (one fp32 plane per group), summed in fixed order by the
+// epilogue, which reads whole rows (deterministic).  The LayerNorm epilogue runs 16 lanes per row.
 #include <string.h>
 
 #include "common.h"
@@ -89,133 +88,165 @@ KAIR_DEV float half_sum32(float v) {
   return v + __shfl_xor(v, 16, 64);
 }
 
-template <int KB, int PD, int NWC, int EPI>
-__global__ __launch_bounds__(64 * NWC, 2) void rowgemm_kernel(const RgArgs a) {
-  static_assert(PD <= KB, "prefetch distance must not exceed the k-steps of a tile");
+// Per-tile epilogue operands (double-buffered across the persistent loop: tile t's are in use while
+// tile t + G's land)
+template <int LPASS, int CPT>
+struct EpiOps {
+  unsigned tof[LPASS], cof[LPASS];   // LN: byte offsets of this lane's rows in x / D and in the copy
+  float mu[LPASS], rs[LPASS], sc[LPASS];
+  float4 xv[LPASS][3];
+  uint4 gv[CPT];                      // GATE: 8 bf16 gate values per chunk
+};
+
+// KB k-steps of 16 split over KS wave groups (KBW each); NWC waves per group, 96 columns per wave.
+// Every wave holds ITS weight fragments (KBW x 3) in registers for the whole launch (loaded once),
+// so a tile's k-loop waits for nothing but its own A rows, which were prefetched during the previous
+// tile's epilogue.  The KS partial products meet in LDS (one fp32 plane per group) and the epilogue
+// sums them in fixed order (deterministic).
+// HOLD < KBW: only the first HOLD k-steps' fragments stay resident, the rest are re-read from L2 at
+// each tile's start (in flight under the resident steps' MFMAs) -- the register budget of the
+// LayerNorm epilogue at K = 576.
+template <int KB, int KS, int NWC, int EPI, int HOLD>
+__global__ __launch_bounds__(64 * NWC * KS, 1) void rowgemm_kernel(const RgArgs a) {
+  static_assert(KB % KS == 0, "k-steps per group");
+  constexpr int KBW = KB / KS, NSTR = KBW - HOLD;
+  static_assert(HOLD >= 1 && HOLD <= KBW && HOLD * NCT <= 27, "weight fragments held in registers");
   static_assert(EPI != EPI_LN || NWC == 2, "the LayerNorm epilogue is laid out for 192 columns");
-  constexpr int NT = 64 * NWC, N = 96 * NWC, LDY = N + 4;
-  constexpr int NCH = N / 8, CPT = RT * NCH / NT;   // STORE / GATE: 8-column chunks per row / per thread
-  static_assert(RT * NCH % NT == 0, "chunks per thread");
-  const int tid = threadIdx.x, lane = tid & 63, cw = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NT = 64 * NWC * KS, N = 96 * NWC, LDY = N + 4, PLANE = RT * LDY;
+  constexpr int NCH = N / 8, NCHUNK = RT * NCH, CPT = (NCHUNK + NT - 1) / NT;   // STORE / GATE chunks
+  constexpr int RPP = NT / 16, LPASS = RT / RPP;                                   // LN: rows per pass
+  static_assert(RT % RPP == 0, "LayerNorm passes");
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cw = wave % NWC, ks = wave / NWC;
   const int l31 = lane & 31, hh = lane >> 5;
-  // the tile's Y (fp32), written by the accumulators (lane = column) and read back row-contiguous
-  __shared__ __attribute__((aligned(16))) float sY[RT * LDY];
+  __shared__ __attribute__((aligned(16))) float sY[KS * PLANE];
   const long G = gridDim.x;
   long tile = blockIdx.x;
   if (tile >= a.ntiles) return;           // the host launches at most ntiles workgroups
 
-  // W: a buffer resource over this wave's fragments (wave-uniform) + one 32-bit lane offset; the
-  // per-fragment offsets are constants passed as the scalar offset (no per-load 64-bit address)
+  // this wave's weight fragments, once: kind 13 [N/32][KB][64 lanes][8], 1 KiB coalesced wave loads
   const Rsrc rW = rsrc(a.W + (long)(NCT * cw) * KB * 512, (long)NCT * KB * 1024);
   const unsigned wl = lane * 16u;
+  bf16x8 rw[HOLD][NCT];
+#pragma unroll
+  for (int i = 0; i < HOLD; ++i)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) rw[i][ct] = bld16(rW, wl, (ct * KB + ks * KBW + i) * 1024u);
   const int c0 = 96 * cw + l31;           // this lane's accumulator column of tile ct: c0 + 32 ct
 
-  // LN row layout: 16 lanes per row (lane jl: columns 4 jl + 64 k, k < 3), 8 rows per pass, 4 passes
-  constexpr int LPASS = RT / (NT / 16);
+  // LN row layout: 16 lanes per row (lane jl: columns 4 jl + 64 k, k < 3), RPP rows per pass.
+  // The dgamma / dbeta partials of a lane's columns live in LDS slots only that lane touches (registers
+  // are the K=576 launch's limit), summed over the RPP row groups in fixed order at the end.
   const int lr = tid >> 4, jl = tid & 15;
-  float4 gam4[3], pg[3], pb[3];
+  __shared__ __attribute__((aligned(16))) float sP[EPI == EPI_LN ? RPP * 2 * 192 : 4];
+  __shared__ __attribute__((aligned(16))) float sGam[EPI == EPI_LN ? 192 : 4];   // gamma, 0 past C
+  if constexpr (EPI == EPI_LN) {
+    for (int c = tid; c < 192; c += NT) sGam[c] = c < a.C ? a.gamma[c] : 0.f;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    pg[k] = pb[k] = gam4[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (EPI == EPI_LN) {
-      const int c = 4 * jl + 64 * k;
-      gam4[k] = make_float4(c < a.C ? a.gamma[c] : 0.f, c + 1 < a.C ? a.gamma[c + 1] : 0.f,
-                            c + 2 < a.C ? a.gamma[c + 2] : 0.f, c + 3 < a.C ? a.gamma[c + 3] : 0.f);
+    for (int k = 0; k < 3; ++k) {
+      *(float4*)(sP + lr * 2 * 192 + 4 * jl + 64 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *(float4*)(sP + lr * 2 * 192 + 192 + 4 * jl + 64 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
   const Rsrc rx = rsrc(a.x, a.xbytes), rD = rsrc(a.D, a.dbytes), rC = rsrc(a.cp, a.cp ? a.cbytes : 0);
 
-  for (; tile < a.ntiles; tile += G) {
-    const long row0 = tile * RT;
-    // ---- epilogue operands of this tile, issued before the k-loop (landed by the epilogue)
-    unsigned tof[LPASS], cof[LPASS];   // LN: byte offsets of this lane's rows in x / D and in the copy
-    float mu[LPASS], rs[LPASS], sc[LPASS];
-    float4 xv[LPASS][3];
-    uint4 gv[CPT];                      // GATE: 8 bf16 gate values per chunk
+  typedef EpiOps<LPASS, CPT> E;
+  auto load_epi = [&](long t, E& e) {
+    const long row0 = t * RT;
     if constexpr (EPI == EPI_LN) {
 #pragma unroll
       for (int p = 0; p < LPASS; ++p) {
-        const long row = row0 + (NT / 16) * p + lr;
+        const long row = row0 + RPP * p + lr;
         const bool ok = row < a.M;
-        const int t = win_to_token32((int)(ok ? row : a.M - 1), a.wm);
-        mu[p] = a.mean[t];
-        rs[p] = a.rstd[t];
-        sc[p] = a.cp_scale ? a.cp_scale[t / a.cp_rps] : 1.f;
+        const int tk = win_to_token32((int)(ok ? row : a.M - 1), a.wm);
+        e.mu[p] = a.mean[tk];
+        e.rs[p] = a.rstd[tk];
+        e.sc[p] = a.cp_scale ? a.cp_scale[tk / a.cp_rps] : 1.f;
         // rows past M: offsets outside the resources (the range check drops those loads and stores)
-        tof[p] = ok ? ((unsigned)t * (unsigned)a.ldx + 4u * jl) * 4u : 0x80000000u;
-        cof[p] = ok ? ((unsigned)token_to_win(t, a.cwm) * (unsigned)a.ldc + 4u * jl) * 2u : 0x80000000u;
+        e.tof[p] = ok ? ((unsigned)tk * (unsigned)a.ldx + 4u * jl) * 4u : 0x80000000u;
+        e.cof[p] = ok ? ((unsigned)token_to_win(tk, a.cwm) * (unsigned)a.ldc + 4u * jl) * 2u : 0x80000000u;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) xv[p][k] = bld4(rx, tof[p] + 256u * k);
+        for (int k = 0; k < 3; ++k) e.xv[p][k] = bld4(rx, e.tof[p] + 256u * k);
       }
     } else if constexpr (EPI == EPI_GATE) {
 #pragma unroll
       for (int i = 0; i < CPT; ++i) {
         const int q = tid + NT * i, r = q / NCH, c8 = (q - r * NCH) * 8;
         const long row = row0 + r < a.M ? row0 + r : a.M - 1;
-        gv[i] = *(const uint4*)(a.gate + row * a.ldg + c8);
+        if (q < NCHUNK) e.gv[i] = *(const uint4*)(a.gate + row * a.ldg + c8);
       }
     }
+  };
+  bf16x8 ra[KBW];
+  auto load_a = [&](long t) {
+    long r = t * RT + l31;
+    if (r >= a.M) r = a.M - 1;
+    const bf16* ap = a.A + r * a.lda + 8 * hh + 16 * KBW * ks;
+#pragma unroll
+    for (int i = 0; i < KBW; ++i) ra[i] = *(const bf16x8*)(ap + 16 * i);
+  };
 
-    // ---- k-loop.  Issue order: the first PD W k-steps, then the whole A tile, W refills after.
-    // vmcnt retires in issue order: the first MFMA waits for A[0] (and the epilogue operands) only,
-    // the refill of W[PD] is the first point at which the whole A tile must have landed.
-    bf16x8 rw[PD][NCT], ra[KB];
-#pragma unroll
-    for (int i = 0; i < PD; ++i)
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) rw[i][ct] = bld16(rW, wl, (ct * KB + i) * 1024u);
-    {
-      long r = row0 + l31;
-      if (r >= a.M) r = a.M - 1;
-      const bf16* ap = a.A + r * a.lda + 8 * hh;
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) ra[kb] = *(const bf16x8*)(ap + 16 * kb);
-    }
+  // one tile: k-loop on the landed A rows, prefetch of the next tile (A, epilogue operands) under the
+  // partial-sum exchange and the epilogue
+  auto run_tile = [&](long t, E& cur, E& nxt) {
+    const long row0 = t * RT;
     f32x16 acc[NCT];
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[ct][r] = 0.f;
+    bf16x8 rs_[NSTR > 0 ? NSTR : 1][NCT];
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      const int s = kb % PD;
-      bf16x8 fw[NCT];
+    for (int i = 0; i < NSTR; ++i)
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) fw[ct] = rw[s][ct];
-      if (kb + PD < KB) {
+      for (int ct = 0; ct < NCT; ++ct) rs_[i][ct] = bld16(rW, wl, (ct * KB + ks * KBW + HOLD + i) * 1024u);
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) rw[s][ct] = bld16(rW, wl, (ct * KB + kb + PD) * 1024u);
-      }
+    for (int i = 0; i < HOLD; ++i)
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[kb], fw[ct], acc[ct], 0, 0, 0);
-    }
-
-    // ---- Y -> LDS (lane = column, register = row), then every epilogue reads whole rows
+      for (int ct = 0; ct < NCT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[i], rw[i][ct], acc[ct], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NSTR; ++i)
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[HOLD + i], rs_[i][ct], acc[ct], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
     float4 dv[LPASS][3];
-    if constexpr (EPI == EPI_LN) {   // D of this lane's rows: in flight across the transpose
+    if constexpr (EPI == EPI_LN) {   // D of this lane's rows: in flight across the exchange
 #pragma unroll
       for (int p = 0; p < LPASS; ++p)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) dv[p][k] = bld4(rD, tof[p] + 256u * k);
+        for (int k = 0; k < 3; ++k) dv[p][k] = bld4(rD, cur.tof[p] + 256u * k);
+    }
+    const long tn = t + G;
+    if (tn < a.ntiles) {
+      load_epi(tn, nxt);
+      load_a(tn);
     }
     __syncthreads();   // the previous tile's epilogue has read sY
+    float* pl = sY + ks * PLANE;
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sY[acc_row(r, hh) * LDY + c0 + 32 * ct] = acc[ct][r];
+      for (int r = 0; r < 16; ++r) pl[acc_row(r, hh) * LDY + c0 + 32 * ct] = acc[ct][r];
     __syncthreads();
 
     if constexpr (EPI == EPI_STORE || EPI == EPI_GATE) {
 #pragma unroll
       for (int i = 0; i < CPT; ++i) {
         const int q = tid + NT * i, r = q / NCH, c8 = (q - r * NCH) * 8;
-        const float4 y0 = *(const float4*)(sY + r * LDY + c8), y1 = *(const float4*)(sY + r * LDY + c8 + 4);
-        float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
-        if constexpr (EPI == EPI_GATE) {
-          const bf16x8 g = __builtin_bit_cast(bf16x8, gv[i]);
+        if (q >= NCHUNK) break;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] *= (float)g[j];
+        for (int g = 0; g < KS; ++g) {
+          const float4 y0 = *(const float4*)(sY + g * PLANE + r * LDY + c8);
+          const float4 y1 = *(const float4*)(sY + g * PLANE + r * LDY + c8 + 4);
+          v[0] += y0.x; v[1] += y0.y; v[2] += y0.z; v[3] += y0.w;
+          v[4] += y1.x; v[5] += y1.y; v[6] += y1.z; v[7] += y1.w;
+        }
+        if constexpr (EPI == EPI_GATE) {
+          const bf16x8 gg = __builtin_bit_cast(bf16x8, cur.gv[i]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] *= (float)gg[j];
         }
         bf16x8 o;
 #pragma unroll
@@ -225,62 +256,89 @@ __global__ __launch_bounds__(64 * NWC, 2) void rowgemm_kernel(const RgArgs a) {
     } else {
       // LayerNorm backward (ln_bwd_kernel maths, layernorm.hip), one row per 16 lanes: with
       // xh = (x - mu) rstd, gy = dy gamma:  dx = rstd (gy - mean_c(gy) - xh mean_c(gy xh)),
-      // dgamma += dy xh, dbeta += dy (rows past M contribute 0: their dy is read as 0 below)
+      // dgamma += dy xh, dbeta += dy (rows past M contribute 0: their dy is read as 0 below).
+      // dy and xh are formed twice (row sums, then the outputs) instead of being held in registers.
 #pragma unroll
       for (int p = 0; p < LPASS; ++p) {
-        const int tr = (NT / 16) * p + lr;
+        const int tr = RPP * p + lr;
         const float live = row0 + tr < a.M ? 1.f : 0.f;
-        float dy[3][4], xh[3][4];
-        float s1 = 0.f, s2 = 0.f;
+        auto dyxh = [&](int k, float* dy, float* xh) {
+          float4 d4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float4 d4 = *(const float4*)(sY + tr * LDY + 4 * jl + 64 * k);
-          const float da[4] = {d4.x, d4.y, d4.z, d4.w}, xa[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
-          const float ga[4] = {gam4[k].x, gam4[k].y, gam4[k].z, gam4[k].w};
+          for (int g = 0; g < KS; ++g) {
+            const float4 y = *(const float4*)(sY + g * PLANE + tr * LDY + 4 * jl + 64 * k);
+            d4.x += y.x; d4.y += y.y; d4.z += y.z; d4.w += y.w;
+          }
+          const float da[4] = {d4.x, d4.y, d4.z, d4.w};
+          const float xa[4] = {cur.xv[p][k].x, cur.xv[p][k].y, cur.xv[p][k].z, cur.xv[p][k].w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const bool in = 4 * jl + 64 * k + j < a.C;
-            dy[k][j] = live * da[j];   // 0 past C: the packed weight rows are 0 there
-            xh[k][j] = in ? (xa[j] - mu[p]) * rs[p] : 0.f;
-            const float gy = dy[k][j] * ga[j];
-            s1 += gy;
-            s2 += gy * xh[k][j];
+            dy[j] = live * da[j];   // 0 past C: the packed weight rows are 0 there
+            xh[j] = in ? (xa[j] - cur.mu[p]) * cur.rs[p] : 0.f;
           }
-          pg[k].x += dy[k][0] * xh[k][0]; pg[k].y += dy[k][1] * xh[k][1];
-          pg[k].z += dy[k][2] * xh[k][2]; pg[k].w += dy[k][3] * xh[k][3];
-          pb[k].x += dy[k][0]; pb[k].y += dy[k][1]; pb[k].z += dy[k][2]; pb[k].w += dy[k][3];
+        };
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          float dy[4], xh[4];
+          dyxh(k, dy, xh);
+          const float4 g4k = *(const float4*)(sGam + 4 * jl + 64 * k);
+          const float ga[4] = {g4k.x, g4k.y, g4k.z, g4k.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float gy = dy[j] * ga[j];
+            s1 += gy;
+            s2 += gy * xh[j];
+          }
         }
         s1 = dpp_sum16(s1) * a.inv_c;
         s2 = dpp_sum16(s2) * a.inv_c;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          const float ga[4] = {gam4[k].x, gam4[k].y, gam4[k].z, gam4[k].w};
+          float dy[4], xh[4];
+          dyxh(k, dy, xh);
+          const float4 g4k = *(const float4*)(sGam + 4 * jl + 64 * k);
+          const float ga[4] = {g4k.x, g4k.y, g4k.z, g4k.w};
           const float cu[4] = {dv[p][k].x, dv[p][k].y, dv[p][k].z, dv[p][k].w};
           float o[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j)   // columns past C keep their value
-            o[j] = 4 * jl + 64 * k + j < a.C ? cu[j] + rs[p] * (dy[k][j] * ga[j] - s1 - xh[k][j] * s2) : cu[j];
-          bst4(rD, tof[p] + 256u * k, make_float4(o[0], o[1], o[2], o[3]));
-          const bf16x4 cb = {(bf16)(sc[p] * o[0]), (bf16)(sc[p] * o[1]), (bf16)(sc[p] * o[2]), (bf16)(sc[p] * o[3])};
-          bst8(rC, cof[p] + 128u * k, cb);
+            o[j] = 4 * jl + 64 * k + j < a.C ? cu[j] + cur.rs[p] * (dy[j] * ga[j] - s1 - xh[j] * s2) : cu[j];
+          bst4(rD, cur.tof[p] + 256u * k, make_float4(o[0], o[1], o[2], o[3]));
+          const float sc = cur.sc[p];
+          const bf16x4 cb = {(bf16)(sc * o[0]), (bf16)(sc * o[1]), (bf16)(sc * o[2]), (bf16)(sc * o[3])};
+          bst8(rC, cur.cof[p] + 128u * k, cb);
+          float4* sg = (float4*)(sP + lr * 2 * 192 + 4 * jl + 64 * k);
+          float4* sb = (float4*)(sP + lr * 2 * 192 + 192 + 4 * jl + 64 * k);
+          float4 g4 = *sg, b4 = *sb;
+          g4.x += dy[0] * xh[0]; g4.y += dy[1] * xh[1]; g4.z += dy[2] * xh[2]; g4.w += dy[3] * xh[3];
+          b4.x += dy[0]; b4.y += dy[1]; b4.z += dy[2]; b4.w += dy[3];
+          *sg = g4;
+          *sb = b4;
         }
       }
     }
+  };
+
+  E e0, e1;
+  load_epi(tile, e0);
+  load_a(tile);
+  for (;;) {   // unrolled by two so the double-buffered operands stay in fixed registers
+    run_tile(tile, e0, e1);
+    tile += G;
+    if (tile >= a.ntiles) break;
+    run_tile(tile, e1, e0);
+    tile += G;
+    if (tile >= a.ntiles) break;
   }
 
-  if constexpr (EPI == EPI_LN) {   // this workgroup's dgamma / dbeta partials: the 8 row groups summed
-    __syncthreads();               // in fixed order (deterministic) through sY
-    constexpr int NG = NT / 16;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      *(float4*)(sY + lr * 2 * 192 + 4 * jl + 64 * k) = pg[k];
-      *(float4*)(sY + lr * 2 * 192 + 192 + 4 * jl + 64 * k) = pb[k];
-    }
-    __syncthreads();
+  if constexpr (EPI == EPI_LN) {   // this workgroup's dgamma / dbeta partials: the row groups' LDS slots
+    __syncthreads();               // summed in fixed order (deterministic)
     for (int c = tid; c < 2 * 192; c += NT) {
       float t = 0.f;
 #pragma unroll
-      for (int g = 0; g < NG; ++g) t += sY[g * 2 * 192 + c];
+      for (int g = 0; g < RPP; ++g) t += sP[g * 2 * 192 + c];
       const int w = c / 192, cc = c - w * 192;
       if (cc < a.C) a.part[(long)blockIdx.x * 2 * a.C + w * a.C + cc] = t;
     }
@@ -298,32 +356,37 @@ int rg_cus() {
   return g_rg_cus;
 }
 
-// persistent grid: as many workgroups as the CUs hold at the kernel's occupancy (registers), at most
-// one per tile
-template <int KB, int PD, int NWC, int EPI>
+// persistent grid: one workgroup per CU (the K-split planes take ~100 KB of LDS), at most one per tile
+template <int KB, int KS, int NWC, int EPI, int HOLD = KB / KS>
 int rg_launch(const RgArgs& a, hipStream_t s, long* grid_out) {
-  auto kern = rowgemm_kernel<KB, PD, NWC, EPI>;
+  auto kern = rowgemm_kernel<KB, KS, NWC, EPI, HOLD>;
   static int per_cu = 0;   // workgroups per CU at this instantiation's occupancy (one cache each)
   if (per_cu == 0) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 64 * NWC, 0) != hipSuccess || n <= 0) n = 4 / NWC;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 64 * NWC * KS, 0) != hipSuccess || n <= 0) n = 1;
     per_cu = n;
   }
   const long tiles = (a.M + RT - 1) / RT, slots = (long)rg_cus() * per_cu;
   const long grid = tiles < slots ? tiles : slots;
   if (grid_out) { *grid_out = grid; return 0; }
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NWC), 0, s, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NWC * KS), 0, s, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
 
-// grid_out != NULL: report the grid (the LN partial count) without launching
-template <int EPI, int NWC>
-int rg_dispatch(int K, const RgArgs& a, hipStream_t s, long* grid_out = nullptr) {
+// grid_out != NULL: report the grid (the LN partial count) without launching.  N = 192: K in
+// {192, 384, 576}; N = 384 (the fc2 input gradient): K = 192.
+template <int EPI>
+int rg_dispatch(int K, int N, const RgArgs& a, hipStream_t s, long* grid_out = nullptr) {
+  if (N == 384) {
+    if constexpr (EPI != EPI_LN)
+      if (K == 192) return rg_launch<12, 2, 4, EPI>(a, s, grid_out);
+    return kair_set_error(KAIR_ERR_ARG, "rowgemm: N = 384 needs K = 192 (got %d)", K);
+  }
   switch (K) {
-    case 192: return rg_launch<12, 4, NWC, EPI>(a, s, grid_out);
-    case 384: return rg_launch<24, 4, NWC, EPI>(a, s, grid_out);
-    case 576: return rg_launch<36, 2, NWC, EPI>(a, s, grid_out);
+    case 192: return rg_launch<12, 4, 2, EPI>(a, s, grid_out);
+    case 384: return rg_launch<24, 4, 2, EPI, EPI == EPI_LN ? 5 : 6>(a, s, grid_out);
+    case 576: return rg_launch<36, 4, 2, EPI, EPI == EPI_LN ? 4 : EPI == EPI_GATE ? 7 : 9>(a, s, grid_out);
     default: return kair_set_error(KAIR_ERR_ARG, "rowgemm: K must be 192, 384 or 576 (got %d)", K);
   }
 }
@@ -351,7 +414,7 @@ extern "C" long kair_rowgemm_ln_blocks(long M, int K) {
   memset(&a, 0, sizeof(a));
   a.M = M;
   long g = 0;
-  if (rg_dispatch<EPI_LN, 2>(K, a, nullptr, &g) != 0) return -1;
+  if (rg_dispatch<EPI_LN>(K, 192, a, nullptr, &g) != 0) return -1;
   return g;
 }
 
@@ -362,7 +425,7 @@ extern "C" int kair_rowgemm_store(const void* A, long lda, long M, int K, const 
   KAIR_CHECK_ARG(out && ldo >= N, "rowgemm_store: out");
   a.out = (bf16*)out; a.ldo = ldo;
   hipStream_t s = (hipStream_t)stream;
-  return N == 192 ? rg_dispatch<EPI_STORE, 2>(K, a, s) : rg_dispatch<EPI_STORE, 4>(K, a, s);
+  return rg_dispatch<EPI_STORE>(K, N, a, s);
 }
 
 extern "C" int kair_rowgemm_gate(const void* A, long lda, long M, int K, const void* W, int N, const void* gate, long ldg,
@@ -372,7 +435,7 @@ extern "C" int kair_rowgemm_gate(const void* A, long lda, long M, int K, const v
   KAIR_CHECK_ARG(out && ldo >= N && gate && ldg >= N, "rowgemm_gate: out / gate");
   a.out = (bf16*)out; a.ldo = ldo; a.gate = (const bf16*)gate; a.ldg = ldg;
   hipStream_t s = (hipStream_t)stream;
-  return N == 192 ? rg_dispatch<EPI_GATE, 2>(K, a, s) : rg_dispatch<EPI_GATE, 4>(K, a, s);
+  return rg_dispatch<EPI_GATE>(K, N, a, s);
 }
 
 extern "C" int kair_rowgemm_lnbwd(const void* A, long lda, long M, int K, const void* W, const float* x, long ldx,
@@ -402,5 +465,5 @@ extern "C" int kair_rowgemm_lnbwd(const void* A, long lda, long M, int K, const 
     a.cp_rps = copy->rows_per_scale > 0 ? copy->rows_per_scale : 1;
     a.cwm = make_winmap(copy->win_H, copy->win_W, copy->win_ws, copy->win_shift);
   }
-  return rg_dispatch<EPI_LN, 2>(K, a, (hipStream_t)stream);
+  return rg_dispatch<EPI_LN>(K, 192, a, (hipStream_t)stream);
 }

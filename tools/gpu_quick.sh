@@ -18,7 +18,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/
   python3 $R/bench.py --steps 8 --warmup 3 $Q --no-roles > $R/gpurun_out/tr32.log 2>&1 || { echo "profile failed"; exit 1; }
 cd $R
 python3 tools/step_breakdown.py gpurun_out/tr32/run_kernel_trace.csv 6 > gpurun_out/b32_breakdown.txt
-for k in "rowgemm_kernel<12, 4, 4, 1>" "attn_bwd_bf16"; do
+for k in "rowgemm_kernel<12, 2, 4, 1" "attn_bwd_bf16"; do
   python3 tools/overlap.py gpurun_out/tr32/run_kernel_trace.csv "$k" 6 > gpurun_out/ovl_$(echo $k | cut -c1-8).txt
 done
 rm -f gpurun_out/tr32/run_kernel_trace.csv
