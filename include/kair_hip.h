@@ -152,7 +152,10 @@ typedef struct {
                         12 kind 10 with hi/lo halves (bf16 only): [Np/32][Kp/16][2][64][8], the hi
                           block of (nb, kb) followed by its lo block;
                         13 kind 10 of the TRANSPOSED weight: [Kp/32][Np/16][64][8], lane l: W[n][k]
-                          with k = 32kb' + l%32 (output), n = 16kb + 8(l/32) + j (contraction) */
+                          with k = 32kb' + l%32 (output), n = 16kb + 8(l/32) + j (contraction);
+                        14 linear in v_mfma_f32_16x16x32 fragment order [Np/16][Kp/32][64][8]: the
+                          operand of rows 16nb.. and k-step kb is one contiguous 1 KiB block (lane l:
+                          row 16nb + l%16, k 32kb + 8(l/16) + j) */
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
   int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp                   */
@@ -301,10 +304,11 @@ int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, const float
                        int w_split, void* stream);
 /* Fused MLP half of a Swin block (bf16; Cp = 192, hidden padded to Hp = 384):
  *   out = x + rowscale * fc2(GELU(fc1(LN2(x))))     network_swinir.py:274-276, Mlp.forward :24-30
- * in one launch over 64-row tiles of token rows.  Saved for the unchanged backward as
- * kair_layernorm_fwd / kair_gemm_nt (pre_kind 1) store them: ln (1.0 at column C), mean / rstd,
- * u = GELU'(x) of the fc1 pre-activation x and h = GELU(x) (1.0 at column hd), both [M][ldh].  w1 [Hp][Cp] and w2 [Cp][Hp]
- * in MFMA-fragment order (kind 10, or kind 12 when w_split); b1 [Hp], b2 [Cp] padded. */
+ * in one launch over row tiles of token rows (M a multiple of 32).  Saved for the unchanged backward
+ * as kair_layernorm_fwd / kair_gemm_nt (pre_kind 1) store them: ln (1.0 at column C), mean / rstd,
+ * u = GELU'(x) of the fc1 pre-activation x and h = GELU(x) (1.0 at column hd), both [M][ldh].
+ * w1 [Hp][Cp] in MFMA-fragment order (kind 10) and w2 [Cp][Hp] in 16x16x32 fragment order (kind 14);
+ * w_split: both in kind 12 (hi/lo pairs, M a multiple of 64).  b1 [Hp], b2 [Cp] padded. */
 int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, const float* beta, float eps, int C,
                       void* ln, long ldln, float* mean, float* rstd, const void* w1, const float* b1, void* u,
                       void* h, long ldh, int hd, const void* w2, const float* b2, const float* rowscale,

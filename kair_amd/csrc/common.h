@@ -73,6 +73,34 @@ KAIR_DEV float dpp_sum16(float v) {
   return v;
 }
 
+// Buffer-resource global access: a wave-uniform descriptor (SGPRs) + a 32-bit per-lane byte offset +
+// a wave-uniform byte offset, so a persistent kernel keeps one VGPR per access stream instead of a
+// 64-bit address; accesses past the resource's size are dropped (loads return 0).
+typedef __amdgpu_buffer_rsrc_t BufRsrc;
+KAIR_DEV BufRsrc buf_rsrc(const void* p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes),
+                                           0x00020000);
+}
+typedef __attribute__((ext_vector_type(4))) unsigned buf_u32x4;
+KAIR_DEV float4 buf_ld4(BufRsrc r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+}
+// Stores fold the uniform offset into the lane offset and pass soffset = 0: ROCm 7.2's hazard
+// recognizer treats a > 8-byte buffer store with an SGPR soffset as free of the "store data VGPRs
+// overwritten by the next VALU instruction" hazard and inserts no wait state, but gfx950 has it --
+// measured: the first data dword of some lanes of buffer_store_dwordx4 replaced by the value a
+// following v_and_b32 wrote into that VGPR (tests/test_mlp_fused_gpu.py).  With soffset 0 the
+// recognizer pads the store.
+KAIR_DEV void buf_st4(BufRsrc r, unsigned voff, unsigned soff, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(buf_u32x4, v), r, (int)(voff + soff), 0, 0);
+}
+KAIR_DEV void buf_st16(BufRsrc r, unsigned voff, unsigned soff, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(buf_u32x4, v), r, (int)(voff + soff), 0, 0);
+}
+KAIR_DEV void buf_st1(BufRsrc r, unsigned voff, unsigned soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(voff + soff), 0, 0);
+}
+
 KAIR_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 KAIR_DEV float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));

@@ -83,6 +83,14 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const int kp = ob * 32 + (ln & 31), np = kb * 16 + 8 * (ln >> 5) + j;
     const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
     if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
+  } else if (mp.kind == 14) {  // linear in v_mfma_f32_16x16x32 fragment order: [Np/16][Kp/32][64 lanes][8]
+    const int KB = Kp / 32;
+    const int j = (int)(t & 7), ln = (int)((t >> 3) & 63);
+    const long blk = t >> 9;
+    const int kb = (int)(blk % KB), nb = (int)(blk / KB);
+    const int np = nb * 16 + (ln & 15), kp = kb * 32 + 8 * (ln >> 4) + j;
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && k >= 0) v = src[(long)n * mp.K + k];
   } else if (mp.kind == 12) {  // linear, fragment order with hi/lo halves: [Np/32][Kp/16][2][64 lanes][8]
     const int KB = Kp / 16;
     const int j = (int)(t & 7), ln = (int)((t >> 3) & 63), half = (int)((t >> 9) & 1);
@@ -512,7 +520,8 @@ static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
   KAIR_CHECK_ARG((mp.kind != 10 && mp.kind != 12) || (Np % 32 == 0 && Kp % 16 == 0),
                  "pack_weight: fragment order needs Np %% 32 == 0, Kp %% 16 == 0");
   KAIR_CHECK_ARG(mp.kind != 13 || (Kp % 32 == 0 && Np % 16 == 0), "pack_weight: transposed fragment order needs Kp %% 32 == 0, Np %% 16 == 0");
-  if (mp.kind == 0 || mp.kind == 3 || mp.kind == 10 || mp.kind == 13) *total = Np * Kp;
+  KAIR_CHECK_ARG(mp.kind != 14 || (Np % 16 == 0 && Kp % 32 == 0), "pack_weight: 16x16x32 fragment order needs Np %% 16 == 0, Kp %% 32 == 0");
+  if (mp.kind == 0 || mp.kind == 3 || mp.kind == 10 || mp.kind == 13 || mp.kind == 14) *total = Np * Kp;
   else if (mp.kind == 12) *total = 2 * Np * Kp;
   else if (mp.kind == 1 || mp.kind == 2) *total = Np * 9 * Kp;
   else if (mp.kind == 7 || mp.kind == 8) *total = Np * 4 * Kp;

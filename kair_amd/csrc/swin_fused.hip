@@ -699,6 +699,252 @@ __global__ __launch_bounds__(1024) void swin_mlp_fwd_kernel(const MlpFwdArgs a) 
 }
 
 
+// ---- MLP half, weights resident in registers (the default, S = 1) --------------------------------
+// Same maths and saved tensors as swin_mlp_fwd_kernel, re-laid out for short dependent chains:
+// one 12-wave workgroup per CU loads BOTH weight matrices once into registers (wave w: W1 rows
+// [32w, 32w+32) -- kind 10, 12 fragments -- and W2 rows [16w, 16w+16) -- kind 14, 12 fragments;
+// 96 VGPRs) and then loops over 32-row tiles.  A tile's chain is LN2 -> fc1 (12 MFMAs per wave,
+// LN rows from LDS) -> GELU pair -> fc2 (24 v_mfma_f32_16x16x32 per wave, h from LDS) -> residual,
+// with no weight traffic at all: the streamed-fragment waits that bounded the 64-row kernel (three
+// L2 / HBM round trips per GEMM phase, a whole tile per CU in flight) are gone, and 32-row tiles
+// give the B = 4 step (M = 9216) 288 tiles for the 256 CUs instead of 144.  The next tile's x rows
+// are issued before this tile's stores (vmcnt retires in issue order); every store reads LDS and
+// writes whole 16-byte row chunks; the output rows of tile t are stored during tile t + G's fc1
+// (sX double-buffered).
+__global__ __launch_bounds__(768, 1) void swin_mlp_fwd_wr_kernel(const MlpFwdArgs a) {
+  constexpr int NW = 12, NT = 64 * NW, RT = 32, CP = 192, HP = 384;
+  constexpr int LDT = CP + 8, LDH = HP + 8, LDX = CP + 4;
+  constexpr int KB1 = CP / 16, KB2 = HP / 32;   // 12 k-steps each
+  typedef __attribute__((address_space(3))) float lds_f;
+  __shared__ __attribute__((aligned(16))) bf16 sT[RT * LDT];        // LN2 rows (bf16, 1.0 at column C)
+  __shared__ __attribute__((aligned(16))) bf16 sH[RT * LDH];        // h = GELU(u)
+  __shared__ __attribute__((aligned(16))) bf16 sG[RT * LDH];        // g = GELU'(u)
+  __shared__ __attribute__((aligned(16))) float sX[2][RT * LDX];    // x rows, then the output rows
+  __shared__ __attribute__((aligned(16))) float sC[HP + 3 * CP];    // b1 | b2 | gamma | beta (0 past C)
+  __shared__ float sMean[RT], sRstd[RT];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l31 = lane & 31, hh = lane >> 5, l15 = lane & 15, q4 = lane >> 4;
+  const long G = gridDim.x;
+  long tile = blockIdx.x;
+  if (tile >= a.nTiles) return;
+
+  // resident weights: W1 fragments (nb = w, kb) of kind 10 and W2 fragments (nb = w, kb) of kind 14
+  bf16x8 w1r[KB1], w2r[KB2];
+#pragma unroll
+  for (int kb = 0; kb < KB1; ++kb) w1r[kb] = *(const bf16x8*)(a.w1 + ((long)(w * KB1 + kb) * 64 + lane) * 8);
+#pragma unroll
+  for (int kb = 0; kb < KB2; ++kb) w2r[kb] = *(const bf16x8*)(a.w2 + ((long)(w * KB2 + kb) * 64 + lane) * 8);
+  for (int i = tid; i < HP; i += NT) sC[i] = a.b1[i];
+  for (int i = tid; i < CP; i += NT) {
+    sC[HP + i] = a.b2[i];
+    sC[HP + CP + i] = i < a.C ? a.gamma[i] : 0.f;
+    sC[HP + 2 * CP + i] = i < a.C ? a.beta[i] : 0.f;
+  }
+  const long M = a.nTiles * RT;
+  const BufRsrc rx = buf_rsrc(a.x, M * a.ldx * 4), rln = buf_rsrc(a.ln, M * a.ldln * 2);
+  const BufRsrc rmu = buf_rsrc(a.mean, M * 4), rrs = buf_rsrc(a.rstd, M * 4);
+  const BufRsrc ru = buf_rsrc(a.u, M * a.ldh * 2), rh = buf_rsrc(a.hact, M * a.ldh * 2);
+  const BufRsrc ro = buf_rsrc(a.out, M * a.ldout * 4);
+  // LN layout: threads 0..511, row lr = tid / 16, lane jl: columns 4 jl + 64 k (k < 3)
+  auto load_x = [&](long t, float4 (&xv)[3], int ti) {
+    const int lr = (ti >> 4) & (RT - 1), jl = ti & 15;
+    const unsigned xoff = ((unsigned)lr * (unsigned)a.ldx + 4u * jl) * 4u;
+    if (ti < 16 * RT && t < a.nTiles) {
+      const unsigned so = (unsigned)(t * RT * a.ldx * 4);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) xv[k] = buf_ld4(rx, xoff + 256u * k, so);
+    }
+  };
+  const float inv_c = 1.0f / (float)a.C;
+  // output rows of tile t from sX[b] (fp32, 16-byte chunks, 2 per thread)
+  auto store_out = [&](long t, int b, int ti) {
+    constexpr int C4 = CP / 4;
+    const unsigned so = (unsigned)(t * RT * a.ldout * 4);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = ti + NT * j, r = i / C4, c = (i - r * C4) * 4;
+      buf_st4(ro, ((unsigned)r * (unsigned)a.ldout + c) * 4u, so, *(const float4*)(&sX[b][r * LDX + c]));
+    }
+  };
+
+  auto run_tile = [&](long t, int b, float4 (&xv)[3], float4 (&xn)[3], long prev) {
+    const long row0 = t * RT;
+    // Registers belong to the resident weights: the LDS constants, the lane-derived addresses and the
+    // column masks are recomputed per tile instead of being hoisted out of the tile loop (opaque copies
+    // of their inputs; the recomputation is a few VALU ops per tile)
+    const lds_f* cst = (const lds_f*)sC;
+    int ti = tid, C = a.C, hd = a.hd;
+    asm volatile("" : "+v"(cst), "+v"(ti), "+s"(C), "+s"(hd));
+    const int lane = ti & 63, l31 = lane & 31, hh = lane >> 5, l15 = lane & 15, q4 = lane >> 4;
+    const int lr = (ti >> 4) & (RT - 1), jl = ti & 15;
+    load_x(t + G, xn, ti);   // the next tile's rows, ahead of every store of this one
+    // ---- LN2 of this tile's rows -> sT (bf16), sX[b] (fp32 x), statistics
+    if (ti < 16 * RT) {   // LN layout: threads 0..511, row lr, lane jl: columns 4 jl + 64 k (k < 3)
+      float sm = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * jl + 64 * k;
+        sm += (cb + 0 < C ? xv[k].x : 0.f) + (cb + 1 < C ? xv[k].y : 0.f) + (cb + 2 < C ? xv[k].z : 0.f) +
+              (cb + 3 < C ? xv[k].w : 0.f);
+      }
+      const float mu = dpp_sum16(sm) * inv_c;
+      float qv = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * jl + 64 * k;
+        const float vv[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = cb + j < C ? vv[j] - mu : 0.f;
+          qv += d * d;
+        }
+      }
+      const float rs = rsqrtf(dpp_sum16(qv) * inv_c + a.eps);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * jl + 64 * k;
+        const float vv[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cc = cb + j;
+          o[j] = (bf16)(cc < C ? (vv[j] - mu) * rs * cst[HP + CP + cc] + cst[HP + 2 * CP + cc] : (cc == C ? 1.f : 0.f));
+        }
+        *(bf16x4*)(sT + lr * LDT + cb) = o;
+        *(float4*)(&sX[b][lr * LDX + cb]) = xv[k];
+      }
+      if (jl == 0) {
+        sMean[lr] = mu;
+        sRstd[lr] = rs;
+      }
+    }
+    __syncthreads();   // (1) LN tile, x rows, statistics visible
+    // ---- stores: LN2 rows + statistics of this tile (one 16-byte chunk per thread), output rows of the
+    // previous tile
+    {
+      constexpr int CH = CP / 8;
+      const int r = ti / CH, c = (ti - r * CH) * 8;
+      buf_st16(rln, ((unsigned)r * (unsigned)a.ldln + c) * 2u, (unsigned)(row0 * a.ldln * 2),
+               *(const uint4*)(sT + r * LDT + c));
+      if (ti < RT) {
+        buf_st1(rmu, 4u * ti, (unsigned)(row0 * 4), sMean[ti]);
+        buf_st1(rrs, 4u * ti, (unsigned)(row0 * 4), sRstd[ti]);
+      }
+      if (prev >= 0) store_out(prev, b ^ 1, ti);
+    }
+    // ---- fc1: hidden columns [32w, 32w+32), rows 0..31: D = W1 . LN^T (lane = row, registers = columns)
+    {
+      f32x16 U;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) U[r] = 0.f;
+      // LDS operand reads in groups of 4 k-steps (a scheduling barrier between groups keeps them from all
+      // being hoisted: the resident weights leave ~70 VGPRs for everything else)
+#pragma unroll
+      for (int k0 = 0; k0 < KB1; k0 += 4) {
+        bf16x8 fl[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fl[i] = *(const bf16x8*)(sT + l31 * LDT + (k0 + i) * 16 + 8 * hh);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) U = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1r[k0 + i], fl[i], U, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // pre-activation u = acc + b1 (fp32) -> h = GELU(u) -> sH, g = GELU'(u) -> sG; h is 1.0 at
+      // column hd and 0 past it
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int col = 32 * w + 8 * gg + 4 * hh;
+        const float xs[4] = {U[4 * gg] + cst[col], U[4 * gg + 1] + cst[col + 1], U[4 * gg + 2] + cst[col + 2],
+                             U[4 * gg + 3] + cst[col + 3]};
+        bf16x4 hv, gv;
+#if KAIR_MLP_VAR == 1
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int cc = col + e;
+          hv[e] = cc < hd ? (bf16)gelu_fast(xs[e]) : (bf16)(cc == hd ? 1.f : 0.f);
+          gv[e] = (bf16)gelu_grad_fast(xs[e]);
+        }
+#else
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          f32x2 y, dy;
+          gelu_pair_fast2((f32x2){xs[e], xs[e + 1]}, y, dy);
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int cc = col + e + q;
+            hv[e + q] = cc < hd ? (bf16)y[q] : (bf16)(cc == hd ? 1.f : 0.f);
+            gv[e + q] = (bf16)dy[q];
+          }
+        }
+#endif
+        *(bf16x4*)(sH + l31 * LDH + col) = hv;
+        *(bf16x4*)(sG + l31 * LDH + col) = gv;
+#if KAIR_MLP_VAR == 2
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+      }
+    }
+    __syncthreads();   // (2) h, g complete; sT free
+    // ---- stores: g and h rows of this tile (2 x 2 chunks per thread)
+    {
+      constexpr int CH = HP / 8;
+      const unsigned so = (unsigned)(row0 * a.ldh * 2);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = ti + NT * j, r = i / CH, c = (i - r * CH) * 8;
+        const unsigned vo = ((unsigned)r * (unsigned)a.ldh + c) * 2u;
+        buf_st16(ru, vo, so, *(const uint4*)(sG + r * LDH + c));
+        buf_st16(rh, vo, so, *(const uint4*)(sH + r * LDH + c));
+      }
+    }
+    // ---- fc2: output columns [16w, 16w+16) for rows 16 rb + (lane & 15); D = W2 . h^T with
+    // v_mfma_f32_16x16x32 (lane: row 16 rb + lane % 16, registers: columns 16w + 4 (lane / 16) + r)
+    {
+      f32x4 Y[2];
+      Y[0] = Y[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < KB2; k0 += 2) {
+        bf16x8 fh[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) fh[i][rb] = *(const bf16x8*)(sH + (16 * rb + l15) * LDH + (k0 + i) * 32 + 8 * q4);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) Y[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2r[k0 + i], fh[i][rb], Y[rb], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const float rsc = a.rowscale ? a.rowscale[t / a.tiles_per_scale] : 1.f;
+      const int col = 16 * w + 4 * q4;
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        float* px = &sX[b][(16 * rb + l15) * LDX + col];
+        const float4 xr = *(const float4*)px;
+        *(float4*)px = make_float4(xr.x + rsc * (Y[rb][0] + cst[HP + col]), xr.y + rsc * (Y[rb][1] + cst[HP + col + 1]),
+                                   xr.z + rsc * (Y[rb][2] + cst[HP + col + 2]), xr.w + rsc * (Y[rb][3] + cst[HP + col + 3]));
+      }
+    }
+    __syncthreads();   // (3) output rows in sX[b] complete; sH / sG free
+  };
+
+  float4 x0[3], x1[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) x0[k] = x1[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  load_x(tile, x0, tid);
+  __syncthreads();   // sC visible
+  long prev = -1;
+  int b = 0;
+  for (;;) {   // unrolled by two so the double-buffered x rows stay in fixed registers
+    run_tile(tile, b, x0, x1, prev);
+    prev = tile; b ^= 1; tile += G;
+    if (tile >= a.nTiles) break;
+    run_tile(tile, b, x1, x0, prev);
+    prev = tile; b ^= 1; tile += G;
+    if (tile >= a.nTiles) break;
+  }
+  store_out(prev, b ^ 1, tid);
+}
+
 // ---- MLP half, backward ---------------------------------------------------------------------------
 // Given D = dL/dout (fp32) and Dc = s_mlp * D (bf16), one persistent warp-specialised launch makes
 //   dU   = (Dc . W2) * GELU'(u)                       (fc2 input gradient through the stored gate)
@@ -1007,30 +1253,31 @@ extern "C" int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, c
                  "swin_mlp_fwd: null pointer");
   KAIR_CHECK_ARG(Cp == 192 && Hp == 384 && C > 0 && C < Cp && hd > 0 && hd < Hp,
                  "swin_mlp_fwd: laid out for Cp 192 / hidden 384 (C %d, Cp %d, hd %d, Hp %d)", C, Cp, hd, Hp);
-  KAIR_CHECK_ARG(M > 0 && M % TOK == 0, "swin_mlp_fwd: M must be a multiple of 64");
+  KAIR_CHECK_ARG(M > 0 && M % (w_split ? TOK : 32) == 0, "swin_mlp_fwd: M must be a multiple of %d", w_split ? TOK : 32);
   KAIR_CHECK_ARG(ldx >= Cp && ldx % 4 == 0 && ldout >= Cp && ldout % 4 == 0 && ldln >= Cp && ldln % 8 == 0 && ldh >= Hp &&
                      ldh % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)b2 & 15) == 0,
                  "swin_mlp_fwd: strides / alignment");
-  KAIR_CHECK_ARG(!rowscale || (rows_per_scale > 0 && rows_per_scale % TOK == 0), "swin_mlp_fwd: rows_per_scale");
+  KAIR_CHECK_ARG(!rowscale || (rows_per_scale > 0 && rows_per_scale % (w_split ? TOK : 32) == 0), "swin_mlp_fwd: rows_per_scale");
   MlpFwdArgs a;
   a.x = x; a.ldx = ldx; a.gamma = gamma; a.beta = beta; a.eps = eps; a.C = C;
   a.ln = (bf16*)ln; a.ldln = ldln; a.mean = mean; a.rstd = rstd;
   a.w1 = (const bf16*)w1; a.b1 = b1; a.u = (bf16*)u; a.hact = (bf16*)h; a.ldh = ldh; a.hd = hd;
   a.w2 = (const bf16*)w2; a.b2 = b2;
-  a.rowscale = rowscale; a.tiles_per_scale = rowscale ? rows_per_scale / TOK : 1;
+  const int rt = w_split ? TOK : 32;   // rows per tile
+  a.rowscale = rowscale; a.tiles_per_scale = rowscale ? rows_per_scale / rt : 1;
   a.out = out; a.ldout = ldout;
-  a.nTiles = M / TOK;
+  a.nTiles = M / rt;
   static const int dbg = kair_dbg_env("KAIR_MLP_DBG");
   a.dbg = dbg;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       ncu <= 0)
     ncu = 256;
-  const long grid = a.nTiles < ncu ? a.nTiles : ncu;   // persistent: one 16-wave workgroup per CU
+  const long grid = a.nTiles < ncu ? a.nTiles : ncu;   // persistent: one workgroup per CU
   if (w_split)
     hipLaunchKernelGGL(swin_mlp_fwd_kernel<2>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(swin_mlp_fwd_kernel<1>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(swin_mlp_fwd_wr_kernel, dim3((unsigned)grid), dim3(768), 0, (hipStream_t)stream, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

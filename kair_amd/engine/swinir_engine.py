@@ -75,10 +75,12 @@ def swinir_flops(net, Hh, Ww):
 class _Lin:
     """A linear layer's packed forms.  n/k groupings map reference rows/cols to padded ones."""
 
-    def __init__(self, eng, mod, n_grp, k_grp, frag=False, split=False, frag_t=False, rows=True):
+    def __init__(self, eng, mod, n_grp, k_grp, frag=False, split=False, frag_t=False, rows=True, frag16=False):
         """rows: pack the plain [Np][Kp] form (the unfused forward GEMM's operand); frag / frag_t: the
         fragment-order forms of the fused forward / MLP-backward kernels, which replace [Np][Kp] /
-        [Kp][Np].  Forms no kernel of the engine reads are not packed (kair_pack_weights per step)."""
+        [Kp][Np]; frag16: the frag form in 16x16x32 fragment order (pack kind 14, the fused MLP
+        kernel's fc2 operand) unless split.  Forms no kernel of the engine reads are not packed
+        (kair_pack_weights per step)."""
         self.w, self.b = mod.weight, mod.bias
         N, K = self.w.shape[:2]      # nn.Linear [N, K] or a 1x1 nn.Conv2d [N, K, 1, 1]
         self.N, self.K = N, K
@@ -94,7 +96,7 @@ class _Lin:
         # MFMA-fragment order of Wp for the fused block kernels: pack kind 10, or kind 12 (hi/lo
         # bf16 pairs, the same ~16-bit weight precision as the split convs) when split
         self.split = bool(frag and split)
-        self.mapg = H.wmap(12 if self.split else 10, N, K, n_grp, k_grp) if frag else None
+        self.mapg = H.wmap(12 if self.split else (14 if frag16 else 10), N, K, n_grp, k_grp) if frag else None
         self.Wg = (torch.empty((2 if self.split else 1) * self.Np, self.Kp, device=dev, dtype=eng.tdt)
                    if frag else None)
         # transposed fragment order (pack kind 13) for the fused MLP backward
@@ -195,7 +197,8 @@ class _Blk:
         self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=fa, split=sp, rows=not fa, frag_t=rg)
         self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=fa, split=sp, rows=not fa, frag_t=rg)
         self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp), frag=fm, split=sp, frag_t=fb or rg, rows=not fm)
-        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=fm, split=sp, frag_t=fb or rg, rows=not fm)
+        self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=fm, split=sp, frag_t=fb or rg, rows=not fm,
+                        frag16=True)
 
     def linears(self):
         return (self.qkv, self.proj, self.fc1, self.fc2)

@@ -1,0 +1,75 @@
+"""kair_swin_mlp_fwd (csrc/swin_fused.hip, the weight-resident kernel) against a float64 torch
+restatement of the MLP half of a Swin block on the same bf16 operands:
+
+    out = x + s * fc2(GELU(fc1(LN2(x))))      network_swinir.py:274-276, Mlp.forward :24-30
+
+with the tensors it saves for backward (ln2 with 1.0 at column C, mean / rstd, GELU'(u), GELU(u)
+with 1.0 at column hd).  Shapes are the classical x4 block's (C 180 -> 192, hidden 360 -> 384), at
+sizes with one tile per workgroup (M = 1152) and several persistent passes (M = 73,728 / 8)."""
+import pytest
+import torch
+
+from kair_amd import _hip as H
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda", 0)
+C, CP, HD, HDP = 180, 192, 360, 384
+
+
+def _pack(w, kind, n_grp, k_grp):
+    Np, Kp = n_grp[0] * n_grp[2], k_grp[0] * k_grp[2]
+    out = torch.empty(Np, Kp, device=dev, dtype=torch.bfloat16)
+    H.pack_weight(w, out, H.wmap(kind, w.shape[0], w.shape[1], n_grp, k_grp))
+    return out
+
+
+@pytest.mark.parametrize("M,rows_per_scale", [(1152, 576), (9216, 2304), (73728 // 8, 2304)])
+def test_swin_mlp_fwd_vs_float64(M, rows_per_scale):
+    g = torch.Generator().manual_seed(3)
+    x = torch.zeros(M, CP)
+    x[:, :C] = torch.randn(M, C, generator=g) * 1.5 + 0.3
+    gamma, beta = 1 + 0.2 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    w1, b1 = 0.05 * torch.randn(HD, C, generator=g), 0.05 * torch.randn(HD, generator=g)
+    w2, b2 = 0.05 * torch.randn(C, HD, generator=g), 0.05 * torch.randn(C, generator=g)
+    nsc = M // rows_per_scale
+    scale = torch.tensor([1.0, 0.0, 1.25, 0.8] * nsc)[:nsc]
+    W1 = _pack(w1.to(dev), 10, (1, HD, HDP), (1, C, CP))
+    W2 = _pack(w2.to(dev), 14, (1, C, CP), (1, HD, HDP))
+    b1p = torch.zeros(HDP); b1p[:HD] = b1
+    b2p = torch.zeros(CP); b2p[:C] = b2
+    xd = x.to(dev)
+    ln = torch.empty(M, CP, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    u = torch.empty(M, HDP, device=dev, dtype=torch.bfloat16)
+    h = torch.empty(M, HDP, device=dev, dtype=torch.bfloat16)
+    out = torch.full((M, CP), 7.0, device=dev)
+    H.swin_mlp_fwd(xd, CP, gamma.to(dev), beta.to(dev), 1e-5, C, ln, CP, mean, rstd, W1, b1p.to(dev), u, h, HDP, HD, W2,
+                   b2p.to(dev), scale.to(dev), rows_per_scale, out, CP, M, CP, HDP)
+    torch.cuda.synchronize()
+
+    xd64 = x[:, :C].double()
+    mu = xd64.mean(1)
+    rs = 1.0 / torch.sqrt(xd64.var(1, unbiased=False) + 1e-5)
+    assert (mean.cpu().double() - mu).abs().max().item() < 1e-5
+    assert ((rstd.cpu().double() - rs).abs() / rs).max().item() < 1e-5
+    lnr = (xd64 - mu[:, None]) * rs[:, None] * gamma.double() + beta.double()
+    lng = ln.cpu().double()
+    assert (lng[:, :C] - lnr).abs().max().item() < 2e-2 * lnr.abs().max().item()   # bf16 rounding
+    assert (lng[:, C] == 1).all() and (lng[:, C + 1:] == 0).all()
+    # the rest of the chain from the kernel's own bf16 LN output and bf16 weights (products in fp64)
+    w1b = w1.to(torch.bfloat16).double()
+    w2b = w2.to(torch.bfloat16).double()
+    uu = lng[:, :C] @ w1b.t() + b1.double()
+    cdf = 0.5 * (1 + torch.erf(uu / 2 ** 0.5))
+    hr = uu * cdf
+    gr = cdf + uu * torch.exp(-0.5 * uu * uu) / (2 * torch.pi) ** 0.5
+    hg, ug = h.cpu().double(), u.cpu().double()
+    assert (hg[:, :HD] - hr).abs().max().item() < 1e-2 * hr.abs().max().item() + 1e-3
+    assert (ug[:, :HD] - gr).abs().max().item() < 1e-2
+    assert (hg[:, HD] == 1).all() and (hg[:, HD + 1:] == 0).all()
+    y = hg[:, :HD] @ w2b.t() + b2.double()
+    s = scale.double().repeat_interleave(rows_per_scale)[:, None]
+    ref = x.double().clone()
+    ref[:, :C] += s * y
+    err = (out.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-4, err
