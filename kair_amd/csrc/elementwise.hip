@@ -120,8 +120,53 @@ __global__ void pack_kernel(const float* __restrict__ src, void* __restrict__ ds
   if (t < total) pack_element(src, dst, dt, mp, t);
 }
 
+// Chunked packing of the bf16 linear forms (kinds 0, 10, 13, 14): one thread makes 8 consecutive
+// packed elements (one 16-byte store) and the threads of a wave walk the SOURCE in row order, so the
+// fp32 master rows are read once and coalesced (the per-element gather re-fetched each source line
+// from a different packed position: ~3-4x the bytes).  A chunk never straddles a padded group
+// (group widths are multiples of 8), so its 8 elements are 8 consecutive packed indices.
+__host__ __device__ inline bool pack_vec(const kair_wmap& mp, int dt) {
+  if (dt != KAIR_BF16) return false;
+  if (mp.kind == 0 || mp.kind == 10 || mp.kind == 14) return mp.kGp % 8 == 0 && (mp.kG * mp.kGp) % 8 == 0;
+  if (mp.kind == 13) return mp.nGp % 8 == 0 && (mp.nG * mp.nGp) % 8 == 0;
+  return false;
+}
+
+KAIR_DEV void pack_chunk(const float* __restrict__ src, bf16* __restrict__ dst, const kair_wmap& mp, long u) {
+  const int Np = mp.nG * mp.nGp, Kp = mp.kG * mp.kGp;
+  float v[8];
+  long t0;
+  if (mp.kind == 13) {   // 8 consecutive contraction rows np0.. of one output column kp
+    const int kp = (int)(u % Kp), np0 = (int)(u / Kp) * 8;
+    const int k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = nperm_fwd(mp, unpad(np0 + j, mp.nG, mp.nGr, mp.nGp));
+      v[j] = (n >= 0 && k >= 0) ? src[(long)n * mp.K + k] : 0.f;
+    }
+    t0 = (((long)(kp >> 5) * (Np / 16) + (np0 >> 4)) * 64 + (kp & 31) + 32 * ((np0 & 15) >> 3)) * 8;
+  } else {               // 8 consecutive columns kp0.. of one row np
+    const int kc = Kp / 8;
+    const int np = (int)(u / kc), kp0 = (int)(u % kc) * 8;
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = unpad(kp0 + j, mp.kG, mp.kGr, mp.kGp);
+      v[j] = (n >= 0 && k >= 0) ? src[(long)n * mp.K + k] : 0.f;
+    }
+    if (mp.kind == 0) t0 = (long)np * Kp + kp0;
+    else if (mp.kind == 10) t0 = (((long)(np >> 5) * (Kp / 16) + (kp0 >> 4)) * 64 + (np & 31) + 32 * ((kp0 & 15) >> 3)) * 8;
+    else t0 = (((long)(np >> 4) * (Kp / 32) + (kp0 >> 5)) * 64 + (np & 15) + 16 * ((kp0 & 31) >> 3)) * 8;
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+  *(bf16x8*)(dst + t0) = o;
+}
+
 // All packs of a network in one launch: table = kair_pack_job[njobs] followed by the first block
 // of every job (long[njobs + 1]); each block finds its job by binary search (uniform, scalar loads).
+// A chunked job (pack_vec) has total / 8 work items, any other job one per packed element.
 __global__ __launch_bounds__(256) void pack_batched_kernel(const kair_pack_job* __restrict__ jobs, int njobs,
                                                            const long* __restrict__ first) {
   const long bid = blockIdx.x;
@@ -133,7 +178,11 @@ __global__ __launch_bounds__(256) void pack_batched_kernel(const kair_pack_job* 
   }
   const kair_pack_job& j = jobs[lo];
   const long t = (bid - first[lo]) * 256 + threadIdx.x;
-  if (t < j.total) pack_element(j.src, j.dst, j.dst_dtype, j.map, t);
+  if (pack_vec(j.map, j.dst_dtype)) {
+    if (t < j.total / 8) pack_chunk(j.src, (bf16*)j.dst, j.map, t);
+  } else if (t < j.total) {
+    pack_element(j.src, j.dst, j.dst_dtype, j.map, t);
+  }
 }
 
 // 64 reference weight elements (+ bias elements) per 1024-thread block; 16 split phases per
@@ -559,7 +608,8 @@ extern "C" long kair_pack_table_build(kair_pack_job* jobs, int njobs, void* tabl
     if (rc) { free(host); return rc; }
     jobs[i].total = total;
     first[i] = nb;
-    nb += (total + 255) / 256;
+    const long items = pack_vec(jobs[i].map, jobs[i].dst_dtype) ? total / 8 : total;
+    nb += (items + 255) / 256;
   }
   first[njobs] = nb;
   memcpy(host, jobs, jb);

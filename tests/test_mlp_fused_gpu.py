@@ -73,3 +73,31 @@ def test_swin_mlp_fwd_vs_float64(M, rows_per_scale):
     ref[:, :C] += s * y
     err = (out.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("N,K,n_grp,k_grp", [
+    (540, 180, (18, 30, 32), (1, 180, 192)),   # qkv: head-padded rows
+    (180, 180, (1, 180, 192), (6, 30, 32)),    # proj: head-padded contraction
+    (360, 180, (1, 360, 384), (1, 180, 192)),  # fc1
+    (180, 360, (1, 180, 192), (1, 360, 384)),  # fc2
+])
+def test_batched_pack_matches_elementwise(N, K, n_grp, k_grp):
+    """kair_pack_weights (one launch; the bf16 linear forms 0 / 10 / 13 / 14 packed 8 elements per
+    thread in source-row order) == kair_pack_weight (one thread per packed element), bit for bit."""
+    g = torch.Generator().manual_seed(N + K)
+    w = torch.randn(N, K, generator=g).to(dev)
+    Np, Kp = n_grp[0] * n_grp[2], k_grp[0] * k_grp[2]
+    jobs, refs = [], []
+    for kind in (0, 3, 10, 13, 14):
+        m = H.wmap(kind, N, K, n_grp, k_grp)
+        shape = (Kp, Np) if kind in (3, 13) else (Np, Kp)
+        ref = torch.empty(shape, device=dev, dtype=torch.bfloat16)
+        H.pack_weight(w, ref, m)
+        dst = torch.full(shape, 3.0, device=dev, dtype=torch.bfloat16)
+        jobs.append((w, dst, m))
+        refs.append(ref)
+    t = H.PackTable(jobs)
+    t.run()
+    torch.cuda.synchronize()
+    for (_, dst, m), ref in zip(jobs, refs):
+        assert torch.equal(dst, ref), m.kind
