@@ -1077,7 +1077,7 @@ constexpr int TNR_BN = 192, TNR_BK = 192, TNR_RB = 32, TNR_NS = 6;
 // the grouped launch runs on the side stream beside the data-gradient chain: a shallower ring
 // (TNR_NSG stages, 96 KiB) leaves room on each CU for a chain workgroup of <= 64 KiB LDS
 constexpr int TNR_NSG = KAIR_TNR_NSG;
-constexpr int BM_ROWS = 0, BM_TAP = 1;
+constexpr int BM_ROWS = 0, BM_TAP = 1, BM_TAP3 = 2;
 
 // One CTA's share of a TN ring product: rows [mbeg, mend) of the (n0, k0) 192x192 tile -> plane P.
 struct TnRingTile {
@@ -1128,6 +1128,13 @@ KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, const Op& Bo, char*
             const int y = fdiv(p, Bo.d_imW), x = p - y * Bo.imW;
             if ((unsigned)(y + tdy) < (unsigned)Bo.imH && (unsigned)(x + tdx) < (unsigned)Bo.imW)
               src = Bp + (long)(m + tshift) * Bld + c;
+          } else if constexpr (BMB == BM_TAP3) {   // 64-channel image: K tile tk = taps 3 tk .. 3 tk + 2
+            const int tp = 3 * (k0 / BKt) + (c >> 6);
+            const int dy = tp / 3 - 1, dx = tp - 3 * (tp / 3) - 1;
+            const int p = m - fdiv(m, Bo.d_hw) * Bo.d_hw.d;
+            const int y = fdiv(p, Bo.d_imW), x = p - y * Bo.imW;
+            if ((unsigned)(y + dy) < (unsigned)Bo.imH && (unsigned)(x + dx) < (unsigned)Bo.imW)
+              src = Bp + (long)(m + dy * Bo.imW + dx) * Bld + (c & 63);
           } else if (k0 + c < K) {
             src = Bp + (long)m * Bld + k0 + c;
           }
@@ -2025,6 +2032,23 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
     rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
     const long grid = (long)ntiles * splits;
     hipLaunchKernelGGL((gemm_tn_ring<AM_ROWS, BM_TAP>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
+                       ntiles, (int)rps);
+    KAIR_CHECK_LAUNCH();
+    return 0;
+  }
+  // conv weight gradient over a 64-channel bf16 image (the reconstruction tail's upsampling convs): the
+  // ring with three taps per 192-wide K tile, each image row fetched once per tile instead of once
+  // per im2col column block
+  if (g_ring_mode && compute == KAIR_BF16 && tn_ring_shape(M, N, K) && K == 9 * 64 && A->dtype == KAIR_BF16 &&
+      B->dtype == KAIR_BF16 && A->mode == KAIR_LD_ROWS && B->mode == KAIR_LD_IM2COL3 && B->im_C == 64 && !B->im_flip &&
+      B->im_up <= 1 && !A->rowscale && !B->rowscale && A->win_ws == 0 && A->ones_col < 0 && B->ones_col < 0 &&
+      A->ld % 8 == 0 && b.ld % 8 == 0 && (long)B->im_H * B->im_W > 0 && M % ((long)B->im_H * B->im_W) == 0) {
+    const int tilesN = (N + TNR_BN - 1) / TNR_BN, tilesK = 3;
+    const int ntiles = tilesN * tilesK;
+    long rps = (M + splits - 1) / splits;
+    rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
+    const long grid = (long)ntiles * splits;
+    hipLaunchKernelGGL((gemm_tn_ring<AM_ROWS, BM_TAP3>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
                        ntiles, (int)rps);
     KAIR_CHECK_LAUNCH();
     return 0;

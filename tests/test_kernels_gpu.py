@@ -547,3 +547,28 @@ def test_gemm_tn_ring_qkvblk_A():
     ref = a.T @ x.double()
     torch.cuda.synchronize()
     assert rel_err(ws.sum(0).cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,Hh,Ww,Cout", [(2, 24, 24, 256), (1, 96, 96, 256), (3, 10, 12, 96)])
+def test_conv_wgrad_tap3_ring(B, Hh, Ww, Cout):
+    """The reconstruction tail's 64-channel conv weight gradients (network_swinir.py:597-600 Upsample,
+    conv 64 -> 4*64) on the ring with three taps per 192-wide K tile (gemm.hip BM_TAP3), against
+    float64 conv2d backward on the same bf16 values."""
+    C = 64
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(B, C, Hh, Ww, generator=g).to(torch.bfloat16).double().requires_grad_(True)
+    w = torch.randn(Cout, C, 3, 3, generator=g, dtype=torch.float64, requires_grad=True)
+    y = torch.nn.functional.conv2d(x, w, padding=1)
+    gy = torch.randn(y.shape, generator=g).to(torch.bfloat16).double()
+    y.backward(gy)
+    M = B * Hh * Ww
+    dy = gy.permute(0, 2, 3, 1).reshape(M, Cout).to(torch.bfloat16)
+    xin = x.detach().permute(0, 2, 3, 1).reshape(M, C).to(torch.bfloat16)
+    K = 9 * C
+    S = H.wgrad_splits(M, Cout, K)
+    ws = torch.full((S, Cout, K), float("nan"), device=dev)
+    H.gemm_tn(H.rows(dy.contiguous().to(dev)), H.im2col(xin.contiguous().to(dev), Hh, Ww, C), ws, S, M, Cout, K, H.BF16)
+    grad = torch.empty(Cout, C, 3, 3, device=dev)
+    H.wgrad_finalize(ws, S, H.wmap(1, Cout, C), grad)
+    torch.cuda.synchronize()
+    assert rel_err(grad, w.grad) < 1e-5
