@@ -160,7 +160,7 @@ def rocprof_name(fn, a):
         kb = K // 16
         epi = {"rowgemm_store": 0, "rowgemm_gate": 1, "rowgemm_lnbwd": 2}[fn]
         ks = 2 if N == 384 else 4   # csrc/rowgemm.hip rg_dispatch: <KB, KS, NWC, EPI, HOLD>
-        hold = {12: kb // ks, 24: 5 if epi == 2 else 6, 36: {0: 9, 1: 7, 2: 4}[epi]}[kb]
+        hold = {12: kb // ks, 24: 6, 36: {0: 9, 1: 7, 2: 5}[epi]}[kb]
         return f"rowgemm_kernel<{kb}, {ks}, {N // 96}, {epi}, {hold}>"
     return {"swin_mlp_fwd": "swin_mlp_fwd_wr_kernel", "swin_attn_fwd": "swin_attn_fwd_kernel<6, 1>",
             "window_attn_bwd": "attn_bwd_bf16_kernel"}.get(fn, fn)

@@ -375,7 +375,9 @@ int rg_launch(const RgArgs& a, hipStream_t s, long* grid_out) {
 }
 
 // grid_out != NULL: report the grid (the LN partial count) without launching.  N = 192: K in
-// {192, 384, 576}; N = 384 (the fc2 input gradient): K = 192.
+// {192, 384, 576}; N = 384 (the fc2 input gradient): K = 192.  HOLD (weight k-steps held in registers)
+// measured: fc1 + LN2 all 6 (a 12-byte spill) and q/k/v + LN1 5 of 9 (20 bytes) beat 5 / 4 with no spill
+// (B = 32 1291 -> 1300, B = 4 558 -> 569); 6 of 9 spills 64 bytes and loses.
 template <int EPI>
 int rg_dispatch(int K, int N, const RgArgs& a, hipStream_t s, long* grid_out = nullptr) {
   if (N == 384) {
@@ -385,8 +387,8 @@ int rg_dispatch(int K, int N, const RgArgs& a, hipStream_t s, long* grid_out = n
   }
   switch (K) {
     case 192: return rg_launch<12, 4, 2, EPI>(a, s, grid_out);
-    case 384: return rg_launch<24, 4, 2, EPI, EPI == EPI_LN ? 5 : 6>(a, s, grid_out);
-    case 576: return rg_launch<36, 4, 2, EPI, EPI == EPI_LN ? 4 : EPI == EPI_GATE ? 7 : 9>(a, s, grid_out);
+    case 384: return rg_launch<24, 4, 2, EPI, 6>(a, s, grid_out);
+    case 576: return rg_launch<36, 4, 2, EPI, EPI == EPI_LN ? 5 : EPI == EPI_GATE ? 7 : 9>(a, s, grid_out);
     default: return kair_set_error(KAIR_ERR_ARG, "rowgemm: K must be 192, 384 or 576 (got %d)", K);
   }
 }
