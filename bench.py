@@ -207,7 +207,7 @@ def cpu_baseline(batch=4, steps=4):
                       f"{steps} timed steps after 1 warm-up, torch CPU {threads} threads"}
 
 
-def fp32_line(bpg, device, drop_path, steps=4, warmup=2):
+def fp32_line(bpg, device, drop_path, steps=12, warmup=3):
     """Throughput of the same training step on the exact-fp32 engine (fp32 MFMA, same kernels and
     program): the parity configuration, whose forward matches the CPU oracle to 1e-7 dB.  A short
     run (the fp32 step is ~10x the bf16 one), timed like the headline."""
