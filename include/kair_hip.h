@@ -478,6 +478,9 @@ int kair_device_arch(char* buf, int len);
  * KAIR_ATTN_STAMP=1 in the environment (s_memtime cycles, 8 per wave: 7 phase boundaries of the
  * wave's third window + its window count).  n = number of u64 values to copy. */
 int kair_debug_attn_stamps(unsigned long long* host, int n);
+/* Perf investigation only: per-wave phase stamps (8 s_memtime values) of the fused attention half's last
+ * window per workgroup (cleared by the read), from a library built with --debug-ablations and KAIR_ATTN_DBG bit 8 set. */
+int kair_debug_fused_stamps(unsigned long long* host, int n);
 
 #ifdef __cplusplus
 }

@@ -156,6 +156,7 @@ _SIGS = {
     "kair_swin_mlp_fwd": [c_vp, c_long, c_vp, c_vp, c_float, c_int, c_vp, c_long, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                           c_long, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_long, c_int, c_int, c_int, c_vp],
     "kair_debug_attn_stamps": [c_vp, c_int],
+    "kair_debug_fused_stamps": [c_vp, c_int],
     "kair_swin_mlp_bwd_ws": [],
     "kair_swin_mlp_bwd": [c_vp, c_long, c_vp, c_long, c_vp, c_vp, c_vp, c_long, c_vp, c_long, c_vp, c_vp, c_vp, c_int,
                           c_vp, c_long, c_vp, c_long, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_long,
@@ -182,6 +183,8 @@ def lib():
             raise RuntimeError(f"kair_amd: HIP kernel library not built ({LIB_PATH}); run `python -m kair_amd.build`")
         L = ctypes.CDLL(LIB_PATH)
         for name, args in _SIGS.items():
+            if name.startswith("kair_debug_") and not hasattr(L, name):
+                continue   # perf-investigation entry points: optional (A/B runs load older builds)
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, c_int)
@@ -663,6 +666,13 @@ def debug_attn_stamps(n=8192 * 8):
     """Phase stamps of the last bf16 attention backward run with KAIR_ATTN_STAMP=1 (perf only)."""
     buf = (ctypes.c_ulonglong * n)()
     check(lib().kair_debug_attn_stamps(ctypes.cast(buf, c_vp), n), "debug_attn_stamps")
+    return list(buf)
+
+
+def debug_fused_stamps(n=4096 * 8):
+    """Phase stamps of the last fused attention half run with KAIR_ATTN_DBG bit 8 (debug builds, perf only)."""
+    buf = (ctypes.c_ulonglong * n)()
+    check(lib().kair_debug_fused_stamps(ctypes.cast(buf, c_vp), n), "debug_fused_stamps")
     return list(buf)
 
 

@@ -23,6 +23,8 @@
 // LayerNorm / QKV / attention / proj kernels it replaces.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -31,6 +33,16 @@ constexpr int TOK = 64, WSZ = 8;
 
 KAIR_DEV int acc_row32(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 KAIR_DEV int shift_region(int coord, int n, int shift) { return coord < n - WSZ ? 0 : (coord < n - shift ? 1 : 2); }
+
+// perf-investigation phase stamps of the fused attention half (debug builds, KAIR_ATTN_DBG bit 8): per
+// wave, s_memtime at the phase boundaries of its workgroup's last window (kair_debug_fused_stamps)
+constexpr int FST_WAVES = 4096, FST_N = 8;
+__device__ unsigned long long g_fused_stamps[FST_WAVES * FST_N];
+KAIR_DEV unsigned long long fst_now() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 
 struct AttnFwdArgs {
   const float* x; long ldx;                  // residual stream fp32 [M][ldx], token order
@@ -99,18 +111,19 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
   static_assert(CP == 192, "the fused attention kernel is laid out for Cp = 192");
   constexpr int NPASS = (RPW + 3) / 4;
   const int g = lane >> 4, jl = lane & 15;
+  // Branch-free (lanes past the window's rows re-read its row 0, past the last window the last window),
+  // so the compiler's vmcnt bookkeeping stays exact across it: the waits for older loads then count
+  // the newer loads and stores instead of draining every store in flight.
   float4 xv[NPASS][3];
   auto load_x = [&](long wn) {
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
       const int i = 4 * p + g, r = w + NH * i;
-      const bool ok = wn < a.nWin && i < RPW && r < TOK;
-      const long base = ok ? win_to_token(wn * TOK + r, a.wm) * a.ldx : 0;
+      const long wc = wn < a.nWin ? wn : a.nWin - 1;
+      const int rr = i < RPW && r < TOK ? r : 0;
+      const long base = win_to_token(wc * TOK + rr, a.wm) * a.ldx;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        xv[p][k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok) xv[p][k] = *(const float4*)(a.x + base + 4 * jl + 64 * k);
-      }
+      for (int k = 0; k < 3; ++k) xv[p][k] = *(const float4*)(a.x + base + 4 * jl + 64 * k);
     }
   };
   load_x(win);
@@ -142,7 +155,11 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
   const float inv_c = 1.0f / (float)a.C;
   const int nWw = a.W / WSZ, nW = (a.H / WSZ) * nWw;
 
+  unsigned long long fts[FST_N];
+  const bool fstamp = KAIR_DBG(a.dbg & 8) && (long)blockIdx.x * NH + w < FST_WAVES;
   for (; win < a.nWin; win += gridDim.x) {
+    const bool fst_on = fstamp;   // every window; the workgroup's last one is what stays
+    if (fst_on) fts[0] = fst_now();
     // row map and shift regions of this window (readers are behind the LN barrier; the previous
     // iteration's last readers are behind its closing barrier)
     const int wi = (int)(win % nW), wy = wi / nWw, wx = wi - wy * nWw;
@@ -201,6 +218,7 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
       }
     }
     __syncthreads();           // LN tile, sX, sRow, sReg visible
+    if (fst_on) fts[1] = fst_now();
 
     // ---- B: q^T, k^T, v of head h = w (weight fragments PF k-steps ahead) -----------------------
     f32x16 QT[2], KT[2], V[2];
@@ -208,23 +226,12 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) QT[t][r] = KT[t][r] = V[t][r] = 0.f;
-#pragma unroll 1
-    for (int kb0 = 0; kb0 < KB; kb0 += PF) {
+    // k-steps in groups of PF; the last group refills nothing, so the loads stay unconditional and the
+    // compiler's vmcnt bookkeeping exact across the loop (a conditional load makes it wait for all)
+    auto qkv_steps = [&](int kb0, auto refill) {
 #pragma unroll
       for (int sl = 0; sl < PF; ++sl) {
         const int kb = kb0 + sl;
-        bf16x8 fq[NS], fk[NS], fv[NS];
-#pragma unroll
-        for (int e = 0; e < NS; ++e) {
-          fq[e] = pq[sl][e];
-          fk[e] = pk[sl][e];
-          fv[e] = pv[sl][e];
-          if (kb + PF < KB) {
-            pq[sl][e] = *(const bf16x8*)(wq + (kb + PF) * WS + e * 512);
-            pk[sl][e] = *(const bf16x8*)(wk + (kb + PF) * WS + e * 512);
-            pv[sl][e] = *(const bf16x8*)(wv + (kb + PF) * WS + e * 512);
-          }
-        }
         bf16x8 fl[2];
 #pragma unroll
         for (int t = 0; t < 2; ++t) fl[t] = *(const bf16x8*)(sT + (t * 32 + l31) * LDT + kb * 16 + 8 * hh);
@@ -232,12 +239,26 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
         for (int e = 0; e < NS; ++e)
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
-            QT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fq[e], fl[t], QT[t], 0, 0, 0);
-            KT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk[e], fl[t], KT[t], 0, 0, 0);
-            V[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl[t], fv[e], V[t], 0, 0, 0);
+            QT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pq[sl][e], fl[t], QT[t], 0, 0, 0);
+            KT[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pk[sl][e], fl[t], KT[t], 0, 0, 0);
+            V[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl[t], pv[sl][e], V[t], 0, 0, 0);
           }
+        // refill the slot after its MFMAs: the load lands in the same registers (no loop-carried
+        // copies, whose reads would make every iteration wait for the loads just issued)
+        if constexpr (decltype(refill)::value) {
+#pragma unroll
+          for (int e = 0; e < NS; ++e) {
+            pq[sl][e] = *(const bf16x8*)(wq + (kb + PF) * WS + e * 512);
+            pk[sl][e] = *(const bf16x8*)(wk + (kb + PF) * WS + e * 512);
+            pv[sl][e] = *(const bf16x8*)(wv + (kb + PF) * WS + e * 512);
+          }
+        }
       }
-    }
+    };
+#pragma unroll 1
+    for (int kb0 = 0; kb0 < KB - PF; kb0 += PF) qkv_steps(kb0, std::true_type{});
+    qkv_steps(KB - PF, std::false_type{});
+    if (fst_on) fts[2] = fst_now();
     // proj weight fragments for the first PF k-steps of phase D, in flight during the attention
     bf16x8 pw[PF][NS];
 #pragma unroll
@@ -291,6 +312,7 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
       }
     }
 
+    if (fst_on) fts[3] = fst_now();
     // ---- C: attention of head h ------------------------------------------------------------------
     f32x16 S[2][2];
 #pragma unroll
@@ -351,6 +373,7 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
         for (int r = 0; r < 16; ++r) S[kt][qt][r] *= inv;
       lse_v[qt] = mx + __logf(sum);
     }
+    if (fst_on) fts[4] = fst_now();
     // O^T = V^T P^T: lane = query, registers = d -> the O tile (LDS)
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -371,8 +394,11 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
         *(bf16x4*)(sO + qi * LDT + h * 32 + d0) = bf16x4{(bf16)r4[0], (bf16)r4[1], (bf16)r4[2], (bf16)r4[3]};
       }
     }
-    load_x(win + gridDim.x);   // the next window's rows, in flight through phase D and the stores
+    load_x(win + gridDim.x);   // the next window's rows and first q/k/v weight fragments, in flight
+    load_w();                  // through phase D
+    const float rs = a.rowscale ? a.rowscale[win / a.win_per_scale] : 1.f;
     __syncthreads();           // the O tile is complete
+    if (fst_on) fts[5] = fst_now();
 
     // ---- D: proj + bias, DropPath scale, fp32 residual from sX ------------------------------------
     f32x16 P[2];
@@ -380,27 +406,33 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) P[t][r] = 0.f;
-#pragma unroll 1
-    for (int kb0 = 0; kb0 < KB; kb0 += PF) {
+    auto proj_steps = [&](int kb0, auto refill) {
 #pragma unroll
       for (int sl = 0; sl < PF; ++sl) {
         const int kb = kb0 + sl;
-        bf16x8 fw[NS];
-#pragma unroll
-        for (int e = 0; e < NS; ++e) {
-          fw[e] = pw[sl][e];
-          if (kb + PF < KB) pw[sl][e] = *(const bf16x8*)(wp + (kb + PF) * WS + e * 512);
-        }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const bf16x8 fo = *(const bf16x8*)(sO + (t * 32 + l31) * LDT + kb * 16 + 8 * hh);
 #pragma unroll
-          for (int e = 0; e < NS; ++e) P[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fo, fw[e], P[t], 0, 0, 0);
+          for (int e = 0; e < NS; ++e) P[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fo, pw[sl][e], P[t], 0, 0, 0);
+        }
+        if constexpr (decltype(refill)::value) {
+#pragma unroll
+          for (int e = 0; e < NS; ++e) pw[sl][e] = *(const bf16x8*)(wp + (kb + PF) * WS + e * 512);
         }
       }
-    }
-    load_w();   // the next window's first q/k/v weight fragments, still ahead of this window's stores
-    const float rs = a.rowscale ? a.rowscale[win / a.win_per_scale] : 1.f;
+    };
+#pragma unroll 1
+    for (int kb0 = 0; kb0 < KB - PF; kb0 += PF) proj_steps(kb0, std::true_type{});
+    proj_steps(KB - PF, std::false_type{});
+    if (fst_on) fts[6] = fst_now();
+    // the next window's x rows (and with them the weight fragments) have landed by now, behind the
+    // proj GEMM: waiting for them HERE, before this window's stores are issued, keeps the next LN
+    // from waiting for those stores to drain (vmcnt retires loads and stores in issue order)
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) asm volatile("" ::"v"(xv[p][k].x), "v"(xv[p][k].y), "v"(xv[p][k].z), "v"(xv[p][k].w));
 
     // ---- stores: mid (token order), then everything saved for backward ---------------------------
     // mid = x + s * (proj + bias), formed in place in sX, then stored row-contiguous
@@ -434,6 +466,18 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
       a.rstd[t] = sRstd[tid];
     }
     __syncthreads();   // every LDS tile / row map of this window consumed
+    if (fst_on) {
+      fts[7] = fst_now();
+      if (lane < FST_N) {
+        // the stamp of phase 0 carries the wave's SIMD (HW_ID bits 5:4) in its top byte
+        const unsigned hwid = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+        unsigned long long v = (fts[0] & 0x00FFFFFFFFFFFFFFull) | ((unsigned long long)((hwid >> 4) & 3) << 56);
+#pragma unroll
+        for (int i = 1; i < FST_N; ++i)
+          if (lane == i) v = fts[i];
+        g_fused_stamps[((long)blockIdx.x * NH + w) * FST_N + lane] = v;
+      }
+    }
   }
 }
 
@@ -1326,5 +1370,18 @@ extern "C" int kair_swin_mlp_bwd(const void* dc, long lddc, const void* gd, long
   hipLaunchKernelGGL(mlp_bwd_param_reduce, dim3((unsigned)((2 * C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws,
                      (int)grid, C, 192, dgamma, dbeta, dparam_acc);
   KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+// copy the fused-attention phase stamps to the host (perf investigation only; zeros in release builds)
+extern "C" int kair_debug_fused_stamps(unsigned long long* host, int n) {
+  KAIR_CHECK_ARG(host && n > 0 && n <= FST_WAVES * FST_N, "debug_fused_stamps: bad args");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_stamps), sizeof(unsigned long long) * n, 0, hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return kair_set_error(KAIR_ERR_HIP, "debug_fused_stamps: copy failed");
+  void* dev = nullptr;   // cleared after the read, so the next read holds only the next launch's windows
+  if (hipGetSymbolAddress(&dev, HIP_SYMBOL(g_fused_stamps)) != hipSuccess ||
+      hipMemset(dev, 0, sizeof(unsigned long long) * FST_WAVES * FST_N) != hipSuccess)
+    return kair_set_error(KAIR_ERR_HIP, "debug_fused_stamps: clear failed");
   return 0;
 }

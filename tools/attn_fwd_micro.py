@@ -7,7 +7,10 @@ import torch
 sys.path.insert(0, "/root/repo")
 from kair_amd import _hip as H
 if len(sys.argv) > 1:
+    import ctypes
     H.LIB_PATH = os.path.abspath(sys.argv[1])
+    _probe = ctypes.CDLL(H.LIB_PATH)   # an older variant may lack newer debug entry points
+    H._SIGS = {k: v for k, v in H._SIGS.items() if hasattr(_probe, k)}
 dev = torch.device("cuda", 0)
 C, CP, NH = 180, 192, 6
 
