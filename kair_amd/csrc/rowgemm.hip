@@ -195,20 +195,25 @@ __global__ __launch_bounds__(64 * NWC * KS, 1) void rowgemm_kernel(const RgArgs 
     for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[ct][r] = 0.f;
-    bf16x8 rs_[NSTR > 0 ? NSTR : 1][NCT];
+    // streamed fragments f = NCT i + ct through a ring of SD registers: the first SD in flight under
+    // the resident steps' MFMAs, each slot refilled right after the MFMA that read it (left to itself
+    // the scheduler sinks every load to its use under the register budget: 12 serial L2 round trips)
+    constexpr int NF = NSTR * NCT, SDM = EPI == EPI_GATE ? 2 : 4, SD = NF < SDM ? (NF > 0 ? NF : 1) : SDM;
+    auto sfrag = [&](int f) { return bld16(rW, wl, ((f % NCT) * KB + ks * KBW + HOLD + f / NCT) * 1024u); };
+    bf16x8 rs_[SD];
 #pragma unroll
-    for (int i = 0; i < NSTR; ++i)
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) rs_[i][ct] = bld16(rW, wl, (ct * KB + ks * KBW + HOLD + i) * 1024u);
+    for (int f = 0; f < SD && f < NF; ++f) rs_[f] = sfrag(f);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < HOLD; ++i)
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[i], rw[i][ct], acc[ct], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < NSTR; ++i)
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct)
-        acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[HOLD + i], rs_[i][ct], acc[ct], 0, 0, 0);
+    for (int f = 0; f < NF; ++f) {
+      acc[f % NCT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[HOLD + f / NCT], rs_[f % SD], acc[f % NCT], 0, 0, 0);
+      if (f + SD < NF) rs_[f % SD] = sfrag(f + SD);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     __builtin_amdgcn_sched_barrier(0);
     float4 dv[LPASS][3];
     if constexpr (EPI == EPI_LN) {   // D of this lane's rows: in flight across the exchange
