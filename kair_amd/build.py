@@ -3,11 +3,14 @@
     python -m kair_amd.build [--force] [-j N]
 
 Objects go to kair_amd/build/, the library to kair_amd/lib/libkair_hip.so (in-tree, so it travels
-to the GPU box with the repo snapshot).  Rebuilds only when a source or header is newer.
+to the GPU box with the repo snapshot).  An object is rebuilt when the content stamp of its source,
+the headers and the compile flags changes (not by mtime: `git stash` round trips and debug builds
+would otherwise leave stale objects behind), the library when any object's stamp changed.
 """
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -24,20 +27,40 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I
          "-Wno-unused-result", "-munsafe-fp-atomics"]
 
 
-def _newest_dep():
-    deps = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
-    return max(os.path.getmtime(p) for p in deps) if deps else 0.0
+def _headers_digest():
+    h = hashlib.sha256()
+    for p in sorted(glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))):
+        h.update(p.encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 
-def _compile(src, force, dep_time):
+def _read(p):
+    try:
+        with open(p) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _compile(src, force, hdr):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), dep_time):
-        return obj, None
+    h = hashlib.sha256(" ".join([HIPCC, *FLAGS, hdr]).encode())
+    with open(src, "rb") as f:
+        h.update(f.read())
+    stamp = h.hexdigest()
+    if not force and os.path.exists(obj) and _read(obj + ".stamp") == stamp:
+        return obj, None, stamp
+    if os.path.exists(obj + ".stamp"):
+        os.remove(obj + ".stamp")
     cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
-    return obj, None
+        return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}", stamp
+    with open(obj + ".stamp", "w") as f:
+        f.write(stamp)
+    return obj, None, stamp
 
 
 def build(force=False, jobs=None, verbose=True, debug_ablations=False):
@@ -49,19 +72,24 @@ def build(force=False, jobs=None, verbose=True, debug_ablations=False):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
-    dep_time = _newest_dep()
+    hdr = _headers_digest()
     jobs = jobs or min(8, len(srcs), os.cpu_count() or 1)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, force, dep_time), srcs))
-    errs = [e for _, e in results if e]
+        results = list(ex.map(lambda s: _compile(s, force, hdr), srcs))
+    errs = [e for _, e, _ in results if e]
     if errs:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
-    objs = [o for o, _ in results]
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+    objs = [o for o, _, _ in results]
+    lib_stamp = hashlib.sha256("".join(st for _, _, st in results).encode()).hexdigest()
+    if force or not os.path.exists(LIB) or _read(LIB + ".stamp") != lib_stamp:
+        if os.path.exists(LIB + ".stamp"):
+            os.remove(LIB + ".stamp")
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        with open(LIB + ".stamp", "w") as f:
+            f.write(lib_stamp)
         if verbose:
             print("built", LIB)
     return LIB
