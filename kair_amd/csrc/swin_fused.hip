@@ -72,11 +72,11 @@ KAIR_DEV bf16x8 pack8r(const f32x16& a, int s) {
 
 // Persistent: one workgroup per CU loops over windows.  Memory-operation order: vmcnt counts
 // loads AND stores in issue order, so a wait for a load issued after a store also waits for that
-// store.  Within an iteration the global loads (the NEXT window's x rows, the weight fragments)
-// are issued ahead of the iteration's stores; the x rows of window i+1 are in flight during
-// window i's proj GEMM and stores (the kernel is otherwise latency-bound: one window is ~50 k
-// cycles of dependent phases on 6 waves).  The fp32 x rows also stay in LDS for the residual,
-// so nothing is re-read.
+// store.  The NEXT window's x rows and first weight fragments are issued before the O-tile barrier
+// and waited for (behind the proj GEMM) before this window's stores are issued, so no later wait
+// drains those stores.  One window is ~37 k cycles of barrier-separated phases, issue-bound on the
+// two SIMDs that carry two of the six waves (tools/attn_fwd_stamps.py).  The fp32 x
+// rows also stay in LDS for the residual, so nothing is re-read.
 
 // NS = 2: hi/lo split weights (pack kind 12), each k-step multiplies the same LN / O fragment by
 // the hi and the lo half, so the products see the fp32 master weights to ~16 mantissa bits.
