@@ -64,6 +64,13 @@ typedef struct {
                           2*ceil(K/64)*64.  The A operand is read once per pair, so the product
                           carries ~16 mantissa bits of the fp32 master weights (bf16 weight
                           rounding biases the output, see DESIGN.md "parity at bf16")        */
+  int a_split;         /* kair_gemm_nt A only (bf16 compute, ROWS / IM2COL3, no rowscale): the
+                          activation enters the product as a hi/lo bf16 pair, x = hi + lo with
+                          lo = bf16(x - hi), adding the product a_lo . w_hi (with w_split also
+                          a_hi . w_lo): ~16 mantissa bits of the activation instead of 8.
+                          fp32 A: lo is formed in the kernel from the fp32 value; bf16 A: ptr
+                          holds the hi plane and lo_ptr the lo plane (same layout)           */
+  const void* lo_ptr;  /* bf16 A with a_split: the lo plane (kair_epilogue.out_lo of its producer) */
 } kair_operand;
 
 typedef enum {
@@ -113,6 +120,10 @@ typedef struct {
                                            weight gradient's operand, written from the halo the conv
                                            loads anyway (no extra read of the fp32 image)           */
   int acopy_ones_col_p1;                /* 1 + channel of a_copy forced to 1.0 (bias gradient); 0 none */
+  void* out_lo;                         /* optional, bf16 `out` in ROWS / PSHUF_SPM mode: the lo plane
+                                           lo = bf16(v - bf16(v)) at the same offsets, so the next
+                                           conv can read the activation as a hi/lo pair
+                                           (kair_operand.a_split)                                  */
 } kair_epilogue;
 
 /* C[m,n] = sum_k A[m,k] * B[n,k]  (+ epilogue).  compute: KAIR_BF16 -> v_mfma_f32_16x16x32_bf16,
@@ -158,7 +169,8 @@ typedef struct {
                           row 16nb + l%16, k 32kb + 8(l/16) + j) */
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
-  int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp                   */
+  int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp (kinds 1 / 9 only: kG*kGr
+                        may be a multiple of K -- tied copies, packed col -> reference col % K)   */
   int n_perm;        /* > 1: the out dim is stored sub-pixel-major for a PixelShuffle(r), n_perm =
                         r*r: packed (unpadded) row s*(N/r^2) + c holds reference row c*r^2 + s
                         (KAIR_OUT_PSHUF_SPM / KAIR_OUT_PUNSHUF_SPM layouts); 0 or 1: identity     */
@@ -335,6 +347,11 @@ int kair_swin_mlp_bwd(const void* dc, long lddc, const void* gd, long ldg, const
  * (network_swinir.py:809-810); mean may be NULL.  Pad channels written 0. */
 int kair_image_to_nhwc(const float* img, void* out, int dtype, int ldc, const float* mean, float img_range,
                        int B, int C, int H, int W, void* stream);
+/* The same as a hi/lo bf16 pair (conv_first of the split-operand engine): channel c < C holds
+ * hi = bf16(x'), channel ldc/2 + c holds bf16(x' - hi); pad channels 0.  Needs 2*C <= ldc, ldc even.
+ * The conv reading it packs its weights tied over both halves (kair_wmap kG*kGr = 2K, kinds 1 / 9). */
+int kair_image_to_nhwc_hilo(const float* img, void* out, int ldc, const float* mean, float img_range,
+                            int B, int C, int H, int W, void* stream);
 /* L1 loss (nn.L1Loss, mean): loss_out[0] = weight*mean|E-H|; grad dE = weight*sign(E-H)/numel written
  * for the last conv's dgrad: NHWC (dtype, channel stride ldc) when ps_r == 1, or in the
  * pre-PixelShuffle(ps_r) layout [b][y/r][x/r][c*r*r + (y%r)*r + x%r] otherwise.  ws: 1024 floats. */

@@ -9,7 +9,10 @@ import os
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libkair_hip.so")
+# KAIR_LIB=debug: the debug-ablation build (python -m kair_amd.build --debug-ablations), for the
+# perf-investigation tools only; the release library is the default and the only one tests / bench use
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                        "libkair_hip_dbg.so" if os.environ.get("KAIR_LIB") == "debug" else "libkair_hip.so")
 
 F32, BF16 = 0, 1
 LD_ROWS, LD_IM2COL3, LD_QKVBLK, LD_S2D = 0, 1, 2, 3
@@ -30,7 +33,7 @@ class Operand(ctypes.Structure):
                 ("im_H", c_int), ("im_W", c_int), ("im_C", c_int), ("im_flip", c_int),
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
                 ("rowscale", c_vp), ("rows_per_scale", c_int), ("ones_col", c_int), ("ones_in_data", c_int),
-                ("im_up", c_int), ("w_split", c_int)]
+                ("im_up", c_int), ("w_split", c_int), ("a_split", c_int), ("lo_ptr", c_vp)]
 
 
 class CopyDesc(ctypes.Structure):
@@ -62,7 +65,7 @@ class Epilogue(ctypes.Structure):
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
                 ("img_mean", c_vp), ("img_range", c_float), ("img_C", c_int), ("img_H", c_int), ("img_W", c_int),
                 ("out_ones_col_p1", c_int), ("resid2", c_vp), ("ldr2", c_long), ("pre_kind", c_int),
-                ("a_copy", c_vp), ("ld_acopy", c_long), ("acopy_ones_col_p1", c_int)]
+                ("a_copy", c_vp), ("ld_acopy", c_long), ("acopy_ones_col_p1", c_int), ("out_lo", c_vp)]
 
 
 class WMap(ctypes.Structure):
@@ -120,6 +123,7 @@ _SIGS = {
     "kair_window_attn_bwd_ex": [c_vp, c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_long,
                                 c_int, c_int, c_float, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "kair_image_to_nhwc": [c_vp, c_vp, c_int, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
+    "kair_image_to_nhwc_hilo": [c_vp, c_vp, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
     "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "kair_charbonnier_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_int, c_int,
                               c_vp, c_vp],
@@ -248,6 +252,16 @@ def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1, one
     return o
 
 
+def asplit(op, lo=None):
+    """Mark a kair_gemm_nt A operand as a hi/lo activation pair: fp32 A forms lo in the kernel, a bf16 A
+    (the hi plane) reads lo from `lo` (its producer's epilogue out_lo)."""
+    op.a_split = 1
+    if lo is not None:
+        op.lo_ptr = ptr(lo)
+        op._keep = (op._keep, lo)
+    return op
+
+
 def im2col(t, H, W, C, flip=False, ones_col=-1, ld=None, up=1, ones_in_data=False):
     """3x3 / pad 1 im2col view of an NHWC map: H x W is the CONV grid, ld the pixel stride
     (default C), up=2 reads the source (H/2 x W/2) through a nearest x2 upsample.  ones_in_data: the
@@ -297,12 +311,14 @@ def qkvblk(t, nh, hdp=32, tok=64, rowscale=None, rows_per_scale=1):
 
 def epilogue(out, mode=OUT_ROWS, ldo=None, win=None, bias=None, act=ACT_NONE, slope=0.0, pre=None, ldp=None,
              resid=None, ldr=None, rowscale=None, rows_per_scale=1, gate=None, ldg=None, gate_kind=0,
-             ps=None, qkv=None, img=None, ones_col=-1, resid2=None, ldr2=None, pre_grad=False, acopy=None):
+             ps=None, qkv=None, img=None, ones_col=-1, resid2=None, ldr2=None, pre_grad=False, acopy=None, out_lo=None):
     """pre_grad: `pre` receives act'(x) instead of x (GELU; read back with gate_kind=4).  acopy = (bf16
-    tensor, ones_col): the 3x3 halo conv also writes its A image there (ones_col >= 0: that channel 1.0)."""
+    tensor, ones_col): the 3x3 halo conv also writes its A image there (ones_col >= 0: that channel 1.0).
+    out_lo: bf16 lo plane bf16(v - bf16(v)) beside a bf16 ROWS / PSHUF_SPM out (same layout)."""
     e = Epilogue()
     e.pre_kind = int(bool(pre_grad))
-    e._keep = (out, bias, pre, resid, rowscale, gate, img, resid2, acopy)
+    e._keep = (out, bias, pre, resid, rowscale, gate, img, resid2, acopy, out_lo)
+    e.out_lo = ptr(out_lo)
     if acopy is not None:
         e.a_copy, e.ld_acopy, e.acopy_ones_col_p1 = ptr(acopy[0]), acopy[0].shape[-1], acopy[1] + 1
     if resid2 is not None:
@@ -509,6 +525,12 @@ def window_attn_bwd(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc,
     check(lib().kair_window_attn_bwd_ex(ptr(qkv), ptr(O), ldo, ptr(dO), lddo, dtype_code(qkv), ptr(table), ptr(lse),
                                         ptr(dqkv), int(dqkv_rows), ptr(dtable), int(dtable_acc), ptr(ws), nWin, nh, hd,
                                         scale, H, W, shift, ptr(mask), mnw, stream_ptr()), "window_attn_bwd")
+
+
+def image_to_nhwc_hilo(img, out, ldc, mean, img_range, B, C, H, W):
+    """bf16 hi/lo pair of the normalised image: hi in channels [0, C), lo in [ldc/2, ldc/2 + C)."""
+    check(lib().kair_image_to_nhwc_hilo(ptr(img), ptr(out), ldc, ptr(mean), img_range, B, C, H, W, stream_ptr()),
+          "image_to_nhwc_hilo")
 
 
 def image_to_nhwc(img, out, ldc, mean, img_range, B, C, H, W):

@@ -20,6 +20,10 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "lib", "libkair_hip.so")
+# debug-ablation builds: their own objects and library (kair_amd._hip loads it only with KAIR_LIB=debug),
+# so a release build() after a debug one in the same process or tree never ships the ablation switches
+OBJ_DBG = os.path.join(HERE, "build_dbg")
+LIB_DBG = os.path.join(HERE, "lib", "libkair_hip_dbg.so")
 INCLUDE = os.path.join(ROOT, "include")
 ARCH = os.environ.get("KAIR_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -44,9 +48,9 @@ def _read(p):
         return None
 
 
-def _compile(src, force, hdr):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    h = hashlib.sha256(" ".join([HIPCC, *FLAGS, hdr]).encode())
+def _compile(src, force, hdr, flags, objdir):
+    obj = os.path.join(objdir, os.path.basename(src) + ".o")
+    h = hashlib.sha256(" ".join([HIPCC, *flags, hdr]).encode())
     with open(src, "rb") as f:
         h.update(f.read())
     stamp = h.hexdigest()
@@ -54,7 +58,7 @@ def _compile(src, force, hdr):
         return obj, None, stamp
     if os.path.exists(obj + ".stamp"):
         os.remove(obj + ".stamp")
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *flags, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}", stamp
@@ -66,33 +70,32 @@ def _compile(src, force, hdr):
 def build(force=False, jobs=None, verbose=True, debug_ablations=False):
     """debug_ablations: compile the perf-investigation ablation switches (KAIR_*_DBG environment bits
     that drop stores / skip GEMMs) into the library -- never for training; the release build has none."""
-    if debug_ablations:
-        FLAGS.append("-DKAIR_DEBUG_ABLATIONS=1")
-        force = True
-    os.makedirs(OBJ, exist_ok=True)
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    flags = FLAGS + (["-DKAIR_DEBUG_ABLATIONS=1"] if debug_ablations else [])   # per call: FLAGS never changes
+    objdir, lib = (OBJ_DBG, LIB_DBG) if debug_ablations else (OBJ, LIB)
+    os.makedirs(objdir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     hdr = _headers_digest()
     jobs = jobs or min(8, len(srcs), os.cpu_count() or 1)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, force, hdr), srcs))
+        results = list(ex.map(lambda s: _compile(s, force, hdr, flags, objdir), srcs))
     errs = [e for _, e, _ in results if e]
     if errs:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
     objs = [o for o, _, _ in results]
     lib_stamp = hashlib.sha256("".join(st for _, _, st in results).encode()).hexdigest()
-    if force or not os.path.exists(LIB) or _read(LIB + ".stamp") != lib_stamp:
-        if os.path.exists(LIB + ".stamp"):
-            os.remove(LIB + ".stamp")
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
+    if force or not os.path.exists(lib) or _read(lib + ".stamp") != lib_stamp:
+        if os.path.exists(lib + ".stamp"):
+            os.remove(lib + ".stamp")
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-        with open(LIB + ".stamp", "w") as f:
+        with open(lib + ".stamp", "w") as f:
             f.write(lib_stamp)
         if verbose:
-            print("built", LIB)
-    return LIB
+            print("built", lib)
+    return lib
 
 
 if __name__ == "__main__":

@@ -41,7 +41,7 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const int kk = (int)(t - (long)np * 9 * Kp);
     const int tap = kk / Kp, cip = kk - tap * Kp;
     const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
-    if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
+    if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci % mp.K) * 9 + tap];   // % K: tied in-dim copies
   } else if (mp.kind == 2) {  // conv dgrad form [Cip][9*Cop], k = tap*Cop + co (loader negates taps)
     const int cip = (int)(t / (9 * Np));
     const int kk = (int)(t - (long)cip * 9 * Np);
@@ -62,7 +62,7 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     if (k < Kc) {
       const int tap = k / Kp, cip = k - tap * Kp;
       const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
-      if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
+      if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci % mp.K) * 9 + tap];   // % K: tied in-dim copies
     }
     const bf16 hi = (bf16)v;
     ((bf16*)dst)[t] = half ? (bf16)(v - (float)hi) : hi;
@@ -415,6 +415,24 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ img, T* __restric
   out[t] = (T)v;
 }
 
+// hi/lo input split: channel c < C holds bf16(v), channel ldc/2 + c holds bf16(v - bf16(v)) (the
+// conv_first weights are packed tied over both halves, so the product sees v to ~16 bits)
+__global__ void image_to_nhwc_hilo_kernel(const float* __restrict__ img, bf16* __restrict__ out, int ldc,
+                                          const float* __restrict__ mean, float range, int C, long HW, long total) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const long pix = t / ldc;
+  const int c = (int)(t - pix * ldc), half = ldc / 2;
+  const int cc = c < half ? c : c - half;
+  float v = 0.f;
+  if (cc < C) {
+    const long b = pix / HW, p = pix - b * HW;
+    v = (img[(b * C + cc) * HW + p] - (mean ? mean[cc] : 0.f)) * range;
+  }
+  const bf16 hi = (bf16)v;
+  out[t] = c < half ? hi : (bf16)(v - (float)hi);
+}
+
 // I: index type (int when every index fits: 32-bit divisions are a fraction of the 64-bit ones)
 // CH: Charbonnier (models/loss.py:208-218) sqrt(d^2 + eps) with gradient d / sqrt(d^2 + eps), else L1
 template <typename T, typename I, bool CH>
@@ -562,7 +580,11 @@ static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
   KAIR_CHECK_ARG((mp.kind != 9 && mp.kind != 12) || dst_dtype == KAIR_BF16,
                  "pack_weight: the hi/lo split forms (kinds 9, 12) are bf16 only");
   KAIR_CHECK_ARG(mp.nG > 0 && mp.nGr > 0 && mp.nGp >= mp.nGr && mp.nG * mp.nGr == mp.N, "pack_weight: bad N map");
-  KAIR_CHECK_ARG(mp.kind == 4 || (mp.kG > 0 && mp.kGr > 0 && mp.kGp >= mp.kGr && mp.kG * mp.kGr == mp.K),
+  // kinds 1 / 9 (conv forward) may repeat the in dim (kG * kGr a multiple of K: tied copies, e.g. the
+  // hi / lo halves of a split input image); every other kind maps it one to one
+  KAIR_CHECK_ARG(mp.kind == 4 ||
+                     (mp.kG > 0 && mp.kGr > 0 && mp.kGp >= mp.kGr &&
+                      (mp.kG * mp.kGr == mp.K || ((mp.kind == 1 || mp.kind == 9) && mp.K > 0 && (mp.kG * mp.kGr) % mp.K == 0))),
                  "pack_weight: bad K map");
   KAIR_CHECK_ARG(mp.n_perm <= 1 || (mp.nG == 1 && mp.N % mp.n_perm == 0), "pack_weight: n_perm needs nG == 1, N %% n_perm == 0");
   const long Np = (long)mp.nG * mp.nGp, Kp = (long)mp.kG * mp.kGp;
@@ -712,6 +734,16 @@ extern "C" int kair_image_to_nhwc(const float* img, void* out, int dtype, int ld
   else
     hipLaunchKernelGGL(image_to_nhwc_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, img, (float*)out, ldc, mean,
                        img_range, C, (long)H * W, total);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_image_to_nhwc_hilo(const float* img, void* out, int ldc, const float* mean, float img_range, int B,
+                                       int C, int H, int W, void* stream) {
+  KAIR_CHECK_ARG(img && out && ldc % 2 == 0 && 2 * C <= ldc, "image_to_nhwc_hilo: needs 2 * C <= ldc (even)");
+  const long total = (long)B * H * W * ldc;
+  hipLaunchKernelGGL(image_to_nhwc_hilo_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, img, (bf16*)out,
+                     ldc, mean, img_range, C, (long)H * W, total);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

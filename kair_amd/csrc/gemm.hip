@@ -45,6 +45,8 @@ struct Op {
   int ones_in_data;
   long M;  // rows of this operand
   int wsplit;  // B only: hi/lo bf16 weight pairs interleaved per 64 columns (kair_operand.w_split)
+  int asplit;  // A only: the activation as a hi/lo bf16 pair (kair_operand.a_split)
+  const void* lo_ptr;   // bf16 A with asplit: the lo plane
   FDiv d_rps, d_imC, d_imW, d_hw, d_tok, d_hdp, d_pw;
 };
 
@@ -61,6 +63,8 @@ Op make_op(const kair_operand& o, long M) {
   op.ones_in_data = o.ones_in_data;
   op.M = M;
   op.wsplit = o.w_split ? 1 : 0;
+  op.asplit = o.a_split ? 1 : 0;
+  op.lo_ptr = o.lo_ptr;
   op.d_rps = make_fdiv(op.rps);
   op.d_imC = make_fdiv(op.imC); op.d_imW = make_fdiv(op.imW); op.d_hw = make_fdiv(op.imH * op.imW);
   op.d_tok = make_fdiv(op.tok); op.d_hdp = make_fdiv(op.hdp); op.d_pw = make_fdiv(op.nh * op.hdp);
@@ -153,7 +157,8 @@ KAIR_DEV void raw_load(const T* p, Raw<T>& r) {
 }
 
 template <int AM, typename T>
-KAIR_DEV void issue_chunk(const Op& op, const RowState& r, int k, int K, Raw<T>& raw, Pend& pd) {
+KAIR_DEV void issue_chunk(const Op& op, const RowState& r, int k, int K, Raw<T>& raw, Pend& pd,
+                          const void* base = nullptr) {
   bool ok = r.valid && k < K;
   long off = 0;
   if constexpr (AM == AM_ROWS) {
@@ -178,7 +183,7 @@ KAIR_DEV void issue_chunk(const Op& op, const RowState& r, int k, int K, Raw<T>&
     const int h = fdiv(rr, op.d_hdp), d = rr - h * op.hdp;
     off = (long)part * op.M * pw + r.base + (long)h * op.tok * op.hdp + d;
   }
-  raw_load<T>((const T*)op.ptr + (ok ? off : 0), raw);
+  raw_load<T>((const T*)(base ? base : op.ptr) + (ok ? off : 0), raw);
   pd.scale = ok ? r.scale : 0.f;
   pd.ones = (r.valid && op.ones_col >= k && op.ones_col < k + 8) ? op.ones_col - k : -1;
 }
@@ -196,8 +201,9 @@ KAIR_DEV void raw_to_f32(const Raw<T>& r, float (&v)[8]) {
   }
 }
 
+// lo (fp32 source, bf16 compute): store the lo half bf16(x - bf16(x)) of the (scaled) value instead
 template <typename CT, typename T>
-KAIR_DEV void commit_chunk(CT* dst, const Raw<T>& raw, const Pend& pd) {
+KAIR_DEV void commit_chunk(CT* dst, const Raw<T>& raw, const Pend& pd, bool lo = false) {
   if constexpr (sizeof(CT) == 2 && sizeof(T) == 2) {
     if (pd.scale == 1.f && pd.ones < 0) {          // common case: raw bf16 straight to LDS
       *(uint4*)dst = raw.a;
@@ -215,7 +221,7 @@ KAIR_DEV void commit_chunk(CT* dst, const Raw<T>& raw, const Pend& pd) {
   if constexpr (sizeof(CT) == 2) {
     bf16x8 q;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) q[j] = (bf16)v[j];
+    for (int j = 0; j < 8; ++j) q[j] = lo ? (bf16)(v[j] - (float)(bf16)v[j]) : (bf16)v[j];
     *(bf16x8*)dst = q;
   } else {
 #pragma unroll
@@ -242,6 +248,7 @@ struct Epi {
   int ones_col;   // -1 none
   const float* resid2; long ldr2;
   bf16* acopy; long ldac; int acones;   // halo conv: bf16 copy of the A image (acones: 1.0 channel, -1 none)
+  bf16* out_lo;                         // bf16 ROWS / PSHUF_SPM out: lo plane bf16(v - bf16(v))
   long M; int N;
   FDiv d_rps, d_tok, d_hdp, d_pw;
   int dbg;   // ring-kernel ablation bits (KAIR_RING_DBG, perf investigation only): 1 no stores, 2 no MFMA, 4 no A loads
@@ -263,6 +270,7 @@ Epi make_epi(const kair_epilogue& o, long M, int N) {
   e.ones_col = o.out_ones_col_p1 - 1;
   e.resid2 = o.resid2; e.ldr2 = o.ldr2;
   e.acopy = (bf16*)o.a_copy; e.ldac = o.ld_acopy; e.acones = o.acopy_ones_col_p1 - 1;
+  e.out_lo = (bf16*)o.out_lo;
   e.M = M; e.N = N;
   e.d_rps = make_fdiv(e.rps); e.d_tok = make_fdiv(e.tok); e.d_hdp = make_fdiv(e.hdp); e.d_pw = make_fdiv(e.nh * e.hdp);
   static const int dbg = kair_dbg_env("KAIR_RING_DBG");
@@ -285,6 +293,13 @@ KAIR_DEV void store8_any(void* p, int dt, long off, const float (&v)[8]) {
     *(float4*)d = make_float4(v[0], v[1], v[2], v[3]);
     *(float4*)(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
+}
+// the lo plane of 8 values stored as bf16 hi: bf16(v - bf16(v))
+KAIR_DEV void store8_lo(bf16* p, long off, const float (&v)[8]) {
+  bf16x8 q;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = (bf16)(v[j] - (float)(bf16)v[j]);
+  *(bf16x8*)(p + off) = q;
 }
 KAIR_DEV void st1(void* p, int dt, long off, float v) {
   if (dt == KAIR_BF16) ((bf16*)p)[off] = (bf16)v;
@@ -341,10 +356,12 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
     if (full && (e.ldo % 8) == 0) {
       store8_any(e.out, e.odt, row * e.ldo + n, v);
       if (e.pre) store8_any(e.pre, e.pdt, row * e.ldp + n, pre);
+      if (e.out_lo) store8_lo(e.out_lo, row * e.ldo + n, v);
     } else {
       for (int j = 0; j < 8 && n + j < e.N; ++j) {
         st1(e.out, e.odt, row * e.ldo + n + j, v[j]);
         if (e.pre) st1(e.pre, e.pdt, row * e.ldp + n + j, pre[j]);
+        if (e.out_lo) e.out_lo[row * e.ldo + n + j] = (bf16)(v[j] - (float)(bf16)v[j]);
       }
     }
   } else if (e.omode == KAIR_OUT_QKVBLK) {
@@ -382,12 +399,14 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
     if (full && c + 8 <= nf && (e.ldo % 8) == 0 && (c % 8) == 0) {
       store8_any(e.out, e.odt, orow * e.ldo + c, v);
       if (e.pre) store8_any(e.pre, e.pdt, orow * e.ldp + c, pre);
+      if (e.out_lo) store8_lo(e.out_lo, orow * e.ldo + c, v);
     } else {
       for (int j = 0; j < 8 && n + j < e.N; ++j) {
         const int nn = n + j, s2 = nn / nf, c2 = nn - s2 * nf, i2 = s2 / r, j2 = s2 - i2 * r;
         const long orow2 = (b * e.psH * r + (long)y * r + i2) * ((long)e.psW * r) + (long)x * r + j2;
         st1(e.out, e.odt, orow2 * e.ldo + c2, v[j]);
         if (e.pre) st1(e.pre, e.pdt, orow2 * e.ldp + c2, pre[j]);
+        if (e.out_lo) e.out_lo[orow2 * e.ldo + c2] = (bf16)(v[j] - (float)(bf16)v[j]);
       }
     }
   } else if (e.omode == KAIR_OUT_PUNSHUF_SPM) {
@@ -495,14 +514,24 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_kernel(Op A, Op B, Epi E, int K
   Raw<CT> vb[PB];
   Pend pa[PA], pb[PB];
   // hi/lo split weights (bf16): K-step kt reads A columns of step kt >> 1 and B columns kt * BK of
-  // the interleaved [hi | lo] rows, so the A chunk is fetched twice from L1/L2 but once from HBM
-  const int sh = (sizeof(CT) == 2 && B.wsplit) ? 1 : 0;
-  const int nk = ((K + BK - 1) / BK) << sh;
-  const int KB = sh ? nk * BK : K;
+  // the interleaved [hi | lo] rows, so the A chunk is fetched twice from L1/L2 but once from HBM.
+  // hi/lo split activations (A.asplit) add a third product per K step, a_lo . w_hi: the lo half
+  // formed from the fp32 source at commit, or read from the lo plane of a bf16 source.
+  const int wsp = (sizeof(CT) == 2 && B.wsplit) ? 1 : 0;
+  const int asp = (sizeof(CT) == 2 && A.asplit) ? 1 : 0;
+  const int NP = 1 + wsp + asp;   // products per K step: (a_hi, w_hi) [, (a_hi, w_lo)] [, (a_lo, w_hi)]
+  const int nks = (K + BK - 1) / BK;
+  const int nk = nks * NP;
+  const int KB = wsp ? 2 * nks * BK : K;
+  bool pend_lo = false;   // the chunk in flight is the lo half of an fp32 A
   auto gload = [&](int kt) {
-    const int ka = (kt >> sh) * BK, kb = kt * BK;
+    const int st = kt / NP, pp = kt - st * NP;
+    const bool alo = asp && pp == NP - 1;
+    const int ka = st * BK, kb = (wsp ? 2 * st + (pp == 1 && !alo) : st) * BK;
+    const void* abase = (alo && sizeof(TA) == 2) ? A.lo_ptr : A.ptr;
+    pend_lo = alo && sizeof(TA) == 4;
 #pragma unroll
-    for (int p = 0; p < PA; ++p) issue_chunk<AM, TA>(A, ra[p], ka + ((tid + p * NT) % CPR) * 8, K, va[p], pa[p]);
+    for (int p = 0; p < PA; ++p) issue_chunk<AM, TA>(A, ra[p], ka + ((tid + p * NT) % CPR) * 8, K, va[p], pa[p], abase);
 #pragma unroll
     for (int p = 0; p < PB; ++p) issue_chunk<AM_ROWS, CT>(B, rb[p], kb + ((tid + p * NT) % CPR) * 8, KB, vb[p], pb[p]);
   };
@@ -512,7 +541,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_kernel(Op A, Op B, Epi E, int K
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
       const int c = tid + p * NT;
-      if (c < CA) commit_chunk<CT, TA>(sA + (c / CPR) * LD + (c % CPR) * 8, va[p], pa[p]);
+      if (c < CA) commit_chunk<CT, TA>(sA + (c / CPR) * LD + (c % CPR) * 8, va[p], pa[p], pend_lo);
     }
 #pragma unroll
     for (int p = 0; p < PB; ++p) {
@@ -1497,7 +1526,7 @@ int launch_ring(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hi
 static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, int N, int K) {
   if (K % RING_BK != 0 || K > 576 || M >= (1L << 30)) return false;
   if (amode != KAIR_LD_ROWS && amode != KAIR_LD_QKVBLK) return false;
-  if (A.rowscale || A.ones_col >= 0) return false;
+  if (A.rowscale || A.ones_col >= 0 || A.asplit || e.out_lo) return false;
   if (amode == KAIR_LD_ROWS && A.ld % 8 != 0) return false;
   if (amode == KAIR_LD_QKVBLK && (A.hdp % 8 != 0)) return false;
   if (B.ld % 8 != 0 || B.ones_col >= 0 || B.wsplit) return false;
@@ -1546,7 +1575,7 @@ constexpr int HC_BM = 96, HC_BN = 192, HC_BK = 64;
 constexpr int HC_HALO_ELEMS = 40960;   // bf16 elements: (RPT + 2) x (XW + 2) x (Cin + 8)
 constexpr int HC_PER = HC_HALO_ELEMS / 8 / 512;
 
-template <typename TA, int EX>
+template <typename TA, int EX, int NPASS>
 __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E, int K, int tilesM) {
   constexpr int WM = 2, WN = 4, TM = HC_BM / WM, TN = HC_BN / WN, RM = TM / 16, RN = TN / 16;
   __shared__ __attribute__((aligned(16))) bf16 sHalo[HC_HALO_ELEMS];
@@ -1557,6 +1586,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
   const int H = A.imH, W = A.imW, C = A.imC;
   const int XW = W < HC_BM ? W : HC_BM, RPT = HC_BM / XW, HWD = XW + 2, HR = RPT + 2, PS = C + 8;
   const int sh = B.wsplit;   // hi/lo split weights: weight chunk j pairs with halo chunk j >> 1
+  // NPASS 2 -- hi/lo split activations (fp32 A, kair_operand.a_split): a second pass over the tile with
+  // the halo refilled by the lo halves bf16(x - bf16(x)) and only the hi weight chunks (the a_lo . w_hi
+  // product), accumulating into the same tile
+  constexpr int npass = NPASS;
   const int cpt = C / HC_BK, nks = (9 * cpt) << sh, c8n = C / 8;
   const int halo_pieces = HR * HWD * c8n;
   const bf16* Bp = (const bf16*)B.ptr;
@@ -1583,11 +1616,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
 #pragma unroll
   for (int jn = 0; jn < RN; ++jn) land(bias4[jn]);
 
-  // weight chunk j (192 rows x 64 k = 24 KiB) -> ring stage j % 3 by LDS-DMA: 3 wave-instructions
+  // weight chunk j (192 rows x 64 k = 24 KiB) -> ring stage js % 3 by LDS-DMA: 3 wave-instructions
   // per wave, each 8 rows x 128 B; source pieces XOR-swizzled by row so the fragment reads are
   // conflict-light.  Rows >= N re-read row N-1: they only feed output columns >= N, never stored.
-  auto bissue = [&](int j) {
-    char* st = (char*)sBw[j % 3];
+  auto bissue = [&](int js, int j) {
+    char* st = (char*)sBw[js % 3];
 #pragma unroll
     for (int ii = 0; ii < 3; ++ii) {
       const int r = (wave * 3 + ii) * 8 + (lane >> 3), q = lane & 7;
@@ -1623,7 +1656,28 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
     const int b = (int)(p0 / ((long)H * W));
     const int rem = (int)(p0 - (long)b * H * W);
     const int y0 = rem / W, x0 = rem - (rem / W) * W;
-    __syncthreads();   // every wave is done reading the previous tile's halo and ring
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 ex[RM][RN];
+    // epilogue operand (fp32 residual): loaded two k-chunks before the end of the last pass, after that
+    // chunk's ring wait, so its latency hides under the last chunks' MFMAs instead of following them
+    // (the younger DMA count is then 0: no chunk is issued after the last one)
+    auto load_resid = [&]() {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < RN; ++jn) {
+          const long m = p0 + wm * TM + i * 16 + fr;
+          const int n = wn * TN + jn * 16 + fq * 4;
+          ex[i][jn] = *(const float4*)(E.resid + m * E.ldr + (n < N ? n : 0));
+        }
+    };
+#pragma unroll
+    for (int pass = 0; pass < npass; ++pass) {
+    const bool last = pass == npass - 1;
+    __syncthreads();   // every wave is done reading the previous tile's (or pass's) halo and ring
     // halo of this tile:
     // all loads first, then the converts and LDS writes
     {
@@ -1656,7 +1710,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
           uint4 q;
           if constexpr (sizeof(TA) == 4) {
             const float4 u = __builtin_bit_cast(float4, lo[i]), v = __builtin_bit_cast(float4, hi[i]);
-            const bf16x8 qq = {(bf16)u.x, (bf16)u.y, (bf16)u.z, (bf16)u.w, (bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+            const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+            bf16x8 qq;
+#pragma unroll
+            for (int e8 = 0; e8 < 8; ++e8) qq[e8] = pass ? (bf16)(f[e8] - (float)(bf16)f[e8]) : (bf16)f[e8];
             q = __builtin_bit_cast(uint4, qq);
           } else {
             q = lo[i];
@@ -1665,7 +1722,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
           if (idx < halo_pieces) {
             const int pix = idx / c8n, c8 = idx - (idx / c8n) * c8n;
             *(uint4*)(sHalo + pix * PS + c8 * 8) = q;
-            if (E.acopy) {   // the tile's own pixels (halo interior): bf16 copy for the weight gradient
+            if (E.acopy && pass == 0) {   // the tile's own pixels (halo interior): bf16 copy for the weight gradient
               const int hr = pix / HWD, hc = pix - (pix / HWD) * HWD;
               if (hr >= 1 && hr <= RPT && hc >= 1 && hc <= XW) {
                 uint4 qc = q;
@@ -1684,40 +1741,25 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
       }
     }
     __syncthreads();   // halo visible
-    bissue(0);
-    if (1 < nks) bissue(1);
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // epilogue operand (fp32 residual): loaded two k-chunks before the end, after that chunk's
-    // ring wait, so its latency hides under the last chunks' MFMAs instead of following them
-    // (the younger DMA count is then 0: no chunk is issued after chunk nks-1)
-    float4 ex[RM][RN];
-    auto load_resid = [&]() {
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int jn = 0; jn < RN; ++jn) {
-          const long m = p0 + wm * TM + i * 16 + fr;
-          const int n = wn * TN + jn * 16 + fq * 4;
-          ex[i][jn] = *(const float4*)(E.resid + m * E.ldr + (n < N ? n : 0));
-        }
-    };
-    for (int j = 0; j < nks; ++j) {
+    // pass 1 (lo halo): the hi weight chunks only, chunk j of the pass = weight chunk j << sh
+    const int nkp = pass ? nks >> sh : nks, wsh = pass ? sh : 0;
+    bissue(0, 0);
+    if (1 < nkp) bissue(1, 1 << wsh);
+    for (int j = 0; j < nkp; ++j) {
       // chunk j landed for this wave (younger: chunk j+1's 3 DMA instructions), then all waves
-      if (j + 1 < nks) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      if (j + 1 < nkp) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       ring_barrier();   // chunk j visible; stage (j+2) % 3 = (j-1) % 3 is free
-      if (j + 2 < nks) bissue(j + 2);
+      if (j + 2 < nkp) bissue(j + 2, (j + 2) << wsh);
       if constexpr (EX == EX_RESID) {
-        if (j == nks - 2) load_resid();
+        if (last && j == nkp - 2) load_resid();
       }
-      compute(j % 3, j);
+      compute(j % 3, j << wsh);
     }
+    }   // pass
     // epilogue: bias (+ act) (+ fp32 residual), 4 consecutive channels per lane
     if constexpr (EX == EX_RESID) {
-      if (nks < 2) load_resid();
+      if ((nks >> (npass - 1 ? sh : 0)) < 2) load_resid();
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -1745,7 +1787,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
           for (int q4 = 0; q4 < 4; ++q4)
             if (n + q4 == E.ones_col) v[q4] = 1.f;
         }
-        if (n < N) st4_any(E.out, E.odt, m * E.ldo + n, v);
+        if (n < N) {
+          st4_any(E.out, E.odt, m * E.ldo + n, v);
+          if (E.out_lo) {
+            const bf16x4 ql = {(bf16)(v[0] - (float)(bf16)v[0]), (bf16)(v[1] - (float)(bf16)v[1]),
+                               (bf16)(v[2] - (float)(bf16)v[2]), (bf16)(v[3] - (float)(bf16)v[3])};
+            *(bf16x4*)(E.out_lo + m * E.ldo + n) = ql;
+          }
+        }
       }
   }
 }
@@ -1755,6 +1804,7 @@ template <typename TA>
 static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, int K) {
   const int H = A.imH, W = A.imW, C = A.imC;
   if (A.up_sh != 0 || C % HC_BK != 0 || C > 192 || K != 9 * C || N > HC_BN || N % 4 != 0) return false;
+  if (A.asplit && sizeof(TA) != 4) return false;   // the two-pass split forms lo from an fp32 image
   if (W <= 0 || H <= 0) return false;
   if (W <= HC_BM) {
     if (HC_BM % W != 0 || H % (HC_BM / W) != 0) return false;
@@ -1768,7 +1818,7 @@ static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, 
   if (e.omode != KAIR_OUT_ROWS || e.win.ws != 0 || e.gate || e.pre || e.resid2 || e.rowscale) return false;
   if (e.ldo % 4 != 0 || ((unsigned long)e.out & 15) || (e.resid && (e.ldr % 4 != 0 || ((unsigned long)e.resid & 15))))
     return false;
-  if (e.acopy && (e.ldac % 8 != 0 || ((unsigned long)e.acopy & 15))) return false;
+  if (e.acopy && (e.ldac % 8 != 0 || e.ldac < C || ((unsigned long)e.acopy & 15))) return false;
   return true;
 }
 
@@ -1791,10 +1841,21 @@ static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int 
   if (g_num_cus == 0) init_num_cus();
   const int tilesM = (int)(M / HC_BM);
   const int grid = tilesM < g_num_cus ? tilesM : g_num_cus;
-  if (E.resid)
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_RESID>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
-  else
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
+  if constexpr (sizeof(TA) == 4) {
+    if (A.asplit) {   // conv_halo_ok: the two-pass split takes an fp32 A only
+      if (E.resid)
+        hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_RESID, 2>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
+      else
+        hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE, 2>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
+      KAIR_CHECK_LAUNCH();
+      return 0;
+    }
+  }
+  if (E.resid) {
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_RESID, 1>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
+  } else {
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE, 1>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
+  }
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1931,6 +1992,15 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
   KAIR_CHECK_ARG(!B->w_split || (compute == KAIR_BF16 && B->ld >= 2L * ((K + 63) / 64) * 64),
                  "gemm_nt: hi/lo split weights need bf16 compute and rows of 2*ceil(K/64)*64 columns");
   KAIR_CHECK_ARG(!A->w_split, "gemm_nt: w_split is a B-operand flag");
+  KAIR_CHECK_ARG(!B->a_split, "gemm_nt: a_split is an A-operand flag");
+  KAIR_CHECK_ARG(!A->a_split || (compute == KAIR_BF16 && (A->mode == KAIR_LD_ROWS || A->mode == KAIR_LD_IM2COL3) &&
+                                 !A->rowscale && A->ones_col < 0 &&
+                                 (A->dtype == KAIR_F32 || (A->lo_ptr && ((uintptr_t)A->lo_ptr % 16) == 0))),
+                 "gemm_nt: a_split needs bf16 compute, a ROWS / IM2COL3 A without rowscale or ones column, and for a "
+                 "bf16 A its 16-byte aligned lo plane");
+  KAIR_CHECK_ARG(!E->out_lo || (E->out_dtype == KAIR_BF16 && (E->out_mode == KAIR_OUT_ROWS || E->out_mode == KAIR_OUT_PSHUF_SPM) &&
+                                ((uintptr_t)E->out_lo % 16) == 0),
+                 "gemm_nt: out_lo needs a bf16 ROWS / PSHUF_SPM output and a 16-byte aligned lo plane");
   KAIR_CHECK_ARG(!E->a_copy || (compute == KAIR_BF16 && A->mode == KAIR_LD_IM2COL3 && A->im_up <= 1),
                  "gemm_nt: a_copy is a side output of the bf16 3x3 conv (no upsample)");
   KAIR_CHECK_ARG((E->out_mode != KAIR_OUT_PSHUF && E->out_mode != KAIR_OUT_PUNSHUF && E->out_mode != KAIR_OUT_PSHUF_NCHW &&

@@ -452,7 +452,9 @@ extern "C" int kair_rowgemm_lnbwd(const void* A, long lda, long M, int K, const 
   RgArgs a;
   if (int rc = rg_common(A, lda, M, K, W, 192, a)) return rc;
   KAIR_CHECK_ARG(x && gamma && mean && rstd && D && part, "rowgemm_lnbwd: null pointer");
-  KAIR_CHECK_ARG(C > 0 && C <= 192 && ldx >= C && ldD >= C, "rowgemm_lnbwd: C %d must be <= 192", C);
+  // the LN epilogue reads and writes all 192 columns of every x / D row (and of every copy row): a
+  // shorter stride would overlap neighbouring rows
+  KAIR_CHECK_ARG(C > 0 && C <= 192 && ldx >= 192 && ldD >= 192, "rowgemm_lnbwd: C %d must be <= 192, ldx / ldD >= 192", C);
   KAIR_CHECK_ARG(M * ldx * 4 < 0x7fffffffL && M * 192 * 2 < 0x7fffffffL, "rowgemm_lnbwd: operands past 2 GiB");
   KAIR_CHECK_ARG(win_ws == 0 || (win_H % win_ws == 0 && win_W % win_ws == 0 && (long)win_H * win_W > 0 &&
                                  M % ((long)win_H * win_W) == 0),
@@ -464,7 +466,7 @@ extern "C" int kair_rowgemm_lnbwd(const void* A, long lda, long M, int K, const 
   a.xbytes = M * ldx * 4; a.dbytes = M * ldD * 4;
   a.wm = make_winmap(win_H, win_W, win_ws, win_shift);
   if (copy && copy->out) {
-    KAIR_CHECK_ARG(copy->dtype == KAIR_BF16 && copy->ld >= C, "rowgemm_lnbwd: the copy is bf16 rows, ld >= C");
+    KAIR_CHECK_ARG(copy->dtype == KAIR_BF16 && copy->ld >= 192, "rowgemm_lnbwd: the copy is bf16 rows, ld >= 192");
     KAIR_CHECK_ARG(copy->win_ws == 0 || (copy->win_H % copy->win_ws == 0 && copy->win_W % copy->win_ws == 0),
                    "rowgemm_lnbwd: copy window geometry");
     a.cp = (bf16*)copy->out; a.ldc = copy->ld; a.cp_scale = copy->rowscale;

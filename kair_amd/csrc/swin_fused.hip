@@ -1308,21 +1308,38 @@ extern "C" int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, c
   a.w1 = (const bf16*)w1; a.b1 = b1; a.u = (bf16*)u; a.hact = (bf16*)h; a.ldh = ldh; a.hd = hd;
   a.w2 = (const bf16*)w2; a.b2 = b2;
   const int rt = w_split ? TOK : 32;   // rows per tile
-  a.rowscale = rowscale; a.tiles_per_scale = rowscale ? rows_per_scale / rt : 1;
-  a.out = out; a.ldout = ldout;
-  a.nTiles = M / rt;
+  a.tiles_per_scale = rowscale ? rows_per_scale / rt : 1;
+  a.ldout = ldout;
   static const int dbg = kair_dbg_env("KAIR_MLP_DBG");
   a.dbg = dbg;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       ncu <= 0)
     ncu = 256;
-  const long grid = a.nTiles < ncu ? a.nTiles : ncu;   // persistent: one workgroup per CU
-  if (w_split)
-    hipLaunchKernelGGL(swin_mlp_fwd_kernel<2>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(swin_mlp_fwd_wr_kernel, dim3((unsigned)grid), dim3(768), 0, (hipStream_t)stream, a);
-  KAIR_CHECK_LAUNCH();
+  // The weight-resident kernel addresses x / out / ln / u / h through buffer resources with 32-bit byte offsets
+  // (num_records 0x7fffffff): launch it over row ranges whose every stream stays below 2^31 bytes, each range
+  // a whole number of tiles and of DropPath scale groups (the rowscale pointer advances with it).
+  long row_bytes = ldx * 4;
+  if (ldout * 4 > row_bytes) row_bytes = ldout * 4;
+  if (ldln * 2 > row_bytes) row_bytes = ldln * 2;
+  if (ldh * 2 > row_bytes) row_bytes = ldh * 2;
+  const long unit = rowscale ? (long)rows_per_scale : (long)rt;
+  const long chunk = ((0x7fffffffL / row_bytes) / unit) * unit;
+  KAIR_CHECK_ARG(chunk > 0, "swin_mlp_fwd: a DropPath scale group exceeds the 2 GiB range of one launch");
+  for (long r0 = 0; r0 < M; r0 += chunk) {
+    const long rows = M - r0 < chunk ? M - r0 : chunk;
+    a.x = x + r0 * ldx; a.out = out + r0 * ldout;
+    a.ln = (bf16*)ln + r0 * ldln; a.mean = mean + r0; a.rstd = rstd + r0;
+    a.u = (bf16*)u + r0 * ldh; a.hact = (bf16*)h + r0 * ldh;
+    a.rowscale = rowscale ? rowscale + r0 / rows_per_scale : nullptr;
+    a.nTiles = rows / rt;
+    const long grid = a.nTiles < ncu ? a.nTiles : ncu;   // persistent: one workgroup per CU
+    if (w_split)
+      hipLaunchKernelGGL(swin_mlp_fwd_kernel<2>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(swin_mlp_fwd_wr_kernel, dim3((unsigned)grid), dim3(768), 0, (hipStream_t)stream, a);
+    KAIR_CHECK_LAUNCH();
+  }
   return 0;
 }
 

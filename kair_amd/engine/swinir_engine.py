@@ -125,9 +125,12 @@ class _Conv:
     bf16 weight rounding shifts every output pixel by the same sum(dW * a) and biases PSNR
     (DESIGN.md "parity at bf16"); activation rounding is unbiased and averages out."""
 
-    def __init__(self, eng, mod, Cop, Cip, need_dgrad=True, split=None, n_perm=0):
+    def __init__(self, eng, mod, Cop, Cip, need_dgrad=True, split=None, n_perm=0, tied_in=False):
         """n_perm = r*r: output channels stored sub-pixel-major for a following PixelShuffle(r)
-        (kair_wmap.n_perm; the KAIR_OUT_PSHUF_SPM / PUNSHUF_SPM epilogues store 16 bytes at a time)."""
+        (kair_wmap.n_perm; the KAIR_OUT_PSHUF_SPM / PUNSHUF_SPM epilogues store 16 bytes at a time).
+        tied_in: the forward form repeats the input channels in both halves of Cip (kair_wmap kG = 2),
+        for an input held as a hi/lo pair in channels [0, Ci) and [Cip/2, Cip/2 + Ci)
+        (kair_image_to_nhwc_hilo); the weight gradient keeps the plain map (the hi channels)."""
         self.w, self.b = mod.weight, mod.bias
         Co, Ci = self.w.shape[:2]
         self.Co, self.Ci, self.Cop, self.Cip = Co, Ci, Cop, Cip
@@ -136,7 +139,8 @@ class _Conv:
         self.split = bool(split) and eng.tdt == torch.bfloat16
         self.n_perm = n_perm
         self.map = H.wmap(1, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
-        self.mapf = H.wmap(9, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm) if self.split else self.map
+        kf_grp = (2, Ci, Cip // 2) if tied_in else (1, Ci, Cip)
+        self.mapf = H.wmap(9 if self.split else 1, Co, Ci, (1, Co, Cop), kf_grp, n_perm=n_perm)
         self.mapd = H.wmap(2, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
         self.mapb = H.wmap(4, Co, 0, (1, Co, Cop), (1, 1, 1), n_perm=n_perm)
         dev = self.w.device
@@ -206,10 +210,15 @@ class _Blk:
 
 class SwinIREngine:
     def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True, fused_mlp=None,
-                 split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=0, side_priority=0):
+                 split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=0, side_priority=0,
+                 split_act=True):
         """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
         see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
         fused block kernels (_Lin, pack kind 12).
+        split_act (bf16 only): the forward convs also read their input activation as a hi/lo bf16
+        pair (kair_operand.a_split: the input image, every RSTB / conv_after_body conv input and the
+        reconstruction tail's activations), the operand roundings that move the evaluation PSNR
+        (tools/drift_ablation.py, DESIGN.md "parity at bf16"); the Swin-block internals stay bf16.
         fused_blocks (bf16 only): each Swin block's attention half and MLP half run as one kernel
         each (kair_swin_attn_fwd, kair_swin_mlp_fwd) where the geometry allows it (6 heads,
         Cp = 192, hidden padded to 384); fused_mlp (default: fused_blocks) selects the MLP-half
@@ -220,6 +229,7 @@ class SwinIREngine:
         self.cd = H.BF16 if compute_dtype == "bf16" else H.F32
         self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
         self.split_conv = bool(split_conv) and compute_dtype == "bf16"
+        self.split_act = bool(split_act) and compute_dtype == "bf16"
         self.C = net.embed_dim
         heads = {l.residual_group.blocks[0].num_heads for l in net.layers}
         if len(heads) != 1:
@@ -258,11 +268,13 @@ class SwinIREngine:
         self.in_ch = net.conv_first.in_channels
         self.img_range = float(net.img_range)
         self.Cin_p = 8
+        # split_act: the input image as a hi/lo pair in channels [0, in_ch) / [4, 4 + in_ch) of Cin_p
+        self.xin_hilo = self.split_act and 2 * self.in_ch <= self.Cin_p
         self.device = net.conv_first.weight.device
         dev = self.device
         self.mean = net.mean.view(-1).to(dev, torch.float32).contiguous()
         # layer objects
-        self.conv_first = _Conv(self, net.conv_first, self.Cp, self.Cin_p, need_dgrad=False)
+        self.conv_first = _Conv(self, net.conv_first, self.Cp, self.Cin_p, need_dgrad=False, tied_in=self.xin_hilo)
         self.pe_norm = net.patch_embed.norm
         self.rstb = []
         for layer in net.layers:
@@ -416,6 +428,9 @@ class SwinIREngine:
                 acts.append(e(hw, nf, dt=T))
             P["ups_act"] = acts
             P["M_hr"] = hw
+            if self.split_act:   # lo planes of the tail activations (hi: a0 / ups_act, the backward's operands)
+                P["a0_lo"] = e(M, nf, dt=T)
+                P["ups_lo"] = [torch.empty_like(a) for a in acts]
         elif self.upsampler == "nearest+conv":
             nf = 64
             P["a0"] = e(M, nf, dt=T)
@@ -430,7 +445,11 @@ class SwinIREngine:
         if infer:
             return P
         # backward scratch
-        P["D"], P["G"] = e(M, Cp), e(M, Cp)
+        # residual-gradient rows: zero-filled once, so their pad columns [C, Cp) are finite zeros.  The LN row
+        # GEMMs write all Cp columns of their bf16 operand copies (scale * D's pad) and the gate / store
+        # contractions read them: a NaN bit pattern left in a pad column would become 0 * NaN = NaN
+        z32 = lambda *s: torch.zeros(*s, device=dev, dtype=f32)
+        P["D"], P["G"] = z32(M, Cp), z32(M, Cp)
         P["dxn"] = e(M, Cp, dt=T)
         if self.fused_mlp_bwd:
             P["mlp_ws"] = e(H.swin_mlp_bwd_ws())
@@ -438,7 +457,7 @@ class SwinIREngine:
         # RSTB's grouped weight-gradient launch (Dm: s_mlp * dL/dout, token order; Da: s_attn * dL/dmid,
         # window order -- the compute-dtype copies LayerNorm backward writes; dU: fc1 pre-activation
         # gradient; dqkv: head-blocked q/k/v gradient)
-        # (zero-filled: the LayerNorm-backward copies write the C real columns only, the GEMMs read Cp)
+        # (zero-filled: kair_layernorm_bwd's copies write the C real columns only, the GEMMs read Cp)
         depth = max(len(blks) for blks, _ in self.rstb)
         z = lambda *s: torch.zeros(*s, device=dev, dtype=T)
         # Two sets (RSTB parity): the side stream still reads one RSTB's while the next RSTB writes the other.
@@ -447,7 +466,7 @@ class SwinIREngine:
                      # by one grouped launch each at the end of the RSTB
                      "ln1p": e(2 * 2048 * Cp), "ln2p": e(2 * 2048 * Cp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
                     for _ in range(depth)] for _ in range(2)]
-        P["G3"] = e(M, Cp)   # third residual-gradient buffer (rotation, see backward())
+        P["G3"] = z32(M, Cp)   # third residual-gradient buffer (rotation, see backward())
         if self.rowgemm:   # LayerNorm-parameter partial rows the fused row GEMMs leave (<= the ln*p buffers' 2048)
             P["rg_nb"] = {k: H.rowgemm_ln_blocks(M, k) for k in (Hdp, 3 * nh * 32)}
             assert max(P["rg_nb"].values()) <= 2048, P["rg_nb"]
@@ -549,7 +568,10 @@ class SwinIREngine:
         self.cur = P
         P["x"] = x
         P["drop"] = drop_scales
-        H.image_to_nhwc(x, P["xin"], self.Cin_p, self.mean, self.img_range, B, self.in_ch, Hh, Ww)
+        if self.xin_hilo:
+            H.image_to_nhwc_hilo(x, P["xin"], self.Cin_p, self.mean, self.img_range, B, self.in_ch, Hh, Ww)
+        else:
+            H.image_to_nhwc(x, P["xin"], self.Cin_p, self.mean, self.img_range, B, self.in_ch, Hh, Ww)
         c = self.conv_first
         H.gemm_nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), c.fwd(), H.epilogue(P["f0"], bias=c.bp), M, Cp,
                   9 * self.Cin_p, cd)
@@ -576,8 +598,8 @@ class SwinIREngine:
         if not isinstance(r, _Resi3):
             # training: the halo conv also leaves the bf16 weight-gradient operand (1.0 in channel C)
             ac = (P["conv_bf"][id(r)][1], self.C) if P.get("conv_halo") else None
-            H.gemm_nt(H.im2col(src, Hh, Ww, Cp), r.fwd(), H.epilogue(out, bias=r.bp, resid=resid, acopy=ac), M, Cp,
-                      9 * Cp, cd)
+            H.gemm_nt(self._ain(H.im2col(src, Hh, Ww, Cp)), r.fwd(), H.epilogue(out, bias=r.bp, resid=resid, acopy=ac), M,
+                      Cp, 9 * Cp, cd)
             return
         t1, t2 = P["r3"][id(r)]
         lk = dict(act=H.ACT_LEAKY, slope=0.2)
@@ -616,20 +638,29 @@ class SwinIREngine:
         self._bias_colsum(P, H.rows(dz1), M, q, r.c1.mapb, g(r.c1.b))
         return None
 
+    def _ain(self, op, lo=None):
+        """A forward conv's input operand: a hi/lo pair under split_act (fp32 source: lo formed in the
+        kernel; bf16 source: its lo plane `lo`), else as is."""
+        return H.asplit(op, lo) if self.split_act else op
+
     def _forward_tail(self, P):
         """Reconstruction tail: P['fb'] (conv_after_body + residual) -> P['E']."""
         cd, Cp, M, B, Hh, Ww = self.cd, self.Cp, P["M"], P["B"], P["H"], P["W"]
+        sa = self.split_act
         if self.upsampler == "pixelshuffle":
             c = self.cbu
-            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
-                      H.epilogue(P["a0"], bias=c.bp, act=H.ACT_LEAKY, slope=0.01), M, 64, 9 * Cp, cd)
-            src, h, w = P["a0"], Hh, Ww
-            for c, r, dst in zip(self.ups, self.ups_r, P["ups_act"]):
-                H.gemm_nt(H.im2col(src, h, w, 64), c.fwd(), H.epilogue(dst, mode=H.OUT_PSHUF_SPM, ldo=64, bias=c.bp,
-                                                                            ps=(r, h, w)), B * h * w, c.Co, 9 * 64, cd)
-                src, h, w = dst, h * r, w * r
+            H.gemm_nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
+                      H.epilogue(P["a0"], bias=c.bp, act=H.ACT_LEAKY, slope=0.01, out_lo=P["a0_lo"] if sa else None), M, 64,
+                      9 * Cp, cd)
+            src, src_lo, h, w = P["a0"], P.get("a0_lo"), Hh, Ww
+            for i, (c, r, dst) in enumerate(zip(self.ups, self.ups_r, P["ups_act"])):
+                dst_lo = P["ups_lo"][i] if sa else None
+                H.gemm_nt(self._ain(H.im2col(src, h, w, 64), src_lo), c.fwd(),
+                          H.epilogue(dst, mode=H.OUT_PSHUF_SPM, ldo=64, bias=c.bp, ps=(r, h, w), out_lo=dst_lo),
+                          B * h * w, c.Co, 9 * 64, cd)
+                src, src_lo, h, w = dst, dst_lo, h * r, w * r
             c = self.last
-            H.gemm_nt(H.im2col(src, h, w, 64), c.fwd(),
+            H.gemm_nt(self._ain(H.im2col(src, h, w, 64), src_lo), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(self.mean, self.img_range, self.in_ch, h, w)),
                       B * h * w, c.Cop, 9 * 64, cd)
         elif self.upsampler == "nearest+conv":
@@ -652,12 +683,12 @@ class SwinIREngine:
         elif self.upsampler in (None, ""):
             # x/range + mean with x = (x_in - mean) * range + conv_last(res)  ==  x_in + conv_last(res) / range
             c = self.last
-            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
+            H.gemm_nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, resid=P["x"],
                                  img=(None, self.img_range, self.in_ch, Hh, Ww)), M, c.Cop, 9 * Cp, cd)
         else:
             c = self.up1
-            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
+            H.gemm_nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_PSHUF_NCHW, ldo=0, bias=c.bp, ps=(self.scale, Hh, Ww),
                                  img=(self.mean, self.img_range, self.in_ch, Hh, Ww)), M, c.Cop, 9 * Cp, cd)
         return P["E"]

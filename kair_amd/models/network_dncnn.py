@@ -80,7 +80,7 @@ class _Base(nn.Module):
 class DnCNN(_Base):
     """network_dncnn.py:40-71: out = x - model(x)."""
 
-    def __init__(self, in_nc=1, out_nc=1, nc=64, nb=17, act_mode="BR", compute_dtype="bf16"):
+    def __init__(self, in_nc=1, out_nc=1, nc=64, nb=17, act_mode="BR", compute_dtype="fp32"):
         super().__init__(in_nc, out_nc, nc, nb, act_mode, compute_dtype)
 
 
@@ -88,5 +88,5 @@ class FDnCNN(_Base):
     """network_dncnn.py:128-149: out = model(x) (x carries the noise-level map channel)."""
     residual = False
 
-    def __init__(self, in_nc=2, out_nc=1, nc=64, nb=20, act_mode="R", compute_dtype="bf16"):
+    def __init__(self, in_nc=2, out_nc=1, nc=64, nb=20, act_mode="R", compute_dtype="fp32"):
         super().__init__(in_nc, out_nc, nc, nb, act_mode, compute_dtype)

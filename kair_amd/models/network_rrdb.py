@@ -48,7 +48,7 @@ class ShortcutBlock(nn.Module):
 
 class RRDB(nn.Module):
     def __init__(self, in_nc=3, out_nc=3, nc=64, nb=23, gc=32, upscale=4, act_mode="L", upsample_mode="upconv",
-                 compute_dtype="bf16"):
+                 compute_dtype="fp32"):
         super().__init__()
         if "R" not in act_mode and "L" not in act_mode:
             raise AssertionError("Examples of activation function: R, L, BR, BL, IR, IL")

@@ -63,7 +63,7 @@ def make_layer(block, n_layers):
 class RRDBNet(nn.Module):
     """network_rrdbnet.py:78-119."""
 
-    def __init__(self, in_nc=3, out_nc=3, nf=64, nb=23, gc=32, sf=4, compute_dtype="bf16"):
+    def __init__(self, in_nc=3, out_nc=3, nf=64, nb=23, gc=32, sf=4, compute_dtype="fp32"):
         super().__init__()
         self.sf = sf
         self.conv_first = nn.Conv2d(in_nc, nf, 3, 1, 1, bias=True)

@@ -71,7 +71,7 @@ class USRNet(nn.Module):
     'bf16' MFMA operands with fp32 accumulation, or 'fp32' exact-MFMA parity mode)."""
 
     def __init__(self, n_iter=8, h_nc=64, in_nc=4, out_nc=3, nc=(64, 128, 256, 512), nb=2, act_mode="R",
-                 downsample_mode="strideconv", upsample_mode="convtranspose", compute_dtype="bf16"):
+                 downsample_mode="strideconv", upsample_mode="convtranspose", compute_dtype="fp32"):
         super().__init__()
         self.d = DataNet()
         self.p = ResUNet(in_nc=in_nc, out_nc=out_nc, nc=nc, nb=nb, act_mode=act_mode, downsample_mode=downsample_mode,

@@ -7,8 +7,11 @@ reference's define_G knows (ffdnet, srmd, dpsr, msrresnet*, imdn, drunet, vrt, r
 scope for this build and raises NotImplementedError naming the type.
 """
 import functools
+import logging
 
 from torch.nn import init
+
+logger = logging.getLogger("kair_amd")
 
 _ON_PATH = ("swinir", "dncnn", "fdncnn", "rrdb", "rrdbnet", "usrnet")
 
@@ -45,6 +48,9 @@ def define_G(opt):
     else:
         raise NotImplementedError("netG [{:s}] is not on the kair_amd MI355X path (supported: {})".format(
             t, ", ".join(_ON_PATH)))
+    logger.info("define_G: %s on the %s engine (%s)", t, ek["compute_dtype"],
+                "netG.compute_dtype" if o.get("compute_dtype") else
+                ("train.amp_enabled" if (opt.get("train") or {}).get("amp_enabled") else "reference default"))
     if opt.get("is_train"):
         init_weights(net, init_type=o.get("init_type", "default") or "default",
                      init_bn_type=o.get("init_bn_type", "uniform") or "uniform", gain=o.get("init_gain", 1) or 1)

@@ -21,7 +21,7 @@ def main():
     dev = torch.device("cuda")
     torch.manual_seed(0)
     net = SwinIR(upscale=4, in_chans=3, img_size=48, window_size=8, img_range=1.0, depths=[2], embed_dim=180,
-                 num_heads=[6], mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.1).to(dev).train()
+                 num_heads=[6], mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.1, compute_dtype="bf16").to(dev).train()
     eng = net.engine()
     x = torch.rand(B, 3, 48, 48, device=dev)
     eng.forward(x, torch.ones(len(eng.blocks), 2, B, device=dev))

@@ -42,17 +42,17 @@ def run(name, steps, warmup, dev):
     g = torch.Generator().manual_seed(1)
     if name == "dncnn":
         from kair_amd.models.network_dncnn import DnCNN
-        mk = lambda: DnCNN(1, 1, 64, 17, "BR")   # noqa: E731
+        mk = lambda: DnCNN(1, 1, 64, 17, "BR", compute_dtype="bf16")   # noqa: E731
         B, shp, sc = 64, (1, 40, 40), 1
     elif name == "swinir_light":
         from kair_amd.models.network_swinir import SwinIR
         mk = lambda: SwinIR(upscale=2, in_chans=3, img_size=64, window_size=8, img_range=1.0, depths=[6] * 4,   # noqa: E731
                             embed_dim=60, num_heads=[6] * 4, mlp_ratio=2, upsampler="pixelshuffledirect",
-                            resi_connection="1conv")
+                            resi_connection="1conv", compute_dtype="bf16")
         B, shp, sc = 64, (3, 64, 64), 2
     elif name == "rrdbnet":
         from kair_amd.models.network_rrdbnet import RRDBNet
-        mk = lambda: RRDBNet(3, 3, 64, 23, 32, 4)   # noqa: E731
+        mk = lambda: RRDBNet(3, 3, 64, 23, 32, 4, compute_dtype="bf16")   # noqa: E731
         B, shp, sc = 16, (3, 32, 32), 4
     elif name == "usrnet":
         return run_usrnet(steps, warmup, dev)
@@ -70,7 +70,7 @@ def run(name, steps, warmup, dev):
 def run_usrnet(steps, warmup, dev):
     from kair_amd.engine.trainer import FusedTrainer
     from kair_amd.models.network_usrnet import USRNet
-    net = USRNet(n_iter=6, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2).to(dev).train()
+    net = USRNet(n_iter=6, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2, compute_dtype="bf16").to(dev).train()
     tr = FusedTrainer(net, None, lr=1e-4, E_decay=0.0, use_graph=True)   # train_usrnet.json: E_decay 0
     g = torch.Generator().manual_seed(2)
     B, lq, sf = 48, 128, 4
