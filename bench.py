@@ -24,6 +24,11 @@ sys.path.insert(0, ROOT)
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, Chip-level parameters)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
+PRECISION_BF16 = ("bf16 MFMA with fp32 accumulation; every forward conv multiplies hi/lo bf16 pairs of its weights AND "
+                  "its input activation (~16-bit operands: the input image, RSTB / conv_after_body inputs, the "
+                  "reconstruction tail), Swin-block GEMM operands bf16; fp32 master weights, residual stream, "
+                  "LayerNorm statistics, softmax and Adam + EMA.  Holds the PSNR bar (psnr fields; "
+                  "tests/test_swinir_gpu.py::test_swinir_classical_full_bf16_psnr_along_training, 160 steps)")
 
 
 def build_net(dtype, drop_path=0.1, seed=0):
@@ -104,8 +109,11 @@ _TIMED = ("gemm_nt", "gemm_tn", "wgrad_finalize", "colsum", "layernorm_fwd", "la
           "swin_attn_fwd", "swin_mlp_fwd", "rowgemm_store", "rowgemm_gate", "rowgemm_lnbwd")
 
 
-def time_roles(tr):
-    """{role: {kernel, launches, ms (mean in-step), bytes, flops}} over one eager fwd + loss + bwd."""
+def time_roles(tr, serial=False):
+    """{role: {kernel, launches, ms (mean in-step), bytes, flops}} over one eager fwd + loss + bwd.
+    serial: the engine's deferred side-stream work runs in place on the main stream for this pass, so
+    every event pair brackets exactly one kernel (its duration, as rocprofv3's kernel trace reports it)
+    instead of its in-step time behind concurrent side-stream work."""
     from kair_amd import _hip as H
     rec = []
 
@@ -122,6 +130,10 @@ def time_roles(tr):
 
     orig = {n: getattr(H, n) for n in _TIMED}
     run0 = H.WgradGroup.run
+    eng = getattr(tr, "engine", None)
+    side0 = getattr(eng, "side_stream", None)
+    if serial and side0 is not None:
+        eng.side_stream = False
 
     def wg_run(self, ws, **kw):
         fr = sys._getframe(1)
@@ -142,6 +154,8 @@ def time_roles(tr):
         for n in _TIMED:
             setattr(H, n, orig[n])
         H.WgradGroup.run = run0
+        if serial and side0 is not None:
+            eng.side_stream = side0
     out = {}
     for role, name, a, e0, e1 in rec:
         d = out.setdefault(role, {"kernel": name, "launches": 0, "ms_total": 0.0, "bytes": _alg_bytes(name, a),
@@ -207,10 +221,11 @@ def cpu_baseline(batch=4, steps=4):
                       f"{steps} timed steps after 1 warm-up, torch CPU {threads} threads"}
 
 
-def fp32_line(bpg, device, drop_path, steps=12, warmup=3):
-    """Throughput of the same training step on the exact-fp32 engine (fp32 MFMA, same kernels and
-    program): the parity configuration, whose forward matches the CPU oracle to 1e-7 dB.  A short
-    run (the fp32 step is ~10x the bf16 one), timed like the headline."""
+def fp32_line(bpg, device, drop_path, steps, warmup, roles=True):
+    """Throughput of the same training step on the exact-fp32 engine (fp32 MFMA, same program): the
+    reference's own arithmetic, whose forward matches the CPU oracle to 1e-7 dB.  Timed like the
+    headline (--steps / --warmup, same batch), with its MFMA roofline (train FLOPs / step time vs the
+    dense fp32 MFMA peak) and its longest kernels."""
     from kair_amd.engine.trainer import FusedTrainer
     from kair_amd.utils.utils_image import synth_sr_batch
     net = build_net("fp32", drop_path).to(device).train()
@@ -226,10 +241,22 @@ def fp32_line(bpg, device, drop_path, steps=12, warmup=3):
         tr.step(L, Hh)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    from kair_amd.engine.swinir_engine import swinir_flops
+    tf = swinir_flops(net, 48, 48)["train"] * bpg * steps / dt / 1e12
+    top = []
+    if roles:
+        rs = time_roles(tr, serial=True)
+        for k, v in sorted(rs.items(), key=lambda kv: -kv[1]["ms_total"])[:5]:
+            top.append({"role": k, "kernel": v["rocprof"], "launches_per_step": v["launches"], "kernel_ms": round(v["ms"], 5),
+                        "step_ms_total": round(v["ms_total"], 4)})
     del tr, net, ema
     return {"value": round(bpg * steps / dt, 2), "unit": "patches/s", "ms_per_step": round(1000 * dt / steps, 3),
             "steps": steps, "warmup": warmup, "dtype": "fp32", "per_gpu_batch": bpg,
-            "note": "parity configuration (exact-f32 MFMA engine); the headline value is the bf16 engine"}
+            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / PEAK_F32_TFLOPS, 4),
+                         "what": "whole training step: train FLOPs per patch (swinir_flops) x patches/s vs dense fp32 MFMA"},
+            "kernels_by_duration": top,
+            "note": "the reference's arithmetic (exact-f32 MFMA engine); the headline is the split-operand bf16 engine"}
 
 
 def psnr_parity(net_gpu, device, n_eval=8):
@@ -471,19 +498,25 @@ def main():
     ms_step = 1000.0 * wall / args.steps
     step_tflops = fl["train"] * gbatch / (wall / args.steps) / 1e12 / world   # per GPU
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
-    roles = {}
+    roles, serial = {}, {}
     if not args.no_roles:
         try:
             roles = time_roles(tr)
+            serial = time_roles(tr, serial=True)
         except Exception as e:  # noqa: BLE001
-            roles = {"error": {"kernel": repr(e), "ms_total": 0.0}}
+            roles = serial = {"error": {"kernel": repr(e), "ms_total": 0.0}}
     peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    TIMING = {"in_step": "in-step mean over the step's launches of this role: one eager fwd+loss+bwd, a HIP event pair "
+                         "on the launch stream around each launch (side-stream concurrency kept, so a launch queued "
+                         "behind side-stream work includes that wait)",
+              "serial": "kernel duration: mean over the step's launches of this role in one eager fwd+loss+bwd with the "
+                        "deferred side-stream work run in place, a HIP event pair around each launch on its stream (the "
+                        "quantity rocprofv3 --kernel-trace reports per dispatch)"}
 
-    def roof(role, d):
+    def roof(role, d, timing="in_step"):
         r = {"bound": "hbm", "kernel": d["rocprof"], "role": role, "launches_per_step": d["launches"],
              "kernel_ms": round(d["ms"], 5), "step_ms_total": round(d["ms_total"], 4),
-             "kernel_ms_timing": "in-step mean over the step's launches of this role: one eager fwd+loss+bwd, a HIP "
-                                 "event pair on the launch stream around each launch (side-stream concurrency kept)"}
+             "kernel_ms_timing": TIMING[timing]}
         if d.get("bytes"):
             gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
             r.update({"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
@@ -495,6 +528,8 @@ def main():
             r.update({"flops_per_launch": d["flops"], "achieved_tflops": round(tf, 2), "mfma_frac": round(tf / peak, 4)})
         return r
     ranked = sorted(((k, v) for k, v in roles.items() if k != "error"), key=lambda kv: -kv[1]["ms_total"])
+    ranked_serial = sorted(((k, v) for k, v in serial.items() if k != "error" and v.get("bytes")),
+                           key=lambda kv: -kv[1]["ms_total"])
     # attention GEMMs (QKV / q.k^T / p.v / proj): the fused attention half, the attention backward, the proj and
     # q/k/v input-gradient row GEMMs -- FLOPs over their in-step time against the dense bf16 MFMA peak
     att_names = ("swin_attn_fwd_kernel", "attn_bwd_bf16_kernel", "rowgemm_kernel<12, 4, 2, 0>", "rowgemm_kernel<36")
@@ -511,6 +546,7 @@ def main():
         "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
         "dtype": args.dtype,
+        "precision": (PRECISION_BF16 if args.dtype == "bf16" else "fp32 operands, exact fp32 MFMA (v_mfma_f32_16x16x4_f32)"),
         "data": ("synthetic: per step a fresh batch synthesised on the GPU (crop / augment / MATLAB bicubic) from "
                  "a 64-image 256x256 HR pool resident in HBM (SURVEY §8d recipe)" if args.data == "pool" else
                  "synthetic (one seeded bicubic-LR / HR batch resident in HBM, SURVEY §8d)"),
@@ -518,7 +554,11 @@ def main():
                    "global_batch": gbatch, "per_gpu_batch": bpg, "lq": 48, "hr": 192, "embed_dim": 180,
                    "depths": [6] * 6, "heads": 6, "window": 8, "drop_path_rate": args.drop_path,
                    "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
-        "roofline": roof(*ranked[0]) if ranked else {"error": roles.get("error", {}).get("kernel", "roles skipped")},
+        # roofline: the step's dominant kernel by summed kernel duration (rocprof's dominant kernel); the
+        # in-step view (waits behind the side stream included) ranks the roles in kernels_in_step
+        "roofline": (roof(*ranked_serial[0], timing="serial") if ranked_serial else
+                     {"error": serial.get("error", {}).get("kernel", "roles skipped")}),
+        "kernels_by_duration": [roof(k, v, timing="serial") for k, v in ranked_serial[:8]],
         "kernels_in_step": [roof(k, v) for k, v in ranked[:8]],
         "attention_gemm_mfma": att_mfma,
         "step_roofline": {"train_flop_per_patch": fl["train"], "achieved_tflops_per_gpu": round(step_tflops, 2),
@@ -528,7 +568,8 @@ def main():
     }
     if args.dtype == "bf16" and world == 1 and not args.no_fp32_line:
         try:
-            out["fp32_parity_line"] = fp32_line(bpg, device, args.drop_path)
+            out["fp32_parity_line"] = fp32_line(bpg, device, args.drop_path, args.steps, args.warmup,
+                                                roles=not args.no_roles)
         except Exception as e:  # noqa: BLE001
             out["fp32_parity_line"] = {"error": repr(e)}
     try:
