@@ -106,7 +106,8 @@ def _alg_flops(fn, a):
 
 _TIMED = ("gemm_nt", "gemm_tn", "wgrad_finalize", "colsum", "layernorm_fwd", "layernorm_bwd", "row_copy", "window_attn_fwd",
           "window_attn_bwd", "ln_param_reduce_grouped", "attn_dtable_grouped", "image_to_nhwc", "l1_loss", "axpy",
-          "swin_attn_fwd", "swin_mlp_fwd", "rowgemm_store", "rowgemm_gate", "rowgemm_lnbwd")
+          "swin_attn_fwd", "swin_mlp_fwd", "rowgemm_store", "rowgemm_gate", "rowgemm_lnbwd", "image_to_nhwc_hilo",
+          "conv3x3_narrow_fwd", "conv3x3_narrow_dgrad", "conv3x3_narrow_wgrad")
 
 
 def time_roles(tr, serial=False):

@@ -64,12 +64,16 @@ typedef struct {
                           2*ceil(K/64)*64.  The A operand is read once per pair, so the product
                           carries ~16 mantissa bits of the fp32 master weights (bf16 weight
                           rounding biases the output, see DESIGN.md "parity at bf16")        */
-  int a_split;         /* kair_gemm_nt A only (bf16 compute, ROWS / IM2COL3, no rowscale): the
+  int a_split;         /* kair_gemm_nt A only (bf16 compute).  1 (ROWS / IM2COL3, no rowscale): the
                           activation enters the product as a hi/lo bf16 pair, x = hi + lo with
                           lo = bf16(x - hi), adding the product a_lo . w_hi (with w_split also
                           a_hi . w_lo): ~16 mantissa bits of the activation instead of 8.
                           fp32 A: lo is formed in the kernel from the fp32 value; bf16 A: ptr
-                          holds the hi plane and lo_ptr the lo plane (same layout)           */
+                          holds the hi plane and lo_ptr the lo plane (same layout).
+                          2 (bf16 IM2COL3 with w_split): the image's im_C channels are the [hi | lo]
+                          halves of one activation and B is packed tied over both halves (kair_wmap
+                          kG = 2), so the plain product is already the split one; the flag lets
+                          the 3x3 halo kernel skip the negligible lo . w_lo chunk products   */
   const void* lo_ptr;  /* bf16 A with a_split: the lo plane (kair_epilogue.out_lo of its producer) */
 } kair_operand;
 
@@ -166,7 +170,10 @@ typedef struct {
                           with k = 32kb' + l%32 (output), n = 16kb + 8(l/32) + j (contraction);
                         14 linear in v_mfma_f32_16x16x32 fragment order [Np/16][Kp/32][64][8]: the
                           operand of rows 16nb.. and k-step kb is one contiguous 1 KiB block (lane l:
-                          row 16nb + l%16, k 32kb + 8(l/16) + j) */
+                          row 16nb + l%16, k 32kb + 8(l/16) + j);
+                        15 conv3x3 forward in the kind-14 fragment order with hi/lo halves (bf16 only):
+                          [Np/16][9*Kp/32][2][64][8], contraction index k = tap*Kp + cip (the
+                          narrow-N conv's register-resident weights, kair_conv3x3_narrow_fwd) */
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
   int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp (kinds 1 / 9 only: kG*kGr
@@ -341,6 +348,27 @@ int kair_swin_mlp_bwd(const void* dc, long lddc, const void* gd, long ldg, const
                       const float* rstd, int C, float* D, long ldD, void* dco, long lddo, const float* rowscale,
                       int rows_per_scale, int H, int W, int shift, float* dgamma, float* dbeta, int dparam_acc,
                       float* ws, long M, int Cp, int Hp, void* stream);
+
+/* Narrow-output 3x3 convs (csrc/tail.hip): a 64-channel NHWC bf16 image <-> NR <= 4 output channels,
+ * the last conv of the reconstruction head (network_swinir.py:745, :817 conv_last).
+ * fwd:   out NCHW [B][NR][H][W] = conv(x) + bias, / img_range + mean (mean may be NULL; resid, optional,
+ *        an NCHW image added last).  x rows [B*H*W][ldx]: channels [0, 64) = hi, and with lo_off > 0 the
+ *        lo halves at [lo_off, lo_off + 64) (split activations); w = pack kind 15 of the conv weight
+ *        (hi/lo split, Np = 16).  W % 64 == 0 for all three (64-pixel row segments).
+ * dgrad: dX = conv^T(dE): dE rows [B*H*W][lde] bf16 (channels [0, NR)), w the fp32 reference weight
+ *        [NR][64][3][3] (re-laid into ws, kair_conv3x3_narrow_dgrad_ws() floats, by the same call); out rows [B*H*W][ldo] (ps_r <= 1) or, with ps_r = r, the PixelUnshuffle(r)
+ *        sub-pixel-major layout of the previous conv's pre-shuffle rows (KAIR_OUT_PUNSHUF_SPM).
+ * wgrad: grad_w [NR][64][3][3] (and grad_b [NR] if non-NULL) = / += (accumulate) sum over pixels, from
+ *        per-workgroup partials in ws (kair_conv3x3_narrow_wgrad_ws(NR) floats) summed in fixed order. */
+int kair_conv3x3_narrow_fwd(const void* x, long ldx, int lo_off, const void* w, const float* bias, int NR,
+                            const float* mean, float img_range, const float* resid, float* out, int B, int H, int W,
+                            void* stream);
+long kair_conv3x3_narrow_dgrad_ws(void);
+int kair_conv3x3_narrow_dgrad(const void* dE, long lde, const float* w, int NR, void* ws, void* out, int out_dtype,
+                              long ldo, int ps_r, int B, int H, int W, void* stream);
+long kair_conv3x3_narrow_wgrad_ws(int NR);
+int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x, long ldx, int NR, float* ws, float* grad_w,
+                              float* grad_b, int accumulate, int B, int H, int W, void* stream);
 
 /* Elementwise / small kernels ------------------------------------------------------------- */
 /* NCHW fp32 image -> NHWC (dtype) with channel stride ldc, x' = (x - mean[c]) * img_range

@@ -124,6 +124,12 @@ _SIGS = {
                                 c_int, c_int, c_float, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "kair_image_to_nhwc": [c_vp, c_vp, c_int, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
     "kair_image_to_nhwc_hilo": [c_vp, c_vp, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
+    "kair_conv3x3_narrow_fwd": [c_vp, c_long, c_int, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_vp, c_int, c_int, c_int,
+                                c_vp],
+    "kair_conv3x3_narrow_dgrad_ws": [],
+    "kair_conv3x3_narrow_dgrad": [c_vp, c_long, c_vp, c_int, c_vp, c_vp, c_int, c_long, c_int, c_int, c_int, c_int, c_vp],
+    "kair_conv3x3_narrow_wgrad_ws": [c_int],
+    "kair_conv3x3_narrow_wgrad": [c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
     "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "kair_charbonnier_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_int, c_int,
                               c_vp, c_vp],
@@ -174,7 +180,8 @@ _SIGS = {
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
 _RESTYPE = {"kair_layernorm_bwd_blocks": c_long, "kair_rowgemm_ln_blocks": c_long, "kair_window_attn_bwd_groups": c_long, "kair_wgrad_grouped_ws": c_long, "kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
-            "kair_pack_table_build": c_long}
+            "kair_pack_table_build": c_long, "kair_conv3x3_narrow_wgrad_ws": c_long,
+            "kair_conv3x3_narrow_dgrad_ws": c_long}
 
 _lib = None
 
@@ -252,10 +259,11 @@ def rows(t, ld=None, win=None, rowscale=None, rows_per_scale=1, ones_col=-1, one
     return o
 
 
-def asplit(op, lo=None):
+def asplit(op, lo=None, pair=False):
     """Mark a kair_gemm_nt A operand as a hi/lo activation pair: fp32 A forms lo in the kernel, a bf16 A
-    (the hi plane) reads lo from `lo` (its producer's epilogue out_lo)."""
-    op.a_split = 1
+    (the hi plane) reads lo from `lo` (its producer's epilogue out_lo).  pair=True: the bf16 image's
+    channels already are the [hi | lo] halves (weights packed tied over them; a_split 2)."""
+    op.a_split = 2 if pair else 1
     if lo is not None:
         op.lo_ptr = ptr(lo)
         op._keep = (op._keep, lo)
@@ -525,6 +533,30 @@ def window_attn_bwd(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc,
     check(lib().kair_window_attn_bwd_ex(ptr(qkv), ptr(O), ldo, ptr(dO), lddo, dtype_code(qkv), ptr(table), ptr(lse),
                                         ptr(dqkv), int(dqkv_rows), ptr(dtable), int(dtable_acc), ptr(ws), nWin, nh, hd,
                                         scale, H, W, shift, ptr(mask), mnw, stream_ptr()), "window_attn_bwd")
+
+
+def conv3x3_narrow_fwd(x, ldx, lo_off, w, bias, NR, mean, img_range, resid, out, B, H, W):
+    """conv_last forward: 64-channel bf16 rows (hi, + lo at lo_off) -> NCHW image (csrc/tail.hip)."""
+    check(lib().kair_conv3x3_narrow_fwd(ptr(x), ldx, lo_off, ptr(w), ptr(bias), NR, ptr(mean), img_range, ptr(resid),
+                                        ptr(out), B, H, W, stream_ptr()), "conv3x3_narrow_fwd")
+
+
+def conv3x3_narrow_dgrad_ws():
+    return lib().kair_conv3x3_narrow_dgrad_ws()
+
+
+def conv3x3_narrow_dgrad(dE, lde, w, NR, ws, out, ldo, ps_r, B, H, W):
+    check(lib().kair_conv3x3_narrow_dgrad(ptr(dE), lde, ptr(w), NR, ptr(ws), ptr(out), dtype_code(out), ldo, ps_r, B, H, W,
+                                          stream_ptr()), "conv3x3_narrow_dgrad")
+
+
+def conv3x3_narrow_wgrad_ws(NR):
+    return lib().kair_conv3x3_narrow_wgrad_ws(NR)
+
+
+def conv3x3_narrow_wgrad(dE, lde, x, ldx, NR, ws, grad_w, grad_b, B, H, W, accumulate=False):
+    check(lib().kair_conv3x3_narrow_wgrad(ptr(dE), lde, ptr(x), ldx, NR, ptr(ws), ptr(grad_w), ptr(grad_b),
+                                          int(accumulate), B, H, W, stream_ptr()), "conv3x3_narrow_wgrad")
 
 
 def image_to_nhwc_hilo(img, out, ldc, mean, img_range, B, C, H, W):

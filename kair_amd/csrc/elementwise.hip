@@ -102,6 +102,18 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const bf16 hi = (bf16)v;
     ((bf16*)dst)[t] = half ? (bf16)(v - (float)hi) : hi;
     return;
+  } else if (mp.kind == 15) {  // conv3x3 forward in 16x16x32 fragment order, hi/lo halves: [Np/16][9*Kp/32][2][64][8]
+    const int KB = 9 * Kp / 32;
+    const int j = (int)(t & 7), ln = (int)((t >> 3) & 63), half = (int)((t >> 9) & 1);
+    const long blk = t >> 10;
+    const int kb = (int)(blk % KB), nb = (int)(blk / KB);
+    const int np = nb * 16 + (ln & 15), kk = kb * 32 + 8 * (ln >> 4) + j;   // kk = tap * Kp + cip
+    const int tap = kk / Kp, cip = kk - tap * Kp;
+    const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci % mp.K) * 9 + tap];
+    const bf16 hi = (bf16)v;
+    ((bf16*)dst)[t] = half ? (bf16)(v - (float)hi) : hi;
+    return;
   } else if (mp.kind == 8) {  // conv2x2 [4*Kp][Np], row = kp*4 + tap (pixel-shuffle forms)
     const int row = (int)(t / Np), np = (int)(t - (long)row * Np);
     const int kp = row >> 2, tap = row & 3;
@@ -577,14 +589,15 @@ inline unsigned nblk(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 }  // namespace
 
 static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
-  KAIR_CHECK_ARG((mp.kind != 9 && mp.kind != 12) || dst_dtype == KAIR_BF16,
-                 "pack_weight: the hi/lo split forms (kinds 9, 12) are bf16 only");
+  KAIR_CHECK_ARG((mp.kind != 9 && mp.kind != 12 && mp.kind != 15) || dst_dtype == KAIR_BF16,
+                 "pack_weight: the hi/lo split forms (kinds 9, 12, 15) are bf16 only");
   KAIR_CHECK_ARG(mp.nG > 0 && mp.nGr > 0 && mp.nGp >= mp.nGr && mp.nG * mp.nGr == mp.N, "pack_weight: bad N map");
   // kinds 1 / 9 (conv forward) may repeat the in dim (kG * kGr a multiple of K: tied copies, e.g. the
   // hi / lo halves of a split input image); every other kind maps it one to one
   KAIR_CHECK_ARG(mp.kind == 4 ||
                      (mp.kG > 0 && mp.kGr > 0 && mp.kGp >= mp.kGr &&
-                      (mp.kG * mp.kGr == mp.K || ((mp.kind == 1 || mp.kind == 9) && mp.K > 0 && (mp.kG * mp.kGr) % mp.K == 0))),
+                      (mp.kG * mp.kGr == mp.K ||
+                       ((mp.kind == 1 || mp.kind == 9 || mp.kind == 15) && mp.K > 0 && (mp.kG * mp.kGr) % mp.K == 0))),
                  "pack_weight: bad K map");
   KAIR_CHECK_ARG(mp.n_perm <= 1 || (mp.nG == 1 && mp.N % mp.n_perm == 0), "pack_weight: n_perm needs nG == 1, N %% n_perm == 0");
   const long Np = (long)mp.nG * mp.nGp, Kp = (long)mp.kG * mp.kGp;
@@ -592,11 +605,13 @@ static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
                  "pack_weight: fragment order needs Np %% 32 == 0, Kp %% 16 == 0");
   KAIR_CHECK_ARG(mp.kind != 13 || (Kp % 32 == 0 && Np % 16 == 0), "pack_weight: transposed fragment order needs Kp %% 32 == 0, Np %% 16 == 0");
   KAIR_CHECK_ARG(mp.kind != 14 || (Np % 16 == 0 && Kp % 32 == 0), "pack_weight: 16x16x32 fragment order needs Np %% 16 == 0, Kp %% 32 == 0");
+  KAIR_CHECK_ARG(mp.kind != 15 || (Np % 16 == 0 && (9 * Kp) % 32 == 0), "pack_weight: kind 15 needs Np %% 16 == 0, 9 Kp %% 32 == 0");
   if (mp.kind == 0 || mp.kind == 3 || mp.kind == 10 || mp.kind == 13 || mp.kind == 14) *total = Np * Kp;
   else if (mp.kind == 12) *total = 2 * Np * Kp;
   else if (mp.kind == 1 || mp.kind == 2) *total = Np * 9 * Kp;
   else if (mp.kind == 7 || mp.kind == 8) *total = Np * 4 * Kp;
   else if (mp.kind == 9) *total = Np * 2 * ((9L * Kp + 63) / 64) * 64;
+  else if (mp.kind == 15) *total = 2 * Np * 9 * Kp;
   else if (mp.kind == 4) *total = Np;
   else return kair_set_error(KAIR_ERR_ARG, "pack_weight: bad kind %d", mp.kind);
   return 0;

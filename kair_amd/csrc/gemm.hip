@@ -63,7 +63,7 @@ Op make_op(const kair_operand& o, long M) {
   op.ones_in_data = o.ones_in_data;
   op.M = M;
   op.wsplit = o.w_split ? 1 : 0;
-  op.asplit = o.a_split ? 1 : 0;
+  op.asplit = o.a_split;   // 0, 1 or 2 (kair_operand.a_split)
   op.lo_ptr = o.lo_ptr;
   op.d_rps = make_fdiv(op.rps);
   op.d_imC = make_fdiv(op.imC); op.d_imW = make_fdiv(op.imW); op.d_hw = make_fdiv(op.imH * op.imW);
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_kernel(Op A, Op B, Epi E, int K
   // hi/lo split activations (A.asplit) add a third product per K step, a_lo . w_hi: the lo half
   // formed from the fp32 source at commit, or read from the lo plane of a bf16 source.
   const int wsp = (sizeof(CT) == 2 && B.wsplit) ? 1 : 0;
-  const int asp = (sizeof(CT) == 2 && A.asplit) ? 1 : 0;
+  const int asp = (sizeof(CT) == 2 && A.asplit == 1) ? 1 : 0;   // a_split 2: the lo half is in the image
   const int NP = 1 + wsp + asp;   // products per K step: (a_hi, w_hi) [, (a_hi, w_lo)] [, (a_lo, w_hi)]
   const int nks = (K + BK - 1) / BK;
   const int nk = nks * NP;
@@ -1574,12 +1574,19 @@ int ring_bn(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStr
 constexpr int HC_BM = 96, HC_BN = 192, HC_BK = 64;
 constexpr int HC_HALO_ELEMS = 40960;   // bf16 elements: (RPT + 2) x (XW + 2) x (Cin + 8)
 constexpr int HC_PER = HC_HALO_ELEMS / 8 / 512;
+constexpr int HC_EM_ROWS = 0, HC_EM_PSHUF = 1;   // epilogue: token rows / PixelShuffle sub-pixel-major (PSHUF_SPM)
 
-template <typename TA, int EX, int NPASS>
+// BN: output channels per tile (192, or 128 for N in (192, 256]: N tiles of one M tile run on
+// consecutive workgroups, each with its own weight rows; the persistent grid is a multiple of the
+// N-tile count so a workgroup's N tile -- its bias and weight rows -- never changes).
+// bf16 A with a_split == 2: the image's channels are [hi | lo] halves of one activation and the
+// weights (hi/lo split, tied over the halves) give 4 chunk products per tap; the lo.lo one is skipped.
+template <typename TA, int EX, int NPASS, int BN, int EM>
 __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E, int K, int tilesM) {
-  constexpr int WM = 2, WN = 4, TM = HC_BM / WM, TN = HC_BN / WN, RM = TM / 16, RN = TN / 16;
+  constexpr int WM = 2, WN = 4, TM = HC_BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
+  constexpr int NI = BN / 64;   // LDS-DMA wave-instructions per weight chunk (8 rows x 128 B each)
   __shared__ __attribute__((aligned(16))) bf16 sHalo[HC_HALO_ELEMS];
-  __shared__ __attribute__((aligned(16))) bf16 sBw[3][HC_BN * HC_BK];   // LDS-DMA ring of weight chunks
+  __shared__ __attribute__((aligned(16))) bf16 sBw[3][BN * HC_BK];   // LDS-DMA ring of weight chunks
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fq = lane >> 4;
@@ -1591,10 +1598,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
   // product), accumulating into the same tile
   constexpr int npass = NPASS;
   const int cpt = C / HC_BK, nks = (9 * cpt) << sh, c8n = C / 8;
+  const bool pair = sizeof(TA) == 2 && A.asplit == 2 && sh && cpt == 2;   // skip lo . lo (chunk 4t + 3)
   const int halo_pieces = HR * HWD * c8n;
-  const bf16* Bp = (const bf16*)B.ptr;
   const TA* Ap = (const TA*)A.ptr;
   const int N = E.N;
+  const int tilesN = (N + BN - 1) / BN, tn = blockIdx.x % tilesN, n0 = tn * BN;
+  const bf16* Bp = (const bf16*)B.ptr + (long)n0 * B.ld;   // this workgroup's weight rows
+  const int Nt = N - n0 < BN ? N - n0 : BN;                 // real rows of the tile
 
   // per-lane constants: halo element offset of each fragment row's centre pixel, weight rows
   int hb[RM];
@@ -1610,22 +1620,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
   float4 bias4[RN];
 #pragma unroll
   for (int jn = 0; jn < RN; ++jn) {
-    const int n = wn * TN + jn * 16 + fq * 4;
+    const int n = n0 + wn * TN + jn * 16 + fq * 4;
     bias4[jn] = *(const float4*)(E.bias && n < N ? E.bias + n : (const float*)g_kair_zero_line);
   }
 #pragma unroll
   for (int jn = 0; jn < RN; ++jn) land(bias4[jn]);
 
-  // weight chunk j (192 rows x 64 k = 24 KiB) -> ring stage js % 3 by LDS-DMA: 3 wave-instructions
-  // per wave, each 8 rows x 128 B; source pieces XOR-swizzled by row so the fragment reads are
-  // conflict-light.  Rows >= N re-read row N-1: they only feed output columns >= N, never stored.
+  // weight chunk j (BN rows x 64 k) -> ring stage js % 3 by LDS-DMA: NI wave-instructions per wave,
+  // each 8 rows x 128 B; source pieces XOR-swizzled by row so the fragment reads are conflict-light.
+  // Rows >= Nt re-read row Nt-1: they only feed output columns >= N, never stored.
   auto bissue = [&](int js, int j) {
     char* st = (char*)sBw[js % 3];
 #pragma unroll
-    for (int ii = 0; ii < 3; ++ii) {
-      const int r = (wave * 3 + ii) * 8 + (lane >> 3), q = lane & 7;
-      const int rr = r < N ? r : N - 1;
-      glds16(Bp + (long)rr * B.ld + j * HC_BK + ((q ^ (r & 7)) << 3), st + (wave * 3 + ii) * 1024);
+    for (int ii = 0; ii < NI; ++ii) {
+      const int r = (wave * NI + ii) * 8 + (lane >> 3), q = lane & 7;
+      const int rr = r < Nt ? r : Nt - 1;
+      glds16(Bp + (long)rr * B.ld + j * HC_BK + ((q ^ (r & 7)) << 3), st + (wave * NI + ii) * 1024);
     }
   };
   f32x4 acc[RM][RN];
@@ -1651,7 +1661,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
     }
   };
 
-  for (int t = blockIdx.x; t < tilesM; t += gridDim.x) {
+  for (int t = blockIdx.x / tilesN; t < tilesM; t += gridDim.x / tilesN) {
     const long p0 = (long)t * HC_BM;
     const int b = (int)(p0 / ((long)H * W));
     const int rem = (int)(p0 - (long)b * H * W);
@@ -1670,7 +1680,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
 #pragma unroll
         for (int jn = 0; jn < RN; ++jn) {
           const long m = p0 + wm * TM + i * 16 + fr;
-          const int n = wn * TN + jn * 16 + fq * 4;
+          const int n = n0 + wn * TN + jn * 16 + fq * 4;
           ex[i][jn] = *(const float4*)(E.resid + m * E.ldr + (n < N ? n : 0));
         }
     };
@@ -1741,20 +1751,26 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
       }
     }
     __syncthreads();   // halo visible
-    // pass 1 (lo halo): the hi weight chunks only, chunk j of the pass = weight chunk j << sh
-    const int nkp = pass ? nks >> sh : nks, wsh = pass ? sh : 0;
+    // pass 1 (lo halo): the hi weight chunks only, chunk j of the pass = weight chunk j << sh;
+    // a [hi | lo] pair image: per tap the weight chunks 4t, 4t+1, 4t+2 (hi.w_hi, hi.w_lo, lo.w_hi)
+    const int nkp = pass ? nks >> sh : (pair ? nks / 4 * 3 : nks), wsh = pass ? sh : 0;
+    auto wchunk = [&](int j) { return pass ? j << wsh : (pair ? (j / 3) * 4 + j % 3 : j); };
     bissue(0, 0);
-    if (1 < nkp) bissue(1, 1 << wsh);
+    if (1 < nkp) bissue(1, wchunk(1));
     for (int j = 0; j < nkp; ++j) {
-      // chunk j landed for this wave (younger: chunk j+1's 3 DMA instructions), then all waves
-      if (j + 1 < nkp) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // chunk j landed for this wave (younger: chunk j+1's NI DMA instructions), then all waves
+      if (j + 1 < nkp) {
+        if constexpr (NI == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       ring_barrier();   // chunk j visible; stage (j+2) % 3 = (j-1) % 3 is free
-      if (j + 2 < nkp) bissue(j + 2, (j + 2) << wsh);
+      if (j + 2 < nkp) bissue(j + 2, wchunk(j + 2));
       if constexpr (EX == EX_RESID) {
         if (last && j == nkp - 2) load_resid();
       }
-      compute(j % 3, j << wsh);
+      compute(j % 3, wchunk(j));
     }
     }   // pass
     // epilogue: bias (+ act) (+ fp32 residual), 4 consecutive channels per lane
@@ -1770,7 +1786,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
 #pragma unroll
       for (int jn = 0; jn < RN; ++jn) {
         const long m = p0 + wm * TM + i * 16 + fr;
-        const int n = wn * TN + jn * 16 + fq * 4;
+        const int n = n0 + wn * TN + jn * 16 + fq * 4;
         const float4 bb = bias4[jn];
         float v[4] = {acc[i][jn][0] + bb.x, acc[i][jn][1] + bb.y, acc[i][jn][2] + bb.z, acc[i][jn][3] + bb.w};
 #pragma unroll
@@ -1788,11 +1804,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
             if (n + q4 == E.ones_col) v[q4] = 1.f;
         }
         if (n < N) {
-          st4_any(E.out, E.odt, m * E.ldo + n, v);
+          long o = m * E.ldo + n;
+          if constexpr (EM == HC_EM_PSHUF) {   // sub-pixel-major columns: n = (i r + j) nf + c -> pixel (y r + i, x r + j)
+            const int r = E.r, nf = N / (r * r);
+            const int bi = (int)(m / ((long)H * W)), pp = (int)(m - (long)bi * H * W), yy = pp / W, xx = pp - yy * W;
+            const int sp = n / nf, cc = n - sp * nf, ii = sp / r, jj = sp - ii * r;
+            o = (((long)bi * H * r + (long)yy * r + ii) * ((long)W * r) + (long)xx * r + jj) * E.ldo + cc;
+          }
+          st4_any(E.out, E.odt, o, v);
           if (E.out_lo) {
             const bf16x4 ql = {(bf16)(v[0] - (float)(bf16)v[0]), (bf16)(v[1] - (float)(bf16)v[1]),
                                (bf16)(v[2] - (float)(bf16)v[2]), (bf16)(v[3] - (float)(bf16)v[3])};
-            *(bf16x4*)(E.out_lo + m * E.ldo + n) = ql;
+            *(bf16x4*)(E.out_lo + o) = ql;
           }
         }
       }
@@ -1803,8 +1826,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
 template <typename TA>
 static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, int K) {
   const int H = A.imH, W = A.imW, C = A.imC;
-  if (A.up_sh != 0 || C % HC_BK != 0 || C > 192 || K != 9 * C || N > HC_BN || N % 4 != 0) return false;
-  if (A.asplit && sizeof(TA) != 4) return false;   // the two-pass split forms lo from an fp32 image
+  if (A.up_sh != 0 || C % HC_BK != 0 || C > 192 || K != 9 * C || N > 256 || N % 4 != 0) return false;
+  // the two-pass split forms lo from an fp32 image; a bf16 image carries it as its [hi | lo] halves (a_split 2)
+  if (A.asplit && !(sizeof(TA) == 4 ? A.asplit == 1 : (A.asplit == 2 && C == 128 && B.wsplit))) return false;
   if (W <= 0 || H <= 0) return false;
   if (W <= HC_BM) {
     if (HC_BM % W != 0 || H % (HC_BM / W) != 0) return false;
@@ -1815,7 +1839,10 @@ static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, 
   if ((long)(RPT + 2) * (XW + 2) * (C + 8) > HC_HALO_ELEMS) return false;
   if (M % HC_BM != 0 || M % ((long)H * W) != 0) return false;
   if (A.ld % 8 != 0 || ((unsigned long)A.ptr & 15) || B.ld % 8 != 0 || ((unsigned long)B.ptr & 15)) return false;
-  if (e.omode != KAIR_OUT_ROWS || e.win.ws != 0 || e.gate || e.pre || e.resid2 || e.rowscale) return false;
+  if (e.omode != KAIR_OUT_ROWS && !(e.omode == KAIR_OUT_PSHUF_SPM && e.psH == H && e.psW == W && e.r > 0 &&
+                                    N % (e.r * e.r) == 0 && (N / (e.r * e.r)) % 4 == 0 && !e.resid && !e.acopy))
+    return false;
+  if (e.win.ws != 0 || e.gate || e.pre || e.resid2 || e.rowscale) return false;
   if (e.ldo % 4 != 0 || ((unsigned long)e.out & 15) || (e.resid && (e.ldr % 4 != 0 || ((unsigned long)e.resid & 15))))
     return false;
   if (e.acopy && (e.ldac % 8 != 0 || e.ldac < C || ((unsigned long)e.acopy & 15))) return false;
@@ -1840,22 +1867,28 @@ template <typename TA>
 static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int K, hipStream_t s) {
   if (g_num_cus == 0) init_num_cus();
   const int tilesM = (int)(M / HC_BM);
-  const int grid = tilesM < g_num_cus ? tilesM : g_num_cus;
+  const bool wide = E.N > HC_BN;   // N in (192, 256]: two 128-wide N tiles
+  const int tilesN = wide ? (E.N + 127) / 128 : 1;
+  long tiles = (long)tilesM * tilesN;
+  int grid = (int)(tiles < g_num_cus ? tiles : (g_num_cus / tilesN) * tilesN);   // a multiple of tilesN
+#define KAIR_HALO(NP, EXV, BNV, EMV) \
+  hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EXV, NP, BNV, EMV>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM)
+#define KAIR_HALO_NP(NP)                                                                  \
+  if (E.resid) KAIR_HALO(NP, EX_RESID, 192, HC_EM_ROWS);                                  \
+  else if (E.omode == KAIR_OUT_PSHUF_SPM && wide) KAIR_HALO(NP, EX_NONE, 128, HC_EM_PSHUF); \
+  else if (E.omode == KAIR_OUT_PSHUF_SPM) KAIR_HALO(NP, EX_NONE, 192, HC_EM_PSHUF);        \
+  else if (wide) KAIR_HALO(NP, EX_NONE, 128, HC_EM_ROWS);                                  \
+  else KAIR_HALO(NP, EX_NONE, 192, HC_EM_ROWS);
   if constexpr (sizeof(TA) == 4) {
     if (A.asplit) {   // conv_halo_ok: the two-pass split takes an fp32 A only
-      if (E.resid)
-        hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_RESID, 2>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
-      else
-        hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE, 2>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
+      KAIR_HALO_NP(2)
       KAIR_CHECK_LAUNCH();
       return 0;
     }
   }
-  if (E.resid) {
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_RESID, 1>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
-  } else {
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE, 1>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM);
-  }
+  KAIR_HALO_NP(1)
+#undef KAIR_HALO_NP
+#undef KAIR_HALO
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1993,11 +2026,15 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
                  "gemm_nt: hi/lo split weights need bf16 compute and rows of 2*ceil(K/64)*64 columns");
   KAIR_CHECK_ARG(!A->w_split, "gemm_nt: w_split is a B-operand flag");
   KAIR_CHECK_ARG(!B->a_split, "gemm_nt: a_split is an A-operand flag");
-  KAIR_CHECK_ARG(!A->a_split || (compute == KAIR_BF16 && (A->mode == KAIR_LD_ROWS || A->mode == KAIR_LD_IM2COL3) &&
-                                 !A->rowscale && A->ones_col < 0 &&
-                                 (A->dtype == KAIR_F32 || (A->lo_ptr && ((uintptr_t)A->lo_ptr % 16) == 0))),
+  KAIR_CHECK_ARG(A->a_split != 1 || (compute == KAIR_BF16 && (A->mode == KAIR_LD_ROWS || A->mode == KAIR_LD_IM2COL3) &&
+                                      !A->rowscale && A->ones_col < 0 &&
+                                      (A->dtype == KAIR_F32 || (A->lo_ptr && ((uintptr_t)A->lo_ptr % 16) == 0))),
                  "gemm_nt: a_split needs bf16 compute, a ROWS / IM2COL3 A without rowscale or ones column, and for a "
                  "bf16 A its 16-byte aligned lo plane");
+  KAIR_CHECK_ARG(A->a_split >= 0 && A->a_split <= 2, "gemm_nt: a_split must be 0, 1 or 2");
+  KAIR_CHECK_ARG(A->a_split != 2 || (compute == KAIR_BF16 && A->dtype == KAIR_BF16 && A->mode == KAIR_LD_IM2COL3 &&
+                                      B->w_split && A->im_C % 2 == 0),
+                 "gemm_nt: a_split 2 marks a bf16 [hi | lo] pair image read through tied hi/lo split weights");
   KAIR_CHECK_ARG(!E->out_lo || (E->out_dtype == KAIR_BF16 && (E->out_mode == KAIR_OUT_ROWS || E->out_mode == KAIR_OUT_PSHUF_SPM) &&
                                 ((uintptr_t)E->out_lo % 16) == 0),
                  "gemm_nt: out_lo needs a bf16 ROWS / PSHUF_SPM output and a 16-byte aligned lo plane");

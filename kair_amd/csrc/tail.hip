@@ -1,0 +1,487 @@
+// Narrow-output 3x3 convolutions for gfx950: the last conv of an image-restoration network maps a
+// 64-channel feature image to the NR <= 4 channels of the output image (SwinIR conv_last,
+// network_swinir.py:745 / :817).  As a generic implicit GEMM its N = NR padded to 16 wastes the MFMA
+// tile and its im2col re-reads the 64-channel image once per K tile; here each of the three products
+// of the training step gets its own kernel, all three built on one access pattern:
+//
+//   Rolling row window.  The image is cut into 64-pixel row segments; a persistent workgroup owns a
+//   contiguous run of output rows of one column strip (a 64-pixel-wide strip of one image) and keeps
+//   the input rows y-1, y, y+1 of its segment (+1 halo pixel each side) in an LDS ring, loading row
+//   y+2 with bulk 16-byte loads while it computes row y.  Every input pixel is fetched from HBM once
+//   (plus two halo rows per run); the nine taps read LDS.
+//
+//   kair_conv3x3_narrow_fwd    E = conv(X) -> NCHW image (v / range + mean): v_mfma_f32_16x16x32_bf16
+//                              with D = W . X^T (a lane ends with 4 output channels of one pixel), the
+//                              hi/lo split weights (pack kind 15) resident in VGPRs for the launch, the
+//                              image a [hi | lo] pair (split activations: 3 products per k-step);
+//   kair_conv3x3_narrow_dgrad  dX = conv^T(dE): MFMA with D = W'^T . dE_im2col^T over k = (tap, n) (36
+//                              -> 2 k-steps), the dE rows staged as 4 channels per pixel; rows or
+//                              PixelUnshuffle sub-pixel-major store (the previous upsampling conv's
+//                              pre-shuffle gradient);
+//   kair_conv3x3_narrow_wgrad  dW = sum_p dE[p] x X[p + tap]: VALU, one wave per tap, lane = (8 channels,
+//                              pixel phase); per-workgroup partials summed in fixed order (deterministic).
+#include <stdlib.h>
+
+#include "common.h"
+
+namespace {
+
+constexpr int NF = 64;      // feature channels of the image side
+constexpr int SEG = 64;     // output pixels per row segment
+constexpr int PXS = SEG + 2;
+
+// A run of output rows: rows [g0, g1) of the global (strip, y) order, strip = b * nseg + segment.
+struct RowRun {
+  long g0, g1;
+};
+KAIR_DEV RowRun row_run(long total, int nblk, int blk) {
+  const long per = (total + nblk - 1) / nblk;
+  RowRun r;
+  r.g0 = (long)blk * per;
+  r.g1 = r.g0 + per < total ? r.g0 + per : total;
+  return r;
+}
+
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------------------------
+struct NarrowFwdArgs {
+  const bf16* x; long ldx; int lo_off;   // [B*H*W][ldx] bf16: hi channels [0, 64), lo [lo_off, lo_off + 64) (0: none)
+  const bf16* w;                        // pack kind 15: [1][18][2][64][8]
+  const float* bias;                    // [16] (>= NR real)
+  const float* mean; float range; int NR;
+  const float* resid;                   // optional NCHW image added after the range (denoising head)
+  float* out;                           // NCHW [B][NR][H][W]
+  int B, H, W;
+};
+
+constexpr int FPST = 136;               // LDS pixel stride (bf16): 128 channels + 8 (272 B: 16 lanes conflict-free)
+constexpr int FROW = PXS * FPST;        // one staged row
+constexpr int FCH = PXS * 16;           // 16-byte chunks per staged row (hi + lo: 16 per pixel)
+constexpr int FPER = (FCH + 255) / 256; // chunks per thread
+
+__global__ __launch_bounds__(256, 1) void conv3x3_narrow_fwd_kernel(const NarrowFwdArgs a) {
+  constexpr int KS = 9 * NF / 32;   // 18 k-steps of 32: (tap, channel half)
+  __shared__ __attribute__((aligned(16))) bf16 sRow[4 * FROW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  bf16x8 wh[KS], wl[KS];
+#pragma unroll
+  for (int kb = 0; kb < KS; ++kb) {
+    wh[kb] = *(const bf16x8*)(a.w + ((long)kb * 2 + 0) * 512 + lane * 8);
+    wl[kb] = *(const bf16x8*)(a.w + ((long)kb * 2 + 1) * 512 + lane * 8);
+  }
+  float bias4[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) bias4[n] = n < a.NR ? a.bias[n] : 0.f;
+  const int nseg = a.W / SEG;
+  const long total = (long)a.B * nseg * a.H;
+  const RowRun run = row_run(total, gridDim.x, blockIdx.x);
+  const bool split = a.lo_off > 0;
+  uint4 pre[FPER];
+  // issue the loads of input row yy of strip st (zeros outside the image): chunk c = pixel c / 16, part c % 16
+  auto load_row = [&](long st, int yy) {
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+#pragma unroll
+    for (int i = 0; i < FPER; ++i) {
+      const int c = tid + 256 * i;
+      const int px = c >> 4, part = c & 15;
+      const int xx = x0 - 1 + px;
+      const bool ok = c < FCH && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W && (split || part < 8);
+      const long off = ok ? ((long)(b * a.H + yy) * a.W + xx) * a.ldx + (part < 8 ? part * 8 : a.lo_off + (part - 8) * 8) : 0;
+      pre[i] = *(const uint4*)(a.x + off);
+      if (!ok) pre[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_row = [&](int yy) {
+    bf16* dst = sRow + (yy & 3) * FROW;
+#pragma unroll
+    for (int i = 0; i < FPER; ++i) {
+      const int c = tid + 256 * i;
+      if (c < FCH) *(uint4*)(dst + (c >> 4) * FPST + (c & 15) * 8) = pre[i];
+    }
+  };
+  const int pl = lane & 15, cq = 8 * (lane >> 4);
+  long cur_strip = -1;
+  for (long g = run.g0; g < run.g1; ++g) {
+    const long st = g / a.H;
+    const int y = (int)(g - st * a.H);
+    if (st != cur_strip) {   // (re)start the window: rows y-1, y, y+1
+      __syncthreads();
+      for (int d = -1; d <= 1; ++d) {
+        load_row(st, y + d);
+        store_row(y + d + 4);   // + 4: slot of a negative row index stays in [0, 4)
+      }
+      cur_strip = st;
+      __syncthreads();
+    }
+    const bool more = g + 1 < run.g1 && (g + 1) / a.H == st;
+    if (more) load_row(st, y + 2);   // in flight during this row's MFMAs
+    // wave w: output pixels x0 + 16 w + pl
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      const bf16* src = sRow + ((y + dy + 4) & 3) * FROW + (1 + 16 * wave + pl + dx) * FPST + cq;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 xh = *(const bf16x8*)(src + 32 * ks);
+        const int kb = tap * 2 + ks;
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[kb], xh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[kb], xh, acc, 0, 0, 0);
+        if (split) {
+          const bf16x8 xl = *(const bf16x8*)(src + 64 + 32 * ks);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[kb], xl, acc, 0, 0, 0);
+        }
+      }
+    }
+    if (lane < 16) {   // D[n][px]: lanes 0..15 hold n = 0..3 of pixel pl
+      const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+      const long HW = (long)a.H * a.W;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        if (n < a.NR) {
+          const long o = ((long)b * a.NR + n) * HW + (long)y * a.W + x0 + 16 * wave + pl;
+          float v = (acc[n] + bias4[n]) / a.range + (a.mean ? a.mean[n] : 0.f);
+          if (a.resid) v += a.resid[o];
+          a.out[o] = v;
+        }
+      }
+    }
+    __syncthreads();   // every wave is done with row y - 1's slot
+    if (more) store_row(y + 2);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// input gradient
+// ---------------------------------------------------------------------------------------------------
+struct NarrowDgradArgs {
+  const bf16* dE; long lde;             // [B*H*W][lde] bf16, channels [0, NR) (NR <= 4; the rest ignored)
+  const bf16* w;                        // [4 c-blocks][2 k-steps][64][8]: W'[c][k = tap*4 + n] in fragment order
+  void* out; int odt; long ldo;         // rows [B*H*W][ldo] (ps_r <= 1) or PixelUnshuffle SPM (ps_r > 1)
+  int ps_r;
+  int B, H, W;
+};
+
+constexpr int DPST = 4;                 // staged dE: 4 channels (8 B) per pixel
+constexpr int DROW = PXS * DPST;
+
+__global__ __launch_bounds__(256) void conv3x3_narrow_dgrad_kernel(const NarrowDgradArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sE[4 * DROW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // weight fragments: A operand rows = output channel (16 per block), k = 8 (l / 16) + j
+  bf16x8 wf[4][2];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) wf[cb][ks] = *(const bf16x8*)(a.w + ((cb * 2 + ks) * 64 + lane) * 8);
+  const int nseg = a.W / SEG;
+  const long total = (long)a.B * nseg * a.H;
+  const RowRun run = row_run(total, gridDim.x, blockIdx.x);
+  uint2 pre = make_uint2(0, 0);
+  auto load_row = [&](long st, int yy) {   // 66 pixels x 8 B: one per thread (threads >= 66 idle)
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+    const int xx = x0 - 1 + tid;
+    const bool ok = tid < PXS && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+    pre = *(const uint2*)(a.dE + (ok ? ((long)(b * a.H + yy) * a.W + xx) * a.lde : 0));
+    if (!ok) pre = make_uint2(0, 0);
+  };
+  auto store_row = [&](int yy) {
+    if (tid < PXS) *(uint2*)(sE + (yy & 3) * DROW + tid * DPST) = pre;
+  };
+  const int pl = lane & 15, kq = lane >> 4;   // B fragment: pixel pl, k = 8 kq + j -> taps 2 kq, 2 kq + 1 (x 4 n)
+  long cur_strip = -1;
+  for (long g = run.g0; g < run.g1; ++g) {
+    const long st = g / a.H;
+    const int y = (int)(g - st * a.H);
+    if (st != cur_strip) {
+      __syncthreads();
+      for (int d = -1; d <= 1; ++d) {
+        load_row(st, y + d);
+        store_row(y + d + 4);
+      }
+      cur_strip = st;
+      __syncthreads();
+    }
+    const bool more = g + 1 < run.g1 && (g + 1) / a.H == st;
+    if (more) load_row(st, y + 2);
+    // dX[q] = sum_tap sum_n dE[q - (dy, dx)][n] W[n][c][tap]: B fragment of pixel q = x0 + 16 wave + pl
+    bf16x8 bfr[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x4 e2[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int tap = 8 * ks + 2 * kq + h;   // k = tap * 4 + n
+        if (tap < 9) {
+          const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+          e2[h] = *(const bf16x4*)(sE + ((y - dy + 4) & 3) * DROW + (1 + 16 * wave + pl - dx) * DPST);
+        } else {
+          e2[h] = bf16x4{};
+        }
+      }
+      bfr[ks] = bf16x8{e2[0][0], e2[0][1], e2[0][2], e2[0][3], e2[1][0], e2[1][1], e2[1][2], e2[1][3]};
+    }
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+    const int x = x0 + 16 * wave + pl;
+    long o;
+    if (a.ps_r > 1) {   // pixel (b, y, x) of the r-times image -> pre-shuffle row (b, y/r, x/r), column (i r + j) 64 + c
+      const int r = a.ps_r, yl = y / r, xl = x / r;
+      o = ((long)(b * (a.H / r) + yl) * (a.W / r) + xl) * a.ldo + ((y - yl * r) * r + (x - xl * r)) * NF;
+    } else {
+      o = ((long)(b * a.H + y) * a.W + x) * a.ldo;
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][0], bfr[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][1], bfr[1], acc, 0, 0, 0);
+      // D[c][q]: lane holds channels 16 cb + 4 kq .. +3 of pixel pl
+      const long oc = o + 16 * cb + 4 * kq;
+      if (a.odt == KAIR_BF16) *(bf16x4*)((bf16*)a.out + oc) = bf16x4{(bf16)acc[0], (bf16)acc[1], (bf16)acc[2], (bf16)acc[3]};
+      else *(float4*)((float*)a.out + oc) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    }
+    __syncthreads();
+    if (more) store_row(y + 2);
+    __syncthreads();
+  }
+}
+
+// W'[c][k] fragment order for the dgrad kernel from the fp32 weight [NR][64][3][3]: k = tap * 4 + n
+__global__ void narrow_dgrad_pack_kernel(const float* __restrict__ w, int NR, bf16* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;   // [4][2][64][8]
+  if (t >= 4 * 2 * 64 * 8) return;
+  const int j = t & 7, ln = (t >> 3) & 63, ks = (t >> 9) & 1, cb = t >> 10;
+  const int c = 16 * cb + (ln & 15), k = 32 * ks + 8 * (ln >> 4) + j;
+  const int tap = k >> 2, n = k & 3;
+  out[t] = (bf16)(tap < 9 && n < NR ? w[((long)n * NF + c) * 9 + tap] : 0.f);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// weight gradient
+// ---------------------------------------------------------------------------------------------------
+struct NarrowWgradArgs {
+  const bf16* dE; long lde;             // [M][lde] bf16, channels [0, NR)
+  const bf16* x; long ldx;              // [M][ldx] bf16 image, channels [0, 64)
+  int NR;
+  int B, H, W;
+  float* part;                          // [gridDim.x][NR * 64 * 9 + NR]
+};
+
+constexpr int WPST = 72;                // staged X: 64 channels + 8 per pixel (144 B)
+constexpr int WROW = PXS * WPST;
+constexpr int WCH = PXS * 8;            // 16-byte chunks per staged X row
+constexpr int WPER = (WCH + 575) / 576;
+
+// 9 waves (wave = tap); lane: channel group cg = lane & 7 (8 channels), pixel phase ph = lane >> 3
+__global__ __launch_bounds__(576) void conv3x3_narrow_wgrad_kernel(const NarrowWgradArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sX[4 * WROW];
+  __shared__ __attribute__((aligned(16))) bf16 sE[SEG * 4];   // dE row y, 4 channels per pixel
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int tap = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cg = lane & 7, ph = lane >> 3;
+  const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+  float acc[4][8], bacc[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    bacc[n] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[n][i] = 0.f;
+  }
+  const int nseg = a.W / SEG;
+  const long total = (long)a.B * nseg * a.H;
+  const RowRun run = row_run(total, gridDim.x, blockIdx.x);
+  uint4 pre[WPER];
+  uint2 pe = make_uint2(0, 0);
+  auto load_row = [&](long st, int yy) {
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+#pragma unroll
+    for (int i = 0; i < WPER; ++i) {
+      const int c = tid + 576 * i;
+      const int px = c >> 3, part = c & 7, xx = x0 - 1 + px;
+      const bool ok = c < WCH && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+      pre[i] = *(const uint4*)(a.x + (ok ? ((long)(b * a.H + yy) * a.W + xx) * a.ldx + part * 8 : 0));
+      if (!ok) pre[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_row = [&](int yy) {
+    bf16* dst = sX + (yy & 3) * WROW;
+#pragma unroll
+    for (int i = 0; i < WPER; ++i) {
+      const int c = tid + 576 * i;
+      if (c < WCH) *(uint4*)(dst + (c >> 3) * WPST + (c & 7) * 8) = pre[i];
+    }
+  };
+  auto load_e = [&](long st, int yy) {   // dE row yy (inside the image), pixels x0 .. x0 + 63
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+    if (tid < SEG) pe = *(const uint2*)(a.dE + ((long)(b * a.H + yy) * a.W + x0 + tid) * a.lde);
+  };
+  long cur_strip = -1;
+  for (long g = run.g0; g < run.g1; ++g) {
+    const long st = g / a.H;
+    const int y = (int)(g - st * a.H);
+    if (st != cur_strip) {
+      __syncthreads();
+      for (int d = -1; d <= 1; ++d) {
+        load_row(st, y + d);
+        store_row(y + d + 4);
+      }
+      cur_strip = st;
+    }
+    load_e(st, y);
+    __syncthreads();   // the previous row's sE readers are done
+    if (tid < SEG) *(uint2*)(sE + tid * 4) = pe;
+    const bool more = g + 1 < run.g1 && (g + 1) / a.H == st;
+    if (more) load_row(st, y + 2);
+    __syncthreads();   // sE (and a restarted window) visible
+    const bf16* xr = sX + ((y + dy + 4) & 3) * WROW;
+#pragma unroll 2
+    for (int i = 0; i < SEG / 8; ++i) {
+      const int px = ph + 8 * i;
+      const bf16x4 e = *(const bf16x4*)(sE + px * 4);
+      const bf16x8 v = *(const bf16x8*)(xr + (1 + px + dx) * WPST + 8 * cg);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const float en = (float)e[n];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[n][k] = fmaf(en, (float)v[k], acc[n][k]);
+      }
+      if (tap == 4 && cg == 0) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bacc[n] += (float)e[n];
+      }
+    }
+    __syncthreads();   // every wave is done with row y - 1's slot
+    if (more) store_row(y + 2);
+  }
+  // reduce over the 8 pixel phases (lane bits 3..5), fixed order
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v = acc[n][i];
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      acc[n][i] = v;
+    }
+    float bv = bacc[n];
+    bv += __shfl_xor(bv, 8, 64);
+    bv += __shfl_xor(bv, 16, 64);
+    bv += __shfl_xor(bv, 32, 64);
+    bacc[n] = bv;
+  }
+  const int stride = a.NR * NF * 9 + a.NR;
+  float* dst = a.part + (long)blockIdx.x * stride;
+  if (ph == 0) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      if (n < a.NR)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dst[(n * NF + 8 * cg + i) * 9 + tap] = acc[n][i];   // reference [NR][64][3][3]
+  }
+  if (tap == 4 && lane == 0) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      if (n < a.NR) dst[a.NR * NF * 9 + n] = bacc[n];
+  }
+}
+
+// grad[e] (+)= sum over workgroups, in order
+__global__ void narrow_wgrad_finalize_kernel(const float* __restrict__ part, int nblk, int NR, float* __restrict__ gw,
+                                             float* __restrict__ gb, int accumulate) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nw = NR * NF * 9, stride = nw + NR;
+  if (e >= stride) return;
+  float s = 0.f;
+  for (int k = 0; k < nblk; ++k) s += part[(long)k * stride + e];
+  if (e < nw) gw[e] = accumulate ? gw[e] + s : s;
+  else if (gb) gb[e - nw] = accumulate ? gb[e - nw] + s : s;
+}
+
+int grid_rows(long total) {
+  const long g = (long)num_cus();
+  return (int)(total < g ? total : g);
+}
+
+}  // namespace
+
+extern "C" int kair_conv3x3_narrow_fwd(const void* x, long ldx, int lo_off, const void* w, const float* bias, int NR,
+                                       const float* mean, float img_range, const float* resid, float* out, int B, int H,
+                                       int W, void* stream) {
+  KAIR_CHECK_ARG(x && w && bias && out && NR >= 1 && NR <= 4 && B > 0 && H > 0 && W > 0, "conv3x3_narrow_fwd: bad args");
+  KAIR_CHECK_ARG(W % SEG == 0, "conv3x3_narrow_fwd: W must be a multiple of 64 (row segments)");
+  KAIR_CHECK_ARG(ldx % 8 == 0 && ldx >= NF && (lo_off == 0 || (lo_off % 8 == 0 && lo_off + NF <= ldx)) &&
+                     ((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0,
+                 "conv3x3_narrow_fwd: x rows of >= 64 bf16 channels (lo half at lo_off), 16-byte aligned");
+  KAIR_CHECK_ARG((long)B * H * W < (1L << 31), "conv3x3_narrow_fwd: too many pixels");
+  NarrowFwdArgs a;
+  a.x = (const bf16*)x; a.ldx = ldx; a.lo_off = lo_off; a.w = (const bf16*)w; a.bias = bias;
+  a.mean = mean; a.range = img_range; a.NR = NR; a.resid = resid; a.out = out;
+  a.B = B; a.H = H; a.W = W;
+  hipLaunchKernelGGL(conv3x3_narrow_fwd_kernel, dim3(grid_rows((long)B * (W / SEG) * H)), dim3(256), 0, (hipStream_t)stream, a);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" long kair_conv3x3_narrow_dgrad_ws(void) { return 4 * 2 * 64 * 8 / 2; }   // floats (bf16 fragments)
+
+extern "C" int kair_conv3x3_narrow_dgrad(const void* dE, long lde, const float* w, int NR, void* ws, void* out, int out_dtype,
+                                         long ldo, int ps_r, int B, int H, int W, void* stream) {
+  KAIR_CHECK_ARG(dE && w && ws && out && NR >= 1 && NR <= 4 && lde >= 4 && lde % 4 == 0 && ((uintptr_t)dE & 7) == 0 &&
+                     ((uintptr_t)ws & 15) == 0,
+                 "conv3x3_narrow_dgrad: dE rows of >= 4 bf16 channels, 8-byte aligned; 16-byte aligned ws");
+  KAIR_CHECK_ARG(out_dtype == KAIR_BF16 || out_dtype == KAIR_F32, "conv3x3_narrow_dgrad: out dtype");
+  KAIR_CHECK_ARG(W % SEG == 0, "conv3x3_narrow_dgrad: W must be a multiple of 64 (row segments)");
+  KAIR_CHECK_ARG(ps_r <= 1 ? ldo >= NF : (H % ps_r == 0 && W % ps_r == 0 && ldo >= (long)ps_r * ps_r * NF),
+                 "conv3x3_narrow_dgrad: output stride / PixelUnshuffle geometry");
+  KAIR_CHECK_ARG(ldo % 4 == 0 && ((uintptr_t)out & 15) == 0 && (long)B * H * W < (1L << 31), "conv3x3_narrow_dgrad: alignment");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(narrow_dgrad_pack_kernel, dim3(16), dim3(256), 0, s, w, NR, (bf16*)ws);
+  NarrowDgradArgs a;
+  a.dE = (const bf16*)dE; a.lde = lde; a.w = (const bf16*)ws; a.out = out; a.odt = out_dtype; a.ldo = ldo; a.ps_r = ps_r;
+  a.B = B; a.H = H; a.W = W;
+  hipLaunchKernelGGL(conv3x3_narrow_dgrad_kernel, dim3(grid_rows((long)B * (W / SEG) * H)), dim3(256), 0, s, a);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" long kair_conv3x3_narrow_wgrad_ws(int NR) {
+  return (long)num_cus() * (NR * NF * 9 + NR);
+}
+
+extern "C" int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x, long ldx, int NR, float* ws, float* grad_w,
+                                         float* grad_b, int accumulate, int B, int H, int W, void* stream) {
+  KAIR_CHECK_ARG(dE && x && ws && grad_w && NR >= 1 && NR <= 4 && lde >= 4 && lde % 4 == 0 && ldx >= NF && ldx % 8 == 0 &&
+                     ((uintptr_t)dE & 7) == 0 && ((uintptr_t)x & 15) == 0,
+                 "conv3x3_narrow_wgrad: bad operands");
+  KAIR_CHECK_ARG(W % SEG == 0, "conv3x3_narrow_wgrad: W must be a multiple of 64 (row segments)");
+  KAIR_CHECK_ARG((long)B * H * W < (1L << 31), "conv3x3_narrow_wgrad: too many pixels");
+  NarrowWgradArgs a;
+  a.dE = (const bf16*)dE; a.lde = lde; a.x = (const bf16*)x; a.ldx = ldx; a.NR = NR;
+  a.B = B; a.H = H; a.W = W;
+  a.part = ws;
+  const int grid = grid_rows((long)B * (W / SEG) * H);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(conv3x3_narrow_wgrad_kernel, dim3(grid), dim3(576), 0, s, a);
+  KAIR_CHECK_LAUNCH();
+  const int stride = NR * NF * 9 + NR;
+  hipLaunchKernelGGL(narrow_wgrad_finalize_kernel, dim3((stride + 255) / 256), dim3(256), 0, s, ws, grid, NR, grad_w,
+                     grad_b, accumulate);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}

@@ -125,12 +125,17 @@ class _Conv:
     bf16 weight rounding shifts every output pixel by the same sum(dW * a) and biases PSNR
     (DESIGN.md "parity at bf16"); activation rounding is unbiased and averages out."""
 
-    def __init__(self, eng, mod, Cop, Cip, need_dgrad=True, split=None, n_perm=0, tied_in=False):
+    def __init__(self, eng, mod, Cop, Cip, need_dgrad=True, split=None, n_perm=0, tied_in=False, fwd_cip=None,
+                 narrow=False):
         """n_perm = r*r: output channels stored sub-pixel-major for a following PixelShuffle(r)
         (kair_wmap.n_perm; the KAIR_OUT_PSHUF_SPM / PUNSHUF_SPM epilogues store 16 bytes at a time).
         tied_in: the forward form repeats the input channels in both halves of Cip (kair_wmap kG = 2),
         for an input held as a hi/lo pair in channels [0, Ci) and [Cip/2, Cip/2 + Ci)
-        (kair_image_to_nhwc_hilo); the weight gradient keeps the plain map (the hi channels)."""
+        (kair_image_to_nhwc_hilo); the weight gradient keeps the plain map (the hi channels).
+        fwd_cip: the forward form's packed input width when it differs from Cip (a [hi | lo] pair image of
+        2 x Cip channels read through tied weights: the SwinIR tail under split_act).
+        narrow: a 64 -> NR <= 4 conv run by the narrow-output kernels (kair_conv3x3_narrow_*): its forward
+        form is pack kind 15 (16x16x32 fragment order, hi/lo halves), the backward reads the fp32 weight."""
         self.w, self.b = mod.weight, mod.bias
         Co, Ci = self.w.shape[:2]
         self.Co, self.Ci, self.Cop, self.Cip = Co, Ci, Cop, Cip
@@ -139,13 +144,19 @@ class _Conv:
         self.split = bool(split) and eng.tdt == torch.bfloat16
         self.n_perm = n_perm
         self.map = H.wmap(1, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
-        kf_grp = (2, Ci, Cip // 2) if tied_in else (1, Ci, Cip)
+        fcip = fwd_cip or Cip
+        self.fcip = fcip
+        kf_grp = (2, Ci, fcip // 2) if tied_in else (1, Ci, Cip)
         self.mapf = H.wmap(9 if self.split else 1, Co, Ci, (1, Co, Cop), kf_grp, n_perm=n_perm)
         self.mapd = H.wmap(2, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
         self.mapb = H.wmap(4, Co, 0, (1, Co, Cop), (1, 1, 1), n_perm=n_perm)
         dev = self.w.device
-        kf = 2 * _rup(9 * Cip, 64) if self.split else 9 * Cip
+        kf = 2 * _rup(9 * fcip, 64) if self.split else 9 * fcip
         self.Wf = torch.empty(Cop, kf, device=dev, dtype=eng.tdt)
+        self.narrow = bool(narrow)
+        if self.narrow:   # the narrow kernels' forward form (their backward reads the fp32 master weight)
+            self.mapn = H.wmap(15, Co, Ci, (1, Co, 16), (1, Ci, Cip))
+            self.Wn = torch.empty(16, 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
         self.Wd = torch.empty(Cip, 9 * Cop, device=dev, dtype=eng.tdt) if need_dgrad else None
         self.bp = torch.empty(Cop, device=dev)
 
@@ -158,6 +169,8 @@ class _Conv:
         jobs = [(w, self.Wf, self.mapf), (b, self.bp, self.mapb)]
         if self.Wd is not None:
             jobs.append((w, self.Wd, self.mapd))
+        if self.narrow:
+            jobs.append((w, self.Wn, self.mapn))
         return jobs
 
 
@@ -286,11 +299,17 @@ class SwinIREngine:
         if self.upsampler == "pixelshuffle":
             self.cbu = _Conv(self, net.conv_before_upsample[0], nf, self.Cp)
             self.ups = []
+            # split_act: a0 / the upsampled activations are stored as [hi | lo] pairs (128 channels), read by
+            # the upsampling convs through weights tied over both halves (the halo kernel skips lo . lo)
             for m in net.upsample:
                 if isinstance(m, torch.nn.Conv2d):   # output channels sub-pixel-major (PSHUF_SPM)
-                    self.ups.append(_Conv(self, m, m.out_channels, nf, n_perm=m.out_channels // nf))
+                    self.ups.append(_Conv(self, m, m.out_channels, nf, n_perm=m.out_channels // nf,
+                                          tied_in=self.split_act, fwd_cip=2 * nf if self.split_act else None))
             self.ups_r = [int(math.isqrt(c.Co // nf)) for c in self.ups]
-            self.last = _Conv(self, net.conv_last, 16, nf)
+            # conv_last 64 -> in_ch on the narrow-output kernels (bf16 engine; HR width a multiple of 16)
+            # (per call: the HR width must be a multiple of 64, else the implicit-GEMM path runs)
+            self.last_narrow = self.tdt == torch.bfloat16 and self.split_conv and self.in_ch <= 4
+            self.last = _Conv(self, net.conv_last, 16, nf, narrow=self.last_narrow)
         elif self.upsampler == "pixelshuffledirect":
             conv = net.upsample[0]
             self.ups_r = [self.scale]
@@ -421,16 +440,15 @@ class SwinIREngine:
         P["fb"] = e(M, Cp)
         if self.upsampler == "pixelshuffle":
             nf = 64
-            P["a0"] = e(M, nf, dt=T)
+            # split_act: [hi | lo] pair rows (ld 2 nf); the backward reads the hi half as its bf16 operand
+            tl = P["tail_ld"] = 2 * nf if self.split_act else nf
+            P["a0"] = e(M, tl, dt=T)
             acts, hw = [], M
             for r in self.ups_r:
                 hw *= r * r
-                acts.append(e(hw, nf, dt=T))
+                acts.append(e(hw, tl, dt=T))
             P["ups_act"] = acts
             P["M_hr"] = hw
-            if self.split_act:   # lo planes of the tail activations (hi: a0 / ups_act, the backward's operands)
-                P["a0_lo"] = e(M, nf, dt=T)
-                P["ups_lo"] = [torch.empty_like(a) for a in acts]
         elif self.upsampler == "nearest+conv":
             nf = 64
             P["a0"] = e(M, nf, dt=T)
@@ -478,6 +496,9 @@ class SwinIREngine:
         P["colsum_ws"] = e(1024 * 256)
         if self.upsampler == "pixelshuffle":
             P["dE"] = e(P["M_hr"], 16, dt=T)
+            if self.last.narrow:
+                P["narrow_ws"] = e(H.conv3x3_narrow_wgrad_ws(self.in_ch))
+                P["narrow_dws"] = e(H.conv3x3_narrow_dgrad_ws())
             dpre, hw = [], M
             for c in self.ups:
                 dpre.append(e(hw, c.Co, dt=T))
@@ -648,19 +669,24 @@ class SwinIREngine:
         cd, Cp, M, B, Hh, Ww = self.cd, self.Cp, P["M"], P["B"], P["H"], P["W"]
         sa = self.split_act
         if self.upsampler == "pixelshuffle":
+            tl = P["tail_ld"]
+            lo = (lambda t: t[:, 64:]) if sa else (lambda t: None)   # the lo half of a pair buffer
             c = self.cbu
             H.gemm_nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
-                      H.epilogue(P["a0"], bias=c.bp, act=H.ACT_LEAKY, slope=0.01, out_lo=P["a0_lo"] if sa else None), M, 64,
+                      H.epilogue(P["a0"], ldo=tl, bias=c.bp, act=H.ACT_LEAKY, slope=0.01, out_lo=lo(P["a0"])), M, 64,
                       9 * Cp, cd)
-            src, src_lo, h, w = P["a0"], P.get("a0_lo"), Hh, Ww
-            for i, (c, r, dst) in enumerate(zip(self.ups, self.ups_r, P["ups_act"])):
-                dst_lo = P["ups_lo"][i] if sa else None
-                H.gemm_nt(self._ain(H.im2col(src, h, w, 64), src_lo), c.fwd(),
-                          H.epilogue(dst, mode=H.OUT_PSHUF_SPM, ldo=64, bias=c.bp, ps=(r, h, w), out_lo=dst_lo),
-                          B * h * w, c.Co, 9 * 64, cd)
-                src, src_lo, h, w = dst, dst_lo, h * r, w * r
+            src, h, w = P["a0"], Hh, Ww
+            for c, r, dst in zip(self.ups, self.ups_r, P["ups_act"]):
+                A = H.asplit(H.im2col(src, h, w, c.fcip), pair=True) if sa else H.im2col(src, h, w, 64)
+                H.gemm_nt(A, c.fwd(), H.epilogue(dst, mode=H.OUT_PSHUF_SPM, ldo=tl, bias=c.bp, ps=(r, h, w), out_lo=lo(dst)),
+                          B * h * w, c.Co, 9 * c.fcip, cd)
+                src, h, w = dst, h * r, w * r
             c = self.last
-            H.gemm_nt(self._ain(H.im2col(src, h, w, 64), src_lo), c.fwd(),
+            if c.narrow and w % 64 == 0:   # 64 -> in_ch: the narrow-output kernel (weights in VGPRs)
+                H.conv3x3_narrow_fwd(src, tl, 64 if sa else 0, c.Wn, c.bp, self.in_ch, self.mean, self.img_range, None,
+                                     P["E"], B, h, w)
+                return P["E"]
+            H.gemm_nt(self._ain(H.im2col(src, h, w, 64, ld=tl), lo(src)), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(self.mean, self.img_range, self.in_ch, h, w)),
                       B * h * w, c.Cop, 9 * 64, cd)
         elif self.upsampler == "nearest+conv":
@@ -814,14 +840,20 @@ class SwinIREngine:
                 h, w = h * r, w * r
             c = self.last
             src = P["ups_act"][-1]
+            tl = P["tail_ld"]   # the activations' row stride (a [hi | lo] pair under split_act: the hi half is read)
             # conv_last: dgrad into the pre-shuffle layout of the last upsampling conv
             r_last = self.ups_r[-1]
-            H.gemm_nt(H.im2col(P["dE"], h, w, 16, flip=True), H.rows(c.Wd),
-                      H.epilogue(P["dpre"][-1], mode=H.OUT_PUNSHUF_SPM, ldo=self.ups[-1].Co,
-                                 ps=(r_last, h // r_last, w // r_last)),
-                      B * h * w, 64, 9 * 16, cd)
-            self._wgrad(P, H.rows(P["dE"]), H.im2col(src, h, w, 64), B * h * w, 16, 9 * 64, c.map, g(c.w))
-            self._bias_colsum(P, H.rows(P["dE"]), B * h * w, 16, c.mapb, g(c.b))
+            if c.narrow and w % 64 == 0:   # the narrow-output kernels (rolling row window, fp32 master weight)
+                H.conv3x3_narrow_dgrad(P["dE"], 16, c.w.detach(), self.in_ch, P["narrow_dws"], P["dpre"][-1], self.ups[-1].Co,
+                                       r_last, B, h, w)
+                H.conv3x3_narrow_wgrad(P["dE"], 16, src, tl, self.in_ch, P["narrow_ws"], g(c.w), g(c.b), B, h, w)
+            else:
+                H.gemm_nt(H.im2col(P["dE"], h, w, 16, flip=True), H.rows(c.Wd),
+                          H.epilogue(P["dpre"][-1], mode=H.OUT_PUNSHUF_SPM, ldo=self.ups[-1].Co,
+                                     ps=(r_last, h // r_last, w // r_last)),
+                          B * h * w, 64, 9 * 16, cd)
+                self._wgrad(P, H.rows(P["dE"]), H.im2col(src, h, w, 64, ld=tl), B * h * w, 16, 9 * 64, c.map, g(c.w))
+                self._bias_colsum(P, H.rows(P["dE"]), B * h * w, 16, c.mapb, g(c.b))
             # upsampling convs, last to first
             for i in range(len(self.ups) - 1, -1, -1):
                 c, r = self.ups[i], self.ups_r[i]
@@ -836,8 +868,8 @@ class SwinIREngine:
                               B * h * w, 64, 9 * c.Co, cd)
                 else:
                     H.gemm_nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),
-                              H.epilogue(P["da0"], gate=P["a0"], gate_kind=2, slope=0.01), M, 64, 9 * c.Co, cd)
-                self._wgrad(P, H.rows(dpre), H.im2col(src, h, w, 64), B * h * w, c.Co, 9 * 64, c.map, g(c.w))
+                              H.epilogue(P["da0"], gate=P["a0"], ldg=tl, gate_kind=2, slope=0.01), M, 64, 9 * c.Co, cd)
+                self._wgrad(P, H.rows(dpre), H.im2col(src, h, w, 64, ld=tl), B * h * w, c.Co, 9 * 64, c.map, g(c.w))
                 self._bias_colsum(P, H.rows(dpre), B * h * w, c.Co, c.mapb, g(c.b))
             c = self.cbu
             H.gemm_nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)

@@ -97,43 +97,63 @@ def test_conv_asplit_fp32_image(shape, resid):
     assert errs[0] < 3e-5 and errs[1] > 8 * errs[0], errs
 
 
-def test_conv_asplit_hilo_planes():
-    """A producer conv writes its bf16 output + lo plane (PSHUF_SPM, out_lo); the next conv reads the
-    pair (a_split with lo_ptr) -- the SwinIR x4 upsampling chain a0 -> ups conv -> conv_last."""
-    B, Hh, Ww, Cin, r = 2, 12, 16, 64, 2
+@pytest.mark.parametrize("hw", [(12, 16), (8, 8)])
+def test_conv_asplit_hilo_pairs(hw):
+    """The SwinIR x4 tail chain under split_act: a producer conv (fp32 image, two-pass split) writes its
+    PixelShuffle output as a [hi | lo] pair (PSHUF_SPM, out_lo = the second half of each 128-wide row);
+    a second upsampling conv reads the pair as one 128-channel image through weights tied over both
+    halves (a_split 2: the halo kernel, N = 256 in two 128-wide tiles, skips lo . lo); conv_last-style
+    N = 16 convs read the hi half with the lo half as lo plane (a_split 1).  (12, 16): halo kernels;
+    (8, 8): 8x8 images, the register-staged fallback for the producer."""
+    B, Cin, r = 2, 64, 2
+    Hh, Ww = hw
     Cmid = 64 * r * r
     g = torch.Generator().manual_seed(17)
     x = torch.randn(B, Cin, Hh, Ww, generator=g)
     w1 = torch.randn(Cmid, Cin, 3, 3, generator=g) * 0.05
     b1 = torch.randn(Cmid, generator=g) * 0.1
-    w2 = torch.randn(3, 64, 3, 3, generator=g) * 0.05
-    mid = torch.nn.functional.pixel_shuffle(torch.nn.functional.conv2d(x.double(), w1.double(), b1.double(), padding=1), r)
-    ref = torch.nn.functional.conv2d(mid, w2.double(), padding=1)
+    w2 = torch.randn(Cmid, 64, 3, 3, generator=g) * 0.05
+    w3 = torch.randn(3, 64, 3, 3, generator=g) * 0.05
+    F = torch.nn.functional
+    mid = F.pixel_shuffle(F.conv2d(x.double(), w1.double(), b1.double(), padding=1), r)
+    mid2 = F.pixel_shuffle(F.conv2d(mid, w2.double(), padding=1), r)
+    ref3 = F.conv2d(mid, w3.double(), padding=1)
     M = B * Hh * Ww
     xin = x.permute(0, 2, 3, 1).contiguous().view(M, Cin).to(dev)
     W1 = torch.empty(Cmid, 2 * ((9 * Cin + 63) // 64) * 64, device=dev, dtype=torch.bfloat16)
     H.pack_weight(w1.to(dev), W1, H.wmap(9, Cmid, Cin, (1, Cmid, Cmid), (1, Cin, Cin), n_perm=r * r))
     b1p = torch.empty(Cmid, device=dev)
     H.pack_weight(b1.to(dev), b1p, H.wmap(4, Cmid, 0, (1, Cmid, Cmid), (1, 1, 1), n_perm=r * r))
-    W2 = split_w(w2, 3, 64, Cop=16)
-    hi = torch.empty(M * r * r, 64, device=dev, dtype=torch.bfloat16)
-    lo = torch.empty_like(hi)
+    pair = torch.empty(M * r * r, 128, device=dev, dtype=torch.bfloat16)
     H.gemm_nt(H.asplit(H.im2col(xin, Hh, Ww, Cin)), H.rows(W1, w_split=True),
-              H.epilogue(hi, mode=H.OUT_PSHUF_SPM, ldo=64, bias=b1p, ps=(r, Hh, Ww), out_lo=lo), M, Cmid, 9 * Cin, H.BF16)
+              H.epilogue(pair, mode=H.OUT_PSHUF_SPM, ldo=128, bias=b1p, ps=(r, Hh, Ww), out_lo=pair[:, 64:]),
+              M, Cmid, 9 * Cin, H.BF16)
     torch.cuda.synchronize()
-    mid_got = (hi.double() + lo.double()).cpu().view(B, Hh * r, Ww * r, 64).permute(0, 3, 1, 2)
+    mid_got = (pair[:, :64].double() + pair[:, 64:].double()).cpu().view(B, Hh * r, Ww * r, 64).permute(0, 3, 1, 2)
     assert rel_err(mid_got, mid) < 3e-5
     h2, w2_ = Hh * r, Ww * r
+    M2 = B * h2 * w2_
+    # second upsampling conv over the pair image, tied split weights
+    W2 = torch.empty(Cmid, 2 * 9 * 128, device=dev, dtype=torch.bfloat16)
+    H.pack_weight(w2.to(dev), W2, H.wmap(9, Cmid, 64, (1, Cmid, Cmid), (2, 64, 64), n_perm=r * r))
+    out2 = torch.empty(M2 * r * r, 64, device=dev)
+    H.gemm_nt(H.asplit(H.im2col(pair, h2, w2_, 128), pair=True), H.rows(W2, w_split=True),
+              H.epilogue(out2, mode=H.OUT_PSHUF_SPM, ldo=64, ps=(r, h2, w2_)), M2, Cmid, 9 * 128, H.BF16)
+    torch.cuda.synchronize()
+    got2 = out2.cpu().view(B, h2 * r, w2_ * r, 64).permute(0, 3, 1, 2)
+    assert rel_err(got2, mid2) < 5e-5
+    # conv_last over the pair: hi half + lo plane, and the hi half alone (plain bf16 activation)
+    W3 = split_w(w3, 3, 64, Cop=16)
     errs = []
     for split in (True, False):
         img = torch.empty(B, 3, h2, w2_, device=dev)
-        A = H.im2col(hi, h2, w2_, 64)
+        A = H.im2col(pair, h2, w2_, 64, ld=128)
         if split:
-            A = H.asplit(A, lo)
-        H.gemm_nt(A, H.rows(W2, w_split=True), H.epilogue(img, mode=H.OUT_NCHW, ldo=0, img=(None, 1.0, 3, h2, w2_)),
-                  B * h2 * w2_, 16, 9 * 64, H.BF16)
+            A = H.asplit(A, pair[:, 64:])
+        H.gemm_nt(A, H.rows(W3, w_split=True), H.epilogue(img, mode=H.OUT_NCHW, ldo=0, img=(None, 1.0, 3, h2, w2_)),
+                  M2, 16, 9 * 64, H.BF16)
         torch.cuda.synchronize()
-        errs.append(rel_err(img, ref))
+        errs.append(rel_err(img, ref3))
     assert errs[0] < 5e-5 and errs[1] > 8 * errs[0], errs
 
 
