@@ -71,7 +71,7 @@ constexpr int FROW = PXS * FPST;        // one staged row
 constexpr int FCH = PXS * 16;           // 16-byte chunks per staged row (hi + lo: 16 per pixel)
 constexpr int FPER = (FCH + 255) / 256; // chunks per thread
 
-__global__ __launch_bounds__(256, 1) void conv3x3_narrow_fwd_kernel(const NarrowFwdArgs a) {
+__global__ __launch_bounds__(256, 2) void conv3x3_narrow_fwd_kernel(const NarrowFwdArgs a) {
   constexpr int KS = 9 * NF / 32;   // 18 k-steps of 32: (tap, channel half)
   __shared__ __attribute__((aligned(16))) bf16 sRow[4 * FROW];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -129,7 +129,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_narrow_fwd_kernel(const Narrow
     const bool more = g + 1 < run.g1 && (g + 1) / a.H == st;
     if (more) load_row(st, y + 2);   // in flight during this row's MFMAs
     // wave w: output pixels x0 + 16 w + pl
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // three independent accumulator chains (hi.w_hi, hi.w_lo, lo.w_hi), summed at the end
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = acc, acc2 = acc;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int dy = tap / 3 - 1, dx = tap % 3 - 1;
@@ -139,13 +140,14 @@ __global__ __launch_bounds__(256, 1) void conv3x3_narrow_fwd_kernel(const Narrow
         const bf16x8 xh = *(const bf16x8*)(src + 32 * ks);
         const int kb = tap * 2 + ks;
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[kb], xh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[kb], xh, acc, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[kb], xh, acc1, 0, 0, 0);
         if (split) {
           const bf16x8 xl = *(const bf16x8*)(src + 64 + 32 * ks);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[kb], xl, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[kb], xl, acc2, 0, 0, 0);
         }
       }
     }
+    acc += acc1 + acc2;
     if (lane < 16) {   // D[n][px]: lanes 0..15 hold n = 0..3 of pixel pl
       const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
       const long HW = (long)a.H * a.W;
@@ -282,25 +284,28 @@ struct NarrowWgradArgs {
   float* part;                          // [gridDim.x][NR * 64 * 9 + NR]
 };
 
-constexpr int WPST = 72;                // staged X: 64 channels + 8 per pixel (144 B)
+constexpr int WPST = 68;                // staged X, fp32: 64 channels + 4 per pixel (272 B)
 constexpr int WROW = PXS * WPST;
-constexpr int WCH = PXS * 8;            // 16-byte chunks per staged X row
+constexpr int WCH = PXS * 8;            // 16-byte bf16 chunks per X row (8 channels each)
 constexpr int WPER = (WCH + 575) / 576;
 
-// 9 waves (wave = tap); lane: channel group cg = lane & 7 (8 channels), pixel phase ph = lane >> 3
+// 9 waves (wave = tap); lane: channel group cg = lane & 7 (8 channels), pixel phase ph = lane >> 3.
+// X rows and the dE row are staged as fp32 (converted once per element, read by all nine taps), the
+// products run as packed fp32 FMAs (v_pk_fma_f32: two channels per instruction).
 __global__ __launch_bounds__(576) void conv3x3_narrow_wgrad_kernel(const NarrowWgradArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 sX[4 * WROW];
-  __shared__ __attribute__((aligned(16))) bf16 sE[SEG * 4];   // dE row y, 4 channels per pixel
+  __shared__ __attribute__((aligned(16))) float sX[4 * WROW];
+  __shared__ __attribute__((aligned(16))) float sE[2 * SEG * 4];   // dE rows y, y+1 (4 channels per pixel)
   const int tid = threadIdx.x, lane = tid & 63;
   const int tap = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cg = lane & 7, ph = lane >> 3;
   const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-  float acc[4][8], bacc[4];
+  f32x2 acc[4][4];
+  float bacc[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
     bacc[n] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[n][i] = 0.f;
+    for (int i = 0; i < 4; ++i) acc[n][i] = f32x2{0.f, 0.f};
   }
   const int nseg = a.W / SEG;
   const long total = (long)a.B * nseg * a.H;
@@ -319,66 +324,88 @@ __global__ __launch_bounds__(576) void conv3x3_narrow_wgrad_kernel(const NarrowW
     }
   };
   auto store_row = [&](int yy) {
-    bf16* dst = sX + (yy & 3) * WROW;
+    float* dst = sX + (yy & 3) * WROW;
 #pragma unroll
     for (int i = 0; i < WPER; ++i) {
       const int c = tid + 576 * i;
-      if (c < WCH) *(uint4*)(dst + (c >> 3) * WPST + (c & 7) * 8) = pre[i];
+      if (c < WCH) {
+        const bf16x8 v = __builtin_bit_cast(bf16x8, pre[i]);
+        float* d = dst + (c >> 3) * WPST + (c & 7) * 8;
+        *(float4*)d = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+        *(float4*)(d + 4) = make_float4((float)v[4], (float)v[5], (float)v[6], (float)v[7]);
+      }
     }
   };
   auto load_e = [&](long st, int yy) {   // dE row yy (inside the image), pixels x0 .. x0 + 63
     const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
     if (tid < SEG) pe = *(const uint2*)(a.dE + ((long)(b * a.H + yy) * a.W + x0 + tid) * a.lde);
   };
+  auto store_e = [&](int yy) {
+    if (tid < SEG) {
+      const bf16x4 e = __builtin_bit_cast(bf16x4, pe);
+      *(float4*)(sE + (yy & 1) * SEG * 4 + tid * 4) = make_float4((float)e[0], (float)e[1], (float)e[2], (float)e[3]);
+    }
+  };
   long cur_strip = -1;
   for (long g = run.g0; g < run.g1; ++g) {
     const long st = g / a.H;
     const int y = (int)(g - st * a.H);
-    if (st != cur_strip) {
+    if (st != cur_strip) {   // (re)start: X rows y-1 .. y+1, dE row y
       __syncthreads();
       for (int d = -1; d <= 1; ++d) {
         load_row(st, y + d);
         store_row(y + d + 4);
       }
+      load_e(st, y);
+      store_e(y);
       cur_strip = st;
+      __syncthreads();
     }
-    load_e(st, y);
-    __syncthreads();   // the previous row's sE readers are done
-    if (tid < SEG) *(uint2*)(sE + tid * 4) = pe;
+    // the next rows' operands (X row y+2, dE row y+1) in flight during this row's products
     const bool more = g + 1 < run.g1 && (g + 1) / a.H == st;
-    if (more) load_row(st, y + 2);
-    __syncthreads();   // sE (and a restarted window) visible
-    const bf16* xr = sX + ((y + dy + 4) & 3) * WROW;
+    if (more) {
+      load_row(st, y + 2);
+      load_e(st, y + 1);
+    }
+    const float* xr = sX + ((y + dy + 4) & 3) * WROW + 8 * cg;
+    const float* er = sE + (y & 1) * SEG * 4;
 #pragma unroll 2
     for (int i = 0; i < SEG / 8; ++i) {
       const int px = ph + 8 * i;
-      const bf16x4 e = *(const bf16x4*)(sE + px * 4);
-      const bf16x8 v = *(const bf16x8*)(xr + (1 + px + dx) * WPST + 8 * cg);
+      const float4 e = *(const float4*)(er + px * 4);
+      const float4 v0 = *(const float4*)(xr + (1 + px + dx) * WPST);
+      const float4 v1 = *(const float4*)(xr + (1 + px + dx) * WPST + 4);
+      const f32x2 v[4] = {f32x2{v0.x, v0.y}, f32x2{v0.z, v0.w}, f32x2{v1.x, v1.y}, f32x2{v1.z, v1.w}};
+      const float en[4] = {e.x, e.y, e.z, e.w};
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const float en = (float)e[n];
+      for (int n = 0; n < 4; ++n)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[n][k] = fmaf(en, (float)v[k], acc[n][k]);
-      }
+        for (int k = 0; k < 4; ++k) acc[n][k] = __builtin_elementwise_fma(f32x2{en[n], en[n]}, v[k], acc[n][k]);
       if (tap == 4 && cg == 0) {
 #pragma unroll
-        for (int n = 0; n < 4; ++n) bacc[n] += (float)e[n];
+        for (int n = 0; n < 4; ++n) bacc[n] += en[n];
       }
     }
-    __syncthreads();   // every wave is done with row y - 1's slot
-    if (more) store_row(y + 2);
+    __syncthreads();   // every wave is done with row y - 1's X slot and dE row y - 1's buffer
+    if (more) {
+      store_row(y + 2);
+      store_e(y + 1);
+    }
+    __syncthreads();
   }
   // reduce over the 8 pixel phases (lane bits 3..5), fixed order
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float v = acc[n][i];
-      v += __shfl_xor(v, 8, 64);
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      acc[n][i] = v;
-    }
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float v = acc[n][i][h];
+        v += __shfl_xor(v, 8, 64);
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        acc[n][i][h] = v;
+      }
     float bv = bacc[n];
     bv += __shfl_xor(bv, 8, 64);
     bv += __shfl_xor(bv, 16, 64);
@@ -392,7 +419,7 @@ __global__ __launch_bounds__(576) void conv3x3_narrow_wgrad_kernel(const NarrowW
     for (int n = 0; n < 4; ++n)
       if (n < a.NR)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dst[(n * NF + 8 * cg + i) * 9 + tap] = acc[n][i];   // reference [NR][64][3][3]
+        for (int i = 0; i < 8; ++i) dst[(n * NF + 8 * cg + i) * 9 + tap] = acc[n][i >> 1][i & 1];   // reference [NR][64][3][3]
   }
   if (tap == 4 && lane == 0) {
 #pragma unroll
@@ -413,8 +440,9 @@ __global__ void narrow_wgrad_finalize_kernel(const float* __restrict__ part, int
   else if (gb) gb[e - nw] = accumulate ? gb[e - nw] + s : s;
 }
 
-int grid_rows(long total) {
-  const long g = (long)num_cus();
+// persistent workgroups: `per_cu` per CU (row runs of equal length)
+int grid_rows(long total, int per_cu) {
+  const long g = (long)num_cus() * per_cu;
   return (int)(total < g ? total : g);
 }
 
@@ -433,7 +461,9 @@ extern "C" int kair_conv3x3_narrow_fwd(const void* x, long ldx, int lo_off, cons
   a.x = (const bf16*)x; a.ldx = ldx; a.lo_off = lo_off; a.w = (const bf16*)w; a.bias = bias;
   a.mean = mean; a.range = img_range; a.NR = NR; a.resid = resid; a.out = out;
   a.B = B; a.H = H; a.W = W;
-  hipLaunchKernelGGL(conv3x3_narrow_fwd_kernel, dim3(grid_rows((long)B * (W / SEG) * H)), dim3(256), 0, (hipStream_t)stream, a);
+  // two workgroups per CU (72 KB LDS, <= 256 VGPRs each): one computes while the other waits on its rows
+  hipLaunchKernelGGL(conv3x3_narrow_fwd_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 2)), dim3(256), 0,
+                     (hipStream_t)stream, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -455,13 +485,13 @@ extern "C" int kair_conv3x3_narrow_dgrad(const void* dE, long lde, const float* 
   NarrowDgradArgs a;
   a.dE = (const bf16*)dE; a.lde = lde; a.w = (const bf16*)ws; a.out = out; a.odt = out_dtype; a.ldo = ldo; a.ps_r = ps_r;
   a.B = B; a.H = H; a.W = W;
-  hipLaunchKernelGGL(conv3x3_narrow_dgrad_kernel, dim3(grid_rows((long)B * (W / SEG) * H)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(conv3x3_narrow_dgrad_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 4)), dim3(256), 0, s, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" long kair_conv3x3_narrow_wgrad_ws(int NR) {
-  return (long)num_cus() * (NR * NF * 9 + NR);
+  return 2L * num_cus() * (NR * NF * 9 + NR);
 }
 
 extern "C" int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x, long ldx, int NR, float* ws, float* grad_w,
@@ -475,7 +505,7 @@ extern "C" int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x
   a.dE = (const bf16*)dE; a.lde = lde; a.x = (const bf16*)x; a.ldx = ldx; a.NR = NR;
   a.B = B; a.H = H; a.W = W;
   a.part = ws;
-  const int grid = grid_rows((long)B * (W / SEG) * H);
+  const int grid = grid_rows((long)B * (W / SEG) * H, 2);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(conv3x3_narrow_wgrad_kernel, dim3(grid), dim3(576), 0, s, a);
   KAIR_CHECK_LAUNCH();
