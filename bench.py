@@ -403,6 +403,8 @@ def main():
                     help="skip the short single-GPU throughput lines of BASELINE.json configs C2 / C3 / C5 (and the "
                          "C1 network on the GPU)")
     ap.add_argument("--no-roles", action="store_true", help="skip the in-step per-kernel timing pass")
+    ap.add_argument("--no-psnr", action="store_true",
+                    help="skip the PSNR parity evaluation (profiling runs: only full-batch dispatches)")
     ap.add_argument("--side-ctas", type=int, default=None,
                     help="A/B: workgroup budget of the side-stream launches (< 0: that many times more row splits)")
     ap.add_argument("--side-priority", type=int, default=0, help="A/B: torch priority of the side stream")
@@ -573,10 +575,11 @@ def main():
                                                 roles=not args.no_roles)
         except Exception as e:  # noqa: BLE001
             out["fp32_parity_line"] = {"error": repr(e)}
-    try:
-        out["psnr"] = psnr_parity(net, device)
-    except Exception as e:  # noqa: BLE001
-        out["psnr"] = {"error": repr(e)}
+    if not args.no_psnr:
+        try:
+            out["psnr"] = psnr_parity(net, device)
+        except Exception as e:  # noqa: BLE001
+            out["psnr"] = {"error": repr(e)}
     if world == 1 and args.dtype == "bf16" and not args.no_other_configs:
         out["other_configs"] = other_configs(device)
     if world == 1 and not args.no_cpu_baseline:

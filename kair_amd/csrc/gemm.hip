@@ -1581,17 +1581,21 @@ constexpr int HC_EM_ROWS = 0, HC_EM_PSHUF = 1;   // epilogue: token rows / Pixel
 // N-tile count so a workgroup's N tile -- its bias and weight rows -- never changes).
 // bf16 A with a_split == 2: the image's channels are [hi | lo] halves of one activation and the
 // weights (hi/lo split, tied over the halves) give 4 chunk products per tap; the lo.lo one is skipped.
-template <typename TA, int EX, int NPASS, int BN, int EM>
+// BM: output pixels per tile, 96 or (128-wide N tiles of images with <= 128 channels) 192 -- twice the
+// pixels per streamed weight chunk, so half the weight traffic from L2 (the upsampling convs' bound).
+template <int BM> struct HaloSize { static constexpr int ELEMS = BM == 96 ? HC_HALO_ELEMS : 57344; };
+template <typename TA, int EX, int NPASS, int BN, int EM, int BM>
 __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E, int K, int tilesM) {
-  constexpr int WM = 2, WN = 4, TM = HC_BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
+  constexpr int WM = 2, WN = 4, TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
   constexpr int NI = BN / 64;   // LDS-DMA wave-instructions per weight chunk (8 rows x 128 B each)
-  __shared__ __attribute__((aligned(16))) bf16 sHalo[HC_HALO_ELEMS];
+  constexpr int HALO = HaloSize<BM>::ELEMS, HPER = HALO / 8 / 512;
+  __shared__ __attribute__((aligned(16))) bf16 sHalo[HALO];
   __shared__ __attribute__((aligned(16))) bf16 sBw[3][BN * HC_BK];   // LDS-DMA ring of weight chunks
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fq = lane >> 4;
   const int H = A.imH, W = A.imW, C = A.imC;
-  const int XW = W < HC_BM ? W : HC_BM, RPT = HC_BM / XW, HWD = XW + 2, HR = RPT + 2, PS = C + 8;
+  const int XW = W < BM ? W : BM, RPT = BM / XW, HWD = XW + 2, HR = RPT + 2, PS = C + 8;
   const int sh = B.wsplit;   // hi/lo split weights: weight chunk j pairs with halo chunk j >> 1
   // NPASS 2 -- hi/lo split activations (fp32 A, kair_operand.a_split): a second pass over the tile with
   // the halo refilled by the lo halves bf16(x - bf16(x)) and only the hi weight chunks (the a_lo . w_hi
@@ -1662,7 +1666,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
   };
 
   for (int t = blockIdx.x / tilesN; t < tilesM; t += gridDim.x / tilesN) {
-    const long p0 = (long)t * HC_BM;
+    const long p0 = (long)t * BM;
     const int b = (int)(p0 / ((long)H * W));
     const int rem = (int)(p0 - (long)b * H * W);
     const int y0 = rem / W, x0 = rem - (rem / W) * W;
@@ -1695,7 +1699,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
       // converted and written: a load whose value a path ignores becomes a branch + wait each
       constexpr int HP = 5;   // pieces per batch (register budget for fp32 pieces)
 #pragma unroll
-      for (int h0 = 0; h0 < HC_PER; h0 += HP) {
+      for (int h0 = 0; h0 < HPER; h0 += HP) {
         uint4 lo[HP], hi[HP];
         bool okv[HP];
 #pragma unroll
@@ -1761,7 +1765,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
       // chunk j landed for this wave (younger: chunk j+1's NI DMA instructions), then all waves
       if (j + 1 < nkp) {
         if constexpr (NI == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if constexpr (NI == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -1863,22 +1868,38 @@ extern "C" int kair_conv3x3_halo_geometry(int H, int W, int C, long M, int N) {
   return M % HC_BM == 0 && M % ((long)H * W) == 0 && C % 8 == 0;
 }
 
+// the 192-pixel tile (128-wide N tiles only): whole rows of width W <= 192 or 192-pixel row pieces
+static bool halo_bm192_ok(const Op& A, long M) {
+  const int H = A.imH, W = A.imW, C = A.imC;
+  if (W <= 192) {
+    if (192 % W != 0 || H % (192 / W) != 0) return false;
+  } else if (W % 192 != 0) {
+    return false;
+  }
+  const int XW = W < 192 ? W : 192, RPT = 192 / XW;
+  return (long)(RPT + 2) * (XW + 2) * (C + 8) <= HaloSize<192>::ELEMS && M % 192 == 0 && M % ((long)H * W) == 0;
+}
+
 template <typename TA>
 static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int K, hipStream_t s) {
   if (g_num_cus == 0) init_num_cus();
-  const int tilesM = (int)(M / HC_BM);
   const bool wide = E.N > HC_BN;   // N in (192, 256]: two 128-wide N tiles
+  const bool big = wide && !E.resid && A.asplit != 1 && halo_bm192_ok(A, M);   // (the two-pass form would spill)
+  const int tilesM = (int)(M / (big ? 192 : HC_BM));
   const int tilesN = wide ? (E.N + 127) / 128 : 1;
   long tiles = (long)tilesM * tilesN;
   int grid = (int)(tiles < g_num_cus ? tiles : (g_num_cus / tilesN) * tilesN);   // a multiple of tilesN
-#define KAIR_HALO(NP, EXV, BNV, EMV) \
-  hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EXV, NP, BNV, EMV>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM)
-#define KAIR_HALO_NP(NP)                                                                  \
-  if (E.resid) KAIR_HALO(NP, EX_RESID, 192, HC_EM_ROWS);                                  \
-  else if (E.omode == KAIR_OUT_PSHUF_SPM && wide) KAIR_HALO(NP, EX_NONE, 128, HC_EM_PSHUF); \
-  else if (E.omode == KAIR_OUT_PSHUF_SPM) KAIR_HALO(NP, EX_NONE, 192, HC_EM_PSHUF);        \
-  else if (wide) KAIR_HALO(NP, EX_NONE, 128, HC_EM_ROWS);                                  \
-  else KAIR_HALO(NP, EX_NONE, 192, HC_EM_ROWS);
+#define KAIR_HALO(NP, EXV, BNV, EMV, BMV) \
+  hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EXV, NP, BNV, EMV, BMV>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM)
+#define KAIR_HALO_NP(NP)                                                                           \
+  if (E.resid) KAIR_HALO(NP, EX_RESID, 192, HC_EM_ROWS, 96);                                       \
+  else if (E.omode == KAIR_OUT_PSHUF_SPM && big) KAIR_HALO(NP, EX_NONE, 128, HC_EM_PSHUF, 192);     \
+  else if (E.omode == KAIR_OUT_PSHUF_SPM && wide) KAIR_HALO(NP, EX_NONE, 128, HC_EM_PSHUF, 96);     \
+  else if (E.omode == KAIR_OUT_PSHUF_SPM) KAIR_HALO(NP, EX_NONE, 192, HC_EM_PSHUF, 96);             \
+  else if (big) KAIR_HALO(NP, EX_NONE, 128, HC_EM_ROWS, 192);                                       \
+  else if (wide) KAIR_HALO(NP, EX_NONE, 128, HC_EM_ROWS, 96);                                       \
+  else if (E.N <= 64) KAIR_HALO(NP, EX_NONE, 64, HC_EM_ROWS, 96);                                   \
+  else KAIR_HALO(NP, EX_NONE, 192, HC_EM_ROWS, 96);
   if constexpr (sizeof(TA) == 4) {
     if (A.asplit) {   // conv_halo_ok: the two-pass split takes an fp32 A only
       KAIR_HALO_NP(2)

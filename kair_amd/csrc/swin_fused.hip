@@ -30,6 +30,9 @@
 namespace {
 
 constexpr int TOK = 64, WSZ = 8;
+#ifndef KAIR_ATTN12
+#define KAIR_ATTN12 1
+#endif
 
 KAIR_DEV int acc_row32(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 KAIR_DEV int shift_region(int coord, int n, int shift) { return coord < n - WSZ ? 0 : (coord < n - shift ? 1 : 2); }
@@ -478,6 +481,357 @@ __global__ __launch_bounds__(64 * NH) void swin_attn_fwd_kernel(const AttnFwdArg
         g_fused_stamps[((long)blockIdx.x * NH + w) * FST_N + lane] = v;
       }
     }
+  }
+}
+
+
+// ---- attention half, 12 waves: two per head ------------------------------------------------------
+// The same program as swin_attn_fwd_kernel, balanced over the four SIMDs: wave w = 2 h + q owns head h
+// and query / token tile q (tokens 32 q .. 32 q + 31) of the window, so every SIMD carries three waves
+// and 1.5 heads' work (the 6-wave kernel's SIMDs 0 / 1 carry two heads each and set the pace of every
+// head phase).  Per window:
+//   A  LayerNorm, rows w + 12 i (16 rows per SIMD);
+//   B  q^T, k^T and v of head h for the wave's 32 tokens (36 MFMAs 32x32x16 instead of 72): its k half
+//      goes to the partner wave through LDS in MFMA-fragment form, its v half through the v-transpose
+//      scratch that also feeds the saved v rows;
+//   C  S^T of the wave's 32 queries x 64 keys, softmax, O^T = V^T P^T into the O tile;
+//   D  proj: wave w makes output channels 32 (w >> 1) .. +31 of token tile w & 1;
+// then the stores, spread over all twelve waves.  Saves exactly what the 6-wave kernel saves.
+template <int NH>
+__global__ __launch_bounds__(128 * NH) void swin_attn_fwd12_kernel(const AttnFwdArgs a) {
+  constexpr int CP = 32 * NH, LDT = CP + 8, LDX = CP + 4, KB = CP / 16;
+  constexpr int NW = 2 * NH, PF = 3, WS = 512;
+  constexpr int RPW = (TOK + NW - 1) / NW;   // LN rows per wave (6)
+  static_assert(KB % PF == 0, "k-steps must be a multiple of the prefetch depth");
+  static_assert(CP == 192, "laid out for Cp = 192");
+  __shared__ __attribute__((aligned(16))) bf16 sT[TOK * LDT];   // LN1 tile
+  // O tile; before phase C it carries the k fragments exchanged between the two waves of a head
+  __shared__ __attribute__((aligned(16))) bf16 sO[TOK * LDT];
+  __shared__ __attribute__((aligned(16))) float sX[TOK * LDX];  // x rows (fp32) for the residual
+  __shared__ float sTabR[NH][232];
+  __shared__ float sBias[3 * NH * 32];
+  __shared__ float sGB[2][CP];
+  __shared__ int sReg[TOK];
+  __shared__ int sRow[TOK];
+  __shared__ float sMean[TOK], sRstd[TOK];
+  constexpr int LDV = 40;
+  __shared__ __attribute__((aligned(16))) bf16 sV[NH][TOK * LDV];   // v rows [tok][d] of each head
+  static_assert(NH * 2 * 2 * 64 * 8 <= TOK * LDT, "the k exchange must fit the O tile");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l31 = lane & 31, hh = lane >> 5;
+  const int h = w >> 1, q = w & 1;   // head, token / query tile
+  const long M = a.nWin * TOK;
+  bf16* sVh = sV[h];
+  bf16* sK = sO;   // [NH][2 tiles][2 s][64 lanes][8]
+  const int c = 32 * h + l31;   // phase D output channel of this lane (channel block h, token tile q)
+  long win = blockIdx.x;
+
+  constexpr int NPASS = (RPW + 3) / 4;
+  const int g = lane >> 4, jl = lane & 15;
+  float4 xv[NPASS][3];
+  auto load_x = [&](long wn) {
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int i = 4 * p + g, r = w + NW * i;
+      const long wc = wn < a.nWin ? wn : a.nWin - 1;
+      const int rr = i < RPW && r < TOK ? r : 0;
+      const long base = win_to_token(wc * TOK + rr, a.wm) * a.ldx;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) xv[p][k] = *(const float4*)(a.x + base + 4 * jl + 64 * k);
+    }
+  };
+  load_x(win);
+  const bf16* wq = a.wqkv + (long)((0 * NH + h) * KB) * WS + lane * 8;
+  const bf16* wk = a.wqkv + (long)((1 * NH + h) * KB) * WS + lane * 8;
+  const bf16* wv = a.wqkv + (long)((2 * NH + h) * KB) * WS + lane * 8;
+  const bf16* wp = a.wproj + (long)(h * KB) * WS + lane * 8;
+  bf16x8 pq[PF], pk[PF], pv[PF];
+  auto load_w = [&]() {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      pq[i] = *(const bf16x8*)(wq + i * WS);
+      pk[i] = *(const bf16x8*)(wk + i * WS);
+      pv[i] = *(const bf16x8*)(wv + i * WS);
+    }
+  };
+  load_w();
+  if (q == 0)
+    for (int i = lane; i < (2 * WSZ - 1) * (2 * WSZ - 1); i += 64) sTabR[h][224 - i] = a.table[i * NH + h];
+  for (int i = tid; i < 3 * NH * 32; i += 64 * NW) sBias[i] = a.bqkv[i];
+  for (int i = tid; i < CP; i += 64 * NW) {
+    sGB[0][i] = i < a.C ? a.gamma[i] : 0.f;
+    sGB[1][i] = i < a.C ? a.beta[i] : 0.f;
+  }
+  const float bvl = a.bqkv[(2 * NH + h) * 32 + l31];
+  const float bc = a.bproj[c];
+  __syncthreads();
+  const float inv_c = 1.0f / (float)a.C;
+  const int nWw = a.W / WSZ, nW = (a.H / WSZ) * nWw;
+
+  for (; win < a.nWin; win += gridDim.x) {
+    // lane-derived values from an opaque copy of the lane id, per window: hoisted out of the loop they
+    // would hold ~30 VGPRs of addresses and masks for its whole length (12 waves: 168 VGPRs each)
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int l31 = lane & 31, hh = lane >> 5, g = lane >> 4, jl = lane & 15;
+    const int c = 32 * h + l31;
+    const int wi = (int)(win % nW), wy = wi / nWw, wx = wi - wy * nWw;
+    if (tid < TOK) {
+      sRow[tid] = (int)win_to_token(win * TOK + tid, a.wm);
+      sReg[tid] = a.shift > 0 ? shift_region(wy * WSZ + (tid >> 3), a.H, a.shift) * 3 +
+                                    shift_region(wx * WSZ + (tid & 7), a.W, a.shift)
+                              : 0;
+    }
+    const bool mixed = a.shift > 0 && (wy == a.H / WSZ - 1 || wx == nWw - 1);
+
+    // ---- A: LayerNorm (16 lanes per row), rows w + 12 i -------------------------------------------
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int i = 4 * p + g, r = w + NW * i;
+      const bool ok = i < RPW && r < TOK;
+      float sm = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * jl + 64 * k;
+        sm += (cb + 0 < a.C ? xv[p][k].x : 0.f) + (cb + 1 < a.C ? xv[p][k].y : 0.f) +
+              (cb + 2 < a.C ? xv[p][k].z : 0.f) + (cb + 3 < a.C ? xv[p][k].w : 0.f);
+      }
+      const float mu = dpp_sum16(sm) * inv_c;
+      float qq = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int cb = 4 * jl + 64 * k;
+        const float vv[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = cb + j < a.C ? vv[j] - mu : 0.f;
+          qq += d * d;
+        }
+      }
+      const float rs = rsqrtf(dpp_sum16(qq) * inv_c + a.eps);
+      if (ok) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int cb = 4 * jl + 64 * k;
+          const float vv[4] = {xv[p][k].x, xv[p][k].y, xv[p][k].z, xv[p][k].w};
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cc = cb + j;
+            o[j] = (bf16)(cc < a.C ? (vv[j] - mu) * rs * sGB[0][cc] + sGB[1][cc] : (cc == a.C ? 1.f : 0.f));
+          }
+          *(bf16x4*)(sT + r * LDT + cb) = o;
+          *(float4*)(sX + r * LDX + cb) = xv[p][k];
+        }
+        if (jl == 0) {
+          sMean[r] = mu;
+          sRstd[r] = rs;
+        }
+      }
+    }
+    __syncthreads();           // LN tile, sX, sRow, sReg visible
+
+    // ---- B: q^T, k^T, v of head h for token tile q ----------------------------------------------
+    f32x16 QT, KT, V;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) QT[r] = KT[r] = V[r] = 0.f;
+    auto qkv_steps = [&](int kb0, auto refill) {
+#pragma unroll
+      for (int sl = 0; sl < PF; ++sl) {
+        const int kb = kb0 + sl;
+        const bf16x8 fl = *(const bf16x8*)(sT + (q * 32 + l31) * LDT + kb * 16 + 8 * hh);
+        QT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pq[sl], fl, QT, 0, 0, 0);
+        KT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pk[sl], fl, KT, 0, 0, 0);
+        V = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl, pv[sl], V, 0, 0, 0);
+        if constexpr (decltype(refill)::value) {
+          pq[sl] = *(const bf16x8*)(wq + (kb + PF) * WS);
+          pk[sl] = *(const bf16x8*)(wk + (kb + PF) * WS);
+          pv[sl] = *(const bf16x8*)(wv + (kb + PF) * WS);
+        }
+      }
+    };
+#pragma unroll 1
+    for (int kb0 = 0; kb0 < KB - PF; kb0 += PF) qkv_steps(kb0, std::true_type{});
+    qkv_steps(KB - PF, std::false_type{});
+    bf16x8 pw[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) pw[i] = *(const bf16x8*)(wp + i * WS);
+    const float* bq = sBias + (0 * NH + h) * 32;
+    const float* bk = sBias + (1 * NH + h) * 32;
+    // fragments [s]: this wave's token tile (Fk / Fv), the partner's (Fk2 / Fv2) -- named, never indexed
+    // by the run-time tile q (a register array indexed at run time goes to scratch)
+    bf16x8 Fq[2], Fk[2], Fv[2], Fk2[2], Fv2[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = acc_row32(8 * s2 + j, hh);
+        Fq[s2][j] = (bf16)(QT[8 * s2 + j] + bq[d]);
+        Fk[s2][j] = (bf16)(KT[8 * s2 + j] + bk[d]);
+        Fv[s2][j] = (bf16)(V[8 * s2 + j] + bvl);
+      }
+    // k fragments to the partner (O tile, unused until phase C writes it), v rows to the scratch
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) *(bf16x8*)(sK + (((h * 2 + q) * 2 + s2) * 64 + lane) * 8) = Fk[s2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sVh[(q * 32 + acc_row32(8 * s2 + j, hh)) * LDV + l31] = Fv[s2][j];
+    if (!KAIR_DBG(a.dbg & 1)) {   // saved q / k of this tile, head-blocked [part][win][h][tok][32]
+      const long part = M * NH * 32;
+      bf16* qb = a.qkv + (win * NH + h) * TOK * 32;
+      const int tok = q * 32 + l31;
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d0 = 8 * gg + 4 * hh, s2 = gg >> 1, j0 = 4 * (gg & 1);
+        const bf16x4 q4 = {Fq[s2][j0], Fq[s2][j0 + 1], Fq[s2][j0 + 2], Fq[s2][j0 + 3]};
+        const bf16x4 k4 = {Fk[s2][j0], Fk[s2][j0 + 1], Fk[s2][j0 + 2], Fk[s2][j0 + 3]};
+        *(bf16x4*)(qb + tok * 32 + d0) = q4;
+        *(bf16x4*)(qb + part + tok * 32 + d0) = k4;
+      }
+    }
+    __syncthreads();   // k fragments and v rows of both tiles visible
+    if (!KAIR_DBG(a.dbg & 1)) {   // saved v rows of this tile, 16-byte stores
+      bf16* vb = a.qkv + 2 * M * NH * 32 + (win * NH + h) * TOK * 32;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int id = lane + 64 * i, tok = q * 32 + (id >> 2), q8 = (id & 3) * 8;
+        *(uint4*)(vb + tok * 32 + q8) = *(const uint4*)(sVh + tok * LDV + q8);
+      }
+    }
+    // the partner's k (fragment form) and v (from the scratch rows: register j of lane (d = l31, hh) is
+    // token row acc_row32(8 s + j, hh) of the other tile)
+    const int o = 1 - q;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      Fk2[s2] = *(const bf16x8*)(sK + (((h * 2 + o) * 2 + s2) * 64 + lane) * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Fv2[s2][j] = sVh[(o * 32 + acc_row32(8 * s2 + j, hh)) * LDV + l31];
+    }
+
+    // ---- C: attention of head h, queries of tile q ----------------------------------------------
+    // S[0]: keys of this wave's tile q, S[1]: keys of the partner's tile o (key tile kt[i] below)
+    f32x16 S[2];
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[i2][r] = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      S[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fk[s2], Fq[s2], S[0], 0, 0, 0);
+      S[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fk2[s2], Fq[s2], S[1], 0, 0, 0);
+    }
+    const int ktile[2] = {q, o};
+    __syncthreads();   // every wave has its partner's k: the O tile is free
+    float lse_v;
+    {
+      const int qi = q * 32 + l31;
+      const float* tb = &sTabR[h][112 - 15 * (qi >> 3) - (qi & 7) + 4 * hh];
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2) {
+        const float* tbk = tb + 60 * ktile[i2];   // 15 * 4 * kt
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float sc = fmaf(S[i2][r], a.scale, tbk[15 * (r >> 2) + (r & 3)]);
+          S[i2][r] = sc;
+          mx = fmaxf(mx, sc);
+        }
+      }
+      if (mixed) {
+        const int rq = sReg[qi];
+        mx = -3.0e38f;
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if (sReg[ktile[i2] * 32 + acc_row32(r, hh)] != rq) S[i2][r] += -100.f;
+            mx = fmaxf(mx, S[i2][r]);
+          }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __expf(S[i2][r] - mx);
+          S[i2][r] = e;
+          sum += e;
+        }
+      sum += __shfl_xor(sum, 32, 64);
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) S[i2][r] *= inv;
+      lse_v = mx + __logf(sum);
+      f32x16 ov;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ov[r] = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        ov = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fv[s2], pack8r(S[0], s2), ov, 0, 0, 0);
+        ov = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fv2[s2], pack8r(S[1], s2), ov, 0, 0, 0);
+      }
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d0 = 8 * gg + 4 * hh;
+        float r4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r4[j] = (h * 32 + d0 + j == a.o_ones_col) ? 1.f : ov[4 * gg + j];
+        *(bf16x4*)(sO + qi * LDT + h * 32 + d0) = bf16x4{(bf16)r4[0], (bf16)r4[1], (bf16)r4[2], (bf16)r4[3]};
+      }
+    }
+    load_x(win + gridDim.x);   // the next window's rows and first q/k/v weight fragments, in flight
+    load_w();                  // through phase D
+    const float rs = a.rowscale ? a.rowscale[win / a.win_per_scale] : 1.f;
+    __syncthreads();           // the O tile is complete
+
+    // ---- D: proj of token tile q, output channels 32 h .. 32 h + 31 ------------------------------
+    f32x16 P;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) P[r] = 0.f;
+    auto proj_steps = [&](int kb0, auto refill) {
+#pragma unroll
+      for (int sl = 0; sl < PF; ++sl) {
+        const int kb = kb0 + sl;
+        const bf16x8 fo = *(const bf16x8*)(sO + (q * 32 + l31) * LDT + kb * 16 + 8 * hh);
+        P = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fo, pw[sl], P, 0, 0, 0);
+        if constexpr (decltype(refill)::value) pw[sl] = *(const bf16x8*)(wp + (kb + PF) * WS);
+      }
+    };
+#pragma unroll 1
+    for (int kb0 = 0; kb0 < KB - PF; kb0 += PF) proj_steps(kb0, std::true_type{});
+    proj_steps(KB - PF, std::false_type{});
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) asm volatile("" ::"v"(xv[p][k].x), "v"(xv[p][k].y), "v"(xv[p][k].z), "v"(xv[p][k].w));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float* px = sX + (q * 32 + acc_row32(r, hh)) * LDX + c;
+      *px = *px + rs * (P[r] + bc);
+    }
+    __syncthreads();
+    constexpr int C4 = CP / 4;
+    for (int i = tid; i < (KAIR_DBG(a.dbg & 2) ? 0 : TOK * C4); i += 64 * NW) {
+      const int r = i / C4, qq = (i - (i / C4) * C4) * 4;
+      *(float4*)(a.out + (long)sRow[r] * a.ldout + qq) = *(const float4*)(sX + r * LDX + qq);
+    }
+    if (hh == 0 && !KAIR_DBG(a.dbg & 2)) a.lse[(win * NH + h) * TOK + q * 32 + l31] = lse_v;
+    constexpr int CH = CP / 8;
+    for (int i = tid; i < (KAIR_DBG(a.dbg & 2) ? 0 : TOK * CH); i += 64 * NW) {
+      const int r = i / CH, qq = (i - (i / CH) * CH) * 8;
+      *(uint4*)(a.ln + (win * TOK + r) * a.ldln + qq) = *(const uint4*)(sT + r * LDT + qq);
+      *(uint4*)(a.O + (win * TOK + r) * a.ldo + qq) = *(const uint4*)(sO + r * LDT + qq);
+    }
+    if (tid < TOK && !KAIR_DBG(a.dbg & 2)) {
+      const long t = sRow[tid];
+      a.mean[t] = sMean[tid];
+      a.rstd[t] = sRstd[tid];
+    }
+    __syncthreads();   // every LDS tile / row map of this window consumed
   }
 }
 
@@ -1282,6 +1636,8 @@ extern "C" int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, 
   const long grid = nWin < ncu ? nWin : ncu;   // persistent: one workgroup per CU
   if (w_split)
     hipLaunchKernelGGL((swin_attn_fwd_kernel<6, 2>), dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
+  else if (KAIR_ATTN12)   // two waves per head (A/B: -DKAIR_ATTN12=0 builds the 6-wave kernel)
+    hipLaunchKernelGGL((swin_attn_fwd12_kernel<6>), dim3((unsigned)grid), dim3(128 * 6), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL((swin_attn_fwd_kernel<6, 1>), dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
   KAIR_CHECK_LAUNCH();

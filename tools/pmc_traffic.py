@@ -24,20 +24,20 @@ def main(d):
     for k, c in acc.items():
         if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
             continue
-        # the bench's full-batch launches only: the same kernel also runs at the PSNR evaluation's
-        # smaller batch (same persistent grid size), so keep dispatches at >= half the longest duration
+        # the profiled program runs full-batch steps only (tools/prof_step.py): the median over every
+        # dispatch of the kernel (robust to a cold first launch), with the dispatch count
         def avg(v):
-            top = max(t for t, _ in v)
-            sel = [x for t, x in v if t >= 0.5 * top]
-            return sum(sel) / len(sel), len(sel)
+            xs = sorted(x for _, x in v)
+            return xs[len(xs) // 2], len(xs)
         fetch, nf = avg(c["FETCH_SIZE"])
         write, nw = avg(c["WRITE_SIZE"])
         fetch *= 2.0 * 1024
         write *= 1024.0
         out[k[:160]] = {"fetch_bytes_corrected": round(fetch), "write_bytes": round(write),
                         "hbm_bytes_per_launch": round(fetch + write), "dispatches": [nf, nw]}
-    json.dump({"source": d, "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes; full-batch dispatches "
-               "(>= half the kernel's longest duration) averaged", "kernels": out}, sys.stdout, indent=1)
+    json.dump({"source": d, "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes; median over all dispatches of "
+               "the kernel (the profiled program runs full-batch training steps only)", "kernels": out},
+              sys.stdout, indent=1)
 
 
 if __name__ == "__main__":
