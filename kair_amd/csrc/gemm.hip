@@ -1574,7 +1574,8 @@ int ring_bn(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStr
 constexpr int HC_BM = 96, HC_BN = 192, HC_BK = 64;
 constexpr int HC_HALO_ELEMS = 40960;   // bf16 elements: (RPT + 2) x (XW + 2) x (Cin + 8)
 constexpr int HC_PER = HC_HALO_ELEMS / 8 / 512;
-constexpr int HC_EM_ROWS = 0, HC_EM_PSHUF = 1;   // epilogue: token rows / PixelShuffle sub-pixel-major (PSHUF_SPM)
+constexpr int HC_EM_ROWS = 0, HC_EM_PSHUF = 1, HC_EM_PUNSHUF = 2;   // epilogue: token rows / PixelShuffle
+                                                                  // sub-pixel-major (PSHUF_SPM) / its inverse
 
 // BN: output channels per tile (192, or 128 for N in (192, 256]: N tiles of one M tile run on
 // consecutive workgroups, each with its own weight rows; the persistent grid is a multiple of the
@@ -1584,7 +1585,10 @@ constexpr int HC_EM_ROWS = 0, HC_EM_PSHUF = 1;   // epilogue: token rows / Pixel
 // BM: output pixels per tile, 96 or (128-wide N tiles of images with <= 128 channels) 192 -- twice the
 // pixels per streamed weight chunk, so half the weight traffic from L2 (the upsampling convs' bound).
 template <int BM> struct HaloSize { static constexpr int ELEMS = BM == 96 ? HC_HALO_ELEMS : 57344; };
-template <typename TA, int EX, int NPASS, int BN, int EM, int BM>
+// CGM > 1: an image of C = 64 CGM channels (C > 192: the upsampling convs' input gradients, C = 256) in
+// CGM passes over the tile, pass p holding channels [64 p, 64 p + 64) in the halo and running the nine
+// weight chunks of that channel group, accumulating.
+template <typename TA, int EX, int NPASS, int BN, int EM, int BM, int CGM>
 __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E, int K, int tilesM) {
   constexpr int WM = 2, WN = 4, TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
   constexpr int NI = BN / 64;   // LDS-DMA wave-instructions per weight chunk (8 rows x 128 B each)
@@ -1595,13 +1599,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fq = lane >> 4;
   const int H = A.imH, W = A.imW, C = A.imC;
-  const int XW = W < BM ? W : BM, RPT = BM / XW, HWD = XW + 2, HR = RPT + 2, PS = C + 8;
+  constexpr bool CG = CGM > 1;
+  const int XW = W < BM ? W : BM, RPT = BM / XW, HWD = XW + 2, HR = RPT + 2, PS = (CG ? HC_BK : C) + 8;
   const int sh = B.wsplit;   // hi/lo split weights: weight chunk j pairs with halo chunk j >> 1
   // NPASS 2 -- hi/lo split activations (fp32 A, kair_operand.a_split): a second pass over the tile with
   // the halo refilled by the lo halves bf16(x - bf16(x)) and only the hi weight chunks (the a_lo . w_hi
   // product), accumulating into the same tile
-  constexpr int npass = NPASS;
-  const int cpt = C / HC_BK, nks = (9 * cpt) << sh, c8n = C / 8;
+  constexpr int npass = CG ? CGM : NPASS;
+  const int cpt = C / HC_BK, nks = (9 * cpt) << sh, c8n = (CG ? HC_BK : C) / 8;
   const bool pair = sizeof(TA) == 2 && A.asplit == 2 && sh && cpt == 2;   // skip lo . lo (chunk 4t + 3)
   const int halo_pieces = HR * HWD * c8n;
   const TA* Ap = (const TA*)A.ptr;
@@ -1648,7 +1653,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
     const int tap = j / cpt, cc = j - tap * cpt;
     int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
     if (A.flip) { dy = -dy; dx = -dx; }
-    const int hoff = (dy * HWD + dx) * PS + cc * HC_BK;
+    const int hoff = (dy * HWD + dx) * PS + (CG ? 0 : cc * HC_BK);   // CG: the halo holds one channel group
 #pragma unroll
     for (int ks = 0; ks < HC_BK / 32; ++ks) {
       bf16x8 af[RM], bfr[RN];
@@ -1709,7 +1714,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
           const int hr = pix / HWD, hc = pix - (pix / HWD) * HWD;
           const int y = y0 - 1 + hr, x = x0 - 1 + hc;
           okv[i] = idx < halo_pieces && y >= 0 && y < H && x >= 0 && x < W;
-          const long src = okv[i] ? ((long)(b * H + y) * W + x) * A.ld + c8 * 8 : 0;
+          const long src = okv[i] ? ((long)(b * H + y) * W + x) * A.ld + (CG ? HC_BK * pass : 0) + c8 * 8 : 0;
           lo[i] = *(const uint4*)(Ap + src);
           if constexpr (sizeof(TA) == 4) hi[i] = *(const uint4*)(Ap + src + 4);
         }
@@ -1727,7 +1732,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
             const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
             bf16x8 qq;
 #pragma unroll
-            for (int e8 = 0; e8 < 8; ++e8) qq[e8] = pass ? (bf16)(f[e8] - (float)(bf16)f[e8]) : (bf16)f[e8];
+            for (int e8 = 0; e8 < 8; ++e8) qq[e8] = (NPASS == 2 && pass) ? (bf16)(f[e8] - (float)(bf16)f[e8]) : (bf16)f[e8];
             q = __builtin_bit_cast(uint4, qq);
           } else {
             q = lo[i];
@@ -1757,8 +1762,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
     __syncthreads();   // halo visible
     // pass 1 (lo halo): the hi weight chunks only, chunk j of the pass = weight chunk j << sh;
     // a [hi | lo] pair image: per tap the weight chunks 4t, 4t+1, 4t+2 (hi.w_hi, hi.w_lo, lo.w_hi)
-    const int nkp = pass ? nks >> sh : (pair ? nks / 4 * 3 : nks), wsh = pass ? sh : 0;
-    auto wchunk = [&](int j) { return pass ? j << wsh : (pair ? (j / 3) * 4 + j % 3 : j); };
+    // CG pass p: the nine taps of channel group p, weight chunk tap * cpt + p
+    const int nkp = CG ? 9 : (pass ? nks >> sh : (pair ? nks / 4 * 3 : nks)), wsh = (!CG && pass) ? sh : 0;
+    auto wchunk = [&](int j) { return CG ? j * cpt + pass : (pass ? j << wsh : (pair ? (j / 3) * 4 + j % 3 : j)); };
     bissue(0, 0);
     if (1 < nkp) bissue(1, wchunk(1));
     for (int j = 0; j < nkp; ++j) {
@@ -1780,7 +1786,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
     }   // pass
     // epilogue: bias (+ act) (+ fp32 residual), 4 consecutive channels per lane
     if constexpr (EX == EX_RESID) {
-      if ((nks >> (npass - 1 ? sh : 0)) < 2) load_resid();
+      if (!CG && (nks >> (npass - 1 ? sh : 0)) < 2) load_resid();
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -1808,6 +1814,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
           for (int q4 = 0; q4 < 4; ++q4)
             if (n + q4 == E.ones_col) v[q4] = 1.f;
         }
+        if (E.gate && n < N) {   // act'(gate) of the same row (ROWS): the input gradient's activation gate
+          float gv[4];
+          ld4_any(E.gate, E.gdt, m * E.ldg + n, gv);
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            if (E.gkind == 2) v[q4] *= (gv[q4] > 0.f ? 1.f : E.slope);
+            else if (E.gkind == 4) v[q4] *= gv[q4];
+            else v[q4] *= (gv[q4] > 0.f ? 1.f : 0.f);
+          }
+        }
         if (n < N) {
           long o = m * E.ldo + n;
           if constexpr (EM == HC_EM_PSHUF) {   // sub-pixel-major columns: n = (i r + j) nf + c -> pixel (y r + i, x r + j)
@@ -1815,6 +1831,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
             const int bi = (int)(m / ((long)H * W)), pp = (int)(m - (long)bi * H * W), yy = pp / W, xx = pp - yy * W;
             const int sp = n / nf, cc = n - sp * nf, ii = sp / r, jj = sp - ii * r;
             o = (((long)bi * H * r + (long)yy * r + ii) * ((long)W * r) + (long)xx * r + jj) * E.ldo + cc;
+          } else if constexpr (EM == HC_EM_PUNSHUF) {   // pixel (y, x) of the r-times grid -> pre-shuffle row
+            const int r = E.r;                          // (y / r, x / r), column (i r + j) N + n
+            const int bi = (int)(m / ((long)H * W)), pp = (int)(m - (long)bi * H * W), yy = pp / W, xx = pp - yy * W;
+            const int yl = yy / r, xl = xx / r;
+            o = (((long)bi * (H / r) + yl) * (W / r) + xl) * E.ldo + ((yy - yl * r) * r + (xx - xl * r)) * N + n;
           }
           st4_any(E.out, E.odt, o, v);
           if (E.out_lo) {
@@ -1831,7 +1852,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
 template <typename TA>
 static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, int K) {
   const int H = A.imH, W = A.imW, C = A.imC;
-  if (A.up_sh != 0 || C % HC_BK != 0 || C > 192 || K != 9 * C || N > 256 || N % 4 != 0) return false;
+  if (A.up_sh != 0 || C % HC_BK != 0 || C > 256 || K != 9 * C || N > 256 || N % 4 != 0) return false;
+  // C in (192, 256]: channel-group passes, plain bf16 operands, 64 outputs
+  if (C > 192 && (sizeof(TA) != 2 || A.asplit || B.wsplit || N > 64 || e.resid || e.acopy)) return false;
   // the two-pass split forms lo from an fp32 image; a bf16 image carries it as its [hi | lo] halves (a_split 2)
   if (A.asplit && !(sizeof(TA) == 4 ? A.asplit == 1 : (A.asplit == 2 && C == 128 && B.wsplit))) return false;
   if (W <= 0 || H <= 0) return false;
@@ -1845,9 +1868,14 @@ static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, 
   if (M % HC_BM != 0 || M % ((long)H * W) != 0) return false;
   if (A.ld % 8 != 0 || ((unsigned long)A.ptr & 15) || B.ld % 8 != 0 || ((unsigned long)B.ptr & 15)) return false;
   if (e.omode != KAIR_OUT_ROWS && !(e.omode == KAIR_OUT_PSHUF_SPM && e.psH == H && e.psW == W && e.r > 0 &&
-                                    N % (e.r * e.r) == 0 && (N / (e.r * e.r)) % 4 == 0 && !e.resid && !e.acopy))
+                                    N % (e.r * e.r) == 0 && (N / (e.r * e.r)) % 4 == 0 && !e.resid && !e.acopy) &&
+      !(e.omode == KAIR_OUT_PUNSHUF_SPM && C > 192 && e.r > 0 && e.psH * e.r == H && e.psW * e.r == W && N % 4 == 0 &&
+        e.ldo >= (long)N * e.r * e.r && !e.resid && !e.acopy))
     return false;
-  if (e.win.ws != 0 || e.gate || e.pre || e.resid2 || e.rowscale) return false;
+  // a gate only on ROWS outputs with 4-aligned rows (bf16 8-byte / fp32 16-byte loads), no residual
+  if (e.gate && (e.omode != KAIR_OUT_ROWS || e.resid || e.ldg % 4 != 0 || e.gkind == 1 || ((unsigned long)e.gate & 15)))
+    return false;
+  if (e.win.ws != 0 || e.pre || e.resid2 || e.rowscale) return false;
   if (e.ldo % 4 != 0 || ((unsigned long)e.out & 15) || (e.resid && (e.ldr % 4 != 0 || ((unsigned long)e.resid & 15))))
     return false;
   if (e.acopy && (e.ldac % 8 != 0 || e.ldac < C || ((unsigned long)e.acopy & 15))) return false;
@@ -1890,7 +1918,20 @@ static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int 
   long tiles = (long)tilesM * tilesN;
   int grid = (int)(tiles < g_num_cus ? tiles : (g_num_cus / tilesN) * tilesN);   // a multiple of tilesN
 #define KAIR_HALO(NP, EXV, BNV, EMV, BMV) \
-  hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EXV, NP, BNV, EMV, BMV>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM)
+  hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EXV, NP, BNV, EMV, BMV, 1>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM)
+  if constexpr (sizeof(TA) == 2) {
+    if (A.imC > 192) {   // conv_halo_ok: 64 outputs, plain operands, C = 256 in four channel-group passes
+      if (A.imC != 256) return kair_set_error(KAIR_ERR_ARG, "halo conv: C in (192, 256) has no channel-group form");
+      if (E.omode == KAIR_OUT_PUNSHUF_SPM)
+        hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE, 1, 64, HC_EM_PUNSHUF, 96, 4>), dim3(grid), dim3(512), 0, s, A, B,
+                           E, K, tilesM);
+      else
+        hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE, 1, 64, HC_EM_ROWS, 96, 4>), dim3(grid), dim3(512), 0, s, A, B, E,
+                           K, tilesM);
+      KAIR_CHECK_LAUNCH();
+      return 0;
+    }
+  }
 #define KAIR_HALO_NP(NP)                                                                           \
   if (E.resid) KAIR_HALO(NP, EX_RESID, 192, HC_EM_ROWS, 96);                                       \
   else if (E.omode == KAIR_OUT_PSHUF_SPM && big) KAIR_HALO(NP, EX_NONE, 128, HC_EM_PSHUF, 192);     \

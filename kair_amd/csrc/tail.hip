@@ -18,8 +18,9 @@
 //                              -> 2 k-steps), the dE rows staged as 4 channels per pixel; rows or
 //                              PixelUnshuffle sub-pixel-major store (the previous upsampling conv's
 //                              pre-shuffle gradient);
-//   kair_conv3x3_narrow_wgrad  dW = sum_p dE[p] x X[p + tap]: VALU, one wave per tap, lane = (8 channels,
-//                              pixel phase); per-workgroup partials summed in fixed order (deterministic).
+//   kair_conv3x3_narrow_wgrad  dW = sum_p dE[p] x X[p + tap]: MFMA over the pixels (32 per k-step), both
+//                              operands read with transposing LDS reads (ds_read_b64_tr_b16), the dE rows
+//                              staged with a halo; per-workgroup partials summed in fixed order.
 #include <stdlib.h>
 
 #include "common.h"
@@ -284,147 +285,134 @@ struct NarrowWgradArgs {
   float* part;                          // [gridDim.x][NR * 64 * 9 + NR]
 };
 
-constexpr int WPST = 68;                // staged X, fp32: 64 channels + 4 per pixel (272 B)
-constexpr int WROW = PXS * WPST;
-constexpr int WCH = PXS * 8;            // 16-byte bf16 chunks per X row (8 channels each)
-constexpr int WPER = (WCH + 575) / 576;
+constexpr int XS = NF + 8;               // staged X row: [64 px][64 + 8] bf16
+constexpr int EPX = PXS * 4;             // staged dE row: [66 px][4] bf16
 
-// 9 waves (wave = tap); lane: channel group cg = lane & 7 (8 channels), pixel phase ph = lane >> 3.
-// X rows and the dE row are staged as fp32 (converted once per element, read by all nine taps), the
-// products run as packed fp32 FMAs (v_pk_fma_f32: two channels per instruction).
-__global__ __launch_bounds__(576) void conv3x3_narrow_wgrad_kernel(const NarrowWgradArgs a) {
-  __shared__ __attribute__((aligned(16))) float sX[4 * WROW];
-  __shared__ __attribute__((aligned(16))) float sE[2 * SEG * 4];   // dE rows y, y+1 (4 channels per pixel)
+// MFMA over the pixels: D[c][(tap, n)] = sum_p X[p][c] dE[p - (dy, dx)][n] (p a pixel of X row Y, the
+// dE rows Y - dy staged with a halo), v_mfma_f32_16x16x32_bf16 with 32 pixels per k-step.  Both operands
+// are pixel-major in LDS and read with ds_read_b64_tr_b16 (8 consecutive pixels per lane): A = X^T
+// (16 channels per wave), B = 4 taps x 4 channels of dE per 16 columns, each lane's 4-column group
+// addressing its own tap's shifted row -- 3 tap groups (taps 0-3, 4-7, 8).  Wave w owns channels
+// 16 w .. 16 w + 15; per X row a wave issues 6 MFMAs, so the kernel runs at the rate its rows stream in.
+__global__ __launch_bounds__(256) void conv3x3_narrow_wgrad_kernel(const NarrowWgradArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sXr[2][SEG * XS];
+  __shared__ __attribute__((aligned(16))) bf16 sEr[4][EPX + 8];   // + a zero tail for tap >= 9 lanes
   const int tid = threadIdx.x, lane = tid & 63;
-  const int tap = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cg = lane & 7, ph = lane >> 3;
-  const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-  f32x2 acc[4][4];
-  float bacc[4];
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, g8 = (lane >> 4) * 8;
+  const int tl = p4 >> 2;   // this lane's tap within a group (its 4-column block)
+  f32x4 acc[3];
 #pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    bacc[n] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[n][i] = f32x2{0.f, 0.f};
-  }
+  for (int tg = 0; tg < 3; ++tg) acc[tg] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[4] = {0.f, 0.f, 0.f, 0.f};
   const int nseg = a.W / SEG;
   const long total = (long)a.B * nseg * a.H;
   const RowRun run = row_run(total, gridDim.x, blockIdx.x);
-  uint4 pre[WPER];
+  uint4 px_[2];
   uint2 pe = make_uint2(0, 0);
-  auto load_row = [&](long st, int yy) {
+  auto load_x = [&](long st, int yy) {   // X row yy (inside the image): 64 px x 8 chunks of 16 B
     const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
 #pragma unroll
-    for (int i = 0; i < WPER; ++i) {
-      const int c = tid + 576 * i;
-      const int px = c >> 3, part = c & 7, xx = x0 - 1 + px;
-      const bool ok = c < WCH && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
-      pre[i] = *(const uint4*)(a.x + (ok ? ((long)(b * a.H + yy) * a.W + xx) * a.ldx + part * 8 : 0));
-      if (!ok) pre[i] = make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      const int cidx = tid + 256 * i, p = cidx >> 3, part = cidx & 7;
+      px_[i] = *(const uint4*)(a.x + ((long)(b * a.H + yy) * a.W + x0 + p) * a.ldx + part * 8);
     }
   };
-  auto store_row = [&](int yy) {
-    float* dst = sX + (yy & 3) * WROW;
+  auto store_x = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < WPER; ++i) {
-      const int c = tid + 576 * i;
-      if (c < WCH) {
-        const bf16x8 v = __builtin_bit_cast(bf16x8, pre[i]);
-        float* d = dst + (c >> 3) * WPST + (c & 7) * 8;
-        *(float4*)d = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
-        *(float4*)(d + 4) = make_float4((float)v[4], (float)v[5], (float)v[6], (float)v[7]);
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int cidx = tid + 256 * i;
+      *(uint4*)(&sXr[buf][(cidx >> 3) * XS + (cidx & 7) * 8]) = px_[i];
     }
   };
-  auto load_e = [&](long st, int yy) {   // dE row yy (inside the image), pixels x0 .. x0 + 63
+  auto load_e = [&](long st, int yy) {   // dE row yy with a one-pixel halo (zeros outside the image)
     const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
-    if (tid < SEG) pe = *(const uint2*)(a.dE + ((long)(b * a.H + yy) * a.W + x0 + tid) * a.lde);
+    const int xx = x0 - 1 + tid;
+    const bool ok = tid < PXS && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+    pe = *(const uint2*)(a.dE + (ok ? ((long)(b * a.H + yy) * a.W + xx) * a.lde : 0));
+    if (!ok) pe = make_uint2(0, 0);
   };
   auto store_e = [&](int yy) {
-    if (tid < SEG) {
-      const bf16x4 e = __builtin_bit_cast(bf16x4, pe);
-      *(float4*)(sE + (yy & 1) * SEG * 4 + tid * 4) = make_float4((float)e[0], (float)e[1], (float)e[2], (float)e[3]);
-    }
+    if (tid < PXS) *(uint2*)(&sEr[yy & 3][tid * 4]) = pe;
+    if (tid >= PXS && tid < PXS + 2) *(uint2*)(&sEr[yy & 3][EPX + (tid - PXS) * 4]) = make_uint2(0, 0);
   };
   long cur_strip = -1;
+  int xb = 0;
   for (long g = run.g0; g < run.g1; ++g) {
     const long st = g / a.H;
     const int y = (int)(g - st * a.H);
-    if (st != cur_strip) {   // (re)start: X rows y-1 .. y+1, dE row y
+    if (st != cur_strip) {   // (re)start: dE rows y-1 .. y+1, X row y
       __syncthreads();
       for (int d = -1; d <= 1; ++d) {
-        load_row(st, y + d);
-        store_row(y + d + 4);
+        load_e(st, y + d);
+        store_e(y + d + 4);
       }
-      load_e(st, y);
-      store_e(y);
+      load_x(st, y);
+      store_x(xb);
       cur_strip = st;
       __syncthreads();
     }
-    // the next rows' operands (X row y+2, dE row y+1) in flight during this row's products
     const bool more = g + 1 < run.g1 && (g + 1) / a.H == st;
-    if (more) {
-      load_row(st, y + 2);
-      load_e(st, y + 1);
+    if (more) {   // the next row's operands in flight during this row's MFMAs
+      load_x(st, y + 1);
+      load_e(st, y + 2);
     }
-    const float* xr = sX + ((y + dy + 4) & 3) * WROW + 8 * cg;
-    const float* er = sE + (y & 1) * SEG * 4;
-#pragma unroll 2
-    for (int i = 0; i < SEG / 8; ++i) {
-      const int px = ph + 8 * i;
-      const float4 e = *(const float4*)(er + px * 4);
-      const float4 v0 = *(const float4*)(xr + (1 + px + dx) * WPST);
-      const float4 v1 = *(const float4*)(xr + (1 + px + dx) * WPST + 4);
-      const f32x2 v[4] = {f32x2{v0.x, v0.y}, f32x2{v0.z, v0.w}, f32x2{v1.x, v1.y}, f32x2{v1.z, v1.w}};
-      const float en[4] = {e.x, e.y, e.z, e.w};
+    const bf16* xr = sXr[xb];
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r0 = 32 * ks + g8 + q;   // rows (pixels) r0 and r0 + 4 of this lane's transposed reads
+      bf16x8 af;
+      {
+        const bf16* base = xr + r0 * XS + 16 * wave + p4;
+        const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base);
+        const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base + 4 * XS));
+        short __attribute__((ext_vector_type(8))) s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af = __builtin_bit_cast(bf16x8, s8);
+      }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc[n][k] = __builtin_elementwise_fma(f32x2{en[n], en[n]}, v[k], acc[n][k]);
-      if (tap == 4 && cg == 0) {
-#pragma unroll
-        for (int n = 0; n < 4; ++n) bacc[n] += en[n];
+      for (int tg = 0; tg < 3; ++tg) {
+        const int tap = 4 * tg + tl;
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        // dE[p - (dy, dx)]: staged row y - dy, pixel index 1 + p - dx; taps >= 9 read the zero tail
+        const bf16* base = tap < 9 ? &sEr[(y - dy + 4) & 3][(1 + r0 - dx) * 4] : &sEr[0][EPX];
+        const int step = tap < 9 ? 16 : 0;   // rows r0 + 4: 4 pixels on (the zero tail stays put)
+        const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base);
+        const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base + step));
+        short __attribute__((ext_vector_type(8))) s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[tg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, s8), acc[tg], 0, 0, 0);
       }
     }
-    __syncthreads();   // every wave is done with row y - 1's X slot and dE row y - 1's buffer
+    if (tid < SEG) {   // bias: every pixel of dE row y once
+      const bf16x4 e = *(const bf16x4*)(&sEr[y & 3][(1 + tid) * 4]);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bacc[n] += (float)e[n];
+    }
+    __syncthreads();   // this row's X buffer and dE row y - 1's slot are free
     if (more) {
-      store_row(y + 2);
-      store_e(y + 1);
+      xb ^= 1;
+      store_x(xb);
+      store_e(y + 2);
     }
     __syncthreads();
   }
-  // reduce over the 8 pixel phases (lane bits 3..5), fixed order
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float v = acc[n][i][h];
-        v += __shfl_xor(v, 8, 64);
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        acc[n][i][h] = v;
-      }
-    float bv = bacc[n];
-    bv += __shfl_xor(bv, 8, 64);
-    bv += __shfl_xor(bv, 16, 64);
-    bv += __shfl_xor(bv, 32, 64);
-    bacc[n] = bv;
-  }
+  // D[c][(tap, n)]: lane holds c = 16 w + 4 (l / 16) + i, tap = 4 tg + (l % 16) / 4, n = l % 4
   const int stride = a.NR * NF * 9 + a.NR;
   float* dst = a.part + (long)blockIdx.x * stride;
-  if (ph == 0) {
+  const int n = lane & 3;
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-      if (n < a.NR)
+  for (int tg = 0; tg < 3; ++tg) {
+    const int tap = 4 * tg + tl;
+    if (tap < 9 && n < a.NR)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dst[(n * NF + 8 * cg + i) * 9 + tap] = acc[n][i >> 1][i & 1];   // reference [NR][64][3][3]
+      for (int i = 0; i < 4; ++i) dst[(n * NF + 16 * wave + 4 * (lane >> 4) + i) * 9 + tap] = acc[tg][i];
   }
-  if (tap == 4 && lane == 0) {
+  if (wave == 0) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-      if (n < a.NR) dst[a.NR * NF * 9 + n] = bacc[n];
+    for (int k = 0; k < 4; ++k) bacc[k] = wave_sum(bacc[k]);
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < a.NR) dst[a.NR * NF * 9 + k] = bacc[k];
   }
 }
 
@@ -435,6 +423,7 @@ __global__ void narrow_wgrad_finalize_kernel(const float* __restrict__ part, int
   const int nw = NR * NF * 9, stride = nw + NR;
   if (e >= stride) return;
   float s = 0.f;
+#pragma unroll 8
   for (int k = 0; k < nblk; ++k) s += part[(long)k * stride + e];
   if (e < nw) gw[e] = accumulate ? gw[e] + s : s;
   else if (gb) gb[e - nw] = accumulate ? gb[e - nw] + s : s;
@@ -491,7 +480,7 @@ extern "C" int kair_conv3x3_narrow_dgrad(const void* dE, long lde, const float* 
 }
 
 extern "C" long kair_conv3x3_narrow_wgrad_ws(int NR) {
-  return 2L * num_cus() * (NR * NF * 9 + NR);
+  return 4L * num_cus() * (NR * NF * 9 + NR);
 }
 
 extern "C" int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x, long ldx, int NR, float* ws, float* grad_w,
@@ -505,9 +494,9 @@ extern "C" int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x
   a.dE = (const bf16*)dE; a.lde = lde; a.x = (const bf16*)x; a.ldx = ldx; a.NR = NR;
   a.B = B; a.H = H; a.W = W;
   a.part = ws;
-  const int grid = grid_rows((long)B * (W / SEG) * H, 2);
+  const int grid = grid_rows((long)B * (W / SEG) * H, 4);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(conv3x3_narrow_wgrad_kernel, dim3(grid), dim3(576), 0, s, a);
+  hipLaunchKernelGGL(conv3x3_narrow_wgrad_kernel, dim3(grid), dim3(256), 0, s, a);
   KAIR_CHECK_LAUNCH();
   const int stride = NR * NF * 9 + NR;
   hipLaunchKernelGGL(narrow_wgrad_finalize_kernel, dim3((stride + 255) / 256), dim3(256), 0, s, ws, grid, NR, grad_w,

@@ -104,3 +104,38 @@ def test_narrow_wgrad():
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     assert rel_err(outs[0][0], w.grad) < 1e-5
     assert rel_err(outs[0][1], b.grad) < 1e-5
+
+
+@pytest.mark.parametrize("mode", ["punshuf", "gate"])
+def test_halo_channel_groups(mode):
+    """The upsampling convs' input gradients (network_swinir.py:584 Upsample, its backward): a 256-channel
+    image (the pre-shuffle gradient) through the 3x3 halo kernel in four 64-channel passes, into the
+    PixelUnshuffle(2) sub-pixel-major layout of the previous conv ("punshuf") or, gated by LeakyReLU'
+    of a stored activation, into plain rows ("gate") -- vs float64 conv_transpose (flipped taps)."""
+    B, Hh, Ww, C, N = 2, 24, 48, 256, 64
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(B, C, Hh, Ww, generator=g).bfloat16().float()
+    w = (torch.randn(C, N, 3, 3, generator=g) * 0.03).bfloat16().float()   # forward conv N -> C
+    # dgrad of a forward conv N -> C: dX = conv_transpose(x, w)
+    ref = F.conv_transpose2d(x.double(), w.double(), padding=1)   # [B, N, H, W]
+    M = B * Hh * Ww
+    xin = x.permute(0, 2, 3, 1).contiguous().view(M, C).to(dev, torch.bfloat16)
+    Wd = torch.empty(N, 9 * C, device=dev, dtype=torch.bfloat16)
+    H.pack_weight(w.to(dev), Wd, H.wmap(2, C, N, (1, C, C), (1, N, N)))
+    A = H.im2col(xin, Hh, Ww, C, flip=True)
+    if mode == "punshuf":
+        r = 2
+        out = torch.full((M // (r * r), r * r * N), float("nan"), device=dev)
+        H.gemm_nt(A, H.rows(Wd), H.epilogue(out, mode=H.OUT_PUNSHUF_SPM, ldo=r * r * N, ps=(r, Hh // r, Ww // r)), M, N,
+                  9 * C, H.BF16)
+        torch.cuda.synchronize()
+        got = out.cpu().view(B, Hh // r, Ww // r, r, r, N).permute(0, 5, 1, 3, 2, 4).reshape(B, N, Hh, Ww)
+    else:
+        gate = torch.randn(M, 128, generator=g).bfloat16()
+        out = torch.full((M, N), float("nan"), device=dev)
+        H.gemm_nt(A, H.rows(Wd), H.epilogue(out, gate=gate.to(dev), ldg=128, gate_kind=2, slope=0.01), M, N, 9 * C, H.BF16)
+        torch.cuda.synchronize()
+        got = out.cpu().view(B, Hh, Ww, N).permute(0, 3, 1, 2)
+        gs = torch.where(gate[:, :N].float() > 0, 1.0, 0.01).view(B, Hh, Ww, N).permute(0, 3, 1, 2)
+        ref = ref * gs.double()
+    assert rel_err(got, ref) < 1e-5
