@@ -1854,7 +1854,7 @@ static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, 
   const int H = A.imH, W = A.imW, C = A.imC;
   if (A.up_sh != 0 || C % HC_BK != 0 || C > 256 || K != 9 * C || N > 256 || N % 4 != 0) return false;
   // C in (192, 256]: channel-group passes, plain bf16 operands, 64 outputs
-  if (C > 192 && (sizeof(TA) != 2 || A.asplit || B.wsplit || N > 64 || e.resid || e.acopy)) return false;
+  if (C > 192 && (C != 256 || sizeof(TA) != 2 || A.asplit || B.wsplit || N > 64 || e.resid || e.acopy)) return false;
   // the two-pass split forms lo from an fp32 image; a bf16 image carries it as its [hi | lo] halves (a_split 2)
   if (A.asplit && !(sizeof(TA) == 4 ? A.asplit == 1 : (A.asplit == 2 && C == 128 && B.wsplit))) return false;
   if (W <= 0 || H <= 0) return false;
@@ -1864,7 +1864,7 @@ static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, 
     return false;
   }
   const int XW = W < HC_BM ? W : HC_BM, RPT = HC_BM / XW;
-  if ((long)(RPT + 2) * (XW + 2) * (C + 8) > HC_HALO_ELEMS) return false;
+  if ((long)(RPT + 2) * (XW + 2) * ((C > 192 ? HC_BK : C) + 8) > HC_HALO_ELEMS) return false;   // the halo of one pass
   if (M % HC_BM != 0 || M % ((long)H * W) != 0) return false;
   if (A.ld % 8 != 0 || ((unsigned long)A.ptr & 15) || B.ld % 8 != 0 || ((unsigned long)B.ptr & 15)) return false;
   if (e.omode != KAIR_OUT_ROWS && !(e.omode == KAIR_OUT_PSHUF_SPM && e.psH == H && e.psW == W && e.r > 0 &&
