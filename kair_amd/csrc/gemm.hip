@@ -1741,7 +1741,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
           if (idx < halo_pieces) {
             const int pix = idx / c8n, c8 = idx - (idx / c8n) * c8n;
             *(uint4*)(sHalo + pix * PS + c8 * 8) = q;
-            if (E.acopy && pass == 0) {   // the tile's own pixels (halo interior): bf16 copy for the weight gradient
+            if (E.acopy && pass == 0 && tn == 0) {   // the tile's own pixels (halo interior): bf16 copy for the weight gradient
               const int hr = pix / HWD, hc = pix - (pix / HWD) * HWD;
               if (hr >= 1 && hr <= RPT && hc >= 1 && hc <= XW) {
                 uint4 qc = q;
@@ -1914,7 +1914,10 @@ static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int 
   const bool wide = E.N > HC_BN;   // N in (192, 256]: two 128-wide N tiles
   const bool big = wide && !E.resid && A.asplit != 1 && halo_bm192_ok(A, M);   // (the two-pass form would spill)
   const int tilesM = (int)(M / (big ? 192 : HC_BM));
-  const int tilesN = wide ? (E.N + 127) / 128 : 1;
+  // few M tiles (small batches: 96 tiles at 4 patches per GPU): 64-wide N tiles put 3x the workgroups
+  // on the chip, each a third of the weight chunks
+  const bool slim = !wide && E.omode == KAIR_OUT_ROWS && E.N > 64 && 2L * tilesM <= g_num_cus;
+  const int tilesN = wide ? (E.N + 127) / 128 : (slim ? (E.N + 63) / 64 : 1);
   long tiles = (long)tilesM * tilesN;
   int grid = (int)(tiles < g_num_cus ? tiles : (g_num_cus / tilesN) * tilesN);   // a multiple of tilesN
 #define KAIR_HALO(NP, EXV, BNV, EMV, BMV) \
@@ -1933,13 +1936,14 @@ static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int 
     }
   }
 #define KAIR_HALO_NP(NP)                                                                           \
-  if (E.resid) KAIR_HALO(NP, EX_RESID, 192, HC_EM_ROWS, 96);                                       \
+  if (E.resid && slim) KAIR_HALO(NP, EX_RESID, 64, HC_EM_ROWS, 96);                                \
+  else if (E.resid) KAIR_HALO(NP, EX_RESID, 192, HC_EM_ROWS, 96);                                  \
   else if (E.omode == KAIR_OUT_PSHUF_SPM && big) KAIR_HALO(NP, EX_NONE, 128, HC_EM_PSHUF, 192);     \
   else if (E.omode == KAIR_OUT_PSHUF_SPM && wide) KAIR_HALO(NP, EX_NONE, 128, HC_EM_PSHUF, 96);     \
   else if (E.omode == KAIR_OUT_PSHUF_SPM) KAIR_HALO(NP, EX_NONE, 192, HC_EM_PSHUF, 96);             \
   else if (big) KAIR_HALO(NP, EX_NONE, 128, HC_EM_ROWS, 192);                                       \
   else if (wide) KAIR_HALO(NP, EX_NONE, 128, HC_EM_ROWS, 96);                                       \
-  else if (E.N <= 64) KAIR_HALO(NP, EX_NONE, 64, HC_EM_ROWS, 96);                                   \
+  else if (E.N <= 64 || slim) KAIR_HALO(NP, EX_NONE, 64, HC_EM_ROWS, 96);                           \
   else KAIR_HALO(NP, EX_NONE, 192, HC_EM_ROWS, 96);
   if constexpr (sizeof(TA) == 4) {
     if (A.asplit) {   // conv_halo_ok: the two-pass split takes an fp32 A only
