@@ -1765,7 +1765,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
     // CG pass p: the nine taps of channel group p, weight chunk tap * cpt + p
     const int nkp = CG ? 9 : (pass ? nks >> sh : (pair ? nks / 4 * 3 : nks)), wsh = (!CG && pass) ? sh : 0;
     auto wchunk = [&](int j) { return CG ? j * cpt + pass : (pass ? j << wsh : (pair ? (j / 3) * 4 + j % 3 : j)); };
-    bissue(0, 0);
+    bissue(0, wchunk(0));   // (a channel-group pass starts at weight chunk `pass`)
     if (1 < nkp) bissue(1, wchunk(1));
     for (int j = 0; j < nkp; ++j) {
       // chunk j landed for this wave (younger: chunk j+1's NI DMA instructions), then all waves

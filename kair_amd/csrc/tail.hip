@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_wgrad_kernel(const NarrowW
   const int n = lane & 3;
 #pragma unroll
   for (int tg = 0; tg < 3; ++tg) {
-    const int tap = 4 * tg + tl;
+    const int tap = 4 * tg + q;   // D column l % 16 = 4 (tap - 4 tg) + n
     if (tap < 9 && n < a.NR)
 #pragma unroll
       for (int i = 0; i < 4; ++i) dst[(n * NF + 16 * wave + 4 * (lane >> 4) + i) * 9 + tap] = acc[tg][i];

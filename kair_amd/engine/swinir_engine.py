@@ -228,7 +228,7 @@ class SwinIREngine:
         """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
         see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
         fused block kernels (_Lin, pack kind 12).
-        split_act (bf16 only): the forward convs also read their input activation as a hi/lo bf16
+        split_act (bf16 with split_conv only): the forward convs also read their input activation as a hi/lo bf16
         pair (kair_operand.a_split: the input image, every RSTB / conv_after_body conv input and the
         reconstruction tail's activations), the operand roundings that move the evaluation PSNR
         (tools/drift_ablation.py, DESIGN.md "parity at bf16"); the Swin-block internals stay bf16.
@@ -242,7 +242,9 @@ class SwinIREngine:
         self.cd = H.BF16 if compute_dtype == "bf16" else H.F32
         self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
         self.split_conv = bool(split_conv) and compute_dtype == "bf16"
-        self.split_act = bool(split_act) and compute_dtype == "bf16"
+        # split activations only pay with split weights (a bf16 weight rounding dominates otherwise), and
+        # the tied pair forms need split weight packs
+        self.split_act = bool(split_act) and self.split_conv
         self.C = net.embed_dim
         heads = {l.residual_group.blocks[0].num_heads for l in net.layers}
         if len(heads) != 1:

@@ -1,7 +1,7 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_fused_gpu.py tests/test_swinir_gpu.py tests/test_swinir_variants_gpu.py tests/test_tail_gpu.py tests/test_split_gpu.py > gpurun_out/r4e_tests.log 2>&1 || { grep -E "Error|error|assert|FAIL" gpurun_out/r4e_tests.log | head -30; tail -5 gpurun_out/r4e_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_fused_gpu.py tests/test_swinir_gpu.py tests/test_swinir_variants_gpu.py tests/test_tail_gpu.py tests/test_split_gpu.py > gpurun_out/r4e_tests.log 2>&1 || { grep -E "Error|error|assert|FAIL" gpurun_out/r4e_tests.log | head -30; tail -5 gpurun_out/r4e_tests.log; exit 1; }
 tail -2 gpurun_out/r4e_tests.log
 timeout -k 10 200 python -u tools/roles.py 32 > gpurun_out/r4e_roles32.txt 2>&1
 timeout -k 10 200 python -u tools/roles.py 4 > gpurun_out/r4e_roles4.txt 2>&1
