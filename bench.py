@@ -177,7 +177,7 @@ def rocprof_name(fn, a):
         ks = 2 if N == 384 else 4   # csrc/rowgemm.hip rg_dispatch: <KB, KS, NWC, EPI, HOLD>
         hold = {12: kb // ks, 24: 6, 36: {0: 9, 1: 7, 2: 5}[epi]}[kb]
         return f"rowgemm_kernel<{kb}, {ks}, {N // 96}, {epi}, {hold}>"
-    return {"swin_mlp_fwd": "swin_mlp_fwd_wr_kernel", "swin_attn_fwd": "swin_attn_fwd_kernel<6, 1>",
+    return {"swin_mlp_fwd": "swin_mlp_fwd_wr_kernel", "swin_attn_fwd": "swin_attn_fwd12_kernel<6>",   # KAIR_ATTN12 (swin_fused.hip)
             "window_attn_bwd": "attn_bwd_bf16_kernel"}.get(fn, fn)
 
 
@@ -535,7 +535,7 @@ def main():
                            key=lambda kv: -kv[1]["ms_total"])
     # attention GEMMs (QKV / q.k^T / p.v / proj): the fused attention half, the attention backward, the proj and
     # q/k/v input-gradient row GEMMs -- FLOPs over their in-step time against the dense bf16 MFMA peak
-    att_names = ("swin_attn_fwd_kernel", "attn_bwd_bf16_kernel", "rowgemm_kernel<12, 4, 2, 0>", "rowgemm_kernel<36")
+    att_names = ("swin_attn_fwd", "attn_bwd_bf16_kernel", "rowgemm_kernel<12, 4, 2, 0>", "rowgemm_kernel<36")
     att = [v for v in roles.values() if v.get("flops") and v["rocprof"].startswith(att_names)]
     att_mfma = None
     if att:

@@ -7,4 +7,6 @@ timeout -k 10 200 python -u tools/roles.py 32 > gpurun_out/r4e_roles32.txt 2>&1
 timeout -k 10 200 python -u tools/roles.py 4 > gpurun_out/r4e_roles4.txt 2>&1
 timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-other-configs --no-fp32-line > gpurun_out/r4e_bench.log 2>&1
 timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-other-configs --no-fp32-line --per-gpu-batch 4 > gpurun_out/r4e_bench4.log 2>&1
-echo OK
+echo OK; grep -h "^{" gpurun_out/r4e_bench.log gpurun_out/r4e_bench4.log | cut -c1-300
+timeout -k 10 200 python -u tools/b4_micro.py > gpurun_out/r4e_b4micro.txt 2>&1
+echo MICRO
