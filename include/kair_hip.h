@@ -173,7 +173,11 @@ typedef struct {
                           row 16nb + l%16, k 32kb + 8(l/16) + j);
                         15 conv3x3 forward in the kind-14 fragment order with hi/lo halves (bf16 only):
                           [Np/16][9*Kp/32][2][64][8], contraction index k = tap*Kp + cip (the
-                          narrow-N conv's register-resident weights, kair_conv3x3_narrow_fwd) */
+                          narrow-N conv's register-resident weights, kair_conv3x3_narrow_fwd;
+                          kair_conv3x3_wr's split form);
+                        16 conv3x3 dgrad form (kind 2) in the kind-14 fragment order (bf16):
+                          [Kp/16][9*Np/32][64][8], rows = input channels, k = tap*Np + cop
+                          (kair_conv3x3_wr's plain form over the output gradient, flip = 1) */
   int N, K;          /* reference dims: linear (out,in); conv (Cout,Cin)                     */
   int nG, nGr, nGp;  /* out dim = nG groups of nGr real rows padded to nGp                   */
   int kG, kGr, kGp;  /* in  dim = kG groups of kGr real cols padded to kGp (kinds 1 / 9 only: kG*kGr
@@ -348,6 +352,21 @@ int kair_swin_mlp_bwd(const void* dc, long lddc, const void* gd, long ldg, const
                       const float* rstd, int C, float* D, long ldD, void* dco, long lddo, const float* rowscale,
                       int rows_per_scale, int H, int W, int shift, float* dgamma, float* dbeta, int dparam_acc,
                       float* ws, long M, int Cp, int Hp, void* stream);
+
+/* 3x3 conv, stride 1, pad 1, with the weights streamed from global memory into registers (one wave
+ * per SIMD, the input tile's halo in LDS; csrc/conv_wr.hip) -- replaces the RSTB conv and its input
+ * gradient of the implicit GEMM (kair_gemm_nt over KAIR_LD_IM2COL3, network_swinir.py:263-279 RSTB.conv).
+ * x: NHWC rows [B*H*W][ldx], fp32 or bf16.  split = 1 (fp32 x): split activations -- the kernel forms
+ * lo = bf16(x - bf16(x)) and multiplies hi.W_hi + hi.W_lo + lo.W_hi (w = pack kind 15, Np = 192);
+ * split = 0: one bf16 product (w = pack kind 16, the dgrad form, with flip = 1 for an input gradient).  n_blocks = Np/16
+ * (12).  out[m][n] = conv + bias[n] (+ resid[m][n]), fp32 or bf16 rows, n < N.  acopy (optional): the
+ * bf16 copy of the image rows (hi half) with 1.0 at column acones (bias gradient), as kair_epilogue
+ * a_copy.  C a multiple of 64, <= 192; N <= 192, N % 4 == 0; tiles of 96 (split) or 144 pixels: whole
+ * rows of W <= tile or tile-sized pieces of wider rows (kair_conv3x3_wr_tile: 0 = unsupported). */
+int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N);
+int kair_conv3x3_wr(const void* x, int x_dtype, long ldx, int split, int flip, const void* w, int n_blocks,
+                    const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo, void* acopy,
+                    long ldac, int acones, int B, int H, int W, int C, int N, void* stream);
 
 /* Narrow-output 3x3 convs (csrc/tail.hip): a 64-channel NHWC bf16 image <-> NR <= 4 output channels,
  * the last conv of the reconstruction head (network_swinir.py:745, :817 conv_last).

@@ -126,6 +126,9 @@ _SIGS = {
     "kair_image_to_nhwc_hilo": [c_vp, c_vp, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
     "kair_conv3x3_narrow_fwd": [c_vp, c_long, c_int, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_vp, c_int, c_int, c_int,
                                 c_vp],
+    "kair_conv3x3_wr_tile": [c_int, c_int, c_int, c_int, c_int, c_int],
+    "kair_conv3x3_wr": [c_vp, c_int, c_long, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_long, c_vp, c_int, c_long, c_vp,
+                        c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "kair_conv3x3_narrow_dgrad_ws": [],
     "kair_conv3x3_narrow_dgrad": [c_vp, c_long, c_vp, c_int, c_vp, c_vp, c_int, c_long, c_int, c_int, c_int, c_int, c_vp],
     "kair_conv3x3_narrow_wgrad_ws": [c_int],
@@ -539,6 +542,25 @@ def conv3x3_narrow_fwd(x, ldx, lo_off, w, bias, NR, mean, img_range, resid, out,
     """conv_last forward: 64-channel bf16 rows (hi, + lo at lo_off) -> NCHW image (csrc/tail.hip)."""
     check(lib().kair_conv3x3_narrow_fwd(ptr(x), ldx, lo_off, ptr(w), ptr(bias), NR, ptr(mean), img_range, ptr(resid),
                                         ptr(out), B, H, W, stream_ptr()), "conv3x3_narrow_fwd")
+
+
+def conv3x3_wr_tile(split, B, H, W, C, N):
+    """Tile (pixels) of kair_conv3x3_wr for this shape, 0 when unsupported."""
+    return lib().kair_conv3x3_wr_tile(int(bool(split)), B, H, W, C, N)
+
+
+def conv3x3_wr(x, ldx, flip, w, bias, resid, out, B, H, W, C, N, ldr=None, ldo=None, acopy=None, ldac=None, acones=-1,
+               n_blocks=12, split=None):
+    """3x3 conv with register-streamed weights (csrc/conv_wr.hip): split (default: x fp32) = split
+    activations with w = pack kind 15 (Np = 192); else one bf16 product with w = pack kind 16 (flip = 1:
+    input gradient), x fp32 or bf16 rows."""
+    if split is None:
+        split = x.dtype == torch.float32
+    check(lib().kair_conv3x3_wr(ptr(x), dtype_code(x), ldx, int(bool(split)), int(flip), ptr(w), n_blocks, ptr(bias), ptr(resid),
+                                ldr if ldr is not None else (resid.shape[-1] if resid is not None else 0),
+                                ptr(out), dtype_code(out), ldo if ldo is not None else out.shape[-1], ptr(acopy),
+                                ldac if ldac is not None else (acopy.shape[-1] if acopy is not None else 0), acones,
+                                B, H, W, C, N, stream_ptr()), "conv3x3_wr")
 
 
 def conv3x3_narrow_dgrad_ws():

@@ -1,0 +1,323 @@
+// 3x3 convolution (stride 1, pad 1) for gfx950 with the weights streamed straight into registers:
+// the RSTB convolutions of SwinIR (network_swinir.py:263-279 RSTB.conv, 3x3 180 -> 180 at the LQ size)
+// and their input gradients, as an implicit GEMM  D[n][p] = sum_k W[n][k] X^T[k][p],  k = tap * C + c.
+//
+// Why not the LDS-ring halo kernel (gemm.hip conv3x3_halo_kernel): that one stages every 64-wide weight
+// chunk through LDS for all eight waves of a 512-thread workgroup, so each chunk costs a workgroup
+// barrier and an LDS-DMA round trip two chunks ahead; at two waves per SIMD both waves arrive at the
+// barrier together and the chunk's LDS reads and DMA waits are exposed (measured: 22-25 % of the MFMA
+// peak, 43 % of the wave cycles parked in s_waitcnt / s_barrier; profiles/r04_conv_micro.txt).
+//
+// Here one 256-thread workgroup per CU runs ONE wave per SIMD.  The input tile's halo lives in LDS for
+// the whole tile (loaded once; with split activations BOTH the hi and the lo halves, 2 x 80 KB), and
+// each wave owns 48 output channels of the tile: its weight fragments come from global memory (pack
+// kind 15 / 16: 16x16x32 fragment order, one coalesced 1 KiB wave load per fragment) into a ring of
+// registers three k-steps deep, its activation fragments from the halo one k-step ahead.  The k-loop
+// has no barrier and no LDS traffic but the operand reads; each wave's only waits are its own loads.
+//
+//   split (fp32 image, kair_operand.a_split semantics): 3 products per k-step  hi.W_hi + hi.W_lo +
+//          lo.W_hi  (lo = bf16(x - bf16(x)) formed while the halo is filled), 96-pixel tiles;
+//   plain (bf16 image, e.g. the input gradient with flipped taps): 1 product, 144-pixel tiles.
+// Epilogue per lane: 4 consecutive output channels of one pixel (bias, fp32 residual, fp32 / bf16
+// rows).  The tile's own pixels can be copied out as bf16 rows (a_copy, + a ones column) for the
+// weight gradient, as the halo kernel does.
+#include "common.h"
+
+namespace {
+
+constexpr int WR_WAVES = 4;          // one per SIMD
+constexpr int WR_NT = 64 * WR_WAVES;
+constexpr int WR_RN = 3;             // 16-wide n fragments per wave: 48 output channels
+constexpr int WR_PD = 3;             // k-steps of weight fragments in flight
+
+struct ConvWrArgs {
+  const void* x; long ldx;           // NHWC image rows: fp32 (split) or bf16
+  const bf16* w;                     // kind 15 (split: [Np/16][KS][2][64][8]) or 16 ([Np/16][KS][64][8])
+  const float* bias;                 // [>= N] or null
+  const float* resid; long ldr;      // fp32 rows or null
+  void* out; int odt; long ldo;
+  bf16* acopy; long ldac; int acones;
+  int B, H, W, C, N, flip;
+  long tilesM;
+  FDiv fc8, fhwd;                    // C / 8 and the halo row width (magic-number divisions)
+};
+
+// bf16 elements of one halo image: split -- two images (hi, lo) of 40,000 (96-pixel tiles); plain -- one
+// of 80,000 (160,000 B: the whole LDS)
+template <bool SPLIT> struct WrGeom {
+  static constexpr int HALO = SPLIT ? 40000 : 80000;
+};
+
+template <typename TX, bool SPLIT, int BM, bool RESID>
+__global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a) {
+  static_assert(!SPLIT || sizeof(TX) == 4, "split activations are formed from an fp32 image");
+  constexpr int RM = BM / 16;
+  constexpr int HALO = WrGeom<SPLIT>::HALO;
+  constexpr int NB = SPLIT ? 2 : 1;                         // weight fragments per (rn, k-step)
+  __shared__ __attribute__((aligned(16))) bf16 sH[SPLIT ? 2 * HALO : HALO];
+  bf16* const sLo = sH + (SPLIT ? HALO : 0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int H = a.H, W = a.W, C = a.C;
+  const int XW = W < BM ? W : BM, RPT = BM / XW, HWD = XW + 2, HR = RPT + 2, PS = C + 8;
+  const int c8n = C / 8, halo_pieces = HR * HWD * c8n;
+  const int cps = C / 32, KS = 9 * cps;                     // k-steps of 32
+  int hb[RM];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int p = i * 16 + fr;
+    const int ry = p / XW, rx = p - (p / XW) * XW;
+    hb[i] = ((ry + 1) * HWD + rx + 1) * PS + fq * 8;
+  }
+  // this wave's weight fragments: n blocks 3 w + rn, k-step s: one 1 KiB wave load per fragment
+  const bf16* wb = a.w + ((long)(3 * wave) * KS * NB) * 512 + lane * 8;
+  auto wfrag = [&](int rn, int s, int half) {
+    return *(const bf16x8*)(wb + (((long)rn * KS + s) * NB + half) * 512);
+  };
+  float4 bias4[WR_RN];
+#pragma unroll
+  for (int rn = 0; rn < WR_RN; ++rn) {
+    const int n = 48 * wave + 16 * rn + 4 * fq;
+    bias4[rn] = a.bias && n < a.N ? *(const float4*)(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  bf16x8 rb[WR_PD][WR_RN][NB];     // weight ring
+  auto issue_w = [&](int slot, int s) {
+#pragma unroll
+    for (int rn = 0; rn < WR_RN; ++rn)
+#pragma unroll
+      for (int h = 0; h < NB; ++h) rb[slot][rn][h] = wfrag(rn, s, h);
+  };
+  bf16x8 ra[2][RM][NB];            // activation fragments, one k-step ahead
+  auto read_a = [&](int buf, int s) {
+    const int tap = s / cps, c0 = (s - tap * cps) * 32;
+    int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    if (a.flip) { dy = -dy; dx = -dx; }
+    const int off = (dy * HWD + dx) * PS + c0;
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      ra[buf][i][0] = *(const bf16x8*)(sH + hb[i] + off);
+      if constexpr (SPLIT) ra[buf][i][1] = *(const bf16x8*)(sLo + hb[i] + off);
+    }
+  };
+
+  const long tiles = a.tilesM;
+  for (long t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const long p0 = t * BM;
+    const int b = (int)(p0 / ((long)H * W));
+    const int rem = (int)(p0 - (long)b * H * W);
+    const int y0 = rem / W, x0 = rem - (rem / W) * W;
+    // the first k-steps' weights in flight under the halo fill
+#pragma unroll
+    for (int u = 0; u < WR_PD; ++u) issue_w(u, u);
+    __syncthreads();   // every wave is done with the previous tile's halo
+    {
+      // pieces per thread in one batch of loads (all issued, then landed, then written): the whole
+      // halo at once where the registers allow it -- each batch is one exposed memory latency
+      constexpr int HP = SPLIT ? 10 : (sizeof(TX) == 4 ? 12 : 16);
+      const int per = (halo_pieces + WR_NT - 1) / WR_NT;
+      for (int h0 = 0; h0 < per; h0 += HP) {
+        uint4 v0[HP], v1[HP];
+        bool okv[HP];
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+          const int idx = tid + WR_NT * (h0 + i);
+          const int pix = fdiv(idx, a.fc8), c8 = idx - pix * c8n;
+          const int hr = fdiv(pix, a.fhwd), hc = pix - hr * HWD;
+          const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+          okv[i] = idx < halo_pieces && y >= 0 && y < H && x >= 0 && x < W;
+          const long src = okv[i] ? ((long)(b * H + y) * W + x) * a.ldx + c8 * 8 : 0;
+          if constexpr (sizeof(TX) == 4) {
+            v0[i] = *(const uint4*)((const float*)a.x + src);
+            v1[i] = *(const uint4*)((const float*)a.x + src + 4);
+          } else {
+            v0[i] = *(const uint4*)((const bf16*)a.x + src);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+          const int idx = tid + WR_NT * (h0 + i);
+          if (idx >= halo_pieces) continue;
+          const int pix = fdiv(idx, a.fc8), c8 = idx - pix * c8n;
+          uint4 qh, ql = make_uint4(0, 0, 0, 0);
+          if constexpr (sizeof(TX) == 4) {
+            const float4 u = __builtin_bit_cast(float4, v0[i]), v = __builtin_bit_cast(float4, v1[i]);
+            const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+            bf16x8 hh, ll;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              hh[e] = (bf16)f[e];
+              if constexpr (SPLIT) ll[e] = (bf16)(f[e] - (float)hh[e]);
+            }
+            qh = __builtin_bit_cast(uint4, hh);
+            if constexpr (SPLIT) ql = __builtin_bit_cast(uint4, ll);
+          } else {
+            qh = v0[i];
+          }
+          if (!okv[i]) qh = ql = make_uint4(0, 0, 0, 0);
+          *(uint4*)(sH + pix * PS + c8 * 8) = qh;
+          if constexpr (SPLIT) *(uint4*)(sLo + pix * PS + c8 * 8) = ql;
+          if (a.acopy) {   // the tile's own pixels: bf16 copy (+ ones column) for the weight gradient
+            const int hr = fdiv(pix, a.fhwd), hc = pix - hr * HWD;
+            if (hr >= 1 && hr <= RPT && hc >= 1 && hc <= XW) {
+              uint4 qc = qh;
+              const int oc = a.acones - c8 * 8;
+              if ((unsigned)oc < 8u) {
+                bf16x8 v8 = __builtin_bit_cast(bf16x8, qc);
+                v8[oc] = (bf16)1.f;
+                qc = __builtin_bit_cast(uint4, v8);
+              }
+              const long px = (long)(b * H + y0 + hr - 1) * W + x0 + hc - 1;
+              *(uint4*)(a.acopy + px * a.ldac + c8 * 8) = qc;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();   // halo visible
+
+    f32x4 acc[RM][WR_RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int rn = 0; rn < WR_RN; ++rn) acc[i][rn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 ex[RESID ? RM : 1][WR_RN];
+    auto load_resid = [&]() {
+      if constexpr (RESID) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int rn = 0; rn < WR_RN; ++rn) {
+            const long m = p0 + i * 16 + fr;
+            const int n = 48 * wave + 16 * rn + 4 * fq;
+            ex[i][rn] = *(const float4*)(a.resid + m * a.ldr + (n < a.N ? n : 0));
+          }
+      }
+    };
+    read_a(0, 0);
+    // k-loop, unrolled by 6 (the weight ring is 3 deep, the activation buffers 2): KS % 6 == 0 (host).
+    // Every load is unconditional (the last steps re-read step KS - 1): a load on only some paths makes
+    // the compiler's wait at the merge the minimum over the paths (vmcnt / lgkmcnt 0 every step).
+    auto step = [&](int u, int s, bool tail) {
+      const int ab = u & 1, ws = u % WR_PD;
+      read_a(ab ^ 1, s + 1 < KS ? s + 1 : KS - 1);
+      if (RESID && tail && u == 3) load_resid();
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int rn = 0; rn < WR_RN; ++rn) {
+          acc[i][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[ws][rn][0], ra[ab][i][0], acc[i][rn], 0, 0, 0);
+          if constexpr (SPLIT) {
+            acc[i][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[ws][rn][1], ra[ab][i][0], acc[i][rn], 0, 0, 0);
+            acc[i][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[ws][rn][0], ra[ab][i][1], acc[i][rn], 0, 0, 0);
+          }
+        }
+      issue_w(ws, s + WR_PD < KS ? s + WR_PD : KS - 1);
+    };
+    for (int s0 = 0; s0 < KS - 6; s0 += 6) {
+#pragma unroll
+      for (int u = 0; u < 6; ++u) step(u, s0 + u, false);
+    }
+#pragma unroll
+    for (int u = 0; u < 6; ++u) step(u, KS - 6 + u, true);
+    // epilogue: 4 consecutive channels of one pixel per lane
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int rn = 0; rn < WR_RN; ++rn) {
+        const long m = p0 + i * 16 + fr;
+        const int n = 48 * wave + 16 * rn + 4 * fq;
+        if (n >= a.N) continue;
+        const float4 bb = bias4[rn];
+        float v[4] = {acc[i][rn][0] + bb.x, acc[i][rn][1] + bb.y, acc[i][rn][2] + bb.z, acc[i][rn][3] + bb.w};
+        if constexpr (RESID) {
+          v[0] += ex[i][rn].x; v[1] += ex[i][rn].y; v[2] += ex[i][rn].z; v[3] += ex[i][rn].w;
+        }
+        const long o = m * a.ldo + n;
+        if (a.odt == KAIR_BF16) *(bf16x4*)((bf16*)a.out + o) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        else *(float4*)((float*)a.out + o) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+  }
+}
+
+int wr_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// geometry of a BM-pixel tile: whole rows of width W <= BM, or BM-pixel pieces of wider rows
+bool wr_geometry(int BM, int halo, long M, int H, int W, int C) {
+  if (W <= 0 || H <= 0 || M <= 0) return false;
+  if (W <= BM) {
+    if (BM % W != 0 || H % (BM / W) != 0) return false;
+  } else if (W % BM != 0) {
+    return false;
+  }
+  const int XW = W < BM ? W : BM, RPT = BM / XW;
+  return (long)(RPT + 2) * (XW + 2) * (C + 8) <= halo && M % BM == 0 && M % ((long)H * W) == 0;
+}
+
+}  // namespace
+
+/* The tile (pixels) kair_conv3x3_wr uses for this shape, or 0 when the shape is not supported. */
+extern "C" int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N) {
+  const long M = (long)B * H * W;
+  if (C <= 0 || C > 192 || C % 64 != 0 || N <= 0 || N > 192 || N % 4 != 0) return 0;
+  if (split) return wr_geometry(96, WrGeom<true>::HALO, M, H, W, C) ? 96 : 0;
+  if (wr_geometry(144, WrGeom<false>::HALO, M, H, W, C)) return 144;
+  return wr_geometry(96, WrGeom<false>::HALO, M, H, W, C) ? 96 : 0;
+}
+
+template <typename TX, bool SPLIT>
+static void wr_launch(const ConvWrArgs& a, int BM, bool resid, int grid, hipStream_t s) {
+  if (BM == 144) {
+    if constexpr (!SPLIT) {
+      if (resid) hipLaunchKernelGGL((conv3x3_wr_kernel<TX, false, 144, true>), dim3(grid), dim3(WR_NT), 0, s, a);
+      else hipLaunchKernelGGL((conv3x3_wr_kernel<TX, false, 144, false>), dim3(grid), dim3(WR_NT), 0, s, a);
+    }
+    return;
+  }
+  if (resid) hipLaunchKernelGGL((conv3x3_wr_kernel<TX, SPLIT, 96, true>), dim3(grid), dim3(WR_NT), 0, s, a);
+  else hipLaunchKernelGGL((conv3x3_wr_kernel<TX, SPLIT, 96, false>), dim3(grid), dim3(WR_NT), 0, s, a);
+}
+
+extern "C" int kair_conv3x3_wr(const void* x, int x_dtype, long ldx, int split, int flip, const void* w, int n_blocks,
+                               const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo, void* acopy,
+                               long ldac, int acones, int B, int H, int W, int C, int N, void* stream) {
+  KAIR_CHECK_ARG(x && w && out && B > 0, "conv3x3_wr: null operand");
+  KAIR_CHECK_ARG(x_dtype == KAIR_F32 || x_dtype == KAIR_BF16, "conv3x3_wr: image dtype");
+  KAIR_CHECK_ARG(!split || x_dtype == KAIR_F32, "conv3x3_wr: split activations are formed from an fp32 image");
+  KAIR_CHECK_ARG(out_dtype == KAIR_F32 || out_dtype == KAIR_BF16, "conv3x3_wr: output dtype");
+  const int BM = kair_conv3x3_wr_tile(split, B, H, W, C, N);
+  KAIR_CHECK_ARG(BM > 0, "conv3x3_wr: unsupported geometry (B %d, H %d, W %d, C %d, N %d)", B, H, W, C, N);
+  KAIR_CHECK_ARG(n_blocks == 12, "conv3x3_wr: the packed weight needs 192 output rows (12 blocks of 16), got %d", n_blocks);
+  KAIR_CHECK_ARG(ldx >= C && ldx % (x_dtype == KAIR_F32 ? 4 : 8) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0,
+                 "conv3x3_wr: image rows 16-byte aligned, ldx >= C");
+  KAIR_CHECK_ARG(ldo >= N && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0, "conv3x3_wr: output rows");
+  KAIR_CHECK_ARG(!resid || (ldr >= N && ldr % 4 == 0 && ((uintptr_t)resid & 15) == 0), "conv3x3_wr: residual rows");
+  KAIR_CHECK_ARG(!bias || ((uintptr_t)bias & 15) == 0, "conv3x3_wr: bias alignment");
+  KAIR_CHECK_ARG(!acopy || (ldac >= C && ldac % 8 == 0 && ((uintptr_t)acopy & 15) == 0), "conv3x3_wr: a_copy rows");
+  const long M = (long)B * H * W;
+  KAIR_CHECK_ARG(M * (ldx > ldo ? ldx : ldo) < (1L << 31), "conv3x3_wr: operands past 2^31 elements");
+  ConvWrArgs a;
+  a.x = x; a.ldx = ldx; a.w = (const bf16*)w; a.bias = bias; a.resid = resid; a.ldr = ldr;
+  a.out = out; a.odt = out_dtype; a.ldo = ldo; a.acopy = (bf16*)acopy; a.ldac = ldac; a.acones = acopy ? acones : -1;
+  a.B = B; a.H = H; a.W = W; a.C = C; a.N = N; a.flip = flip;
+  a.tilesM = M / BM;
+  a.fc8 = make_fdiv(C / 8);
+  a.fhwd = make_fdiv((W < BM ? W : BM) + 2);
+  const int ncu = wr_num_cus();
+  const int grid = (int)(a.tilesM < ncu ? a.tilesM : ncu);
+  hipStream_t s = (hipStream_t)stream;
+  if (split) wr_launch<float, true>(a, BM, resid != nullptr, grid, s);
+  else if (x_dtype == KAIR_F32) wr_launch<float, false>(a, BM, resid != nullptr, grid, s);
+  else wr_launch<bf16, false>(a, BM, resid != nullptr, grid, s);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}

@@ -114,6 +114,16 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
     const bf16 hi = (bf16)v;
     ((bf16*)dst)[t] = half ? (bf16)(v - (float)hi) : hi;
     return;
+  } else if (mp.kind == 16) {  // conv3x3 input-gradient form (kind 2) in 16x16x32 fragment order:
+                               // [Kp/16][9*Np/32][64][8], rows = input channels cip, k = tap*Np + cop
+    const int KB = 9 * Np / 32;
+    const int j = (int)(t & 7), ln = (int)((t >> 3) & 63);
+    const long blk = t >> 9;
+    const int kb = (int)(blk % KB), cb = (int)(blk / KB);
+    const int cip = cb * 16 + (ln & 15), kk = kb * 32 + 8 * (ln >> 4) + j;
+    const int tap = kk / Np, cop = kk - tap * Np;
+    const int n = nperm_fwd(mp, unpad(cop, mp.nG, mp.nGr, mp.nGp)), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
+    if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci) * 9 + tap];
   } else if (mp.kind == 8) {  // conv2x2 [4*Kp][Np], row = kp*4 + tap (pixel-shuffle forms)
     const int row = (int)(t / Np), np = (int)(t - (long)row * Np);
     const int kp = row >> 2, tap = row & 3;
@@ -606,9 +616,10 @@ static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
   KAIR_CHECK_ARG(mp.kind != 13 || (Kp % 32 == 0 && Np % 16 == 0), "pack_weight: transposed fragment order needs Kp %% 32 == 0, Np %% 16 == 0");
   KAIR_CHECK_ARG(mp.kind != 14 || (Np % 16 == 0 && Kp % 32 == 0), "pack_weight: 16x16x32 fragment order needs Np %% 16 == 0, Kp %% 32 == 0");
   KAIR_CHECK_ARG(mp.kind != 15 || (Np % 16 == 0 && (9 * Kp) % 32 == 0), "pack_weight: kind 15 needs Np %% 16 == 0, 9 Kp %% 32 == 0");
+  KAIR_CHECK_ARG(mp.kind != 16 || (Kp % 16 == 0 && (9 * Np) % 32 == 0), "pack_weight: kind 16 needs Kp %% 16 == 0, 9 Np %% 32 == 0");
   if (mp.kind == 0 || mp.kind == 3 || mp.kind == 10 || mp.kind == 13 || mp.kind == 14) *total = Np * Kp;
   else if (mp.kind == 12) *total = 2 * Np * Kp;
-  else if (mp.kind == 1 || mp.kind == 2) *total = Np * 9 * Kp;
+  else if (mp.kind == 1 || mp.kind == 2 || mp.kind == 16) *total = Np * 9 * Kp;
   else if (mp.kind == 7 || mp.kind == 8) *total = Np * 4 * Kp;
   else if (mp.kind == 9) *total = Np * 2 * ((9L * Kp + 63) / 64) * 64;
   else if (mp.kind == 15) *total = 2 * Np * 9 * Kp;

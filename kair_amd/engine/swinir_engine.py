@@ -126,7 +126,7 @@ class _Conv:
     (DESIGN.md "parity at bf16"); activation rounding is unbiased and averages out."""
 
     def __init__(self, eng, mod, Cop, Cip, need_dgrad=True, split=None, n_perm=0, tied_in=False, fwd_cip=None,
-                 narrow=False):
+                 narrow=False, wr=False):
         """n_perm = r*r: output channels stored sub-pixel-major for a following PixelShuffle(r)
         (kair_wmap.n_perm; the KAIR_OUT_PSHUF_SPM / PUNSHUF_SPM epilogues store 16 bytes at a time).
         tied_in: the forward form repeats the input channels in both halves of Cip (kair_wmap kG = 2),
@@ -135,7 +135,8 @@ class _Conv:
         fwd_cip: the forward form's packed input width when it differs from Cip (a [hi | lo] pair image of
         2 x Cip channels read through tied weights: the SwinIR tail under split_act).
         narrow: a 64 -> NR <= 4 conv run by the narrow-output kernels (kair_conv3x3_narrow_*): its forward
-        form is pack kind 15 (16x16x32 fragment order, hi/lo halves), the backward reads the fp32 weight."""
+        form is pack kind 15 (16x16x32 fragment order, hi/lo halves), the backward reads the fp32 weight.
+        wr: a 192 -> 192 conv also packed for kair_conv3x3_wr: forward pack kind 15, input gradient kind 16."""
         self.w, self.b = mod.weight, mod.bias
         Co, Ci = self.w.shape[:2]
         self.Co, self.Ci, self.Cop, self.Cip = Co, Ci, Cop, Cip
@@ -159,6 +160,12 @@ class _Conv:
             self.Wn = torch.empty(16, 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
         self.Wd = torch.empty(Cip, 9 * Cop, device=dev, dtype=eng.tdt) if need_dgrad else None
         self.bp = torch.empty(Cop, device=dev)
+        self.wr = bool(wr) and Cop == 192 and Cip == 192 and self.split
+        if self.wr:
+            self.map15 = H.wmap(15, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
+            self.Wf15 = torch.empty(Cop * 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
+            self.map16 = H.wmap(16, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
+            self.Wd16 = torch.empty(Cip * 9 * Cop, device=dev, dtype=torch.bfloat16)
 
     def fwd(self):
         """The forward GEMM's B operand."""
@@ -171,6 +178,8 @@ class _Conv:
             jobs.append((w, self.Wd, self.mapd))
         if self.narrow:
             jobs.append((w, self.Wn, self.mapn))
+        if self.wr:
+            jobs += [(w, self.Wf15, self.map15), (w, self.Wd16, self.map16)]
         return jobs
 
 
@@ -194,7 +203,9 @@ class _Resi3:
 
 
 def _resi(eng, m):
-    return _Resi3(eng, m) if isinstance(m, torch.nn.Sequential) else _Conv(eng, m, eng.Cp, eng.Cp)
+    if isinstance(m, torch.nn.Sequential):
+        return _Resi3(eng, m)
+    return _Conv(eng, m, eng.Cp, eng.Cp, wr=getattr(eng, "conv_wr", False))
 
 
 class _Blk:
@@ -224,7 +235,7 @@ class _Blk:
 class SwinIREngine:
     def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True, fused_mlp=None,
                  split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=0, side_priority=0,
-                 split_act=True):
+                 split_act=True, conv_wr=True):
         """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
         see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
         fused block kernels (_Lin, pack kind 12).
@@ -285,6 +296,10 @@ class SwinIREngine:
         self.Cin_p = 8
         # split_act: the input image as a hi/lo pair in channels [0, in_ch) / [4, 4 + in_ch) of Cin_p
         self.xin_hilo = self.split_act and 2 * self.in_ch <= self.Cin_p
+        # the '1conv' RSTB / conv_after_body convs (192 -> 192) and their input gradients on the
+        # register-streamed-weight kernel (kair_conv3x3_wr, csrc/conv_wr.hip) where the per-GPU batch gives
+        # it enough tiles (plan: P["conv_wr"]); the LDS-ring halo kernel otherwise
+        self.conv_wr = bool(conv_wr) and self.split_act and self.Cp == 192 and self.C % 4 == 0
         self.device = net.conv_first.weight.device
         dev = self.device
         self.mean = net.mean.view(-1).to(dev, torch.float32).contiguous()
@@ -354,6 +369,7 @@ class SwinIREngine:
         self.side_ctas = int(side_ctas)
         # '1conv' weight gradients on the tap-per-tile ring (bf16 copies of G and the conv input)
         self.conv_tap = self.tdt == torch.bfloat16 and self.Cp == 192 and self.C % 4 == 0
+        self.conv_wr_min_tiles = 256   # P["conv_wr"]: 96-pixel tiles needed (one per CU)
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -525,6 +541,12 @@ class SwinIREngine:
             # bf16 operands of each '1conv' weight gradient: (G, conv input with 1.0 in channel C), written by
             # the halo convs (forward: input, backward dgrad: G) or, off that path, copied when the job runs
             P["conv_halo"] = H.conv_halo_geometry(Hh, Ww, Cp, M, Cp)
+            # the register-streamed-weight conv: one 96-pixel tile per workgroup per CU round, so only with
+            # at least a full round of tiles (B = 32: 768 tiles; B = 4: 96 -> the halo kernel's N tiles)
+            P["conv_wr"] = bool(self.conv_wr and H.conv3x3_wr_tile(1, B, Hh, Ww, Cp, Cp) == 96 and
+                                H.conv3x3_wr_tile(0, B, Hh, Ww, Cp, Cp) > 0 and M // 96 >= self.conv_wr_min_tiles)
+            if P["conv_wr"]:
+                P["conv_halo"] = True   # the wr kernel leaves the same bf16 copies
             P["conv_bf"] = {}
             for r in [c for _, c in self.rstb] + [self.cab]:
                 if not isinstance(r, _Resi3):
@@ -621,6 +643,11 @@ class SwinIREngine:
         if not isinstance(r, _Resi3):
             # training: the halo conv also leaves the bf16 weight-gradient operand (1.0 in channel C)
             ac = (P["conv_bf"][id(r)][1], self.C) if P.get("conv_halo") else None
+            if P.get("conv_wr") and r.wr:
+                assert src.dtype == torch.float32 and resid.dtype == torch.float32
+                H.conv3x3_wr(src, Cp, 0, r.Wf15, r.bp, resid, out, P["B"], Hh, Ww, Cp, Cp, acopy=ac[0], acones=ac[1],
+                             split=True)
+                return
             H.gemm_nt(self._ain(H.im2col(src, Hh, Ww, Cp)), r.fwd(), H.epilogue(out, bias=r.bp, resid=resid, acopy=ac), M,
                       Cp, 9 * Cp, cd)
             return
@@ -638,7 +665,10 @@ class SwinIREngine:
         g = lambda p: grads[p]
         if not isinstance(r, _Resi3):
             ac = (P["conv_bf"][id(r)][0], -1) if P.get("conv_halo") else None
-            H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.Wd), H.epilogue(D, acopy=ac), M, Cp, 9 * Cp, cd)
+            if P.get("conv_wr") and r.wr:
+                H.conv3x3_wr(G, Cp, 1, r.Wd16, None, None, D, P["B"], Hh, Ww, Cp, Cp, acopy=ac[0], split=False)
+            else:
+                H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.Wd), H.epilogue(D, acopy=ac), M, Cp, 9 * Cp, cd)
             if self.conv_tap:   # bf16 operands: the halo convs' copies (else taken when the job runs)
                 return ("tap", G, src, r, g(r.w), g(r.b))
             return (H.rows(G), H.im2col(src, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, r.map, g(r.w), g(r.b), self.C)

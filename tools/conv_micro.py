@@ -59,6 +59,21 @@ t = timeit(lambda: H.gemm_nt(H.im2col(x16, Hh, Ww, Cp), H.rows(Ws, w_split=True)
 rows.append(("rstb fwd bf16 (2 products)", t, 2 * fl))
 t = timeit(lambda: H.gemm_nt(H.im2col(x16, Hh, Ww, Cp, flip=True), H.rows(Wd), H.epilogue(out), M, Cp, 9 * Cp, H.BF16))
 rows.append(("rstb dgrad bf16 (1 product)", t, fl))
+t = timeit(lambda: H.gemm_nt(H.im2col(x32, Hh, Ww, Cp, flip=True), H.rows(Wd), H.epilogue(out), M, Cp, 9 * Cp, H.BF16))
+rows.append(("rstb dgrad fp32 G (1 product)", t, fl))
+# the register-streamed-weight kernel (csrc/conv_wr.hip) on the same shapes
+w32 = torch.randn(C, C, 3, 3, device=dev) * 0.05
+Wf = torch.empty(192 * 2 * 9 * Cp, device=dev, dtype=torch.bfloat16)
+H.pack_weight(w32, Wf, H.wmap(15, C, C, (1, C, Cp), (1, C, Cp)))
+Wdf = torch.empty(192 * 9 * Cp, device=dev, dtype=torch.bfloat16)
+H.pack_weight(w32, Wdf, H.wmap(16, C, C, (1, C, Cp), (1, C, Cp)))
+ac = torch.empty(M, Cp, device=dev, dtype=torch.bfloat16)
+t = timeit(lambda: H.conv3x3_wr(x32, Cp, 0, Wf, bias, resid, out, B, Hh, Ww, Cp, Cp, acopy=ac, acones=C))
+rows.append(("wr: rstb fwd fp32 split (3 products)", t, 3 * fl))
+t = timeit(lambda: H.conv3x3_wr(x16, Cp, 1, Wdf, None, None, out, B, Hh, Ww, Cp, Cp))
+rows.append(("wr: rstb dgrad bf16 (1 product)", t, fl))
+t = timeit(lambda: H.conv3x3_wr(x32, Cp, 1, Wdf, None, None, out, B, Hh, Ww, Cp, Cp, acopy=ac, split=False))
+rows.append(("wr: rstb dgrad fp32 G + a_copy (1 product)", t, fl))
 # upsampling conv 2 of x4: 64 -> 256 over 96 x 96, [hi | lo] pair input, PixelShuffle output
 h2, w2 = 96, 96
 M2 = B * h2 * w2
