@@ -411,6 +411,10 @@ def main():
     ap.add_argument("--main-priority", type=int, default=0, help="A/B: torch priority of the step's capture stream")
     ap.add_argument("--no-side-stream", action="store_true",
                     help="A/B: run the deferred per-RSTB gradient work in place on the main stream")
+    ap.add_argument("--split-linear", action="store_true",
+                    help="A/B: hi/lo split weights in the fused Swin-block linears (SwinIREngine split_linear)")
+    ap.add_argument("--conv-wr-min-tiles", type=int, default=None,
+                    help="A/B: 96-pixel tiles from which the RSTB convs run on kair_conv3x3_wr (< 0: never)")
     ap.add_argument("--dry-run", action="store_true", help="exercise the rank launch on the CPU (gloo) and exit")
     ap.add_argument("--data", default="pool", choices=["pool", "static"],
                     help="pool: every step synthesises a fresh batch on the GPU from an HBM-resident HR pool "
@@ -451,12 +455,19 @@ def main():
     if world > 1:   # replicas start identical (DDP construction broadcast, model_base.py:116)
         for t in list(net.state_dict().values()) + list(ema.state_dict().values()):
             dist.broadcast(t, 0)
-    if args.no_side_stream or args.side_ctas is not None or args.side_priority:
+    if args.no_side_stream or args.side_ctas is not None or args.side_priority or args.split_linear:
         from kair_amd.engine.swinir_engine import SwinIREngine
         kw = {"side_stream": not args.no_side_stream, "side_priority": args.side_priority}
+        if args.split_linear:
+            kw["split_linear"] = True
         if args.side_ctas is not None:
             kw["side_ctas"] = args.side_ctas
         net._engine = SwinIREngine(net, args.dtype, **kw)
+    if args.conv_wr_min_tiles is not None:
+        eng = net.engine()
+        if args.conv_wr_min_tiles < 0:
+            eng.conv_wr = False
+        eng.conv_wr_min_tiles = max(0, args.conv_wr_min_tiles)
     tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999, use_graph=not args.no_graph, stream_priority=args.main_priority)
     if args.data == "pool":
         from kair_amd.data.gpu_synth import PatchSynth, synthetic_pool

@@ -27,7 +27,6 @@ namespace {
 
 constexpr int WR_WAVES = 4;          // one per SIMD
 constexpr int WR_NT = 64 * WR_WAVES;
-constexpr int WR_RN = 3;             // 16-wide n fragments per wave: 48 output channels
 constexpr int WR_PD = 3;             // k-steps of weight fragments in flight
 
 struct ConvWrArgs {
@@ -37,6 +36,8 @@ struct ConvWrArgs {
   const float* resid; long ldr;      // fp32 rows or null
   void* out; int odt; long ldo;
   bf16* acopy; long ldac; int acones;
+  bf16* out_lo;                      // pair output: bf16(v - bf16(v)) at the same offsets (bf16 out only)
+  int ps_r;                          // > 0: PixelShuffle(ps_r) sub-pixel-major output (n = (i r + j) nf + c)
   int B, H, W, C, N, flip;
   long tilesM;
   FDiv fc8, fhwd;                    // C / 8 and the halo row width (magic-number divisions)
@@ -48,9 +49,13 @@ template <bool SPLIT> struct WrGeom {
   static constexpr int HALO = SPLIT ? 40000 : 80000;
 };
 
-template <typename TX, bool SPLIT, int BM, bool RESID>
+// SPLIT with an fp32 image: lo formed in the halo fill; SPLIT with a bf16 image ("pair"): the image rows
+// are [hi | lo] halves of C channels each (the split tail's activations), read into the two halos.
+// RN: 16-wide output fragments per wave (3: N <= 192, 4: N <= 256).  EM 1: PixelShuffle sub-pixel-major
+// store (+ the lo plane of a bf16 pair output).
+template <typename TX, bool SPLIT, int BM, bool RESID, int RN, int EM>
 __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a) {
-  static_assert(!SPLIT || sizeof(TX) == 4, "split activations are formed from an fp32 image");
+  constexpr bool PAIR = SPLIT && sizeof(TX) == 2;
   constexpr int RM = BM / 16;
   constexpr int HALO = WrGeom<SPLIT>::HALO;
   constexpr int NB = SPLIT ? 2 : 1;                         // weight fragments per (rn, k-step)
@@ -70,21 +75,21 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
     hb[i] = ((ry + 1) * HWD + rx + 1) * PS + fq * 8;
   }
   // this wave's weight fragments: n blocks 3 w + rn, k-step s: one 1 KiB wave load per fragment
-  const bf16* wb = a.w + ((long)(3 * wave) * KS * NB) * 512 + lane * 8;
+  const bf16* wb = a.w + ((long)(RN * wave) * KS * NB) * 512 + lane * 8;
   auto wfrag = [&](int rn, int s, int half) {
     return *(const bf16x8*)(wb + (((long)rn * KS + s) * NB + half) * 512);
   };
-  float4 bias4[WR_RN];
+  float4 bias4[RN];
 #pragma unroll
-  for (int rn = 0; rn < WR_RN; ++rn) {
-    const int n = 48 * wave + 16 * rn + 4 * fq;
+  for (int rn = 0; rn < RN; ++rn) {
+    const int n = 16 * RN * wave + 16 * rn + 4 * fq;
     bias4[rn] = a.bias && n < a.N ? *(const float4*)(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
-  bf16x8 rb[WR_PD][WR_RN][NB];     // weight ring
+  bf16x8 rb[WR_PD][RN][NB];        // weight ring
   auto issue_w = [&](int slot, int s) {
 #pragma unroll
-    for (int rn = 0; rn < WR_RN; ++rn)
+    for (int rn = 0; rn < RN; ++rn)
 #pragma unroll
       for (int h = 0; h < NB; ++h) rb[slot][rn][h] = wfrag(rn, s, h);
   };
@@ -114,7 +119,7 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
     {
       // pieces per thread in one batch of loads (all issued, then landed, then written): the whole
       // halo at once where the registers allow it -- each batch is one exposed memory latency
-      constexpr int HP = SPLIT ? 10 : (sizeof(TX) == 4 ? 12 : 16);
+      constexpr int HP = PAIR ? 5 : SPLIT ? 10 : (sizeof(TX) == 4 ? 12 : 16);
       const int per = (halo_pieces + WR_NT - 1) / WR_NT;
       for (int h0 = 0; h0 < per; h0 += HP) {
         uint4 v0[HP], v1[HP];
@@ -132,6 +137,7 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
             v1[i] = *(const uint4*)((const float*)a.x + src + 4);
           } else {
             v0[i] = *(const uint4*)((const bf16*)a.x + src);
+            if constexpr (PAIR) v1[i] = *(const uint4*)((const bf16*)a.x + src + C);
           }
         }
 #pragma unroll
@@ -153,6 +159,7 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
             if constexpr (SPLIT) ql = __builtin_bit_cast(uint4, ll);
           } else {
             qh = v0[i];
+            if constexpr (PAIR) ql = v1[i];
           }
           if (!okv[i]) qh = ql = make_uint4(0, 0, 0, 0);
           *(uint4*)(sH + pix * PS + c8 * 8) = qh;
@@ -176,20 +183,20 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
     }
     __syncthreads();   // halo visible
 
-    f32x4 acc[RM][WR_RN];
+    f32x4 acc[RM][RN];
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
-      for (int rn = 0; rn < WR_RN; ++rn) acc[i][rn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 ex[RESID ? RM : 1][WR_RN];
+      for (int rn = 0; rn < RN; ++rn) acc[i][rn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 ex[RESID ? RM : 1][RN];
     auto load_resid = [&]() {
       if constexpr (RESID) {
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
-          for (int rn = 0; rn < WR_RN; ++rn) {
+          for (int rn = 0; rn < RN; ++rn) {
             const long m = p0 + i * 16 + fr;
-            const int n = 48 * wave + 16 * rn + 4 * fq;
+            const int n = 16 * RN * wave + 16 * rn + 4 * fq;
             ex[i][rn] = *(const float4*)(a.resid + m * a.ldr + (n < a.N ? n : 0));
           }
       }
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int rn = 0; rn < WR_RN; ++rn) {
+        for (int rn = 0; rn < RN; ++rn) {
           acc[i][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[ws][rn][0], ra[ab][i][0], acc[i][rn], 0, 0, 0);
           if constexpr (SPLIT) {
             acc[i][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[ws][rn][1], ra[ab][i][0], acc[i][rn], 0, 0, 0);
@@ -224,18 +231,31 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
-      for (int rn = 0; rn < WR_RN; ++rn) {
+      for (int rn = 0; rn < RN; ++rn) {
         const long m = p0 + i * 16 + fr;
-        const int n = 48 * wave + 16 * rn + 4 * fq;
+        const int n = 16 * RN * wave + 16 * rn + 4 * fq;
         if (n >= a.N) continue;
         const float4 bb = bias4[rn];
         float v[4] = {acc[i][rn][0] + bb.x, acc[i][rn][1] + bb.y, acc[i][rn][2] + bb.z, acc[i][rn][3] + bb.w};
         if constexpr (RESID) {
           v[0] += ex[i][rn].x; v[1] += ex[i][rn].y; v[2] += ex[i][rn].z; v[3] += ex[i][rn].w;
         }
-        const long o = m * a.ldo + n;
-        if (a.odt == KAIR_BF16) *(bf16x4*)((bf16*)a.out + o) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        else *(float4*)((float*)a.out + o) = make_float4(v[0], v[1], v[2], v[3]);
+        long o = m * a.ldo + n;
+        if constexpr (EM == 1) {   // sub-pixel-major columns: n = (i r + j) nf + c -> pixel (y r + i, x r + j)
+          const int r = a.ps_r, nf = a.N / (r * r);
+          const int bi = (int)(m / ((long)H * W)), pp = (int)(m - (long)bi * H * W), yy = pp / W, xx = pp - yy * W;
+          const int sp = n / nf, cc = n - sp * nf, ii = sp / r, jj = sp - ii * r;
+          o = (((long)bi * H * r + (long)yy * r + ii) * ((long)W * r) + (long)xx * r + jj) * a.ldo + cc;
+        }
+        if (a.odt == KAIR_BF16) {
+          const bf16x4 hv = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          *(bf16x4*)((bf16*)a.out + o) = hv;
+          if (a.out_lo)
+            *(bf16x4*)(a.out_lo + o) = bf16x4{(bf16)(v[0] - (float)hv[0]), (bf16)(v[1] - (float)hv[1]),
+                                              (bf16)(v[2] - (float)hv[2]), (bf16)(v[3] - (float)hv[3])};
+        } else {
+          *(float4*)((float*)a.out + o) = make_float4(v[0], v[1], v[2], v[3]);
+        }
       }
   }
 }
@@ -265,49 +285,49 @@ bool wr_geometry(int BM, int halo, long M, int H, int W, int C) {
 
 }  // namespace
 
-/* The tile (pixels) kair_conv3x3_wr uses for this shape, or 0 when the shape is not supported. */
+/* The tile (pixels) kair_conv3x3_wr uses for this shape, or 0 when the shape is not supported.  split:
+ * two halos (split activations, fp32 image, or a bf16 [hi | lo] pair image of C channels per half). */
 extern "C" int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N) {
   const long M = (long)B * H * W;
-  if (C <= 0 || C > 192 || C % 64 != 0 || N <= 0 || N > 192 || N % 4 != 0) return 0;
+  if (C <= 0 || C > 192 || C % 64 != 0 || N <= 0 || N > 256 || N % 4 != 0) return 0;
   if (split) return wr_geometry(96, WrGeom<true>::HALO, M, H, W, C) ? 96 : 0;
+  if (N > 192) return 0;
   if (wr_geometry(144, WrGeom<false>::HALO, M, H, W, C)) return 144;
   return wr_geometry(96, WrGeom<false>::HALO, M, H, W, C) ? 96 : 0;
 }
 
-template <typename TX, bool SPLIT>
-static void wr_launch(const ConvWrArgs& a, int BM, bool resid, int grid, hipStream_t s) {
-  if (BM == 144) {
-    if constexpr (!SPLIT) {
-      if (resid) hipLaunchKernelGGL((conv3x3_wr_kernel<TX, false, 144, true>), dim3(grid), dim3(WR_NT), 0, s, a);
-      else hipLaunchKernelGGL((conv3x3_wr_kernel<TX, false, 144, false>), dim3(grid), dim3(WR_NT), 0, s, a);
-    }
-    return;
-  }
-  if (resid) hipLaunchKernelGGL((conv3x3_wr_kernel<TX, SPLIT, 96, true>), dim3(grid), dim3(WR_NT), 0, s, a);
-  else hipLaunchKernelGGL((conv3x3_wr_kernel<TX, SPLIT, 96, false>), dim3(grid), dim3(WR_NT), 0, s, a);
-}
+#define KAIR_WR(TXV, SPV, BMV, RV, RNV, EMV) \
+  hipLaunchKernelGGL((conv3x3_wr_kernel<TXV, SPV, BMV, RV, RNV, EMV>), dim3(grid), dim3(WR_NT), 0, s, a)
 
-extern "C" int kair_conv3x3_wr(const void* x, int x_dtype, long ldx, int split, int flip, const void* w, int n_blocks,
-                               const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo, void* acopy,
-                               long ldac, int acones, int B, int H, int W, int C, int N, void* stream) {
+extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int split, int flip, const void* w, int n_blocks,
+                                  const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo,
+                                  void* out_lo, int ps_r, void* acopy, long ldac, int acones, int B, int H, int W, int C,
+                                  int N, void* stream) {
   KAIR_CHECK_ARG(x && w && out && B > 0, "conv3x3_wr: null operand");
   KAIR_CHECK_ARG(x_dtype == KAIR_F32 || x_dtype == KAIR_BF16, "conv3x3_wr: image dtype");
-  KAIR_CHECK_ARG(!split || x_dtype == KAIR_F32, "conv3x3_wr: split activations are formed from an fp32 image");
   KAIR_CHECK_ARG(out_dtype == KAIR_F32 || out_dtype == KAIR_BF16, "conv3x3_wr: output dtype");
+  const bool pair = split && x_dtype == KAIR_BF16;
   const int BM = kair_conv3x3_wr_tile(split, B, H, W, C, N);
   KAIR_CHECK_ARG(BM > 0, "conv3x3_wr: unsupported geometry (B %d, H %d, W %d, C %d, N %d)", B, H, W, C, N);
-  KAIR_CHECK_ARG(n_blocks == 12, "conv3x3_wr: the packed weight needs 192 output rows (12 blocks of 16), got %d", n_blocks);
-  KAIR_CHECK_ARG(ldx >= C && ldx % (x_dtype == KAIR_F32 ? 4 : 8) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0,
-                 "conv3x3_wr: image rows 16-byte aligned, ldx >= C");
-  KAIR_CHECK_ARG(ldo >= N && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0, "conv3x3_wr: output rows");
+  const int RN = N > 192 ? 4 : 3;
+  KAIR_CHECK_ARG(n_blocks == 4 * RN, "conv3x3_wr: the packed weight needs %d output rows (%d blocks of 16), got %d blocks",
+                 64 * RN, 4 * RN, n_blocks);
+  KAIR_CHECK_ARG(ldx >= (pair ? 2 * C : C) && ldx % (x_dtype == KAIR_F32 ? 4 : 8) == 0 && ((uintptr_t)x & 15) == 0 &&
+                     ((uintptr_t)w & 15) == 0,
+                 "conv3x3_wr: image rows 16-byte aligned, ldx >= C (2 C for a [hi | lo] pair)");
+  KAIR_CHECK_ARG(ps_r >= 0 && (ps_r == 0 || (N % (ps_r * ps_r) == 0 && (N / (ps_r * ps_r)) % 4 == 0 && !resid)),
+                 "conv3x3_wr: PixelShuffle output needs N %% r^2 == 0, N / r^2 %% 4 == 0 and no residual");
+  KAIR_CHECK_ARG(ldo >= (ps_r ? N / (ps_r * ps_r) : N) && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0, "conv3x3_wr: output rows");
+  KAIR_CHECK_ARG(!out_lo || (out_dtype == KAIR_BF16 && ((uintptr_t)out_lo & 7) == 0), "conv3x3_wr: out_lo needs a bf16 output");
   KAIR_CHECK_ARG(!resid || (ldr >= N && ldr % 4 == 0 && ((uintptr_t)resid & 15) == 0), "conv3x3_wr: residual rows");
   KAIR_CHECK_ARG(!bias || ((uintptr_t)bias & 15) == 0, "conv3x3_wr: bias alignment");
-  KAIR_CHECK_ARG(!acopy || (ldac >= C && ldac % 8 == 0 && ((uintptr_t)acopy & 15) == 0), "conv3x3_wr: a_copy rows");
+  KAIR_CHECK_ARG(!acopy || (!pair && ldac >= C && ldac % 8 == 0 && ((uintptr_t)acopy & 15) == 0), "conv3x3_wr: a_copy rows");
   const long M = (long)B * H * W;
-  KAIR_CHECK_ARG(M * (ldx > ldo ? ldx : ldo) < (1L << 31), "conv3x3_wr: operands past 2^31 elements");
+  KAIR_CHECK_ARG(M * (ldx > ldo ? ldx : ldo) * (ps_r ? ps_r * ps_r : 1) < (1L << 31), "conv3x3_wr: operands past 2^31 elements");
   ConvWrArgs a;
   a.x = x; a.ldx = ldx; a.w = (const bf16*)w; a.bias = bias; a.resid = resid; a.ldr = ldr;
   a.out = out; a.odt = out_dtype; a.ldo = ldo; a.acopy = (bf16*)acopy; a.ldac = ldac; a.acones = acopy ? acones : -1;
+  a.out_lo = (bf16*)out_lo; a.ps_r = ps_r;
   a.B = B; a.H = H; a.W = W; a.C = C; a.N = N; a.flip = flip;
   a.tilesM = M / BM;
   a.fc8 = make_fdiv(C / 8);
@@ -315,9 +335,30 @@ extern "C" int kair_conv3x3_wr(const void* x, int x_dtype, long ldx, int split, 
   const int ncu = wr_num_cus();
   const int grid = (int)(a.tilesM < ncu ? a.tilesM : ncu);
   hipStream_t s = (hipStream_t)stream;
-  if (split) wr_launch<float, true>(a, BM, resid != nullptr, grid, s);
-  else if (x_dtype == KAIR_F32) wr_launch<float, false>(a, BM, resid != nullptr, grid, s);
-  else wr_launch<bf16, false>(a, BM, resid != nullptr, grid, s);
+  const bool rs = resid != nullptr;
+  if (pair) {   // the SwinIR x4 upsampling convs: [hi | lo] pair in, PixelShuffle [hi | lo] pair out
+    KAIR_CHECK_ARG(RN == 4 && ps_r > 0 && !rs, "conv3x3_wr: the pair form is built for N in (192, 256] with a PixelShuffle store");
+    KAIR_WR(bf16, true, 96, false, 4, 1);
+  } else {
+    KAIR_CHECK_ARG(RN == 3 && ps_r == 0, "conv3x3_wr: N <= 192 row outputs for this form");
+    if (split) {
+      if (rs) KAIR_WR(float, true, 96, true, 3, 0); else KAIR_WR(float, true, 96, false, 3, 0);
+    } else if (x_dtype == KAIR_F32) {
+      if (BM == 144) { if (rs) KAIR_WR(float, false, 144, true, 3, 0); else KAIR_WR(float, false, 144, false, 3, 0); }
+      else { if (rs) KAIR_WR(float, false, 96, true, 3, 0); else KAIR_WR(float, false, 96, false, 3, 0); }
+    } else {
+      if (BM == 144) { if (rs) KAIR_WR(bf16, false, 144, true, 3, 0); else KAIR_WR(bf16, false, 144, false, 3, 0); }
+      else { if (rs) KAIR_WR(bf16, false, 96, true, 3, 0); else KAIR_WR(bf16, false, 96, false, 3, 0); }
+    }
+  }
+#undef KAIR_WR
   KAIR_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int kair_conv3x3_wr(const void* x, int x_dtype, long ldx, int split, int flip, const void* w, int n_blocks,
+                               const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo, void* acopy,
+                               long ldac, int acones, int B, int H, int W, int C, int N, void* stream) {
+  return kair_conv3x3_wr_ex(x, x_dtype, ldx, split, flip, w, n_blocks, bias, resid, ldr, out, out_dtype, ldo, nullptr, 0,
+                            acopy, ldac, acones, B, H, W, C, N, stream);
 }

@@ -161,6 +161,11 @@ class _Conv:
         self.Wd = torch.empty(Cip, 9 * Cop, device=dev, dtype=eng.tdt) if need_dgrad else None
         self.bp = torch.empty(Cop, device=dev)
         self.wr = bool(wr) and Cop == 192 and Cip == 192 and self.split
+        # wr_pair: an upsampling conv (64 -> 256, sub-pixel-major rows) reading a [hi | lo] pair image
+        self.wr_pair = bool(wr) and not self.wr and tied_in and Cip == 64 and fcip == 128 and Cop == 256 and self.split
+        if self.wr_pair:
+            self.mapp = H.wmap(15, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
+            self.Wp15 = torch.empty(Cop * 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
         if self.wr:
             self.map15 = H.wmap(15, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
             self.Wf15 = torch.empty(Cop * 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
@@ -180,6 +185,8 @@ class _Conv:
             jobs.append((w, self.Wn, self.mapn))
         if self.wr:
             jobs += [(w, self.Wf15, self.map15), (w, self.Wd16, self.map16)]
+        if self.wr_pair:
+            jobs.append((w, self.Wp15, self.mapp))
         return jobs
 
 
@@ -321,7 +328,8 @@ class SwinIREngine:
             for m in net.upsample:
                 if isinstance(m, torch.nn.Conv2d):   # output channels sub-pixel-major (PSHUF_SPM)
                     self.ups.append(_Conv(self, m, m.out_channels, nf, n_perm=m.out_channels // nf,
-                                          tied_in=self.split_act, fwd_cip=2 * nf if self.split_act else None))
+                                          tied_in=self.split_act, fwd_cip=2 * nf if self.split_act else None,
+                                          wr=self.conv_wr))
             self.ups_r = [int(math.isqrt(c.Co // nf)) for c in self.ups]
             # conv_last 64 -> in_ch on the narrow-output kernels (bf16 engine; HR width a multiple of 16)
             # (per call: the HR width must be a multiple of 64, else the implicit-GEMM path runs)
@@ -369,7 +377,7 @@ class SwinIREngine:
         self.side_ctas = int(side_ctas)
         # '1conv' weight gradients on the tap-per-tile ring (bf16 copies of G and the conv input)
         self.conv_tap = self.tdt == torch.bfloat16 and self.Cp == 192 and self.C % 4 == 0
-        self.conv_wr_min_tiles = 256   # P["conv_wr"]: 96-pixel tiles needed (one per CU)
+        self.conv_wr_min_tiles = 64    # P["conv_wr"]: 96-pixel tiles needed (B = 4: 96 tiles, 1.04x faster than the halo kernel)
 
     def grad_segments(self):
         """Parameter groups in the order backward() completes their gradients; seg_hook() fires
@@ -709,6 +717,12 @@ class SwinIREngine:
                       9 * Cp, cd)
             src, h, w = P["a0"], Hh, Ww
             for c, r, dst in zip(self.ups, self.ups_r, P["ups_act"]):
+                if (c.wr_pair and self.conv_wr and H.conv3x3_wr_tile(1, B, h, w, 64, c.Co) == 96 and
+                        B * h * w // 96 >= self.conv_wr_min_tiles):   # kair_conv3x3_wr, pair form
+                    H.conv3x3_wr(src, tl, 0, c.Wp15, c.bp, None, dst, B, h, w, 64, c.Co, ldo=tl, split=True,
+                                 out_lo=lo(dst), ps_r=r)
+                    src, h, w = dst, h * r, w * r
+                    continue
                 A = H.asplit(H.im2col(src, h, w, c.fcip), pair=True) if sa else H.im2col(src, h, w, 64)
                 H.gemm_nt(A, c.fwd(), H.epilogue(dst, mode=H.OUT_PSHUF_SPM, ldo=tl, bias=c.bp, ps=(r, h, w), out_lo=lo(dst)),
                           B * h * w, c.Co, 9 * c.fcip, cd)

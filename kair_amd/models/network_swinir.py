@@ -354,6 +354,12 @@ class SwinIR(nn.Module):
         self.split_conv = split_conv
         self.fused_blocks = fused_blocks
         self._engine = None
+        # evaluation numerics of the bf16 engine: the Swin-block linears also multiply hi/lo split weight
+        # pairs (SwinIREngine split_linear) in eval-mode forwards, on top of the training step's split conv
+        # weights and activations -- the bf16 rounding of the linear weights is half of the forward's
+        # remaining output error (profiles/r04_drift_ablation.txt); eval is not on the timed path
+        self.eval_split_linear = True
+        self._engine_eval = None
 
     @staticmethod
     def _init_weights(m):
@@ -380,13 +386,25 @@ class SwinIR(nn.Module):
             self._engine = SwinIREngine(self, self.compute_dtype, self.split_conv, self.fused_blocks)
         return self._engine
 
+    def eval_engine(self):
+        """The engine of eval-mode forwards: the training engine, or for bf16 with eval_split_linear its
+        split-linear twin (same kernels, hi/lo weight pairs in the fused block kernels)."""
+        if self.compute_dtype != "bf16" or not self.eval_split_linear:
+            return self.engine()
+        if self._engine_eval is None or self._engine_eval.net_ref() is not self:
+            self._engine_eval = SwinIREngine(self, self.compute_dtype, self.split_conv, self.fused_blocks, split_linear=True,
+                                             side_stream=False)
+        return self._engine_eval
+
     def _apply(self, fn, *args, **kwargs):
         self._engine = None     # packed buffers live on the old device / dtype
+        self._engine_eval = None
         return super()._apply(fn, *args, **kwargs)
 
     def set_compute_dtype(self, dtype):
         self.compute_dtype = dtype
         self._engine = None
+        self._engine_eval = None
         self._set_op_compute()
         return self
 
@@ -416,7 +434,8 @@ class SwinIR(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("kair_amd SwinIR runs on the MI355X (HIP) only; got a CPU tensor (no CPU fallback)")
         params = [p for p in self.parameters()]
-        return SwinIRFunction.run(self.engine(), x, params)
+        eng = self.engine() if self.training else self.eval_engine()
+        return SwinIRFunction.run(eng, x, params)
 
     def flops(self):
         """Training FLOPs are tracked by kair_amd.engine.swinir_engine.swinir_flops()."""

@@ -87,6 +87,35 @@ def test_conv_wr_dgrad(shape, odt, xdt):
         assert torch.equal(ac.cpu(), gin.bfloat16().cpu())
 
 
+@pytest.mark.parametrize("hw", [(24, 48), (8, 96)])
+def test_conv_wr_pair_pshuf(hw):
+    """The x4 upsampling conv under split activations: a bf16 [hi | lo] pair image of 64 channels (two
+    halos), 64 -> 256 with hi/lo split weights (kind 15, Np = 256, sub-pixel-major rows), PixelShuffle(2)
+    store of a [hi | lo] pair (out_lo) -> ~2^-16 of the fp64 conv + pixel_shuffle."""
+    B, r = 2, 2
+    Hh, Ww = hw
+    g = torch.Generator().manual_seed(Hh + Ww)
+    x = torch.randn(B, 64, Hh, Ww, generator=g)
+    w = torch.randn(256, 64, 3, 3, generator=g) * 0.05
+    b = torch.randn(256, generator=g) * 0.1
+    ref = F.pixel_shuffle(F.conv2d(x.double(), w.double(), b.double(), padding=1), r)   # [B, 64, 2H, 2W]
+    M = B * Hh * Ww
+    rows = x.permute(0, 2, 3, 1).reshape(M, 64)
+    hi = rows.bfloat16()
+    lo = (rows - hi.float()).bfloat16()
+    pair = torch.cat([hi, lo], 1).contiguous().to(dev)
+    Wf = torch.empty(256 * 2 * 9 * 64, device=dev, dtype=torch.bfloat16)
+    H.pack_weight(w.to(dev), Wf, H.wmap(15, 256, 64, (1, 256, 256), (1, 64, 64), n_perm=r * r))
+    bp = torch.empty(256, device=dev)
+    H.pack_weight(b.to(dev), bp, H.wmap(4, 256, 0, (1, 256, 256), (1, 1, 1), n_perm=r * r))
+    out = torch.full((M * r * r, 128), float("nan"), device=dev, dtype=torch.bfloat16)
+    assert H.conv3x3_wr_tile(1, B, Hh, Ww, 64, 256) == 96
+    H.conv3x3_wr(pair, 128, 0, Wf, bp, None, out, B, Hh, Ww, 64, 256, ldo=128, split=True, out_lo=out[:, 64:], ps_r=r)
+    torch.cuda.synchronize()
+    got = (out[:, :64].double() + out[:, 64:].double()).cpu().view(B, Hh * r, Ww * r, 64).permute(0, 3, 1, 2)
+    assert rel_err(got, ref) < 3e-5
+
+
 def test_conv_wr_rejects():
     x = torch.zeros(2 * 48 * 48, 192, device=dev)
     w = torch.zeros(192 * 2 * 9 * 192, device=dev, dtype=torch.bfloat16)
