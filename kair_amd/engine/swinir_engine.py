@@ -421,6 +421,10 @@ class SwinIREngine:
 
     def pack(self, force=False):
         net = self.net_ref()
+        # repack_always: an engine whose parameters are updated outside torch (the fused trainer's Adam
+        # kernel writes the flat parameter buffer; versions do not move) and that no step graph repacks
+        # -- the eval-mode twin (SwinIR.eval_engine)
+        force = force or getattr(self, "repack_always", False)
         ver = None if force else tuple(p._version for p in net.parameters())
         if ver is not None and ver == self._packed_version:
             return

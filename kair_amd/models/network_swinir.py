@@ -394,6 +394,7 @@ class SwinIR(nn.Module):
         if self._engine_eval is None or self._engine_eval.net_ref() is not self:
             self._engine_eval = SwinIREngine(self, self.compute_dtype, self.split_conv, self.fused_blocks, split_linear=True,
                                              side_stream=False)
+            self._engine_eval.repack_always = True   # the trainer's Adam kernel leaves parameter versions alone
         return self._engine_eval
 
     def _apply(self, fn, *args, **kwargs):
