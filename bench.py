@@ -24,11 +24,13 @@ sys.path.insert(0, ROOT)
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, Chip-level parameters)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
-PRECISION_BF16 = ("bf16 MFMA with fp32 accumulation; every forward conv multiplies hi/lo bf16 pairs of its weights AND "
-                  "its input activation (~16-bit operands: the input image, RSTB / conv_after_body inputs, the "
-                  "reconstruction tail), Swin-block GEMM operands bf16; fp32 master weights, residual stream, "
-                  "LayerNorm statistics, softmax and Adam + EMA.  Holds the PSNR bar (psnr fields; "
-                  "tests/test_swinir_gpu.py::test_swinir_classical_full_bf16_psnr_along_training, 160 steps)")
+PRECISION_BF16 = ("training step: bf16 MFMA with fp32 accumulation; every forward conv multiplies hi/lo bf16 pairs of "
+                  "its weights AND its input activation (~16-bit operands: the input image, RSTB / conv_after_body "
+                  "inputs, the reconstruction tail), Swin-block GEMM operands bf16; fp32 master weights, residual "
+                  "stream, LayerNorm statistics, softmax and Adam + EMA.  Evaluation (the psnr fields, eval-mode "
+                  "forwards): the same kernels with the Swin-block linear weights as hi/lo pairs too "
+                  "(SwinIR.eval_engine).  Holds the PSNR bar: "
+                  "tests/test_swinir_gpu.py::test_swinir_classical_full_bf16_psnr_along_training, 160 steps")
 
 
 def build_net(dtype, drop_path=0.1, seed=0):
