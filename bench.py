@@ -109,7 +109,7 @@ def _alg_flops(fn, a):
 _TIMED = ("gemm_nt", "gemm_tn", "wgrad_finalize", "colsum", "layernorm_fwd", "layernorm_bwd", "row_copy", "window_attn_fwd",
           "window_attn_bwd", "ln_param_reduce_grouped", "attn_dtable_grouped", "image_to_nhwc", "l1_loss", "axpy",
           "swin_attn_fwd", "swin_mlp_fwd", "rowgemm_store", "rowgemm_gate", "rowgemm_lnbwd", "image_to_nhwc_hilo",
-          "conv3x3_narrow_fwd", "conv3x3_narrow_dgrad", "conv3x3_narrow_wgrad")
+          "conv3x3_narrow_fwd", "conv3x3_narrow_dgrad", "conv3x3_narrow_wgrad", "conv3x3_wr")
 
 
 def time_roles(tr, serial=False):
@@ -179,7 +179,7 @@ def rocprof_name(fn, a):
         ks = 2 if N == 384 else 4   # csrc/rowgemm.hip rg_dispatch: <KB, KS, NWC, EPI, HOLD>
         hold = {12: kb // ks, 24: 6, 36: {0: 9, 1: 7, 2: 5}[epi]}[kb]
         return f"rowgemm_kernel<{kb}, {ks}, {N // 96}, {epi}, {hold}>"
-    return {"swin_mlp_fwd": "swin_mlp_fwd_wr_kernel", "swin_attn_fwd": "swin_attn_fwd12_kernel<6>",   # KAIR_ATTN12 (swin_fused.hip)
+    return {"conv3x3_wr": "conv3x3_wr_kernel", "swin_mlp_fwd": "swin_mlp_fwd_wr_kernel", "swin_attn_fwd": "swin_attn_fwd12_kernel<6>",   # KAIR_ATTN12 (swin_fused.hip)
             "window_attn_bwd": "attn_bwd_bf16_kernel"}.get(fn, fn)
 
 

@@ -38,6 +38,7 @@ struct ConvWrArgs {
   bf16* acopy; long ldac; int acones;
   bf16* out_lo;                      // pair output: bf16(v - bf16(v)) at the same offsets (bf16 out only)
   int ps_r;                          // > 0: PixelShuffle(ps_r) sub-pixel-major output (n = (i r + j) nf + c)
+  int act; float slope;              // KAIR_ACT_LEAKY: LeakyReLU(slope) before the store (no residual)
   int B, H, W, C, N, flip;
   long tilesM;
   FDiv fc8, fhwd;                    // C / 8 and the halo row width (magic-number divisions)
@@ -240,6 +241,10 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
         if constexpr (RESID) {
           v[0] += ex[i][rn].x; v[1] += ex[i][rn].y; v[2] += ex[i][rn].z; v[3] += ex[i][rn].w;
         }
+        if (a.act == KAIR_ACT_LEAKY) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : v[q] * a.slope;
+        }
         long o = m * a.ldo + n;
         if constexpr (EM == 1) {   // sub-pixel-major columns: n = (i r + j) nf + c -> pixel (y r + i, x r + j)
           const int r = a.ps_r, nf = a.N / (r * r);
@@ -301,15 +306,15 @@ extern "C" int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N
 
 extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int split, int flip, const void* w, int n_blocks,
                                   const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo,
-                                  void* out_lo, int ps_r, void* acopy, long ldac, int acones, int B, int H, int W, int C,
-                                  int N, void* stream) {
+                                  void* out_lo, int ps_r, int act, float slope, void* acopy, long ldac, int acones, int B,
+                                  int H, int W, int C, int N, void* stream) {
   KAIR_CHECK_ARG(x && w && out && B > 0, "conv3x3_wr: null operand");
   KAIR_CHECK_ARG(x_dtype == KAIR_F32 || x_dtype == KAIR_BF16, "conv3x3_wr: image dtype");
   KAIR_CHECK_ARG(out_dtype == KAIR_F32 || out_dtype == KAIR_BF16, "conv3x3_wr: output dtype");
   const bool pair = split && x_dtype == KAIR_BF16;
   const int BM = kair_conv3x3_wr_tile(split, B, H, W, C, N);
   KAIR_CHECK_ARG(BM > 0, "conv3x3_wr: unsupported geometry (B %d, H %d, W %d, C %d, N %d)", B, H, W, C, N);
-  const int RN = N > 192 ? 4 : 3;
+  const int RN = N > 192 ? 4 : N > 64 ? 3 : 1;
   KAIR_CHECK_ARG(n_blocks == 4 * RN, "conv3x3_wr: the packed weight needs %d output rows (%d blocks of 16), got %d blocks",
                  64 * RN, 4 * RN, n_blocks);
   KAIR_CHECK_ARG(ldx >= (pair ? 2 * C : C) && ldx % (x_dtype == KAIR_F32 ? 4 : 8) == 0 && ((uintptr_t)x & 15) == 0 &&
@@ -328,6 +333,8 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
   a.x = x; a.ldx = ldx; a.w = (const bf16*)w; a.bias = bias; a.resid = resid; a.ldr = ldr;
   a.out = out; a.odt = out_dtype; a.ldo = ldo; a.acopy = (bf16*)acopy; a.ldac = ldac; a.acones = acopy ? acones : -1;
   a.out_lo = (bf16*)out_lo; a.ps_r = ps_r;
+  KAIR_CHECK_ARG(act == KAIR_ACT_NONE || (act == KAIR_ACT_LEAKY && !resid), "conv3x3_wr: act none, or LeakyReLU without residual");
+  a.act = act; a.slope = slope;
   a.B = B; a.H = H; a.W = W; a.C = C; a.N = N; a.flip = flip;
   a.tilesM = M / BM;
   a.fc8 = make_fdiv(C / 8);
@@ -339,6 +346,9 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
   if (pair) {   // the SwinIR x4 upsampling convs: [hi | lo] pair in, PixelShuffle [hi | lo] pair out
     KAIR_CHECK_ARG(RN == 4 && ps_r > 0 && !rs, "conv3x3_wr: the pair form is built for N in (192, 256] with a PixelShuffle store");
     KAIR_WR(bf16, true, 96, false, 4, 1);
+  } else if (RN == 1) {   // conv_before_upsample (192 -> 64): split, row output (+ LeakyReLU, + lo plane)
+    KAIR_CHECK_ARG(split && x_dtype == KAIR_F32 && ps_r == 0, "conv3x3_wr: the N <= 64 form takes an fp32 image, split, rows");
+    if (rs) KAIR_WR(float, true, 96, true, 1, 0); else KAIR_WR(float, true, 96, false, 1, 0);
   } else {
     KAIR_CHECK_ARG(RN == 3 && ps_r == 0, "conv3x3_wr: N <= 192 row outputs for this form");
     if (split) {
@@ -360,5 +370,5 @@ extern "C" int kair_conv3x3_wr(const void* x, int x_dtype, long ldx, int split, 
                                const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo, void* acopy,
                                long ldac, int acones, int B, int H, int W, int C, int N, void* stream) {
   return kair_conv3x3_wr_ex(x, x_dtype, ldx, split, flip, w, n_blocks, bias, resid, ldr, out, out_dtype, ldo, nullptr, 0,
-                            acopy, ldac, acones, B, H, W, C, N, stream);
+                            KAIR_ACT_NONE, 0.f, acopy, ldac, acones, B, H, W, C, N, stream);
 }

@@ -416,17 +416,32 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_wgrad_kernel(const NarrowW
   }
 }
 
-// grad[e] (+)= sum over workgroups, in order
-__global__ void narrow_wgrad_finalize_kernel(const float* __restrict__ part, int nblk, int NR, float* __restrict__ gw,
-                                             float* __restrict__ gb, int accumulate) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+// grad[e] (+)= sum over workgroups, in fixed order: 16 elements x 16 partial ranges per 256-thread
+// workgroup (each thread sums its range's partials; the 16 range sums then added in range order), so the
+// ~1,700 outputs x 1,024 partials spread over ~110 workgroups instead of one thread per output
+constexpr int FIN_E = 16, FIN_R = 16;
+__global__ __launch_bounds__(256) void narrow_wgrad_finalize_kernel(const float* __restrict__ part, int nblk, int NR,
+                                                                    float* __restrict__ gw, float* __restrict__ gb,
+                                                                    int accumulate) {
+  __shared__ float sp[FIN_R][FIN_E];
   const int nw = NR * NF * 9, stride = nw + NR;
-  if (e >= stride) return;
+  const int el = threadIdx.x % FIN_E, rg = threadIdx.x / FIN_E;
+  const int e = blockIdx.x * FIN_E + el;
+  const int per = (nblk + FIN_R - 1) / FIN_R, k0 = rg * per, k1 = k0 + per < nblk ? k0 + per : nblk;
   float s = 0.f;
+  if (e < stride) {
 #pragma unroll 8
-  for (int k = 0; k < nblk; ++k) s += part[(long)k * stride + e];
-  if (e < nw) gw[e] = accumulate ? gw[e] + s : s;
-  else if (gb) gb[e - nw] = accumulate ? gb[e - nw] + s : s;
+    for (int k = k0; k < k1; ++k) s += part[(long)k * stride + e];
+  }
+  sp[rg][el] = s;
+  __syncthreads();
+  if (rg == 0 && e < stride) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < FIN_R; ++r) t += sp[r][el];
+    if (e < nw) gw[e] = accumulate ? gw[e] + t : t;
+    else if (gb) gb[e - nw] = accumulate ? gb[e - nw] + t : t;
+  }
 }
 
 // persistent workgroups: `per_cu` per CU (row runs of equal length)
@@ -499,7 +514,7 @@ extern "C" int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x
   hipLaunchKernelGGL(conv3x3_narrow_wgrad_kernel, dim3(grid), dim3(256), 0, s, a);
   KAIR_CHECK_LAUNCH();
   const int stride = NR * NF * 9 + NR;
-  hipLaunchKernelGGL(narrow_wgrad_finalize_kernel, dim3((stride + 255) / 256), dim3(256), 0, s, ws, grid, NR, grad_w,
+  hipLaunchKernelGGL(narrow_wgrad_finalize_kernel, dim3((stride + FIN_E - 1) / FIN_E), dim3(256), 0, s, ws, grid, NR, grad_w,
                      grad_b, accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;

@@ -166,6 +166,11 @@ class _Conv:
         if self.wr_pair:
             self.mapp = H.wmap(15, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
             self.Wp15 = torch.empty(Cop * 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
+        # wr_n64: conv_before_upsample (192 -> 64) on kair_conv3x3_wr's N <= 64 form
+        self.wr_n64 = bool(wr) and not self.wr and not self.wr_pair and Cop == 64 and Cip == 192 and self.split and not tied_in
+        if self.wr_n64:
+            self.mapc = H.wmap(15, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
+            self.Wc15 = torch.empty(Cop * 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
         if self.wr:
             self.map15 = H.wmap(15, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
             self.Wf15 = torch.empty(Cop * 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
@@ -187,6 +192,8 @@ class _Conv:
             jobs += [(w, self.Wf15, self.map15), (w, self.Wd16, self.map16)]
         if self.wr_pair:
             jobs.append((w, self.Wp15, self.mapp))
+        if self.wr_n64:
+            jobs.append((w, self.Wc15, self.mapc))
         return jobs
 
 
@@ -321,7 +328,7 @@ class SwinIREngine:
         self.cab = _resi(self, net.conv_after_body)
         nf = 64
         if self.upsampler == "pixelshuffle":
-            self.cbu = _Conv(self, net.conv_before_upsample[0], nf, self.Cp)
+            self.cbu = _Conv(self, net.conv_before_upsample[0], nf, self.Cp, wr=self.conv_wr)
             self.ups = []
             # split_act: a0 / the upsampled activations are stored as [hi | lo] pairs (128 channels), read by
             # the upsampling convs through weights tied over both halves (the halo kernel skips lo . lo)
@@ -716,9 +723,14 @@ class SwinIREngine:
             tl = P["tail_ld"]
             lo = (lambda t: t[:, 64:]) if sa else (lambda t: None)   # the lo half of a pair buffer
             c = self.cbu
-            H.gemm_nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
-                      H.epilogue(P["a0"], ldo=tl, bias=c.bp, act=H.ACT_LEAKY, slope=0.01, out_lo=lo(P["a0"])), M, 64,
-                      9 * Cp, cd)
+            if (c.wr_n64 and self.conv_wr and H.conv3x3_wr_tile(1, B, Hh, Ww, Cp, 64) == 96 and
+                    M // 96 >= self.conv_wr_min_tiles):
+                H.conv3x3_wr(P["fb"], Cp, 0, c.Wc15, c.bp, None, P["a0"], B, Hh, Ww, Cp, 64, ldo=tl, split=True,
+                             out_lo=lo(P["a0"]), act=H.ACT_LEAKY, slope=0.01)
+            else:
+                H.gemm_nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
+                          H.epilogue(P["a0"], ldo=tl, bias=c.bp, act=H.ACT_LEAKY, slope=0.01, out_lo=lo(P["a0"])), M, 64,
+                          9 * Cp, cd)
             src, h, w = P["a0"], Hh, Ww
             for c, r, dst in zip(self.ups, self.ups_r, P["ups_act"]):
                 if (c.wr_pair and self.conv_wr and H.conv3x3_wr_tile(1, B, h, w, 64, c.Co) == 96 and

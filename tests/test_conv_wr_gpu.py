@@ -116,6 +116,29 @@ def test_conv_wr_pair_pshuf(hw):
     assert rel_err(got, ref) < 3e-5
 
 
+def test_conv_wr_cbu_leaky_pair():
+    """conv_before_upsample (network_swinir.py:742) under split activations: fp32 image of 180 channels
+    (padded 192), 180 -> 64 with split weights (kind 15, Np = 64), LeakyReLU(0.01), stored as a bf16
+    [hi | lo] pair (out_lo) -> ~2^-16 of fp64."""
+    B, Hh, Ww, C, N = 2, 48, 48, 180, 64
+    g = torch.Generator().manual_seed(44)
+    x = torch.randn(B, C, Hh, Ww, generator=g)
+    w = torch.randn(N, C, 3, 3, generator=g) * 0.05
+    b = torch.randn(N, generator=g) * 0.1
+    ref = F.leaky_relu(F.conv2d(x.double(), w.double(), b.double(), padding=1), 0.01)
+    M = B * Hh * Ww
+    xin = torch.zeros(M, 192)
+    xin[:, :C] = x.permute(0, 2, 3, 1).reshape(M, C)
+    Wc = torch.empty(64 * 2 * 9 * 192, device=dev, dtype=torch.bfloat16)
+    H.pack_weight(w.to(dev), Wc, H.wmap(15, N, C, (1, N, 64), (1, C, 192)))
+    out = torch.full((M, 128), float("nan"), device=dev, dtype=torch.bfloat16)
+    H.conv3x3_wr(xin.to(dev), 192, 0, Wc, b.to(dev), None, out, B, Hh, Ww, 192, N, ldo=128, split=True,
+                 out_lo=out[:, 64:], act=H.ACT_LEAKY, slope=0.01)
+    torch.cuda.synchronize()
+    got = (out[:, :64].double() + out[:, 64:].double()).cpu().view(B, Hh, Ww, N).permute(0, 3, 1, 2)
+    assert rel_err(got, ref) < 3e-5
+
+
 def test_conv_wr_rejects():
     x = torch.zeros(2 * 48 * 48, 192, device=dev)
     w = torch.zeros(192 * 2 * 9 * 192, device=dev, dtype=torch.bfloat16)
