@@ -372,11 +372,14 @@ int kair_conv3x3_wr(const void* x, int x_dtype, long ldx, int split, int flip, c
  * n_blocks 16) and a PixelShuffle(ps_r) sub-pixel-major store (packed column n = (i r + j) N/r^2 + c ->
  * pixel (y r + i, x r + j), channel c; ldo = the shuffled rows' stride) with, for a bf16 output, the lo
  * plane bf16(v - bf16(v)) at the same offsets from out_lo (a pair output for the next split conv).  N <= 64
- * (n_blocks 4, split, row output: conv_before_upsample) with act KAIR_ACT_LEAKY(slope) and out_lo. */
+ * (n_blocks 4, split, row output: conv_before_upsample) with act KAIR_ACT_LEAKY(slope) and out_lo.  The
+ * upsampling convs' input gradients: plain bf16 image of C <= 256 channels, N <= 64, with ps_r < 0 a
+ * PixelUnshuffle(-ps_r) store into the previous conv's pre-shuffle rows (KAIR_OUT_PUNSHUF_SPM layout) or a
+ * LeakyReLU' gate (gate bf16 rows, ldg; v *= gate > 0 ? 1 : slope). */
 int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int split, int flip, const void* w, int n_blocks,
                        const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo, void* out_lo,
-                       int ps_r, int act, float slope, void* acopy, long ldac, int acones, int B, int H, int W, int C,
-                       int N, void* stream);
+                       int ps_r, int act, float slope, const void* gate, long ldg, void* acopy, long ldac, int acones,
+                       int B, int H, int W, int C, int N, void* stream);
 
 /* Narrow-output 3x3 convs (csrc/tail.hip): a 64-channel NHWC bf16 image <-> NR <= 4 output channels,
  * the last conv of the reconstruction head (network_swinir.py:745, :817 conv_last).

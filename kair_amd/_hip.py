@@ -130,7 +130,8 @@ _SIGS = {
     "kair_conv3x3_wr": [c_vp, c_int, c_long, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_long, c_vp, c_int, c_long, c_vp,
                         c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "kair_conv3x3_wr_ex": [c_vp, c_int, c_long, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_long, c_vp, c_int, c_long, c_vp,
-                           c_int, c_int, c_float, c_vp, c_long, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+                           c_int, c_int, c_float, c_vp, c_long, c_vp, c_long, c_int, c_int, c_int, c_int, c_int, c_int,
+                           c_vp],
     "kair_conv3x3_narrow_dgrad_ws": [],
     "kair_conv3x3_narrow_dgrad": [c_vp, c_long, c_vp, c_int, c_vp, c_vp, c_int, c_long, c_int, c_int, c_int, c_int, c_vp],
     "kair_conv3x3_narrow_wgrad_ws": [c_int],
@@ -552,11 +553,12 @@ def conv3x3_wr_tile(split, B, H, W, C, N):
 
 
 def conv3x3_wr(x, ldx, flip, w, bias, resid, out, B, H, W, C, N, ldr=None, ldo=None, acopy=None, ldac=None, acones=-1,
-               n_blocks=None, split=None, out_lo=None, ps_r=0, act=ACT_NONE, slope=0.0):
+               n_blocks=None, split=None, out_lo=None, ps_r=0, act=ACT_NONE, slope=0.0, gate=None, ldg=None):
     """3x3 conv with register-streamed weights (csrc/conv_wr.hip, kair_conv3x3_wr_ex).  split (default: x
     fp32): two halos -- split activations of an fp32 image, or a bf16 [hi | lo] pair image of C channels
     per half -- with w = pack kind 15; else one bf16 product with w = pack kind 16 (flip = 1: input
-    gradient).  ps_r > 0: PixelShuffle sub-pixel-major store (+ out_lo: the lo plane of a bf16 pair)."""
+    gradient).  ps_r > 0: PixelShuffle sub-pixel-major store (+ out_lo: the lo plane of a bf16 pair); ps_r < 0:
+    PixelUnshuffle(-ps_r) store; gate: LeakyReLU'(gate) (slope) on the rows."""
     if split is None:
         split = x.dtype == torch.float32
     if n_blocks is None:
@@ -564,7 +566,8 @@ def conv3x3_wr(x, ldx, flip, w, bias, resid, out, B, H, W, C, N, ldr=None, ldo=N
     check(lib().kair_conv3x3_wr_ex(ptr(x), dtype_code(x), ldx, int(bool(split)), int(flip), ptr(w), n_blocks, ptr(bias),
                                    ptr(resid), ldr if ldr is not None else (resid.shape[-1] if resid is not None else 0),
                                    ptr(out), dtype_code(out), ldo if ldo is not None else out.shape[-1], ptr(out_lo), ps_r,
-                                   act, slope, ptr(acopy), ldac if ldac is not None else (acopy.shape[-1] if acopy is not None else 0),
+                                   act, slope, ptr(gate), ldg if ldg is not None else (gate.shape[-1] if gate is not None else 0),
+                                   ptr(acopy), ldac if ldac is not None else (acopy.shape[-1] if acopy is not None else 0),
                                    acones, B, H, W, C, N, stream_ptr()), "conv3x3_wr")
 
 

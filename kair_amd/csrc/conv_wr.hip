@@ -39,6 +39,8 @@ struct ConvWrArgs {
   bf16* out_lo;                      // pair output: bf16(v - bf16(v)) at the same offsets (bf16 out only)
   int ps_r;                          // > 0: PixelShuffle(ps_r) sub-pixel-major output (n = (i r + j) nf + c)
   int act; float slope;              // KAIR_ACT_LEAKY: LeakyReLU(slope) before the store (no residual)
+  const bf16* gate; long ldg;        // v *= (gate[m][n] > 0 ? 1 : slope): LeakyReLU' of a stored activation (rows)
+  int psH, psW;                      // EM 2: the pre-shuffle grid (H / r, W / r) of the PixelUnshuffle store
   int B, H, W, C, N, flip;
   long tilesM;
   FDiv fc8, fhwd;                    // C / 8 and the halo row width (magic-number divisions)
@@ -52,8 +54,9 @@ template <bool SPLIT> struct WrGeom {
 
 // SPLIT with an fp32 image: lo formed in the halo fill; SPLIT with a bf16 image ("pair"): the image rows
 // are [hi | lo] halves of C channels each (the split tail's activations), read into the two halos.
-// RN: 16-wide output fragments per wave (3: N <= 192, 4: N <= 256).  EM 1: PixelShuffle sub-pixel-major
-// store (+ the lo plane of a bf16 pair output).
+// RN: 16-wide output fragments per wave (1: N <= 64, 3: N <= 192, 4: N <= 256).  EM 1: PixelShuffle
+// sub-pixel-major store (+ the lo plane of a bf16 pair output); EM 2: its inverse, PixelUnshuffle (an
+// upsampling conv's input gradient into the previous conv's pre-shuffle rows).
 template <typename TX, bool SPLIT, int BM, bool RESID, int RN, int EM>
 __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a) {
   constexpr bool PAIR = SPLIT && sizeof(TX) == 2;
@@ -245,12 +248,22 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : v[q] * a.slope;
         }
+        if (a.gate) {
+          const bf16x4 gv = *(const bf16x4*)(a.gate + m * a.ldg + n);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] *= (float)gv[q] > 0.f ? 1.f : a.slope;
+        }
         long o = m * a.ldo + n;
         if constexpr (EM == 1) {   // sub-pixel-major columns: n = (i r + j) nf + c -> pixel (y r + i, x r + j)
           const int r = a.ps_r, nf = a.N / (r * r);
           const int bi = (int)(m / ((long)H * W)), pp = (int)(m - (long)bi * H * W), yy = pp / W, xx = pp - yy * W;
           const int sp = n / nf, cc = n - sp * nf, ii = sp / r, jj = sp - ii * r;
           o = (((long)bi * H * r + (long)yy * r + ii) * ((long)W * r) + (long)xx * r + jj) * a.ldo + cc;
+        } else if constexpr (EM == 2) {   // pixel (y, x) -> pre-shuffle row (y / r, x / r), column (i r + j) N + n
+          const int r = a.ps_r;
+          const int bi = (int)(m / ((long)H * W)), pp = (int)(m - (long)bi * H * W), yy = pp / W, xx = pp - yy * W;
+          const int yl = yy / r, xl = xx / r;
+          o = (((long)bi * a.psH + yl) * a.psW + xl) * a.ldo + ((yy - yl * r) * r + (xx - xl * r)) * a.N + n;
         }
         if (a.odt == KAIR_BF16) {
           const bf16x4 hv = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
@@ -294,8 +307,8 @@ bool wr_geometry(int BM, int halo, long M, int H, int W, int C) {
  * two halos (split activations, fp32 image, or a bf16 [hi | lo] pair image of C channels per half). */
 extern "C" int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N) {
   const long M = (long)B * H * W;
-  if (C <= 0 || C > 192 || C % 64 != 0 || N <= 0 || N > 256 || N % 4 != 0) return 0;
-  if (split) return wr_geometry(96, WrGeom<true>::HALO, M, H, W, C) ? 96 : 0;
+  if (C <= 0 || C > 256 || C % 64 != 0 || N <= 0 || N > 256 || N % 4 != 0) return 0;
+  if (split) return C <= 192 && wr_geometry(96, WrGeom<true>::HALO, M, H, W, C) ? 96 : 0;
   if (N > 192) return 0;
   if (wr_geometry(144, WrGeom<false>::HALO, M, H, W, C)) return 144;
   return wr_geometry(96, WrGeom<false>::HALO, M, H, W, C) ? 96 : 0;
@@ -306,8 +319,8 @@ extern "C" int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N
 
 extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int split, int flip, const void* w, int n_blocks,
                                   const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo,
-                                  void* out_lo, int ps_r, int act, float slope, void* acopy, long ldac, int acones, int B,
-                                  int H, int W, int C, int N, void* stream) {
+                                  void* out_lo, int ps_r, int act, float slope, const void* gate, long ldg, void* acopy,
+                                  long ldac, int acones, int B, int H, int W, int C, int N, void* stream) {
   KAIR_CHECK_ARG(x && w && out && B > 0, "conv3x3_wr: null operand");
   KAIR_CHECK_ARG(x_dtype == KAIR_F32 || x_dtype == KAIR_BF16, "conv3x3_wr: image dtype");
   KAIR_CHECK_ARG(out_dtype == KAIR_F32 || out_dtype == KAIR_BF16, "conv3x3_wr: output dtype");
@@ -320,9 +333,15 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
   KAIR_CHECK_ARG(ldx >= (pair ? 2 * C : C) && ldx % (x_dtype == KAIR_F32 ? 4 : 8) == 0 && ((uintptr_t)x & 15) == 0 &&
                      ((uintptr_t)w & 15) == 0,
                  "conv3x3_wr: image rows 16-byte aligned, ldx >= C (2 C for a [hi | lo] pair)");
-  KAIR_CHECK_ARG(ps_r >= 0 && (ps_r == 0 || (N % (ps_r * ps_r) == 0 && (N / (ps_r * ps_r)) % 4 == 0 && !resid)),
+  // ps_r > 0: PixelShuffle store of a split / pair conv; ps_r < 0: PixelUnshuffle(-ps_r) store of a plain one
+  const int pr = ps_r < 0 ? -ps_r : ps_r;
+  KAIR_CHECK_ARG(ps_r <= 0 || (N % (pr * pr) == 0 && (N / (pr * pr)) % 4 == 0 && !resid),
                  "conv3x3_wr: PixelShuffle output needs N %% r^2 == 0, N / r^2 %% 4 == 0 and no residual");
-  KAIR_CHECK_ARG(ldo >= (ps_r ? N / (ps_r * ps_r) : N) && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0, "conv3x3_wr: output rows");
+  KAIR_CHECK_ARG(ps_r >= 0 || (H % pr == 0 && W % pr == 0 && !resid && ldo >= (long)N * pr * pr),
+                 "conv3x3_wr: PixelUnshuffle output needs H, W multiples of r, ldo >= N r^2, no residual");
+  KAIR_CHECK_ARG(ldo >= (ps_r > 0 ? N / (pr * pr) : N) && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0, "conv3x3_wr: output rows");
+  KAIR_CHECK_ARG(!gate || (ps_r == 0 && !resid && ldg >= N && ldg % 4 == 0 && ((uintptr_t)gate & 7) == 0),
+                 "conv3x3_wr: a gate needs a row output, no residual, 8-byte aligned bf16 rows");
   KAIR_CHECK_ARG(!out_lo || (out_dtype == KAIR_BF16 && ((uintptr_t)out_lo & 7) == 0), "conv3x3_wr: out_lo needs a bf16 output");
   KAIR_CHECK_ARG(!resid || (ldr >= N && ldr % 4 == 0 && ((uintptr_t)resid & 15) == 0), "conv3x3_wr: residual rows");
   KAIR_CHECK_ARG(!bias || ((uintptr_t)bias & 15) == 0, "conv3x3_wr: bias alignment");
@@ -332,8 +351,11 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
   ConvWrArgs a;
   a.x = x; a.ldx = ldx; a.w = (const bf16*)w; a.bias = bias; a.resid = resid; a.ldr = ldr;
   a.out = out; a.odt = out_dtype; a.ldo = ldo; a.acopy = (bf16*)acopy; a.ldac = ldac; a.acones = acopy ? acones : -1;
-  a.out_lo = (bf16*)out_lo; a.ps_r = ps_r;
-  KAIR_CHECK_ARG(act == KAIR_ACT_NONE || (act == KAIR_ACT_LEAKY && !resid), "conv3x3_wr: act none, or LeakyReLU without residual");
+  a.out_lo = (bf16*)out_lo; a.ps_r = pr;
+  a.gate = (const bf16*)gate; a.ldg = ldg;
+  a.psH = pr ? H / pr : 0; a.psW = pr ? W / pr : 0;
+  KAIR_CHECK_ARG(act == KAIR_ACT_NONE || (act == KAIR_ACT_LEAKY && !resid && !gate),
+                 "conv3x3_wr: act none, or LeakyReLU without residual / gate");
   a.act = act; a.slope = slope;
   a.B = B; a.H = H; a.W = W; a.C = C; a.N = N; a.flip = flip;
   a.tilesM = M / BM;
@@ -346,6 +368,10 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
   if (pair) {   // the SwinIR x4 upsampling convs: [hi | lo] pair in, PixelShuffle [hi | lo] pair out
     KAIR_CHECK_ARG(RN == 4 && ps_r > 0 && !rs, "conv3x3_wr: the pair form is built for N in (192, 256] with a PixelShuffle store");
     KAIR_WR(bf16, true, 96, false, 4, 1);
+  } else if (RN == 1 && !split) {   // the upsampling convs' input gradients (256 -> 64): unshuffled or gated rows
+    KAIR_CHECK_ARG(x_dtype == KAIR_BF16 && ps_r <= 0 && !rs, "conv3x3_wr: the plain N <= 64 form takes a bf16 image");
+    if (BM == 144) { if (ps_r < 0) KAIR_WR(bf16, false, 144, false, 1, 2); else KAIR_WR(bf16, false, 144, false, 1, 0); }
+    else { if (ps_r < 0) KAIR_WR(bf16, false, 96, false, 1, 2); else KAIR_WR(bf16, false, 96, false, 1, 0); }
   } else if (RN == 1) {   // conv_before_upsample (192 -> 64): split, row output (+ LeakyReLU, + lo plane)
     KAIR_CHECK_ARG(split && x_dtype == KAIR_F32 && ps_r == 0, "conv3x3_wr: the N <= 64 form takes an fp32 image, split, rows");
     if (rs) KAIR_WR(float, true, 96, true, 1, 0); else KAIR_WR(float, true, 96, false, 1, 0);
@@ -370,5 +396,5 @@ extern "C" int kair_conv3x3_wr(const void* x, int x_dtype, long ldx, int split, 
                                const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo, void* acopy,
                                long ldac, int acones, int B, int H, int W, int C, int N, void* stream) {
   return kair_conv3x3_wr_ex(x, x_dtype, ldx, split, flip, w, n_blocks, bias, resid, ldr, out, out_dtype, ldo, nullptr, 0,
-                            KAIR_ACT_NONE, 0.f, acopy, ldac, acones, B, H, W, C, N, stream);
+                            KAIR_ACT_NONE, 0.f, nullptr, 0, acopy, ldac, acones, B, H, W, C, N, stream);
 }

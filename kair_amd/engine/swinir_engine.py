@@ -163,14 +163,18 @@ class _Conv:
         self.wr = bool(wr) and Cop == 192 and Cip == 192 and self.split
         # wr_pair: an upsampling conv (64 -> 256, sub-pixel-major rows) reading a [hi | lo] pair image
         self.wr_pair = bool(wr) and not self.wr and tied_in and Cip == 64 and fcip == 128 and Cop == 256 and self.split
-        if self.wr_pair:
+        if self.wr_pair:   # + its input-gradient form (kind 16, rows = the 64 input channels)
             self.mapp = H.wmap(15, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
             self.Wp15 = torch.empty(Cop * 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
+            self.mapp16 = H.wmap(16, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
+            self.Wp16 = torch.empty(Cip * 9 * Cop, device=dev, dtype=torch.bfloat16)
         # wr_n64: conv_before_upsample (192 -> 64) on kair_conv3x3_wr's N <= 64 form
         self.wr_n64 = bool(wr) and not self.wr and not self.wr_pair and Cop == 64 and Cip == 192 and self.split and not tied_in
         if self.wr_n64:
             self.mapc = H.wmap(15, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
             self.Wc15 = torch.empty(Cop * 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
+            self.mapc16 = H.wmap(16, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
+            self.Wc16 = torch.empty(Cip * 9 * Cop, device=dev, dtype=torch.bfloat16)
         if self.wr:
             self.map15 = H.wmap(15, Co, Ci, (1, Co, Cop), (1, Ci, Cip))
             self.Wf15 = torch.empty(Cop * 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
@@ -191,9 +195,9 @@ class _Conv:
         if self.wr:
             jobs += [(w, self.Wf15, self.map15), (w, self.Wd16, self.map16)]
         if self.wr_pair:
-            jobs.append((w, self.Wp15, self.mapp))
+            jobs += [(w, self.Wp15, self.mapp), (w, self.Wp16, self.mapp16)]
         if self.wr_n64:
-            jobs.append((w, self.Wc15, self.mapc))
+            jobs += [(w, self.Wc15, self.mapc), (w, self.Wc16, self.mapc16)]
         return jobs
 
 
@@ -922,7 +926,16 @@ class SwinIREngine:
                 h, w = h // r, w // r
                 dpre = P["dpre"][i]
                 src = P["ups_act"][i - 1] if i > 0 else P["a0"]
-                if i > 0:
+                wr_d = (c.wr_pair and self.conv_wr and H.conv3x3_wr_tile(0, B, h, w, c.Co, 64) > 0 and
+                        B * h * w // 96 >= self.conv_wr_min_tiles)
+                if wr_d and i > 0:   # kair_conv3x3_wr: PixelUnshuffle store into the previous conv's pre-shuffle rows
+                    rp = self.ups_r[i - 1]
+                    H.conv3x3_wr(dpre, c.Co, 1, c.Wp16, None, None, P["dpre"][i - 1], B, h, w, c.Co, 64,
+                                 ldo=self.ups[i - 1].Co, split=False, ps_r=-rp)
+                elif wr_d:           # ... or the LeakyReLU'(a0) gate of conv_before_upsample's output
+                    H.conv3x3_wr(dpre, c.Co, 1, c.Wp16, None, None, P["da0"], B, h, w, c.Co, 64, split=False,
+                                 gate=P["a0"], ldg=tl, slope=0.01)
+                elif i > 0:
                     rp = self.ups_r[i - 1]
                     H.gemm_nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),
                               H.epilogue(P["dpre"][i - 1], mode=H.OUT_PUNSHUF_SPM, ldo=self.ups[i - 1].Co,
@@ -934,7 +947,11 @@ class SwinIREngine:
                 self._wgrad(P, H.rows(dpre), H.im2col(src, h, w, 64, ld=tl), B * h * w, c.Co, 9 * 64, c.map, g(c.w))
                 self._bias_colsum(P, H.rows(dpre), B * h * w, c.Co, c.mapb, g(c.b))
             c = self.cbu
-            H.gemm_nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)
+            if (c.wr_n64 and self.conv_wr and H.conv3x3_wr_tile(0, B, Hh, Ww, 64, Cp) > 0 and
+                    M // 96 >= self.conv_wr_min_tiles):
+                H.conv3x3_wr(P["da0"], 64, 1, c.Wc16, None, None, P["dfb"], B, Hh, Ww, 64, Cp, split=False)
+            else:
+                H.gemm_nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)
             self._wgrad(P, H.rows(P["da0"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, 64, 9 * Cp, c.map,
                         g(c.w), g(c.b), self.C)
         elif self.upsampler == "nearest+conv":

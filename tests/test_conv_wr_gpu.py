@@ -139,6 +139,39 @@ def test_conv_wr_cbu_leaky_pair():
     assert rel_err(got, ref) < 3e-5
 
 
+@pytest.mark.parametrize("mode,hw", [("punshuf", (24, 96)), ("gate", (24, 48)), ("punshuf", (48, 48))])
+def test_conv_wr_ups_dgrad(mode, hw):
+    """The upsampling convs' input gradients (network_swinir.py:584 Upsample, its backward): the 256-channel
+    pre-shuffle gradient (bf16) through kind-16 weights (rows = the 64 input channels, columns
+    sub-pixel-major), stored PixelUnshuffle(2)-ed into the previous conv's pre-shuffle rows, or gated
+    by LeakyReLU'(a0) of the stored [hi | lo] activation -- vs fp64 conv_transpose2d."""
+    B, C, N = 2, 256, 64
+    Hh, Ww = hw
+    g = torch.Generator().manual_seed(31 + Hh)
+    x = torch.randn(B, C, Hh, Ww, generator=g).bfloat16().float()
+    w = (torch.randn(C, N, 3, 3, generator=g) * 0.03).bfloat16().float()   # forward conv N -> C
+    ref = F.conv_transpose2d(x.double(), w.double(), padding=1)            # [B, N, H, W]
+    M = B * Hh * Ww
+    xin = x.permute(0, 2, 3, 1).contiguous().view(M, C).to(dev, torch.bfloat16)
+    Wd = torch.empty(N * 9 * C, device=dev, dtype=torch.bfloat16)
+    H.pack_weight(w.to(dev), Wd, H.wmap(16, C, N, (1, C, C), (1, N, N)))
+    if mode == "punshuf":
+        r = 2
+        out = torch.full((M // (r * r), r * r * N), float("nan"), device=dev, dtype=torch.bfloat16)
+        H.conv3x3_wr(xin, C, 1, Wd, None, None, out, B, Hh, Ww, C, N, ldo=r * r * N, split=False, ps_r=-r)
+        torch.cuda.synchronize()
+        got = out.float().cpu().view(B, Hh // r, Ww // r, r, r, N).permute(0, 5, 1, 3, 2, 4).reshape(B, N, Hh, Ww)
+    else:
+        gate = torch.randn(M, 128, generator=g).bfloat16()
+        out = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+        H.conv3x3_wr(xin, C, 1, Wd, None, None, out, B, Hh, Ww, C, N, split=False, gate=gate.to(dev), ldg=128, slope=0.01)
+        torch.cuda.synchronize()
+        got = out.float().cpu().view(B, Hh, Ww, N).permute(0, 3, 1, 2)
+        gs = torch.where(gate[:, :N].float() > 0, 1.0, 0.01).view(B, Hh, Ww, N).permute(0, 3, 1, 2)
+        ref = ref * gs.double()
+    assert rel_err(got, ref) < 4e-3   # bf16 output
+
+
 def test_conv_wr_rejects():
     x = torch.zeros(2 * 48 * 48, 192, device=dev)
     w = torch.zeros(192 * 2 * 9 * 192, device=dev, dtype=torch.bfloat16)
