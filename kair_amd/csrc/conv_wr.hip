@@ -27,7 +27,12 @@ namespace {
 
 constexpr int WR_WAVES = 4;          // one per SIMD
 constexpr int WR_NT = 64 * WR_WAVES;
-constexpr int WR_PD = 3;             // k-steps of weight fragments in flight
+// k-steps of weight fragments in flight: 3 where a k-step is 18+ MFMAs per wave, 9 for the narrow
+// (RN = 1) forms whose k-step is 6-18 MFMAs (~100-300 cycles: three steps would not cover an L2 hit)
+// (6 for the split N <= 64 form: 18 MFMAs per step, and the registers of 9 spill)
+template <int RN, bool SPLIT> struct WrPD {
+  static constexpr int PD = RN != 1 ? 3 : SPLIT ? 6 : 9, UNR = RN == 1 && !SPLIT ? 18 : 6;
+};
 
 struct ConvWrArgs {
   const void* x; long ldx;           // NHWC image rows: fp32 (split) or bf16
@@ -90,7 +95,8 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
     bias4[rn] = a.bias && n < a.N ? *(const float4*)(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
-  bf16x8 rb[WR_PD][RN][NB];        // weight ring
+  constexpr int PD = WrPD<RN, SPLIT>::PD, UNR = WrPD<RN, SPLIT>::UNR;   // UNR: lcm(PD, 2); KS = 18 C / 64 is a multiple
+  bf16x8 rb[PD][RN][NB];           // weight ring
   auto issue_w = [&](int slot, int s) {
 #pragma unroll
     for (int rn = 0; rn < RN; ++rn)
@@ -118,7 +124,7 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
     const int y0 = rem / W, x0 = rem - (rem / W) * W;
     // the first k-steps' weights in flight under the halo fill
 #pragma unroll
-    for (int u = 0; u < WR_PD; ++u) issue_w(u, u);
+    for (int u = 0; u < PD; ++u) issue_w(u, u);
     __syncthreads();   // every wave is done with the previous tile's halo
     {
       // pieces per thread in one batch of loads (all issued, then landed, then written): the whole
@@ -206,13 +212,13 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
       }
     };
     read_a(0, 0);
-    // k-loop, unrolled by 6 (the weight ring is 3 deep, the activation buffers 2): KS % 6 == 0 (host).
+    // k-loop, unrolled by UNR (the weight ring is PD deep, the activation buffers 2): KS % UNR == 0.
     // Every load is unconditional (the last steps re-read step KS - 1): a load on only some paths makes
     // the compiler's wait at the merge the minimum over the paths (vmcnt / lgkmcnt 0 every step).
     auto step = [&](int u, int s, bool tail) {
-      const int ab = u & 1, ws = u % WR_PD;
+      const int ab = u & 1, ws = u % PD;
       read_a(ab ^ 1, s + 1 < KS ? s + 1 : KS - 1);
-      if (RESID && tail && u == 3) load_resid();
+      if (RESID && tail && u == UNR - 3) load_resid();
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -223,14 +229,14 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
             acc[i][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[ws][rn][0], ra[ab][i][1], acc[i][rn], 0, 0, 0);
           }
         }
-      issue_w(ws, s + WR_PD < KS ? s + WR_PD : KS - 1);
+      issue_w(ws, s + PD < KS ? s + PD : KS - 1);
     };
-    for (int s0 = 0; s0 < KS - 6; s0 += 6) {
+    for (int s0 = 0; s0 < KS - UNR; s0 += UNR) {
 #pragma unroll
-      for (int u = 0; u < 6; ++u) step(u, s0 + u, false);
+      for (int u = 0; u < UNR; ++u) step(u, s0 + u, false);
     }
 #pragma unroll
-    for (int u = 0; u < 6; ++u) step(u, KS - 6 + u, true);
+    for (int u = 0; u < UNR; ++u) step(u, KS - UNR + u, true);
     // epilogue: 4 consecutive channels of one pixel per lane
 #pragma unroll
     for (int i = 0; i < RM; ++i)
@@ -308,10 +314,23 @@ bool wr_geometry(int BM, int halo, long M, int H, int W, int C) {
 extern "C" int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N) {
   const long M = (long)B * H * W;
   if (C <= 0 || C > 256 || C % 64 != 0 || N <= 0 || N > 256 || N % 4 != 0) return 0;
-  if (split) return C <= 192 && wr_geometry(96, WrGeom<true>::HALO, M, H, W, C) ? 96 : 0;
-  if (N > 192) return 0;
-  if (wr_geometry(144, WrGeom<false>::HALO, M, H, W, C)) return 144;
-  return wr_geometry(96, WrGeom<false>::HALO, M, H, W, C) ? 96 : 0;
+  if (split && C > 192) return 0;
+  if (!split && N > 192) return 0;
+  // the largest tile that still gives >= 3/4 of a workgroup per CU, else the smallest that fits: at
+  // B = 4 (M = 9,216) 48-pixel tiles put 192 workgroups on the chip instead of 96 / 64
+  static const int cand_split[] = {96, 48}, cand_plain[] = {144, 96, 48};
+  const int* cand = split ? cand_split : cand_plain;
+  const int nc = split ? 2 : 3;
+  const long want = 3L * wr_num_cus() / 4;
+  int best = 0;
+  for (int i = 0; i < nc; ++i) {
+    const int bm = cand[i];
+    if (!(split ? wr_geometry(bm, WrGeom<true>::HALO, M, H, W, C) : wr_geometry(bm, WrGeom<false>::HALO, M, H, W, C)))
+      continue;
+    best = bm;
+    if (M / bm >= want) return bm;
+  }
+  return best;
 }
 
 #define KAIR_WR(TXV, SPV, BMV, RV, RNV, EMV) \
@@ -365,28 +384,32 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
   const int grid = (int)(a.tilesM < ncu ? a.tilesM : ncu);
   hipStream_t s = (hipStream_t)stream;
   const bool rs = resid != nullptr;
+#define KAIR_WR3(TXV, SPV, RV, RNV, EMV)                                                   \
+  do {                                                                                     \
+    if (BM == 48) KAIR_WR(TXV, SPV, 48, RV, RNV, EMV);                                     \
+    else if (BM == 96) KAIR_WR(TXV, SPV, 96, RV, RNV, EMV);                                \
+    else if constexpr (!SPV) KAIR_WR(TXV, SPV, 144, RV, RNV, EMV);                         \
+  } while (0)
   if (pair) {   // the SwinIR x4 upsampling convs: [hi | lo] pair in, PixelShuffle [hi | lo] pair out
     KAIR_CHECK_ARG(RN == 4 && ps_r > 0 && !rs, "conv3x3_wr: the pair form is built for N in (192, 256] with a PixelShuffle store");
-    KAIR_WR(bf16, true, 96, false, 4, 1);
+    KAIR_WR3(bf16, true, false, 4, 1);
   } else if (RN == 1 && !split) {   // the upsampling convs' input gradients (256 -> 64): unshuffled or gated rows
     KAIR_CHECK_ARG(x_dtype == KAIR_BF16 && ps_r <= 0 && !rs, "conv3x3_wr: the plain N <= 64 form takes a bf16 image");
-    if (BM == 144) { if (ps_r < 0) KAIR_WR(bf16, false, 144, false, 1, 2); else KAIR_WR(bf16, false, 144, false, 1, 0); }
-    else { if (ps_r < 0) KAIR_WR(bf16, false, 96, false, 1, 2); else KAIR_WR(bf16, false, 96, false, 1, 0); }
+    if (ps_r < 0) KAIR_WR3(bf16, false, false, 1, 2); else KAIR_WR3(bf16, false, false, 1, 0);
   } else if (RN == 1) {   // conv_before_upsample (192 -> 64): split, row output (+ LeakyReLU, + lo plane)
     KAIR_CHECK_ARG(split && x_dtype == KAIR_F32 && ps_r == 0, "conv3x3_wr: the N <= 64 form takes an fp32 image, split, rows");
-    if (rs) KAIR_WR(float, true, 96, true, 1, 0); else KAIR_WR(float, true, 96, false, 1, 0);
+    if (rs) KAIR_WR3(float, true, true, 1, 0); else KAIR_WR3(float, true, false, 1, 0);
   } else {
     KAIR_CHECK_ARG(RN == 3 && ps_r == 0, "conv3x3_wr: N <= 192 row outputs for this form");
     if (split) {
-      if (rs) KAIR_WR(float, true, 96, true, 3, 0); else KAIR_WR(float, true, 96, false, 3, 0);
+      if (rs) KAIR_WR3(float, true, true, 3, 0); else KAIR_WR3(float, true, false, 3, 0);
     } else if (x_dtype == KAIR_F32) {
-      if (BM == 144) { if (rs) KAIR_WR(float, false, 144, true, 3, 0); else KAIR_WR(float, false, 144, false, 3, 0); }
-      else { if (rs) KAIR_WR(float, false, 96, true, 3, 0); else KAIR_WR(float, false, 96, false, 3, 0); }
+      if (rs) KAIR_WR3(float, false, true, 3, 0); else KAIR_WR3(float, false, false, 3, 0);
     } else {
-      if (BM == 144) { if (rs) KAIR_WR(bf16, false, 144, true, 3, 0); else KAIR_WR(bf16, false, 144, false, 3, 0); }
-      else { if (rs) KAIR_WR(bf16, false, 96, true, 3, 0); else KAIR_WR(bf16, false, 96, false, 3, 0); }
+      if (rs) KAIR_WR3(bf16, false, true, 3, 0); else KAIR_WR3(bf16, false, false, 3, 0);
     }
   }
+#undef KAIR_WR3
 #undef KAIR_WR
   KAIR_CHECK_LAUNCH();
   return 0;

@@ -566,7 +566,7 @@ class SwinIREngine:
             P["conv_halo"] = H.conv_halo_geometry(Hh, Ww, Cp, M, Cp)
             # the register-streamed-weight conv: one 96-pixel tile per workgroup per CU round, so only with
             # at least a full round of tiles (B = 32: 768 tiles; B = 4: 96 -> the halo kernel's N tiles)
-            P["conv_wr"] = bool(self.conv_wr and H.conv3x3_wr_tile(1, B, Hh, Ww, Cp, Cp) == 96 and
+            P["conv_wr"] = bool(self.conv_wr and H.conv3x3_wr_tile(1, B, Hh, Ww, Cp, Cp) > 0 and
                                 H.conv3x3_wr_tile(0, B, Hh, Ww, Cp, Cp) > 0 and M // 96 >= self.conv_wr_min_tiles)
             if P["conv_wr"]:
                 P["conv_halo"] = True   # the wr kernel leaves the same bf16 copies
@@ -727,7 +727,7 @@ class SwinIREngine:
             tl = P["tail_ld"]
             lo = (lambda t: t[:, 64:]) if sa else (lambda t: None)   # the lo half of a pair buffer
             c = self.cbu
-            if (c.wr_n64 and self.conv_wr and H.conv3x3_wr_tile(1, B, Hh, Ww, Cp, 64) == 96 and
+            if (c.wr_n64 and self.conv_wr and H.conv3x3_wr_tile(1, B, Hh, Ww, Cp, 64) > 0 and
                     M // 96 >= self.conv_wr_min_tiles):
                 H.conv3x3_wr(P["fb"], Cp, 0, c.Wc15, c.bp, None, P["a0"], B, Hh, Ww, Cp, 64, ldo=tl, split=True,
                              out_lo=lo(P["a0"]), act=H.ACT_LEAKY, slope=0.01)
@@ -737,7 +737,7 @@ class SwinIREngine:
                           9 * Cp, cd)
             src, h, w = P["a0"], Hh, Ww
             for c, r, dst in zip(self.ups, self.ups_r, P["ups_act"]):
-                if (c.wr_pair and self.conv_wr and H.conv3x3_wr_tile(1, B, h, w, 64, c.Co) == 96 and
+                if (c.wr_pair and self.conv_wr and H.conv3x3_wr_tile(1, B, h, w, 64, c.Co) > 0 and
                         B * h * w // 96 >= self.conv_wr_min_tiles):   # kair_conv3x3_wr, pair form
                     H.conv3x3_wr(src, tl, 0, c.Wp15, c.bp, None, dst, B, h, w, 64, c.Co, ldo=tl, split=True,
                                  out_lo=lo(dst), ps_r=r)

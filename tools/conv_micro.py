@@ -86,3 +86,20 @@ t = timeit(lambda: H.gemm_nt(H.asplit(H.im2col(pair, h2, w2, 128), pair=True), H
 rows.append(("ups conv pair 64->256 @96^2 (3 products)", t, 3 * 2.0 * M2 * 256 * 9 * 64))
 for name, t, f in rows:
     print("%-44s %8.1f us %7.1f TFLOP/s (%.3f of 2.5 PF)" % (name, t, f / t * 1e-6, f / t * 1e-6 / 2500))
+
+# the x4 upsampling conv's input gradient at 96^2: 256 -> 64, PixelUnshuffle store (wr) vs the halo kernel's
+# four channel-group passes
+Gd = torch.randn(M2, 256, device=dev).bfloat16()
+w_up = torch.randn(256, 64, 3, 3, device=dev) * 0.03
+Wd16 = torch.empty(64 * 9 * 256, device=dev, dtype=torch.bfloat16)
+H.pack_weight(w_up, Wd16, H.wmap(16, 256, 64, (1, 256, 256), (1, 64, 64), n_perm=4))
+Wd2 = torch.empty(64, 9 * 256, device=dev, dtype=torch.bfloat16)
+H.pack_weight(w_up, Wd2, H.wmap(2, 256, 64, (1, 256, 256), (1, 64, 64), n_perm=4))
+dprev = torch.empty(M2 // 4, 256, device=dev, dtype=torch.bfloat16)
+fl_d = 2.0 * M2 * 64 * 9 * 256
+t = timeit(lambda: H.gemm_nt(H.im2col(Gd, h2, w2, 256, flip=True), H.rows(Wd2),
+                             H.epilogue(dprev, mode=H.OUT_PUNSHUF_SPM, ldo=256, ps=(2, h2 // 2, w2 // 2)), M2, 64, 9 * 256,
+                             H.BF16))
+print("%-44s %8.1f us %7.1f TFLOP/s (%.3f of 2.5 PF)" % ("ups dgrad 256->64 @96^2 halo CG", t, fl_d / t * 1e-6, fl_d / t * 1e-6 / 2500))
+t = timeit(lambda: H.conv3x3_wr(Gd, 256, 1, Wd16, None, None, dprev, B, h2, w2, 256, 64, ldo=256, split=False, ps_r=-2))
+print("%-44s %8.1f us %7.1f TFLOP/s (%.3f of 2.5 PF)" % ("wr: ups dgrad 256->64 @96^2 punshuf", t, fl_d / t * 1e-6, fl_d / t * 1e-6 / 2500))
