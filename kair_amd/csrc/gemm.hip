@@ -1117,6 +1117,10 @@ struct TnRingTile {
   float* P;                                     // this split's fp32 [N][K] plane
 };
 
+// the chunk permutation of LDS row r (see tn_ring_body): rows {0, 2, 8, 10} + 16 k and {1, 3, 9, 11} + 16 k
+// -- the rows one 32-lane half reads together -- get distinct chunk offsets 0 / 2 / 4 / 6
+KAIR_DEV int tn_sw(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
+
 template <int AMA, int BMB, int NS>
 KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, const Op& Bo, char* smem) {
   constexpr int BNt = TNR_BN, BKt = TNR_BK, RB = TNR_RB;
@@ -1139,6 +1143,10 @@ KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, const Op& Bo, char*
   const int tap = BMB == BM_TAP ? k0 / BKt : 0;
   const int tdy = tap / 3 - 1, tdx = tap - 3 * (tap / 3) - 1;
   const int tshift = BMB == BM_TAP ? tdy * Bo.imW + tdx : 0;
+  // LDS rows of 384 B put rows r and r + 2 (and r + 8) on the same banks: the transposed fragment reads
+  // (rows g8 + q and + 4 of a 32-lane half) were 4-way conflicted (PMC: 75 % of the LDS cycles).  The
+  // 16-byte chunks of row r sit XOR-permuted by tn_sw(r) (even, < 8: a chunk pair stays adjacent, a row
+  // stays within its 24 chunks); the DMA fetches, for each LDS slot, the logical chunk that lands there.
   auto issue = [&](int j) {
     const int m0 = mbeg + j * RB;
     char* st = smem + (j % NS) * STAGE;
@@ -1147,7 +1155,7 @@ KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, const Op& Bo, char*
       const int g = wave * 3 + i;                // 0..23: 12 KiB of A then 12 KiB of B
       const bool isB = g >= 12;
       const int off = (isB ? g - 12 : g) * 1024 + lane * 16;
-      const int r = off / ROWB, c = (off - (off / ROWB) * ROWB) >> 1;
+      const int r = off / ROWB, c = (((off - (off / ROWB) * ROWB) >> 4) ^ tn_sw(r)) << 3;
       const int m = m0 + r;
       const void* src = g_kair_zero_line;
       if (m < mend) {
@@ -1194,6 +1202,7 @@ KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, const Op& Bo, char*
     for (int i = 0; i < RN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, g8 = (lane >> 4) * 8;
+  const int R0 = g8 + q, sw0 = tn_sw(R0), sw4 = tn_sw(R0 + 4);   // this lane's two fragment rows
   for (int j = 0; j < nchunks; ++j) {
     const int ahead = (nchunks - 1 - j) < (NS - 2) ? (nchunks - 1 - j) : (NS - 2);
     if (ahead >= 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
@@ -1208,17 +1217,21 @@ KAIR_DEV void tn_ring_body(const TnRingTile& t, const Op& A, const Op& Bo, char*
     bf16x8 af[RN], bfr[RK];
 #pragma unroll
     for (int i = 0; i < RN; ++i) {
-      const bf16* base = sA + (g8 + q) * BNt + wn * 96 + i * 16 + p4;
+      const int ch = wn * 12 + 2 * i + (p4 >> 3);   // logical 16-byte chunk of the 8-byte read
+      const bf16* base = sA + R0 * BNt + ((ch ^ sw0) << 3) + (p4 & 7);
+      const bf16* base4 = sA + (R0 + 4) * BNt + ((ch ^ sw4) << 3) + (p4 & 7);
       const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base);
-      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base + 4 * BNt));
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base4);
       short __attribute__((ext_vector_type(8))) s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       af[i] = __builtin_bit_cast(bf16x8, s8);
     }
 #pragma unroll
     for (int jk = 0; jk < RK; ++jk) {
-      const bf16* base = sB + (g8 + q) * BKt + wk * 48 + jk * 16 + p4;
+      const int ch = wk * 6 + 2 * jk + (p4 >> 3);
+      const bf16* base = sB + R0 * BKt + ((ch ^ sw0) << 3) + (p4 & 7);
+      const bf16* base4 = sB + (R0 + 4) * BKt + ((ch ^ sw4) << 3) + (p4 & 7);
       const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base);
-      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)(base + 4 * BKt));
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)base4);
       short __attribute__((ext_vector_type(8))) s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       bfr[jk] = __builtin_bit_cast(bf16x8, s8);
     }
