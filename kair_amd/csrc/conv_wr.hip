@@ -344,8 +344,13 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
   KAIR_CHECK_ARG(x_dtype == KAIR_F32 || x_dtype == KAIR_BF16, "conv3x3_wr: image dtype");
   KAIR_CHECK_ARG(out_dtype == KAIR_F32 || out_dtype == KAIR_BF16, "conv3x3_wr: output dtype");
   const bool pair = split && x_dtype == KAIR_BF16;
-  const int BM = kair_conv3x3_wr_tile(split, B, H, W, C, N);
+  int BM = kair_conv3x3_wr_tile(split, B, H, W, C, N);
   KAIR_CHECK_ARG(BM > 0, "conv3x3_wr: unsupported geometry (B %d, H %d, W %d, C %d, N %d)", B, H, W, C, N);
+  if (BM == 144 && resid) {   // the 144-pixel plain form has no residual instantiation (its registers spill)
+    const long Mg = (long)B * H * W;
+    BM = wr_geometry(96, WrGeom<false>::HALO, Mg, H, W, C) ? 96 : wr_geometry(48, WrGeom<false>::HALO, Mg, H, W, C) ? 48 : 0;
+    KAIR_CHECK_ARG(BM > 0, "conv3x3_wr: no tile for a plain conv with a residual at this geometry");
+  }
   const int RN = N > 192 ? 4 : N > 64 ? 3 : 1;
   KAIR_CHECK_ARG(n_blocks == 4 * RN, "conv3x3_wr: the packed weight needs %d output rows (%d blocks of 16), got %d blocks",
                  64 * RN, 4 * RN, n_blocks);
@@ -388,7 +393,7 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
   do {                                                                                     \
     if (BM == 48) KAIR_WR(TXV, SPV, 48, RV, RNV, EMV);                                     \
     else if (BM == 96) KAIR_WR(TXV, SPV, 96, RV, RNV, EMV);                                \
-    else if constexpr (!SPV) KAIR_WR(TXV, SPV, 144, RV, RNV, EMV);                         \
+    else if constexpr (!SPV && !RV) KAIR_WR(TXV, SPV, 144, RV, RNV, EMV);                  \
   } while (0)
   if (pair) {   // the SwinIR x4 upsampling convs: [hi | lo] pair in, PixelShuffle [hi | lo] pair out
     KAIR_CHECK_ARG(RN == 4 && ps_r > 0 && !rs, "conv3x3_wr: the pair form is built for N in (192, 256] with a PixelShuffle store");
