@@ -73,9 +73,16 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
   const int H = a.H, W = a.W, C = a.C;
-  const int XW = W < BM ? W : BM, RPT = BM / XW, HWD = XW + 2, HR = RPT + 2, PS = C + 8;
-  const int c8n = C / 8, halo_pieces = HR * HWD * c8n;
-  const int cps = C / 32, KS = 9 * cps;                     // k-steps of 32
+  // CGP 2 (192-pixel tiles, plain): the channels in two halves, one halo pass each, accumulating
+  constexpr int CGP = BM == 192 ? 2 : 1;
+  static_assert(CGP == 1 || (!SPLIT && !RESID), "channel-half passes: plain image, no residual");
+  const int CH = C / CGP;
+  const int XW = W < BM ? W : BM, RPT = BM / XW, HWD = XW + 2, HR = RPT + 2, PS = CH + 8;
+  const int c8n = CH / 8, halo_pieces = HR * HWD * c8n;
+  const int cps = C / 32, cpsP = CH / 32, KSP = 9 * cpsP, KS = 9 * cps;   // k-steps of 32: per pass, all
+  int pass = 0;
+  // a pass's k-step sl -> the weight's k-step (k = tap * C + c)
+  auto wstep = [&](int sl) { const int tap = sl / cpsP; return tap * cps + pass * cpsP + (sl - tap * cpsP); };
   int hb[RM];
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
@@ -105,7 +112,7 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
   };
   bf16x8 ra[2][RM][NB];            // activation fragments, one k-step ahead
   auto read_a = [&](int buf, int s) {
-    const int tap = s / cps, c0 = (s - tap * cps) * 32;
+    const int tap = s / cpsP, c0 = (s - tap * cpsP) * 32;
     int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
     if (a.flip) { dy = -dy; dx = -dx; }
     const int off = (dy * HWD + dx) * PS + c0;
@@ -122,10 +129,29 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
     const int b = (int)(p0 / ((long)H * W));
     const int rem = (int)(p0 - (long)b * H * W);
     const int y0 = rem / W, x0 = rem - (rem / W) * W;
+    f32x4 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) acc[i][rn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 ex[RESID ? RM : 1][RN];
+    auto load_resid = [&]() {
+      if constexpr (RESID) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int rn = 0; rn < RN; ++rn) {
+            const long m = p0 + i * 16 + fr;
+            const int n = 16 * RN * wave + 16 * rn + 4 * fq;
+            ex[i][rn] = *(const float4*)(a.resid + m * a.ldr + (n < a.N ? n : 0));
+          }
+      }
+    };
+    for (pass = 0; pass < CGP; ++pass) {
     // the first k-steps' weights in flight under the halo fill
 #pragma unroll
-    for (int u = 0; u < PD; ++u) issue_w(u, u);
-    __syncthreads();   // every wave is done with the previous tile's halo
+    for (int u = 0; u < PD; ++u) issue_w(u, wstep(u));
+    __syncthreads();   // every wave is done with the previous tile's (or pass's) halo
     {
       // pieces per thread in one batch of loads (all issued, then landed, then written): the whole
       // halo at once where the registers allow it -- each batch is one exposed memory latency
@@ -141,7 +167,7 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
           const int hr = fdiv(pix, a.fhwd), hc = pix - hr * HWD;
           const int y = y0 - 1 + hr, x = x0 - 1 + hc;
           okv[i] = idx < halo_pieces && y >= 0 && y < H && x >= 0 && x < W;
-          const long src = okv[i] ? ((long)(b * H + y) * W + x) * a.ldx + c8 * 8 : 0;
+          const long src = okv[i] ? ((long)(b * H + y) * W + x) * a.ldx + pass * CH + c8 * 8 : 0;
           if constexpr (sizeof(TX) == 4) {
             v0[i] = *(const uint4*)((const float*)a.x + src);
             v1[i] = *(const uint4*)((const float*)a.x + src + 4);
@@ -193,31 +219,13 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
     }
     __syncthreads();   // halo visible
 
-    f32x4 acc[RM][RN];
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int rn = 0; rn < RN; ++rn) acc[i][rn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 ex[RESID ? RM : 1][RN];
-    auto load_resid = [&]() {
-      if constexpr (RESID) {
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
-          for (int rn = 0; rn < RN; ++rn) {
-            const long m = p0 + i * 16 + fr;
-            const int n = 16 * RN * wave + 16 * rn + 4 * fq;
-            ex[i][rn] = *(const float4*)(a.resid + m * a.ldr + (n < a.N ? n : 0));
-          }
-      }
-    };
     read_a(0, 0);
-    // k-loop, unrolled by UNR (the weight ring is PD deep, the activation buffers 2): KS % UNR == 0.
-    // Every load is unconditional (the last steps re-read step KS - 1): a load on only some paths makes
+    // k-loop, unrolled by UNR (the weight ring is PD deep, the activation buffers 2): KSP % UNR == 0.
+    // Every load is unconditional (the last steps re-read step KSP - 1): a load on only some paths makes
     // the compiler's wait at the merge the minimum over the paths (vmcnt / lgkmcnt 0 every step).
     auto step = [&](int u, int s, bool tail) {
       const int ab = u & 1, ws = u % PD;
-      read_a(ab ^ 1, s + 1 < KS ? s + 1 : KS - 1);
+      read_a(ab ^ 1, s + 1 < KSP ? s + 1 : KSP - 1);
       if (RESID && tail && u == UNR - 3) load_resid();
 #pragma unroll
       for (int i = 0; i < RM; ++i)
@@ -229,14 +237,15 @@ __global__ __launch_bounds__(WR_NT, 1) void conv3x3_wr_kernel(const ConvWrArgs a
             acc[i][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[ws][rn][0], ra[ab][i][1], acc[i][rn], 0, 0, 0);
           }
         }
-      issue_w(ws, s + PD < KS ? s + PD : KS - 1);
+      issue_w(ws, wstep(s + PD < KSP ? s + PD : KSP - 1));
     };
-    for (int s0 = 0; s0 < KS - UNR; s0 += UNR) {
+    for (int s0 = 0; s0 < KSP - UNR; s0 += UNR) {
 #pragma unroll
       for (int u = 0; u < UNR; ++u) step(u, s0 + u, false);
     }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) step(u, KS - UNR + u, true);
+    for (int u = 0; u < UNR; ++u) step(u, KSP - UNR + u, CGP == 1 || pass == CGP - 1);
+    }   // pass
     // epilogue: 4 consecutive channels of one pixel per lane
 #pragma unroll
     for (int i = 0; i < RM; ++i)
@@ -318,15 +327,19 @@ extern "C" int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N
   if (!split && N > 192) return 0;
   // the largest tile that still gives >= 3/4 of a workgroup per CU, else the smallest that fits: at
   // B = 4 (M = 9,216) 48-pixel tiles put 192 workgroups on the chip instead of 96 / 64
-  static const int cand_split[] = {96, 48}, cand_plain[] = {144, 96, 48};
-  const int* cand = split ? cand_split : cand_plain;
+  // plain C = 256 (the upsampling convs' input gradients): 192-pixel tiles in two channel-half passes
+  // first (the 256-channel halo of a 96-pixel tile re-reads every input row three times)
+  static const int cand_split[] = {96, 48}, cand_plain[] = {144, 96, 48}, cand_256[] = {192, 96, 48};
+  const int* cand = split ? cand_split : C == 256 ? cand_256 : cand_plain;
   const int nc = split ? 2 : 3;
   const long want = 3L * wr_num_cus() / 4;
   int best = 0;
   for (int i = 0; i < nc; ++i) {
     const int bm = cand[i];
-    if (!(split ? wr_geometry(bm, WrGeom<true>::HALO, M, H, W, C) : wr_geometry(bm, WrGeom<false>::HALO, M, H, W, C)))
+    if (!(split ? wr_geometry(bm, WrGeom<true>::HALO, M, H, W, C)
+                : wr_geometry(bm, WrGeom<false>::HALO, M, H, W, bm == 192 ? C / 2 : C)))
       continue;
+    if (bm == 192 && N > 64) continue;   // (only the N <= 64 input-gradient forms have the two-pass tile)
     best = bm;
     if (M / bm >= want) return bm;
   }
@@ -383,7 +396,7 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
   a.act = act; a.slope = slope;
   a.B = B; a.H = H; a.W = W; a.C = C; a.N = N; a.flip = flip;
   a.tilesM = M / BM;
-  a.fc8 = make_fdiv(C / 8);
+  a.fc8 = make_fdiv(C / (BM == 192 ? 2 : 1) / 8);
   a.fhwd = make_fdiv((W < BM ? W : BM) + 2);
   const int ncu = wr_num_cus();
   const int grid = (int)(a.tilesM < ncu ? a.tilesM : ncu);
@@ -400,7 +413,10 @@ extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int spli
     KAIR_WR3(bf16, true, false, 4, 1);
   } else if (RN == 1 && !split) {   // the upsampling convs' input gradients (256 -> 64): unshuffled or gated rows
     KAIR_CHECK_ARG(x_dtype == KAIR_BF16 && ps_r <= 0 && !rs, "conv3x3_wr: the plain N <= 64 form takes a bf16 image");
-    if (ps_r < 0) KAIR_WR3(bf16, false, false, 1, 2); else KAIR_WR3(bf16, false, false, 1, 0);
+    if (BM == 192) {
+      KAIR_CHECK_ARG(!acopy, "conv3x3_wr: no a_copy with the two-pass tile");
+      if (ps_r < 0) KAIR_WR(bf16, false, 192, false, 1, 2); else KAIR_WR(bf16, false, 192, false, 1, 0);
+    } else if (ps_r < 0) KAIR_WR3(bf16, false, false, 1, 2); else KAIR_WR3(bf16, false, false, 1, 0);
   } else if (RN == 1) {   // conv_before_upsample (192 -> 64): split, row output (+ LeakyReLU, + lo plane)
     KAIR_CHECK_ARG(split && x_dtype == KAIR_F32 && ps_r == 0, "conv3x3_wr: the N <= 64 form takes an fp32 image, split, rows");
     if (rs) KAIR_WR3(float, true, true, 1, 0); else KAIR_WR3(float, true, false, 1, 0);

@@ -142,14 +142,17 @@ def test_conv_wr_cbu_leaky_pair():
     assert rel_err(got, ref) < 3e-5
 
 
-@pytest.mark.parametrize("mode,hw", [("punshuf", (24, 96)), ("gate", (24, 48)), ("punshuf", (48, 48))])
-def test_conv_wr_ups_dgrad(mode, hw):
+@pytest.mark.parametrize("mode,hw,B", [("punshuf", (24, 96), 2), ("gate", (24, 48), 2), ("punshuf", (48, 48), 2),
+                                       ("punshuf", (96, 96), 4), ("gate", (48, 48), 16)])
+def test_conv_wr_ups_dgrad(mode, hw, B):
     """The upsampling convs' input gradients (network_swinir.py:584 Upsample, its backward): the 256-channel
     pre-shuffle gradient (bf16) through kind-16 weights (rows = the 64 input channels, columns
     sub-pixel-major), stored PixelUnshuffle(2)-ed into the previous conv's pre-shuffle rows, or gated
     by LeakyReLU'(a0) of the stored [hi | lo] activation -- vs fp64 conv_transpose2d."""
-    B, C, N = 2, 256, 64
+    C, N = 256, 64
     Hh, Ww = hw
+    # the last two shapes have enough pixels for the 192-pixel tile in two channel-half passes
+    assert H.conv3x3_wr_tile(0, B, Hh, Ww, C, N) == (192 if B * Hh * Ww >= 36864 else 48)
     g = torch.Generator().manual_seed(31 + Hh)
     x = torch.randn(B, C, Hh, Ww, generator=g).bfloat16().float()
     w = (torch.randn(C, N, 3, 3, generator=g) * 0.03).bfloat16().float()   # forward conv N -> C
