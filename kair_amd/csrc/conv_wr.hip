@@ -339,7 +339,9 @@ extern "C" int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N
     if (!(split ? wr_geometry(bm, WrGeom<true>::HALO, M, H, W, C)
                 : wr_geometry(bm, WrGeom<false>::HALO, M, H, W, bm == 192 ? C / 2 : C)))
       continue;
-    if (bm == 192 && N > 64) continue;   // (only the N <= 64 input-gradient forms have the two-pass tile)
+    // (only the N <= 64 input-gradient forms have the two-pass tile, and it pays only where a 96-pixel
+    // tile is a single image row: W >= 96 -- at 48^2 it measured 68 -> 90 us)
+    if (bm == 192 && (N > 64 || W < 96)) continue;
     best = bm;
     if (M / bm >= want) return bm;
   }

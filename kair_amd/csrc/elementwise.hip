@@ -497,6 +497,46 @@ __global__ void l1_kernel(const float* __restrict__ E, const float* __restrict__
   if (threadIdx.x == 0) ws[blockIdx.x] = red[0];
 }
 
+// the same loss and gradient for the usual layout (r = 1, 16 bf16 slots per pixel, C <= 4): one thread per
+// pixel -- its C channel reads coalesced across the wave (NCHW planes), its 16 slots stored as two 16-byte
+// pieces -- instead of one thread per slot (16 threads per pixel, plane-strided reads, 2-byte stores)
+template <bool CH>
+__global__ void l1_pix16_kernel(const float* __restrict__ E, const float* __restrict__ H, bf16* __restrict__ dE,
+                                float gscale, int C, int HW, int npix, float* __restrict__ ws, float eps) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += gridDim.x * blockDim.x) {
+    const int b = pix / HW, pp = pix - b * HW;
+    bf16x8 g0 = {}, g1 = {};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c >= C) break;
+      const long i = ((long)b * C + c) * HW + pp;
+      const float d = E[i] - H[i];
+      float g;
+      if constexpr (CH) {
+        const float q = sqrtf(d * d + eps);
+        s += q;
+        g = q > 0.f ? gscale * d / q : 0.f;
+      } else {
+        s += fabsf(d);
+        g = d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f);
+      }
+      g0[c] = (bf16)g;
+    }
+    uint4* o = (uint4*)(dE + (long)pix * 16);
+    o[0] = __builtin_bit_cast(uint4, g0);
+    o[1] = __builtin_bit_cast(uint4, g1);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ws[blockIdx.x] = red[0];
+}
+
 __global__ void l1_final(const float* __restrict__ ws, int nb, float scale, float* out) {
   __shared__ float red[256];
   float s = 0.f;
@@ -785,6 +825,14 @@ static int pixel_loss(const float* E, const float* H, float* loss_out, void* dE,
   const float gs = (float)(weight / numel);
   // int indices when the largest index (dE element or image element) and the grid stride fit
   const bool i32 = (double)npix * ldc < 2.0e9 && numel < 2.0e9;
+  if (ps_r == 1 && ldc == 16 && C <= 4 && dtype == KAIR_BF16 && npix < (1L << 31) && ((uintptr_t)dE & 15) == 0) {
+    if (charb) hipLaunchKernelGGL(l1_pix16_kernel<true>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
+    else hipLaunchKernelGGL(l1_pix16_kernel<false>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
+    KAIR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);
+    KAIR_CHECK_LAUNCH();
+    return 0;
+  }
 #define KAIR_PIXEL_LOSS(T, I, CHV)                                                                                       \
   hipLaunchKernelGGL((l1_kernel<T, I, CHV>), dim3(nb), dim3(256), 0, s, E, H, (T*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws, \
                      eps)

@@ -151,8 +151,9 @@ def test_conv_wr_ups_dgrad(mode, hw, B):
     by LeakyReLU'(a0) of the stored [hi | lo] activation -- vs fp64 conv_transpose2d."""
     C, N = 256, 64
     Hh, Ww = hw
-    # the last two shapes have enough pixels for the 192-pixel tile in two channel-half passes
-    assert H.conv3x3_wr_tile(0, B, Hh, Ww, C, N) == (192 if B * Hh * Ww >= 36864 else 48)
+    # (96, 96) x 4 has enough pixels for the 192-pixel tile in two channel-half passes (rows of >= 96)
+    assert H.conv3x3_wr_tile(0, B, Hh, Ww, C, N) == (192 if B * Hh * Ww >= 36864 and Ww >= 96 else
+                                                     96 if B * Hh * Ww >= 18432 else 48)
     g = torch.Generator().manual_seed(31 + Hh)
     x = torch.randn(B, C, Hh, Ww, generator=g).bfloat16().float()
     w = (torch.randn(C, N, 3, 3, generator=g) * 0.03).bfloat16().float()   # forward conv N -> C

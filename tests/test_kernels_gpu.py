@@ -428,6 +428,35 @@ def test_window_attention_fwd_bwd(dtype, shift):
         assert torch.equal(dr.cpu(), blocked)
 
 
+@pytest.mark.parametrize("charb", [False, True])
+def test_pixel_loss_bf16_rows(charb):
+    """The training step's loss layout (bf16 dE rows of 16 slots, r = 1: kair_l1_loss's pixel-per-thread
+    kernel): loss value, gradient (bf16 of torch's) and zero pad slots, L1 and Charbonnier."""
+    g = torch.Generator().manual_seed(29)
+    B, C, Hh, Ww = 3, 3, 40, 24
+    E = torch.rand(B, C, Hh, Ww, generator=g)
+    Ht = torch.rand(B, C, Hh, Ww, generator=g)
+    Ht[:, :, :4] = E[:, :, :4]   # exact zeros of d
+    Er = E.clone().requires_grad_(True)
+    d = Er - Ht
+    eps = 1e-3
+    ref = (torch.sqrt(d * d + eps) if charb else d.abs()).mean()
+    ref.backward()
+    out = torch.empty(1, device=dev)
+    dE = torch.full((B * Hh * Ww, 16), float("nan"), device=dev, dtype=torch.bfloat16)
+    ws = torch.empty(1024, device=dev)
+    H.l1_loss(E.to(dev), Ht.to(dev), out, dE, 16, 1.0, B, C, Hh, Ww, ws, **({"charb_eps": eps} if charb else {}))
+    torch.cuda.synchronize()
+    assert abs(out.item() - ref.item()) < 1e-5 * ref.item()
+    got = dE.float().cpu().view(B, Hh, Ww, 16)
+    gg = got[..., :C].permute(0, 3, 1, 2)
+    if charb:   # bf16 of a differently-ordered fp32 expression: within one bf16 ulp
+        assert (gg - Er.grad).abs().max().item() <= 2 ** -8 * Er.grad.abs().max().item()
+    else:       # +-1 / numel or 0: exact
+        assert torch.equal(gg, Er.grad.bfloat16().float())
+    assert (got[..., C:] == 0).all()
+
+
 def test_l1_and_adam():
     g = torch.Generator().manual_seed(23)
     E = torch.rand(2, 3, 8, 8, generator=g)
