@@ -286,7 +286,8 @@ int kair_window_attn_fwd(const void* qkv, int dtype, const float* table, void* O
                          long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
                          const float* mask, int mask_nw, void* stream);
 /* Backward: dO rows [nWin*64, lddo] (dtype, same layout as O); writes dqkv head-blocked (dtype);
- * dtable (+)= bias-table gradient (ws: nh*64*64*partials floats, kair_window_attn_bwd_ws()). */
+ * dtable (+)= bias-table gradient (ws: partials*nh*225 floats, kair_window_attn_bwd_ws(): each wave bins
+ * its (group, head) 64 x 64 bias gradient into the 225 relative positions before it leaves LDS). */
 long kair_window_attn_bwd_ws(long nWin, int nh);
 int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
                          const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
@@ -301,7 +302,7 @@ int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo, const void
                             int shift, const float* mask, int mask_nw, void* stream);
 
 /* Deferred bias-table gradient: kair_window_attn_bwd with dtable = NULL leaves its per-group
- * partials (kair_window_attn_bwd_groups() planes of [nh][64][64]) in ws; one grouped launch then
+ * partials (kair_window_attn_bwd_groups() planes of [nh][225]) in ws; one grouped launch then
  * reduces several blocks' partials into their dtable (+)= (network_swinir.py:94-98 gather, backward):
  * up to 32 jobs, deterministic. */
 long kair_window_attn_bwd_groups(long nWin, int nh, int dtype);

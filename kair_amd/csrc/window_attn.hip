@@ -35,6 +35,52 @@ KAIR_DEV void wave_sync() {
 
 KAIR_DEV int relidx(int q, int k) { return ((q >> 3) - (k >> 3) + WS - 1) * (2 * WS - 1) + ((q & 7) - (k & 7) + WS - 1); }
 
+// The relative-position bias gradient of one (group, head) tile, binned inside the wave that made it:
+// out[idx] = sum of db[q][k] over the window's (query, key) pairs with relidx(q, k) = idx (the
+// backward of network_swinir.py:132-135's table gather).  The per-group output is 225 floats instead
+// of the 64 x 64 tile (16 KB per (group, head) at B = 4's one window per wave).  Stage 1: lane
+// (qy, ky) sums its 8 x 8 block of db along the 15 diagonals qx - kx; stage 2: lane = bin (dy, dx)
+// sums the blocks with qy - ky = dy.  Fixed order (deterministic).  scr: 1024 floats of the wave's LDS.
+constexpr int NBIN = (2 * WS - 1) * (2 * WS - 1);
+template <bool VEC>
+KAIR_DEV void bin_dbias(const float* db, int ldb, float* scr, float* __restrict__ out, int lane) {
+  const int qy = lane >> 3, ky = lane & 7;
+  float d[2 * WS - 1];
+#pragma unroll
+  for (int j = 0; j < 2 * WS - 1; ++j) d[j] = 0.f;
+#pragma unroll
+  for (int qx = 0; qx < WS; ++qx) {
+    const float* row = db + (qy * WS + qx) * ldb + ky * WS;
+    float v[WS];
+    if constexpr (VEC) {
+      const float4 a = *(const float4*)row, b = *(const float4*)(row + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int kx = 0; kx < WS; ++kx) v[kx] = row[kx];
+    }
+#pragma unroll
+    for (int kx = 0; kx < WS; ++kx) d[qx - kx + WS - 1] += v[kx];
+  }
+#pragma unroll
+  for (int j = 0; j < 2 * WS - 1; ++j) scr[lane * 16 + j] = d[j];
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = lane + 64 * i;
+    if (idx < NBIN) {
+      const int dy = idx / (2 * WS - 1) - (WS - 1), j = idx % (2 * WS - 1);
+      float s = 0.f;
+#pragma unroll
+      for (int y = 0; y < WS; ++y) {
+        const int kyy = y - dy;
+        if (kyy >= 0 && kyy < WS) s += scr[(y * WS + kyy) * 16 + j];
+      }
+      out[idx] = s;
+    }
+  }
+}
+
 KAIR_DEV int region(int coord, int n, int shift) { return coord < n - WS ? 0 : (coord < n - shift ? 1 : 2); }
 
 // region id of token t of window `wi` (index within the image) on the shifted H x W grid
@@ -573,14 +619,18 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const typename AT<BF>::T*
       for (int r = 0; r < 16; ++r) dq_out[(qt * 32 + acc_row(r, hh)) * HDP + l31] = (T)(aq[r] * scale);
     }
   }
-  // partial bias gradient of this (group, head): [q][key]
-  float* out = dB_part + (grp * nh + h) * TOK * TOK;
+  // partial bias gradient of this (group, head): [q][key] through the wave's (free) dS tile, binned
+  wave_sync();
+  float* dbt = (float*)sdS[w];   // fp32: [64][65]; bf16: [64][72] bf16 = [64][36] floats -- too small
+  static_assert(!BF, "the binned bias gradient needs the fp32 dS tile (the bf16 mode uses attn_bwd_bf16_kernel)");
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) out[(qt * 32 + acc_row(r, hh)) * TOK + kt * 32 + l31] = dB[qt][kt][r];
+      for (int r = 0; r < 16; ++r) dbt[(qt * 32 + acc_row(r, hh)) * 65 + kt * 32 + l31] = dB[qt][kt][r];
+  wave_sync();
+  bin_dbias<false>(dbt, 65, (float*)sQ[w], dB_part + (grp * nh + h) * NBIN, lane);
 }
 
 // perf-investigation phase stamps (KAIR_ATTN_STAMP=1, read with kair_debug_attn_stamps): per wave,
@@ -836,77 +886,49 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restri
       }
     }
   }
-  // partial bias gradient of this (group, head): [q][key], row-contiguous 16-byte stores
+  // partial bias gradient of this (group, head), binned (the q / dO tiles are free scratch now)
   wave_sync();
-  float* out = dB_part + (grp * nh + h) * TOK * TOK;
-#pragma unroll
-  for (int i = 0; i < TOK * TOK / 4 / 64; ++i) {
-    const int c = lane + 64 * i, row = c >> 4, c4 = (c & 15) * 4;
-    *(float4*)(out + row * TOK + c4) = *(const float4*)(db + row * LDB + c4);
+  static_assert(2 * TOK * LD * sizeof(bf16) >= 1024 * sizeof(float), "bin scratch");
+  bin_dbias<true>(db, LDB, (float*)sQG[w], dB_part + (grp * nh + h) * NBIN, lane);
+}
+
+// dtable[idx][h] (+)= sum over groups of the binned per-group partials [group][h][idx] (coalesced,
+// one thread per (h, idx), the groups split over the 16 waves and summed in fixed order)
+__global__ __launch_bounds__(1024) void attn_dtable_sum_kernel(const float* __restrict__ part, long ngroups, int nh,
+                                                               float* dtable, int acc) {
+  const long n = (long)nh * NBIN;
+  const long t = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s = split_sum16(part, ngroups, n, t, t < n);
+  if (t < n && threadIdx.x < 64) {
+    const int h = (int)(t / NBIN), idx = (int)(t - (long)h * NBIN);
+    float* o = dtable + idx * nh + h;
+    *o = acc ? *o + s : s;
   }
 }
 
-// stage 1: dB[h][q][k] = sum over groups of the per-group partials (coalesced, one thread per entry)
-__global__ __launch_bounds__(1024) void attn_dbias_sum_kernel(const float* __restrict__ dB_part, long ngroups, int nh,
-                                                              float* __restrict__ dB) {
-  const long n = (long)nh * TOK * TOK;
-  const long t = (long)blockIdx.x * 64 + (threadIdx.x & 63);
-  const float s = split_sum16(dB_part, ngroups, n, t, t < n);
-  if (t < n && threadIdx.x < 64) dB[t] = s;
-}
-
-// stage 2: dtable[idx][h] (+)= sum_{(q,k): relidx(q,k)=idx} dB[h][q][k] — one wave per (idx, h):
-// lane = query token q, its key k = q - (dy, dx) when inside the window; wave sum in fixed order.
-__global__ __launch_bounds__(256) void attn_dtable_kernel(const float* __restrict__ dB, int nh, float* dtable, int acc) {
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int nidx = (2 * WS - 1) * (2 * WS - 1);
-  if (t >= nidx * nh) return;
-  const int idx = t / nh, h = t - (t / nh) * nh;
-  const int dy = idx / (2 * WS - 1) - (WS - 1), dx = idx % (2 * WS - 1) - (WS - 1);
-  const int qy = lane >> 3, qx = lane & 7, ky = qy - dy, kx = qx - dx;
-  float v = 0.f;
-  if (ky >= 0 && ky < WS && kx >= 0 && kx < WS) v = dB[(long)h * TOK * TOK + lane * TOK + ky * WS + kx];
-  v = wave_sum(v);
-  if (lane == 0) dtable[idx * nh + h] = acc ? dtable[idx * nh + h] + v : v;
-}
-
-// Grouped bias-table gradient (kair_attn_dtable_grouped): the two stages above for every block of a
-// group, one launch per stage; a block finds its job by a scalar scan of the first-block offsets.
-struct DtabJob { const float* part; float* dtable; long ngroups; int nh, acc, blk0, blk1; };
+// Grouped bias-table gradient (kair_attn_dtable_grouped): the sum above for every block of a group in
+// one launch; a workgroup finds its job by a scalar scan of the first-block offsets.
+struct DtabJob { const float* part; float* dtable; long ngroups; int nh, acc, blk0; };
 constexpr int DTAB_MAX = 32;
 struct DtabGroup { DtabJob j[DTAB_MAX]; int njobs; };
 
-KAIR_DEV int dtab_job(const DtabGroup& g, int b, bool second) {
+KAIR_DEV int dtab_job(const DtabGroup& g, int b) {
   int ji = 0;
   for (int i = 1; i < g.njobs; ++i)
-    if ((second ? g.j[i].blk1 : g.j[i].blk0) <= b) ji = i;
+    if (g.j[i].blk0 <= b) ji = i;
   return __builtin_amdgcn_readfirstlane(ji);
 }
 
-__global__ __launch_bounds__(1024) void attn_dbias_sum_grouped(const DtabGroup g) {
-  const DtabJob& jb = g.j[dtab_job(g, blockIdx.x, false)];
-  const long n = (long)jb.nh * TOK * TOK;
+__global__ __launch_bounds__(1024) void attn_dtable_grouped(const DtabGroup g) {
+  const DtabJob& jb = g.j[dtab_job(g, blockIdx.x)];
+  const long n = (long)jb.nh * NBIN;
   const long t = (long)(blockIdx.x - jb.blk0) * 64 + (threadIdx.x & 63);
   const float s = split_sum16(jb.part, jb.ngroups, n, t, t < n);
-  if (t < n && threadIdx.x < 64) (const_cast<float*>(jb.part) + jb.ngroups * n)[t] = s;
-}
-
-__global__ __launch_bounds__(256) void attn_dtable_grouped(const DtabGroup g) {
-  const DtabJob& jb = g.j[dtab_job(g, blockIdx.x, true)];
-  const int nh = jb.nh;
-  const float* dB = jb.part + jb.ngroups * nh * TOK * TOK;
-  const int t = (blockIdx.x - jb.blk1) * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int nidx = (2 * WS - 1) * (2 * WS - 1);
-  if (t >= nidx * nh) return;
-  const int idx = t / nh, h = t - (t / nh) * nh;
-  const int dy = idx / (2 * WS - 1) - (WS - 1), dx = idx % (2 * WS - 1) - (WS - 1);
-  const int qy = lane >> 3, qx = lane & 7, ky = qy - dy, kx = qx - dx;
-  float v = 0.f;
-  if (ky >= 0 && ky < WS && kx >= 0 && kx < WS) v = dB[(long)h * TOK * TOK + lane * TOK + ky * WS + kx];
-  v = wave_sum(v);
-  if (lane == 0) jb.dtable[idx * nh + h] = jb.acc ? jb.dtable[idx * nh + h] + v : v;
+  if (t < n && threadIdx.x < 64) {
+    const int h = (int)(t / NBIN), idx = (int)(t - (long)h * NBIN);
+    float* o = jb.dtable + idx * jb.nh + h;
+    *o = jb.acc ? *o + s : s;
+  }
 }
 
 constexpr int WPG = 4;  // windows per backward wave (fp32 parity path)
@@ -966,7 +988,7 @@ extern "C" int kair_debug_attn_stamps(unsigned long long* host, int n) {
 
 extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) {
   const long g32 = bwd_groups(nWin, WPG), g16 = bwd_groups(nWin, bwd_wpg_bf16(nWin, nh));
-  return ((g32 > g16 ? g32 : g16) + 1) * nh * TOK * TOK;
+  return (g32 > g16 ? g32 : g16) * nh * NBIN;
 }
 
 extern "C" int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
@@ -993,11 +1015,8 @@ extern "C" int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo,
                        ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw);
   KAIR_CHECK_LAUNCH();
   if (!dtable) return 0;   // deferred: the per-group partials stay in ws for kair_attn_dtable_grouped
-  float* dB = ws + ngroups * nh * TOK * TOK;
-  hipLaunchKernelGGL(attn_dbias_sum_kernel, dim3((nh * TOK * TOK + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dB);
-  KAIR_CHECK_LAUNCH();
-  const int nt = (2 * WS - 1) * (2 * WS - 1) * nh;
-  hipLaunchKernelGGL(attn_dtable_kernel, dim3((nt + 3) / 4), dim3(256), 0, s, dB, nh, dtable, dtable_accumulate);
+  hipLaunchKernelGGL(attn_dtable_sum_kernel, dim3((nh * NBIN + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dtable,
+                     dtable_accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1019,20 +1038,16 @@ extern "C" int kair_attn_dtable_grouped(const kair_attn_dtable_job* jobs, int nj
   KAIR_CHECK_ARG(jobs && njobs > 0 && njobs <= DTAB_MAX, "attn_dtable_grouped: 1..%d jobs", DTAB_MAX);
   DtabGroup g;
   memset(&g, 0, sizeof(g));
-  int b0 = 0, b1 = 0;
+  int b0 = 0;
   for (int i = 0; i < njobs; ++i) {
     const kair_attn_dtable_job& J = jobs[i];
     KAIR_CHECK_ARG(J.ws && J.dtable && J.nh > 0 && J.nWin > 0, "attn_dtable_grouped: job %d", i);
-    g.j[i] = DtabJob{J.ws, J.dtable, kair_window_attn_bwd_groups(J.nWin, J.nh, J.dtype), J.nh, J.accumulate ? 1 : 0,
-                     b0, b1};
-    b0 += (J.nh * TOK * TOK + 63) / 64;
-    b1 += ((2 * WS - 1) * (2 * WS - 1) * J.nh + 3) / 4;
+    g.j[i] = DtabJob{J.ws, J.dtable, kair_window_attn_bwd_groups(J.nWin, J.nh, J.dtype), J.nh, J.accumulate ? 1 : 0, b0};
+    b0 += (J.nh * NBIN + 63) / 64;
   }
   g.njobs = njobs;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(attn_dbias_sum_grouped, dim3(b0), dim3(1024), 0, s, g);
-  KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(attn_dtable_grouped, dim3(b1), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(attn_dtable_grouped, dim3(b0), dim3(1024), 0, s, g);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
