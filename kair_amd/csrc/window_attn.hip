@@ -652,14 +652,15 @@ KAIR_DEV unsigned long long stamp_now() {
 // transposed (D[d][token]: lane = token, 4 consecutive d per register group), so each lane
 // stores 8 bytes at a time instead of 2.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void attn_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ O,
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ O,
                                                             long ldo, const bf16* __restrict__ dO, long lddo,
                                                             const float* __restrict__ table, const float* __restrict__ lse,
                                                             bf16* __restrict__ dqkv, float* __restrict__ dB_part,
                                                             long nWin, int nh, int wpg, float scale, int H, int W,
                                                             int shift, const float* __restrict__ amask, int mask_nw,
                                                             int stamp, int rows) {
-  constexpr int LD = AT<true>::LD, LDD = 72, NW = 4, LDB = 72;
+  constexpr int LD = AT<true>::LD, LDD = 72, LDB = 72;
   static_assert(TOK * LDD <= 2 * TOK * LD, "the dS tile reuses the q / dO tiles");
   // per wave: q and dO tiles (after dV / dK they hold the dS tile), k tile, and the running bias
   // gradient [q][key] in fp32 (row stride 72: the two lane halves' rows 4 apart fall in opposite
@@ -977,6 +978,13 @@ extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* tab
 }
 
 static const int g_stamp = kair_dbg_env("KAIR_ATTN_STAMP");
+// waves per workgroup of the bf16 backward: 2 (71 KB of LDS, two workgroups per CU) spreads the
+// (group, head) waves over every CU where 4-wave workgroups fill only 216 of 256 at B = 4 (A/B with
+// KAIR_ATTN_BWD_NW=4: B = 4 630.7 -> 633.7 patches/s, B = 32 1,430 -> 1,438)
+static const int g_bwd_nw = [] {
+  const char* e = getenv("KAIR_ATTN_BWD_NW");
+  return e && atoi(e) == 4 ? 4 : 2;
+}();
 
 // copy the attention-backward phase stamps to the host (perf investigation only)
 extern "C" int kair_debug_attn_stamps(unsigned long long* host, int n) {
@@ -1003,11 +1011,15 @@ extern "C" int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo,
   KAIR_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0, "window_attn_bwd: strides");
   const int wpg = dtype == KAIR_BF16 ? bwd_wpg_bf16(nWin, nh) : WPG;
   const long ngroups = bwd_groups(nWin, wpg);
-  const int nw = dtype == KAIR_BF16 ? 4 : NWAVES<false>;
+  const int nw = dtype == KAIR_BF16 ? g_bwd_nw : NWAVES<false>;
   const long nb = (ngroups * nh + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
+  if (dtype == KAIR_BF16 && nw == 2)
+    hipLaunchKernelGGL(attn_bwd_bf16_kernel<2>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
+                       (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw,
+                       g_stamp, dqkv_rows);
+  else if (dtype == KAIR_BF16)
+    hipLaunchKernelGGL(attn_bwd_bf16_kernel<4>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
                        (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw,
                        g_stamp, dqkv_rows);
   else
