@@ -180,7 +180,7 @@ def rocprof_name(fn, a):
         hold = {12: kb // ks, 24: 6, 36: {0: 9, 1: 7, 2: 5}[epi]}[kb]
         return f"rowgemm_kernel<{kb}, {ks}, {N // 96}, {epi}, {hold}>"
     return {"conv3x3_wr": "conv3x3_wr_kernel", "swin_mlp_fwd": "swin_mlp_fwd_wr_kernel", "swin_attn_fwd": "swin_attn_fwd12_kernel<6>",   # KAIR_ATTN12 (swin_fused.hip)
-            "window_attn_bwd": "attn_bwd_bf16_kernel"}.get(fn, fn)
+            "window_attn_bwd": "attn_bwd_bf16_kernel<2>"}.get(fn, fn)
 
 
 def pmc_traffic(key):
@@ -251,7 +251,7 @@ def fp32_line(bpg, device, drop_path, steps, warmup, roles=True):
         rs = time_roles(tr, serial=True)
         for k, v in sorted(rs.items(), key=lambda kv: -kv[1]["ms_total"])[:5]:
             # the fp32 engine's kernels: the fp32 attention backward and the plain fp32 GEMMs (rocprof names)
-            kname = {"attn_bwd_bf16_kernel": "attn_bwd_kernel<false>"}.get(v["rocprof"], v["rocprof"])
+            kname = {"attn_bwd_bf16_kernel<2>": "attn_bwd_kernel<false>"}.get(v["rocprof"], v["rocprof"])
             top.append({"role": k, "kernel": kname, "launches_per_step": v["launches"], "kernel_ms": round(v["ms"], 5),
                         "step_ms_total": round(v["ms_total"], 4)})
     del tr, net, ema
