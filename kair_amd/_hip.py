@@ -12,7 +12,9 @@ import torch
 # KAIR_LIB=debug: the debug-ablation build (python -m kair_amd.build --debug-ablations), for the
 # perf-investigation tools only; the release library is the default and the only one tests / bench use
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
-                        "libkair_hip_dbg.so" if os.environ.get("KAIR_LIB") == "debug" else "libkair_hip.so")
+                        {"debug": "libkair_hip_dbg.so", "base": "libkair_hip_base.so"}.get(os.environ.get("KAIR_LIB"),
+                                                                                          "libkair_hip.so"))
+# KAIR_LIB=base: an A/B baseline library (same ABI, earlier sources) placed there by hand; never shipped
 
 F32, BF16 = 0, 1
 LD_ROWS, LD_IM2COL3, LD_QKVBLK, LD_S2D = 0, 1, 2, 3

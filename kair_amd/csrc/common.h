@@ -238,22 +238,18 @@ KAIR_DEV float split_sum16(const float* __restrict__ part, long nparts, long pla
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   float s0 = 0.f, s1 = 0.f;
   if (valid) {
-    long i = ty;
-    for (; i + 112 < nparts; i += 128) {   // 8 loads in flight, then the pair loop's s0/s1 order
+    // 8 loads in flight (clamped, so the last partial batch issues them together too), summed
+    // alternately into s0 / s1 in part order
+    for (long i = ty; i < nparts; i += 128) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(i + 16 * u) * plane + off];
+      for (int u = 0; u < 8; ++u) v[u] = part[(i + 16 * u < nparts ? i + 16 * u : nparts - 1) * plane + off];
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
-        s0 += v[u];
-        s1 += v[u + 1];
+        if (i + 16 * u < nparts) s0 += v[u];
+        if (i + 16 * (u + 1) < nparts) s1 += v[u + 1];
       }
     }
-    for (; i + 16 < nparts; i += 32) {
-      s0 += part[i * plane + off];
-      s1 += part[(i + 16) * plane + off];
-    }
-    if (i < nparts) s0 += part[i * plane + off];
   }
   red[ty][tx] = s0 + s1;
   __syncthreads();

@@ -260,17 +260,17 @@ KAIR_DEV void finalize4_body(const float* __restrict__ part, int splits, const k
     // (a load-add chain waits out one memory latency per split); the sum order is unchanged
     const float4* p = (const float4*)part + e4;
     const long st = plane / 4;
-    int sp = ph;
-    for (; sp + 28 < splits; sp += 32) {
+    // (the last, partial batch too: a phase with 7 of 28 splits used to run 7 dependent round trips)
+    for (int sp = ph; sp < splits; sp += 32) {
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[(long)(sp + 4 * u) * st];
+      for (int u = 0; u < 8; ++u) {
+        const int spu = sp + 4 * u < splits ? sp + 4 * u : splits - 1;   // clamped: every load issues
+        v[u] = p[(long)spu * st];
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
-    }
-    for (; sp < splits; sp += 4) {
-      const float4 v = p[(long)sp * st];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      for (int u = 0; u < 8; ++u)
+        if (sp + 4 * u < splits) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
     }
   }
   red[ph][q] = s;

@@ -142,3 +142,36 @@ def test_c5_rrdbnet_full():
     ref = ocv.RRDBNet(3, 3, 64, 23, 32, 4)
     x = torch.rand(1, 3, 32, 32, generator=torch.Generator().manual_seed(6))
     run_pair(net, ref, x, 4)
+
+
+def test_c2_swinir_light_full_bf16():
+    """C2 at its option file's precision (bf16; train_swinir_sr_lightweight.json), full size, one 64-px
+    patch: the bf16 engine's forward and every parameter gradient against the float64 oracle.  Bounds
+    are 2-4x the errors measured on the MI355X (printed; round 4: output 9.9e-5 relative, |dPSNR| of the
+    output against the HR target 2.4e-5 dB, worst gradient 6.1e-3 relative -- a LayerNorm weight, whose
+    gradient sums over 4,096 tokens through bf16 operands)."""
+    from kair_amd.models.network_swinir import SwinIR
+    torch.manual_seed(3)
+    net = SwinIR(upscale=2, in_chans=3, img_size=64, window_size=8, img_range=1.0, depths=[6] * 4, embed_dim=60,
+                 num_heads=[6] * 4, mlp_ratio=2, upsampler="pixelshuffledirect", resi_connection="1conv",
+                 drop_path_rate=0.0, compute_dtype="bf16")
+    ref = osw.SwinIR(2, 3, 64, 8, 1.0, [6] * 4, 60, [6] * 4, 2, "pixelshuffledirect")
+    ref.load_state_dict(net.state_dict(), strict=True)
+    ref64 = ref.double()
+    x = torch.rand(1, 3, 64, 64, generator=torch.Generator().manual_seed(4))
+    Hh = torch.rand(1, 3, 128, 128, generator=torch.Generator().manual_seed(7))
+    net = net.to(dev).train()
+    E = net(x.to(dev))
+    torch.nn.functional.l1_loss(E.float(), Hh.to(dev)).backward()
+    E64 = ref64(x.double())
+    torch.nn.functional.l1_loss(E64, Hh.double()).backward()
+    e_out = rel(E, E64)
+    psnr = lambda a: (10 * torch.log10(1.0 / ((a.detach().double().cpu().clamp(0, 1) - Hh.double()) ** 2).mean())).item()  # noqa: E731
+    d_psnr = abs(psnr(E) - psnr(E64))
+    g64 = {k: p.grad for k, p in ref64.named_parameters()}
+    ours = grad_errs({k: p.grad for k, p in net.named_parameters()}, g64)
+    worst = max(ours.items(), key=lambda kv: kv[1])
+    print(f"C2 bf16: output rel {e_out:.2e}, |dPSNR| {d_psnr:.2e} dB, worst grad {worst[0]} {worst[1]:.2e}")
+    assert e_out < 3e-4
+    assert d_psnr < 1e-4
+    assert worst[1] < 1.5e-2, worst
