@@ -2000,12 +2000,19 @@ int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, in
 // Cp = 192 conv weight gradients (N = 192, K = 9 * 192): one 192-wide N tile instead of a full
 // and a half-empty 128-wide one (B = 32: 946 -> 953 patches/s; B = 4 unchanged)
 static bool tn192_shape(int N, int K) { return N > 128 && N <= 192 && K > 128; }
+// narrow weight gradients (N <= 32 output channels, e.g. RRDB's growth-32 dense-block convs): a
+// 128 x 128 tile would be 3/4 empty along N; a 32 x 256 one does the same work in half the tiles
+static bool tn_narrow_shape(int N, int K) { return N <= 32 && K > 64; }
 
 template <typename CT, typename TA, typename TB, int AMA, int AMB>
 int launch_tn(const Op& a, const Op& b, float* ws, int splits, long M, int N, int K, long rps, hipStream_t s) {
   if (tn192_shape(N, K)) {   // one 192-wide N tile (Cp = 192 conv weight gradients): no half-empty tile
     const int tilesK = (K + 127) / 128;
     hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 192, 128>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
+                       ws, M, N, K, rps, tilesK);
+  } else if (tn_narrow_shape(N, K)) {   // N <= 32 (dense-block growth convs): one 32 x 256 tile, no 3/4-empty N
+    const int tilesK = (K + 255) / 256;
+    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 32, 256>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
                        ws, M, N, K, rps, tilesK);
   } else if (N <= 64 && K <= 64) {
     const int tilesN = (N + 63) / 64, tilesK = (K + 63) / 64;
@@ -2159,7 +2166,8 @@ extern "C" int kair_wgrad_splits(long M, int N, int K) {
     if (s > maxs) s = maxs;
     return (int)(s < 1 ? 1 : s);
   }
-  const long tiles = (N <= 64 && K <= 64) ? 1 : (long)((N + 127) / 128) * ((K + 127) / 128);
+  const long tiles = tn_narrow_shape(N, K) ? (K + 255) / 256
+                     : (N <= 64 && K <= 64) ? 1 : (long)((N + 127) / 128) * ((K + 127) / 128);
   // enough (tile, split) CTAs for ~2 per CU, but >= 1024 rows per split so the fp32 partial
   // planes stay small next to the operand traffic (wgrad_finalize reads them all back)
   long s = 512 / (tiles > 0 ? tiles : 1);
@@ -2167,7 +2175,9 @@ extern "C" int kair_wgrad_splits(long M, int N, int K) {
     if (g_num_cus == 0) init_num_cus();
     s = g_num_cus / ((K + 127) / 128);
   }
-  const long maxs = (M + 1023) / 1024;
+  // (narrow tiles: >= 512 rows -- their partial planes are 1/4 the size, and the half-as-many tiles
+  // need the splits to fill the CUs)
+  const long maxs = tn_narrow_shape(N, K) ? (M + 511) / 512 : (M + 1023) / 1024;
   if (s > maxs) s = maxs;
   if (s < 1) s = 1;
   return (int)s;
