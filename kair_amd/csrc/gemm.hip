@@ -2003,6 +2003,7 @@ static bool tn192_shape(int N, int K) { return N > 128 && N <= 192 && K > 128; }
 // narrow weight gradients (N <= 32 output channels, e.g. RRDB's growth-32 dense-block convs): a
 // 128 x 128 tile would be 3/4 empty along N; a 32 x 256 one does the same work in half the tiles
 static bool tn_narrow_shape(int N, int K) { return N <= 32 && K > 64; }
+static bool tn_narrow64_shape(int N, int K) { return N > 32 && N <= 64 && K > 64; }
 
 template <typename CT, typename TA, typename TB, int AMA, int AMB>
 int launch_tn(const Op& a, const Op& b, float* ws, int splits, long M, int N, int K, long rps, hipStream_t s) {
@@ -2013,6 +2014,10 @@ int launch_tn(const Op& a, const Op& b, float* ws, int splits, long M, int N, in
   } else if (tn_narrow_shape(N, K)) {   // N <= 32 (dense-block growth convs): one 32 x 256 tile, no 3/4-empty N
     const int tilesK = (K + 255) / 256;
     hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 32, 256>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
+                       ws, M, N, K, rps, tilesK);
+  } else if (tn_narrow64_shape(N, K)) {   // 32 < N <= 64: one 64 x 128 tile, no half-empty 128-wide N
+    const int tilesK = (K + 127) / 128;
+    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 64, 128>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
                        ws, M, N, K, rps, tilesK);
   } else if (N <= 64 && K <= 64) {
     const int tilesN = (N + 63) / 64, tilesK = (K + 63) / 64;
@@ -2177,7 +2182,7 @@ extern "C" int kair_wgrad_splits(long M, int N, int K) {
   }
   // (narrow tiles: >= 512 rows -- their partial planes are 1/4 the size, and the half-as-many tiles
   // need the splits to fill the CUs)
-  const long maxs = tn_narrow_shape(N, K) ? (M + 511) / 512 : (M + 1023) / 1024;
+  const long maxs = tn_narrow_shape(N, K) || tn_narrow64_shape(N, K) ? (M + 511) / 512 : (M + 1023) / 1024;
   if (s > maxs) s = maxs;
   if (s < 1) s = 1;
   return (int)s;

@@ -213,7 +213,7 @@ def test_conv_pixelshuffle_and_nchw(compute):
 @pytest.mark.parametrize("in_data", [False, True])
 @pytest.mark.parametrize("compute", [H.F32, H.BF16])
 @pytest.mark.parametrize("M,N,K", [(5000, 576, 192), (4096, 64, 64), (777, 192, 384), (2000, 384, 200),
-                                   (3000, 32, 576), (1500, 24, 152)])
+                                   (3000, 32, 576), (1500, 24, 152), (2500, 64, 1728)])
 def test_gemm_tn_wgrad(compute, M, N, K, in_data):
     """in_data=True: the ones column is stored by the producer (bf16: the LDS-DMA ring kernel)."""
     g = torch.Generator().manual_seed(11)
