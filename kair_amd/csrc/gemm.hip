@@ -2011,6 +2011,9 @@ int launch_tn(const Op& a, const Op& b, float* ws, int splits, long M, int N, in
     const int tilesK = (K + 127) / 128;
     hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 192, 128>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
                        ws, M, N, K, rps, tilesK);
+  } else if (tn_narrow_shape(N, K) && K <= 160) {   // e.g. 16 -> 16-channel 3x3 convs (K = 144): one 32 x 160 tile
+    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 32, 160>), dim3(1, splits), dim3(NT), 0, s, a, b,
+                       ws, M, N, K, rps, 1);
   } else if (tn_narrow_shape(N, K)) {   // N <= 32 (dense-block growth convs): one 32 x 256 tile, no 3/4-empty N
     const int tilesK = (K + 255) / 256;
     hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 32, 256>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
