@@ -398,7 +398,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--global-batch", type=int, default=32)
     ap.add_argument("--per-gpu-batch", type=int, default=None, help="weak scaling: fixed batch per GPU")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--drop-path", type=float, default=0.1)
@@ -515,7 +515,7 @@ def main():
     value = gbatch * args.steps / wall
     ms_step = 1000.0 * wall / args.steps
     step_tflops = fl["train"] * gbatch / (wall / args.steps) / 1e12 / world   # per GPU
-    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    peak = PEAK_F32_TFLOPS if args.dtype == "fp32" else PEAK_BF16_TFLOPS
     roles, serial = {}, {}
     if not args.no_roles:
         try:
@@ -523,7 +523,7 @@ def main():
             serial = time_roles(tr, serial=True)
         except Exception as e:  # noqa: BLE001
             roles = serial = {"error": {"kernel": repr(e), "ms_total": 0.0}}
-    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    peak = PEAK_F32_TFLOPS if args.dtype == "fp32" else PEAK_BF16_TFLOPS
     TIMING = {"in_step": "in-step mean over the step's launches of this role: one eager fwd+loss+bwd, a HIP event pair "
                          "on the launch stream around each launch (side-stream concurrency kept, so a launch queued "
                          "behind side-stream work includes that wait)",

@@ -28,7 +28,17 @@ extern "C" {
 #define KAIR_ERR_ARG (-1)
 #define KAIR_ERR_HIP (-2)
 
-typedef enum { KAIR_F32 = 0, KAIR_BF16 = 1 } kair_dtype;
+typedef enum { KAIR_F32 = 0, KAIR_BF16 = 1, KAIR_F16 = 3 } kair_dtype;
+/* `compute` of kair_gemm_nt / kair_gemm_tn besides the dtypes: the split-fp16 ("x3") arithmetic of the
+ * fp32 engine on the 16-bit matrix cores.  Every operand x enters as a pair of fp16 values of x * 2^e
+ * (hi = f16(x 2^e), lo = f16(x 2^e - hi); e = kair_operand.x3_exp, a power-of-2 scale that centres the
+ * operand in fp16's range) and every product as hi.hi + hi.lo + lo.hi with fp32 accumulation, rescaled by
+ * 2^-(eA + eB): ~2^-21 relative per product, the precision class of fp32 arithmetic (one bf16 product:
+ * 2^-8; bf16 pairs: 2^-16).  Operands: fp32 (split in the kernel) or fp16 hi planes with
+ * kair_operand.lo_ptr (their stored values carry x3_exp).  Packed weights (kinds 9 / 17 / 18 / 19 with an
+ * fp16 destination) hold w * 2^KAIR_X3_WEXP. */
+#define KAIR_COMPUTE_X3 2
+#define KAIR_X3_WEXP 12
 
 /* How a GEMM operand element (row m, column k) is addressed. */
 typedef enum {
@@ -74,7 +84,10 @@ typedef struct {
                           halves of one activation and B is packed tied over both halves (kair_wmap
                           kG = 2), so the plain product is already the split one; the flag lets
                           the 3x3 halo kernel skip the negligible lo . w_lo chunk products   */
-  const void* lo_ptr;  /* bf16 A with a_split: the lo plane (kair_epilogue.out_lo of its producer) */
+  const void* lo_ptr;  /* bf16 A with a_split: the lo plane (kair_epilogue.out_lo of its producer);
+                          x3 compute: the lo plane of an fp16 operand                           */
+  int x3_exp;          /* x3 compute: the operand's power-of-2 exponent (fp32: applied before the fp16
+                          split; fp16 planes: carried by the stored values); packed weights KAIR_X3_WEXP */
 } kair_operand;
 
 typedef enum {
@@ -127,7 +140,9 @@ typedef struct {
   void* out_lo;                         /* optional, bf16 `out` in ROWS / PSHUF_SPM mode: the lo plane
                                            lo = bf16(v - bf16(v)) at the same offsets, so the next
                                            conv can read the activation as a hi/lo pair
-                                           (kair_operand.a_split)                                  */
+                                           (kair_operand.a_split); x3 compute with an fp16 `out` (ROWS /
+                                           QKVBLK): the fp16 lo plane of v * 2^x3_out_exp          */
+  int x3_out_exp;                       /* x3 compute, fp16 out: the stored pair holds v * 2^x3_out_exp */
 } kair_epilogue;
 
 /* C[m,n] = sum_k A[m,k] * B[n,k]  (+ epilogue).  compute: KAIR_BF16 -> v_mfma_f32_16x16x32_bf16,
@@ -300,6 +315,21 @@ int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo, const void
                             const float* table, const float* lse, void* dqkv, int dqkv_rows, float* dtable,
                             int dtable_accumulate, float* ws, long nWin, int nh, int hd, float scale, int H, int W,
                             int shift, const float* mask, int mask_nw, void* stream);
+
+/* Split-fp16 ("x3", KAIR_COMPUTE_X3) window attention: the fp32 reference's arithmetic on the 16-bit
+ * matrix cores.  Every tensor is an fp16 pair of planes holding x 2^e (hi = f16(x 2^e), lo = f16(x 2^e -
+ * hi)) in the bf16 layouts above and every product hi.hi + hi.lo + lo.hi.  fwd: qkv / qkv_lo head-blocked
+ * (exponent e_in), O / O_lo rows (written with e_out), lse fp32.  bwd: q/k/v and O carry e_act, dO carries
+ * e_grad and dqkv / dqkv_lo are written with e_grad as token rows [nWin*64][3*nh*32] (window order,
+ * column (part*nh + h)*32 + d); dtable (natural units) as kair_window_attn_bwd (NULL: partials left in ws
+ * for kair_attn_dtable_grouped with dtype KAIR_COMPUTE_X3). */
+int kair_window_attn_fwd_x3(const void* qkv, const void* qkv_lo, const float* table, void* O, void* O_lo, long ldo,
+                            float* lse, long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
+                            int e_in, int e_out, void* stream);
+int kair_window_attn_bwd_x3(const void* qkv, const void* qkv_lo, const void* O, const void* O_lo, long ldo,
+                            const void* dO, const void* dO_lo, long lddo, const float* table, const float* lse,
+                            void* dqkv, void* dqkv_lo, float* dtable, int dtable_accumulate, float* ws, long nWin,
+                            int nh, int hd, float scale, int H, int W, int shift, int e_act, int e_grad, void* stream);
 
 /* Deferred bias-table gradient: kair_window_attn_bwd with dtable = NULL leaves its per-group
  * partials (kair_window_attn_bwd_groups() planes of [nh][225]) in ws; one grouped launch then

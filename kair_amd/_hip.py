@@ -16,7 +16,9 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
                                                                                           "libkair_hip.so"))
 # KAIR_LIB=base: an A/B baseline library (same ABI, earlier sources) placed there by hand; never shipped
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 3
+X3 = 2   # KAIR_COMPUTE_X3: split-fp16 arithmetic (hi.hi + hi.lo + lo.hi of power-of-2-scaled fp16 pairs)
+X3_WEXP = 12   # KAIR_X3_WEXP: the exponent of the fp16 weight packs
 LD_ROWS, LD_IM2COL3, LD_QKVBLK, LD_S2D = 0, 1, 2, 3
 USR_SRC_NCHW, USR_SRC_PSF, USR_SRC_ZUP, USR_SRC_NHWC = 0, 1, 2, 3
 USR_COL_FB, USR_COL_FBFY, USR_COL_DATA_FWD, USR_COL_DATA_BWD = 0, 1, 2, 3
@@ -35,7 +37,7 @@ class Operand(ctypes.Structure):
                 ("im_H", c_int), ("im_W", c_int), ("im_C", c_int), ("im_flip", c_int),
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
                 ("rowscale", c_vp), ("rows_per_scale", c_int), ("ones_col", c_int), ("ones_in_data", c_int),
-                ("im_up", c_int), ("w_split", c_int), ("a_split", c_int), ("lo_ptr", c_vp)]
+                ("im_up", c_int), ("w_split", c_int), ("a_split", c_int), ("lo_ptr", c_vp), ("x3_exp", c_int)]
 
 
 class CopyDesc(ctypes.Structure):
@@ -67,7 +69,8 @@ class Epilogue(ctypes.Structure):
                 ("qkv_nh", c_int), ("qkv_hdp", c_int), ("qkv_tok", c_int),
                 ("img_mean", c_vp), ("img_range", c_float), ("img_C", c_int), ("img_H", c_int), ("img_W", c_int),
                 ("out_ones_col_p1", c_int), ("resid2", c_vp), ("ldr2", c_long), ("pre_kind", c_int),
-                ("a_copy", c_vp), ("ld_acopy", c_long), ("acopy_ones_col_p1", c_int), ("out_lo", c_vp)]
+                ("a_copy", c_vp), ("ld_acopy", c_long), ("acopy_ones_col_p1", c_int), ("out_lo", c_vp),
+                ("x3_out_exp", c_int)]
 
 
 class WMap(ctypes.Structure):
@@ -184,6 +187,10 @@ _SIGS = {
     "kair_rowgemm_ln_blocks": [c_long, c_int],
     "kair_rowgemm_lnbwd": [c_vp, c_long, c_long, c_int, c_vp, c_vp, c_long, c_vp, c_vp, c_vp, c_int, c_vp, c_long,
                            c_int, c_int, c_int, c_int, ctypes.POINTER(CopyDesc), c_vp, c_vp],
+    "kair_window_attn_fwd_x3": [c_vp, c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_long, c_int, c_int, c_float, c_int, c_int,
+                                c_int, c_int, c_int, c_int, c_vp],
+    "kair_window_attn_bwd_x3": [c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_vp, c_long, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                c_vp, c_long, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_int, c_vp],
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
@@ -236,6 +243,8 @@ def dtype_code(t):
         return F32
     if t.dtype == torch.bfloat16:
         return BF16
+    if t.dtype == torch.float16:
+        return F16
     raise TypeError(f"unsupported dtype {t.dtype}")
 
 
@@ -541,6 +550,31 @@ def window_attn_bwd(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc,
     check(lib().kair_window_attn_bwd_ex(ptr(qkv), ptr(O), ldo, ptr(dO), lddo, dtype_code(qkv), ptr(table), ptr(lse),
                                         ptr(dqkv), int(dqkv_rows), ptr(dtable), int(dtable_acc), ptr(ws), nWin, nh, hd,
                                         scale, H, W, shift, ptr(mask), mnw, stream_ptr()), "window_attn_bwd")
+
+
+def window_attn_fwd_x3(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, ones_col=-1, e_in=0, e_out=0):
+    """Split-fp16 window attention forward: qkv / O are [2, ...] fp16 (hi plane, lo plane) of x 2^e."""
+    check(lib().kair_window_attn_fwd_x3(ptr(qkv[0]), ptr(qkv[1]), ptr(table), ptr(O[0]), ptr(O[1]), ldo, ptr(lse), nWin,
+                                        nh, hd, scale, H, W, shift, ones_col, e_in, e_out, stream_ptr()),
+          "window_attn_fwd_x3")
+
+
+def window_attn_bwd_x3(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc, ws, nWin, nh, hd, scale, H, W, shift,
+                       e_act=0, e_grad=0):
+    """Split-fp16 window attention backward: qkv, O, dO and dqkv (token rows [M][3 nh 32]) are [2, ...] fp16 planes;
+    q/k/v and O carry e_act, dO and dqkv e_grad."""
+    check(lib().kair_window_attn_bwd_x3(ptr(qkv[0]), ptr(qkv[1]), ptr(O[0]), ptr(O[1]), ldo, ptr(dO[0]), ptr(dO[1]), lddo,
+                                        ptr(table), ptr(lse), ptr(dqkv[0]), ptr(dqkv[1]), ptr(dtable), int(dtable_acc),
+                                        ptr(ws), nWin, nh, hd, scale, H, W, shift, e_act, e_grad, stream_ptr()),
+          "window_attn_bwd_x3")
+
+
+def with_lo(op, lo):
+    """Attach the lo plane of a 16-bit operand pair (split-fp16 GEMMs of kair_gemm_nt / kair_gemm_tn compute X3;
+    the bf16 engine's a_split)."""
+    op.lo_ptr = ptr(lo)
+    op._keep = (op._keep, lo)
+    return op
 
 
 def conv3x3_narrow_fwd(x, ldx, lo_off, w, bias, NR, mean, img_range, resid, out, B, H, W):

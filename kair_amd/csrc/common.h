@@ -11,6 +11,13 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) short short4v;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef _Float16 f16;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+// 8-wide vector of a 16-bit element type (bf16 / fp16)
+template <typename T> struct V8;
+template <> struct V8<__bf16> { typedef bf16x8 t; };
+template <> struct V8<_Float16> { typedef f16x8 t; };
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 #define KAIR_DEV __device__ __forceinline__
@@ -276,3 +283,16 @@ struct FinGroup {
   long nblocks;
 };
 int kair_launch_finalize_grouped(const FinGroup& g, hipStream_t s);
+
+// split-bf16 window attention (attn_x3.hip): windows per backward wave, and the bias-table partial sum
+// shared with window_attn.hip
+long kair_attn_x3_wpg(long nWin, int nh);
+int kair_attn_dtable_sum(const float* ws, long ngroups, int nh, float* dtable, int accumulate, hipStream_t s);
+
+// split-fp16 GEMMs (gemm_x3.hip), reached through kair_gemm_nt / kair_gemm_tn with compute KAIR_COMPUTE_X3,
+// and the operand validation they share with gemm.hip
+int kair_check_operand(const kair_operand* o, const char* what);
+int kair_gemm_nt_x3(const kair_operand* A, const kair_operand* B, const kair_epilogue* E, long M, int N, int K,
+                    void* stream);
+int kair_gemm_tn_x3(const kair_operand* A, const kair_operand* B, float* ws, int splits, long M, int N, int K,
+                    void* stream);

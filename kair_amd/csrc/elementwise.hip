@@ -27,7 +27,53 @@ KAIR_DEV int nperm_inv(const kair_wmap& mp, int co) {  // reference -> packed (u
   return (co % mp.n_perm) * nf + co / mp.n_perm;
 }
 
+// Row geometry of the split forms 17 / 18 / 19 (hi/lo pairs of kinds 0 / 2 / 3, kair_wmap): the plain
+// form's row length and the kind it splits
+__host__ __device__ inline void split_rows(const kair_wmap& mp, int* base, long* rowlen, long* rows) {
+  const long Np = (long)mp.nG * mp.nGp, Kp = (long)mp.kG * mp.kGp;
+  if (mp.kind == 17) { *base = 0; *rowlen = Kp; *rows = Np; }
+  else if (mp.kind == 18) { *base = 2; *rowlen = 9 * Np; *rows = Kp; }
+  else { *base = 3; *rowlen = Np; *rows = Kp; }
+}
+
+// Reference value of element t of a plain linear / conv-dgrad / transposed-linear form (kinds 0, 2, 3)
+KAIR_DEV float pack_value(const float* __restrict__ src, const kair_wmap& mp, int kind, long t) {
+  const int Np = mp.nG * mp.nGp, Kp = mp.kG * mp.kGp;
+  if (kind == 2) {
+    const int cip = (int)(t / (9 * Np));
+    const int kk = (int)(t - (long)cip * 9 * Np);
+    const int tap = kk / Np, cop = kk - tap * Np;
+    const int n = nperm_fwd(mp, unpad(cop, mp.nG, mp.nGr, mp.nGp)), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
+    return (n >= 0 && ci >= 0) ? src[((long)n * mp.K + ci) * 9 + tap] : 0.f;
+  }
+  int np, kp;
+  if (kind == 0) { np = (int)(t / Kp); kp = (int)(t - (long)np * Kp); }
+  else { kp = (int)(t / Np); np = (int)(t - (long)kp * Np); }
+  const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), k = unpad(kp, mp.kG, mp.kGr, mp.kGp);
+  return (n >= 0 && k >= 0) ? src[(long)n * mp.K + k] : 0.f;
+}
+
 KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst, int dt, const kair_wmap& mp, long t) {
+  if (mp.kind >= 17 && mp.kind <= 19) {   // hi/lo split rows: 64-column chunks alternate hi / lo
+    int base;
+    long rowlen, rows;
+    split_rows(mp, &base, &rowlen, &rows);
+    const long KS = 2 * ((rowlen + 63) / 64) * 64;
+    const long row = t / KS;
+    const long kk = t - row * KS;
+    const int half = (int)((kk >> 6) & 1);
+    const long k = ((kk >> 7) << 6) + (kk & 63);
+    const float v = k < rowlen ? pack_value(src, mp, base, row * rowlen + k) : 0.f;
+    if (dt == KAIR_F16) {   // x3 weights: the fp16 pair of w * 2^KAIR_X3_WEXP
+      const float w = ldexpf(v, KAIR_X3_WEXP);
+      const f16 hi = (f16)w;
+      ((f16*)dst)[t] = half ? (f16)(w - (float)hi) : hi;
+      return;
+    }
+    const bf16 hi = (bf16)v;
+    ((bf16*)dst)[t] = half ? (bf16)(v - (float)hi) : hi;
+    return;
+  }
   const int Np = mp.nG * mp.nGp, Kp = mp.kG * mp.kGp;
   float v = 0.f;
   if (mp.kind == 0 || mp.kind == 3) {  // linear [Np][Kp] (or transposed [Kp][Np])
@@ -63,6 +109,12 @@ KAIR_DEV void pack_element(const float* __restrict__ src, void* __restrict__ dst
       const int tap = k / Kp, cip = k - tap * Kp;
       const int n = nperm_fwd(mp, unpad(np, mp.nG, mp.nGr, mp.nGp)), ci = unpad(cip, mp.kG, mp.kGr, mp.kGp);
       if (n >= 0 && ci >= 0) v = src[((long)n * mp.K + ci % mp.K) * 9 + tap];   // % K: tied in-dim copies
+    }
+    if (dt == KAIR_F16) {   // x3 weights: the fp16 pair of w * 2^KAIR_X3_WEXP
+      const float w = ldexpf(v, KAIR_X3_WEXP);
+      const f16 hf = (f16)w;
+      ((f16*)dst)[t] = half ? (f16)(w - (float)hf) : hf;
+      return;
     }
     const bf16 hi = (bf16)v;
     ((bf16*)dst)[t] = half ? (bf16)(v - (float)hi) : hi;
@@ -639,8 +691,13 @@ inline unsigned nblk(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 }  // namespace
 
 static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
-  KAIR_CHECK_ARG((mp.kind != 9 && mp.kind != 12 && mp.kind != 15) || dst_dtype == KAIR_BF16,
-                 "pack_weight: the hi/lo split forms (kinds 9, 12, 15) are bf16 only");
+  KAIR_CHECK_ARG((mp.kind != 12 && mp.kind != 15) || dst_dtype == KAIR_BF16,
+                 "pack_weight: the hi/lo split forms 12 / 15 are bf16 only");
+  KAIR_CHECK_ARG(mp.kind != 9 || dst_dtype == KAIR_BF16 || dst_dtype == KAIR_F16,
+                 "pack_weight: kind 9 is a bf16 or (x3) fp16 pair form");
+  KAIR_CHECK_ARG(dst_dtype == KAIR_F32 || dst_dtype == KAIR_BF16 || ((mp.kind == 9 || (mp.kind >= 17 && mp.kind <= 19)) &&
+                                                                     dst_dtype == KAIR_F16),
+                 "pack_weight: fp16 destinations are the x3 pair forms (kinds 9, 17, 18, 19)");
   KAIR_CHECK_ARG(mp.nG > 0 && mp.nGr > 0 && mp.nGp >= mp.nGr && mp.nG * mp.nGr == mp.N, "pack_weight: bad N map");
   // kinds 1 / 9 (conv forward) may repeat the in dim (kG * kGr a multiple of K: tied copies, e.g. the
   // hi / lo halves of a split input image); every other kind maps it one to one
@@ -657,6 +714,14 @@ static int pack_total(const kair_wmap& mp, int dst_dtype, long* total) {
   KAIR_CHECK_ARG(mp.kind != 14 || (Np % 16 == 0 && Kp % 32 == 0), "pack_weight: 16x16x32 fragment order needs Np %% 16 == 0, Kp %% 32 == 0");
   KAIR_CHECK_ARG(mp.kind != 15 || (Np % 16 == 0 && (9 * Kp) % 32 == 0), "pack_weight: kind 15 needs Np %% 16 == 0, 9 Kp %% 32 == 0");
   KAIR_CHECK_ARG(mp.kind != 16 || (Kp % 16 == 0 && (9 * Np) % 32 == 0), "pack_weight: kind 16 needs Kp %% 16 == 0, 9 Np %% 32 == 0");
+  if (mp.kind >= 17 && mp.kind <= 19) {   // hi/lo split rows of kinds 0 / 2 / 3
+    KAIR_CHECK_ARG(dst_dtype == KAIR_BF16 || dst_dtype == KAIR_F16, "pack_weight: kinds 17-19 are bf16 / fp16 pairs");
+    int base;
+    long rowlen, rows;
+    split_rows(mp, &base, &rowlen, &rows);
+    *total = rows * 2 * ((rowlen + 63) / 64) * 64;
+    return 0;
+  }
   if (mp.kind == 0 || mp.kind == 3 || mp.kind == 10 || mp.kind == 13 || mp.kind == 14) *total = Np * Kp;
   else if (mp.kind == 12) *total = 2 * Np * Kp;
   else if (mp.kind == 1 || mp.kind == 2 || mp.kind == 16) *total = Np * 9 * Kp;

@@ -20,457 +20,9 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "common.h"
+#include "gemm_common.h"
 
 namespace {
-
-constexpr int NT = 256;
-enum { AM_ROWS = 0, AM_IM2COL = 1, AM_QKV = 2, AM_S2D = 3 };
-
-template <typename CT> struct KStep { static constexpr int BK = sizeof(CT) == 2 ? 64 : 32; };
-
-// ------------------------------------------------------------------------------------------
-// operand description (trimmed copy of kair_operand, passed by value)
-// ------------------------------------------------------------------------------------------
-struct Op {
-  const void* ptr;
-  long ld;
-  WinMap win;
-  int imH, imW, imC, flip;
-  int up_sh;   // IM2COL: log2 of the nearest-upsample factor (source image imH>>up_sh x imW>>up_sh)
-  int nh, hdp, tok;
-  const float* rowscale;
-  int rps;
-  int ones_col;
-  int ones_in_data;
-  long M;  // rows of this operand
-  int wsplit;  // B only: hi/lo bf16 weight pairs interleaved per 64 columns (kair_operand.w_split)
-  int asplit;  // A only: the activation as a hi/lo bf16 pair (kair_operand.a_split)
-  const void* lo_ptr;   // bf16 A with asplit: the lo plane
-  FDiv d_rps, d_imC, d_imW, d_hw, d_tok, d_hdp, d_pw;
-};
-
-Op make_op(const kair_operand& o, long M) {
-  Op op;
-  op.ptr = o.ptr; op.ld = o.ld;
-  op.win = make_winmap(o.win_H, o.win_W, o.win_ws, o.win_shift);
-  op.imH = o.im_H; op.imW = o.im_W; op.imC = o.im_C; op.flip = o.im_flip;
-  op.up_sh = o.im_up == 2 ? 1 : 0;
-  if ((o.mode == KAIR_LD_IM2COL3 || o.mode == KAIR_LD_S2D) && op.ld == 0) op.ld = o.im_C;
-  op.nh = o.qkv_nh; op.hdp = o.qkv_hdp; op.tok = o.qkv_tok;
-  op.rowscale = o.rowscale; op.rps = o.rows_per_scale > 0 ? o.rows_per_scale : 1;
-  op.ones_col = o.ones_col;
-  op.ones_in_data = o.ones_in_data;
-  op.M = M;
-  op.wsplit = o.w_split ? 1 : 0;
-  op.asplit = o.a_split;   // 0, 1 or 2 (kair_operand.a_split)
-  op.lo_ptr = o.lo_ptr;
-  op.d_rps = make_fdiv(op.rps);
-  op.d_imC = make_fdiv(op.imC); op.d_imW = make_fdiv(op.imW); op.d_hw = make_fdiv(op.imH * op.imW);
-  op.d_tok = make_fdiv(op.tok); op.d_hdp = make_fdiv(op.hdp); op.d_pw = make_fdiv(op.nh * op.hdp);
-  return op;
-}
-
-KAIR_DEV void zero8(float (&v)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = 0.f;
-}
-
-template <typename T>
-KAIR_DEV void gload8(const T* p, float (&v)[8]) {
-  if constexpr (sizeof(T) == 2) {
-    const bf16x8 q = *(const bf16x8*)p;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
-  } else {
-    const float4 a = *(const float4*)p;
-    const float4 b = *(const float4*)(p + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  }
-}
-
-// Per-chunk row state: resolved once before the K loop.
-struct RowState {
-  long base;   // element offset of the row start (ROWS) / pixel index (IM2COL) / token offset (QKV)
-  int y, x;    // IM2COL pixel coordinates
-  float scale;
-  bool valid;
-};
-
-template <int AM, typename T>
-KAIR_DEV RowState row_state(const Op& op, long m) {
-  RowState r;
-  r.valid = m < op.M;
-  r.scale = 1.f;
-  r.y = r.x = 0;
-  r.base = 0;
-  if (!r.valid) return r;
-  if constexpr (AM == AM_ROWS) {
-    const long t = win_to_token(m, op.win);
-    r.base = t * op.ld;
-    if (op.rowscale) r.scale = op.rowscale[fdiv((int)t, op.d_rps)];
-  } else if constexpr (AM == AM_IM2COL) {
-    const int hw = op.d_hw.d;
-    const int b = fdiv((int)m, op.d_hw);
-    const int p = (int)m - b * hw;
-    r.y = fdiv(p, op.d_imW);
-    r.x = p - r.y * op.imW;
-    r.base = (long)b * (hw >> (2 * op.up_sh));   // first pixel of image b in the SOURCE image
-  } else if constexpr (AM == AM_S2D) {
-    const int hw = op.d_hw.d;
-    const int b = fdiv((int)m, op.d_hw);
-    const int p = (int)m - b * hw;
-    r.y = fdiv(p, op.d_imW);
-    r.x = p - r.y * op.imW;
-    r.base = (long)b * (4L * hw);                // the source image is 2H x 2W
-  } else {
-    const int win = fdiv((int)m, op.d_tok);
-    const int t = (int)m - win * op.tok;
-    r.base = ((long)win * op.nh * op.tok + t) * op.hdp;
-    if (op.rowscale) r.scale = op.rowscale[fdiv((int)m, op.d_rps)];
-  }
-  return r;
-}
-
-// Two-phase chunk loads: issue() computes the address of 8 consecutive columns [k, k+8) of a
-// resolved row and starts the global load into raw registers WITHOUT consuming it (invalid chunks
-// load from the buffer start and are masked later); commit() converts / masks / scales and writes
-// LDS after the MFMAs of the current step, so the load latency overlaps them.
-template <typename T> struct Raw;
-template <> struct Raw<bf16> { uint4 a; };
-template <> struct Raw<float> { uint4 a, b; };
-
-struct Pend {
-  float scale;   // 0 => masked chunk
-  int ones;      // index in [0, 8) of the fused ones column, else -1
-};
-
-template <typename T>
-KAIR_DEV void raw_load(const T* p, Raw<T>& r) {
-  if constexpr (sizeof(T) == 2) {
-    r.a = *(const uint4*)p;
-  } else {
-    r.a = *(const uint4*)p;
-    r.b = *(const uint4*)(p + 4);
-  }
-}
-
-template <int AM, typename T>
-KAIR_DEV void issue_chunk(const Op& op, const RowState& r, int k, int K, Raw<T>& raw, Pend& pd,
-                          const void* base = nullptr) {
-  bool ok = r.valid && k < K;
-  long off = 0;
-  if constexpr (AM == AM_ROWS) {
-    off = r.base + k;
-  } else if constexpr (AM == AM_IM2COL) {
-    const int tap = fdiv(k, op.d_imC);
-    const int c = k - tap * op.imC;
-    int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-    if (op.flip) { dy = -dy; dx = -dx; }
-    const int y = r.y + dy, x = r.x + dx;
-    ok = ok && y >= 0 && y < op.imH && x >= 0 && x < op.imW;
-    off = (r.base + (long)(y >> op.up_sh) * (op.imW >> op.up_sh) + (x >> op.up_sh)) * op.ld + c;
-  } else if constexpr (AM == AM_S2D) {
-    const int tap = fdiv(k, op.d_imC);
-    const int c = k - tap * op.imC;
-    const int y = 2 * r.y + (tap >> 1), x = 2 * r.x + (tap & 1);
-    off = (r.base + (long)y * (2 * op.imW) + x) * op.ld + c;
-  } else {
-    const int pw = op.d_pw.d;
-    const int part = fdiv(k, op.d_pw);
-    const int rr = k - part * pw;
-    const int h = fdiv(rr, op.d_hdp), d = rr - h * op.hdp;
-    off = (long)part * op.M * pw + r.base + (long)h * op.tok * op.hdp + d;
-  }
-  raw_load<T>((const T*)(base ? base : op.ptr) + (ok ? off : 0), raw);
-  pd.scale = ok ? r.scale : 0.f;
-  pd.ones = (r.valid && op.ones_col >= k && op.ones_col < k + 8) ? op.ones_col - k : -1;
-}
-
-template <typename T>
-KAIR_DEV void raw_to_f32(const Raw<T>& r, float (&v)[8]) {
-  if constexpr (sizeof(T) == 2) {
-    const bf16x8 q = __builtin_bit_cast(bf16x8, r.a);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
-  } else {
-    const float4 a = __builtin_bit_cast(float4, r.a), b = __builtin_bit_cast(float4, r.b);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  }
-}
-
-// lo (fp32 source, bf16 compute): store the lo half bf16(x - bf16(x)) of the (scaled) value instead
-template <typename CT, typename T>
-KAIR_DEV void commit_chunk(CT* dst, const Raw<T>& raw, const Pend& pd, bool lo = false) {
-  if constexpr (sizeof(CT) == 2 && sizeof(T) == 2) {
-    if (pd.scale == 1.f && pd.ones < 0) {          // common case: raw bf16 straight to LDS
-      *(uint4*)dst = raw.a;
-      return;
-    }
-    if (pd.scale == 0.f && pd.ones < 0) {
-      *(uint4*)dst = make_uint4(0, 0, 0, 0);
-      return;
-    }
-  }
-  float v[8];
-  raw_to_f32<T>(raw, v);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (j == pd.ones) ? 1.f : (pd.scale == 0.f ? 0.f : v[j] * pd.scale);
-  if constexpr (sizeof(CT) == 2) {
-    bf16x8 q;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) q[j] = lo ? (bf16)(v[j] - (float)(bf16)v[j]) : (bf16)v[j];
-    *(bf16x8*)dst = q;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) *(float2*)(dst + j) = make_float2(v[j], v[j + 1]);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// epilogue
-// ------------------------------------------------------------------------------------------
-struct Epi {
-  void* out; int odt, omode; long ldo;
-  WinMap win;
-  const float* bias;
-  int act; float slope;
-  void* pre; int pdt; long ldp;
-  const float* resid; long ldr;
-  const float* rowscale; int rps;
-  const void* gate; int gdt; long ldg; int gkind;
-  int prek;   // 1: pre receives act'(x) (GELU)
-  int r, psH, psW;
-  int nh, hdp, tok;
-  const float* mean; float range; int imgC, imgH, imgW;
-  int ones_col;   // -1 none
-  const float* resid2; long ldr2;
-  bf16* acopy; long ldac; int acones;   // halo conv: bf16 copy of the A image (acones: 1.0 channel, -1 none)
-  bf16* out_lo;                         // bf16 ROWS / PSHUF_SPM out: lo plane bf16(v - bf16(v))
-  long M; int N;
-  FDiv d_rps, d_tok, d_hdp, d_pw;
-  int dbg;   // ring-kernel ablation bits (KAIR_RING_DBG, perf investigation only): 1 no stores, 2 no MFMA, 4 no A loads
-};
-
-Epi make_epi(const kair_epilogue& o, long M, int N) {
-  Epi e;
-  e.out = o.out; e.odt = o.out_dtype; e.omode = o.out_mode; e.ldo = o.ldo;
-  e.win = make_winmap(o.win_H, o.win_W, o.win_ws, o.win_shift);
-  e.bias = o.bias; e.act = o.act; e.slope = o.slope;
-  e.pre = o.out_pre; e.pdt = o.pre_dtype; e.ldp = o.ldp;
-  e.resid = o.resid; e.ldr = o.ldr;
-  e.rowscale = o.rowscale; e.rps = o.rows_per_scale > 0 ? o.rows_per_scale : 1;
-  e.gate = o.gate; e.gdt = o.gate_dtype; e.ldg = o.ldg; e.gkind = o.gate_kind;
-  e.prek = o.pre_kind;
-  e.r = o.ps_r; e.psH = o.ps_H; e.psW = o.ps_W;
-  e.nh = o.qkv_nh; e.hdp = o.qkv_hdp; e.tok = o.qkv_tok;
-  e.mean = o.img_mean; e.range = o.img_range; e.imgC = o.img_C; e.imgH = o.img_H; e.imgW = o.img_W;
-  e.ones_col = o.out_ones_col_p1 - 1;
-  e.resid2 = o.resid2; e.ldr2 = o.ldr2;
-  e.acopy = (bf16*)o.a_copy; e.ldac = o.ld_acopy; e.acones = o.acopy_ones_col_p1 - 1;
-  e.out_lo = (bf16*)o.out_lo;
-  e.M = M; e.N = N;
-  e.d_rps = make_fdiv(e.rps); e.d_tok = make_fdiv(e.tok); e.d_hdp = make_fdiv(e.hdp); e.d_pw = make_fdiv(e.nh * e.hdp);
-  static const int dbg = kair_dbg_env("KAIR_RING_DBG");
-  e.dbg = dbg;
-  return e;
-}
-
-KAIR_DEV void load8_any(const void* p, int dt, long off, float (&v)[8]) {
-  if (dt == KAIR_BF16) gload8<bf16>((const bf16*)p + off, v);
-  else gload8<float>((const float*)p + off, v);
-}
-KAIR_DEV void store8_any(void* p, int dt, long off, const float (&v)[8]) {
-  if (dt == KAIR_BF16) {
-    bf16x8 q;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) q[j] = (bf16)v[j];
-    *(bf16x8*)((bf16*)p + off) = q;
-  } else {
-    float* d = (float*)p + off;
-    *(float4*)d = make_float4(v[0], v[1], v[2], v[3]);
-    *(float4*)(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
-  }
-}
-// the lo plane of 8 values stored as bf16 hi: bf16(v - bf16(v))
-KAIR_DEV void store8_lo(bf16* p, long off, const float (&v)[8]) {
-  bf16x8 q;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) q[j] = (bf16)(v[j] - (float)(bf16)v[j]);
-  *(bf16x8*)(p + off) = q;
-}
-KAIR_DEV void st1(void* p, int dt, long off, float v) {
-  if (dt == KAIR_BF16) ((bf16*)p)[off] = (bf16)v;
-  else ((float*)p)[off] = v;
-}
-
-// finish 8 consecutive columns [n, n+8) of GEMM row m (n % 8 == 0)
-KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
-  if (m >= e.M || n >= e.N) return;
-  const bool full = n + 8 <= e.N;
-  if (e.bias) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] += (n + j < e.N) ? e.bias[n + j] : 0.f;
-  }
-  float pre[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    pre[j] = (e.prek && e.act == KAIR_ACT_GELU) ? gelu_erf_grad(v[j]) : v[j];
-    if (e.act == KAIR_ACT_GELU) v[j] = gelu_erf(v[j]);
-    else if (e.act == KAIR_ACT_LEAKY) v[j] = v[j] > 0.f ? v[j] : v[j] * e.slope;
-    else if (e.act == KAIR_ACT_RELU) v[j] = fmaxf(v[j], 0.f);
-  }
-  if (e.omode == KAIR_OUT_ROWS) {
-    const long row = win_to_token(m, e.win);
-    if (e.gate) {
-      float g[8];
-      if (full) load8_any(e.gate, e.gdt, row * e.ldg + n, g);
-      else
-        for (int j = 0; j < 8; ++j)
-          g[j] = n + j < e.N ? (e.gdt == KAIR_BF16 ? (float)((const bf16*)e.gate)[row * e.ldg + n + j]
-                                                    : ((const float*)e.gate)[row * e.ldg + n + j]) : 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (e.gkind == 1) v[j] *= gelu_erf_grad(g[j]);
-        else if (e.gkind == 2) v[j] *= (g[j] > 0.f ? 1.f : e.slope);
-        else if (e.gkind == 4) v[j] *= g[j];
-        else v[j] *= (g[j] > 0.f ? 1.f : 0.f);
-      }
-    }
-    if (e.resid) {
-      const float s = e.rowscale ? e.rowscale[fdiv((int)row, e.d_rps)] : 1.f;
-      for (int j = 0; j < 8; ++j)
-        if (n + j < e.N) v[j] = e.resid[row * e.ldr + n + j] + s * v[j];
-    }
-    if (e.resid2) {
-      for (int j = 0; j < 8; ++j)
-        if (n + j < e.N) v[j] += e.resid2[row * e.ldr2 + n + j];
-    }
-    if (e.ones_col >= n && e.ones_col < n + 8) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (n + j == e.ones_col) v[j] = 1.f;
-    }
-    if (full && (e.ldo % 8) == 0) {
-      store8_any(e.out, e.odt, row * e.ldo + n, v);
-      if (e.pre) store8_any(e.pre, e.pdt, row * e.ldp + n, pre);
-      if (e.out_lo) store8_lo(e.out_lo, row * e.ldo + n, v);
-    } else {
-      for (int j = 0; j < 8 && n + j < e.N; ++j) {
-        st1(e.out, e.odt, row * e.ldo + n + j, v[j]);
-        if (e.pre) st1(e.pre, e.pdt, row * e.ldp + n + j, pre[j]);
-        if (e.out_lo) e.out_lo[row * e.ldo + n + j] = (bf16)(v[j] - (float)(bf16)v[j]);
-      }
-    }
-  } else if (e.omode == KAIR_OUT_QKVBLK) {
-    const int pw = e.nh * e.hdp;
-    const int part = fdiv(n, e.d_pw), rr = n - part * pw;
-    const int h = fdiv(rr, e.d_hdp), d = rr - h * e.hdp;
-    const long win = fdiv((int)m, e.d_tok);
-    const int t = (int)(m - win * e.tok);
-    store8_any(e.out, e.odt, (long)part * e.M * pw + ((win * e.nh + h) * e.tok + t) * e.hdp + d, v);
-  } else if (e.omode == KAIR_OUT_PSHUF || e.omode == KAIR_OUT_PSHUF_NCHW) {
-    const int r = e.r, r2 = r * r;
-    const long hw = (long)e.psH * e.psW;
-    const long b = m / hw;
-    const int p = (int)(m - b * hw), y = p / e.psW, x = p - (p / e.psW) * e.psW;
-    for (int j = 0; j < 8 && n + j < e.N; ++j) {
-      const int nn = n + j;
-      const int c = nn / r2, ij = nn - c * r2, i = ij / r, jj = ij - i * r;
-      if (e.omode == KAIR_OUT_PSHUF) {
-        const long orow = (b * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + jj;
-        st1(e.out, e.odt, orow * e.ldo + c, v[j]);
-        if (e.pre) st1(e.pre, e.pdt, orow * e.ldp + c, pre[j]);
-      } else if (c < e.imgC) {
-        const float o = v[j] / e.range + (e.mean ? e.mean[c] : 0.f);
-        ((float*)e.out)[((b * e.imgC + c) * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + jj] = o;
-      }
-    }
-  } else if (e.omode == KAIR_OUT_PSHUF_SPM) {
-    // columns sub-pixel-major: n = (i*r + j)*nf + c, so a chunk of 8 is 8 channels of one pixel
-    const int r = e.r, nf = e.N / (r * r);
-    const long hw = (long)e.psH * e.psW;
-    const long b = m / hw;
-    const int p = (int)(m - b * hw), y = p / e.psW, x = p - (p / e.psW) * e.psW;
-    const int sp = n / nf, c = n - sp * nf, i = sp / r, jj = sp - i * r;
-    const long orow = (b * e.psH * r + (long)y * r + i) * ((long)e.psW * r) + (long)x * r + jj;
-    if (full && c + 8 <= nf && (e.ldo % 8) == 0 && (c % 8) == 0) {
-      store8_any(e.out, e.odt, orow * e.ldo + c, v);
-      if (e.pre) store8_any(e.pre, e.pdt, orow * e.ldp + c, pre);
-      if (e.out_lo) store8_lo(e.out_lo, orow * e.ldo + c, v);
-    } else {
-      for (int j = 0; j < 8 && n + j < e.N; ++j) {
-        const int nn = n + j, s2 = nn / nf, c2 = nn - s2 * nf, i2 = s2 / r, j2 = s2 - i2 * r;
-        const long orow2 = (b * e.psH * r + (long)y * r + i2) * ((long)e.psW * r) + (long)x * r + j2;
-        st1(e.out, e.odt, orow2 * e.ldo + c2, v[j]);
-        if (e.pre) st1(e.pre, e.pdt, orow2 * e.ldp + c2, pre[j]);
-        if (e.out_lo) e.out_lo[orow2 * e.ldo + c2] = (bf16)(v[j] - (float)(bf16)v[j]);
-      }
-    }
-  } else if (e.omode == KAIR_OUT_PUNSHUF_SPM) {
-    // pixel (b, Y, X) of the shuffled image, column c -> pre-shuffle row (b, Y/r, X/r), column
-    // (i*r + j)*N + c: a chunk of 8 columns is 8 contiguous pre-shuffle channels
-    const int r = e.r;
-    const long HW = (long)e.psH * r * e.psW * r;
-    const long b = m / HW;
-    const long p = m - b * HW;
-    const int Y = (int)(p / (e.psW * r)), X = (int)(p - (long)Y * e.psW * r);
-    const int y = Y / r, i = Y - y * r, x = X / r, jj = X - x * r;
-    const long orow = (b * e.psH + y) * e.psW + x;
-    const long o0 = orow * e.ldo + (long)(i * r + jj) * e.N + n;
-    if (e.gate) {
-      float g[8];
-      if (full) load8_any(e.gate, e.gdt, orow * e.ldg + (long)(i * r + jj) * e.N + n, g);
-      else
-        for (int j = 0; j < 8; ++j)
-          g[j] = n + j < e.N ? (e.gdt == KAIR_BF16 ? (float)((const bf16*)e.gate)[orow * e.ldg + (long)(i * r + jj) * e.N + n + j]
-                                                    : ((const float*)e.gate)[orow * e.ldg + (long)(i * r + jj) * e.N + n + j]) : 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] *= (e.gkind == 2) ? (g[j] > 0.f ? 1.f : e.slope) : (e.gkind == 4 ? g[j] : (g[j] > 0.f ? 1.f : 0.f));
-    }
-    if (full && (e.ldo % 8) == 0 && (e.N % 8) == 0) {
-      store8_any(e.out, e.odt, o0, v);
-    } else {
-      for (int j = 0; j < 8 && n + j < e.N; ++j) st1(e.out, e.odt, o0 + j, v[j]);
-    }
-  } else if (e.omode == KAIR_OUT_PUNSHUF) {
-    const int r = e.r;
-    const long HW = (long)e.psH * r * e.psW * r;
-    const long b = m / HW;
-    const long p = m - b * HW;
-    const int Y = (int)(p / (e.psW * r)), X = (int)(p - (long)Y * e.psW * r);
-    const int y = Y / r, i = Y - y * r, x = X / r, jj = X - x * r;
-    const long orow = (b * e.psH + y) * e.psW + x;
-    for (int j = 0; j < 8 && n + j < e.N; ++j) {
-      const int oc = (n + j) * r * r + i * r + jj;
-      float val = v[j];
-      if (e.gate) {
-        const float g = e.gdt == KAIR_BF16 ? (float)((const bf16*)e.gate)[orow * e.ldg + oc]
-                                            : ((const float*)e.gate)[orow * e.ldg + oc];
-        val *= (e.gkind == 2) ? (g > 0.f ? 1.f : e.slope) : (e.gkind == 4 ? g : (g > 0.f ? 1.f : 0.f));
-      }
-      st1(e.out, e.odt, orow * e.ldo + oc, val);
-    }
-  } else {  // NCHW image; resid (optional): an NCHW image of the same shape added after the range
-    const long hw = (long)e.imgH * e.imgW;
-    const long b = m / hw;
-    const long p = m - b * hw;
-    for (int j = 0; j < 8 && n + j < e.imgC && n + j < e.N; ++j) {
-      const long o = (b * e.imgC + n + j) * hw + p;
-      ((float*)e.out)[o] = v[j] / e.range + (e.mean ? e.mean[n + j] : 0.f) + (e.resid ? e.resid[o] : 0.f);
-    }
-  }
-}
-
-// bijective XCD-aware remap: consecutive logical tiles share an XCD (L2)
-KAIR_DEV int xcd_remap(int hw, int nwg) {
-  const int q = nwg / 8, r = nwg % 8;
-  const int x = hw % 8, pos = hw / 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + pos;
-}
 
 // ------------------------------------------------------------------------------------------
 // NT kernel
@@ -2083,11 +1635,11 @@ extern "C" int kair_device_arch(char* buf, int len) {
   return 0;
 }
 
-static int check_operand(const kair_operand* o, const char* what) {
+int kair_check_operand(const kair_operand* o, const char* what) {
   KAIR_CHECK_ARG(o && o->ptr, "%s: null operand", what);
-  KAIR_CHECK_ARG(o->dtype == KAIR_F32 || o->dtype == KAIR_BF16, "%s: bad dtype", what);
+  KAIR_CHECK_ARG(o->dtype == KAIR_F32 || o->dtype == KAIR_BF16 || o->dtype == KAIR_F16, "%s: bad dtype", what);
   KAIR_CHECK_ARG(o->mode >= 0 && o->mode <= 3, "%s: bad mode", what);
-  const int esz = o->dtype == KAIR_BF16 ? 2 : 4;
+  const int esz = o->dtype == KAIR_F32 ? 4 : 2;
   KAIR_CHECK_ARG(((uintptr_t)o->ptr % 16) == 0, "%s: pointer not 16-byte aligned", what);
   if (o->mode == KAIR_LD_ROWS) KAIR_CHECK_ARG((o->ld * esz) % 16 == 0, "%s: row stride not 16-byte aligned", what);
   if (o->mode == KAIR_LD_IM2COL3) {
@@ -2109,9 +1661,10 @@ static int check_operand(const kair_operand* o, const char* what) {
 extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const kair_epilogue* E, long M, int N, int K,
                             int compute, void* stream) {
   int rc;
-  if ((rc = check_operand(A, "gemm_nt A"))) return rc;
-  if ((rc = check_operand(B, "gemm_nt B"))) return rc;
+  if ((rc = kair_check_operand(A, "gemm_nt A"))) return rc;
+  if ((rc = kair_check_operand(B, "gemm_nt B"))) return rc;
   KAIR_CHECK_ARG(E && E->out, "gemm_nt: null epilogue/out");
+  if (compute == KAIR_COMPUTE_X3) return kair_gemm_nt_x3(A, B, E, M, N, K, stream);   // gemm_x3.hip
   KAIR_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 8 == 0, "gemm_nt: bad M/N/K (%ld,%d,%d), K%%8 must be 0", M, N, K);
   KAIR_CHECK_ARG(B->mode == KAIR_LD_ROWS && B->dtype == compute && B->win_ws == 0,
                  "gemm_nt: B must be packed rows of the compute dtype");
@@ -2129,9 +1682,11 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
   KAIR_CHECK_ARG(A->a_split != 2 || (compute == KAIR_BF16 && A->dtype == KAIR_BF16 && A->mode == KAIR_LD_IM2COL3 &&
                                       B->w_split && A->im_C % 2 == 0),
                  "gemm_nt: a_split 2 marks a bf16 [hi | lo] pair image read through tied hi/lo split weights");
-  KAIR_CHECK_ARG(!E->out_lo || (E->out_dtype == KAIR_BF16 && (E->out_mode == KAIR_OUT_ROWS || E->out_mode == KAIR_OUT_PSHUF_SPM) &&
+  KAIR_CHECK_ARG(!E->out_lo || (E->out_dtype == KAIR_BF16 &&
+                                (E->out_mode == KAIR_OUT_ROWS || E->out_mode == KAIR_OUT_PSHUF_SPM ||
+                                 E->out_mode == KAIR_OUT_QKVBLK) &&
                                 ((uintptr_t)E->out_lo % 16) == 0),
-                 "gemm_nt: out_lo needs a bf16 ROWS / PSHUF_SPM output and a 16-byte aligned lo plane");
+                 "gemm_nt: out_lo needs a bf16 ROWS / PSHUF_SPM / QKVBLK output and a 16-byte aligned lo plane");
   KAIR_CHECK_ARG(!E->a_copy || (compute == KAIR_BF16 && A->mode == KAIR_LD_IM2COL3 && A->im_up <= 1),
                  "gemm_nt: a_copy is a side output of the bf16 3x3 conv (no upsample)");
   KAIR_CHECK_ARG((E->out_mode != KAIR_OUT_PSHUF && E->out_mode != KAIR_OUT_PUNSHUF && E->out_mode != KAIR_OUT_PSHUF_NCHW &&
@@ -2194,12 +1749,13 @@ extern "C" int kair_wgrad_splits(long M, int N, int K) {
 extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float* ws, int splits, long M, int N, int K,
                             int compute, void* stream) {
   int rc;
-  if ((rc = check_operand(A, "gemm_tn A"))) return rc;
-  if ((rc = check_operand(B, "gemm_tn B"))) return rc;
+  if ((rc = kair_check_operand(A, "gemm_tn A"))) return rc;
+  if ((rc = kair_check_operand(B, "gemm_tn B"))) return rc;
   KAIR_CHECK_ARG(ws, "gemm_tn: null workspace");
   KAIR_CHECK_ARG(M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % 8 == 0 && splits > 0, "gemm_tn: bad sizes");
   KAIR_CHECK_ARG(A->mode != KAIR_LD_IM2COL3 && A->mode != KAIR_LD_S2D, "gemm_tn: A cannot be im2col / space-to-depth");
   KAIR_CHECK_ARG(B->mode != KAIR_LD_QKVBLK, "gemm_tn: B cannot be q/k/v blocked");
+  if (compute == KAIR_COMPUTE_X3) return kair_gemm_tn_x3(A, B, ws, splits, M, N, K, stream);   // gemm_x3.hip
   KAIR_CHECK_ARG(compute == KAIR_BF16 || (A->dtype == KAIR_F32 && B->dtype == KAIR_F32),
                  "gemm_tn: fp32 compute needs fp32 operands");
   KAIR_CHECK_ARG(A->mode != KAIR_LD_QKVBLK || A->dtype == compute, "gemm_tn: q/k/v operand dtype");
@@ -2338,8 +1894,8 @@ extern "C" int kair_wgrad_grouped_ex(const kair_wgrad_job* jobs, int njobs, long
   long tile0 = 0, off = 0, blk0 = 0;
   for (int i = 0; i < njobs; ++i) {
     const kair_wgrad_job& J = jobs[i];
-    if ((rc = check_operand(&J.A, "wgrad_grouped A"))) return rc;
-    if ((rc = check_operand(&J.B, "wgrad_grouped B"))) return rc;
+    if ((rc = kair_check_operand(&J.A, "wgrad_grouped A"))) return rc;
+    if ((rc = kair_check_operand(&J.B, "wgrad_grouped B"))) return rc;
     KAIR_CHECK_ARG(J.A.dtype == KAIR_BF16 && J.B.dtype == KAIR_BF16, "wgrad_grouped: job %d operands must be bf16", i);
     KAIR_CHECK_ARG((J.A.mode == KAIR_LD_ROWS || J.A.mode == KAIR_LD_QKVBLK) && J.B.mode == KAIR_LD_ROWS,
                    "wgrad_grouped: job %d: A rows or q/k/v blocked, B rows", i);

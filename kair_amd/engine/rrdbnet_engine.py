@@ -37,6 +37,11 @@ class ConvEngineBase:
         self._packed_version = None
         self._pack_table = None
         self.blocks = []          # no stochastic depth in the conv nets (FusedTrainer checks this)
+        self.seg_hook = None      # called between the gradient segments of backward() (grad_segments())
+
+    def _segment_done(self):
+        if self.seg_hook is not None:
+            self.seg_hook()
 
     def convs(self):
         raise NotImplementedError
@@ -100,6 +105,7 @@ class RRDBNetEngine(ConvEngineBase):
                     "up": [net.upconv1] + ([net.upconv2] if net.sf == 4 else []), "hr": net.HRconv,
                     "last": net.conv_last, "act": 2, "slope": 0.2}
         self.act, self.slope = spec["act"], spec["slope"]
+        self._spec_mods = spec   # the modules grad_segments() groups
         self.act_epi = H.ACT_LEAKY if self.act == 2 else H.ACT_RELU
         first = spec["first"]
         self.device = first.weight.device
@@ -127,6 +133,24 @@ class RRDBNetEngine(ConvEngineBase):
 
     def convs(self):
         return [self.conv_first] + [c for r in self.rdbs for c in r] + [self.trunk] + self.up + [self.hr, self.last]
+
+    RRDB_PER_SEGMENT = 3   # RRDBs per data-parallel gradient bucket (~8.6 MB of fp32 gradients at nf 64, gc 32)
+
+    def grad_segments(self):
+        """Parameter groups in the order backward() completes their gradients (the data-parallel trainer
+        all-reduces each as one bucket while the rest of backward runs; reference DDP: model_base.py:113-119):
+        the tail (trunk_conv, upsampling convs, HRconv, conv_last), then the RRDB trunk in groups of
+        RRDB_PER_SEGMENT, last to first, the first group together with conv_first."""
+        sp = self._spec_mods
+        plist = lambda mods: [p for m in mods for p in m.parameters()]
+        segs = [plist([sp["trunk"]] + list(sp["up"]) + [sp["hr"], sp["last"]])]
+        rr = sp["rrdbs"]
+        k = self.RRDB_PER_SEGMENT
+        starts = list(range(0, len(rr), k))
+        for s0 in reversed(starts[1:]):
+            segs.append(plist([m for trip in rr[s0:s0 + k] for m in trip]))
+        segs.append(plist([sp["first"]] + [m for trip in rr[:k] for m in trip]))
+        return segs
 
     # ------------------------------------------------------------------------------------
     def _build_plan(self, key, infer):
@@ -265,13 +289,17 @@ class RRDBNetEngine(ConvEngineBase):
         H.act_grad_cast(P["Gt"], nf, None, 0, P["dzt"], nf, M, nf, 0)
         H.gemm_nt(H.im2col(P["dzt"], Hh, Ww, nf, flip=True), H.rows(c.Wd), H.epilogue(P["G_R"]), M, nf, 9 * nf, cd)
         self.conv_wgrad(P, c, P["dzt"], nf, H.im2col(P["dense"][-1], Hh, Ww, nf, ld=CD), M, grads, P["Gt"], nf)
+        self._segment_done()   # the tail's gradients are final
         # RRDB trunk, last to first.  G_R = dL/d(RRDB output)
         gy = P["gy"]
+        k = self.RRDB_PER_SEGMENT
         for i in range(self.nrr - 1, -1, -1):
             H.act_grad_cast(P["G_R"], nf, None, 0, gy, nf, M, nf, 0, 0.0, 0.2)     # dL/d RDB3 output
             for r in (3 * i + 2, 3 * i + 1, 3 * i):
                 self._rdb_bwd(P, r, grads)                                          # gy -> dL/d RDB input
             H.axpby(P["G_R"], gy, 1.0, 1.0)                                          # + skip
+            if i % k == 0 and i > 0:
+                self._segment_done()   # RRDBs i .. i + k - 1 are final (the first group joins conv_first)
         # conv_first: dL/d fea = Gt (long skip) + G_R (trunk)
         H.axpby(P["G_R"], P["Gt"], 1.0, 1.0)
         H.act_grad_cast(P["G_R"], nf, None, 0, P["dzt"], nf, M, nf, 0)

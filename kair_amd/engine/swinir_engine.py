@@ -90,8 +90,17 @@ class _Lin:
         self.Np = n_grp[0] * n_grp[2]
         self.Kp = k_grp[0] * k_grp[2]
         dev = self.w.device
-        self.Wp = torch.empty(self.Np, self.Kp, device=dev, dtype=eng.tdt) if rows else None
-        self.Wt = torch.empty(self.Kp, self.Np, device=dev, dtype=eng.tdt) if not frag_t else None
+        # fp32x3 engine: the rows forms hold fp16 pairs of w 2^KAIR_X3_WEXP interleaved per 64 columns (pack
+        # kinds 17 / 19), multiplied hi.hi + hi.lo + lo.hi by kair_gemm_nt (compute KAIR_COMPUTE_X3)
+        self.x3 = eng.x3
+        if self.x3:   # (self.map stays the plain kind-0 map: the weight gradient's finalize layout)
+            self.pmap, self.pmapT = H.wmap(17, N, K, n_grp, k_grp), H.wmap(19, N, K, n_grp, k_grp)
+            self.Wp = torch.empty(self.Np, 2 * _rup(self.Kp, 64), device=dev, dtype=torch.float16) if rows else None
+            self.Wt = torch.empty(self.Kp, 2 * _rup(self.Np, 64), device=dev, dtype=torch.float16) if not frag_t else None
+        else:
+            self.pmap, self.pmapT = self.map, self.mapT
+            self.Wp = torch.empty(self.Np, self.Kp, device=dev, dtype=eng.tdt) if rows else None
+            self.Wt = torch.empty(self.Kp, self.Np, device=dev, dtype=eng.tdt) if not frag_t else None
         self.bp = torch.empty(self.Np, device=dev)
         # MFMA-fragment order of Wp for the fused block kernels: pack kind 10, or kind 12 (hi/lo
         # bf16 pairs, the same ~16-bit weight precision as the split convs) when split
@@ -107,9 +116,9 @@ class _Lin:
         w, b = self.w.detach(), self.b.detach()
         jobs = [(b, self.bp, self.mapb)]
         if self.Wp is not None:
-            jobs.append((w, self.Wp, self.map))
+            jobs.append((w, self.Wp, self.pmap))
         if self.Wt is not None:
-            jobs.append((w, self.Wt, self.mapT))
+            jobs.append((w, self.Wt, self.pmapT))
         if self.Wg is not None:
             jobs.append((w, self.Wg, self.mapg))
         if self.Wgt is not None:
@@ -142,7 +151,8 @@ class _Conv:
         self.Co, self.Ci, self.Cop, self.Cip = Co, Ci, Cop, Cip
         if split is None:
             split = getattr(eng, "split_conv", False)
-        self.split = bool(split) and eng.tdt == torch.bfloat16
+        self.split = (bool(split) and eng.tdt == torch.bfloat16) or eng.x3
+        self.x3 = eng.x3
         self.n_perm = n_perm
         self.map = H.wmap(1, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
         fcip = fwd_cip or Cip
@@ -153,12 +163,17 @@ class _Conv:
         self.mapb = H.wmap(4, Co, 0, (1, Co, Cop), (1, 1, 1), n_perm=n_perm)
         dev = self.w.device
         kf = 2 * _rup(9 * fcip, 64) if self.split else 9 * fcip
-        self.Wf = torch.empty(Cop, kf, device=dev, dtype=eng.tdt)
+        self.Wf = torch.empty(Cop, kf, device=dev, dtype=torch.float16 if self.x3 else
+                              (torch.bfloat16 if self.split else eng.tdt))
         self.narrow = bool(narrow)
         if self.narrow:   # the narrow kernels' forward form (their backward reads the fp32 master weight)
             self.mapn = H.wmap(15, Co, Ci, (1, Co, 16), (1, Ci, Cip))
             self.Wn = torch.empty(16, 2 * 9 * Cip, device=dev, dtype=torch.bfloat16)
-        self.Wd = torch.empty(Cip, 9 * Cop, device=dev, dtype=eng.tdt) if need_dgrad else None
+        if self.x3:   # fp16 pairs of the dgrad form (pack kind 18)
+            self.mapd = H.wmap(18, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
+            self.Wd = torch.empty(Cip, 2 * _rup(9 * Cop, 64), device=dev, dtype=torch.float16) if need_dgrad else None
+        else:
+            self.Wd = torch.empty(Cip, 9 * Cop, device=dev, dtype=eng.tdt) if need_dgrad else None
         self.bp = torch.empty(Cop, device=dev)
         self.wr = bool(wr) and Cop == 192 and Cip == 192 and self.split
         # wr_pair: an upsampling conv (64 -> 256, sub-pixel-major rows) reading a [hi | lo] pair image
@@ -266,9 +281,17 @@ class SwinIREngine:
         Cp = 192, hidden padded to 384); fused_mlp (default: fused_blocks) selects the MLP-half
         kernel separately."""
         self.net_ref = weakref.ref(net)
-        if compute_dtype not in ("bf16", "fp32"):
+        if compute_dtype not in ("bf16", "fp32", "fp32x3"):
             raise ValueError(compute_dtype)
-        self.cd = H.BF16 if compute_dtype == "bf16" else H.F32
+        # fp32x3: the fp32 reference's arithmetic on the 16-bit matrix cores -- every contraction multiplies
+        # fp16 pairs of power-of-2-scaled operands (hi.hi + hi.lo + lo.hi, fp32 accumulation; ~2^-21 relative
+        # per product), operands fp32 (split inside the kernels) or fp16 hi/lo planes; the unfused launch
+        # sequence of the fp32 engine.  Exponents: weights KAIR_X3_WEXP (packs), activations 0, gradients
+        # P["e_g"] (the loss normalisation, _x3_grad_exp), so every operand sits in fp16's normal range
+        self.x3 = compute_dtype == "fp32x3"
+        self._ax = 0   # x3: the exponent of the GEMM A operands / fp16 outputs of the phase being issued
+        self.cd = H.BF16 if compute_dtype in ("bf16", "fp32x3") else H.F32
+        self.tn_cd = H.X3 if self.x3 else self.cd   # kair_gemm_tn compute of the weight gradients
         self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
         self.split_conv = bool(split_conv) and compute_dtype == "bf16"
         # split activations only pay with split weights (a bf16 weight rounding dominates otherwise), and
@@ -459,7 +482,10 @@ class SwinIREngine:
         Cp, Hdp, nh = self.Cp, self.Hdp, self.nh
         nWin = M // WS_TOK
         e = lambda *s, dt=f32: torch.empty(*s, device=dev, dtype=dt)
+        hf = torch.float16
         P = {"B": B, "H": Hh, "W": Ww, "M": M, "nWin": nWin}
+        # fp32x3: the exponent of the backward's data gradients (the mean loss over the output image)
+        P["e_g"] = self._x3_grad_exp(B * self.in_ch * Hh * self.scale * Ww * self.scale)
         P["xin"] = e(M, self.Cin_p, dt=T)
         P["f0"] = e(M, Cp)
         P["pe_mean"], P["pe_rstd"] = e(M), e(M)
@@ -471,7 +497,9 @@ class SwinIREngine:
                 continue
             blocks.append({
                 "mid": e(M, Cp), "out": e(M, Cp), "ln1": e(M, Cp, dt=T), "m1": e(M), "r1": e(M),
-                "qkv": e(3 * M * nh * 32, dt=T), "O": e(M, nh * 32, dt=T), "lse": e(nWin * nh * WS_TOK),
+                # fp32x3: q/k/v and O as hi/lo bf16 planes [2, ...] (the split attention kernels' operands)
+                "qkv": e(2, 3 * M * nh * 32, dt=hf) if self.x3 else e(3 * M * nh * 32, dt=T),
+                "O": e(2, M, nh * 32, dt=hf) if self.x3 else e(M, nh * 32, dt=T), "lse": e(nWin * nh * WS_TOK),
                 "ln2": e(M, Cp, dt=T), "m2": e(M), "r2": e(M), "u": e(M, Hdp, dt=T), "h": e(M, Hdp, dt=T)})
         P["blocks"] = blocks
         P["rstb_out"] = [e(M, Cp) for _ in range(min(2, len(self.rstb)) if infer else len(self.rstb))]
@@ -520,7 +548,9 @@ class SwinIREngine:
         depth = max(len(blks) for blks, _ in self.rstb)
         z = lambda *s: torch.zeros(*s, device=dev, dtype=T)
         # Two sets (RSTB parity): the side stream still reads one RSTB's while the next RSTB writes the other.
-        P["gw"] = [[{"Dm": z(M, Cp), "Da": z(M, Cp), "dU": e(M, Hdp, dt=T), "dqkv": e(3 * M * nh * 32, dt=T),
+        P["gw"] = [[{"Dm": z(M, Cp), "Da": z(M, Cp), "dU": e(M, Hdp, dt=T),
+                     # fp32x3: dq/dk/dv as token rows [M][3 nh 32], hi/lo fp16 planes
+                     "dqkv": e(2, M, 3 * nh * 32, dt=hf) if self.x3 else e(3 * M * nh * 32, dt=T),
                      # LN1 / LN2 parameter partials and the attention bias-table partials of the block, reduced
                      # by one grouped launch each at the end of the RSTB
                      "ln1p": e(2 * 2048 * Cp), "ln2p": e(2 * 2048 * Cp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
@@ -529,7 +559,7 @@ class SwinIREngine:
         if self.rowgemm:   # LayerNorm-parameter partial rows the fused row GEMMs leave (<= the ln*p buffers' 2048)
             P["rg_nb"] = {k: H.rowgemm_ln_blocks(M, k) for k in (Hdp, 3 * nh * 32)}
             assert max(P["rg_nb"].values()) <= 2048, P["rg_nb"]
-        P["dO"] = e(M, nh * 32, dt=T)
+        P["dO"] = e(2, M, nh * 32, dt=hf) if self.x3 else e(M, nh * 32, dt=T)
         P["ln_ws"] = e(2 * 2048 * Cp)   # kair_layernorm_bwd: 2 * 2048 * C floats
         P["attn_ws"] = e(H.window_attn_bwd_ws(nWin, nh))
         P["loss"] = e(1)
@@ -634,6 +664,7 @@ class SwinIREngine:
         HW = Hh * Ww
         x = x.contiguous()
         self.cur = P
+        self._ax = 0   # fp32x3: forward operands are activations (exponent 0)
         P["x"] = x
         P["drop"] = drop_scales
         if self.xin_hilo:
@@ -641,7 +672,7 @@ class SwinIREngine:
         else:
             H.image_to_nhwc(x, P["xin"], self.Cin_p, self.mean, self.img_range, B, self.in_ch, Hh, Ww)
         c = self.conv_first
-        H.gemm_nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), c.fwd(), H.epilogue(P["f0"], bias=c.bp), M, Cp,
+        self._nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), c.fwd(), H.epilogue(P["f0"], bias=c.bp), M, Cp,
                   9 * self.Cin_p, cd)
         n = self.pe_norm
         H.layernorm_fwd(P["f0"], Cp, P["s0"], Cp, n.weight, n.bias, P["pe_mean"], P["pe_rstd"], M, self.C, n.eps)
@@ -671,14 +702,14 @@ class SwinIREngine:
                 H.conv3x3_wr(src, Cp, 0, r.Wf15, r.bp, resid, out, P["B"], Hh, Ww, Cp, Cp, acopy=ac[0], acones=ac[1],
                              split=True)
                 return
-            H.gemm_nt(self._ain(H.im2col(src, Hh, Ww, Cp)), r.fwd(), H.epilogue(out, bias=r.bp, resid=resid, acopy=ac), M,
+            self._nt(self._ain(H.im2col(src, Hh, Ww, Cp)), r.fwd(), H.epilogue(out, bias=r.bp, resid=resid, acopy=ac), M,
                       Cp, 9 * Cp, cd)
             return
         t1, t2 = P["r3"][id(r)]
         lk = dict(act=H.ACT_LEAKY, slope=0.2)
-        H.gemm_nt(H.im2col(src, Hh, Ww, Cp), r.c1.fwd(), H.epilogue(t1, bias=r.c1.bp, **lk), M, r.Cq, 9 * Cp, cd)
-        H.gemm_nt(H.rows(t1), H.rows(r.c2.Wp), H.epilogue(t2, bias=r.c2.bp, **lk), M, r.Cq, r.Cq, cd)
-        H.gemm_nt(H.im2col(t2, Hh, Ww, r.Cq), r.c3.fwd(), H.epilogue(out, bias=r.c3.bp, resid=resid), M, Cp, 9 * r.Cq, cd)
+        self._nt(H.im2col(src, Hh, Ww, Cp), r.c1.fwd(), H.epilogue(t1, bias=r.c1.bp, **lk), M, r.Cq, 9 * Cp, cd)
+        self._nt(H.rows(t1), H.rows(r.c2.Wp), H.epilogue(t2, bias=r.c2.bp, **lk), M, r.Cq, r.Cq, cd)
+        self._nt(H.im2col(t2, Hh, Ww, r.Cq), r.c3.fwd(), H.epilogue(out, bias=r.c3.bp, resid=resid), M, Cp, 9 * r.Cq, cd)
 
     def _resi_bwd(self, r, P, G, src, D, grads):
         """resi_conv backward for out = resi_conv(src) + resid: G = dL/d out (fp32 rows) -> D = dL/d src
@@ -691,7 +722,7 @@ class SwinIREngine:
             if P.get("conv_wr") and r.wr:
                 H.conv3x3_wr(G, Cp, 1, r.Wd16, None, None, D, P["B"], Hh, Ww, Cp, Cp, acopy=ac[0], split=False)
             else:
-                H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.Wd), H.epilogue(D, acopy=ac), M, Cp, 9 * Cp, cd)
+                self._nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.Wd), H.epilogue(D, acopy=ac), M, Cp, 9 * Cp, cd)
             if self.conv_tap:   # bf16 operands: the halo convs' copies (else taken when the job runs)
                 return ("tap", G, src, r, g(r.w), g(r.b))
             return (H.rows(G), H.im2col(src, Hh, Ww, Cp, ones_col=self.C), M, Cp, 9 * Cp, r.map, g(r.w), g(r.b), self.C)
@@ -701,15 +732,15 @@ class SwinIREngine:
         # 3x3 Cq -> C: dL/d t2, gated by LeakyReLU'(t2 pre-activation)
         dz2 = P["r3_dz"][0].view(-1)[:M * q].view(M, q)
         dz1 = P["r3_dz"][1].view(-1)[:M * q].view(M, q)
-        H.gemm_nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.c3.Wd), H.epilogue(dz2, gate=t2, **lk), M, q, 9 * Cp, cd)
+        self._nt(H.im2col(G, Hh, Ww, Cp, flip=True), H.rows(r.c3.Wd), H.epilogue(dz2, gate=t2, **lk), M, q, 9 * Cp, cd)
         self._wgrad(P, H.rows(G), H.im2col(t2, Hh, Ww, q), M, Cp, 9 * q, r.c3.map, g(r.c3.w))
         self._bias_colsum(P, H.rows(G), M, Cp, r.c3.mapb, g(r.c3.b))
         # 1x1 Cq -> Cq
-        H.gemm_nt(H.rows(dz2), H.rows(r.c2.Wt), H.epilogue(dz1, gate=t1, **lk), M, q, q, cd)
+        self._nt(H.rows(dz2), H.rows(r.c2.Wt), H.epilogue(dz1, gate=t1, **lk), M, q, q, cd)
         self._wgrad(P, H.rows(dz2), H.rows(t1), M, q, q, r.c2.map, g(r.c2.w))
         self._bias_colsum(P, H.rows(dz2), M, q, r.c2.mapb, g(r.c2.b))
         # 3x3 C -> Cq
-        H.gemm_nt(H.im2col(dz1, Hh, Ww, q, flip=True), H.rows(r.c1.Wd), H.epilogue(D), M, Cp, 9 * q, cd)
+        self._nt(H.im2col(dz1, Hh, Ww, q, flip=True), H.rows(r.c1.Wd), H.epilogue(D), M, Cp, 9 * q, cd)
         self._wgrad(P, H.rows(dz1), H.im2col(src, Hh, Ww, Cp), M, q, 9 * Cp, r.c1.map, g(r.c1.w))
         self._bias_colsum(P, H.rows(dz1), M, q, r.c1.mapb, g(r.c1.b))
         return None
@@ -718,6 +749,27 @@ class SwinIREngine:
         """A forward conv's input operand: a hi/lo pair under split_act (fp32 source: lo formed in the
         kernel; bf16 source: its lo plane `lo`), else as is."""
         return H.asplit(op, lo) if self.split_act else op
+
+    def _nt(self, A, B, E, M, N, K, cd):
+        """kair_gemm_nt; under fp32x3 the split-fp16 arithmetic (compute KAIR_COMPUTE_X3): A is fp32 (split in the
+        kernel) or an fp16 pair (its lo plane attached with H.with_lo) carrying the phase exponent (forward 0,
+        backward the gradient exponent), B a split-packed fp16 weight (2^KAIR_X3_WEXP), an fp16 output the
+        pair of v 2^(phase exponent)."""
+        if self.x3:
+            if A.dtype == H.F16 and not A.lo_ptr:
+                raise RuntimeError("fp32x3: an fp16 GEMM operand needs its lo plane")
+            A.x3_exp, B.x3_exp = self._ax, H.X3_WEXP
+            if E.out_dtype == H.F16:
+                E.x3_out_exp = self._ax
+            H.gemm_nt(A, B, E, M, N, K, H.X3)
+            return
+        H.gemm_nt(A, B, E, M, N, K, cd)
+
+    @staticmethod
+    def _x3_grad_exp(numel):
+        """The fp32x3 gradient exponent: the mean-loss gradient is O(1 / numel) per output element, so data
+        gradients times 2^(log2 numel - 2) sit near 2^-2 at the loss, 2^16 below fp16's overflow."""
+        return max(0, int(round(math.log2(max(numel, 1)))) - 2)
 
     def _forward_tail(self, P):
         """Reconstruction tail: P['fb'] (conv_after_body + residual) -> P['E']."""
@@ -732,7 +784,7 @@ class SwinIREngine:
                 H.conv3x3_wr(P["fb"], Cp, 0, c.Wc15, c.bp, None, P["a0"], B, Hh, Ww, Cp, 64, ldo=tl, split=True,
                              out_lo=lo(P["a0"]), act=H.ACT_LEAKY, slope=0.01)
             else:
-                H.gemm_nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
+                self._nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
                           H.epilogue(P["a0"], ldo=tl, bias=c.bp, act=H.ACT_LEAKY, slope=0.01, out_lo=lo(P["a0"])), M, 64,
                           9 * Cp, cd)
             src, h, w = P["a0"], Hh, Ww
@@ -744,7 +796,7 @@ class SwinIREngine:
                     src, h, w = dst, h * r, w * r
                     continue
                 A = H.asplit(H.im2col(src, h, w, c.fcip), pair=True) if sa else H.im2col(src, h, w, 64)
-                H.gemm_nt(A, c.fwd(), H.epilogue(dst, mode=H.OUT_PSHUF_SPM, ldo=tl, bias=c.bp, ps=(r, h, w), out_lo=lo(dst)),
+                self._nt(A, c.fwd(), H.epilogue(dst, mode=H.OUT_PSHUF_SPM, ldo=tl, bias=c.bp, ps=(r, h, w), out_lo=lo(dst)),
                           B * h * w, c.Co, 9 * c.fcip, cd)
                 src, h, w = dst, h * r, w * r
             c = self.last
@@ -752,35 +804,35 @@ class SwinIREngine:
                 H.conv3x3_narrow_fwd(src, tl, 64 if sa else 0, c.Wn, c.bp, self.in_ch, self.mean, self.img_range, None,
                                      P["E"], B, h, w)
                 return P["E"]
-            H.gemm_nt(self._ain(H.im2col(src, h, w, 64, ld=tl), lo(src)), c.fwd(),
+            self._nt(self._ain(H.im2col(src, h, w, 64, ld=tl), lo(src)), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(self.mean, self.img_range, self.in_ch, h, w)),
                       B * h * w, c.Cop, 9 * 64, cd)
         elif self.upsampler == "nearest+conv":
             c = self.cbu
-            H.gemm_nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
+            self._nt(H.im2col(P["fb"], Hh, Ww, Cp), c.fwd(),
                       H.epilogue(P["a0"], bias=c.bp, act=H.ACT_LEAKY, slope=0.01), M, 64, 9 * Cp, cd)
             src, h, w = P["a0"], Hh, Ww
             for c, dst in zip(self.nup, P["nup_act"]):   # lrelu(conv(nearest x2)): im2col reads through the upsample
                 h, w = 2 * h, 2 * w
-                H.gemm_nt(H.im2col(src, h, w, 64, up=2), c.fwd(), H.epilogue(dst, bias=c.bp, act=H.ACT_LEAKY, slope=0.2),
+                self._nt(H.im2col(src, h, w, 64, up=2), c.fwd(), H.epilogue(dst, bias=c.bp, act=H.ACT_LEAKY, slope=0.2),
                           B * h * w, 64, 9 * 64, cd)
                 src = dst
             c = self.hrc
-            H.gemm_nt(H.im2col(src, h, w, 64), c.fwd(), H.epilogue(P["nhr"], bias=c.bp, act=H.ACT_LEAKY, slope=0.2),
+            self._nt(H.im2col(src, h, w, 64), c.fwd(), H.epilogue(P["nhr"], bias=c.bp, act=H.ACT_LEAKY, slope=0.2),
                       B * h * w, 64, 9 * 64, cd)
             c = self.last
-            H.gemm_nt(H.im2col(P["nhr"], h, w, 64), c.fwd(),
+            self._nt(H.im2col(P["nhr"], h, w, 64), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(self.mean, self.img_range, self.in_ch, h, w)),
                       B * h * w, c.Cop, 9 * 64, cd)
         elif self.upsampler in (None, ""):
             # x/range + mean with x = (x_in - mean) * range + conv_last(res)  ==  x_in + conv_last(res) / range
             c = self.last
-            H.gemm_nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
+            self._nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, resid=P["x"],
                                  img=(None, self.img_range, self.in_ch, Hh, Ww)), M, c.Cop, 9 * Cp, cd)
         else:
             c = self.up1
-            H.gemm_nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
+            self._nt(self._ain(H.im2col(P["fb"], Hh, Ww, Cp)), c.fwd(),
                       H.epilogue(P["E"], mode=H.OUT_PSHUF_NCHW, ldo=0, bias=c.bp, ps=(self.scale, Hh, Ww),
                                  img=(self.mean, self.img_range, self.in_ch, Hh, Ww)), M, c.Cop, 9 * Cp, cd)
         return P["E"]
@@ -804,13 +856,22 @@ class SwinIREngine:
             H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps, win,
                             one_col=self.C)
             l = blk.qkv
-            H.gemm_nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
-                                                                   qkv=(nh, 32, WS_TOK)), M, l.Np, Cp, cd)
-            H.window_attn_fwd(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale, Hh,
-                              Ww, blk.shift, ones_col=self.C // nh)
+            if self.x3:   # q/k/v and O as hi/lo planes, the split attention kernels in between
+                self._nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"][0], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
+                                                                     qkv=(nh, 32, WS_TOK), out_lo=S["qkv"][1]),
+                         M, l.Np, Cp, cd)
+                H.window_attn_fwd_x3(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale,
+                                     Hh, Ww, blk.shift, ones_col=self.C // nh, e_in=0, e_out=0)
+                A_o = H.with_lo(H.rows(S["O"][0]), S["O"][1])
+            else:
+                self._nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
+                                                                     qkv=(nh, 32, WS_TOK)), M, l.Np, Cp, cd)
+                H.window_attn_fwd(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale,
+                                  Hh, Ww, blk.shift, ones_col=self.C // nh)
+                A_o = H.rows(S["O"])
             l = blk.proj
-            H.gemm_nt(H.rows(S["O"]), H.rows(l.Wp), H.epilogue(S["mid"], win=win, bias=l.bp, resid=x, rowscale=s_attn,
-                                                                rows_per_scale=HW), M, Cp, nh * 32, cd)
+            self._nt(A_o, H.rows(l.Wp), H.epilogue(S["mid"], win=win, bias=l.bp, resid=x, rowscale=s_attn,
+                                                  rows_per_scale=HW), M, Cp, nh * 32, cd)
         if self.fused_mlp:   # LN2 -> fc1 + GELU -> fc2 + residual in one launch
             f1, f2 = blk.fc1, blk.fc2
             H.swin_mlp_fwd(S["mid"], Cp, blk.n2.weight, blk.n2.bias, blk.n2.eps, self.C, S["ln2"], Cp, S["m2"], S["r2"],
@@ -820,10 +881,10 @@ class SwinIREngine:
         H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps,
                         one_col=self.C)
         l = blk.fc1
-        H.gemm_nt(H.rows(S["ln2"]), H.rows(l.Wp), H.epilogue(S["h"], bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N,
+        self._nt(H.rows(S["ln2"]), H.rows(l.Wp), H.epilogue(S["h"], bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N,
                                                                pre_grad=True), M, l.Np, Cp, cd)
         l = blk.fc2
-        H.gemm_nt(H.rows(S["h"]), H.rows(l.Wp), H.epilogue(S["out"], bias=l.bp, resid=S["mid"], rowscale=s_mlp,
+        self._nt(H.rows(S["h"]), H.rows(l.Wp), H.epilogue(S["out"], bias=l.bp, resid=S["mid"], rowscale=s_mlp,
                                                             rows_per_scale=HW), M, Cp, self.Hdp, cd)
         return S["out"]
 
@@ -832,12 +893,14 @@ class SwinIREngine:
     # ------------------------------------------------------------------------------------
     def _wgrad(self, P, A, Bop, M, N, K, layer_map, wgrad, bgrad=None, ones_col=-1, ws=None, max_ctas=0):
         S = H.wgrad_splits(M, N, K)
+        if self.x3:   # (gradient, activation) operands
+            A.x3_exp, Bop.x3_exp = P["e_g"], 0
         if max_ctas > 0:   # fewer row splits: at most max_ctas (tile, split) workgroups
             S = max(1, min(S, max_ctas // H.wgrad_tiles(N, K)))
         elif max_ctas < 0:   # more, shorter ones (-max_ctas times the splits, >= 32 rows each)
             S = min(S * -max_ctas, -(-M // 32))
         ws = P["wg_ws"] if ws is None else ws
-        H.gemm_tn(A, Bop, ws, S, M, N, K, self.cd)
+        H.gemm_tn(A, Bop, ws, S, M, N, K, self.tn_cd)
         H.wgrad_finalize(ws, S, layer_map, wgrad, bgrad, ones_col)
 
     def _run_conv_job(self, P, job, ws=None, max_ctas=0):
@@ -869,6 +932,7 @@ class SwinIREngine:
         # E = v / img_range + ...: dL/dv = dL/dE / img_range, folded into the loss kernel's gradient scale
         # (which also scales the reported loss, undone below)
         wr = loss_weight / self.img_range
+        P["e_g"] = self._x3_grad_exp(B * self.in_ch * Hh * self.scale * Ww * self.scale)
         if self.upsampler == "pixelshuffledirect":
             H.l1_loss(P["E"], H_img, P["loss"], P["dE"], self.up1.Cop, wr, B, self.in_ch, Hh * self.scale,
                       Ww * self.scale, P["loss_ws"], ps_r=self.scale, charb_eps=charb_eps)
@@ -887,6 +951,9 @@ class SwinIREngine:
         # dE = gE through the same layout the loss kernel writes: reuse l1 machinery is not possible,
         # so scatter with the image->nhwc kernel (channel stride / pre-shuffle layout).
         inv = 1.0 / self.img_range   # E = v / img_range + ...
+        if self.x3:   # an arbitrary upstream gradient: its exponent from its own range (one host sync)
+            mx = float(gE.abs().max()) * inv
+            P["e_g"] = int(-math.floor(math.log2(mx))) - 2 if mx > 0 and math.isfinite(mx) else 0
         if self.upsampler != "pixelshuffledirect":
             H.image_to_nhwc(gE.contiguous(), P["dE"], 16, None, inv, B, self.in_ch, Hh * self.scale, Ww * self.scale)
         else:
@@ -896,6 +963,7 @@ class SwinIREngine:
 
     def backward(self, grads, P):
         cd = self.cd
+        self._ax = P["e_g"]   # fp32x3: backward GEMM A operands / fp16 outputs are data gradients
         B, Hh, Ww, M = P["B"], P["H"], P["W"], P["M"]
         Cp = self.Cp
         g = lambda p: grads[p]
@@ -914,7 +982,7 @@ class SwinIREngine:
                                        r_last, B, h, w)
                 H.conv3x3_narrow_wgrad(P["dE"], 16, src, tl, self.in_ch, P["narrow_ws"], g(c.w), g(c.b), B, h, w)
             else:
-                H.gemm_nt(H.im2col(P["dE"], h, w, 16, flip=True), H.rows(c.Wd),
+                self._nt(H.im2col(P["dE"], h, w, 16, flip=True), H.rows(c.Wd),
                           H.epilogue(P["dpre"][-1], mode=H.OUT_PUNSHUF_SPM, ldo=self.ups[-1].Co,
                                      ps=(r_last, h // r_last, w // r_last)),
                           B * h * w, 64, 9 * 16, cd)
@@ -937,12 +1005,12 @@ class SwinIREngine:
                                  gate=P["a0"], ldg=tl, slope=0.01)
                 elif i > 0:
                     rp = self.ups_r[i - 1]
-                    H.gemm_nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),
+                    self._nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),
                               H.epilogue(P["dpre"][i - 1], mode=H.OUT_PUNSHUF_SPM, ldo=self.ups[i - 1].Co,
                                          ps=(rp, h // rp, w // rp)),
                               B * h * w, 64, 9 * c.Co, cd)
                 else:
-                    H.gemm_nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),
+                    self._nt(H.im2col(dpre, h, w, c.Co, flip=True), H.rows(c.Wd),
                               H.epilogue(P["da0"], gate=P["a0"], ldg=tl, gate_kind=2, slope=0.01), M, 64, 9 * c.Co, cd)
                 self._wgrad(P, H.rows(dpre), H.im2col(src, h, w, 64, ld=tl), B * h * w, c.Co, 9 * 64, c.map, g(c.w))
                 self._bias_colsum(P, H.rows(dpre), B * h * w, c.Co, c.mapb, g(c.b))
@@ -951,14 +1019,14 @@ class SwinIREngine:
                     M // 96 >= self.conv_wr_min_tiles):
                 H.conv3x3_wr(P["da0"], 64, 1, c.Wc16, None, None, P["dfb"], B, Hh, Ww, 64, Cp, split=False)
             else:
-                H.gemm_nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)
+                self._nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)
             self._wgrad(P, H.rows(P["da0"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, 64, 9 * Cp, c.map,
                         g(c.w), g(c.b), self.C)
         elif self.upsampler == "nearest+conv":
             self._nearest_tail_bwd(P, grads)
         else:   # pixelshuffledirect (one conv + PixelShuffle) or the denoising conv_last (E = x + conv_last / range)
             c = self.up1 if self.upsampler == "pixelshuffledirect" else self.last
-            H.gemm_nt(H.im2col(P["dE"], Hh, Ww, c.Cop, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * c.Cop, cd)
+            self._nt(H.im2col(P["dE"], Hh, Ww, c.Cop, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * c.Cop, cd)
             self._wgrad(P, H.rows(P["dE"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, c.Cop, 9 * Cp, c.map,
                         g(c.w), g(c.b), self.C)
         # ---- conv_after_body (fb = cab(nf) + f0) ------------------------------------------
@@ -1038,12 +1106,12 @@ class SwinIREngine:
         h, w = 4 * Hh, 4 * Ww
         ML = B * h * w
         c = self.last
-        H.gemm_nt(H.im2col(P["dE"], h, w, 16, flip=True), H.rows(c.Wd),
+        self._nt(H.im2col(P["dE"], h, w, 16, flip=True), H.rows(c.Wd),
                   H.epilogue(P["dz_hr"], gate=P["nhr"], gate_kind=2, slope=0.2), ML, 64, 9 * 16, cd)
         self._wgrad(P, H.rows(P["dE"]), H.im2col(P["nhr"], h, w, 64), ML, 16, 9 * 64, c.map, g(c.w))
         self._bias_colsum(P, H.rows(P["dE"]), ML, 16, c.mapb, g(c.b))
         c = self.hrc
-        H.gemm_nt(H.im2col(P["dz_hr"], h, w, 64, flip=True), H.rows(c.Wd),
+        self._nt(H.im2col(P["dz_hr"], h, w, 64, flip=True), H.rows(c.Wd),
                   H.epilogue(P["dz_u"], gate=P["nup_act"][1], gate_kind=2, slope=0.2), ML, 64, 9 * 64, cd)
         self._wgrad(P, H.rows(P["dz_hr"]), H.im2col(P["nup_act"][1], h, w, 64), ML, 64, 9 * 64, c.map, g(c.w))
         self._bias_colsum(P, H.rows(P["dz_hr"]), ML, 64, c.mapb, g(c.b))
@@ -1053,7 +1121,7 @@ class SwinIREngine:
             Mi = B * h * w
             src = P["nup_act"][0] if i == 1 else P["a0"]
             G_hi = P["G_hi"][:Mi]
-            H.gemm_nt(H.im2col(dz, h, w, 64, flip=True), H.rows(c.Wd), H.epilogue(G_hi), Mi, 64, 9 * 64, cd)
+            self._nt(H.im2col(dz, h, w, 64, flip=True), H.rows(c.Wd), H.epilogue(G_hi), Mi, 64, 9 * 64, cd)
             self._wgrad(P, H.rows(dz), H.im2col(src, h, w, 64, up=2), Mi, 64, 9 * 64, c.map, g(c.w))
             self._bias_colsum(P, H.rows(dz), Mi, 64, c.mapb, g(c.b))
             h, w = h // 2, w // 2
@@ -1064,7 +1132,7 @@ class SwinIREngine:
             H.act_grad_cast(G_lo, 64, src, 64, nxt, 64, Mo, 64, 2, 0.2 if i == 1 else 0.01)
             dz = nxt
         c = self.cbu
-        H.gemm_nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)
+        self._nt(H.im2col(P["da0"], Hh, Ww, 64, flip=True), H.rows(c.Wd), H.epilogue(P["dfb"]), M, Cp, 9 * 64, cd)
         self._wgrad(P, H.rows(P["da0"]), H.im2col(P["fb"], Hh, Ww, Cp, ones_col=self.C), M, 64, 9 * Cp, c.map,
                     g(c.w), g(c.b), self.C)
 
@@ -1138,19 +1206,22 @@ class SwinIREngine:
             self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False, P["rg_nb"][self.Hdp]))
         else:
             # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
-            H.gemm_nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
-            H.gemm_nt(H.rows(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
+            self._nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
+            self._nt(H.rows(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
             H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, None, None, False,
                             W["ln2p"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win))
             self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False))
         self._wg(P, H.rows(dU), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), self.Hdp, Cp, fc1, grads, self.C)
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         proj, qkv = blk.proj, blk.qkv
+        if self.x3:
+            self._block_bwd_attn_x3(blk, P, S, x_in, D, bi, grads, j, par)
+            return
         self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
         if self.rowgemm:
             H.rowgemm_store(Da, M, Cp, proj.Wgt, Cp, P["dO"])
         else:
-            H.gemm_nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
+            self._nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
         rows = self.rowgemm   # dq/dk/dv as token rows [M][3 nh 32]: the row GEMM's A operand
         H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
                           W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, dqkv_rows=rows)
@@ -1168,10 +1239,42 @@ class SwinIREngine:
                             W["ln1p"], win=win, copy=cp)
             self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False, P["rg_nb"][qkv.Np]))
         else:
-            H.gemm_nt(H.qkvblk(dqkv, nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
+            self._nt(H.qkvblk(dqkv, nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
             H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
                             W["ln1p"], M, self.C, win, copy=cp)
             self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False))
+
+
+    def _block_bwd_attn_x3(self, blk, P, S, x_in, D, bi, grads, j, par):
+        """The attention half of _block_bwd under fp32x3: O, dO, q/k/v and dq/dk/dv as hi/lo bf16 planes, the
+        split attention backward, split GEMMs (kair_gemm_nt a_split / w_split, kair_gemm_tn x3)."""
+        cd, g = self.cd, (lambda p: grads[p])
+        M, Cp, nh, Hh, Ww = P["M"], self.Cp, self.nh, P["H"], P["W"]
+        HW = Hh * Ww
+        win = (Hh, Ww, 8, blk.shift)
+        drop = P["drop"]
+        hd = self.C // nh
+        W = P["gw"][par][j]
+        Da, dqkv = W["Da"], W["dqkv"]
+        proj, qkv = blk.proj, blk.qkv
+        self._wg(P, H.rows(Da), H.with_lo(H.rows(S["O"][0], ones_col=hd, ones_in_data=True), S["O"][1]), Cp, nh * 32,
+                 proj, grads, hd)
+        self._nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"][0], out_lo=P["dO"][1]), M, nh * 32, Cp, cd)
+        H.window_attn_bwd_x3(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
+                             W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, e_act=0, e_grad=P["e_g"])
+        self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, H.X3, g(blk.table), False))
+        rows_hi, rows_lo = dqkv[0], dqkv[1]
+        self._wg(P, H.with_lo(H.rows(rows_hi), rows_lo), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp,
+                 qkv, grads, self.C)
+        n = blk.n1
+        cp = None
+        if j > 0:   # the previous block's MLP operand: s_mlp(prev) * dL/d x_in
+            cp = H.copy_desc(P["gw"][par][j - 1]["Dm"], rowscale=drop[bi - 1, 1] if drop is not None else None,
+                             rows_per_scale=HW)
+        self._nt(H.with_lo(H.rows(rows_hi), rows_lo), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
+        H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
+                        W["ln1p"], M, self.C, win, copy=cp)
+        self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False))
 
 
 class SwinIRFunction(torch.autograd.Function):

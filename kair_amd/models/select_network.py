@@ -57,21 +57,33 @@ def define_G(opt):
     return net
 
 
+_X3_NETS = ("swinir",)   # networks with a split-fp16 (fp32x3) engine
+
+
 def compute_dtype_of(opt):
     """The engine's arithmetic, decided by the option file as the reference decides it:
-      netG.compute_dtype ('bf16' / 'fp32')  explicit choice (build-side key, absent from reference files);
+      netG.compute_dtype ('bf16' / 'fp32' / 'fp32x3')  explicit choice (build-side key, absent from
+                                            reference files);
       train.amp_enabled: true               the reference's reduced-precision mode (model_plain.py:32-35,
                                             261-275: fp16 autocast + GradScaler) -> the bf16 MFMA engine
                                             (fp32 master weights / accumulation; bf16 keeps fp32's exponent
                                             range, so no loss scaling and no {iter}_scaler.pth);
-      otherwise                             'fp32': the reference's default fp32 arithmetic (exact-fp32 MFMA)."""
+      otherwise                             the reference's default fp32 arithmetic: 'fp32x3' where the
+                                            network has that engine (SwinIR: every product on the 16-bit
+                                            matrix cores as three fp16 products of power-of-2-scaled hi/lo
+                                            pairs, ~2^-21 relative -- it passes the exact-fp32 engine's oracle
+                                            bars, tests/test_x3_gpu.py), else 'fp32' (exact-fp32 MFMA)."""
     o = opt["netG"]
     if o.get("compute_dtype"):
-        if o["compute_dtype"] not in ("bf16", "fp32"):
-            raise ValueError(f"netG.compute_dtype must be 'bf16' or 'fp32' (got {o['compute_dtype']!r})")
+        if o["compute_dtype"] not in ("bf16", "fp32", "fp32x3"):
+            raise ValueError(f"netG.compute_dtype must be 'bf16', 'fp32' or 'fp32x3' (got {o['compute_dtype']!r})")
+        if o["compute_dtype"] == "fp32x3" and o.get("net_type") not in _X3_NETS:
+            raise ValueError(f"netG.compute_dtype 'fp32x3' is available for {_X3_NETS} (got {o.get('net_type')!r})")
         return o["compute_dtype"]
     tr = opt.get("train") or {}
-    return "bf16" if tr.get("amp_enabled") else "fp32"
+    if tr.get("amp_enabled"):
+        return "bf16"
+    return "fp32x3" if o.get("net_type") in _X3_NETS else "fp32"
 
 
 def _engine_kwargs(opt):

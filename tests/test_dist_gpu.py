@@ -28,12 +28,20 @@ B = 4
 
 
 CONFIGS = {"fp32-small": dict(dtype="fp32", C=60, img=16, tol=1e-5, tol_upd=1e-4),
-           "bf16-c4": dict(dtype="bf16", C=180, img=24, tol=5e-4, tol_upd=5e-3)}
+           "bf16-c4": dict(dtype="bf16", C=180, img=24, tol=5e-4, tol_upd=5e-3),
+           # the split-bf16 engine (the reference's fp32 arithmetic) at the C4 width
+           "fp32x3-c4": dict(dtype="fp32x3", C=180, img=24, tol=1e-5, tol_upd=1e-4),
+           # C5: RRDBNet x4 (ESRGAN generator) with its gradient segments (tail, RRDB groups last to first,
+           # the first group with conv_first: rrdbnet_engine.grad_segments), 6 RRDBs -> 3 buckets
+           "rrdbnet-c5": dict(net="rrdbnet", dtype="bf16", nb=6, img=16, sf=4, tol=5e-4, tol_upd=5e-3)}
 
 
 def _net(cfg):
-    from kair_amd.models.network_swinir import SwinIR
     torch.manual_seed(5)
+    if cfg.get("net") == "rrdbnet":
+        from kair_amd.models.network_rrdbnet import RRDBNet
+        return RRDBNet(in_nc=3, out_nc=3, nf=64, nb=cfg["nb"], gc=32, sf=cfg["sf"], compute_dtype=cfg["dtype"])
+    from kair_amd.models.network_swinir import SwinIR
     return SwinIR(upscale=2, in_chans=3, img_size=cfg["img"], window_size=8, img_range=1.0, depths=[2, 2],
                   embed_dim=cfg["C"], num_heads=[6, 6], mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.0,
                   compute_dtype=cfg["dtype"])
@@ -41,8 +49,8 @@ def _net(cfg):
 
 def _data(cfg):
     g = torch.Generator().manual_seed(17)
-    n = cfg["img"]
-    return torch.rand(B, 3, n, n, generator=g), torch.rand(B, 3, 2 * n, 2 * n, generator=g)
+    n, sf = cfg["img"], cfg.get("sf", 2)
+    return torch.rand(B, 3, n, n, generator=g), torch.rand(B, 3, sf * n, sf * n, generator=g)
 
 
 def _run(rank, world, port, out_dir, name):
@@ -61,8 +69,9 @@ def _run(rank, world, port, out_dir, name):
         net, ema = net.to(dev).train(), ema.to(dev).eval()
         tr = FusedTrainer(net, ema, lr=1e-3, E_decay=0.9, use_graph=True, bucket_mb=0.01)
         eng = tr.engine
-        kernels = {"fused_attn": eng.fused_attn, "fused_mlp": eng.fused_mlp, "rowgemm": eng.rowgemm,
-                   "grouped_wgrad": eng.grouped_wgrad, "side_stream": eng.side_stream, "split_act": eng.split_act}
+        kernels = ({"fused_attn": eng.fused_attn, "fused_mlp": eng.fused_mlp, "rowgemm": eng.rowgemm,
+                    "grouped_wgrad": eng.grouped_wgrad, "side_stream": eng.side_stream, "split_act": eng.split_act}
+                   if hasattr(eng, "fused_attn") else {})
         p0 = tr.flat_p.detach().cpu().clone()
         L, Hh = _data(cfg)
         per = B // world
@@ -99,6 +108,8 @@ def test_fused_trainer_world2_matches_single_process(name):
         assert single.exitcode == 0
         r0, r1, s = (torch.load(os.path.join(d, f), weights_only=True) for f in ("r0_w2.pt", "r1_w2.pt", "r0_w1.pt"))
     assert r0["segmented"] and r0["buckets"] > 1   # the overlapped per-bucket all-reduce path ran
+    if name == "rrdbnet-c5":
+        assert r0["buckets"] == 3, r0["buckets"]
     if name == "bf16-c4":   # the production kernel set ran under the segmented capture
         assert all(r0["kernels"].values()), r0["kernels"]
     # the ranks stay in lockstep

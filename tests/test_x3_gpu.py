@@ -1,0 +1,305 @@
+"""The split-bf16 ("fp32x3") path: every contraction as hi.hi + hi.lo + lo.hi of hi/lo bf16 pairs, the
+fp32 reference's arithmetic on the bf16 matrix cores (the reference trains SwinIR classical x4 in fp32:
+models/model_plain.py:31-36, options/swinir/train_swinir_sr_classical.json has no amp_enabled).
+
+Kernels are checked against float64 torch references at the fp32 engine's tolerances (2e-5 .. 5e-5
+relative); the whole network passes the fp32 engine's own oracle bars unchanged (outputs < 1e-4, gradients
+< 1e-3 / 2e-3, PSNR < 1e-3 dB, the 3-step ModelPlain trajectory < 1e-4)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from conftest import load_golden, sub_grads, sub_state  # noqa: E402
+from kair_amd import _hip as H  # noqa: E402
+from kair_amd.engine.trainer import FusedTrainer  # noqa: E402
+from kair_amd.models.network_swinir import SwinIR  # noqa: E402
+from oracle import image as oimg  # noqa: E402
+from oracle import swinir as osw  # noqa: E402
+from test_kernels_gpu import _attn_ref  # noqa: E402
+
+dev = torch.device("cuda")
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def hilo(x, e=0):
+    """The fp16 pair planes of x * 2^e: [2, *x.shape] (hi = f16(x 2^e), lo = f16(x 2^e - hi))."""
+    w = x * 2.0 ** e
+    hi = w.to(torch.float16)
+    lo = (w - hi.float()).to(torch.float16)
+    return torch.stack([hi, lo])
+
+
+@pytest.mark.parametrize("kind,base", [(17, 0), (18, 2), (19, 3)])
+def test_split_pack_kinds(kind, base):
+    """Pack kinds 17 / 18 / 19: fp16 pairs of w 2^KAIR_X3_WEXP for kinds 0 / 2 / 3, interleaved per 64 columns;
+    (hi + lo) 2^-KAIR_X3_WEXP reproduces the plain fp32 form to ~2^-21 relative."""
+    g = torch.Generator().manual_seed(3)
+    if base == 2:
+        N, K = 72, 40
+        w = torch.randn(N, K, 3, 3, generator=g)
+        m, mb = H.wmap(kind, N, K, (1, N, 80), (1, K, 48)), H.wmap(base, N, K, (1, N, 80), (1, K, 48))
+        rows, rowlen = 48, 9 * 80
+    else:
+        N, K = 100, 70
+        w = torch.randn(N, K, generator=g)
+        m, mb = H.wmap(kind, N, K, (1, N, 104), (1, K, 72)), H.wmap(base, N, K, (1, N, 104), (1, K, 72))
+        rows, rowlen = (104, 72) if base == 0 else (72, 104)
+    wd = w.to(dev)
+    plain = torch.empty(rows, rowlen, device=dev)
+    H.pack_weight(wd, plain, mb)
+    KS = 2 * (-(-rowlen // 64)) * 64
+    sp = torch.full((rows, KS), float("nan"), device=dev, dtype=torch.float16)
+    H.pack_weight(wd, sp, m)
+    torch.cuda.synchronize()
+    s = sp.double().cpu().view(rows, KS // 128, 2, 64) * 2.0 ** -H.X3_WEXP
+    recon = (s[:, :, 0] + s[:, :, 1]).reshape(rows, -1)[:, :rowlen]
+    assert torch.isfinite(s).all()
+    assert rel(recon, plain) < 1e-6
+    assert (s[:, :, 0].reshape(rows, -1)[:, rowlen:] == 0).all()
+
+
+@pytest.mark.parametrize("a_bf, b_bf, b_im2col", [(False, False, False), (True, True, False), (False, True, False),
+                                                  (False, False, True), (True, False, True)])
+@pytest.mark.parametrize("M,N,K", [(3000, 576, 192), (777, 64, 40), (2304, 192, 384)])
+def test_gemm_tn_x3(a_bf, b_bf, b_im2col, M, N, K):
+    """kair_gemm_tn compute KAIR_COMPUTE_X3: fp32 operands split in the kernel (with an exponent), or fp16 pair
+    planes carrying one; the bias column injected (ones_col) -- against float64, tighter than the fp32 path."""
+    g = torch.Generator().manual_seed(5)
+    dy = torch.randn(M, N, generator=g) * 1e-6   # a gradient-sized operand, exponent 20
+    if b_im2col:
+        if M % 16:
+            pytest.skip("im2col case needs M = 16 * W")
+        Cin = 32 if K >= 288 else 8
+        B_, Hh, Ww = 1, 16, M // 16
+        x = torch.randn(M, Cin, generator=g)
+        xi = x.view(B_, Hh, Ww, Cin).permute(0, 3, 1, 2)
+        cols = torch.nn.functional.unfold(xi.double(), 3, padding=1)   # [1, Cin*9, HW], c-major taps
+        cols = cols.view(Cin, 9, M).permute(2, 1, 0).reshape(M, 9 * Cin)   # k = tap*Cin + c
+        K = 9 * Cin
+        ref = dy.double().T @ cols
+        Bsrc = x
+    else:
+        x = torch.randn(M, K, generator=g)
+        ones = K - 3
+        xr = x.clone()
+        xr[:, ones] = 1.0
+        ref = dy.double().T @ xr.double()
+        Bsrc = x
+    S = H.wgrad_splits(M, N, K)
+    ws = torch.empty(S, N, K, device=dev)
+    if a_bf:
+        ap = hilo(dy.to(dev), 20)
+        A = H.with_lo(H.rows(ap[0]), ap[1])
+    else:
+        A = H.rows(dy.to(dev))
+    A.x3_exp = 20
+    if b_bf:
+        bp = hilo(Bsrc.to(dev))
+        Bop = H.rows(bp[0], ones_col=K - 3) if not b_im2col else H.im2col(bp[0], Hh, Ww, Bsrc.shape[1])
+        Bop = H.with_lo(Bop, bp[1])
+    else:
+        Bop = H.rows(Bsrc.to(dev), ones_col=K - 3) if not b_im2col else H.im2col(Bsrc.to(dev), Hh, Ww, Bsrc.shape[1])
+    H.gemm_tn(A, Bop, ws, S, M, N, K, H.X3)
+    torch.cuda.synchronize()
+    assert rel(ws.sum(0), ref) < 2e-6
+
+
+def test_gemm_nt_x3_rows_and_qkvblk():
+    """kair_gemm_nt as the fp32x3 engine calls it (compute KAIR_COMPUTE_X3): fp32 A and an fp16 pair A, split-packed
+    fp16 weights (kind 17), ROWS fp32 and head-blocked q/k/v fp16-pair outputs (with an output exponent)."""
+    g = torch.Generator().manual_seed(7)
+    M, N, K, C = 4 * 64, 3 * 6 * 32, 192, 180
+    x = torch.zeros(M, K)
+    x[:, :C] = torch.randn(M, C, generator=g)
+    w = torch.randn(3 * 180, C, generator=g) * 0.05
+    b = torch.randn(3 * 180, generator=g) * 0.1
+    grp_n, grp_k = (18, 30, 32), (1, C, K)
+    Wp = torch.empty(N, 2 * 192, device=dev, dtype=torch.float16)
+    H.pack_weight(w.to(dev), Wp, H.wmap(17, 540, C, grp_n, grp_k))
+    bp = torch.empty(N, device=dev)
+    H.pack_weight(b.to(dev), bp, H.wmap(4, 540, 0, grp_n, (1, 1, 1)))
+    ref = x[:, :C].double() @ w.double().T + b.double()   # [M][540], column (part, h, d)
+    refp = torch.zeros(M, 18, 32, dtype=torch.float64)
+    refp[..., :30] = ref.view(M, 18, 30)
+    def wop():
+        o = H.rows(Wp)
+        o.x3_exp = H.X3_WEXP
+        return o
+    for a_mode in ("f32", "pair"):
+        def aop():
+            if a_mode == "f32":
+                o = H.rows(x.to(dev))
+            else:
+                xp = hilo(x.to(dev), 3)
+                o = H.with_lo(H.rows(xp[0]), xp[1])
+            o.x3_exp = 0 if a_mode == "f32" else 3
+            return o
+        out = torch.empty(M, N, device=dev)
+        H.gemm_nt(aop(), wop(), H.epilogue(out, bias=bp), M, N, K, H.X3)
+        qkv = torch.empty(2, 3 * M * 6 * 32, device=dev, dtype=torch.float16)
+        E = H.epilogue(qkv[0], mode=H.OUT_QKVBLK, ldo=0, bias=bp, qkv=(6, 32, 64), out_lo=qkv[1])
+        E.x3_out_exp = 2
+        H.gemm_nt(aop(), wop(), E, M, N, K, H.X3)
+        torch.cuda.synchronize()
+        assert rel(out.view(M, 18, 32), refp) < 2e-6
+        blk = (qkv[0].double() + qkv[1].double()).cpu().view(3, M // 64, 6, 64, 32).permute(1, 3, 0, 2, 4).reshape(M, 18, 32)
+        assert rel(blk / 4, refp) < 2e-6
+
+
+@pytest.mark.parametrize("shift", [0, 4])
+def test_window_attention_x3(shift):
+    """kair_window_attn_fwd_x3 / _bwd_x3 against float64 autograd of WindowAttention (network_swinir.py:114-145)
+    at the fp32 kernels' tolerances (fwd 2e-5, bwd 5e-5); dq/dk/dv as token rows."""
+    B, Hh, Ww, nh, hd = 2, 16, 24, 6, 30
+    nWin = B * (Hh // 8) * (Ww // 8)
+    scale = hd ** -0.5
+    g = torch.Generator().manual_seed(19)
+    q, k, v = (torch.randn(nWin, nh, 64, hd, generator=g) for _ in range(3))
+    table = torch.randn(225, nh, generator=g) * 0.5
+    qr, kr, vr, tr = (t.double().clone().requires_grad_(True) for t in (q, k, v, table))
+    o = _attn_ref(qr, kr, vr, tr, nh, shift, Hh, Ww, scale)
+    go = torch.randn(o.shape, generator=g, dtype=torch.float64)
+    o.backward(go)
+    qkv = torch.zeros(3, nWin, nh, 64, 32)
+    qkv[0, ..., :hd], qkv[1, ..., :hd], qkv[2, ..., :hd] = q, k, v
+    e_act, e_grad = 1, 24    # exponents of the stored pairs: q/k/v / O and the gradients (dO ~ 1e-7 below)
+    qkv_p = hilo(qkv.view(-1).to(dev), e_act)
+    O = torch.empty(2, nWin * 64, nh * 32, device=dev, dtype=torch.float16)
+    lse = torch.empty(nWin, nh, 64, device=dev)
+    H.window_attn_fwd_x3(qkv_p, table.to(dev), O, nh * 32, lse, nWin, nh, hd, scale, Hh, Ww, shift, e_in=e_act, e_out=e_act)
+    torch.cuda.synchronize()
+    Of = (O[0].double() + O[1].double()).cpu().view(nWin, 64, nh, 32) * 2.0 ** -e_act
+    assert rel(Of[..., :hd].permute(0, 2, 1, 3), o.detach()) < 2e-6
+    assert Of[..., hd:].abs().max() == 0
+    dO = torch.zeros(nWin, 64, nh, 32)
+    dO[..., :hd] = go.float().permute(0, 2, 1, 3) * 1e-7
+    dO_p = hilo(dO.view(nWin * 64, nh * 32).to(dev), e_grad)
+    dqkv = torch.empty(2, nWin * 64, 3 * nh * 32, device=dev, dtype=torch.float16)
+    dtab = torch.empty(225, nh, device=dev)
+    ws = torch.empty(H.window_attn_bwd_ws(nWin, nh), device=dev)
+    H.window_attn_bwd_x3(qkv_p, O, nh * 32, dO_p, nh * 32, table.to(dev), lse, dqkv, dtab, False, ws, nWin, nh, hd, scale,
+                         Hh, Ww, shift, e_act=e_act, e_grad=e_grad)
+    torch.cuda.synchronize()
+    d = (dqkv[0].double() + dqkv[1].double()).cpu().view(nWin, 64, 3, nh, 32)[..., :hd].permute(2, 0, 3, 1, 4)
+    d = d * 2.0 ** -e_grad * 1e7
+    assert rel(d[0], qr.grad) < 5e-6
+    assert rel(d[1], kr.grad) < 5e-6
+    assert rel(d[2], vr.grad) < 5e-6
+    assert rel(dtab * 1e7, tr.grad) < 5e-6
+
+
+def small(ups, sc, dt):
+    return SwinIR(upscale=sc, in_chans=3, img_size=16, window_size=8, img_range=1.0, depths=[2, 2], embed_dim=60,
+                  num_heads=[6, 6], mlp_ratio=2, upsampler=ups, resi_connection="1conv", drop_path_rate=0.0,
+                  compute_dtype=dt)
+
+
+@pytest.mark.parametrize("tag,ups,sc", [("classical", "pixelshuffle", 4), ("light", "pixelshuffledirect", 2)])
+def test_swinir_small_x3_vs_golden(tag, ups, sc):
+    """The fp32 engine's golden bars (tests/test_swinir_gpu.py::test_swinir_small_vs_golden, fp32 row)."""
+    z = load_golden("swinir_small")
+    pre = tag + "."
+    net = small(ups, sc, "fp32x3")
+    net.load_state_dict(sub_state(z, pre), strict=True)
+    net = net.to(dev).train()
+    L = torch.from_numpy(z[pre + "L"]).to(dev)
+    Hh = torch.from_numpy(z[pre + "H"]).to(dev)
+    E = net(L)
+    assert rel(E, torch.from_numpy(z[pre + "E"])) < 1e-4
+    loss = torch.nn.functional.l1_loss(E, Hh)
+    loss.backward()
+    g = sub_grads(z, pre)
+    worst = max((rel(p.grad, g[k]), k) for k, p in net.named_parameters())
+    assert worst[0] < 2e-3, worst
+
+
+def test_swinir_classical_full_x3_vs_oracle():
+    """test_swinir_gpu.py::test_swinir_classical_full_fp32_vs_oracle's bars on the split-bf16 engine."""
+    from test_swinir_gpu import classical_x4, synth_batch
+    net = classical_x4("fp32x3")
+    ref = osw.SwinIR(4, 3, 48, 8, 1.0, [6] * 6, 180, [6] * 6, 2, "pixelshuffle")
+    ref.load_state_dict(net.state_dict(), strict=True)
+    L, Hh = synth_batch(2)
+    Er = ref(L)
+    torch.nn.functional.l1_loss(Er, Hh).backward()
+    net = net.to(dev).train()
+    E = net(L.to(dev))
+    assert rel(E, Er) < 1e-4
+    for i in range(2):
+        pf_gpu, pf_cpu = oimg.psnr_float(E[i].cpu(), Hh[i]), oimg.psnr_float(Er[i].detach(), Hh[i])
+        assert abs(pf_gpu - pf_cpu) < 1e-3
+        pu_gpu = oimg.calculate_psnr(oimg.tensor2uint(E[i].cpu()), oimg.tensor2uint(Hh[i]), border=4)
+        pu_cpu = oimg.calculate_psnr(oimg.tensor2uint(Er[i].detach()), oimg.tensor2uint(Hh[i]), border=4)
+        assert abs(pu_gpu - pu_cpu) < 1e-3
+    torch.nn.functional.l1_loss(E, Hh.to(dev)).backward()
+    gref = dict(ref.named_parameters())
+    worst = max((rel(p.grad, gref[k].grad), k) for k, p in net.named_parameters())
+    assert worst[0] < 1e-3, worst
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_trainer_x3_matches_reference_trajectory(use_graph):
+    """3 fused-trainer steps on the split-bf16 engine against the reference ModelPlain trajectory (1e-4)."""
+    z = load_golden("train_trajectory")
+    mk = lambda: SwinIR(upscale=4, in_chans=3, img_size=16, window_size=8, img_range=1.0, depths=[2, 2], embed_dim=60,
+                        num_heads=[6, 6], mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.0,
+                        compute_dtype="fp32x3")
+    net, ema = mk(), mk()
+    net.load_state_dict(sub_state(z, "init."), strict=True)
+    ema.load_state_dict(sub_state(z, "init."), strict=True)
+    net, ema = net.to(dev).train(), ema.to(dev).eval()
+    tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999, use_graph=use_graph)
+    milestones, lr0 = [2, 100], 2e-4
+    losses = []
+    for s in range(1, 4):
+        tr.lr = lr0 * 0.5 ** sum(1 for m in milestones if m <= s)
+        loss = tr.step(torch.from_numpy(z[f"step{s}.L"]).to(dev), torch.from_numpy(z[f"step{s}.H"]).to(dev))
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, z["losses"], rtol=1e-4)
+    fg, fe = sub_state(z, "final.G."), sub_state(z, "final.E.")
+    for k, v in net.state_dict().items():
+        assert rel(v.float(), fg[k].float()) < 1e-4, k
+    for k, v in ema.state_dict().items():
+        assert rel(v.float(), fe[k].float()) < 1e-4, k
+
+
+def test_droppath_injected_masks_x3_vs_oracle():
+    """DropPath with the same keep masks in the split-bf16 engine and the oracle (fwd + every gradient)."""
+    torch.manual_seed(4)
+    net = SwinIR(upscale=2, in_chans=3, img_size=16, window_size=8, img_range=1.0, depths=[2, 2], embed_dim=60,
+                 num_heads=[6, 6], mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.3, compute_dtype="fp32x3")
+    ref = osw.SwinIR(2, 3, 16, 8, 1.0, [2, 2], 60, [6, 6], 2, "pixelshuffle")
+    ref.load_state_dict(net.state_dict(), strict=True)
+    B = 3
+    keep = torch.tensor([1.0 - b.drop_path_rate for l in net.layers for b in l.residual_group.blocks])
+    g = torch.Generator().manual_seed(9)
+    D = (torch.rand(len(keep), 2, B, generator=g) < 0.6).float() / keep.view(-1, 1, 1)
+    D[1, 0, 0] = 0.0
+    D[1, 1, 0] = 1.0 / keep[1]
+    L = torch.rand(B, 3, 16, 16, generator=g)
+    gE = torch.randn(B, 3, 32, 32, generator=g)
+    keeps = [(D[i, 0].view(B, 1, 1), D[i, 1].view(B, 1, 1)) for i in range(len(keep))]
+    Er = ref(L, keeps)
+    Er.backward(gE)
+    net = net.to(dev).train()
+    eng = net.engine()
+    E = eng.forward(L.to(dev), D.to(dev)).clone()
+    params = list(net.parameters())
+    flat = torch.zeros(sum(p.numel() for p in params), device=dev)
+    grads, off = {}, 0
+    for p in params:
+        grads[p] = flat[off:off + p.numel()].view_as(p)
+        off += p.numel()
+    eng.backward_from_grad(gE.to(dev), grads)
+    assert rel(E, Er.detach()) < 1e-4
+    gref = dict(ref.named_parameters())
+    worst = max((rel(grads[p], gref[k].grad), k) for k, p in net.named_parameters())
+    assert worst[0] < 2e-3, worst

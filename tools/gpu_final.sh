@@ -1,23 +1,19 @@
 #!/bin/bash
-# End-of-round GPU record: -m gpu tests, smoke, the default bench line, rocprofv3 kernel-trace stats
-# at B=32 and a per-step breakdown at B=4, and the two PMC passes (HBM traffic) -> gpurun_out/
+# round-4 closing evidence: the full -m gpu suite, the default bench line (all fields), the B = 4 line,
+# per-call-site step breakdowns, then the rocprofv3 stats / PMC passes (tools/gpu_profile_r4.sh)
 set -o pipefail
-R=$(pwd); mkdir -p $R/gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; echo "tests failed"; exit 1; }
-tail -1 gpurun_out/t.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s.log 2>&1 || { tail gpurun_out/s.log; echo "smoke failed"; exit 1; }
-tail -1 gpurun_out/s.log
-timeout -k 10 600 python bench.py > gpurun_out/b.log 2>&1 || { tail -20 gpurun_out/b.log; echo "bench failed"; exit 1; }
-tail -1 gpurun_out/b.log | cut -c1-200
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- \
-  python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32-line --no-other-configs > $R/gpurun_out/p.log 2>&1 || { echo "profile failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/tr4 -o run -- \
-  python3 $R/bench.py --global-batch 4 --steps 8 --warmup 3 --no-cpu-baseline --no-fp32-line --no-other-configs > $R/gpurun_out/tr4.log 2>&1 || { echo "profile4 failed"; exit 1; }
-cd $R
-python3 tools/step_breakdown.py gpurun_out/prof/run_kernel_trace.csv 5 > gpurun_out/b32_breakdown.txt
-python3 tools/step_breakdown.py gpurun_out/tr4/run_kernel_trace.csv 6 > gpurun_out/tr4_breakdown.txt
-rm -f gpurun_out/tr4/run_kernel_trace.csv gpurun_out/prof/run_kernel_trace.csv
-head -3 gpurun_out/b32_breakdown.txt; head -3 gpurun_out/tr4_breakdown.txt
-timeout -k 10 600 bash tools/gpu_pmc.sh || { echo "pmc failed"; exit 1; }
-echo done
+mkdir -p gpurun_out/final4
+bash tools/gpu_tests.sh || exit 1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")" > gpurun_out/final4/smoke.log 2>&1 || { tail -5 gpurun_out/final4/smoke.log; exit 1; }
+tail -1 gpurun_out/final4/smoke.log
+timeout -k 10 600 python -u bench.py > gpurun_out/final4/bench_default.log 2>&1 || { tail -5 gpurun_out/final4/bench_default.log; exit 1; }
+grep -h "^{" gpurun_out/final4/bench_default.log | cut -c1-300
+timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-other-configs --no-fp32-line --no-psnr --per-gpu-batch 4 > gpurun_out/final4/bench4.log 2>&1 || exit 1
+grep -h "^{" gpurun_out/final4/bench4.log | cut -c1-200
+for b in 8 16; do   # the per-GPU shapes of the N = 4 / N = 2 strong-scaling runs
+  timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-other-configs --no-fp32-line --no-psnr --per-gpu-batch $b > gpurun_out/final4/bench$b.log 2>&1 || exit 1
+  grep -h "^{" gpurun_out/final4/bench$b.log | cut -c1-200
+done
+timeout -k 10 200 python -u tools/roles.py 32 > gpurun_out/final4/roles32.txt 2>&1 || exit 1
+timeout -k 10 200 python -u tools/roles.py 4 > gpurun_out/final4/roles4.txt 2>&1 || exit 1
+bash tools/gpu_profile_r4.sh
