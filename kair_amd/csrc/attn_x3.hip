@@ -3,8 +3,9 @@
 // models/model_plain.py:31-36 with no amp_enabled in options/swinir/train_swinir_sr_classical.json).
 //
 // Every operand x is carried as an fp16 pair of x 2^e (hi = f16(x 2^e), lo = f16(x 2^e - hi); e a power-of-2
-// exponent that centres the tensor in fp16's range: 0 for q/k/v, O and the probabilities, the engine's
-// gradient exponent for dO, dS and dq/dk/dv) and every product as three v_mfma_f32_32x32x16_f16:
+// exponent that puts the bulk of the tensor at 2^2 .. 2^10, so the lo half stays a normal fp16 number: the
+// engine's activation exponent for q/k/v and O, P_EXP for the probabilities, its gradient exponent for dO, dS
+// and dq/dk/dv) and every product as three v_mfma_f32_32x32x16_f16:
 // hi.hi + hi.lo + lo.hi, fp32 accumulation, rescaled by 2^-(eA + eB).  The pair holds 22 mantissa bits, so a
 // product is exact to ~2^-21: the fp32 computation's precision class (a bf16 pair reaches 2^-16, one bf16
 // product 2^-8).  The fp32 MFMA (v_mfma_f32_32x32x2_f32) runs at 1/16 of the 16-bit rate; three 16-bit
@@ -22,6 +23,7 @@
 namespace {
 
 constexpr int FWD_NW = 4;
+constexpr int P_EXP = 6;   // the probabilities' exponent: P ~ 1/64 -> ~1, its lo half a normal fp16 number
 
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 KAIR_DEV f16x8 as_f16(const bf16x8& v) { return __builtin_bit_cast(f16x8, v); }
@@ -145,8 +147,8 @@ __global__ __launch_bounds__(64 * FWD_NW) void attn_fwd_x3_kernel(const f16* __r
       for (int r = 0; r < 16; ++r) acc[kt][qt][r] *= inv;
     if (hh == 0) lse[task * TOK + qi] = mx + __logf(sum);
   }
-  // O^T = V^T P^T : tile [qt] rows = d, lane = query (P in [0, 1]: exponent 0)
-  const float so = ldexpf(1.f, e_out - e_in), sone = ldexpf(1.f, e_out);
+  // O^T = V^T P^T : tile [qt] rows = d, lane = query (P with exponent P_EXP)
+  const float so = ldexpf(1.f, e_out - e_in - P_EXP), sone = ldexpf(1.f, e_out), sp = ldexpf(1.f, P_EXP);
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     f32x16 o;
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(64 * FWD_NW) void attn_fwd_x3_kernel(const f16* __r
       for (int s = 0; s < 2; ++s) {
         const f16x8 vh = hrows_perm(sV[w][0], kt * 32, s, lane), vl = hrows_perm(sV[w][1], kt * 32, s, lane);
         f16x8 ph, pl;
-        pack8_pair(acc[kt][qt], s, 1.f, ph, pl);
+        pack8_pair(acc[kt][qt], s, sp, ph, pl);
         o = mfma32(vh, ph, o);
         o = mfma32(vh, pl, o);
         o = mfma32(vl, ph, o);
@@ -216,7 +218,8 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
   // to natural units (S, dP, delta, P, dS) before it is combined
   const float s_qk = ldexpf(1.f, -2 * e_act), s_dp = ldexpf(1.f, -(e_grad + e_act));
   const float s_o = ldexpf(1.f, -e_act), s_g = ldexpf(1.f, -e_grad), s_gup = ldexpf(1.f, e_grad);
-  const float s_dv = 1.f;                    // dO^T P: (e_grad) x (0) -> stored with e_grad as it is
+  const float s_dv = ldexpf(1.f, -P_EXP);    // dO^T P: (e_grad) x (P_EXP) -> e_grad
+  const float s_p = ldexpf(1.f, P_EXP);
   const float s_dk = ldexpf(1.f, -e_act);    // Q^T dS, K^T dS^T: (e_act) x (e_grad) -> e_grad
 
   // the running bias gradient [q][key] in LDS (row stride 72: the two lane halves' rows 4 apart fall in
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
           const f16x8 gl = hrows_perm(sQG[1] + TOK * LD, qt * 32, s, lane);
           const f16x8 qh = hrows_perm(sQG[0], qt * 32, s, lane), ql = hrows_perm(sQG[1], qt * 32, s, lane);
           f16x8 ph, pl, dh, dl;
-          pack8_pair(S[qt][kt], s, 1.f, ph, pl);
+          pack8_pair(S[qt][kt], s, s_p, ph, pl);
           pack8_pair(dP[qt][kt], s, s_gup, dh, dl);
           av = mfma32(gh, ph, av);
           av = mfma32(gh, pl, av);

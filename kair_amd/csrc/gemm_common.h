@@ -190,8 +190,9 @@ KAIR_DEV void raw_to_f32(const Raw<T>& r, float (&v)[8]) {
 }
 
 // lo (fp32 source, bf16 compute): store the lo half bf16(x - bf16(x)) of the (scaled) value instead
+// onev: the value of an injected ones column (x3: 2^e, the operand's own scale)
 template <typename CT, typename T>
-KAIR_DEV void commit_chunk(CT* dst, const Raw<T>& raw, const Pend& pd, bool lo = false) {
+KAIR_DEV void commit_chunk(CT* dst, const Raw<T>& raw, const Pend& pd, bool lo = false, float onev = 1.f) {
   if constexpr (sizeof(CT) == 2 && sizeof(T) == 2) {
     if (pd.scale == 1.f && pd.ones < 0) {          // common case: raw bf16 straight to LDS
       *(uint4*)dst = raw.a;
@@ -205,7 +206,7 @@ KAIR_DEV void commit_chunk(CT* dst, const Raw<T>& raw, const Pend& pd, bool lo =
   float v[8];
   raw_to_f32<T>(raw, v);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (j == pd.ones) ? 1.f : (pd.scale == 0.f ? 0.f : v[j] * pd.scale);
+  for (int j = 0; j < 8; ++j) v[j] = (j == pd.ones) ? onev : (pd.scale == 0.f ? 0.f : v[j] * pd.scale);
   if constexpr (sizeof(CT) == 2) {
     typename V8<CT>::t q;
 #pragma unroll

@@ -30,14 +30,15 @@ KAIR_DEV void commit_lo_plane(f16* dst, const Raw<f16>& raw, const Pend& pd) {
   *(f16x8*)dst = q;
 }
 
-// commit one 8-column chunk of an x3 operand as its hi and lo planes (fp32: split with the operand's scale)
+// commit one 8-column chunk of an x3 operand as its hi and lo planes (fp32: split with the operand's scale);
+// an injected ones column reads 2^e (onev), the operand's own scale
 template <typename T>
-KAIR_DEV void commit_pair(f16* hi, f16* lo, const RawX3<T>& raw, const Pend& pd) {
+KAIR_DEV void commit_pair(f16* hi, f16* lo, const RawX3<T>& raw, const Pend& pd, float onev) {
   if constexpr (sizeof(T) == 4) {
-    commit_chunk<f16, T>(hi, raw.h, pd, false);
-    commit_chunk<f16, T>(lo, raw.h, pd, true);
+    commit_chunk<f16, T>(hi, raw.h, pd, false, onev);
+    commit_chunk<f16, T>(lo, raw.h, pd, true, onev);
   } else {
-    commit_chunk<f16, T>(hi, raw.h, pd, false);
+    commit_chunk<f16, T>(hi, raw.h, pd, false, onev);
     commit_lo_plane(lo, raw.l, pd);
   }
 }
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_x3_kernel(Op A, Op B, Epi E, in
       const int c = tid + p * NT;
       if (c < CA) {
         const int o = (c / CPR) * LD + (c % CPR) * 8;
-        commit_pair<TA>(s0 + o, s0 + PLANE + o, va[p], pa[p]);
+        commit_pair<TA>(s0 + o, s0 + PLANE + o, va[p], pa[p], 1.f);
       }
     }
 #pragma unroll
@@ -254,6 +255,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_tn_x3_kernel(Op A, Op B, float* ws
       }
     }
   };
+  const float onea = ldexpf(1.f, A.x3_exp), oneb = ldexpf(1.f, B.x3_exp);
   auto sstore = [&](int st) {
     f16* sAh = lds + st * STAGE;
     f16* sBh = sAh + BMr * LDA;
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_tn_x3_kernel(Op A, Op B, float* ws
       const int c = tid + p * NT;
       if (c < CA) {
         const int o = (c / CPA) * LDA + (c % CPA) * 8;
-        commit_pair<TA>(sAh + o, sAh + PL + o, va[p], pa[p]);
+        commit_pair<TA>(sAh + o, sAh + PL + o, va[p], pa[p], onea);
       }
     }
 #pragma unroll
@@ -270,7 +272,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_tn_x3_kernel(Op A, Op B, float* ws
       const int c = tid + p * NT;
       if (c < CB) {
         const int o = (c / CPB) * LDB + (c % CPB) * 8;
-        commit_pair<TB>(sBh + o, sBh + PL + o, vb[p], pb[p]);
+        commit_pair<TB>(sBh + o, sBh + PL + o, vb[p], pb[p], oneb);
       }
     }
   };
@@ -398,8 +400,7 @@ int x3_operand_ok(const kair_operand* o, const char* what) {
   KAIR_CHECK_ARG(o->dtype == KAIR_F32 || (o->dtype == KAIR_F16 && o->lo_ptr && ((uintptr_t)o->lo_ptr % 16) == 0),
                  "%s: x3 operands are fp32 or fp16 hi planes with their lo plane (lo_ptr)", what);
   KAIR_CHECK_ARG(o->x3_exp > -100 && o->x3_exp < 100, "%s: x3 exponent out of range", what);
-  // the injected bias column reads 1.0 (an unscaled operand) and no per-row scale rides on a stored pair
-  KAIR_CHECK_ARG(o->ones_col < 0 || o->x3_exp == 0, "%s: x3 ones column needs exponent 0", what);
+  // no per-row scale rides on a stored pair (an injected ones column reads 2^x3_exp)
   KAIR_CHECK_ARG(!o->rowscale || o->dtype == KAIR_F32, "%s: x3 row scale needs an fp32 operand", what);
   return 0;
 }

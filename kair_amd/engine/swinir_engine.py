@@ -286,8 +286,10 @@ class SwinIREngine:
         # fp32x3: the fp32 reference's arithmetic on the 16-bit matrix cores -- every contraction multiplies
         # fp16 pairs of power-of-2-scaled operands (hi.hi + hi.lo + lo.hi, fp32 accumulation; ~2^-21 relative
         # per product), operands fp32 (split inside the kernels) or fp16 hi/lo planes; the unfused launch
-        # sequence of the fp32 engine.  Exponents: weights KAIR_X3_WEXP (packs), activations 0, gradients
-        # P["e_g"] (the loss normalisation, _x3_grad_exp), so every operand sits in fp16's normal range
+        # sequence of the fp32 engine.  Exponents put the bulk of every operand at 2^2 .. 2^10 -- the lo half
+        # (2^-11 of the value) then stays a normal fp16 number (>= 2^-14) while the largest values keep
+        # >= 16x headroom below fp16's 65504: weights KAIR_X3_WEXP (packs: |w| ~ 0.02 -> ~2^6),
+        # activations X3_AEXP (O(1) -> 2^4), gradients P["e_g"] (the loss normalisation, _x3_grad_exp)
         self.x3 = compute_dtype == "fp32x3"
         self._ax = 0   # x3: the exponent of the GEMM A operands / fp16 outputs of the phase being issued
         self.cd = H.BF16 if compute_dtype in ("bf16", "fp32x3") else H.F32
@@ -664,7 +666,7 @@ class SwinIREngine:
         HW = Hh * Ww
         x = x.contiguous()
         self.cur = P
-        self._ax = 0   # fp32x3: forward operands are activations (exponent 0)
+        self._ax = self.X3_AEXP   # fp32x3: forward operands are activations
         P["x"] = x
         P["drop"] = drop_scales
         if self.xin_hilo:
@@ -759,17 +761,21 @@ class SwinIREngine:
             if A.dtype == H.F16 and not A.lo_ptr:
                 raise RuntimeError("fp32x3: an fp16 GEMM operand needs its lo plane")
             A.x3_exp, B.x3_exp = self._ax, H.X3_WEXP
+            if A.ones_col >= 0:
+                raise RuntimeError("fp32x3: no injected ones column on a GEMM A operand")
             if E.out_dtype == H.F16:
                 E.x3_out_exp = self._ax
             H.gemm_nt(A, B, E, M, N, K, H.X3)
             return
         H.gemm_nt(A, B, E, M, N, K, cd)
 
+    X3_AEXP = 4   # fp32x3 activation exponent
+
     @staticmethod
     def _x3_grad_exp(numel):
         """The fp32x3 gradient exponent: the mean-loss gradient is O(1 / numel) per output element, so data
-        gradients times 2^(log2 numel - 2) sit near 2^-2 at the loss, 2^16 below fp16's overflow."""
-        return max(0, int(round(math.log2(max(numel, 1)))) - 2)
+        gradients times 2^(log2 numel + 4) sit near 2^4 at the loss, 2^12 below fp16's overflow."""
+        return int(round(math.log2(max(numel, 1)))) + 4
 
     def _forward_tail(self, P):
         """Reconstruction tail: P['fb'] (conv_after_body + residual) -> P['E']."""
@@ -861,7 +867,7 @@ class SwinIREngine:
                                                                      qkv=(nh, 32, WS_TOK), out_lo=S["qkv"][1]),
                          M, l.Np, Cp, cd)
                 H.window_attn_fwd_x3(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale,
-                                     Hh, Ww, blk.shift, ones_col=self.C // nh, e_in=0, e_out=0)
+                                     Hh, Ww, blk.shift, ones_col=self.C // nh, e_in=self.X3_AEXP, e_out=self.X3_AEXP)
                 A_o = H.with_lo(H.rows(S["O"][0]), S["O"][1])
             else:
                 self._nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
@@ -894,7 +900,7 @@ class SwinIREngine:
     def _wgrad(self, P, A, Bop, M, N, K, layer_map, wgrad, bgrad=None, ones_col=-1, ws=None, max_ctas=0):
         S = H.wgrad_splits(M, N, K)
         if self.x3:   # (gradient, activation) operands
-            A.x3_exp, Bop.x3_exp = P["e_g"], 0
+            A.x3_exp, Bop.x3_exp = P["e_g"], self.X3_AEXP
         if max_ctas > 0:   # fewer row splits: at most max_ctas (tile, split) workgroups
             S = max(1, min(S, max_ctas // H.wgrad_tiles(N, K)))
         elif max_ctas < 0:   # more, shorter ones (-max_ctas times the splits, >= 32 rows each)
@@ -953,7 +959,7 @@ class SwinIREngine:
         inv = 1.0 / self.img_range   # E = v / img_range + ...
         if self.x3:   # an arbitrary upstream gradient: its exponent from its own range (one host sync)
             mx = float(gE.abs().max()) * inv
-            P["e_g"] = int(-math.floor(math.log2(mx))) - 2 if mx > 0 and math.isfinite(mx) else 0
+            P["e_g"] = 8 - int(math.ceil(math.log2(mx))) if mx > 0 and math.isfinite(mx) else 0   # max -> <= 2^8
         if self.upsampler != "pixelshuffledirect":
             H.image_to_nhwc(gE.contiguous(), P["dE"], 16, None, inv, B, self.in_ch, Hh * self.scale, Ww * self.scale)
         else:
@@ -1261,7 +1267,8 @@ class SwinIREngine:
                  proj, grads, hd)
         self._nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"][0], out_lo=P["dO"][1]), M, nh * 32, Cp, cd)
         H.window_attn_bwd_x3(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
-                             W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, e_act=0, e_grad=P["e_g"])
+                             W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, e_act=self.X3_AEXP,
+                             e_grad=P["e_g"])
         self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, H.X3, g(blk.table), False))
         rows_hi, rows_lo = dqkv[0], dqkv[1]
         self._wg(P, H.with_lo(H.rows(rows_hi), rows_lo), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp,

@@ -73,7 +73,7 @@ def test_gemm_tn_x3(a_bf, b_bf, b_im2col, M, N, K):
     """kair_gemm_tn compute KAIR_COMPUTE_X3: fp32 operands split in the kernel (with an exponent), or fp16 pair
     planes carrying one; the bias column injected (ones_col) -- against float64, tighter than the fp32 path."""
     g = torch.Generator().manual_seed(5)
-    dy = torch.randn(M, N, generator=g) * 1e-6   # a gradient-sized operand, exponent 20
+    dy = torch.randn(M, N, generator=g) * 1e-6   # a gradient-sized operand, exponent 24
     if b_im2col:
         if M % 16:
             pytest.skip("im2col case needs M = 16 * W")
@@ -96,17 +96,18 @@ def test_gemm_tn_x3(a_bf, b_bf, b_im2col, M, N, K):
     S = H.wgrad_splits(M, N, K)
     ws = torch.empty(S, N, K, device=dev)
     if a_bf:
-        ap = hilo(dy.to(dev), 20)
+        ap = hilo(dy.to(dev), 24)
         A = H.with_lo(H.rows(ap[0]), ap[1])
     else:
         A = H.rows(dy.to(dev))
-    A.x3_exp = 20
+    A.x3_exp = 24
     if b_bf:
-        bp = hilo(Bsrc.to(dev))
+        bp = hilo(Bsrc.to(dev), 4)
         Bop = H.rows(bp[0], ones_col=K - 3) if not b_im2col else H.im2col(bp[0], Hh, Ww, Bsrc.shape[1])
         Bop = H.with_lo(Bop, bp[1])
     else:
         Bop = H.rows(Bsrc.to(dev), ones_col=K - 3) if not b_im2col else H.im2col(Bsrc.to(dev), Hh, Ww, Bsrc.shape[1])
+    Bop.x3_exp = 4
     H.gemm_tn(A, Bop, ws, S, M, N, K, H.X3)
     torch.cuda.synchronize()
     assert rel(ws.sum(0), ref) < 2e-6
@@ -138,9 +139,9 @@ def test_gemm_nt_x3_rows_and_qkvblk():
             if a_mode == "f32":
                 o = H.rows(x.to(dev))
             else:
-                xp = hilo(x.to(dev), 3)
+                xp = hilo(x.to(dev), 4)
                 o = H.with_lo(H.rows(xp[0]), xp[1])
-            o.x3_exp = 0 if a_mode == "f32" else 3
+            o.x3_exp = 4
             return o
         out = torch.empty(M, N, device=dev)
         H.gemm_nt(aop(), wop(), H.epilogue(out, bias=bp), M, N, K, H.X3)
@@ -170,7 +171,7 @@ def test_window_attention_x3(shift):
     o.backward(go)
     qkv = torch.zeros(3, nWin, nh, 64, 32)
     qkv[0, ..., :hd], qkv[1, ..., :hd], qkv[2, ..., :hd] = q, k, v
-    e_act, e_grad = 1, 24    # exponents of the stored pairs: q/k/v / O and the gradients (dO ~ 1e-7 below)
+    e_act, e_grad = 4, 26    # exponents of the stored pairs: q/k/v / O and the gradients (dO ~ 1e-7 below)
     qkv_p = hilo(qkv.view(-1).to(dev), e_act)
     O = torch.empty(2, nWin * 64, nh * 32, device=dev, dtype=torch.float16)
     lse = torch.empty(nWin, nh, 64, device=dev)

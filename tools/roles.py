@@ -1,7 +1,7 @@
 """Every libkair launch of one SwinIR classical x4 training step, by call site, with its kernel duration
 (bench.time_roles serial: the side-stream work in place, a HIP event pair around each launch).
 
-    python tools/roles.py [B] [--in-step]
+    python tools/roles.py [B] [--in-step] [--dtype bf16|fp32|fp32x3]
 """
 import os
 import sys
@@ -19,8 +19,9 @@ from kair_amd.utils.utils_image import synth_sr_batch  # noqa: E402
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else 32
     dev = torch.device("cuda", 0)
-    net = bench.build_net("bf16", 0.1).to(dev).train()
-    ema = bench.build_net("bf16", 0.1).to(dev).eval()
+    dt = sys.argv[sys.argv.index("--dtype") + 1] if "--dtype" in sys.argv else "bf16"
+    net = bench.build_net(dt, 0.1).to(dev).train()
+    ema = bench.build_net(dt, 0.1).to(dev).eval()
     ema.load_state_dict(net.state_dict())
     tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999)
     L, Hh = synth_sr_batch(B, 48, 4, seed=1000, device=dev)
