@@ -492,6 +492,55 @@ KAIR_DEV void epi_chunk(const Epi& e, long m, int n, float (&v)[8]) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// LDS-DMA ring plumbing (the persistent ring kernels of gemm.hip and gemm_x3.hip)
+// ------------------------------------------------------------------------------------------
+KAIR_DEV void ring_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4 into lds_base + 16 * lane) issued from
+// inline asm.  hipcc treats the builtin form as a pending LDS write and emits s_waitcnt vmcnt(0)
+// before the next ds_read of the shared array -- every chunk of a ring would drain all the DMA (and
+// stores) in flight.  Hidden in asm, the DMA is waited for only by the ring's own counted vmcnt.
+KAIR_DEV void glds16(const void* src, const char* lds_base) {
+  const unsigned la = __builtin_amdgcn_readfirstlane(
+      (unsigned)(unsigned long)(__attribute__((address_space(3))) const char*)lds_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(la) : "memory", "m0");
+}
+
+// Wait for an ordinary (compiler-visible) load's result HERE, on every path: a load still pending
+// at a loop back-edge on any path makes hipcc wait vmcnt(0) at the next write of its register.
+KAIR_DEV void land(float& v) { asm volatile("" : "+v"(v)); }
+KAIR_DEV void land(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
+// ring epilogue operand kinds (compile-time, so the plain kernels carry no epilogue loads at all)
+enum { EX_NONE = 0, EX_RESID = 1, EX_GATE_BF16 = 2, EX_GATE_F32 = 3 };
+
+// a zero line for masked loads (read-only; zero-initialised device memory)
+__device__ __attribute__((aligned(64))) unsigned char g_kair_zero_line[64];
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit field: waiting for more
+// than asked is always safe)
+#define KAIR_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+KAIR_DEV void vm_wait(int n) {
+  n = __builtin_amdgcn_readfirstlane(n);   // scalar branch tree, not exec-masked
+  switch (n < 63 ? n : 63) {
+    KAIR_VMW(0) KAIR_VMW(1) KAIR_VMW(2) KAIR_VMW(3) KAIR_VMW(4) KAIR_VMW(5) KAIR_VMW(6) KAIR_VMW(7)
+    KAIR_VMW(8) KAIR_VMW(9) KAIR_VMW(10) KAIR_VMW(11) KAIR_VMW(12) KAIR_VMW(13) KAIR_VMW(14) KAIR_VMW(15)
+    KAIR_VMW(16) KAIR_VMW(17) KAIR_VMW(18) KAIR_VMW(19) KAIR_VMW(20) KAIR_VMW(21) KAIR_VMW(22) KAIR_VMW(23)
+    KAIR_VMW(24) KAIR_VMW(25) KAIR_VMW(26) KAIR_VMW(27) KAIR_VMW(28) KAIR_VMW(29) KAIR_VMW(30) KAIR_VMW(31)
+    KAIR_VMW(32) KAIR_VMW(33) KAIR_VMW(34) KAIR_VMW(35) KAIR_VMW(36) KAIR_VMW(37) KAIR_VMW(38) KAIR_VMW(39)
+    KAIR_VMW(40) KAIR_VMW(41) KAIR_VMW(42) KAIR_VMW(43) KAIR_VMW(44) KAIR_VMW(45) KAIR_VMW(46) KAIR_VMW(47)
+    KAIR_VMW(48) KAIR_VMW(49) KAIR_VMW(50) KAIR_VMW(51) KAIR_VMW(52) KAIR_VMW(53) KAIR_VMW(54) KAIR_VMW(55)
+    KAIR_VMW(56) KAIR_VMW(57) KAIR_VMW(58) KAIR_VMW(59) KAIR_VMW(60) KAIR_VMW(61) KAIR_VMW(62)
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+  }
+}
+#undef KAIR_VMW
+
 // bijective XCD-aware remap: consecutive logical tiles share an XCD (L2)
 KAIR_DEV int xcd_remap(int hw, int nwg) {
   const int q = nwg / 8, r = nwg % 8;

@@ -335,6 +335,427 @@ __global__ __launch_bounds__(NT, 2) void gemm_tn_x3_kernel(Op A, Op B, float* ws
       }
 }
 
+// ------------------------------------------------------------------------------------------
+// NT ring (x3): the streaming form of the NT product for the hot shapes (Swin linears, 192-channel 3x3
+// convs).  512 threads, one CTA per CU, persistent over the 128 x 192 output tiles of ONE N-tile; every
+// operand byte reaches LDS by LDS-DMA (global_load_lds_dwordx4) through an XR_NS-deep ring of 32-deep
+// k-chunks that runs on across tile boundaries:
+//   A chunk: 128 rows x 128 B -- fp32 (32 values, split into the fp16 pair at the fragment read, with the
+//            operand's 2^e) or an fp16 pair (hi 32 | lo 32);
+//   B chunk: 192 rows x 128 B -- the hi 32 | lo 32 of the split-packed weight row.
+// 16-byte units of LDS row r sit at slot (unit ^ (r & 7)) (source-side XOR swizzle, the fragment reads
+// are conflict-light).  8 waves as 4 (rows) x 2 (columns), wave tile 32 x 96; the MFMA operands are
+// swapped (D = B A^T) so after a v_permlane16_swap of fragment pairs each lane owns 8 consecutive output
+// columns of one row and finishes them with the shared 8-column epilogue.
+// ------------------------------------------------------------------------------------------
+constexpr int XR_BM = 128, XR_BN = 192, XR_NS = 4;
+constexpr int XR_ABYTES = XR_BM * 128, XR_STAGE = XR_ABYTES + XR_BN * 128;   // 16 + 24 KiB
+constexpr int XR_DMA = 5;   // DMA wave-instructions per wave per chunk (2 A + 3 B)
+
+enum { XE_ROWS_F32 = 0, XE_ROWS_PAIR = 1, XE_QKV = 2 };
+
+template <typename TA, int AM, int EM, int EX>
+__global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
+  __shared__ __attribute__((aligned(16))) char smem[XR_NS * XR_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fq = lane >> 4, q8 = lane & 7;
+  const int cta = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = cta % tilesN, mstride = gridDim.x / tilesN, mt0 = cta / tilesN;
+  if (mt0 >= tilesM) return;
+  const int ntile = (tilesM - mt0 + mstride - 1) / mstride;
+  const int nk = K / 32;
+  const int total = ntile * nk;
+  const int n0 = nt * XR_BN;
+  const f16* zero = (const f16*)g_kair_zero_line;
+
+  // epilogue columns (fixed per CTA): after the permlane swap of fragment pair (2p, 2p + 1) a lane owns
+  // columns c8[p] .. + 8 of fragment 2p + (fq & 1); their bias, and (QKV) the column part of the offset
+  int c8[3];
+  long colo[3];
+  float bias8[3][8];
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    const int n = n0 + wn * 96 + (2 * p + (fq & 1)) * 16 + (fq >> 1) * 8;
+    c8[p] = n;
+    if constexpr (EM == XE_QKV) {
+      const int pw = E.nh * E.hdp;
+      const int part = fdiv(n, E.d_pw), rr = n - part * pw;
+      const int h = fdiv(rr, E.d_hdp), d = rr - h * E.hdp;
+      colo[p] = (long)part * E.M * pw + (long)h * E.tok * E.hdp + d;
+    } else {
+      colo[p] = 0;
+    }
+    const float4 b0 = *(const float4*)(E.bias ? E.bias + n : (const float*)g_kair_zero_line);
+    const float4 b1 = *(const float4*)(E.bias ? E.bias + n + 4 : (const float*)g_kair_zero_line);
+    bias8[p][0] = b0.x; bias8[p][1] = b0.y; bias8[p][2] = b0.z; bias8[p][3] = b0.w;
+    bias8[p][4] = b1.x; bias8[p][5] = b1.y; bias8[p][6] = b1.z; bias8[p][7] = b1.w;
+  }
+
+  // B loader: this lane's three weight rows (fixed for the CTA), unit already swizzled
+  const f16* bsrc[3];
+#pragma unroll
+  for (int ii = 0; ii < 3; ++ii) {
+    const int r = (wave * 3 + ii) * 8 + (lane >> 3), u = q8 ^ (r & 7);
+    bsrc[ii] = n0 + r < (int)B.M ? (const f16*)B.ptr + (long)(n0 + r) * B.ld + (u < 4 ? u * 8 : 64 + (u - 4) * 8) : nullptr;
+  }
+  // A loader: this lane's two rows of the tile being loaded
+  long aoff[2];
+  int ay[2], ax[2], au[2];
+  bool aok[2];
+  auto load_rows = [&](int i) {
+    const int mt = mt0 + i * mstride;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int r = (wave * 2 + ii) * 8 + (lane >> 3);
+      const int m = mt * XR_BM + r;
+      au[ii] = q8 ^ (r & 7);
+      aok[ii] = m < (int)A.M;
+      const int mm = aok[ii] ? m : 0;
+      if constexpr (AM == AM_ROWS) {
+        aoff[ii] = (long)win_to_token32(mm, A.win) * A.ld;
+      } else {
+        const int hw = A.d_hw.d;
+        const int b = fdiv(mm, A.d_hw), p = mm - b * hw;
+        ay[ii] = fdiv(p, A.d_imW);
+        ax[ii] = p - ay[ii] * A.imW;
+        aoff[ii] = (long)b * (hw >> (2 * A.up_sh));
+      }
+    }
+  };
+  int lj = 0, lt = 0, lkc = 0, ls = 0;   // next chunk to issue: tile lt, k-chunk lkc, stage ls
+  auto issue_next = [&]() {
+    if (lkc == 0) load_rows(lt);
+    const int k0 = lkc * 32;
+    char* st = smem + ls * XR_STAGE;
+    int dy = 0, dx = 0, c0 = k0;
+    if constexpr (AM == AM_IM2COL) {
+      const int tap = fdiv(k0, A.d_imC);
+      c0 = k0 - tap * A.imC;
+      dy = tap / 3 - 1;
+      dx = tap - (tap / 3) * 3 - 1;
+      if (A.flip) { dy = -dy; dx = -dx; }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const void* src = zero;
+      if constexpr (sizeof(TA) == 2) {
+        const f16* pl = (const f16*)(au[ii] < 4 ? A.ptr : A.lo_ptr);
+        if (aok[ii]) src = pl + aoff[ii] + k0 + (au[ii] & 3) * 8;
+      } else if constexpr (AM == AM_ROWS) {
+        if (aok[ii]) src = (const float*)A.ptr + aoff[ii] + k0 + au[ii] * 4;
+      } else {
+        const int y = ay[ii] + dy, x = ax[ii] + dx;
+        if (aok[ii] && y >= 0 && y < A.imH && x >= 0 && x < A.imW)
+          src = (const float*)A.ptr + (aoff[ii] + (long)(y >> A.up_sh) * (A.imW >> A.up_sh) + (x >> A.up_sh)) * A.ld + c0 +
+                au[ii] * 4;
+      }
+      if (!KAIR_DBG(E.dbg & 4)) glds16(src, st + (wave * 2 + ii) * 1024);
+    }
+    const int kb = (k0 >> 6) * 128 + (k0 & 63);
+#pragma unroll
+    for (int ii = 0; ii < 3; ++ii)
+      if (!KAIR_DBG(E.dbg & 4)) glds16(bsrc[ii] ? (const void*)(bsrc[ii] + kb) : (const void*)zero, st + XR_ABYTES + (wave * 3 + ii) * 1024);
+    ++lj;
+    if (++lkc == nk) { lkc = 0; ++lt; }
+    if (++ls == XR_NS) ls = 0;
+  };
+
+#pragma unroll
+  for (int j = 0; j < XR_NS - 1; ++j)
+    if (lj < total) issue_next();
+
+  f32x4 acc[2][6];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jn = 0; jn < 6; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float as = A.x3s;
+  int kc = 0, cs = 0, ct = 0;   // consumer: chunk j = ct * nk + kc in stage cs
+  for (int j = 0; j < total; ++j) {
+    const int ahead = (total - 1 - j) < (XR_NS - 2) ? (total - 1 - j) : (XR_NS - 2);
+    vm_wait(XR_DMA * ahead);
+    ring_barrier();   // chunk j is in LDS for every wave; stage (j-1) % NS is free
+    if (lj < total) issue_next();
+    const char* st = smem + cs * XR_STAGE;
+    if (!KAIR_DBG(E.dbg & 2)) {
+    f16x8 ah[2], al[2], bh[6], bl[6];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = wm * 32 + i * 16 + fr;
+      const char* row = st + r * 128;
+      if constexpr (sizeof(TA) == 2) {
+        ah[i] = *(const f16x8*)(row + ((fq ^ (r & 7)) << 4));
+        al[i] = *(const f16x8*)(row + (((4 + fq) ^ (r & 7)) << 4));
+      } else {
+        const float4 x0 = *(const float4*)(row + (((2 * fq) ^ (r & 7)) << 4));
+        const float4 x1 = *(const float4*)(row + (((2 * fq + 1) ^ (r & 7)) << 4));
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const float w = xv[c] * as;
+          ah[i][c] = (f16)w;
+          al[i][c] = (f16)(w - (float)ah[i][c]);
+        }
+      }
+    }
+#pragma unroll
+    for (int jn = 0; jn < 6; ++jn) {
+      const int n = wn * 96 + jn * 16 + fr;
+      const char* row = st + XR_ABYTES + n * 128;
+      bh[jn] = *(const f16x8*)(row + ((fq ^ (n & 7)) << 4));
+      bl[jn] = *(const f16x8*)(row + (((4 + fq) ^ (n & 7)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 6; ++jn) {
+        acc[i][jn] = mfma16(bh[jn], ah[i], acc[i][jn]);
+        acc[i][jn] = mfma16(bl[jn], ah[i], acc[i][jn]);
+        acc[i][jn] = mfma16(bh[jn], al[i], acc[i][jn]);
+      }
+    }
+    if (kc == nk - 1 && !KAIR_DBG(E.dbg & 1)) {
+      // Epilogue from registers.  Every operand load of the tile is issued before the first store (one
+      // memory round trip per tile); fragment pairs re-laid by v_permlane16_swap give this lane columns
+      // [c8[p], c8[p] + 8) of rows m0 + {0, 16}.
+      const int m0 = (mt0 + ct * mstride) * XR_BM + wm * 32 + fr;
+      int rowv[2];
+      bool okm[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int m = m0 + i * 16;
+        okm[i] = m < (int)E.M;
+        const int mm = okm[i] ? m : 0;
+        if constexpr (EM == XE_QKV) {
+          const int win = fdiv(mm, E.d_tok);
+          rowv[i] = win * E.nh * E.tok + (mm - win * E.tok);
+        } else {
+          rowv[i] = win_to_token32(mm, E.win);
+        }
+      }
+      float4 ex[2][3][2];
+      float rs[2] = {1.f, 1.f};
+      if constexpr (EX != EX_NONE) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const float* src = EX == EX_RESID ? E.resid + (long)rowv[i] * E.ldr : (const float*)E.gate + (long)rowv[i] * E.ldg;
+            ex[i][p][0] = *(const float4*)(src + c8[p]);
+            ex[i][p][1] = *(const float4*)(src + c8[p] + 4);
+          }
+        if constexpr (EX == EX_RESID) {
+          if (E.rowscale) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) rs[i] = E.rowscale[fdiv(rowv[i], E.d_rps)];
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          float v[8];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][c]),
+                                                            __float_as_uint(acc[i][2 * p + 1][c]), false, false);
+            v[c] = __uint_as_float(r[0]) * E.acc_scale + bias8[p][c];
+            v[4 + c] = __uint_as_float(r[1]) * E.acc_scale + bias8[p][4 + c];
+          }
+          const int n = c8[p];
+          if constexpr (EM == XE_QKV) {
+            if (okm[i]) store8_f16pair(E.out, E.out_lo, colo[p] + (long)rowv[i] * E.hdp, v, E.oscale);
+          } else {
+            float pre[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+              pre[c] = v[c];
+              if (E.act == KAIR_ACT_GELU) {
+                if (E.prek) pre[c] = gelu_erf_grad(v[c]);
+                v[c] = gelu_erf(v[c]);
+              } else if (E.act == KAIR_ACT_LEAKY) v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
+              else if (E.act == KAIR_ACT_RELU) v[c] = fmaxf(v[c], 0.f);
+            }
+            if constexpr (EX != EX_NONE) {
+              const float x8[8] = {ex[i][p][0].x, ex[i][p][0].y, ex[i][p][0].z, ex[i][p][0].w,
+                                   ex[i][p][1].x, ex[i][p][1].y, ex[i][p][1].z, ex[i][p][1].w};
+#pragma unroll
+              for (int c = 0; c < 8; ++c) {
+                if constexpr (EX == EX_RESID) v[c] = x8[c] + rs[i] * v[c];
+                else if (E.gkind == 4) v[c] *= x8[c];
+                else if (E.gkind == 1) v[c] *= gelu_erf_grad(x8[c]);
+                else if (E.gkind == 2) v[c] *= (x8[c] > 0.f ? 1.f : E.slope);
+                else v[c] *= (x8[c] > 0.f ? 1.f : 0.f);
+              }
+            }
+            if (E.ones_col >= n && E.ones_col < n + 8) {
+#pragma unroll
+              for (int c = 0; c < 8; ++c)
+                if (n + c == E.ones_col) v[c] = 1.f;
+            }
+            const long rr = rowv[i];
+            if (okm[i]) {
+              if constexpr (EM == XE_ROWS_PAIR) {
+                store8_f16pair(E.out, E.out_lo, rr * E.ldo + n, v, E.oscale);
+              } else {
+                float* d = (float*)E.out + rr * E.ldo + n;
+                *(float4*)d = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4*)(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+              }
+              if (E.pre) {
+                float* d = (float*)E.pre + rr * E.ldp + n;
+                *(float4*)d = make_float4(pre[0], pre[1], pre[2], pre[3]);
+                *(float4*)(d + 4) = make_float4(pre[4], pre[5], pre[6], pre[7]);
+              }
+            }
+          }
+        }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 6; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (++kc == nk) { kc = 0; ++ct; }
+    if (++cs == XR_NS) cs = 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// TN ring (x3): the weight gradients of the Swin linears and the 192-channel 3x3 convs from fp32 operands.
+//   P[s][n][k] = sum_{m in split s} A[m][n] B[m][k],  one 192 x 192 (n, k) tile per CTA, one CTA per CU.
+// A and B row chunks (32 rows x 192 fp32 columns, 24 KiB each) stream through an XR_TNS-deep LDS ring by
+// LDS-DMA; 16-byte unit u of chunk row r sits at slot u ^ (((r >> 3) & 3) << 2), so a fragment's column
+// read (8 rows per 16-lane group, the four groups 8 rows apart) touches 64 distinct banks.  Fragments are
+// eight ds_read_b32 down a column, split into the fp16 pair at the read (each operand's 2^e); D = B^T A,
+// so each lane stores 4 consecutive k (16 B).  8 waves as 2 (n) x 4 (k), wave tile 96 x 48.
+// BT_TAP: B is the 3x3 / pad-1 im2col of a 192-channel map and K-tile tk IS tap tk (row m reads pixel
+// m + dy W + dx; a zero line outside the image): the conv weight gradient reads each operand ~once.
+// Rows past the split read a zero line.  B's bias "ones" column must already be in the data.
+// ------------------------------------------------------------------------------------------
+constexpr int XT_RB = 32, XT_NS = 3;
+constexpr int XT_PART = XT_RB * 192 * 4, XT_STAGE = 2 * XT_PART;   // 24 + 24 KiB
+constexpr int XT_DMA = 6;   // DMA wave-instructions per wave per chunk (3 A + 3 B)
+enum { BT_ROWS = 0, BT_TAP = 1 };
+
+template <int BT>
+__global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
+                                                         int rps, float acc_scale) {
+  __shared__ __attribute__((aligned(16))) char smem[XT_NS * XT_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave >> 2, wk = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int n0 = (tile / tilesK) * 192, k0 = (tile % tilesK) * 192;
+  const int mbeg = split * rps;
+  const int mend = mbeg + rps < M ? mbeg + rps : M;
+  const int nch = mbeg < mend ? (mend - mbeg + XT_RB - 1) / XT_RB : 0;
+  const float* zero = (const float*)g_kair_zero_line;
+
+  // DMA geometry of this lane (the same for every chunk): wave-instruction g covers slots [64 g, 64 g + 64)
+  int dr[3], dcA[3], dcB[3];
+#pragma unroll
+  for (int ii = 0; ii < 3; ++ii) {
+    const int s = (wave * 3 + ii) * 64 + lane;
+    const int r = s / 48, q = s - r * 48;
+    const int u = q ^ (((r >> 3) & 3) << 2);
+    dr[ii] = r;
+    dcA[ii] = n0 + u * 4 < N ? n0 + u * 4 : -1;
+    dcB[ii] = k0 + u * 4 < K ? (BT == BT_TAP ? u * 4 : k0 + u * 4) : -1;
+  }
+  int dy = 0, dx = 0;
+  if constexpr (BT == BT_TAP) {
+    const int tap = k0 / 192;
+    dy = tap / 3 - 1;
+    dx = tap - (tap / 3) * 3 - 1;
+  }
+  int lc = 0, ls = 0;   // next chunk to issue, its stage
+  auto issue_next = [&]() {
+    char* st = smem + ls * XT_STAGE;
+    const int m0 = mbeg + lc * XT_RB;
+#pragma unroll
+    for (int ii = 0; ii < 3; ++ii) {
+      const int m = m0 + dr[ii];
+      const bool ok = m < mend;
+      const int mm = ok ? m : 0;
+      const void* sa = zero;
+      if (ok && dcA[ii] >= 0) sa = (const float*)A.ptr + (long)win_to_token32(mm, A.win) * A.ld + dcA[ii];
+      const void* sb = zero;
+      if constexpr (BT == BT_ROWS) {
+        if (ok && dcB[ii] >= 0) sb = (const float*)B.ptr + (long)win_to_token32(mm, B.win) * B.ld + dcB[ii];
+      } else {
+        const int hw = B.d_hw.d;
+        const int b = fdiv(mm, B.d_hw), p = mm - b * hw;
+        const int y = fdiv(p, B.d_imW), x = p - y * B.imW;
+        const int yy = y + dy, xx = x + dx;
+        if (ok && dcB[ii] >= 0 && yy >= 0 && yy < B.imH && xx >= 0 && xx < B.imW)
+          sb = (const float*)B.ptr + ((long)b * hw + (long)yy * B.imW + xx) * B.ld + dcB[ii];
+      }
+      glds16(sa, st + (wave * 3 + ii) * 1024);
+      glds16(sb, st + XT_PART + (wave * 3 + ii) * 1024);
+    }
+    ++lc;
+    if (++ls == XT_NS) ls = 0;
+  };
+
+#pragma unroll
+  for (int j = 0; j < XT_NS - 1; ++j)
+    if (lc < nch) issue_next();
+
+  f32x4 acc[3][6];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float sa = A.x3s, sb = B.x3s;
+  // a lane's column c of a chunk part: byte (fq * 8 + j) * 768 + slot(c) * 16 + (c & 3) * 4 for rows j = 0..7
+  auto frag = [&](const char* part, int c, float s, f16x8& hi, f16x8& lo) {
+    const char* p = part + fq * 8 * 768 + ((((c >> 2) ^ (fq << 2))) << 4) + (c & 3) * 4;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float w = *(const float*)(p + j * 768) * s;
+      hi[j] = (f16)w;
+      lo[j] = (f16)(w - (float)hi[j]);
+    }
+  };
+  int cs = 0;
+  for (int j = 0; j < nch; ++j) {
+    const int ahead = (nch - 1 - j) < (XT_NS - 2) ? (nch - 1 - j) : (XT_NS - 2);
+    vm_wait(XT_DMA * ahead);
+    ring_barrier();   // chunk j in LDS for every wave; stage (j - 1) % NS free
+    if (lc < nch) issue_next();
+    const char* st = smem + cs * XT_STAGE;
+    f16x8 ah[6], al[6], bh[3], bl[3];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) frag(st, wn * 96 + i * 16 + fr, sa, ah[i], al[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) frag(st + XT_PART, wk * 48 + i * 16 + fr, sb, bh[i], bl[i]);
+#pragma unroll
+    for (int ik = 0; ik < 3; ++ik)
+#pragma unroll
+      for (int in = 0; in < 6; ++in) {
+        acc[ik][in] = mfma16(bh[ik], ah[in], acc[ik][in]);
+        acc[ik][in] = mfma16(bl[ik], ah[in], acc[ik][in]);
+        acc[ik][in] = mfma16(bh[ik], al[in], acc[ik][in]);
+      }
+    if (++cs == XT_NS) cs = 0;
+  }
+  float* P = ws + (long)split * N * K;
+#pragma unroll
+  for (int ik = 0; ik < 3; ++ik)
+#pragma unroll
+    for (int in = 0; in < 6; ++in) {
+      const int k = k0 + wk * 48 + ik * 16 + fq * 4, n = n0 + wn * 96 + in * 16 + fr;
+      if (n < N && k < K)
+        *(float4*)(P + (long)n * K + k) = make_float4(acc[ik][in][0] * acc_scale, acc[ik][in][1] * acc_scale,
+                                                      acc[ik][in][2] * acc_scale, acc[ik][in][3] * acc_scale);
+    }
+}
+
 int g_x3_cus = 0;
 int x3_cus() {
   if (g_x3_cus == 0) {
@@ -395,6 +816,65 @@ int tn_x3_b(const Op& a, const Op& b, int bmode, int bdt, float* ws, int splits,
                          : launch_tn_x3<TA, float, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, acc_scale, s);
 }
 
+// the ring takes N-tiles of 192 columns, 32-deep k-chunks (im2col: one tap per chunk) and 16-byte aligned rows
+bool nt_x3_ring_ok(const kair_operand* A, const kair_operand* B, const kair_epilogue* E, int N, int K) {
+  static const int off = [] { const char* e = getenv("KAIR_X3_RING"); return e && e[0] == '0'; }();
+  if (off || N % XR_BN != 0 || K % 32 != 0 || (uintptr_t)B->ptr % 16 != 0 || (uintptr_t)A->ptr % 16 != 0) return false;
+  // epilogues: fp32 rows (bias, activation [+ pre], residual [x row scale] or fp32 gate, ones column) or fp16
+  // pair rows / head-blocked q, k, v (bias); 16-byte aligned rows throughout
+  const bool pair = E->out_dtype == KAIR_F16;
+  if (E->out_mode == KAIR_OUT_QKVBLK) {
+    if (!pair || E->qkv_hdp % 8 || (uintptr_t)E->out % 16 || E->act || E->out_pre || E->resid || E->gate || E->rowscale) return false;
+  } else {
+    if (E->out_mode != KAIR_OUT_ROWS || E->ldo % 4 || (uintptr_t)E->out % 16) return false;
+    if (E->resid2 || E->a_copy || (E->resid && E->gate)) return false;
+    if (pair && (E->act || E->out_pre || E->resid || E->gate || E->ldo % 8)) return false;
+    if (E->out_pre && (E->pre_dtype != KAIR_F32 || E->ldp % 4 || (uintptr_t)E->out_pre % 16)) return false;
+    if (E->resid && (E->ldr % 4 || (uintptr_t)E->resid % 16)) return false;
+    if (E->gate && (E->gate_dtype != KAIR_F32 || E->ldg % 4 || (uintptr_t)E->gate % 16)) return false;
+    if (E->rowscale && !E->resid) return false;
+  }
+  if (A->mode == KAIR_LD_ROWS) return A->dtype == KAIR_F16 ? A->ld % 8 == 0 : A->ld % 4 == 0;
+  return A->mode == KAIR_LD_IM2COL3 && A->dtype == KAIR_F32 && A->im_C % 32 == 0 && (A->ld == 0 ? A->im_C : A->ld) % 4 == 0;
+}
+
+template <typename TA, int AM>
+int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int K, hipStream_t s) {
+  const int tilesN = N / XR_BN;
+  const int tilesM = (int)((M + XR_BM - 1) / XR_BM);
+  int per = x3_cus() / tilesN;
+  if (per < 1) per = 1;
+  const int rounds = (tilesM + per - 1) / per;
+  per = (tilesM + rounds - 1) / rounds;   // the same makespan on as few CUs as it needs
+  const dim3 g(per * tilesN), bl(512);
+  if (e.omode == KAIR_OUT_QKVBLK)
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_QKV, EX_NONE>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+  else if (e.odt == KAIR_F16)
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_PAIR, EX_NONE>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+  else if (e.resid)
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_RESID>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+  else if (e.gate)
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_GATE_F32>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+  else
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_NONE>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+// the TN ring: fp32 rows (16-byte aligned, N and K % 4), B rows or the tap-per-tile im2col of a 192-channel
+// map (K = 9 x 192, no flip / upsample); a bias ones column only as data (ones_in_data)
+bool tn_x3_ring_ok(const kair_operand* A, const kair_operand* B, int N, int K) {
+  static const int off = [] { const char* e = getenv("KAIR_X3_RING"); return e && e[0] == '0'; }();
+  if (off || A->dtype != KAIR_F32 || B->dtype != KAIR_F32 || A->mode != KAIR_LD_ROWS || N % 4 || K % 4) return false;
+  if (A->ld % 4 || (uintptr_t)A->ptr % 16 || (uintptr_t)B->ptr % 16 || A->rowscale || B->rowscale) return false;
+  if (A->ones_col >= 0 && !A->ones_in_data) return false;
+  if (B->ones_col >= 0 && !B->ones_in_data) return false;
+  if (B->mode == KAIR_LD_ROWS) return B->ld % 4 == 0;
+  const long ld = B->ld == 0 ? B->im_C : B->ld;
+  return B->mode == KAIR_LD_IM2COL3 && B->im_C == 192 && K == 9 * 192 && !B->im_flip && B->im_up != 2 && ld % 4 == 0 &&
+         B->win_ws == 0;
+}
+
 // an x3 operand: fp32, or an fp16 hi plane with its 16-byte aligned lo plane
 int x3_operand_ok(const kair_operand* o, const char* what) {
   KAIR_CHECK_ARG(o->dtype == KAIR_F32 || (o->dtype == KAIR_F16 && o->lo_ptr && ((uintptr_t)o->lo_ptr % 16) == 0),
@@ -431,6 +911,11 @@ int kair_gemm_nt_x3(const kair_operand* A, const kair_operand* B, const kair_epi
   Epi e = make_epi(*E, M, N);
   e.acc_scale = ldexpf(1.f, -(A->x3_exp + B->x3_exp));
   hipStream_t s = (hipStream_t)stream;
+  if (nt_x3_ring_ok(A, B, E, N, K)) {
+    if (A->mode == KAIR_LD_IM2COL3) return launch_nt_x3_ring<float, AM_IM2COL>(a, b, e, M, N, K, s);
+    return A->dtype == KAIR_F16 ? launch_nt_x3_ring<f16, AM_ROWS>(a, b, e, M, N, K, s)
+                                : launch_nt_x3_ring<float, AM_ROWS>(a, b, e, M, N, K, s);
+  }
   if (A->dtype == KAIR_F16)
     return A->mode == KAIR_LD_ROWS ? nt_x3_tiles<f16, AM_ROWS>(a, b, e, M, N, K, s) : nt_x3_tiles<f16, AM_IM2COL>(a, b, e, M, N, K, s);
   return A->mode == KAIR_LD_ROWS ? nt_x3_tiles<float, AM_ROWS>(a, b, e, M, N, K, s) : nt_x3_tiles<float, AM_IM2COL>(a, b, e, M, N, K, s);
@@ -450,6 +935,16 @@ int kair_gemm_tn_x3(const kair_operand* A, const kair_operand* B, float* ws, int
   rps = (rps + 31) / 32 * 32;
   const float sc = ldexpf(1.f, -(A->x3_exp + B->x3_exp));
   hipStream_t s = (hipStream_t)stream;
+  if (tn_x3_ring_ok(A, B, N, K)) {
+    const int tilesN = (N + 191) / 192, tilesK = (K + 191) / 192, nt = tilesN * tilesK;
+    const dim3 g(nt * splits), bl(512);
+    if (B->mode == KAIR_LD_IM2COL3)
+      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_TAP>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
+    else
+      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
+    KAIR_CHECK_LAUNCH();
+    return 0;
+  }
   return A->dtype == KAIR_F16 ? tn_x3_b<f16>(a, b, B->mode, B->dtype, ws, splits, M, N, K, rps, sc, s)
                               : tn_x3_b<float>(a, b, B->mode, B->dtype, ws, splits, M, N, K, rps, sc, s);
 }

@@ -155,6 +155,93 @@ def test_gemm_nt_x3_rows_and_qkvblk():
         assert rel(blk / 4, refp) < 2e-6
 
 
+def _wsplit(w):
+    """kind-17 split pack of a [N][K] weight (fp16 pairs of w 2^KAIR_X3_WEXP) and its operand."""
+    N, K = w.shape
+    Wp = torch.empty(N, 2 * (-(-K // 64)) * 64, device=dev, dtype=torch.float16)
+    H.pack_weight(w.to(dev), Wp, H.wmap(17, N, K))
+    o = H.rows(Wp)
+    o.x3_exp = H.X3_WEXP
+    return o, Wp
+
+
+def test_gemm_nt_x3_ring_epilogues():
+    """The persistent LDS-DMA ring form of kair_gemm_nt x3 (N % 192 == 0, K % 32 == 0): ragged M with a GELU +
+    GELU' epilogue, window-ordered rows of an fp16 pair A with a DropPath-scaled residual, and a flipped 3x3
+    im2col of an fp32 map with a multiplicative gate -- each against float64."""
+    g = torch.Generator().manual_seed(11)
+    # (a) fp32 rows, M not a multiple of the 128-row tile, 7 k-chunks, two N-tiles
+    M, N, K = 1000, 384, 224
+    x, w, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05, torch.randn(N, generator=g) * 0.1
+    Wo, keep = _wsplit(w)
+    A = H.rows(x.to(dev))
+    A.x3_exp = 4
+    out, pre = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+    H.gemm_nt(A, Wo, H.epilogue(out, bias=b.to(dev), act=H.ACT_GELU, pre=pre, pre_grad=True), M, N, K, H.X3)
+    h = x.double() @ w.double().T + b.double()
+    cdf = 0.5 * (1 + torch.erf(h / 2 ** 0.5))
+    torch.cuda.synchronize()
+    assert rel(out, h * cdf) < 2e-6
+    assert rel(pre, cdf + h * torch.exp(-h * h / 2) / (2 * torch.pi) ** 0.5) < 2e-6
+    # (b) fp16 pair rows read and written through the Swin window map (shift 4), residual + per-image scale
+    Bn, Hh, Ww, N, K = 3, 16, 16, 192, 192
+    M = Bn * Hh * Ww
+    x, w = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05
+    r, s = torch.randn(M, N, generator=g), torch.tensor([0.5, 1.25, 2.0])
+    Wo, keep = _wsplit(w)
+    xp = hilo(x.to(dev), 4)
+    A = H.with_lo(H.rows(xp[0], win=(Hh, Ww, 8, 4)), xp[1])
+    A.x3_exp = 4
+    out = torch.empty(M, N, device=dev)
+    H.gemm_nt(A, Wo, H.epilogue(out, win=(Hh, Ww, 8, 4), resid=r.to(dev), rowscale=s.to(dev), rows_per_scale=Hh * Ww),
+              M, N, K, H.X3)
+    ref = r.double() + s.double().repeat_interleave(Hh * Ww)[:, None] * (x.double() @ w.double().T)
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 2e-6
+    # (c) flipped 3x3 im2col of a 64-channel fp32 map (the conv input gradient), gated
+    Bn, Hh, Ww, C, N = 2, 12, 20, 64, 192
+    M, K = Bn * Hh * Ww, 9 * C
+    x, w, gt = torch.randn(M, C, generator=g), torch.randn(N, K, generator=g) * 0.05, torch.randn(M, N, generator=g)
+    Wo, keep = _wsplit(w)
+    A = H.im2col(x.to(dev), Hh, Ww, C, flip=True)
+    A.x3_exp = 4
+    out = torch.empty(M, N, device=dev)
+    H.gemm_nt(A, Wo, H.epilogue(out, gate=gt.to(dev), gate_kind=4), M, N, K, H.X3)
+    cols = torch.nn.functional.unfold(x.view(Bn, Hh, Ww, C).permute(0, 3, 1, 2).double(), 3, padding=1)
+    cols = cols.view(Bn, C, 9, Hh * Ww).permute(0, 3, 2, 1).reshape(M, 9, C).flip(1).reshape(M, K)
+    torch.cuda.synchronize()
+    assert rel(out, (cols @ w.double().T) * gt.double()) < 2e-6
+
+
+@pytest.mark.parametrize("conv", [False, True])
+def test_gemm_tn_x3_ring(conv):
+    """The LDS-DMA ring form of kair_gemm_tn x3 (fp32 operands, 192 x 192 tiles): ragged splits over 3 N-tiles with
+    the bias ones column carried in B's data, and the tap-per-tile im2col of a 192-channel map (conv weight
+    gradient, K = 9 x 192) -- the split partial planes summed against float64."""
+    g = torch.Generator().manual_seed(13)
+    if conv:
+        Bn, Hh, Ww, C, N = 2, 12, 20, 192, 192
+        M, K = Bn * Hh * Ww, 9 * C
+        x = torch.randn(M, C, generator=g)
+        cols = torch.nn.functional.unfold(x.view(Bn, Hh, Ww, C).permute(0, 3, 1, 2).double(), 3, padding=1)
+        ref_b = cols.view(Bn, C, 9, Hh * Ww).permute(0, 3, 2, 1).reshape(M, K)
+        Bop = H.im2col(x.to(dev), Hh, Ww, C)
+    else:
+        M, N, K = 3000, 576, 192
+        x = torch.randn(M, K, generator=g)
+        x[:, K - 12] = 1.0
+        ref_b = x.double()
+        Bop = H.rows(x.to(dev), ones_col=K - 12, ones_in_data=True)
+    dy = torch.randn(M, N, generator=g) * 1e-6
+    A = H.rows(dy.to(dev))
+    A.x3_exp, Bop.x3_exp = 24, 4
+    S = H.wgrad_splits(M, N, K)
+    ws = torch.empty(S, N, K, device=dev)
+    H.gemm_tn(A, Bop, ws, S, M, N, K, H.X3)
+    torch.cuda.synchronize()
+    assert rel(ws.sum(0), dy.double().T @ ref_b) < 2e-6
+
+
 @pytest.mark.parametrize("shift", [0, 4])
 def test_window_attention_x3(shift):
     """kair_window_attn_fwd_x3 / _bwd_x3 against float64 autograd of WindowAttention (network_swinir.py:114-145)
