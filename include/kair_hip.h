@@ -322,7 +322,8 @@ int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo, const void
  * (exponent e_in), O / O_lo rows (written with e_out), lse fp32.  bwd: q/k/v and O carry e_act, dO carries
  * e_grad and dqkv / dqkv_lo are written with e_grad as token rows [nWin*64][3*nh*32] (window order,
  * column (part*nh + h)*32 + d); dtable (natural units) as kair_window_attn_bwd (NULL: partials left in ws
- * for kair_attn_dtable_grouped with dtype KAIR_COMPUTE_X3). */
+ * for kair_attn_dtable_grouped with dtype KAIR_COMPUTE_X3).  O_lo = NULL: O is fp32 rows in natural units
+ * (16-byte aligned, ldo % 4 == 0; the ones column reads 1.0); dqkv_lo = NULL: dqkv is fp32 in natural units. */
 int kair_window_attn_fwd_x3(const void* qkv, const void* qkv_lo, const float* table, void* O, void* O_lo, long ldo,
                             float* lse, long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
                             int e_in, int e_out, void* stream);

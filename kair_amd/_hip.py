@@ -552,19 +552,28 @@ def window_attn_bwd(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc,
                                         scale, H, W, shift, ptr(mask), mnw, stream_ptr()), "window_attn_bwd")
 
 
+def _planes(t):
+    """(hi, lo) pointers of an x3 tensor: an fp16 pair [2, ...] or an fp32 tensor in natural units (lo NULL)."""
+    return (ptr(t), None) if t.dtype == torch.float32 else (ptr(t[0]), ptr(t[1]))
+
+
 def window_attn_fwd_x3(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, ones_col=-1, e_in=0, e_out=0):
-    """Split-fp16 window attention forward: qkv / O are [2, ...] fp16 (hi plane, lo plane) of x 2^e."""
-    check(lib().kair_window_attn_fwd_x3(ptr(qkv[0]), ptr(qkv[1]), ptr(table), ptr(O[0]), ptr(O[1]), ldo, ptr(lse), nWin,
+    """Split-fp16 window attention forward: qkv is [2, ...] fp16 (hi plane, lo plane) of x 2^e_in; O the same
+    with e_out, or an fp32 tensor (natural units)."""
+    o, ol = _planes(O)
+    check(lib().kair_window_attn_fwd_x3(ptr(qkv[0]), ptr(qkv[1]), ptr(table), o, ol, ldo, ptr(lse), nWin,
                                         nh, hd, scale, H, W, shift, ones_col, e_in, e_out, stream_ptr()),
           "window_attn_fwd_x3")
 
 
 def window_attn_bwd_x3(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc, ws, nWin, nh, hd, scale, H, W, shift,
                        e_act=0, e_grad=0):
-    """Split-fp16 window attention backward: qkv, O, dO and dqkv (token rows [M][3 nh 32]) are [2, ...] fp16 planes;
-    q/k/v and O carry e_act, dO and dqkv e_grad."""
-    check(lib().kair_window_attn_bwd_x3(ptr(qkv[0]), ptr(qkv[1]), ptr(O[0]), ptr(O[1]), ldo, ptr(dO[0]), ptr(dO[1]), lddo,
-                                        ptr(table), ptr(lse), ptr(dqkv[0]), ptr(dqkv[1]), ptr(dtable), int(dtable_acc),
+    """Split-fp16 window attention backward: qkv, dO are [2, ...] fp16 planes; O and dqkv (token rows [M][3 nh 32])
+    fp16 pairs or fp32 (natural units); q/k/v and O pairs carry e_act, dO and a dqkv pair e_grad."""
+    o, ol = _planes(O)
+    dq, dql = _planes(dqkv)
+    check(lib().kair_window_attn_bwd_x3(ptr(qkv[0]), ptr(qkv[1]), o, ol, ldo, ptr(dO[0]), ptr(dO[1]), lddo,
+                                        ptr(table), ptr(lse), dq, dql, ptr(dtable), int(dtable_acc),
                                         ptr(ws), nWin, nh, hd, scale, H, W, shift, e_act, e_grad, stream_ptr()),
           "window_attn_bwd_x3")
 

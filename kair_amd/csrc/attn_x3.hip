@@ -15,7 +15,8 @@
 // token rows (window order, head h at columns h*32..), lse [nWin][nh][64]; each fp16 tensor has its lo
 // plane in a second buffer of the same layout.  The backward writes dq/dk/dv as token rows
 // [nWin*64][3*nh*32] (column (part*nh + h)*32 + d), hi and lo planes: the A operand of the q/k/v
-// input- and weight-gradient GEMMs.
+// input- and weight-gradient GEMMs.  O and dq/dk/dv may instead be fp32 in natural units (a null lo
+// plane): the form the fp32-operand ring GEMMs of gemm_x3.hip stream by LDS-DMA.
 #include <string.h>
 
 #include "attn_common.h"
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(64 * FWD_NW) void attn_fwd_x3_kernel(const f16* __r
   }
   // O^T = V^T P^T : tile [qt] rows = d, lane = query (P with exponent P_EXP)
   const float so = ldexpf(1.f, e_out - e_in - P_EXP), sone = ldexpf(1.f, e_out), sp = ldexpf(1.f, P_EXP);
+  const float so_nat = ldexpf(1.f, -e_in - P_EXP);
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     f32x16 o;
@@ -171,12 +173,18 @@ __global__ __launch_bounds__(64 * FWD_NW) void attn_fwd_x3_kernel(const f16* __r
     for (int g = 0; g < 4; ++g) {
       const int d0 = 8 * g + 4 * hh;
       float v[4];
+      if (Ol) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (h * HDP + d0 + j == ones_col) ? sone : o[4 * g + j] * so;
-      f16x4 qh, ql;
-      pair4(v, 1.f, qh, ql);
-      *(f16x4*)(O + orow + d0) = qh;
-      *(f16x4*)(Ol + orow + d0) = ql;
+        for (int j = 0; j < 4; ++j) v[j] = (h * HDP + d0 + j == ones_col) ? sone : o[4 * g + j] * so;
+        f16x4 qh, ql;
+        pair4(v, 1.f, qh, ql);
+        *(f16x4*)(O + orow + d0) = qh;
+        *(f16x4*)(Ol + orow + d0) = ql;
+      } else {   // fp32 O in natural units
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (h * HDP + d0 + j == ones_col) ? 1.f : o[4 * g + j] * so_nat;
+        *(float4*)((float*)O + orow + d0) = make_float4(v[0], v[1], v[2], v[3]);
+      }
     }
   }
 }
@@ -280,22 +288,39 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
       ldfrag(dOl + win * TOK * lddo + h * HDP, lddo, Fgl);
       ldfrag(qkv + 2 * part + blk, HDP, Fvh);
       ldfrag(qkvl + 2 * part + blk, HDP, Fvl);
-      ldfrag(O + win * TOK * ldo + h * HDP, ldo, Foh);
-      ldfrag(Ol + win * TOK * ldo + h * HDP, ldo, Fol);
       stfrag(sQG[0] + TOK * LD, Fgh);
       stfrag(sQG[1] + TOK * LD, Fgl);
+      float dsum[2] = {0.f, 0.f};
+      if (Ol) {
+        ldfrag(O + win * TOK * ldo + h * HDP, ldo, Foh);
+        ldfrag(Ol + win * TOK * ldo + h * HDP, ldo, Fol);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              dsum[t] += ((float)Fgh[t][s][j] + (float)Fgl[t][s][j]) * ((float)Foh[t][s][j] + (float)Fol[t][s][j]) * s_o;
+      } else {   // fp32 O (natural units)
+        const float* Of = (const float*)O + win * TOK * ldo + h * HDP;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const float* op = Of + (long)(t * 32 + l31) * ldo + 16 * s + 8 * hh;
+            const float4 a = *(const float4*)op, b = *(const float4*)(op + 4);
+            const float ov[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dsum[t] += ((float)Fgh[t][s][j] + (float)Fgl[t][s][j]) * ov[j];
+          }
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        float d = 0.f;
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            d += ((float)Fgh[t][s][j] + (float)Fgl[t][s][j]) * ((float)Foh[t][s][j] + (float)Fol[t][s][j]);
+        float d = dsum[t];
         d += __shfl_xor(d, 32, 64);
         if (hh == 0) {
           sRow[0][t * 32 + l31] = lse[(win * nh + h) * TOK + t * 32 + l31];
-          sRow[1][t * 32 + l31] = d * (s_g * s_o);
+          sRow[1][t * 32 + l31] = d * s_g;
         }
       }
 #pragma unroll
@@ -361,7 +386,8 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
     // dV^T = dO^T P and dK^T = scale * Q^T dS : tiles [kt], rows = d, lane = key; token-row outputs carrying
     // e_grad (dS enters as the pair of dS 2^e_grad)
     f16* dq_out = dqkv + win * TOK * tstr + h * HDP;
-    f16* dql_out = dqkvl + win * TOK * tstr + h * HDP;
+    f16* dql_out = dqkvl ? dqkvl + win * TOK * tstr + h * HDP : nullptr;
+    float* dqf = (float*)dqkv + win * TOK * tstr + h * HDP;
     const long koff = (long)nh * HDP, voff = 2L * nh * HDP;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -394,14 +420,19 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
           va[j] = av[4 * g + j] * s_dv;
           ka[j] = ak[4 * g + j] * (scale * s_dk);
         }
-        f16x4 vh, vl, kh, kl;
-        pair4(va, 1.f, vh, vl);
-        pair4(ka, 1.f, kh, kl);
         const long o = key * tstr + 8 * g + 4 * hh;
-        *(f16x4*)(dq_out + voff + o) = vh;
-        *(f16x4*)(dql_out + voff + o) = vl;
-        *(f16x4*)(dq_out + koff + o) = kh;
-        *(f16x4*)(dql_out + koff + o) = kl;
+        if (dqkvl) {
+          f16x4 vh, vl, kh, kl;
+          pair4(va, 1.f, vh, vl);
+          pair4(ka, 1.f, kh, kl);
+          *(f16x4*)(dq_out + voff + o) = vh;
+          *(f16x4*)(dql_out + voff + o) = vl;
+          *(f16x4*)(dq_out + koff + o) = kh;
+          *(f16x4*)(dql_out + koff + o) = kl;
+        } else {   // fp32 dq/dk/dv in natural units
+          *(float4*)(dqf + voff + o) = make_float4(va[0] * s_g, va[1] * s_g, va[2] * s_g, va[3] * s_g);
+          *(float4*)(dqf + koff + o) = make_float4(ka[0] * s_g, ka[1] * s_g, ka[2] * s_g, ka[3] * s_g);
+        }
       }
     }
     // dQ^T = scale * K^T dS^T : the dS pair through LDS ([q][key] row-major), over the q / dO tiles
@@ -438,10 +469,14 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
         float qa[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) qa[j] = aq[4 * g + j] * (scale * s_dk);
-        f16x4 qh, ql;
-        pair4(qa, 1.f, qh, ql);
-        *(f16x4*)(dq_out + qi * tstr + 8 * g + 4 * hh) = qh;
-        *(f16x4*)(dql_out + qi * tstr + 8 * g + 4 * hh) = ql;
+        if (dqkvl) {
+          f16x4 qh, ql;
+          pair4(qa, 1.f, qh, ql);
+          *(f16x4*)(dq_out + qi * tstr + 8 * g + 4 * hh) = qh;
+          *(f16x4*)(dql_out + qi * tstr + 8 * g + 4 * hh) = ql;
+        } else {
+          *(float4*)(dqf + qi * tstr + 8 * g + 4 * hh) = make_float4(qa[0] * s_g, qa[1] * s_g, qa[2] * s_g, qa[3] * s_g);
+        }
       }
     }
   }
@@ -475,14 +510,14 @@ long kair_attn_x3_wpg(long nWin, int nh) {
 extern "C" int kair_window_attn_fwd_x3(const void* qkv, const void* qkv_lo, const float* table, void* O, void* O_lo, long ldo,
                                        float* lse, long nWin, int nh, int hd, float scale, int H, int W, int shift,
                                        int ones_col, int e_in, int e_out, void* stream) {
-  KAIR_CHECK_ARG(qkv && qkv_lo && table && O && O_lo && lse, "window_attn_fwd_x3: null pointer");
+  KAIR_CHECK_ARG(qkv && qkv_lo && table && O && lse, "window_attn_fwd_x3: null pointer");
   KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_fwd_x3: head_dim %d must be <= 32", hd);
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)),
                  "window_attn_fwd_x3: grid %dx%d / shift %d", H, W, shift);
   KAIR_CHECK_ARG(ldo >= nh * HDP && ldo % 8 == 0, "window_attn_fwd_x3: ldo");
   KAIR_CHECK_ARG(ones_col < 0 || (ones_col < nh * HDP && ones_col % HDP >= hd), "window_attn_fwd_x3: ones column must be a pad column");
-  KAIR_CHECK_ARG(((uintptr_t)qkv % 16) == 0 && ((uintptr_t)qkv_lo % 16) == 0 && ((uintptr_t)O % 8) == 0 &&
-                     ((uintptr_t)O_lo % 8) == 0,
+  KAIR_CHECK_ARG(((uintptr_t)qkv % 16) == 0 && ((uintptr_t)qkv_lo % 16) == 0 && ((uintptr_t)O % (O_lo ? 8 : 16)) == 0 &&
+                     ((uintptr_t)O_lo % 8) == 0 && (O_lo || ldo % 4 == 0),
                  "window_attn_fwd_x3: alignment");
   const long tasks = nWin * nh;
   const long nb = (tasks + FWD_NW - 1) / FWD_NW;
@@ -499,8 +534,8 @@ extern "C" int kair_window_attn_bwd_x3(const void* qkv, const void* qkv_lo, cons
                                        void* dqkv, void* dqkv_lo, float* dtable, int dtable_accumulate, float* ws, long nWin,
                                        int nh, int hd, float scale, int H, int W, int shift, int e_act, int e_grad,
                                        void* stream) {
-  KAIR_CHECK_ARG(qkv && qkv_lo && O && O_lo && dO && dO_lo && table && lse && dqkv && dqkv_lo && ws,
-                 "window_attn_bwd_x3: null pointer");
+  KAIR_CHECK_ARG(qkv && qkv_lo && O && dO && dO_lo && table && lse && dqkv && ws, "window_attn_bwd_x3: null pointer");
+  KAIR_CHECK_ARG((O_lo || (uintptr_t)O % 16 == 0) && (dqkv_lo || (uintptr_t)dqkv % 16 == 0), "window_attn_bwd_x3: alignment");
   KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_bwd_x3: head_dim");
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)), "window_attn_bwd_x3: geometry");
   KAIR_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0, "window_attn_bwd_x3: strides");

@@ -499,9 +499,9 @@ class SwinIREngine:
                 continue
             blocks.append({
                 "mid": e(M, Cp), "out": e(M, Cp), "ln1": e(M, Cp, dt=T), "m1": e(M), "r1": e(M),
-                # fp32x3: q/k/v and O as hi/lo bf16 planes [2, ...] (the split attention kernels' operands)
+                # fp32x3: q/k/v as hi/lo fp16 planes [2, ...] (the split attention kernels' operands), O fp32
                 "qkv": e(2, 3 * M * nh * 32, dt=hf) if self.x3 else e(3 * M * nh * 32, dt=T),
-                "O": e(2, M, nh * 32, dt=hf) if self.x3 else e(M, nh * 32, dt=T), "lse": e(nWin * nh * WS_TOK),
+                "O": e(M, nh * 32, dt=T), "lse": e(nWin * nh * WS_TOK),
                 "ln2": e(M, Cp, dt=T), "m2": e(M), "r2": e(M), "u": e(M, Hdp, dt=T), "h": e(M, Hdp, dt=T)})
         P["blocks"] = blocks
         P["rstb_out"] = [e(M, Cp) for _ in range(min(2, len(self.rstb)) if infer else len(self.rstb))]
@@ -551,8 +551,8 @@ class SwinIREngine:
         z = lambda *s: torch.zeros(*s, device=dev, dtype=T)
         # Two sets (RSTB parity): the side stream still reads one RSTB's while the next RSTB writes the other.
         P["gw"] = [[{"Dm": z(M, Cp), "Da": z(M, Cp), "dU": e(M, Hdp, dt=T),
-                     # fp32x3: dq/dk/dv as token rows [M][3 nh 32], hi/lo fp16 planes
-                     "dqkv": e(2, M, 3 * nh * 32, dt=hf) if self.x3 else e(3 * M * nh * 32, dt=T),
+                     # fp32x3: dq/dk/dv as fp32 token rows [M][3 nh 32] (the ring GEMMs' operand)
+                     "dqkv": e(M, 3 * nh * 32, dt=T) if self.x3 else e(3 * M * nh * 32, dt=T),
                      # LN1 / LN2 parameter partials and the attention bias-table partials of the block, reduced
                      # by one grouped launch each at the end of the RSTB
                      "ln1p": e(2 * 2048 * Cp), "ln2p": e(2 * 2048 * Cp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
@@ -862,13 +862,13 @@ class SwinIREngine:
             H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps, win,
                             one_col=self.C)
             l = blk.qkv
-            if self.x3:   # q/k/v and O as hi/lo planes, the split attention kernels in between
+            if self.x3:   # q/k/v as hi/lo planes into the split attention kernels, O out as fp32
                 self._nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"][0], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
                                                                      qkv=(nh, 32, WS_TOK), out_lo=S["qkv"][1]),
                          M, l.Np, Cp, cd)
                 H.window_attn_fwd_x3(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale,
                                      Hh, Ww, blk.shift, ones_col=self.C // nh, e_in=self.X3_AEXP, e_out=self.X3_AEXP)
-                A_o = H.with_lo(H.rows(S["O"][0]), S["O"][1])
+                A_o = H.rows(S["O"])
             else:
                 self._nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
                                                                      qkv=(nh, 32, WS_TOK)), M, l.Np, Cp, cd)
@@ -1252,8 +1252,8 @@ class SwinIREngine:
 
 
     def _block_bwd_attn_x3(self, blk, P, S, x_in, D, bi, grads, j, par):
-        """The attention half of _block_bwd under fp32x3: O, dO, q/k/v and dq/dk/dv as hi/lo bf16 planes, the
-        split attention backward, split GEMMs (kair_gemm_nt a_split / w_split, kair_gemm_tn x3)."""
+        """The attention half of _block_bwd under fp32x3: q/k/v and dO as hi/lo fp16 planes, O and dq/dk/dv fp32, the
+        split attention backward, split GEMMs (kair_gemm_nt / kair_gemm_tn compute X3)."""
         cd, g = self.cd, (lambda p: grads[p])
         M, Cp, nh, Hh, Ww = P["M"], self.Cp, self.nh, P["H"], P["W"]
         HW = Hh * Ww
@@ -1263,22 +1263,19 @@ class SwinIREngine:
         W = P["gw"][par][j]
         Da, dqkv = W["Da"], W["dqkv"]
         proj, qkv = blk.proj, blk.qkv
-        self._wg(P, H.rows(Da), H.with_lo(H.rows(S["O"][0], ones_col=hd, ones_in_data=True), S["O"][1]), Cp, nh * 32,
-                 proj, grads, hd)
+        self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
         self._nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"][0], out_lo=P["dO"][1]), M, nh * 32, Cp, cd)
         H.window_attn_bwd_x3(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
                              W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, e_act=self.X3_AEXP,
                              e_grad=P["e_g"])
         self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, H.X3, g(blk.table), False))
-        rows_hi, rows_lo = dqkv[0], dqkv[1]
-        self._wg(P, H.with_lo(H.rows(rows_hi), rows_lo), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp,
-                 qkv, grads, self.C)
+        self._wg(P, H.rows(dqkv), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads, self.C)
         n = blk.n1
         cp = None
         if j > 0:   # the previous block's MLP operand: s_mlp(prev) * dL/d x_in
             cp = H.copy_desc(P["gw"][par][j - 1]["Dm"], rowscale=drop[bi - 1, 1] if drop is not None else None,
                              rows_per_scale=HW)
-        self._nt(H.with_lo(H.rows(rows_hi), rows_lo), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
+        self._nt(H.rows(dqkv), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
         H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
                         W["ln1p"], M, self.C, win, copy=cp)
         self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False))

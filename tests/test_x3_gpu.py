@@ -242,10 +242,12 @@ def test_gemm_tn_x3_ring(conv):
     assert rel(ws.sum(0), dy.double().T @ ref_b) < 2e-6
 
 
+@pytest.mark.parametrize("f32_out", [False, True])
 @pytest.mark.parametrize("shift", [0, 4])
-def test_window_attention_x3(shift):
+def test_window_attention_x3(shift, f32_out):
     """kair_window_attn_fwd_x3 / _bwd_x3 against float64 autograd of WindowAttention (network_swinir.py:114-145)
-    at the fp32 kernels' tolerances (fwd 2e-5, bwd 5e-5); dq/dk/dv as token rows."""
+    at the fp32 kernels' tolerances (fwd 2e-5, bwd 5e-5); dq/dk/dv as token rows; O and dq/dk/dv as fp16 pairs or
+    (f32_out, the engine's form) fp32 in natural units."""
     B, Hh, Ww, nh, hd = 2, 16, 24, 6, 30
     nWin = B * (Hh // 8) * (Ww // 8)
     scale = hd ** -0.5
@@ -260,24 +262,36 @@ def test_window_attention_x3(shift):
     qkv[0, ..., :hd], qkv[1, ..., :hd], qkv[2, ..., :hd] = q, k, v
     e_act, e_grad = 4, 26    # exponents of the stored pairs: q/k/v / O and the gradients (dO ~ 1e-7 below)
     qkv_p = hilo(qkv.view(-1).to(dev), e_act)
-    O = torch.empty(2, nWin * 64, nh * 32, device=dev, dtype=torch.float16)
+    if f32_out:
+        O = torch.full((nWin * 64, nh * 32), float("nan"), device=dev)
+    else:
+        O = torch.empty(2, nWin * 64, nh * 32, device=dev, dtype=torch.float16)
     lse = torch.empty(nWin, nh, 64, device=dev)
     H.window_attn_fwd_x3(qkv_p, table.to(dev), O, nh * 32, lse, nWin, nh, hd, scale, Hh, Ww, shift, e_in=e_act, e_out=e_act)
     torch.cuda.synchronize()
-    Of = (O[0].double() + O[1].double()).cpu().view(nWin, 64, nh, 32) * 2.0 ** -e_act
+    if f32_out:
+        Of = O.double().cpu().view(nWin, 64, nh, 32)
+    else:
+        Of = (O[0].double() + O[1].double()).cpu().view(nWin, 64, nh, 32) * 2.0 ** -e_act
     assert rel(Of[..., :hd].permute(0, 2, 1, 3), o.detach()) < 2e-6
     assert Of[..., hd:].abs().max() == 0
     dO = torch.zeros(nWin, 64, nh, 32)
     dO[..., :hd] = go.float().permute(0, 2, 1, 3) * 1e-7
     dO_p = hilo(dO.view(nWin * 64, nh * 32).to(dev), e_grad)
-    dqkv = torch.empty(2, nWin * 64, 3 * nh * 32, device=dev, dtype=torch.float16)
+    if f32_out:
+        dqkv = torch.full((nWin * 64, 3 * nh * 32), float("nan"), device=dev)
+    else:
+        dqkv = torch.empty(2, nWin * 64, 3 * nh * 32, device=dev, dtype=torch.float16)
     dtab = torch.empty(225, nh, device=dev)
     ws = torch.empty(H.window_attn_bwd_ws(nWin, nh), device=dev)
     H.window_attn_bwd_x3(qkv_p, O, nh * 32, dO_p, nh * 32, table.to(dev), lse, dqkv, dtab, False, ws, nWin, nh, hd, scale,
                          Hh, Ww, shift, e_act=e_act, e_grad=e_grad)
     torch.cuda.synchronize()
-    d = (dqkv[0].double() + dqkv[1].double()).cpu().view(nWin, 64, 3, nh, 32)[..., :hd].permute(2, 0, 3, 1, 4)
-    d = d * 2.0 ** -e_grad * 1e7
+    if f32_out:
+        d = dqkv.double().cpu().view(nWin, 64, 3, nh, 32)[..., :hd].permute(2, 0, 3, 1, 4) * 1e7
+    else:
+        d = (dqkv[0].double() + dqkv[1].double()).cpu().view(nWin, 64, 3, nh, 32)[..., :hd].permute(2, 0, 3, 1, 4)
+        d = d * 2.0 ** -e_grad * 1e7
     assert rel(d[0], qr.grad) < 5e-6
     assert rel(d[1], kr.grad) < 5e-6
     assert rel(d[2], vr.grad) < 5e-6
