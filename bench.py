@@ -30,7 +30,16 @@ PRECISION_BF16 = ("training step: bf16 MFMA with fp32 accumulation; every forwar
                   "stream, LayerNorm statistics, softmax and Adam + EMA.  Evaluation (the psnr fields, eval-mode "
                   "forwards): the same kernels with the Swin-block linear weights as hi/lo pairs too "
                   "(SwinIR.eval_engine).  Holds the PSNR bar: "
-                  "tests/test_swinir_gpu.py::test_swinir_classical_full_bf16_psnr_along_training, 160 steps")
+                  "tests/test_swinir_gpu.py::test_swinir_classical_full_psnr_along_training[bf16], 160 steps")
+PRECISION_X3 = ("training step at the fp32 reference's precision class: every operand x of every GEMM, conv and window-"
+                "attention product is carried as an fp16 pair of x 2^e (hi = f16(x 2^e), lo = f16(x 2^e - hi), e a power "
+                "of two per tensor class) and every product as hi.hi + hi.lo + lo.hi on v_mfma_f32_{16x16x32,32x32x16}_f16 "
+                "with fp32 accumulation (~2^-21 per product); fp32 master weights, residual stream, LayerNorm statistics, "
+                "softmax, GELU (erf), Adam + EMA.  Passes the exact-fp32 engine's oracle bars unchanged: tests/test_x3_gpu.py "
+                "(classical x4 full network vs the CPU oracle: outputs < 1e-4, gradients < 1e-3, PSNR < 1e-3 dB; the "
+                "3-step ModelPlain trajectory < 1e-4)")
+PRECISION_F32 = "fp32 operands, exact fp32 MFMA (v_mfma_f32_16x16x4_f32)"
+PRECISION = {"bf16": PRECISION_BF16, "fp32x3": PRECISION_X3, "fp32": PRECISION_F32}
 
 
 def build_net(dtype, drop_path=0.1, seed=0):
@@ -85,6 +94,24 @@ def _alg_bytes(fn, a):
     if fn == "rowgemm_lnbwd":         # A in, x in, D in + out, bf16 copy out, mean / rstd
         M, K, C = a[1], a[2], a[8]
         return M * (_REAL[K] * 2 + C * 4 + 2 * C * 4 + C * 2 + 8)
+    if fn == "gemm_nt" and a[6] == X3:   # x3: fp32 / fp16-pair operands 4 B per element; A (an im2col: its map)
+        A, E, M, N, K = a[0], a[2], a[3], a[4], a[5]   # once, the split weight once, out (+ pre, resid / gate)
+        ka = A.im_C if A.mode == 1 else K
+        nn = _REAL.get(N, N)
+        per_row = _REAL.get(ka, ka) + nn * (1 + bool(E.out_pre) + bool(E.resid) + bool(E.gate))
+        return 4 * (M * per_row + nn * _REAL.get(K, K))
+    if fn == "gemm_tn" and a[7] == X3:   # x3 weight gradient: both operands once, the split partial planes out
+        B, S, M, N, K = a[1], a[3], a[4], a[5], a[6]
+        kb = B.im_C if B.mode == 1 else K
+        return 4 * (M * (_REAL.get(N, N) + _REAL.get(kb, kb)) + S * N * K)
+    if fn == "window_attn_fwd_x3":    # q, k, v in (fp16 pairs), O out, lse
+        nWin, nh, hd = a[5], a[6], a[7]
+        M = nWin * T
+        return M * nh * (4 * hd * 4 + 4)
+    if fn == "window_attn_bwd_x3":    # q, k, v, O, dO, lse in; dq, dk, dv out
+        nWin, nh, hd = a[11], a[12], a[13]
+        M = nWin * T
+        return M * nh * (8 * hd * 4 + 4)
     return None
 
 
@@ -99,6 +126,18 @@ def _alg_flops(fn, a):
     if fn == "window_attn_bwd":        # S, dP, dV, dK, dQ: five 64 x 64 x hd products per (window, head)
         nWin, nh, hd = a[11], a[12], a[13]
         return nWin * nh * 5 * 2 * T * T * hd
+    if fn == "gemm_nt" and a[6] == X3:
+        M, N, K = a[3], a[4], a[5]
+        return 2 * M * _REAL.get(N, N) * _REAL.get(K, K) if a[0].mode != 1 else 2 * M * N * K
+    if fn == "gemm_tn" and a[7] == X3:
+        M, N, K = a[4], a[5], a[6]
+        return 2 * M * _REAL.get(N, N) * _REAL.get(K, K) if a[1].mode != 1 else 2 * M * N * K
+    if fn == "window_attn_fwd_x3":
+        nWin, nh, hd = a[5], a[6], a[7]
+        return nWin * nh * 2 * 2 * T * T * hd
+    if fn == "window_attn_bwd_x3":
+        nWin, nh, hd = a[11], a[12], a[13]
+        return nWin * nh * 5 * 2 * T * T * hd
     if fn in ("rowgemm_gate", "rowgemm_store", "rowgemm_lnbwd"):
         M, K = a[1], a[2]
         N = a[4] if fn != "rowgemm_lnbwd" else 192
@@ -106,7 +145,9 @@ def _alg_flops(fn, a):
     return None
 
 
+X3 = 2   # kair_amd._hip.X3 (compute argument of the x3 GEMM launches)
 _TIMED = ("gemm_nt", "gemm_tn", "wgrad_finalize", "colsum", "layernorm_fwd", "layernorm_bwd", "row_copy", "window_attn_fwd",
+          "window_attn_fwd_x3", "window_attn_bwd_x3",
           "window_attn_bwd", "ln_param_reduce_grouped", "attn_dtable_grouped", "image_to_nhwc", "l1_loss", "axpy",
           "swin_attn_fwd", "swin_mlp_fwd", "rowgemm_store", "rowgemm_gate", "rowgemm_lnbwd", "image_to_nhwc_hilo",
           "conv3x3_narrow_fwd", "conv3x3_narrow_dgrad", "conv3x3_narrow_wgrad", "conv3x3_wr")
@@ -120,9 +161,14 @@ def time_roles(tr, serial=False):
     from kair_amd import _hip as H
     rec = []
 
+    # the engine's thin launch helpers: a role is named by their caller (the layer's call site), not by them
+    helpers = ("_nt", "_wgrad", "_wg", "_run_conv_job", "_bias_colsum")
+
     def wrap(name, f):
         def g(*a, **k):
             fr = sys._getframe(1)
+            while fr.f_back is not None and fr.f_code.co_name in helpers:
+                fr = fr.f_back
             role = f"{name} @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -161,12 +207,18 @@ def time_roles(tr, serial=False):
             eng.side_stream = side0
     out = {}
     for role, name, a, e0, e1 in rec:
-        d = out.setdefault(role, {"kernel": name, "launches": 0, "ms_total": 0.0, "bytes": _alg_bytes(name, a),
-                                  "flops": _alg_flops(name, a), "rocprof": rocprof_name(name, a)})
+        d = out.setdefault(role, {"kernel": name, "launches": 0, "ms_total": 0.0, "bytes_total": 0, "flops_total": 0,
+                                  "rocprof": rocprof_name(name, a)})
         d["launches"] += 1
         d["ms_total"] += e0.elapsed_time(e1)
+        b, f = _alg_bytes(name, a), _alg_flops(name, a)
+        d["bytes_total"] = None if (b is None or d["bytes_total"] is None) else d["bytes_total"] + b
+        d["flops_total"] = None if (f is None or d["flops_total"] is None) else d["flops_total"] + f
     for d in out.values():
-        d["ms"] = d["ms_total"] / d["launches"]
+        n = d["launches"]
+        d["ms"] = d["ms_total"] / n
+        d["bytes"] = d["bytes_total"] / n if d["bytes_total"] else None   # mean per launch
+        d["flops"] = d["flops_total"] / n if d["flops_total"] else None
     return out
 
 
@@ -179,8 +231,22 @@ def rocprof_name(fn, a):
         ks = 2 if N == 384 else 4   # csrc/rowgemm.hip rg_dispatch: <KB, KS, NWC, EPI, HOLD>
         hold = {12: kb // ks, 24: 6, 36: {0: 9, 1: 7, 2: 5}[epi]}[kb]
         return f"rowgemm_kernel<{kb}, {ks}, {N // 96}, {epi}, {hold}>"
+    if fn == "gemm_nt" and a[6] == X3:
+        return "gemm_nt_x3_ring" if _x3_ring_nt(a) else "gemm_nt_x3_kernel"
+    if fn == "gemm_tn" and a[7] == X3:
+        return "gemm_tn_x3_ring" if a[0].dtype == 0 and a[1].dtype == 0 and a[5] % 4 == 0 else "gemm_tn_x3_kernel"
+    if fn == "window_attn_fwd_x3":
+        return "attn_fwd_x3_kernel"
+    if fn == "window_attn_bwd_x3":
+        return "attn_bwd_x3_kernel"
     return {"conv3x3_wr": "conv3x3_wr_kernel", "swin_mlp_fwd": "swin_mlp_fwd_wr_kernel", "swin_attn_fwd": "swin_attn_fwd12_kernel<6>",   # KAIR_ATTN12 (swin_fused.hip)
             "window_attn_bwd": "attn_bwd_bf16_kernel<2>"}.get(fn, fn)
+
+
+def _x3_ring_nt(a):
+    """Whether an x3 gemm_nt launch takes the ring kernel (gemm_x3.hip nt_x3_ring_ok, the common cases)."""
+    A, N, K = a[0], a[4], a[5]
+    return N % 192 == 0 and K % 32 == 0 and (A.mode == 0 or (A.mode == 1 and A.dtype == 0 and A.im_C % 32 == 0))
 
 
 def pmc_traffic(key):
@@ -224,15 +290,15 @@ def cpu_baseline(batch=4, steps=4):
                       f"{steps} timed steps after 1 warm-up, torch CPU {threads} threads"}
 
 
-def fp32_line(bpg, device, drop_path, steps, warmup, roles=True):
-    """Throughput of the same training step on the exact-fp32 engine (fp32 MFMA, same program): the
-    reference's own arithmetic, whose forward matches the CPU oracle to 1e-7 dB.  Timed like the
-    headline (--steps / --warmup, same batch), with its MFMA roofline (train FLOPs / step time vs the
-    dense fp32 MFMA peak) and its longest kernels."""
+def engine_line(dtype, bpg, device, drop_path, steps, warmup, roles=True):
+    """Throughput of the same training step on another engine of the same program (same batch, --steps /
+    --warmup): "fp32" the exact-f32 MFMA engine (the reference's arithmetic, forward within 1e-7 dB of the
+    CPU oracle), "bf16" the 16-bit engine (bf16 MFMA, hi/lo bf16 pairs on the conv inputs and weights), with
+    the step's MFMA roofline (train FLOPs / step time vs the engine's dense MFMA peak) and its longest kernels."""
     from kair_amd.engine.trainer import FusedTrainer
     from kair_amd.utils.utils_image import synth_sr_batch
-    net = build_net("fp32", drop_path).to(device).train()
-    ema = build_net("fp32", drop_path).to(device).eval()
+    net = build_net(dtype, drop_path).to(device).train()
+    ema = build_net(dtype, drop_path).to(device).eval()
     ema.load_state_dict(net.state_dict())
     tr = FusedTrainer(net, ema, lr=2e-4, E_decay=0.999)
     L, Hh = synth_sr_batch(bpg, 48, 4, seed=1000, device=device)
@@ -246,33 +312,36 @@ def fp32_line(bpg, device, drop_path, steps, warmup, roles=True):
     dt = time.perf_counter() - t0
     from kair_amd.engine.swinir_engine import swinir_flops
     tf = swinir_flops(net, 48, 48)["train"] * bpg * steps / dt / 1e12
+    peak = PEAK_F32_TFLOPS if dtype == "fp32" else PEAK_BF16_TFLOPS
     top = []
     if roles:
         rs = time_roles(tr, serial=True)
         for k, v in sorted(rs.items(), key=lambda kv: -kv[1]["ms_total"])[:5]:
-            # the fp32 engine's kernels: the fp32 attention backward and the plain fp32 GEMMs (rocprof names)
-            kname = {"attn_bwd_bf16_kernel<2>": "attn_bwd_kernel<false>"}.get(v["rocprof"], v["rocprof"])
+            # the fp32 engine's attention backward is the fp32 kernel (rocprof name)
+            kname = {"attn_bwd_bf16_kernel<2>": "attn_bwd_kernel<false>"}.get(v["rocprof"], v["rocprof"]) if dtype == "fp32" \
+                else v["rocprof"]
             top.append({"role": k, "kernel": kname, "launches_per_step": v["launches"], "kernel_ms": round(v["ms"], 5),
                         "step_ms_total": round(v["ms_total"], 4)})
     del tr, net, ema
     return {"value": round(bpg * steps / dt, 2), "unit": "patches/s", "ms_per_step": round(1000 * dt / steps, 3),
-            "steps": steps, "warmup": warmup, "dtype": "fp32", "per_gpu_batch": bpg,
-            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tf / PEAK_F32_TFLOPS, 4),
-                         "what": "whole training step: train FLOPs per patch (swinir_flops) x patches/s vs dense fp32 MFMA"},
-            "kernels_by_duration": top,
-            "note": "the reference's arithmetic (exact-f32 MFMA engine); the headline is the split-operand bf16 engine"}
+            "steps": steps, "warmup": warmup, "dtype": dtype, "per_gpu_batch": bpg, "precision": PRECISION[dtype],
+            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(tf / peak, 4),
+                         "what": "whole training step: train FLOPs per patch (swinir_flops) x patches/s vs the dense MFMA "
+                                 "peak of the engine's operand type"},
+            "kernels_by_duration": top}
 
 
-def psnr_parity(net_gpu, device, n_eval=8):
+def psnr_parity(net_gpu, device, dtype, n_eval=8):
     """PSNR of the GPU forward vs the CPU oracle on the same (trained) weights, DropPath off (eval),
     averaged per image over n_eval held-out 48-px patches as the reference's test loop averages
-    (main_train_psnr.py: avg_psnr over the test set), float and uint8 / border-4.
+    (main_train_psnr.py: avg_psnr over the test set), float and uint8 / border-4; the largest single-image
+    deviation beside the means.
 
-    The fp32 parity engine (same kernels, exact-f32 MFMA) must match the oracle to 1e-3 dB; the bf16
-    engine's deviation is reported beside it.  One patch alone is not an evaluation set: bf16
-    activation rounding moves a single 192x192 uint8 PSNR by up to ~1e-3 dB either way, the
-    8-patch mean by ~3e-4 (tools/parity_seeds.py, DESIGN.md "parity at bf16")."""
+    The exact-fp32 engine and the fp32x3 engine (the headline) must match the oracle to 1e-3 dB; a bf16
+    engine's deviation is reported the same way.  One patch alone is not an evaluation set: bf16 activation
+    rounding moves a single 192x192 uint8 PSNR by up to ~1e-3 dB either way, the 8-patch mean by ~3e-4
+    (tools/parity_seeds.py, DESIGN.md "parity at bf16")."""
     from oracle import swinir as osw
     from kair_amd.utils import utils_image as U
     ref = osw.SwinIR(4, 3, 48, 8, 1.0, [6] * 6, 180, [6] * 6, 2, "pixelshuffle")
@@ -294,20 +363,23 @@ def psnr_parity(net_gpu, device, n_eval=8):
         pf = [U.psnr_float(X[i:i + 1], Hh[i:i + 1]) for i in range(n_eval)]
         pu = [U.calculate_psnr(U.tensor2uint(X[i]), U.tensor2uint(Hh[i]), border=4) for i in range(n_eval)]
         return pf, pu
-    (bf, bu), (ff, fu), (rf, ru) = per_image(E), per_image(E32), per_image(Er)
+    (hf, hu), (ff, fu), (rf, ru) = per_image(E), per_image(E32), per_image(Er)
     mean = lambda v: sum(v) / len(v)
     dmax = lambda a, b: max(abs(x - y) for x, y in zip(a, b))
     return {"eval": f"{n_eval} held-out 48-px LQ patches (synth seed 77), per-image PSNR averaged",
-            "cpu_oracle_db": round(mean(rf), 5), "fp32_gpu_db": round(mean(ff), 5),
-            "fp32_delta_db": round(abs(mean(ff) - mean(rf)), 7),
-            "uint8_border4_cpu_db": round(mean(ru), 5), "uint8_border4_fp32_gpu_db": round(mean(fu), 5),
-            "uint8_fp32_delta_db": round(abs(mean(fu) - mean(ru)), 7),
-            "bf16_gpu_db": round(mean(bf), 5), "bf16_delta_db": round(abs(mean(bf) - mean(rf)), 6),
-            "uint8_border4_bf16_gpu_db": round(mean(bu), 5), "uint8_bf16_delta_db": round(abs(mean(bu) - mean(ru)), 6),
-            "bf16_max_single_image_delta_db": round(dmax(bf, rf), 6),
-            "uint8_bf16_max_single_image_delta_db": round(dmax(bu, ru), 6),
-            "max_abs_fp32_vs_oracle": float((E32 - Er).abs().max()),
-            "max_abs_bf16_vs_oracle": float((E - Er).abs().max())}
+            "headline_dtype": dtype, "cpu_oracle_db": round(mean(rf), 5),
+            "headline_gpu_db": round(mean(hf), 5), "headline_delta_db": round(abs(mean(hf) - mean(rf)), 7),
+            "uint8_border4_cpu_db": round(mean(ru), 5), "uint8_border4_headline_gpu_db": round(mean(hu), 5),
+            "uint8_headline_delta_db": round(abs(mean(hu) - mean(ru)), 7),
+            "headline_max_single_image_delta_db": round(dmax(hf, rf), 7),
+            "uint8_headline_max_single_image_delta_db": round(dmax(hu, ru), 7),
+            "max_abs_headline_vs_oracle": float((E - Er).abs().max()),
+            "fp32_gpu_db": round(mean(ff), 5), "fp32_delta_db": round(abs(mean(ff) - mean(rf)), 7),
+            "uint8_border4_fp32_gpu_db": round(mean(fu), 5), "uint8_fp32_delta_db": round(abs(mean(fu) - mean(ru)), 7),
+            "max_abs_fp32_vs_oracle": float((E32 - Er).abs().max())}
+
+
+OTHER_STEPS, OTHER_WARMUP = 20, 5
 
 
 def other_configs(device):
@@ -324,11 +396,11 @@ def other_configs(device):
     res = {}
     for name, label in labels.items():
         try:
-            B, dt, loss = bm.run(name, 5, 3, device)
+            B, dt, loss = bm.run(name, OTHER_STEPS, OTHER_WARMUP, device)
             pps = B / dt
             tf = pps * bm.TRAIN_GFLOP[name] / 1e3
             res[name] = {"config": label, "value": round(pps, 2), "unit": "patches/s", "ms_per_step": round(dt * 1e3, 3),
-                         "steps": 5, "warmup": 3, "train_gflop_per_patch": bm.TRAIN_GFLOP[name],
+                         "steps": OTHER_STEPS, "warmup": OTHER_WARMUP, "train_gflop_per_patch": bm.TRAIN_GFLOP[name],
                          "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
                                       "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4)},
                          "final_loss": round(loss, 6)}
@@ -398,11 +470,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--global-batch", type=int, default=32)
     ap.add_argument("--per-gpu-batch", type=int, default=None, help="weak scaling: fixed batch per GPU")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3"])
+    ap.add_argument("--dtype", default="fp32x3", choices=["bf16", "fp32", "fp32x3"],
+                    help="fp32x3 (default): the reference's fp32 precision class on the fp16 matrix cores (split pairs); "
+                         "bf16: the 16-bit engine; fp32: exact fp32 MFMA")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--drop-path", type=float, default=0.1)
-    ap.add_argument("--no-fp32-line", action="store_true", help="skip the fp32 parity-config throughput line")
+    ap.add_argument("--no-fp32-line", action="store_true", help="skip the other engines' throughput lines")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the short single-GPU throughput lines of BASELINE.json configs C2 / C3 / C5 (and the "
                          "C1 network on the GPU)")
@@ -515,7 +589,8 @@ def main():
     value = gbatch * args.steps / wall
     ms_step = 1000.0 * wall / args.steps
     step_tflops = fl["train"] * gbatch / (wall / args.steps) / 1e12 / world   # per GPU
-    peak = PEAK_F32_TFLOPS if args.dtype == "fp32" else PEAK_BF16_TFLOPS
+    # the MFMA peak a FLOP of this engine is priced against: fp32x3 delivers fp32 FLOPs (3 fp16 products each)
+    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     roles, serial = {}, {}
     if not args.no_roles:
         try:
@@ -523,7 +598,6 @@ def main():
             serial = time_roles(tr, serial=True)
         except Exception as e:  # noqa: BLE001
             roles = serial = {"error": {"kernel": repr(e), "ms_total": 0.0}}
-    peak = PEAK_F32_TFLOPS if args.dtype == "fp32" else PEAK_BF16_TFLOPS
     TIMING = {"in_step": "in-step mean over the step's launches of this role: one eager fwd+loss+bwd, a HIP event pair "
                          "on the launch stream around each launch (side-stream concurrency kept, so a launch queued "
                          "behind side-stream work includes that wait)",
@@ -544,13 +618,18 @@ def main():
         if d.get("flops"):
             tf = d["flops"] / (d["ms"] * 1e-3) / 1e12
             r.update({"flops_per_launch": d["flops"], "achieved_tflops": round(tf, 2), "mfma_frac": round(tf / peak, 4)})
+            if args.dtype == "fp32x3":   # fp32-equivalent FLOPs vs the fp32 MFMA peak; 3 fp16 products per FLOP issued
+                r.update({"mfma_frac_vs": "dense fp32 MFMA peak (the fp32 FLOPs the split arithmetic delivers)",
+                          "issued_frac_of_fp16_peak": round(3 * tf / PEAK_BF16_TFLOPS, 4)})
         return r
     ranked = sorted(((k, v) for k, v in roles.items() if k != "error"), key=lambda kv: -kv[1]["ms_total"])
     ranked_serial = sorted(((k, v) for k, v in serial.items() if k != "error" and v.get("bytes")),
                            key=lambda kv: -kv[1]["ms_total"])
     # attention GEMMs (QKV / q.k^T / p.v / proj): the fused attention half, the attention backward, the proj and
-    # q/k/v input-gradient row GEMMs -- FLOPs over their in-step time against the dense bf16 MFMA peak
-    att_names = ("swin_attn_fwd", "attn_bwd_bf16_kernel", "rowgemm_kernel<12, 4, 2, 0>", "rowgemm_kernel<36")
+    # q/k/v input-gradient row GEMMs (bf16) / the split window-attention kernels (fp32x3) -- FLOPs over their
+    # in-step time against the engine's MFMA peak
+    att_names = ("swin_attn_fwd", "attn_bwd_bf16_kernel", "rowgemm_kernel<12, 4, 2, 0>", "rowgemm_kernel<36",
+                 "attn_fwd_x3_kernel", "attn_bwd_x3_kernel")
     att = [v for v in roles.values() if v.get("flops") and v["rocprof"].startswith(att_names)]
     att_mfma = None
     if att:
@@ -559,12 +638,14 @@ def main():
         tf = fl_att / (ms_att * 1e-3) / 1e12
         att_mfma = {"kernels": sorted({v["rocprof"] for v in att}), "flops_per_step": fl_att, "ms_per_step": round(ms_att, 4),
                     "achieved_tflops": round(tf, 2), "peak_tflops": peak, "mfma_frac": round(tf / peak, 4)}
+        if args.dtype == "fp32x3":
+            att_mfma["issued_frac_of_fp16_peak"] = round(3 * tf / PEAK_BF16_TFLOPS, 4)
     out = {
         "metric": "train patches/sec + PSNR, SwinIR x4 48-px LQ, at 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
         "dtype": args.dtype,
-        "precision": (PRECISION_BF16 if args.dtype == "bf16" else "fp32 operands, exact fp32 MFMA (v_mfma_f32_16x16x4_f32)"),
+        "precision": PRECISION[args.dtype],
         "data": ("synthetic: per step a fresh batch synthesised on the GPU (crop / augment / MATLAB bicubic) from "
                  "a 64-image 256x256 HR pool resident in HBM (SURVEY §8d recipe)" if args.data == "pool" else
                  "synthetic (one seeded bicubic-LR / HR batch resident in HBM, SURVEY §8d)"),
@@ -580,22 +661,27 @@ def main():
         "kernels_in_step": [roof(k, v) for k, v in ranked[:8]],
         "attention_gemm_mfma": att_mfma,
         "step_roofline": {"train_flop_per_patch": fl["train"], "achieved_tflops_per_gpu": round(step_tflops, 2),
-                          "frac_of_bf16_peak": round(step_tflops / peak, 4)},
+                          "peak_tflops": peak, "frac_of_peak": round(step_tflops / peak, 4),
+                          **({"issued_frac_of_fp16_peak": round(3 * step_tflops / PEAK_BF16_TFLOPS, 4)}
+                             if args.dtype == "fp32x3" else {})},
         "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
         "final_loss": round(final_loss, 6),
     }
-    if args.dtype == "bf16" and world == 1 and not args.no_fp32_line:
-        try:
-            out["fp32_parity_line"] = fp32_line(bpg, device, args.drop_path, args.steps, args.warmup,
-                                                roles=not args.no_roles)
-        except Exception as e:  # noqa: BLE001
-            out["fp32_parity_line"] = {"error": repr(e)}
+    if world == 1 and not args.no_fp32_line:   # the other engines of the same program, same step
+        for dt in ("fp32", "bf16"):
+            if dt == args.dtype:
+                continue
+            try:
+                out[f"{dt}_engine_line"] = engine_line(dt, bpg, device, args.drop_path, args.steps, args.warmup,
+                                                      roles=not args.no_roles)
+            except Exception as e:  # noqa: BLE001
+                out[f"{dt}_engine_line"] = {"error": repr(e)}
     if not args.no_psnr:
         try:
-            out["psnr"] = psnr_parity(net, device)
+            out["psnr"] = psnr_parity(net, device, args.dtype)
         except Exception as e:  # noqa: BLE001
             out["psnr"] = {"error": repr(e)}
-    if world == 1 and args.dtype == "bf16" and not args.no_other_configs:
+    if world == 1 and not args.no_other_configs:
         out["other_configs"] = other_configs(device)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()

@@ -590,6 +590,9 @@ int kair_debug_attn_stamps(unsigned long long* host, int n);
 /* Perf investigation only: per-wave phase stamps (8 s_memtime values) of the fused attention half's last
  * window per workgroup (cleared by the read), from a library built with --debug-ablations and KAIR_ATTN_DBG bit 8 set. */
 int kair_debug_fused_stamps(unsigned long long* host, int n);
+/* Perf investigation only: phase stamps of the last x3 NT ring launch (CTAs 0-3, 8 waves, iterations 0-63, 5
+ * s_memtime values each; cleared by the read), from a --debug-ablations library with KAIR_RING_DBG bit 8 set. */
+int kair_debug_x3_stamps(unsigned long long* host, int n);
 
 #ifdef __cplusplus
 }

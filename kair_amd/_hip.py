@@ -178,6 +178,7 @@ _SIGS = {
                           c_long, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_long, c_int, c_int, c_int, c_vp],
     "kair_debug_attn_stamps": [c_vp, c_int],
     "kair_debug_fused_stamps": [c_vp, c_int],
+    "kair_debug_x3_stamps": [c_vp, c_int],
     "kair_swin_mlp_bwd_ws": [],
     "kair_swin_mlp_bwd": [c_vp, c_long, c_vp, c_long, c_vp, c_vp, c_vp, c_long, c_vp, c_long, c_vp, c_vp, c_vp, c_int,
                           c_vp, c_long, c_vp, c_long, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_long,
@@ -209,8 +210,8 @@ def lib():
             raise RuntimeError(f"kair_amd: HIP kernel library not built ({LIB_PATH}); run `python -m kair_amd.build`")
         L = ctypes.CDLL(LIB_PATH)
         for name, args in _SIGS.items():
-            if name.startswith("kair_debug_") and not hasattr(L, name):
-                continue   # perf-investigation entry points: optional (A/B runs load older builds)
+            if (name.startswith("kair_debug_") or os.environ.get("KAIR_LIB") == "base") and not hasattr(L, name):
+                continue   # perf-investigation entry points, and an A/B baseline build's older symbol set
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, c_int)
@@ -796,6 +797,15 @@ def debug_attn_stamps(n=8192 * 8):
     buf = (ctypes.c_ulonglong * n)()
     check(lib().kair_debug_attn_stamps(ctypes.cast(buf, c_vp), n), "debug_attn_stamps")
     return list(buf)
+
+
+def debug_x3_stamps(n=4 * 8 * 64 * 5):
+    """Phase stamps of the last x3 NT ring launch run with KAIR_RING_DBG bit 8 (debug builds, perf only):
+    [CTA 0..3][wave][iteration 0..63][loop top, chunk waited, barrier + DMA issued, MFMAs done, epilogue done]."""
+    import numpy as np
+    buf = np.zeros(n, dtype=np.uint64)
+    check(lib().kair_debug_x3_stamps(ctypes.c_void_p(buf.ctypes.data), n), "debug_x3_stamps")
+    return buf
 
 
 def debug_fused_stamps(n=4096 * 8):

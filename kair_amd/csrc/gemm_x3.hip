@@ -354,7 +354,18 @@ constexpr int XR_DMA = 5;   // DMA wave-instructions per wave per chunk (2 A + 3
 
 enum { XE_ROWS_F32 = 0, XE_ROWS_PAIR = 1, XE_QKV = 2 };
 
-template <typename TA, int AM, int EM, int EX>
+// perf-investigation phase stamps of the NT ring (debug builds, KAIR_RING_DBG bit 8): CTAs 0..XS_CTAS-1, every
+// wave, iterations 0..XS_IT-1, s_memtime at XS_N points (loop top, after the chunk wait, after the barrier +
+// DMA issue, after the MFMAs, after the epilogue); read with kair_debug_x3_stamps
+constexpr int XS_CTAS = 4, XS_IT = 64, XS_N = 5;
+__device__ unsigned long long g_x3_stamps[XS_CTAS * 8 * XS_IT * XS_N];
+KAIR_DEV unsigned long long x3_now() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+template <typename TA, int AM, int EM, int EX, bool GELU>
 __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
   __shared__ __attribute__((aligned(16))) char smem[XR_NS * XR_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -473,56 +484,76 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
 
   const float as = A.x3s;
   int kc = 0, cs = 0, ct = 0;   // consumer: chunk j = ct * nk + kc in stage cs
+  // store instructions this wave issued at iterations j-1, j-2, j-3: younger than chunk j's DMA (issued at
+  // iteration j-3 before that iteration's epilogue), so chunk j's counted wait adds them
+  int sq1 = 0, sq2 = 0, sq3 = 0;
+  const bool stamping = KAIR_DBG(E.dbg & 8) && blockIdx.x < XS_CTAS;
+  unsigned long long* stp = g_x3_stamps + ((long)blockIdx.x * 8 + wave) * XS_IT * XS_N;
+  auto stamp = [&](int j, int k) {
+    if (stamping && j < XS_IT) {
+      const unsigned long long t = x3_now();
+      if (lane == 0) stp[j * XS_N + k] = t;
+    }
+  };
   for (int j = 0; j < total; ++j) {
+    stamp(j, 0);
     const int ahead = (total - 1 - j) < (XR_NS - 2) ? (total - 1 - j) : (XR_NS - 2);
-    vm_wait(XR_DMA * ahead);
+    vm_wait(XR_DMA * ahead + sq1 + sq2 + sq3);
+    stamp(j, 1);
     ring_barrier();   // chunk j is in LDS for every wave; stage (j-1) % NS is free
     if (lj < total) issue_next();
-    const char* st = smem + cs * XR_STAGE;
-    if (!KAIR_DBG(E.dbg & 2)) {
-    f16x8 ah[2], al[2], bh[6], bl[6];
+    stamp(j, 2);
+    const bool tile_end = kc == nk - 1 && !KAIR_DBG(E.dbg & 1);
+    auto mfma_chunk = [&]() {
+      if (KAIR_DBG(E.dbg & 2)) return;
+      const char* st = smem + cs * XR_STAGE;
+      f16x8 ah[2], al[2], bh[6], bl[6];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = wm * 32 + i * 16 + fr;
-      const char* row = st + r * 128;
-      if constexpr (sizeof(TA) == 2) {
-        ah[i] = *(const f16x8*)(row + ((fq ^ (r & 7)) << 4));
-        al[i] = *(const f16x8*)(row + (((4 + fq) ^ (r & 7)) << 4));
-      } else {
-        const float4 x0 = *(const float4*)(row + (((2 * fq) ^ (r & 7)) << 4));
-        const float4 x1 = *(const float4*)(row + (((2 * fq + 1) ^ (r & 7)) << 4));
-        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm * 32 + i * 16 + fr;
+        const char* row = st + r * 128;
+        if constexpr (sizeof(TA) == 2) {
+          ah[i] = *(const f16x8*)(row + ((fq ^ (r & 7)) << 4));
+          al[i] = *(const f16x8*)(row + (((4 + fq) ^ (r & 7)) << 4));
+        } else {
+          const float4 x0 = *(const float4*)(row + (((2 * fq) ^ (r & 7)) << 4));
+          const float4 x1 = *(const float4*)(row + (((2 * fq + 1) ^ (r & 7)) << 4));
+          const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const float w = xv[c] * as;
-          ah[i][c] = (f16)w;
-          al[i][c] = (f16)(w - (float)ah[i][c]);
+          for (int c = 0; c < 8; ++c) {
+            const float w = xv[c] * as;
+            ah[i][c] = (f16)w;
+            al[i][c] = (f16)(w - (float)ah[i][c]);
+          }
         }
       }
-    }
-#pragma unroll
-    for (int jn = 0; jn < 6; ++jn) {
-      const int n = wn * 96 + jn * 16 + fr;
-      const char* row = st + XR_ABYTES + n * 128;
-      bh[jn] = *(const f16x8*)(row + ((fq ^ (n & 7)) << 4));
-      bl[jn] = *(const f16x8*)(row + (((4 + fq) ^ (n & 7)) << 4));
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int jn = 0; jn < 6; ++jn) {
-        acc[i][jn] = mfma16(bh[jn], ah[i], acc[i][jn]);
-        acc[i][jn] = mfma16(bl[jn], ah[i], acc[i][jn]);
-        acc[i][jn] = mfma16(bh[jn], al[i], acc[i][jn]);
+        const int n = wn * 96 + jn * 16 + fr;
+        const char* row = st + XR_ABYTES + n * 128;
+        bh[jn] = *(const f16x8*)(row + ((fq ^ (n & 7)) << 4));
+        bl[jn] = *(const f16x8*)(row + (((4 + fq) ^ (n & 7)) << 4));
       }
-    }
-    if (kc == nk - 1 && !KAIR_DBG(E.dbg & 1)) {
-      // Epilogue from registers.  Every operand load of the tile is issued before the first store (one
-      // memory round trip per tile); fragment pairs re-laid by v_permlane16_swap give this lane columns
-      // [c8[p], c8[p] + 8) of rows m0 + {0, 16}.
-      const int m0 = (mt0 + ct * mstride) * XR_BM + wm * 32 + fr;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 6; ++jn) {
+          acc[i][jn] = mfma16(bh[jn], ah[i], acc[i][jn]);
+          acc[i][jn] = mfma16(bl[jn], ah[i], acc[i][jn]);
+          acc[i][jn] = mfma16(bh[jn], al[i], acc[i][jn]);
+        }
+    };
+    int sj = 0;
+    if (!tile_end) {
+      mfma_chunk();
+      stamp(j, 3);
+    } else {
+      // A tile's last chunk: its epilogue operands are loaded before the MFMAs (their latency overlaps them),
+      // unconditionally and in this one straight-line branch -- no control-flow merge between a load and its
+      // use, so hipcc never holds a pending epilogue load across the loop back-edge.
       int rowv[2];
       bool okm[2];
+      const int m0 = (mt0 + ct * mstride) * XR_BM + wm * 32 + fr;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int m = m0 + i * 16;
@@ -546,13 +577,24 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
             ex[i][p][0] = *(const float4*)(src + c8[p]);
             ex[i][p][1] = *(const float4*)(src + c8[p] + 4);
           }
-        if constexpr (EX == EX_RESID) {
-          if (E.rowscale) {
+      }
+      if constexpr (EX == EX_RESID) {
+        const bool hs = E.rowscale != nullptr;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) rs[i] = E.rowscale[fdiv(rowv[i], E.d_rps)];
-          }
+        for (int i = 0; i < 2; ++i) {
+          const float r = *(hs ? E.rowscale + fdiv(rowv[i], E.d_rps) : (const float*)g_kair_zero_line);
+          rs[i] = hs ? r : 1.f;
         }
       }
+      mfma_chunk();
+      stamp(j, 3);
+      // Epilogue from registers: fragment pairs re-laid by v_permlane16_swap give this lane columns
+      // [c8[p], c8[p] + 8) of rows m0 + {0, 16}.  sj counts the store instructions that MUST issue (rows with
+      // at least one valid lane in the wave); a compiler that also issues fully masked ones only makes the
+      // next chunk waits stricter.
+      const int nst = EM == XE_ROWS_F32 ? (E.pre ? 4 : 2) : (E.out_lo ? 2 : 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) sj += __ballot(okm[i]) != 0 ? 3 * nst : 0;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -573,10 +615,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
               pre[c] = v[c];
-              if (E.act == KAIR_ACT_GELU) {
-                if (E.prek) pre[c] = gelu_erf_grad(v[c]);
-                v[c] = gelu_erf(v[c]);
-              } else if (E.act == KAIR_ACT_LEAKY) v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
+              if constexpr (GELU) {   // (the erf GELU only in its own instantiations: code size)
+                if (E.act == KAIR_ACT_GELU) {
+                  if (E.prek) pre[c] = gelu_erf_grad(v[c]);
+                  v[c] = gelu_erf(v[c]);
+                }
+              }
+              if (E.act == KAIR_ACT_LEAKY) v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
               else if (E.act == KAIR_ACT_RELU) v[c] = fmaxf(v[c], 0.f);
             }
             if constexpr (EX != EX_NONE) {
@@ -586,7 +631,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
               for (int c = 0; c < 8; ++c) {
                 if constexpr (EX == EX_RESID) v[c] = x8[c] + rs[i] * v[c];
                 else if (E.gkind == 4) v[c] *= x8[c];
-                else if (E.gkind == 1) v[c] *= gelu_erf_grad(x8[c]);
+                else if (GELU && E.gkind == 1) v[c] *= gelu_erf_grad(x8[c]);
                 else if (E.gkind == 2) v[c] *= (x8[c] > 0.f ? 1.f : E.slope);
                 else v[c] *= (x8[c] > 0.f ? 1.f : 0.f);
               }
@@ -618,6 +663,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
 #pragma unroll
         for (int jn = 0; jn < 6; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    stamp(j, 4);
+    sq3 = sq2; sq2 = sq1; sq1 = sj;
     if (++kc == nk) { kc = 0; ++ct; }
     if (++cs == XR_NS) cs = 0;
   }
@@ -833,6 +880,7 @@ bool nt_x3_ring_ok(const kair_operand* A, const kair_operand* B, const kair_epil
     if (E->resid && (E->ldr % 4 || (uintptr_t)E->resid % 16)) return false;
     if (E->gate && (E->gate_dtype != KAIR_F32 || E->ldg % 4 || (uintptr_t)E->gate % 16)) return false;
     if (E->rowscale && !E->resid) return false;
+    if (E->act == KAIR_ACT_GELU && (E->resid || E->gate)) return false;   // no such instantiation
   }
   if (A->mode == KAIR_LD_ROWS) return A->dtype == KAIR_F16 ? A->ld % 8 == 0 : A->ld % 4 == 0;
   return A->mode == KAIR_LD_IM2COL3 && A->dtype == KAIR_F32 && A->im_C % 32 == 0 && (A->ld == 0 ? A->im_C : A->ld) % 4 == 0;
@@ -848,15 +896,19 @@ int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int
   per = (tilesM + rounds - 1) / rounds;   // the same makespan on as few CUs as it needs
   const dim3 g(per * tilesN), bl(512);
   if (e.omode == KAIR_OUT_QKVBLK)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_QKV, EX_NONE>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_QKV, EX_NONE, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
   else if (e.odt == KAIR_F16)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_PAIR, EX_NONE>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_PAIR, EX_NONE, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
   else if (e.resid)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_RESID>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_RESID, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+  else if (e.gate && e.gkind == 1)
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_GATE_F32, true>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
   else if (e.gate)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_GATE_F32>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_GATE_F32, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+  else if (e.act == KAIR_ACT_GELU)
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_NONE, true>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
   else
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_NONE>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_NONE, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -886,6 +938,19 @@ int x3_operand_ok(const kair_operand* o, const char* what) {
 }
 
 }  // namespace
+
+// copy the NT ring's phase stamps to the host and clear them (perf investigation only; zeros in release builds)
+extern "C" int kair_debug_x3_stamps(unsigned long long* host, int n) {
+  KAIR_CHECK_ARG(host && n > 0 && n <= XS_CTAS * 8 * XS_IT * XS_N, "debug_x3_stamps: bad args");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x3_stamps), sizeof(unsigned long long) * n, 0, hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return kair_set_error(KAIR_ERR_HIP, "debug_x3_stamps: copy failed");
+  void* dev = nullptr;
+  if (hipGetSymbolAddress(&dev, HIP_SYMBOL(g_x3_stamps)) != hipSuccess ||
+      hipMemset(dev, 0, sizeof(unsigned long long) * XS_CTAS * 8 * XS_IT * XS_N) != hipSuccess)
+    return kair_set_error(KAIR_ERR_HIP, "debug_x3_stamps: clear failed");
+  return 0;
+}
 
 int kair_gemm_nt_x3(const kair_operand* A, const kair_operand* B, const kair_epilogue* E, long M, int N, int K,
                     void* stream) {

@@ -336,6 +336,9 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_wgrad_kernel(const NarrowW
     if (tid < PXS) *(uint2*)(&sEr[yy & 3][tid * 4]) = pe;
     if (tid >= PXS && tid < PXS + 2) *(uint2*)(&sEr[yy & 3][EPX + (tid - PXS) * 4]) = make_uint2(0, 0);
   };
+  // the zero tails of all four dE slots (taps >= 9 read slot 0's): set once here, and store_e only ever
+  // rewrites a tail with zeros, so every slot's tail is zero whichever slots a strip restart fills
+  if (tid < 8) *(uint2*)(&sEr[tid >> 1][EPX + (tid & 1) * 4]) = make_uint2(0, 0);
   long cur_strip = -1;
   int xb = 0;
   for (long g = run.g0; g < run.g1; ++g) {
