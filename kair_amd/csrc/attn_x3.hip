@@ -499,10 +499,10 @@ int x3_cus() {
 
 }  // namespace
 
-// windows per backward wave: enough (group, head) waves for 4 per CU in one round (the bf16 kernel's
-// grouping, so kair_window_attn_bwd_groups / _ws cover both)
+// windows per backward wave: enough (group, head) waves for ONE round at the residency the backward's LDS
+// allows (3 one-wave workgroups of ~50 KB per CU; kair_window_attn_bwd_groups / _ws size the partials from it)
 long kair_attn_x3_wpg(long nWin, int nh) {
-  const long slots = 4L * x3_cus();
+  const long slots = 3L * x3_cus();
   const long w = (nWin * nh + slots - 1) / slots;
   return w < 1 ? 1 : w;
 }

@@ -12,6 +12,8 @@
 // Operands: fp32 (split at the LDS commit, read from HBM once) or fp16 hi planes with their lo planes
 // (kair_operand.lo_ptr).  LDS holds hi and lo planes of both operands; 32-deep k-steps (NT) / 32-row
 // reduction steps (TN), double-buffered by register staging as the bf16 kernels (gemm.hip).
+#include <type_traits>
+
 #include "gemm_common.h"
 
 namespace {
@@ -348,15 +350,20 @@ __global__ __launch_bounds__(NT, 2) void gemm_tn_x3_kernel(Op A, Op B, float* ws
 // swapped (D = B A^T) so after a v_permlane16_swap of fragment pairs each lane owns 8 consecutive output
 // columns of one row and finishes them with the shared 8-column epilogue.
 // ------------------------------------------------------------------------------------------
-constexpr int XR_BM = 128, XR_BN = 192, XR_NS = 4;
-constexpr int XR_ABYTES = XR_BM * 128, XR_STAGE = XR_ABYTES + XR_BN * 128;   // 16 + 24 KiB
-constexpr int XR_DMA = 5;   // DMA wave-instructions per wave per chunk (2 A + 3 B)
+constexpr int XR_BM = 128, XR_NB = 3, XR_ASTAGE = XR_BM * 128;   // B ring (L2-resident weights) depth; A stage 16 KiB
+// the N-tile BN (64 / 128 / 192 / 256 columns) sets the B stage (BN x 128 B) and the A ring depth (HBM: the deeper
+// ring, as deep as the 160 KiB allow: 5 stages up to BN = 192, 4 at 256)
+template <int BN> struct XR {
+  static constexpr int BSTAGE = BN * 128, NA = BN <= 192 ? 5 : 4, LDS = NA * XR_ASTAGE + XR_NB * BSTAGE + BN * 4;
+  static constexpr int RN = BN / 32;    // 16-column fragments per wave (2 x 2 waves per group: BN / 2 columns each)
+  static constexpr int BI = BN / 64;    // B DMA wave-instructions per wave per chunk
+};
 
 enum { XE_ROWS_F32 = 0, XE_ROWS_PAIR = 1, XE_QKV = 2 };
 
 // perf-investigation phase stamps of the NT ring (debug builds, KAIR_RING_DBG bit 8): CTAs 0..XS_CTAS-1, every
-// wave, iterations 0..XS_IT-1, s_memtime at XS_N points (loop top, after the chunk wait, after the barrier +
-// DMA issue, after the MFMAs, after the epilogue); read with kair_debug_x3_stamps
+// wave, intervals 0..XS_IT-1, s_memtime at XS_N points (interval top, after the chunk wait, after the barrier +
+// DMA issue, after the group's first phase, after its second); read with kair_debug_x3_stamps
 constexpr int XS_CTAS = 4, XS_IT = 64, XS_N = 5;
 __device__ unsigned long long g_x3_stamps[XS_CTAS * 8 * XS_IT * XS_N];
 KAIR_DEV unsigned long long x3_now() {
@@ -365,11 +372,28 @@ KAIR_DEV unsigned long long x3_now() {
   return t;
 }
 
-template <typename TA, int AM, int EM, int EX, bool GELU>
+// fp32-rows epilogue activation / gate forms (compile-time: a run-time uniform test per element became a scalar
+// branch per element, ~6.5 k cycles per tile epilogue)
+enum { XA_NONE = 0, XA_GELU = 1, XA_GELU_X = 2, XA_LEAKY = 3 };   // GELU: pre = GELU'(x); GELU_X: pre = x
+enum { XG_MUL = 4, XG_LEAKY = 2 };                                 // kair_epilogue.gate_kind 4 / 2
+
+// Two wave groups in ping-pong (MI355X_MICROARCH "Two waves per SIMD"): waves 0-3 (group 0, one per SIMD) own
+// rows 0-63 of the tile, waves 4-7 (group 1, the other wave of each SIMD) rows 64-127; each wave 32 rows x BN / 2
+// columns.  Between two barriers (one per k-chunk t) group 0 reads chunk t's fragments then multiplies them, group 1
+// multiplies chunk t-1 (fragments read in the previous interval) then reads chunk t's: while one wave of a SIMD
+// waits on LDS, splits fp32 operands or runs its epilogue, its partner keeps the matrix pipe busy.  Chunk t's A
+// part is issued NA - 1 intervals ahead (A ring of NA), its B part 2 ahead (B ring of 3, L2-resident weights); a
+// wave waits for its own pieces of chunk t with a counted vmcnt (the DMA, epilogue loads and stores it issued
+// after them) before the barrier that opens interval t.
+template <typename TA, int AM, int EM, int EX, int ACT, int GK, int BN>
 __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
-  __shared__ __attribute__((aligned(16))) char smem[XR_NS * XR_STAGE];
+  constexpr int NA = XR<BN>::NA, RN = XR<BN>::RN, NP = RN / 2, BI = XR<BN>::BI, BSTAGE = XR<BN>::BSTAGE, WC = BN / 2;
+  __shared__ __attribute__((aligned(16))) char smem[XR<BN>::LDS];
+  char* const sA = smem;
+  char* const sB = smem + NA * XR_ASTAGE;
+  float* const sBias = (float*)(sB + XR_NB * BSTAGE);   // the N-tile's bias (zeros without one), read by the epilogue
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int grp = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
   const int fr = lane & 15, fq = lane >> 4, q8 = lane & 7;
   const int cta = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = cta % tilesN, mstride = gridDim.x / tilesN, mt0 = cta / tilesN;
@@ -377,18 +401,18 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
   const int ntile = (tilesM - mt0 + mstride - 1) / mstride;
   const int nk = K / 32;
   const int total = ntile * nk;
-  const int n0 = nt * XR_BN;
+  const int n0 = nt * BN;
   const f16* zero = (const f16*)g_kair_zero_line;
 
   // epilogue columns (fixed per CTA): after the permlane swap of fragment pair (2p, 2p + 1) a lane owns
   // columns c8[p] .. + 8 of fragment 2p + (fq & 1); their bias, and (QKV) the column part of the offset
-  int c8[3];
-  long colo[3];
-  float bias8[3][8];
+  int c8[NP], oc[NP];
+  long colo[NP];
 #pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    const int n = n0 + wn * 96 + (2 * p + (fq & 1)) * 16 + (fq >> 1) * 8;
+  for (int p = 0; p < NP; ++p) {
+    const int n = n0 + wn * WC + (2 * p + (fq & 1)) * 16 + (fq >> 1) * 8;
     c8[p] = n;
+    oc[p] = E.ones_col - n;   // in [0, 8): this lane's column of the ones column
     if constexpr (EM == XE_QKV) {
       const int pw = E.nh * E.hdp;
       const int part = fdiv(n, E.d_pw), rr = n - part * pw;
@@ -397,24 +421,21 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
     } else {
       colo[p] = 0;
     }
-    const float4 b0 = *(const float4*)(E.bias ? E.bias + n : (const float*)g_kair_zero_line);
-    const float4 b1 = *(const float4*)(E.bias ? E.bias + n + 4 : (const float*)g_kair_zero_line);
-    bias8[p][0] = b0.x; bias8[p][1] = b0.y; bias8[p][2] = b0.z; bias8[p][3] = b0.w;
-    bias8[p][4] = b1.x; bias8[p][5] = b1.y; bias8[p][6] = b1.z; bias8[p][7] = b1.w;
   }
-
-  // B loader: this lane's three weight rows (fixed for the CTA), unit already swizzled
-  const f16* bsrc[3];
+  for (int i = tid; i < BN; i += 512) sBias[i] = E.bias && n0 + i < E.N ? E.bias[n0 + i] : 0.f;   // (visible after the
+                                                                                                // first barrier)
+  // B loader: this lane's BI weight rows (fixed for the CTA), unit already swizzled
+  const f16* bsrc[BI];
 #pragma unroll
-  for (int ii = 0; ii < 3; ++ii) {
-    const int r = (wave * 3 + ii) * 8 + (lane >> 3), u = q8 ^ (r & 7);
+  for (int ii = 0; ii < BI; ++ii) {
+    const int r = (wave * BI + ii) * 8 + (lane >> 3), u = q8 ^ (r & 7);
     bsrc[ii] = n0 + r < (int)B.M ? (const f16*)B.ptr + (long)(n0 + r) * B.ld + (u < 4 ? u * 8 : 64 + (u - 4) * 8) : nullptr;
   }
   // A loader: this lane's two rows of the tile being loaded
   long aoff[2];
   int ay[2], ax[2], au[2];
   bool aok[2];
-  auto load_rows = [&](int i) {
+  auto load_rows = [&](int i) __attribute__((always_inline)) {
     const int mt = mt0 + i * mstride;
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii) {
@@ -434,11 +455,12 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       }
     }
   };
-  int lj = 0, lt = 0, lkc = 0, ls = 0;   // next chunk to issue: tile lt, k-chunk lkc, stage ls
-  auto issue_next = [&]() {
-    if (lkc == 0) load_rows(lt);
-    const int k0 = lkc * 32;
-    char* st = smem + ls * XR_STAGE;
+  // issue cursors: A chunk (tile at, k-chunk ak, stage as_), B k-chunk bk in stage bs
+  int at = 0, ak = 0, as_ = 0, bk = 0, bs = 0;
+  auto issue_a = [&]() __attribute__((always_inline)) {
+    if (ak == 0) load_rows(at);
+    const int k0 = ak * 32;
+    char* st = sA + as_ * XR_ASTAGE;
     int dy = 0, dx = 0, c0 = k0;
     if constexpr (AM == AM_IM2COL) {
       const int tap = fdiv(k0, A.d_imC);
@@ -461,213 +483,247 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
           src = (const float*)A.ptr + (aoff[ii] + (long)(y >> A.up_sh) * (A.imW >> A.up_sh) + (x >> A.up_sh)) * A.ld + c0 +
                 au[ii] * 4;
       }
-      if (!KAIR_DBG(E.dbg & 4)) glds16(src, st + (wave * 2 + ii) * 1024);
+      if (!KAIR_DBG(E.dbg & 36)) glds16(src, st + (wave * 2 + ii) * 1024);
     }
-    const int kb = (k0 >> 6) * 128 + (k0 & 63);
-#pragma unroll
-    for (int ii = 0; ii < 3; ++ii)
-      if (!KAIR_DBG(E.dbg & 4)) glds16(bsrc[ii] ? (const void*)(bsrc[ii] + kb) : (const void*)zero, st + XR_ABYTES + (wave * 3 + ii) * 1024);
-    ++lj;
-    if (++lkc == nk) { lkc = 0; ++lt; }
-    if (++ls == XR_NS) ls = 0;
+    if (++ak == nk) { ak = 0; ++at; }
+    if (++as_ == NA) as_ = 0;
   };
-
+  auto issue_b = [&]() __attribute__((always_inline)) {
+    const int k0 = bk * 32, kb = (k0 >> 6) * 128 + (k0 & 63);
+    char* st = sB + bs * BSTAGE;
 #pragma unroll
-  for (int j = 0; j < XR_NS - 1; ++j)
-    if (lj < total) issue_next();
+    for (int ii = 0; ii < BI; ++ii)
+      if (!KAIR_DBG(E.dbg & 20)) glds16(bsrc[ii] ? (const void*)(bsrc[ii] + kb) : (const void*)zero, st + (wave * BI + ii) * 1024);
+    if (++bk == nk) bk = 0;
+    if (++bs == XR_NB) bs = 0;
+  };
+  // interval u issues A chunk u + NA - 1 and B chunk u + NB - 1 (when in range); the prologue runs the virtual
+  // intervals -(NA - 1) .. -1.  nA / nB: the DMA instructions one interval issues.
+  auto nA = [&](int u) __attribute__((always_inline)) { return u + NA - 1 >= 0 && u + NA - 1 < total ? 2 : 0; };
+  auto nB = [&](int u) __attribute__((always_inline)) { return u + XR_NB - 1 >= 0 && u + XR_NB - 1 < total ? BI : 0; };
+  for (int u = -(NA - 1); u < 0; ++u) {
+    if (nA(u)) issue_a();
+    if (nB(u)) issue_b();
+  }
 
-  f32x4 acc[2][6];
+  f32x4 acc[2][RN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int jn = 0; jn < 6; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f16x8 ah[2], al[2], bh[RN], bl[RN];   // this wave's fragments of the chunk it multiplies next
 
   const float as = A.x3s;
-  int kc = 0, cs = 0, ct = 0;   // consumer: chunk j = ct * nk + kc in stage cs
-  // store instructions this wave issued at iterations j-1, j-2, j-3: younger than chunk j's DMA (issued at
-  // iteration j-3 before that iteration's epilogue), so chunk j's counted wait adds them
-  int sq1 = 0, sq2 = 0, sq3 = 0;
-  const bool stamping = KAIR_DBG(E.dbg & 8) && blockIdx.x < XS_CTAS;
-  unsigned long long* stp = g_x3_stamps + ((long)blockIdx.x * 8 + wave) * XS_IT * XS_N;
-  auto stamp = [&](int j, int k) {
-    if (stamping && j < XS_IT) {
-      const unsigned long long t = x3_now();
-      if (lane == 0) stp[j * XS_N + k] = t;
+  // chunk c's fragments from stages (c % NA, c % NB): A rows of this wave, B columns of this wave
+  auto load_frags = [&](int sa, int sb) __attribute__((always_inline)) {
+    const char* stA = sA + sa * XR_ASTAGE;
+    const char* stB = sB + sb * BSTAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = grp * 64 + wm * 32 + i * 16 + fr;
+      const char* row = stA + r * 128;
+      if constexpr (sizeof(TA) == 2) {
+        ah[i] = *(const f16x8*)(row + ((fq ^ (r & 7)) << 4));
+        al[i] = *(const f16x8*)(row + (((4 + fq) ^ (r & 7)) << 4));
+      } else {
+        const float4 x0 = *(const float4*)(row + (((2 * fq) ^ (r & 7)) << 4));
+        const float4 x1 = *(const float4*)(row + (((2 * fq + 1) ^ (r & 7)) << 4));
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const float w = xv[c] * as;
+          ah[i][c] = (f16)w;
+          al[i][c] = (f16)(w - (float)ah[i][c]);
+        }
+      }
+    }
+#pragma unroll
+    for (int jn = 0; jn < RN; ++jn) {
+      const int n = wn * WC + jn * 16 + fr;
+      const char* row = stB + n * 128;
+      bh[jn] = *(const f16x8*)(row + ((fq ^ (n & 7)) << 4));
+      bl[jn] = *(const f16x8*)(row + (((4 + fq) ^ (n & 7)) << 4));
     }
   };
-  for (int j = 0; j < total; ++j) {
-    stamp(j, 0);
-    const int ahead = (total - 1 - j) < (XR_NS - 2) ? (total - 1 - j) : (XR_NS - 2);
-    vm_wait(XR_DMA * ahead + sq1 + sq2 + sq3);
-    stamp(j, 1);
-    ring_barrier();   // chunk j is in LDS for every wave; stage (j-1) % NS is free
-    if (lj < total) issue_next();
-    stamp(j, 2);
-    const bool tile_end = kc == nk - 1 && !KAIR_DBG(E.dbg & 1);
-    auto mfma_chunk = [&]() {
-      if (KAIR_DBG(E.dbg & 2)) return;
-      const char* st = smem + cs * XR_STAGE;
-      f16x8 ah[2], al[2], bh[6], bl[6];
+  auto mfma_chunk = [&]() __attribute__((always_inline)) {
+    if (KAIR_DBG(E.dbg & 2)) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn) {
+        acc[i][jn] = mfma16(bh[jn], ah[i], acc[i][jn]);
+        acc[i][jn] = mfma16(bl[jn], ah[i], acc[i][jn]);
+        acc[i][jn] = mfma16(bh[jn], al[i], acc[i][jn]);
+      }
+  };
+  // multiply the fragments in registers into acc; the tile's last chunk also runs its epilogue, its operands
+  // loaded after the MFMAs (the partner group's phase covers their latency) and used in the same straight-line
+  // branch (no control-flow merge between a load and its use: hipcc never holds a pending load across the loop
+  // back-edge).
+  // Returns the vector-memory instructions issued (epilogue loads + the stores that MUST issue: rows with at least
+  // one valid lane in the wave -- a compiler that also issues fully masked ones only makes later waits stricter).
+  auto compute = [&](bool tile_end, int ct) __attribute__((always_inline)) -> int {
+    if (!tile_end || KAIR_DBG(E.dbg & 1)) {
+      mfma_chunk();
+      return 0;
+    }
+    int nvm = 0;
+    int rowv[2];
+    bool okm[2];
+    const int m0 = (mt0 + ct * mstride) * XR_BM + grp * 64 + wm * 32 + fr;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = m0 + i * 16;
+      okm[i] = m < (int)E.M;
+      const int mm = okm[i] ? m : 0;
+      if constexpr (EM == XE_QKV) {
+        const int win = fdiv(mm, E.d_tok);
+        rowv[i] = win * E.nh * E.tok + (mm - win * E.tok);
+      } else {
+        rowv[i] = win_to_token32(mm, E.win);
+      }
+    }
+    mfma_chunk();   // (the fragments die here: the epilogue operands load after it, under the partner's work)
+    float4 ex[2][NP][2];
+    float rs[2] = {1.f, 1.f};
+    if constexpr (EX != EX_NONE) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const float* src = EX == EX_RESID ? E.resid + (long)rowv[i] * E.ldr : (const float*)E.gate + (long)rowv[i] * E.ldg;
+          ex[i][p][0] = *(const float4*)(src + c8[p]);
+          ex[i][p][1] = *(const float4*)(src + c8[p] + 4);
+        }
+      nvm += 4 * NP;
+    }
+    if constexpr (EX == EX_RESID) {
+      const bool hs = E.rowscale != nullptr;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int r = wm * 32 + i * 16 + fr;
-        const char* row = st + r * 128;
-        if constexpr (sizeof(TA) == 2) {
-          ah[i] = *(const f16x8*)(row + ((fq ^ (r & 7)) << 4));
-          al[i] = *(const f16x8*)(row + (((4 + fq) ^ (r & 7)) << 4));
+        const float r = *(hs ? E.rowscale + fdiv(rowv[i], E.d_rps) : (const float*)g_kair_zero_line);
+        rs[i] = hs ? r : 1.f;
+      }
+      nvm += 2;
+    }
+    const int nst = EM == XE_ROWS_F32 ? (E.pre ? 4 : 2) : (E.out_lo ? 2 : 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) nvm += __ballot(okm[i]) != 0 ? NP * nst : 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        float v[8];
+        const float4 b0 = *(const float4*)(sBias + c8[p] - n0), b1 = *(const float4*)(sBias + c8[p] - n0 + 4);
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][c]),
+                                                          __float_as_uint(acc[i][2 * p + 1][c]), false, false);
+          v[c] = __uint_as_float(r[0]) * E.acc_scale + bv[c];
+          v[4 + c] = __uint_as_float(r[1]) * E.acc_scale + bv[4 + c];
+        }
+        const int n = c8[p];
+        if constexpr (EM == XE_QKV) {
+          if (okm[i]) store8_f16pair(E.out, E.out_lo, colo[p] + (long)rowv[i] * E.hdp, v, E.oscale);
         } else {
-          const float4 x0 = *(const float4*)(row + (((2 * fq) ^ (r & 7)) << 4));
-          const float4 x1 = *(const float4*)(row + (((2 * fq + 1) ^ (r & 7)) << 4));
-          const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          float pre[8];
 #pragma unroll
           for (int c = 0; c < 8; ++c) {
-            const float w = xv[c] * as;
-            ah[i][c] = (f16)w;
-            al[i][c] = (f16)(w - (float)ah[i][c]);
+            pre[c] = v[c];
+            if constexpr (ACT == XA_GELU || ACT == XA_GELU_X) {
+              if constexpr (ACT == XA_GELU) pre[c] = gelu_erf_grad(v[c]);
+              v[c] = gelu_erf(v[c]);
+            } else if constexpr (ACT == XA_LEAKY) {
+              v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
+            }
           }
-        }
-      }
-#pragma unroll
-      for (int jn = 0; jn < 6; ++jn) {
-        const int n = wn * 96 + jn * 16 + fr;
-        const char* row = st + XR_ABYTES + n * 128;
-        bh[jn] = *(const f16x8*)(row + ((fq ^ (n & 7)) << 4));
-        bl[jn] = *(const f16x8*)(row + (((4 + fq) ^ (n & 7)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int jn = 0; jn < 6; ++jn) {
-          acc[i][jn] = mfma16(bh[jn], ah[i], acc[i][jn]);
-          acc[i][jn] = mfma16(bl[jn], ah[i], acc[i][jn]);
-          acc[i][jn] = mfma16(bh[jn], al[i], acc[i][jn]);
-        }
-    };
-    int sj = 0;
-    if (!tile_end) {
-      mfma_chunk();
-      stamp(j, 3);
-    } else {
-      // A tile's last chunk: its epilogue operands are loaded before the MFMAs (their latency overlaps them),
-      // unconditionally and in this one straight-line branch -- no control-flow merge between a load and its
-      // use, so hipcc never holds a pending epilogue load across the loop back-edge.
-      int rowv[2];
-      bool okm[2];
-      const int m0 = (mt0 + ct * mstride) * XR_BM + wm * 32 + fr;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int m = m0 + i * 16;
-        okm[i] = m < (int)E.M;
-        const int mm = okm[i] ? m : 0;
-        if constexpr (EM == XE_QKV) {
-          const int win = fdiv(mm, E.d_tok);
-          rowv[i] = win * E.nh * E.tok + (mm - win * E.tok);
-        } else {
-          rowv[i] = win_to_token32(mm, E.win);
-        }
-      }
-      float4 ex[2][3][2];
-      float rs[2] = {1.f, 1.f};
-      if constexpr (EX != EX_NONE) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            const float* src = EX == EX_RESID ? E.resid + (long)rowv[i] * E.ldr : (const float*)E.gate + (long)rowv[i] * E.ldg;
-            ex[i][p][0] = *(const float4*)(src + c8[p]);
-            ex[i][p][1] = *(const float4*)(src + c8[p] + 4);
-          }
-      }
-      if constexpr (EX == EX_RESID) {
-        const bool hs = E.rowscale != nullptr;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const float r = *(hs ? E.rowscale + fdiv(rowv[i], E.d_rps) : (const float*)g_kair_zero_line);
-          rs[i] = hs ? r : 1.f;
-        }
-      }
-      mfma_chunk();
-      stamp(j, 3);
-      // Epilogue from registers: fragment pairs re-laid by v_permlane16_swap give this lane columns
-      // [c8[p], c8[p] + 8) of rows m0 + {0, 16}.  sj counts the store instructions that MUST issue (rows with
-      // at least one valid lane in the wave); a compiler that also issues fully masked ones only makes the
-      // next chunk waits stricter.
-      const int nst = EM == XE_ROWS_F32 ? (E.pre ? 4 : 2) : (E.out_lo ? 2 : 1);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) sj += __ballot(okm[i]) != 0 ? 3 * nst : 0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          float v[8];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][c]),
-                                                            __float_as_uint(acc[i][2 * p + 1][c]), false, false);
-            v[c] = __uint_as_float(r[0]) * E.acc_scale + bias8[p][c];
-            v[4 + c] = __uint_as_float(r[1]) * E.acc_scale + bias8[p][4 + c];
-          }
-          const int n = c8[p];
-          if constexpr (EM == XE_QKV) {
-            if (okm[i]) store8_f16pair(E.out, E.out_lo, colo[p] + (long)rowv[i] * E.hdp, v, E.oscale);
-          } else {
-            float pre[8];
+          if constexpr (EX != EX_NONE) {
+            const float x8[8] = {ex[i][p][0].x, ex[i][p][0].y, ex[i][p][0].z, ex[i][p][0].w,
+                                 ex[i][p][1].x, ex[i][p][1].y, ex[i][p][1].z, ex[i][p][1].w};
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-              pre[c] = v[c];
-              if constexpr (GELU) {   // (the erf GELU only in its own instantiations: code size)
-                if (E.act == KAIR_ACT_GELU) {
-                  if (E.prek) pre[c] = gelu_erf_grad(v[c]);
-                  v[c] = gelu_erf(v[c]);
-                }
-              }
-              if (E.act == KAIR_ACT_LEAKY) v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
-              else if (E.act == KAIR_ACT_RELU) v[c] = fmaxf(v[c], 0.f);
+              if constexpr (EX == EX_RESID) v[c] = x8[c] + rs[i] * v[c];
+              else if constexpr (GK == XG_MUL) v[c] *= x8[c];
+              else v[c] *= (x8[c] > 0.f ? 1.f : E.slope);
             }
-            if constexpr (EX != EX_NONE) {
-              const float x8[8] = {ex[i][p][0].x, ex[i][p][0].y, ex[i][p][0].z, ex[i][p][0].w,
-                                   ex[i][p][1].x, ex[i][p][1].y, ex[i][p][1].z, ex[i][p][1].w};
+          }
 #pragma unroll
-              for (int c = 0; c < 8; ++c) {
-                if constexpr (EX == EX_RESID) v[c] = x8[c] + rs[i] * v[c];
-                else if (E.gkind == 4) v[c] *= x8[c];
-                else if (GELU && E.gkind == 1) v[c] *= gelu_erf_grad(x8[c]);
-                else if (E.gkind == 2) v[c] *= (x8[c] > 0.f ? 1.f : E.slope);
-                else v[c] *= (x8[c] > 0.f ? 1.f : 0.f);
-              }
+          for (int c = 0; c < 8; ++c) v[c] = c == oc[p] ? 1.f : v[c];   // the ones column (lane-varying select)
+          const long rr = rowv[i];
+          if (okm[i]) {
+            if constexpr (EM == XE_ROWS_PAIR) {
+              store8_f16pair(E.out, E.out_lo, rr * E.ldo + n, v, E.oscale);
+            } else {
+              float* d = (float*)E.out + rr * E.ldo + n;
+              *(float4*)d = make_float4(v[0], v[1], v[2], v[3]);
+              *(float4*)(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
             }
-            if (E.ones_col >= n && E.ones_col < n + 8) {
-#pragma unroll
-              for (int c = 0; c < 8; ++c)
-                if (n + c == E.ones_col) v[c] = 1.f;
-            }
-            const long rr = rowv[i];
-            if (okm[i]) {
-              if constexpr (EM == XE_ROWS_PAIR) {
-                store8_f16pair(E.out, E.out_lo, rr * E.ldo + n, v, E.oscale);
-              } else {
-                float* d = (float*)E.out + rr * E.ldo + n;
-                *(float4*)d = make_float4(v[0], v[1], v[2], v[3]);
-                *(float4*)(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
-              }
-              if (E.pre) {
-                float* d = (float*)E.pre + rr * E.ldp + n;
-                *(float4*)d = make_float4(pre[0], pre[1], pre[2], pre[3]);
-                *(float4*)(d + 4) = make_float4(pre[4], pre[5], pre[6], pre[7]);
-              }
+            if (E.pre) {
+              float* d = (float*)E.pre + rr * E.ldp + n;
+              *(float4*)d = make_float4(pre[0], pre[1], pre[2], pre[3]);
+              *(float4*)(d + 4) = make_float4(pre[4], pre[5], pre[6], pre[7]);
             }
           }
         }
+      }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int jn = 0; jn < 6; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    return nvm;
+  };
+
+  const bool stamping = KAIR_DBG(E.dbg & 8) && blockIdx.x < XS_CTAS;
+  unsigned long long* stp = g_x3_stamps + ((long)blockIdx.x * 8 + wave) * XS_IT * XS_N;
+  auto stamp = [&](int t, int k) __attribute__((always_inline)) {
+    if (stamping && t < XS_IT) {
+      const unsigned long long tt = x3_now();
+      if (lane == 0) stp[t * XS_N + k] = tt;
     }
-    stamp(j, 4);
-    sq3 = sq2; sq2 = sq1; sq1 = sj;
-    if (++kc == nk) { kc = 0; ++ct; }
-    if (++cs == XR_NS) cs = 0;
-  }
+  };
+  // The interval loop, specialised per group (a run-time group test would keep every register of both roles
+  // live across the loop).  Consumer state: the chunk this wave multiplies next (k-chunk kc of tile ct) and the
+  // stages of the chunk whose fragments it reads next.  Both loops pass the same barriers (one per interval).
+  auto run = [&](auto G) __attribute__((always_inline)) {
+    constexpr int g = decltype(G)::value;
+    int kc = 0, ct = 0, ra = 0, rb = 0;
+    int e1 = 0, e2 = 0;   // non-DMA vector-memory instructions this wave issued in intervals t-1, t-2
+    for (int t = 0; t <= total; ++t) {
+      stamp(t, 0);
+      if (t < total) vm_wait(e2 + nA(t - 1) + nB(t - 1) + e1);   // chunk t (its B part: issued in interval t-2)
+      stamp(t, 1);
+      ring_barrier();   // chunk t is in LDS for every wave; chunk t-1's stages are free
+      if (nA(t)) issue_a();
+      if (nB(t)) issue_b();
+      stamp(t, 2);
+      int e0 = 0;
+      if constexpr (g == 0) {   // read chunk t, multiply it
+        if (t < total) {
+          load_frags(ra, rb);
+          stamp(t, 3);
+          e0 = compute(kc == nk - 1, ct);
+          if (++kc == nk) { kc = 0; ++ct; }
+        }
+      } else {                  // multiply chunk t-1, read chunk t
+        if (t >= 1) {
+          e0 = compute(kc == nk - 1, ct);
+          if (++kc == nk) { kc = 0; ++ct; }
+        }
+        stamp(t, 3);
+        if (t < total) load_frags(ra, rb);
+      }
+      if (t < total) {
+        if (++ra == NA) ra = 0;
+        if (++rb == XR_NB) rb = 0;
+      }
+      stamp(t, 4);
+      e2 = e1;
+      e1 = e0;
+    }
+  };
+  if (grp == 0) run(std::integral_constant<int, 0>{});
+  else run(std::integral_constant<int, 1>{});
 }
 
 // ------------------------------------------------------------------------------------------
@@ -863,15 +919,21 @@ int tn_x3_b(const Op& a, const Op& b, int bmode, int bdt, float* ws, int splits,
                          : launch_tn_x3<TA, float, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, acc_scale, s);
 }
 
+// the ring's N-tile for N columns (0: none): 192 for multiples of 192, else one tile of 64 / 128
+int nt_x3_ring_bn(int N) {
+  if (N % 192 == 0) return 192;
+  return N == 64 || N == 128 ? N : 0;
+}
+
 // the ring takes N-tiles of 192 columns, 32-deep k-chunks (im2col: one tap per chunk) and 16-byte aligned rows
 bool nt_x3_ring_ok(const kair_operand* A, const kair_operand* B, const kair_epilogue* E, int N, int K) {
   static const int off = [] { const char* e = getenv("KAIR_X3_RING"); return e && e[0] == '0'; }();
-  if (off || N % XR_BN != 0 || K % 32 != 0 || (uintptr_t)B->ptr % 16 != 0 || (uintptr_t)A->ptr % 16 != 0) return false;
+  if (off || nt_x3_ring_bn(N) == 0 || K % 32 != 0 || (uintptr_t)B->ptr % 16 != 0 || (uintptr_t)A->ptr % 16 != 0) return false;
   // epilogues: fp32 rows (bias, activation [+ pre], residual [x row scale] or fp32 gate, ones column) or fp16
   // pair rows / head-blocked q, k, v (bias); 16-byte aligned rows throughout
   const bool pair = E->out_dtype == KAIR_F16;
   if (E->out_mode == KAIR_OUT_QKVBLK) {
-    if (!pair || E->qkv_hdp % 8 || (uintptr_t)E->out % 16 || E->act || E->out_pre || E->resid || E->gate || E->rowscale) return false;
+    if (nt_x3_ring_bn(N) != 192 || !pair || E->qkv_hdp % 8 || (uintptr_t)E->out % 16 || E->act || E->out_pre || E->resid || E->gate || E->rowscale) return false;
   } else {
     if (E->out_mode != KAIR_OUT_ROWS || E->ldo % 4 || (uintptr_t)E->out % 16) return false;
     if (E->resid2 || E->a_copy || (E->resid && E->gate)) return false;
@@ -880,37 +942,55 @@ bool nt_x3_ring_ok(const kair_operand* A, const kair_operand* B, const kair_epil
     if (E->resid && (E->ldr % 4 || (uintptr_t)E->resid % 16)) return false;
     if (E->gate && (E->gate_dtype != KAIR_F32 || E->ldg % 4 || (uintptr_t)E->gate % 16)) return false;
     if (E->rowscale && !E->resid) return false;
-    if (E->act == KAIR_ACT_GELU && (E->resid || E->gate)) return false;   // no such instantiation
+    // the instantiated forms: activation (GELU / LeakyReLU) only without residual / gate; gates 4 (multiply) and 2
+    if (E->act && (E->resid || E->gate || (E->act != KAIR_ACT_GELU && E->act != KAIR_ACT_LEAKY))) return false;
+    if (E->gate && E->gate_kind != XG_MUL && E->gate_kind != XG_LEAKY) return false;
+    if (nt_x3_ring_bn(N) != 192 &&   // the 64 / 128 / 256-column tiles carry the tail's forms only
+        (pair || E->resid || E->out_pre || (E->gate && E->gate_kind != XG_LEAKY) || (E->act && E->act != KAIR_ACT_LEAKY)))
+      return false;
   }
   if (A->mode == KAIR_LD_ROWS) return A->dtype == KAIR_F16 ? A->ld % 8 == 0 : A->ld % 4 == 0;
   return A->mode == KAIR_LD_IM2COL3 && A->dtype == KAIR_F32 && A->im_C % 32 == 0 && (A->ld == 0 ? A->im_C : A->ld) % 4 == 0;
 }
 
-template <typename TA, int AM>
+template <typename TA, int AM, int BN>
 int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int K, hipStream_t s) {
-  const int tilesN = N / XR_BN;
+  const int tilesN = N / BN;
   const int tilesM = (int)((M + XR_BM - 1) / XR_BM);
   int per = x3_cus() / tilesN;
   if (per < 1) per = 1;
   const int rounds = (tilesM + per - 1) / per;
   per = (tilesM + rounds - 1) / rounds;   // the same makespan on as few CUs as it needs
   const dim3 g(per * tilesN), bl(512);
-  if (e.omode == KAIR_OUT_QKVBLK)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_QKV, EX_NONE, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
-  else if (e.odt == KAIR_F16)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_PAIR, EX_NONE, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
-  else if (e.resid)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_RESID, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
-  else if (e.gate && e.gkind == 1)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_GATE_F32, true>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
-  else if (e.gate)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_GATE_F32, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
-  else if (e.act == KAIR_ACT_GELU)
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_NONE, true>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
-  else
-    hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, XE_ROWS_F32, EX_NONE, false>), g, bl, 0, s, a, b, e, K, tilesN, tilesM);
+#define XR_LAUNCH(EM, EX, ACT, GK) \
+  hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN>), g, bl, 0, s, a, b, e, K, tilesN, tilesM)
+  if constexpr (BN == 192) {   // the Swin linears and the 192-channel convs: every epilogue form
+    if (e.omode == KAIR_OUT_QKVBLK) XR_LAUNCH(XE_QKV, EX_NONE, XA_NONE, 0);
+    else if (e.odt == KAIR_F16) XR_LAUNCH(XE_ROWS_PAIR, EX_NONE, XA_NONE, 0);
+    else if (e.resid) XR_LAUNCH(XE_ROWS_F32, EX_RESID, XA_NONE, 0);
+    else if (e.gate && e.gkind == XG_MUL) XR_LAUNCH(XE_ROWS_F32, EX_GATE_F32, XA_NONE, XG_MUL);
+    else if (e.gate) XR_LAUNCH(XE_ROWS_F32, EX_GATE_F32, XA_NONE, XG_LEAKY);
+    else if (e.act == KAIR_ACT_GELU && e.prek) XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_GELU, 0);
+    else if (e.act == KAIR_ACT_GELU) XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_GELU_X, 0);
+    else if (e.act == KAIR_ACT_LEAKY) XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_LEAKY, 0);
+    else XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_NONE, 0);
+  } else {   // the reconstruction tail's narrow / wide convs: fp32 rows, LeakyReLU or its gate (nt_x3_ring_ok)
+    if (e.gate) XR_LAUNCH(XE_ROWS_F32, EX_GATE_F32, XA_NONE, XG_LEAKY);
+    else if (e.act == KAIR_ACT_LEAKY) XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_LEAKY, 0);
+    else XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_NONE, 0);
+  }
+#undef XR_LAUNCH
   KAIR_CHECK_LAUNCH();
   return 0;
+}
+
+template <typename TA, int AM>
+int nt_x3_ring_dispatch(const Op& a, const Op& b, const Epi& e, long M, int N, int K, hipStream_t s) {
+  switch (nt_x3_ring_bn(N)) {
+    case 64: return launch_nt_x3_ring<TA, AM, 64>(a, b, e, M, N, K, s);
+    case 128: return launch_nt_x3_ring<TA, AM, 128>(a, b, e, M, N, K, s);
+    default: return launch_nt_x3_ring<TA, AM, 192>(a, b, e, M, N, K, s);
+  }
 }
 
 // the TN ring: fp32 rows (16-byte aligned, N and K % 4), B rows or the tap-per-tile im2col of a 192-channel
@@ -977,9 +1057,9 @@ int kair_gemm_nt_x3(const kair_operand* A, const kair_operand* B, const kair_epi
   e.acc_scale = ldexpf(1.f, -(A->x3_exp + B->x3_exp));
   hipStream_t s = (hipStream_t)stream;
   if (nt_x3_ring_ok(A, B, E, N, K)) {
-    if (A->mode == KAIR_LD_IM2COL3) return launch_nt_x3_ring<float, AM_IM2COL>(a, b, e, M, N, K, s);
-    return A->dtype == KAIR_F16 ? launch_nt_x3_ring<f16, AM_ROWS>(a, b, e, M, N, K, s)
-                                : launch_nt_x3_ring<float, AM_ROWS>(a, b, e, M, N, K, s);
+    if (A->mode == KAIR_LD_IM2COL3) return nt_x3_ring_dispatch<float, AM_IM2COL>(a, b, e, M, N, K, s);
+    return A->dtype == KAIR_F16 ? nt_x3_ring_dispatch<f16, AM_ROWS>(a, b, e, M, N, K, s)
+                                : nt_x3_ring_dispatch<float, AM_ROWS>(a, b, e, M, N, K, s);
   }
   if (A->dtype == KAIR_F16)
     return A->mode == KAIR_LD_ROWS ? nt_x3_tiles<f16, AM_ROWS>(a, b, e, M, N, K, s) : nt_x3_tiles<f16, AM_IM2COL>(a, b, e, M, N, K, s);

@@ -211,6 +211,21 @@ def test_gemm_nt_x3_ring_epilogues():
     cols = cols.view(Bn, C, 9, Hh * Ww).permute(0, 3, 2, 1).reshape(M, 9, C).flip(1).reshape(M, K)
     torch.cuda.synchronize()
     assert rel(out, (cols @ w.double().T) * gt.double()) < 2e-6
+    # (d) the tail's tile widths: 64 columns with LeakyReLU (conv_before_upsample), 256 plain (the x4 upsampling convs)
+    for N, leaky in ((64, True), (256, False)):
+        M, K = 700, 576
+        x, w, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05, torch.randn(N, generator=g)
+        Wo, keep = _wsplit(w)
+        A = H.rows(x.to(dev))
+        A.x3_exp = 4
+        out = torch.empty(M, N, device=dev)
+        kw = dict(act=H.ACT_LEAKY, slope=0.01) if leaky else {}
+        H.gemm_nt(A, Wo, H.epilogue(out, bias=b.to(dev), **kw), M, N, K, H.X3)
+        ref = x.double() @ w.double().T + b.double()
+        if leaky:
+            ref = torch.where(ref > 0, ref, 0.01 * ref)
+        torch.cuda.synchronize()
+        assert rel(out, ref) < 2e-6, N
 
 
 @pytest.mark.parametrize("conv", [False, True])

@@ -92,6 +92,30 @@ def nt_conv():
     return run, 2.0 * 3 * M * 192 * 1728, 4 * M * 192 * 2
 
 
+def attn_case(bwd):
+    """The split window attention at C4's block shape: 1152 windows x 6 heads (head dim 30), shift 4."""
+    nWin, nh, hd = M // 64, 6, 30
+    qkv = pair(torch.randn(3 * M * nh * 32, device=dev), 4)
+    table = torch.randn(225, nh, device=dev) * 0.5
+    O = torch.empty(M, nh * 32, device=dev)
+    lse = torch.empty(nWin * nh * 64, device=dev)
+    H.window_attn_fwd_x3(qkv, table, O, nh * 32, lse, nWin, nh, hd, hd ** -0.5, 48, 48, 4, ones_col=hd, e_in=4, e_out=4)
+    dO = pair(torch.randn(M, nh * 32, device=dev) * 1e-6, 24)
+    dqkv = torch.empty(M, 3 * nh * 32, device=dev)
+    ws = torch.empty(H.window_attn_bwd_ws(nWin, nh), device=dev)
+
+    def run():
+        if bwd:
+            H.window_attn_bwd_x3(qkv, O, nh * 32, dO, nh * 32, table, lse, dqkv, None, False, ws, nWin, nh, hd, hd ** -0.5,
+                                 48, 48, 4, e_act=4, e_grad=24)
+        else:
+            H.window_attn_fwd_x3(qkv, table, O, nh * 32, lse, nWin, nh, hd, hd ** -0.5, 48, 48, 4, ones_col=hd, e_in=4,
+                                 e_out=4)
+    fl = nWin * nh * (5 if bwd else 2) * 2 * 64 * 64 * hd
+    nb = M * nh * ((8 if bwd else 4) * hd * 4 + 4)
+    return run, 3.0 * fl, nb
+
+
 def cases():
     return {
         "nt_qkv_fwd": nt_case(576, 192, False, True, None),
@@ -110,6 +134,8 @@ def cases():
         "tn_proj_f32": tn_case(192, 192, False, False),
         "nt_conv_fwd": nt_conv(),
         "tn_conv_tap": tn_case(192, 1728, False, False, conv=True),
+        "attn_fwd": attn_case(False),
+        "attn_bwd": attn_case(True),
     }
 
 
