@@ -401,8 +401,11 @@ class SwinIREngine:
         self._dtab_pending = []   # (partials, nWin, nh, dtype, dtable, accumulate) of its attention blocks
         self._conv_pending = []   # the RSTB conv's weight gradient (_wgrad arguments)
         self._side = None         # side stream of the deferred per-RSTB gradient work
-        # side_stream=False: the deferred per-RSTB work runs in place on the main stream (A/B timing)
-        self.side_stream = self.grouped_wgrad and torch.cuda.is_available() and bool(side_stream)
+        # side_stream=False: the deferred per-RSTB work runs in place on the main stream (A/B timing).  fp32x3
+        # defers its block weight gradients (one TN ring + finalize each) the same way: they fill the CUs the
+        # data-gradient chain's 192-column ring GEMMs leave idle (576 tiles: 3 rounds on 192 CUs)
+        self.x3_side = self.x3 and self.Hdp <= 576
+        self.side_stream = (self.grouped_wgrad or self.x3_side) and torch.cuda.is_available() and bool(side_stream)
         self.side_priority = side_priority   # torch stream priority of the side stream (0: default)
         # workgroup budget of the side-stream launches (0: uncapped).  The weight-gradient kernels hold one
         # 512-thread workgroup per CU; spread over the chip they keep the next RSTB's data-gradient kernels
@@ -609,7 +612,8 @@ class SwinIREngine:
                     P["conv_bf"][id(r)][1][:, self.C] = 1.0
         # one shared wgrad workspace sized for the largest (splits * N * K)
         P["wg_ws"] = e(self._max_wgrad_ws(M, P))
-        P["wg_ws2"] = e(P["wg_ws"].numel() * max(1, -self.side_ctas)) if self.grouped_wgrad else None   # the side stream's
+        P["wg_ws2"] = (e(P["wg_ws"].numel() * max(1, -self.side_ctas)) if self.grouped_wgrad or self.side_stream
+                       else None)   # the side stream's
         return P
 
     def _wgrad_shapes(self, M, P):
@@ -1145,7 +1149,7 @@ class SwinIREngine:
     def _wg(self, P, A, Bop, N, K, lin, grads, ones_col):
         """One block linear's weight gradient: queued for the RSTB's grouped launch, or issued now."""
         g_w, g_b = grads[lin.w], grads[lin.b]
-        if self.grouped_wgrad:
+        if self.grouped_wgrad or (self.x3_side and self.side_stream):
             self._wg_pending.append((A, Bop, N, K, lin.map, g_w, g_b, ones_col))
         else:
             self._wgrad(P, A, Bop, P["M"], N, K, lin.map, g_w, g_b, ones_col)
@@ -1164,8 +1168,12 @@ class SwinIREngine:
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             if self._wg_pending:
                 jobs, self._wg_pending = self._wg_pending, []
-                for i in range(0, len(jobs), H.WgradGroup.WG_MAX):
-                    H.WgradGroup(jobs[i:i + H.WgradGroup.WG_MAX], P["M"]).run(ws, max_ctas=cap)
+                if self.x3:   # one split-fp16 TN ring + finalize per linear, in queue order
+                    for A, Bop, N, K, m, g_w, g_b, oc in jobs:
+                        self._wgrad(P, A, Bop, P["M"], N, K, m, g_w, g_b, oc, ws=ws, max_ctas=cap)
+                else:
+                    for i in range(0, len(jobs), H.WgradGroup.WG_MAX):
+                        H.WgradGroup(jobs[i:i + H.WgradGroup.WG_MAX], P["M"]).run(ws, max_ctas=cap)
             # grouped launches take at most 32 jobs each (LNP_MAX / DTAB_MAX): deep RSTBs run in chunks
             if self._lnp_pending:
                 jobs, self._lnp_pending = self._lnp_pending, []
