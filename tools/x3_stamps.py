@@ -26,21 +26,19 @@ def main():
     st = H.debug_x3_stamps().astype(np.int64).reshape(4, 8, 64, 5)
     print(name)
     for c in range(4):
-        s = st[c]
-        ok = (s[:, :, 0] > 0).all(axis=0)
-        n = int(ok.sum())
-        if n < 2:
-            continue
-        s = s[:, :n]
-        d = np.diff(s, axis=2).mean(axis=(0, 1))
-        it = np.diff(s[:, :, 0], axis=1).mean()
-        spread = (s[:, :, 0].max(axis=0) - s[:, :, 0].min(axis=0)).mean()
-        print(f"CTA {c}: {n} iterations, {it:7.0f} cycles/iteration; wait {d[0]:6.0f}  barrier+issue {d[1]:6.0f}  "
-              f"mfma {d[2]:6.0f}  epilogue {d[3]:6.0f}; wave skew at loop top {spread:6.0f}")
-        ep = s[:, :, 4] - s[:, :, 3]
-        big = np.argsort(-ep.mean(axis=0))[:3]
-        print("   longest epilogue iterations:", [(int(i), int(ep[:, i].mean())) for i in big],
-              " wait per iteration (wave 0):", (s[0, :16, 1] - s[0, :16, 0]).tolist())
+        for g, (p1, p2) in enumerate((("frags", "mfma+epi"), ("mfma+epi", "frags"))):
+            s = st[c, 4 * g:4 * g + 4]
+            ok = (s > 0).all(axis=(0, 2))   # intervals every wave of the group stamped at every point
+            idx = np.nonzero(ok)[0]
+            if len(idx) < 3:
+                continue
+            s = s[:, idx]
+            d = np.diff(s, axis=2).mean(axis=(0, 1))
+            it = np.diff(s[:, :, 0], axis=1).mean()
+            skew = (st[c, :, idx, 0].max(axis=1) - st[c, :, idx, 0].min(axis=1)).mean()
+            ph2 = s[:, :, 4] - s[:, :, 3]
+            print(f"CTA {c} group {g}: {len(idx)} intervals, {it:6.0f} cycles/interval; wait {d[0]:5.0f}  barrier+DMA "
+                  f"{d[1]:5.0f}  {p1} {d[2]:5.0f}  {p2} {d[3]:5.0f}  (max {ph2.mean(axis=0).max():5.0f}); skew {skew:5.0f}")
 
 
 if __name__ == "__main__":
