@@ -150,7 +150,8 @@ _TIMED = ("gemm_nt", "gemm_tn", "wgrad_finalize", "colsum", "layernorm_fwd", "la
           "window_attn_fwd_x3", "window_attn_bwd_x3",
           "window_attn_bwd", "ln_param_reduce_grouped", "attn_dtable_grouped", "image_to_nhwc", "l1_loss", "axpy",
           "swin_attn_fwd", "swin_mlp_fwd", "rowgemm_store", "rowgemm_gate", "rowgemm_lnbwd", "image_to_nhwc_hilo",
-          "conv3x3_narrow_fwd", "conv3x3_narrow_dgrad", "conv3x3_narrow_wgrad", "conv3x3_wr")
+          "conv3x3_narrow_fwd", "conv3x3_narrow_dgrad", "conv3x3_narrow_wgrad", "conv3x3_wr",
+          "conv3x3_narrow_fwd_x3", "conv3x3_narrow_dgrad_x3", "conv3x3_narrow_wgrad_x3")
 
 
 def time_roles(tr, serial=False):

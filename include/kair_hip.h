@@ -434,6 +434,22 @@ long kair_conv3x3_narrow_wgrad_ws(int NR);
 int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x, long ldx, int NR, float* ws, float* grad_w,
                               float* grad_b, int accumulate, int B, int H, int W, void* stream);
 
+/* fp32x3 forms of the three narrow convs (the fp32 engine's arithmetic, KAIR_COMPUTE_X3): fp32 operands, each
+ * staged into LDS as the fp16 pair of v 2^e and multiplied hi.hi + lo.hi + hi.lo (fp32 accumulation).  x: fp32
+ * rows [B*H*W][ldx], channels [0, 64), exponent ex; dE: fp32 rows [B*H*W][lde] (channels [0, 4) read, the
+ * weights zero for n >= NR), exponent eg; w: the fp32 conv weight [NR][64][3][3] (split as w 2^KAIR_X3_WEXP
+ * into ws, kair_conv3x3_narrow_x3_ws() floats, by the fwd / dgrad call itself; one ws per concurrent call).
+ * Outputs as the bf16 forms: fwd the NCHW image, dgrad fp32 rows or the PixelUnshuffle(ps_r) sub-pixel-major
+ * layout, wgrad grad_w / grad_b from per-workgroup partials in ws (kair_conv3x3_narrow_wgrad_ws(NR) floats). */
+long kair_conv3x3_narrow_x3_ws(void);
+int kair_conv3x3_narrow_fwd_x3(const float* x, long ldx, int ex, const float* w, const float* bias, int NR, void* ws,
+                               const float* mean, float img_range, const float* resid, float* out, int B, int H, int W,
+                               void* stream);
+int kair_conv3x3_narrow_dgrad_x3(const float* dE, long lde, int eg, const float* w, int NR, void* ws, float* out, long ldo,
+                                 int ps_r, int B, int H, int W, void* stream);
+int kair_conv3x3_narrow_wgrad_x3(const float* dE, long lde, int eg, const float* x, long ldx, int ex, int NR, float* ws,
+                                 float* grad_w, float* grad_b, int accumulate, int B, int H, int W, void* stream);
+
 /* Elementwise / small kernels ------------------------------------------------------------- */
 /* NCHW fp32 image -> NHWC (dtype) with channel stride ldc, x' = (x - mean[c]) * img_range
  * (network_swinir.py:809-810); mean may be NULL.  Pad channels written 0. */

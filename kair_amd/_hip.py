@@ -141,6 +141,13 @@ _SIGS = {
     "kair_conv3x3_narrow_dgrad": [c_vp, c_long, c_vp, c_int, c_vp, c_vp, c_int, c_long, c_int, c_int, c_int, c_int, c_vp],
     "kair_conv3x3_narrow_wgrad_ws": [c_int],
     "kair_conv3x3_narrow_wgrad": [c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "kair_conv3x3_narrow_x3_ws": [],
+    "kair_conv3x3_narrow_fwd_x3": [c_vp, c_long, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_float, c_vp, c_vp, c_int, c_int,
+                                   c_int, c_vp],
+    "kair_conv3x3_narrow_dgrad_x3": [c_vp, c_long, c_int, c_vp, c_int, c_vp, c_vp, c_long, c_int, c_int, c_int, c_int,
+                                     c_vp],
+    "kair_conv3x3_narrow_wgrad_x3": [c_vp, c_long, c_int, c_vp, c_long, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int,
+                                     c_int, c_int, c_vp],
     "kair_l1_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "kair_charbonnier_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_float, c_int, c_int, c_int, c_int,
                               c_vp, c_vp],
@@ -197,7 +204,7 @@ _SIGS = {
 }
 _RESTYPE = {"kair_layernorm_bwd_blocks": c_long, "kair_rowgemm_ln_blocks": c_long, "kair_window_attn_bwd_groups": c_long, "kair_wgrad_grouped_ws": c_long, "kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
             "kair_pack_table_build": c_long, "kair_conv3x3_narrow_wgrad_ws": c_long,
-            "kair_conv3x3_narrow_dgrad_ws": c_long}
+            "kair_conv3x3_narrow_dgrad_ws": c_long, "kair_conv3x3_narrow_x3_ws": c_long}
 
 _lib = None
 
@@ -633,6 +640,26 @@ def conv3x3_narrow_wgrad_ws(NR):
 def conv3x3_narrow_wgrad(dE, lde, x, ldx, NR, ws, grad_w, grad_b, B, H, W, accumulate=False):
     check(lib().kair_conv3x3_narrow_wgrad(ptr(dE), lde, ptr(x), ldx, NR, ptr(ws), ptr(grad_w), ptr(grad_b),
                                           int(accumulate), B, H, W, stream_ptr()), "conv3x3_narrow_wgrad")
+
+
+def conv3x3_narrow_x3_ws():
+    return lib().kair_conv3x3_narrow_x3_ws()
+
+
+def conv3x3_narrow_fwd_x3(x, ldx, ex, w, bias, NR, ws, mean, img_range, resid, out, B, H, W):
+    """conv_last forward at the fp32 engine's arithmetic: 64-channel fp32 rows -> NCHW image (csrc/tail.hip)."""
+    check(lib().kair_conv3x3_narrow_fwd_x3(ptr(x), ldx, ex, ptr(w), ptr(bias), NR, ptr(ws), ptr(mean), img_range, ptr(resid),
+                                           ptr(out), B, H, W, stream_ptr()), "conv3x3_narrow_fwd_x3")
+
+
+def conv3x3_narrow_dgrad_x3(dE, lde, eg, w, NR, ws, out, ldo, ps_r, B, H, W):
+    check(lib().kair_conv3x3_narrow_dgrad_x3(ptr(dE), lde, eg, ptr(w), NR, ptr(ws), ptr(out), ldo, ps_r, B, H, W,
+                                             stream_ptr()), "conv3x3_narrow_dgrad_x3")
+
+
+def conv3x3_narrow_wgrad_x3(dE, lde, eg, x, ldx, ex, NR, ws, grad_w, grad_b, B, H, W, accumulate=False):
+    check(lib().kair_conv3x3_narrow_wgrad_x3(ptr(dE), lde, eg, ptr(x), ldx, ex, NR, ptr(ws), ptr(grad_w), ptr(grad_b),
+                                             int(accumulate), B, H, W, stream_ptr()), "conv3x3_narrow_wgrad_x3")
 
 
 def image_to_nhwc_hilo(img, out, ldc, mean, img_range, B, C, H, W):

@@ -453,6 +453,403 @@ int grid_rows(long total, int per_cu) {
   return (int)(total < g ? total : g);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// fp32x3 forms (the fp32 engine's arithmetic, gemm_x3.hip): fp32 operands, each staged into LDS as the fp16
+// pair of v 2^e (hi = f16(v 2^e), lo = f16(v 2^e - hi)), every product hi.hi + lo.hi + hi.lo on
+// v_mfma_f32_16x16x32_f16, fp32 accumulation rescaled by 2^-(eA + eB).  Same row windows, fragment orders
+// and MFMA shapes as the bf16 kernels above; the weights come from the fp32 master weight [NR][64][3][3]
+// (x 2^KAIR_X3_WEXP) through a pack launch into ws.
+// ---------------------------------------------------------------------------------------------------
+KAIR_DEV void split4(const float4 v, float s, f16x4& h, f16x4& l) {
+  const float a[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = (f16)a[j];
+    l[j] = (f16)(a[j] - (float)h[j]);
+  }
+}
+
+KAIR_DEV f16x8 cat8(const f16x4& a, const f16x4& b) { return f16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}; }
+
+// 8 consecutive rows (pixels) of one column of a 16-bit LDS plane: two ds_read_b64_tr_b16, the second at + d
+KAIR_DEV f16x8 tr8(const f16* p, int d) {
+  typedef __attribute__((address_space(3))) short4v* lp;
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)p), hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p + d));
+  short __attribute__((ext_vector_type(8))) s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(f16x8, s8);
+}
+
+KAIR_DEV f32x4 mfma_h(const f16x8& a, const f16x8& b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+
+// fp16 pair of w 2^KAIR_X3_WEXP
+KAIR_DEV f16 wsplit(float w, int half) {
+  const float v = ldexpf(w, KAIR_X3_WEXP);
+  const f16 h = (f16)v;
+  return half ? (f16)(v - (float)h) : h;
+}
+
+// forward fragments [18 kb][hi, lo][64][8]: A row n = lane % 16, k = 8 (lane / 16) + j of k-step kb
+// (tap = kb / 2, channel 32 (kb % 2) + k) -- the kind-15 order
+__global__ void narrow_fwd_x3_pack_kernel(const float* __restrict__ w, int NR, f16* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 18 * 2 * 64 * 8) return;
+  const int j = t & 7, ln = (t >> 3) & 63, half = (t >> 9) & 1, kb = t >> 10;
+  const int n = ln & 15, c = 32 * (kb & 1) + 8 * (ln >> 4) + j, tap = kb >> 1;
+  out[t] = wsplit(n < NR ? w[((long)n * NF + c) * 9 + tap] : 0.f, half);
+}
+
+// input-gradient fragments [4 cb][2 ks][hi, lo][64][8]: row c = 16 cb + lane % 16, k = tap * 4 + n
+__global__ void narrow_dgrad_x3_pack_kernel(const float* __restrict__ w, int NR, f16* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 4 * 2 * 2 * 64 * 8) return;
+  const int j = t & 7, ln = (t >> 3) & 63, half = (t >> 9) & 1, ks = (t >> 10) & 1, cb = t >> 11;
+  const int c = 16 * cb + (ln & 15), k = 32 * ks + 8 * (ln >> 4) + j;
+  const int tap = k >> 2, n = k & 3;
+  out[t] = wsplit(tap < 9 && n < NR ? w[((long)n * NF + c) * 9 + tap] : 0.f, half);
+}
+
+struct NarrowFwdX3Args {
+  const float* x; long ldx;             // [B*H*W][ldx] fp32, channels [0, 64)
+  const f16* w;                         // narrow_fwd_x3_pack_kernel fragments
+  const float* bias; const float* mean; float range; int NR;
+  const float* resid; float* out;       // as NarrowFwdArgs
+  int B, H, W;
+  float sx, oscale;                     // 2^ex, 2^-(ex + KAIR_X3_WEXP)
+};
+
+// the staged row as kair_conv3x3_narrow_fwd's pair layout (FPST halves per pixel: hi [0, 64), lo [64, 128));
+// a 16-byte chunk c of the fp32 row is pixel c / 16, channels 4 (c % 16) .. + 3
+__global__ __launch_bounds__(256, 2) void conv3x3_narrow_fwd_x3_kernel(const NarrowFwdX3Args a) {
+  constexpr int KS = 9 * NF / 32;
+  __shared__ __attribute__((aligned(16))) f16 sRow[4 * FROW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  f16x8 wh[KS], wl[KS];
+#pragma unroll
+  for (int kb = 0; kb < KS; ++kb) {
+    wh[kb] = *(const f16x8*)(a.w + ((long)kb * 2 + 0) * 512 + lane * 8);
+    wl[kb] = *(const f16x8*)(a.w + ((long)kb * 2 + 1) * 512 + lane * 8);
+  }
+  float bias4[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) bias4[n] = n < a.NR ? a.bias[n] : 0.f;
+  const int nseg = a.W / SEG;
+  const long total = (long)a.B * nseg * a.H;
+  const RowRun run = row_run(total, gridDim.x, blockIdx.x);
+  float4 pre[FPER];
+  auto load_row = [&](long st, int yy) {
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+#pragma unroll
+    for (int i = 0; i < FPER; ++i) {
+      const int c = tid + 256 * i;
+      const int xx = x0 - 1 + (c >> 4);
+      const bool ok = c < FCH && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+      pre[i] = *(const float4*)(a.x + (ok ? ((long)(b * a.H + yy) * a.W + xx) * a.ldx + (c & 15) * 4 : 0));
+      if (!ok) pre[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_row = [&](int yy) {
+    f16* dst = sRow + (yy & 3) * FROW;
+#pragma unroll
+    for (int i = 0; i < FPER; ++i) {
+      const int c = tid + 256 * i;
+      if (c < FCH) {
+        f16x4 h, l;
+        split4(pre[i], a.sx, h, l);
+        f16* p = dst + (c >> 4) * FPST + (c & 15) * 4;
+        *(f16x4*)p = h;
+        *(f16x4*)(p + NF) = l;
+      }
+    }
+  };
+  const int pl = lane & 15, cq = 8 * (lane >> 4);
+  long cur_strip = -1;
+  for (long g = run.g0; g < run.g1; ++g) {
+    const long st = g / a.H;
+    const int y = (int)(g - st * a.H);
+    if (st != cur_strip) {
+      __syncthreads();
+      for (int d = -1; d <= 1; ++d) {
+        load_row(st, y + d);
+        store_row(y + d + 4);
+      }
+      cur_strip = st;
+      __syncthreads();
+    }
+    const bool more = g + 1 < run.g1 && (g + 1) / a.H == st;
+    if (more) load_row(st, y + 2);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = acc, acc2 = acc;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      const f16* src = sRow + ((y + dy + 4) & 3) * FROW + (1 + 16 * wave + pl + dx) * FPST + cq;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const f16x8 xh = *(const f16x8*)(src + 32 * ks), xl = *(const f16x8*)(src + NF + 32 * ks);
+        const int kb = tap * 2 + ks;
+        acc = mfma_h(wh[kb], xh, acc);
+        acc1 = mfma_h(wl[kb], xh, acc1);
+        acc2 = mfma_h(wh[kb], xl, acc2);
+      }
+    }
+    acc += acc1 + acc2;
+    if (lane < 16) {
+      const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+      const long HW = (long)a.H * a.W;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        if (n < a.NR) {
+          const long o = ((long)b * a.NR + n) * HW + (long)y * a.W + x0 + 16 * wave + pl;
+          float v = (acc[n] * a.oscale + bias4[n]) / a.range + (a.mean ? a.mean[n] : 0.f);
+          if (a.resid) v += a.resid[o];
+          a.out[o] = v;
+        }
+      }
+    }
+    __syncthreads();
+    if (more) store_row(y + 2);
+    __syncthreads();
+  }
+}
+
+struct NarrowDgradX3Args {
+  const float* dE; long lde;            // [B*H*W][lde] fp32, channels [0, 4) read (weights 0 for n >= NR)
+  const f16* w;                         // narrow_dgrad_x3_pack_kernel fragments
+  float* out; long ldo; int ps_r;       // fp32 rows or PixelUnshuffle SPM, as NarrowDgradArgs
+  int B, H, W;
+  float se, oscale;                     // 2^eg, 2^-(eg + KAIR_X3_WEXP)
+};
+
+__global__ __launch_bounds__(256) void conv3x3_narrow_dgrad_x3_kernel(const NarrowDgradX3Args a) {
+  __shared__ __attribute__((aligned(16))) f16 sEh[4 * DROW], sEl[4 * DROW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  f16x8 wf[4][2][2];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) wf[cb][ks][h] = *(const f16x8*)(a.w + (((cb * 2 + ks) * 2 + h) * 64 + lane) * 8);
+  const int nseg = a.W / SEG;
+  const long total = (long)a.B * nseg * a.H;
+  const RowRun run = row_run(total, gridDim.x, blockIdx.x);
+  float4 pre = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load_row = [&](long st, int yy) {
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+    const int xx = x0 - 1 + tid;
+    const bool ok = tid < PXS && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+    pre = *(const float4*)(a.dE + (ok ? ((long)(b * a.H + yy) * a.W + xx) * a.lde : 0));
+    if (!ok) pre = make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto store_row = [&](int yy) {
+    if (tid < PXS) {
+      f16x4 h, l;
+      split4(pre, a.se, h, l);
+      *(f16x4*)(sEh + (yy & 3) * DROW + tid * DPST) = h;
+      *(f16x4*)(sEl + (yy & 3) * DROW + tid * DPST) = l;
+    }
+  };
+  const int pl = lane & 15, kq = lane >> 4;
+  long cur_strip = -1;
+  for (long g = run.g0; g < run.g1; ++g) {
+    const long st = g / a.H;
+    const int y = (int)(g - st * a.H);
+    if (st != cur_strip) {
+      __syncthreads();
+      for (int d = -1; d <= 1; ++d) {
+        load_row(st, y + d);
+        store_row(y + d + 4);
+      }
+      cur_strip = st;
+      __syncthreads();
+    }
+    const bool more = g + 1 < run.g1 && (g + 1) / a.H == st;
+    if (more) load_row(st, y + 2);
+    f16x8 bh[2], bl[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x4 eh[2], el[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int tap = 8 * ks + 2 * kq + h;
+        if (tap < 9) {
+          const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+          const int o = ((y - dy + 4) & 3) * DROW + (1 + 16 * wave + pl - dx) * DPST;
+          eh[h] = *(const f16x4*)(sEh + o);
+          el[h] = *(const f16x4*)(sEl + o);
+        } else {
+          eh[h] = f16x4{};
+          el[h] = f16x4{};
+        }
+      }
+      bh[ks] = cat8(eh[0], eh[1]);
+      bl[ks] = cat8(el[0], el[1]);
+    }
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+    const int x = x0 + 16 * wave + pl;
+    long o;
+    if (a.ps_r > 1) {
+      const int r = a.ps_r, yl = y / r, xl = x / r;
+      o = ((long)(b * (a.H / r) + yl) * (a.W / r) + xl) * a.ldo + ((y - yl * r) * r + (x - xl * r)) * NF;
+    } else {
+      o = ((long)(b * a.H + y) * a.W + x) * a.ldo;
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = acc;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        acc = mfma_h(wf[cb][ks][0], bh[ks], acc);
+        acc1 = mfma_h(wf[cb][ks][1], bh[ks], acc1);
+        acc1 = mfma_h(wf[cb][ks][0], bl[ks], acc1);
+      }
+      acc += acc1;
+      *(float4*)(a.out + o + 16 * cb + 4 * kq) =
+          make_float4(acc[0] * a.oscale, acc[1] * a.oscale, acc[2] * a.oscale, acc[3] * a.oscale);
+    }
+    __syncthreads();
+    if (more) store_row(y + 2);
+    __syncthreads();
+  }
+}
+
+struct NarrowWgradX3Args {
+  const float* dE; long lde;            // [M][lde] fp32, channels [0, 4)
+  const float* x; long ldx;             // [M][ldx] fp32 image, channels [0, 64)
+  int NR;
+  int B, H, W;
+  float* part;                          // [gridDim.x][NR * 64 * 9 + NR]
+  float se, sx, oscale, bscale;         // 2^eg, 2^ex, 2^-(eg + ex), 2^-eg
+};
+
+// conv3x3_narrow_wgrad_kernel's MFMA over the pixels with both operands as fp16 pairs: an X row is 64 px x 16
+// chunks of 4 fp32 channels (4 per thread), split into its hi and lo planes
+__global__ __launch_bounds__(256) void conv3x3_narrow_wgrad_x3_kernel(const NarrowWgradX3Args a) {
+  __shared__ __attribute__((aligned(16))) f16 sXh[2][SEG * XS], sXl[2][SEG * XS];
+  __shared__ __attribute__((aligned(16))) f16 sEh[4][EPX + 8], sEl[4][EPX + 8];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, g8 = (lane >> 4) * 8;
+  const int tl = p4 >> 2;
+  f32x4 acc[3];
+#pragma unroll
+  for (int tg = 0; tg < 3; ++tg) acc[tg] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int nseg = a.W / SEG;
+  const long total = (long)a.B * nseg * a.H;
+  const RowRun run = row_run(total, gridDim.x, blockIdx.x);
+  float4 px_[4];
+  float4 pe = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load_x = [&](long st, int yy) {
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cidx = tid + 256 * i;
+      px_[i] = *(const float4*)(a.x + ((long)(b * a.H + yy) * a.W + x0 + (cidx >> 4)) * a.ldx + (cidx & 15) * 4);
+    }
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cidx = tid + 256 * i, o = (cidx >> 4) * XS + (cidx & 15) * 4;
+      f16x4 h, l;
+      split4(px_[i], a.sx, h, l);
+      *(f16x4*)(&sXh[buf][o]) = h;
+      *(f16x4*)(&sXl[buf][o]) = l;
+    }
+  };
+  auto load_e = [&](long st, int yy) {
+    const int b = (int)(st / nseg), x0 = (int)(st - (long)b * nseg) * SEG;
+    const int xx = x0 - 1 + tid;
+    const bool ok = tid < PXS && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+    pe = *(const float4*)(a.dE + (ok ? ((long)(b * a.H + yy) * a.W + xx) * a.lde : 0));
+    if (!ok) pe = make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto store_e = [&](int yy) {
+    if (tid < PXS) {
+      f16x4 h, l;
+      split4(pe, a.se, h, l);
+      *(f16x4*)(&sEh[yy & 3][tid * 4]) = h;
+      *(f16x4*)(&sEl[yy & 3][tid * 4]) = l;
+    }
+  };
+  // zero tails of every slot of both planes (taps >= 9 read slot 0's; store_e never writes them)
+  if (tid < 16) {
+    f16* t = (tid & 8 ? &sEl[0][0] : &sEh[0][0]) + ((tid >> 1) & 3) * (EPX + 8) + EPX + (tid & 1) * 4;
+    *(f16x4*)t = f16x4{};
+  }
+  long cur_strip = -1;
+  int xb = 0;
+  for (long g = run.g0; g < run.g1; ++g) {
+    const long st = g / a.H;
+    const int y = (int)(g - st * a.H);
+    if (st != cur_strip) {
+      __syncthreads();
+      for (int d = -1; d <= 1; ++d) {
+        load_e(st, y + d);
+        store_e(y + d + 4);
+      }
+      load_x(st, y);
+      store_x(xb);
+      cur_strip = st;
+      __syncthreads();
+    }
+    const bool more = g + 1 < run.g1 && (g + 1) / a.H == st;
+    if (more) {
+      load_x(st, y + 1);
+      load_e(st, y + 2);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r0 = 32 * ks + g8 + q;
+      const int xo = r0 * XS + 16 * wave + p4;
+      const f16x8 ah = tr8(&sXh[xb][xo], 4 * XS), al = tr8(&sXl[xb][xo], 4 * XS);
+#pragma unroll
+      for (int tg = 0; tg < 3; ++tg) {
+        const int tap = 4 * tg + tl;
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const int eo = tap < 9 ? ((y - dy + 4) & 3) * (EPX + 8) + (1 + r0 - dx) * 4 : EPX;
+        const int step = tap < 9 ? 16 : 0;   // rows r0 + 4: 4 pixels on (the zero tail stays put)
+        const f16x8 eh = tr8(&sEh[0][0] + eo, step), el = tr8(&sEl[0][0] + eo, step);
+        acc[tg] = mfma_h(ah, eh, acc[tg]);
+        acc[tg] = mfma_h(al, eh, acc[tg]);
+        acc[tg] = mfma_h(ah, el, acc[tg]);
+      }
+    }
+    if (tid < SEG) {
+      const f16x4 h = *(const f16x4*)(&sEh[y & 3][(1 + tid) * 4]), l = *(const f16x4*)(&sEl[y & 3][(1 + tid) * 4]);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bacc[n] += (float)h[n] + (float)l[n];
+    }
+    __syncthreads();
+    if (more) {
+      xb ^= 1;
+      store_x(xb);
+      store_e(y + 2);
+    }
+    __syncthreads();
+  }
+  const int stride = a.NR * NF * 9 + a.NR;
+  float* dst = a.part + (long)blockIdx.x * stride;
+  const int n = lane & 3;
+#pragma unroll
+  for (int tg = 0; tg < 3; ++tg) {
+    const int tap = 4 * tg + q;
+    if (tap < 9 && n < a.NR)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[(n * NF + 16 * wave + 4 * (lane >> 4) + i) * 9 + tap] = acc[tg][i] * a.oscale;
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bacc[k] = wave_sum(bacc[k]);
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < a.NR) dst[a.NR * NF * 9 + k] = bacc[k] * a.bscale;
+  }
+}
+
 }  // namespace
 
 extern "C" int kair_conv3x3_narrow_fwd(const void* x, long ldx, int lo_off, const void* w, const float* bias, int NR,
@@ -515,6 +912,69 @@ extern "C" int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x
   const int grid = grid_rows((long)B * (W / SEG) * H, 4);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(conv3x3_narrow_wgrad_kernel, dim3(grid), dim3(256), 0, s, a);
+  KAIR_CHECK_LAUNCH();
+  const int stride = NR * NF * 9 + NR;
+  hipLaunchKernelGGL(narrow_wgrad_finalize_kernel, dim3((stride + FIN_E - 1) / FIN_E), dim3(256), 0, s, ws, grid, NR, grad_w,
+                     grad_b, accumulate);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- fp32x3 forms ---------------------------------------------------------------------------------
+extern "C" long kair_conv3x3_narrow_x3_ws(void) { return 18 * 2 * 64 * 8 / 2; }   // floats (fp16 fragments)
+
+extern "C" int kair_conv3x3_narrow_fwd_x3(const float* x, long ldx, int ex, const float* w, const float* bias, int NR,
+                                          void* ws, const float* mean, float img_range, const float* resid, float* out,
+                                          int B, int H, int W, void* stream) {
+  KAIR_CHECK_ARG(x && w && ws && bias && out && NR >= 1 && NR <= 4 && B > 0 && H > 0 && W > 0, "conv3x3_narrow_fwd_x3: bad args");
+  KAIR_CHECK_ARG(W % SEG == 0, "conv3x3_narrow_fwd_x3: W must be a multiple of 64 (row segments)");
+  KAIR_CHECK_ARG(ldx % 4 == 0 && ldx >= NF && ((uintptr_t)x & 15) == 0 && ((uintptr_t)ws & 15) == 0,
+                 "conv3x3_narrow_fwd_x3: x rows of >= 64 fp32 channels, 16-byte aligned; 16-byte aligned ws");
+  KAIR_CHECK_ARG((long)B * H * W < (1L << 31), "conv3x3_narrow_fwd_x3: too many pixels");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(narrow_fwd_x3_pack_kernel, dim3(18 * 2 * 64 * 8 / 256), dim3(256), 0, s, w, NR, (f16*)ws);
+  NarrowFwdX3Args a;
+  a.x = x; a.ldx = ldx; a.w = (const f16*)ws; a.bias = bias; a.mean = mean; a.range = img_range; a.NR = NR;
+  a.resid = resid; a.out = out; a.B = B; a.H = H; a.W = W;
+  a.sx = ldexpf(1.f, ex); a.oscale = ldexpf(1.f, -(ex + KAIR_X3_WEXP));
+  hipLaunchKernelGGL(conv3x3_narrow_fwd_x3_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 2)), dim3(256), 0, s, a);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_conv3x3_narrow_dgrad_x3(const float* dE, long lde, int eg, const float* w, int NR, void* ws, float* out,
+                                            long ldo, int ps_r, int B, int H, int W, void* stream) {
+  KAIR_CHECK_ARG(dE && w && ws && out && NR >= 1 && NR <= 4 && lde >= 4 && lde % 4 == 0 && ((uintptr_t)dE & 15) == 0 &&
+                     ((uintptr_t)ws & 15) == 0,
+                 "conv3x3_narrow_dgrad_x3: dE rows of >= 4 fp32 channels, 16-byte aligned; 16-byte aligned ws");
+  KAIR_CHECK_ARG(W % SEG == 0, "conv3x3_narrow_dgrad_x3: W must be a multiple of 64 (row segments)");
+  KAIR_CHECK_ARG(ps_r <= 1 ? ldo >= NF : (H % ps_r == 0 && W % ps_r == 0 && ldo >= (long)ps_r * ps_r * NF),
+                 "conv3x3_narrow_dgrad_x3: output stride / PixelUnshuffle geometry");
+  KAIR_CHECK_ARG(ldo % 4 == 0 && ((uintptr_t)out & 15) == 0 && (long)B * H * W < (1L << 31), "conv3x3_narrow_dgrad_x3: alignment");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(narrow_dgrad_x3_pack_kernel, dim3(4 * 2 * 2 * 64 * 8 / 256), dim3(256), 0, s, w, NR, (f16*)ws);
+  NarrowDgradX3Args a;
+  a.dE = dE; a.lde = lde; a.w = (const f16*)ws; a.out = out; a.ldo = ldo; a.ps_r = ps_r; a.B = B; a.H = H; a.W = W;
+  a.se = ldexpf(1.f, eg); a.oscale = ldexpf(1.f, -(eg + KAIR_X3_WEXP));
+  hipLaunchKernelGGL(conv3x3_narrow_dgrad_x3_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 4)), dim3(256), 0, s, a);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_conv3x3_narrow_wgrad_x3(const float* dE, long lde, int eg, const float* x, long ldx, int ex, int NR,
+                                            float* ws, float* grad_w, float* grad_b, int accumulate, int B, int H, int W,
+                                            void* stream) {
+  KAIR_CHECK_ARG(dE && x && ws && grad_w && NR >= 1 && NR <= 4 && lde >= 4 && lde % 4 == 0 && ldx >= NF && ldx % 4 == 0 &&
+                     ((uintptr_t)dE & 15) == 0 && ((uintptr_t)x & 15) == 0,
+                 "conv3x3_narrow_wgrad_x3: bad operands");
+  KAIR_CHECK_ARG(W % SEG == 0, "conv3x3_narrow_wgrad_x3: W must be a multiple of 64 (row segments)");
+  KAIR_CHECK_ARG((long)B * H * W < (1L << 31), "conv3x3_narrow_wgrad_x3: too many pixels");
+  NarrowWgradX3Args a;
+  a.dE = dE; a.lde = lde; a.x = x; a.ldx = ldx; a.NR = NR; a.B = B; a.H = H; a.W = W; a.part = ws;
+  a.se = ldexpf(1.f, eg); a.sx = ldexpf(1.f, ex); a.oscale = ldexpf(1.f, -(eg + ex)); a.bscale = ldexpf(1.f, -eg);
+  const int grid = grid_rows((long)B * (W / SEG) * H, 4);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(conv3x3_narrow_wgrad_x3_kernel, dim3(grid), dim3(256), 0, s, a);
   KAIR_CHECK_LAUNCH();
   const int stride = NR * NF * 9 + NR;
   hipLaunchKernelGGL(narrow_wgrad_finalize_kernel, dim3((stride + FIN_E - 1) / FIN_E), dim3(256), 0, s, ws, grid, NR, grad_w,

@@ -356,6 +356,7 @@ class SwinIREngine:
         self.norm = net.norm
         self.cab = _resi(self, net.conv_after_body)
         nf = 64
+        self.last_narrow_x3 = False
         if self.upsampler == "pixelshuffle":
             self.cbu = _Conv(self, net.conv_before_upsample[0], nf, self.Cp, wr=self.conv_wr)
             self.ups = []
@@ -371,6 +372,8 @@ class SwinIREngine:
             # (per call: the HR width must be a multiple of 64, else the implicit-GEMM path runs)
             self.last_narrow = self.tdt == torch.bfloat16 and self.split_conv and self.in_ch <= 4
             self.last = _Conv(self, net.conv_last, 16, nf, narrow=self.last_narrow)
+            # ... and their fp32x3 forms (csrc/tail.hip *_x3: fp16 pairs of the fp32 operands, as kair_gemm_nt_x3)
+            self.last_narrow_x3 = self.x3 and self.in_ch <= 4
         elif self.upsampler == "pixelshuffledirect":
             conv = net.upsample[0]
             self.ups_r = [self.scale]
@@ -523,6 +526,8 @@ class SwinIREngine:
                 acts.append(e(hw, tl, dt=T))
             P["ups_act"] = acts
             P["M_hr"] = hw
+            if self.last_narrow_x3:
+                P["narrow_fws"] = e(H.conv3x3_narrow_x3_ws())
         elif self.upsampler == "nearest+conv":
             nf = 64
             P["a0"] = e(M, nf, dt=T)
@@ -572,9 +577,9 @@ class SwinIREngine:
         P["colsum_ws"] = e(1024 * 256)
         if self.upsampler == "pixelshuffle":
             P["dE"] = e(P["M_hr"], 16, dt=T)
-            if self.last.narrow:
+            if self.last.narrow or self.last_narrow_x3:
                 P["narrow_ws"] = e(H.conv3x3_narrow_wgrad_ws(self.in_ch))
-                P["narrow_dws"] = e(H.conv3x3_narrow_dgrad_ws())
+                P["narrow_dws"] = e(H.conv3x3_narrow_x3_ws() if self.x3 else H.conv3x3_narrow_dgrad_ws())
             dpre, hw = [], M
             for c in self.ups:
                 dpre.append(e(hw, c.Co, dt=T))
@@ -810,6 +815,10 @@ class SwinIREngine:
                           B * h * w, c.Co, 9 * c.fcip, cd)
                 src, h, w = dst, h * r, w * r
             c = self.last
+            if self.last_narrow_x3 and w % 64 == 0:
+                H.conv3x3_narrow_fwd_x3(src, tl, self.X3_AEXP, c.w.detach(), c.bp, self.in_ch, P["narrow_fws"], self.mean,
+                                        self.img_range, None, P["E"], B, h, w)
+                return P["E"]
             if c.narrow and w % 64 == 0:   # 64 -> in_ch: the narrow-output kernel (weights in VGPRs)
                 H.conv3x3_narrow_fwd(src, tl, 64 if sa else 0, c.Wn, c.bp, self.in_ch, self.mean, self.img_range, None,
                                      P["E"], B, h, w)
@@ -987,7 +996,12 @@ class SwinIREngine:
             tl = P["tail_ld"]   # the activations' row stride (a [hi | lo] pair under split_act: the hi half is read)
             # conv_last: dgrad into the pre-shuffle layout of the last upsampling conv
             r_last = self.ups_r[-1]
-            if c.narrow and w % 64 == 0:   # the narrow-output kernels (rolling row window, fp32 master weight)
+            if self.last_narrow_x3 and w % 64 == 0:
+                H.conv3x3_narrow_dgrad_x3(P["dE"], 16, P["e_g"], c.w.detach(), self.in_ch, P["narrow_dws"], P["dpre"][-1],
+                                          self.ups[-1].Co, r_last, B, h, w)
+                H.conv3x3_narrow_wgrad_x3(P["dE"], 16, P["e_g"], src, tl, self.X3_AEXP, self.in_ch, P["narrow_ws"], g(c.w),
+                                          g(c.b), B, h, w)
+            elif c.narrow and w % 64 == 0:   # the narrow-output kernels (rolling row window, fp32 master weight)
                 H.conv3x3_narrow_dgrad(P["dE"], 16, c.w.detach(), self.in_ch, P["narrow_dws"], P["dpre"][-1], self.ups[-1].Co,
                                        r_last, B, h, w)
                 H.conv3x3_narrow_wgrad(P["dE"], 16, src, tl, self.in_ch, P["narrow_ws"], g(c.w), g(c.b), B, h, w)

@@ -139,3 +139,76 @@ def test_halo_channel_groups(mode):
         gs = torch.where(gate[:, :N].float() > 0, 1.0, 0.01).view(B, Hh, Ww, N).permute(0, 3, 1, 2)
         ref = ref * gs.double()
     assert rel_err(got, ref) < 1e-5
+
+
+# ---- fp32x3 forms (fp32 operands as fp16 pairs, three products): the fp32 engine's 1e-5-class bar ----------
+def rows_of(t, ld):
+    """NCHW fp32 -> NHWC fp32 rows of ld channels (zero padded)."""
+    B, C, Hh, Ww = t.shape
+    r = torch.zeros(B * Hh * Ww, ld)
+    r[:, :C] = t.permute(0, 2, 3, 1).reshape(-1, C)
+    return r
+
+
+@pytest.mark.parametrize("NR,shape", [(3, (2, 32, 64)), (1, (1, 16, 128)), (3, (1, 48, 192))])
+def test_narrow_fwd_x3(NR, shape):
+    B, Hh, Ww = shape
+    g = torch.Generator().manual_seed(40 + NR + Ww)
+    x = torch.randn(B, 64, Hh, Ww, generator=g)
+    w = torch.randn(NR, 64, 3, 3, generator=g) * 0.05
+    b = torch.randn(NR, generator=g) * 0.1
+    mean = torch.tensor([0.4488, 0.4371, 0.4040])[:NR]
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1) + mean.double().view(1, -1, 1, 1)
+    bp = torch.zeros(16, device=dev)
+    bp[:NR] = b.to(dev)
+    ws = torch.empty(H.conv3x3_narrow_x3_ws(), device=dev)
+    out = torch.full((B, NR, Hh, Ww), float("nan"), device=dev)
+    H.conv3x3_narrow_fwd_x3(rows_of(x, 64).to(dev), 64, 4, w.to(dev), bp, NR, ws, mean.to(dev), 1.0, None, out, B, Hh, Ww)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 2e-6
+
+
+@pytest.mark.parametrize("ps_r", [0, 2])
+def test_narrow_dgrad_x3(ps_r):
+    B, Hh, Ww, NR = 2, 16, 64, 3
+    g = torch.Generator().manual_seed(49 + ps_r)
+    dE = torch.randn(B, NR, Hh, Ww, generator=g) * 2.0 ** -12   # a mean-loss gradient's scale, exponent 12 + 4
+    w = torch.randn(NR, 64, 3, 3, generator=g) * 0.05
+    x = torch.zeros(B, 64, Hh, Ww, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x, w.double(), padding=1).backward(dE.double())
+    ref = x.grad
+    dEd = rows_of(dE, 16).to(dev)
+    ws = torch.empty(H.conv3x3_narrow_x3_ws(), device=dev)
+    if ps_r:
+        r = ps_r
+        out = torch.full((B * (Hh // r) * (Ww // r), r * r * 64), float("nan"), device=dev)
+        H.conv3x3_narrow_dgrad_x3(dEd, 16, 16, w.to(dev), NR, ws, out, r * r * 64, r, B, Hh, Ww)
+        torch.cuda.synchronize()
+        got = out.cpu().view(B, Hh // r, Ww // r, r, r, 64).permute(0, 5, 1, 3, 2, 4).reshape(B, 64, Hh, Ww)
+    else:
+        out = torch.full((B * Hh * Ww, 64), float("nan"), device=dev)
+        H.conv3x3_narrow_dgrad_x3(dEd, 16, 16, w.to(dev), NR, ws, out, 64, 0, B, Hh, Ww)
+        torch.cuda.synchronize()
+        got = out.cpu().view(B, Hh, Ww, 64).permute(0, 3, 1, 2)
+    assert rel_err(got, ref) < 2e-6
+
+
+def test_narrow_wgrad_x3():
+    B, Hh, Ww, NR = 2, 48, 64, 3
+    g = torch.Generator().manual_seed(61)
+    x = torch.randn(B, 64, Hh, Ww, generator=g)
+    dE = torch.randn(B, NR, Hh, Ww, generator=g) * 2.0 ** -12
+    w = torch.zeros(NR, 64, 3, 3, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(NR, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.double(), w, b, padding=1).backward(dE.double())
+    ws = torch.empty(H.conv3x3_narrow_wgrad_ws(NR), device=dev)
+    outs = []
+    for _ in range(2):
+        gw = torch.full((NR, 64, 3, 3), float("nan"), device=dev)
+        gb = torch.full((NR,), float("nan"), device=dev)
+        H.conv3x3_narrow_wgrad_x3(rows_of(dE, 16).to(dev), 16, 16, rows_of(x, 64).to(dev), 64, 4, NR, ws, gw, gb, B, Hh, Ww)
+        torch.cuda.synchronize()
+        outs.append((gw.cpu(), gb.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert rel_err(outs[0][0], w.grad) < 2e-6
+    assert rel_err(outs[0][1], b.grad) < 2e-6

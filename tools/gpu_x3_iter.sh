@@ -5,7 +5,7 @@ set -o pipefail
 out=gpurun_out/${1:-x3}
 mkdir -p $out
 sel=${2:+-k "$2"}
-timeout -k 10 600 python -u -m pytest tests/test_x3_gpu.py -v -x $sel --timeout 300 --timeout-method thread > $out/tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_x3_gpu.py tests/test_tail_gpu.py -v -x $sel --timeout 300 --timeout-method thread > $out/tests.log 2>&1; rc=$?
 grep -E "PASS|FAIL|Error|assert" $out/tests.log | tail -30
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 240 python -u tools/x3_micro.py > $out/micro.log 2>&1 || exit $?
