@@ -246,8 +246,11 @@ def rocprof_name(fn, a):
 
 def _x3_ring_nt(a):
     """Whether an x3 gemm_nt launch takes the ring kernel (gemm_x3.hip nt_x3_ring_ok, the common cases)."""
-    A, N, K = a[0], a[4], a[5]
-    return N % 192 == 0 and K % 32 == 0 and (A.mode == 0 or (A.mode == 1 and A.dtype == 0 and A.im_C % 32 == 0))
+    A, E, N, K = a[0], a[2], a[4], a[5]
+    bn = 192 if N % 192 == 0 else (N if N in (64, 128) else 0)   # nt_x3_ring_bn
+    return (bn > 0 and K % 32 == 0 and (E.out_mode in (0, 1) or (E.out_mode == 6 and bn == 128)) and   # rows / q,k,v /
+                                                                                                    # PixelShuffle
+            (A.mode == 0 or (A.mode == 1 and A.dtype == 0 and A.im_C % 32 == 0)))
 
 
 def pmc_traffic(key):

@@ -359,7 +359,9 @@ template <int BN> struct XR {
   static constexpr int BI = BN / 64;    // B DMA wave-instructions per wave per chunk
 };
 
-enum { XE_ROWS_F32 = 0, XE_ROWS_PAIR = 1, XE_QKV = 2 };
+// XE_PSHUF / XE_PUNSHUF: fp32 stores in the PixelShuffle / PixelUnshuffle sub-pixel-major layouts (KAIR_OUT_PSHUF_SPM /
+// KAIR_OUT_PUNSHUF_SPM: the upsampling convs' outputs and input gradients), bias only
+enum { XE_ROWS_F32 = 0, XE_ROWS_PAIR = 1, XE_QKV = 2, XE_PSHUF = 3, XE_PUNSHUF = 4 };
 
 // perf-investigation phase stamps of the NT ring (debug builds, KAIR_RING_DBG bit 8): CTAs 0..XS_CTAS-1, every
 // wave, intervals 0..XS_IT-1, s_memtime at XS_N points (interval top, after the chunk wait, after the barrier +
@@ -418,8 +420,11 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       const int part = fdiv(n, E.d_pw), rr = n - part * pw;
       const int h = fdiv(rr, E.d_hdp), d = rr - h * E.hdp;
       colo[p] = (long)part * E.M * pw + (long)h * E.tok * E.hdp + d;
+    } else if constexpr (EM == XE_PSHUF) {   // column n = (i r + j) nf + c: sub-pixel (i, j) of the row's pixel
+      const int nf = E.N / (E.r * E.r), sp = n / nf, c = n - sp * nf, i = sp / E.r, j = sp - i * E.r;
+      colo[p] = ((long)i * E.psW * E.r + j) * E.ldo + c;
     } else {
-      colo[p] = 0;
+      colo[p] = n;
     }
   }
   for (int i = tid; i < BN; i += 512) sBias[i] = E.bias && n0 + i < E.N ? E.bias[n0 + i] : 0.f;   // (visible after the
@@ -570,6 +575,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
     }
     int nvm = 0;
     int rowv[2];
+    long roff[2];   // the shuffled forms' row part of the store offset
     bool okm[2];
     const int m0 = (mt0 + ct * mstride) * XR_BM + grp * 64 + wm * 32 + fr;
 #pragma unroll
@@ -577,9 +583,19 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       const int m = m0 + i * 16;
       okm[i] = m < (int)E.M;
       const int mm = okm[i] ? m : 0;
+      roff[i] = 0;
       if constexpr (EM == XE_QKV) {
         const int win = fdiv(mm, E.d_tok);
         rowv[i] = win * E.nh * E.tok + (mm - win * E.tok);
+      } else if constexpr (EM == XE_PSHUF) {   // pixel (b, y, x) of [psH, psW] -> (b, y r, x r) of the r-times image
+        const int hw = E.psH * E.psW, b = mm / hw, pp = mm - b * hw, y = pp / E.psW, x = pp - y * E.psW;
+        rowv[i] = mm;
+        roff[i] = (((long)b * E.psH * E.r + (long)y * E.r) * ((long)E.psW * E.r) + (long)x * E.r) * E.ldo;
+      } else if constexpr (EM == XE_PUNSHUF) {   // pixel (b, Y, X) of the r-times image -> row (b, Y/r, X/r), block (Y%r, X%r)
+        const int Wr = E.psW * E.r, HWr = E.psH * E.r * Wr, b = mm / HWr, pp = mm - b * HWr, Y = pp / Wr, X = pp - Y * Wr;
+        const int y = Y / E.r, x = X / E.r;
+        rowv[i] = mm;
+        roff[i] = (((long)b * E.psH + y) * E.psW + x) * E.ldo + (long)((Y - y * E.r) * E.r + (X - x * E.r)) * E.N;
       } else {
         rowv[i] = win_to_token32(mm, E.win);
       }
@@ -652,11 +668,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
 #pragma unroll
           for (int c = 0; c < 8; ++c) v[c] = c == oc[p] ? 1.f : v[c];   // the ones column (lane-varying select)
           const long rr = rowv[i];
-          if (okm[i]) {
+          // (ablation bit 128: every value computed, no store issued -- the store path's share of the epilogue)
+          const bool st = !KAIR_DBG(E.dbg & 128) || v[0] == 1.2345e-30f;
+          if (okm[i] && st) {
             if constexpr (EM == XE_ROWS_PAIR) {
               store8_f16pair(E.out, E.out_lo, rr * E.ldo + n, v, E.oscale);
             } else {
-              float* d = (float*)E.out + rr * E.ldo + n;
+              float* d = (float*)E.out + (EM == XE_PSHUF || EM == XE_PUNSHUF ? roff[i] + colo[p] : rr * E.ldo + n);
               *(float4*)d = make_float4(v[0], v[1], v[2], v[3]);
               *(float4*)(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
             }
@@ -926,10 +944,11 @@ int tn_x3_b(const Op& a, const Op& b, int bmode, int bdt, float* ws, int splits,
                          : launch_tn_x3<TA, float, AM_IM2COL>(a, b, ws, splits, M, N, K, rps, acc_scale, s);
 }
 
-// the ring's N-tile for N columns (0: none): 192 for multiples of 192, else one tile of 64 / 128
+// the ring's N-tile for N columns (0: none): 192 for multiples of 192, else one tile of 64 or tiles of 128
 int nt_x3_ring_bn(int N) {
   if (N % 192 == 0) return 192;
-  return N == 64 || N == 128 ? N : 0;
+  if (N == 64) return 64;
+  return N % 128 == 0 ? 128 : 0;
 }
 
 // the ring takes N-tiles of 192 columns, 32-deep k-chunks (im2col: one tap per chunk) and 16-byte aligned rows
@@ -939,7 +958,15 @@ bool nt_x3_ring_ok(const kair_operand* A, const kair_operand* B, const kair_epil
   // epilogues: fp32 rows (bias, activation [+ pre], residual [x row scale] or fp32 gate, ones column) or fp16
   // pair rows / head-blocked q, k, v (bias); 16-byte aligned rows throughout
   const bool pair = E->out_dtype == KAIR_F16;
-  if (E->out_mode == KAIR_OUT_QKVBLK) {
+  if (E->out_mode == KAIR_OUT_PSHUF_SPM || E->out_mode == KAIR_OUT_PUNSHUF_SPM) {   // fp32, bias only
+    const int r = E->ps_r;
+    if (pair || E->act || E->out_pre || E->resid || E->gate || E->rowscale || E->resid2 || E->a_copy || E->out_lo ||
+        E->out_ones_col_p1 > 0 || E->win_ws || r < 1 || E->ldo % 4 || (uintptr_t)E->out % 16 || N % 8 ||
+        nt_x3_ring_bn(N) != 128)   // 128-column tiles only: the x4 upsampling convs' forward (N = 256; 64-column
+                                   // tiles lose to the generic kernel at K = 2,304: 799 vs 546 us in-step)
+      return false;
+    if (E->out_mode == KAIR_OUT_PSHUF_SPM && (N % (r * r) || (N / (r * r)) % 8)) return false;
+  } else if (E->out_mode == KAIR_OUT_QKVBLK) {
     if (nt_x3_ring_bn(N) != 192 || !pair || E->qkv_hdp % 8 || (uintptr_t)E->out % 16 || E->act || E->out_pre || E->resid || E->gate || E->rowscale) return false;
   } else {
     if (E->out_mode != KAIR_OUT_ROWS || E->ldo % 4 || (uintptr_t)E->out % 16) return false;
@@ -981,8 +1008,10 @@ int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int
     else if (e.act == KAIR_ACT_GELU) XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_GELU_X, 0);
     else if (e.act == KAIR_ACT_LEAKY) XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_LEAKY, 0);
     else XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_NONE, 0);
-  } else {   // the reconstruction tail's narrow / wide convs: fp32 rows, LeakyReLU or its gate (nt_x3_ring_ok)
-    if (e.gate) XR_LAUNCH(XE_ROWS_F32, EX_GATE_F32, XA_NONE, XG_LEAKY);
+  } else {   // the reconstruction tail's narrow / wide convs: fp32 rows, LeakyReLU or its gate, shuffles (nt_x3_ring_ok)
+    if (e.omode == KAIR_OUT_PSHUF_SPM) XR_LAUNCH(XE_PSHUF, EX_NONE, XA_NONE, 0);
+    else if (e.omode == KAIR_OUT_PUNSHUF_SPM) XR_LAUNCH(XE_PUNSHUF, EX_NONE, XA_NONE, 0);
+    else if (e.gate) XR_LAUNCH(XE_ROWS_F32, EX_GATE_F32, XA_NONE, XG_LEAKY);
     else if (e.act == KAIR_ACT_LEAKY) XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_LEAKY, 0);
     else XR_LAUNCH(XE_ROWS_F32, EX_NONE, XA_NONE, 0);
   }

@@ -4,13 +4,16 @@ they touch the GPU) run FusedTrainer with segmented HIP graphs and the per-bucke
 FusedTrainer on the 4-patch batch (DropPath off), so the only difference is the order of the fp32
 gradient sums (rank partial sums vs one batch sum).
 
-Two configurations (reference: the DDP step of models/model_base.py:113-119, main_train_psnr.py:122-130):
+Four configurations (reference: the DDP step of models/model_base.py:113-119, main_train_psnr.py:122-130):
   * "fp32-small": embed 60, the exact-fp32 engine -- agreement to ~1e-6 relative;
   * "bf16-c4": the C4 production kernel set -- embed 180 / 6 heads / hidden 360, split-operand bf16
     engine with the fused attention and MLP halves, the row GEMMs with fused LayerNorm backward, the
     grouped block weight gradients on the side stream, halo convs -- under the same segmented capture;
     the per-sample forward and data gradients are row-wise identical between the shard and the batch,
-    so parameters / EMA agree to the fp32 re-association of the weight-gradient sums."""
+    so parameters / EMA agree to the fp32 re-association of the weight-gradient sums;
+  * "fp32x3-c4": the headline engine (fp16-pair arithmetic of the fp32 reference) at the C4 width, its
+    deferred block weight gradients on the side stream;
+  * "rrdbnet-c5": RRDBNet x4 with its gradient segments (network_rrdbnet.py:74-101), 3 buckets."""
 import os
 import socket
 import tempfile

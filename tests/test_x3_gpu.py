@@ -226,6 +226,25 @@ def test_gemm_nt_x3_ring_epilogues():
             ref = torch.where(ref > 0, ref, 0.01 * ref)
         torch.cuda.synchronize()
         assert rel(out, ref) < 2e-6, N
+    # (e) the upsampling convs' stores: PixelShuffle(2) sub-pixel-major (forward, 256 columns = 2 tiles of 128) and
+    # PixelUnshuffle(2) into the previous conv's pre-shuffle rows (input gradient, 64 columns)
+    Bn, h, w_ = 2, 6, 10
+    for mode, N in ((H.OUT_PSHUF_SPM, 256), (H.OUT_PUNSHUF_SPM, 64)):
+        M = Bn * h * w_ * (1 if mode == H.OUT_PSHUF_SPM else 4)
+        K = 576
+        x, w, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05, torch.randn(N, generator=g)
+        Wo, keep = _wsplit(w)
+        A = H.rows(x.to(dev))
+        A.x3_exp = 4
+        y = x.double() @ w.double().T + b.double()
+        out = torch.full((Bn * h * w_ * 4, 64) if mode == H.OUT_PSHUF_SPM else (Bn * h * w_, 256), float("nan"), device=dev)
+        H.gemm_nt(A, Wo, H.epilogue(out, mode=mode, ldo=out.shape[1], bias=b.to(dev), ps=(2, h, w_)), M, N, K, H.X3)
+        if mode == H.OUT_PSHUF_SPM:   # row (b, y, x), column (i 2 + j) 64 + c -> pixel (b, 2y + i, 2x + j), channel c
+            ref = y.view(Bn, h, w_, 2, 2, 64).permute(0, 1, 3, 2, 4, 5).reshape(-1, 64)
+        else:                         # pixel (b, 2y + i, 2x + j), channel c -> row (b, y, x), column (i 2 + j) 64 + c
+            ref = y.view(Bn, h, 2, w_, 2, 64).permute(0, 1, 3, 2, 4, 5).reshape(-1, 256)
+        torch.cuda.synchronize()
+        assert rel(out, ref) < 2e-6, mode
 
 
 @pytest.mark.parametrize("conv", [False, True])

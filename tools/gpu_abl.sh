@@ -1,5 +1,5 @@
 # Ablations of the x3 ring GEMMs (debug-ablation build, KAIR_RING_DBG bits: 1 no epilogue, 2 no MFMA, 4 no DMA,
-# 16 no B (weight) DMA, 32 no A DMA)
+# 16 no B (weight) DMA, 32 no A DMA, 64 no fragment loads, 128 no epilogue stores)
 #   usage: bash tools/gpu_abl.sh OUTDIR [filter]
 set -o pipefail
 out=gpurun_out/${1:-abl}
