@@ -190,27 +190,34 @@ __global__ __launch_bounds__(64 * FWD_NW) void attn_fwd_x3_kernel(const f16* __r
 }
 
 // ------------------------------------------------------------------------------------------
-// backward: one wave per (head, group of windows), one wave per workgroup (50 KB of LDS: q / dO / k
-// hi and lo tiles for the transposed fragment reads and the running bias gradient [q][key] in fp32).
+// backward: one 2-wave workgroup per (head, group of windows); wave w owns the keys 32 w .. 32 w + 31 of every
+// window (S, dP, P, dS, dV, dK of its key half; its partial dQ over those keys, the two halves summed through
+// LDS, each wave finishing 32 queries).  50 KB of LDS per workgroup: the window's q / dO hi and lo tiles (each
+// wave stages 32 rows), then the two waves' dS tiles; each wave's k tile, then its dQ-partial exchange slot; the
+// running bias gradient [q][key] fp32 (each entry belongs to one lane of one wave).  3 workgroups per CU.
 // P is recomputed from q, k and the saved log-sum-exp.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restrict__ qkv, const f16* __restrict__ qkvl,
+constexpr int BWD_NW = 2;
+__global__ __launch_bounds__(64 * BWD_NW, 2) void attn_bwd_x3_kernel(const f16* __restrict__ qkv, const f16* __restrict__ qkvl,
                                                             const f16* __restrict__ O, const f16* __restrict__ Ol, long ldo,
                                                             const f16* __restrict__ dO, const f16* __restrict__ dOl, long lddo,
                                                             const float* __restrict__ table, const float* __restrict__ lse,
                                                             f16* __restrict__ dqkv, f16* __restrict__ dqkvl,
                                                             float* __restrict__ dB_part, long nWin, int nh, int wpg,
                                                             float scale, int H, int W, int shift, int e_act, int e_grad) {
-  constexpr int LD = ATT_LD, LDD = 72;
-  static_assert(TOK * LDD <= 2 * TOK * LD, "the dS tile reuses the q / dO tiles");
-  // plane p (0 hi, 1 lo): [q | dO] tiles, after dV / dK the dS tile [q][key] (row stride LDD)
+  constexpr int LD = ATT_LD, LDB = 72;
+  // plane p (0 hi, 1 lo): [q | dO] tiles [64][LD]; after dV / dK wave w's dS tile [q][its 32 keys] at w * TOK * LD
   __shared__ __attribute__((aligned(16))) f16 sQG[2][2 * TOK * LD];
-  __shared__ __attribute__((aligned(16))) f16 sK[2][TOK * LD];
-  __shared__ __attribute__((aligned(16))) float sDB[TOK * 72];   // running bias gradient [q][key]
+  // [wave][plane]: the wave's k rows [32][LD]; after its dQ MFMAs, its exchange slot (16 floats per lane)
+  __shared__ __attribute__((aligned(16))) f16 sK[BWD_NW][2][32 * LD];
+  __shared__ __attribute__((aligned(16))) float sDB[TOK * LDB];   // running bias gradient [q][key]
   __shared__ float sTab[232];
   __shared__ float sRow[2][TOK];  // lse, delta
   __shared__ int sReg[TOK];
-  const int lane = threadIdx.x;
+  static_assert(2 * 32 * LD * sizeof(f16) >= 64 * 16 * sizeof(float), "dQ exchange slot");
+  static_assert(2 * 32 * LD * sizeof(f16) >= 1024 * sizeof(float), "bin scratch");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long gtask = blockIdx.x;
   const long ngroups = (nWin + wpg - 1) / wpg;
   if (gtask >= ngroups * nh) return;
@@ -219,7 +226,7 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
   const long M = nWin * TOK;
   const long part = M * nh * HDP;
   const int l31 = lane & 31, hh = lane >> 5;
-  for (int i = lane; i < NBIN; i += 64) sTab[i] = table[i * nh + h];
+  for (int i = tid; i < NBIN; i += 64 * BWD_NW) sTab[i] = table[i * nh + h];
   const int nW = (H / WS) * (W / WS);
   const long tstr = 3L * nh * HDP;
   // exponents: q/k/v and O carry e_act, dO / dS / dq,dk,dv carry e_grad; everything below is rescaled
@@ -229,113 +236,109 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
   const float s_dv = ldexpf(1.f, -P_EXP);    // dO^T P: (e_grad) x (P_EXP) -> e_grad
   const float s_p = ldexpf(1.f, P_EXP);
   const float s_dk = ldexpf(1.f, -e_act);    // Q^T dS, K^T dS^T: (e_act) x (e_grad) -> e_grad
+  // (row stride 72: the two lane halves' rows 4 apart fall in opposite bank halves)
+  for (int i = tid; i < TOK * LDB / 4; i += 64 * BWD_NW) ((float4*)sDB)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  // the running bias gradient [q][key] in LDS (row stride 72: the two lane halves' rows 4 apart fall in
-  // opposite bank halves); each entry belongs to one lane, so no synchronisation is needed for it
-  constexpr int LDB = 72;
-  for (int i = lane; i < TOK * LDB / 4; i += 64) ((float4*)sDB)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-
-  auto ldfrag = [&](const f16* g, long ld, f16x8 (&f)[2][2]) {
+  // fragment f[s] of token t * 32 + l31 (8 consecutive d at 16 s + 8 hh) and its LDS image (row r0 + l31)
+  auto ldfrag = [&](const f16* g, long ld, int t, f16x8 (&f)[2]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) f[t][s] = *(const f16x8*)(g + (long)(t * 32 + l31) * ld + 16 * s + 8 * hh);
+    for (int s = 0; s < 2; ++s) f[s] = *(const f16x8*)(g + (long)(t * 32 + l31) * ld + 16 * s + 8 * hh);
   };
-  auto stfrag = [&](f16* tile, const f16x8 (&f)[2][2]) {
+  auto stfrag = [&](f16* tile, int r0, const f16x8 (&f)[2]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int s = 0; s < 2; ++s) *(f16x8*)(tile + (r0 + l31) * LD + 16 * s + 8 * hh) = f[s];
+  };
+  // the wave's own token half f[w] of a [2][2] fragment set (a select: a register array indexed by the run-time
+  // wave index would live in scratch)
+  auto stown = [&](f16* tile, const f16x8 (&f)[2][2]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) *(f16x8*)(tile + (t * 32 + l31) * LD + 16 * s + 8 * hh) = f[t][s];
+    for (int s = 0; s < 2; ++s) *(f16x8*)(tile + (32 * w + l31) * LD + 16 * s + 8 * hh) = w ? f[1][s] : f[0][s];
   };
 
   const long w0 = grp * wpg;
   long w1 = w0 + wpg;
   if (w1 > nWin) w1 = nWin;
+  const int ki = w * 32 + l31;   // this lane's key
   for (long win = w0; win < w1; ++win) {
     const long blk = (win * nh + h) * TOK * HDP;
-    wave_sync();   // the previous window's LDS tiles are no longer read
-    f32x16 S[2][2], dP[2][2];
+    __syncthreads();   // the previous window's tiles and exchange slots are no longer read
+    f32x16 S[2], dP[2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int r = 0; r < 16; ++r) { S[a][r] = 0.f; dP[a][r] = 0.f; }
+    {   // S = Q K_w^T : tiles [qt], lane = key, regs = query
+      f16x8 Fqh[2][2], Fql[2][2], Fkh[2], Fkl[2];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { S[a][b][r] = 0.f; dP[a][b][r] = 0.f; }
-    {   // S = Q K^T : tiles [qt][kt], lane = key, regs = query
-      f16x8 Fqh[2][2], Fql[2][2], Fkh[2][2], Fkl[2][2];
-      ldfrag(qkv + blk, HDP, Fqh);
-      ldfrag(qkvl + blk, HDP, Fql);
-      ldfrag(qkv + part + blk, HDP, Fkh);
-      ldfrag(qkvl + part + blk, HDP, Fkl);
-      stfrag(sQG[0], Fqh);
-      stfrag(sQG[1], Fql);
-      stfrag(sK[0], Fkh);
-      stfrag(sK[1], Fkl);
+      for (int t = 0; t < 2; ++t) {
+        ldfrag(qkv + blk, HDP, t, Fqh[t]);
+        ldfrag(qkvl + blk, HDP, t, Fql[t]);
+      }
+      ldfrag(qkv + part + blk, HDP, w, Fkh);
+      ldfrag(qkvl + part + blk, HDP, w, Fkl);
+      stown(sQG[0], Fqh);
+      stown(sQG[1], Fql);
+      stfrag(sK[w][0], 0, Fkh);
+      stfrag(sK[w][1], 0, Fkl);
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-            S[qt][kt] = mfma32(Fqh[qt][s], Fkh[kt][s], S[qt][kt]);
-            S[qt][kt] = mfma32(Fqh[qt][s], Fkl[kt][s], S[qt][kt]);
-            S[qt][kt] = mfma32(Fql[qt][s], Fkh[kt][s], S[qt][kt]);
-          }
+        for (int qt = 0; qt < 2; ++qt) {
+          S[qt] = mfma32(Fqh[qt][s], Fkh[s], S[qt]);
+          S[qt] = mfma32(Fqh[qt][s], Fkl[s], S[qt]);
+          S[qt] = mfma32(Fql[qt][s], Fkh[s], S[qt]);
+        }
     }
-    {   // dP = dO V^T ; delta = rowsum(dO o O) from the fp32 sums of the planes
-      f16x8 Fgh[2][2], Fgl[2][2], Fvh[2][2], Fvl[2][2], Foh[2][2], Fol[2][2];
-      ldfrag(dO + win * TOK * lddo + h * HDP, lddo, Fgh);
-      ldfrag(dOl + win * TOK * lddo + h * HDP, lddo, Fgl);
-      ldfrag(qkv + 2 * part + blk, HDP, Fvh);
-      ldfrag(qkvl + 2 * part + blk, HDP, Fvl);
-      stfrag(sQG[0] + TOK * LD, Fgh);
-      stfrag(sQG[1] + TOK * LD, Fgl);
-      float dsum[2] = {0.f, 0.f};
+    {   // dP = dO V_w^T ; delta = rowsum(dO o O) for the queries 32 w + l31, from the fp32 sums of the planes
+      f16x8 Fgh[2][2], Fgl[2][2], Fvh[2], Fvl[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        ldfrag(dO + win * TOK * lddo + h * HDP, lddo, t, Fgh[t]);
+        ldfrag(dOl + win * TOK * lddo + h * HDP, lddo, t, Fgl[t]);
+      }
+      ldfrag(qkv + 2 * part + blk, HDP, w, Fvh);
+      ldfrag(qkvl + 2 * part + blk, HDP, w, Fvl);
+      stown(sQG[0] + TOK * LD, Fgh);
+      stown(sQG[1] + TOK * LD, Fgl);
+      float dsum = 0.f;
       if (Ol) {
-        ldfrag(O + win * TOK * ldo + h * HDP, ldo, Foh);
-        ldfrag(Ol + win * TOK * ldo + h * HDP, ldo, Fol);
+        f16x8 Foh[2], Fol[2];
+        ldfrag(O + win * TOK * ldo + h * HDP, ldo, w, Foh);
+        ldfrag(Ol + win * TOK * ldo + h * HDP, ldo, w, Fol);
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int s = 0; s < 2; ++s) {
+          const f16x8 gh = w ? Fgh[1][s] : Fgh[0][s], gl = w ? Fgl[1][s] : Fgl[0][s];
 #pragma unroll
-          for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              dsum[t] += ((float)Fgh[t][s][j] + (float)Fgl[t][s][j]) * ((float)Foh[t][s][j] + (float)Fol[t][s][j]) * s_o;
+          for (int j = 0; j < 8; ++j) dsum += ((float)gh[j] + (float)gl[j]) * ((float)Foh[s][j] + (float)Fol[s][j]) * s_o;
+        }
       } else {   // fp32 O (natural units)
         const float* Of = (const float*)O + win * TOK * ldo + h * HDP;
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int s = 0; s < 2; ++s) {
+          const float* op = Of + (long)(w * 32 + l31) * ldo + 16 * s + 8 * hh;
+          const float4 a = *(const float4*)op, b = *(const float4*)(op + 4);
+          const float ov[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          const f16x8 gh = w ? Fgh[1][s] : Fgh[0][s], gl = w ? Fgl[1][s] : Fgl[0][s];
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const float* op = Of + (long)(t * 32 + l31) * ldo + 16 * s + 8 * hh;
-            const float4 a = *(const float4*)op, b = *(const float4*)(op + 4);
-            const float ov[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-            for (int j = 0; j < 8; ++j) dsum[t] += ((float)Fgh[t][s][j] + (float)Fgl[t][s][j]) * ov[j];
-          }
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        float d = dsum[t];
-        d += __shfl_xor(d, 32, 64);
-        if (hh == 0) {
-          sRow[0][t * 32 + l31] = lse[(win * nh + h) * TOK + t * 32 + l31];
-          sRow[1][t * 32 + l31] = d * s_g;
+          for (int j = 0; j < 8; ++j) dsum += ((float)gh[j] + (float)gl[j]) * ov[j];
         }
+      }
+      dsum += __shfl_xor(dsum, 32, 64);
+      if (hh == 0) {
+        sRow[0][w * 32 + l31] = lse[(win * nh + h) * TOK + w * 32 + l31];
+        sRow[1][w * 32 + l31] = dsum * s_g;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-            dP[qt][kt] = mfma32(Fgh[qt][s], Fvh[kt][s], dP[qt][kt]);
-            dP[qt][kt] = mfma32(Fgh[qt][s], Fvl[kt][s], dP[qt][kt]);
-            dP[qt][kt] = mfma32(Fgl[qt][s], Fvh[kt][s], dP[qt][kt]);
-          }
+        for (int qt = 0; qt < 2; ++qt) {
+          dP[qt] = mfma32(Fgh[qt][s], Fvh[s], dP[qt]);
+          dP[qt] = mfma32(Fgh[qt][s], Fvl[s], dP[qt]);
+          dP[qt] = mfma32(Fgl[qt][s], Fvh[s], dP[qt]);
+        }
     }
-    sReg[lane] = shift > 0 ? token_region((int)(win % nW), lane, H, W, shift) : 0;
-    wave_sync();
+    if (w == 0) sReg[lane] = shift > 0 ? token_region((int)(win % nW), lane, H, W, shift) : 0;
+    __syncthreads();   // the q / dO tiles, lse / delta and the token regions of both halves
 
     // P = exp(S*scale + bias + mask - lse) ; dS = P (dP - delta), natural units.  Lane = key ki, register r
     // of tile qt = query 32 qt + 8 (r/4) + r%4 + 4 hh: every LDS operand at a compile-time offset from a
@@ -346,9 +349,7 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
     const float* rd = &sRow[1][4 * hh];
     const int* rg = &sReg[4 * hh];
     const float sqk = scale * s_qk;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const int ki = kt * 32 + l31;
+    {
       const int rk = sReg[ki];
       const float* tb = &sTab[15 * (WS - 1 - (ki >> 3)) + (WS - 1 - (ki & 7)) + 4 * hh];
       float* dbl = sDB + 4 * hh * LDB + ki;
@@ -373,24 +374,23 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const int r = r0 + u;
-            const float p = __expf(fmaf(S[qt][kt][r], sqk, tv[u]) - lv[u]);
-            S[qt][kt][r] = p;
-            const float d = p * (dP[qt][kt][r] * s_dp - dv[u]);
-            dP[qt][kt][r] = d;
+            const float p = __expf(fmaf(S[qt][r], sqk, tv[u]) - lv[u]);
+            S[qt][r] = p;
+            const float d = p * (dP[qt][r] * s_dp - dv[u]);
+            dP[qt][r] = d;
             bv[u] += d;
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) dbl[(32 * qt + 8 * ((r0 + u) >> 2) + ((r0 + u) & 3)) * LDB] = bv[u];
         }
     }
-    // dV^T = dO^T P and dK^T = scale * Q^T dS : tiles [kt], rows = d, lane = key; token-row outputs carrying
-    // e_grad (dS enters as the pair of dS 2^e_grad)
+    // dV^T = dO^T P and dK^T = scale * Q^T dS of the wave's keys: rows = d, lane = key; token-row outputs
+    // carrying e_grad (dS enters as the pair of dS 2^e_grad)
     f16* dq_out = dqkv + win * TOK * tstr + h * HDP;
     f16* dql_out = dqkvl ? dqkvl + win * TOK * tstr + h * HDP : nullptr;
     float* dqf = (float*)dqkv + win * TOK * tstr + h * HDP;
     const long koff = (long)nh * HDP, voff = 2L * nh * HDP;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    {
       f32x16 av, ak;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { av[r] = 0.f; ak[r] = 0.f; }
@@ -402,8 +402,8 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
           const f16x8 gl = hrows_perm(sQG[1] + TOK * LD, qt * 32, s, lane);
           const f16x8 qh = hrows_perm(sQG[0], qt * 32, s, lane), ql = hrows_perm(sQG[1], qt * 32, s, lane);
           f16x8 ph, pl, dh, dl;
-          pack8_pair(S[qt][kt], s, s_p, ph, pl);
-          pack8_pair(dP[qt][kt], s, s_gup, dh, dl);
+          pack8_pair(S[qt], s, s_p, ph, pl);
+          pack8_pair(dP[qt], s, s_gup, dh, dl);
           av = mfma32(gh, ph, av);
           av = mfma32(gh, pl, av);
           av = mfma32(gl, ph, av);
@@ -411,7 +411,6 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
           ak = mfma32(qh, dl, ak);
           ak = mfma32(ql, dh, ak);
         }
-      const long key = kt * 32 + l31;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float va[4], ka[4];
@@ -420,7 +419,7 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
           va[j] = av[4 * g + j] * s_dv;
           ka[j] = ak[4 * g + j] * (scale * s_dk);
         }
-        const long o = key * tstr + 8 * g + 4 * hh;
+        const long o = (long)ki * tstr + 8 * g + 4 * hh;
         if (dqkvl) {
           f16x4 vh, vl, kh, kl;
           pair4(va, 1.f, vh, vl);
@@ -435,40 +434,51 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
         }
       }
     }
-    // dQ^T = scale * K^T dS^T : the dS pair through LDS ([q][key] row-major), over the q / dO tiles
-    wave_sync();   // the dV / dK fragment reads of q and dO are complete
+    // dQ^T = scale * K^T dS^T, each wave over its keys: its dS pair [q][32 keys] through its half of sQG
+    __syncthreads();   // both waves' dV / dK fragment reads of the q / dO tiles are complete
+    f16* dsh = sQG[0] + w * TOK * LD;
+    f16* dsl = sQG[1] + w * TOK * LD;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float v = dP[qt][kt][r] * s_gup;
-          const f16 vh = (f16)v;
-          const int o = (qt * 32 + acc_row(r, hh)) * LDD + kt * 32 + l31;
-          sQG[0][o] = vh;
-          sQG[1][o] = (f16)(v - (float)vh);
-        }
-    wave_sync();
+      for (int r = 0; r < 16; ++r) {
+        const float v = dP[qt][r] * s_gup;
+        const f16 vh = (f16)v;
+        const int o = (qt * 32 + acc_row(r, hh)) * LD + l31;
+        dsh[o] = vh;
+        dsl[o] = (f16)(v - (float)vh);
+      }
+    wave_sync();   // (the wave reads back only its own tile)
+    f32x16 aq[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-      f32x16 aq;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) aq[r] = 0.f;
+      for (int r = 0; r < 16; ++r) aq[qt][r] = 0.f;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const f16x8 kh = hrows_nat(sK[0], 0, s, lane), kl = hrows_nat(sK[1], 0, s, lane);
-        const f16x8 dh = hcols(sQG[0], LDD, qt * 32 + l31, s, lane), dl = hcols(sQG[1], LDD, qt * 32 + l31, s, lane);
-        aq = mfma32(kh, dh, aq);
-        aq = mfma32(kh, dl, aq);
-        aq = mfma32(kl, dh, aq);
+      for (int s = 0; s < 2; ++s) {
+        const f16x8 kh = hrows_nat(sK[w][0], 0, s, lane), kl = hrows_nat(sK[w][1], 0, s, lane);
+        const f16x8 dh = hcols(dsh, LD, qt * 32 + l31, s, lane), dl = hcols(dsl, LD, qt * 32 + l31, s, lane);
+        aq[qt] = mfma32(kh, dh, aq[qt]);
+        aq[qt] = mfma32(kh, dl, aq[qt]);
+        aq[qt] = mfma32(kl, dh, aq[qt]);
       }
-      const long qi = qt * 32 + l31;
+    }
+    // the two key halves' partials: wave w finishes the queries of tile qt = w, the other tile's partial goes
+    // to the partner through this wave's exchange slot (its k tile is no longer read)
+    wave_sync();
+    const f32x16 aqs = w ? aq[0] : aq[1], aqk = w ? aq[1] : aq[0];   // (selects, not a run-time register index)
+    float* xo = (float*)&sK[w][0][0];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xo[r * 64 + lane] = aqs[r];
+    __syncthreads();
+    const float* xi = (const float*)&sK[1 - w][0][0];
+    {
+      const long qi = w * 32 + l31;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float qa[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) qa[j] = aq[4 * g + j] * (scale * s_dk);
+        for (int j = 0; j < 4; ++j) qa[j] = (aqk[4 * g + j] + xi[(4 * g + j) * 64 + lane]) * (scale * s_dk);
         if (dqkvl) {
           f16x4 qh, ql;
           pair4(qa, 1.f, qh, ql);
@@ -480,10 +490,9 @@ __global__ __launch_bounds__(64, 1) void attn_bwd_x3_kernel(const f16* __restric
       }
     }
   }
-  // partial bias gradient of this (group, head), binned (the k tiles are free scratch now)
-  wave_sync();
-  static_assert(2 * TOK * LD * sizeof(f16) >= 1024 * sizeof(float), "bin scratch");
-  bin_dbias<true>(sDB, LDB, (float*)sK, dB_part + (grp * nh + h) * NBIN, lane);
+  // partial bias gradient of this (group, head), binned by wave 0 (its k tile is free scratch now)
+  __syncthreads();
+  if (w == 0) bin_dbias<true>(sDB, LDB, (float*)&sK[0][0][0], dB_part + (grp * nh + h) * NBIN, lane);
 }
 
 int g_x3_cus = 0;
@@ -500,7 +509,7 @@ int x3_cus() {
 }  // namespace
 
 // windows per backward wave: enough (group, head) waves for ONE round at the residency the backward's LDS
-// allows (3 one-wave workgroups of ~50 KB per CU; kair_window_attn_bwd_groups / _ws size the partials from it)
+// allows (3 two-wave workgroups of ~50 KB per CU; kair_window_attn_bwd_groups / _ws size the partials from it)
 long kair_attn_x3_wpg(long nWin, int nh) {
   const long slots = 3L * x3_cus();
   const long w = (nWin * nh + slots - 1) / slots;
@@ -543,7 +552,7 @@ extern "C" int kair_window_attn_bwd_x3(const void* qkv, const void* qkv_lo, cons
   const long ngroups = (nWin + wpg - 1) / wpg;
   hipStream_t s = (hipStream_t)stream;
   KAIR_CHECK_ARG(e_act > -60 && e_act < 60 && e_grad > -60 && e_grad < 60, "window_attn_bwd_x3: exponents");
-  hipLaunchKernelGGL(attn_bwd_x3_kernel, dim3((unsigned)(ngroups * nh)), dim3(64), 0, s, (const f16*)qkv, (const f16*)qkv_lo,
+  hipLaunchKernelGGL(attn_bwd_x3_kernel, dim3((unsigned)(ngroups * nh)), dim3(64 * BWD_NW), 0, s, (const f16*)qkv, (const f16*)qkv_lo,
                      (const f16*)O, (const f16*)O_lo, ldo, (const f16*)dO, (const f16*)dO_lo, lddo, table, lse, (f16*)dqkv,
                      (f16*)dqkv_lo, ws, nWin, nh, (int)wpg, scale, H, W, shift, e_act, e_grad);
   KAIR_CHECK_LAUNCH();
