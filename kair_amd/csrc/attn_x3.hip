@@ -58,7 +58,7 @@ KAIR_DEV void pair4(const float (&v)[4], float sc, f16x4& hi, f16x4& lo) {
 // S^T = K Q^T operands), v hi / lo planes staged in LDS for the transposed P.V fragments; O^T = V^T P^T
 // (lane = query) stored 8 bytes per plane per register group.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64 * FWD_NW) void attn_fwd_x3_kernel(const f16* __restrict__ qkv, const f16* __restrict__ qkvl,
+__global__ __launch_bounds__(64 * FWD_NW, 3) void attn_fwd_x3_kernel(const f16* __restrict__ qkv, const f16* __restrict__ qkvl,
                                                                   const float* __restrict__ table, f16* __restrict__ O,
                                                                   f16* __restrict__ Ol, long ldo, float* __restrict__ lse,
                                                                   long nWin, int nh, float scale, int H, int W, int shift,

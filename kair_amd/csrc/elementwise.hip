@@ -589,6 +589,41 @@ __global__ void l1_pix16_kernel(const float* __restrict__ E, const float* __rest
   if (threadIdx.x == 0) ws[blockIdx.x] = red[0];
 }
 
+// fp32 gradient rows of 4 slots per pixel (C <= 4; the fp32x3 engine's conv_last narrow kernels read 4 channels):
+// one thread per pixel, one 16-byte store
+template <bool CH>
+__global__ void l1_pix4f_kernel(const float* __restrict__ E, const float* __restrict__ H, float* __restrict__ dE,
+                                float gscale, int C, int HW, int npix, float* __restrict__ ws, float eps) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += gridDim.x * blockDim.x) {
+    const int b = pix / HW, pp = pix - b * HW;
+    float g4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c >= C) break;
+      const long i = ((long)b * C + c) * HW + pp;
+      const float d = E[i] - H[i];
+      if constexpr (CH) {
+        const float q = sqrtf(d * d + eps);
+        s += q;
+        g4[c] = q > 0.f ? gscale * d / q : 0.f;
+      } else {
+        s += fabsf(d);
+        g4[c] = d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f);
+      }
+    }
+    *(float4*)(dE + (long)pix * 4) = make_float4(g4[0], g4[1], g4[2], g4[3]);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ws[blockIdx.x] = red[0];
+}
+
 __global__ void l1_final(const float* __restrict__ ws, int nb, float scale, float* out) {
   __shared__ float red[256];
   float s = 0.f;
@@ -890,8 +925,11 @@ static int pixel_loss(const float* E, const float* H, float* loss_out, void* dE,
   const float gs = (float)(weight / numel);
   // int indices when the largest index (dE element or image element) and the grid stride fit
   const bool i32 = (double)npix * ldc < 2.0e9 && numel < 2.0e9;
-  if (ps_r == 1 && ldc == 16 && C <= 4 && dtype == KAIR_BF16 && npix < (1L << 31) && ((uintptr_t)dE & 15) == 0) {
-    if (charb) hipLaunchKernelGGL(l1_pix16_kernel<true>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
+  const bool pix4f = ps_r == 1 && ldc == 4 && C <= 4 && dtype == KAIR_F32 && npix < (1L << 31) && ((uintptr_t)dE & 15) == 0;
+  if (pix4f || (ps_r == 1 && ldc == 16 && C <= 4 && dtype == KAIR_BF16 && npix < (1L << 31) && ((uintptr_t)dE & 15) == 0)) {
+    if (pix4f && charb) hipLaunchKernelGGL(l1_pix4f_kernel<true>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
+    else if (pix4f) hipLaunchKernelGGL(l1_pix4f_kernel<false>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
+    else if (charb) hipLaunchKernelGGL(l1_pix16_kernel<true>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
     else hipLaunchKernelGGL(l1_pix16_kernel<false>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
     KAIR_CHECK_LAUNCH();
     hipLaunchKernelGGL(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);

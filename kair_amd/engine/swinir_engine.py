@@ -576,7 +576,10 @@ class SwinIREngine:
         P["loss_ws"] = e(1024)
         P["colsum_ws"] = e(1024 * 256)
         if self.upsampler == "pixelshuffle":
-            P["dE"] = e(P["M_hr"], 16, dt=T)
+            # the HR-image gradient rows: 4 fp32 slots when only the fp32x3 narrow kernels read them (conv_last at
+            # an HR width % 64 == 0), else the 16 slots of the implicit-GEMM conv_last's K = 9 x 16
+            P["dE_ld"] = 4 if self.last_narrow_x3 and (Ww * self.scale) % 64 == 0 else 16
+            P["dE"] = e(P["M_hr"], P["dE_ld"], dt=T)
             if self.last.narrow or self.last_narrow_x3:
                 P["narrow_ws"] = e(H.conv3x3_narrow_wgrad_ws(self.in_ch))
                 P["narrow_dws"] = e(H.conv3x3_narrow_x3_ws() if self.x3 else H.conv3x3_narrow_dgrad_ws())
@@ -956,8 +959,8 @@ class SwinIREngine:
             H.l1_loss(P["E"], H_img, P["loss"], P["dE"], self.up1.Cop, wr, B, self.in_ch, Hh * self.scale,
                       Ww * self.scale, P["loss_ws"], ps_r=self.scale, charb_eps=charb_eps)
         else:
-            H.l1_loss(P["E"], H_img, P["loss"], P["dE"], 16, wr, B, self.in_ch, Hh * self.scale, Ww * self.scale,
-                      P["loss_ws"], charb_eps=charb_eps)
+            H.l1_loss(P["E"], H_img, P["loss"], P["dE"], P.get("dE_ld", 16), wr, B, self.in_ch, Hh * self.scale,
+                      Ww * self.scale, P["loss_ws"], charb_eps=charb_eps)
         if self.img_range != 1.0:
             P["loss"].mul_(self.img_range)
         self.backward(grads, P)
@@ -974,7 +977,8 @@ class SwinIREngine:
             mx = float(gE.abs().max()) * inv
             P["e_g"] = 8 - int(math.ceil(math.log2(mx))) if mx > 0 and math.isfinite(mx) else 0   # max -> <= 2^8
         if self.upsampler != "pixelshuffledirect":
-            H.image_to_nhwc(gE.contiguous(), P["dE"], 16, None, inv, B, self.in_ch, Hh * self.scale, Ww * self.scale)
+            H.image_to_nhwc(gE.contiguous(), P["dE"], P.get("dE_ld", 16), None, inv, B, self.in_ch, Hh * self.scale,
+                            Ww * self.scale)
         else:
             tmp = torch.nn.functional.pixel_unshuffle(gE.contiguous(), self.scale)   # [B, C*r*r, H, W]
             H.image_to_nhwc(tmp.contiguous(), P["dE"], self.up1.Cop, None, inv, B, tmp.shape[1], Hh, Ww)
@@ -997,9 +1001,9 @@ class SwinIREngine:
             # conv_last: dgrad into the pre-shuffle layout of the last upsampling conv
             r_last = self.ups_r[-1]
             if self.last_narrow_x3 and w % 64 == 0:
-                H.conv3x3_narrow_dgrad_x3(P["dE"], 16, P["e_g"], c.w.detach(), self.in_ch, P["narrow_dws"], P["dpre"][-1],
+                H.conv3x3_narrow_dgrad_x3(P["dE"], P["dE_ld"], P["e_g"], c.w.detach(), self.in_ch, P["narrow_dws"], P["dpre"][-1],
                                           self.ups[-1].Co, r_last, B, h, w)
-                H.conv3x3_narrow_wgrad_x3(P["dE"], 16, P["e_g"], src, tl, self.X3_AEXP, self.in_ch, P["narrow_ws"], g(c.w),
+                H.conv3x3_narrow_wgrad_x3(P["dE"], P["dE_ld"], P["e_g"], src, tl, self.X3_AEXP, self.in_ch, P["narrow_ws"], g(c.w),
                                           g(c.b), B, h, w)
             elif c.narrow and w % 64 == 0:   # the narrow-output kernels (rolling row window, fp32 master weight)
                 H.conv3x3_narrow_dgrad(P["dE"], 16, c.w.detach(), self.in_ch, P["narrow_dws"], P["dpre"][-1], self.ups[-1].Co,
