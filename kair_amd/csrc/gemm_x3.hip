@@ -462,18 +462,33 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
   };
   // issue cursors: A chunk (tile at, k-chunk ak, stage as_), B k-chunk bk in stage bs
   int at = 0, ak = 0, as_ = 0, bk = 0, bs = 0;
+  // im2col: the current tap and channel offset (k = tap * C + c0, advanced per chunk: K = 9 C, C % 32 == 0) and
+  // the lane's two source pixel rows for that tap (nullptr: outside the image / past M), recomputed per tap
+  int a_tap = 0, a_c0 = 0;
+  const float* arow[2] = {nullptr, nullptr};
+  auto set_tap = [&]() __attribute__((always_inline)) {
+    int dy = a_tap / 3 - 1, dx = a_tap - (a_tap / 3) * 3 - 1;
+    if (A.flip) { dy = -dy; dx = -dx; }
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int y = ay[ii] + dy, x = ax[ii] + dx;
+      arow[ii] = aok[ii] && y >= 0 && y < A.imH && x >= 0 && x < A.imW
+                     ? (const float*)A.ptr + (aoff[ii] + (long)(y >> A.up_sh) * (A.imW >> A.up_sh) + (x >> A.up_sh)) * A.ld +
+                           au[ii] * 4
+                     : nullptr;
+    }
+  };
   auto issue_a = [&]() __attribute__((always_inline)) {
-    if (ak == 0) load_rows(at);
+    if (ak == 0) {
+      load_rows(at);
+      if constexpr (AM == AM_IM2COL) {
+        a_tap = 0;
+        a_c0 = 0;
+        set_tap();
+      }
+    }
     const int k0 = ak * 32;
     char* st = sA + as_ * XR_ASTAGE;
-    int dy = 0, dx = 0, c0 = k0;
-    if constexpr (AM == AM_IM2COL) {
-      const int tap = fdiv(k0, A.d_imC);
-      c0 = k0 - tap * A.imC;
-      dy = tap / 3 - 1;
-      dx = tap - (tap / 3) * 3 - 1;
-      if (A.flip) { dy = -dy; dx = -dx; }
-    }
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii) {
       const void* src = zero;
@@ -483,12 +498,16 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       } else if constexpr (AM == AM_ROWS) {
         if (aok[ii]) src = (const float*)A.ptr + aoff[ii] + k0 + au[ii] * 4;
       } else {
-        const int y = ay[ii] + dy, x = ax[ii] + dx;
-        if (aok[ii] && y >= 0 && y < A.imH && x >= 0 && x < A.imW)
-          src = (const float*)A.ptr + (aoff[ii] + (long)(y >> A.up_sh) * (A.imW >> A.up_sh) + (x >> A.up_sh)) * A.ld + c0 +
-                au[ii] * 4;
+        if (arow[ii]) src = arow[ii] + a_c0;
       }
       if (!KAIR_DBG(E.dbg & 36)) glds16(src, st + (wave * 2 + ii) * 1024);
+    }
+    if constexpr (AM == AM_IM2COL) {
+      a_c0 += 32;
+      if (a_c0 == A.imC) {
+        a_c0 = 0;
+        if (++a_tap < 9) set_tap();
+      }
     }
     if (++ak == nk) { ak = 0; ++at; }
     if (++as_ == NA) as_ = 0;
@@ -710,7 +729,16 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
     int e1 = 0, e2 = 0;   // non-DMA vector-memory instructions this wave issued in intervals t-1, t-2
     for (int t = 0; t <= total; ++t) {
       stamp(t, 0);
-      if (t < total) vm_wait(e2 + nA(t - 1) + nB(t - 1) + e1);   // chunk t (its B part: issued in interval t-2)
+      if (t < total) {   // chunk t (its B part: issued in interval t-2)
+        const int n = e2 + nA(t - 1) + nB(t - 1) + e1;
+        if (n == 2 + BI) {   // the steady state (no epilogue stores pending): one immediate wait, not the branch tree
+          if constexpr (BI == 3) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+          else if constexpr (BI == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        } else {
+          vm_wait(n);
+        }
+      }
       stamp(t, 1);
       ring_barrier();   // chunk t is in LDS for every wave; chunk t-1's stages are free
       if (nA(t)) issue_a();
@@ -984,7 +1012,8 @@ bool nt_x3_ring_ok(const kair_operand* A, const kair_operand* B, const kair_epil
       return false;
   }
   if (A->mode == KAIR_LD_ROWS) return A->dtype == KAIR_F16 ? A->ld % 8 == 0 : A->ld % 4 == 0;
-  return A->mode == KAIR_LD_IM2COL3 && A->dtype == KAIR_F32 && A->im_C % 32 == 0 && (A->ld == 0 ? A->im_C : A->ld) % 4 == 0;
+  return A->mode == KAIR_LD_IM2COL3 && A->dtype == KAIR_F32 && A->im_C % 32 == 0 && K == 9 * A->im_C &&
+         (A->ld == 0 ? A->im_C : A->ld) % 4 == 0;
 }
 
 template <typename TA, int AM, int BN>
