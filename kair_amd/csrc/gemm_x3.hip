@@ -794,6 +794,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
 constexpr int XT_RB = 32, XT_NS = 3;
 constexpr int XT_PART = XT_RB * 192 * 4, XT_STAGE = 2 * XT_PART;   // 24 + 24 KiB
 constexpr int XT_DMA = 6;   // DMA wave-instructions per wave per chunk (3 A + 3 B)
+static_assert(XT_DMA * (XT_NS - 2) == 6, "the steady-state wait immediate in gemm_tn_x3_ring");
 enum { BT_ROWS = 0, BT_TAP = 1 };
 
 template <int BT>
@@ -829,6 +830,28 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
     dx = tap - (tap / 3) * 3 - 1;
   }
   int lc = 0, ls = 0;   // next chunk to issue, its stage
+  // Identity row maps (the engine's operands: both in token order or both in window order): each lane's three
+  // source rows advance by XT_RB rows per chunk, so the addresses are kept as running pointers (and, for the
+  // tap form, the row's pixel column / row for the halo test) instead of being rebuilt per chunk
+  const bool lin = A.win.ws == 0 && (BT == BT_TAP || B.win.ws == 0);
+  const float* pa[3];
+  const float* pb[3];
+  int px[3], py[3];
+#pragma unroll
+  for (int ii = 0; ii < 3; ++ii) {
+    const long m = mbeg + dr[ii];
+    pa[ii] = (const float*)A.ptr + m * A.ld + (dcA[ii] >= 0 ? dcA[ii] : 0);
+    if constexpr (BT == BT_ROWS) {
+      pb[ii] = (const float*)B.ptr + m * B.ld + (dcB[ii] >= 0 ? dcB[ii] : 0);
+      px[ii] = py[ii] = 0;
+    } else {
+      const int mm = m < M ? (int)m : 0;
+      const int p = mm - fdiv(mm, B.d_hw) * B.d_hw.d;
+      py[ii] = fdiv(p, B.d_imW);
+      px[ii] = p - py[ii] * B.imW;
+      pb[ii] = (const float*)B.ptr + (m + (long)dy * B.imW + dx) * B.ld + (dcB[ii] >= 0 ? dcB[ii] : 0);
+    }
+  }
   auto issue_next = [&]() {
     char* st = smem + ls * XT_STAGE;
     const int m0 = mbeg + lc * XT_RB;
@@ -836,19 +859,36 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
     for (int ii = 0; ii < 3; ++ii) {
       const int m = m0 + dr[ii];
       const bool ok = m < mend;
-      const int mm = ok ? m : 0;
       const void* sa = zero;
-      if (ok && dcA[ii] >= 0) sa = (const float*)A.ptr + (long)win_to_token32(mm, A.win) * A.ld + dcA[ii];
       const void* sb = zero;
-      if constexpr (BT == BT_ROWS) {
-        if (ok && dcB[ii] >= 0) sb = (const float*)B.ptr + (long)win_to_token32(mm, B.win) * B.ld + dcB[ii];
+      if (lin) {
+        if (ok && dcA[ii] >= 0) sa = pa[ii];
+        if constexpr (BT == BT_ROWS) {
+          if (ok && dcB[ii] >= 0) sb = pb[ii];
+        } else {
+          const int yy = py[ii] + dy, xx = px[ii] + dx;
+          if (ok && dcB[ii] >= 0 && yy >= 0 && yy < B.imH && xx >= 0 && xx < B.imW) sb = pb[ii];
+          px[ii] += XT_RB;
+          while (px[ii] >= B.imW) {   // (once per chunk for image widths >= 32)
+            px[ii] -= B.imW;
+            if (++py[ii] == B.imH) py[ii] = 0;
+          }
+        }
+        pa[ii] += (long)XT_RB * A.ld;
+        pb[ii] += (long)XT_RB * B.ld;
       } else {
-        const int hw = B.d_hw.d;
-        const int b = fdiv(mm, B.d_hw), p = mm - b * hw;
-        const int y = fdiv(p, B.d_imW), x = p - y * B.imW;
-        const int yy = y + dy, xx = x + dx;
-        if (ok && dcB[ii] >= 0 && yy >= 0 && yy < B.imH && xx >= 0 && xx < B.imW)
-          sb = (const float*)B.ptr + ((long)b * hw + (long)yy * B.imW + xx) * B.ld + dcB[ii];
+        const int mm = ok ? m : 0;
+        if (ok && dcA[ii] >= 0) sa = (const float*)A.ptr + (long)win_to_token32(mm, A.win) * A.ld + dcA[ii];
+        if constexpr (BT == BT_ROWS) {
+          if (ok && dcB[ii] >= 0) sb = (const float*)B.ptr + (long)win_to_token32(mm, B.win) * B.ld + dcB[ii];
+        } else {
+          const int hw = B.d_hw.d;
+          const int b = fdiv(mm, B.d_hw), p = mm - b * hw;
+          const int y = fdiv(p, B.d_imW), x = p - y * B.imW;
+          const int yy = y + dy, xx = x + dx;
+          if (ok && dcB[ii] >= 0 && yy >= 0 && yy < B.imH && xx >= 0 && xx < B.imW)
+            sb = (const float*)B.ptr + ((long)b * hw + (long)yy * B.imW + xx) * B.ld + dcB[ii];
+        }
       }
       glds16(sa, st + (wave * 3 + ii) * 1024);
       glds16(sb, st + XT_PART + (wave * 3 + ii) * 1024);
@@ -881,7 +921,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
   int cs = 0;
   for (int j = 0; j < nch; ++j) {
     const int ahead = (nch - 1 - j) < (XT_NS - 2) ? (nch - 1 - j) : (XT_NS - 2);
-    vm_wait(XT_DMA * ahead);
+    if (ahead == XT_NS - 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // XT_DMA * (XT_NS - 2): steady state
+    else vm_wait(XT_DMA * ahead);
     ring_barrier();   // chunk j in LDS for every wave; stage (j - 1) % NS free
     if (lc < nch) issue_next();
     const char* st = smem + cs * XT_STAGE;
