@@ -92,7 +92,7 @@ class _Lin:
         dev = self.w.device
         # fp32x3 engine: the rows forms hold fp16 pairs of w 2^KAIR_X3_WEXP interleaved per 64 columns (pack
         # kinds 17 / 19), multiplied hi.hi + hi.lo + lo.hi by kair_gemm_nt (compute KAIR_COMPUTE_X3)
-        self.x3 = eng.x3
+        self.x3 = getattr(eng, "x3", False)
         if self.x3:   # (self.map stays the plain kind-0 map: the weight gradient's finalize layout)
             self.pmap, self.pmapT = H.wmap(17, N, K, n_grp, k_grp), H.wmap(19, N, K, n_grp, k_grp)
             self.Wp = torch.empty(self.Np, 2 * _rup(self.Kp, 64), device=dev, dtype=torch.float16) if rows else None
@@ -151,8 +151,9 @@ class _Conv:
         self.Co, self.Ci, self.Cop, self.Cip = Co, Ci, Cop, Cip
         if split is None:
             split = getattr(eng, "split_conv", False)
-        self.split = (bool(split) and eng.tdt == torch.bfloat16) or eng.x3
-        self.x3 = eng.x3
+        x3 = getattr(eng, "x3", False)   # (the RRDBNet / USRNet engines share this class and have no x3 form)
+        self.split = (bool(split) and eng.tdt == torch.bfloat16) or x3
+        self.x3 = x3
         self.n_perm = n_perm
         self.map = H.wmap(1, Co, Ci, (1, Co, Cop), (1, Ci, Cip), n_perm=n_perm)
         fcip = fwd_cip or Cip
