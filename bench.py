@@ -235,13 +235,23 @@ def rocprof_name(fn, a):
     if fn == "gemm_nt" and a[6] == X3:
         return "gemm_nt_x3_ring" if _x3_ring_nt(a) else "gemm_nt_x3_kernel"
     if fn == "gemm_tn" and a[7] == X3:
-        return "gemm_tn_x3_ring" if a[0].dtype == 0 and a[1].dtype == 0 and a[5] % 4 == 0 else "gemm_tn_x3_kernel"
+        return "gemm_tn_x3_ring" if _x3_ring_tn(a) else "gemm_tn_x3_kernel"
     if fn == "window_attn_fwd_x3":
         return "attn_fwd_x3_kernel"
     if fn == "window_attn_bwd_x3":
         return "attn_bwd_x3_kernel"
     return {"conv3x3_wr": "conv3x3_wr_kernel", "swin_mlp_fwd": "swin_mlp_fwd_wr_kernel", "swin_attn_fwd": "swin_attn_fwd12_kernel<6>",   # KAIR_ATTN12 (swin_fused.hip)
             "window_attn_bwd": "attn_bwd_bf16_kernel<2>"}.get(fn, fn)
+
+
+def _x3_ring_tn(a):
+    """Whether an x3 gemm_tn launch takes the ring kernel (gemm_x3.hip tn_x3_ring_ok)."""
+    A, B, N, K = a[0], a[1], a[5], a[6]
+    ones_ok = lambda o: o.ones_col < 0 or o.ones_in_data
+    return (A.dtype == 0 and B.dtype == 0 and A.mode == 0 and N % 4 == 0 and K % 4 == 0 and ones_ok(A)
+            and not A.rowscale and not B.rowscale and
+            (B.mode == 0 or (B.mode == 1 and B.im_C % 4 == 0 and K == 9 * B.im_C and not B.im_flip and B.im_up != 2
+                              and N % 192 == 0)))
 
 
 def _x3_ring_nt(a):

@@ -201,6 +201,34 @@ KAIR_DEV void gelu_pair_fast2(f32x2 x, f32x2& y, f32x2& dy) {
   y = x * cdf;
   dy = cdf + x * 0.39894228040143268f * e;
 }
+// erf_f32 / GELU / GELU' of two elements at once: both polynomials as packed fp32 (v_pk_fma_f32 / v_pk_mul_f32,
+// two elements per instruction); exp, compares and selects stay per element.  The same arithmetic as erf_f32,
+// gelu_erf and gelu_erf_grad, element for element
+KAIR_DEV f32x2 erf_f32x2(f32x2 a) {
+  const f32x2 t = {fabsf(a.x), fabsf(a.y)}, s = a * a;
+  f32x2 p = {-5.96761703e-4f, -5.96761703e-4f};
+  p = __builtin_elementwise_fma(p, s, (f32x2){4.99119423e-3f, 4.99119423e-3f});
+  p = __builtin_elementwise_fma(p, s, (f32x2){-2.67681349e-2f, -2.67681349e-2f});
+  p = __builtin_elementwise_fma(p, s, (f32x2){1.12819925e-1f, 1.12819925e-1f});
+  p = __builtin_elementwise_fma(p, s, (f32x2){-3.76125336e-1f, -3.76125336e-1f});
+  p = __builtin_elementwise_fma(p, s, (f32x2){1.28379166e-1f, 1.28379166e-1f});
+  p = __builtin_elementwise_fma(p, a, a);
+  f32x2 r = __builtin_elementwise_fma((f32x2){-1.72853470e-5f, -1.72853470e-5f}, t, (f32x2){3.83197126e-4f, 3.83197126e-4f});
+  const f32x2 u = __builtin_elementwise_fma((f32x2){-3.88396438e-3f, -3.88396438e-3f}, t, (f32x2){2.42546219e-2f, 2.42546219e-2f});
+  r = __builtin_elementwise_fma(r, s, u);
+  r = __builtin_elementwise_fma(r, t, (f32x2){-1.06777877e-1f, -1.06777877e-1f});
+  r = __builtin_elementwise_fma(r, t, (f32x2){-6.34846687e-1f, -6.34846687e-1f});
+  r = __builtin_elementwise_fma(r, t, (f32x2){-1.28717512e-1f, -1.28717512e-1f});
+  r = __builtin_elementwise_fma(r, t, -t);
+  const f32x2 q = {copysignf(1.0f - __expf(r.x), a.x), copysignf(1.0f - __expf(r.y), a.y)};
+  return (f32x2){t.x > 0.927734375f ? q.x : p.x, t.y > 0.927734375f ? q.y : p.y};
+}
+KAIR_DEV void gelu_erf_pair2(f32x2 x, f32x2& y, f32x2& dy) {
+  const f32x2 cdf = 0.5f * (1.0f + erf_f32x2(x * 0.70710678118654752f));
+  y = x * cdf;
+  const f32x2 e = {__expf(-0.5f * x.x * x.x), __expf(-0.5f * x.y * x.y)};
+  dy = __builtin_elementwise_fma(x * 0.39894228040143268f, e, cdf);
+}
 KAIR_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 KAIR_DEV float gelu_grad_fast(float x) {
   const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));

@@ -665,14 +665,28 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
         } else {
           float pre[8];
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            pre[c] = v[c];
-            if constexpr (ACT == XA_GELU || ACT == XA_GELU_X) {
-              if constexpr (ACT == XA_GELU) pre[c] = gelu_erf_grad(v[c]);
-              v[c] = gelu_erf(v[c]);
-            } else if constexpr (ACT == XA_LEAKY) {
-              v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
+          for (int c = 0; c < 8; ++c) pre[c] = v[c];
+          if constexpr (ACT == XA_GELU) {   // GELU and GELU' of element pairs (packed fp32 polynomials)
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+              f32x2 y2, d2;
+              gelu_erf_pair2((f32x2){v[c], v[c + 1]}, y2, d2);
+              v[c] = y2.x;
+              v[c + 1] = y2.y;
+              pre[c] = d2.x;
+              pre[c + 1] = d2.y;
             }
+          } else if constexpr (ACT == XA_GELU_X) {
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+              const f32x2 x2 = {v[c], v[c + 1]};
+              const f32x2 y2 = x2 * (0.5f * (1.0f + erf_f32x2(x2 * 0.70710678118654752f)));
+              v[c] = y2.x;
+              v[c + 1] = y2.y;
+            }
+          } else if constexpr (ACT == XA_LEAKY) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) v[c] = v[c] > 0.f ? v[c] : v[c] * E.slope;
           }
           if constexpr (EX != EX_NONE) {
             const float x8[8] = {ex[i][p][0].x, ex[i][p][0].y, ex[i][p][0].z, ex[i][p][0].w,
@@ -813,7 +827,9 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
   const float* zero = (const float*)g_kair_zero_line;
 
   // DMA geometry of this lane (the same for every chunk): wave-instruction g covers slots [64 g, 64 g + 64)
-  int dr[3], dcA[3], dcB[3];
+  // tap form: the lane's 4 columns k .. k + 3 of the K = 9 C contraction are channels c .. c + 3 of tap k / C (C % 4
+  // == 0), so each lane reads ONE shifted image (its own dy, dx) for the whole launch
+  int dr[3], dcA[3], dcB[3], dy[3], dx[3];
 #pragma unroll
   for (int ii = 0; ii < 3; ++ii) {
     const int s = (wave * 3 + ii) * 64 + lane;
@@ -821,13 +837,16 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
     const int u = q ^ (((r >> 3) & 3) << 2);
     dr[ii] = r;
     dcA[ii] = n0 + u * 4 < N ? n0 + u * 4 : -1;
-    dcB[ii] = k0 + u * 4 < K ? (BT == BT_TAP ? u * 4 : k0 + u * 4) : -1;
-  }
-  int dy = 0, dx = 0;
-  if constexpr (BT == BT_TAP) {
-    const int tap = k0 / 192;
-    dy = tap / 3 - 1;
-    dx = tap - (tap / 3) * 3 - 1;
+    const int k = k0 + u * 4;
+    dy[ii] = dx[ii] = 0;
+    if constexpr (BT == BT_TAP) {
+      const int tap = k < K ? k / B.imC : 0;
+      dcB[ii] = k < K ? k - tap * B.imC : -1;
+      dy[ii] = tap / 3 - 1;
+      dx[ii] = tap - (tap / 3) * 3 - 1;
+    } else {
+      dcB[ii] = k < K ? k : -1;
+    }
   }
   int lc = 0, ls = 0;   // next chunk to issue, its stage
   // Identity row maps (the engine's operands: both in token order or both in window order): each lane's three
@@ -849,7 +868,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
       const int p = mm - fdiv(mm, B.d_hw) * B.d_hw.d;
       py[ii] = fdiv(p, B.d_imW);
       px[ii] = p - py[ii] * B.imW;
-      pb[ii] = (const float*)B.ptr + (m + (long)dy * B.imW + dx) * B.ld + (dcB[ii] >= 0 ? dcB[ii] : 0);
+      pb[ii] = (const float*)B.ptr + (m + (long)dy[ii] * B.imW + dx[ii]) * B.ld + (dcB[ii] >= 0 ? dcB[ii] : 0);
     }
   }
   auto issue_next = [&]() {
@@ -866,7 +885,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
         if constexpr (BT == BT_ROWS) {
           if (ok && dcB[ii] >= 0) sb = pb[ii];
         } else {
-          const int yy = py[ii] + dy, xx = px[ii] + dx;
+          const int yy = py[ii] + dy[ii], xx = px[ii] + dx[ii];
           if (ok && dcB[ii] >= 0 && yy >= 0 && yy < B.imH && xx >= 0 && xx < B.imW) sb = pb[ii];
           px[ii] += XT_RB;
           while (px[ii] >= B.imW) {   // (once per chunk for image widths >= 32)
@@ -885,7 +904,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
           const int hw = B.d_hw.d;
           const int b = fdiv(mm, B.d_hw), p = mm - b * hw;
           const int y = fdiv(p, B.d_imW), x = p - y * B.imW;
-          const int yy = y + dy, xx = x + dx;
+          const int yy = y + dy[ii], xx = x + dx[ii];
           if (ok && dcB[ii] >= 0 && yy >= 0 && yy < B.imH && xx >= 0 && xx < B.imW)
             sb = (const float*)B.ptr + ((long)b * hw + (long)yy * B.imW + xx) * B.ld + dcB[ii];
         }
@@ -908,6 +927,9 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
     for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const float sa = A.x3s, sb = B.x3s;
+  // B's injected ones column (the bias gradient of a conv weight gradient: k = ones_col reads 1.0 for every row,
+  // whatever the data / halo there), as its K-tile column (-1: none in this tile)
+  const int bones = B.ones_col >= 0 && !B.ones_in_data && B.ones_col >= k0 && B.ones_col < k0 + 192 ? B.ones_col - k0 : -1;
   // a lane's column c of a chunk part: byte (fq * 8 + j) * 768 + slot(c) * 16 + (c & 3) * 4 for rows j = 0..7
   auto frag = [&](const char* part, int c, float s, f16x8& hi, f16x8& lo) {
     const char* p = part + fq * 8 * 768 + ((((c >> 2) ^ (fq << 2))) << 4) + (c & 3) * 4;
@@ -931,6 +953,18 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
     for (int i = 0; i < 6; ++i) frag(st, wn * 96 + i * 16 + fr, sa, ah[i], al[i]);
 #pragma unroll
     for (int i = 0; i < 3; ++i) frag(st + XT_PART, wk * 48 + i * 16 + fr, sb, bh[i], bl[i]);
+    if (bones >= 0) {   // (uniform: only the K tile holding the ones column) its lanes' fragment reads 1.0 in every row
+      const f16 oh = (f16)sb, ol = (f16)(sb - (float)oh);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (wk * 48 + i * 16 + fr == bones) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            bh[i][j] = oh;
+            bl[i][j] = ol;
+          }
+        }
+    }
 #pragma unroll
     for (int ik = 0; ik < 3; ++ik)
 #pragma unroll
@@ -1099,18 +1133,19 @@ int nt_x3_ring_dispatch(const Op& a, const Op& b, const Epi& e, long M, int N, i
   }
 }
 
-// the TN ring: fp32 rows (16-byte aligned, N and K % 4), B rows or the tap-per-tile im2col of a 192-channel
-// map (K = 9 x 192, no flip / upsample); a bias ones column only as data (ones_in_data)
+// the TN ring: fp32 rows (16-byte aligned, N and K % 4), B rows or the per-lane-tap im2col of a C-channel (C % 4)
+// map (K = 9 C, no flip / upsample); B's bias ones column as data (ones_in_data) or injected, A's only as data
 bool tn_x3_ring_ok(const kair_operand* A, const kair_operand* B, int N, int K) {
   static const int off = [] { const char* e = getenv("KAIR_X3_RING"); return e && e[0] == '0'; }();
   if (off || A->dtype != KAIR_F32 || B->dtype != KAIR_F32 || A->mode != KAIR_LD_ROWS || N % 4 || K % 4) return false;
   if (A->ld % 4 || (uintptr_t)A->ptr % 16 || (uintptr_t)B->ptr % 16 || A->rowscale || B->rowscale) return false;
   if (A->ones_col >= 0 && !A->ones_in_data) return false;
-  if (B->ones_col >= 0 && !B->ones_in_data) return false;
   if (B->mode == KAIR_LD_ROWS) return B->ld % 4 == 0;
   const long ld = B->ld == 0 ? B->im_C : B->ld;
-  return B->mode == KAIR_LD_IM2COL3 && B->im_C == 192 && K == 9 * 192 && !B->im_flip && B->im_up != 2 && ld % 4 == 0 &&
-         B->win_ws == 0;
+  // (192-column N tiles: the RSTB / conv_after_body convs; the tail's N = 64 / 256 convs measured faster on the
+  // generic kernel, 190 vs 398 and 428 vs 452 us)
+  return B->mode == KAIR_LD_IM2COL3 && B->im_C % 4 == 0 && K == 9 * B->im_C && !B->im_flip && B->im_up != 2 && ld % 4 == 0 &&
+         B->win_ws == 0 && N % 192 == 0;
 }
 
 // an x3 operand: fp32, or an fp16 hi plane with its 16-byte aligned lo plane

@@ -247,19 +247,23 @@ def test_gemm_nt_x3_ring_epilogues():
         assert rel(out, ref) < 2e-6, mode
 
 
-@pytest.mark.parametrize("conv", [False, True])
+@pytest.mark.parametrize("conv", [None, "c192", "c64"])
 def test_gemm_tn_x3_ring(conv):
     """The LDS-DMA ring form of kair_gemm_tn x3 (fp32 operands, 192 x 192 tiles): ragged splits over 3 N-tiles with
-    the bias ones column carried in B's data, and the tap-per-tile im2col of a 192-channel map (conv weight
-    gradient, K = 9 x 192) -- the split partial planes summed against float64."""
+    the bias ones column carried in B's data, and the per-lane-tap im2col of a C-channel map (conv weight gradient,
+    K = 9 C: the 192-channel RSTB convs, one tap per K tile; the 64-channel upsampling convs with N = 256, three
+    taps per K tile and a partial N tile; an injected bias ones column) -- the split partial planes summed
+    against float64."""
     g = torch.Generator().manual_seed(13)
     if conv:
-        Bn, Hh, Ww, C, N = 2, 12, 20, 192, 192
+        Bn, Hh, Ww, C, N = (2, 12, 20, 192, 192) if conv == "c192" else (2, 16, 40, 64, 256)
         M, K = Bn * Hh * Ww, 9 * C
         x = torch.randn(M, C, generator=g)
         cols = torch.nn.functional.unfold(x.view(Bn, Hh, Ww, C).permute(0, 3, 1, 2).double(), 3, padding=1)
         ref_b = cols.view(Bn, C, 9, Hh * Ww).permute(0, 3, 2, 1).reshape(M, K)
-        Bop = H.im2col(x.to(dev), Hh, Ww, C)
+        oc = C + 7   # an injected bias ones column (tap 1: halo rows included)
+        ref_b[:, oc] = 1.0
+        Bop = H.im2col(x.to(dev), Hh, Ww, C, ones_col=oc)
     else:
         M, N, K = 3000, 576, 192
         x = torch.randn(M, K, generator=g)
