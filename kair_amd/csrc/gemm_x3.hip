@@ -408,13 +408,21 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
 
   // epilogue columns (fixed per CTA): after the permlane swap of fragment pair (2p, 2p + 1) a lane owns
   // columns c8[p] .. + 8 of fragment 2p + (fq & 1); their bias, and (QKV) the column part of the offset
+  // SW: the 16-bit-output and shuffled forms re-lay fragment pair (2p, 2p + 1) with v_permlane16_swap so a lane owns
+  // 8 consecutive columns (16-byte fp16-pair stores); the fp32-row form keeps the MFMA layout, a lane's 4 columns
+  // 4 fq .. + 3 of each fragment (16-byte stores; a store instruction covers 64 contiguous bytes of 16 rows).  A
+  // lane's 8 values are the two 4-column chunks at c8[p] and c8[p] + CB.
+  constexpr bool SW = EM != XE_ROWS_F32;
+  constexpr int CB = SW ? 4 : 16;   // the second chunk's column offset
   int c8[NP], oc[NP];
   long colo[NP];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    const int n = n0 + wn * WC + (2 * p + (fq & 1)) * 16 + (fq >> 1) * 8;
+    const int n = SW ? n0 + wn * WC + (2 * p + (fq & 1)) * 16 + (fq >> 1) * 8 : n0 + wn * WC + 2 * p * 16 + 4 * fq;
     c8[p] = n;
-    oc[p] = E.ones_col - n;   // in [0, 8): this lane's column of the ones column
+    // this lane's slot (of 8) holding the ones column, or out of [0, 8)
+    oc[p] = E.ones_col >= n + CB && E.ones_col < n + CB + 4 ? 4 + E.ones_col - n - CB
+                                                            : (E.ones_col >= n && E.ones_col < n + 4 ? E.ones_col - n : -1);
     if constexpr (EM == XE_QKV) {
       const int pw = E.nh * E.hdp;
       const int part = fdiv(n, E.d_pw), rr = n - part * pw;
@@ -629,7 +637,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
         for (int p = 0; p < NP; ++p) {
           const float* src = EX == EX_RESID ? E.resid + (long)rowv[i] * E.ldr : (const float*)E.gate + (long)rowv[i] * E.ldg;
           ex[i][p][0] = *(const float4*)(src + c8[p]);
-          ex[i][p][1] = *(const float4*)(src + c8[p] + 4);
+          ex[i][p][1] = *(const float4*)(src + c8[p] + CB);
         }
       nvm += 4 * NP;
     }
@@ -650,14 +658,19 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         float v[8];
-        const float4 b0 = *(const float4*)(sBias + c8[p] - n0), b1 = *(const float4*)(sBias + c8[p] - n0 + 4);
+        const float4 b0 = *(const float4*)(sBias + c8[p] - n0), b1 = *(const float4*)(sBias + c8[p] + CB - n0);
         const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][c]),
-                                                          __float_as_uint(acc[i][2 * p + 1][c]), false, false);
-          v[c] = __uint_as_float(r[0]) * E.acc_scale + bv[c];
-          v[4 + c] = __uint_as_float(r[1]) * E.acc_scale + bv[4 + c];
+          if constexpr (SW) {
+            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][c]),
+                                                            __float_as_uint(acc[i][2 * p + 1][c]), false, false);
+            v[c] = __uint_as_float(r[0]) * E.acc_scale + bv[c];
+            v[4 + c] = __uint_as_float(r[1]) * E.acc_scale + bv[4 + c];
+          } else {
+            v[c] = acc[i][2 * p][c] * E.acc_scale + bv[c];
+            v[4 + c] = acc[i][2 * p + 1][c] * E.acc_scale + bv[4 + c];
+          }
         }
         const int n = c8[p];
         if constexpr (EM == XE_QKV) {
@@ -709,12 +722,12 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
             } else {
               float* d = (float*)E.out + (EM == XE_PSHUF || EM == XE_PUNSHUF ? roff[i] + colo[p] : rr * E.ldo + n);
               *(float4*)d = make_float4(v[0], v[1], v[2], v[3]);
-              *(float4*)(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+              *(float4*)(d + CB) = make_float4(v[4], v[5], v[6], v[7]);
             }
             if (E.pre) {
               float* d = (float*)E.pre + rr * E.ldp + n;
               *(float4*)d = make_float4(pre[0], pre[1], pre[2], pre[3]);
-              *(float4*)(d + 4) = make_float4(pre[4], pre[5], pre[6], pre[7]);
+              *(float4*)(d + CB) = make_float4(pre[4], pre[5], pre[6], pre[7]);
             }
           }
         }
