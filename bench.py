@@ -257,10 +257,10 @@ def _x3_ring_tn(a):
 def _x3_ring_nt(a):
     """Whether an x3 gemm_nt launch takes the ring kernel (gemm_x3.hip nt_x3_ring_ok, the common cases)."""
     A, E, N, K = a[0], a[2], a[4], a[5]
-    bn = 192 if N % 192 == 0 else (N if N in (64, 128) else 0)   # nt_x3_ring_bn
+    bn = 192 if N % 192 == 0 else (64 if N == 64 else (128 if N % 128 == 0 else 0))   # nt_x3_ring_bn
     return (bn > 0 and K % 32 == 0 and (E.out_mode in (0, 1) or (E.out_mode == 6 and bn == 128)) and   # rows / q,k,v /
                                                                                                     # PixelShuffle
-            (A.mode == 0 or (A.mode == 1 and A.dtype == 0 and A.im_C % 32 == 0)))
+            (A.mode == 0 or (A.mode == 1 and A.dtype == 0 and A.im_C % 32 == 0 and K == 9 * A.im_C)))
 
 
 def pmc_traffic(key):
