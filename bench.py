@@ -71,10 +71,18 @@ def _time(launch, reps):
 _REAL = {576: 540, 384: 360, 192: 180}   # padded operand width -> the reference's width (C 180, 2C, 3C)
 
 
-def _alg_bytes(fn, a):
+def _alg_bytes(fn, a, kw=None):
     """Algorithmic bytes of one launch (reference-width operands read / written once, fp32 4 B, bf16 2 B),
     or None for launch kinds without a formula (never the dominant ones)."""
     T = 64
+    kw = kw or {}
+    if fn == "layernorm_fwd":         # x in (fp32), y out, mean / rstd
+        x, y, M, C = a[0], a[2], a[8], a[9]
+        return M * C * (4 + y.element_size()) + 8 * M
+    if fn == "layernorm_bwd":         # x, dy in; dx out (+ in when accumulating); the operand copy; mean / rstd
+        dy, acc, M, C = a[2], a[9], a[14], a[15]
+        cp = kw.get("copy", a[17] if len(a) > 17 else None)
+        return M * C * (4 + dy.element_size() + (8 if acc else 4) + (0 if cp is None else (4 if cp.dtype == 0 else 2))) + 8 * M
     if fn == "swin_mlp_fwd":          # x in + out (fp32), ln2, GELU' and GELU (bf16), mean / rstd; weights once
         C, hd, M = a[5], a[15], a[22]
         return (M // T) * (2 * T * C * 4 + T * C * 2 + 2 * T * hd * 2 + T * 8) + 2 * 2 * C * hd
@@ -154,13 +162,62 @@ _TIMED = ("gemm_nt", "gemm_tn", "wgrad_finalize", "colsum", "layernorm_fwd", "la
           "conv3x3_narrow_fwd_x3", "conv3x3_narrow_dgrad_x3", "conv3x3_narrow_wgrad_x3")
 
 
-def time_roles(tr, serial=False):
-    """{role: {kernel, launches, ms (mean in-step), bytes, flops}} over one eager fwd + loss + bwd.
-    serial: the engine's deferred side-stream work runs in place on the main stream for this pass, so
-    every event pair brackets exactly one kernel (its duration, as rocprofv3's kernel trace reports it)
-    instead of its in-step time behind concurrent side-stream work."""
+class _GraphEvents:
+    """HIP events recorded as EXTERNAL event nodes of a captured graph (hipEventRecordWithFlags(...,
+    hipEventRecordExternal)): replaying the graph stamps them, so a pair around a launch gives that kernel's
+    duration inside the graph-replayed step -- the same execution (stream concurrency, back-to-back launches,
+    no host gaps) that rocprofv3 --kernel-trace records for the timed bench step."""
+
+    def __init__(self):
+        import ctypes
+        path = "libamdhip64.so"
+        try:   # the HIP runtime this process already loaded (torch's), not a second copy
+            with open("/proc/self/maps") as f:
+                for line in f:
+                    if "libamdhip64" in line:
+                        path = line.split()[-1]
+                        break
+        except OSError:
+            pass
+        self.ct = ctypes
+        self.rt = ctypes.CDLL(path)
+        self.rt.hipEventRecordWithFlags.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+        self.rt.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+        self.rt.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.events = []
+
+    def record(self):
+        ev = self.ct.c_void_p()
+        if self.rt.hipEventCreateWithFlags(self.ct.byref(ev), 0) != 0:
+            raise RuntimeError("hipEventCreateWithFlags failed")
+        self.events.append(ev)
+        rc = self.rt.hipEventRecordWithFlags(ev, self.ct.c_void_p(torch.cuda.current_stream().cuda_stream), 1)
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecordWithFlags(external) failed ({rc})")
+        return ev
+
+    def elapsed(self, e0, e1):
+        ms = self.ct.c_float()
+        if self.rt.hipEventElapsedTime(self.ct.byref(ms), e0, e1) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value
+
+    def close(self):
+        for ev in self.events:
+            self.rt.hipEventDestroy(ev)
+        self.events = []
+
+
+def time_roles(tr, serial=False, graph=False, replays=3):
+    """{role: {kernel, launches, ms (mean per launch), bytes, flops}} over one fwd + loss + bwd.
+    graph: the pass is captured as a HIP graph with an external event node on the launch stream before and
+    after every libkair launch, and replayed `replays` times; a launch's time is its mean over the replays --
+    the kernel durations of the graph-replayed bench step (what the committed rocprofv3 summary of the bench
+    command averages).  Otherwise eager, a torch event pair per launch; serial: the engine's deferred side-stream
+    work runs in place on the main stream for this pass (every event pair brackets exactly one kernel)."""
     from kair_amd import _hip as H
     rec = []
+    gev = _GraphEvents() if graph else None
 
     # the engine's thin launch helpers: a role is named by their caller (the layer's call site), not by them
     helpers = ("_nt", "_wgrad", "_wg", "_run_conv_job", "_bias_colsum")
@@ -171,11 +228,16 @@ def time_roles(tr, serial=False):
             while fr.f_back is not None and fr.f_code.co_name in helpers:
                 fr = fr.f_back
             role = f"{name} @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}"
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            f(*a, **k)
-            e1.record()
-            rec.append((role, name, a, e0, e1))
+            if gev is not None:
+                e0 = gev.record()
+                f(*a, **k)
+                e1 = gev.record()
+            else:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                f(*a, **k)
+                e1.record()
+            rec.append((role, name, (a, k), e0, e1))
         return g
 
     orig = {n: getattr(H, n) for n in _TIMED}
@@ -187,32 +249,61 @@ def time_roles(tr, serial=False):
 
     def wg_run(self, ws, **kw):
         fr = sys._getframe(1)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        run0(self, ws, **kw)
-        e1.record()
-        rec.append((f"wgrad_grouped @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}", "wgrad_grouped", (), e0, e1))
+        if gev is not None:
+            e0 = gev.record()
+            run0(self, ws, **kw)
+            e1 = gev.record()
+        else:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            run0(self, ws, **kw)
+            e1.record()
+        rec.append((f"wgrad_grouped @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}", "wgrad_grouped", ((), {}),
+                    e0, e1))
     for n in _TIMED:
         setattr(H, n, wrap(n, orig[n]))
     H.WgradGroup.run = wg_run
+    times = None
     try:
-        for _ in range(2):   # the second pass is the one kept (first-touch effects out of the way)
-            rec.clear()
-            tr._fwd_bwd(*tr.static)
-        torch.cuda.synchronize()
+        if gev is not None:
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream()
+            cs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cs):
+                g.capture_begin(pool=torch.cuda.graph_pool_handle())
+                tr._fwd_bwd(*tr.static)
+                g.capture_end()
+            torch.cuda.current_stream().wait_stream(cs)
+            torch.cuda.synchronize()
+            times = [0.0] * len(rec)
+            for _ in range(replays):
+                g.replay()
+                torch.cuda.synchronize()
+                for i, (_, _, _, e0, e1) in enumerate(rec):
+                    times[i] += gev.elapsed(e0, e1) / replays
+            del g
+        else:
+            for _ in range(2):   # the second pass is the one kept (first-touch effects out of the way)
+                rec.clear()
+                tr._fwd_bwd(*tr.static)
+            torch.cuda.synchronize()
+            times = [e0.elapsed_time(e1) for _, _, _, e0, e1 in rec]
     finally:
         for n in _TIMED:
             setattr(H, n, orig[n])
         H.WgradGroup.run = run0
         if serial and side0 is not None:
             eng.side_stream = side0
+        if gev is not None:
+            gev.close()
     out = {}
-    for role, name, a, e0, e1 in rec:
+    for (role, name, (a, kw), _, _), ms in zip(rec, times):
         d = out.setdefault(role, {"kernel": name, "launches": 0, "ms_total": 0.0, "bytes_total": 0, "flops_total": 0,
                                   "rocprof": rocprof_name(name, a)})
         d["launches"] += 1
-        d["ms_total"] += e0.elapsed_time(e1)
-        b, f = _alg_bytes(name, a), _alg_flops(name, a)
+        d["ms_total"] += ms
+        b, f = _alg_bytes(name, a, kw), _alg_flops(name, a)
         d["bytes_total"] = None if (b is None or d["bytes_total"] is None) else d["bytes_total"] + b
         d["flops_total"] = None if (f is None or d["flops_total"] is None) else d["flops_total"] + f
     for d in out.values():
@@ -233,9 +324,13 @@ def rocprof_name(fn, a):
         hold = {12: kb // ks, 24: 6, 36: {0: 9, 1: 7, 2: 5}[epi]}[kb]
         return f"rowgemm_kernel<{kb}, {ks}, {N // 96}, {epi}, {hold}>"
     if fn == "gemm_nt" and a[6] == X3:
-        return "gemm_nt_x3_ring" if _x3_ring_nt(a) else "gemm_nt_x3_kernel"
+        return _x3_nt_ring_name(a) if _x3_ring_nt(a) else "gemm_nt_x3_kernel"
     if fn == "gemm_tn" and a[7] == X3:
-        return "gemm_tn_x3_ring" if _x3_ring_tn(a) else "gemm_tn_x3_kernel"
+        if _x3_ring_tn(a):
+            return f"gemm_tn_x3_ring<{1 if a[1].mode == 1 else 0}>"
+        return "gemm_tn_x3_kernel"
+    if fn in ("layernorm_fwd", "layernorm_bwd"):
+        return {"layernorm_fwd": "ln_fwd_kernel", "layernorm_bwd": "ln_bwd_kernel"}[fn]
     if fn == "window_attn_fwd_x3":
         return "attn_fwd_x3_kernel"
     if fn == "window_attn_bwd_x3":
@@ -252,6 +347,34 @@ def _x3_ring_tn(a):
             and not A.rowscale and not B.rowscale and
             (B.mode == 0 or (B.mode == 1 and B.im_C % 4 == 0 and K == 9 * B.im_C and not B.im_flip and B.im_up != 2
                               and N % 192 == 0)))
+
+
+def _x3_nt_ring_name(a):
+    """rocprofv3's name of the NT ring instantiation an x3 gemm_nt launch takes: gemm_nt_x3_ring<TA, AM, EM, EX,
+    ACT, GK, BN> as gemm_x3.hip launch_nt_x3_ring selects it."""
+    A, E, N = a[0], a[2], a[4]
+    bn = 192 if N % 192 == 0 else (64 if N == 64 else 128)
+    ta = "_Float16" if A.dtype == 3 else "float"
+    am = 1 if A.mode == 1 else 0
+    if bn == 192:
+        if E.out_mode == 1:
+            f = (2, 0, 0, 0)                       # XE_QKV
+        elif E.out_dtype == 3:
+            f = (1, 0, 0, 0)                       # XE_ROWS_PAIR
+        elif E.resid:
+            f = (0, 1, 0, 0)                       # EX_RESID
+        elif E.gate:
+            f = (0, 3, 0, 4 if E.gate_kind == 4 else 2)
+        elif E.act == 1:
+            f = (0, 0, 1 if E.pre_kind else 2, 0)  # XA_GELU / XA_GELU_X
+        elif E.act == 2:
+            f = (0, 0, 3, 0)                       # XA_LEAKY
+        else:
+            f = (0, 0, 0, 0)
+    else:
+        f = ((3, 0, 0, 0) if E.out_mode == 6 else (4, 0, 0, 0) if E.out_mode == 7 else (0, 3, 0, 2) if E.gate else
+             (0, 0, 3, 0) if E.act == 2 else (0, 0, 0, 0))
+    return f"gemm_nt_x3_ring<{ta}, {am}, {f[0]}, {f[1]}, {f[2]}, {f[3]}, {bn}>"
 
 
 def _x3_ring_nt(a):
@@ -329,7 +452,10 @@ def engine_line(dtype, bpg, device, drop_path, steps, warmup, roles=True):
     peak = PEAK_F32_TFLOPS if dtype == "fp32" else PEAK_BF16_TFLOPS
     top = []
     if roles:
-        rs = time_roles(tr, serial=True)
+        try:
+            rs = time_roles(tr, graph=True)
+        except Exception:  # noqa: BLE001
+            rs = time_roles(tr, serial=True)
         for k, v in sorted(rs.items(), key=lambda kv: -kv[1]["ms_total"])[:5]:
             # the fp32 engine's attention backward is the fp32 kernel (rocprof name)
             kname = {"attn_bwd_bf16_kernel<2>": "attn_bwd_kernel<false>"}.get(v["rocprof"], v["rocprof"]) if dtype == "fp32" \
@@ -396,11 +522,21 @@ def psnr_parity(net_gpu, device, dtype, n_eval=8):
 OTHER_STEPS, OTHER_WARMUP = 20, 5
 
 
+# the precision each config's reference option file trains at (models/model_plain.py:31-36: no amp_enabled -> fp32):
+# C2 is quoted in bf16 by BASELINE.json itself; C3 (train_usrnet.json) and C5 (train_rrdb_psnr.json) are fp32, so
+# they are also timed on an engine of that precision class (REF_DTYPE: fp32x3 where the engine has the split-fp16
+# arithmetic, else the exact-fp32 MFMA engine), priced against that engine's MFMA ceiling
+REF_DTYPE = {"usrnet": "fp32", "rrdbnet": "fp32", "dncnn": "fp32"}
+CEILING = {"bf16": (PEAK_BF16_TFLOPS, "dense bf16 MFMA peak"), "fp32x3": (PEAK_BF16_TFLOPS / 3, "dense f16 MFMA peak / 3"),
+           "fp32": (PEAK_F32_TFLOPS, "dense fp32 MFMA peak")}
+
+
 def other_configs(device):
     """The other BASELINE.json configs, one short fused-trainer run each (USRNet with (k, sf, sigma) inputs)
     on this GPU (tools/bench_models.py; synthetic seeded inputs resident in HBM): patches/s and the
-    fraction of the dense bf16 MFMA peak their training FLOPs reach.  C1 (DnCNN) is a CPU config in
-    the reference; its network's GPU step is reported for completeness."""
+    fraction of the MFMA ceiling of the engine's arithmetic their training FLOPs reach -- in bf16 and, for the
+    configs whose option files train in fp32, at that precision class too (REF_DTYPE).  C1 (DnCNN) is a CPU
+    config in the reference; its network's GPU step is reported for completeness."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
     import bench_models as bm
     labels = {"swinir_light": "C2 SwinIR-lightweight x2, 64-px LQ, batch 64",
@@ -409,18 +545,24 @@ def other_configs(device):
               "dncnn": "C1 DnCNN sigma 25, 40x40, batch 64 (GPU step of the CPU config's network)"}
     res = {}
     for name, label in labels.items():
-        try:
-            B, dt, loss = bm.run(name, OTHER_STEPS, OTHER_WARMUP, device)
-            pps = B / dt
-            tf = pps * bm.TRAIN_GFLOP[name] / 1e3
-            res[name] = {"config": label, "value": round(pps, 2), "unit": "patches/s", "ms_per_step": round(dt * 1e3, 3),
-                         "steps": OTHER_STEPS, "warmup": OTHER_WARMUP, "train_gflop_per_patch": bm.TRAIN_GFLOP[name],
-                         "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
-                                      "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4)},
-                         "final_loss": round(loss, 6)}
-        except Exception as e:  # noqa: BLE001
-            res[name] = {"config": label, "error": repr(e)}
-        torch.cuda.empty_cache()
+        for dt in ["bf16"] + ([REF_DTYPE[name]] if name in REF_DTYPE else []):
+            key = name if dt == "bf16" else f"{name}_{dt}"
+            try:
+                B, sec, loss = bm.run(name, OTHER_STEPS, OTHER_WARMUP, device, dt)
+                pps = B / sec
+                tf = pps * bm.TRAIN_GFLOP[name] / 1e3
+                pk, what = CEILING[dt]
+                res[key] = {"config": label, "dtype": dt, "value": round(pps, 2), "unit": "patches/s",
+                            "ms_per_step": round(sec * 1e3, 3), "steps": OTHER_STEPS, "warmup": OTHER_WARMUP,
+                            "train_gflop_per_patch": bm.TRAIN_GFLOP[name],
+                            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": round(pk, 1), "peak_what": what,
+                                         "unit": "TFLOP/s", "frac": round(tf / pk, 4)},
+                            "final_loss": round(loss, 6)}
+                if dt == REF_DTYPE.get(name):
+                    res[key]["precision"] = "the reference option file's precision class (fp32)"
+            except Exception as e:  # noqa: BLE001
+                res[key] = {"config": label, "dtype": dt, "error": repr(e)}
+            torch.cuda.empty_cache()
     return res
 
 
@@ -572,6 +714,7 @@ def main():
 
     for _ in range(args.warmup):
         loss = tr.step(*batch())
+    tr.check_range()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -581,6 +724,7 @@ def main():
     e0.record()
     for _ in range(args.steps):
         loss = tr.step(*batch())
+    tr.check_range()   # fp32x3 range guard: the last step's flag (every earlier one is settled inside step())
     e1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -603,57 +747,83 @@ def main():
     value = gbatch * args.steps / wall
     ms_step = 1000.0 * wall / args.steps
     step_tflops = fl["train"] * gbatch / (wall / args.steps) / 1e12 / world   # per GPU
-    # the MFMA peak a FLOP of this engine is priced against: fp32x3 delivers fp32 FLOPs (3 fp16 products each)
-    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
-    roles, serial = {}, {}
+    # the MFMA ceiling a FLOP of this engine is priced against: bf16 the dense bf16 peak; fp32x3 issues THREE fp16
+    # products per fp32 FLOP on the f16 pipe (2.5 PF dense), so its ceiling is 2.5 PF / 3; exact fp32 the fp32 peak
+    peak = {"bf16": PEAK_BF16_TFLOPS, "fp32x3": PEAK_BF16_TFLOPS / 3, "fp32": PEAK_F32_TFLOPS}[args.dtype]
+    peak_what = {"bf16": "dense bf16 MFMA peak (2.5 PF)",
+                 "fp32x3": "dense f16 MFMA peak / 3 (2.5 PF / 3 = 833 TF: three fp16 products per fp32 FLOP)",
+                 "fp32": "dense fp32 MFMA peak (157.3 TF)"}[args.dtype]
+    roles, timing = {}, "graph"
     if not args.no_roles:
-        try:
-            roles = time_roles(tr)
-            serial = time_roles(tr, serial=True)
+        try:   # kernel durations inside the graph-replayed step (external event nodes)
+            roles = time_roles(tr, graph=True)
         except Exception as e:  # noqa: BLE001
-            roles = serial = {"error": {"kernel": repr(e), "ms_total": 0.0}}
-    TIMING = {"in_step": "in-step mean over the step's launches of this role: one eager fwd+loss+bwd, a HIP event pair "
-                         "on the launch stream around each launch (side-stream concurrency kept, so a launch queued "
-                         "behind side-stream work includes that wait)",
-              "serial": "kernel duration: mean over the step's launches of this role in one eager fwd+loss+bwd with the "
-                        "deferred side-stream work run in place, a HIP event pair around each launch on its stream (the "
-                        "quantity rocprofv3 --kernel-trace reports per dispatch)"}
+            try:   # fallback: an eager pass (side-stream concurrency kept), named as such in the line
+                roles, timing = time_roles(tr), f"in_step (graph events failed: {e!r})"
+            except Exception as e2:  # noqa: BLE001
+                roles = {"error": {"kernel": repr(e2), "ms_total": 0.0}}
+    TIMING = ("kernel duration inside the graph-replayed training step: one capture of fwd+loss+bwd with an external "
+              "HIP event node (hipEventRecordWithFlags, hipEventRecordExternal) on the launch stream before and after every "
+              "libkair launch, side stream included, replayed 3 times; mean per launch -- the quantity rocprofv3 "
+              "--kernel-trace reports for the graph-replayed bench step (profiles/*_kernel_stats.csv)") if timing == "graph" \
+        else "eager in-step mean per launch: " + timing
 
-    def roof(role, d, timing="in_step"):
-        r = {"bound": "hbm", "kernel": d["rocprof"], "role": role, "launches_per_step": d["launches"],
-             "kernel_ms": round(d["ms"], 5), "step_ms_total": round(d["ms_total"], 4),
-             "kernel_ms_timing": TIMING[timing]}
+    def roof(name, d):
+        r = {"bound": "hbm", "kernel": d["rocprof"], "role": name, "launches_per_step": d["launches"],
+             "kernel_ms": round(d["ms"], 5), "step_ms_total": round(d["ms_total"], 4), "kernel_ms_timing": TIMING}
         if d.get("bytes"):
             gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
             r.update({"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
-                      "bytes_per_launch": d["bytes"], "traffic": pmc_traffic(d["rocprof"])})
+                      "bytes_per_launch": round(d["bytes"]), "traffic": pmc_traffic(d["rocprof"])})
         else:
             r.update({"achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": None, "traffic": None})
         if d.get("flops"):
             tf = d["flops"] / (d["ms"] * 1e-3) / 1e12
-            r.update({"flops_per_launch": d["flops"], "achieved_tflops": round(tf, 2), "mfma_frac": round(tf / peak, 4)})
-            if args.dtype == "fp32x3":   # fp32-equivalent FLOPs vs the fp32 MFMA peak; 3 fp16 products per FLOP issued
-                r.update({"mfma_frac_vs": "dense fp32 MFMA peak (the fp32 FLOPs the split arithmetic delivers)",
-                          "issued_frac_of_fp16_peak": round(3 * tf / PEAK_BF16_TFLOPS, 4)})
+            r.update({"flops_per_launch": d["flops"], "achieved_tflops": round(tf, 2), "mfma_frac": round(tf / peak, 4),
+                      "mfma_peak": peak_what})
+            if args.dtype == "fp32x3":
+                r["frac_of_fp32_peak"] = round(tf / PEAK_F32_TFLOPS, 4)
         return r
-    ranked = sorted(((k, v) for k, v in roles.items() if k != "error"), key=lambda kv: -kv[1]["ms_total"])
-    ranked_serial = sorted(((k, v) for k, v in serial.items() if k != "error" and v.get("bytes")),
-                           key=lambda kv: -kv[1]["ms_total"])
+    good = {k: v for k, v in roles.items() if k != "error"}
+    ranked = sorted(good.items(), key=lambda kv: -kv[1]["ms_total"])
+    # per kernel (rocprofv3's grouping: one template instantiation, every role that launches it): total time per
+    # step, launches, mean duration and mean algorithmic bytes / FLOPs per launch
+    kern = {}
+    for v in good.values():
+        d = kern.setdefault(v["rocprof"], {"rocprof": v["rocprof"], "launches": 0, "ms_total": 0.0, "b": 0, "f": 0,
+                                           "roles": 0, "nb": False, "nf": False})
+        d["launches"] += v["launches"]
+        d["ms_total"] += v["ms_total"]
+        d["roles"] += 1
+        if v.get("bytes"):
+            d["b"] += v["bytes"] * v["launches"]
+        else:
+            d["nb"] = True
+        if v.get("flops"):
+            d["f"] += v["flops"] * v["launches"]
+        else:
+            d["nf"] = True
+    for d in kern.values():
+        d["ms"] = d["ms_total"] / d["launches"]
+        d["bytes"] = None if d["nb"] else d["b"] / d["launches"]
+        d["flops"] = None if d["nf"] else d["f"] / d["launches"]
+    kranked = sorted(kern.items(), key=lambda kv: -kv[1]["ms_total"])
     # attention GEMMs (QKV / q.k^T / p.v / proj): the fused attention half, the attention backward, the proj and
     # q/k/v input-gradient row GEMMs (bf16) / the split window-attention kernels (fp32x3) -- FLOPs over their
-    # in-step time against the engine's MFMA peak
+    # in-step time against the engine's MFMA ceiling
     att_names = ("swin_attn_fwd", "attn_bwd_bf16_kernel", "rowgemm_kernel<12, 4, 2, 0>", "rowgemm_kernel<36",
                  "attn_fwd_x3_kernel", "attn_bwd_x3_kernel")
-    att = [v for v in roles.values() if v.get("flops") and v["rocprof"].startswith(att_names)]
+    att = [v for v in good.values() if v.get("flops") and v["rocprof"].startswith(att_names)]
     att_mfma = None
     if att:
         fl_att = sum(v["flops"] * v["launches"] for v in att)
         ms_att = sum(v["ms_total"] for v in att)
         tf = fl_att / (ms_att * 1e-3) / 1e12
         att_mfma = {"kernels": sorted({v["rocprof"] for v in att}), "flops_per_step": fl_att, "ms_per_step": round(ms_att, 4),
-                    "achieved_tflops": round(tf, 2), "peak_tflops": peak, "mfma_frac": round(tf / peak, 4)}
+                    "achieved_tflops": round(tf, 2), "peak_tflops": round(peak, 1), "peak": peak_what,
+                    "mfma_frac": round(tf / peak, 4)}
         if args.dtype == "fp32x3":
-            att_mfma["issued_frac_of_fp16_peak"] = round(3 * tf / PEAK_BF16_TFLOPS, 4)
+            att_mfma["frac_of_fp32_peak"] = round(tf / PEAK_F32_TFLOPS, 4)
     out = {
         "metric": "train patches/sec + PSNR, SwinIR x4 48-px LQ, at 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "patches/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -667,17 +837,19 @@ def main():
                    "global_batch": gbatch, "per_gpu_batch": bpg, "lq": 48, "hr": 192, "embed_dim": 180,
                    "depths": [6] * 6, "heads": 6, "window": 8, "drop_path_rate": args.drop_path,
                    "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
-        # roofline: the step's dominant kernel by summed kernel duration (rocprof's dominant kernel); the
-        # in-step view (waits behind the side stream included) ranks the roles in kernels_in_step
-        "roofline": (roof(*ranked_serial[0], timing="serial") if ranked_serial else
-                     {"error": serial.get("error", {}).get("kernel", "roles skipped")}),
-        "kernels_by_duration": [roof(k, v, timing="serial") for k, v in ranked_serial[:8]],
-        "kernels_in_step": [roof(k, v) for k, v in ranked[:8]],
+        # roofline: the step's dominant kernel -- the kernel (template instantiation, all its roles) with the
+        # largest summed duration in the graph-replayed step, as rocprofv3 ranks the bench command's kernels
+        "roofline": (roof(f"all {kranked[0][1]['roles']} role(s) of the kernel", kranked[0][1]) if kranked else
+                     {"error": roles.get("error", {}).get("kernel", "roles skipped")}),
+        "kernels_by_duration": [roof(f"{v['roles']} role(s)", v) for _, v in kranked[:10]],
+        "roles_by_duration": [roof(k, v) for k, v in ranked[:12]],
         "attention_gemm_mfma": att_mfma,
         "step_roofline": {"train_flop_per_patch": fl["train"], "achieved_tflops_per_gpu": round(step_tflops, 2),
-                          "peak_tflops": peak, "frac_of_peak": round(step_tflops / peak, 4),
-                          **({"issued_frac_of_fp16_peak": round(3 * step_tflops / PEAK_BF16_TFLOPS, 4)}
+                          "peak_tflops": round(peak, 1), "peak": peak_what, "frac_of_peak": round(step_tflops / peak, 4),
+                          **({"frac_of_fp32_peak": round(step_tflops / PEAK_F32_TFLOPS, 4)}
                              if args.dtype == "fp32x3" else {})},
+        "range_guard": ({"events": tr.range_events, "act_exp": tr.engine.X3_AEXP, "grad_exp_offset": tr.engine.x3_gexp_off}
+                        if getattr(tr, "range_guard", False) else None),
         "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
         "final_loss": round(final_loss, 6),
     }

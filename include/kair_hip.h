@@ -503,6 +503,18 @@ int kair_sumpool2x(const float* src, long lds, float* dst, long ldd, int B, int 
  * the host before each (graph-replayed) step; ema may be NULL (E_decay = 0). */
 int kair_adam_ema(float* p, const float* g, float* m, float* v, float* ema, long n, const float* lr_t,
                   float beta1, float beta2, float eps, float weight_decay, float ema_decay, void* stream);
+/* kair_adam_ema with a device skip flag (NULL: never): *skip != 0 drops the step -- parameters, moments and
+ * EMA untouched -- the way torch.cuda.amp.GradScaler.step skips an inf/NaN step.  The fp32x3 range guard. */
+int kair_adam_ema_ex(float* p, const float* g, float* m, float* v, float* ema, long n, const float* lr_t,
+                     float beta1, float beta2, float eps, float weight_decay, float ema_decay, const unsigned* skip,
+                     void* stream);
+/* fp32x3 range guard: *flag = (any non-finite g: 1) | (non-finite *loss: 2) | (any |p| >= p_limit or
+ * non-finite p: 4), over the flat gradient / parameter buffers of n floats (loss may be NULL).  A split-fp16
+ * operand that leaves fp16's range turns into inf/NaN in every product it enters, so the step's gradients
+ * show it; p_limit = 2^(16 - KAIR_X3_WEXP) bounds the weights' fp16 window.  (No reference counterpart: the
+ * fp32 reference has no operand window.) */
+int kair_range_check(const float* g, const float* p, long n, const float* loss, float p_limit, unsigned* flag,
+                     void* stream);
 
 /* USRNet (network_usrnet_v1.py) -------------------------------------------------------------
  * Complex plane sets are float2 [planes][W][H] (TRANSPOSED: column-major per plane).            */

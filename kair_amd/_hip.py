@@ -163,6 +163,9 @@ _SIGS = {
                            c_vp],
     "kair_sumpool2x": [c_vp, c_long, c_vp, c_long, c_int, c_int, c_int, c_int, c_int, c_vp],
     "kair_adam_ema": [c_vp, c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp],
+    "kair_adam_ema_ex": [c_vp, c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp,
+                         c_vp],
+    "kair_range_check": [c_vp, c_vp, c_long, c_vp, c_float, c_vp, c_vp],
     "kair_usr_fft_rows": [c_vp, c_int, c_int, c_long, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],
     "kair_usr_fft_cols": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
                           c_vp],
@@ -687,9 +690,20 @@ def axpy(y, x, a, n=None):
     check(lib().kair_axpy(ptr(y), ptr(x), a, n if n is not None else y.numel(), stream_ptr()), "axpy")
 
 
-def adam_ema(p, g, m, v, ema, n, lr_t, beta1, beta2, eps, wd, decay):
+def adam_ema(p, g, m, v, ema, n, lr_t, beta1, beta2, eps, wd, decay, skip=None):
+    """skip: an int32 device flag (kair_range_check): nonzero drops the step (kair_adam_ema_ex)."""
+    if skip is not None:
+        check(lib().kair_adam_ema_ex(ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), n, ptr(lr_t), beta1, beta2, eps, wd, decay,
+                                     ptr(skip), stream_ptr()), "adam_ema_ex")
+        return
     check(lib().kair_adam_ema(ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), n, ptr(lr_t), beta1, beta2, eps, wd, decay,
                               stream_ptr()), "adam_ema")
+
+
+def range_check(g, p, loss, p_limit, flag):
+    """fp32x3 range guard: flag[0] = 1 (non-finite gradient) | 2 (non-finite loss) | 4 (|p| >= p_limit)."""
+    check(lib().kair_range_check(ptr(g), ptr(p), g.numel(), ptr(loss), float(p_limit), ptr(flag), stream_ptr()),
+          "range_check")
 
 
 def axpby(y, x, a, b, n=None):

@@ -1,4 +1,4 @@
-// Window-attention helpers shared by the bf16 / fp32 kernels (window_attn.hip) and the split-bf16
+// Window-attention helpers shared by the bf16 / fp32 kernels (window_attn.hip) and the fp16-pair (fp32x3)
 // ("x3") kernels (attn_x3.hip): Swin window geometry (ws = 8, 64 tokens, head dim padded to 32),
 // the relative-position index and its binned gradient, the shifted-window region ids, and the
 // MFMA-fragment reads of [64][32] bf16 LDS tiles.

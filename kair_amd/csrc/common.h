@@ -334,7 +334,7 @@ struct FinGroup {
 };
 int kair_launch_finalize_grouped(const FinGroup& g, hipStream_t s);
 
-// split-bf16 window attention (attn_x3.hip): windows per backward wave, and the bias-table partial sum
+// fp16-pair (fp32x3) window attention (attn_x3.hip): windows per backward wave, and the bias-table partial sum
 // shared with window_attn.hip
 long kair_attn_x3_wpg(long nWin, int nh);
 int kair_attn_dtable_sum(const float* ws, long ngroups, int nh, float* dtable, int accumulate, hipStream_t s);

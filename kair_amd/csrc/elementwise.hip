@@ -637,10 +637,43 @@ __global__ void l1_final(const float* __restrict__ ws, int nb, float scale, floa
   if (threadIdx.x == 0) out[0] = red[0] * scale;
 }
 
-// lr_t[0] = step_size = lr / (1 - b1^t),  lr_t[1] = sqrt(1 - b2^t)
+// fp32x3 range guard (kair_range_check): flag |= 1 for a non-finite gradient, 2 for a non-finite loss, 4 for a
+// parameter outside [-p_limit, p_limit] (the fp16 window of the x3 weight packs) or non-finite.  A split operand
+// that leaves fp16's range becomes inf in its hi half and NaN/inf in every product it enters, so one pass over the
+// step's gradients sees it wherever it happened (forward activations reach the weight gradients through the wgrad
+// products).  One atomic OR per workgroup that found something (vector atomic; none on a clean step).
+__global__ void range_check_kernel(const float* __restrict__ g, const float* __restrict__ p, long n,
+                                   const float* __restrict__ loss, float p_limit, unsigned* __restrict__ flag) {
+  unsigned bits = 0;
+  const long n4 = n / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 gv = ((const float4*)g)[i];
+    const float4 pv = ((const float4*)p)[i];
+    // (x - x) is 0 for finite x and NaN for inf / NaN: one test per four values
+    const float gs = (gv.x - gv.x) + (gv.y - gv.y) + (gv.z - gv.z) + (gv.w - gv.w);
+    if (gs != 0.f) bits |= 1u;
+    const float pm = fmaxf(fmaxf(fabsf(pv.x), fabsf(pv.y)), fmaxf(fabsf(pv.z), fabsf(pv.w)));
+    if (!(pm < p_limit)) bits |= 4u;   // (NaN compares false)
+  }
+  for (long i = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    if (g[i] - g[i] != 0.f) bits |= 1u;
+    if (!(fabsf(p[i]) < p_limit)) bits |= 4u;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && loss && loss[0] - loss[0] != 0.f) bits |= 2u;
+  __shared__ unsigned red;
+  if (threadIdx.x == 0) red = 0;
+  __syncthreads();
+  if (bits) atomicOr(&red, bits);
+  __syncthreads();
+  if (threadIdx.x == 0 && red) atomicOr(flag, red);
+}
+
+// lr_t[0] = step_size = lr / (1 - b1^t),  lr_t[1] = sqrt(1 - b2^t);  skip: a range-guard flag -- nonzero: the
+// step is dropped (parameters, moments and EMA untouched), as torch's GradScaler skips an inf step
 __global__ void adam_ema_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                 float* __restrict__ v, float* __restrict__ ema, long n, const float* __restrict__ lr_t,
-                                float b1, float b2, float eps, float wd, float decay) {
+                                float b1, float b2, float eps, float wd, float decay, const unsigned* __restrict__ skip) {
+  if (skip && *skip) return;
   const float step = lr_t[0], bc2s = lr_t[1];
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float gi = g[i];
@@ -975,7 +1008,34 @@ extern "C" int kair_adam_ema(float* p, const float* g, float* m, float* v, float
   long nb = (n + 255) / 256;
   if (nb > 8192) nb = 8192;
   hipLaunchKernelGGL(adam_ema_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n, lr_t,
-                     beta1, beta2, eps, weight_decay, ema_decay);
+                     beta1, beta2, eps, weight_decay, ema_decay, (const unsigned*)nullptr);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_adam_ema_ex(float* p, const float* g, float* m, float* v, float* ema, long n, const float* lr_t,
+                                float beta1, float beta2, float eps, float weight_decay, float ema_decay,
+                                const unsigned* skip, void* stream) {
+  KAIR_CHECK_ARG(p && g && m && v && lr_t && n > 0, "adam_ema_ex: bad args");
+  long nb = (n + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(adam_ema_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n, lr_t,
+                     beta1, beta2, eps, weight_decay, ema_decay, skip);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_range_check(const float* g, const float* p, long n, const float* loss, float p_limit, unsigned* flag,
+                                void* stream) {
+  KAIR_CHECK_ARG(g && p && flag && n > 0 && p_limit > 0.f, "range_check: bad args");
+  if (hipMemsetAsync(flag, 0, sizeof(unsigned), (hipStream_t)stream) != hipSuccess) {
+    KAIR_CHECK_ARG(false, "range_check: memset failed");
+  }
+  long nb = (n / 4 + 255) / 256;
+  if (nb > 2048) nb = 2048;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(range_check_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, g, p, n, loss, p_limit,
+                     flag);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

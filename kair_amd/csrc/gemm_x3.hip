@@ -4,7 +4,8 @@
 // The pair carries 22 of fp32's 24 mantissa bits, so a product is exact to ~2^-21 -- the precision class of
 // the fp32 reference (SwinIR classical x4 trains in fp32: models/model_plain.py:31-36 with no amp_enabled in
 // options/swinir/train_swinir_sr_classical.json); the power-of-2 exponent keeps the operand inside fp16's
-// range (weights 2^KAIR_X3_WEXP, activations 2^0, gradients 2^(log2 of the loss normalisation)).
+// range (weights 2^KAIR_X3_WEXP, activations 2^4, gradients 2^(log2 of the loss normalisation / loss weight) + 4;
+// the activation / gradient exponents drop when the range guard fires, SwinIREngine.x3_backoff).
 //
 //   kair_gemm_nt_x3 : C[m,n] = sum_k A[m,k] B[n,k]            (nn.Linear / 3x3 nn.Conv2d forward + dgrad)
 //   kair_gemm_tn_x3 : P[s][n,k] = sum_{m in s} A[m,n] B[m,k]   (their weight gradients, split over m)

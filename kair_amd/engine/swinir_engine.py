@@ -293,6 +293,11 @@ class SwinIREngine:
         # activations X3_AEXP (O(1) -> 2^4), gradients P["e_g"] (the loss normalisation, _x3_grad_exp)
         self.x3 = compute_dtype == "fp32x3"
         self._ax = 0   # x3: the exponent of the GEMM A operands / fp16 outputs of the phase being issued
+        # x3 exponents of the activation class and of the gradient class (offset over the loss normalisation);
+        # lowered together by x3_backoff() when the range guard sees an operand leave fp16's window
+        self.X3_AEXP = 4
+        self.x3_gexp_off = 4
+        self.x3_backoffs = 0
         self.cd = H.BF16 if compute_dtype in ("bf16", "fp32x3") else H.F32
         self.tn_cd = H.X3 if self.x3 else self.cd   # kair_gemm_tn compute of the weight gradients
         self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
@@ -782,13 +787,33 @@ class SwinIREngine:
             return
         H.gemm_nt(A, B, E, M, N, K, cd)
 
-    X3_AEXP = 4   # fp32x3 activation exponent
+    X3_AEXP = 4   # fp32x3 activation exponent (default; per engine: self.X3_AEXP, lowered by x3_backoff)
+    X3_BACKOFF_STEP = 6      # exponent drop per range-guard event (x 1/64)
+    X3_BACKOFF_MAX = 4       # events before the guard gives up and raises
 
-    @staticmethod
-    def _x3_grad_exp(numel):
-        """The fp32x3 gradient exponent: the mean-loss gradient is O(1 / numel) per output element, so data
-        gradients times 2^(log2 numel + 4) sit near 2^4 at the loss, 2^12 below fp16's overflow."""
-        return int(round(math.log2(max(numel, 1)))) + 4
+    def _x3_grad_exp(self, numel, weight=1.0):
+        """The fp32x3 gradient exponent: the mean-loss gradient is O(weight / numel) per output element (weight: the
+        loss weight over img_range), so data gradients times 2^(log2(numel / weight) + 4) sit near 2^4 at the loss,
+        2^12 below fp16's overflow."""
+        return int(round(math.log2(max(numel, 1) / max(abs(weight), 1e-30)))) + self.x3_gexp_off
+
+    def x3_backoff(self, step=None):
+        """Range guard reaction (kair_range_check saw an inf / NaN the split operands can cause): lower the
+        activation and gradient exponents by `step` (default X3_BACKOFF_STEP) so every operand class gains that
+        much headroom below fp16's 65504 (the lo halves of the smallest values go subnormal first: an absolute
+        error <= 2^-25 of the scaled unit, i.e. fp32 rounding class for O(1) data).  The caller re-runs the step
+        (re-captured graph).  Raises after X3_BACKOFF_MAX events: the data is not finite in fp32 either."""
+        if not self.x3:
+            raise RuntimeError("x3_backoff: not an fp32x3 engine")
+        if self.x3_backoffs >= self.X3_BACKOFF_MAX:
+            raise RuntimeError(f"fp32x3 range guard: the step is still non-finite after {self.x3_backoffs} exponent "
+                               f"back-offs (activation 2^{self.X3_AEXP}, gradient offset 2^{self.x3_gexp_off}): the data "
+                               f"is not finite, or a weight left its pack window |w| < 2^{16 - H.X3_WEXP}")
+        step = self.X3_BACKOFF_STEP if step is None else int(step)
+        self.X3_AEXP -= step
+        self.x3_gexp_off -= step
+        self.x3_backoffs += 1
+        return self.X3_AEXP, self.x3_gexp_off
 
     def _forward_tail(self, P):
         """Reconstruction tail: P['fb'] (conv_after_body + residual) -> P['E']."""
@@ -955,7 +980,7 @@ class SwinIREngine:
         # E = v / img_range + ...: dL/dv = dL/dE / img_range, folded into the loss kernel's gradient scale
         # (which also scales the reported loss, undone below)
         wr = loss_weight / self.img_range
-        P["e_g"] = self._x3_grad_exp(B * self.in_ch * Hh * self.scale * Ww * self.scale)
+        P["e_g"] = self._x3_grad_exp(B * self.in_ch * Hh * self.scale * Ww * self.scale, wr)
         if self.upsampler == "pixelshuffledirect":
             H.l1_loss(P["E"], H_img, P["loss"], P["dE"], self.up1.Cop, wr, B, self.in_ch, Hh * self.scale,
                       Ww * self.scale, P["loss_ws"], ps_r=self.scale, charb_eps=charb_eps)
@@ -967,8 +992,9 @@ class SwinIREngine:
         self.backward(grads, P)
         return P["loss"]
 
-    def backward_from_grad(self, gE, grads):
-        """Backward given dL/dE (NCHW fp32), for the generic autograd path."""
+    def backward_from_grad(self, gE, grads, e_off=0):
+        """Backward given dL/dE (NCHW fp32), for the generic autograd path.  e_off: fp32x3 gradient-exponent shift
+        (the range guard's retry, SwinIRFunction.backward)."""
         P = self.cur
         B, Hh, Ww = P["B"], P["H"], P["W"]
         # dE = gE through the same layout the loss kernel writes: reuse l1 machinery is not possible,
@@ -976,7 +1002,7 @@ class SwinIREngine:
         inv = 1.0 / self.img_range   # E = v / img_range + ...
         if self.x3:   # an arbitrary upstream gradient: its exponent from its own range (one host sync)
             mx = float(gE.abs().max()) * inv
-            P["e_g"] = 8 - int(math.ceil(math.log2(mx))) if mx > 0 and math.isfinite(mx) else 0   # max -> <= 2^8
+            P["e_g"] = (8 - int(math.ceil(math.log2(mx))) if mx > 0 and math.isfinite(mx) else 0) + e_off   # max -> <= 2^8
         if self.upsampler != "pixelshuffledirect":
             H.image_to_nhwc(gE.contiguous(), P["dE"], P.get("dE_ld", 16), None, inv, B, self.in_ch, Hh * self.scale,
                             Ww * self.scale)
@@ -1335,6 +1361,14 @@ class SwinIRFunction(torch.autograd.Function):
             drop = drop_path_scales(engine, x.shape[0], x.device)
         with plan_mode(engine, mode):
             E = engine.forward(x.float(), drop)
+            # fp32x3 range guard (eager path, one host sync): an activation that left the fp16 window shows as a
+            # non-finite output -> lower the exponents and run the forward again (the trainer's graph step has the
+            # same guard on device, FusedTrainer._check_range)
+            while engine.x3 and not bool(torch.isfinite(E).all()):
+                if not bool(torch.isfinite(x).all()):
+                    raise RuntimeError("kair_amd SwinIR: non-finite input")
+                engine.x3_backoff()
+                E = engine.forward(x.float(), drop)
         ctx.engine = engine
         ctx.params = params
         ctx.lease = Lease(engine.cur) if mode == "lease" else None
@@ -1359,6 +1393,15 @@ class SwinIRFunction(torch.autograd.Function):
             full = torch.zeros_like(P["E"])
             full[:, :, :gE.shape[2], :gE.shape[3]] = gE
         eng.backward_from_grad(full.float(), grads)
+        if eng.x3 and bool(torch.isfinite(full).all()):
+            # range guard: a data gradient that left the fp16 window makes the parameter gradients non-finite ->
+            # rerun the backward (the saved activations are unchanged) with the gradient exponent lowered
+            e_off = 0
+            while not bool(torch.isfinite(flat).all()):
+                if e_off <= -eng.X3_BACKOFF_STEP * eng.X3_BACKOFF_MAX:
+                    raise RuntimeError("fp32x3 range guard: the backward stays non-finite after exponent back-offs")
+                e_off -= eng.X3_BACKOFF_STEP
+                eng.backward_from_grad(full.float(), grads, e_off=e_off)
         ctx.lease.release()
         return (None, None, None) + tuple(grads[p] for p in ctx.params)
 

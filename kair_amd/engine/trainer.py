@@ -102,6 +102,22 @@ class FusedTrainer:
         self.static = None
         self.warm = 0
         self.engine._packed_version = None
+        # fp32x3 range guard: the split-fp16 operands have a fixed power-of-2 window per tensor class; a value that
+        # leaves it (fp16 overflow) turns the step's gradients non-finite.  Each step ends with kair_range_check over
+        # the flat gradients / parameters (+ the loss on one GPU) into a device flag that the Adam kernel reads (a
+        # flagged step updates nothing); the host reads the flag one step later (pinned copy + event), lowers the
+        # engine's exponents (x3_backoff) and re-runs the flagged step on its own batch before going on.
+        self.range_guard = bool(getattr(self.engine, "x3", False))
+        self.range_events = []   # (step, flag bits, (activation exp, gradient exp offset) after the back-off)
+        if self.range_guard:
+            self.rflag = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self.rflag_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            self.rflag_evt = torch.cuda.Event()
+            self._rflag_pending = False
+            # parameters: only non-finite ones are flagged here (a weight outside its pack window, |w| >= 2^(16 -
+            # KAIR_X3_WEXP) = 16, overflows its fp16 pack and shows in the gradients like any other operand; the
+            # activation / gradient back-off cannot cure it, so the guard raises after X3_BACKOFF_MAX re-runs)
+            self.p_limit = 3.0e38
         if any(b.dp > 0 for b in self.engine.blocks):
             from .swinir_engine import drop_path_scales
             drop_path_scales(self.engine, 1, self.device)   # materialise the keep-prob table eagerly
@@ -125,15 +141,52 @@ class FusedTrainer:
             eng.forward(L, drop)
         return eng.backward_from_loss(Hh, self.grads, self.loss_weight, charb_eps=self.charb_eps)
 
-    def _update(self):
+    def _update(self, loss=None):
+        skip = None
+        if self.range_guard:
+            # (world > 1: gradients and parameters only -- identical on every rank after the all-reduce -- so every
+            # rank drops and re-runs the same steps; a rank's own loss would not be)
+            H.range_check(self.flat_g, self.flat_p, loss if self.world == 1 else None, self.p_limit, self.rflag)
+            skip = self.rflag
         H.adam_ema(self.flat_p, self.flat_g, self.m, self.v, self.flat_e, self.flat_p.numel(), self.scal,
-                   self.betas[0], self.betas[1], self.eps, self.wd, self.E_decay if self.flat_e is not None else 0.0)
+                   self.betas[0], self.betas[1], self.eps, self.wd, self.E_decay if self.flat_e is not None else 0.0,
+                   skip=skip)
 
     def _body(self, L, Hh, *cond):
         loss = self._fwd_bwd(L, Hh, *cond)
         self._allreduce()
-        self._update()
+        self._update(loss)
         return loss
+
+    # ---- fp32x3 range guard -----------------------------------------------------------------
+    def _post_step(self):
+        if self.range_guard:
+            self.rflag_host.copy_(self.rflag, non_blocking=True)
+            self.rflag_evt.record()
+            self._rflag_pending = True
+
+    def check_range(self):
+        """Read the range flag of the last step (waits for it) and, if the step was flagged, back the exponents off
+        and re-run it on the same batch -- repeatedly, until it is clean or the engine gives up (RuntimeError).
+        step() calls this for the previous step; call it once after the last step of a run."""
+        while self.range_guard and self._rflag_pending:
+            self.rflag_evt.synchronize()
+            self._rflag_pending = False
+            bits = int(self.rflag_host[0])
+            if bits == 0:
+                return
+            if bits & 4:
+                raise RuntimeError(f"fp32x3 range guard: a parameter is not finite at step {self.t}")
+            exps = self.engine.x3_backoff()
+            self.range_events.append((self.t, bits, exps))
+            # re-run step t (its Adam scalars are still in self.scal, its batch in the static / last inputs)
+            if not self.use_graph or self.graph is None:
+                self._body(*self._last_args)
+            else:
+                self._capture()
+                self._replay()
+            self.engine._packed_version = None
+            self._post_step()
 
     def _set_scalars(self):
         self.t += 1
@@ -182,7 +235,7 @@ class FusedTrainer:
                 gu.capture_begin(pool=pool)
                 if self.world > 1:
                     self.flat_g.mul_(1.0 / self.world)
-                self._update()
+                self._update(self.loss_out)
                 gu.capture_end()
         torch.cuda.current_stream().wait_stream(cs)
         torch.cuda.synchronize()
@@ -211,11 +264,15 @@ class FusedTrainer:
     def step(self, L, Hh, *cond):
         """One training step on the batch (L, Hh) (device tensors); cond: the network's extra forward
         inputs (USRNet: k [B,1,kh,kw], sf int, sigma [B,1,1,1]).  Returns the device loss [1].
-        The graph is re-recorded when any input's shape or a non-tensor input (sf) changes."""
+        The graph is re-recorded when any input's shape or a non-tensor input (sf) changes.
+        fp32x3: first settles the previous step's range flag (check_range), which may re-run that step."""
+        self.check_range()
         self._set_scalars()
         if not self.use_graph:
+            self._last_args = (L, Hh) + tuple(cond)
             out = self._body(L, Hh, *cond)
             self.engine._packed_version = None
+            self._post_step()
             return out
         args = (L, Hh) + tuple(cond)
         key = tuple(a.shape if torch.is_tensor(a) else ("const", a) for a in args)
@@ -229,6 +286,7 @@ class FusedTrainer:
                 dst.copy_(src)
         if self.graph is None and self.warm >= 2:
             self._capture()                  # records only; the replay below executes this step
+        self._last_args = self.static
         if self.graph is not None:
             self._replay()
             out = self.loss_out
@@ -236,4 +294,5 @@ class FusedTrainer:
             self.warm += 1
             out = self._body(*self.static)
         self.engine._packed_version = None   # params were updated in place by the Adam kernel
+        self._post_step()
         return out

@@ -247,6 +247,7 @@ class ModelPlain(ModelBase):
         if self.trainer is not None:
             self.trainer.lr = self.G_optimizer.param_groups[0]["lr"]
             loss = self.trainer.step(self.L, self.H, *self._step_cond())
+            self.trainer.check_range()   # fp32x3: settle this step's range flag now (the loss is read below anyway)
             self.E = None  # the fused step keeps E in its plan buffer; test() recomputes
             self.log_dict["G_loss"] = loss.item()
             return

@@ -1,10 +1,12 @@
-"""The split-bf16 ("fp32x3") path: every contraction as hi.hi + hi.lo + lo.hi of hi/lo bf16 pairs, the
-fp32 reference's arithmetic on the bf16 matrix cores (the reference trains SwinIR classical x4 in fp32:
-models/model_plain.py:31-36, options/swinir/train_swinir_sr_classical.json has no amp_enabled).
+"""The fp16-pair ("fp32x3") path: every contraction as hi.hi + hi.lo + lo.hi of hi/lo fp16 pairs of power-of-2
+scaled operands (x 2^e: weights 2^12, activations 2^4, data gradients 2^(log2 numel + 4)), the fp32 reference's
+arithmetic on the 16-bit matrix cores (the reference trains SwinIR classical x4 in fp32: models/model_plain.py:31-36,
+options/swinir/train_swinir_sr_classical.json has no amp_enabled).
 
 Kernels are checked against float64 torch references at the fp32 engine's tolerances (2e-5 .. 5e-5
-relative); the whole network passes the fp32 engine's own oracle bars unchanged (outputs < 1e-4, gradients
-< 1e-3 / 2e-3, PSNR < 1e-3 dB, the 3-step ModelPlain trajectory < 1e-4)."""
+relative); the whole classical x4 network against the CPU oracle at SURVEY.md §8d's fp32 bar (outputs < 1e-5
+relative), gradients < 1e-3, PSNR < 1e-3 dB; the 3-step ModelPlain trajectory < 1e-4.  The range guard that
+keeps the fixed exponents safe: tests/test_x3_range_gpu.py."""
 import numpy as np
 import pytest
 import torch
@@ -362,7 +364,8 @@ def test_swinir_small_x3_vs_golden(tag, ups, sc):
 
 
 def test_swinir_classical_full_x3_vs_oracle():
-    """test_swinir_gpu.py::test_swinir_classical_full_fp32_vs_oracle's bars on the split-bf16 engine."""
+    """The full classical x4 network on the fp16-pair engine vs the CPU oracle: outputs within SURVEY.md §8d's fp32
+    bar (1e-5 relative; measured ~1e-6), PSNR float / uint8 within 1e-3 dB, every gradient within 1e-3."""
     from test_swinir_gpu import classical_x4, synth_batch
     net = classical_x4("fp32x3")
     ref = osw.SwinIR(4, 3, 48, 8, 1.0, [6] * 6, 180, [6] * 6, 2, "pixelshuffle")
@@ -372,7 +375,8 @@ def test_swinir_classical_full_x3_vs_oracle():
     torch.nn.functional.l1_loss(Er, Hh).backward()
     net = net.to(dev).train()
     E = net(L.to(dev))
-    assert rel(E, Er) < 1e-4
+    print("classical x4 fp32x3: output rel", rel(E, Er))
+    assert rel(E, Er) < 1e-5
     for i in range(2):
         pf_gpu, pf_cpu = oimg.psnr_float(E[i].cpu(), Hh[i]), oimg.psnr_float(Er[i].detach(), Hh[i])
         assert abs(pf_gpu - pf_cpu) < 1e-3
@@ -382,12 +386,13 @@ def test_swinir_classical_full_x3_vs_oracle():
     torch.nn.functional.l1_loss(E, Hh.to(dev)).backward()
     gref = dict(ref.named_parameters())
     worst = max((rel(p.grad, gref[k].grad), k) for k, p in net.named_parameters())
+    print("classical x4 fp32x3: worst gradient rel", worst)
     assert worst[0] < 1e-3, worst
 
 
 @pytest.mark.parametrize("use_graph", [False, True])
 def test_trainer_x3_matches_reference_trajectory(use_graph):
-    """3 fused-trainer steps on the split-bf16 engine against the reference ModelPlain trajectory (1e-4)."""
+    """3 fused-trainer steps on the fp16-pair engine against the reference ModelPlain trajectory (1e-4)."""
     z = load_golden("train_trajectory")
     mk = lambda: SwinIR(upscale=4, in_chans=3, img_size=16, window_size=8, img_range=1.0, depths=[2, 2], embed_dim=60,
                         num_heads=[6, 6], mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.0,
@@ -412,7 +417,7 @@ def test_trainer_x3_matches_reference_trajectory(use_graph):
 
 
 def test_droppath_injected_masks_x3_vs_oracle():
-    """DropPath with the same keep masks in the split-bf16 engine and the oracle (fwd + every gradient)."""
+    """DropPath with the same keep masks in the fp16-pair engine and the oracle (fwd + every gradient)."""
     torch.manual_seed(4)
     net = SwinIR(upscale=2, in_chans=3, img_size=16, window_size=8, img_range=1.0, depths=[2, 2], embed_dim=60,
                  num_heads=[6, 6], mlp_ratio=2, upsampler="pixelshuffle", drop_path_rate=0.3, compute_dtype="fp32x3")

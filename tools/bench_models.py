@@ -36,26 +36,28 @@ def timed(step, steps, warmup):
     return (time.perf_counter() - t0) / steps, out
 
 
-def run(name, steps, warmup, dev):
+def run(name, steps, warmup, dev, dtype="bf16"):
+    """dtype: the engine's compute dtype -- "bf16" (bf16 MFMA, fp32 accumulation), "fp32" (exact fp32 MFMA: the
+    reference's arithmetic for the fp32 option files, C3 / C5) or "fp32x3" where the engine has it."""
     from kair_amd.engine.trainer import FusedTrainer
     torch.manual_seed(0)
     g = torch.Generator().manual_seed(1)
     if name == "dncnn":
         from kair_amd.models.network_dncnn import DnCNN
-        mk = lambda: DnCNN(1, 1, 64, 17, "BR", compute_dtype="bf16")   # noqa: E731
+        mk = lambda: DnCNN(1, 1, 64, 17, "BR", compute_dtype=dtype)   # noqa: E731
         B, shp, sc = 64, (1, 40, 40), 1
     elif name == "swinir_light":
         from kair_amd.models.network_swinir import SwinIR
         mk = lambda: SwinIR(upscale=2, in_chans=3, img_size=64, window_size=8, img_range=1.0, depths=[6] * 4,   # noqa: E731
                             embed_dim=60, num_heads=[6] * 4, mlp_ratio=2, upsampler="pixelshuffledirect",
-                            resi_connection="1conv", compute_dtype="bf16")
+                            resi_connection="1conv", compute_dtype=dtype)
         B, shp, sc = 64, (3, 64, 64), 2
     elif name == "rrdbnet":
         from kair_amd.models.network_rrdbnet import RRDBNet
-        mk = lambda: RRDBNet(3, 3, 64, 23, 32, 4, compute_dtype="bf16")   # noqa: E731
+        mk = lambda: RRDBNet(3, 3, 64, 23, 32, 4, compute_dtype=dtype)   # noqa: E731
         B, shp, sc = 16, (3, 32, 32), 4
     elif name == "usrnet":
-        return run_usrnet(steps, warmup, dev)
+        return run_usrnet(steps, warmup, dev, dtype)
     else:
         raise SystemExit(f"unknown config {name}")
     net, ema = mk().to(dev).train(), mk().to(dev).eval()
@@ -67,10 +69,10 @@ def run(name, steps, warmup, dev):
     return B, dt, float(loss.item())
 
 
-def run_usrnet(steps, warmup, dev):
+def run_usrnet(steps, warmup, dev, dtype="bf16"):
     from kair_amd.engine.trainer import FusedTrainer
     from kair_amd.models.network_usrnet import USRNet
-    net = USRNet(n_iter=6, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2, compute_dtype="bf16").to(dev).train()
+    net = USRNet(n_iter=6, h_nc=32, in_nc=4, out_nc=3, nc=[16, 32, 64, 64], nb=2, compute_dtype=dtype).to(dev).train()
     tr = FusedTrainer(net, None, lr=1e-4, E_decay=0.0, use_graph=True)   # train_usrnet.json: E_decay 0
     g = torch.Generator().manual_seed(2)
     B, lq, sf = 48, 128, 4
@@ -90,16 +92,17 @@ def main():
     ap.add_argument("configs", nargs="*", default=["dncnn", "swinir_light", "rrdbnet", "usrnet"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for name in a.configs:
-        B, dt, loss = run(name, a.steps, a.warmup, dev)
+        B, dt, loss = run(name, a.steps, a.warmup, dev, a.dtype)
         pps = B / dt
         tf = pps * TRAIN_GFLOP[name] / 1e3
         print(json.dumps({"config": name, "patches_per_s": round(pps, 2), "ms_per_step": round(dt * 1e3, 3), "batch": B,
                           "train_gflop_per_patch": TRAIN_GFLOP[name], "achieved_tflops": round(tf, 2),
                           "frac_of_bf16_peak": round(tf / PEAK_BF16_TFLOPS, 4), "loss": round(loss, 6),
-                          "dtype": "bf16", "n_gpus": 1}), flush=True)
+                          "dtype": a.dtype, "n_gpus": 1}), flush=True)
         torch.cuda.empty_cache()
 
 
