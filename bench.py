@@ -168,7 +168,7 @@ class _GraphEvents:
     duration inside the graph-replayed step -- the same execution (stream concurrency, back-to-back launches,
     no host gaps) that rocprofv3 --kernel-trace records for the timed bench step."""
 
-    def __init__(self):
+    def __init__(self, n=4096):
         import ctypes
         path = "libamdhip64.so"
         try:   # the HIP runtime this process already loaded (torch's), not a second copy
@@ -185,12 +185,18 @@ class _GraphEvents:
         self.rt.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
         self.rt.hipEventDestroy.argtypes = [ctypes.c_void_p]
         self.events = []
+        for _ in range(n):   # created up front: no event creation inside the capture
+            ev = ctypes.c_void_p()
+            if self.rt.hipEventCreateWithFlags(ctypes.byref(ev), 0) != 0:
+                raise RuntimeError("hipEventCreateWithFlags failed")
+            self.events.append(ev)
+        self.used = 0
 
     def record(self):
-        ev = self.ct.c_void_p()
-        if self.rt.hipEventCreateWithFlags(self.ct.byref(ev), 0) != 0:
-            raise RuntimeError("hipEventCreateWithFlags failed")
-        self.events.append(ev)
+        if self.used == len(self.events):
+            raise RuntimeError("graph timing: event pool exhausted")
+        ev = self.events[self.used]
+        self.used += 1
         rc = self.rt.hipEventRecordWithFlags(ev, self.ct.c_void_p(torch.cuda.current_stream().cuda_stream), 1)
         if rc != 0:
             raise RuntimeError(f"hipEventRecordWithFlags(external) failed ({rc})")
@@ -272,8 +278,10 @@ def time_roles(tr, serial=False, graph=False, replays=3):
             cs.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(cs):
                 g.capture_begin(pool=torch.cuda.graph_pool_handle())
-                tr._fwd_bwd(*tr.static)
-                g.capture_end()
+                try:
+                    tr._fwd_bwd(*tr.static)
+                finally:   # end the capture whatever happened inside it (a graph destroyed mid-capture aborts)
+                    g.capture_end()
             torch.cuda.current_stream().wait_stream(cs)
             torch.cuda.synchronize()
             times = [0.0] * len(rec)

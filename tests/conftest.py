@@ -36,3 +36,22 @@ def sub_grads(z, prefix):
 def gpu_available():
     import torch
     return torch.cuda.is_available()
+
+
+def state_rel_excluding_kbias(sd, sdr, embed_dim):
+    """{key: relative L2 distance} of two SwinIR state dicts, with the KEY part of every attn.qkv.bias left out, and
+    the largest absolute difference over those key-bias parts.  The key bias has an identically zero gradient in
+    exact arithmetic (softmax is invariant to a per-query constant: q . (k + b) = q . k + q . b), so in any fp32
+    implementation its gradient is rounding noise, and Adam's first steps (m / sqrt(v)) turn that noise into +-lr
+    moves whose signs no two summation orders share: those elements are compared by the bound |diff| <= 2 lr steps
+    instead (tests pass it as kbias_bound)."""
+    import torch
+    C = embed_dim
+    out, kmax = {}, 0.0
+    for k in sdr:
+        a, b = sd[k].detach().double().cpu(), sdr[k].detach().double().cpu()
+        if k.endswith("attn.qkv.bias"):
+            kmax = max(kmax, (a[C:2 * C] - b[C:2 * C]).abs().max().item())
+            a, b = torch.cat([a[:C], a[2 * C:]]), torch.cat([b[:C], b[2 * C:]])
+        out[k] = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+    return out, kmax

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():
     pytest.skip("needs a HIP device", allow_module_level=True)
 
-from conftest import load_golden, sub_grads, sub_state  # noqa: E402
+from conftest import load_golden, state_rel_excluding_kbias, sub_grads, sub_state  # noqa: E402
 from kair_amd.models.network_swinir import SwinIR  # noqa: E402
 from kair_amd.engine.trainer import FusedTrainer  # noqa: E402
 from oracle import swinir as osw  # noqa: E402
@@ -131,12 +131,13 @@ def test_fused_trainer_variant_vs_oracle_trainer(tag, dt):
         loss = tr.step(L.to(dev), Hh.to(dev)).item()
         _, lo = otr.optimize_parameters(L, Hh)
         assert abs(loss - lo) < 1e-4 * abs(lo), (loss, lo)
-    sd, sdr = net.state_dict(), ref.state_dict()
-    for k in sdr:
-        assert rel(sd[k].float(), sdr[k].float()) < 1e-4, k
-    sd, sdr = ema.state_dict(), ref_e.state_dict()
-    for k in sdr:
-        assert rel(sd[k].float(), sdr[k].float()) < 1e-4, k
+    # (the key part of each qkv bias: zero gradient in exact arithmetic, Adam's +-lr moves on rounding noise --
+    # conftest.state_rel_excluding_kbias -- bounded by 2 lr per step)
+    for mine, theirs in ((net, ref), (ema, ref_e)):
+        r, kmax = state_rel_excluding_kbias(mine.state_dict(), theirs.state_dict(), 60)
+        worst = max((v, k) for k, v in r.items())
+        assert worst[0] < 1e-4, worst
+        assert kmax <= 2 * 2e-4 * 4, kmax
 
 
 def test_charbonnier_loss_kernel():
@@ -185,8 +186,9 @@ def test_fused_trainer_charbonnier_vs_oracle_trainer(dt):
         loss = tr.step(L.to(dev), Hh.to(dev)).item()
         _, lo = otr.optimize_parameters(L, Hh)
         assert abs(loss - lo) < 1e-4 * abs(lo), (loss, lo)
-    sd, sdr = net.state_dict(), ref.state_dict()
-    for k in sdr:
+    r, kmax = state_rel_excluding_kbias(net.state_dict(), ref.state_dict(), 60)
+    for k, v in r.items():
         # Adam's first steps normalise each gradient element, so summation-order noise on a bias
         # element whose gradient is near zero moves it by up to lr: biases 1e-3, weights 1e-4
-        assert rel(sd[k].float(), sdr[k].float()) < (1e-3 if sdr[k].dim() == 1 else 1e-4), k
+        assert v < (1e-3 if ref.state_dict()[k].dim() == 1 else 1e-4), (k, v)
+    assert kmax <= 2 * 2e-4 * 4, kmax

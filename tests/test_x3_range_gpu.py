@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():
     pytest.skip("needs a HIP device", allow_module_level=True)
 
+from conftest import state_rel_excluding_kbias  # noqa: E402
 from kair_amd import _hip as H  # noqa: E402
 from kair_amd.engine.trainer import FusedTrainer  # noqa: E402
 from kair_amd.models.network_swinir import SwinIR  # noqa: E402
@@ -96,15 +97,17 @@ def _train(net, ema, ref, ref_e, scale=1.0, loss_weight=1.0, steps=4, use_graph=
     return tr, losses, olosses
 
 
-def _assert_matches(net, ema, ref, ref_e, losses, olosses, tol=1e-4):
+def _assert_matches(net, ema, ref, ref_e, losses, olosses, tol=1e-4, steps=4, lr=2e-4):
+    """Losses and the trained G / EMA states vs the oracle trainer at `tol` (relative L2 per tensor); the key part
+    of each qkv bias (zero gradient in exact arithmetic: Adam moves it by +-lr on rounding noise) within 2 lr per
+    step (conftest.state_rel_excluding_kbias)."""
     for a, b in zip(losses, olosses):
         assert abs(a - b) < tol * abs(b), (losses, olosses)
-    sd, sdr = net.state_dict(), ref.state_dict()
-    worst = max((rel(sd[k].float(), sdr[k].float()), k) for k in sdr)
-    assert worst[0] < tol, worst
-    sd, sdr = ema.state_dict(), ref_e.state_dict()
-    worst = max((rel(sd[k].float(), sdr[k].float()), k) for k in sdr)
-    assert worst[0] < tol, worst
+    for mine, theirs in ((net, ref), (ema, ref_e)):
+        r, kmax = state_rel_excluding_kbias(mine.state_dict(), theirs.state_dict(), 60)
+        worst = max((v, k) for k, v in r.items())
+        assert worst[0] < tol, worst
+        assert kmax <= 2 * lr * steps, kmax
 
 
 @pytest.mark.parametrize("use_graph", [True, False])
