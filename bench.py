@@ -162,68 +162,57 @@ _TIMED = ("gemm_nt", "gemm_tn", "wgrad_finalize", "colsum", "layernorm_fwd", "la
           "conv3x3_narrow_fwd_x3", "conv3x3_narrow_dgrad_x3", "conv3x3_narrow_wgrad_x3")
 
 
-class _GraphEvents:
-    """HIP events recorded as EXTERNAL event nodes of a captured graph (hipEventRecordWithFlags(...,
-    hipEventRecordExternal)): replaying the graph stamps them, so a pair around a launch gives that kernel's
-    duration inside the graph-replayed step -- the same execution (stream concurrency, back-to-back launches,
-    no host gaps) that rocprofv3 --kernel-trace records for the timed bench step."""
+class _GraphStamps:
+    """Stream-ordered timestamps inside a captured graph: kair_timestamp writes the device's 100 MHz real-time
+    counter into stamps[i] when its one-lane launch runs, one before and one after every libkair launch on the
+    launch's own stream (the side stream's too).  Replaying the graph stamps the graph-replayed step itself --
+    stream concurrency, back-to-back launches, no host gaps -- what rocprofv3 --kernel-trace records for the timed
+    bench step.  A stamp pair with nothing between it (calibrated at the head of the capture) is subtracted."""
+
+    NCAL = 16
 
     def __init__(self, n=4096):
-        import ctypes
-        path = "libamdhip64.so"
-        try:   # the HIP runtime this process already loaded (torch's), not a second copy
-            with open("/proc/self/maps") as f:
-                for line in f:
-                    if "libamdhip64" in line:
-                        path = line.split()[-1]
-                        break
-        except OSError:
-            pass
-        self.ct = ctypes
-        self.rt = ctypes.CDLL(path)
-        self.rt.hipEventRecordWithFlags.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
-        self.rt.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
-        self.rt.hipEventDestroy.argtypes = [ctypes.c_void_p]
-        self.events = []
-        for _ in range(n):   # created up front: no event creation inside the capture
-            ev = ctypes.c_void_p()
-            if self.rt.hipEventCreateWithFlags(ctypes.byref(ev), 0) != 0:
-                raise RuntimeError("hipEventCreateWithFlags failed")
-            self.events.append(ev)
-        self.used = 0
+        from kair_amd import _hip as H
+        self.H = H
+        self.buf = torch.zeros(2 * n + 2 * self.NCAL, dtype=torch.int64, device="cuda")
+        self.used = 2 * self.NCAL
+
+    def calibrate(self):
+        for i in range(self.NCAL):
+            self.H.timestamp(self.buf, 2 * i)
+            self.H.timestamp(self.buf, 2 * i + 1)
 
     def record(self):
-        if self.used == len(self.events):
-            raise RuntimeError("graph timing: event pool exhausted")
-        ev = self.events[self.used]
+        if self.used == self.buf.numel():
+            raise RuntimeError("graph timing: stamp buffer exhausted")
+        i = self.used
         self.used += 1
-        rc = self.rt.hipEventRecordWithFlags(ev, self.ct.c_void_p(torch.cuda.current_stream().cuda_stream), 1)
-        if rc != 0:
-            raise RuntimeError(f"hipEventRecordWithFlags(external) failed ({rc})")
-        return ev
+        self.H.timestamp(self.buf, i)
+        return i
 
-    def elapsed(self, e0, e1):
-        ms = self.ct.c_float()
-        if self.rt.hipEventElapsedTime(self.ct.byref(ms), e0, e1) != 0:
-            raise RuntimeError("hipEventElapsedTime failed")
-        return ms.value
+    def read(self):
+        t = self.buf.cpu().tolist()
+        cal = sorted(t[2 * i + 1] - t[2 * i] for i in range(self.NCAL))
+        self.cal = cal[len(cal) // 2]
+        self.t = t
+
+    def elapsed(self, i0, i1):   # ms
+        return max(0, self.t[i1] - self.t[i0] - self.cal) * 1e-5
 
     def close(self):
-        for ev in self.events:
-            self.rt.hipEventDestroy(ev)
-        self.events = []
+        pass
 
 
 def time_roles(tr, serial=False, graph=False, replays=3):
     """{role: {kernel, launches, ms (mean per launch), bytes, flops}} over one fwd + loss + bwd.
-    graph: the pass is captured as a HIP graph with an external event node on the launch stream before and
-    after every libkair launch, and replayed `replays` times; a launch's time is its mean over the replays --
+    graph: the pass is captured as a HIP graph with a device timestamp launch (kair_timestamp) on the launch stream
+    before and after every libkair launch, and replayed `replays` times; a launch's time is its mean over the replays --
     the kernel durations of the graph-replayed bench step (what the committed rocprofv3 summary of the bench
     command averages).  Otherwise eager, a torch event pair per launch; serial: the engine's deferred side-stream
     work runs in place on the main stream for this pass (every event pair brackets exactly one kernel)."""
     from kair_amd import _hip as H
     rec = []
-    gev = _GraphEvents() if graph else None
+    gev = _GraphStamps() if graph else None
 
     # the engine's thin launch helpers: a role is named by their caller (the layer's call site), not by them
     helpers = ("_nt", "_wgrad", "_wg", "_run_conv_job", "_bias_colsum")
@@ -279,6 +268,7 @@ def time_roles(tr, serial=False, graph=False, replays=3):
             with torch.cuda.stream(cs):
                 g.capture_begin(pool=torch.cuda.graph_pool_handle())
                 try:
+                    gev.calibrate()
                     tr._fwd_bwd(*tr.static)
                 finally:   # end the capture whatever happened inside it (a graph destroyed mid-capture aborts)
                     g.capture_end()
@@ -288,6 +278,7 @@ def time_roles(tr, serial=False, graph=False, replays=3):
             for _ in range(replays):
                 g.replay()
                 torch.cuda.synchronize()
+                gev.read()
                 for i, (_, _, _, e0, e1) in enumerate(rec):
                     times[i] += gev.elapsed(e0, e1) / replays
             del g
@@ -770,10 +761,11 @@ def main():
                 roles, timing = time_roles(tr), f"in_step (graph events failed: {e!r})"
             except Exception as e2:  # noqa: BLE001
                 roles = {"error": {"kernel": repr(e2), "ms_total": 0.0}}
-    TIMING = ("kernel duration inside the graph-replayed training step: one capture of fwd+loss+bwd with an external "
-              "HIP event node (hipEventRecordWithFlags, hipEventRecordExternal) on the launch stream before and after every "
-              "libkair launch, side stream included, replayed 3 times; mean per launch -- the quantity rocprofv3 "
-              "--kernel-trace reports for the graph-replayed bench step (profiles/*_kernel_stats.csv)") if timing == "graph" \
+    TIMING = ("kernel duration inside the graph-replayed training step: one capture of fwd+loss+bwd with a stream-ordered "
+              "device timestamp (kair_timestamp: the 100 MHz real-time counter) on the launch stream before and after every "
+              "libkair launch, side stream included, minus an empty stamp pair; replayed 3 times; mean per launch -- the "
+              "quantity rocprofv3 --kernel-trace reports for the graph-replayed bench step (profiles/*_kernel_stats.csv)") \
+        if timing == "graph" \
         else "eager in-step mean per launch: " + timing
 
     def roof(name, d):

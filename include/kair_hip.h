@@ -515,6 +515,9 @@ int kair_adam_ema_ex(float* p, const float* g, float* m, float* v, float* ema, l
  * fp32 reference has no operand window.) */
 int kair_range_check(const float* g, const float* p, long n, const float* loss, float p_limit, unsigned* flag,
                      void* stream);
+/* Measurement: buf[idx] = the device real-time counter (100 MHz) when this one-lane launch runs, stream-ordered --
+ * stamps around the kernels of a captured HIP graph (bench.py's in-graph kernel durations). */
+int kair_timestamp(unsigned long long* buf, int idx, void* stream);
 
 /* USRNet (network_usrnet_v1.py) -------------------------------------------------------------
  * Complex plane sets are float2 [planes][W][H] (TRANSPOSED: column-major per plane).            */

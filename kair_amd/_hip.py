@@ -166,6 +166,7 @@ _SIGS = {
     "kair_adam_ema_ex": [c_vp, c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp,
                          c_vp],
     "kair_range_check": [c_vp, c_vp, c_long, c_vp, c_float, c_vp, c_vp],
+    "kair_timestamp": [c_vp, c_int, c_vp],
     "kair_usr_fft_rows": [c_vp, c_int, c_int, c_long, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],
     "kair_usr_fft_cols": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
                           c_vp],
@@ -698,6 +699,11 @@ def adam_ema(p, g, m, v, ema, n, lr_t, beta1, beta2, eps, wd, decay, skip=None):
         return
     check(lib().kair_adam_ema(ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), n, ptr(lr_t), beta1, beta2, eps, wd, decay,
                               stream_ptr()), "adam_ema")
+
+
+def timestamp(buf, idx):
+    """buf[idx] (int64 device tensor) = the device real-time counter (100 MHz) when this stream position runs."""
+    check(lib().kair_timestamp(ptr(buf), idx, stream_ptr()), "timestamp")
 
 
 def range_check(g, p, loss, p_limit, flag):

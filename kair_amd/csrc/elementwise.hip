@@ -1025,6 +1025,20 @@ extern "C" int kair_adam_ema_ex(float* p, const float* g, float* m, float* v, fl
   return 0;
 }
 
+// measurement: one lane writes the device's constant-rate real-time counter (100 MHz, s_memrealtime) into buf[idx]
+// when the launch runs -- stream-ordered stamps around the kernels of a captured graph (bench.py's in-graph
+// kernel durations)
+__global__ void timestamp_kernel(unsigned long long* buf, int idx) {
+  if (threadIdx.x == 0) buf[idx] = __builtin_amdgcn_s_memrealtime();
+}
+
+extern "C" int kair_timestamp(unsigned long long* buf, int idx, void* stream) {
+  KAIR_CHECK_ARG(buf && idx >= 0, "timestamp: bad args");
+  hipLaunchKernelGGL(timestamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, buf, idx);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int kair_range_check(const float* g, const float* p, long n, const float* loss, float p_limit, unsigned* flag,
                                 void* stream) {
   KAIR_CHECK_ARG(g && p && flag && n > 0 && p_limit > 0.f, "range_check: bad args");

@@ -797,12 +797,13 @@ class SwinIREngine:
         2^12 below fp16's overflow."""
         return int(round(math.log2(max(numel, 1) / max(abs(weight), 1e-30)))) + self.x3_gexp_off
 
-    def x3_backoff(self, step=None):
-        """Range guard reaction (kair_range_check saw an inf / NaN the split operands can cause): lower the
-        activation and gradient exponents by `step` (default X3_BACKOFF_STEP) so every operand class gains that
-        much headroom below fp16's 65504 (the lo halves of the smallest values go subnormal first: an absolute
-        error <= 2^-25 of the scaled unit, i.e. fp32 rounding class for O(1) data).  The caller re-runs the step
-        (re-captured graph).  Raises after X3_BACKOFF_MAX events: the data is not finite in fp32 either."""
+    def x3_backoff(self, step=None, act=True, grad=True):
+        """Range guard reaction (kair_range_check saw an inf / NaN the split operands can cause): lower the activation
+        exponent (act: a forward overflow, the loss went non-finite) and / or the gradient exponent (grad: a backward
+        overflow) by `step` (default X3_BACKOFF_STEP), so that operand class gains that much headroom below fp16's
+        65504 (the lo halves of its smallest values go subnormal first: an absolute error <= 2^-25 of the scaled
+        unit).  The caller re-runs the step (re-captured graph).  Raises after X3_BACKOFF_MAX events: the data is not
+        finite in fp32 either, or a weight left its pack window."""
         if not self.x3:
             raise RuntimeError("x3_backoff: not an fp32x3 engine")
         if self.x3_backoffs >= self.X3_BACKOFF_MAX:
@@ -810,8 +811,10 @@ class SwinIREngine:
                                f"back-offs (activation 2^{self.X3_AEXP}, gradient offset 2^{self.x3_gexp_off}): the data "
                                f"is not finite, or a weight left its pack window |w| < 2^{16 - H.X3_WEXP}")
         step = self.X3_BACKOFF_STEP if step is None else int(step)
-        self.X3_AEXP -= step
-        self.x3_gexp_off -= step
+        if act:
+            self.X3_AEXP -= step
+        if grad:
+            self.x3_gexp_off -= step
         self.x3_backoffs += 1
         return self.X3_AEXP, self.x3_gexp_off
 
@@ -1367,7 +1370,7 @@ class SwinIRFunction(torch.autograd.Function):
             while engine.x3 and not bool(torch.isfinite(E).all()):
                 if not bool(torch.isfinite(x).all()):
                     raise RuntimeError("kair_amd SwinIR: non-finite input")
-                engine.x3_backoff()
+                engine.x3_backoff(act=True, grad=False)
                 E = engine.forward(x.float(), drop)
         ctx.engine = engine
         ctx.params = params

@@ -177,7 +177,12 @@ class FusedTrainer:
                 return
             if bits & 4:
                 raise RuntimeError(f"fp32x3 range guard: a parameter is not finite at step {self.t}")
-            exps = self.engine.x3_backoff()
+            # one GPU: a non-finite loss means the forward overflowed (activation exponent), a finite loss with
+            # non-finite gradients the backward (gradient exponent); several ranks see only the all-reduced
+            # gradients (the same bits everywhere), so both exponents drop
+            fwd = bool(bits & 2) or self.world > 1
+            bwd = not (bits & 2) or self.world > 1
+            exps = self.engine.x3_backoff(act=fwd, grad=bwd)
             self.range_events.append((self.t, bits, exps))
             # re-run step t (its Adam scalars are still in self.scal, its batch in the static / last inputs)
             if not self.use_graph or self.graph is None:

@@ -97,16 +97,21 @@ def _train(net, ema, ref, ref_e, scale=1.0, loss_weight=1.0, steps=4, use_graph=
     return tr, losses, olosses
 
 
-def _assert_matches(net, ema, ref, ref_e, losses, olosses, tol=1e-4, steps=4, lr=2e-4):
-    """Losses and the trained G / EMA states vs the oracle trainer at `tol` (relative L2 per tensor); the key part
-    of each qkv bias (zero gradient in exact arithmetic: Adam moves it by +-lr on rounding noise) within 2 lr per
-    step (conftest.state_rel_excluding_kbias)."""
+def _assert_matches(net, ema, ref, ref_e, losses, olosses, tol=1e-4, steps=4, lr=2e-4, btol=2e-3):
+    """Losses and the trained G / EMA states vs the oracle trainer: weights at `tol` (relative L2 per tensor);
+    1-D parameters (biases, LayerNorm affine, initialised at 0 / 1: after a few steps they ARE Adam's m / sqrt(v)
+    updates, which normalise each element's gradient, so a near-zero gradient element moves by up to lr on
+    summation-order noise) at `btol`; the key part of each qkv bias (zero gradient in exact arithmetic) within
+    2 lr per step (conftest.state_rel_excluding_kbias)."""
     for a, b in zip(losses, olosses):
         assert abs(a - b) < tol * abs(b), (losses, olosses)
     for mine, theirs in ((net, ref), (ema, ref_e)):
-        r, kmax = state_rel_excluding_kbias(mine.state_dict(), theirs.state_dict(), 60)
-        worst = max((v, k) for k, v in r.items())
+        sd = theirs.state_dict()
+        r, kmax = state_rel_excluding_kbias(mine.state_dict(), sd, 60)
+        worst = max((v, k) for k, v in r.items() if sd[k].dim() > 1)
         assert worst[0] < tol, worst
+        worst = max((v, k) for k, v in r.items() if sd[k].dim() <= 1)
+        assert worst[0] < btol, worst
         assert kmax <= 2 * lr * steps, kmax
 
 
@@ -118,7 +123,7 @@ def test_guard_activations_near_1e4(use_graph):
     tr, losses, olosses = _train(net, ema, ref, ref_e, scale=1e4, use_graph=use_graph)
     assert tr.range_events, "the guard never fired"
     assert tr.range_events[0][0] == 1   # flagged at the first step, which was re-run
-    assert tr.engine.X3_AEXP < 4
+    assert tr.engine.X3_AEXP < 4 and tr.engine.x3_gexp_off == 4   # only the activation class backed off
     _assert_matches(net, ema, ref, ref_e, losses, olosses)
 
 
@@ -131,6 +136,7 @@ def test_guard_forced_gradient_exponent():
         eng.x3_gexp_off += 12
     tr, losses, olosses = _train(net, ema, ref, ref_e, setup=force)
     assert tr.range_events and tr.range_events[0][1] & 1, tr.range_events
+    assert tr.engine.X3_AEXP == 4   # only the gradient class backed off
     _assert_matches(net, ema, ref, ref_e, losses, olosses)
 
 
