@@ -326,7 +326,7 @@ def rocprof_name(fn, a):
         return _x3_nt_ring_name(a) if _x3_ring_nt(a) else "gemm_nt_x3_kernel"
     if fn == "gemm_tn" and a[7] == X3:
         if _x3_ring_tn(a):
-            return f"gemm_tn_x3_ring<{1 if a[1].mode == 1 else 0}>"
+            return f"gemm_tn_x3_ring<{1 if a[1].mode == 1 else 0}, {'true' if a[0].dtype == 3 else 'false'}>"
         return "gemm_tn_x3_kernel"
     if fn in ("layernorm_fwd", "layernorm_bwd"):
         return {"layernorm_fwd": "ln_fwd_kernel", "layernorm_bwd": "ln_bwd_kernel"}[fn]
@@ -342,6 +342,8 @@ def _x3_ring_tn(a):
     """Whether an x3 gemm_tn launch takes the ring kernel (gemm_x3.hip tn_x3_ring_ok)."""
     A, B, N, K = a[0], a[1], a[5], a[6]
     ones_ok = lambda o: o.ones_col < 0 or o.ones_in_data
+    if A.dtype == 3 and B.dtype == 3:   # fp16 pairs (row operands)
+        return A.mode == 0 and B.mode == 0 and N % 8 == 0 and K % 8 == 0 and ones_ok(A) and ones_ok(B)
     return (A.dtype == 0 and B.dtype == 0 and A.mode == 0 and N % 4 == 0 and K % 4 == 0 and ones_ok(A)
             and not A.rowscale and not B.rowscale and
             (B.mode == 0 or (B.mode == 1 and B.im_C % 4 == 0 and K == 9 * B.im_C and not B.im_flip and B.im_up != 2

@@ -258,8 +258,14 @@ int kair_colsum(const kair_operand* G, long M, int Np, const kair_wmap* map, flo
 int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype, long ldy, const float* gamma,
                        const float* beta, float* mean, float* rstd, long M, int C, float eps,
                        int win_H, int win_W, int win_ws, int win_shift, int one_col, void* stream);
+/* kair_layernorm_fwd with an x3 fp16-pair output (the fp32x3 engine's GEMM operand, split once here instead of
+ * in every consuming GEMM): y_hi = f16(y 2^x3_exp), y_lo = f16(y 2^x3_exp - y_hi); the ones column reads 2^x3_exp. */
+int kair_layernorm_fwd_x3(const float* x, long ldx, void* y_hi, void* y_lo, long ldy, const float* gamma,
+                          const float* beta, float* mean, float* rstd, long M, int C, float eps,
+                          int win_H, int win_W, int win_ws, int win_shift, int one_col, int x3_exp, void* stream);
 /* A row-scaled, cast copy of an fp32 token-row matrix (the next GEMM's A operand):
- * out[token_to_win(t)][c] = rowscale[t / rows_per_scale] * src[t][c]  (window order when win_ws > 0). */
+ * out[token_to_win(t)][c] = rowscale[t / rows_per_scale] * src[t][c]  (window order when win_ws > 0).
+ * dtype KAIR_F16: an x3 fp16 pair -- out holds hi = f16(v 2^x3_exp), out_lo lo = f16(v 2^x3_exp - hi). */
 typedef struct {
   void* out;
   int dtype;
@@ -267,6 +273,8 @@ typedef struct {
   const float* rowscale; /* NULL => 1 */
   int rows_per_scale;
   int win_H, win_W, win_ws, win_shift;
+  void* out_lo;          /* dtype KAIR_F16: the lo plane (same layout as out)                          */
+  int x3_exp;            /* dtype KAIR_F16: the pair's power-of-2 exponent                              */
 } kair_copy_desc;
 int kair_row_copy(const float* src, long ld_src, long M, int C, const kair_copy_desc* copy, void* stream);
 

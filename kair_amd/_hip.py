@@ -42,14 +42,19 @@ class Operand(ctypes.Structure):
 
 class CopyDesc(ctypes.Structure):
     _fields_ = [("out", c_vp), ("dtype", c_int), ("ld", c_long), ("rowscale", c_vp), ("rows_per_scale", c_int),
-                ("win_H", c_int), ("win_W", c_int), ("win_ws", c_int), ("win_shift", c_int)]
+                ("win_H", c_int), ("win_W", c_int), ("win_ws", c_int), ("win_shift", c_int), ("out_lo", c_vp),
+                ("x3_exp", c_int)]
 
 
-def copy_desc(out, ld=None, rowscale=None, rows_per_scale=1, win=None):
-    """Row-scaled cast copy target (GEMM A operand); win puts the rows in Swin window order."""
+def copy_desc(out, ld=None, rowscale=None, rows_per_scale=1, win=None, x3_exp=0):
+    """Row-scaled cast copy target (GEMM A operand); win puts the rows in Swin window order.  out an fp16 pair
+    [2, ...] (hi plane, lo plane): the x3 pair of v 2^x3_exp."""
     d = CopyDesc()
     d._keep = (out, rowscale)
-    d.out, d.dtype = ptr(out), dtype_code(out)
+    if out.dtype == torch.float16:
+        d.out, d.out_lo, d.dtype, d.x3_exp = ptr(out[0]), ptr(out[1]), F16, int(x3_exp)
+    else:
+        d.out, d.dtype = ptr(out), dtype_code(out)
     d.ld = ld if ld is not None else out.shape[-1]
     d.rowscale, d.rows_per_scale = ptr(rowscale), rows_per_scale
     if win:
@@ -117,6 +122,8 @@ _SIGS = {
     "kair_colsum": [ctypes.POINTER(Operand), c_long, c_int, ctypes.POINTER(WMap), c_vp, c_vp, c_int, c_vp],
     "kair_layernorm_fwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_float, c_int,
                            c_int, c_int, c_int, c_int, c_vp],
+    "kair_layernorm_fwd_x3": [c_vp, c_long, c_vp, c_vp, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_float, c_int,
+                              c_int, c_int, c_int, c_int, c_int, c_vp],
     "kair_layernorm_bwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_vp, c_vp, c_int,
                            c_vp, c_long, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(CopyDesc), c_vp],
     "kair_row_copy": [c_vp, c_long, c_long, c_int, ctypes.POINTER(CopyDesc), c_vp],
@@ -504,6 +511,12 @@ def colsum(G, M, Np, m, bias_grad, ws, accumulate=False):
 def layernorm_fwd(x, ldx, y, ldy, gamma, beta, mean, rstd, M, C, eps=1e-5, win=(0, 0, 0, 0), one_col=-1):
     check(lib().kair_layernorm_fwd(ptr(x), ldx, ptr(y), dtype_code(y), ldy, ptr(gamma), ptr(beta), ptr(mean), ptr(rstd),
                                    M, C, eps, *win, one_col, stream_ptr()), "layernorm_fwd")
+
+
+def layernorm_fwd_x3(x, ldx, y, ldy, gamma, beta, mean, rstd, M, C, eps=1e-5, win=(0, 0, 0, 0), one_col=-1, x3_exp=0):
+    """LayerNorm forward into an fp16 pair y [2, M, ldy] (hi, lo planes) of y 2^x3_exp (the fp32x3 GEMM operand)."""
+    check(lib().kair_layernorm_fwd_x3(ptr(x), ldx, ptr(y[0]), ptr(y[1]), ldy, ptr(gamma), ptr(beta), ptr(mean), ptr(rstd),
+                                      M, C, eps, *win, one_col, int(x3_exp), stream_ptr()), "layernorm_fwd_x3")
 
 
 def layernorm_bwd(x, ldx, dy, ldy, gamma, mean, rstd, dx, ld_dx, dx_acc, dgamma, dbeta, dparam_acc, ws, M, C,

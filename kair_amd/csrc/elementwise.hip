@@ -388,6 +388,27 @@ __global__ void row_copy_kernel(const float* __restrict__ src, long lds, T* __re
   }
 }
 
+// the x3 fp16-pair form: hi / lo planes of scale(t) * src[t] * 2^e
+__global__ void row_copy_pair_kernel(const float* __restrict__ src, long lds, f16* __restrict__ hi, f16* __restrict__ lo,
+                                     long ldd, const float* __restrict__ scale, int rps, WinMap wm, long M, int C4, float es) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C4) return;
+  const long t = i / C4;
+  const int c = (int)(i - t * C4) * 4;
+  const float4 v = *(const float4*)(src + t * lds + c);
+  const float sc = (scale ? scale[t / rps] : 1.f) * es;
+  const float w[4] = {sc * v.x, sc * v.y, sc * v.z, sc * v.w};
+  f16x4 h, l;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = (f16)w[j];
+    l[j] = (f16)(w[j] - (float)h[j]);
+  }
+  const long o = token_to_win(t, wm) * ldd + c;
+  *(f16x4*)(hi + o) = h;
+  *(f16x4*)(lo + o) = l;
+}
+
 template <typename T>
 __global__ void colsum_partial(const T* __restrict__ g, long ld, long M, int Np, float* __restrict__ ws, long rows_per) {
   const int c = blockIdx.y * blockDim.x + threadIdx.x;
@@ -889,7 +910,12 @@ extern "C" int kair_row_copy(const float* src, long lds, long M, int C, const ka
   const int rps = copy->rows_per_scale > 0 ? copy->rows_per_scale : 1;
   const long n = M * (C / 4);
   hipStream_t s = (hipStream_t)stream;
-  if (copy->dtype == KAIR_BF16)
+  if (copy->dtype == KAIR_F16) {
+    KAIR_CHECK_ARG(copy->out_lo && ((uintptr_t)copy->out % 8) == 0 && ((uintptr_t)copy->out_lo % 8) == 0,
+                   "row_copy: an fp16 pair copy needs its 8-byte aligned lo plane (out_lo)");
+    hipLaunchKernelGGL(row_copy_pair_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (f16*)copy->out,
+                       (f16*)copy->out_lo, copy->ld, copy->rowscale, rps, wm, M, C / 4, ldexpf(1.f, copy->x3_exp));
+  } else if (copy->dtype == KAIR_BF16)
     hipLaunchKernelGGL(row_copy_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (bf16*)copy->out, copy->ld,
                        copy->rowscale, rps, wm, M, C / 4);
   else

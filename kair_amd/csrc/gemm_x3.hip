@@ -651,7 +651,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       }
       nvm += 2;
     }
-    const int nst = EM == XE_ROWS_F32 ? (E.pre ? 4 : 2) : (E.out_lo ? 2 : 1);
+    const int nst = EM == XE_ROWS_F32 ? (E.pre ? 4 : 2) : (E.out_lo ? 2 : 1) + (EM == XE_ROWS_PAIR && E.pre ? 2 : 0);
 #pragma unroll
     for (int i = 0; i < 2; ++i) nvm += __ballot(okm[i]) != 0 ? NP * nst : 0;
 #pragma unroll
@@ -825,9 +825,19 @@ constexpr int XT_DMA = 6;   // DMA wave-instructions per wave per chunk (3 A + 3
 static_assert(XT_DMA * (XT_NS - 2) == 6, "the steady-state wait immediate in gemm_tn_x3_ring");
 enum { BT_ROWS = 0, BT_TAP = 1 };
 
-template <int BT>
+// PR (BT_ROWS only): A and B are fp16 pairs (hi plane ptr, lo plane lo_ptr, values x 2^e): a chunk row holds the
+// 192 hi columns in logical units 0..23 and the 192 lo columns in units 24..47 (8 halves per unit), unit u at slot
+// u ^ xt_swz_pair(r); fragments are two ds_read_b64_tr_b16 per plane (the 4 x 16 transposed read: a lane's 8
+// halves are column lane & 15 over rows 8 (lane >> 4) .. + 7), so no split at the read.  The swizzle spreads the
+// four rows of one transposed read over four 8-bank groups and the two 16-lane halves of a 32-lane group over
+// the two bank halves: conflict-free.
+KAIR_DEV int xt_swz_pair(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
+
+template <int BT, bool PR>
 __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
                                                          int rps, float acc_scale) {
+  static_assert(!PR || BT == BT_ROWS, "fp16-pair operands: row operands only");
+  constexpr int ES = PR ? 2 : 4;   // operand element bytes
   __shared__ __attribute__((aligned(16))) char smem[XT_NS * XT_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wk = wave & 3;
@@ -838,28 +848,42 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
   const int mbeg = split * rps;
   const int mend = mbeg + rps < M ? mbeg + rps : M;
   const int nch = mbeg < mend ? (mend - mbeg + XT_RB - 1) / XT_RB : 0;
-  const float* zero = (const float*)g_kair_zero_line;
+  const char* zero = (const char*)g_kair_zero_line;
 
   // DMA geometry of this lane (the same for every chunk): wave-instruction g covers slots [64 g, 64 g + 64)
   // tap form: the lane's 4 columns k .. k + 3 of the K = 9 C contraction are channels c .. c + 3 of tap k / C (C % 4
   // == 0), so each lane reads ONE shifted image (its own dy, dx) for the whole launch
+  // pair form: the lane's 8 columns of one plane (pl = 0 hi, 1 lo)
   int dr[3], dcA[3], dcB[3], dy[3], dx[3];
+  const char* baseA[3];
+  const char* baseB[3];
 #pragma unroll
   for (int ii = 0; ii < 3; ++ii) {
     const int s = (wave * 3 + ii) * 64 + lane;
     const int r = s / 48, q = s - r * 48;
-    const int u = q ^ (((r >> 3) & 3) << 2);
     dr[ii] = r;
-    dcA[ii] = n0 + u * 4 < N ? n0 + u * 4 : -1;
-    const int k = k0 + u * 4;
     dy[ii] = dx[ii] = 0;
-    if constexpr (BT == BT_TAP) {
-      const int tap = k < K ? k / B.imC : 0;
-      dcB[ii] = k < K ? k - tap * B.imC : -1;
-      dy[ii] = tap / 3 - 1;
-      dx[ii] = tap - (tap / 3) * 3 - 1;
+    if constexpr (PR) {
+      const int u = q ^ xt_swz_pair(r);
+      const int pl = u >= 24 ? 1 : 0, col = (u - 24 * pl) * 8;
+      dcA[ii] = n0 + col < N ? n0 + col : -1;
+      dcB[ii] = k0 + col < K ? k0 + col : -1;
+      baseA[ii] = (const char*)(pl ? A.lo_ptr : A.ptr);
+      baseB[ii] = (const char*)(pl ? B.lo_ptr : B.ptr);
     } else {
-      dcB[ii] = k < K ? k : -1;
+      const int u = q ^ (((r >> 3) & 3) << 2);
+      dcA[ii] = n0 + u * 4 < N ? n0 + u * 4 : -1;
+      const int k = k0 + u * 4;
+      baseA[ii] = (const char*)A.ptr;
+      baseB[ii] = (const char*)B.ptr;
+      if constexpr (BT == BT_TAP) {
+        const int tap = k < K ? k / B.imC : 0;
+        dcB[ii] = k < K ? k - tap * B.imC : -1;
+        dy[ii] = tap / 3 - 1;
+        dx[ii] = tap - (tap / 3) * 3 - 1;
+      } else {
+        dcB[ii] = k < K ? k : -1;
+      }
     }
   }
   int lc = 0, ls = 0;   // next chunk to issue, its stage
@@ -867,22 +891,22 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
   // source rows advance by XT_RB rows per chunk, so the addresses are kept as running pointers (and, for the
   // tap form, the row's pixel column / row for the halo test) instead of being rebuilt per chunk
   const bool lin = A.win.ws == 0 && (BT == BT_TAP || B.win.ws == 0);
-  const float* pa[3];
-  const float* pb[3];
+  const char* pa[3];
+  const char* pb[3];
   int px[3], py[3];
 #pragma unroll
   for (int ii = 0; ii < 3; ++ii) {
     const long m = mbeg + dr[ii];
-    pa[ii] = (const float*)A.ptr + m * A.ld + (dcA[ii] >= 0 ? dcA[ii] : 0);
+    pa[ii] = baseA[ii] + (m * A.ld + (dcA[ii] >= 0 ? dcA[ii] : 0)) * ES;
     if constexpr (BT == BT_ROWS) {
-      pb[ii] = (const float*)B.ptr + m * B.ld + (dcB[ii] >= 0 ? dcB[ii] : 0);
+      pb[ii] = baseB[ii] + (m * B.ld + (dcB[ii] >= 0 ? dcB[ii] : 0)) * ES;
       px[ii] = py[ii] = 0;
     } else {
       const int mm = m < M ? (int)m : 0;
       const int p = mm - fdiv(mm, B.d_hw) * B.d_hw.d;
       py[ii] = fdiv(p, B.d_imW);
       px[ii] = p - py[ii] * B.imW;
-      pb[ii] = (const float*)B.ptr + (m + (long)dy[ii] * B.imW + dx[ii]) * B.ld + (dcB[ii] >= 0 ? dcB[ii] : 0);
+      pb[ii] = baseB[ii] + ((m + (long)dy[ii] * B.imW + dx[ii]) * B.ld + (dcB[ii] >= 0 ? dcB[ii] : 0)) * ES;
     }
   }
   auto issue_next = [&]() {
@@ -907,20 +931,20 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
             if (++py[ii] == B.imH) py[ii] = 0;
           }
         }
-        pa[ii] += (long)XT_RB * A.ld;
-        pb[ii] += (long)XT_RB * B.ld;
+        pa[ii] += (long)XT_RB * A.ld * ES;
+        pb[ii] += (long)XT_RB * B.ld * ES;
       } else {
         const int mm = ok ? m : 0;
-        if (ok && dcA[ii] >= 0) sa = (const float*)A.ptr + (long)win_to_token32(mm, A.win) * A.ld + dcA[ii];
+        if (ok && dcA[ii] >= 0) sa = baseA[ii] + ((long)win_to_token32(mm, A.win) * A.ld + dcA[ii]) * ES;
         if constexpr (BT == BT_ROWS) {
-          if (ok && dcB[ii] >= 0) sb = (const float*)B.ptr + (long)win_to_token32(mm, B.win) * B.ld + dcB[ii];
+          if (ok && dcB[ii] >= 0) sb = baseB[ii] + ((long)win_to_token32(mm, B.win) * B.ld + dcB[ii]) * ES;
         } else {
           const int hw = B.d_hw.d;
           const int b = fdiv(mm, B.d_hw), p = mm - b * hw;
           const int y = fdiv(p, B.d_imW), x = p - y * B.imW;
           const int yy = y + dy[ii], xx = x + dx[ii];
           if (ok && dcB[ii] >= 0 && yy >= 0 && yy < B.imH && xx >= 0 && xx < B.imW)
-            sb = (const float*)B.ptr + ((long)b * hw + (long)yy * B.imW + xx) * B.ld + dcB[ii];
+            sb = baseB[ii] + (((long)b * hw + (long)yy * B.imW + xx) * B.ld + dcB[ii]) * ES;
         }
       }
       glds16(sa, st + (wave * 3 + ii) * 1024);
@@ -943,7 +967,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
   const float sa = A.x3s, sb = B.x3s;
   // B's injected ones column (the bias gradient of a conv weight gradient: k = ones_col reads 1.0 for every row,
   // whatever the data / halo there), as its K-tile column (-1: none in this tile)
-  const int bones = B.ones_col >= 0 && !B.ones_in_data && B.ones_col >= k0 && B.ones_col < k0 + 192 ? B.ones_col - k0 : -1;
+  const int bones = !PR && B.ones_col >= 0 && !B.ones_in_data && B.ones_col >= k0 && B.ones_col < k0 + 192 ? B.ones_col - k0 : -1;
   // a lane's column c of a chunk part: byte (fq * 8 + j) * 768 + slot(c) * 16 + (c & 3) * 4 for rows j = 0..7
   auto frag = [&](const char* part, int c, float s, f16x8& hi, f16x8& lo) {
     const char* p = part + fq * 8 * 768 + ((((c >> 2) ^ (fq << 2))) << 4) + (c & 3) * 4;
@@ -954,6 +978,19 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
       lo[j] = (f16)(w - (float)hi[j]);
     }
   };
+  // pair form: the 16-column fragment at column cb (% 16 == 0) of plane pl: rows 8 fq + q4 and + 4 (q4 = (lane & 15) >> 2),
+  // columns cb + 4 (lane & 3) .. + 3 in each 4 x 16 transposed read
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+  auto frag_tr = [&](const char* part, int pl, int cb) -> f16x8 {
+    const int c = cb + p4, u = pl * 24 + (c >> 3), ob = (c & 7) * 2;
+    const int r0 = fq * 8 + q4, r1 = r0 + 4;
+    const char* a0 = part + r0 * 768 + ((u ^ xt_swz_pair(r0)) << 4) + ob;
+    const char* a1 = part + r1 * 768 + ((u ^ xt_swz_pair(r1)) << 4) + ob;
+    const short4v x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)a0);
+    const short4v y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)a1);
+    short __attribute__((ext_vector_type(8))) s8 = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    return __builtin_bit_cast(f16x8, s8);
+  };
   int cs = 0;
   for (int j = 0; j < nch; ++j) {
     const int ahead = (nch - 1 - j) < (XT_NS - 2) ? (nch - 1 - j) : (XT_NS - 2);
@@ -963,21 +1000,34 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
     if (lc < nch) issue_next();
     const char* st = smem + cs * XT_STAGE;
     f16x8 ah[6], al[6], bh[3], bl[3];
+    if constexpr (PR) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) frag(st, wn * 96 + i * 16 + fr, sa, ah[i], al[i]);
+      for (int i = 0; i < 6; ++i) {
+        ah[i] = frag_tr(st, 0, wn * 96 + i * 16);
+        al[i] = frag_tr(st, 1, wn * 96 + i * 16);
+      }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) frag(st + XT_PART, wk * 48 + i * 16 + fr, sb, bh[i], bl[i]);
-    if (bones >= 0) {   // (uniform: only the K tile holding the ones column) its lanes' fragment reads 1.0 in every row
-      const f16 oh = (f16)sb, ol = (f16)(sb - (float)oh);
+      for (int i = 0; i < 3; ++i) {
+        bh[i] = frag_tr(st + XT_PART, 0, wk * 48 + i * 16);
+        bl[i] = frag_tr(st + XT_PART, 1, wk * 48 + i * 16);
+      }
+    } else {
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
-        if (wk * 48 + i * 16 + fr == bones) {
+      for (int i = 0; i < 6; ++i) frag(st, wn * 96 + i * 16 + fr, sa, ah[i], al[i]);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            bh[i][j] = oh;
-            bl[i][j] = ol;
+      for (int i = 0; i < 3; ++i) frag(st + XT_PART, wk * 48 + i * 16 + fr, sb, bh[i], bl[i]);
+      if (bones >= 0) {   // (uniform: only the K tile holding the ones column) its lanes' fragment reads 1.0 in every row
+        const f16 oh = (f16)sb, ol = (f16)(sb - (float)oh);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          if (wk * 48 + i * 16 + fr == bones) {
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+              bh[i][jj] = oh;
+              bl[i][jj] = ol;
+            }
           }
-        }
+      }
     }
 #pragma unroll
     for (int ik = 0; ik < 3; ++ik)
@@ -1088,7 +1138,11 @@ bool nt_x3_ring_ok(const kair_operand* A, const kair_operand* B, const kair_epil
   } else {
     if (E->out_mode != KAIR_OUT_ROWS || E->ldo % 4 || (uintptr_t)E->out % 16) return false;
     if (E->resid2 || E->a_copy || (E->resid && E->gate)) return false;
-    if (pair && (E->act || E->out_pre || E->resid || E->gate || E->ldo % 8)) return false;
+    // fp16-pair rows: plain (bias), GELU with its fp32 GELU' (the fc1 forward: h as the fc2 operand pair), or the
+    // fp32 multiply gate (the fc2 input gradient: dU as the fc1 dgrad / wgrad operand pair)
+    if (pair && (E->resid || E->ldo % 8 || (E->act && (E->act != KAIR_ACT_GELU || !E->pre_kind || !E->out_pre)) ||
+                 (E->out_pre && !E->act) || (E->gate && E->gate_kind != XG_MUL)))
+      return false;
     if (E->out_pre && (E->pre_dtype != KAIR_F32 || E->ldp % 4 || (uintptr_t)E->out_pre % 16)) return false;
     if (E->resid && (E->ldr % 4 || (uintptr_t)E->resid % 16)) return false;
     if (E->gate && (E->gate_dtype != KAIR_F32 || E->ldg % 4 || (uintptr_t)E->gate % 16)) return false;
@@ -1118,6 +1172,8 @@ int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int
   hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN>), g, bl, 0, s, a, b, e, K, tilesN, tilesM)
   if constexpr (BN == 192) {   // the Swin linears and the 192-channel convs: every epilogue form
     if (e.omode == KAIR_OUT_QKVBLK) XR_LAUNCH(XE_QKV, EX_NONE, XA_NONE, 0);
+    else if (e.odt == KAIR_F16 && e.gate) XR_LAUNCH(XE_ROWS_PAIR, EX_GATE_F32, XA_NONE, XG_MUL);
+    else if (e.odt == KAIR_F16 && e.act == KAIR_ACT_GELU) XR_LAUNCH(XE_ROWS_PAIR, EX_NONE, XA_GELU, 0);
     else if (e.odt == KAIR_F16) XR_LAUNCH(XE_ROWS_PAIR, EX_NONE, XA_NONE, 0);
     else if (e.resid) XR_LAUNCH(XE_ROWS_F32, EX_RESID, XA_NONE, 0);
     else if (e.gate && e.gkind == XG_MUL) XR_LAUNCH(XE_ROWS_F32, EX_GATE_F32, XA_NONE, XG_MUL);
@@ -1151,7 +1207,14 @@ int nt_x3_ring_dispatch(const Op& a, const Op& b, const Epi& e, long M, int N, i
 // map (K = 9 C, no flip / upsample); B's bias ones column as data (ones_in_data) or injected, A's only as data
 bool tn_x3_ring_ok(const kair_operand* A, const kair_operand* B, int N, int K) {
   static const int off = [] { const char* e = getenv("KAIR_X3_RING"); return e && e[0] == '0'; }();
-  if (off || A->dtype != KAIR_F32 || B->dtype != KAIR_F32 || A->mode != KAIR_LD_ROWS || N % 4 || K % 4) return false;
+  if (off) return false;
+  if (A->dtype == KAIR_F16 && B->dtype == KAIR_F16) {   // fp16 pairs: row operands, 16-byte aligned 8-column units
+    return A->mode == KAIR_LD_ROWS && B->mode == KAIR_LD_ROWS && N % 8 == 0 && K % 8 == 0 && A->ld % 8 == 0 &&
+           B->ld % 8 == 0 && (uintptr_t)A->ptr % 16 == 0 && (uintptr_t)A->lo_ptr % 16 == 0 && (uintptr_t)B->ptr % 16 == 0 &&
+           (uintptr_t)B->lo_ptr % 16 == 0 && !A->rowscale && !B->rowscale && (A->ones_col < 0 || A->ones_in_data) &&
+           (B->ones_col < 0 || B->ones_in_data);
+  }
+  if (A->dtype != KAIR_F32 || B->dtype != KAIR_F32 || A->mode != KAIR_LD_ROWS || N % 4 || K % 4) return false;
   if (A->ld % 4 || (uintptr_t)A->ptr % 16 || (uintptr_t)B->ptr % 16 || A->rowscale || B->rowscale) return false;
   if (A->ones_col >= 0 && !A->ones_in_data) return false;
   if (B->mode == KAIR_LD_ROWS) return B->ld % 4 == 0;
@@ -1238,10 +1301,12 @@ int kair_gemm_tn_x3(const kair_operand* A, const kair_operand* B, float* ws, int
   if (tn_x3_ring_ok(A, B, N, K)) {
     const int tilesN = (N + 191) / 192, tilesK = (K + 191) / 192, nt = tilesN * tilesK;
     const dim3 g(nt * splits), bl(512);
-    if (B->mode == KAIR_LD_IM2COL3)
-      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_TAP>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
+    if (A->dtype == KAIR_F16)
+      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS, true>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
+    else if (B->mode == KAIR_LD_IM2COL3)
+      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_TAP, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
     else
-      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
+      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
     KAIR_CHECK_LAUNCH();
     return 0;
   }

@@ -9,6 +9,8 @@
 
 #include <string.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -31,6 +33,18 @@ template <> KAIR_DEV void store4<bf16>(bf16* p, float a, float b, float c, float
   bf16x4 q = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
   *(bf16x4*)p = q;
 }
+// x3 fp16 pair of 4 values: hi = f16(v s), lo = f16(v s - hi) (the fp32x3 engine's GEMM operand format)
+KAIR_DEV void store4_pair(f16* hi, f16* lo, long off, float a, float b, float c, float d, float s) {
+  const float w[4] = {a * s, b * s, c * s, d * s};
+  f16x4 h, l;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = (f16)w[j];
+    l[j] = (f16)(w[j] - (float)h[j]);
+  }
+  *(f16x4*)(hi + off) = h;
+  *(f16x4*)(lo + off) = l;
+}
 template <typename T> KAIR_DEV float4 load4(const T* p);
 template <> KAIR_DEV float4 load4<float>(const float* p) { return *(const float4*)p; }
 template <> KAIR_DEV float4 load4<bf16>(const bf16* p) {
@@ -38,11 +52,13 @@ template <> KAIR_DEV float4 load4<bf16>(const bf16* p) {
   return make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
 }
 
+// T = f16: y / y_lo are the hi / lo planes of the x3 pair of y 2^e (ys = 2^e)
 template <typename T>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, long ldx, T* __restrict__ y, long ldy,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
-                                                      int C, float eps, WinMap wm, int one_col) {
+                                                      int C, float eps, WinMap wm, int one_col, f16* __restrict__ y_lo,
+                                                      float ys) {
   const int sub = threadIdx.x & (LPR - 1);
   const long grp = (long)blockIdx.x * ROWS_PER_BLOCK_ITER + (threadIdx.x >> 4);
   const long ng = (long)gridDim.x * ROWS_PER_BLOCK_ITER;
@@ -91,7 +107,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
         const float xv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = (xv[j] - mu) * rs * ga[i][j] + be[i][j];   // pad columns: 0 (or the ones column)
-        store4<T>(y + r * ldy + c, o[0], o[1], o[2], o[3]);
+        if constexpr (sizeof(T) == 2 && !std::is_same_v<T, bf16>) store4_pair(y, y_lo, r * ldy + c, o[0], o[1], o[2], o[3], ys);
+        else store4<T>(y + r * ldy + c, o[0], o[1], o[2], o[3]);
       }
     }
     if (sub == 0) {
@@ -107,7 +124,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
                                                       float* dx, long ld_dx, int dx_acc, float* __restrict__ part,
                                                       long M, int C, WinMap wm, void* cp, int cp_dt, long ldc,
-                                                      const float* __restrict__ cp_scale, int cp_rps, WinMap cwm) {
+                                                      const float* __restrict__ cp_scale, int cp_rps, WinMap cwm,
+                                                      f16* __restrict__ cp_lo, float cp_s) {
   const int sub = threadIdx.x & (LPR - 1);
   const long grp = (long)blockIdx.x * ROWS_PER_BLOCK_ITER + (threadIdx.x >> 4);
   const long ng = (long)gridDim.x * ROWS_PER_BLOCK_ITER;
@@ -167,6 +185,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
         *(float4*)o = cu;
         if (cp) {   // GEMM-operand copy of the finished gradient row: scaled, cast, optionally window-ordered
           if (cp_dt == KAIR_BF16) store4<bf16>((bf16*)cp + cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w);
+          else if (cp_dt == KAIR_F16) store4_pair((f16*)cp, cp_lo, cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w, cp_s);
           else store4<float>((float*)cp + cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w);
         }
       }
@@ -325,10 +344,31 @@ extern "C" int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype
   hipStream_t s = (hipStream_t)stream;
   if (y_dtype == KAIR_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (bf16*)y, ldy, gamma, beta,
-                       mean, rstd, M, C, eps, wm, one_col);
+                       mean, rstd, M, C, eps, wm, one_col, (f16*)nullptr, 1.f);
   else
     hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (float*)y, ldy, gamma, beta,
-                       mean, rstd, M, C, eps, wm, one_col);
+                       mean, rstd, M, C, eps, wm, one_col, (f16*)nullptr, 1.f);
+  KAIR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kair_layernorm_fwd_x3(const float* x, long ldx, void* y_hi, void* y_lo, long ldy, const float* gamma,
+                                     const float* beta, float* mean, float* rstd, long M, int C, float eps, int win_H,
+                                     int win_W, int win_ws, int win_shift, int one_col, int x3_exp, void* stream) {
+  KAIR_CHECK_ARG(x && y_hi && y_lo && gamma && beta && mean && rstd, "layernorm_fwd_x3: null pointer");
+  KAIR_CHECK_ARG(C > 0 && C <= 256 && ldx >= C && ldy >= C && ldy <= 256 && M > 0 && M < KAIR_MAX_MAPPED_ROWS,
+                 "layernorm_fwd_x3: bad sizes");
+  KAIR_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)y_hi % 8) == 0 &&
+                     ((uintptr_t)y_lo % 8) == 0,
+                 "layernorm_fwd_x3: strides / alignment");
+  KAIR_CHECK_ARG(win_ws == 0 || (win_H % win_ws == 0 && win_W % win_ws == 0), "layernorm_fwd_x3: window geometry");
+  KAIR_CHECK_ARG(one_col < 0 || (one_col >= C && one_col < ldy), "layernorm_fwd_x3: ones column must be a pad column");
+  KAIR_CHECK_ARG(x3_exp > -100 && x3_exp < 100, "layernorm_fwd_x3: exponent");
+  const WinMap wm = make_winmap(win_H, win_W, win_ws, win_shift);
+  long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;
+  if (nb > 1024) nb = 1024;
+  hipLaunchKernelGGL(ln_fwd_kernel<f16>, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, x, ldx, (f16*)y_hi, ldy,
+                     gamma, beta, mean, rstd, M, C, eps, wm, one_col, (f16*)y_lo, ldexpf(1.f, x3_exp));
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -344,6 +384,8 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
   KAIR_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && ld_dx % 4 == 0, "layernorm_bwd: strides must be multiples of 4");
   const WinMap wm = make_winmap(win_H, win_W, win_ws, win_shift);
   void* cp = nullptr;
+  f16* cp_lo = nullptr;
+  float cp_s = 1.f;
   int cp_dt = KAIR_F32, cp_rps = 1;
   long ldc = 0;
   const float* cp_scale = nullptr;
@@ -355,15 +397,23 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
     cp = copy->out; cp_dt = copy->dtype; ldc = copy->ld; cp_scale = copy->rowscale;
     cp_rps = copy->rows_per_scale > 0 ? copy->rows_per_scale : 1;
     cwm = make_winmap(copy->win_H, copy->win_W, copy->win_ws, copy->win_shift);
+    if (cp_dt == KAIR_F16) {
+      KAIR_CHECK_ARG(copy->out_lo && ((uintptr_t)copy->out % 8) == 0 && ((uintptr_t)copy->out_lo % 8) == 0,
+                     "layernorm_bwd: an fp16 pair copy needs its 8-byte aligned lo plane (out_lo)");
+      cp_lo = (f16*)copy->out_lo;
+      cp_s = ldexpf(1.f, copy->x3_exp);
+    }
   }
   hipStream_t s = (hipStream_t)stream;
   const long nb = ln_bwd_blocks(M);
   if (dy_dtype == KAIR_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const bf16*)dy, ldy, gamma,
-                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm);
+                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm,
+                       cp_lo, cp_s);
   else
     hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const float*)dy, ldy, gamma,
-                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm);
+                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm,
+                       cp_lo, cp_s);
   KAIR_CHECK_LAUNCH();
   if (!dgamma) return 0;   // deferred: the [nb][2C] partials stay in ws for kair_ln_param_reduce_grouped
   hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 7) / 8), dim3(256), 0, s, ws, (int)nb, C, dgamma, dbeta,

@@ -509,12 +509,15 @@ class SwinIREngine:
             if infer and bi >= 2:
                 blocks.append(blocks[bi % 2])
                 continue
+            # fp32x3: every Swin-block GEMM operand -- ln1, q/k/v, O, ln2, h -- is stored ONCE by its producer as the
+            # fp16 pair [2, ...] (hi plane, lo plane) of v 2^X3_AEXP, so the consuming ring GEMMs (forward NT, weight-
+            # gradient TN) and the attention kernels read pairs instead of splitting fp32 rows at every fragment load
+            pr = (lambda *sh: e(2, *sh, dt=hf)) if self.x3 else (lambda *sh: e(*sh, dt=T))
             blocks.append({
-                "mid": e(M, Cp), "out": e(M, Cp), "ln1": e(M, Cp, dt=T), "m1": e(M), "r1": e(M),
-                # fp32x3: q/k/v as hi/lo fp16 planes [2, ...] (the split attention kernels' operands), O fp32
+                "mid": e(M, Cp), "out": e(M, Cp), "ln1": pr(M, Cp), "m1": e(M), "r1": e(M),
                 "qkv": e(2, 3 * M * nh * 32, dt=hf) if self.x3 else e(3 * M * nh * 32, dt=T),
-                "O": e(M, nh * 32, dt=T), "lse": e(nWin * nh * WS_TOK),
-                "ln2": e(M, Cp, dt=T), "m2": e(M), "r2": e(M), "u": e(M, Hdp, dt=T), "h": e(M, Hdp, dt=T)})
+                "O": pr(M, nh * 32), "lse": e(nWin * nh * WS_TOK),
+                "ln2": pr(M, Cp), "m2": e(M), "r2": e(M), "u": e(M, Hdp, dt=T), "h": pr(M, Hdp)})
         P["blocks"] = blocks
         P["rstb_out"] = [e(M, Cp) for _ in range(min(2, len(self.rstb)) if infer else len(self.rstb))]
         if infer:
@@ -563,10 +566,13 @@ class SwinIREngine:
         # (zero-filled: kair_layernorm_bwd's copies write the C real columns only, the GEMMs read Cp)
         depth = max(len(blks) for blks, _ in self.rstb)
         z = lambda *s: torch.zeros(*s, device=dev, dtype=T)
+        # fp32x3: the block's gradient operands as fp16 pairs [2, ...] of v 2^e_g (zero-filled pads as above)
+        zp = (lambda *sh: torch.zeros(2, *sh, device=dev, dtype=hf)) if self.x3 else z
+        ep = (lambda *sh: e(2, *sh, dt=hf)) if self.x3 else (lambda *sh: e(*sh, dt=T))
         # Two sets (RSTB parity): the side stream still reads one RSTB's while the next RSTB writes the other.
-        P["gw"] = [[{"Dm": z(M, Cp), "Da": z(M, Cp), "dU": e(M, Hdp, dt=T),
-                     # fp32x3: dq/dk/dv as fp32 token rows [M][3 nh 32] (the ring GEMMs' operand)
-                     "dqkv": e(M, 3 * nh * 32, dt=T) if self.x3 else e(3 * M * nh * 32, dt=T),
+        P["gw"] = [[{"Dm": zp(M, Cp), "Da": zp(M, Cp), "dU": ep(M, Hdp),
+                     # fp32x3: dq/dk/dv as token rows [M][3 nh 32] (pairs: the ring GEMMs' operand)
+                     "dqkv": ep(M, 3 * nh * 32) if self.x3 else e(3 * M * nh * 32, dt=T),
                      # LN1 / LN2 parameter partials and the attention bias-table partials of the block, reduced
                      # by one grouped launch each at the end of the RSTB
                      "ln1p": e(2 * 2048 * Cp), "ln2p": e(2 * 2048 * Cp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
@@ -765,6 +771,13 @@ class SwinIREngine:
         self._bias_colsum(P, H.rows(dz1), M, q, r.c1.mapb, g(r.c1.b))
         return None
 
+    @staticmethod
+    def _op(t, **kw):
+        """A row operand of tensor t: an fp16 pair [2, M, N] (fp32x3: hi plane + its lo plane) or plain rows."""
+        if t.dtype == torch.float16 and t.dim() == 3 and t.shape[0] == 2:
+            return H.with_lo(H.rows(t[0], **kw), t[1])
+        return H.rows(t, **kw)
+
     def _ain(self, op, lo=None):
         """A forward conv's input operand: a hi/lo pair under split_act (fp32 source: lo formed in the
         kernel; bf16 source: its lo plane `lo`), else as is."""
@@ -904,16 +917,20 @@ class SwinIREngine:
                             S["lse"], blk.proj.Wg, blk.proj.bp, s_attn, HW, S["mid"], Cp, P["nWin"], nh, Hh, Ww,
                             blk.shift, w_split=blk.qkv.split)
         else:
-            H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps, win,
-                            one_col=self.C)
+            if self.x3:   # ln1 as the fp16 pair of its qkv / wgrad consumers
+                H.layernorm_fwd_x3(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps,
+                                   win, one_col=self.C, x3_exp=self.X3_AEXP)
+            else:
+                H.layernorm_fwd(x, Cp, S["ln1"], Cp, blk.n1.weight, blk.n1.bias, S["m1"], S["r1"], M, self.C, blk.n1.eps,
+                                win, one_col=self.C)
             l = blk.qkv
-            if self.x3:   # q/k/v as hi/lo planes into the split attention kernels, O out as fp32
-                self._nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"][0], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
-                                                                     qkv=(nh, 32, WS_TOK), out_lo=S["qkv"][1]),
+            if self.x3:   # q/k/v as hi/lo planes into the split attention kernels, O out as a pair too
+                self._nt(self._op(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"][0], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
+                                                                       qkv=(nh, 32, WS_TOK), out_lo=S["qkv"][1]),
                          M, l.Np, Cp, cd)
                 H.window_attn_fwd_x3(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale,
                                      Hh, Ww, blk.shift, ones_col=self.C // nh, e_in=self.X3_AEXP, e_out=self.X3_AEXP)
-                A_o = H.rows(S["O"])
+                A_o = self._op(S["O"])
             else:
                 self._nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
                                                                      qkv=(nh, 32, WS_TOK)), M, l.Np, Cp, cd)
@@ -929,14 +946,20 @@ class SwinIREngine:
                            f1.Wg, f1.bp, S["u"], S["h"], self.Hdp, f1.N, f2.Wg, f2.bp, s_mlp, HW, S["out"], Cp, M, Cp,
                            self.Hdp, w_split=f1.split)
             return S["out"]
-        H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps,
-                        one_col=self.C)
+        if self.x3:
+            H.layernorm_fwd_x3(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C,
+                               blk.n2.eps, one_col=self.C, x3_exp=self.X3_AEXP)
+        else:
+            H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps,
+                            one_col=self.C)
         l = blk.fc1
-        self._nt(H.rows(S["ln2"]), H.rows(l.Wp), H.epilogue(S["h"], bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N,
-                                                               pre_grad=True), M, l.Np, Cp, cd)
+        hp = S["h"]
+        E1 = (H.epilogue(hp[0], out_lo=hp[1], bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N, pre_grad=True)
+              if self.x3 else H.epilogue(hp, bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N, pre_grad=True))
+        self._nt(self._op(S["ln2"]), H.rows(l.Wp), E1, M, l.Np, Cp, cd)
         l = blk.fc2
-        self._nt(H.rows(S["h"]), H.rows(l.Wp), H.epilogue(S["out"], bias=l.bp, resid=S["mid"], rowscale=s_mlp,
-                                                            rows_per_scale=HW), M, Cp, self.Hdp, cd)
+        self._nt(self._op(S["h"]), H.rows(l.Wp), H.epilogue(S["out"], bias=l.bp, resid=S["mid"], rowscale=s_mlp,
+                                                              rows_per_scale=HW), M, Cp, self.Hdp, cd)
         return S["out"]
 
     # ------------------------------------------------------------------------------------
@@ -1124,7 +1147,7 @@ class SwinIREngine:
             drop = P["drop"]
             H.row_copy(D, Cp, M, Cp, H.copy_desc(P["gw"][par][len(blks) - 1]["Dm"],
                                                  rowscale=drop[bi - 1, 1] if drop is not None else None,
-                                                 rows_per_scale=Hh * Ww))
+                                                 rows_per_scale=Hh * Ww, x3_exp=P["e_g"]))
             for j in range(len(blks) - 1, -1, -1):
                 bi -= 1
                 x_in = P["blocks"][bi - 1]["out"] if j > 0 else (P["rstb_out"][gi - 1] if gi > 0 else P["s0"])
@@ -1254,7 +1277,7 @@ class SwinIREngine:
         # MLP: out = mid + s_mlp * fc2(gelu(fc1(LN2(mid))))
         fc2, fc1 = blk.fc2, blk.fc1
         n = blk.n2
-        self._wg(P, H.rows(Dm), H.rows(S["h"], ones_col=fc2.K, ones_in_data=True), Cp, self.Hdp, fc2, grads, fc2.K)
+        self._wg(P, self._op(Dm), self._op(S["h"], ones_col=fc2.K, ones_in_data=True), Cp, self.Hdp, fc2, grads, fc2.K)
         if self.fused_mlp_bwd:
             # fc2 / fc1 input gradients + LN2 backward in one launch
             H.swin_mlp_bwd(Dm, S["u"], fc2.Wgt, fc1.Wgt, dU, S["mid"], n.weight, S["m2"], S["r2"], self.C, D, Da,
@@ -1268,12 +1291,15 @@ class SwinIREngine:
             self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False, P["rg_nb"][self.Hdp]))
         else:
             # S["u"] holds GELU'(fc1 pre-activation), stored by the forward (pre_grad): a plain multiply here
-            self._nt(H.rows(Dm), H.rows(fc2.Wt), H.epilogue(dU, gate=S["u"], gate_kind=4), M, self.Hdp, Cp, cd)
-            self._nt(H.rows(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
+            Eu = (H.epilogue(dU[0], out_lo=dU[1], gate=S["u"], gate_kind=4) if self.x3 else
+                  H.epilogue(dU, gate=S["u"], gate_kind=4))
+            self._nt(self._op(Dm), H.rows(fc2.Wt), Eu, M, self.Hdp, Cp, cd)
+            self._nt(self._op(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
             H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, None, None, False,
-                            W["ln2p"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win))
+                            W["ln2p"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win,
+                                                                   x3_exp=P["e_g"]))
             self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False))
-        self._wg(P, H.rows(dU), H.rows(S["ln2"], ones_col=self.C, ones_in_data=True), self.Hdp, Cp, fc1, grads, self.C)
+        self._wg(P, self._op(dU), self._op(S["ln2"], ones_col=self.C, ones_in_data=True), self.Hdp, Cp, fc1, grads, self.C)
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         proj, qkv = blk.proj, blk.qkv
         if self.x3:
@@ -1319,19 +1345,19 @@ class SwinIREngine:
         W = P["gw"][par][j]
         Da, dqkv = W["Da"], W["dqkv"]
         proj, qkv = blk.proj, blk.qkv
-        self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
-        self._nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"][0], out_lo=P["dO"][1]), M, nh * 32, Cp, cd)
+        self._wg(P, self._op(Da), self._op(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
+        self._nt(self._op(Da), H.rows(proj.Wt), H.epilogue(P["dO"][0], out_lo=P["dO"][1]), M, nh * 32, Cp, cd)
         H.window_attn_bwd_x3(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
                              W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, e_act=self.X3_AEXP,
                              e_grad=P["e_g"])
         self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, H.X3, g(blk.table), False))
-        self._wg(P, H.rows(dqkv), H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads, self.C)
+        self._wg(P, self._op(dqkv), self._op(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads, self.C)
         n = blk.n1
         cp = None
         if j > 0:   # the previous block's MLP operand: s_mlp(prev) * dL/d x_in
             cp = H.copy_desc(P["gw"][par][j - 1]["Dm"], rowscale=drop[bi - 1, 1] if drop is not None else None,
-                             rows_per_scale=HW)
-        self._nt(H.rows(dqkv), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
+                             rows_per_scale=HW, x3_exp=P["e_g"])
+        self._nt(self._op(dqkv), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
         H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
                         W["ln1p"], M, self.C, win, copy=cp)
         self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False))

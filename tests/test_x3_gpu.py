@@ -115,6 +115,74 @@ def test_gemm_tn_x3(a_bf, b_bf, b_im2col, M, N, K):
     assert rel(ws.sum(0), ref) < 2e-6
 
 
+@pytest.mark.parametrize("N,K", [(576, 192), (192, 384), (384, 192), (192, 192)])
+def test_gemm_tn_x3_ring_pairs(N, K):
+    """The TN ring on fp16-pair operands (the fp32x3 block weight gradients: A = the gradient pair at its exponent,
+    B = the activation pair with the bias ones column in its data): transposed LDS reads, no split -- against float64
+    over ragged splits (M not a multiple of the 32-row chunk)."""
+    g = torch.Generator().manual_seed(15)
+    M = 3001
+    dy = torch.randn(M, N, generator=g) * 1e-6
+    x = torch.randn(M, K, generator=g)
+    x[:, K - 3] = 1.0
+    ref = dy.double().T @ x.double()
+    S = H.wgrad_splits(M, N, K)
+    ws = torch.empty(S, N, K, device=dev)
+    ap, bp = hilo(dy.to(dev), 24), hilo(x.to(dev), 4)
+    A = H.with_lo(H.rows(ap[0]), ap[1])
+    A.x3_exp = 24
+    Bop = H.with_lo(H.rows(bp[0], ones_col=K - 3, ones_in_data=True), bp[1])
+    Bop.x3_exp = 4
+    H.gemm_tn(A, Bop, ws, S, M, N, K, H.X3)
+    torch.cuda.synchronize()
+    assert rel(ws.sum(0), ref) < 2e-6
+
+
+def test_layernorm_x3_pair_forms():
+    """kair_layernorm_fwd_x3 (window-ordered fp16-pair output with the ones column at 2^e), and the pair forms of
+    the GEMM-operand copies (kair_copy_desc dtype F16: kair_layernorm_bwd's copy, kair_row_copy) -- (hi + lo) 2^-e
+    against float64 to ~2^-21."""
+    g = torch.Generator().manual_seed(19)
+    Bn, Hh, Ww, C, Cp = 2, 16, 16, 180, 192
+    M = Bn * Hh * Ww
+    x = torch.zeros(M, Cp)
+    x[:, :C] = torch.randn(M, C, generator=g) * 3 + 0.5
+    gam, bet = 1 + 0.1 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    y = torch.empty(2, M, Cp, device=dev, dtype=torch.float16)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    win = (Hh, Ww, 8, 4)
+    H.layernorm_fwd_x3(x.to(dev), Cp, y, Cp, gam.to(dev), bet.to(dev), mean, rstd, M, C, 1e-5, win, one_col=C, x3_exp=4)
+    xd = x[:, :C].double()
+    ref = (xd - xd.mean(1, keepdim=True)) / torch.sqrt(xd.var(1, unbiased=False, keepdim=True) + 1e-5) * gam.double() + bet.double()
+    # window order: output row r holds token win_to_token(r): compare through the fp32 kernel's own map
+    y32 = torch.empty(M, Cp, device=dev)
+    H.layernorm_fwd(x.to(dev), Cp, y32, Cp, gam.to(dev), bet.to(dev), mean, rstd, M, C, 1e-5, win, one_col=C)
+    torch.cuda.synchronize()
+    rec = (y[0].double() + y[1].double()).cpu() / 16
+    assert rel(rec, y32) < 1e-6 and (rec[:, C] == 1).all() and (rec[:, C + 1:] == 0).all()
+    tok = torch.sort(y32[:, 0].double().cpu())[0]
+    assert rel(tok, torch.sort(ref[:, 0])[0]) < 1e-6
+    # pair copies: row_copy (row scale per image) and the LayerNorm backward's operand copy, gradient-sized values
+    src = torch.randn(M, Cp, generator=g) * 1e-5
+    sc = torch.tensor([0.5, 2.0])
+    cp = torch.zeros(2, M, Cp, device=dev, dtype=torch.float16)
+    H.row_copy(src.to(dev), Cp, M, Cp, H.copy_desc(cp, rowscale=sc.to(dev), rows_per_scale=Hh * Ww, x3_exp=20))
+    torch.cuda.synchronize()
+    want = src.double() * sc.double().repeat_interleave(Hh * Ww)[:, None]
+    assert rel((cp[0].double() + cp[1].double()).cpu() * 2.0 ** -20, want) < 1e-6
+    dy = torch.randn(M, Cp, generator=g) * 1e-5
+    dx = torch.zeros(M, Cp, device=dev)
+    ws = torch.empty(2 * 2048 * Cp, device=dev)
+    cp2 = torch.zeros(2, M, Cp, device=dev, dtype=torch.float16)
+    cp32 = torch.zeros(M, Cp, device=dev)
+    for out, e in ((cp2, 20), (cp32, 0)):
+        dx.zero_()
+        H.layernorm_bwd(x.to(dev), Cp, dy.to(dev), Cp, gam.to(dev), mean, rstd, dx, Cp, False, None, None, False, ws, M, C,
+                        win, copy=H.copy_desc(out, rowscale=sc.to(dev), rows_per_scale=Hh * Ww, win=win, x3_exp=e))
+    torch.cuda.synchronize()
+    assert rel((cp2[0].double() + cp2[1].double()).cpu() * 2.0 ** -20, cp32) < 1e-6
+
+
 def test_gemm_nt_x3_rows_and_qkvblk():
     """kair_gemm_nt as the fp32x3 engine calls it (compute KAIR_COMPUTE_X3): fp32 A and an fp16 pair A, split-packed
     fp16 weights (kind 17), ROWS fp32 and head-blocked q/k/v fp16-pair outputs (with an output exponent)."""
@@ -213,6 +281,39 @@ def test_gemm_nt_x3_ring_epilogues():
     cols = cols.view(Bn, C, 9, Hh * Ww).permute(0, 3, 2, 1).reshape(M, 9, C).flip(1).reshape(M, K)
     torch.cuda.synchronize()
     assert rel(out, (cols @ w.double().T) * gt.double()) < 2e-6
+    # (d) fp16-pair rows out with GELU and its fp32 GELU' (the fc1 forward of the pair engine), ones column at 2^e
+    M, N, K = 1000, 384, 192
+    x, w, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.05, torch.randn(N, generator=g) * 0.1
+    Wo, keep = _wsplit(w)
+    xp = hilo(x.to(dev), 4)
+    A = H.with_lo(H.rows(xp[0]), xp[1])
+    A.x3_exp = 4
+    hp, pre = torch.empty(2, M, N, device=dev, dtype=torch.float16), torch.empty(M, N, device=dev)
+    E = H.epilogue(hp[0], out_lo=hp[1], bias=b.to(dev), act=H.ACT_GELU, pre=pre, pre_grad=True, ones_col=N - 20)
+    E.x3_out_exp = 4
+    H.gemm_nt(A, Wo, E, M, N, K, H.X3)
+    h = x.double() @ w.double().T + b.double()
+    cdf = 0.5 * (1 + torch.erf(h / 2 ** 0.5))
+    want = h * cdf
+    want[:, N - 20] = 1.0
+    torch.cuda.synchronize()
+    assert rel((hp[0].double() + hp[1].double()).cpu() / 16, want) < 2e-6
+    pw = cdf + h * torch.exp(-h * h / 2) / (2 * torch.pi) ** 0.5
+    keepc = [c for c in range(N) if c != N - 20]
+    assert rel(pre[:, keepc], pw[:, keepc]) < 2e-6
+    # (e) fp16-pair A (a gradient pair) -> fp16-pair rows out through the fp32 multiply gate (the fc2 input gradient)
+    M, N, K = 777, 384, 192
+    dy, w, gt = torch.randn(M, K, generator=g) * 1e-5, torch.randn(N, K, generator=g) * 0.05, torch.rand(M, N, generator=g)
+    Wo, keep = _wsplit(w)
+    dp = hilo(dy.to(dev), 20)
+    A = H.with_lo(H.rows(dp[0]), dp[1])
+    A.x3_exp = 20
+    up = torch.empty(2, M, N, device=dev, dtype=torch.float16)
+    E = H.epilogue(up[0], out_lo=up[1], gate=gt.to(dev), gate_kind=4)
+    E.x3_out_exp = 20
+    H.gemm_nt(A, Wo, E, M, N, K, H.X3)
+    torch.cuda.synchronize()
+    assert rel((up[0].double() + up[1].double()).cpu() * 2.0 ** -20, (dy.double() @ w.double().T) * gt.double()) < 2e-6
     # (d) the tail's tile widths: 64 columns with LeakyReLU (conv_before_upsample), 256 plain (the x4 upsampling convs)
     for N, leaky in ((64, True), (256, False)):
         M, K = 700, 576
