@@ -388,12 +388,16 @@ enum { XG_MUL = 4, XG_LEAKY = 2 };                                 // kair_epilo
 // part is issued NA - 1 intervals ahead (A ring of NA), its B part 2 ahead (B ring of 3, L2-resident weights); a
 // wave waits for its own pieces of chunk t with a counted vmcnt (the DMA, epilogue loads and stores it issued
 // after them) before the barrier that opens interval t.
-template <typename TA, int AM, int EM, int EX, int ACT, int GK, int BN>
+template <typename TA, int AM, int EM, int EX, int ACT, int GK, int BN, int BM = XR_BM>
 __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
   constexpr int NA = XR<BN>::NA, RN = XR<BN>::RN, NP = RN / 2, BI = XR<BN>::BI, BSTAGE = XR<BN>::BSTAGE, WC = BN / 2;
-  __shared__ __attribute__((aligned(16))) char smem[XR<BN>::LDS];
+  // BM = 128 rows per tile (a wave multiplies 2 row fragments) or 64 (1: twice the tiles for small M -- the B = 4 per-GPU
+  // shape of the 8-GPU run has 72 128-row tiles per N-tile for 256 CUs); RI row fragments / A DMA instructions per wave
+  constexpr int RI = BM / 64, ASTAGE = BM * 128;
+  static_assert(RI == 1 || RI == 2, "64- or 128-row tiles");
+  __shared__ __attribute__((aligned(16))) char smem[NA * XR_ASTAGE + XR_NB * BSTAGE + BN * 4];
   char* const sA = smem;
-  char* const sB = smem + NA * XR_ASTAGE;
+  char* const sB = smem + NA * ASTAGE;
   float* const sBias = (float*)(sB + XR_NB * BSTAGE);   // the N-tile's bias (zeros without one), read by the epilogue
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
@@ -446,15 +450,15 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
     bsrc[ii] = n0 + r < (int)B.M ? (const f16*)B.ptr + (long)(n0 + r) * B.ld + (u < 4 ? u * 8 : 64 + (u - 4) * 8) : nullptr;
   }
   // A loader: this lane's two rows of the tile being loaded
-  long aoff[2];
-  int ay[2], ax[2], au[2];
-  bool aok[2];
+  long aoff[RI];
+  int ay[RI], ax[RI], au[RI];
+  bool aok[RI];
   auto load_rows = [&](int i) __attribute__((always_inline)) {
     const int mt = mt0 + i * mstride;
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii) {
-      const int r = (wave * 2 + ii) * 8 + (lane >> 3);
-      const int m = mt * XR_BM + r;
+    for (int ii = 0; ii < RI; ++ii) {
+      const int r = (wave * RI + ii) * 8 + (lane >> 3);
+      const int m = mt * BM + r;
       au[ii] = q8 ^ (r & 7);
       aok[ii] = m < (int)A.M;
       const int mm = aok[ii] ? m : 0;
@@ -474,12 +478,14 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
   // im2col: the current tap and channel offset (k = tap * C + c0, advanced per chunk: K = 9 C, C % 32 == 0) and
   // the lane's two source pixel rows for that tap (nullptr: outside the image / past M), recomputed per tap
   int a_tap = 0, a_c0 = 0;
-  const float* arow[2] = {nullptr, nullptr};
+  const float* arow[RI];
+#pragma unroll
+  for (int ii = 0; ii < RI; ++ii) arow[ii] = nullptr;
   auto set_tap = [&]() __attribute__((always_inline)) {
     int dy = a_tap / 3 - 1, dx = a_tap - (a_tap / 3) * 3 - 1;
     if (A.flip) { dy = -dy; dx = -dx; }
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii) {
+    for (int ii = 0; ii < RI; ++ii) {
       const int y = ay[ii] + dy, x = ax[ii] + dx;
       arow[ii] = aok[ii] && y >= 0 && y < A.imH && x >= 0 && x < A.imW
                      ? (const float*)A.ptr + (aoff[ii] + (long)(y >> A.up_sh) * (A.imW >> A.up_sh) + (x >> A.up_sh)) * A.ld +
@@ -497,9 +503,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       }
     }
     const int k0 = ak * 32;
-    char* st = sA + as_ * XR_ASTAGE;
+    char* st = sA + as_ * ASTAGE;
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii) {
+    for (int ii = 0; ii < RI; ++ii) {
       const void* src = zero;
       if constexpr (sizeof(TA) == 2) {
         const f16* pl = (const f16*)(au[ii] < 4 ? A.ptr : A.lo_ptr);
@@ -509,7 +515,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       } else {
         if (arow[ii]) src = arow[ii] + a_c0;
       }
-      if (!KAIR_DBG(E.dbg & 36)) glds16(src, st + (wave * 2 + ii) * 1024);
+      if (!KAIR_DBG(E.dbg & 36)) glds16(src, st + (wave * RI + ii) * 1024);
     }
     if constexpr (AM == AM_IM2COL) {
       a_c0 += 32;
@@ -532,29 +538,29 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
   };
   // interval u issues A chunk u + NA - 1 and B chunk u + NB - 1 (when in range); the prologue runs the virtual
   // intervals -(NA - 1) .. -1.  nA / nB: the DMA instructions one interval issues.
-  auto nA = [&](int u) __attribute__((always_inline)) { return u + NA - 1 >= 0 && u + NA - 1 < total ? 2 : 0; };
+  auto nA = [&](int u) __attribute__((always_inline)) { return u + NA - 1 >= 0 && u + NA - 1 < total ? RI : 0; };
   auto nB = [&](int u) __attribute__((always_inline)) { return u + XR_NB - 1 >= 0 && u + XR_NB - 1 < total ? BI : 0; };
   for (int u = -(NA - 1); u < 0; ++u) {
     if (nA(u)) issue_a();
     if (nB(u)) issue_b();
   }
 
-  f32x4 acc[2][RN];
+  f32x4 acc[RI][RN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < RI; ++i)
 #pragma unroll
     for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f16x8 ah[2], al[2], bh[RN], bl[RN];   // this wave's fragments of the chunk it multiplies next
+  f16x8 ah[RI], al[RI], bh[RN], bl[RN];   // this wave's fragments of the chunk it multiplies next
 
   const float as = A.x3s;
   // chunk c's fragments from stages (c % NA, c % NB): A rows of this wave, B columns of this wave
   auto load_frags = [&](int sa, int sb) __attribute__((always_inline)) {
     if (KAIR_DBG(E.dbg & 64)) return;
-    const char* stA = sA + sa * XR_ASTAGE;
+    const char* stA = sA + sa * ASTAGE;
     const char* stB = sB + sb * BSTAGE;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = grp * 64 + wm * 32 + i * 16 + fr;
+    for (int i = 0; i < RI; ++i) {
+      const int r = grp * (BM / 2) + wm * (BM / 4) + i * 16 + fr;
       const char* row = stA + r * 128;
       if constexpr (sizeof(TA) == 2) {
         ah[i] = *(const f16x8*)(row + ((fq ^ (r & 7)) << 4));
@@ -582,7 +588,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
   auto mfma_chunk = [&]() __attribute__((always_inline)) {
     if (KAIR_DBG(E.dbg & 2)) return;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RI; ++i)
 #pragma unroll
       for (int jn = 0; jn < RN; ++jn) {
         acc[i][jn] = mfma16(bh[jn], ah[i], acc[i][jn]);
@@ -602,12 +608,12 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       return 0;
     }
     int nvm = 0;
-    int rowv[2];
-    long roff[2];   // the shuffled forms' row part of the store offset
-    bool okm[2];
-    const int m0 = (mt0 + ct * mstride) * XR_BM + grp * 64 + wm * 32 + fr;
+    int rowv[RI];
+    long roff[RI];   // the shuffled forms' row part of the store offset
+    bool okm[RI];
+    const int m0 = (mt0 + ct * mstride) * BM + grp * (BM / 2) + wm * (BM / 4) + fr;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < RI; ++i) {
       const int m = m0 + i * 16;
       okm[i] = m < (int)E.M;
       const int mm = okm[i] ? m : 0;
@@ -629,33 +635,35 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       }
     }
     mfma_chunk();   // (the fragments die here: the epilogue operands load after it, under the partner's work)
-    float4 ex[2][NP][2];
-    float rs[2] = {1.f, 1.f};
+    float4 ex[RI][NP][2];
+    float rs[RI];
+#pragma unroll
+    for (int i = 0; i < RI; ++i) rs[i] = 1.f;
     if constexpr (EX != EX_NONE) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < RI; ++i)
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           const float* src = EX == EX_RESID ? E.resid + (long)rowv[i] * E.ldr : (const float*)E.gate + (long)rowv[i] * E.ldg;
           ex[i][p][0] = *(const float4*)(src + c8[p]);
           ex[i][p][1] = *(const float4*)(src + c8[p] + CB);
         }
-      nvm += 4 * NP;
+      nvm += 2 * RI * NP;
     }
     if constexpr (EX == EX_RESID) {
       const bool hs = E.rowscale != nullptr;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < RI; ++i) {
         const float r = *(hs ? E.rowscale + fdiv(rowv[i], E.d_rps) : (const float*)g_kair_zero_line);
         rs[i] = hs ? r : 1.f;
       }
-      nvm += 2;
+      nvm += RI;
     }
     const int nst = EM == XE_ROWS_F32 ? (E.pre ? 4 : 2) : (E.out_lo ? 2 : 1) + (EM == XE_ROWS_PAIR && E.pre ? 2 : 0);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) nvm += __ballot(okm[i]) != 0 ? NP * nst : 0;
+    for (int i = 0; i < RI; ++i) nvm += __ballot(okm[i]) != 0 ? NP * nst : 0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RI; ++i)
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         float v[8];
@@ -734,7 +742,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
         }
       }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RI; ++i)
 #pragma unroll
       for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
     return nvm;
@@ -759,10 +767,11 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       stamp(t, 0);
       if (t < total) {   // chunk t (its B part: issued in interval t-2)
         const int n = e2 + nA(t - 1) + nB(t - 1) + e1;
-        if (n == 2 + BI) {   // the steady state (no epilogue stores pending): one immediate wait, not the branch tree
-          if constexpr (BI == 3) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-          else if constexpr (BI == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        if (n == RI + BI) {   // the steady state (no epilogue stores pending): one immediate wait, not the branch tree
+          if constexpr (RI + BI == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+          else if constexpr (RI + BI == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          else if constexpr (RI + BI == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         } else {
           vm_wait(n);
         }
@@ -1159,17 +1168,17 @@ bool nt_x3_ring_ok(const kair_operand* A, const kair_operand* B, const kair_epil
          (A->ld == 0 ? A->im_C : A->ld) % 4 == 0;
 }
 
-template <typename TA, int AM, int BN>
+template <typename TA, int AM, int BN, int BM>
 int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int K, hipStream_t s) {
   const int tilesN = N / BN;
-  const int tilesM = (int)((M + XR_BM - 1) / XR_BM);
+  const int tilesM = (int)((M + BM - 1) / BM);
   int per = x3_cus() / tilesN;
   if (per < 1) per = 1;
   const int rounds = (tilesM + per - 1) / per;
   per = (tilesM + rounds - 1) / rounds;   // the same makespan on as few CUs as it needs
   const dim3 g(per * tilesN), bl(512);
 #define XR_LAUNCH(EM, EX, ACT, GK) \
-  hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN>), g, bl, 0, s, a, b, e, K, tilesN, tilesM)
+  hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN, BM>), g, bl, 0, s, a, b, e, K, tilesN, tilesM)
   if constexpr (BN == 192) {   // the Swin linears and the 192-channel convs: every epilogue form
     if (e.omode == KAIR_OUT_QKVBLK) XR_LAUNCH(XE_QKV, EX_NONE, XA_NONE, 0);
     else if (e.odt == KAIR_F16 && e.gate) XR_LAUNCH(XE_ROWS_PAIR, EX_GATE_F32, XA_NONE, XG_MUL);
@@ -1197,9 +1206,13 @@ int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int
 template <typename TA, int AM>
 int nt_x3_ring_dispatch(const Op& a, const Op& b, const Epi& e, long M, int N, int K, hipStream_t s) {
   switch (nt_x3_ring_bn(N)) {
-    case 64: return launch_nt_x3_ring<TA, AM, 64>(a, b, e, M, N, K, s);
-    case 128: return launch_nt_x3_ring<TA, AM, 128>(a, b, e, M, N, K, s);
-    default: return launch_nt_x3_ring<TA, AM, 192>(a, b, e, M, N, K, s);
+    case 64: return launch_nt_x3_ring<TA, AM, 64, XR_BM>(a, b, e, M, N, K, s);
+    case 128: return launch_nt_x3_ring<TA, AM, 128, XR_BM>(a, b, e, M, N, K, s);
+    default:
+      // 64-row tiles when the 128-row ones leave CUs idle (fewer tiles than CUs: the small per-GPU batches of a
+      // multi-GPU run, e.g. B = 4 -> M = 9,216: 72 tiles per N-tile)
+      if ((M + XR_BM - 1) / XR_BM * (N / 192) < x3_cus()) return launch_nt_x3_ring<TA, AM, 192, 64>(a, b, e, M, N, K, s);
+      return launch_nt_x3_ring<TA, AM, 192, XR_BM>(a, b, e, M, N, K, s);
   }
 }
 

@@ -17,7 +17,7 @@ from kair_amd import _hip as H  # noqa: E402
 from tools.gemm_micro import timeit  # noqa: E402
 
 dev = torch.device("cuda")
-M = 32 * 48 * 48
+M = int(os.environ.get("X3_MICRO_B", "32")) * 48 * 48   # X3_MICRO_B: the per-GPU batch (B = 4: the 8-GPU shape)
 PEAK_F16 = 2500.0
 
 
@@ -117,19 +117,21 @@ def attn_case(bwd):
 
 
 def cases():
-    return {
-        "nt_qkv_fwd": nt_case(576, 192, False, True, None),
+    return {   # the pair engine's forms (round 6: every block operand an fp16 pair) and, *_f32, the fp32-operand forms
+        "nt_qkv_fwd": nt_case(576, 192, True, True, None),
         "nt_proj_fwd": nt_case(192, 192, True, False, "resid"),
-        "nt_fc1_fwd": nt_case(384, 192, False, False, "gelu"),
-        "nt_fc2_fwd": nt_case(192, 384, False, False, "resid"),
-        "nt_fc2_dgrad": nt_case(384, 192, False, False, "gate"),
-        "nt_fc1_dgrad": nt_case(192, 384, False, False, None),
-        "nt_proj_dgrad": nt_case(192, 192, False, True, None),
+        "nt_fc1_fwd": nt_case(384, 192, True, True, "gelu"),
+        "nt_fc1_fwd_f32": nt_case(384, 192, False, False, "gelu"),
+        "nt_fc2_fwd": nt_case(192, 384, True, False, "resid"),
+        "nt_fc2_dgrad": nt_case(384, 192, True, True, "gate"),
+        "nt_fc2_dgrad_f32": nt_case(384, 192, False, False, "gate"),
+        "nt_fc1_dgrad": nt_case(192, 384, True, False, None),
+        "nt_proj_dgrad": nt_case(192, 192, True, True, None),
         "nt_qkv_dgrad": nt_case(192, 576, True, False, None),
-        "tn_qkv": tn_case(576, 192, True, False),
-        "tn_proj": tn_case(192, 192, False, True),
-        "tn_fc1": tn_case(384, 192, False, False),
-        "tn_fc2": tn_case(192, 384, False, False),
+        "tn_qkv": tn_case(576, 192, True, True),
+        "tn_proj": tn_case(192, 192, True, True),
+        "tn_fc1": tn_case(384, 192, True, True),
+        "tn_fc2": tn_case(192, 384, True, True),
         "tn_qkv_f32": tn_case(576, 192, False, False),
         "tn_proj_f32": tn_case(192, 192, False, False),
         "nt_conv_fwd": nt_conv(),
