@@ -525,9 +525,9 @@ OTHER_STEPS, OTHER_WARMUP = 20, 5
 
 # the precision each config's reference option file trains at (models/model_plain.py:31-36: no amp_enabled -> fp32):
 # C2 is quoted in bf16 by BASELINE.json itself; C3 (train_usrnet.json) and C5 (train_rrdb_psnr.json) are fp32, so
-# they are also timed on an engine of that precision class (REF_DTYPE: fp32x3 where the engine has the split-fp16
-# arithmetic, else the exact-fp32 MFMA engine), priced against that engine's MFMA ceiling
-REF_DTYPE = {"usrnet": "fp32", "rrdbnet": "fp32", "dncnn": "fp32"}
+# they are also timed on the engines of that precision class (REF_DTYPE: fp32x3 where the engine has the split-fp16
+# arithmetic -- C5 -- and the exact-fp32 MFMA engine), priced against that engine's MFMA ceiling
+REF_DTYPE = {"usrnet": ["fp32"], "rrdbnet": ["fp32x3", "fp32"], "dncnn": ["fp32"]}
 CEILING = {"bf16": (PEAK_BF16_TFLOPS, "dense bf16 MFMA peak"), "fp32x3": (PEAK_BF16_TFLOPS / 3, "dense f16 MFMA peak / 3"),
            "fp32": (PEAK_F32_TFLOPS, "dense fp32 MFMA peak")}
 
@@ -546,7 +546,7 @@ def other_configs(device):
               "dncnn": "C1 DnCNN sigma 25, 40x40, batch 64 (GPU step of the CPU config's network)"}
     res = {}
     for name, label in labels.items():
-        for dt in ["bf16"] + ([REF_DTYPE[name]] if name in REF_DTYPE else []):
+        for dt in ["bf16"] + REF_DTYPE.get(name, []):
             key = name if dt == "bf16" else f"{name}_{dt}"
             try:
                 B, sec, loss = bm.run(name, OTHER_STEPS, OTHER_WARMUP, device, dt)
@@ -559,7 +559,7 @@ def other_configs(device):
                             "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": round(pk, 1), "peak_what": what,
                                          "unit": "TFLOP/s", "frac": round(tf / pk, 4)},
                             "final_loss": round(loss, 6)}
-                if dt == REF_DTYPE.get(name):
+                if dt in REF_DTYPE.get(name, []):
                     res[key]["precision"] = "the reference option file's precision class (fp32)"
             except Exception as e:  # noqa: BLE001
                 res[key] = {"config": label, "dtype": dt, "error": repr(e)}

@@ -13,6 +13,7 @@ gradients of the five convs into one fp32 buffer of the same width (dgrad epilog
 gates them with LeakyReLU' read from the saved post-activation slices, and reduces weight / bias
 gradients with the split-M TN GEMM + deterministic finalize / column sums.
 """
+import math
 import weakref
 
 import torch
@@ -28,10 +29,19 @@ class ConvEngineBase:
 
     def __init__(self, net, compute_dtype):
         self.net_ref = weakref.ref(net)
-        if compute_dtype not in ("bf16", "fp32"):
+        if compute_dtype not in ("bf16", "fp32", "fp32x3"):
             raise ValueError(compute_dtype)
+        # fp32x3 (the reference's fp32 precision class on the 16-bit matrix cores, as SwinIREngine): fp32 activations
+        # and gradients in HBM, every conv product as hi.hi + hi.lo + lo.hi of power-of-2-scaled fp16 pairs (the
+        # split in the GEMM kernels, weights packed as fp16 pairs), fp32 accumulation; cd stays F32 for the
+        # fp32-rows bookkeeping (gate_cast), the launches go through _nt / conv_wgrad with compute KAIR_COMPUTE_X3
+        self.x3 = compute_dtype == "fp32x3"
         self.cd = H.BF16 if compute_dtype == "bf16" else H.F32
         self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
+        self.X3_AEXP = 4          # activation exponent (lowered by x3_backoff)
+        self.x3_gexp_off = 4      # gradient exponent over the loss normalisation
+        self.x3_backoffs = 0
+        self._ax = self.X3_AEXP   # the exponent of the GEMM A operands of the phase being issued
         self.plans = PlanPool(self._build_plan)
         self.plan_mode = "primary"
         self._packed_version = None
@@ -42,6 +52,36 @@ class ConvEngineBase:
     def _segment_done(self):
         if self.seg_hook is not None:
             self.seg_hook()
+
+    X3_BACKOFF_STEP, X3_BACKOFF_MAX = 6, 4
+
+    def _nt(self, A, B, E, M, N, K):
+        """kair_gemm_nt in the engine's arithmetic; fp32x3: A carries the phase exponent, B the weight packs'."""
+        if self.x3:
+            A.x3_exp, B.x3_exp = self._ax, H.X3_WEXP
+            H.gemm_nt(A, B, E, M, N, K, H.X3)
+        else:
+            H.gemm_nt(A, B, E, M, N, K, self.cd)
+
+    def _x3_grad_exp(self, numel, weight=1.0):
+        """Data gradients of a mean loss are O(weight / numel): times 2^(log2(numel / weight) + 4) they sit near 2^4."""
+        return int(round(math.log2(max(numel, 1) / max(abs(weight), 1e-30)))) + self.x3_gexp_off
+
+    def x3_backoff(self, step=None, act=True, grad=True):
+        """The range guard's reaction (FusedTrainer.check_range; SwinIREngine.x3_backoff)."""
+        if not self.x3:
+            raise RuntimeError("x3_backoff: not an fp32x3 engine")
+        if self.x3_backoffs >= self.X3_BACKOFF_MAX:
+            raise RuntimeError(f"fp32x3 range guard: the step is still non-finite after {self.x3_backoffs} exponent "
+                               f"back-offs: the data is not finite, or a weight left its pack window |w| < "
+                               f"2^{16 - H.X3_WEXP}")
+        step = self.X3_BACKOFF_STEP if step is None else int(step)
+        if act:
+            self.X3_AEXP -= step
+        if grad:
+            self.x3_gexp_off -= step
+        self.x3_backoffs += 1
+        return self.X3_AEXP, self.x3_gexp_off
 
     def convs(self):
         raise NotImplementedError
@@ -72,7 +112,10 @@ class ConvEngineBase:
         bias_src: the fp32 rows dz was cast from (bias gradient summed before rounding)."""
         K = 9 * c.Cip
         S = H.wgrad_splits(M, c.Cop, K)
-        H.gemm_tn(H.rows(dz, ld=ld_dz), src_op, P["wg_ws"], S, M, c.Cop, K, self.cd)
+        A = H.rows(dz, ld=ld_dz)
+        if self.x3:   # (gradient, activation) operands
+            A.x3_exp, src_op.x3_exp = P["e_g"], self.X3_AEXP
+        H.gemm_tn(A, src_op, P["wg_ws"], S, M, c.Cop, K, H.X3 if self.x3 else self.cd)
         H.wgrad_finalize(P["wg_ws"], S, c.map, grads[c.w])
         if bias_src is None:
             bias_src, ld_bias = dz, ld_dz
@@ -201,10 +244,11 @@ class RRDBNetEngine(ConvEngineBase):
         M = P["M"]
         x = x.contiguous()
         self.cur = P
+        self._ax = self.X3_AEXP   # fp32x3: forward operands are activations
         H.image_to_nhwc(x, P["xin"], self.Cin_p, None, 1.0, B, self.in_ch, Hh, Ww)
         c = self.conv_first
-        H.gemm_nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), c.fwd(), H.epilogue(P["fea"], bias=c.bp), M, nf,
-                  9 * self.Cin_p, cd)
+        self._nt(H.im2col(P["xin"], Hh, Ww, self.Cin_p), c.fwd(), H.epilogue(P["fea"], bias=c.bp), M, nf,
+                  9 * self.Cin_p)
         dense = P["dense"]
         H.row_copy(P["fea"], nf, M, nf, H.copy_desc(dense[0], ld=CD))
         rr_in = P["fea"]
@@ -213,34 +257,34 @@ class RRDBNetEngine(ConvEngineBase):
             D = dense[r]
             for j in range(4):          # x_{j+1} = lrelu(conv_{j+1}(cat(x, x1..x_j)))
                 c, cin = cs[j], nf + j * gc
-                H.gemm_nt(H.im2col(D, Hh, Ww, cin, ld=CD), c.fwd(),
-                          H.epilogue(D[:, cin:cin + gc], ldo=CD, bias=c.bp, act=self.act_epi, slope=self.slope), M, gc, 9 * cin, cd)
+                self._nt(H.im2col(D, Hh, Ww, cin, ld=CD), c.fwd(),
+                          H.epilogue(D[:, cin:cin + gc], ldo=CD, bias=c.bp, act=self.act_epi, slope=self.slope), M, gc, 9 * cin)
             c = cs[4]                    # y = x + 0.2 * conv5(cat(x, x1..x4))
             y = P["y"][r]
-            H.gemm_nt(H.im2col(D, Hh, Ww, CD, ld=CD), c.fwd(),
-                      H.epilogue(y, bias=c.bp, resid=x_in, rowscale=P["alpha"], rows_per_scale=M), M, nf, 9 * CD, cd)
+            self._nt(H.im2col(D, Hh, Ww, CD, ld=CD), c.fwd(),
+                      H.epilogue(y, bias=c.bp, resid=x_in, rowscale=P["alpha"], rows_per_scale=M), M, nf, 9 * CD)
             if r % 3 == 2:               # RRDB: out = 0.2 * RDB3 + x   (in place over y)
                 H.axpby(y, rr_in, 1.0, 0.2)
                 rr_in = y
             H.row_copy(y, nf, M, nf, H.copy_desc(dense[r + 1], ld=CD))
         c = self.trunk                   # fea = fea + trunk_conv(trunk)
-        H.gemm_nt(H.im2col(dense[-1], Hh, Ww, nf, ld=CD), c.fwd(), H.epilogue(P["fea2"], bias=c.bp, resid=P["fea"]),
-                  M, nf, 9 * nf, cd)
+        self._nt(H.im2col(dense[-1], Hh, Ww, nf, ld=CD), c.fwd(), H.epilogue(P["fea2"], bias=c.bp, resid=P["fea"]),
+                  M, nf, 9 * nf)
         H.row_copy(P["fea2"], nf, M, nf, H.copy_desc(P["fea2b"]))
         src = P["fea2b"]
         for c, (hh, ww), dst in zip(self.up, P["levels"], P["upa"]):   # lrelu(upconv(nearest x2))
-            H.gemm_nt(H.im2col(src, hh, ww, nf, up=2), c.fwd(), H.epilogue(dst, bias=c.bp, act=self.act_epi, slope=self.slope),
-                      B * hh * ww, nf, 9 * nf, cd)
+            self._nt(H.im2col(src, hh, ww, nf, up=2), c.fwd(), H.epilogue(dst, bias=c.bp, act=self.act_epi, slope=self.slope),
+                      B * hh * ww, nf, 9 * nf)
             src = dst
         HL, WL = P["levels"][-1]
         ML = P["ML"]
         c = self.hr
-        H.gemm_nt(H.im2col(src, HL, WL, nf), c.fwd(), H.epilogue(P["hr"], bias=c.bp, act=self.act_epi, slope=self.slope), ML,
-                  nf, 9 * nf, cd)
+        self._nt(H.im2col(src, HL, WL, nf), c.fwd(), H.epilogue(P["hr"], bias=c.bp, act=self.act_epi, slope=self.slope), ML,
+                  nf, 9 * nf)
         c = self.last
-        H.gemm_nt(H.im2col(P["hr"], HL, WL, nf), c.fwd(),
+        self._nt(H.im2col(P["hr"], HL, WL, nf), c.fwd(),
                   H.epilogue(P["E"], mode=H.OUT_NCHW, ldo=0, bias=c.bp, img=(None, 1.0, self.out_ch, HL, WL)), ML, c.Cop,
-                  9 * nf, cd)
+                  9 * nf)
         return P["E"]
 
     # ------------------------------------------------------------------------------------
@@ -248,6 +292,7 @@ class RRDBNetEngine(ConvEngineBase):
         P = self.cur
         HL, WL = P["levels"][-1]
         H.l1_loss(P["E"], H_img, P["loss"], P["dE"], 16, loss_weight, P["B"], self.out_ch, HL, WL, P["loss_ws"], charb_eps=charb_eps)
+        P["e_g"] = self._x3_grad_exp(P["B"] * self.out_ch * HL * WL, loss_weight)
         self.backward(grads, P)
         return P["loss"]
 
@@ -255,21 +300,25 @@ class RRDBNetEngine(ConvEngineBase):
         P = self.cur
         HL, WL = P["levels"][-1]
         H.image_to_nhwc(gE.contiguous(), P["dE"], 16, None, 1.0, P["B"], self.out_ch, HL, WL)
+        if self.x3:   # an arbitrary upstream gradient: its exponent from its own range (one host sync)
+            mx = float(gE.abs().max())
+            P["e_g"] = (8 - int(math.ceil(math.log2(mx)))) if mx > 0 and math.isfinite(mx) else 0
         self.backward(grads, P)
 
     def backward(self, grads, P):
         cd, nf, gc, CD = self.cd, self.nf, self.gc, self.CD
+        self._ax = P.get("e_g", 0)   # fp32x3: backward GEMM A operands are data gradients
         B, Hh, Ww, M, ML = P["B"], P["H"], P["W"], P["M"], P["ML"]
         HL, WL = P["levels"][-1]
         # conv_last
         c = self.last
-        H.gemm_nt(H.im2col(P["dE"], HL, WL, 16, flip=True), H.rows(c.Wd), H.epilogue(P["G_hr"]), ML, nf, 9 * 16, cd)
+        self._nt(H.im2col(P["dE"], HL, WL, 16, flip=True), H.rows(c.Wd), H.epilogue(P["G_hr"]), ML, nf, 9 * 16)
         self.conv_wgrad(P, c, P["dE"], 16, H.im2col(P["hr"], HL, WL, nf), ML, grads)
         # HRconv (lrelu)
         c = self.hr
         bs = self.gate_cast(P, P["G_hr"], nf, P["hr"], nf, P["dz_hr"], nf, ML, nf, self.act, self.slope)
         G = P["G_lv"][-1]
-        H.gemm_nt(H.im2col(P["dz_hr"], HL, WL, nf, flip=True), H.rows(c.Wd), H.epilogue(G), ML, nf, 9 * nf, cd)
+        self._nt(H.im2col(P["dz_hr"], HL, WL, nf, flip=True), H.rows(c.Wd), H.epilogue(G), ML, nf, 9 * nf)
         self.conv_wgrad(P, c, P["dz_hr"], nf, H.im2col(P["upa"][-1], HL, WL, nf), ML, grads, *bs)
         # upsampling convs, last to first: G = dL/d(post-lrelu output of up[i])
         for i in range(len(self.up) - 1, -1, -1):
@@ -278,7 +327,7 @@ class RRDBNetEngine(ConvEngineBase):
             dz = P["dz_hr"][:Mi]
             bs = self.gate_cast(P, G, nf, a, nf, dz, nf, Mi, nf, self.act, self.slope)
             Ghi = P["G_hi"][:Mi]
-            H.gemm_nt(H.im2col(dz, hh, ww, nf, flip=True), H.rows(c.Wd), H.epilogue(Ghi), Mi, nf, 9 * nf, cd)
+            self._nt(H.im2col(dz, hh, ww, nf, flip=True), H.rows(c.Wd), H.epilogue(Ghi), Mi, nf, 9 * nf)
             src = P["upa"][i - 1] if i > 0 else P["fea2b"]
             self.conv_wgrad(P, c, dz, nf, H.im2col(src, hh, ww, nf, up=2), Mi, grads, *bs)
             Gn = P["G_lv"][i - 1] if i > 0 else P["Gt"]
@@ -287,7 +336,7 @@ class RRDBNetEngine(ConvEngineBase):
         # fea2 = fea + trunk_conv(R):  Gt = dL/d fea2
         c = self.trunk
         H.act_grad_cast(P["Gt"], nf, None, 0, P["dzt"], nf, M, nf, 0)
-        H.gemm_nt(H.im2col(P["dzt"], Hh, Ww, nf, flip=True), H.rows(c.Wd), H.epilogue(P["G_R"]), M, nf, 9 * nf, cd)
+        self._nt(H.im2col(P["dzt"], Hh, Ww, nf, flip=True), H.rows(c.Wd), H.epilogue(P["G_R"]), M, nf, 9 * nf)
         self.conv_wgrad(P, c, P["dzt"], nf, H.im2col(P["dense"][-1], Hh, Ww, nf, ld=CD), M, grads, P["Gt"], nf)
         self._segment_done()   # the tail's gradients are final
         # RRDB trunk, last to first.  G_R = dL/d(RRDB output)
@@ -313,14 +362,14 @@ class RRDBNetEngine(ConvEngineBase):
         cs, D, Gd, gy = self.rdbs[r], P["dense"][r], P["Gd"], P["gy"]
         c = cs[4]
         bs = self.gate_cast(P, gy, nf, None, 0, P["dz5"], nf, M, nf, 0, 0.0, 0.2)
-        H.gemm_nt(H.im2col(P["dz5"], Hh, Ww, nf, flip=True), H.rows(c.Wd), H.epilogue(Gd), M, CD, 9 * nf, cd)
+        self._nt(H.im2col(P["dz5"], Hh, Ww, nf, flip=True), H.rows(c.Wd), H.epilogue(Gd), M, CD, 9 * nf)
         self.conv_wgrad(P, c, P["dz5"], nf, H.im2col(D, Hh, Ww, CD, ld=CD), M, grads, *bs)
         for j in range(3, -1, -1):
             c, cin = cs[j], nf + j * gc
             dz = P["dzg"]
             bs = self.gate_cast(P, Gd[:, cin:], CD, D[:, cin:], CD, dz, gc, M, gc, self.act, self.slope)
-            H.gemm_nt(H.im2col(dz, Hh, Ww, gc, flip=True), H.rows(c.Wd), H.epilogue(Gd, ldo=CD, resid=Gd, ldr=CD), M, cin,
-                      9 * gc, cd)
+            self._nt(H.im2col(dz, Hh, Ww, gc, flip=True), H.rows(c.Wd), H.epilogue(Gd, ldo=CD, resid=Gd, ldr=CD), M, cin,
+                      9 * gc)
             self.conv_wgrad(P, c, dz, gc, H.im2col(D, Hh, Ww, cin, ld=CD), M, grads, *bs)
         H.axpby_rows(gy, nf, Gd, CD, M, nf, 1.0, 1.0)
 

@@ -57,7 +57,7 @@ def define_G(opt):
     return net
 
 
-_X3_NETS = ("swinir",)   # networks with a split-fp16 (fp32x3) engine
+_X3_NETS = ("swinir", "rrdbnet", "rrdb")   # networks with a split-fp16 (fp32x3) engine
 
 
 def compute_dtype_of(opt):
@@ -72,7 +72,8 @@ def compute_dtype_of(opt):
                                             network has that engine (SwinIR: every product on the 16-bit
                                             matrix cores as three fp16 products of power-of-2-scaled hi/lo
                                             pairs, ~2^-21 relative -- it passes the exact-fp32 engine's oracle
-                                            bars, tests/test_x3_gpu.py), else 'fp32' (exact-fp32 MFMA)."""
+                                            bars, tests/test_x3_gpu.py; RRDBNet / RRDB: tests/test_full_configs_gpu.py
+                                            test_c5_rrdbnet_full[fp32x3]), else 'fp32' (exact-fp32 MFMA)."""
     o = opt["netG"]
     if o.get("compute_dtype"):
         if o["compute_dtype"] not in ("bf16", "fp32", "fp32x3"):

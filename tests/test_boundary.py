@@ -123,13 +123,15 @@ def test_custom_ops_registered_and_refuse_cpu():
 
 def test_precision_is_an_option_file_decision():
     """define_G's arithmetic follows the option file (select_network.compute_dtype_of): the reference's
-    fp32 by default (SwinIR: the split-fp16 engine 'fp32x3' that holds the fp32 engine's oracle bars; the conv
-    nets: exact fp32), its amp_enabled reduced-precision mode -> the bf16 engine, netG.compute_dtype explicit."""
+    fp32 by default (SwinIR, RRDBNet / RRDB: the fp16-pair engine 'fp32x3' that holds the fp32 engine's oracle bars;
+    the other conv nets: exact fp32), its amp_enabled reduced-precision mode -> the bf16 engine, netG.compute_dtype
+    explicit."""
     from kair_amd.models.select_network import compute_dtype_of
     base = {"netG": {"net_type": "swinir"}}
     assert compute_dtype_of(base) == "fp32x3"
     assert compute_dtype_of({**base, "train": {"amp_enabled": False}}) == "fp32x3"
-    assert compute_dtype_of({"netG": {"net_type": "rrdbnet"}}) == "fp32"
+    assert compute_dtype_of({"netG": {"net_type": "rrdbnet"}}) == "fp32x3"
+    assert compute_dtype_of({"netG": {"net_type": "dncnn"}}) == "fp32"
     with pytest.raises(ValueError):
         compute_dtype_of({"netG": {"net_type": "dncnn", "compute_dtype": "fp32x3"}})
     assert compute_dtype_of({**base, "train": {"amp_enabled": True}}) == "bf16"

@@ -13,8 +13,8 @@ Four configurations (reference: the DDP step of models/model_base.py:113-119, ma
     so parameters / EMA agree to the fp32 re-association of the weight-gradient sums;
   * "fp32x3-c4": the headline engine (fp16-pair arithmetic of the fp32 reference) at the C4 width, its
     deferred block weight gradients on the side stream;
-  * "rrdbnet-c5": RRDBNet x4 with its gradient segments (network_rrdbnet.py:74-101), 3 buckets, at the
-    precision options/train_rrdb_psnr.json trains in (fp32: no amp_enabled, select_network.compute_dtype_of)."""
+  * "rrdbnet-c5": RRDBNet x4 with its gradient segments (network_rrdbnet.py:74-101), 3 buckets, on the engine
+    options/train_rrdb_psnr.json maps to (fp32 arithmetic: no amp_enabled -> fp32x3, select_network.compute_dtype_of)."""
 import os
 import socket
 import tempfile
@@ -40,7 +40,7 @@ CONFIGS = {"fp32-small": dict(dtype="fp32", C=60, img=16, tol=1e-5, tol_upd=1e-4
            # (RRDBNet: 6 x 15 convs deep with 0.2-scaled residuals; at lr 1e-3 Adam normalises every gradient element,
            # so the shard / batch re-association of near-zero bias gradients moves those elements by up to lr: the
            # parameter distance is 2.4e-5 after 5 steps while the updates agree to 8e-5)
-           "rrdbnet-c5": dict(net="rrdbnet", dtype="fp32", nb=6, img=16, sf=4, tol=5e-5, tol_upd=2e-4)}
+           "rrdbnet-c5": dict(net="rrdbnet", dtype="fp32x3", nb=6, img=16, sf=4, tol=5e-5, tol_upd=2e-4)}
 
 
 def _net(cfg):

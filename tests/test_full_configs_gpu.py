@@ -135,10 +135,13 @@ def test_c2_swinir_light_full():
     run_pair(net, ref, x, 2)
 
 
-def test_c5_rrdbnet_full():
+@pytest.mark.parametrize("dt", ["fp32", "fp32x3"])
+def test_c5_rrdbnet_full(dt):
+    """C5 RRDBNet x4 (23 RRDBs) at options/train_rrdb_psnr.json's precision (fp32): the exact-fp32 engine and the
+    fp16-pair engine (fp32x3, the option file's default mapping) against the float64 oracle at the fp32 bars."""
     from kair_amd.models.network_rrdbnet import RRDBNet
     torch.manual_seed(5)
-    net = RRDBNet(3, 3, 64, 23, 32, 4, compute_dtype="fp32")
+    net = RRDBNet(3, 3, 64, 23, 32, 4, compute_dtype=dt)
     ref = ocv.RRDBNet(3, 3, 64, 23, 32, 4)
     x = torch.rand(1, 3, 32, 32, generator=torch.Generator().manual_seed(6))
     run_pair(net, ref, x, 4)
