@@ -641,7 +641,8 @@ def main():
     ap.add_argument("--no-psnr", action="store_true",
                     help="skip the PSNR parity evaluation (profiling runs: only full-batch dispatches)")
     ap.add_argument("--side-ctas", type=int, default=None,
-                    help="A/B: workgroup budget of the side-stream launches (< 0: that many times more row splits)")
+                    help="A/B: workgroup budget of the side-stream launches (0: uncapped; < 0: that many times more row "
+                         "splits; default: the engine's -- 192 for fp32x3, uncapped for bf16)")
     ap.add_argument("--side-priority", type=int, default=0, help="A/B: torch priority of the side stream")
     ap.add_argument("--main-priority", type=int, default=0, help="A/B: torch priority of the step's capture stream")
     ap.add_argument("--no-side-stream", action="store_true",

@@ -268,7 +268,7 @@ class _Blk:
 
 class SwinIREngine:
     def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True, fused_mlp=None,
-                 split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=0, side_priority=0,
+                 split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=None, side_priority=0,
                  split_act=True, conv_wr=True):
         """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
         see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
@@ -422,6 +422,11 @@ class SwinIREngine:
         # grouped launch, the attention backward 80 -> 340 us behind the conv weight gradient).  Measured
         # (profiles/r03_side_ctas_ab.txt): a cap makes the side work critical at B=32 (48 CTAs: 1080 -> 808
         # patches/s) and gains ~2% at B=4 (96 CTAs) -- so uncapped by default.
+        # fp32x3: the deferred weight gradients (one TN ring + finalize per block linear) capped at 192 workgroups: fewer
+        # row splits (the partial planes the finalize re-reads shrink by 1 / 4) and 64 CUs left to the main chain --
+        # B = 32 639 -> 650 patches/s against uncapped (profiles/r06_side_ctas_ab.txt)
+        if side_ctas is None:
+            side_ctas = 192 if self.x3 else 0
         self.side_ctas = int(side_ctas)
         # '1conv' weight gradients on the tap-per-tile ring (bf16 copies of G and the conv input)
         self.conv_tap = self.tdt == torch.bfloat16 and self.Cp == 192 and self.C % 4 == 0
