@@ -225,8 +225,9 @@ def time_roles(tr, serial=False, graph=False, replays=3):
             role = f"{name} @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}"
             if gev is not None:
                 e0 = gev.record()
+                s0 = H.trace_count()
                 f(*a, **k)
-                e1 = gev.record()
+                e1 = (gev.record(), s0 if H.trace_count() == s0 + 1 else -1)   # (end stamp, kernel trace slot)
             else:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -247,7 +248,7 @@ def time_roles(tr, serial=False, graph=False, replays=3):
         if gev is not None:
             e0 = gev.record()
             run0(self, ws, **kw)
-            e1 = gev.record()
+            e1 = (gev.record(), -1)
         else:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -259,28 +260,39 @@ def time_roles(tr, serial=False, graph=False, replays=3):
         setattr(H, n, wrap(n, orig[n]))
     H.WgradGroup.run = wg_run
     times = None
+    traced = 0
     try:
         if gev is not None:
             torch.cuda.synchronize()
+            tbuf = torch.zeros(4096, 2, dtype=torch.int64, device="cuda")   # kair_trace slots [start, end]
             g = torch.cuda.CUDAGraph()
             cs = torch.cuda.Stream()
             cs.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(cs):
                 g.capture_begin(pool=torch.cuda.graph_pool_handle())
+                H.trace_begin(tbuf)
                 try:
                     gev.calibrate()
                     tr._fwd_bwd(*tr.static)
                 finally:   # end the capture whatever happened inside it (a graph destroyed mid-capture aborts)
+                    H.trace_end()
                     g.capture_end()
             torch.cuda.current_stream().wait_stream(cs)
             torch.cuda.synchronize()
             times = [0.0] * len(rec)
             for _ in range(replays):
+                tbuf[:, 0].fill_(-1)   # UINT64_MAX: the atomic-min start
+                tbuf[:, 1].zero_()
                 g.replay()
                 torch.cuda.synchronize()
                 gev.read()
-                for i, (_, _, _, e0, e1) in enumerate(rec):
-                    times[i] += gev.elapsed(e0, e1) / replays
+                tt = tbuf.cpu().tolist()
+                for i, (_, _, _, e0, (e1, slot)) in enumerate(rec):
+                    if slot >= 0 and tt[slot][1] > 0:   # traced kernel: its first-start / last-end window
+                        times[i] += max(0, tt[slot][1] - tt[slot][0]) * 1e-5 / replays
+                    else:                               # stamp pair around the launch on its stream
+                        times[i] += gev.elapsed(e0, e1) / replays
+            traced = sum(1 for r in rec if r[4][1] >= 0)
             del g
         else:
             for _ in range(2):   # the second pass is the one kept (first-touch effects out of the way)
@@ -297,9 +309,11 @@ def time_roles(tr, serial=False, graph=False, replays=3):
         if gev is not None:
             gev.close()
     out = {}
-    for (role, name, (a, kw), _, _), ms in zip(rec, times):
+    for (role, name, (a, kw), _, e1), ms in zip(rec, times):
         d = out.setdefault(role, {"kernel": name, "launches": 0, "ms_total": 0.0, "bytes_total": 0, "flops_total": 0,
-                                  "rocprof": rocprof_name(name, a)})
+                                  "rocprof": rocprof_name(name, a),
+                                  "timing": "kernel trace" if (isinstance(e1, tuple) and e1[1] >= 0) else
+                                            ("stamps" if gev is not None else "events")})
         d["launches"] += 1
         d["ms_total"] += ms
         b, f = _alg_bytes(name, a, kw), _alg_flops(name, a)
@@ -764,16 +778,19 @@ def main():
                 roles, timing = time_roles(tr), f"in_step (graph events failed: {e!r})"
             except Exception as e2:  # noqa: BLE001
                 roles = {"error": {"kernel": repr(e2), "ms_total": 0.0}}
-    TIMING = ("kernel duration inside the graph-replayed training step: one capture of fwd+loss+bwd with a stream-ordered "
-              "device timestamp (kair_timestamp: the 100 MHz real-time counter) on the launch stream before and after every "
-              "libkair launch, side stream included, minus an empty stamp pair; replayed 3 times; mean per launch -- the "
-              "quantity rocprofv3 --kernel-trace reports for the graph-replayed bench step (profiles/*_kernel_stats.csv)") \
+    TIMING = ("kernel duration inside the graph-replayed training step (one capture of fwd+loss+bwd, replayed 3 times, mean "
+              "per launch): for the fp32x3 ring GEMMs and window-attention kernels the launch's first-workgroup start to "
+              "last-wave end from the device real-time counter (kair_trace_begin: in-kernel atomic min / max) -- the "
+              "quantity rocprofv3 --kernel-trace reports (profiles/*_kernel_stats.csv); for the other kernels a stream-"
+              "ordered device timestamp launch before and after (kair_timestamp), minus an empty stamp pair, which also "
+              "counts the wait for CUs the concurrent stream holds") \
         if timing == "graph" \
         else "eager in-step mean per launch: " + timing
 
     def roof(name, d):
         r = {"bound": "hbm", "kernel": d["rocprof"], "role": name, "launches_per_step": d["launches"],
-             "kernel_ms": round(d["ms"], 5), "step_ms_total": round(d["ms_total"], 4), "kernel_ms_timing": TIMING}
+             "kernel_ms": round(d["ms"], 5), "step_ms_total": round(d["ms_total"], 4), "kernel_ms_timing": TIMING,
+             "timed_by": d.get("timing")}
         if d.get("bytes"):
             gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
             r.update({"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
@@ -794,7 +811,7 @@ def main():
     kern = {}
     for v in good.values():
         d = kern.setdefault(v["rocprof"], {"rocprof": v["rocprof"], "launches": 0, "ms_total": 0.0, "b": 0, "f": 0,
-                                           "roles": 0, "nb": False, "nf": False})
+                                           "roles": 0, "nb": False, "nf": False, "timing": v.get("timing")})
         d["launches"] += v["launches"]
         d["ms_total"] += v["ms_total"]
         d["roles"] += 1

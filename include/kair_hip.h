@@ -526,6 +526,14 @@ int kair_range_check(const float* g, const float* p, long n, const float* loss, 
 /* Measurement: buf[idx] = the device real-time counter (100 MHz) when this one-lane launch runs, stream-ordered --
  * stamps around the kernels of a captured HIP graph (bench.py's in-graph kernel durations). */
 int kair_timestamp(unsigned long long* buf, int idx, void* stream);
+/* Measurement: open a kernel trace into buf [n][2] (uint64 {start, end} of the 100 MHz device counter; the caller
+ * sets start = UINT64_MAX, end = 0 before each run).  Until kair_trace_end, each launch of an instrumented kernel (the
+ * fp32x3 ring GEMMs and window-attention kernels) takes the next slot (kair_trace_count: slots taken so far) and
+ * records its first-workgroup start and last-wave end there, including inside captured graphs (the slot is bound
+ * at capture).  kair_trace_end returns the slots taken.  Host state of the calling thread; not for production. */
+int kair_trace_begin(unsigned long long* buf, int n);
+int kair_trace_count(void);
+int kair_trace_end(void);
 
 /* USRNet (network_usrnet_v1.py) -------------------------------------------------------------
  * Complex plane sets are float2 [planes][W][H] (TRANSPOSED: column-major per plane).            */

@@ -174,6 +174,9 @@ _SIGS = {
                          c_vp],
     "kair_range_check": [c_vp, c_vp, c_long, c_vp, c_float, c_vp, c_vp],
     "kair_timestamp": [c_vp, c_int, c_vp],
+    "kair_trace_begin": [c_vp, c_int],
+    "kair_trace_count": [],
+    "kair_trace_end": [],
     "kair_usr_fft_rows": [c_vp, c_int, c_int, c_long, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],
     "kair_usr_fft_cols": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
                           c_vp],
@@ -717,6 +720,19 @@ def adam_ema(p, g, m, v, ema, n, lr_t, beta1, beta2, eps, wd, decay, skip=None):
 def timestamp(buf, idx):
     """buf[idx] (int64 device tensor) = the device real-time counter (100 MHz) when this stream position runs."""
     check(lib().kair_timestamp(ptr(buf), idx, stream_ptr()), "timestamp")
+
+
+def trace_begin(buf):
+    """Open a kernel trace into buf (int64 [n, 2] device tensor; see kair_trace_begin)."""
+    check(lib().kair_trace_begin(ptr(buf), buf.shape[0]), "trace_begin")
+
+
+def trace_count():
+    return lib().kair_trace_count()
+
+
+def trace_end():
+    return lib().kair_trace_end()
 
 
 def range_check(g, p, loss, p_limit, flag):

@@ -52,6 +52,20 @@ int kair_set_error(int code, const char* fmt, ...);
 #define KAIR_DBG(x) (KAIR_DEBUG_ABLATIONS && (x))
 int kair_dbg_env(const char* name);
 
+// Measurement (bench.py: kernel durations inside the graph-replayed step, the quantity rocprofv3's kernel trace
+// reports).  While a trace is open (kair_trace_begin) each instrumented launch -- the x3 ring GEMMs and window-
+// attention kernels -- takes the next slot [start, end] of the caller's device buffer (kair_trace_take, host side)
+// and its workgroups fold the device real-time counter into it: an atomic min at entry (one lane per workgroup), an
+// atomic max at each wave's exit, i.e. the launch's first-start / last-end window.  No trace open: a null pointer
+// and two untaken branches per wave.  Vector (global) atomics only.
+unsigned long long* kair_trace_take();
+KAIR_DEV void trace_enter(unsigned long long* tr) {
+  if (tr && threadIdx.x == 0) atomicMin(tr, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+KAIR_DEV void trace_exit(unsigned long long* tr) {
+  if (tr && (threadIdx.x & 63) == 0) atomicMax(tr + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 template <typename T> KAIR_DEV float to_f(T v) { return (float)v; }
 template <typename T> KAIR_DEV T from_f(float v) { return (T)v; }
 

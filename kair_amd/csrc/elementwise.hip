@@ -1051,6 +1051,33 @@ extern "C" int kair_adam_ema_ex(float* p, const float* g, float* m, float* v, fl
   return 0;
 }
 
+// the open trace of kair_trace_begin (measurement only; host-side bookkeeping of the launching thread)
+static unsigned long long* g_trace_buf = nullptr;
+static int g_trace_n = 0, g_trace_next = -1;
+
+unsigned long long* kair_trace_take() {
+  if (!g_trace_buf || g_trace_next < 0 || g_trace_next >= g_trace_n) return nullptr;
+  return g_trace_buf + 2 * (g_trace_next++);
+}
+
+extern "C" int kair_trace_begin(unsigned long long* buf, int n) {
+  KAIR_CHECK_ARG(buf && n > 0, "trace_begin: bad args");
+  g_trace_buf = buf;
+  g_trace_n = n;
+  g_trace_next = 0;
+  return 0;
+}
+
+extern "C" int kair_trace_count(void) { return g_trace_next; }
+
+extern "C" int kair_trace_end(void) {
+  const int used = g_trace_next;
+  g_trace_buf = nullptr;
+  g_trace_n = 0;
+  g_trace_next = -1;
+  return used;
+}
+
 // measurement: one lane writes the device's constant-rate real-time counter (100 MHz, s_memrealtime) into buf[idx]
 // when the launch runs -- stream-ordered stamps around the kernels of a captured graph (bench.py's in-graph
 // kernel durations)

@@ -389,7 +389,8 @@ enum { XG_MUL = 4, XG_LEAKY = 2 };                                 // kair_epilo
 // wave waits for its own pieces of chunk t with a counted vmcnt (the DMA, epilogue loads and stores it issued
 // after them) before the barrier that opens interval t.
 template <typename TA, int AM, int EM, int EX, int ACT, int GK, int BN, int BM = XR_BM>
-__global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
+__global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM,
+                                                         unsigned long long* tr) {
   constexpr int NA = XR<BN>::NA, RN = XR<BN>::RN, NP = RN / 2, BI = XR<BN>::BI, BSTAGE = XR<BN>::BSTAGE, WC = BN / 2;
   // BM = 128 rows per tile (a wave multiplies 2 row fragments) or 64 (1: twice the tiles for small M -- the B = 4 per-GPU
   // shape of the 8-GPU run has 72 128-row tiles per N-tile for 256 CUs); RI row fragments / A DMA instructions per wave
@@ -404,6 +405,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
   const int fr = lane & 15, fq = lane >> 4, q8 = lane & 7;
   const int cta = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = cta % tilesN, mstride = gridDim.x / tilesN, mt0 = cta / tilesN;
+  trace_enter(tr);
   if (mt0 >= tilesM) return;
   const int ntile = (tilesM - mt0 + mstride - 1) / mstride;
   const int nk = K / 32;
@@ -814,6 +816,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
     __builtin_amdgcn_s_setprio(1);
     run(std::integral_constant<int, 1>{});
   }
+  trace_exit(tr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -844,7 +847,7 @@ KAIR_DEV int xt_swz_pair(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
 
 template <int BT, bool PR>
 __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
-                                                         int rps, float acc_scale) {
+                                                         int rps, float acc_scale, unsigned long long* tr) {
   static_assert(!PR || BT == BT_ROWS, "fp16-pair operands: row operands only");
   constexpr int ES = PR ? 2 : 4;   // operand element bytes
   __shared__ __attribute__((aligned(16))) char smem[XT_NS * XT_STAGE];
@@ -858,6 +861,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
   const int mend = mbeg + rps < M ? mbeg + rps : M;
   const int nch = mbeg < mend ? (mend - mbeg + XT_RB - 1) / XT_RB : 0;
   const char* zero = (const char*)g_kair_zero_line;
+  trace_enter(tr);
 
   // DMA geometry of this lane (the same for every chunk): wave-instruction g covers slots [64 g, 64 g + 64)
   // tap form: the lane's 4 columns k .. k + 3 of the K = 9 C contraction are channels c .. c + 3 of tap k / C (C % 4
@@ -1058,6 +1062,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
         *(float4*)(P + (long)n * K + k) = make_float4(acc[ik][in][0] * acc_scale, acc[ik][in][1] * acc_scale,
                                                       acc[ik][in][2] * acc_scale, acc[ik][in][3] * acc_scale);
     }
+  trace_exit(tr);
 }
 
 int g_x3_cus = 0;
@@ -1177,8 +1182,9 @@ int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int
   const int rounds = (tilesM + per - 1) / per;
   per = (tilesM + rounds - 1) / rounds;   // the same makespan on as few CUs as it needs
   const dim3 g(per * tilesN), bl(512);
+  unsigned long long* tr = kair_trace_take();
 #define XR_LAUNCH(EM, EX, ACT, GK) \
-  hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN, BM>), g, bl, 0, s, a, b, e, K, tilesN, tilesM)
+  hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN, BM>), g, bl, 0, s, a, b, e, K, tilesN, tilesM, tr)
   if constexpr (BN == 192) {   // the Swin linears and the 192-channel convs: every epilogue form
     if (e.omode == KAIR_OUT_QKVBLK) XR_LAUNCH(XE_QKV, EX_NONE, XA_NONE, 0);
     else if (e.odt == KAIR_F16 && e.gate) XR_LAUNCH(XE_ROWS_PAIR, EX_GATE_F32, XA_NONE, XG_MUL);
@@ -1314,12 +1320,13 @@ int kair_gemm_tn_x3(const kair_operand* A, const kair_operand* B, float* ws, int
   if (tn_x3_ring_ok(A, B, N, K)) {
     const int tilesN = (N + 191) / 192, tilesK = (K + 191) / 192, nt = tilesN * tilesK;
     const dim3 g(nt * splits), bl(512);
+    unsigned long long* tr = kair_trace_take();
     if (A->dtype == KAIR_F16)
-      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS, true>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
+      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS, true>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc, tr);
     else if (B->mode == KAIR_LD_IM2COL3)
-      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_TAP, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
+      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_TAP, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc, tr);
     else
-      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
+      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc, tr);
     KAIR_CHECK_LAUNCH();
     return 0;
   }
