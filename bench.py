@@ -162,78 +162,71 @@ _TIMED = ("gemm_nt", "gemm_tn", "wgrad_finalize", "colsum", "layernorm_fwd", "la
           "conv3x3_narrow_fwd_x3", "conv3x3_narrow_dgrad_x3", "conv3x3_narrow_wgrad_x3")
 
 
-class _GraphStamps:
-    """Stream-ordered timestamps inside a captured graph: kair_timestamp writes the device's 100 MHz real-time
-    counter into stamps[i] when its one-lane launch runs, one before and one after every libkair launch on the
-    launch's own stream (the side stream's too).  Replaying the graph stamps the graph-replayed step itself --
-    stream concurrency, back-to-back launches, no host gaps -- what rocprofv3 --kernel-trace records for the timed
-    bench step.  A stamp pair with nothing between it (calibrated at the head of the capture) is subtracted."""
+def _demangle(symbols):
+    """Readable kernel names (template instantiation, no return type / parameters) for mangled symbols, through
+    llvm-cxxfilt (a child process) when it is there; the symbol itself otherwise."""
+    import shutil
+    import subprocess
+    tool = shutil.which("llvm-cxxfilt") or next((t for t in ("/opt/rocm/lib/llvm/bin/llvm-cxxfilt",) if os.path.exists(t)),
+                                                 None) or shutil.which("c++filt")
+    out = list(symbols)
+    if tool and out:
+        try:
+            res = subprocess.run([tool], input="\n".join(out) + "\n", capture_output=True, text=True, timeout=60)
+            dem = res.stdout.splitlines()
+            if len(dem) == len(out):
+                out = dem
+        except (OSError, subprocess.SubprocessError):
+            pass
 
-    NCAL = 16
-
-    def __init__(self, n=4096):
-        from kair_amd import _hip as H
-        self.H = H
-        self.buf = torch.zeros(2 * n + 2 * self.NCAL, dtype=torch.int64, device="cuda")
-        self.used = 2 * self.NCAL
-
-    def calibrate(self):
-        for i in range(self.NCAL):
-            self.H.timestamp(self.buf, 2 * i)
-            self.H.timestamp(self.buf, 2 * i + 1)
-
-    def record(self):
-        if self.used == self.buf.numel():
-            raise RuntimeError("graph timing: stamp buffer exhausted")
-        i = self.used
-        self.used += 1
-        self.H.timestamp(self.buf, i)
-        return i
-
-    def read(self):
-        t = self.buf.cpu().tolist()
-        cal = sorted(t[2 * i + 1] - t[2 * i] for i in range(self.NCAL))
-        self.cal = cal[len(cal) // 2]
-        self.t = t
-
-    def elapsed(self, i0, i1):   # ms
-        return max(0, self.t[i1] - self.t[i0] - self.cal) * 1e-5
-
-    def close(self):
-        pass
+    def short(n):
+        n = n.replace("(anonymous namespace)::", "")
+        if n.startswith("void "):
+            n = n[5:]
+        depth = 0
+        for i, ch in enumerate(n):
+            depth += ch == "<"
+            depth -= ch == ">"
+            if ch == "(" and depth == 0 and i > 0:
+                return n[:i]
+        return n
+    return {s: short(d) for s, d in zip(symbols, out)}
 
 
-def time_roles(tr, serial=False, graph=False, replays=3):
-    """{role: {kernel, launches, ms (mean per launch), bytes, flops}} over one fwd + loss + bwd.
-    graph: the pass is captured as a HIP graph with a device timestamp launch (kair_timestamp) on the launch stream
-    before and after every libkair launch, and replayed `replays` times; a launch's time is its mean over the replays --
-    the kernel durations of the graph-replayed bench step (what the committed rocprofv3 summary of the bench
-    command averages).  Otherwise eager, a torch event pair per launch; serial: the engine's deferred side-stream
-    work runs in place on the main stream for this pass (every event pair brackets exactly one kernel)."""
+def time_roles(tr, serial=False, passes=2):
+    """In-step kernel durations of one fwd + loss + bwd of the timed configuration, run eagerly with its side-stream
+    concurrency (serial: the engine's deferred side-stream work in place on the main stream instead) inside a kernel
+    timing window (kair_ktime_begin): every libkair launch is dispatched with hipExtLaunchKernel and an event pair
+    the runtime stamps with the dispatch packet's start / end -- the kernel duration rocprofv3 --kernel-trace
+    reports.  The pass is queued whole behind a held wave (kair_gate_hold) and released at once, so it runs back to
+    back like the graph-replayed step, not at the host's launch pace.  The last of `passes` passes is kept.
+
+    Returns (roles, kernels):
+      roles    {call site: {kernel, launches, ms_total, ms, bytes, flops}} -- a call site's launches are the libkair
+               calls made there (the engine's thin helpers skipped), its time the kernels those calls dispatched;
+      kernels  {kernel: {kernel, symbol, launches, ms_total, ms, bytes, flops, roles}} -- rocprofv3's grouping (one
+               template instantiation); bytes / flops: the algorithmic bytes / FLOPs per launch, each call's figure
+               (_alg_bytes / _alg_flops) attributed to the longest kernel it dispatched, averaged over the attributed
+               launches (ms_attr: their mean duration)."""
     from kair_amd import _hip as H
-    rec = []
-    gev = _GraphStamps() if graph else None
+    rec = []   # (role, fn, (args, kwargs), first slot, end slot)
 
     # the engine's thin launch helpers: a role is named by their caller (the layer's call site), not by them
     helpers = ("_nt", "_wgrad", "_wg", "_run_conv_job", "_bias_colsum")
 
+    def site():
+        fr = sys._getframe(2)
+        while fr.f_back is not None and fr.f_code.co_name in helpers:
+            fr = fr.f_back
+        return f"{os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}"
+
     def wrap(name, f):
         def g(*a, **k):
-            fr = sys._getframe(1)
-            while fr.f_back is not None and fr.f_code.co_name in helpers:
-                fr = fr.f_back
-            role = f"{name} @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}"
-            if gev is not None:
-                e0 = gev.record()
-                s0 = H.trace_count()
-                f(*a, **k)
-                e1 = (gev.record(), s0 if H.trace_count() == s0 + 1 else -1)   # (end stamp, kernel trace slot)
-            else:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                f(*a, **k)
-                e1.record()
-            rec.append((role, name, (a, k), e0, e1))
+            where = site()
+            s0 = H.ktime_count()
+            r = f(*a, **k)
+            rec.append((f"{name} @ {where}", name, (a, k), s0, H.ktime_count()))
+            return r
         return g
 
     orig = {n: getattr(H, n) for n in _TIMED}
@@ -244,161 +237,101 @@ def time_roles(tr, serial=False, graph=False, replays=3):
         eng.side_stream = False
 
     def wg_run(self, ws, **kw):
-        fr = sys._getframe(1)
-        if gev is not None:
-            e0 = gev.record()
-            run0(self, ws, **kw)
-            e1 = (gev.record(), -1)
-        else:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            run0(self, ws, **kw)
-            e1.record()
-        rec.append((f"wgrad_grouped @ {os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}", "wgrad_grouped", ((), {}),
-                    e0, e1))
+        where = site()
+        s0 = H.ktime_count()
+        r = run0(self, ws, **kw)
+        rec.append((f"wgrad_grouped @ {where}", "wgrad_grouped", ((), {}), s0, H.ktime_count()))
+        return r
     for n in _TIMED:
         setattr(H, n, wrap(n, orig[n]))
     H.WgradGroup.run = wg_run
-    times = None
-    traced = 0
+    nslot, gate = 0, []
     try:
-        if gev is not None:
+        for _ in range(passes):
             torch.cuda.synchronize()
-            tbuf = torch.zeros(4096, 2, dtype=torch.int64, device="cuda")   # kair_trace slots [start, end]
-            g = torch.cuda.CUDAGraph()
-            cs = torch.cuda.Stream()
-            cs.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(cs):
-                g.capture_begin(pool=torch.cuda.graph_pool_handle())
-                H.trace_begin(tbuf)
-                try:
-                    gev.calibrate()
-                    tr._fwd_bwd(*tr.static)
-                finally:   # end the capture whatever happened inside it (a graph destroyed mid-capture aborts)
-                    H.trace_end()
-                    g.capture_end()
-            torch.cuda.current_stream().wait_stream(cs)
-            torch.cuda.synchronize()
-            times = [0.0] * len(rec)
-            for _ in range(replays):
-                tbuf[:, 0].fill_(-1)   # UINT64_MAX: the atomic-min start
-                tbuf[:, 1].zero_()
-                g.replay()
-                torch.cuda.synchronize()
-                gev.read()
-                tt = tbuf.cpu().tolist()
-                for i, (_, _, _, e0, (e1, slot)) in enumerate(rec):
-                    if slot >= 0 and tt[slot][1] > 0:   # traced kernel: its first-start / last-end window
-                        times[i] += max(0, tt[slot][1] - tt[slot][0]) * 1e-5 / replays
-                    else:                               # stamp pair around the launch on its stream
-                        times[i] += gev.elapsed(e0, e1) / replays
-            traced = sum(1 for r in rec if r[4][1] >= 0)
-            del g
-        else:
-            for _ in range(2):   # the second pass is the one kept (first-touch effects out of the way)
-                rec.clear()
+            H.gate_hold(5000)   # the pass is queued whole behind a held wave, then runs back to back
+            rec.clear()
+            H.ktime_begin(8192)
+            try:
                 tr._fwd_bwd(*tr.static)
+            finally:
+                nslot = H.ktime_end()
+                H.gate_release()
             torch.cuda.synchronize()
-            times = [e0.elapsed_time(e1) for _, _, _, e0, e1 in rec]
+            gate.append(H.gate_status())
     finally:
         for n in _TIMED:
             setattr(H, n, orig[n])
         H.WgradGroup.run = run0
         if serial and side0 is not None:
             eng.side_stream = side0
-        if gev is not None:
-            gev.close()
-    out = {}
-    for (role, name, (a, kw), _, e1), ms in zip(rec, times):
-        d = out.setdefault(role, {"kernel": name, "launches": 0, "ms_total": 0.0, "bytes_total": 0, "flops_total": 0,
-                                  "rocprof": rocprof_name(name, a),
-                                  "timing": "kernel trace" if (isinstance(e1, tuple) and e1[1] >= 0) else
-                                            ("stamps" if gev is not None else "events")})
+    if nslot >= 8192:
+        raise RuntimeError("time_roles: kernel timing window full (8192 launches)")
+    if gate[-1] != 1:
+        raise RuntimeError("time_roles: the launch gate timed out before the pass was queued (a host sync inside "
+                           "the pass?)")
+    slot = {i: H.ktime_read(i) for i in range(nslot)}
+    names = _demangle(sorted({sym for _, sym in slot.values()}))
+    # each slot belongs to the innermost recorded call whose range holds it
+    owner = {}
+    for j in sorted(range(len(rec)), key=lambda j: rec[j][4] - rec[j][3]):
+        for i in range(rec[j][3], rec[j][4]):
+            owner.setdefault(i, j)
+    roles, kernels = {}, {}
+    for i, (ms, sym) in slot.items():
+        kn = names.get(sym, sym)
+        d = kernels.setdefault(kn, {"kernel": kn, "symbol": sym, "launches": 0, "ms_total": 0.0, "b": 0, "f": 0,
+                                    "nb": 0, "nf": 0, "ms_b": 0.0, "ms_f": 0.0, "roles": set()})
         d["launches"] += 1
         d["ms_total"] += ms
-        b, f = _alg_bytes(name, a, kw), _alg_flops(name, a)
-        d["bytes_total"] = None if (b is None or d["bytes_total"] is None) else d["bytes_total"] + b
-        d["flops_total"] = None if (f is None or d["flops_total"] is None) else d["flops_total"] + f
-    for d in out.values():
+        j = owner.get(i)
+        role = rec[j][0] if j is not None else f"(outside the timed helpers) {kn}"
+        d["roles"].add(role)
+    for j, (role, fn, (a, k), s0, s1) in enumerate(rec):
+        mine = [i for i in range(s0, s1) if owner.get(i) == j]
+        r = roles.setdefault(role, {"launches": 0, "ms_total": 0.0, "b": 0, "f": 0, "nb": False, "nf": False, "k": {}})
+        r["launches"] += 1
+        if not mine:
+            continue
+        r["ms_total"] += sum(slot[i][0] for i in mine)
+        top = max(mine, key=lambda i: slot[i][0])
+        kn = names.get(slot[top][1], slot[top][1])
+        r["k"][kn] = r["k"].get(kn, 0) + 1
+        b, f = _alg_bytes(fn, a, k), _alg_flops(fn, a)
+        d = kernels[kn]
+        if b:
+            r["b"] += b
+            d["b"] += b
+            d["nb"] += 1
+            d["ms_b"] += slot[top][0]
+        else:
+            r["nb"] = True
+        if f:
+            r["f"] += f
+            d["f"] += f
+            d["nf"] += 1
+            d["ms_f"] += slot[top][0]
+        else:
+            r["nf"] = True
+    out_roles = {}
+    for role, r in roles.items():
+        n = r["launches"]
+        out_roles[role] = {"kernel": max(r["k"], key=r["k"].get) if r["k"] else "(no libkair launch)", "launches": n,
+                           "ms_total": r["ms_total"], "ms": r["ms_total"] / n,
+                           "bytes": None if (r["nb"] or not r["b"]) else r["b"] / n,
+                           "flops": None if (r["nf"] or not r["f"]) else r["f"] / n}
+    for d in kernels.values():
         n = d["launches"]
         d["ms"] = d["ms_total"] / n
-        d["bytes"] = d["bytes_total"] / n if d["bytes_total"] else None   # mean per launch
-        d["flops"] = d["flops_total"] / n if d["flops_total"] else None
-    return out
-
-
-def rocprof_name(fn, a):
-    """The kernel name rocprofv3 reports for a launch (to match the committed profiles / PMC passes)."""
-    if fn.startswith("rowgemm_"):
-        K, N = a[2], (a[4] if fn != "rowgemm_lnbwd" else 192)
-        kb = K // 16
-        epi = {"rowgemm_store": 0, "rowgemm_gate": 1, "rowgemm_lnbwd": 2}[fn]
-        ks = 2 if N == 384 else 4   # csrc/rowgemm.hip rg_dispatch: <KB, KS, NWC, EPI, HOLD>
-        hold = {12: kb // ks, 24: 6, 36: {0: 9, 1: 7, 2: 5}[epi]}[kb]
-        return f"rowgemm_kernel<{kb}, {ks}, {N // 96}, {epi}, {hold}>"
-    if fn == "gemm_nt" and a[6] == X3:
-        return _x3_nt_ring_name(a) if _x3_ring_nt(a) else "gemm_nt_x3_kernel"
-    if fn == "gemm_tn" and a[7] == X3:
-        if _x3_ring_tn(a):
-            return f"gemm_tn_x3_ring<{1 if a[1].mode == 1 else 0}, {'true' if a[0].dtype == 3 else 'false'}>"
-        return "gemm_tn_x3_kernel"
-    if fn in ("layernorm_fwd", "layernorm_bwd"):
-        return {"layernorm_fwd": "ln_fwd_kernel", "layernorm_bwd": "ln_bwd_kernel"}[fn]
-    if fn == "window_attn_fwd_x3":
-        return "attn_fwd_x3_kernel"
-    if fn == "window_attn_bwd_x3":
-        return "attn_bwd_x3_kernel"
-    return {"conv3x3_wr": "conv3x3_wr_kernel", "swin_mlp_fwd": "swin_mlp_fwd_wr_kernel", "swin_attn_fwd": "swin_attn_fwd12_kernel<6>",   # KAIR_ATTN12 (swin_fused.hip)
-            "window_attn_bwd": "attn_bwd_bf16_kernel<2>"}.get(fn, fn)
-
-
-def _x3_ring_tn(a):
-    """Whether an x3 gemm_tn launch takes the ring kernel (gemm_x3.hip tn_x3_ring_ok)."""
-    A, B, N, K = a[0], a[1], a[5], a[6]
-    ones_ok = lambda o: o.ones_col < 0 or o.ones_in_data
-    if A.dtype == 3 and B.dtype == 3:   # fp16 pairs (row operands)
-        return A.mode == 0 and B.mode == 0 and N % 8 == 0 and K % 8 == 0 and ones_ok(A) and ones_ok(B)
-    return (A.dtype == 0 and B.dtype == 0 and A.mode == 0 and N % 4 == 0 and K % 4 == 0 and ones_ok(A)
-            and not A.rowscale and not B.rowscale and
-            (B.mode == 0 or (B.mode == 1 and B.im_C % 4 == 0 and K == 9 * B.im_C and not B.im_flip and B.im_up != 2
-                              and N % 192 == 0)))
-
-
-def _x3_nt_ring_name(a):
-    """rocprofv3's name of the NT ring instantiation an x3 gemm_nt launch takes: gemm_nt_x3_ring<TA, AM, EM, EX,
-    ACT, GK, BN> as gemm_x3.hip launch_nt_x3_ring selects it."""
-    A, E, N = a[0], a[2], a[4]
-    bn = 192 if N % 192 == 0 else (64 if N == 64 else 128)
-    ta = "_Float16" if A.dtype == 3 else "float"
-    am = 1 if A.mode == 1 else 0
-    if bn == 192:
-        if E.out_mode == 1:
-            f = (2, 0, 0, 0)                       # XE_QKV
-        elif E.out_dtype == 3:
-            f = (1, 0, 0, 0)                       # XE_ROWS_PAIR
-        elif E.resid:
-            f = (0, 1, 0, 0)                       # EX_RESID
-        elif E.gate:
-            f = (0, 3, 0, 4 if E.gate_kind == 4 else 2)
-        elif E.act == 1:
-            f = (0, 0, 1 if E.pre_kind else 2, 0)  # XA_GELU / XA_GELU_X
-        elif E.act == 2:
-            f = (0, 0, 3, 0)                       # XA_LEAKY
-        else:
-            f = (0, 0, 0, 0)
-    else:
-        f = ((3, 0, 0, 0) if E.out_mode == 6 else (4, 0, 0, 0) if E.out_mode == 7 else (0, 3, 0, 2) if E.gate else
-             (0, 0, 3, 0) if E.act == 2 else (0, 0, 0, 0))
-    return f"gemm_nt_x3_ring<{ta}, {am}, {f[0]}, {f[1]}, {f[2]}, {f[3]}, {bn}>"
-
-
-def _x3_ring_nt(a):
-    """Whether an x3 gemm_nt launch takes the ring kernel (gemm_x3.hip nt_x3_ring_ok, the common cases)."""
-    A, E, N, K = a[0], a[2], a[4], a[5]
-    bn = 192 if N % 192 == 0 else (64 if N == 64 else (128 if N % 128 == 0 else 0))   # nt_x3_ring_bn
-    return (bn > 0 and K % 32 == 0 and (E.out_mode in (0, 1) or (E.out_mode == 6 and bn == 128)) and   # rows / q,k,v /
-                                                                                                    # PixelShuffle
-            (A.mode == 0 or (A.mode == 1 and A.dtype == 0 and A.im_C % 32 == 0 and K == 9 * A.im_C)))
+        d["bytes"] = d["b"] / d["nb"] if d["nb"] else None
+        d["flops"] = d["f"] / d["nf"] if d["nf"] else None
+        d["ms_bytes"] = d["ms_b"] / d["nb"] if d["nb"] else None   # mean duration of the launches those figures cover
+        d["ms_flops"] = d["ms_f"] / d["nf"] if d["nf"] else None
+        d["attributed"] = max(d["nb"], d["nf"])
+        d["roles"] = len(d["roles"])
+        for x in ("b", "f", "nb", "nf", "ms_b", "ms_f"):
+            del d[x]
+    return out_roles, kernels
 
 
 def pmc_traffic(key):
@@ -467,15 +400,9 @@ def engine_line(dtype, bpg, device, drop_path, steps, warmup, roles=True):
     peak = PEAK_F32_TFLOPS if dtype == "fp32" else PEAK_BF16_TFLOPS
     top = []
     if roles:
-        try:
-            rs = time_roles(tr, graph=True)
-        except Exception:  # noqa: BLE001
-            rs = time_roles(tr, serial=True)
-        for k, v in sorted(rs.items(), key=lambda kv: -kv[1]["ms_total"])[:5]:
-            # the fp32 engine's attention backward is the fp32 kernel (rocprof name)
-            kname = {"attn_bwd_bf16_kernel<2>": "attn_bwd_kernel<false>"}.get(v["rocprof"], v["rocprof"]) if dtype == "fp32" \
-                else v["rocprof"]
-            top.append({"role": k, "kernel": kname, "launches_per_step": v["launches"], "kernel_ms": round(v["ms"], 5),
+        _, ks = time_roles(tr)
+        for v in sorted(ks.values(), key=lambda v: -v["ms_total"])[:5]:
+            top.append({"kernel": v["kernel"], "launches_per_step": v["launches"], "kernel_ms": round(v["ms"], 5),
                         "step_ms_total": round(v["ms_total"], 4)})
     del tr, net, ema
     return {"value": round(bpg * steps / dt, 2), "unit": "patches/s", "ms_per_step": round(1000 * dt / steps, 3),
@@ -769,77 +696,57 @@ def main():
     peak_what = {"bf16": "dense bf16 MFMA peak (2.5 PF)",
                  "fp32x3": "dense f16 MFMA peak / 3 (2.5 PF / 3 = 833 TF: three fp16 products per fp32 FLOP)",
                  "fp32": "dense fp32 MFMA peak (157.3 TF)"}[args.dtype]
-    roles, timing = {}, "graph"
+    roles, kernels, roles_err = {}, {}, None
     if not args.no_roles:
-        try:   # kernel durations inside the graph-replayed step (external event nodes)
-            roles = time_roles(tr, graph=True)
+        try:
+            roles, kernels = time_roles(tr)
         except Exception as e:  # noqa: BLE001
-            try:   # fallback: an eager pass (side-stream concurrency kept), named as such in the line
-                roles, timing = time_roles(tr), f"in_step (graph events failed: {e!r})"
-            except Exception as e2:  # noqa: BLE001
-                roles = {"error": {"kernel": repr(e2), "ms_total": 0.0}}
-    TIMING = ("kernel duration inside the graph-replayed training step (one capture of fwd+loss+bwd, replayed 3 times, mean "
-              "per launch): for the fp32x3 ring GEMMs and window-attention kernels the launch's first-workgroup start to "
-              "last-wave end from the device real-time counter (kair_trace_begin: in-kernel atomic min / max) -- the "
-              "quantity rocprofv3 --kernel-trace reports (profiles/*_kernel_stats.csv); for the other kernels a stream-"
-              "ordered device timestamp launch before and after (kair_timestamp), minus an empty stamp pair, which also "
-              "counts the wait for CUs the concurrent stream holds") \
-        if timing == "graph" \
-        else "eager in-step mean per launch: " + timing
+            roles_err = repr(e)
+    TIMING = ("kernel duration as rocprofv3 --kernel-trace reports it (the dispatch packet's start / end timestamps, "
+              "hipExtLaunchKernel event pairs of a kair_ktime window), mean per launch over an eager fwd+loss+bwd pass "
+              "of the timed configuration with the step's side-stream concurrency, queued whole behind a held wave "
+              "(kair_gate_hold) and released at once so it runs back to back as the graph-replayed step does "
+              "(bench.time_roles)")
 
-    def roof(name, d):
-        r = {"bound": "hbm", "kernel": d["rocprof"], "role": name, "launches_per_step": d["launches"],
-             "kernel_ms": round(d["ms"], 5), "step_ms_total": round(d["ms_total"], 4), "kernel_ms_timing": TIMING,
-             "timed_by": d.get("timing")}
-        if d.get("bytes"):
-            gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+    def roof(d, role=None):
+        r = {"bound": "hbm", "kernel": d["kernel"], "launches_per_step": d["launches"], "kernel_ms": round(d["ms"], 5),
+             "step_ms_total": round(d["ms_total"], 4)}
+        if role is not None:
+            r["role"] = role
+        else:
+            r.update({"roles": d["roles"], "symbol": d["symbol"], "attributed_launches": d["attributed"]})
+        # the figures cover the launches they were attributed to: all of them (then their mean is the kernel's), or
+        # the attributed ones' own mean duration
+        ms_b = d["ms"] if role is not None else d.get("ms_bytes")
+        ms_f = d["ms"] if role is not None else d.get("ms_flops")
+        if d.get("bytes") and ms_b:
+            gbs = d["bytes"] / (ms_b * 1e-3) / 1e9
             r.update({"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
-                      "bytes_per_launch": round(d["bytes"]), "traffic": pmc_traffic(d["rocprof"])})
+                      "bytes_per_launch": round(d["bytes"]),
+                      "traffic": pmc_traffic(d["symbol"]) if role is None else None})
         else:
             r.update({"achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": None, "traffic": None})
-        if d.get("flops"):
-            tf = d["flops"] / (d["ms"] * 1e-3) / 1e12
+        if d.get("flops") and ms_f:
+            tf = d["flops"] / (ms_f * 1e-3) / 1e12
             r.update({"flops_per_launch": d["flops"], "achieved_tflops": round(tf, 2), "mfma_frac": round(tf / peak, 4),
                       "mfma_peak": peak_what})
             if args.dtype == "fp32x3":
                 r["frac_of_fp32_peak"] = round(tf / PEAK_F32_TFLOPS, 4)
         return r
-    good = {k: v for k, v in roles.items() if k != "error"}
-    ranked = sorted(good.items(), key=lambda kv: -kv[1]["ms_total"])
-    # per kernel (rocprofv3's grouping: one template instantiation, every role that launches it): total time per
-    # step, launches, mean duration and mean algorithmic bytes / FLOPs per launch
-    kern = {}
-    for v in good.values():
-        d = kern.setdefault(v["rocprof"], {"rocprof": v["rocprof"], "launches": 0, "ms_total": 0.0, "b": 0, "f": 0,
-                                           "roles": 0, "nb": False, "nf": False, "timing": v.get("timing")})
-        d["launches"] += v["launches"]
-        d["ms_total"] += v["ms_total"]
-        d["roles"] += 1
-        if v.get("bytes"):
-            d["b"] += v["bytes"] * v["launches"]
-        else:
-            d["nb"] = True
-        if v.get("flops"):
-            d["f"] += v["flops"] * v["launches"]
-        else:
-            d["nf"] = True
-    for d in kern.values():
-        d["ms"] = d["ms_total"] / d["launches"]
-        d["bytes"] = None if d["nb"] else d["b"] / d["launches"]
-        d["flops"] = None if d["nf"] else d["f"] / d["launches"]
-    kranked = sorted(kern.items(), key=lambda kv: -kv[1]["ms_total"])
+    ranked = sorted(roles.items(), key=lambda kv: -kv[1]["ms_total"])
+    kranked = sorted(kernels.values(), key=lambda v: -v["ms_total"])
     # attention GEMMs (QKV / q.k^T / p.v / proj): the fused attention half, the attention backward, the proj and
     # q/k/v input-gradient row GEMMs (bf16) / the split window-attention kernels (fp32x3) -- FLOPs over their
     # in-step time against the engine's MFMA ceiling
-    att_names = ("swin_attn_fwd", "attn_bwd_bf16_kernel", "rowgemm_kernel<12, 4, 2, 0>", "rowgemm_kernel<36",
+    att_names = ("swin_attn_fwd", "attn_bwd_bf16_kernel", "rowgemm_kernel<12, 4, 2, 0", "rowgemm_kernel<36",
                  "attn_fwd_x3_kernel", "attn_bwd_x3_kernel")
-    att = [v for v in good.values() if v.get("flops") and v["rocprof"].startswith(att_names)]
+    att = [v for v in kernels.values() if v.get("flops") and v["kernel"].startswith(att_names) and v["ms_flops"]]
     att_mfma = None
     if att:
-        fl_att = sum(v["flops"] * v["launches"] for v in att)
-        ms_att = sum(v["ms_total"] for v in att)
+        fl_att = sum(v["flops"] * v["attributed"] for v in att)
+        ms_att = sum(v["ms_flops"] * v["attributed"] for v in att)
         tf = fl_att / (ms_att * 1e-3) / 1e12
-        att_mfma = {"kernels": sorted({v["rocprof"] for v in att}), "flops_per_step": fl_att, "ms_per_step": round(ms_att, 4),
+        att_mfma = {"kernels": sorted(v["kernel"] for v in att), "flops_per_step": fl_att, "ms_per_step": round(ms_att, 4),
                     "achieved_tflops": round(tf, 2), "peak_tflops": round(peak, 1), "peak": peak_what,
                     "mfma_frac": round(tf / peak, 4)}
         if args.dtype == "fp32x3":
@@ -857,12 +764,12 @@ def main():
                    "global_batch": gbatch, "per_gpu_batch": bpg, "lq": 48, "hr": 192, "embed_dim": 180,
                    "depths": [6] * 6, "heads": 6, "window": 8, "drop_path_rate": args.drop_path,
                    "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
-        # roofline: the step's dominant kernel -- the kernel (template instantiation, all its roles) with the
-        # largest summed duration in the graph-replayed step, as rocprofv3 ranks the bench command's kernels
-        "roofline": (roof(f"all {kranked[0][1]['roles']} role(s) of the kernel", kranked[0][1]) if kranked else
-                     {"error": roles.get("error", {}).get("kernel", "roles skipped")}),
-        "kernels_by_duration": [roof(f"{v['roles']} role(s)", v) for _, v in kranked[:10]],
-        "roles_by_duration": [roof(k, v) for k, v in ranked[:12]],
+        # roofline: the step's dominant kernel -- the kernel (template instantiation, all its call sites) with the
+        # largest summed duration in the step, as rocprofv3 ranks the bench command's kernels
+        "roofline": ({**roof(kranked[0]), "kernel_ms_timing": TIMING} if kranked else
+                     {"error": roles_err or "roles skipped"}),
+        "kernels_by_duration": [roof(v) for v in kranked[:10]],
+        "roles_by_duration": [roof(v, k) for k, v in ranked[:12]],
         "attention_gemm_mfma": att_mfma,
         "step_roofline": {"train_flop_per_patch": fl["train"], "achieved_tflops_per_gpu": round(step_tflops, 2),
                           "peak_tflops": round(peak, 1), "peak": peak_what, "frac_of_peak": round(step_tflops / peak, 4),

@@ -523,17 +523,22 @@ int kair_adam_ema_ex(float* p, const float* g, float* m, float* v, float* ema, l
  * fp32 reference has no operand window.) */
 int kair_range_check(const float* g, const float* p, long n, const float* loss, float p_limit, unsigned* flag,
                      void* stream);
-/* Measurement: buf[idx] = the device real-time counter (100 MHz) when this one-lane launch runs, stream-ordered --
- * stamps around the kernels of a captured HIP graph (bench.py's in-graph kernel durations). */
-int kair_timestamp(unsigned long long* buf, int idx, void* stream);
-/* Measurement: open a kernel trace into buf [n][2] (uint64 {start, end} of the 100 MHz device counter; the caller
- * sets start = UINT64_MAX, end = 0 before each run).  Until kair_trace_end, each launch of an instrumented kernel (the
- * fp32x3 ring GEMMs and window-attention kernels) takes the next slot (kair_trace_count: slots taken so far) and
- * records its first-workgroup start and last-wave end there, including inside captured graphs (the slot is bound
- * at capture).  kair_trace_end returns the slots taken.  Host state of the calling thread; not for production. */
-int kair_trace_begin(unsigned long long* buf, int n);
-int kair_trace_count(void);
-int kair_trace_end(void);
+/* Measurement (bench.py's in-step kernel table; no reference counterpart): open a kernel timing window of n slots.
+ * Until kair_ktime_end, each libkair launch into a non-capturing stream takes the next slot and is dispatched with
+ * hipExtLaunchKernel and the slot's event pair, which the runtime stamps with the dispatch packet's start / end (the
+ * kernel duration rocprofv3 --kernel-trace reports).  kair_ktime_count: slots taken (by the last window once closed);
+ * kair_ktime_read(i): slot i's duration in ms (waits for it) and the kernel's symbol name.  Host state of the
+ * calling thread. */
+int kair_ktime_begin(int n);
+int kair_ktime_count(void);
+int kair_ktime_end(void);
+int kair_ktime_read(int i, float* ms, const char** name);
+
+/* Measurement: kair_gate_hold queues one wave on the stream that waits until kair_gate_release (or timeout_ms), so
+ * an eager pass queued behind it runs back to back; kair_gate_status: 0 pending, 1 released, 2 timed out. */
+int kair_gate_hold(int timeout_ms, void* stream);
+int kair_gate_release(void);
+int kair_gate_status(void);
 
 /* USRNet (network_usrnet_v1.py) -------------------------------------------------------------
  * Complex plane sets are float2 [planes][W][H] (TRANSPOSED: column-major per plane).            */

@@ -173,10 +173,13 @@ _SIGS = {
     "kair_adam_ema_ex": [c_vp, c_vp, c_vp, c_vp, c_vp, c_long, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp,
                          c_vp],
     "kair_range_check": [c_vp, c_vp, c_long, c_vp, c_float, c_vp, c_vp],
-    "kair_timestamp": [c_vp, c_int, c_vp],
-    "kair_trace_begin": [c_vp, c_int],
-    "kair_trace_count": [],
-    "kair_trace_end": [],
+    "kair_gate_hold": [c_int, c_vp],
+    "kair_gate_release": [],
+    "kair_gate_status": [],
+    "kair_ktime_begin": [c_int],
+    "kair_ktime_count": [],
+    "kair_ktime_end": [],
+    "kair_ktime_read": [c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_char_p)],
     "kair_usr_fft_rows": [c_vp, c_int, c_int, c_long, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],
     "kair_usr_fft_cols": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
                           c_vp],
@@ -717,22 +720,40 @@ def adam_ema(p, g, m, v, ema, n, lr_t, beta1, beta2, eps, wd, decay, skip=None):
                               stream_ptr()), "adam_ema")
 
 
-def timestamp(buf, idx):
-    """buf[idx] (int64 device tensor) = the device real-time counter (100 MHz) when this stream position runs."""
-    check(lib().kair_timestamp(ptr(buf), idx, stream_ptr()), "timestamp")
+def ktime_begin(n=4096):
+    """Open a kernel timing window of n slots (kair_ktime_begin): every later libkair launch into a non-capturing
+    stream is timed by its dispatch packet's start / end, as rocprofv3 --kernel-trace times it."""
+    check(lib().kair_ktime_begin(n), "ktime_begin")
 
 
-def trace_begin(buf):
-    """Open a kernel trace into buf (int64 [n, 2] device tensor; see kair_trace_begin)."""
-    check(lib().kair_trace_begin(ptr(buf), buf.shape[0]), "trace_begin")
+def ktime_count():
+    return lib().kair_ktime_count()
 
 
-def trace_count():
-    return lib().kair_trace_count()
+def ktime_end():
+    return lib().kair_ktime_end()
 
 
-def trace_end():
-    return lib().kair_trace_end()
+def gate_hold(timeout_ms=5000):
+    """Hold the current stream behind one waiting wave until gate_release() (or timeout_ms): an eager pass queued
+    behind it then runs back to back (kair_gate_hold)."""
+    check(lib().kair_gate_hold(timeout_ms, stream_ptr()), "gate_hold")
+
+
+def gate_release():
+    check(lib().kair_gate_release(), "gate_release")
+
+
+def gate_status():
+    """0 pending, 1 released by the host, 2 the wave's time limit passed first."""
+    return lib().kair_gate_status()
+
+
+def ktime_read(i):
+    """(duration ms, kernel symbol) of slot i of the last window; waits for that launch."""
+    ms, name = ctypes.c_float(), ctypes.c_char_p()
+    check(lib().kair_ktime_read(i, ctypes.byref(ms), ctypes.byref(name)), "ktime_read")
+    return ms.value, (name.value or b"").decode(errors="replace")
 
 
 def range_check(g, p, loss, p_limit, flag):

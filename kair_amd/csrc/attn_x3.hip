@@ -62,15 +62,13 @@ __global__ __launch_bounds__(64 * FWD_NW, 3) void attn_fwd_x3_kernel(const f16* 
                                                                   const float* __restrict__ table, f16* __restrict__ O,
                                                                   f16* __restrict__ Ol, long ldo, float* __restrict__ lse,
                                                                   long nWin, int nh, float scale, int H, int W, int shift,
-                                                                  int ones_col, int e_in, int e_out,
-                                                                  unsigned long long* tr) {
+                                                                  int ones_col, int e_in, int e_out) {
   constexpr int LD = ATT_LD, NW = FWD_NW;
   __shared__ __attribute__((aligned(16))) f16 sV[NW][2][TOK * LD];
   __shared__ float sTab[NW][232];
   __shared__ int sReg[NW][TOK];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long task = (long)blockIdx.x * NW + w;
-  trace_enter(tr);
   if (task >= nWin * nh) return;
   const long win = task / nh;
   const int h = (int)(task - win * nh);
@@ -189,7 +187,6 @@ __global__ __launch_bounds__(64 * FWD_NW, 3) void attn_fwd_x3_kernel(const f16* 
       }
     }
   }
-  trace_exit(tr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -207,8 +204,7 @@ __global__ __launch_bounds__(64 * BWD_NW, 2) void attn_bwd_x3_kernel(const f16* 
                                                             const float* __restrict__ table, const float* __restrict__ lse,
                                                             f16* __restrict__ dqkv, f16* __restrict__ dqkvl,
                                                             float* __restrict__ dB_part, long nWin, int nh, int wpg,
-                                                            float scale, int H, int W, int shift, int e_act, int e_grad,
-                                                            unsigned long long* tr) {
+                                                            float scale, int H, int W, int shift, int e_act, int e_grad) {
   constexpr int LD = ATT_LD, LDB = 72;
   // plane p (0 hi, 1 lo): [q | dO] tiles [64][LD]; after dV / dK wave w's dS tile [q][its 32 keys] at w * TOK * LD
   __shared__ __attribute__((aligned(16))) f16 sQG[2][2 * TOK * LD];
@@ -224,7 +220,6 @@ __global__ __launch_bounds__(64 * BWD_NW, 2) void attn_bwd_x3_kernel(const f16* 
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long gtask = blockIdx.x;
   const long ngroups = (nWin + wpg - 1) / wpg;
-  trace_enter(tr);
   if (gtask >= ngroups * nh) return;
   const int h = (int)(gtask % nh);
   const long grp = gtask / nh;
@@ -498,7 +493,6 @@ __global__ __launch_bounds__(64 * BWD_NW, 2) void attn_bwd_x3_kernel(const f16* 
   // partial bias gradient of this (group, head), binned by wave 0 (its k tile is free scratch now)
   __syncthreads();
   if (w == 0) bin_dbias<true>(sDB, LDB, (float*)&sK[0][0][0], dB_part + (grp * nh + h) * NBIN, lane);
-  trace_exit(tr);
 }
 
 int g_x3_cus = 0;
@@ -537,9 +531,9 @@ extern "C" int kair_window_attn_fwd_x3(const void* qkv, const void* qkv_lo, cons
   const long tasks = nWin * nh;
   const long nb = (tasks + FWD_NW - 1) / FWD_NW;
   KAIR_CHECK_ARG(e_in > -60 && e_in < 60 && e_out > -60 && e_out < 60, "window_attn_fwd_x3: exponents");
-  hipLaunchKernelGGL(attn_fwd_x3_kernel, dim3((unsigned)nb), dim3(64 * FWD_NW), 0, (hipStream_t)stream, (const f16*)qkv,
+  KAIR_LAUNCH(attn_fwd_x3_kernel, dim3((unsigned)nb), dim3(64 * FWD_NW), 0, (hipStream_t)stream, (const f16*)qkv,
                      (const f16*)qkv_lo, table, (f16*)O, (f16*)O_lo, ldo, lse, nWin, nh, scale, H, W, shift, ones_col, e_in,
-                     e_out, kair_trace_take());
+                     e_out);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -558,9 +552,9 @@ extern "C" int kair_window_attn_bwd_x3(const void* qkv, const void* qkv_lo, cons
   const long ngroups = (nWin + wpg - 1) / wpg;
   hipStream_t s = (hipStream_t)stream;
   KAIR_CHECK_ARG(e_act > -60 && e_act < 60 && e_grad > -60 && e_grad < 60, "window_attn_bwd_x3: exponents");
-  hipLaunchKernelGGL(attn_bwd_x3_kernel, dim3((unsigned)(ngroups * nh)), dim3(64 * BWD_NW), 0, s, (const f16*)qkv, (const f16*)qkv_lo,
+  KAIR_LAUNCH(attn_bwd_x3_kernel, dim3((unsigned)(ngroups * nh)), dim3(64 * BWD_NW), 0, s, (const f16*)qkv, (const f16*)qkv_lo,
                      (const f16*)O, (const f16*)O_lo, ldo, (const f16*)dO, (const f16*)dO_lo, lddo, table, lse, (f16*)dqkv,
-                     (f16*)dqkv_lo, ws, nWin, nh, (int)wpg, scale, H, W, shift, e_act, e_grad, kair_trace_take());
+                     (f16*)dqkv_lo, ws, nWin, nh, (int)wpg, scale, H, W, shift, e_act, e_grad);
   KAIR_CHECK_LAUNCH();
   if (!dtable) return 0;   // deferred: the per-group partials stay in ws for kair_attn_dtable_grouped (dtype x3)
   kair_attn_dtable_sum(ws, ngroups, nh, dtable, dtable_accumulate, s);

@@ -178,16 +178,16 @@ extern "C" int kair_bn_fwd(const float* z, long ldz, void* out, int out_dtype, l
   if (training) {
     const long rpb = (M + BN_NB - 1) / BN_NB;
     const dim3 gp(BN_NB, (C + 63) / 64), bp(1024), gf((C + 63) / 64);
-    hipLaunchKernelGGL((bn_partial<0, float>), gp, bp, 0, s, z, ldz, nullptr, 0, nullptr, 0, M, C, rpb, nullptr, nullptr, 0,
+    KAIR_LAUNCH((bn_partial<0, float>), gp, bp, 0, s, z, ldz, nullptr, 0, nullptr, 0, M, C, rpb, nullptr, nullptr, 0,
                        0.f, ws, nullptr);
     KAIR_CHECK_LAUNCH();
-    hipLaunchKernelGGL(bn_final<0>, gf, bp, 0, s, ws, nullptr, BN_NB, C, M, eps, momentum, mean, rstd, nullptr, nullptr,
+    KAIR_LAUNCH(bn_final<0>, gf, bp, 0, s, ws, nullptr, BN_NB, C, M, eps, momentum, mean, rstd, nullptr, nullptr,
                        nullptr, nullptr, 0, nullptr);
     KAIR_CHECK_LAUNCH();
-    hipLaunchKernelGGL((bn_partial<1, float>), gp, bp, 0, s, z, ldz, nullptr, 0, nullptr, 0, M, C, rpb, mean, nullptr, 0,
+    KAIR_LAUNCH((bn_partial<1, float>), gp, bp, 0, s, z, ldz, nullptr, 0, nullptr, 0, M, C, rpb, mean, nullptr, 0,
                        0.f, ws, nullptr);
     KAIR_CHECK_LAUNCH();
-    hipLaunchKernelGGL(bn_final<1>, gf, bp, 0, s, ws, nullptr, BN_NB, C, M, eps, momentum, mean, rstd, running_mean,
+    KAIR_LAUNCH(bn_final<1>, gf, bp, 0, s, ws, nullptr, BN_NB, C, M, eps, momentum, mean, rstd, running_mean,
                        running_var, nullptr, nullptr, 0, nullptr);
     KAIR_CHECK_LAUNCH();
   } else {
@@ -196,10 +196,10 @@ extern "C" int kair_bn_fwd(const float* z, long ldz, void* out, int out_dtype, l
   }
   const long n = M * C;
   if (out_dtype == KAIR_BF16)
-    hipLaunchKernelGGL(bn_apply_fwd<bf16>, dim3(nblk(n, 256)), dim3(256), 0, s, z, ldz, (bf16*)out, ldo, M, C, gamma, beta,
+    KAIR_LAUNCH(bn_apply_fwd<bf16>, dim3(nblk(n, 256)), dim3(256), 0, s, z, ldz, (bf16*)out, ldo, M, C, gamma, beta,
                        mu, rstd, rv, eps, act, slope);
   else
-    hipLaunchKernelGGL(bn_apply_fwd<float>, dim3(nblk(n, 256)), dim3(256), 0, s, z, ldz, (float*)out, ldo, M, C, gamma, beta,
+    KAIR_LAUNCH(bn_apply_fwd<float>, dim3(nblk(n, 256)), dim3(256), 0, s, z, ldz, (float*)out, ldo, M, C, gamma, beta,
                        mu, rstd, rv, eps, act, slope);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -218,30 +218,30 @@ extern "C" int kair_bn_bwd(const float* z, long ldz, const void* a, int a_dtype,
   float* part2 = ws + (long)BN_NB * C;
   float* stash = ws + 2L * BN_NB * C;
   if (a_dtype == KAIR_BF16)
-    hipLaunchKernelGGL((bn_partial<2, bf16>), gp, bp, 0, s, z, ldz, (const bf16*)a, lda, da, ldda, M, C, rpb, mean, rstd,
+    KAIR_LAUNCH((bn_partial<2, bf16>), gp, bp, 0, s, z, ldz, (const bf16*)a, lda, da, ldda, M, C, rpb, mean, rstd,
                        act, slope, part, part2);
   else
-    hipLaunchKernelGGL((bn_partial<2, float>), gp, bp, 0, s, z, ldz, (const float*)a, lda, da, ldda, M, C, rpb, mean, rstd,
+    KAIR_LAUNCH((bn_partial<2, float>), gp, bp, 0, s, z, ldz, (const float*)a, lda, da, ldda, M, C, rpb, mean, rstd,
                        act, slope, part, part2);
   KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_final<2>, gf, bp, 0, s, part, part2, BN_NB, C, M, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr,
+  KAIR_LAUNCH(bn_final<2>, gf, bp, 0, s, part, part2, BN_NB, C, M, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr,
                      dgamma, dbeta, accumulate, stash);
   KAIR_CHECK_LAUNCH();
   const long n = M * C;
   const dim3 ga(nblk(n, 256)), ba(256);
   if (a_dtype == KAIR_BF16) {
     if (dz_dtype == KAIR_BF16)
-      hipLaunchKernelGGL((bn_apply_bwd<bf16, bf16>), ga, ba, 0, s, z, ldz, (const bf16*)a, lda, da, ldda, (bf16*)dz, lddz, M, C,
+      KAIR_LAUNCH((bn_apply_bwd<bf16, bf16>), ga, ba, 0, s, z, ldz, (const bf16*)a, lda, da, ldda, (bf16*)dz, lddz, M, C,
                          gamma, mean, rstd, stash, act, slope);
     else
-      hipLaunchKernelGGL((bn_apply_bwd<bf16, float>), ga, ba, 0, s, z, ldz, (const bf16*)a, lda, da, ldda, (float*)dz, lddz, M,
+      KAIR_LAUNCH((bn_apply_bwd<bf16, float>), ga, ba, 0, s, z, ldz, (const bf16*)a, lda, da, ldda, (float*)dz, lddz, M,
                          C, gamma, mean, rstd, stash, act, slope);
   } else {
     if (dz_dtype == KAIR_BF16)
-      hipLaunchKernelGGL((bn_apply_bwd<float, bf16>), ga, ba, 0, s, z, ldz, (const float*)a, lda, da, ldda, (bf16*)dz, lddz, M,
+      KAIR_LAUNCH((bn_apply_bwd<float, bf16>), ga, ba, 0, s, z, ldz, (const float*)a, lda, da, ldda, (bf16*)dz, lddz, M,
                          C, gamma, mean, rstd, stash, act, slope);
     else
-      hipLaunchKernelGGL((bn_apply_bwd<float, float>), ga, ba, 0, s, z, ldz, (const float*)a, lda, da, ldda, (float*)dz, lddz,
+      KAIR_LAUNCH((bn_apply_bwd<float, float>), ga, ba, 0, s, z, ldz, (const float*)a, lda, da, ldda, (float*)dz, lddz,
                          M, C, gamma, mean, rstd, stash, act, slope);
   }
   KAIR_CHECK_LAUNCH();

@@ -2,6 +2,7 @@
 // Wave64 everywhere; bf16 storage is the compiler's __bf16 (RNE conversions via v_cvt_pk_bf16_f32).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include "kair_hip.h"
@@ -52,19 +53,18 @@ int kair_set_error(int code, const char* fmt, ...);
 #define KAIR_DBG(x) (KAIR_DEBUG_ABLATIONS && (x))
 int kair_dbg_env(const char* name);
 
-// Measurement (bench.py: kernel durations inside the graph-replayed step, the quantity rocprofv3's kernel trace
-// reports).  While a trace is open (kair_trace_begin) each instrumented launch -- the x3 ring GEMMs and window-
-// attention kernels -- takes the next slot [start, end] of the caller's device buffer (kair_trace_take, host side)
-// and its workgroups fold the device real-time counter into it: an atomic min at entry (one lane per workgroup), an
-// atomic max at each wave's exit, i.e. the launch's first-start / last-end window.  No trace open: a null pointer
-// and two untaken branches per wave.  Vector (global) atomics only.
-unsigned long long* kair_trace_take();
-KAIR_DEV void trace_enter(unsigned long long* tr) {
-  if (tr && threadIdx.x == 0) atomicMin(tr, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-}
-KAIR_DEV void trace_exit(unsigned long long* tr) {
-  if (tr && (threadIdx.x & 63) == 0) atomicMax(tr + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-}
+// Every libkair launch: KAIR_LAUNCH(kernel, grid, block, lds, stream, args...).  Outside a kernel timing window
+// (kair_ktime_begin, bench.py) a plain launch; inside one, hipExtLaunchKernel with the slot's event pair, which the
+// runtime stamps with the dispatch packet's start / end -- the kernel duration rocprofv3 --kernel-trace reports.
+bool kair_ktime_take(const void* fn, hipStream_t s, hipEvent_t* e0, hipEvent_t* e1);
+#define KAIR_LAUNCH(k, grid, block, lds, stream, ...)                                                        \
+  do {                                                                                                      \
+    hipEvent_t kt_e0_, kt_e1_;                                                                              \
+    if (kair_ktime_take(reinterpret_cast<const void*>(k), (stream), &kt_e0_, &kt_e1_))                     \
+      hipExtLaunchKernelGGL(k, (grid), (block), (lds), (stream), kt_e0_, kt_e1_, 0, __VA_ARGS__);            \
+    else                                                                                                    \
+      k<<<(grid), (block), (lds), (stream)>>>(__VA_ARGS__);                                                 \
+  } while (0)
 
 template <typename T> KAIR_DEV float to_f(T v) { return (float)v; }
 template <typename T> KAIR_DEV T from_f(float v) { return (T)v; }

@@ -349,7 +349,7 @@ extern "C" int kair_conv3x3_wr_tile(int split, int B, int H, int W, int C, int N
 }
 
 #define KAIR_WR(TXV, SPV, BMV, RV, RNV, EMV) \
-  hipLaunchKernelGGL((conv3x3_wr_kernel<TXV, SPV, BMV, RV, RNV, EMV>), dim3(grid), dim3(WR_NT), 0, s, a)
+  KAIR_LAUNCH((conv3x3_wr_kernel<TXV, SPV, BMV, RV, RNV, EMV>), dim3(grid), dim3(WR_NT), 0, s, a)
 
 extern "C" int kair_conv3x3_wr_ex(const void* x, int x_dtype, long ldx, int split, int flip, const void* w, int n_blocks,
                                   const float* bias, const float* resid, long ldr, void* out, int out_dtype, long ldo,

@@ -5,6 +5,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <vector>
+
 #include "common.h"
 
 namespace {
@@ -826,7 +828,7 @@ extern "C" int kair_pack_weight(const float* src, void* dst, int dst_dtype, cons
   KAIR_CHECK_ARG(src && dst && map, "pack_weight: null pointer");
   long total;
   if (int rc = pack_total(*map, dst_dtype, &total)) return rc;
-  hipLaunchKernelGGL(pack_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, src, dst, dst_dtype, *map,
+  KAIR_LAUNCH(pack_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, src, dst, dst_dtype, *map,
                      total);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -865,13 +867,13 @@ extern "C" int kair_pack_weights(const void* table_dev, int njobs, long nblocks,
   KAIR_CHECK_ARG(table_dev && njobs > 0 && nblocks > 0, "pack_weights: bad args");
   const kair_pack_job* jobs = (const kair_pack_job*)table_dev;
   const long* first = (const long*)((const char*)table_dev + (size_t)njobs * sizeof(kair_pack_job));
-  hipLaunchKernelGGL(pack_batched_kernel, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs, first);
+  KAIR_LAUNCH(pack_batched_kernel, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs, first);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
 
 int kair_launch_finalize_grouped(const FinGroup& g, hipStream_t s) {
-  hipLaunchKernelGGL(wgrad_finalize_grouped_kernel, dim3((unsigned)g.nblocks), dim3(256), 0, s, g);
+  KAIR_LAUNCH(wgrad_finalize_grouped_kernel, dim3((unsigned)g.nblocks), dim3(256), 0, s, g);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -890,10 +892,10 @@ extern "C" int kair_wgrad_finalize(const float* partial, int splits, const kair_
   const long nw = (long)mp.N * mp.K * taps;
   const long tot = nw + (bias_grad ? mp.N : 0);
   if ((Np * Kt) % 4 == 0 && ((uintptr_t)partial % 16) == 0) {
-    hipLaunchKernelGGL(wgrad_finalize4_kernel, dim3(nblk(Np * Kt / 4, 64)), dim3(256), 0, (hipStream_t)stream, partial,
+    KAIR_LAUNCH(wgrad_finalize4_kernel, dim3(nblk(Np * Kt / 4, 64)), dim3(256), 0, (hipStream_t)stream, partial,
                        splits, mp, grad_ref, bias_grad, ones_col, accumulate, Kt, Np * Kt, taps);
   } else {
-    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(nblk(tot, 64)), dim3(1024), 0, (hipStream_t)stream, partial, splits, mp,
+    KAIR_LAUNCH(wgrad_finalize_kernel, dim3(nblk(tot, 64)), dim3(1024), 0, (hipStream_t)stream, partial, splits, mp,
                        grad_ref, bias_grad, ones_col, accumulate, nw, Kt, Np * Kt, taps);
   }
   KAIR_CHECK_LAUNCH();
@@ -913,13 +915,13 @@ extern "C" int kair_row_copy(const float* src, long lds, long M, int C, const ka
   if (copy->dtype == KAIR_F16) {
     KAIR_CHECK_ARG(copy->out_lo && ((uintptr_t)copy->out % 8) == 0 && ((uintptr_t)copy->out_lo % 8) == 0,
                    "row_copy: an fp16 pair copy needs its 8-byte aligned lo plane (out_lo)");
-    hipLaunchKernelGGL(row_copy_pair_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (f16*)copy->out,
+    KAIR_LAUNCH(row_copy_pair_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (f16*)copy->out,
                        (f16*)copy->out_lo, copy->ld, copy->rowscale, rps, wm, M, C / 4, ldexpf(1.f, copy->x3_exp));
   } else if (copy->dtype == KAIR_BF16)
-    hipLaunchKernelGGL(row_copy_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (bf16*)copy->out, copy->ld,
+    KAIR_LAUNCH(row_copy_kernel<bf16>, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (bf16*)copy->out, copy->ld,
                        copy->rowscale, rps, wm, M, C / 4);
   else
-    hipLaunchKernelGGL(row_copy_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (float*)copy->out, copy->ld,
+    KAIR_LAUNCH(row_copy_kernel<float>, dim3(nblk(n, 256)), dim3(256), 0, s, src, lds, (float*)copy->out, copy->ld,
                        copy->rowscale, rps, wm, M, C / 4);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -935,15 +937,15 @@ extern "C" int kair_colsum(const kair_operand* G, long M, int Np, const kair_wma
   hipStream_t s = (hipStream_t)stream;
   const bool vec = Np % 8 == 0 && Np <= 256 && G->ld % 8 == 0 && ((uintptr_t)G->ptr & 15) == 0;
   if (vec && G->dtype == KAIR_BF16)
-    hipLaunchKernelGGL(colsum_partial_v<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)G->ptr, G->ld, M, Np, ws, rows_per);
+    KAIR_LAUNCH(colsum_partial_v<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)G->ptr, G->ld, M, Np, ws, rows_per);
   else if (vec)
-    hipLaunchKernelGGL(colsum_partial_v<float>, dim3(nb), dim3(256), 0, s, (const float*)G->ptr, G->ld, M, Np, ws, rows_per);
+    KAIR_LAUNCH(colsum_partial_v<float>, dim3(nb), dim3(256), 0, s, (const float*)G->ptr, G->ld, M, Np, ws, rows_per);
   else if (G->dtype == KAIR_BF16)
-    hipLaunchKernelGGL(colsum_partial<bf16>, grid, dim3(256), 0, s, (const bf16*)G->ptr, G->ld, M, Np, ws, rows_per);
+    KAIR_LAUNCH(colsum_partial<bf16>, grid, dim3(256), 0, s, (const bf16*)G->ptr, G->ld, M, Np, ws, rows_per);
   else
-    hipLaunchKernelGGL(colsum_partial<float>, grid, dim3(256), 0, s, (const float*)G->ptr, G->ld, M, Np, ws, rows_per);
+    KAIR_LAUNCH(colsum_partial<float>, grid, dim3(256), 0, s, (const float*)G->ptr, G->ld, M, Np, ws, rows_per);
   KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_final, dim3(nblk(map->N, 8)), dim3(256), 0, s, ws, nb, Np, *map, bias_grad, accumulate);
+  KAIR_LAUNCH(colsum_final, dim3(nblk(map->N, 8)), dim3(256), 0, s, ws, nb, Np, *map, bias_grad, accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -954,10 +956,10 @@ extern "C" int kair_image_to_nhwc(const float* img, void* out, int dtype, int ld
   const long total = (long)B * H * W * ldc;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(image_to_nhwc_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, s, img, (bf16*)out, ldc, mean,
+    KAIR_LAUNCH(image_to_nhwc_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, s, img, (bf16*)out, ldc, mean,
                        img_range, C, (long)H * W, total);
   else
-    hipLaunchKernelGGL(image_to_nhwc_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, img, (float*)out, ldc, mean,
+    KAIR_LAUNCH(image_to_nhwc_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, img, (float*)out, ldc, mean,
                        img_range, C, (long)H * W, total);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -967,7 +969,7 @@ extern "C" int kair_image_to_nhwc_hilo(const float* img, void* out, int ldc, con
                                        int C, int H, int W, void* stream) {
   KAIR_CHECK_ARG(img && out && ldc % 2 == 0 && 2 * C <= ldc, "image_to_nhwc_hilo: needs 2 * C <= ldc (even)");
   const long total = (long)B * H * W * ldc;
-  hipLaunchKernelGGL(image_to_nhwc_hilo_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, img, (bf16*)out,
+  KAIR_LAUNCH(image_to_nhwc_hilo_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, img, (bf16*)out,
                      ldc, mean, img_range, C, (long)H * W, total);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -986,17 +988,17 @@ static int pixel_loss(const float* E, const float* H, float* loss_out, void* dE,
   const bool i32 = (double)npix * ldc < 2.0e9 && numel < 2.0e9;
   const bool pix4f = ps_r == 1 && ldc == 4 && C <= 4 && dtype == KAIR_F32 && npix < (1L << 31) && ((uintptr_t)dE & 15) == 0;
   if (pix4f || (ps_r == 1 && ldc == 16 && C <= 4 && dtype == KAIR_BF16 && npix < (1L << 31) && ((uintptr_t)dE & 15) == 0)) {
-    if (pix4f && charb) hipLaunchKernelGGL(l1_pix4f_kernel<true>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
-    else if (pix4f) hipLaunchKernelGGL(l1_pix4f_kernel<false>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
-    else if (charb) hipLaunchKernelGGL(l1_pix16_kernel<true>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
-    else hipLaunchKernelGGL(l1_pix16_kernel<false>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
+    if (pix4f && charb) KAIR_LAUNCH(l1_pix4f_kernel<true>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
+    else if (pix4f) KAIR_LAUNCH(l1_pix4f_kernel<false>, dim3(nb), dim3(256), 0, s, E, H, (float*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
+    else if (charb) KAIR_LAUNCH(l1_pix16_kernel<true>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
+    else KAIR_LAUNCH(l1_pix16_kernel<false>, dim3(nb), dim3(256), 0, s, E, H, (bf16*)dE, gs, C, Hh * Ww, (int)npix, ws, eps);
     KAIR_CHECK_LAUNCH();
-    hipLaunchKernelGGL(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);
+    KAIR_LAUNCH(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);
     KAIR_CHECK_LAUNCH();
     return 0;
   }
 #define KAIR_PIXEL_LOSS(T, I, CHV)                                                                                       \
-  hipLaunchKernelGGL((l1_kernel<T, I, CHV>), dim3(nb), dim3(256), 0, s, E, H, (T*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws, \
+  KAIR_LAUNCH((l1_kernel<T, I, CHV>), dim3(nb), dim3(256), 0, s, E, H, (T*)dE, ldc, ps_r, gs, C, Hh, Ww, npix, ws, \
                      eps)
   if (charb) {
     if (dtype == KAIR_BF16 && i32) KAIR_PIXEL_LOSS(bf16, int, true);
@@ -1011,7 +1013,7 @@ static int pixel_loss(const float* E, const float* H, float* loss_out, void* dE,
   }
 #undef KAIR_PIXEL_LOSS
   KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);
+  KAIR_LAUNCH(l1_final, dim3(1), dim3(256), 0, s, ws, nb, (float)(weight / numel), loss_out);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1033,7 +1035,7 @@ extern "C" int kair_adam_ema(float* p, const float* g, float* m, float* v, float
   KAIR_CHECK_ARG(p && g && m && v && lr_t && n > 0, "adam_ema: bad args");
   long nb = (n + 255) / 256;
   if (nb > 8192) nb = 8192;
-  hipLaunchKernelGGL(adam_ema_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n, lr_t,
+  KAIR_LAUNCH(adam_ema_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n, lr_t,
                      beta1, beta2, eps, weight_decay, ema_decay, (const unsigned*)nullptr);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -1045,52 +1047,108 @@ extern "C" int kair_adam_ema_ex(float* p, const float* g, float* m, float* v, fl
   KAIR_CHECK_ARG(p && g && m && v && lr_t && n > 0, "adam_ema_ex: bad args");
   long nb = (n + 255) / 256;
   if (nb > 8192) nb = 8192;
-  hipLaunchKernelGGL(adam_ema_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n, lr_t,
+  KAIR_LAUNCH(adam_ema_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n, lr_t,
                      beta1, beta2, eps, weight_decay, ema_decay, skip);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
 
-// the open trace of kair_trace_begin (measurement only; host-side bookkeeping of the launching thread)
-static unsigned long long* g_trace_buf = nullptr;
-static int g_trace_n = 0, g_trace_next = -1;
+// Kernel timing window (bench.py's in-step kernel table): while open, every libkair launch (KAIR_LAUNCH) goes through
+// hipExtLaunchKernel with an event pair that the runtime stamps with the dispatch packet's own start / end timestamps
+// -- the times rocprofv3 --kernel-trace reports -- and the slot remembers the kernel's host symbol.  Host-side
+// bookkeeping of the launching thread; launches into a capturing stream are never timed (events cannot be captured).
+namespace {
+struct KtSlot {
+  hipEvent_t e0, e1;
+  const void* fn;
+};
+std::vector<KtSlot> g_kt;
+int g_kt_next = -1, g_kt_used = 0;   // next slot (-1: window closed), slots filled by the last window
+}   // namespace
 
-unsigned long long* kair_trace_take() {
-  if (!g_trace_buf || g_trace_next < 0 || g_trace_next >= g_trace_n) return nullptr;
-  return g_trace_buf + 2 * (g_trace_next++);
+bool kair_ktime_take(const void* fn, hipStream_t s, hipEvent_t* e0, hipEvent_t* e1) {
+  if (g_kt_next < 0 || g_kt_next >= (int)g_kt.size()) return false;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return false;
+  KtSlot& k = g_kt[g_kt_next++];
+  k.fn = fn;
+  *e0 = k.e0;
+  *e1 = k.e1;
+  return true;
 }
 
-extern "C" int kair_trace_begin(unsigned long long* buf, int n) {
-  KAIR_CHECK_ARG(buf && n > 0, "trace_begin: bad args");
-  g_trace_buf = buf;
-  g_trace_n = n;
-  g_trace_next = 0;
+extern "C" int kair_ktime_begin(int n) {
+  KAIR_CHECK_ARG(n > 0 && n <= (1 << 16), "ktime_begin: slot count out of range");
+  while ((int)g_kt.size() < n) {
+    KtSlot k{nullptr, nullptr, nullptr};
+    if (hipEventCreate(&k.e0) != hipSuccess || hipEventCreate(&k.e1) != hipSuccess)
+      return kair_set_error(KAIR_ERR_HIP, "ktime_begin: hipEventCreate failed");
+    g_kt.push_back(k);
+  }
+  g_kt_next = 0;
+  g_kt_used = 0;
   return 0;
 }
 
-extern "C" int kair_trace_count(void) { return g_trace_next; }
+extern "C" int kair_ktime_count(void) { return g_kt_next >= 0 ? g_kt_next : g_kt_used; }
 
-extern "C" int kair_trace_end(void) {
-  const int used = g_trace_next;
-  g_trace_buf = nullptr;
-  g_trace_n = 0;
-  g_trace_next = -1;
-  return used;
+extern "C" int kair_ktime_end(void) {
+  if (g_kt_next >= 0) g_kt_used = g_kt_next;
+  g_kt_next = -1;
+  return g_kt_used;
 }
 
-// measurement: one lane writes the device's constant-rate real-time counter (100 MHz, s_memrealtime) into buf[idx]
-// when the launch runs -- stream-ordered stamps around the kernels of a captured graph (bench.py's in-graph
-// kernel durations)
-__global__ void timestamp_kernel(unsigned long long* buf, int idx) {
-  if (threadIdx.x == 0) buf[idx] = __builtin_amdgcn_s_memrealtime();
+extern "C" int kair_ktime_read(int i, float* ms, const char** name) {
+  KAIR_CHECK_ARG(ms && name && i >= 0 && i < kair_ktime_count(), "ktime_read: slot out of range");
+  const KtSlot& k = g_kt[i];
+  if (hipEventSynchronize(k.e1) != hipSuccess || hipEventElapsedTime(ms, k.e0, k.e1) != hipSuccess)
+    return kair_set_error(KAIR_ERR_HIP, "ktime_read: event query failed");
+  *name = hipKernelNameRefByPtr(k.fn, nullptr);
+  if (!*name) *name = "";
+  return 0;
 }
 
-extern "C" int kair_timestamp(unsigned long long* buf, int idx, void* stream) {
-  KAIR_CHECK_ARG(buf && idx >= 0, "timestamp: bad args");
-  hipLaunchKernelGGL(timestamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, buf, idx);
+// Launch gate (bench.py's kernel table): one wave that holds its stream until the host releases it (or a time limit
+// passes), so the host can queue a whole eager pass behind it and the pass then runs back to back, with the stream
+// concurrency of the graph-replayed step instead of the host's launch pace.  The flag and status words live in
+// host-mapped memory; the wave polls with system-scope vector loads and reports with a vector store.
+namespace {
+unsigned* g_gate_host = nullptr;   // [0] release flag (host writes), [1] status (kernel writes: 1 released, 2 timed out)
+unsigned* g_gate_dev = nullptr;
+}   // namespace
+
+__global__ void gate_kernel(const unsigned* flag, unsigned* status, unsigned long long limit) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned seen = 0;
+  while (!(seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) &&
+         __builtin_amdgcn_s_memrealtime() - t0 < limit)
+    __builtin_amdgcn_s_sleep(8);
+  __hip_atomic_store(status, seen ? 1u : 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" int kair_gate_hold(int timeout_ms, void* stream) {
+  KAIR_CHECK_ARG(timeout_ms > 0 && timeout_ms <= 10000, "gate_hold: timeout out of range (1 .. 10000 ms)");
+  if (!g_gate_host) {
+    if (hipHostMalloc((void**)&g_gate_host, 2 * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&g_gate_dev, g_gate_host, 0) != hipSuccess)
+      return kair_set_error(KAIR_ERR_HIP, "gate_hold: host-mapped flag allocation failed");
+  }
+  __atomic_store_n(&g_gate_host[0], 0u, __ATOMIC_SEQ_CST);
+  __atomic_store_n(&g_gate_host[1], 0u, __ATOMIC_SEQ_CST);
+  KAIR_LAUNCH(gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, g_gate_dev, g_gate_dev + 1,
+              (unsigned long long)timeout_ms * 100000ull);   // the 100 MHz real-time counter
   KAIR_CHECK_LAUNCH();
   return 0;
 }
+
+extern "C" int kair_gate_release(void) {
+  KAIR_CHECK_ARG(g_gate_host != nullptr, "gate_release: no gate held");
+  __atomic_store_n(&g_gate_host[0], 1u, __ATOMIC_SEQ_CST);
+  return 0;
+}
+
+extern "C" int kair_gate_status(void) { return g_gate_host ? (int)__atomic_load_n(&g_gate_host[1], __ATOMIC_SEQ_CST) : 0; }
 
 extern "C" int kair_range_check(const float* g, const float* p, long n, const float* loss, float p_limit, unsigned* flag,
                                 void* stream) {
@@ -1101,7 +1159,7 @@ extern "C" int kair_range_check(const float* g, const float* p, long n, const fl
   long nb = (n / 4 + 255) / 256;
   if (nb > 2048) nb = 2048;
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(range_check_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, g, p, n, loss, p_limit,
+  KAIR_LAUNCH(range_check_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, g, p, n, loss, p_limit,
                      flag);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -1112,7 +1170,7 @@ extern "C" int kair_axpby(float* y, const float* x, float a, float b, long n, vo
   long nb = (n + 255) / 256;
   if (nb > 8192) nb = 8192;
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(axpby_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, y, x, a, b, n);
+  KAIR_LAUNCH(axpby_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, y, x, a, b, n);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1120,7 +1178,7 @@ extern "C" int kair_axpby(float* y, const float* x, float a, float b, long n, vo
 extern "C" int kair_axpby_rows(float* y, long ldy, const float* x, long ldx, long M, int C, float a, float b,
                                 void* stream) {
   KAIR_CHECK_ARG(y && x && M > 0 && C > 0 && ldy >= C && ldx >= C, "axpby_rows: bad args");
-  hipLaunchKernelGGL(axpby_rows_kernel, dim3(nblk(M * C, 256)), dim3(256), 0, (hipStream_t)stream, y, ldy, x, ldx, M, C, a, b);
+  KAIR_LAUNCH(axpby_rows_kernel, dim3(nblk(M * C, 256)), dim3(256), 0, (hipStream_t)stream, y, ldy, x, ldx, M, C, a, b);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1133,17 +1191,17 @@ extern "C" int kair_act_grad_cast(const float* G, long ldg, const void* X, int x
   const dim3 g(nblk(n, 256)), b(256);
   if (x_dtype == KAIR_BF16) {
     if (out_dtype == KAIR_BF16)
-      hipLaunchKernelGGL((act_grad_cast_kernel<bf16, bf16>), g, b, 0, s, G, ldg, (const bf16*)X, ldx, (bf16*)out, ldo, M, C,
+      KAIR_LAUNCH((act_grad_cast_kernel<bf16, bf16>), g, b, 0, s, G, ldg, (const bf16*)X, ldx, (bf16*)out, ldo, M, C,
                          kind, slope, scale);
     else
-      hipLaunchKernelGGL((act_grad_cast_kernel<bf16, float>), g, b, 0, s, G, ldg, (const bf16*)X, ldx, (float*)out, ldo, M,
+      KAIR_LAUNCH((act_grad_cast_kernel<bf16, float>), g, b, 0, s, G, ldg, (const bf16*)X, ldx, (float*)out, ldo, M,
                          C, kind, slope, scale);
   } else {
     if (out_dtype == KAIR_BF16)
-      hipLaunchKernelGGL((act_grad_cast_kernel<float, bf16>), g, b, 0, s, G, ldg, (const float*)X, ldx, (bf16*)out, ldo, M,
+      KAIR_LAUNCH((act_grad_cast_kernel<float, bf16>), g, b, 0, s, G, ldg, (const float*)X, ldx, (bf16*)out, ldo, M,
                          C, kind, slope, scale);
     else
-      hipLaunchKernelGGL((act_grad_cast_kernel<float, float>), g, b, 0, s, G, ldg, (const float*)X, ldx, (float*)out, ldo,
+      KAIR_LAUNCH((act_grad_cast_kernel<float, float>), g, b, 0, s, G, ldg, (const float*)X, ldx, (float*)out, ldo,
                          M, C, kind, slope, scale);
   }
   KAIR_CHECK_LAUNCH();
@@ -1154,7 +1212,7 @@ extern "C" int kair_sumpool2x(const float* src, long lds, float* dst, long ldd, 
                               void* stream) {
   KAIR_CHECK_ARG(src && dst && B > 0 && H > 0 && W > 0 && C > 0 && lds >= C && ldd >= C, "sumpool2x: bad args");
   const long n = (long)B * H * W * C;
-  hipLaunchKernelGGL(sumpool2x_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, src, lds, dst, ldd, B, H, W,
+  KAIR_LAUNCH(sumpool2x_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, src, lds, dst, ldd, B, H, W,
                      C, accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -1165,7 +1223,7 @@ extern "C" int kair_axpy(float* y, const float* x, float a, long n, void* stream
   long nb = (n / 4 + 255) / 256;
   if (nb > 4096) nb = 4096;
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(axpy_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, y, x, a, n);
+  KAIR_LAUNCH(axpy_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, y, x, a, n);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

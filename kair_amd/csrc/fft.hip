@@ -581,7 +581,7 @@ extern "C" int kair_usr_fft_rows(const float* src, int src_mode, int C, long ld,
   const int R = row_block(H, W);
   RowSrc s{src, src_mode, C > 0 ? C : 1, ld, kh, kw, sf};
   const size_t lds = (size_t)(W + 2 * R * (W + 1)) * sizeof(float2);
-  hipLaunchKernelGGL(fft_rows_fwd_kernel, dim3(H / R, planes), dim3(256), lds, (hipStream_t)stream, s, (float2*)T, H, W, R,
+  KAIR_LAUNCH(fft_rows_fwd_kernel, dim3(H / R, planes), dim3(256), lds, (hipStream_t)stream, s, (float2*)T, H, W, R,
                      pw);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -603,7 +603,7 @@ extern "C" int kair_usr_fft_cols(int mode, const void* T, void* T_out, const voi
             alpha_stride, part, C, H, W, sf};
   const size_t lds = (size_t)(H + 2 * sf * (H + 1)) * sizeof(float2);
   KAIR_CHECK_ARG(lds <= 150 * 1024, "usr_fft_cols: sf %d x H %d lines exceed LDS", sf, H);
-  hipLaunchKernelGGL(fft_cols_kernel, dim3(W / sf, planes), dim3(256), lds, (hipStream_t)stream, a, mode, ph);
+  KAIR_LAUNCH(fft_cols_kernel, dim3(W / sf, planes), dim3(256), lds, (hipStream_t)stream, a, mode, ph);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -620,10 +620,10 @@ extern "C" int kair_usr_ifft_rows(const void* T, void* dst, int nhwc, int dst_dt
   hipStream_t s = (hipStream_t)stream;
   const int Cc = C > 0 ? C : 1;
   if (dst_dtype == KAIR_BF16)
-    hipLaunchKernelGGL(fft_rows_inv_kernel<bf16>, dim3(H / R, planes), dim3(256), lds, s, (const float2*)T, (bf16*)dst, nhwc,
+    KAIR_LAUNCH(fft_rows_inv_kernel<bf16>, dim3(H / R, planes), dim3(256), lds, s, (const float2*)T, (bf16*)dst, nhwc,
                        Cc, ld, scale, H, W, R, pw);
   else
-    hipLaunchKernelGGL(fft_rows_inv_kernel<float>, dim3(H / R, planes), dim3(256), lds, s, (const float2*)T, (float*)dst,
+    KAIR_LAUNCH(fft_rows_inv_kernel<float>, dim3(H / R, planes), dim3(256), lds, s, (const float2*)T, (float*)dst,
                        nhwc, Cc, ld, scale, H, W, R, pw);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -632,7 +632,7 @@ extern "C" int kair_usr_ifft_rows(const void* T, void* dst, int nhwc, int dst_dt
 extern "C" int kair_usr_seg_sum(const float* ws, int seglen, int nseg, float scale, float* out, int ostride,
                                 int accumulate, void* stream) {
   KAIR_CHECK_ARG(ws && out && seglen > 0 && nseg > 0, "usr_seg_sum: bad args");
-  hipLaunchKernelGGL(seg_sum_kernel, dim3(nseg), dim3(256), 0, (hipStream_t)stream, ws, seglen, scale, out, ostride,
+  KAIR_LAUNCH(seg_sum_kernel, dim3(nseg), dim3(256), 0, (hipStream_t)stream, ws, seglen, scale, out, ostride,
                      accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -643,9 +643,9 @@ extern "C" int kair_usr_chan_sum(const float* x, long ld, int c, long HW, int B,
   KAIR_CHECK_ARG(x && ws && out && ld > c && c >= 0 && HW > 0 && B > 0, "usr_chan_sum: bad args");
   const int nchunk = KAIR_USR_CHAN_CHUNKS;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(chan_sum_partial_kernel, dim3(nchunk, B), dim3(256), 0, s, x, ld, c, HW, nchunk, ws);
+  KAIR_LAUNCH(chan_sum_partial_kernel, dim3(nchunk, B), dim3(256), 0, s, x, ld, c, HW, nchunk, ws);
   KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(seg_sum_kernel, dim3(B), dim3(256), 0, s, ws, nchunk, 1.0f, out, ostride, accumulate);
+  KAIR_LAUNCH(seg_sum_kernel, dim3(B), dim3(256), 0, s, ws, nchunk, 1.0f, out, ostride, accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -653,7 +653,7 @@ extern "C" int kair_usr_chan_sum(const float* x, long ld, int c, long HW, int B,
 extern "C" int kair_usr_upsample_nearest(const float* L, float* out, int planes, int h, int w, int sf, void* stream) {
   KAIR_CHECK_ARG(L && out && planes > 0 && h > 0 && w > 0 && sf > 0, "usr_upsample_nearest: bad args");
   const long total = (long)planes * h * sf * w * sf;
-  hipLaunchKernelGGL(upsample_nearest_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, L, out, h, w, sf,
+  KAIR_LAUNCH(upsample_nearest_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, L, out, h, w, sf,
                      total);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -665,10 +665,10 @@ extern "C" int kair_usr_pack_input(const float* x, const float* beta, int beta_s
   const long npix = (long)B * HW;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(pack_input_kernel<bf16>, dim3(nblk(npix, 256)), dim3(256), 0, s, x, beta, beta_stride, (bf16*)out, ld,
+    KAIR_LAUNCH(pack_input_kernel<bf16>, dim3(nblk(npix, 256)), dim3(256), 0, s, x, beta, beta_stride, (bf16*)out, ld,
                        C, HW, npix);
   else
-    hipLaunchKernelGGL(pack_input_kernel<float>, dim3(nblk(npix, 256)), dim3(256), 0, s, x, beta, beta_stride, (float*)out,
+    KAIR_LAUNCH(pack_input_kernel<float>, dim3(nblk(npix, 256)), dim3(256), 0, s, x, beta, beta_stride, (float*)out,
                        ld, C, HW, npix);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -684,10 +684,10 @@ extern "C" int kair_usr_pad(const void* src, void* dst, int dtype, int mode, int
   const long total = mode == KAIR_USR_CROP_NCHW ? npix : npix * ldc;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(usr_pad_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, s, (const bf16*)src, (bf16*)dst, mode, ldc,
+    KAIR_LAUNCH(usr_pad_kernel<bf16>, dim3(nblk(total, 256)), dim3(256), 0, s, (const bf16*)src, (bf16*)dst, mode, ldc,
                        H, W, Hp, Wp, total);
   else
-    hipLaunchKernelGGL(usr_pad_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, (const float*)src, (float*)dst, mode,
+    KAIR_LAUNCH(usr_pad_kernel<float>, dim3(nblk(total, 256)), dim3(256), 0, s, (const float*)src, (float*)dst, mode,
                        ldc, H, W, Hp, Wp, total);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -700,7 +700,7 @@ extern "C" int kair_hypanet_fwd(const float* sigma, float sf, const float* W1, c
   const size_t lds = (size_t)B * (2 * hc + no) * sizeof(float);
   KAIR_CHECK_ARG(lds <= 64 * 1024, "hypanet_fwd: batch too large for one block");
   HypaParams P{W1, b1, W2, b2, W3, b3};
-  hipLaunchKernelGGL(hypanet_fwd_kernel, dim3(1), dim3(256), lds, (hipStream_t)stream, sigma, sf, P, hc, no, B, ab);
+  KAIR_LAUNCH(hypanet_fwd_kernel, dim3(1), dim3(256), lds, (hipStream_t)stream, sigma, sf, P, hc, no, B, ab);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -715,7 +715,7 @@ extern "C" int kair_hypanet_bwd(const float* sigma, float sf, const float* W1, c
   KAIR_CHECK_ARG(lds <= 64 * 1024, "hypanet_bwd: batch too large for one block");
   HypaParams P{W1, b1, W2, b2, W3, b3};
   HypaGrads G{gW1, gb1, gW2, gb2, gW3, gb3};
-  hipLaunchKernelGGL(hypanet_bwd_kernel, dim3(1), dim3(256), lds, (hipStream_t)stream, sigma, sf, P, hc, no, B, gab, G,
+  KAIR_LAUNCH(hypanet_bwd_kernel, dim3(1), dim3(256), lds, (hipStream_t)stream, sigma, sf, P, hc, no, B, gab, G,
                      accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;

@@ -972,7 +972,7 @@ int launch_nt(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipS
   const int tilesN = (N + BN - 1) / BN;
   const long nwg = tilesM * tilesN;
   if (nwg > 0x7fffffff) return kair_set_error(KAIR_ERR_ARG, "gemm_nt: grid too large");
-  hipLaunchKernelGGL((gemm_nt_kernel<CT, TA, AM, BM, BN, WM, WN>), dim3((unsigned)nwg), dim3(NT), 0, s, A, B, E, K, tilesN,
+  KAIR_LAUNCH((gemm_nt_kernel<CT, TA, AM, BM, BN, WM, WN>), dim3((unsigned)nwg), dim3(NT), 0, s, A, B, E, K, tilesN,
                      (int)nwg);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -1029,15 +1029,15 @@ int launch_ring(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hi
   if (grid > need) grid = need;
   const dim3 g(grid), b(512);
   if (E.omode == KAIR_OUT_QKVBLK)
-    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_QKV, EX_NONE>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
+    KAIR_LAUNCH((gemm_nt_ring<BN, NS, AM, EM_QKV, EX_NONE>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
   else if (E.resid)
-    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_RESID>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
+    KAIR_LAUNCH((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_RESID>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
   else if (E.gate && E.gdt == KAIR_BF16)
-    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_GATE_BF16>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
+    KAIR_LAUNCH((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_GATE_BF16>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
   else if (E.gate)
-    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_GATE_F32>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
+    KAIR_LAUNCH((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_GATE_F32>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
   else
-    hipLaunchKernelGGL((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_NONE>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
+    KAIR_LAUNCH((gemm_nt_ring<BN, NS, AM, EM_ROWS, EX_NONE>), g, b, 0, s, A, B, E, K, tilesN, tilesM);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1441,15 +1441,15 @@ static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int 
   long tiles = (long)tilesM * tilesN;
   int grid = (int)(tiles < g_num_cus ? tiles : (g_num_cus / tilesN) * tilesN);   // a multiple of tilesN
 #define KAIR_HALO(NP, EXV, BNV, EMV, BMV) \
-  hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EXV, NP, BNV, EMV, BMV, 1>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM)
+  KAIR_LAUNCH((conv3x3_halo_kernel<TA, EXV, NP, BNV, EMV, BMV, 1>), dim3(grid), dim3(512), 0, s, A, B, E, K, tilesM)
   if constexpr (sizeof(TA) == 2) {
     if (A.imC > 192) {   // conv_halo_ok: 64 outputs, plain operands, C = 256 in four channel-group passes
       if (A.imC != 256) return kair_set_error(KAIR_ERR_ARG, "halo conv: C in (192, 256) has no channel-group form");
       if (E.omode == KAIR_OUT_PUNSHUF_SPM)
-        hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE, 1, 64, HC_EM_PUNSHUF, 96, 4>), dim3(grid), dim3(512), 0, s, A, B,
+        KAIR_LAUNCH((conv3x3_halo_kernel<TA, EX_NONE, 1, 64, HC_EM_PUNSHUF, 96, 4>), dim3(grid), dim3(512), 0, s, A, B,
                            E, K, tilesM);
       else
-        hipLaunchKernelGGL((conv3x3_halo_kernel<TA, EX_NONE, 1, 64, HC_EM_ROWS, 96, 4>), dim3(grid), dim3(512), 0, s, A, B, E,
+        KAIR_LAUNCH((conv3x3_halo_kernel<TA, EX_NONE, 1, 64, HC_EM_ROWS, 96, 4>), dim3(grid), dim3(512), 0, s, A, B, E,
                            K, tilesM);
       KAIR_CHECK_LAUNCH();
       return 0;
@@ -1516,26 +1516,26 @@ template <typename CT, typename TA, typename TB, int AMA, int AMB>
 int launch_tn(const Op& a, const Op& b, float* ws, int splits, long M, int N, int K, long rps, hipStream_t s) {
   if (tn192_shape(N, K)) {   // one 192-wide N tile (Cp = 192 conv weight gradients): no half-empty tile
     const int tilesK = (K + 127) / 128;
-    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 192, 128>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
+    KAIR_LAUNCH((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 192, 128>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
                        ws, M, N, K, rps, tilesK);
   } else if (tn_narrow_shape(N, K) && K <= 160) {   // e.g. 16 -> 16-channel 3x3 convs (K = 144): one 32 x 160 tile
-    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 32, 160>), dim3(1, splits), dim3(NT), 0, s, a, b,
+    KAIR_LAUNCH((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 32, 160>), dim3(1, splits), dim3(NT), 0, s, a, b,
                        ws, M, N, K, rps, 1);
   } else if (tn_narrow_shape(N, K)) {   // N <= 32 (dense-block growth convs): one 32 x 256 tile, no 3/4-empty N
     const int tilesK = (K + 255) / 256;
-    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 32, 256>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
+    KAIR_LAUNCH((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 32, 256>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
                        ws, M, N, K, rps, tilesK);
   } else if (tn_narrow64_shape(N, K)) {   // 32 < N <= 64: one 64 x 128 tile, no half-empty 128-wide N
     const int tilesK = (K + 127) / 128;
-    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 64, 128>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
+    KAIR_LAUNCH((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 64, 128>), dim3(tilesK, splits), dim3(NT), 0, s, a, b,
                        ws, M, N, K, rps, tilesK);
   } else if (N <= 64 && K <= 64) {
     const int tilesN = (N + 63) / 64, tilesK = (K + 63) / 64;
-    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 64, 64>), dim3(tilesN * tilesK, splits), dim3(NT), 0, s, a, b,
+    KAIR_LAUNCH((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 64, 64>), dim3(tilesN * tilesK, splits), dim3(NT), 0, s, a, b,
                        ws, M, N, K, rps, tilesK);
   } else {
     const int tilesN = (N + 127) / 128, tilesK = (K + 127) / 128;
-    hipLaunchKernelGGL((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 128, 128>), dim3(tilesN * tilesK, splits), dim3(NT), 0, s, a,
+    KAIR_LAUNCH((gemm_tn_kernel<CT, TA, TB, AMA, AMB, 128, 128>), dim3(tilesN * tilesK, splits), dim3(NT), 0, s, a,
                        b, ws, M, N, K, rps, tilesK);
   }
   KAIR_CHECK_LAUNCH();
@@ -1728,10 +1728,10 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
     rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
     const long grid = (long)ntiles * splits;
     if (A->mode == KAIR_LD_ROWS)
-      hipLaunchKernelGGL((gemm_tn_ring<AM_ROWS, BM_ROWS>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
+      KAIR_LAUNCH((gemm_tn_ring<AM_ROWS, BM_ROWS>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
                          ntiles, (int)rps);
     else
-      hipLaunchKernelGGL((gemm_tn_ring<AM_QKV, BM_ROWS>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
+      KAIR_LAUNCH((gemm_tn_ring<AM_QKV, BM_ROWS>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
                          ntiles, (int)rps);
     KAIR_CHECK_LAUNCH();
     return 0;
@@ -1746,7 +1746,7 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
     long rps = (M + splits - 1) / splits;
     rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
     const long grid = (long)ntiles * splits;
-    hipLaunchKernelGGL((gemm_tn_ring<AM_ROWS, BM_TAP>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
+    KAIR_LAUNCH((gemm_tn_ring<AM_ROWS, BM_TAP>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
                        ntiles, (int)rps);
     KAIR_CHECK_LAUNCH();
     return 0;
@@ -1763,7 +1763,7 @@ extern "C" int kair_gemm_tn(const kair_operand* A, const kair_operand* B, float*
     long rps = (M + splits - 1) / splits;
     rps = (rps + TNR_RB - 1) / TNR_RB * TNR_RB;
     const long grid = (long)ntiles * splits;
-    hipLaunchKernelGGL((gemm_tn_ring<AM_ROWS, BM_TAP3>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
+    KAIR_LAUNCH((gemm_tn_ring<AM_ROWS, BM_TAP3>), dim3((unsigned)grid), dim3(512), 0, s0, a, b, ws, (int)M, N, K, tilesK,
                        ntiles, (int)rps);
     KAIR_CHECK_LAUNCH();
     return 0;
@@ -1883,7 +1883,7 @@ extern "C" int kair_wgrad_grouped_ex(const kair_wgrad_job* jobs, int njobs, long
   g.njobs = njobs; g.ntiles = (int)ntiles; g.M = (int)M; g.rps = (int)rps;
   f.njobs = njobs; f.splits = splits; f.nblocks = blk0;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(gemm_tn_ring_grouped, dim3((unsigned)(ntiles * splits)), dim3(512), 0, s, g);
+  KAIR_LAUNCH(gemm_tn_ring_grouped, dim3((unsigned)(ntiles * splits)), dim3(512), 0, s, g);
   KAIR_CHECK_LAUNCH();
   return kair_launch_finalize_grouped(f, s);
 }

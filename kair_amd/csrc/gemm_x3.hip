@@ -389,8 +389,7 @@ enum { XG_MUL = 4, XG_LEAKY = 2 };                                 // kair_epilo
 // wave waits for its own pieces of chunk t with a counted vmcnt (the DMA, epilogue loads and stores it issued
 // after them) before the barrier that opens interval t.
 template <typename TA, int AM, int EM, int EX, int ACT, int GK, int BN, int BM = XR_BM>
-__global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM,
-                                                         unsigned long long* tr) {
+__global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
   constexpr int NA = XR<BN>::NA, RN = XR<BN>::RN, NP = RN / 2, BI = XR<BN>::BI, BSTAGE = XR<BN>::BSTAGE, WC = BN / 2;
   // BM = 128 rows per tile (a wave multiplies 2 row fragments) or 64 (1: twice the tiles for small M -- the B = 4 per-GPU
   // shape of the 8-GPU run has 72 128-row tiles per N-tile for 256 CUs); RI row fragments / A DMA instructions per wave
@@ -405,7 +404,6 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
   const int fr = lane & 15, fq = lane >> 4, q8 = lane & 7;
   const int cta = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = cta % tilesN, mstride = gridDim.x / tilesN, mt0 = cta / tilesN;
-  trace_enter(tr);
   if (mt0 >= tilesM) return;
   const int ntile = (tilesM - mt0 + mstride - 1) / mstride;
   const int nk = K / 32;
@@ -816,7 +814,6 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
     __builtin_amdgcn_s_setprio(1);
     run(std::integral_constant<int, 1>{});
   }
-  trace_exit(tr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -847,7 +844,7 @@ KAIR_DEV int xt_swz_pair(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
 
 template <int BT, bool PR>
 __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
-                                                         int rps, float acc_scale, unsigned long long* tr) {
+                                                         int rps, float acc_scale) {
   static_assert(!PR || BT == BT_ROWS, "fp16-pair operands: row operands only");
   constexpr int ES = PR ? 2 : 4;   // operand element bytes
   __shared__ __attribute__((aligned(16))) char smem[XT_NS * XT_STAGE];
@@ -861,7 +858,6 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
   const int mend = mbeg + rps < M ? mbeg + rps : M;
   const int nch = mbeg < mend ? (mend - mbeg + XT_RB - 1) / XT_RB : 0;
   const char* zero = (const char*)g_kair_zero_line;
-  trace_enter(tr);
 
   // DMA geometry of this lane (the same for every chunk): wave-instruction g covers slots [64 g, 64 g + 64)
   // tap form: the lane's 4 columns k .. k + 3 of the K = 9 C contraction are channels c .. c + 3 of tap k / C (C % 4
@@ -1062,7 +1058,6 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
         *(float4*)(P + (long)n * K + k) = make_float4(acc[ik][in][0] * acc_scale, acc[ik][in][1] * acc_scale,
                                                       acc[ik][in][2] * acc_scale, acc[ik][in][3] * acc_scale);
     }
-  trace_exit(tr);
 }
 
 int g_x3_cus = 0;
@@ -1082,7 +1077,7 @@ int launch_nt_x3(const Op& A, const Op& B, const Epi& E, long M, int N, int K, h
   const int tilesN = (N + BN - 1) / BN;
   const long nwg = tilesM * tilesN;
   if (nwg > 0x7fffffff) return kair_set_error(KAIR_ERR_ARG, "gemm_nt x3: grid too large");
-  hipLaunchKernelGGL((gemm_nt_x3_kernel<TA, AM, BM, BN>), dim3((unsigned)nwg), dim3(NT), 0, s, A, B, E, K, tilesN, (int)nwg);
+  KAIR_LAUNCH((gemm_nt_x3_kernel<TA, AM, BM, BN>), dim3((unsigned)nwg), dim3(NT), 0, s, A, B, E, K, tilesN, (int)nwg);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1104,11 +1099,11 @@ template <typename TA, typename TB, int AMB>
 int launch_tn_x3(const Op& a, const Op& b, float* ws, int splits, long M, int N, int K, long rps, float acc_scale,
                  hipStream_t s) {
   if (N <= 64 && K <= 64) {
-    hipLaunchKernelGGL((gemm_tn_x3_kernel<TA, TB, AMB, 64, 64>), dim3(1, splits), dim3(NT), 0, s, a, b, ws, M, N, K, rps, 1,
+    KAIR_LAUNCH((gemm_tn_x3_kernel<TA, TB, AMB, 64, 64>), dim3(1, splits), dim3(NT), 0, s, a, b, ws, M, N, K, rps, 1,
                        acc_scale);
   } else {
     const int tilesN = (N + 127) / 128, tilesK = (K + 127) / 128;
-    hipLaunchKernelGGL((gemm_tn_x3_kernel<TA, TB, AMB, 128, 128>), dim3(tilesN * tilesK, splits), dim3(NT), 0, s, a, b, ws,
+    KAIR_LAUNCH((gemm_tn_x3_kernel<TA, TB, AMB, 128, 128>), dim3(tilesN * tilesK, splits), dim3(NT), 0, s, a, b, ws,
                        M, N, K, rps, tilesK, acc_scale);
   }
   KAIR_CHECK_LAUNCH();
@@ -1182,9 +1177,8 @@ int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int
   const int rounds = (tilesM + per - 1) / per;
   per = (tilesM + rounds - 1) / rounds;   // the same makespan on as few CUs as it needs
   const dim3 g(per * tilesN), bl(512);
-  unsigned long long* tr = kair_trace_take();
 #define XR_LAUNCH(EM, EX, ACT, GK) \
-  hipLaunchKernelGGL((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN, BM>), g, bl, 0, s, a, b, e, K, tilesN, tilesM, tr)
+  KAIR_LAUNCH((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN, BM>), g, bl, 0, s, a, b, e, K, tilesN, tilesM)
   if constexpr (BN == 192) {   // the Swin linears and the 192-channel convs: every epilogue form
     if (e.omode == KAIR_OUT_QKVBLK) XR_LAUNCH(XE_QKV, EX_NONE, XA_NONE, 0);
     else if (e.odt == KAIR_F16 && e.gate) XR_LAUNCH(XE_ROWS_PAIR, EX_GATE_F32, XA_NONE, XG_MUL);
@@ -1216,7 +1210,8 @@ int nt_x3_ring_dispatch(const Op& a, const Op& b, const Epi& e, long M, int N, i
     case 128: return launch_nt_x3_ring<TA, AM, 128, XR_BM>(a, b, e, M, N, K, s);
     default:
       // 64-row tiles when the 128-row ones leave CUs idle (fewer tiles than CUs: the small per-GPU batches of a
-      // multi-GPU run, e.g. B = 4 -> M = 9,216: 72 tiles per N-tile)
+      // multi-GPU run, e.g. B = 4 -> M = 9,216: 72 tiles per N-tile); at B = 32 (576 tiles, 3 rounds on 192 CUs) the
+      // 64-row tiles measured slower on every block GEMM (profiles/r06_bm64_ab.txt)
       if ((M + XR_BM - 1) / XR_BM * (N / 192) < x3_cus()) return launch_nt_x3_ring<TA, AM, 192, 64>(a, b, e, M, N, K, s);
       return launch_nt_x3_ring<TA, AM, 192, XR_BM>(a, b, e, M, N, K, s);
   }
@@ -1320,13 +1315,12 @@ int kair_gemm_tn_x3(const kair_operand* A, const kair_operand* B, float* ws, int
   if (tn_x3_ring_ok(A, B, N, K)) {
     const int tilesN = (N + 191) / 192, tilesK = (K + 191) / 192, nt = tilesN * tilesK;
     const dim3 g(nt * splits), bl(512);
-    unsigned long long* tr = kair_trace_take();
-    if (A->dtype == KAIR_F16)
-      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS, true>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc, tr);
+      if (A->dtype == KAIR_F16)
+      KAIR_LAUNCH((gemm_tn_x3_ring<BT_ROWS, true>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
     else if (B->mode == KAIR_LD_IM2COL3)
-      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_TAP, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc, tr);
+      KAIR_LAUNCH((gemm_tn_x3_ring<BT_TAP, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
     else
-      hipLaunchKernelGGL((gemm_tn_x3_ring<BT_ROWS, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc, tr);
+      KAIR_LAUNCH((gemm_tn_x3_ring<BT_ROWS, false>), g, bl, 0, s, a, b, ws, (int)M, N, K, tilesK, nt, (int)rps, sc);
     KAIR_CHECK_LAUNCH();
     return 0;
   }

@@ -321,7 +321,7 @@ extern "C" int kair_ln_param_reduce_grouped(const kair_ln_param_job* jobs, int n
     blk += (2 * J.C + 7) / 8;
   }
   g.njobs = njobs;
-  hipLaunchKernelGGL(ln_param_reduce_grouped, dim3(blk), dim3(256), 0, (hipStream_t)stream, g);
+  KAIR_LAUNCH(ln_param_reduce_grouped, dim3(blk), dim3(256), 0, (hipStream_t)stream, g);
   KAIR_CHECK_LAUNCH();
   return 0;
 }  // ws holds LN_BLOCKS * 2 * C floats (kair_hip.h)
@@ -343,10 +343,10 @@ extern "C" int kair_layernorm_fwd(const float* x, long ldx, void* y, int y_dtype
   if (nb > max_nb) nb = max_nb;
   hipStream_t s = (hipStream_t)stream;
   if (y_dtype == KAIR_BF16)
-    hipLaunchKernelGGL(ln_fwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (bf16*)y, ldy, gamma, beta,
+    KAIR_LAUNCH(ln_fwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (bf16*)y, ldy, gamma, beta,
                        mean, rstd, M, C, eps, wm, one_col, (f16*)nullptr, 1.f);
   else
-    hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (float*)y, ldy, gamma, beta,
+    KAIR_LAUNCH(ln_fwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (float*)y, ldy, gamma, beta,
                        mean, rstd, M, C, eps, wm, one_col, (f16*)nullptr, 1.f);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -367,7 +367,7 @@ extern "C" int kair_layernorm_fwd_x3(const float* x, long ldx, void* y_hi, void*
   const WinMap wm = make_winmap(win_H, win_W, win_ws, win_shift);
   long nb = (M + ROWS_PER_BLOCK_ITER - 1) / ROWS_PER_BLOCK_ITER;
   if (nb > 1024) nb = 1024;
-  hipLaunchKernelGGL(ln_fwd_kernel<f16>, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, x, ldx, (f16*)y_hi, ldy,
+  KAIR_LAUNCH(ln_fwd_kernel<f16>, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, x, ldx, (f16*)y_hi, ldy,
                      gamma, beta, mean, rstd, M, C, eps, wm, one_col, (f16*)y_lo, ldexpf(1.f, x3_exp));
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -407,16 +407,16 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
   hipStream_t s = (hipStream_t)stream;
   const long nb = ln_bwd_blocks(M);
   if (dy_dtype == KAIR_BF16)
-    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const bf16*)dy, ldy, gamma,
+    KAIR_LAUNCH(ln_bwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const bf16*)dy, ldy, gamma,
                        mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm,
                        cp_lo, cp_s);
   else
-    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const float*)dy, ldy, gamma,
+    KAIR_LAUNCH(ln_bwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const float*)dy, ldy, gamma,
                        mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm,
                        cp_lo, cp_s);
   KAIR_CHECK_LAUNCH();
   if (!dgamma) return 0;   // deferred: the [nb][2C] partials stay in ws for kair_ln_param_reduce_grouped
-  hipLaunchKernelGGL(ln_param_reduce, dim3((2 * C + 7) / 8), dim3(256), 0, s, ws, (int)nb, C, dgamma, dbeta,
+  KAIR_LAUNCH(ln_param_reduce, dim3((2 * C + 7) / 8), dim3(256), 0, s, ws, (int)nb, C, dgamma, dbeta,
                      dparam_accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;

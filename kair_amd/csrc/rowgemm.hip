@@ -374,7 +374,7 @@ int rg_launch(const RgArgs& a, hipStream_t s, long* grid_out) {
   const long tiles = (a.M + RT - 1) / RT, slots = (long)rg_cus() * per_cu;
   const long grid = tiles < slots ? tiles : slots;
   if (grid_out) { *grid_out = grid; return 0; }
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NWC * KS), 0, s, a);
+  KAIR_LAUNCH(kern, dim3((unsigned)grid), dim3(64 * NWC * KS), 0, s, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

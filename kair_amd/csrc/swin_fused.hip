@@ -1635,11 +1635,11 @@ extern "C" int kair_swin_attn_fwd(const float* x, long ldx, const float* gamma, 
     ncu = 256;
   const long grid = nWin < ncu ? nWin : ncu;   // persistent: one workgroup per CU
   if (w_split)
-    hipLaunchKernelGGL((swin_attn_fwd_kernel<6, 2>), dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
+    KAIR_LAUNCH((swin_attn_fwd_kernel<6, 2>), dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
   else if (KAIR_ATTN12)   // two waves per head (A/B: -DKAIR_ATTN12=0 builds the 6-wave kernel)
-    hipLaunchKernelGGL((swin_attn_fwd12_kernel<6>), dim3((unsigned)grid), dim3(128 * 6), 0, (hipStream_t)stream, a);
+    KAIR_LAUNCH((swin_attn_fwd12_kernel<6>), dim3((unsigned)grid), dim3(128 * 6), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL((swin_attn_fwd_kernel<6, 1>), dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
+    KAIR_LAUNCH((swin_attn_fwd_kernel<6, 1>), dim3((unsigned)grid), dim3(64 * 6), 0, (hipStream_t)stream, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -1691,9 +1691,9 @@ extern "C" int kair_swin_mlp_fwd(const float* x, long ldx, const float* gamma, c
     a.nTiles = rows / rt;
     const long grid = a.nTiles < ncu ? a.nTiles : ncu;   // persistent: one workgroup per CU
     if (w_split)
-      hipLaunchKernelGGL(swin_mlp_fwd_kernel<2>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
+      KAIR_LAUNCH(swin_mlp_fwd_kernel<2>, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, a);
     else
-      hipLaunchKernelGGL(swin_mlp_fwd_wr_kernel, dim3((unsigned)grid), dim3(768), 0, (hipStream_t)stream, a);
+      KAIR_LAUNCH(swin_mlp_fwd_wr_kernel, dim3((unsigned)grid), dim3(768), 0, (hipStream_t)stream, a);
     KAIR_CHECK_LAUNCH();
   }
   return 0;
@@ -1738,9 +1738,9 @@ extern "C" int kair_swin_mlp_bwd(const void* dc, long lddc, const void* gd, long
       ncu <= 0)
     ncu = 256;
   const long grid = a.nTiles < ncu ? a.nTiles : ncu;
-  hipLaunchKernelGGL(swin_mlp_bwd_kernel, dim3((unsigned)grid), dim3(512), 0, (hipStream_t)stream, a);
+  KAIR_LAUNCH(swin_mlp_bwd_kernel, dim3((unsigned)grid), dim3(512), 0, (hipStream_t)stream, a);
   KAIR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(mlp_bwd_param_reduce, dim3((unsigned)((2 * C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws,
+  KAIR_LAUNCH(mlp_bwd_param_reduce, dim3((unsigned)((2 * C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws,
                      (int)grid, C, 192, dgamma, dbeta, dparam_acc);
   KAIR_CHECK_LAUNCH();
   return 0;

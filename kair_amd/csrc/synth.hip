@@ -200,11 +200,11 @@ extern "C" int kair_synth_sr(const float* pool, int C, int Hs, int Ws, const int
   const int rpb = (LS + nband - 1) / nband;
   const size_t lds = (size_t)rpb * Wmax * sizeof(float);
   if (lds <= 60 * 1024) {
-    hipLaunchKernelGGL(synth_sr_sep_kernel, dim3((unsigned)(B * C * nband)), dim3(256), lds, (hipStream_t)stream, pool, C,
+    KAIR_LAUNCH(synth_sr_sep_kernel, dim3((unsigned)(B * C * nband)), dim3(256), lds, (hipStream_t)stream, pool, C,
                        Hs, Ws, (const int4*)params, PS, sf, wh, ih, ww, iw, P, Wmax, nband, outH, outL);
   } else {
     const long total = (long)B * C * PS * PS + (long)B * C * LS * LS;
-    hipLaunchKernelGGL(synth_sr_kernel, dim3((unsigned)nblocks(total)), dim3(256), 0, (hipStream_t)stream, pool, C, Hs, Ws,
+    KAIR_LAUNCH(synth_sr_kernel, dim3((unsigned)nblocks(total)), dim3(256), 0, (hipStream_t)stream, pool, C, Hs, Ws,
                        (const int4*)params, B, PS, sf, wh, ih, ww, iw, P, outH, outL);
   }
   KAIR_CHECK_LAUNCH();
@@ -216,7 +216,7 @@ extern "C" int kair_synth_dn(const float* pool, int C, int Hs, int Ws, const int
   KAIR_CHECK_ARG(pool && params && outH && outL, "synth_dn: null pointer");
   KAIR_CHECK_ARG(C > 0 && B > 0 && PS > 0 && PS <= Hs && PS <= Ws, "synth_dn: bad sizes");
   const long total = (long)B * C * PS * PS;
-  hipLaunchKernelGGL(synth_dn_kernel, dim3((unsigned)nblocks(total)), dim3(256), 0, (hipStream_t)stream, pool, C, Hs, Ws,
+  KAIR_LAUNCH(synth_dn_kernel, dim3((unsigned)nblocks(total)), dim3(256), 0, (hipStream_t)stream, pool, C, Hs, Ws,
                      (const int4*)params, B, PS, sigma, seed, step, outH, outL);
   KAIR_CHECK_LAUNCH();
   return 0;

@@ -866,7 +866,7 @@ extern "C" int kair_conv3x3_narrow_fwd(const void* x, long ldx, int lo_off, cons
   a.mean = mean; a.range = img_range; a.NR = NR; a.resid = resid; a.out = out;
   a.B = B; a.H = H; a.W = W;
   // two workgroups per CU (72 KB LDS, <= 256 VGPRs each): one computes while the other waits on its rows
-  hipLaunchKernelGGL(conv3x3_narrow_fwd_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 2)), dim3(256), 0,
+  KAIR_LAUNCH(conv3x3_narrow_fwd_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 2)), dim3(256), 0,
                      (hipStream_t)stream, a);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -885,11 +885,11 @@ extern "C" int kair_conv3x3_narrow_dgrad(const void* dE, long lde, const float* 
                  "conv3x3_narrow_dgrad: output stride / PixelUnshuffle geometry");
   KAIR_CHECK_ARG(ldo % 4 == 0 && ((uintptr_t)out & 15) == 0 && (long)B * H * W < (1L << 31), "conv3x3_narrow_dgrad: alignment");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(narrow_dgrad_pack_kernel, dim3(16), dim3(256), 0, s, w, NR, (bf16*)ws);
+  KAIR_LAUNCH(narrow_dgrad_pack_kernel, dim3(16), dim3(256), 0, s, w, NR, (bf16*)ws);
   NarrowDgradArgs a;
   a.dE = (const bf16*)dE; a.lde = lde; a.w = (const bf16*)ws; a.out = out; a.odt = out_dtype; a.ldo = ldo; a.ps_r = ps_r;
   a.B = B; a.H = H; a.W = W;
-  hipLaunchKernelGGL(conv3x3_narrow_dgrad_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 4)), dim3(256), 0, s, a);
+  KAIR_LAUNCH(conv3x3_narrow_dgrad_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 4)), dim3(256), 0, s, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -911,10 +911,10 @@ extern "C" int kair_conv3x3_narrow_wgrad(const void* dE, long lde, const void* x
   a.part = ws;
   const int grid = grid_rows((long)B * (W / SEG) * H, 4);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(conv3x3_narrow_wgrad_kernel, dim3(grid), dim3(256), 0, s, a);
+  KAIR_LAUNCH(conv3x3_narrow_wgrad_kernel, dim3(grid), dim3(256), 0, s, a);
   KAIR_CHECK_LAUNCH();
   const int stride = NR * NF * 9 + NR;
-  hipLaunchKernelGGL(narrow_wgrad_finalize_kernel, dim3((stride + FIN_E - 1) / FIN_E), dim3(256), 0, s, ws, grid, NR, grad_w,
+  KAIR_LAUNCH(narrow_wgrad_finalize_kernel, dim3((stride + FIN_E - 1) / FIN_E), dim3(256), 0, s, ws, grid, NR, grad_w,
                      grad_b, accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -932,12 +932,12 @@ extern "C" int kair_conv3x3_narrow_fwd_x3(const float* x, long ldx, int ex, cons
                  "conv3x3_narrow_fwd_x3: x rows of >= 64 fp32 channels, 16-byte aligned; 16-byte aligned ws");
   KAIR_CHECK_ARG((long)B * H * W < (1L << 31), "conv3x3_narrow_fwd_x3: too many pixels");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(narrow_fwd_x3_pack_kernel, dim3(18 * 2 * 64 * 8 / 256), dim3(256), 0, s, w, NR, (f16*)ws);
+  KAIR_LAUNCH(narrow_fwd_x3_pack_kernel, dim3(18 * 2 * 64 * 8 / 256), dim3(256), 0, s, w, NR, (f16*)ws);
   NarrowFwdX3Args a;
   a.x = x; a.ldx = ldx; a.w = (const f16*)ws; a.bias = bias; a.mean = mean; a.range = img_range; a.NR = NR;
   a.resid = resid; a.out = out; a.B = B; a.H = H; a.W = W;
   a.sx = ldexpf(1.f, ex); a.oscale = ldexpf(1.f, -(ex + KAIR_X3_WEXP));
-  hipLaunchKernelGGL(conv3x3_narrow_fwd_x3_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 2)), dim3(256), 0, s, a);
+  KAIR_LAUNCH(conv3x3_narrow_fwd_x3_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 2)), dim3(256), 0, s, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -952,11 +952,11 @@ extern "C" int kair_conv3x3_narrow_dgrad_x3(const float* dE, long lde, int eg, c
                  "conv3x3_narrow_dgrad_x3: output stride / PixelUnshuffle geometry");
   KAIR_CHECK_ARG(ldo % 4 == 0 && ((uintptr_t)out & 15) == 0 && (long)B * H * W < (1L << 31), "conv3x3_narrow_dgrad_x3: alignment");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(narrow_dgrad_x3_pack_kernel, dim3(4 * 2 * 2 * 64 * 8 / 256), dim3(256), 0, s, w, NR, (f16*)ws);
+  KAIR_LAUNCH(narrow_dgrad_x3_pack_kernel, dim3(4 * 2 * 2 * 64 * 8 / 256), dim3(256), 0, s, w, NR, (f16*)ws);
   NarrowDgradX3Args a;
   a.dE = dE; a.lde = lde; a.w = (const f16*)ws; a.out = out; a.ldo = ldo; a.ps_r = ps_r; a.B = B; a.H = H; a.W = W;
   a.se = ldexpf(1.f, eg); a.oscale = ldexpf(1.f, -(eg + KAIR_X3_WEXP));
-  hipLaunchKernelGGL(conv3x3_narrow_dgrad_x3_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 4)), dim3(256), 0, s, a);
+  KAIR_LAUNCH(conv3x3_narrow_dgrad_x3_kernel, dim3(grid_rows((long)B * (W / SEG) * H, 4)), dim3(256), 0, s, a);
   KAIR_CHECK_LAUNCH();
   return 0;
 }
@@ -974,10 +974,10 @@ extern "C" int kair_conv3x3_narrow_wgrad_x3(const float* dE, long lde, int eg, c
   a.se = ldexpf(1.f, eg); a.sx = ldexpf(1.f, ex); a.oscale = ldexpf(1.f, -(eg + ex)); a.bscale = ldexpf(1.f, -eg);
   const int grid = grid_rows((long)B * (W / SEG) * H, 4);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(conv3x3_narrow_wgrad_x3_kernel, dim3(grid), dim3(256), 0, s, a);
+  KAIR_LAUNCH(conv3x3_narrow_wgrad_x3_kernel, dim3(grid), dim3(256), 0, s, a);
   KAIR_CHECK_LAUNCH();
   const int stride = NR * NF * 9 + NR;
-  hipLaunchKernelGGL(narrow_wgrad_finalize_kernel, dim3((stride + FIN_E - 1) / FIN_E), dim3(256), 0, s, ws, grid, NR, grad_w,
+  KAIR_LAUNCH(narrow_wgrad_finalize_kernel, dim3((stride + FIN_E - 1) / FIN_E), dim3(256), 0, s, ws, grid, NR, grad_w,
                      grad_b, accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;

@@ -861,10 +861,10 @@ extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* tab
   const long nb = (tasks + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(attn_fwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
+    KAIR_LAUNCH(attn_fwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
                        lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
   else
-    hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, table, (float*)O,
+    KAIR_LAUNCH(attn_fwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, table, (float*)O,
                        ldo, lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -896,7 +896,7 @@ extern "C" long kair_window_attn_bwd_ws(long nWin, int nh) {
 }
 
 int kair_attn_dtable_sum(const float* ws, long ngroups, int nh, float* dtable, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(attn_dtable_sum_kernel, dim3((nh * NBIN + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dtable,
+  KAIR_LAUNCH(attn_dtable_sum_kernel, dim3((nh * NBIN + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dtable,
                      accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -918,19 +918,19 @@ extern "C" int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo,
   const long nb = (ngroups * nh + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == KAIR_BF16 && nw == 2)
-    hipLaunchKernelGGL(attn_bwd_bf16_kernel<2>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
+    KAIR_LAUNCH(attn_bwd_bf16_kernel<2>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
                        (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw,
                        g_stamp, dqkv_rows);
   else if (dtype == KAIR_BF16)
-    hipLaunchKernelGGL(attn_bwd_bf16_kernel<4>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
+    KAIR_LAUNCH(attn_bwd_bf16_kernel<4>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
                        (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw,
                        g_stamp, dqkv_rows);
   else
-    hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
+    KAIR_LAUNCH(attn_bwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, (const float*)O,
                        ldo, (const float*)dO, lddo, table, lse, (float*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw);
   KAIR_CHECK_LAUNCH();
   if (!dtable) return 0;   // deferred: the per-group partials stay in ws for kair_attn_dtable_grouped
-  hipLaunchKernelGGL(attn_dtable_sum_kernel, dim3((nh * NBIN + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dtable,
+  KAIR_LAUNCH(attn_dtable_sum_kernel, dim3((nh * NBIN + 63) / 64), dim3(1024), 0, s, ws, ngroups, nh, dtable,
                      dtable_accumulate);
   KAIR_CHECK_LAUNCH();
   return 0;
@@ -963,7 +963,7 @@ extern "C" int kair_attn_dtable_grouped(const kair_attn_dtable_job* jobs, int nj
   }
   g.njobs = njobs;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(attn_dtable_grouped, dim3(b0), dim3(1024), 0, s, g);
+  KAIR_LAUNCH(attn_dtable_grouped, dim3(b0), dim3(1024), 0, s, g);
   KAIR_CHECK_LAUNCH();
   return 0;
 }

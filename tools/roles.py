@@ -1,5 +1,6 @@
 """Every libkair launch of one SwinIR classical x4 training step, by call site, with its kernel duration
-(bench.time_roles serial: the side-stream work in place, a HIP event pair around each launch).
+(bench.time_roles: dispatch-packet timestamps of every launch, as rocprofv3 --kernel-trace reports them;
+serial by default: the side-stream work in place).
 
     python tools/roles.py [B] [--in-step] [--dtype bf16|fp32|fp32x3]
 """
@@ -28,12 +29,15 @@ def main():
     for _ in range(3):
         tr.step(L, Hh)
     torch.cuda.synchronize()
-    roles = bench.time_roles(tr, serial="--in-step" not in sys.argv)
-    tot = sum(v["ms_total"] for v in roles.values())
-    print(f"B = {B}: {tot:.3f} ms of kernel time over {sum(v['launches'] for v in roles.values())} launches")
+    roles, kernels = bench.time_roles(tr, serial="--in-step" not in sys.argv)
+    tot = sum(v["ms_total"] for v in kernels.values())
+    print(f"B = {B}: {tot:.3f} ms of kernel time over {sum(v['launches'] for v in kernels.values())} launches")
     for k, v in sorted(roles.items(), key=lambda kv: -kv[1]["ms_total"]):
         gbs = f"{v['bytes'] / (v['ms'] * 1e-3) / 1e9:7.0f} GB/s" if v.get("bytes") else " " * 12
-        print(f"{v['ms_total']:8.3f} ms {v['launches']:4d}x {1e3 * v['ms']:8.1f} us {gbs}  {v['rocprof'][:40]:40s} {k}")
+        print(f"{v['ms_total']:8.3f} ms {v['launches']:4d}x {1e3 * v['ms']:8.1f} us {gbs}  {v['kernel'][:40]:40s} {k}")
+    print("per kernel:")
+    for v in sorted(kernels.values(), key=lambda v: -v["ms_total"]):
+        print(f"{v['ms_total']:8.3f} ms {v['launches']:4d}x {1e3 * v['ms']:8.1f} us  {v['kernel']}")
 
 
 if __name__ == "__main__":
