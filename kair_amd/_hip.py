@@ -446,11 +446,13 @@ def gemm_tn(A, B, ws, splits, M, N, K, compute):
     check(lib().kair_gemm_tn(ctypes.byref(A), ctypes.byref(B), ptr(ws), splits, M, N, K, compute, stream_ptr()), "gemm_tn")
 
 
-def wgrad_grouped_ws(shapes, M):
-    """Workspace floats of a kair_wgrad_grouped launch over linears of packed (N, K) shapes."""
+def wgrad_grouped_ws(shapes, M, x3=False):
+    """Workspace floats of a kair_wgrad_grouped launch over linears of packed (N, K) shapes (x3: fp16-pair jobs,
+    the fp32x3 TN ring's 192 x 192 tiles)."""
     arr = (WgradJob * len(shapes))()
     for i, (N, K) in enumerate(shapes):
         arr[i].N, arr[i].K = N, K
+        arr[i].A.dtype = F16 if x3 else BF16
     return lib().kair_wgrad_grouped_ws(arr, len(shapes), M)
 
 

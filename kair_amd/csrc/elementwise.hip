@@ -240,9 +240,72 @@ KAIR_DEV void pack_chunk(const float* __restrict__ src, bf16* __restrict__ dst, 
   *(bf16x8*)(dst + t0) = o;
 }
 
+// Chunked packing of the split pair forms (kinds 9, 17, 18, 19; x3 fp16 pairs of w 2^KAIR_X3_WEXP or bf16 hi / lo):
+// one thread makes 8 consecutive columns of one packed row -- its hi and lo halves, two 16-byte stores -- with 32-bit
+// index math and the row's output channel / tap resolved once (the per-element form re-derived both per element in
+// 64-bit divides, ~300 us for the classical x4 network's 47 M packed elements per step).  Row geometry: kind 9 rows
+// Np of 9 Kp (tap-major), 17 rows Np of Kp, 18 rows Kp of 9 Np (tap-major), 19 rows Kp of Np; a chunk never straddles
+// a tap (Kp / Np % 8 == 0, pack_pair_vec).
+__host__ __device__ inline bool pack_pair_vec(const kair_wmap& mp, int dt) {
+  if (dt != KAIR_F16 && dt != KAIR_BF16) return false;
+  const int Np = mp.nG * mp.nGp, Kp = mp.kG * mp.kGp;
+  if (mp.kind == 9 || mp.kind == 17) return Kp % 8 == 0;
+  if (mp.kind == 18 || mp.kind == 19) return Np % 8 == 0;
+  return false;
+}
+
+KAIR_DEV void pack_pair_chunk(const float* __restrict__ src, void* __restrict__ dst, int dt, const kair_wmap& mp, int u) {
+  const int Np = mp.nG * mp.nGp, Kp = mp.kG * mp.kGp;
+  const bool rows_n = mp.kind == 9 || mp.kind == 17;   // rows are output channels (else input channels)
+  const int rowlen = mp.kind == 9 ? 9 * Kp : mp.kind == 17 ? Kp : mp.kind == 18 ? 9 * Np : Np;
+  const int rl64 = (rowlen + 63) / 64 * 64, cpr = rl64 / 8;
+  const int row = u / cpr, k0 = (u - row * cpr) * 8;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  if (k0 < rowlen) {
+    const int rr = rows_n ? nperm_fwd(mp, unpad(row, mp.nG, mp.nGr, mp.nGp)) : unpad(row, mp.kG, mp.kGr, mp.kGp);
+    const int seg = (mp.kind == 9) ? Kp : (mp.kind == 18) ? Np : rowlen;   // tap-major forms: one tap per segment
+    const int tap = k0 / seg, c0 = k0 - tap * seg;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      int n, k;
+      if (rows_n) { n = rr; k = unpad(c, mp.kG, mp.kGr, mp.kGp); }
+      else { n = nperm_fwd(mp, unpad(c, mp.nG, mp.nGr, mp.nGp)); k = rr; }
+      if (n < 0 || k < 0) continue;
+      if (mp.kind == 9) v[j] = src[((long)n * mp.K + k % mp.K) * 9 + tap];   // % K: tied in-dim copies
+      else if (mp.kind == 18) v[j] = src[((long)n * mp.K + k) * 9 + tap];
+      else v[j] = src[(long)n * mp.K + k];
+    }
+  }
+  const long o = (long)row * 2 * rl64 + ((k0 >> 6) << 7) + (k0 & 63);
+  if (dt == KAIR_F16) {
+    f16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float w = ldexpf(v[j], KAIR_X3_WEXP);
+      hi[j] = (f16)w;
+      lo[j] = (f16)(w - (float)hi[j]);
+    }
+    *(f16x8*)((f16*)dst + o) = hi;
+    *(f16x8*)((f16*)dst + o + 64) = lo;
+  } else {
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      hi[j] = (bf16)v[j];
+      lo[j] = (bf16)(v[j] - (float)hi[j]);
+    }
+    *(bf16x8*)((bf16*)dst + o) = hi;
+    *(bf16x8*)((bf16*)dst + o + 64) = lo;
+  }
+}
+
 // All packs of a network in one launch: table = kair_pack_job[njobs] followed by the first block
 // of every job (long[njobs + 1]); each block finds its job by binary search (uniform, scalar loads).
-// A chunked job (pack_vec) has total / 8 work items, any other job one per packed element.
+// A chunked job (pack_vec) has total / 8 work items, a pair-chunked one (pack_pair_vec) total / 16, any other job
+// one per packed element.
 __global__ __launch_bounds__(256) void pack_batched_kernel(const kair_pack_job* __restrict__ jobs, int njobs,
                                                            const long* __restrict__ first) {
   const long bid = blockIdx.x;
@@ -256,6 +319,8 @@ __global__ __launch_bounds__(256) void pack_batched_kernel(const kair_pack_job* 
   const long t = (bid - first[lo]) * 256 + threadIdx.x;
   if (pack_vec(j.map, j.dst_dtype)) {
     if (t < j.total / 8) pack_chunk(j.src, (bf16*)j.dst, j.map, t);
+  } else if (pack_pair_vec(j.map, j.dst_dtype)) {
+    if (t < j.total / 16) pack_pair_chunk(j.src, j.dst, j.dst_dtype, j.map, (int)t);
   } else if (t < j.total) {
     pack_element(j.src, j.dst, j.dst_dtype, j.map, t);
   }
@@ -852,7 +917,9 @@ extern "C" long kair_pack_table_build(kair_pack_job* jobs, int njobs, void* tabl
     if (rc) { free(host); return rc; }
     jobs[i].total = total;
     first[i] = nb;
-    const long items = pack_vec(jobs[i].map, jobs[i].dst_dtype) ? total / 8 : total;
+    const long items = pack_vec(jobs[i].map, jobs[i].dst_dtype) ? total / 8
+                       : pack_pair_vec(jobs[i].map, jobs[i].dst_dtype) ? total / 16 : total;
+    if (items >= (1L << 31)) { free(host); return kair_set_error(KAIR_ERR_ARG, "pack_table_build: job %d too large", i); }
     nb += (items + 255) / 256;
   }
   first[njobs] = nb;

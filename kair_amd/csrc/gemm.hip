@@ -1817,9 +1817,18 @@ static int grouped_splits_capped(long M, long ntiles, int max_ctas) {
   return s;
 }
 
+// fp32x3 pair jobs (gemm_x3.hip): 192 x 192 tiles
+static long grouped_tiles_x3(const kair_wgrad_job* jobs, int njobs) {
+  long t = 0;
+  for (int i = 0; i < njobs; ++i) t += (long)((jobs[i].N + 191) / 192) * ((jobs[i].K + 191) / 192);
+  return t;
+}
+int kair_wgrad_grouped_x3(const kair_wgrad_job* jobs, int njobs, long M, float* ws, int splits, void* stream);
+
 extern "C" long kair_wgrad_grouped_ws(const kair_wgrad_job* jobs, int njobs, long M) {
   if (!jobs || njobs <= 0 || M <= 0) return 0;
-  const int splits = grouped_splits(M, grouped_tiles(jobs, njobs));
+  const bool x3 = jobs[0].A.dtype == KAIR_F16;
+  const int splits = grouped_splits(M, x3 ? grouped_tiles_x3(jobs, njobs) : grouped_tiles(jobs, njobs));
   long nk = 0;
   for (int i = 0; i < njobs; ++i) nk += (long)jobs[i].N * jobs[i].K;
   return (long)splits * nk;
@@ -1837,6 +1846,14 @@ extern "C" int kair_wgrad_grouped_ex(const kair_wgrad_job* jobs, int njobs, long
                  "wgrad_grouped: 1..%d jobs, M > 0 and a workspace", KAIR_WG_MAX);
   KAIR_CHECK_ARG(((uintptr_t)ws % 16) == 0, "wgrad_grouped: workspace not 16-byte aligned");
   int rc;
+  if (jobs[0].A.dtype == KAIR_F16) {   // fp32x3: fp16-pair operands on the x3 TN ring
+    for (int i = 0; i < njobs; ++i) {
+      if ((rc = kair_check_operand(&jobs[i].A, "wgrad_grouped A"))) return rc;
+      if ((rc = kair_check_operand(&jobs[i].B, "wgrad_grouped B"))) return rc;
+    }
+    return kair_wgrad_grouped_x3(jobs, njobs, M, ws, grouped_splits_capped(M, grouped_tiles_x3(jobs, njobs), max_ctas),
+                                 stream);
+  }
   TnGroup g;
   FinGroup f;
   memset(&g, 0, sizeof(g));

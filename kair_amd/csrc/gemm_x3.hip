@@ -13,6 +13,8 @@
 // Operands: fp32 (split at the LDS commit, read from HBM once) or fp16 hi planes with their lo planes
 // (kair_operand.lo_ptr).  LDS holds hi and lo planes of both operands; 32-deep k-steps (NT) / 32-row
 // reduction steps (TN), double-buffered by register staging as the bf16 kernels (gemm.hip).
+#include <string.h>
+
 #include <type_traits>
 
 #include "gemm_common.h"
@@ -842,17 +844,15 @@ enum { BT_ROWS = 0, BT_TAP = 1 };
 // the two bank halves: conflict-free.
 KAIR_DEV int xt_swz_pair(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
 
+// one CTA's (tile, split) of the TN ring: the launch forms below (one product, or a group of them) pick its operands
 template <int BT, bool PR>
-__global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
-                                                         int rps, float acc_scale) {
+KAIR_DEV void tn_x3_body(const Op& A, const Op& B, float* ws, int M, int N, int K, int tilesK, int tile, int split, int rps,
+                         float acc_scale, char* smem) {
   static_assert(!PR || BT == BT_ROWS, "fp16-pair operands: row operands only");
   constexpr int ES = PR ? 2 : 4;   // operand element bytes
-  __shared__ __attribute__((aligned(16))) char smem[XT_NS * XT_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wk = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = bid % ntiles, split = bid / ntiles;
   const int n0 = (tile / tilesK) * 192, k0 = (tile % tilesK) * 192;
   const int mbeg = split * rps;
   const int mend = mbeg + rps < M ? mbeg + rps : M;
@@ -1060,6 +1060,48 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws,
     }
 }
 
+template <int BT, bool PR>
+__global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring(Op A, Op B, float* ws, int M, int N, int K, int tilesK, int ntiles,
+                                                         int rps, float acc_scale) {
+  __shared__ __attribute__((aligned(16))) char smem[XT_NS * XT_STAGE];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  tn_x3_body<BT, PR>(A, B, ws, M, N, K, tilesK, bid % ntiles, bid / ntiles, rps, acc_scale, smem);
+}
+
+// Grouped form (kair_wgrad_grouped with fp16-pair operands): the weight gradients of several Swin linears -- an
+// RSTB's, queued for the side stream -- in ONE launch.  Every job is a pair-row product P = A^T B over the same M rows
+// in `splits` row ranges; CTA -> (split, global tile), the job found by a scalar scan of the tile offsets.  One launch
+// instead of one per linear: the partial planes are (CTAs x one tile) for the whole group rather than per linear (an
+// RSTB's 24 linears at B = 32: 28 MB instead of 24 x 28 MB written and read back by the finalize), and small batches
+// get long enough workgroups.  The job table is the kernel argument (captured by value).
+struct TnX3Job {
+  const void* ah; const void* al; const void* bh; const void* bl;   // hi / lo planes of A (gradient) and B (activation)
+  float* ws;                                                        // this job's [splits][N][K] partial planes
+  long lda, ldb;
+  int N, K, tilesK, tile0;
+  float acc_scale;
+};
+struct TnX3Group {
+  TnX3Job j[KAIR_WG_MAX];
+  int njobs, ntiles, M, rps;
+};
+
+__global__ __launch_bounds__(512, 1) void gemm_tn_x3_ring_grouped(const TnX3Group g) {
+  __shared__ __attribute__((aligned(16))) char smem[XT_NS * XT_STAGE];
+  const int cta = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = cta % g.ntiles, split = cta / g.ntiles;
+  int ji = 0;
+  for (int i = 1; i < g.njobs; ++i)
+    if (g.j[i].tile0 <= tile) ji = i;
+  ji = __builtin_amdgcn_readfirstlane(ji);
+  const TnX3Job& jb = g.j[ji];
+  Op a{}, b{};   // the fields the pair-row body reads: planes, strides, no window map / ones column
+  a.ptr = jb.ah; a.lo_ptr = jb.al; a.ld = jb.lda; a.ones_col = -1; a.x3s = 1.f;
+  b.ptr = jb.bh; b.lo_ptr = jb.bl; b.ld = jb.ldb; b.ones_col = -1; b.x3s = 1.f;
+  tn_x3_body<BT_ROWS, true>(a, b, jb.ws, g.M, jb.N, jb.K, jb.tilesK, tile - jb.tile0, split, g.rps, jb.acc_scale, smem);
+}
+
+
 int g_x3_cus = 0;
 int x3_cus() {
   if (g_x3_cus == 0) {
@@ -1250,6 +1292,45 @@ int x3_operand_ok(const kair_operand* o, const char* what) {
 }
 
 }  // namespace
+
+// every job fp16 pairs in rows, 16-byte aligned 8-column units, no window map (tn_x3_ring_ok's pair branch)
+int kair_wgrad_grouped_x3(const kair_wgrad_job* jobs, int njobs, long M, float* ws, int splits, void* stream) {
+  TnX3Group g;
+  FinGroup f;
+  memset(&g, 0, sizeof(g));
+  memset(&f, 0, sizeof(f));
+  long rps = (M + splits - 1) / splits;
+  rps = (rps + XT_RB - 1) / XT_RB * XT_RB;
+  long tile0 = 0, off = 0, blk0 = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const kair_wgrad_job& J = jobs[i];
+    KAIR_CHECK_ARG(J.A.dtype == KAIR_F16 && J.B.dtype == KAIR_F16 && tn_x3_ring_ok(&J.A, &J.B, J.N, J.K) &&
+                       J.A.win_ws == 0 && J.B.win_ws == 0,
+                   "wgrad_grouped x3: job %d: fp16-pair row operands (16-byte aligned, N, K %% 8, no window map)", i);
+    KAIR_CHECK_ARG(J.grad && J.map.kind == 0 && (long)J.map.nG * J.map.nGp == J.N && (long)J.map.kG * J.map.kGp == J.K,
+                   "wgrad_grouped x3: job %d needs a linear map whose packed dims are (N, K)", i);
+    KAIR_CHECK_ARG(!J.bias_grad || (J.ones_col >= 0 && J.ones_col < J.K), "wgrad_grouped x3: job %d bias needs ones_col", i);
+    const int tilesK = (J.K + 191) / 192;
+    TnX3Job& t = g.j[i];
+    t.ah = J.A.ptr; t.al = J.A.lo_ptr; t.bh = J.B.ptr; t.bl = J.B.lo_ptr;
+    t.ws = ws + off;
+    t.lda = J.A.ld; t.ldb = J.B.ld;
+    t.N = J.N; t.K = J.K; t.tilesK = tilesK; t.tile0 = (int)tile0;
+    t.acc_scale = ldexpf(1.f, -(J.A.x3_exp + J.B.x3_exp));
+    tile0 += (long)((J.N + 191) / 192) * tilesK;
+    FinJob& q = f.j[i];
+    q.part = ws + off; q.grad = J.grad; q.bias = J.bias_grad; q.mp = J.map; q.ones_col = J.bias_grad ? J.ones_col : -1;
+    q.Kt = J.K; q.plane = (long)J.N * J.K; q.blk0 = blk0;
+    blk0 += ((long)J.N * J.K / 4 + 63) / 64;
+    off += (long)splits * J.N * J.K;
+  }
+  g.njobs = njobs; g.ntiles = (int)tile0; g.M = (int)M; g.rps = (int)rps;
+  f.njobs = njobs; f.splits = splits; f.nblocks = blk0;
+  hipStream_t s = (hipStream_t)stream;
+  KAIR_LAUNCH(gemm_tn_x3_ring_grouped, dim3((unsigned)(tile0 * splits)), dim3(512), 0, s, g);
+  KAIR_CHECK_LAUNCH();
+  return kair_launch_finalize_grouped(f, s);
+}
 
 // copy the NT ring's phase stamps to the host and clear them (perf investigation only; zeros in release builds)
 extern "C" int kair_debug_x3_stamps(unsigned long long* host, int n) {

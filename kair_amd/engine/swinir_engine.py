@@ -17,6 +17,7 @@ step can be captured in a HIP graph (kair_amd/engine/trainer.py).
 """
 import contextlib
 import math
+import os
 import weakref
 
 import torch
@@ -427,6 +428,9 @@ class SwinIREngine:
         # B = 32 639 -> 650 patches/s against uncapped (profiles/r06_side_ctas_ab.txt)
         if side_ctas is None:
             side_ctas = 192 if self.x3 else 0
+        # fp32x3: an RSTB's deferred block weight gradients as ONE grouped TN-ring launch + one grouped finalize
+        # (kair_wgrad_grouped with fp16-pair jobs) instead of a launch pair per linear (KAIR_X3_GROUPED=0: A/B)
+        self.x3_grouped = self.x3_side and self.side_stream and os.environ.get("KAIR_X3_GROUPED", "1") != "0"
         self.side_ctas = int(side_ctas)
         # '1conv' weight gradients on the tap-per-tile ring (bf16 copies of G and the conv input)
         self.conv_tap = self.tdt == torch.bfloat16 and self.Cp == 192 and self.C % 4 == 0
@@ -674,11 +678,12 @@ class SwinIREngine:
 
     def _max_wgrad_ws(self, M, P):
         ws = max(H.wgrad_splits(m, n, k) * n * k for m, n, k in self._wgrad_shapes(M, P))
-        if self.grouped_wgrad:
+        if self.grouped_wgrad or self.x3_grouped:
             Cp, Hdp, nh = self.Cp, self.Hdp, self.nh
             depth = max(len(blks) for blks, _ in self.rstb)
             shapes = [(Cp, Hdp), (Hdp, Cp), (Cp, nh * 32), (3 * nh * 32, Cp)] * depth
-            ws = max(ws, H.wgrad_grouped_ws(shapes, M))
+            for i in range(0, len(shapes), H.WgradGroup.WG_MAX):
+                ws = max(ws, H.wgrad_grouped_ws(shapes[i:i + H.WgradGroup.WG_MAX], M, x3=self.x3))
         return ws
 
     # ------------------------------------------------------------------------------------
@@ -1244,7 +1249,12 @@ class SwinIREngine:
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             if self._wg_pending:
                 jobs, self._wg_pending = self._wg_pending, []
-                if self.x3:   # one split-fp16 TN ring + finalize per linear, in queue order
+                if self.x3:   # fp16-pair operands at the step's exponents (gradient, activation)
+                    for A, Bop, *_ in jobs:
+                        A.x3_exp, Bop.x3_exp = P["e_g"], self.X3_AEXP
+                if self.x3 and not (self.x3_grouped and all(
+                        A.dtype == H.F16 and Bop.dtype == H.F16 and A.win_ws == 0 and Bop.win_ws == 0
+                        for A, Bop, *_ in jobs)):   # one split-fp16 TN ring + finalize per linear, in queue order
                     for A, Bop, N, K, m, g_w, g_b, oc in jobs:
                         self._wgrad(P, A, Bop, P["M"], N, K, m, g_w, g_b, oc, ws=ws, max_ctas=cap)
                 else:

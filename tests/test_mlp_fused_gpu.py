@@ -101,3 +101,35 @@ def test_batched_pack_matches_elementwise(N, K, n_grp, k_grp):
     torch.cuda.synchronize()
     for (_, dst, m), ref in zip(jobs, refs):
         assert torch.equal(dst, ref), m.kind
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N, K, n_grp, k_grp", [
+    (180, 180, (1, 180, 192), (6, 30, 32)),    # Swin proj / RSTB conv: padded groups
+    (540, 180, (1, 540, 576), (1, 180, 192)),  # qkv
+    (64, 180, (1, 64, 64), (1, 180, 192)),     # conv_before_upsample-like widths
+])
+def test_batched_pair_pack_matches_elementwise(dt, N, K, n_grp, k_grp):
+    """kair_pack_weights on the split pair forms (kinds 9 / 17 / 18 / 19: the fp32x3 engine's fp16 pairs of w 2^12,
+    or bf16 hi / lo; 8 columns of one packed row per thread) == kair_pack_weight (one thread per packed element),
+    bit for bit."""
+    g = torch.Generator().manual_seed(N + 3 * K)
+    w_lin = torch.randn(N, K, generator=g).to(dev)
+    w_conv = torch.randn(N, K, 3, 3, generator=g).to(dev)
+    Np, Kp = n_grp[0] * n_grp[2], k_grp[0] * k_grp[2]
+    r64 = lambda n: 2 * ((n + 63) // 64) * 64
+    shapes = {9: (Np, r64(9 * Kp)), 17: (Np, r64(Kp)), 18: (Kp, r64(9 * Np)), 19: (Kp, r64(Np))}
+    jobs, refs = [], []
+    for kind, shape in shapes.items():
+        w = w_conv if kind in (9, 18) else w_lin
+        m = H.wmap(kind, N, K, n_grp, k_grp)
+        ref = torch.empty(shape, device=dev, dtype=dt)
+        H.pack_weight(w, ref, m)
+        dst = torch.full(shape, 3.0, device=dev, dtype=dt)
+        jobs.append((w, dst, m))
+        refs.append(ref)
+    t = H.PackTable(jobs)
+    t.run()
+    torch.cuda.synchronize()
+    for (_, dst, m), ref in zip(jobs, refs):
+        assert torch.equal(dst, ref), m.kind

@@ -138,6 +138,39 @@ def test_gemm_tn_x3_ring_pairs(N, K):
     assert rel(ws.sum(0), ref) < 2e-6
 
 
+@pytest.mark.parametrize("M, max_ctas", [(3001, 192), (9216, 192), (9216, 0)])
+def test_wgrad_grouped_x3_pairs(M, max_ctas):
+    """kair_wgrad_grouped on fp16-pair jobs (the fp32x3 engine's per-RSTB grouped block weight gradients: one TN-ring
+    launch over a Swin block's qkv / proj / fc1 / fc2 shapes + one grouped finalize into the reference-layout
+    gradients and biases) against float64, the side stream's workgroup cap and ragged row splits included."""
+    g = torch.Generator().manual_seed(23)
+    C, Cp, Hd, Hdp = 180, 192, 360, 384
+    shapes = [(Cp, Hdp, C, Hd), (Hdp, Cp, Hd, C), (Cp, Cp, C, C), (576, Cp, 540, C)]   # (Np, Kp, N, K): fc2 fc1 proj qkv
+    jobs, refs, keep = [], [], []
+    for Np, Kp, N, K in shapes:
+        dy = torch.zeros(M, Np)
+        dy[:, :N] = torch.randn(M, N, generator=g) * 1e-5
+        x = torch.zeros(M, Kp)
+        x[:, :K] = torch.randn(M, K, generator=g)
+        x[:, K] = 1.0   # the bias ones column, in the data
+        ap, bp = hilo(dy.to(dev), 20), hilo(x.to(dev), 4)
+        A = H.with_lo(H.rows(ap[0]), ap[1])
+        A.x3_exp = 20
+        Bop = H.with_lo(H.rows(bp[0], ones_col=K, ones_in_data=True), bp[1])
+        Bop.x3_exp = 4
+        m = H.wmap(0, N, K, (1, N, Np), (1, K, Kp))
+        gw, gb = torch.full((N, K), 7.0, device=dev), torch.full((N,), 7.0, device=dev)
+        jobs.append((A, Bop, Np, Kp, m, gw, gb, K))
+        keep += [ap, bp]
+        refs.append((gw, gb, dy[:, :N].double().T @ x[:, :K].double(), dy[:, :N].double().sum(0)))
+    grp = H.WgradGroup(jobs, M)
+    ws = torch.empty(grp.ws_floats, device=dev)
+    grp.run(ws, max_ctas=max_ctas)
+    torch.cuda.synchronize()
+    for gw, gb, rw, rb in refs:
+        assert rel(gw, rw) < 2e-6 and rel(gb, rb) < 2e-6
+
+
 def test_layernorm_x3_pair_forms():
     """kair_layernorm_fwd_x3 (window-ordered fp16-pair output with the ones column at 2^e), and the pair forms of
     the GEMM-operand copies (kair_copy_desc dtype F16: kair_layernorm_bwd's copy, kair_row_copy) -- (hi + lo) 2^-e
