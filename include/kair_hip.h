@@ -229,7 +229,10 @@ int kair_wgrad_finalize(const float* partial, int splits, const kair_wmap* map, 
  * ones_col_i of that sum (B_i holds 1.0 there: ones_in_data).  A: ROWS or QKVBLK (one q/k/v
  * geometry per group); B: ROWS.  Up to 24 jobs sharing M rows; ws: kair_wgrad_grouped_ws() floats.
  * Replaces the weight-gradient half of nn.Linear backward (network_swinir.py:19-20, 105, 107) for
- * every block of an RSTB at once; the sums are in fixed order (deterministic). */
+ * every block of an RSTB at once; the sums are in fixed order (deterministic).
+ * fp32x3 (round 6): jobs whose A and B are fp16 pairs (dtype KAIR_F16 + lo_ptr, x3_exp each; ROWS, no window map,
+ * 16-byte aligned, N and K % 8) run on the split-fp16 TN ring (192 x 192 tiles, three fp16-pair products per
+ * multiply, accumulator x 2^-(eA + eB)) -- one launch for all jobs, then the same grouped finalize. */
 typedef struct {
   kair_operand A, B;
   int N, K;

@@ -423,14 +423,16 @@ class SwinIREngine:
         # grouped launch, the attention backward 80 -> 340 us behind the conv weight gradient).  Measured
         # (profiles/r03_side_ctas_ab.txt): a cap makes the side work critical at B=32 (48 CTAs: 1080 -> 808
         # patches/s) and gains ~2% at B=4 (96 CTAs) -- so uncapped by default.
-        # fp32x3: the deferred weight gradients (one TN ring + finalize per block linear) capped at 192 workgroups: fewer
-        # row splits (the partial planes the finalize re-reads shrink by 1 / 4) and 64 CUs left to the main chain --
-        # B = 32 639 -> 650 patches/s against uncapped (profiles/r06_side_ctas_ab.txt)
+        # fp32x3: the deferred weight gradients capped at 192 workgroups (B = 32 639 -> 650 patches/s against uncapped
+        # with one launch per linear, profiles/r06_side_ctas_ab.txt); with the grouped launch (one per RSTB) 96 at the
+        # small per-GPU batches of a multi-GPU run (M < 36,864 rows, B < 16: B = 4 333 -> 344, B = 8 429 -> 443; B = 16
+        # and 32 unchanged, profiles/r06_side_ctas_grouped_ab.txt) -- the x3_side_cap rule
+        self.side_ctas_auto = side_ctas is None and self.x3
         if side_ctas is None:
             side_ctas = 192 if self.x3 else 0
         # fp32x3: an RSTB's deferred block weight gradients as ONE grouped TN-ring launch + one grouped finalize
         # (kair_wgrad_grouped with fp16-pair jobs) instead of a launch pair per linear (KAIR_X3_GROUPED=0: A/B)
-        self.x3_grouped = self.x3_side and self.side_stream and os.environ.get("KAIR_X3_GROUPED", "1") != "0"
+        self.x3_grouped = self.x3_side and os.environ.get("KAIR_X3_GROUPED", "1") != "0"
         self.side_ctas = int(side_ctas)
         # '1conv' weight gradients on the tap-per-tile ring (bf16 copies of G and the conv input)
         self.conv_tap = self.tdt == torch.bfloat16 and self.Cp == 192 and self.C % 4 == 0
@@ -1230,7 +1232,7 @@ class SwinIREngine:
     def _wg(self, P, A, Bop, N, K, lin, grads, ones_col):
         """One block linear's weight gradient: queued for the RSTB's grouped launch, or issued now."""
         g_w, g_b = grads[lin.w], grads[lin.b]
-        if self.grouped_wgrad or (self.x3_side and self.side_stream):
+        if self.grouped_wgrad or (self.x3_side and (self.side_stream or self.x3_grouped)):
             self._wg_pending.append((A, Bop, N, K, lin.map, g_w, g_b, ones_col))
         else:
             self._wgrad(P, A, Bop, P["M"], N, K, lin.map, g_w, g_b, ones_col)
@@ -1245,7 +1247,7 @@ class SwinIREngine:
             side = self._side
             side.wait_stream(torch.cuda.current_stream())
         ws = P["wg_ws2"] if side is not None else P["wg_ws"]
-        cap = self.side_ctas if side is not None else 0
+        cap = (self.side_ctas if not self.side_ctas_auto else (96 if P["M"] < 36864 else 192)) if side is not None else 0
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             if self._wg_pending:
                 jobs, self._wg_pending = self._wg_pending, []

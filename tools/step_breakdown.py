@@ -1,40 +1,49 @@
-"""Per-step kernel time breakdown from a rocprofv3 kernel trace of bench.py.
+"""Where a training step's GPU time goes, from a rocprofv3 --kernel-trace CSV of bench.py.
 
-    python tools/step_breakdown.py gpurun_out/qprof/run_kernel_trace.csv [step_index]
-A step is delimited by consecutive first-block launches of the fused attention kernel (or the first
-LayerNorm when the fused path is off)."""
+    python tools/step_breakdown.py KERNEL_TRACE_CSV [TOP]
+
+Takes the middle of the run (40 %..85 % of the dispatches: graph-replayed timed steps), counts steps by the Adam
+kernel, and prints per step: the span, the GPU-busy union of all kernels, the summed kernel time, and the kernels by
+summed duration (launches per step, mean duration).
+"""
 import collections
 import csv
-import re
 import sys
 
 
-def short(n):
-    n = re.sub(r"\(anonymous namespace\)::", "", n)
-    n = re.sub(r"\((.*)", "", n)
-    return n[:70]
+def union(iv):
+    iv = sorted(iv)
+    tot, (cs, ce) = 0, iv[0]
+    for s, e in iv[1:]:
+        if s > ce:
+            tot += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    return tot + ce - cs
 
 
-def main(path, k=5):
-    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    names = [r["Kernel_Name"] for r in rows]
-    key = "swin_attn_fwd" if any("swin_attn_fwd" in n for n in names) else "layernorm_fwd"
-    idx = [i for i, n in enumerate(names) if key in n]
-    per = 36 if key == "swin_attn_fwd" else None
-    starts = idx[::per] if per else idx
-    a, b = starts[k], starts[k + 1]
-    t = collections.defaultdict(float)
-    c = collections.Counter()
-    for r in rows[a:b]:
-        s = short(r["Kernel_Name"])
-        t[s] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        c[s] += 1
-    span = (int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
-    tot = sum(t.values())
-    print(f"step span {span / 1e3:.3f} ms, kernel time {tot / 1e3:.3f} ms, {b - a} launches")
-    for s, v in sorted(t.items(), key=lambda x: -x[1]):
-        print(f"{v / 1e3:8.3f} ms {100 * v / tot:5.1f}% {c[s]:4d}x {v / c[s]:8.1f} us  {s}")
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    top = int(sys.argv[2]) if len(sys.argv) > 2 else 25
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    w = rows[int(len(rows) * 0.40):int(len(rows) * 0.85)]
+    steps = sum(1 for r in w if "adam_ema" in r["Kernel_Name"])
+    t0 = int(w[0]["Start_Timestamp"])
+    t1 = max(int(r["End_Timestamp"]) for r in w)
+    iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in w]
+    busy = union(iv)
+    ksum = sum(e - s for s, e in iv)
+    print(f"{steps} steps: {(t1 - t0) / steps / 1e3:.1f} us span per step, GPU busy {busy / steps / 1e3:.1f} us, "
+          f"kernel time {ksum / steps / 1e3:.1f} us, {len(w) / steps:.1f} launches")
+    per = collections.defaultdict(lambda: [0, 0])
+    for r in w:
+        d = per[r["Kernel_Name"]]
+        d[0] += 1
+        d[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    for name, (n, ns) in sorted(per.items(), key=lambda kv: -kv[1][1])[:top]:
+        print(f"{ns / steps / 1e3:9.1f} us/step {n / steps:6.1f}x {ns / n / 1e3:8.2f} us  {name[:110]}")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 5)
+    main()
