@@ -391,7 +391,7 @@ enum { XG_MUL = 4, XG_LEAKY = 2 };                                 // kair_epilo
 // wave waits for its own pieces of chunk t with a counted vmcnt (the DMA, epilogue loads and stores it issued
 // after them) before the barrier that opens interval t.
 template <typename TA, int AM, int EM, int EX, int ACT, int GK, int BN, int BM = XR_BM>
-__global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM) {
+__global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int K, int tilesN, int tilesM, int m_base) {
   constexpr int NA = XR<BN>::NA, RN = XR<BN>::RN, NP = RN / 2, BI = XR<BN>::BI, BSTAGE = XR<BN>::BSTAGE, WC = BN / 2;
   // BM = 128 rows per tile (a wave multiplies 2 row fragments) or 64 (1: twice the tiles for small M -- the B = 4 per-GPU
   // shape of the 8-GPU run has 72 128-row tiles per N-tile for 256 CUs); RI row fragments / A DMA instructions per wave
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
 #pragma unroll
     for (int ii = 0; ii < RI; ++ii) {
       const int r = (wave * RI + ii) * 8 + (lane >> 3);
-      const int m = mt * BM + r;
+      const int m = m_base + mt * BM + r;
       au[ii] = q8 ^ (r & 7);
       aok[ii] = m < (int)A.M;
       const int mm = aok[ii] ? m : 0;
@@ -613,7 +613,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
     int rowv[RI];
     long roff[RI];   // the shuffled forms' row part of the store offset
     bool okm[RI];
-    const int m0 = (mt0 + ct * mstride) * BM + grp * (BM / 2) + wm * (BM / 4) + fr;
+    const int m0 = m_base + (mt0 + ct * mstride) * BM + grp * (BM / 2) + wm * (BM / 4) + fr;
 #pragma unroll
     for (int i = 0; i < RI; ++i) {
       const int m = m0 + i * 16;
@@ -1210,17 +1210,18 @@ bool nt_x3_ring_ok(const kair_operand* A, const kair_operand* B, const kair_epil
          (A->ld == 0 ? A->im_C : A->ld) % 4 == 0;
 }
 
+// rows [m_base, M) of the product
 template <typename TA, int AM, int BN, int BM>
-int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int K, hipStream_t s) {
+int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int K, hipStream_t s, long m_base = 0) {
   const int tilesN = N / BN;
-  const int tilesM = (int)((M + BM - 1) / BM);
+  const int tilesM = (int)((M - m_base + BM - 1) / BM);
   int per = x3_cus() / tilesN;
   if (per < 1) per = 1;
   const int rounds = (tilesM + per - 1) / per;
   per = (tilesM + rounds - 1) / rounds;   // the same makespan on as few CUs as it needs
   const dim3 g(per * tilesN), bl(512);
 #define XR_LAUNCH(EM, EX, ACT, GK) \
-  KAIR_LAUNCH((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN, BM>), g, bl, 0, s, a, b, e, K, tilesN, tilesM)
+  KAIR_LAUNCH((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN, BM>), g, bl, 0, s, a, b, e, K, tilesN, tilesM, (int)m_base)
   if constexpr (BN == 192) {   // the Swin linears and the 192-channel convs: every epilogue form
     if (e.omode == KAIR_OUT_QKVBLK) XR_LAUNCH(XE_QKV, EX_NONE, XA_NONE, 0);
     else if (e.odt == KAIR_F16 && e.gate) XR_LAUNCH(XE_ROWS_PAIR, EX_GATE_F32, XA_NONE, XG_MUL);
@@ -1251,10 +1252,18 @@ int nt_x3_ring_dispatch(const Op& a, const Op& b, const Epi& e, long M, int N, i
     case 64: return launch_nt_x3_ring<TA, AM, 64, XR_BM>(a, b, e, M, N, K, s);
     case 128: return launch_nt_x3_ring<TA, AM, 128, XR_BM>(a, b, e, M, N, K, s);
     default:
-      // 64-row tiles when the 128-row ones leave CUs idle (fewer tiles than CUs: the small per-GPU batches of a
-      // multi-GPU run, e.g. B = 4 -> M = 9,216: 72 tiles per N-tile); at B = 32 (576 tiles, 3 rounds on 192 CUs) the
-      // 64-row tiles measured slower on every block GEMM (profiles/r06_bm64_ab.txt)
-      if ((M + XR_BM - 1) / XR_BM * (N / 192) < x3_cus()) return launch_nt_x3_ring<TA, AM, 192, 64>(a, b, e, M, N, K, s);
+      // 64-row tiles when they finish sooner: rounds of tiles per CU (x3_cus / N-tiles CTAs per N-tile) at a 64-row
+      // tile's cost of 0.66 of a 128-row one (profiles/r06_bm64_ab.txt: the same rows take 1.31x as long in 64-row
+      // tiles).  B = 4 (M = 9,216): N = 192 -> 64 rows (1 round of 144 tiles instead of 72 on 72 CUs), N = 384 / 576
+      // -> 128 rows (one round; 64-row tiles need two); B = 32: 128 rows everywhere
+      {
+        const long per = x3_cus() / (N / 192) > 0 ? x3_cus() / (N / 192) : 1;
+        const long r128 = ((M + XR_BM - 1) / XR_BM + per - 1) / per, r64 = ((M + 63) / 64 + per - 1) / per;
+        if (66 * r64 < 100 * r128) return launch_nt_x3_ring<TA, AM, 192, 64>(a, b, e, M, N, K, s);
+      }
+      // (a last round of 128-row tiles at most half full -- B = 32, N = 192: 576 tiles = 2 rounds of 256 + 64 -- run
+      // as 64-row tiles in a second launch from m_base measured slower: B = 32 650 -> 638, B = 16 548 -> 522 patches/s;
+      // the side stream's weight gradients already fill the idle CUs; profiles/r06_nt_split_ab.txt)
       return launch_nt_x3_ring<TA, AM, 192, XR_BM>(a, b, e, M, N, K, s);
   }
 }
