@@ -526,6 +526,20 @@ int kair_adam_ema_ex(float* p, const float* g, float* m, float* v, float* ema, l
  * fp32 reference has no operand window.) */
 int kair_range_check(const float* g, const float* p, long n, const float* loss, float p_limit, unsigned* flag,
                      void* stream);
+/* fp32x3: the input-gradient GEMM of a Swin linear fused with the LayerNorm backward in front of it (network_swinir.py
+ * :199 / :205 norm1 / norm2 -> qkv / fc1; replaces kair_gemm_nt into a dxn buffer + kair_layernorm_bwd, same math):
+ *   dxn = A B^T (A: fp16-pair gradient rows, B: the split-packed weight, N = 192 >= C: one tile holds whole rows),
+ *   row r of the GEMM (window order when win_ws > 0) is token t;
+ *   D[t] += rstd (g - mean_c(g) - xh mean_c(g xh)),  g = dxn gamma,  xh = (x[t] - mean[t]) rstd[t]   (c < C);
+ *   copy (optional, fp16 pair): the finished D row as in kair_layernorm_bwd;
+ *   part: [kair_gemm_nt_x3_lnbwd_parts(M, N)][2 C] dgamma / dbeta partial rows (one per 16 GEMM rows) for
+ *   kair_ln_param_reduce_grouped. */
+long kair_gemm_nt_x3_lnbwd_parts(long M, int N);
+int kair_gemm_nt_x3_lnbwd(const kair_operand* A, const kair_operand* B, long M, int N, int K, int win_H, int win_W,
+                          int win_ws, int win_shift, const float* x, long ldx, const float* gamma, const float* mean,
+                          const float* rstd, int C, float* D, long ldd, float* part, const kair_copy_desc* copy,
+                          void* stream);
+
 /* Measurement (bench.py's in-step kernel table; no reference counterpart): open a kernel timing window of n slots.
  * Until kair_ktime_end, each libkair launch into a non-capturing stream takes the next slot and is dispatched with
  * hipExtLaunchKernel and the slot's event pair, which the runtime stamps with the dispatch packet's start / end (the

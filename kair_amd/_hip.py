@@ -127,6 +127,10 @@ _SIGS = {
     "kair_layernorm_bwd": [c_vp, c_long, c_vp, c_int, c_long, c_vp, c_vp, c_vp, c_vp, c_long, c_int, c_vp, c_vp, c_int,
                            c_vp, c_long, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(CopyDesc), c_vp],
     "kair_row_copy": [c_vp, c_long, c_long, c_int, ctypes.POINTER(CopyDesc), c_vp],
+    "kair_gemm_nt_x3_lnbwd": [ctypes.POINTER(Operand), ctypes.POINTER(Operand), c_long, c_int, c_int, c_int, c_int, c_int,
+                              c_int, c_vp, c_long, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_vp, ctypes.POINTER(CopyDesc),
+                              c_vp],
+    "kair_gemm_nt_x3_lnbwd_parts": [c_long, c_int],
     "kair_window_attn_fwd": [c_vp, c_int, c_vp, c_vp, c_long, c_vp, c_long, c_int, c_int, c_float, c_int, c_int, c_int,
                              c_int, c_vp, c_int, c_vp],
     "kair_window_attn_bwd_ws": [c_long, c_int],
@@ -219,7 +223,7 @@ _SIGS = {
     "kair_last_error": [],
     "kair_device_arch": [ctypes.c_char_p, c_int],
 }
-_RESTYPE = {"kair_layernorm_bwd_blocks": c_long, "kair_rowgemm_ln_blocks": c_long, "kair_window_attn_bwd_groups": c_long, "kair_wgrad_grouped_ws": c_long, "kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
+_RESTYPE = {"kair_gemm_nt_x3_lnbwd_parts": c_long, "kair_layernorm_bwd_blocks": c_long, "kair_rowgemm_ln_blocks": c_long, "kair_window_attn_bwd_groups": c_long, "kair_wgrad_grouped_ws": c_long, "kair_swin_mlp_bwd_ws": c_long, "kair_bn_ws": c_long, "kair_last_error": ctypes.c_char_p, "kair_window_attn_bwd_ws": c_long, "kair_pack_table_bytes": c_long,
             "kair_pack_table_build": c_long, "kair_conv3x3_narrow_wgrad_ws": c_long,
             "kair_conv3x3_narrow_dgrad_ws": c_long, "kair_conv3x3_narrow_x3_ws": c_long}
 
@@ -532,6 +536,18 @@ def layernorm_bwd(x, ldx, dy, ldy, gamma, mean, rstd, dx, ld_dx, dx_acc, dgamma,
     check(lib().kair_layernorm_bwd(ptr(x), ldx, ptr(dy), dtype_code(dy), ldy, ptr(gamma), ptr(mean), ptr(rstd), ptr(dx),
                                    ld_dx, int(dx_acc), ptr(dgamma), ptr(dbeta), int(dparam_acc), ptr(ws), M, C, *win,
                                    ctypes.byref(copy) if copy is not None else None, stream_ptr()), "layernorm_bwd")
+
+
+def gemm_nt_lnbwd(A, B, M, N, K, x, ldx, gamma, mean, rstd, C, D, ldd, part, win=(0, 0, 0, 0), copy=None):
+    """fp32x3: dxn = A B^T fused with the LayerNorm backward (kair_gemm_nt_x3_lnbwd): D[t] += LN'(dxn), the optional
+    fp16-pair copy of D, dgamma / dbeta partial rows in part (gemm_nt_lnbwd_parts(M, N) rows of 2 C)."""
+    check(lib().kair_gemm_nt_x3_lnbwd(ctypes.byref(A), ctypes.byref(B), M, N, K, *win, ptr(x), ldx, ptr(gamma), ptr(mean),
+                                      ptr(rstd), C, ptr(D), ldd, ptr(part),
+                                      ctypes.byref(copy) if copy is not None else None, stream_ptr()), "gemm_nt_x3_lnbwd")
+
+
+def gemm_nt_lnbwd_parts(M, N):
+    return lib().kair_gemm_nt_x3_lnbwd_parts(M, N)
 
 
 def row_copy(src, ld_src, M, C, copy):

@@ -36,10 +36,11 @@ KAIR_DEV f32x16 mfma32(const f16x8& a, const f16x8& b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 // the fp16 pair of 8 accumulator elements (the pack8 operand order) scaled by sc
+// (products made opaque before the split: common.h opaque)
 KAIR_DEV void pack8_pair(const f32x16& a, int s, float sc, f16x8& hi, f16x8& lo) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float v = a[8 * s + j] * sc;
+    const float v = opaque(a[8 * s + j] * sc);
     hi[j] = (f16)v;
     lo[j] = (f16)(v - (float)hi[j]);
   }
@@ -47,7 +48,7 @@ KAIR_DEV void pack8_pair(const f32x16& a, int s, float sc, f16x8& hi, f16x8& lo)
 KAIR_DEV void pair4(const float (&v)[4], float sc, f16x4& hi, f16x4& lo) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float w = v[j] * sc;
+    const float w = opaque(v[j] * sc);
     hi[j] = (f16)w;
     lo[j] = (f16)(w - (float)hi[j]);
   }
@@ -442,7 +443,7 @@ __global__ __launch_bounds__(64 * BWD_NW, 2) void attn_bwd_x3_kernel(const f16* 
     for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float v = dP[qt][r] * s_gup;
+        const float v = opaque(dP[qt][r] * s_gup);   // (not fused into the conversion: common.h opaque)
         const f16 vh = (f16)v;
         const int o = (qt * 32 + acc_row(r, hh)) * LD + l31;
         dsh[o] = vh;

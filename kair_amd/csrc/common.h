@@ -66,6 +66,16 @@ bool kair_ktime_take(const void* fn, hipStream_t s, hipEvent_t* e0, hipEvent_t* 
       k<<<(grid), (block), (lds), (stream)>>>(__VA_ARGS__);                                                 \
   } while (0)
 
+// An fp32 value the compiler may not fuse into the fp16 conversion after it: a pair split hi = f16(w), lo = f16(w - hi)
+// of a product w = a b (b not a power of two) otherwise becomes hi = v_fma_mix(a, b) -- the exact product rounded once
+// to fp16 -- beside a second, fp32-rounded conversion for the stored hi: at double-rounding points (~2^-13 of the
+// values) the stored hi and the lo computed against the other one disagree by one hi ulp.  ("fp contract(off)" and
+// __fmul_rn do not stop this fusion.)
+KAIR_DEV float opaque(float w) {
+  asm volatile("" : "+v"(w));
+  return w;
+}
+
 template <typename T> KAIR_DEV float to_f(T v) { return (float)v; }
 template <typename T> KAIR_DEV T from_f(float v) { return (T)v; }
 

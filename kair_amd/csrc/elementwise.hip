@@ -464,7 +464,7 @@ __global__ void row_copy_pair_kernel(const float* __restrict__ src, long lds, f1
   const int c = (int)(i - t * C4) * 4;
   const float4 v = *(const float4*)(src + t * lds + c);
   const float sc = (scale ? scale[t / rps] : 1.f) * es;
-  const float w[4] = {sc * v.x, sc * v.y, sc * v.z, sc * v.w};
+  const float w[4] = {opaque(sc * v.x), opaque(sc * v.y), opaque(sc * v.z), opaque(sc * v.w)};   // (common.h opaque)
   f16x4 h, l;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {

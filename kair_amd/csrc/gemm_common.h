@@ -243,6 +243,13 @@ struct Epi {
   float oscale;      // x3, fp16 out: 2^x3_out_exp
   FDiv d_rps, d_tok, d_hdp, d_pw;
   int dbg;   // ring-kernel ablation bits (KAIR_RING_DBG, perf investigation only): 1 no stores, 2 no MFMA, 4 no A loads
+  // EX_LNB (x3 NT ring, kair_gemm_nt_x3_lnbwd): the GEMM is the LayerNorm's input-gradient producer; out is the
+  // accumulated fp32 gradient D (token rows, read-modify-write), bias the LayerNorm weight gamma
+  const float* lnx; long lnldx;             // the LayerNorm input rows (token order)
+  const float* lnmu; const float* lnrs;     // its saved row mean / rstd
+  float* lnpart; int lnC;                   // dgamma / dbeta partial rows [tile * 4 + row wave][2 C]; real channels
+  void* cpo; void* cplo; long cpld;         // optional fp16-pair operand copy of the finished D rows
+  const float* cprs; FDiv d_cprps; WinMap cpwin; float cps;
 };
 
 Epi make_epi(const kair_epilogue& o, long M, int N) {
@@ -268,6 +275,9 @@ Epi make_epi(const kair_epilogue& o, long M, int N) {
   e.d_rps = make_fdiv(e.rps); e.d_tok = make_fdiv(e.tok); e.d_hdp = make_fdiv(e.hdp); e.d_pw = make_fdiv(e.nh * e.hdp);
   static const int dbg = kair_dbg_env("KAIR_RING_DBG");
   e.dbg = dbg;
+  e.lnx = nullptr; e.lnldx = 0; e.lnmu = e.lnrs = nullptr; e.lnpart = nullptr; e.lnC = 0;
+  e.cpo = e.cplo = nullptr; e.cpld = 0; e.cprs = nullptr; e.d_cprps = make_fdiv(1); e.cpwin = make_winmap(0, 0, 0, 0);
+  e.cps = 1.f;
   return e;
 }
 
@@ -517,7 +527,7 @@ KAIR_DEV void land(float& v) { asm volatile("" : "+v"(v)); }
 KAIR_DEV void land(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
 
 // ring epilogue operand kinds (compile-time, so the plain kernels carry no epilogue loads at all)
-enum { EX_NONE = 0, EX_RESID = 1, EX_GATE_BF16 = 2, EX_GATE_F32 = 3 };
+enum { EX_NONE = 0, EX_RESID = 1, EX_GATE_BF16 = 2, EX_GATE_F32 = 3, EX_LNB = 4 };   // EX_LNB: x3 NT ring only
 
 // a zero line for masked loads (read-only; zero-initialised device memory)
 __device__ __attribute__((aligned(64))) unsigned char g_kair_zero_line[64];
@@ -540,6 +550,15 @@ KAIR_DEV void vm_wait(int n) {
   }
 }
 #undef KAIR_VMW
+
+// sum over the 16 lanes of a DPP row, every lane gets the same bits (quad swaps, then the half-row and row mirrors)
+KAIR_DEV float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));    // quad_perm 1,0,3,2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));    // quad_perm 2,3,0,1
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));   // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));   // row_mirror
+  return v;
+}
 
 // bijective XCD-aware remap: consecutive logical tiles share an XCD (L2)
 KAIR_DEV int xcd_remap(int hw, int nwg) {

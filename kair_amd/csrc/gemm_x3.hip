@@ -397,7 +397,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
   // shape of the 8-GPU run has 72 128-row tiles per N-tile for 256 CUs); RI row fragments / A DMA instructions per wave
   constexpr int RI = BM / 64, ASTAGE = BM * 128;
   static_assert(RI == 1 || RI == 2, "64- or 128-row tiles");
-  __shared__ __attribute__((aligned(16))) char smem[NA * XR_ASTAGE + XR_NB * BSTAGE + BN * 4];
+  // EX_LNB: + the row-sum exchange of partner waves ([4 row waves][2 column halves][32 rows][2]) and 8 wave flags
+  constexpr int XLDS = EX == EX_LNB ? (4 * 2 * 32 * 2 + 8) * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[NA * XR_ASTAGE + XR_NB * BSTAGE + BN * 4 + XLDS];
   char* const sA = smem;
   char* const sB = smem + NA * ASTAGE;
   float* const sBias = (float*)(sB + XR_NB * BSTAGE);   // the N-tile's bias (zeros without one), read by the epilogue
@@ -442,8 +444,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       colo[p] = n;
     }
   }
-  for (int i = tid; i < BN; i += 512) sBias[i] = E.bias && n0 + i < E.N ? E.bias[n0 + i] : 0.f;   // (visible after the
-                                                                                                // first barrier)
+  // (visible after the first barrier; EX_LNB: the LayerNorm weight over the real channels, zeros beyond)
+  for (int i = tid; i < BN; i += 512) sBias[i] = E.bias && n0 + i < (EX == EX_LNB ? E.lnC : E.N) ? E.bias[n0 + i] : 0.f;
+  if constexpr (EX == EX_LNB)
+    if (tid < 8) ((int*)(sBias + BN + 4 * 2 * 32 * 2))[tid] = 0;
   // B loader: this lane's BI weight rows (fixed for the CTA), unit already swizzled
   const f16* bsrc[BI];
 #pragma unroll
@@ -598,6 +602,138 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
         acc[i][jn] = mfma16(bh[jn], al[i], acc[i][jn]);
       }
   };
+  // EX_LNB: the LayerNorm backward of the finished rows (network_swinir.py:199 / :205 norm1 / norm2 backward, as
+  // kair_layernorm_bwd): dxn = the GEMM tile (the LayerNorm output's gradient), x / mean / rstd the LayerNorm's
+  //   xh = (x - mu) rs,  gy = dxn gamma,  D += rs (gy - mean_c(gy) - xh mean_c(gy xh)),
+  // then the optional fp16-pair copy of the finished D row (the next GEMMs' operand) and this row wave's dgamma /
+  // dbeta partial sums (sum over its rows of dxn xh, dxn) -- one N-tile holds whole rows (N = 192 >= C).  A lane owns
+  // 24 columns (3 chunk pairs, SW = false) of RI rows; the row sums go over the 4 lanes of a row (xor 16, 32) and the
+  // partner wave that owns the other 96 columns, exchanged through LDS: each wave writes its sums and a per-tile flag,
+  // then waits (s_sleep poll) for its partner's -- both run this epilogue in the same interval.  All loads issue
+  // unconditionally (rows clamped), so the returned count is exact; stores as the rows / columns allow.
+  auto ln_epilogue = [&](int ct, const int (&rowv)[RI], const bool (&okm)[RI], int nvm) __attribute__((always_inline)) -> int {
+    float* const xch = sBias + BN;
+    volatile int* const flg = (volatile int*)(xch + 4 * 2 * 32 * 2);
+    const int rw = grp * 2 + wm, C = E.lnC;
+    const long slot0 = ((long)(m_base / BM + mt0 + ct * mstride) * 4 + rw) * RI;
+    long tr[RI];
+    float mu[RI], rsd[RI];
+#pragma unroll
+    for (int i = 0; i < RI; ++i) {
+      tr[i] = okm[i] ? rowv[i] : 0;   // (clamped: every load issues)
+      mu[i] = E.lnmu[tr[i]];
+      rsd[i] = E.lnrs[tr[i]];
+    }
+    nvm += 2 * RI;
+    // phase 1, per row fragment: the row sums of this wave's 96 columns -> LDS, and the fragment's dgamma / dbeta
+    // partial row (the sum over its 16 rows = the 16 lanes of a DPP row) -> part[slot]
+#pragma unroll
+    for (int i = 0; i < RI; ++i) {
+      const float* xr = E.lnx + tr[i] * E.lnldx;
+      float xh[24];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 q = *(const float4*)(xr + c8[p] + 16 * h);
+          xh[p * 8 + h * 4 + 0] = q.x; xh[p * 8 + h * 4 + 1] = q.y;
+          xh[p * 8 + h * 4 + 2] = q.z; xh[p * 8 + h * 4 + 3] = q.w;
+        }
+      nvm += 2 * NP;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 24; ++j) {
+        const int p = j >> 3, h = (j >> 2) & 1, c4 = j & 3, cc = c8[p] + 16 * h + c4;
+        const float v = acc[i][2 * p + h][c4] * E.acc_scale;
+        xh[j] = cc < C ? (xh[j] - mu[i]) * rsd[i] : 0.f;
+        const float gy = v * sBias[cc - n0];
+        s1 += gy;
+        s2 += gy * xh[j];
+      }
+      s1 += __shfl_xor(s1, 16);
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 16);
+      s2 += __shfl_xor(s2, 32);
+      if (fq == 0) {
+        xch[((rw * 2 + wn) * 32 + i * 16 + fr) * 2] = s1;
+        xch[((rw * 2 + wn) * 32 + i * 16 + fr) * 2 + 1] = s2;
+      }
+      float* const pg = E.lnpart + (slot0 + i) * 2 * C;
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float dg[4], db[4];
+#pragma unroll
+          for (int c4 = 0; c4 < 4; ++c4) {
+            const float v = acc[i][2 * p + h][c4] * E.acc_scale;
+            dg[c4] = row16_sum(v * xh[p * 8 + h * 4 + c4]);
+            db[c4] = row16_sum(v);
+          }
+          const int c = c8[p] + 16 * h;
+          if (fr == 0 && c < C) {
+            *(float4*)(pg + c) = make_float4(dg[0], dg[1], dg[2], dg[3]);
+            *(float4*)(pg + C + c) = make_float4(db[0], db[1], db[2], db[3]);
+          }
+          nvm += n0 + wn * WC + 32 * p + 16 * h < C ? 2 : 0;   // (lane fq = 0's column: at least that lane stores)
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's row sums are in LDS
+    if (lane == 0) flg[wave] = ct + 1;
+    while (flg[wave ^ 1] != ct + 1) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+    // phase 2, per row fragment and 4-column chunk: the partner's sums, D += dx, the operand copy
+#pragma unroll
+    for (int i = 0; i < RI; ++i) {
+      const volatile float* a0 = xch + ((rw * 2 + 0) * 32 + i * 16 + fr) * 2;
+      const volatile float* a1 = xch + ((rw * 2 + 1) * 32 + i * 16 + fr) * 2;
+      const float S1 = (a0[0] + a1[0]) / (float)C, S2 = (a0[1] + a1[1]) / (float)C;   // column half 0 + half 1
+      float sc = E.cps;
+      if (E.cprs) {
+        sc *= E.cprs[fdiv((int)tr[i], E.d_cprps)];
+        nvm += 1;
+      }
+      const long cr = E.cpo ? token_to_win(tr[i], E.cpwin) : 0;
+      const float* xr = E.lnx + tr[i] * E.lnldx;
+      float* const dr = (float*)E.out + tr[i] * E.ldo;
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = c8[p] + 16 * h;
+          const float4 xq = *(const float4*)(xr + c), dq = *(const float4*)(dr + c);
+          const float xa[4] = {xq.x, xq.y, xq.z, xq.w}, da[4] = {dq.x, dq.y, dq.z, dq.w};
+          float o[4];
+#pragma unroll
+          for (int c4 = 0; c4 < 4; ++c4) {
+            const int cc = c + c4;
+            const float v = acc[i][2 * p + h][c4] * E.acc_scale;
+            const float xhat = (xa[c4] - mu[i]) * rsd[i];
+            o[c4] = da[c4] + (cc < C ? rsd[i] * (v * sBias[cc - n0] - S1 - xhat * S2) : 0.f);
+          }
+          if (okm[i]) {
+            *(float4*)(dr + c) = make_float4(o[0], o[1], o[2], o[3]);
+            if (E.cpo) {
+              f16x4 hi, lo;
+#pragma unroll
+              for (int c4 = 0; c4 < 4; ++c4) {
+                const float w = opaque(o[c4] * sc);   // (common.h opaque: no fused conversion)
+                hi[c4] = (f16)w;
+                lo[c4] = (f16)(w - (float)hi[c4]);
+              }
+              *(f16x4*)((f16*)E.cpo + cr * E.cpld + c) = hi;
+              *(f16x4*)((f16*)E.cplo + cr * E.cpld + c) = lo;
+            }
+          }
+        }
+      nvm += 4 * NP + (__ballot(okm[i]) != 0 ? 2 * NP * (E.cpo ? 3 : 1) : 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RI; ++i)
+#pragma unroll
+      for (int jn = 0; jn < RN; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    return nvm;
+  };
   // multiply the fragments in registers into acc; the tile's last chunk also runs its epilogue, its operands
   // loaded after the MFMAs (the partner group's phase covers their latency) and used in the same straight-line
   // branch (no control-flow merge between a load and its use: hipcc never holds a pending load across the loop
@@ -637,6 +773,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
       }
     }
     mfma_chunk();   // (the fragments die here: the epilogue operands load after it, under the partner's work)
+    if constexpr (EX == EX_LNB) return ln_epilogue(ct, rowv, okm, nvm);
     float4 ex[RI][NP][2];
     float rs[RI];
 #pragma unroll
@@ -1223,6 +1360,13 @@ int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int
 #define XR_LAUNCH(EM, EX, ACT, GK) \
   KAIR_LAUNCH((gemm_nt_x3_ring<TA, AM, EM, EX, ACT, GK, BN, BM>), g, bl, 0, s, a, b, e, K, tilesN, tilesM, (int)m_base)
   if constexpr (BN == 192) {   // the Swin linears and the 192-channel convs: every epilogue form
+    if constexpr (sizeof(TA) == 2 && AM == AM_ROWS && BM == 64) {   // fp16-pair rows: the LayerNorm-backward epilogue
+      if (e.lnx) {
+        XR_LAUNCH(XE_ROWS_F32, EX_LNB, XA_NONE, 0);
+        KAIR_CHECK_LAUNCH();
+        return 0;
+      }
+    }
     if (e.omode == KAIR_OUT_QKVBLK) XR_LAUNCH(XE_QKV, EX_NONE, XA_NONE, 0);
     else if (e.odt == KAIR_F16 && e.gate) XR_LAUNCH(XE_ROWS_PAIR, EX_GATE_F32, XA_NONE, XG_MUL);
     else if (e.odt == KAIR_F16 && e.act == KAIR_ACT_GELU) XR_LAUNCH(XE_ROWS_PAIR, EX_NONE, XA_GELU, 0);
@@ -1246,21 +1390,23 @@ int launch_nt_x3_ring(const Op& a, const Op& b, const Epi& e, long M, int N, int
   return 0;
 }
 
+// the row tile of the 192-column NT ring: 64-row tiles when they finish sooner -- rounds of tiles per CU
+// (x3_cus / N-tiles CTAs per N-tile) at a 64-row tile's cost of 0.66 of a 128-row one (profiles/r06_bm64_ab.txt:
+// the same rows take 1.31x as long in 64-row tiles).  B = 4 (M = 9,216): N = 192 -> 64 rows (1 round of 144 tiles
+// instead of 72 on 72 CUs), N = 384 / 576 -> 128 rows (one round; 64-row tiles need two); B = 32: 128 rows everywhere
+int nt_x3_bm192(long M, int N) {
+  const long per = x3_cus() / (N / 192) > 0 ? x3_cus() / (N / 192) : 1;
+  const long r128 = ((M + XR_BM - 1) / XR_BM + per - 1) / per, r64 = ((M + 63) / 64 + per - 1) / per;
+  return 66 * r64 < 100 * r128 ? 64 : XR_BM;
+}
+
 template <typename TA, int AM>
 int nt_x3_ring_dispatch(const Op& a, const Op& b, const Epi& e, long M, int N, int K, hipStream_t s) {
   switch (nt_x3_ring_bn(N)) {
     case 64: return launch_nt_x3_ring<TA, AM, 64, XR_BM>(a, b, e, M, N, K, s);
     case 128: return launch_nt_x3_ring<TA, AM, 128, XR_BM>(a, b, e, M, N, K, s);
     default:
-      // 64-row tiles when they finish sooner: rounds of tiles per CU (x3_cus / N-tiles CTAs per N-tile) at a 64-row
-      // tile's cost of 0.66 of a 128-row one (profiles/r06_bm64_ab.txt: the same rows take 1.31x as long in 64-row
-      // tiles).  B = 4 (M = 9,216): N = 192 -> 64 rows (1 round of 144 tiles instead of 72 on 72 CUs), N = 384 / 576
-      // -> 128 rows (one round; 64-row tiles need two); B = 32: 128 rows everywhere
-      {
-        const long per = x3_cus() / (N / 192) > 0 ? x3_cus() / (N / 192) : 1;
-        const long r128 = ((M + XR_BM - 1) / XR_BM + per - 1) / per, r64 = ((M + 63) / 64 + per - 1) / per;
-        if (66 * r64 < 100 * r128) return launch_nt_x3_ring<TA, AM, 192, 64>(a, b, e, M, N, K, s);
-      }
+      if (nt_x3_bm192(M, N) == 64) return launch_nt_x3_ring<TA, AM, 192, 64>(a, b, e, M, N, K, s);
       // (a last round of 128-row tiles at most half full -- B = 32, N = 192: 576 tiles = 2 rounds of 256 + 64 -- run
       // as 64-row tiles in a second launch from m_base measured slower: B = 32 650 -> 638, B = 16 548 -> 522 patches/s;
       // the side stream's weight gradients already fill the idle CUs; profiles/r06_nt_split_ab.txt)
@@ -1386,6 +1532,50 @@ int kair_gemm_nt_x3(const kair_operand* A, const kair_operand* B, const kair_epi
   if (A->dtype == KAIR_F16)
     return A->mode == KAIR_LD_ROWS ? nt_x3_tiles<f16, AM_ROWS>(a, b, e, M, N, K, s) : nt_x3_tiles<f16, AM_IM2COL>(a, b, e, M, N, K, s);
   return A->mode == KAIR_LD_ROWS ? nt_x3_tiles<float, AM_ROWS>(a, b, e, M, N, K, s) : nt_x3_tiles<float, AM_IM2COL>(a, b, e, M, N, K, s);
+}
+
+extern "C" long kair_gemm_nt_x3_lnbwd_parts(long M, int N) {
+  if (M <= 0 || N != 192) return 0;
+  return (M + 63) / 64 * 4;   // (64-row tile, row wave): 16 rows each
+}
+
+extern "C" int kair_gemm_nt_x3_lnbwd(const kair_operand* A, const kair_operand* B, long M, int N, int K, int win_H,
+                                     int win_W, int win_ws, int win_shift, const float* x, long ldx, const float* gamma,
+                                     const float* mean, const float* rstd, int C, float* D, long ldd, float* part,
+                                     const kair_copy_desc* copy, void* stream) {
+  int rc;
+  if ((rc = x3_operand_ok(A, "gemm_nt_x3_lnbwd A"))) return rc;
+  KAIR_CHECK_ARG(x && gamma && mean && rstd && D && part, "gemm_nt_x3_lnbwd: null pointer");
+  KAIR_CHECK_ARG(N == 192 && C > 0 && C <= N && C % 4 == 0 && M > 0 && M < KAIR_MAX_MAPPED_ROWS,
+                 "gemm_nt_x3_lnbwd: one 192-column tile holding the C <= 192 channels (C %% 4 == 0)");
+  KAIR_CHECK_ARG(A->dtype == KAIR_F16 && A->mode == KAIR_LD_ROWS, "gemm_nt_x3_lnbwd: A must be fp16-pair rows");
+  KAIR_CHECK_ARG(ldx % 4 == 0 && ldd % 4 == 0 && ldx >= N && ldd >= N && ((uintptr_t)x % 16) == 0 && ((uintptr_t)D % 16) == 0,
+                 "gemm_nt_x3_lnbwd: x / D rows of >= 192 columns, 16-byte aligned");
+  kair_epilogue E;
+  memset(&E, 0, sizeof(E));
+  E.out = D; E.out_dtype = KAIR_F32; E.out_mode = KAIR_OUT_ROWS; E.ldo = ldd;
+  E.win_H = win_H; E.win_W = win_W; E.win_ws = win_ws; E.win_shift = win_shift;
+  E.bias = gamma;
+  KAIR_CHECK_ARG(nt_x3_ring_ok(A, B, &E, N, K), "gemm_nt_x3_lnbwd: shape / operands outside the NT ring");
+  KAIR_CHECK_ARG(win_ws == 0 || (win_H % win_ws == 0 && win_W % win_ws == 0), "gemm_nt_x3_lnbwd: window geometry");
+  const Op a = make_op(*A, M), b = make_op(*B, N);
+  Epi e = make_epi(E, M, N);
+  e.acc_scale = ldexpf(1.f, -(A->x3_exp + B->x3_exp));
+  e.lnx = x; e.lnldx = ldx; e.lnmu = mean; e.lnrs = rstd; e.lnpart = part; e.lnC = C;
+  if (copy && copy->out) {
+    KAIR_CHECK_ARG(copy->dtype == KAIR_F16 && copy->out_lo && copy->ld % 4 == 0 && copy->ld >= N &&
+                       ((uintptr_t)copy->out % 8) == 0 && ((uintptr_t)copy->out_lo % 8) == 0,
+                   "gemm_nt_x3_lnbwd: the copy is an fp16 pair (out + out_lo, 8-byte aligned, ld %% 4 == 0)");
+    KAIR_CHECK_ARG(copy->win_ws == 0 || (copy->win_H % copy->win_ws == 0 && copy->win_W % copy->win_ws == 0),
+                   "gemm_nt_x3_lnbwd: copy window geometry");
+    e.cpo = copy->out; e.cplo = copy->out_lo; e.cpld = copy->ld;
+    e.cprs = copy->rowscale;
+    e.d_cprps = make_fdiv(copy->rows_per_scale > 0 ? copy->rows_per_scale : 1);
+    e.cpwin = make_winmap(copy->win_H, copy->win_W, copy->win_ws, copy->win_shift);
+    e.cps = ldexpf(1.f, copy->x3_exp);
+  }
+  // 64-row tiles at every M: with this epilogue the 128-row form exceeds the 256 VGPRs of two waves per SIMD (spills)
+  return launch_nt_x3_ring<f16, AM_ROWS, 192, 64>(a, b, e, M, N, K, (hipStream_t)stream);
 }
 
 int kair_gemm_tn_x3(const kair_operand* A, const kair_operand* B, float* ws, int splits, long M, int N, int K,

@@ -185,7 +185,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
         *(float4*)o = cu;
         if (cp) {   // GEMM-operand copy of the finished gradient row: scaled, cast, optionally window-ordered
           if (cp_dt == KAIR_BF16) store4<bf16>((bf16*)cp + cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w);
-          else if (cp_dt == KAIR_F16) store4_pair((f16*)cp, cp_lo, cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w, cp_s);
+          else if (cp_dt == KAIR_F16)   // (opaque products: the pair splits the fp32-rounded value, common.h)
+            store4_pair((f16*)cp, cp_lo, cr * ldc + c, opaque(sc * cu.x), opaque(sc * cu.y), opaque(sc * cu.z),
+                        opaque(sc * cu.w), cp_s);
           else store4<float>((float*)cp + cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w);
         }
       }

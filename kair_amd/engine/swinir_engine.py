@@ -433,6 +433,12 @@ class SwinIREngine:
         # fp32x3: an RSTB's deferred block weight gradients as ONE grouped TN-ring launch + one grouped finalize
         # (kair_wgrad_grouped with fp16-pair jobs) instead of a launch pair per linear (KAIR_X3_GROUPED=0: A/B)
         self.x3_grouped = self.x3_side and os.environ.get("KAIR_X3_GROUPED", "1") != "0"
+        # fp32x3: the LayerNorm backwards fused into the qkv / fc1 input-gradient GEMMs' epilogue (kair_gemm_nt_x3_lnbwd,
+        # KAIR_X3_LNFUSE=1).  Off by default: measured slower (B = 32 660 -> 614, B = 4 349 -> 340 patches/s,
+        # profiles/r06_x3_lnfuse_ab.txt) -- the LayerNorm backward's own traffic (x, D read, D and its operand copy
+        # written) stays and now runs in the ring's epilogue intervals, in 64-row tiles (the 128-row form spills)
+        self.x3_lnfuse = (self.x3 and self.Cp == 192 and self.C % 4 == 0 and not self.rowgemm and not fused_mlp_bwd and
+                          os.environ.get("KAIR_X3_LNFUSE", "0") == "1")
         self.side_ctas = int(side_ctas)
         # '1conv' weight gradients on the tap-per-tile ring (bf16 copies of G and the conv input)
         self.conv_tap = self.tdt == torch.bfloat16 and self.Cp == 192 and self.C % 4 == 0
@@ -580,13 +586,15 @@ class SwinIREngine:
         # fp32x3: the block's gradient operands as fp16 pairs [2, ...] of v 2^e_g (zero-filled pads as above)
         zp = (lambda *sh: torch.zeros(2, *sh, device=dev, dtype=hf)) if self.x3 else z
         ep = (lambda *sh: e(2, *sh, dt=hf)) if self.x3 else (lambda *sh: e(*sh, dt=T))
+        # (the fused fp32x3 LayerNorm backward leaves one partial row per 16 GEMM rows)
+        lnp = max(2 * 2048 * Cp, 2 * self.C * H.gemm_nt_lnbwd_parts(M, Cp) if self.x3_lnfuse else 0)
         # Two sets (RSTB parity): the side stream still reads one RSTB's while the next RSTB writes the other.
         P["gw"] = [[{"Dm": zp(M, Cp), "Da": zp(M, Cp), "dU": ep(M, Hdp),
                      # fp32x3: dq/dk/dv as token rows [M][3 nh 32] (pairs: the ring GEMMs' operand)
                      "dqkv": ep(M, 3 * nh * 32) if self.x3 else e(3 * M * nh * 32, dt=T),
                      # LN1 / LN2 parameter partials and the attention bias-table partials of the block, reduced
                      # by one grouped launch each at the end of the RSTB
-                     "ln1p": e(2 * 2048 * Cp), "ln2p": e(2 * 2048 * Cp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
+                     "ln1p": e(lnp), "ln2p": e(lnp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
                     for _ in range(depth)] for _ in range(2)]
         P["G3"] = z32(M, Cp)   # third residual-gradient buffer (rotation, see backward())
         if self.rowgemm:   # LayerNorm-parameter partial rows the fused row GEMMs leave (<= the ln*p buffers' 2048)
@@ -794,6 +802,12 @@ class SwinIREngine:
         """A forward conv's input operand: a hi/lo pair under split_act (fp32 source: lo formed in the
         kernel; bf16 source: its lo plane `lo`), else as is."""
         return H.asplit(op, lo) if self.split_act else op
+
+    def _nt_lnbwd(self, A, B, M, K, x, gamma, mean, rstd, D, part, win=(0, 0, 0, 0), copy=None):
+        """fp32x3: the input-gradient GEMM A B^T of the Linear after a LayerNorm (N = Cp = 192) fused with that
+        LayerNorm's backward into D (kair_gemm_nt_x3_lnbwd), exponents as in _nt."""
+        A.x3_exp, B.x3_exp = self._ax, H.X3_WEXP
+        H.gemm_nt_lnbwd(A, B, M, self.Cp, K, x, self.Cp, gamma, mean, rstd, self.C, D, self.Cp, part, win=win, copy=copy)
 
     def _nt(self, A, B, E, M, N, K, cd):
         """kair_gemm_nt; under fp32x3 the split-fp16 arithmetic (compute KAIR_COMPUTE_X3): A is fp32 (split in the
@@ -1311,11 +1325,17 @@ class SwinIREngine:
             Eu = (H.epilogue(dU[0], out_lo=dU[1], gate=S["u"], gate_kind=4) if self.x3 else
                   H.epilogue(dU, gate=S["u"], gate_kind=4))
             self._nt(self._op(Dm), H.rows(fc2.Wt), Eu, M, self.Hdp, Cp, cd)
-            self._nt(self._op(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
-            H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, None, None, False,
-                            W["ln2p"], M, self.C, copy=H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win,
-                                                                   x3_exp=P["e_g"]))
-            self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False))
+            cpy = H.copy_desc(Da, rowscale=s_attn, rows_per_scale=HW, win=win, x3_exp=P["e_g"])
+            if self.x3_lnfuse:   # fc1 input gradient + LN2 backward in one launch
+                self._nt_lnbwd(self._op(dU), H.rows(fc1.Wt), M, self.Hdp, S["mid"], n.weight, S["m2"], S["r2"], D,
+                               W["ln2p"], copy=cpy)
+                self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False,
+                                          H.gemm_nt_lnbwd_parts(M, Cp)))
+            else:
+                self._nt(self._op(dU), H.rows(fc1.Wt), H.epilogue(P["dxn"]), M, Cp, self.Hdp, cd)
+                H.layernorm_bwd(S["mid"], Cp, P["dxn"], Cp, n.weight, S["m2"], S["r2"], D, Cp, True, None, None, False,
+                                W["ln2p"], M, self.C, copy=cpy)
+                self._lnp_pending.append((W["ln2p"], M, self.C, g(n.weight), g(n.bias), False))
         self._wg(P, self._op(dU), self._op(S["ln2"], ones_col=self.C, ones_in_data=True), self.Hdp, Cp, fc1, grads, self.C)
         # attention: mid = x + s_attn * proj(attn(LN1(x)))   (window order inside)
         proj, qkv = blk.proj, blk.qkv
@@ -1374,6 +1394,11 @@ class SwinIREngine:
         if j > 0:   # the previous block's MLP operand: s_mlp(prev) * dL/d x_in
             cp = H.copy_desc(P["gw"][par][j - 1]["Dm"], rowscale=drop[bi - 1, 1] if drop is not None else None,
                              rows_per_scale=HW, x3_exp=P["e_g"])
+        if self.x3_lnfuse:   # q/k/v input gradient + LN1 backward in one launch
+            self._nt_lnbwd(self._op(dqkv), H.rows(qkv.Wt), M, qkv.Np, x_in, n.weight, S["m1"], S["r1"], D, W["ln1p"],
+                           win=win, copy=cp)
+            self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False, H.gemm_nt_lnbwd_parts(M, Cp)))
+            return
         self._nt(self._op(dqkv), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
         H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
                         W["ln1p"], M, self.C, win, copy=cp)

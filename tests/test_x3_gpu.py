@@ -268,6 +268,72 @@ def _wsplit(w):
     return o, Wp
 
 
+@pytest.mark.parametrize("M, win, with_copy", [(1000, False, True), (3 * 16 * 16, True, True), (2 * 24 * 24, True, False)])
+def test_gemm_nt_x3_lnbwd_fused(M, win, with_copy):
+    """kair_gemm_nt_x3_lnbwd (the q/k/v or fc1 input-gradient GEMM fused with the LayerNorm backward in front of it)
+    against float64: D += LN'(A W^T) over token rows (GEMM rows in window order when win), the fp16-pair operand copy
+    of D (row-scaled, window order), and the dgamma / dbeta partial rows reduced by ln_param_reduce_grouped; ragged M,
+    padded channels (C = 180 of 192)."""
+    g = torch.Generator().manual_seed(37)
+    C, Cp, K = 180, 192, 384
+    geo = (16, 16, 8, 4) if M == 768 else ((24, 24, 8, 0) if win else (0, 0, 0, 0))
+    HW = geo[0] * geo[1] if win else M
+    dy = torch.randn(M, K, generator=g) * 1e-5
+    w = torch.zeros(Cp, K)
+    w[:C] = torch.randn(C, K, generator=g) * 0.05
+    x = torch.zeros(M, Cp)
+    x[:, :C] = torch.randn(M, C, generator=g) * 2 + 0.3
+    gam = 1 + 0.1 * torch.randn(C, generator=g)
+    D0 = torch.zeros(M, Cp)
+    D0[:, :C] = torch.randn(M, C, generator=g) * 1e-5
+    mu = x[:, :C].double().mean(1)
+    rs = 1 / torch.sqrt(x[:, :C].double().var(1, unbiased=False) + 1e-5)
+    Wo, keep = _wsplit(w)
+    dp = hilo(dy.to(dev), 20)
+    A = H.with_lo(H.rows(dp[0]), dp[1])   # GEMM rows = dy rows (window order when win)
+    A.x3_exp = 20
+    D = D0.to(dev)
+    nb = H.gemm_nt_lnbwd_parts(M, Cp)
+    part = torch.full((nb * 2 * C,), float("nan"), device=dev)
+    nimg = -(-M // HW)
+    sc = torch.rand(nimg, generator=g) + 0.5
+    cp = torch.zeros(2, M, Cp, device=dev, dtype=torch.float16)
+    desc = H.copy_desc(cp, rowscale=sc.to(dev), rows_per_scale=HW, win=geo if win else None, x3_exp=20) if with_copy else None
+    H.gemm_nt_lnbwd(A, Wo, M, Cp, K, x.to(dev), Cp, gam.to(dev), mu.float().to(dev), rs.float().to(dev), C, D, Cp, part,
+                    win=geo if win else (0, 0, 0, 0), copy=desc)
+    dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    H.ln_param_reduce_grouped([(part, M, C, dg, db, False, nb)])
+    torch.cuda.synchronize()
+    # float64 reference, token order: GEMM row r is token win_to_token(r)
+    dxn_r = dy.double() @ w.double().T                       # [M][Cp] in GEMM-row order
+    if win:
+        ref32 = torch.empty(M, Cp, device=dev)
+        tok = torch.empty(M, 8, device=dev)
+        H.row_copy(torch.arange(M, dtype=torch.float32, device=dev)[:, None].repeat(1, 8).contiguous(), 8, M, 8,
+                   H.copy_desc(tok, win=geo))   # tok[token_to_win(t)] = t
+        perm = tok[:, 0].long().cpu()                      # GEMM row r holds token perm[r]
+        dxn = torch.empty_like(dxn_r)
+        dxn[perm] = dxn_r
+    else:
+        perm = torch.arange(M)
+        dxn = dxn_r
+    xh = (x[:, :C].double() - mu[:, None]) * rs[:, None]
+    gy = dxn[:, :C] * gam.double()
+    dx = rs[:, None] * (gy - gy.mean(1, keepdim=True) - xh * (gy * xh).mean(1, keepdim=True))
+    Dref = D0.double().clone()
+    Dref[:, :C] += dx
+    assert rel(D[:, :C], Dref[:, :C]) < 1e-6 and (D[:, C:] == 0).all()
+    assert rel(dg, (dxn[:, :C] * xh).sum(0)) < 1e-5 and rel(db, dxn[:, :C].sum(0)) < 1e-5
+    if with_copy:
+        want = Dref * sc.double().repeat_interleave(HW)[:M, None]
+        got = (cp[0].double() + cp[1].double()).cpu() * 2.0 ** -20
+        if win:
+            got_tok = torch.empty_like(got)
+            got_tok[perm] = got   # copy row r (window order) holds token perm[r]
+            got = got_tok
+        assert rel(got[:, :C], want[:, :C]) < 1e-6
+
+
 def test_gemm_nt_x3_ring_epilogues():
     """The persistent LDS-DMA ring form of kair_gemm_nt x3 (N % 192 == 0, K % 32 == 0): ragged M with a GELU +
     GELU' epilogue, window-ordered rows of an fp16 pair A with a DropPath-scaled residual, and a flipped 3x3
@@ -521,6 +587,32 @@ def test_swinir_classical_full_x3_vs_oracle():
     gref = dict(ref.named_parameters())
     worst = max((rel(p.grad, gref[k].grad), k) for k, p in net.named_parameters())
     print("classical x4 fp32x3: worst gradient rel", worst)
+    assert worst[0] < 1e-3, worst
+
+
+def test_swinir_x3_lnfuse_engine(monkeypatch):
+    """The opt-in fused LayerNorm backward (KAIR_X3_LNFUSE=1: kair_gemm_nt_x3_lnbwd at both LayerNorms of every Swin
+    block) against the CPU oracle at the fp32 bars: 2 RSTBs of embed 180 (the one-tile C <= 192 the fused epilogue
+    needs), output and every gradient."""
+    monkeypatch.setenv("KAIR_X3_LNFUSE", "1")
+    torch.manual_seed(5)
+    kw = dict(upscale=2, in_chans=3, img_size=16, window_size=8, img_range=1.0, depths=[2, 2], embed_dim=180,
+              num_heads=[6, 6], mlp_ratio=2, upsampler="pixelshuffle", resi_connection="1conv")
+    net = SwinIR(drop_path_rate=0.0, compute_dtype="fp32x3", **kw)
+    ref = osw.SwinIR(2, 3, 16, 8, 1.0, [2, 2], 180, [6, 6], 2, "pixelshuffle")
+    ref.load_state_dict(net.state_dict(), strict=True)
+    g = torch.Generator().manual_seed(6)
+    L, Hh = torch.rand(2, 3, 16, 16, generator=g), torch.rand(2, 3, 32, 32, generator=g)
+    Er = ref(L)
+    torch.nn.functional.l1_loss(Er, Hh).backward()
+    net = net.to(dev).train()
+    assert net.engine().x3_lnfuse
+    E = net(L.to(dev))
+    torch.nn.functional.l1_loss(E, Hh.to(dev)).backward()
+    assert rel(E, Er) < 1e-5
+    gref = dict(ref.named_parameters())
+    worst = max((rel(p.grad, gref[k].grad), k) for k, p in net.named_parameters())
+    print("lnfuse: worst gradient rel", worst)
     assert worst[0] < 1e-3, worst
 
 
