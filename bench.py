@@ -112,6 +112,9 @@ def _alg_bytes(fn, a, kw=None):
         B, S, M, N, K = a[1], a[3], a[4], a[5], a[6]
         kb = B.im_C if B.mode == 1 else K
         return 4 * (M * (_REAL.get(N, N) + _REAL.get(kb, kb)) + S * N * K)
+    if fn == "wgrad_grouped" and a and a[0]._keep[0][0].dtype == 3:   # fp32x3 grouped weight gradients (WgradGroup):
+        grp = a[0]                                                     # every job's two pair operands once
+        return sum(4 * grp.M * (_REAL.get(N, N) + _REAL.get(K, K)) for _, _, N, K, *_ in grp._keep)
     if fn == "window_attn_fwd_x3":    # q, k, v in (fp16 pairs), O out, lse
         nWin, nh, hd = a[5], a[6], a[7]
         M = nWin * T
@@ -140,6 +143,9 @@ def _alg_flops(fn, a):
     if fn == "gemm_tn" and a[7] == X3:
         M, N, K = a[4], a[5], a[6]
         return 2 * M * _REAL.get(N, N) * _REAL.get(K, K) if a[1].mode != 1 else 2 * M * N * K
+    if fn == "wgrad_grouped" and a and a[0]._keep[0][0].dtype == 3:
+        grp = a[0]
+        return sum(2 * grp.M * _REAL.get(N, N) * _REAL.get(K, K) for _, _, N, K, *_ in grp._keep)
     if fn == "window_attn_fwd_x3":
         nWin, nh, hd = a[5], a[6], a[7]
         return nWin * nh * 2 * 2 * T * T * hd
@@ -171,9 +177,10 @@ def _demangle(symbols):
                                                  None) or shutil.which("c++filt")
     out = list(symbols)
     if tool and out:
-        try:
-            res = subprocess.run([tool], input="\n".join(out) + "\n", capture_output=True, text=True, timeout=60)
-            dem = res.stdout.splitlines()
+        try:   # (binutils' demangler predates _Float16's DF16_: spelled as half, then renamed back)
+            res = subprocess.run([tool], input="\n".join(x.replace("DF16_", "Dh") for x in out) + "\n",
+                                 capture_output=True, text=True, timeout=60)
+            dem = [d.replace("half", "_Float16") for d in res.stdout.splitlines()]
             if len(dem) == len(out):
                 out = dem
         except (OSError, subprocess.SubprocessError):
@@ -240,7 +247,7 @@ def time_roles(tr, serial=False, passes=2):
         where = site()
         s0 = H.ktime_count()
         r = run0(self, ws, **kw)
-        rec.append((f"wgrad_grouped @ {where}", "wgrad_grouped", ((), {}), s0, H.ktime_count()))
+        rec.append((f"wgrad_grouped @ {where}", "wgrad_grouped", ((self,), {}), s0, H.ktime_count()))
         return r
     for n in _TIMED:
         setattr(H, n, wrap(n, orig[n]))
@@ -334,17 +341,18 @@ def time_roles(tr, serial=False, passes=2):
     return out_roles, kernels
 
 
-def pmc_traffic(key):
-    """HBM bytes per launch of kernel `key` from the newest committed rocprofv3 PMC summary
-    (profiles/rNN_pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950
-    correction + WRITE_SIZE, KiB -> bytes), or None when absent."""
+def pmc_traffic(*keys):
+    """HBM bytes per launch of the kernel named by any of `keys` (its symbol, its demangled name) from the newest
+    committed rocprofv3 PMC summary (profiles/rNN_pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2
+    per the gfx950 correction + WRITE_SIZE, KiB -> bytes), or None when absent."""
     import glob
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")))
     try:
         with open(paths[-1]) as f:
             rec = json.load(f)
         for name, v in rec["kernels"].items():
-            if key in name:
+            # rocprofv3 names: the symbol (possibly cut at 160 characters) or "void (anonymous namespace)::name(args)"
+            if any(k and (k == name or k.startswith(name) or (k + "(") in name) for k in keys):
                 return v["hbm_bytes_per_launch"]
     except (IndexError, OSError, KeyError, ValueError):
         pass
@@ -723,7 +731,7 @@ def main():
             gbs = d["bytes"] / (ms_b * 1e-3) / 1e9
             r.update({"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
                       "bytes_per_launch": round(d["bytes"]),
-                      "traffic": pmc_traffic(d["symbol"]) if role is None else None})
+                      "traffic": pmc_traffic(d["symbol"], d["kernel"]) if role is None else None})
         else:
             r.update({"achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": None, "traffic": None})
         if d.get("flops") and ms_f:
