@@ -60,6 +60,8 @@ KAIR_DEV f16x8 trfrag(const f16* base, int ld) {
 // NT: 256 threads (2 x 2 waves), BM x BN output tile, k-steps of 32.  B is a split-packed weight: rows of
 // 64-column chunks alternating hi / lo (pack kinds 9 / 17 / 18 / 19, fp16 destination).
 // ------------------------------------------------------------------------------------------
+// (visiting a 3x3 im2col's k-chunks channel-chunk-major -- the nine taps of a 32-channel chunk back to back -- left the
+// 96^2 PixelUnshuffle input gradient at 548 us against 552 tap-major: not what bounds it; profiles/r06_im2col_order_ab.txt)
 template <typename TA, int AM, int BM, int BN>
 __global__ __launch_bounds__(NT, 2) void gemm_nt_x3_kernel(Op A, Op B, Epi E, int K, int tilesN, int nwg) {
   constexpr int BK = 32, LD = BK + 8;

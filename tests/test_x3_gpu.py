@@ -334,6 +334,25 @@ def test_gemm_nt_x3_lnbwd_fused(M, win, with_copy):
         assert rel(got[:, :C], want[:, :C]) < 1e-6
 
 
+@pytest.mark.parametrize("C", [64, 256])
+def test_gemm_nt_x3_im2col_generic(C):
+    """The generic x3 NT kernel on a flipped 3x3 im2col of a C-channel map (the upsampling convs' input gradients)
+    against float64 over ragged tiles (N = 48 of a 64-column tile, M not a multiple of 128)."""
+    g = torch.Generator().manual_seed(41)
+    Bn, Hh, Ww, N = 2, 10, 18, 48
+    M, K = Bn * Hh * Ww, 9 * C
+    x, w = torch.randn(M, C, generator=g), torch.randn(N, K, generator=g) * 0.05
+    Wo, keep = _wsplit(w)
+    A = H.im2col(x.to(dev), Hh, Ww, C, flip=True)
+    A.x3_exp = 4
+    out = torch.empty(M, N, device=dev)
+    H.gemm_nt(A, Wo, H.epilogue(out), M, N, K, H.X3)
+    cols = torch.nn.functional.unfold(x.view(Bn, Hh, Ww, C).permute(0, 3, 1, 2).double(), 3, padding=1)
+    cols = cols.view(Bn, C, 9, Hh * Ww).permute(0, 3, 2, 1).reshape(M, 9, C).flip(1).reshape(M, K)
+    torch.cuda.synchronize()
+    assert rel(out, cols @ w.double().T) < 2e-6
+
+
 def test_gemm_nt_x3_ring_epilogues():
     """The persistent LDS-DMA ring form of kair_gemm_nt x3 (N % 192 == 0, K % 32 == 0): ragged M with a GELU +
     GELU' epilogue, window-ordered rows of an fp16 pair A with a DropPath-scaled residual, and a flipped 3x3
