@@ -401,7 +401,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x3_ring(Op A, Op B, Epi E, int
   static_assert(RI == 1 || RI == 2, "64- or 128-row tiles");
   // EX_LNB: + the row-sum exchange of partner waves ([4 row waves][2 column halves][32 rows][2]) and 8 wave flags
   constexpr int XLDS = EX == EX_LNB ? (4 * 2 * 32 * 2 + 8) * 4 : 0;
-  __shared__ __attribute__((aligned(16))) char smem[NA * XR_ASTAGE + XR_NB * BSTAGE + BN * 4 + XLDS];
+  // (64-row tiles keep the 5-stage A ring: 9 stages in the same LDS measured B = 4 348 -> 343, profiles/r06_nt_ring_depth_ab.txt)
+  __shared__ __attribute__((aligned(16))) char smem[NA * ASTAGE + XR_NB * BSTAGE + BN * 4 + XLDS];
   char* const sA = smem;
   char* const sB = smem + NA * ASTAGE;
   float* const sBias = (float*)(sB + XR_NB * BSTAGE);   // the N-tile's bias (zeros without one), read by the epilogue
