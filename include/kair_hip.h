@@ -319,13 +319,18 @@ int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, const void* d
                          const float* table, const float* lse, void* dqkv, float* dtable, int dtable_accumulate,
                          float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
                          const float* mask, int mask_nw, void* stream);
-/* Same, dqkv_rows != 0 (bf16 only): dqkv written as token rows [nWin*64][3*nh*32] in window order,
- * column (part*nh + h)*32 + d -- the plain A operand of the q/k/v input-gradient GEMM (hipBLASLt)
- * and of the q/k/v weight gradient. */
+/* Same, dqkv_rows != 0 (bf16 only): dqkv written as token rows [nWin*64][3*nh*hp] in window order,
+ * column (part*nh + h)*hp + d -- the plain A operand of the q/k/v input-gradient GEMM and of the q/k/v
+ * weight gradient.  head_pad hp: 32 (the layouts above), or 16 (bf16, head_dim <= 16: every "32" of the
+ * q/k/v, O, dO and dqkv layouts reads 16 -- SwinIR-lightweight's head dim 10, network_swinir.py:85). */
 int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
                             const float* table, const float* lse, void* dqkv, int dqkv_rows, float* dtable,
                             int dtable_accumulate, float* ws, long nWin, int nh, int hd, float scale, int H, int W,
-                            int shift, const float* mask, int mask_nw, void* stream);
+                            int shift, const float* mask, int mask_nw, int head_pad, void* stream);
+/* kair_window_attn_fwd with the head pad explicit (32, or 16 in bf16 as kair_window_attn_bwd_ex). */
+int kair_window_attn_fwd_ex(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
+                            long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
+                            const float* mask, int mask_nw, int head_pad, void* stream);
 
 /* Split-fp16 ("x3", KAIR_COMPUTE_X3) window attention: the fp32 reference's arithmetic on the 16-bit
  * matrix cores.  Every tensor is an fp16 pair of planes holding x 2^e (hi = f16(x 2^e), lo = f16(x 2^e -

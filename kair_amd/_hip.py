@@ -137,7 +137,9 @@ _SIGS = {
     "kair_window_attn_bwd": [c_vp, c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_long, c_int,
                              c_int, c_float, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "kair_window_attn_bwd_ex": [c_vp, c_vp, c_long, c_vp, c_long, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_long,
-                                c_int, c_int, c_float, c_int, c_int, c_int, c_vp, c_int, c_vp],
+                                c_int, c_int, c_float, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp],
+    "kair_window_attn_fwd_ex": [c_vp, c_int, c_vp, c_vp, c_long, c_vp, c_long, c_int, c_int, c_float, c_int, c_int, c_int,
+                                c_int, c_vp, c_int, c_int, c_vp],
     "kair_image_to_nhwc": [c_vp, c_vp, c_int, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
     "kair_image_to_nhwc_hilo": [c_vp, c_vp, c_int, c_vp, c_float, c_int, c_int, c_int, c_int, c_vp],
     "kair_conv3x3_narrow_fwd": [c_vp, c_long, c_int, c_vp, c_vp, c_int, c_vp, c_float, c_vp, c_vp, c_int, c_int, c_int,
@@ -554,10 +556,11 @@ def row_copy(src, ld_src, M, C, copy):
     check(lib().kair_row_copy(ptr(src), ld_src, M, C, ctypes.byref(copy), stream_ptr()), "row_copy")
 
 
-def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, ones_col=-1, mask=None):
+def window_attn_fwd(qkv, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, ones_col=-1, mask=None, head_pad=32):
+    """head_pad: 32, or 16 (bf16, head_dim <= 16): the per-head width of the qkv / O layouts."""
     mnw = mask.shape[0] if mask is not None else 0
-    check(lib().kair_window_attn_fwd(ptr(qkv), dtype_code(qkv), ptr(table), ptr(O), ldo, ptr(lse), nWin, nh, hd, scale,
-                                     H, W, shift, ones_col, ptr(mask), mnw, stream_ptr()), "window_attn_fwd")
+    check(lib().kair_window_attn_fwd_ex(ptr(qkv), dtype_code(qkv), ptr(table), ptr(O), ldo, ptr(lse), nWin, nh, hd, scale,
+                                        H, W, shift, ones_col, ptr(mask), mnw, head_pad, stream_ptr()), "window_attn_fwd")
 
 
 GROUP_MAX = 32   # jobs per kair_ln_param_reduce_grouped / kair_attn_dtable_grouped launch (LNP_MAX, DTAB_MAX)
@@ -593,12 +596,12 @@ def window_attn_bwd_ws(nWin, nh):
 
 
 def window_attn_bwd(qkv, O, ldo, dO, lddo, table, lse, dqkv, dtable, dtable_acc, ws, nWin, nh, hd, scale, H, W, shift,
-                    mask=None, dqkv_rows=False):
-    """dqkv_rows: dqkv as token rows [nWin*64, 3*nh*32] (bf16) instead of head-blocked."""
+                    mask=None, dqkv_rows=False, head_pad=32):
+    """dqkv_rows: dqkv as token rows [nWin*64, 3*nh*head_pad] (bf16) instead of head-blocked."""
     mnw = mask.shape[0] if mask is not None else 0
     check(lib().kair_window_attn_bwd_ex(ptr(qkv), ptr(O), ldo, ptr(dO), lddo, dtype_code(qkv), ptr(table), ptr(lse),
                                         ptr(dqkv), int(dqkv_rows), ptr(dtable), int(dtable_acc), ptr(ws), nWin, nh, hd,
-                                        scale, H, W, shift, ptr(mask), mnw, stream_ptr()), "window_attn_bwd")
+                                        scale, H, W, shift, ptr(mask), mnw, head_pad, stream_ptr()), "window_attn_bwd")
 
 
 def _planes(t):

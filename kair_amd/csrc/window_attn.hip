@@ -190,12 +190,17 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename AT<BF>::T*
 // S^T = K Q^T product consumes), only v staged in LDS (for the transposed P.V fragments), so a
 // wave needs 6 KiB of LDS and 8 waves fit a CU; O is produced transposed (O^T = V^T P^T: lane =
 // query, 4 consecutive d per register group) and stored 8 bytes at a time.
+// HP: the head pad of the q / k / v / O layout -- 32, or 16 for head dims below 16 (SwinIR-lightweight's 10,
+// network_swinir.py:85 with embed_dim 60 / 6 heads): one K = 16 step for S, half the HBM bytes per head; the
+// P.V product keeps its 32-row MFMA tile (rows d >= 16 read zeroed LDS columns and are not stored).
 // ------------------------------------------------------------------------------------------
+template <int HP>
 __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(const bf16* __restrict__ qkv, const float* __restrict__ table,
                                                             bf16* __restrict__ O, long ldo, float* __restrict__ lse,
                                                             long nWin, int nh, float scale, int H, int W, int shift,
                                                             int ones_col, const float* __restrict__ amask, int mask_nw) {
-  constexpr int LD = AT<true>::LD, NW = 4;
+  constexpr int LD = AT<true>::LD, NW = 4, NS = HP / 16;
+  static_assert(HP == 16 || HP == 32, "head pad");
   __shared__ __attribute__((aligned(16))) bf16 sV[NW][TOK * LD];
   __shared__ float sTab[NW][232];
   __shared__ int sReg[NW][TOK];
@@ -205,15 +210,15 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(const bf16* __restri
   const long win = task / nh;
   const int h = (int)(task - win * nh);
   const long M = nWin * TOK;
-  const long blk = (win * nh + h) * TOK * HDP;
-  const long part = M * nh * HDP;
+  const long blk = (win * nh + h) * TOK * HP;
+  const long part = M * nh * HP;
   const int l31 = lane & 31, hh = lane >> 5;
-  bf16x8 Fq[2][2], Fk[2][2], Fv[2][2];
+  bf16x8 Fq[2][NS], Fk[2][NS], Fv[2][NS];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const long o = (long)(t * 32 + l31) * HDP + 16 * s + 8 * hh;
+    for (int s = 0; s < NS; ++s) {
+      const long o = (long)(t * 32 + l31) * HP + 16 * s + 8 * hh;
       Fq[t][s] = *(const bf16x8*)(qkv + blk + o);
       Fk[t][s] = *(const bf16x8*)(qkv + part + blk + o);
       Fv[t][s] = *(const bf16x8*)(qkv + 2 * part + blk + o);
@@ -222,7 +227,10 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(const bf16* __restri
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) *(bf16x8*)(v + (t * 32 + l31) * LD + 16 * s + 8 * hh) = Fv[t][s];
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 z = {};
+      *(bf16x8*)(v + (t * 32 + l31) * LD + 16 * s + 8 * hh) = s < NS ? Fv[t][s < NS ? s : 0] : z;
+    }
   for (int i = lane; i < (2 * WS - 1) * (2 * WS - 1); i += 64) sTab[w][i] = table[i * nh + h];
   const int nW = (H / WS) * (W / WS);
   sReg[w][lane] = shift > 0 ? token_region((int)(win % nW), lane, H, W, shift) : 0;
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(const bf16* __restri
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < NS; ++s)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -290,13 +298,13 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(const bf16* __restri
       for (int s = 0; s < 2; ++s)
         o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_rows_perm(v, kt * 32, s, lane), pack8(acc[kt][qt], s), o, 0, 0, 0);
     const int qi = qt * 32 + l31;
-    bf16* orow = O + (win * TOK + qi) * ldo + h * HDP;
+    bf16* orow = O + (win * TOK + qi) * ldo + h * HP;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < HP / 8; ++g) {
       const int d0 = 8 * g + 4 * hh;
       float r4[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r4[j] = (h * HDP + d0 + j == ones_col) ? 1.f : o[4 * g + j];
+      for (int j = 0; j < 4; ++j) r4[j] = (h * HP + d0 + j == ones_col) ? 1.f : o[4 * g + j];
       const bf16x4 q4 = {(bf16)r4[0], (bf16)r4[1], (bf16)r4[2], (bf16)r4[3]};
       *(bf16x4*)(orow + d0) = q4;
     }
@@ -545,7 +553,7 @@ KAIR_DEV unsigned long long stamp_now() {
 // transposed (D[d][token]: lane = token, 4 consecutive d per register group), so each lane
 // stores 8 bytes at a time instead of 2.
 // ------------------------------------------------------------------------------------------
-template <int NW>
+template <int NW, int HP>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ O,
                                                             long ldo, const bf16* __restrict__ dO, long lddo,
                                                             const float* __restrict__ table, const float* __restrict__ lse,
@@ -553,7 +561,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __re
                                                             long nWin, int nh, int wpg, float scale, int H, int W,
                                                             int shift, const float* __restrict__ amask, int mask_nw,
                                                             int stamp, int rows) {
-  constexpr int LD = AT<true>::LD, LDD = 72, LDB = 72;
+  constexpr int LD = AT<true>::LD, LDD = 72, LDB = 72, NS = HP / 16;
+  static_assert(HP == 16 || HP == 32, "head pad");
   static_assert(TOK * LDD <= 2 * TOK * LD, "the dS tile reuses the q / dO tiles");
   // per wave: q and dO tiles (after dV / dK they hold the dS tile), k tile, and the running bias
   // gradient [q][key] in fp32 (row stride 72: the two lane halves' rows 4 apart fall in opposite
@@ -571,7 +580,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __re
   const int h = (int)(gtask % nh);
   const long grp = gtask / nh;
   const long M = nWin * TOK;
-  const long part = M * nh * HDP;
+  const long part = M * nh * HP;
   const int l31 = lane & 31, hh = lane >> 5;
   bf16* q = sQG[w]; bf16* go = sQG[w] + TOK * LD; bf16* k = sK[w]; bf16* ds = sQG[w];
   float* db = sDB[w];
@@ -579,22 +588,32 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __re
   for (int i = lane; i < TOK * LDB / 4; i += 64) ((float4*)db)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   const int nW = (H / WS) * (W / WS);
 
-  // register fragments of one window: rows t*32 + l31, columns 16 s + 8 hh
-  bf16x8 Fq[2][2], Fk[2][2], Fv[2][2], Fg[2][2], Fo[2][2];
+  // register fragments of one window: rows t*32 + l31, columns 16 s + 8 hh.  HP = 16: the q / k / dO LDS tiles'
+  // columns 16..31 feed only the transposed products' rows d >= 16, which are not stored; zeroed once so those
+  // rows start from defined values (later windows leave the finite dS tile there)
+  if constexpr (HP == 16) {
+    const bf16x8 z = {};
+    for (int i = lane; i < 3 * TOK * 2; i += 64) {
+      const int r = i >> 1;
+      bf16* t = r < 2 * TOK ? sQG[w] + r * LD : sK[w] + (r - 2 * TOK) * LD;
+      *(bf16x8*)(t + 16 + 8 * (i & 1)) = z;
+    }
+  }
+  bf16x8 Fq[2][NS], Fk[2][NS], Fv[2][NS], Fg[2][NS], Fo[2][NS];
   float Fl[2];
-  auto ldfrag = [&](const bf16* g, long ld, bf16x8 (&f)[2][2]) {
+  auto ldfrag = [&](const bf16* g, long ld, bf16x8 (&f)[2][NS]) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) f[t][s] = *(const bf16x8*)(g + (long)(t * 32 + l31) * ld + 16 * s + 8 * hh);
+      for (int s = 0; s < NS; ++s) f[t][s] = *(const bf16x8*)(g + (long)(t * 32 + l31) * ld + 16 * s + 8 * hh);
   };
   auto load_win = [&](long win) {
-    const long blk = (win * nh + h) * TOK * HDP;
-    ldfrag(qkv + blk, HDP, Fq);
-    ldfrag(qkv + part + blk, HDP, Fk);
-    ldfrag(qkv + 2 * part + blk, HDP, Fv);
-    ldfrag(dO + win * TOK * lddo + h * HDP, lddo, Fg);
-    ldfrag(O + win * TOK * ldo + h * HDP, ldo, Fo);
+    const long blk = (win * nh + h) * TOK * HP;
+    ldfrag(qkv + blk, HP, Fq);
+    ldfrag(qkv + part + blk, HP, Fk);
+    ldfrag(qkv + 2 * part + blk, HP, Fv);
+    ldfrag(dO + win * TOK * lddo + h * HP, lddo, Fg);
+    ldfrag(O + win * TOK * ldo + h * HP, ldo, Fo);
 #pragma unroll
     for (int t = 0; t < 2; ++t) Fl[t] = lse[(win * nh + h) * TOK + t * 32 + l31];
   };
@@ -608,12 +627,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __re
   for (long win = w0; win < w1; ++win) {
     const bool st_on = stamping && win == w0 + 2;
     if (st_on) ts[0] = stamp_now();
-    const long blk = (win * nh + h) * TOK * HDP;
+    const long blk = (win * nh + h) * TOK * HP;
     wave_sync();   // the previous window's LDS tiles are no longer read
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < NS; ++s) {
         const int o = (t * 32 + l31) * LD + 16 * s + 8 * hh;
         *(bf16x8*)(q + o) = Fq[t][s];
         *(bf16x8*)(k + o) = Fk[t][s];
@@ -623,7 +642,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __re
     for (int t = 0; t < 2; ++t) {
       float d = 0.f;
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 8; ++j) d += (float)Fg[t][s][j] * (float)Fo[t][s][j];
       d += __shfl_xor(d, 32, 64);
@@ -644,7 +663,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __re
 #pragma unroll
         for (int r = 0; r < 16; ++r) { S[a][b][r] = 0.f; dP[a][b][r] = 0.f; }
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
@@ -714,10 +733,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __re
     // dV^T = dO^T P and dK^T = scale * Q^T dS : tiles [kt], rows = d, lane = key
     // head-blocked [3][nWin][nh][64][32] (token stride 32), or token rows [M][3 nh 32] (rows != 0:
     // columns (part * nh + h) * 32 + d, the q/k/v input-gradient GEMM's plain A operand)
-    const long tstr = rows ? 3L * nh * HDP : HDP;
-    bf16* dq_out = rows ? dqkv + win * TOK * tstr + h * HDP : dqkv + blk;
-    bf16* dk_out = rows ? dq_out + nh * HDP : dqkv + part + blk;
-    bf16* dv_out = rows ? dq_out + 2 * nh * HDP : dqkv + 2 * part + blk;
+    const long tstr = rows ? 3L * nh * HP : HP;
+    bf16* dq_out = rows ? dqkv + win * TOK * tstr + h * HP : dqkv + blk;
+    bf16* dk_out = rows ? dq_out + nh * HP : dqkv + part + blk;
+    bf16* dv_out = rows ? dq_out + 2 * nh * HP : dqkv + 2 * part + blk;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       f32x16 av, ak;
@@ -732,7 +751,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __re
         }
       const int key = kt * 32 + l31;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < HP / 8; ++g) {
         const bf16x4 vv = {(bf16)av[4 * g], (bf16)av[4 * g + 1], (bf16)av[4 * g + 2], (bf16)av[4 * g + 3]};
         const bf16x4 kk = {(bf16)(ak[4 * g] * scale), (bf16)(ak[4 * g + 1] * scale), (bf16)(ak[4 * g + 2] * scale),
                            (bf16)(ak[4 * g + 3] * scale)};
@@ -762,7 +781,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(const bf16* __re
                                                     aq, 0, 0, 0);
       const int qi = qt * 32 + l31;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < HP / 8; ++g) {
         const bf16x4 vq = {(bf16)(aq[4 * g] * scale), (bf16)(aq[4 * g + 1] * scale), (bf16)(aq[4 * g + 2] * scale),
                            (bf16)(aq[4 * g + 3] * scale)};
         *(bf16x4*)(dq_out + qi * tstr + 8 * g + 4 * hh) = vq;
@@ -846,28 +865,41 @@ static long bwd_groups(long nWin, int wpg) { return (nWin + wpg - 1) / wpg; }
 
 }  // namespace
 
-extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
-                                    long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
-                                    const float* mask, int mask_nw, void* stream) {
+extern "C" int kair_window_attn_fwd_ex(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
+                                       long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
+                                       const float* mask, int mask_nw, int head_pad, void* stream) {
   KAIR_CHECK_ARG(!mask || (mask_nw > 0 && shift == 0), "window_attn_fwd: an explicit mask needs mask_nw > 0 and shift 0");
   KAIR_CHECK_ARG(qkv && table && O && lse, "window_attn_fwd: null pointer");
-  KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_fwd: head_dim %d must be <= 32", hd);
+  KAIR_CHECK_ARG(head_pad == HDP || (head_pad == 16 && dtype == KAIR_BF16), "window_attn_fwd: head pad %d (32, or 16 in bf16)",
+                 head_pad);
+  const int hp = head_pad;
+  KAIR_CHECK_ARG(hd > 0 && hd <= hp && nh > 0 && nWin > 0, "window_attn_fwd: head_dim %d must be <= %d", hd, hp);
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)),
                  "window_attn_fwd: grid %dx%d / shift %d", H, W, shift);
-  KAIR_CHECK_ARG(ldo >= nh * HDP && ldo % 8 == 0, "window_attn_fwd: ldo");
-  KAIR_CHECK_ARG(ones_col < 0 || (ones_col < nh * HDP && ones_col % HDP >= hd), "window_attn_fwd: ones column must be a pad column");
+  KAIR_CHECK_ARG(ldo >= nh * hp && ldo % 8 == 0, "window_attn_fwd: ldo");
+  KAIR_CHECK_ARG(ones_col < 0 || (ones_col < nh * hp && ones_col % hp >= hd), "window_attn_fwd: ones column must be a pad column");
   const long tasks = nWin * nh;
   const int nw = dtype == KAIR_BF16 ? NWAVES<true> : NWAVES<false>;
   const long nb = (tasks + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == KAIR_BF16)
-    KAIR_LAUNCH(attn_fwd_bf16_kernel, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
+  if (dtype == KAIR_BF16 && hp == 16)
+    KAIR_LAUNCH(attn_fwd_bf16_kernel<16>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
+                       lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
+  else if (dtype == KAIR_BF16)
+    KAIR_LAUNCH(attn_fwd_bf16_kernel<32>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
                        lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
   else
     KAIR_LAUNCH(attn_fwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, table, (float*)O,
                        ldo, lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
   KAIR_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int kair_window_attn_fwd(const void* qkv, int dtype, const float* table, void* O, long ldo, float* lse,
+                                    long nWin, int nh, int hd, float scale, int H, int W, int shift, int ones_col,
+                                    const float* mask, int mask_nw, void* stream) {
+  return kair_window_attn_fwd_ex(qkv, dtype, table, O, ldo, lse, nWin, nh, hd, scale, H, W, shift, ones_col, mask, mask_nw,
+                                 HDP, stream);
 }
 
 static const int g_stamp = kair_dbg_env("KAIR_ATTN_STAMP");
@@ -905,11 +937,13 @@ int kair_attn_dtable_sum(const float* ws, long ngroups, int nh, float* dtable, i
 extern "C" int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo, const void* dO, long lddo, int dtype,
                                        const float* table, const float* lse, void* dqkv, int dqkv_rows, float* dtable,
                                        int dtable_accumulate, float* ws, long nWin, int nh, int hd, float scale, int H, int W,
-                                       int shift, const float* mask, int mask_nw, void* stream) {
+                                       int shift, const float* mask, int mask_nw, int head_pad, void* stream) {
   KAIR_CHECK_ARG(!dqkv_rows || dtype == KAIR_BF16, "window_attn_bwd: token-row dqkv is a bf16 layout");
+  KAIR_CHECK_ARG(head_pad == HDP || (head_pad == 16 && dtype == KAIR_BF16), "window_attn_bwd: head pad %d (32, or 16 in bf16)",
+                 head_pad);
   KAIR_CHECK_ARG(!mask || (mask_nw > 0 && shift == 0), "window_attn_bwd: an explicit mask needs mask_nw > 0 and shift 0");
   KAIR_CHECK_ARG(qkv && O && dO && table && lse && dqkv && ws, "window_attn_bwd: null pointer");
-  KAIR_CHECK_ARG(hd > 0 && hd <= HDP && nh > 0 && nWin > 0, "window_attn_bwd: head_dim");
+  KAIR_CHECK_ARG(hd > 0 && hd <= head_pad && nh > 0 && nWin > 0, "window_attn_bwd: head_dim");
   KAIR_CHECK_ARG(H % WS == 0 && W % WS == 0 && (shift == 0 || (shift > 0 && shift < WS)), "window_attn_bwd: geometry");
   KAIR_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0, "window_attn_bwd: strides");
   const int wpg = dtype == KAIR_BF16 ? bwd_wpg_bf16(nWin, nh) : WPG;
@@ -917,12 +951,16 @@ extern "C" int kair_window_attn_bwd_ex(const void* qkv, const void* O, long ldo,
   const int nw = dtype == KAIR_BF16 ? g_bwd_nw : NWAVES<false>;
   const long nb = (ngroups * nh + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == KAIR_BF16 && nw == 2)
-    KAIR_LAUNCH(attn_bwd_bf16_kernel<2>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
+  if (dtype == KAIR_BF16 && head_pad == 16)
+    KAIR_LAUNCH((attn_bwd_bf16_kernel<2, 16>), dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O,
+                       ldo, (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask,
+                       mask_nw, g_stamp, dqkv_rows);
+  else if (dtype == KAIR_BF16 && nw == 2)
+    KAIR_LAUNCH((attn_bwd_bf16_kernel<2, 32>), dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
                        (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw,
                        g_stamp, dqkv_rows);
   else if (dtype == KAIR_BF16)
-    KAIR_LAUNCH(attn_bwd_bf16_kernel<4>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
+    KAIR_LAUNCH((attn_bwd_bf16_kernel<4, 32>), dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, (const bf16*)O, ldo,
                        (const bf16*)dO, lddo, table, lse, (bf16*)dqkv, ws, nWin, nh, wpg, scale, H, W, shift, mask, mask_nw,
                        g_stamp, dqkv_rows);
   else
@@ -941,7 +979,7 @@ extern "C" int kair_window_attn_bwd(const void* qkv, const void* O, long ldo, co
                                     float* ws, long nWin, int nh, int hd, float scale, int H, int W, int shift,
                                     const float* mask, int mask_nw, void* stream) {
   return kair_window_attn_bwd_ex(qkv, O, ldo, dO, lddo, dtype, table, lse, dqkv, 0, dtable, dtable_accumulate, ws, nWin, nh,
-                                 hd, scale, H, W, shift, mask, mask_nw, stream);
+                                 hd, scale, H, W, shift, mask, mask_nw, HDP, stream);
 }
 
 extern "C" long kair_window_attn_bwd_groups(long nWin, int nh, int dtype) {

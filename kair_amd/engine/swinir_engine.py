@@ -257,8 +257,9 @@ class _Blk:
         sp = eng.split_linear
         fa, fm, fb, rg = eng.fused_attn, eng.fused_mlp, eng.fused_mlp_bwd, eng.rowgemm
         # frag_t (pack kind 13): the input-gradient operand of the row GEMMs / the fused MLP backward
-        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, 32), (1, C, Cp), frag=fa, split=sp, rows=not fa, frag_t=rg)
-        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, 32), frag=fa, split=sp, rows=not fa, frag_t=rg)
+        hp = eng.hp
+        self.qkv = _Lin(eng, blk.attn.qkv, (3 * nh, hd, hp), (1, C, Cp), frag=fa, split=sp, rows=not fa, frag_t=rg)
+        self.proj = _Lin(eng, blk.attn.proj, (1, C, Cp), (nh, hd, hp), frag=fa, split=sp, rows=not fa, frag_t=rg)
         self.fc1 = _Lin(eng, blk.mlp.fc1, (1, Hd, eng.Hdp), (1, C, Cp), frag=fm, split=sp, frag_t=fb or rg, rows=not fm)
         self.fc2 = _Lin(eng, blk.mlp.fc2, (1, C, Cp), (1, Hd, eng.Hdp), frag=fm, split=sp, frag_t=fb or rg, rows=not fm,
                         frag16=True)
@@ -270,7 +271,7 @@ class _Blk:
 class SwinIREngine:
     def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True, fused_mlp=None,
                  split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=None, side_priority=0,
-                 split_act=True, conv_wr=True):
+                 split_act=True, conv_wr=True, head_pad=None):
         """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
         see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
         fused block kernels (_Lin, pack kind 12).
@@ -326,6 +327,13 @@ class SwinIREngine:
         if fused_mlp is None:
             fused_mlp = fused_blocks
         self.fused_mlp = bool(fused_mlp) and compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384
+        # head pad of the q/k/v / O / dO layouts: 16 for head dims below 16 on the unfused bf16 path (SwinIR-lightweight,
+        # 60 / 6 = 10: half the attention bytes of a 32 pad, kair_window_attn_fwd_ex), else 32; head_pad=32 forces the
+        # wide layout (A/B timing, parity of both layouts)
+        hp16 = compute_dtype == "bf16" and hd < 16 and not self.fused_attn and not (self.Cp == 192 and self.Hdp == 384)
+        self.hp = 16 if hp16 and head_pad in (None, 16) else 32
+        if head_pad not in (None, 16, 32) or (head_pad == 16 and self.hp != 16):
+            raise ValueError(f"head_pad {head_pad}: 32, or 16 for bf16 head dims below 16 on the unfused path")
         # the MLP-half backward kernel: off by default -- 205 us per block at B = 32 against 172-186 us
         # for the fc2 / fc1 input-gradient GEMMs + LN2 backward it replaces (its memory
         # waves' LayerNorm rows and the tile loads run latency-exposed); fused_mlp_bwd=True enables it
@@ -339,7 +347,7 @@ class SwinIREngine:
         # fc2 (GELU' gate), fc1 + LayerNorm-2 backward, proj, q/k/v + LayerNorm-1 backward -- bf16, Cp = 192
         # geometry (classical / real-world x4); other widths run the same products on kair_gemm_nt +
         # kair_layernorm_bwd.  No library GEMM is on the training path.
-        self.rowgemm = (compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384 and self.nh * 32 == self.Cp)
+        self.rowgemm = (compute_dtype == "bf16" and self.Cp == 192 and self.Hdp == 384 and self.nh * self.hp == self.Cp)
         self.upsampler, self.scale = net.upsampler, net.upscale
         self.in_ch = net.conv_first.in_channels
         self.img_range = float(net.img_range)
@@ -404,7 +412,7 @@ class SwinIREngine:
         # launch (kair_wgrad_grouped: 4 linears x depth blocks) where the bf16 TN ring takes the shapes;
         # otherwise one gemm_tn + finalize per linear, issued in place
         self.grouped_wgrad = (self.tdt == torch.bfloat16 and self.Cp > 64 and self.Hdp <= 576 and
-                              3 * self.nh * 32 <= 576 and
+                              3 * self.nh * self.hp <= 576 and
                               max(len(l.residual_group.blocks) for l in net.layers) <= H.WgradGroup.WG_MAX // 4)
         self._wg_pending = []
         self._lnp_pending = []    # (partials, M, C, dgamma, dbeta, accumulate) of the RSTB's LayerNorms
@@ -510,7 +518,7 @@ class SwinIREngine:
         B, Hh, Ww = key
         dev, T, f32 = self.device, self.tdt, torch.float32
         M = B * Hh * Ww
-        Cp, Hdp, nh = self.Cp, self.Hdp, self.nh
+        Cp, Hdp, nh, hp = self.Cp, self.Hdp, self.nh, self.hp
         nWin = M // WS_TOK
         e = lambda *s, dt=f32: torch.empty(*s, device=dev, dtype=dt)
         hf = torch.float16
@@ -532,8 +540,8 @@ class SwinIREngine:
             pr = (lambda *sh: e(2, *sh, dt=hf)) if self.x3 else (lambda *sh: e(*sh, dt=T))
             blocks.append({
                 "mid": e(M, Cp), "out": e(M, Cp), "ln1": pr(M, Cp), "m1": e(M), "r1": e(M),
-                "qkv": e(2, 3 * M * nh * 32, dt=hf) if self.x3 else e(3 * M * nh * 32, dt=T),
-                "O": pr(M, nh * 32), "lse": e(nWin * nh * WS_TOK),
+                "qkv": e(2, 3 * M * nh * hp, dt=hf) if self.x3 else e(3 * M * nh * hp, dt=T),
+                "O": pr(M, nh * hp), "lse": e(nWin * nh * WS_TOK),
                 "ln2": pr(M, Cp), "m2": e(M), "r2": e(M), "u": e(M, Hdp, dt=T), "h": pr(M, Hdp)})
         P["blocks"] = blocks
         P["rstb_out"] = [e(M, Cp) for _ in range(min(2, len(self.rstb)) if infer else len(self.rstb))]
@@ -591,16 +599,16 @@ class SwinIREngine:
         # Two sets (RSTB parity): the side stream still reads one RSTB's while the next RSTB writes the other.
         P["gw"] = [[{"Dm": zp(M, Cp), "Da": zp(M, Cp), "dU": ep(M, Hdp),
                      # fp32x3: dq/dk/dv as token rows [M][3 nh 32] (pairs: the ring GEMMs' operand)
-                     "dqkv": ep(M, 3 * nh * 32) if self.x3 else e(3 * M * nh * 32, dt=T),
+                     "dqkv": ep(M, 3 * nh * hp) if self.x3 else e(3 * M * nh * hp, dt=T),
                      # LN1 / LN2 parameter partials and the attention bias-table partials of the block, reduced
                      # by one grouped launch each at the end of the RSTB
                      "ln1p": e(lnp), "ln2p": e(lnp), "attn_ws": e(H.window_attn_bwd_ws(nWin, nh))}
                     for _ in range(depth)] for _ in range(2)]
         P["G3"] = z32(M, Cp)   # third residual-gradient buffer (rotation, see backward())
         if self.rowgemm:   # LayerNorm-parameter partial rows the fused row GEMMs leave (<= the ln*p buffers' 2048)
-            P["rg_nb"] = {k: H.rowgemm_ln_blocks(M, k) for k in (Hdp, 3 * nh * 32)}
+            P["rg_nb"] = {k: H.rowgemm_ln_blocks(M, k) for k in (Hdp, 3 * nh * hp)}
             assert max(P["rg_nb"].values()) <= 2048, P["rg_nb"]
-        P["dO"] = e(2, M, nh * 32, dt=hf) if self.x3 else e(M, nh * 32, dt=T)
+        P["dO"] = e(2, M, nh * hp, dt=hf) if self.x3 else e(M, nh * hp, dt=T)
         P["ln_ws"] = e(2 * 2048 * Cp)   # kair_layernorm_bwd: 2 * 2048 * C floats
         P["attn_ws"] = e(H.window_attn_bwd_ws(nWin, nh))
         P["loss"] = e(1)
@@ -667,7 +675,7 @@ class SwinIREngine:
 
         for blks, conv in self.rstb:
             for _ in blks:
-                out += [(M, Cp, Hdp), (M, Hdp, Cp), (M, Cp, nh * 32), (M, 3 * nh * 32, Cp)]
+                out += [(M, Cp, Hdp), (M, Hdp, Cp), (M, Cp, nh * self.hp), (M, 3 * nh * self.hp, Cp)]
             out += resi(conv)
         out += resi(self.cab)
         if self.upsampler == "nearest+conv":
@@ -691,7 +699,7 @@ class SwinIREngine:
         if self.grouped_wgrad or self.x3_grouped:
             Cp, Hdp, nh = self.Cp, self.Hdp, self.nh
             depth = max(len(blks) for blks, _ in self.rstb)
-            shapes = [(Cp, Hdp), (Hdp, Cp), (Cp, nh * 32), (3 * nh * 32, Cp)] * depth
+            shapes = [(Cp, Hdp), (Hdp, Cp), (Cp, nh * self.hp), (3 * nh * self.hp, Cp)] * depth
             for i in range(0, len(shapes), H.WgradGroup.WG_MAX):
                 ws = max(ws, H.wgrad_grouped_ws(shapes[i:i + H.WgradGroup.WG_MAX], M, x3=self.x3))
         return ws
@@ -929,7 +937,7 @@ class SwinIREngine:
 
     def _block_fwd(self, blk, P, S, x, bi):
         cd = self.cd
-        M, Cp, nh, Hh, Ww = P["M"], self.Cp, self.nh, P["H"], P["W"]
+        M, Cp, nh, hp, Hh, Ww = P["M"], self.Cp, self.nh, self.hp, P["H"], P["W"]
         HW = Hh * Ww
         win = (Hh, Ww, 8, blk.shift)
         drop = P["drop"]
@@ -959,13 +967,13 @@ class SwinIREngine:
                 A_o = self._op(S["O"])
             else:
                 self._nt(H.rows(S["ln1"]), H.rows(l.Wp), H.epilogue(S["qkv"], mode=H.OUT_QKVBLK, ldo=0, bias=l.bp,
-                                                                     qkv=(nh, 32, WS_TOK)), M, l.Np, Cp, cd)
-                H.window_attn_fwd(S["qkv"], blk.table, S["O"], nh * 32, S["lse"], P["nWin"], nh, self.C // nh, blk.scale,
-                                  Hh, Ww, blk.shift, ones_col=self.C // nh)
+                                                                     qkv=(nh, hp, WS_TOK)), M, l.Np, Cp, cd)
+                H.window_attn_fwd(S["qkv"], blk.table, S["O"], nh * hp, S["lse"], P["nWin"], nh, self.C // nh, blk.scale,
+                                  Hh, Ww, blk.shift, ones_col=self.C // nh, head_pad=hp)
                 A_o = H.rows(S["O"])
             l = blk.proj
             self._nt(A_o, H.rows(l.Wp), H.epilogue(S["mid"], win=win, bias=l.bp, resid=x, rowscale=s_attn,
-                                                  rows_per_scale=HW), M, Cp, nh * 32, cd)
+                                                  rows_per_scale=HW), M, Cp, nh * hp, cd)
         if self.fused_mlp:   # LN2 -> fc1 + GELU -> fc2 + residual in one launch
             f1, f2 = blk.fc1, blk.fc2
             H.swin_mlp_fwd(S["mid"], Cp, blk.n2.weight, blk.n2.bias, blk.n2.eps, self.C, S["ln2"], Cp, S["m2"], S["r2"],
@@ -979,9 +987,9 @@ class SwinIREngine:
             H.layernorm_fwd(S["mid"], Cp, S["ln2"], Cp, blk.n2.weight, blk.n2.bias, S["m2"], S["r2"], M, self.C, blk.n2.eps,
                             one_col=self.C)
         l = blk.fc1
-        hp = S["h"]
-        E1 = (H.epilogue(hp[0], out_lo=hp[1], bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N, pre_grad=True)
-              if self.x3 else H.epilogue(hp, bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N, pre_grad=True))
+        hb = S["h"]
+        E1 = (H.epilogue(hb[0], out_lo=hb[1], bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N, pre_grad=True)
+              if self.x3 else H.epilogue(hb, bias=l.bp, act=H.ACT_GELU, pre=S["u"], ones_col=l.N, pre_grad=True))
         self._nt(self._op(S["ln2"]), H.rows(l.Wp), E1, M, l.Np, Cp, cd)
         l = blk.fc2
         self._nt(self._op(S["h"]), H.rows(l.Wp), H.epilogue(S["out"], bias=l.bp, resid=S["mid"], rowscale=s_mlp,
@@ -1342,16 +1350,17 @@ class SwinIREngine:
         if self.x3:
             self._block_bwd_attn_x3(blk, P, S, x_in, D, bi, grads, j, par)
             return
-        self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * 32, proj, grads, hd)
+        hp = self.hp
+        self._wg(P, H.rows(Da), H.rows(S["O"], ones_col=hd, ones_in_data=True), Cp, nh * hp, proj, grads, hd)
         if self.rowgemm:
             H.rowgemm_store(Da, M, Cp, proj.Wgt, Cp, P["dO"])
         else:
-            self._nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * 32, Cp, cd)
+            self._nt(H.rows(Da), H.rows(proj.Wt), H.epilogue(P["dO"]), M, nh * hp, Cp, cd)
         rows = self.rowgemm   # dq/dk/dv as token rows [M][3 nh 32]: the row GEMM's A operand
-        H.window_attn_bwd(S["qkv"], S["O"], nh * 32, P["dO"], nh * 32, blk.table, S["lse"], dqkv, None, False,
-                          W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, dqkv_rows=rows)
+        H.window_attn_bwd(S["qkv"], S["O"], nh * hp, P["dO"], nh * hp, blk.table, S["lse"], dqkv, None, False,
+                          W["attn_ws"], P["nWin"], nh, hd, blk.scale, Hh, Ww, blk.shift, dqkv_rows=rows, head_pad=hp)
         self._dtab_pending.append((W["attn_ws"], P["nWin"], nh, self.cd, g(blk.table), False))
-        A_qkv = H.rows(dqkv.view(M, qkv.Np)) if rows else H.qkvblk(dqkv, nh)
+        A_qkv = H.rows(dqkv.view(M, qkv.Np)) if rows else H.qkvblk(dqkv, nh, hdp=hp)
         self._wg(P, A_qkv, H.rows(S["ln1"], ones_col=self.C, ones_in_data=True), qkv.Np, Cp, qkv, grads, self.C)
         n = blk.n1
         cp = None
@@ -1364,7 +1373,7 @@ class SwinIREngine:
                             W["ln1p"], win=win, copy=cp)
             self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False, P["rg_nb"][qkv.Np]))
         else:
-            self._nt(H.qkvblk(dqkv, nh), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
+            self._nt(H.qkvblk(dqkv, nh, hdp=hp), H.rows(qkv.Wt), H.epilogue(P["dxn"]), M, Cp, qkv.Np, cd)
             H.layernorm_bwd(x_in, Cp, P["dxn"], Cp, n.weight, S["m1"], S["r1"], D, Cp, True, None, None, False,
                             W["ln1p"], M, self.C, win, copy=cp)
             self._lnp_pending.append((W["ln1p"], M, self.C, g(n.weight), g(n.bias), False))

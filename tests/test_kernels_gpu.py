@@ -429,6 +429,79 @@ def test_window_attention_fwd_bwd(dtype, shift):
         assert torch.equal(dr.cpu(), blocked)
 
 
+@pytest.mark.parametrize("hd", [10, 15, 16])
+@pytest.mark.parametrize("shift", [0, 4])
+def test_window_attention_head_pad16(hd, shift):
+    """bf16, head pad 16 (kair_window_attn_fwd_ex / _bwd_ex head_pad=16; SwinIR-lightweight's head dim 10,
+    network_swinir.py:85): against the fp32 autograd reference at the bf16 bars of the pad-32 test, and bit-equal
+    to the pad-32 kernels on the same values (the pad-32 tiles' columns 16..31 are zeros, so both contract the
+    same products in the same order).  The ones column (proj bias gradient) lands in the pad."""
+    B, Hh, Ww, nh = 2, 16, 24, 6
+    nWin = B * (Hh // 8) * (Ww // 8)
+    scale = hd ** -0.5
+    g = torch.Generator().manual_seed(23)
+    q, k, v = (torch.randn(nWin, nh, 64, hd, generator=g).bfloat16().float() for _ in range(3))
+    table = torch.randn(225, nh, generator=g) * 0.5
+    qr, kr, vr, tr = (t.clone().requires_grad_(True) for t in (q, k, v, table))
+    o = _attn_ref(qr, kr, vr, tr, nh, shift, Hh, Ww, scale)
+    go = torch.randn(o.shape, generator=g).bfloat16().float()
+    o.backward(go)
+    ones = hd if hd < 16 else -1
+    res = {}
+    for hp in (16, 32):
+        qkv = torch.zeros(3, nWin, nh, 64, hp)
+        qkv[0, ..., :hd], qkv[1, ..., :hd], qkv[2, ..., :hd] = q, k, v
+        qkv_d = qkv.to(dev, torch.bfloat16).contiguous()
+        O = torch.full((nWin * 64, nh * hp), float("nan"), device=dev, dtype=torch.bfloat16)
+        lse = torch.empty(nWin, nh, 64, device=dev)
+        H.window_attn_fwd(qkv_d, table.to(dev), O, nh * hp, lse, nWin, nh, hd, scale, Hh, Ww, shift, ones_col=ones,
+                          head_pad=hp)
+        dO = torch.zeros(nWin, 64, nh, hp)
+        dO[..., :hd] = go.permute(0, 2, 1, 3)
+        dO_d = dO.view(nWin * 64, nh * hp).to(dev, torch.bfloat16)
+        dqkv = torch.full_like(qkv_d, float("nan"))
+        dr = torch.full((nWin * 64, 3 * nh * hp), float("nan"), device=dev, dtype=torch.bfloat16)
+        dtab = torch.empty(225, nh, device=dev)
+        ws = torch.empty(H.window_attn_bwd_ws(nWin, nh), device=dev)
+        H.window_attn_bwd(qkv_d, O, nh * hp, dO_d, nh * hp, table.to(dev), lse, dqkv, dtab, False, ws, nWin, nh, hd,
+                          scale, Hh, Ww, shift, head_pad=hp)
+        dtab1 = dtab.clone()
+        H.window_attn_bwd(qkv_d, O, nh * hp, dO_d, nh * hp, table.to(dev), lse, dr, dtab, False, ws, nWin, nh, hd,
+                          scale, Hh, Ww, shift, dqkv_rows=True, head_pad=hp)
+        torch.cuda.synchronize()
+        Ov = O.cpu().view(nWin, 64, nh, hp)
+        res[hp] = (Ov[..., :hd], lse.cpu(), dqkv.cpu()[..., :hd], dtab1.cpu(),
+                   dr.cpu().view(nWin, 64, 3, nh, hp)[..., :hd])
+        if hp == 16:
+            got = Ov[..., :hd].float().permute(0, 2, 1, 3)
+            assert rel_err(got, o.detach()) < 1.5e-2
+            if ones >= 0:   # pad columns: the ones column of head 0, zeros elsewhere
+                pad = Ov[..., hd:].float()
+                assert pad[:, :, 0, 0].eq(1).all() and pad[:, :, 0, 1:].eq(0).all() and pad[:, :, 1:].eq(0).all()
+            d = dqkv.float().cpu()
+            for i, ref in enumerate((qr.grad, kr.grad, vr.grad)):
+                assert rel_err(d[i, ..., :hd], ref) < 3e-2
+            assert rel_err(dtab1.cpu(), tr.grad) < 3e-2
+            blocked = dqkv.cpu().permute(1, 3, 0, 2, 4)   # [win][tok][part][h][d]
+            assert torch.equal(dr.cpu().view(nWin, 64, 3, nh, hp), blocked)
+    for a, b in zip(res[16], res[32]):
+        assert torch.equal(a, b)
+
+
+def test_window_attention_head_pad_checks():
+    """head_pad 16 is a bf16 layout; the head dim must fit the pad."""
+    nWin, nh = 2, 2
+    qkv = torch.zeros(3 * nWin * nh * 64 * 16, device=dev)
+    O = torch.zeros(nWin * 64, nh * 16, device=dev)
+    lse = torch.empty(nWin * nh * 64, device=dev)
+    tab = torch.zeros(225, nh, device=dev)
+    with pytest.raises(RuntimeError, match="head pad"):
+        H.window_attn_fwd(qkv, tab, O, nh * 16, lse, nWin, nh, 10, 0.3, 8, 16, 0, head_pad=16)
+    qb, Ob = qkv.bfloat16(), O.bfloat16()
+    with pytest.raises(RuntimeError, match="head_dim"):
+        H.window_attn_fwd(qb, tab, Ob, nh * 16, lse, nWin, nh, 20, 0.3, 8, 16, 0, head_pad=16)
+
+
 @pytest.mark.parametrize("charb", [False, True])
 def test_pixel_loss_bf16_rows(charb):
     """The training step's loss layout (bf16 dE rows of 16 slots, r = 1: kair_l1_loss's pixel-per-thread

@@ -36,9 +36,10 @@ def timed(step, steps, warmup):
     return (time.perf_counter() - t0) / steps, out
 
 
-def run(name, steps, warmup, dev, dtype="bf16"):
+def run(name, steps, warmup, dev, dtype="bf16", head_pad=None):
     """dtype: the engine's compute dtype -- "bf16" (bf16 MFMA, fp32 accumulation), "fp32" (exact fp32 MFMA: the
-    reference's arithmetic for the fp32 option files, C3 / C5) or "fp32x3" where the engine has it."""
+    reference's arithmetic for the fp32 option files, C3 / C5) or "fp32x3" where the engine has it.
+    head_pad (SwinIR): the engine's q/k/v head pad (None: its choice -- 16 for C2's head dim 10; 32: A/B)."""
     from kair_amd.engine.trainer import FusedTrainer
     torch.manual_seed(0)
     g = torch.Generator().manual_seed(1)
@@ -62,6 +63,9 @@ def run(name, steps, warmup, dev, dtype="bf16"):
         raise SystemExit(f"unknown config {name}")
     net, ema = mk().to(dev).train(), mk().to(dev).eval()
     ema.load_state_dict(net.state_dict())
+    if head_pad is not None:
+        from kair_amd.engine.swinir_engine import SwinIREngine
+        net._engine = SwinIREngine(net, dtype, net.split_conv, net.fused_blocks, head_pad=head_pad)
     tr = FusedTrainer(net, ema, lr=1e-4, E_decay=0.999, use_graph=True)
     L = torch.rand(B, *shp, generator=g).to(dev)
     Hh = torch.rand(B, shp[0], shp[1] * sc, shp[2] * sc, generator=g).to(dev)
@@ -93,10 +97,11 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3"])
+    ap.add_argument("--head-pad", type=int, default=None, choices=[16, 32])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for name in a.configs:
-        B, dt, loss = run(name, a.steps, a.warmup, dev, a.dtype)
+        B, dt, loss = run(name, a.steps, a.warmup, dev, a.dtype, a.head_pad)
         pps = B / dt
         tf = pps * TRAIN_GFLOP[name] / 1e3
         print(json.dumps({"config": name, "patches_per_s": round(pps, 2), "ms_per_step": round(dt * 1e3, 3), "batch": B,
