@@ -1013,7 +1013,7 @@ int nt_tiles(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipSt
 
 // 4-column register epilogue: ROWS / QKV outputs whose vectors are 4-aligned
 static bool epi4_ok(const Epi& e, int N) {
-  if (N % 4 != 0 || N <= 64 || e.resid2) return false;
+  if (N % 4 != 0 || N < 64 || e.resid2) return false;
   if (e.omode == KAIR_OUT_QKVBLK) return e.hdp % 4 == 0;
   if (e.omode != KAIR_OUT_ROWS) return false;
   return e.ldo % 4 == 0 && (!e.pre || e.ldp % 4 == 0) && (!e.resid || e.ldr % 4 == 0) && (!e.gate || e.ldg % 4 == 0);
@@ -1042,6 +1042,24 @@ int launch_ring(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hi
   return 0;
 }
 
+// The ring's N tile.  Narrow outputs take ONE N tile, so A streams through the ring once: N <= 64 (the
+// SwinIR-lightweight block's Cp = 64 projections: fc2 / proj forward, fc1 input gradient) a 64-wide tile,
+// N <= 96 a 96-wide one, N <= 128 at K <= 192 (its fc1 forward and gated fc2 input gradient, Hdp = 128) a 192-wide
+// one rather than two 96-wide tiles that read A twice.  Wider outputs (the classical Cp = 192 geometry): a gated
+// epilogue (the fc2 input gradient, N = 384) four 96-wide N tiles rather than two 192-wide ones -- each CTA's
+// epilogue reads half the gate columns per tile (B = 32: 1015 -> 1019 patches/s); one 192-wide N tile leaves the
+// persistent CTAs unevenly loaded (B = 32: 576 M-tiles on 256 CUs -> 3 vs 2.25 on average), two 96-wide tiles
+// balance better (815 -> 823 patches/s) except for the q/k/v output.
+static int ring_bn_of(const Epi& E, int N, int K) {
+  if (N <= 64) return 64;
+  if (N <= 96 && K <= 384) return 96;
+  if (N <= 128 && K <= 192) return 192;
+  if (E.gate && K <= 192) return 96;
+  if (K <= 192 && !(N <= 192 && E.omode != KAIR_OUT_QKVBLK)) return 192;
+  if (K <= 384) return 96;
+  return 64;
+}
+
 // ring kernel: bf16 A (rows, optionally window-mapped, or head-blocked q/k/v) with no row scale
 static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, int N, int K) {
   if (K % RING_BK != 0 || K > 576 || M >= (1L << 30)) return false;
@@ -1062,7 +1080,8 @@ static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, i
   if (e.omode == KAIR_OUT_QKVBLK && e.hdp % 8) return false;
   if (e.rowscale && (!e.resid || (M + e.rps - 1) / e.rps > RING_RS_MAX)) return false;
   if (e.omode == KAIR_OUT_QKVBLK) {         // the staged store groups whole heads per wave
-    const int TN = (K <= 192 ? 192 : K <= 384 ? 96 : 64) / 2;
+    const int bn = ring_bn_of(e, N, K);
+    const int TN = bn == 96 ? 96 : bn / 2;
     if (e.hdp <= 0 || TN % e.hdp != 0) return false;
   }
   return epi4_ok(e, N);
@@ -1070,15 +1089,9 @@ static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, i
 
 template <int AM>
 int ring_bn(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
-  // one 192-wide N tile leaves the persistent CTAs unevenly loaded (B = 32: 576 M-tiles on 256 CUs
-  // -> 3 vs 2.25 on average); two 96-wide tiles balance better (measured 815 -> 823 patches/s;
-  // against one 192-wide tile)
-  constexpr int split_n = 1;
-  // a gated epilogue (the fc2 input gradient, N = 384): four 96-wide N tiles rather than two 192-wide
-  // ones -- each CTA's epilogue reads half the gate columns per tile (B = 32: 1015 -> 1019 patches/s)
-  if (E.gate && K <= 192) return launch_ring<96, 5, AM>(A, B, E, M, N, K, s);
-  if (K <= 192 && !(split_n && N <= 192 && E.omode != KAIR_OUT_QKVBLK)) return launch_ring<192, 5, AM>(A, B, E, M, N, K, s);
-  if (K <= 384) return launch_ring<96, 5, AM>(A, B, E, M, N, K, s);
+  const int bn = ring_bn_of(E, N, K);
+  if (bn == 192) return launch_ring<192, 5, AM>(A, B, E, M, N, K, s);
+  if (bn == 96) return launch_ring<96, 5, AM>(A, B, E, M, N, K, s);
   return launch_ring<64, 5, AM>(A, B, E, M, N, K, s);
 }
 
@@ -1489,7 +1502,7 @@ int nt_modes(int mode, const Op& A, const Op& B, const Epi& E, long M, int N, in
   if constexpr (sizeof(CT) == 2 && sizeof(TA) == 2) {
     if (g_ring_mode && ring_ok(mode, A, B, E, M, N, K)) {
       if (g_num_cus == 0) init_num_cus();
-      const int bn = K <= 192 ? 192 : (K <= 384 ? 96 : 64);   // ring_bn's choice
+      const int bn = ring_bn_of(E, N, K);
       const long tiles = ((M + RING_BM - 1) / RING_BM) * ((N + bn - 1) / bn);
       if (tiles >= g_ring_min_tiles) {
         if (mode == KAIR_LD_ROWS) return ring_bn<AM_ROWS>(A, B, E, M, N, K, s);

@@ -605,6 +605,59 @@ def test_gemm_stream_epilogues(a_dtype):
     assert rel_err(qkv.float(), refq) < 1e-2
 
 
+@pytest.mark.parametrize("N,K,epi", [(64, 128, "resid"), (64, 64, "plain"), (128, 64, "gate"), (128, 64, "gelu"),
+                                     (96, 64, "resid"), (64, 256, "plain")])
+def test_gemm_ring_narrow_n(N, K, epi):
+    """bf16 NT GEMMs with N <= 128 on the LDS-DMA ring kernel in ONE N tile (gemm.hip ring_bn_of: 64 / 96 / 192 wide):
+    the SwinIR-lightweight block shapes (Cp = 64, Hdp = 128) -- residual + DropPath row scale, GELU with its
+    derivative stored and a ones column, the GELU' gate -- at M >= one 128-row tile per CU, ragged last tile."""
+    B, Hh, Ww = 3, 104, 128
+    M = B * Hh * Ww   # 39,936 rows: 312 full 128-row tiles, and a ragged 39,899
+    for m in (M, M - 37):
+        g = torch.Generator().manual_seed(N + K + m)
+        a = torch.randn(m, K, generator=g).bfloat16()
+        w = (torch.randn(N, K, generator=g) * 0.1).bfloat16()
+        bias = torch.randn(N, generator=g)
+        y = a.double() @ w.double().T + bias.double()
+        out = torch.full((m, N), float("nan"), device=dev)
+        kw = {}
+        if epi == "resid":
+            res = torch.randn(m, N, generator=g)
+            scale = torch.tensor([0.5, 2.0, 1.25])
+            rps = (m + 2) // 3
+            kw = dict(resid=res.to(dev), rowscale=scale.to(dev), rows_per_scale=rps)
+            ref = res.double() + scale.double().repeat_interleave(rps)[:m, None] * y
+        elif epi == "gate":
+            gate = torch.randn(m, N, generator=g).bfloat16()
+            kw = dict(gate=gate.to(dev), gate_kind=4)
+            ref = y * gate.double()
+        elif epi == "gelu":
+            pre = torch.empty(m, N, device=dev, dtype=torch.bfloat16)
+            kw = dict(act=H.ACT_GELU, pre=pre, pre_grad=True, ones_col=N - 3)
+            ref = torch.nn.functional.gelu(y)
+            ref[:, N - 3] = 1.0
+        else:
+            ref = y
+        A_d, W_d, E_d = H.rows(a.to(dev)), H.rows(w.to(dev)), H.epilogue(out, bias=bias.to(dev), **kw)
+        torch.cuda.synchronize()
+        H.ktime_begin(8)
+        try:
+            H.gemm_nt(A_d, W_d, E_d, m, N, K, H.BF16)
+        finally:
+            n = H.ktime_end()
+        torch.cuda.synchronize()
+        assert n == 1 and "gemm_nt_ring" in H.ktime_read(0)[1], H.ktime_read(0)[1]
+        assert torch.isfinite(out).all()
+        assert rel_err(out, ref) < (5e-3 if epi == "gelu" else 1e-5)
+        if epi == "gelu":   # GELU'(y), bf16
+            t = y.clone()
+            t.requires_grad_(True)
+            torch.nn.functional.gelu(t).sum().backward()
+            dref = t.grad
+            dref[:, N - 3] = pre.double().cpu()[:, N - 3]   # the ones column's pre value is not specified
+            assert rel_err(pre, dref) < 1e-2
+
+
 def test_gemm_qkvblk_A_operand():
     """A read from the head-blocked q/k/v layout (the q/k/v input-gradient GEMM), K = 576."""
     nWin, nh, tok, hdp = 12, 6, 64, 32
