@@ -281,7 +281,7 @@ KAIR_DEV void epi4(const Epi& e, long m, long row, float rs, int n, float (&v)[4
 //    compiler that also issues fully masked ones only makes the wait stricter.
 // ------------------------------------------------------------------------------------------
 constexpr int RING_BM = 128, RING_BK = 64;
-constexpr int RING_B_ELEMS = 38400;   // max BN * (K + 8) over the (BN, K) pairs dispatched below
+constexpr int RING_B_ELEMS = 38400;   // max BN * (Kr + 8) over the (BN, K) pairs dispatched below (Kr: K up to 64)
 constexpr int RING_RS_MAX = 1024;     // per-sample residual scales kept in LDS by the ring kernel
 
 
@@ -290,6 +290,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
   constexpr int BM = RING_BM, BK = RING_BK;
   // 8 waves as WM (rows) x WN (columns); each wave's columns split into 16-wide fragment pairs
   constexpr int WN = BN == 96 ? 1 : 2, WM = 8 / WN, WROWS = BM / WM;
+  // K % 64 != 0 (head-padded projections, e.g. 6 heads x 16 = 96): the last chunk is partial -- its pieces past K
+  // load the zero line and the B slice is zero there, so the chunk contracts exact zeros
   constexpr int TN = BN / WN, RM = WROWS / 16, RN = TN / 16;
   constexpr int STAGE_BYTES = BM * BK * 2;   // 16 KiB
   constexpr int NP = RN / 2;                  // fragment pairs per wave row (8-column epilogue groups)
@@ -297,7 +299,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE_BYTES + RING_B_ELEMS * 2 + RING_RS_MAX * 4];
   bf16* sB = (bf16*)(smem + NS * STAGE_BYTES);
   float* sRS = (float*)(smem + NS * STAGE_BYTES + RING_B_ELEMS * 2);
-  const int LDB = K + 8;
+  const int Kr = (K + BK - 1) / BK * BK;
+  const int LDB = Kr + 8;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
   const int mt0 = cta / tilesN;
   if (mt0 >= tilesM) return;
   const int ntile_m = (tilesM - mt0 + mstride - 1) / mstride;
-  const int nk = K / BK;
+  const int nk = Kr / BK;
   const int total = ntile_m * nk;
   const int n0 = nt * BN;
 
@@ -318,7 +321,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
     // all loads first (<= 10 16-byte pieces per thread: BN * K <= RING_B_ELEMS), then the LDS
     // stores, so the slice costs one L2 round trip rather than one per piece
     constexpr int PER = (RING_B_ELEMS / 8 + 511) / 512;
-    const int cpr = K / 8;
+    const int cpr = Kr / 8;
     uint4 v[PER];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -326,15 +329,15 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
       const int r = c / cpr, k8 = (c - r * cpr) * 8;
       // unconditional (clamped) loads, zeroed after: a conditional load becomes a branch with its
       // own wait, i.e. one L2 round trip per piece
-      const bool ok = c < BN * cpr && n0 + r < B.M;
+      const bool ok = c < BN * cpr && n0 + r < B.M && k8 < K;
       const long row = ok ? n0 + r : 0;
       v[i] = *(const uint4*)(bp + row * B.ld + (ok ? k8 : 0));
     }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * 512;
-      const int r = c / cpr;
-      if (!(c < BN * cpr && n0 + r < B.M)) v[i] = make_uint4(0, 0, 0, 0);
+      const int r = c / cpr, k8 = (c - r * cpr) * 8;
+      if (!(c < BN * cpr && n0 + r < B.M && k8 < K)) v[i] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -408,16 +411,17 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_ring(Op A, Op B, Epi E, int K,
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
         const int k = lkc * BK + ((q8 ^ rsw[ii]) << 3);
+        const int kk = k < K ? k : 0;
         long off;
         if constexpr (AM == AM_ROWS) {
-          off = rbase[ii] + k;
+          off = rbase[ii] + kk;
         } else {
           const int pw = A.d_pw.d;
-          const int part = fdiv(k, A.d_pw), rr = k - part * pw;
+          const int part = fdiv(kk, A.d_pw), rr = kk - part * pw;
           const int h = fdiv(rr, A.d_hdp), d = rr - h * A.hdp;
           off = (long)part * A.M * pw + rbase[ii] + (long)h * A.tok * A.hdp + d;
         }
-        glds16((const bf16*)A.ptr + off, st + (wave * 2 + ii) * 1024);
+        glds16(k < K ? (const void*)((const bf16*)A.ptr + off) : (const void*)g_kair_zero_line, st + (wave * 2 + ii) * 1024);
       }
     }
     ++lj;
@@ -1044,15 +1048,22 @@ int launch_ring(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hi
 
 // The ring's N tile.  Narrow outputs take ONE N tile, so A streams through the ring once: N <= 64 (the
 // SwinIR-lightweight block's Cp = 64 projections: fc2 / proj forward, fc1 input gradient) a 64-wide tile,
-// N <= 96 a 96-wide one, N <= 128 at K <= 192 (its fc1 forward and gated fc2 input gradient, Hdp = 128) a 192-wide
-// one rather than two 96-wide tiles that read A twice.  Wider outputs (the classical Cp = 192 geometry): a gated
+// N <= 96 a 96-wide one, N <= 128 at K <= 256 (its fc1 forward and gated fc2 input gradient, Hdp = 128) a 128-wide
+// one (against a 192-wide tile, whose second wave column had 32 of 96 columns to store: C2 2,171 -> 2,240 patches/s) rather than two
+// 96-wide tiles that read A twice.  Wider outputs (the classical Cp = 192 geometry): a gated
 // epilogue (the fc2 input gradient, N = 384) four 96-wide N tiles rather than two 192-wide ones -- each CTA's
 // epilogue reads half the gate columns per tile (B = 32: 1015 -> 1019 patches/s); one 192-wide N tile leaves the
 // persistent CTAs unevenly loaded (B = 32: 576 M-tiles on 256 CUs -> 3 vs 2.25 on average), two 96-wide tiles
 // balance better (815 -> 823 patches/s) except for the q/k/v output.
+static const int g_ring_bn128 = [] {   // KAIR_RING_BN128=0: N <= 128 on the 192-wide tile (A/B)
+  const char* e = getenv("KAIR_RING_BN128");
+  return e && atoi(e) == 0 ? 0 : 1;
+}();
 static int ring_bn_of(const Epi& E, int N, int K) {
+  K = (K + RING_BK - 1) / RING_BK * RING_BK;   // the chunked K
   if (N <= 64) return 64;
   if (N <= 96 && K <= 384) return 96;
+  if (N <= 128 && K <= 256 && g_ring_bn128) return 128;
   if (N <= 128 && K <= 192) return 192;
   if (E.gate && K <= 192) return 96;
   if (K <= 192 && !(N <= 192 && E.omode != KAIR_OUT_QKVBLK)) return 192;
@@ -1062,7 +1073,7 @@ static int ring_bn_of(const Epi& E, int N, int K) {
 
 // ring kernel: bf16 A (rows, optionally window-mapped, or head-blocked q/k/v) with no row scale
 static bool ring_ok(int amode, const Op& A, const Op& B, const Epi& e, long M, int N, int K) {
-  if (K % RING_BK != 0 || K > 576 || M >= (1L << 30)) return false;
+  if (K % 8 != 0 || K > 576 || M >= (1L << 30)) return false;
   if (amode != KAIR_LD_ROWS && amode != KAIR_LD_QKVBLK) return false;
   if (A.rowscale || A.ones_col >= 0 || A.asplit || e.out_lo) return false;
   if (amode == KAIR_LD_ROWS && A.ld % 8 != 0) return false;
@@ -1091,6 +1102,7 @@ template <int AM>
 int ring_bn(const Op& A, const Op& B, const Epi& E, long M, int N, int K, hipStream_t s) {
   const int bn = ring_bn_of(E, N, K);
   if (bn == 192) return launch_ring<192, 5, AM>(A, B, E, M, N, K, s);
+  if (bn == 128) return launch_ring<128, 5, AM>(A, B, E, M, N, K, s);
   if (bn == 96) return launch_ring<96, 5, AM>(A, B, E, M, N, K, s);
   return launch_ring<64, 5, AM>(A, B, E, M, N, K, s);
 }
@@ -1680,6 +1692,12 @@ extern "C" int kair_gemm_nt(const kair_operand* A, const kair_operand* B, const 
 static bool tn_ring_shape(long M, int N, int K) {
   return N <= 576 && K <= 576 && N % 8 == 0 && K % 8 == 0 && N > 64 && K > 64 && M < (1L << 30);
 }
+// the grouped launch takes narrow linears too (SwinIR-lightweight: Cp = 64 with Hdp = 128 and 6 x 16 heads): one
+// 192 x 192 tile holds a whole 64 x 128 weight -- its pieces past N / K load the zero line -- and the group's
+// splits fill the chip (the single-linear path keeps N, K > 64: its split count is shared with the generic kernel)
+static bool tn_ring_shape_grouped(long M, int N, int K) {
+  return N <= 576 && K <= 576 && N % 8 == 0 && K % 8 == 0 && N >= 16 && K >= 16 && M < (1L << 30);
+}
 // 3x3 conv weight gradient over a 192-channel image: the ring with one tap per K tile (BM_TAP)
 static bool tn_tap_shape(long M, int N, int K) {
   return N <= 576 && N % 8 == 0 && N > 64 && K == 9 * TNR_BK && M < (1L << 30);
@@ -1887,7 +1905,7 @@ extern "C" int kair_wgrad_grouped_ex(const kair_wgrad_job* jobs, int njobs, long
     KAIR_CHECK_ARG(!J.A.rowscale && !J.B.rowscale && J.A.win_ws == 0 && J.B.win_ws == 0 && J.A.ones_col < 0 &&
                        (J.B.ones_col < 0 || J.B.ones_in_data),
                    "wgrad_grouped: job %d: no row scale / window map / injected ones column", i);
-    KAIR_CHECK_ARG(tn_ring_shape(M, J.N, J.K) && (J.A.mode != KAIR_LD_ROWS || J.A.ld % 8 == 0) && J.B.ld % 8 == 0,
+    KAIR_CHECK_ARG(tn_ring_shape_grouped(M, J.N, J.K) && (J.A.mode != KAIR_LD_ROWS || J.A.ld % 8 == 0) && J.B.ld % 8 == 0,
                    "wgrad_grouped: job %d shape (N %d, K %d) / strides", i, J.N, J.K);
     KAIR_CHECK_ARG(J.grad && J.map.kind == 0 && (long)J.map.nG * J.map.nGp == J.N && (long)J.map.kG * J.map.kGp == J.K,
                    "wgrad_grouped: job %d needs a linear map whose packed dims are (N, K)", i);

@@ -190,123 +190,147 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const typename AT<BF>::T*
 // S^T = K Q^T product consumes), only v staged in LDS (for the transposed P.V fragments), so a
 // wave needs 6 KiB of LDS and 8 waves fit a CU; O is produced transposed (O^T = V^T P^T: lane =
 // query, 4 consecutive d per register group) and stored 8 bytes at a time.
+// Each wave runs `tpw` consecutive (window, head) tasks and loads the next task's q / k / v fragments and
+// bias-table column while the current one computes (2 waves per SIMD: one task per wave left every load's
+// latency exposed -- 1.75 TB/s at SwinIR-lightweight's shapes).
 // HP: the head pad of the q / k / v / O layout -- 32, or 16 for head dims below 16 (SwinIR-lightweight's 10,
 // network_swinir.py:85 with embed_dim 60 / 6 heads): one K = 16 step for S, half the HBM bytes per head; the
 // P.V product keeps its 32-row MFMA tile (rows d >= 16 read zeroed LDS columns and are not stored).
 // ------------------------------------------------------------------------------------------
 template <int HP>
-__global__ __launch_bounds__(256) void attn_fwd_bf16_kernel(const bf16* __restrict__ qkv, const float* __restrict__ table,
+__global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(const bf16* __restrict__ qkv, const float* __restrict__ table,
                                                             bf16* __restrict__ O, long ldo, float* __restrict__ lse,
                                                             long nWin, int nh, float scale, int H, int W, int shift,
-                                                            int ones_col, const float* __restrict__ amask, int mask_nw) {
-  constexpr int LD = AT<true>::LD, NW = 4, NS = HP / 16;
+                                                            int ones_col, const float* __restrict__ amask, int mask_nw,
+                                                            int tpw) {
+  constexpr int LD = AT<true>::LD, NW = 4, NS = HP / 16, NT = ((2 * WS - 1) * (2 * WS - 1) + 63) / 64;
   static_assert(HP == 16 || HP == 32, "head pad");
   __shared__ __attribute__((aligned(16))) bf16 sV[NW][TOK * LD];
-  __shared__ float sTab[NW][232];
+  __shared__ float sTab[NW][NT * 64];
   __shared__ int sReg[NW][TOK];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long task = (long)blockIdx.x * NW + w;
-  if (task >= nWin * nh) return;
-  const long win = task / nh;
-  const int h = (int)(task - win * nh);
+  const long ntask = nWin * nh;
+  const long task0 = ((long)blockIdx.x * NW + w) * tpw;
+  if (task0 >= ntask) return;
+  const long task1 = task0 + tpw < ntask ? task0 + tpw : ntask;
   const long M = nWin * TOK;
-  const long blk = (win * nh + h) * TOK * HP;
   const long part = M * nh * HP;
   const int l31 = lane & 31, hh = lane >> 5;
-  bf16x8 Fq[2][NS], Fk[2][NS], Fv[2][NS];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const long o = (long)(t * 32 + l31) * HP + 16 * s + 8 * hh;
-      Fq[t][s] = *(const bf16x8*)(qkv + blk + o);
-      Fk[t][s] = *(const bf16x8*)(qkv + part + blk + o);
-      Fv[t][s] = *(const bf16x8*)(qkv + 2 * part + blk + o);
-    }
-  bf16* v = sV[w];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 z = {};
-      *(bf16x8*)(v + (t * 32 + l31) * LD + 16 * s + 8 * hh) = s < NS ? Fv[t][s < NS ? s : 0] : z;
-    }
-  for (int i = lane; i < (2 * WS - 1) * (2 * WS - 1); i += 64) sTab[w][i] = table[i * nh + h];
   const int nW = (H / WS) * (W / WS);
-  sReg[w][lane] = shift > 0 ? token_region((int)(win % nW), lane, H, W, shift) : 0;
+  bf16x8 Fq[2][NS], Fk[2][NS], Fv[2][NS];
+  float Ft[NT];
+  auto load_task = [&](long task) {
+    const long win = task / nh;
+    const int h = (int)(task - win * nh);
+    const long blk = (win * nh + h) * TOK * HP;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const long o = (long)(t * 32 + l31) * HP + 16 * s + 8 * hh;
+        Fq[t][s] = *(const bf16x8*)(qkv + blk + o);
+        Fk[t][s] = *(const bf16x8*)(qkv + part + blk + o);
+        Fv[t][s] = *(const bf16x8*)(qkv + 2 * part + blk + o);
+      }
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {   // clamped index: unconditional loads (no branch, no extra wait)
+      const int ti = lane + 64 * i < (2 * WS - 1) * (2 * WS - 1) ? lane + 64 * i : 0;
+      Ft[i] = table[ti * nh + h];
+    }
+  };
+  load_task(task0);
+  bf16* v = sV[w];
+  for (long task = task0; task < task1; ++task) {
+    const long win = task / nh;
+    const int h = (int)(task - win * nh);
+    wave_sync();   // the previous task's LDS reads are complete
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 z = {};
+        *(bf16x8*)(v + (t * 32 + l31) * LD + 16 * s + 8 * hh) = s < NS ? Fv[t][s < NS ? s : 0] : z;
+      }
+#pragma unroll
+    for (int i = 0; i < NT; ++i) sTab[w][lane + 64 * i] = Ft[i];
+    sReg[w][lane] = shift > 0 ? token_region((int)(win % nW), lane, H, W, shift) : 0;
 
-  // S^T = K Q^T : tiles [kt][qt], lane column = query, registers = keys
-  f32x16 acc[2][2];
+    // S^T = K Q^T : tiles [kt][qt], lane column = query, registers = keys
+    f32x16 acc[2][2];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 #pragma unroll
-  for (int s = 0; s < NS; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-        acc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fk[kt][s], Fq[qt][s], acc[kt][qt], 0, 0, 0);
-  wave_sync();
-  // scores: scale, bias, mask ; softmax over keys (registers + lane^32)
+        for (int qt = 0; qt < 2; ++qt)
+          acc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Fk[kt][s], Fq[qt][s], acc[kt][qt], 0, 0, 0);
+    // the next task's fragments load under this task's softmax, P.V and stores (the last task reloads itself,
+    // so every path reaches the loop back-edge with the same loads pending)
+    load_task(task + 1 < task1 ? task + 1 : task);
+    wave_sync();
+    // scores: scale, bias, mask ; softmax over keys (registers + lane^32)
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qi = qt * 32 + l31;
-    const int rq = sReg[w][qi];
-    float mx = -3.0e38f;
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qi = qt * 32 + l31;
+      const int rq = sReg[w][qi];
+      float mx = -3.0e38f;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ki = kt * 32 + acc_row(r, hh);
-        float sc = acc[kt][qt][r] * scale + sTab[w][relidx(qi, ki)];
-        if (shift > 0 && sReg[w][ki] != rq) sc += -100.f;
-        if (amask) sc += amask[((win % mask_nw) * TOK + qi) * TOK + ki];
-        acc[kt][qt][r] = sc;
-        mx = fmaxf(mx, sc);
+        for (int r = 0; r < 16; ++r) {
+          const int ki = kt * 32 + acc_row(r, hh);
+          float sc = acc[kt][qt][r] * scale + sTab[w][relidx(qi, ki)];
+          if (shift > 0 && sReg[w][ki] != rq) sc += -100.f;
+          if (amask) sc += amask[((win % mask_nw) * TOK + qi) * TOK + ki];
+          acc[kt][qt][r] = sc;
+          mx = fmaxf(mx, sc);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __expf(acc[kt][qt][r] - mx);
+          acc[kt][qt][r] = e;
+          sum += e;
+        }
+      sum += __shfl_xor(sum, 32, 64);
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[kt][qt][r] *= inv;
+      if (hh == 0) lse[task * TOK + qi] = mx + __logf(sum);
+    }
+    // O^T = V^T P^T : tile [qt] rows = d, lane = query
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 o;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_rows_perm(v, kt * 32, s, lane), pack8(acc[kt][qt], s), o, 0, 0, 0);
+      const int qi = qt * 32 + l31;
+      bf16* orow = O + (win * TOK + qi) * ldo + h * HP;
+#pragma unroll
+      for (int g = 0; g < HP / 8; ++g) {
+        const int d0 = 8 * g + 4 * hh;
+        float r4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r4[j] = (h * HP + d0 + j == ones_col) ? 1.f : o[4 * g + j];
+        const bf16x4 q4 = {(bf16)r4[0], (bf16)r4[1], (bf16)r4[2], (bf16)r4[3]};
+        *(bf16x4*)(orow + d0) = q4;
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float e = __expf(acc[kt][qt][r] - mx);
-        acc[kt][qt][r] = e;
-        sum += e;
-      }
-    sum += __shfl_xor(sum, 32, 64);
-    const float inv = 1.f / sum;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[kt][qt][r] *= inv;
-    if (hh == 0) lse[task * TOK + qi] = mx + __logf(sum);
-  }
-  // O^T = V^T P^T : tile [qt] rows = d, lane = query
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    f32x16 o;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_rows_perm(v, kt * 32, s, lane), pack8(acc[kt][qt], s), o, 0, 0, 0);
-    const int qi = qt * 32 + l31;
-    bf16* orow = O + (win * TOK + qi) * ldo + h * HP;
-#pragma unroll
-    for (int g = 0; g < HP / 8; ++g) {
-      const int d0 = 8 * g + 4 * hh;
-      float r4[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) r4[j] = (h * HP + d0 + j == ones_col) ? 1.f : o[4 * g + j];
-      const bf16x4 q4 = {(bf16)r4[0], (bf16)r4[1], (bf16)r4[2], (bf16)r4[3]};
-      *(bf16x4*)(orow + d0) = q4;
     }
   }
 }
@@ -849,8 +873,9 @@ constexpr int WPG = 4;  // windows per backward wave (fp32 parity path)
 // bf16 backward: windows per wave so that the (group, head) waves fill every CU's 4 wave slots in
 // one round (1 wave per SIMD: the kernel holds ~500 VGPRs) -- e.g. 1152 windows x 6 heads on 256
 // CUs -> 7 windows per wave, 990 waves
+static int g_attn_ncu = 0;
 static int bwd_wpg_bf16(long nWin, int nh) {
-  static int ncu = 0;
+  int& ncu = g_attn_ncu;
   if (ncu == 0) {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
@@ -862,6 +887,20 @@ static int bwd_wpg_bf16(long nWin, int nh) {
   return (int)(w < 1 ? 1 : w);
 }
 static long bwd_groups(long nWin, int wpg) { return (nWin + wpg - 1) / wpg; }
+
+// bf16 forward: (window, head) tasks per wave so that one round of waves (occ per SIMD: 3 at head pad 16, 2 at
+// 32 -- the kernels' register occupancy) covers them all (KAIR_ATTN_FWD_TPW=n forces n: A/B)
+static int fwd_tpw_bf16(long tasks, int occ) {
+  static const int forced = [] {
+    const char* e = getenv("KAIR_ATTN_FWD_TPW");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced > 0) return forced;
+  bwd_wpg_bf16(1, 1);   // (initialises the CU count)
+  const long slots = 4L * occ * g_attn_ncu;
+  const long t = (tasks + slots - 1) / slots;
+  return (int)(t < 1 ? 1 : t);
+}
 
 }  // namespace
 
@@ -880,17 +919,21 @@ extern "C" int kair_window_attn_fwd_ex(const void* qkv, int dtype, const float* 
   KAIR_CHECK_ARG(ones_col < 0 || (ones_col < nh * hp && ones_col % hp >= hd), "window_attn_fwd: ones column must be a pad column");
   const long tasks = nWin * nh;
   const int nw = dtype == KAIR_BF16 ? NWAVES<true> : NWAVES<false>;
-  const long nb = (tasks + nw - 1) / nw;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == KAIR_BF16 && hp == 16)
-    KAIR_LAUNCH(attn_fwd_bf16_kernel<16>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
-                       lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
-  else if (dtype == KAIR_BF16)
-    KAIR_LAUNCH(attn_fwd_bf16_kernel<32>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
-                       lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
-  else
+  if (dtype == KAIR_BF16) {
+    const int tpw = fwd_tpw_bf16(tasks, hp == 16 ? 3 : 2);
+    const long nb = (tasks + (long)nw * tpw - 1) / ((long)nw * tpw);
+    if (hp == 16)
+      KAIR_LAUNCH(attn_fwd_bf16_kernel<16>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
+                  lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw, tpw);
+    else
+      KAIR_LAUNCH(attn_fwd_bf16_kernel<32>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const bf16*)qkv, table, (bf16*)O, ldo,
+                  lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw, tpw);
+  } else {
+    const long nb = (tasks + nw - 1) / nw;
     KAIR_LAUNCH(attn_fwd_kernel<false>, dim3((unsigned)nb), dim3(64 * nw), 0, s, (const float*)qkv, table, (float*)O,
                        ldo, lse, nWin, nh, scale, H, W, shift, ones_col, mask, mask_nw);
+  }
   KAIR_CHECK_LAUNCH();
   return 0;
 }

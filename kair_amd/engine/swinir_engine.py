@@ -271,7 +271,7 @@ class _Blk:
 class SwinIREngine:
     def __init__(self, net, compute_dtype="bf16", split_conv=True, fused_blocks=True, fused_mlp=None,
                  split_linear=None, fused_mlp_bwd=False, side_stream=True, side_ctas=None, side_priority=0,
-                 split_act=True, conv_wr=True, head_pad=None):
+                 split_act=True, conv_wr=True, head_pad=None, grouped_wgrad=None):
         """split_conv (bf16 only): forward 3x3 convs multiply hi/lo bf16 weight pairs (_Conv), i.e.
         see the fp32 master weights to ~16 bits; split_linear does the same for the linears of the
         fused block kernels (_Lin, pack kind 12).
@@ -410,8 +410,9 @@ class SwinIREngine:
         self.seg_hook = None   # called between the gradient segments of backward() (grad_segments())
         # Swin-block weight gradients: deferred to the end of each RSTB and issued as ONE grouped
         # launch (kair_wgrad_grouped: 4 linears x depth blocks) where the bf16 TN ring takes the shapes;
-        # otherwise one gemm_tn + finalize per linear, issued in place
-        self.grouped_wgrad = (self.tdt == torch.bfloat16 and self.Cp > 64 and self.Hdp <= 576 and
+        # otherwise one gemm_tn + finalize per linear, issued in place.  Narrow blocks (Cp = 64, SwinIR-lightweight) too:
+        # one 192 x 192 ring tile per linear (profiles/r06_c2_head_pad16_ab.txt); grouped_wgrad=False: per linear (A/B)
+        self.grouped_wgrad = (grouped_wgrad is not False and self.tdt == torch.bfloat16 and self.Hdp <= 576 and
                               3 * self.nh * self.hp <= 576 and
                               max(len(l.residual_group.blocks) for l in net.layers) <= H.WgradGroup.WG_MAX // 4)
         self._wg_pending = []

@@ -606,11 +606,14 @@ def test_gemm_stream_epilogues(a_dtype):
 
 
 @pytest.mark.parametrize("N,K,epi", [(64, 128, "resid"), (64, 64, "plain"), (128, 64, "gate"), (128, 64, "gelu"),
-                                     (96, 64, "resid"), (64, 256, "plain")])
+                                     (96, 64, "resid"), (64, 256, "plain"), (64, 96, "resid"), (128, 96, "gelu"),
+                                     (96, 40, "plain"), (192, 168, "plain")])
 def test_gemm_ring_narrow_n(N, K, epi):
-    """bf16 NT GEMMs with N <= 128 on the LDS-DMA ring kernel in ONE N tile (gemm.hip ring_bn_of: 64 / 96 / 192 wide):
-    the SwinIR-lightweight block shapes (Cp = 64, Hdp = 128) -- residual + DropPath row scale, GELU with its
-    derivative stored and a ones column, the GELU' gate -- at M >= one 128-row tile per CU, ragged last tile."""
+    """bf16 NT GEMMs on the LDS-DMA ring kernel, N <= 128 in ONE N tile (gemm.hip ring_bn_of: 64 / 96 / 128 wide) and
+    K % 64 != 0 (a partial last chunk: zero-line pieces past K, a zero B slice there): the SwinIR-lightweight block
+    shapes (Cp = 64, Hdp = 128, 6 heads x 16 = 96) -- residual + DropPath row scale, GELU with its derivative stored
+    and a ones column, the GELU' gate -- at M >= one 128-row tile per CU, ragged last tile.  A is allocated with
+    exactly K columns, so a piece read past K on the last row would leave the buffer."""
     B, Hh, Ww = 3, 104, 128
     M = B * Hh * Ww   # 39,936 rows: 312 full 128-row tiles, and a ragged 39,899
     for m in (M, M - 37):
@@ -672,6 +675,71 @@ def test_gemm_qkvblk_A_operand():
     ref = a @ w.to(torch.bfloat16).double().T
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 1e-2
+
+
+def test_gemm_qkvblk_A_ring_head_pad16():
+    """The q/k/v input-gradient GEMM of the 16-wide head layout on the ring: A head-blocked [3][nWin][6][64][16],
+    K = 288 (4.5 chunks of 64: a partial last chunk), N = Cp = 64, M = 600 windows x 64 tokens."""
+    nWin, nh, tok, hdp = 600, 6, 64, 16
+    M, N, K = nWin * tok, 64, 3 * nh * hdp
+    g = torch.Generator().manual_seed(14)
+    blk = torch.randn(3, nWin, nh, tok, hdp, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16()
+    out = torch.full((M, N), float("nan"), device=dev)
+    A_d, W_d, E_d = H.qkvblk(blk.to(dev).reshape(-1), nh, hdp=hdp), H.rows(w.to(dev)), H.epilogue(out)
+    torch.cuda.synchronize()
+    H.ktime_begin(8)
+    try:
+        H.gemm_nt(A_d, W_d, E_d, M, N, K, H.BF16)
+    finally:
+        n = H.ktime_end()
+    torch.cuda.synchronize()
+    assert n == 1 and "gemm_nt_ring" in H.ktime_read(0)[1], H.ktime_read(0)[1]
+    a = blk.double().permute(1, 3, 0, 2, 4).reshape(M, K)
+    assert rel_err(out, a @ w.double().T) < 1e-5
+
+
+@pytest.mark.parametrize("M", [3001, 40000])
+def test_wgrad_grouped_narrow_bf16(M):
+    """kair_wgrad_grouped (bf16 TN ring, one launch) over a SwinIR-lightweight block's linears -- Cp = 64, Hdp = 128,
+    6 heads x 16: fc2 (64 x 128), fc1 (128 x 64), proj (64 x 96, A = the token rows of O), qkv (288 x 64, A head-blocked
+    [3][M/64][6][64][16]) -- with the bias ones columns in the data, against float64 on the bf16 operands."""
+    g = torch.Generator().manual_seed(31)
+    M = M // 64 * 64
+    C, Cp, Hd, Hdp, nh, hd, hp = 60, 64, 120, 128, 6, 10, 16
+    jobs, refs, keep = [], [], []
+    # (Np, Kp, N, K, n_grp, k_grp, qkv-blocked A)
+    for Np, Kp, N, K, ng, kg, blk in [(Cp, Hdp, C, Hd, (1, C, Cp), (1, Hd, Hdp), False),
+                                      (Hdp, Cp, Hd, C, (1, Hd, Hdp), (1, C, Cp), False),
+                                      (Cp, nh * hp, C, C, (1, C, Cp), (nh, hd, hp), False),
+                                      (3 * nh * hp, Cp, 3 * C, C, (3 * nh, hd, hp), (1, C, Cp), True)]:
+        dy = torch.zeros(M, Np)
+        cols = torch.tensor([i // ng[1] * ng[2] + i % ng[1] for i in range(N)])
+        dy[:, cols] = torch.randn(M, N, generator=g).bfloat16().float()
+        x = torch.zeros(M, Kp)
+        kcols = torch.tensor([i // kg[1] * kg[2] + i % kg[1] for i in range(K)])
+        x[:, kcols] = torch.randn(M, K, generator=g).bfloat16().float()
+        ones = int(kcols[-1]) + 1   # the first pad column after the last real one
+        x[:, ones] = 1.0
+        if blk:   # head-blocked [3][nWin][nh][64][hp] of the token-row gradient [M][3 nh hp]
+            a = dy.view(M // 64, 64, 3, nh, hp).permute(2, 0, 3, 1, 4).contiguous().to(dev, torch.bfloat16).reshape(-1)
+            A = H.qkvblk(a, nh, hdp=hp)
+        else:
+            a = dy.to(dev, torch.bfloat16)
+            A = H.rows(a)
+        b = x.to(dev, torch.bfloat16)
+        Bop = H.rows(b, ones_col=ones, ones_in_data=True)
+        m = H.wmap(0, N, K, ng, kg)
+        gw, gb = torch.full((N, K), 7.0, device=dev), torch.full((N,), 7.0, device=dev)
+        jobs.append((A, Bop, Np, Kp, m, gw, gb, ones))
+        keep += [a, b]
+        refs.append((gw, gb, dy[:, cols].double().T @ x[:, kcols].double(), dy[:, cols].double().sum(0)))
+    grp = H.WgradGroup(jobs, M)
+    ws = torch.empty(grp.ws_floats, device=dev)
+    grp.run(ws)
+    torch.cuda.synchronize()
+    for gw, gb, rw, rb in refs:
+        assert rel_err(gw, rw) < 1e-5 and rel_err(gb, rb) < 1e-5
 
 
 @pytest.mark.parametrize("dtype", [H.F32, H.BF16])
