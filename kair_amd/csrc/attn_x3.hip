@@ -512,8 +512,11 @@ int x3_cus() {
 // windows per backward wave: enough (group, head) waves for ONE round at the residency the backward's LDS
 // allows (3 two-wave workgroups of ~50 KB per CU; kair_window_attn_bwd_groups / _ws size the partials from it)
 long kair_attn_x3_wpg(long nWin, int nh) {
-  const long slots = 3L * x3_cus();
-  const long w = (nWin * nh + slots - 1) / slots;
+  // groups per head that fit one round of workgroups, then windows per group (as bwd_wpg_bf16: rounding the
+  // windows per group up from nWin * nh / slots can leave a few workgroups for a second round)
+  long per = 3L * x3_cus() / nh;
+  if (per < 1) per = 1;
+  const long w = (nWin + per - 1) / per;
   return w < 1 ? 1 : w;
 }
 

@@ -882,8 +882,12 @@ static int bwd_wpg_bf16(long nWin, int nh) {
       ncu = n;
     if (ncu <= 0) ncu = 256;
   }
-  const long slots = 4L * ncu;
-  const long w = (nWin * nh + slots - 1) / slots;
+  // windows per group from the groups per head that fit one round: ceil(nWin * nh / slots) could leave
+  // ngroups * nh just above the slots (SwinIR-lightweight, 4,096 windows x 6 heads: 24 per wave -> 1,026 waves on
+  // 1,024 slots, one workgroup running a second round alone -- the kernel's time doubled)
+  long per = 4L * ncu / nh;
+  if (per < 1) per = 1;
+  const long w = (nWin + per - 1) / per;
   return (int)(w < 1 ? 1 : w);
 }
 static long bwd_groups(long nWin, int wpg) { return (nWin + wpg - 1) / wpg; }
