@@ -36,7 +36,7 @@ def timed(step, steps, warmup):
     return (time.perf_counter() - t0) / steps, out
 
 
-def run(name, steps, warmup, dev, dtype="bf16", head_pad=None, grouped_wgrad=None):
+def run(name, steps, warmup, dev, dtype="bf16", head_pad=None, grouped_wgrad=None, side_ctas=None):
     """dtype: the engine's compute dtype -- "bf16" (bf16 MFMA, fp32 accumulation), "fp32" (exact fp32 MFMA: the
     reference's arithmetic for the fp32 option files, C3 / C5) or "fp32x3" where the engine has it.
     head_pad (SwinIR): the engine's q/k/v head pad (None: its choice -- 16 for C2's head dim 10; 32: A/B)."""
@@ -63,10 +63,10 @@ def run(name, steps, warmup, dev, dtype="bf16", head_pad=None, grouped_wgrad=Non
         raise SystemExit(f"unknown config {name}")
     net, ema = mk().to(dev).train(), mk().to(dev).eval()
     ema.load_state_dict(net.state_dict())
-    if head_pad is not None or grouped_wgrad is not None:
+    if head_pad is not None or grouped_wgrad is not None or side_ctas is not None:
         from kair_amd.engine.swinir_engine import SwinIREngine
         net._engine = SwinIREngine(net, dtype, net.split_conv, net.fused_blocks, head_pad=head_pad,
-                                   grouped_wgrad=grouped_wgrad)
+                                   grouped_wgrad=grouped_wgrad, side_ctas=side_ctas)
     tr = FusedTrainer(net, ema, lr=1e-4, E_decay=0.999, use_graph=True)
     L = torch.rand(B, *shp, generator=g).to(dev)
     Hh = torch.rand(B, shp[0], shp[1] * sc, shp[2] * sc, generator=g).to(dev)
@@ -100,10 +100,12 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3"])
     ap.add_argument("--head-pad", type=int, default=None, choices=[16, 32])
     ap.add_argument("--no-grouped-wgrad", action="store_true", help="SwinIR: one weight-gradient launch per linear (A/B)")
+    ap.add_argument("--side-ctas", type=int, default=None, help="SwinIR: side-stream workgroup cap (0: uncapped)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for name in a.configs:
-        B, dt, loss = run(name, a.steps, a.warmup, dev, a.dtype, a.head_pad, False if a.no_grouped_wgrad else None)
+        B, dt, loss = run(name, a.steps, a.warmup, dev, a.dtype, a.head_pad, False if a.no_grouped_wgrad else None,
+                          a.side_ctas)
         pps = B / dt
         tf = pps * TRAIN_GFLOP[name] / 1e3
         print(json.dumps({"config": name, "patches_per_s": round(pps, 2), "ms_per_step": round(dt * 1e3, 3), "batch": B,
