@@ -1129,7 +1129,7 @@ constexpr int HC_EM_ROWS = 0, HC_EM_PSHUF = 1, HC_EM_PUNSHUF = 2;   // epilogue:
 // weights (hi/lo split, tied over the halves) give 4 chunk products per tap; the lo.lo one is skipped.
 // BM: output pixels per tile, 96 or (128-wide N tiles of images with <= 128 channels) 192 -- twice the
 // pixels per streamed weight chunk, so half the weight traffic from L2 (the upsampling convs' bound).
-template <int BM> struct HaloSize { static constexpr int ELEMS = BM == 96 ? HC_HALO_ELEMS : 57344; };
+template <int BM> struct HaloSize { static constexpr int ELEMS = BM == 192 ? 57344 : HC_HALO_ELEMS; };
 // CGM > 1: an image of C = 64 CGM channels (C > 192: the upsampling convs' input gradients, C = 256) in
 // CGM passes over the tile, pass p holding channels [64 p, 64 p + 64) in the halo and running the nine
 // weight chunks of that channel group, accumulating.
@@ -1394,6 +1394,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Op A, Op B, Epi E,
 }
 
 // halo conv applicability (host): geometry, epilogue features and alignment the kernel assumes
+// The halo tile's pixel count: 96 (whole rows of a width dividing 96, or 96-pixel pieces of a row 96 divides), else
+// 128 for a plain ROWS conv with <= 64 outputs (SwinIR-lightweight's 64-pixel rows, Cp = 64: two whole rows per tile;
+// neither 96 | 64 nor 64 | 96, so its RSTB convs ran on the register-staged im2col kernel at 201 us), else 0 (none).
+static int halo_bm_of(int H, int W, int C, int N, const Epi& e) {
+  auto fits = [&](int bm) { return W <= bm ? (bm % W == 0 && H % (bm / W) == 0) : W % bm == 0; };
+  if (fits(HC_BM)) return HC_BM;
+  if (fits(128) && N <= 64 && C <= 192 && e.omode == KAIR_OUT_ROWS && !e.acopy && !e.gate) return 128;
+  return 0;
+}
+
 template <typename TA>
 static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, int K) {
   const int H = A.imH, W = A.imW, C = A.imC;
@@ -1403,14 +1413,11 @@ static bool conv_halo_ok(const Op& A, const Op& B, const Epi& e, long M, int N, 
   // the two-pass split forms lo from an fp32 image; a bf16 image carries it as its [hi | lo] halves (a_split 2)
   if (A.asplit && !(sizeof(TA) == 4 ? A.asplit == 1 : (A.asplit == 2 && C == 128 && B.wsplit))) return false;
   if (W <= 0 || H <= 0) return false;
-  if (W <= HC_BM) {
-    if (HC_BM % W != 0 || H % (HC_BM / W) != 0) return false;
-  } else if (W % HC_BM != 0) {
-    return false;
-  }
-  const int XW = W < HC_BM ? W : HC_BM, RPT = HC_BM / XW;
+  const int bm = halo_bm_of(H, W, C, N, e);
+  if (bm == 0) return false;
+  const int XW = W < bm ? W : bm, RPT = bm / XW;
   if ((long)(RPT + 2) * (XW + 2) * ((C > 192 ? HC_BK : C) + 8) > HC_HALO_ELEMS) return false;   // the halo of one pass
-  if (M % HC_BM != 0 || M % ((long)H * W) != 0) return false;
+  if (M % bm != 0 || M % ((long)H * W) != 0) return false;
   if (A.ld % 8 != 0 || ((unsigned long)A.ptr & 15) || B.ld % 8 != 0 || ((unsigned long)B.ptr & 15)) return false;
   if (e.omode != KAIR_OUT_ROWS && !(e.omode == KAIR_OUT_PSHUF_SPM && e.psH == H && e.psW == W && e.r > 0 &&
                                     N % (e.r * e.r) == 0 && (N / (e.r * e.r)) % 4 == 0 && !e.resid && !e.acopy) &&
@@ -1458,7 +1465,8 @@ static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int 
   if (g_num_cus == 0) init_num_cus();
   const bool wide = E.N > HC_BN;   // N in (192, 256]: two 128-wide N tiles
   const bool big = wide && !E.resid && A.asplit != 1 && halo_bm192_ok(A, M);   // (the two-pass form would spill)
-  const int tilesM = (int)(M / (big ? 192 : HC_BM));
+  const bool t128 = halo_bm_of(A.imH, A.imW, A.imC, E.N, E) == 128;           // (N <= 64, ROWS: one 64-wide N tile)
+  const int tilesM = (int)(M / (big ? 192 : (t128 ? 128 : HC_BM)));
   // few M tiles (small batches: 96 tiles at 4 patches per GPU): 64-wide N tiles put 3x the workgroups
   // on the chip, each a third of the weight chunks
   const bool slim = !wide && E.omode == KAIR_OUT_ROWS && E.N > 64 && 2L * tilesM <= g_num_cus;
@@ -1481,7 +1489,9 @@ static int launch_conv_halo(const Op& A, const Op& B, const Epi& E, long M, int 
     }
   }
 #define KAIR_HALO_NP(NP)                                                                           \
-  if (E.resid && slim) KAIR_HALO(NP, EX_RESID, 64, HC_EM_ROWS, 96);                                \
+  if (t128 && E.resid) KAIR_HALO(NP, EX_RESID, 64, HC_EM_ROWS, 128);                               \
+  else if (t128) KAIR_HALO(NP, EX_NONE, 64, HC_EM_ROWS, 128);                                      \
+  else if (E.resid && slim) KAIR_HALO(NP, EX_RESID, 64, HC_EM_ROWS, 96);                           \
   else if (E.resid) KAIR_HALO(NP, EX_RESID, 192, HC_EM_ROWS, 96);                                  \
   else if (E.omode == KAIR_OUT_PSHUF_SPM && big) KAIR_HALO(NP, EX_NONE, 128, HC_EM_PSHUF, 192);     \
   else if (E.omode == KAIR_OUT_PSHUF_SPM && wide) KAIR_HALO(NP, EX_NONE, 128, HC_EM_PSHUF, 96);     \

@@ -97,13 +97,15 @@ def test_conv3x3_implicit_gemm(compute, flip):
     assert rel_err(got, ref) < TOL[compute][0]
 
 
-@pytest.mark.parametrize("shape", [(2, 48, 48, 192, 192), (1, 12, 96, 64, 64), (1, 6, 192, 64, 180), (3, 24, 32, 128, 96)])
+@pytest.mark.parametrize("shape", [(2, 48, 48, 192, 192), (1, 12, 96, 64, 64), (1, 6, 192, 64, 180), (3, 24, 32, 128, 96),
+                                   (2, 16, 64, 64, 64), (1, 6, 128, 64, 60)])
 @pytest.mark.parametrize("flip", [False, True])
 @pytest.mark.parametrize("a_f32", [False, True])
 @pytest.mark.parametrize("resid", [False, True])
 def test_conv3x3_halo_path(shape, flip, a_f32, resid):
     """bf16 3x3 convs whose geometry selects the LDS-halo kernel (W | 96 or 96 | W, Cin % 64 == 0,
-    N <= 192): fp32 or bf16 input rows, forward or flipped taps, bias + optional fp32 residual."""
+    N <= 192; or the 128-pixel tile for N <= 64 where 128 | W or W | 128 -- SwinIR-lightweight's 64-pixel
+    rows): fp32 or bf16 input rows, forward or flipped taps, bias + optional fp32 residual."""
     B, Hh, Ww, Cin, Cout = shape
     g = torch.Generator().manual_seed(Hh * Ww + Cin)
     x = torch.randn(B, Cin, Hh, Ww, generator=g).bfloat16().float()
@@ -121,9 +123,16 @@ def test_conv3x3_halo_path(shape, flip, a_f32, resid):
     M = B * Hh * Ww
     out = torch.empty(M, Cout, device=dev)
     A = xin.to(dev, torch.float32 if a_f32 else torch.bfloat16)
-    H.gemm_nt(H.im2col(A, Hh, Ww, Cin, flip=flip), H.rows(packed.to(dev, torch.bfloat16)),
-              H.epilogue(out, bias=bias.to(dev), resid=r.to(dev) if resid else None), M, Cout, 9 * Cin, H.BF16)
+    ops = (H.im2col(A, Hh, Ww, Cin, flip=flip), H.rows(packed.to(dev, torch.bfloat16)),
+           H.epilogue(out, bias=bias.to(dev), resid=r.to(dev) if resid else None))
     torch.cuda.synchronize()
+    H.ktime_begin(8)
+    try:
+        H.gemm_nt(*ops, M, Cout, 9 * Cin, H.BF16)
+    finally:
+        nk = H.ktime_end()
+    torch.cuda.synchronize()
+    assert nk == 1 and "conv3x3_halo_kernel" in H.ktime_read(0)[1], H.ktime_read(0)[1]
     got = out.cpu()
     if resid:
         got = got - r
