@@ -72,14 +72,22 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
       ga[i][j] = c < C ? gamma[c] : 0.f;
       be[i][j] = c < C ? beta[c] : (c == one_col ? 1.f : 0.f);   // ones column for the weight-gradient GEMM
     }
-  for (long r = grp; r < M; r += ng) {        // r = output row (window order if wm.ws > 0)
+  // two rows per iteration, both rows' loads issued before either is reduced: one dependent load per row left each
+  // 16-lane group latency-bound on its rows (C <= 64: a single float4 per lane and row)
+  auto load_row = [&](long r, float4 (&v)[NV]) {
     const long t = win_to_token(r, wm);
-    float4 v[NV];
-    float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (sub + LPR * i) * 4;
       v[i] = c < C ? *(const float4*)(x + t * ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    return t;
+  };
+  auto finish_row = [&](long r, long t, float4 (&v)[NV]) {   // r = output row (window order if wm.ws > 0)
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (sub + LPR * i) * 4;
       if (c + 4 > C) {  // column group straddling C: pad lanes do not count
         if (c + 1 >= C) v[i].y = 0.f;
         if (c + 2 >= C) v[i].z = 0.f;
@@ -115,6 +123,18 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
       mean_out[t] = mu;
       rstd_out[t] = rs;
     }
+  };
+  long r = grp;
+  for (; r + ng < M; r += 2 * ng) {
+    float4 va[NV], vb[NV];
+    const long ta = load_row(r, va), tb = load_row(r + ng, vb);
+    finish_row(r, ta, va);
+    finish_row(r + ng, tb, vb);
+  }
+  if (r < M) {
+    float4 va[NV];
+    const long ta = load_row(r, va);
+    finish_row(r, ta, va);
   }
 }
 
