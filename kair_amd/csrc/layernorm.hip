@@ -138,7 +138,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-template <typename T>
+// NVK: float4 groups per lane (NV; 1 for C <= 64 -- SwinIR-lightweight's 60 -- where the narrow form keeps two rows
+// in flight per 16-lane group: both rows' x / dy / mean / rstd / accumulated-gradient loads before either reduction)
+template <typename T, int NVK>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, long ldx, const T* __restrict__ dy,
                                                       long ldy, const float* __restrict__ gamma,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -149,31 +151,42 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   const int sub = threadIdx.x & (LPR - 1);
   const long grp = (long)blockIdx.x * ROWS_PER_BLOCK_ITER + (threadIdx.x >> 4);
   const long ng = (long)gridDim.x * ROWS_PER_BLOCK_ITER;
-  float dg[NV][4], db[NV][4], g[NV][4];
+  float dg[NV][4], db[NV][4], g[NVK][4];
 #pragma unroll
   for (int i = 0; i < NV; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = (sub + LPR * i) * 4 + j;
       dg[i][j] = db[i][j] = 0.f;
-      g[i][j] = c < C ? gamma[c] : 0.f;
+      if (i < NVK) g[i < NVK ? i : 0][j] = c < C ? gamma[c] : 0.f;
     }
-  for (long r = grp; r < M; r += ng) {
+  struct RowIn { long t; float mu, rs; float4 xv[NVK], dv[NVK], cur[NVK]; };
+  auto load_row = [&](long r, RowIn& in) {
     const long t = win_to_token(r, wm);
-    const float mu = mean[t], rs = rstd[t];
-    float xh[NV][4], gy[NV][4];
-    float4 cur[NV];   // the accumulated gradient row, loaded together with x and dy (one round trip)
-    float s1 = 0.f, s2 = 0.f;
+    in.t = t;
+    in.mu = mean[t];
+    in.rs = rstd[t];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
+    for (int i = 0; i < NVK; ++i) {
       const int c = (sub + LPR * i) * 4;
-      float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), dv = xv;
-      cur[i] = xv;
+      float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), dv = xv, cu = xv;
       if (c < C) {
         xv = *(const float4*)(x + t * ldx + c);
         dv = load4<T>(dy + r * ldy + c);
-        if (dx_acc) cur[i] = *(const float4*)(dx + t * ld_dx + c);
+        if (dx_acc) cu = *(const float4*)(dx + t * ld_dx + c);
       }
+      in.xv[i] = xv; in.dv[i] = dv; in.cur[i] = cu;
+    }
+  };
+  auto finish_row = [&](RowIn& in) {
+    const long t = in.t;
+    const float mu = in.mu, rs = in.rs;
+    float xh[NVK][4], gy[NVK][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NVK; ++i) {
+      const int c = (sub + LPR * i) * 4;
+      const float4 xv = in.xv[i], dv = in.dv[i];
       const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, da[4] = {dv.x, dv.y, dv.z, dv.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -193,11 +206,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
     const float sc = cp && cp_scale ? cp_scale[(int)t / cp_rps] : 1.f;
     const long cr = cp ? token_to_win(t, cwm) : 0;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
+    for (int i = 0; i < NVK; ++i) {
       const int c = (sub + LPR * i) * 4;
       if (c < C) {
         float* o = dx + t * ld_dx + c;
-        float4 cu = cur[i];
+        float4 cu = in.cur[i];
         float d[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) d[j] = (c + j < C) ? rs * (gy[i][j] - s1 - xh[i][j] * s2) : 0.f;
@@ -209,6 +222,77 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
             store4_pair((f16*)cp, cp_lo, cr * ldc + c, opaque(sc * cu.x), opaque(sc * cu.y), opaque(sc * cu.z),
                         opaque(sc * cu.w), cp_s);
           else store4<float>((float*)cp + cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w);
+        }
+      }
+    }
+  };
+  if constexpr (NVK == 1) {
+    long r = grp;
+    for (; r + ng < M; r += 2 * ng) {
+      RowIn ra, rb;
+      load_row(r, ra);
+      load_row(r + ng, rb);
+      finish_row(ra);
+      finish_row(rb);
+    }
+    if (r < M) {
+      RowIn ra;
+      load_row(r, ra);
+      finish_row(ra);
+    }
+  } else {   // (the wide form: one row per iteration, as measured for the classical geometry)
+    for (long r = grp; r < M; r += ng) {
+      const long t = win_to_token(r, wm);
+      const float mu = mean[t], rs = rstd[t];
+      float xh[NV][4], gy[NV][4];
+      float4 cur[NV];   // the accumulated gradient row, loaded together with x and dy (one round trip)
+      float s1 = 0.f, s2 = 0.f;
+  #pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = (sub + LPR * i) * 4;
+        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), dv = xv;
+        cur[i] = xv;
+        if (c < C) {
+          xv = *(const float4*)(x + t * ldx + c);
+          dv = load4<T>(dy + r * ldy + c);
+          if (dx_acc) cur[i] = *(const float4*)(dx + t * ld_dx + c);
+        }
+        const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, da[4] = {dv.x, dv.y, dv.z, dv.w};
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = c + j < C;
+          xh[i][j] = ok ? (xa[j] - mu) * rs : 0.f;
+          const float d = ok ? da[j] : 0.f;
+          gy[i][j] = d * g[i][j];
+          dg[i][j] += d * xh[i][j];
+          db[i][j] += d;
+          s1 += gy[i][j];
+          s2 += gy[i][j] * xh[i][j];
+        }
+      }
+      s1 = group_sum16(s1) / C;
+      s2 = group_sum16(s2) / C;
+      // GEMM-operand copy row and scale: once per row
+      const float sc = cp && cp_scale ? cp_scale[(int)t / cp_rps] : 1.f;
+      const long cr = cp ? token_to_win(t, cwm) : 0;
+  #pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = (sub + LPR * i) * 4;
+        if (c < C) {
+          float* o = dx + t * ld_dx + c;
+          float4 cu = cur[i];
+          float d[4];
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) d[j] = (c + j < C) ? rs * (gy[i][j] - s1 - xh[i][j] * s2) : 0.f;
+          cu.x += d[0]; cu.y += d[1]; cu.z += d[2]; cu.w += d[3];
+          *(float4*)o = cu;
+          if (cp) {   // GEMM-operand copy of the finished gradient row: scaled, cast, optionally window-ordered
+            if (cp_dt == KAIR_BF16) store4<bf16>((bf16*)cp + cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w);
+            else if (cp_dt == KAIR_F16)   // (opaque products: the pair splits the fp32-rounded value, common.h)
+              store4_pair((f16*)cp, cp_lo, cr * ldc + c, opaque(sc * cu.x), opaque(sc * cu.y), opaque(sc * cu.z),
+                          opaque(sc * cu.w), cp_s);
+            else store4<float>((float*)cp + cr * ldc + c, sc * cu.x, sc * cu.y, sc * cu.z, sc * cu.w);
+          }
         }
       }
     }
@@ -428,14 +512,17 @@ extern "C" int kair_layernorm_bwd(const float* x, long ldx, const void* dy, int 
   }
   hipStream_t s = (hipStream_t)stream;
   const long nb = ln_bwd_blocks(M);
-  if (dy_dtype == KAIR_BF16)
-    KAIR_LAUNCH(ln_bwd_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const bf16*)dy, ldy, gamma,
-                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm,
-                       cp_lo, cp_s);
-  else
-    KAIR_LAUNCH(ln_bwd_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const float*)dy, ldy, gamma,
-                       mean, rstd, dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm,
-                       cp_lo, cp_s);
+#define KAIR_LNB(TT, NVV)                                                                                            \
+  KAIR_LAUNCH((ln_bwd_kernel<TT, NVV>), dim3((unsigned)nb), dim3(256), 0, s, x, ldx, (const TT*)dy, ldy, gamma, mean, rstd, \
+              dx_acc, ld_dx, dx_accumulate, ws, M, C, wm, cp, cp_dt, ldc, cp_scale, cp_rps, cwm, cp_lo, cp_s)
+  if (dy_dtype == KAIR_BF16) {
+    if (C <= 64) KAIR_LNB(bf16, 1);
+    else KAIR_LNB(bf16, NV);
+  } else {
+    if (C <= 64) KAIR_LNB(float, 1);
+    else KAIR_LNB(float, NV);
+  }
+#undef KAIR_LNB
   KAIR_CHECK_LAUNCH();
   if (!dgamma) return 0;   // deferred: the [nb][2C] partials stay in ws for kair_ln_param_reduce_grouped
   KAIR_LAUNCH(ln_param_reduce, dim3((2 * C + 7) / 8), dim3(256), 0, s, ws, (int)nb, C, dgamma, dbeta,

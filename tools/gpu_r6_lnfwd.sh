@@ -1,7 +1,7 @@
 #!/bin/bash
-# round 6: LayerNorm forward with two rows in flight per 16-lane group -- parity, C2 and the headline
+# round 6: LayerNorm forward / narrow backward with two rows in flight per 16-lane group -- parity, C2 and the headline
 set -o pipefail
-R=$(pwd); O=$R/gpurun_out/lnfwd; mkdir -p $O
+R=$(pwd); O=$R/gpurun_out/lnbwd; mkdir -p $O
 T="python3 -u -m pytest -x -q --timeout 300 --timeout-method thread"
 timeout -k 10 600 $T tests/test_kernels_gpu.py tests/test_x3_gpu.py tests/test_full_configs_gpu.py tests/test_swinir_gpu.py > $O/t.txt 2>&1 || { tail -30 $O/t.txt; exit 1; }
 tail -1 $O/t.txt
