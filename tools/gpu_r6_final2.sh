@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 6 checkpoints after the C2 work: the whole GPU suite, smoke(), the default bench line
 set -o pipefail
-R=$(pwd); O=$R/gpurun_out/r6fin4; mkdir -p $O
+R=$(pwd); O=$R/gpurun_out/r6fin5; mkdir -p $O
 timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/t_all.log 2>&1
 rc=$?; tail -3 $O/t_all.log
 if [ $rc -ne 0 ]; then echo "pytest rc $rc: stopping"; grep -B2 -A15 "Error\|assert" $O/t_all.log | head -60; exit $rc; fi
